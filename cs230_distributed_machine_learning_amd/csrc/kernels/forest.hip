@@ -1,0 +1,871 @@
+// forest.hip — batched level-wise random-forest builder and predictor for CDNA4 (gfx950).
+//
+// Replaces the delegated scikit-learn tree builders the reference calls per task
+// (aws-prod/worker/worker.py:315 `model.fit`, :326/:341 `cross_val_score` -> 5 more
+// fits, :322/:336 `predict`).  Instead of one CPU fit per (candidate, fold) this builds
+// EVERY tree of MANY fits (candidates x CV folds x trees) at once, breadth-first,
+// against one HBM-resident binned copy of the dataset.  Folds and bootstraps are never
+// materialised: a row's role (train/test) comes from a per-split uint8 vector and its
+// bootstrap weight is recomputed from a counter hash (forest_common.h).
+//
+// Work per level is bucketed by node size so every node gets a right-sized worker:
+//   * wave tier  (count <= wave_max):  one 64-lane wave per node; LDS histogram,
+//     wave-scan over the 256 bins, wave-argmax, ballot-based stable partition — one
+//     fused kernel, no global histogram traffic;
+//   * block tier (count <= block_max): one 256-thread workgroup per node, same fused
+//     pipeline with 4 waves evaluating features in parallel;
+//   * large tier (count > block_max):  per (node, row-chunk) workgroups build LDS
+//     histograms and flush them with ONE coalesced atomic pass into a per-node global
+//     histogram; a per-node kernel scans/selects; a chunked kernel partitions.
+// Histograms are integer (uint32) for classification, so results are bit-identical
+// to the CPU builder whatever the atomic arrival order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include <type_traits>
+#include <algorithm>
+#include <stdio.h>
+#include "forest_common.h"
+
+namespace dml {
+
+struct OpenNode {
+  int32_t tree, node, start, count, depth, pad;
+  uint64_t key;
+};
+
+// ctypes-facing argument block: every field is 8 bytes (pointers as int64).
+struct ForestArgs {
+  int64_t Xb, ld, n, d;
+  int64_t ycls, yreg, n_classes, is_reg;
+  int64_t roles, n_splits;
+  int64_t specs, T;
+  int64_t active_count;  // int32[T]  (count phase output)
+  int64_t row_off;       // int64[T+1] device offsets (exclusive prefix of active_count)
+  int64_t rows_total;
+  int64_t max_active;    // max over trees of active_count
+  int64_t nodes, node_val, pool_cap;  // NodeRec*, double* [pool_cap*VC]
+  int64_t tree_W;        // double[T]
+  int64_t workspace, workspace_bytes;
+  int64_t wave_max, block_max, chunk;
+  int64_t kg_wave, kg_block, kg_large;
+  int64_t slack_wave;
+  // outputs
+  int64_t n_nodes_out, status_out, levels_out, large_rounds_out;
+};
+
+enum CounterSlot { kCntSets = 0 /*6*/, kPool = 6, kOverflow = 7, kNeedMore = 8, kOpenOvf = 9, kNumCounters = 16 };
+
+struct LState {
+  OpenNode on;
+  int32_t pos, nonconst, g, done;
+  int32_t best_feat, best_bin, split, nl;
+  double best_gain;
+};
+
+struct Ctx {
+  const uint8_t* Xb;
+  int64_t ld;
+  int32_t n, d, C, CH, VC, is_reg;
+  const int32_t* ycls;
+  const float* yreg;
+  const uint8_t* roles;
+  const TreeSpec* specs;
+  int32_t T;
+  int32_t* active_count;
+  const int64_t* row_off;
+  uint32_t* rows_cur;
+  uint32_t* rows_next;
+  NodeRec* nodes;
+  double* node_val;
+  int64_t pool_cap;
+  double* tree_W;
+  OpenNode* open[2][3];
+  int64_t open_cap[3];
+  int32_t* counters;
+  int32_t* cursors;      // [T]
+  LState* lstate;
+  int16_t* lperm;        // [cap_large][d]
+  double* lbest_left;    // [cap_large][CH]
+  void* ghist;           // [cap_large][kg_large][CH][256] (u32 or f32)
+  int32_t* lcursor;      // [cap_large][2]
+  int64_t large_cap;
+  int32_t wave_max, block_max, chunk, kg_wave, kg_block, kg_large, slack_wave;
+};
+
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ int lane_prefix(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+// ------------------------------------------------------------------------------------
+// node bookkeeping
+// ------------------------------------------------------------------------------------
+__device__ double node_impurity(const Ctx& c, int node, int crit) {
+  const double* v = c.node_val + (int64_t)node * c.VC;
+  if (c.is_reg) return mse_impurity(v[0], v[1], v[2]);
+  ClsAcc a;
+  a.init();
+  for (int k = 0; k < c.C; ++k) a.add(v[k]);
+  return cls_impurity(a, crit);
+}
+
+__device__ double node_weight(const Ctx& c, int node) {
+  const double* v = c.node_val + (int64_t)node * c.VC;
+  if (c.is_reg) return v[0];
+  double w = 0.0;
+  for (int k = 0; k < c.C; ++k) w += v[k];
+  return w;
+}
+
+// decide whether a freshly created node is worth visiting; enqueue it into `set`
+__device__ void enqueue_or_leaf(const Ctx& c, int tree, int node, int start, int count, int depth,
+                                uint64_t key, int set) {
+  const TreeSpec& s = c.specs[tree];
+  if (leaf_by_counts(s, count, depth)) return;
+  if (node_impurity(c, node, s.criterion) <= kEps) return;
+  const int tier = count <= c.wave_max ? 0 : (count <= c.block_max ? 1 : 2);
+  const int idx = atomicAdd(&c.counters[set * 3 + tier], 1);
+  if (idx >= c.open_cap[tier]) {
+    atomicOr(&c.counters[kOpenOvf], 1);
+    return;
+  }
+  OpenNode on;
+  on.tree = tree; on.node = node; on.start = start; on.count = count; on.depth = depth; on.pad = 0;
+  on.key = key;
+  c.open[set][tier][idx] = on;
+}
+
+// allocate two children, write parent record and children stats. returns left index or -1.
+__device__ int make_children(const Ctx& c, int node, int feat, int bin, const double* left_ch) {
+  const int base = atomicAdd(&c.counters[kPool], 2);
+  if ((int64_t)base + 2 > c.pool_cap) {
+    atomicOr(&c.counters[kOverflow], 1);
+    return -1;
+  }
+  NodeRec leaf; leaf.split = -1; leaf.left = -1;
+  c.nodes[base] = leaf;
+  c.nodes[base + 1] = leaf;
+  const double* pv = c.node_val + (int64_t)node * c.VC;
+  double* lv = c.node_val + (int64_t)base * c.VC;
+  double* rv = lv + c.VC;
+  for (int k = 0; k < c.VC; ++k) {
+    lv[k] = left_ch[k];
+    rv[k] = pv[k] - left_ch[k];
+  }
+  NodeRec rec; rec.split = pack_split(feat, bin); rec.left = base;
+  c.nodes[node] = rec;
+  return base;
+}
+
+// ------------------------------------------------------------------------------------
+// histogram scan / evaluation — executed by ONE wave on one feature's [CH][256] image
+// ------------------------------------------------------------------------------------
+template <typename CT>
+__device__ __forceinline__ void scan256(CT* p, int lane) {
+  CT v0 = p[4 * lane], v1 = p[4 * lane + 1], v2 = p[4 * lane + 2], v3 = p[4 * lane + 3];
+  v1 += v0; v2 += v1; v3 += v2;
+  CT t = v3;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    CT o = __shfl_up(t, off);
+    if (lane >= off) t += o;
+  }
+  CT ex = __shfl_up(t, 1);
+  if (lane == 0) ex = (CT)0;
+  p[4 * lane] = v0 + ex; p[4 * lane + 1] = v1 + ex; p[4 * lane + 2] = v2 + ex; p[4 * lane + 3] = v3 + ex;
+}
+
+template <bool REG>
+__device__ void eval_feature(typename std::conditional<REG, float, uint32_t>::type* h, int C, int CH,
+                             const TreeSpec& s, int lane, double* out_gain, int* out_bin, int* out_nc) {
+  using CT = typename std::conditional<REG, float, uint32_t>::type;
+  for (int ch = 0; ch < CH; ++ch) scan256<CT>(h + ch * 256, lane);
+  wave_lds_sync();
+  const CT tot_rows = h[(CH - 1) * 256 + 255];
+  const CT msl = (CT)s.min_samples_leaf;
+  double best = -INFINITY;
+  int bb = -1;
+  bool nc = false;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int b = lane * 4 + i;
+    if (b == 255) break;
+    const CT rl = h[(CH - 1) * 256 + b];
+    const CT rr = tot_rows - rl;
+    nc |= (rl > (CT)0 && rr > (CT)0);
+    if (rl < msl || rr < msl) continue;
+    double g;
+    if constexpr (!REG) {
+      ClsAcc L, R;
+      L.init(); R.init();
+      for (int k = 0; k < C; ++k) {
+        const double lc = (double)h[k * 256 + b];
+        const double tc = (double)h[k * 256 + 255];
+        L.add(lc);
+        R.add(tc - lc);
+      }
+      g = cls_proxy(L, R, s.criterion);
+    } else {
+      const double l0 = (double)h[b], t0 = (double)h[255];
+      const double l1 = (double)h[256 + b], t1 = (double)h[256 + 255];
+      g = mse_proxy(l0, l1, t0 - l0, t1 - l1);
+    }
+    if (g > best) { best = g; bb = b; }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double og = __shfl_xor(best, off);
+    const int ob = __shfl_xor(bb, off);
+    if (og > best || (og == best && ob >= 0 && (bb < 0 || ob < bb))) { best = og; bb = ob; }
+  }
+  const bool any_nc = __ballot(nc) != 0ull;
+  if (lane == 0) { *out_gain = best; *out_bin = bb; *out_nc = any_nc ? 1 : 0; }
+}
+
+// scratch block at the end of a fused kernel's LDS
+struct Scratch {
+  double best_gain;
+  int32_t best_feat, best_bin, nonconst, pos, g, base, nl, done;
+  int32_t wcnt[8];  // per-wave partition counts (L: 0..3, R: 4..7)
+  int32_t tile_base[2];
+};
+
+template <typename CT>
+__device__ __forceinline__ void hist_add_row(CT* hist, const Ctx& c, const int16_t* feats, int g, uint32_t row,
+                                             uint32_t w) {
+  const uint8_t* xr = c.Xb + (int64_t)row * c.ld;
+  const int span = c.CH * 256;
+  if constexpr (std::is_same<CT, uint32_t>::value) {
+    const int y = c.ycls[row];
+    for (int j = 0; j < g; ++j) {
+      const int b = xr[feats[j]];
+      CT* hj = hist + j * span;
+      atomicAdd(&hj[y * 256 + b], w);
+      atomicAdd(&hj[c.C * 256 + b], 1u);
+    }
+  } else {
+    const float yv = c.yreg[row];
+    const float fw = (float)w, wy = fw * yv, wyy = wy * yv;
+    for (int j = 0; j < g; ++j) {
+      const int b = xr[feats[j]];
+      CT* hj = hist + j * span;
+      atomicAdd(&hj[b], fw);
+      atomicAdd(&hj[256 + b], wy);
+      atomicAdd(&hj[512 + b], wyy);
+      atomicAdd(&hj[768 + b], 1.0f);
+    }
+  }
+}
+
+// serial selection over an evaluated group (thread 0). returns true when search is done.
+template <typename CT>
+__device__ void select_group(const Ctx& c, const TreeSpec& s, const int16_t* feats, int g, const double* rg,
+                             const int* rb, const int* rn, const CT* hist, double* best_left, int& nonconst,
+                             double& best_gain, int& best_feat, int& best_bin) {
+  const int span = c.CH * 256;
+  for (int j = 0; j < g; ++j) {
+    if (!rn[j]) continue;
+    ++nonconst;
+    if (rb[j] >= 0 && rg[j] > best_gain) {
+      best_gain = rg[j];
+      best_feat = feats[j];
+      best_bin = rb[j];
+      for (int ch = 0; ch < c.CH; ++ch) best_left[ch] = (double)hist[j * span + ch * 256 + rb[j]];
+    }
+    if (nonconst >= s.max_features) break;
+  }
+}
+
+// final split decision given the best candidate; returns true if node splits
+__device__ bool accept_split(const Ctx& c, const TreeSpec& s, int node, int tree, const double* best_left) {
+  const double* pv = c.node_val + (int64_t)node * c.VC;
+  const double Wt = c.tree_W[tree];
+  double impN, impL, impR, wN, wL, wR;
+  if (c.is_reg) {
+    wN = pv[0]; wL = best_left[0]; wR = pv[0] - best_left[0];
+    impN = mse_impurity(pv[0], pv[1], pv[2]);
+    impL = mse_impurity(best_left[0], best_left[1], best_left[2]);
+    impR = mse_impurity(pv[0] - best_left[0], pv[1] - best_left[1], pv[2] - best_left[2]);
+  } else {
+    ClsAcc N, L, R;
+    N.init(); L.init(); R.init();
+    for (int k = 0; k < c.C; ++k) { N.add(pv[k]); L.add(best_left[k]); R.add(pv[k] - best_left[k]); }
+    wN = N.w; wL = L.w; wR = R.w;
+    impN = cls_impurity(N, s.criterion); impL = cls_impurity(L, s.criterion); impR = cls_impurity(R, s.criterion);
+  }
+  const double imp = improvement(Wt, wN, impN, wL, impL, wR, impR);
+  return !(imp + kEps < (double)s.min_impurity_decrease);
+}
+
+// ------------------------------------------------------------------------------------
+// fused per-node kernel (wave tier NT=64, block tier NT=256)
+// ------------------------------------------------------------------------------------
+template <int NT, bool REG>
+__global__ __launch_bounds__(NT) void k_nodes(Ctx c, int tier, int set_cur) {
+  using CT = typename std::conditional<REG, float, uint32_t>::type;
+  constexpr int NW = NT / 64;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const OpenNode on = c.open[set_cur][tier][blockIdx.x];
+  const TreeSpec& s = c.specs[on.tree];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int d = c.d;
+  const int KG = NT == 64 ? c.kg_wave : c.kg_block;
+  const int slack = NT == 64 ? c.slack_wave : 0;
+  const int perm_bytes = ((d * 2 + 15) / 16) * 16;
+  int16_t* perm = (int16_t*)smem;
+  CT* hist = (CT*)(smem + perm_bytes);
+  const int span = c.CH * 256;
+  unsigned char* tail = smem + perm_bytes + (size_t)KG * span * sizeof(CT);
+  double* rg = (double*)tail;
+  int* rb = (int*)(rg + KG);
+  int* rn = rb + KG;
+  double* best_left = (double*)(((uintptr_t)(rn + KG) + 15) & ~(uintptr_t)15);
+  Scratch* sc = (Scratch*)(best_left + ((c.CH + 1) & ~1));
+
+  for (int i = tid; i < d; i += NT) perm[i] = (int16_t)i;
+  if (tid == 0) {
+    sc->best_gain = -INFINITY; sc->best_feat = -1; sc->best_bin = -1;
+    sc->nonconst = 0; sc->pos = 0; sc->done = 0;
+  }
+  __syncthreads();
+  const uint32_t* rows = c.rows_cur + c.row_off[on.tree];
+  const int k = s.max_features;
+  while (true) {
+    const int pos = sc->pos, nonconst = sc->nonconst;
+    if (nonconst >= k || pos >= d) break;
+    const int g = min(KG, min(k - nonconst + slack, d - pos));
+    if (tid == 0) {
+      for (int j = pos; j < pos + g; ++j) {
+        const int t = perm_pick(on.key, j, d);
+        const int16_t tmp = perm[j]; perm[j] = perm[t]; perm[t] = tmp;
+      }
+    }
+    for (int i = tid; i < g * span; i += NT) hist[i] = (CT)0;
+    __syncthreads();
+    const int16_t* feats = perm + pos;
+    for (int r = tid; r < on.count; r += NT) {
+      const uint32_t row = rows[on.start + r];
+      hist_add_row<CT>(hist, c, feats, g, row, boot_weight(s, row));
+    }
+    __syncthreads();
+    for (int j = wid; j < g; j += NW) eval_feature<REG>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j);
+    __syncthreads();
+    if (tid == 0) {
+      int nc = sc->nonconst, bf = sc->best_feat, bbin = sc->best_bin;
+      double bg = sc->best_gain;
+      select_group<CT>(c, s, feats, g, rg, rb, rn, hist, best_left, nc, bg, bf, bbin);
+      sc->nonconst = nc; sc->best_gain = bg; sc->best_feat = bf; sc->best_bin = bbin;
+      sc->pos = pos + g;
+    }
+    __syncthreads();
+  }
+  // ---- decision
+  if (tid == 0) {
+    int base = -1;
+    if (sc->best_feat >= 0 && accept_split(c, s, on.node, on.tree, best_left))
+      base = make_children(c, on.node, sc->best_feat, sc->best_bin, best_left);
+    sc->base = base;
+    sc->nl = base >= 0 ? (int)best_left[c.CH - 1] : 0;
+  }
+  __syncthreads();
+  const int base = sc->base;
+  if (base < 0) return;
+  const int feat = sc->best_feat, bin = sc->best_bin, nl = sc->nl;
+  uint32_t* out = c.rows_next + c.row_off[on.tree] + on.start;
+  int baseL = 0, baseR = 0;
+  for (int t0 = 0; t0 < on.count; t0 += NT) {
+    const int r = t0 + tid;
+    const bool valid = r < on.count;
+    const uint32_t row = valid ? rows[on.start + r] : 0u;
+    const bool left = valid && c.Xb[(int64_t)row * c.ld + feat] <= bin;
+    const bool right = valid && !left;
+    const uint64_t ml = __ballot(left), mr = __ballot(right);
+    const int pl = lane_prefix(ml), pr = lane_prefix(mr);
+    int offL = 0, offR = 0, totL, totR;
+    if constexpr (NW == 1) {
+      totL = __popcll(ml); totR = __popcll(mr);
+    } else {
+      if (lane == 0) { sc->wcnt[wid] = __popcll(ml); sc->wcnt[4 + wid] = __popcll(mr); }
+      __syncthreads();
+      totL = 0; totR = 0;
+      for (int w = 0; w < NW; ++w) {
+        if (w < wid) { offL += sc->wcnt[w]; offR += sc->wcnt[4 + w]; }
+        totL += sc->wcnt[w]; totR += sc->wcnt[4 + w];
+      }
+      __syncthreads();
+    }
+    if (left) out[baseL + offL + pl] = row;
+    if (right) out[nl + baseR + offR + pr] = row;
+    baseL += totL; baseR += totR;
+  }
+  if (tid == 0) {
+    const int set_next = 1 - set_cur;
+    enqueue_or_leaf(c, on.tree, base, on.start, nl, on.depth + 1, child_key(on.key, 0), set_next);
+    enqueue_or_leaf(c, on.tree, base + 1, on.start + nl, on.count - nl, on.depth + 1, child_key(on.key, 1), set_next);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// large tier
+// ------------------------------------------------------------------------------------
+__global__ void k_large_prep(Ctx c, int set_cur, int nL) {
+  const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= nL) return;
+  LState st;
+  st.on = c.open[set_cur][2][slot];
+  const TreeSpec& s = c.specs[st.on.tree];
+  int16_t* perm = c.lperm + (int64_t)slot * c.d;
+  for (int i = 0; i < c.d; ++i) perm[i] = (int16_t)i;
+  st.pos = 0; st.nonconst = 0; st.done = 0; st.best_feat = -1; st.best_bin = -1; st.split = 0; st.nl = 0;
+  st.best_gain = -INFINITY;
+  st.g = min(c.kg_large, min(s.max_features, c.d));
+  for (int j = 0; j < st.g; ++j) {
+    const int t = perm_pick(st.on.key, j, c.d);
+    const int16_t tmp = perm[j]; perm[j] = perm[t]; perm[t] = tmp;
+  }
+  c.lstate[slot] = st;
+  c.lcursor[2 * slot] = 0;
+  c.lcursor[2 * slot + 1] = 0;
+}
+
+template <bool REG>
+__global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
+  using CT = typename std::conditional<REG, float, uint32_t>::type;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int slot = blockIdx.y;
+  const LState& st = c.lstate[slot];
+  if (st.done) return;
+  const int r0 = blockIdx.x * c.chunk;
+  if (r0 >= st.on.count) return;
+  const int r1 = min(r0 + c.chunk, st.on.count);
+  const TreeSpec& s = c.specs[st.on.tree];
+  const int g = st.g;
+  const int span = c.CH * 256;
+  __shared__ int16_t feats[64];
+  CT* hist = (CT*)smem;
+  const int16_t* perm = c.lperm + (int64_t)slot * c.d + st.pos;
+  for (int j = threadIdx.x; j < g; j += 256) feats[j] = perm[j];
+  for (int i = threadIdx.x; i < g * span; i += 256) hist[i] = (CT)0;
+  __syncthreads();
+  const uint32_t* rows = c.rows_cur + c.row_off[st.on.tree] + st.on.start;
+  for (int r = r0 + threadIdx.x; r < r1; r += 256) {
+    const uint32_t row = rows[r];
+    hist_add_row<CT>(hist, c, feats, g, row, boot_weight(s, row));
+  }
+  __syncthreads();
+  CT* gh = (CT*)c.ghist + (int64_t)slot * c.kg_large * span;
+  for (int i = threadIdx.x; i < g * span; i += 256) {
+    const CT v = hist[i];
+    if (v != (CT)0) atomicAdd(&gh[i], v);
+  }
+}
+
+template <bool REG>
+__global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
+  using CT = typename std::conditional<REG, float, uint32_t>::type;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int slot = blockIdx.x;
+  LState& st = c.lstate[slot];
+  if (st.done) return;
+  const TreeSpec& s = c.specs[st.on.tree];
+  const int g = st.g, span = c.CH * 256;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  CT* hist = (CT*)smem;
+  double* rg = (double*)(smem + (size_t)c.kg_large * span * sizeof(CT));
+  int* rb = (int*)(rg + c.kg_large);
+  int* rn = rb + c.kg_large;
+  const CT* gh = (const CT*)c.ghist + (int64_t)slot * c.kg_large * span;
+  for (int i = tid; i < g * span; i += 256) hist[i] = gh[i];
+  __syncthreads();
+  for (int j = wid; j < g; j += 4) eval_feature<REG>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j);
+  __syncthreads();
+  if (tid != 0) return;
+  const int16_t* feats = c.lperm + (int64_t)slot * c.d + st.pos;
+  double* best_left = c.lbest_left + (int64_t)slot * c.CH;
+  int nc = st.nonconst, bf = st.best_feat, bbin = st.best_bin;
+  double bg = st.best_gain;
+  select_group<CT>(c, s, feats, g, rg, rb, rn, hist, best_left, nc, bg, bf, bbin);
+  st.nonconst = nc; st.best_gain = bg; st.best_feat = bf; st.best_bin = bbin;
+  st.pos += g;
+  if (st.nonconst < s.max_features && st.pos < c.d) {
+    // need more features: extend the permutation lazily and ask the host for a round
+    const int g2 = min(c.kg_large, min(s.max_features - st.nonconst, c.d - st.pos));
+    int16_t* perm = c.lperm + (int64_t)slot * c.d;
+    for (int j = st.pos; j < st.pos + g2; ++j) {
+      const int t = perm_pick(st.on.key, j, c.d);
+      const int16_t tmp = perm[j]; perm[j] = perm[t]; perm[t] = tmp;
+    }
+    st.g = g2;
+    atomicOr(&c.counters[kNeedMore], 1);
+    return;
+  }
+  st.done = 1;
+  int base = -1;
+  if (st.best_feat >= 0 && accept_split(c, s, st.on.node, st.on.tree, best_left))
+    base = make_children(c, st.on.node, st.best_feat, st.best_bin, best_left);
+  if (base < 0) return;
+  st.split = 1;
+  st.nl = (int)best_left[c.CH - 1];
+  const int set_next = 1 - set_cur;
+  enqueue_or_leaf(c, st.on.tree, base, st.on.start, st.nl, st.on.depth + 1, child_key(st.on.key, 0), set_next);
+  enqueue_or_leaf(c, st.on.tree, base + 1, st.on.start + st.nl, st.on.count - st.nl, st.on.depth + 1,
+                  child_key(st.on.key, 1), set_next);
+}
+
+__global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
+  const int slot = blockIdx.y;
+  const LState& st = c.lstate[slot];
+  if (!st.split) return;
+  const int r0 = blockIdx.x * c.chunk;
+  if (r0 >= st.on.count) return;
+  const int r1 = min(r0 + c.chunk, st.on.count);
+  const int feat = st.best_feat, bin = st.best_bin, nl = st.nl;
+  const uint32_t* rows = c.rows_cur + c.row_off[st.on.tree] + st.on.start;
+  uint32_t* out = c.rows_next + c.row_off[st.on.tree] + st.on.start;
+  __shared__ int wcnt[8];
+  __shared__ int tbase[2];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int t0 = r0; t0 < r1; t0 += 256) {
+    const int r = t0 + tid;
+    const bool valid = r < r1;
+    const uint32_t row = valid ? rows[r] : 0u;
+    const bool left = valid && c.Xb[(int64_t)row * c.ld + feat] <= bin;
+    const bool right = valid && !left;
+    const uint64_t ml = __ballot(left), mr = __ballot(right);
+    if (lane == 0) { wcnt[wid] = __popcll(ml); wcnt[4 + wid] = __popcll(mr); }
+    __syncthreads();
+    int offL = 0, offR = 0, totL = 0, totR = 0;
+    for (int w = 0; w < 4; ++w) {
+      if (w < wid) { offL += wcnt[w]; offR += wcnt[4 + w]; }
+      totL += wcnt[w]; totR += wcnt[4 + w];
+    }
+    if (tid == 0) {
+      tbase[0] = atomicAdd(&c.lcursor[2 * slot], totL);
+      tbase[1] = atomicAdd(&c.lcursor[2 * slot + 1], totR);
+    }
+    __syncthreads();
+    if (left) out[tbase[0] + offL + lane_prefix(ml)] = row;
+    if (right) out[nl + tbase[1] + offR + lane_prefix(mr)] = row;
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// tree roots: active-row count, fill, root statistics
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_count_active(Ctx c) {
+  const int t = blockIdx.y;
+  const TreeSpec& s = c.specs[t];
+  const uint8_t* role = c.roles + (int64_t)s.split * c.n;
+  int cnt = 0;
+  const int r0 = blockIdx.x * 1024;
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + i * 256 + threadIdx.x;
+    if (r < c.n && role[r] == 1 && boot_weight(s, (uint32_t)r) > 0) ++cnt;
+  }
+  __shared__ int red[4];
+  for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int tot = red[0] + red[1] + red[2] + red[3];
+    if (tot) atomicAdd(&c.active_count[t], tot);
+  }
+}
+
+template <bool REG>
+__global__ __launch_bounds__(256) void k_fill_active(Ctx c) {
+  const int t = blockIdx.y;
+  const TreeSpec& s = c.specs[t];
+  const uint8_t* role = c.roles + (int64_t)s.split * c.n;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ int wcnt[16];
+  __shared__ int base_s;
+  __shared__ double acc[kMaxClasses];
+  for (int k = tid; k < kMaxClasses; k += 256) acc[k] = 0.0;
+  const int r0 = blockIdx.x * 1024;
+  uint32_t wts[4];
+  bool act[4];
+  int mine = 0;
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + tid * 4 + i;
+    wts[i] = (r < c.n && role[r] == 1) ? boot_weight(s, (uint32_t)r) : 0u;
+    act[i] = wts[i] > 0;
+    mine += act[i];
+  }
+  // block exclusive scan of `mine` (rows stay in ascending order inside the block)
+  int incl = mine;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(incl, off);
+    if (lane >= off) incl += o;
+  }
+  if (lane == 63) wcnt[wid] = incl;
+  __syncthreads();
+  if (tid == 0) {
+    int tot = 0;
+    for (int w = 0; w < 4; ++w) { const int v = wcnt[w]; wcnt[8 + w] = tot; tot += v; }
+    base_s = tot ? atomicAdd(&c.cursors[t], tot) : 0;
+  }
+  __syncthreads();
+  int p = base_s + wcnt[8 + wid] + incl - mine;
+  uint32_t* out = c.rows_cur + c.row_off[t];
+  for (int i = 0; i < 4; ++i) {
+    if (!act[i]) continue;
+    const uint32_t r = (uint32_t)(r0 + tid * 4 + i);
+    out[p++] = r;
+    const double w = (double)wts[i];
+    if constexpr (REG) {
+      const double y = (double)c.yreg[r];
+      atomicAdd(&acc[0], w);
+      atomicAdd(&acc[1], w * y);
+      atomicAdd(&acc[2], w * y * y);
+    } else {
+      atomicAdd(&acc[c.ycls[r]], w);
+    }
+  }
+  __syncthreads();
+  for (int k = tid; k < c.VC; k += 256)
+    if (acc[k] != 0.0) atomicAdd(&c.node_val[(int64_t)t * c.VC + k], acc[k]);
+}
+
+__global__ void k_init_counters(Ctx c) { c.counters[kPool] = c.T; }
+
+__global__ void k_roots(Ctx c) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= c.T) return;
+  NodeRec leaf; leaf.split = -1; leaf.left = -1;
+  c.nodes[t] = leaf;
+  c.tree_W[t] = node_weight(c, t);
+  const int cnt = c.active_count[t];
+  if (cnt == 0) return;
+  enqueue_or_leaf(c, t, t, 0, cnt, 0, root_key(c.specs[t].seed), 0);
+}
+
+// ------------------------------------------------------------------------------------
+// host orchestration
+// ------------------------------------------------------------------------------------
+static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct Layout {
+  size_t rows_b, open[2][3], counters, cursors, lstate, lperm, lbest, ghist, lcursor, total;
+  int64_t open_cap[3], large_cap;
+};
+
+static Layout plan(const ForestArgs* a) {
+  Layout L{};
+  const int64_t R = a->rows_total, T = a->T;
+  const int64_t C = a->is_reg ? 3 : a->n_classes;
+  const int64_t CH = a->is_reg ? 4 : a->n_classes + 1;
+  L.open_cap[0] = R / 2 + T + 16;
+  L.open_cap[1] = R / (a->wave_max + 1) + T + 16;
+  L.open_cap[2] = R / (a->block_max + 1) + T + 16;
+  L.large_cap = L.open_cap[2];
+  (void)C;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
+  L.rows_b = take((size_t)R * 4);
+  for (int s = 0; s < 2; ++s)
+    for (int t = 0; t < 3; ++t) L.open[s][t] = take((size_t)L.open_cap[t] * sizeof(OpenNode));
+  L.counters = take(kNumCounters * 4);
+  L.cursors = take((size_t)T * 4);
+  L.lstate = take((size_t)L.large_cap * sizeof(LState));
+  L.lperm = take((size_t)L.large_cap * a->d * 2);
+  L.lbest = take((size_t)L.large_cap * CH * 8);
+  L.ghist = take((size_t)L.large_cap * a->kg_large * CH * 256 * 4);
+  L.lcursor = take((size_t)L.large_cap * 8);
+  L.total = off;
+  return L;
+}
+
+static size_t fused_lds(const ForestArgs* a, int KG) {
+  const int CH = a->is_reg ? 4 : (int)a->n_classes + 1;
+  size_t perm_bytes = ((a->d * 2 + 15) / 16) * 16;
+  size_t b = perm_bytes + (size_t)KG * CH * 256 * 4;
+  b += KG * 8 + 2 * KG * 4;
+  b = align_up(b, 16) + ((CH + 1) & ~1) * 8 + sizeof(Scratch) + 16;
+  return b;
+}
+
+static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
+  Ctx c{};
+  unsigned char* ws = (unsigned char*)a->workspace;
+  c.Xb = (const uint8_t*)a->Xb; c.ld = a->ld; c.n = (int)a->n; c.d = (int)a->d;
+  c.is_reg = (int)a->is_reg;
+  c.C = c.is_reg ? 1 : (int)a->n_classes;
+  c.CH = c.is_reg ? 4 : (int)a->n_classes + 1;
+  c.VC = c.is_reg ? 3 : (int)a->n_classes;
+  c.ycls = (const int32_t*)a->ycls; c.yreg = (const float*)a->yreg;
+  c.roles = (const uint8_t*)a->roles; c.specs = (const TreeSpec*)a->specs; c.T = (int)a->T;
+  c.active_count = (int32_t*)a->active_count; c.row_off = (const int64_t*)a->row_off;
+  c.nodes = (NodeRec*)a->nodes; c.node_val = (double*)a->node_val; c.pool_cap = a->pool_cap;
+  c.tree_W = (double*)a->tree_W;
+  c.rows_next = (uint32_t*)(ws + L.rows_b);
+  for (int s = 0; s < 2; ++s)
+    for (int t = 0; t < 3; ++t) c.open[s][t] = (OpenNode*)(ws + L.open[s][t]);
+  for (int t = 0; t < 3; ++t) c.open_cap[t] = L.open_cap[t];
+  c.counters = (int32_t*)(ws + L.counters);
+  c.cursors = (int32_t*)(ws + L.cursors);
+  c.lstate = (LState*)(ws + L.lstate);
+  c.lperm = (int16_t*)(ws + L.lperm);
+  c.lbest_left = (double*)(ws + L.lbest);
+  c.ghist = (void*)(ws + L.ghist);
+  c.lcursor = (int32_t*)(ws + L.lcursor);
+  c.large_cap = L.large_cap;
+  c.wave_max = (int)a->wave_max; c.block_max = (int)a->block_max; c.chunk = (int)a->chunk;
+  c.kg_wave = (int)a->kg_wave; c.kg_block = (int)a->kg_block; c.kg_large = (int)a->kg_large;
+  c.slack_wave = (int)a->slack_wave;
+  return c;
+}
+
+static int g_last_err_line = 0;
+static hipError_t g_last_err = hipSuccess;
+#define HIP_OK(x)                                       \
+  do {                                                  \
+    hipError_t e_ = (x);                                \
+    if (e_ != hipSuccess) {                             \
+      g_last_err = e_; g_last_err_line = __LINE__;      \
+      return 100 + (int)e_;                             \
+    }                                                   \
+  } while (0)
+
+static int32_t* pinned_counters() {
+  static int32_t* p = nullptr;
+  if (!p) {
+    if (hipHostMalloc((void**)&p, 64 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess) p = nullptr;
+  }
+  return p;
+}
+
+}  // namespace dml
+
+using namespace dml;
+
+extern "C" {
+
+const char* dml_forest_last_error(int* line) {
+  if (line) *line = g_last_err_line;
+  return hipGetErrorString(g_last_err);
+}
+
+int dml_forest_sizeof_treespec() { return (int)sizeof(TreeSpec); }
+int dml_forest_sizeof_args() { return (int)sizeof(ForestArgs); }
+int dml_forest_sizeof_node() { return (int)sizeof(NodeRec); }
+
+// bytes of workspace the build needs (rows_total, d, classes, tiers must be set);
+// the rows_a buffer (rows_total uint32) is carved right after it.
+int64_t dml_forest_workspace_bytes(const ForestArgs* a) {
+  Layout L = plan(a);
+  return (int64_t)(L.total + align_up((size_t)a->rows_total * 4, 256));
+}
+
+// phase 1: count active (train & bootstrap weight > 0) rows per tree into a->active_count
+int dml_forest_count(ForestArgs* a, hipStream_t st) {
+  Ctx c{};
+  c.n = (int)a->n; c.roles = (const uint8_t*)a->roles; c.specs = (const TreeSpec*)a->specs;
+  c.active_count = (int32_t*)a->active_count;
+  HIP_OK(hipMemsetAsync(c.active_count, 0, a->T * 4, st));
+  dim3 grid((unsigned)((a->n + 1023) / 1024), (unsigned)a->T);
+  k_count_active<<<grid, 256, 0, st>>>(c);
+  HIP_OK(hipGetLastError());
+  return 0;
+}
+
+// phase 2: build every tree; status_out: 0 ok, 1 node-pool overflow, 4 open-list overflow
+int dml_forest_build(ForestArgs* a, hipStream_t st) {
+  Layout L = plan(a);
+  if ((size_t)a->workspace_bytes < (size_t)dml_forest_workspace_bytes(a)) return 2;
+  Ctx c = make_ctx(a, L);
+  uint32_t* rows_a = (uint32_t*)(((unsigned char*)a->workspace) + L.total);
+  c.rows_cur = rows_a;
+  int32_t* h = pinned_counters();
+  if (!h) return 3;
+  const bool reg = a->is_reg != 0;
+  if (!reg && (a->n_classes < 1 || a->n_classes > kMaxClasses)) return 5;
+  if (a->d > 32767) return 6;
+
+  HIP_OK(hipMemsetAsync(c.counters, 0, kNumCounters * 4, st));
+  HIP_OK(hipMemsetAsync(c.cursors, 0, a->T * 4, st));
+  HIP_OK(hipMemsetAsync(c.node_val, 0, (size_t)a->T * c.VC * 8, st));
+  k_init_counters<<<1, 1, 0, st>>>(c);
+  dim3 gfill((unsigned)((a->n + 1023) / 1024), (unsigned)a->T);
+  if (reg) k_fill_active<true><<<gfill, 256, 0, st>>>(c);
+  else k_fill_active<false><<<gfill, 256, 0, st>>>(c);
+  k_roots<<<(unsigned)((a->T + 255) / 256), 256, 0, st>>>(c);
+  HIP_OK(hipGetLastError());
+
+  const size_t lds_w = fused_lds(a, (int)a->kg_wave);
+  const size_t lds_b = fused_lds(a, (int)a->kg_block);
+  const int CH = c.CH;
+  const size_t lds_hl = (size_t)a->kg_large * CH * 256 * 4;
+  const size_t lds_sl = lds_hl + a->kg_large * 16 + 64;
+  const size_t lds_max = 160 * 1024;
+  if (lds_w > lds_max || lds_b > lds_max || lds_sl > lds_max) return 7;
+  {
+    const int need = (int)std::max(lds_w, std::max(lds_b, lds_sl));
+    static int attr_set = 0;
+    if (need > 64 * 1024 && need > attr_set) {
+      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<256, true>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_hist_large<false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_hist_large<true>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_split_large<false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_split_large<true>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      attr_set = need;
+    }
+  }
+  const unsigned nchunks = (unsigned)((a->max_active + a->chunk - 1) / a->chunk);
+  int cur = 0, levels = 0, large_rounds = 0;
+  while (true) {
+    HIP_OK(hipMemcpyAsync(h, c.counters, kNumCounters * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (h[kOpenOvf]) { a->status_out = 4; break; }
+    const int nw = h[cur * 3 + 0], nb = h[cur * 3 + 1], nL = h[cur * 3 + 2];
+    if (nw + nb + nL == 0) break;
+    if (++levels > 1 << 20) return 8;
+    HIP_OK(hipMemsetAsync(c.counters + (1 - cur) * 3, 0, 12, st));
+    if (nw) {
+      if (reg) k_nodes<64, true><<<nw, 64, lds_w, st>>>(c, 0, cur);
+      else k_nodes<64, false><<<nw, 64, lds_w, st>>>(c, 0, cur);
+    }
+    if (nb) {
+      if (reg) k_nodes<256, true><<<nb, 256, lds_b, st>>>(c, 1, cur);
+      else k_nodes<256, false><<<nb, 256, lds_b, st>>>(c, 1, cur);
+    }
+    if (nL) {
+      k_large_prep<<<(nL + 63) / 64, 64, 0, st>>>(c, cur, nL);
+      while (true) {
+        ++large_rounds;
+        HIP_OK(hipMemsetAsync(c.ghist, 0, (size_t)nL * a->kg_large * CH * 256 * 4, st));
+        HIP_OK(hipMemsetAsync(c.counters + kNeedMore, 0, 4, st));
+        dim3 gh(nchunks, (unsigned)nL);
+        if (reg) {
+          k_hist_large<true><<<gh, 256, lds_hl, st>>>(c);
+          k_split_large<true><<<nL, 256, lds_sl, st>>>(c, cur);
+        } else {
+          k_hist_large<false><<<gh, 256, lds_hl, st>>>(c);
+          k_split_large<false><<<nL, 256, lds_sl, st>>>(c, cur);
+        }
+        HIP_OK(hipMemcpyAsync(h + 32, c.counters + kNeedMore, 4, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        if (!h[32]) break;
+      }
+      k_partition_large<<<dim3(nchunks, (unsigned)nL), 256, 0, st>>>(c);
+    }
+    HIP_OK(hipGetLastError());
+    uint32_t* t = c.rows_cur; c.rows_cur = c.rows_next; c.rows_next = t;
+    cur = 1 - cur;
+  }
+  HIP_OK(hipMemcpyAsync(h, c.counters, kNumCounters * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  a->n_nodes_out = h[kPool];
+  a->levels_out = levels;
+  a->large_rounds_out = large_rounds;
+  if (a->status_out != 4) a->status_out = h[kOverflow] ? 1 : (h[kOpenOvf] ? 4 : 0);
+  return 0;
+}
+
+}  // extern "C"

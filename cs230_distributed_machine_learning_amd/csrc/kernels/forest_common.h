@@ -1,0 +1,162 @@
+// forest_common.h — definitions shared by the HIP forest builder (forest.hip) and the
+// C++ CPU builder (../runtime/forest_cpu.cpp).  Everything that decides the SHAPE of a
+// tree lives here (RNG streams, bootstrap weights, per-node feature order, split
+// scoring, leaf rules), so the two builders grow identical trees and the GPU path can
+// be checked exactly against the CPU path.
+//
+// Semantics follow scikit-learn's BestSplitter/DepthFirstTreeBuilder as used by
+// RandomForest{Classifier,Regressor} (the reference's compute delegate, called at
+// aws-prod/worker/worker.py:315,326,341), re-expressed on 256-bin quantised features:
+//   * leaf if depth>=max_depth, n<min_samples_split, n<2*min_samples_leaf, or pure;
+//   * features are visited in a per-node random order and the search stops after
+//     max_features NON-constant features (constant ones do not count);
+//   * best split = max proxy improvement, first strictly-better wins (ties go to the
+//     earliest visited feature, then the lowest bin);
+//   * split rejected if improvement + eps < min_impurity_decrease.
+// Bootstrap uses Poisson(lambda) per-row weights (lambda = max_samples fraction,
+// 1.0 by default) instead of an exact multinomial draw: same expectation and
+// asymptotic distribution, no per-tree index array, recomputable anywhere.
+//
+// Scores are computed from per-channel sums in a FIXED order with fp-contraction off
+// so both builders evaluate bit-identical doubles.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define DML_HD __host__ __device__ __forceinline__
+#define DML_HDM __host__ __device__ __forceinline__
+#else
+#include <math.h>
+#define DML_HD static inline
+#define DML_HDM inline
+#endif
+
+namespace dml {
+
+constexpr int kBins = 256;        // uint8 bins
+constexpr int kPoisTable = 12;    // Poisson CDF thresholds kept per tree
+constexpr int kMaxClasses = 64;   // classification channels supported by the builders
+
+enum Criterion : int32_t { kGini = 0, kEntropy = 1, kMSE = 2 };
+
+// Per-tree build specification (POD, identical layout on host, device and ctypes).
+struct TreeSpec {
+  uint64_t seed;            // tree seed: bootstrap stream and root node key
+  int32_t split;            // which role vector (split) the tree trains on
+  int32_t fit;              // owning fit index
+  int32_t max_depth;        // INT32_MAX for None
+  int32_t min_samples_split;
+  int32_t min_samples_leaf;
+  int32_t max_features;     // k (>=1, <= n_features)
+  int32_t bootstrap;        // 0/1
+  int32_t criterion;        // Criterion
+  float min_impurity_decrease;
+  float pad0;
+  uint32_t pois_cdf[kPoisTable];  // P(K<=j) * 2^32 (saturated), j = 0..11
+};
+
+// node record written by both builders
+struct NodeRec {
+  int32_t split;  // feature*256 + bin, or -1 for a leaf
+  int32_t left;   // index of left child (right = left + 1), -1 for a leaf
+};
+
+DML_HD int32_t pack_split(int feat, int bin) { return feat * kBins + bin; }
+
+// ---- RNG ------------------------------------------------------------------------
+DML_HD uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+DML_HD uint32_t hash_u32(uint64_t key, uint64_t ctr) {
+  return (uint32_t)(splitmix64(key ^ splitmix64(ctr + 0x632BE59BD9B4E019ull)) >> 32);
+}
+
+// bootstrap weight of `row` for the tree
+DML_HD uint32_t boot_weight(const TreeSpec& t, uint32_t row) {
+  if (!t.bootstrap) return 1u;
+  const uint32_t u = hash_u32(t.seed, 0xB0075ull * 0x100000000ull + row);
+  uint32_t k = 0;
+  while (k < (uint32_t)kPoisTable && u >= t.pois_cdf[k]) ++k;
+  return k;
+}
+
+DML_HD uint64_t root_key(uint64_t seed) { return splitmix64(seed ^ 0x7EE5EEDull); }
+
+DML_HD uint64_t child_key(uint64_t parent, int side) {
+  return splitmix64(parent * 0x9E3779B97F4A7C15ull + 0x51ED27ull + (uint64_t)side);
+}
+
+// swap target for position `pos` of the node's lazy Fisher-Yates feature permutation
+DML_HD int perm_pick(uint64_t node_key, int pos, int n_features) {
+  const uint32_t h = hash_u32(node_key, 0xFEA7ull + (uint64_t)pos);
+  const uint32_t span = (uint32_t)(n_features - pos);
+  return pos + (int)(((uint64_t)h * span) >> 32);
+}
+
+// ---- impurity from channel sums ----------------------------------------------------
+#if defined(__HIPCC__)
+#pragma clang fp contract(off)
+#endif
+
+DML_HD double dlog2(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return ::log2(x);
+#else
+  return log2(x);
+#endif
+}
+
+// Accumulator for one side of a classification split, fed class sums in class order.
+struct ClsAcc {
+  double w, sq, clogc;
+  DML_HDM void init() { w = 0.0; sq = 0.0; clogc = 0.0; }
+  DML_HDM void add(double c) {
+    w += c;
+    sq += c * c;
+    if (c > 0.0) clogc += c * dlog2(c);
+  }
+};
+
+// impurity of a node from its accumulator
+DML_HD double cls_impurity(const ClsAcc& a, int crit) {
+  if (a.w <= 0.0) return 0.0;
+  if (crit == kEntropy) return dlog2(a.w) - a.clogc / a.w;   // -sum p log2 p
+  return 1.0 - a.sq / (a.w * a.w);                           // gini
+}
+
+// proxy improvement (larger is better) ~ -(wl*imp_l + wr*imp_r) up to a constant
+DML_HD double cls_proxy(const ClsAcc& l, const ClsAcc& r, int crit) {
+  if (crit == kEntropy) return (l.clogc - l.w * dlog2(l.w)) + (r.clogc - r.w * dlog2(r.w));
+  return l.sq / l.w + r.sq / r.w;
+}
+
+// regression: s0 = sum w, s1 = sum w*y, s2 = sum w*y^2
+DML_HD double mse_impurity(double s0, double s1, double s2) {
+  if (s0 <= 0.0) return 0.0;
+  const double m = s1 / s0;
+  return s2 / s0 - m * m;
+}
+
+DML_HD double mse_proxy(double l0, double l1, double r0, double r1) {
+  return l1 * l1 / l0 + r1 * r1 / r0;
+}
+
+// sklearn's impurity_improvement(), scaled by the node's share of the tree's weight
+DML_HD double improvement(double W_tree, double W_node, double imp_node, double wl, double imp_l,
+                          double wr, double imp_r) {
+  return (W_node / W_tree) * (imp_node - (wr / W_node) * imp_r - (wl / W_node) * imp_l);
+}
+
+constexpr double kEps = 1e-7;  // sklearn EPSILON for purity / min_impurity_decrease tests
+
+// leaf-by-counts rule (before any split search)
+DML_HD bool leaf_by_counts(const TreeSpec& t, int count, int depth) {
+  return depth >= t.max_depth || count < t.min_samples_split || count < 2 * t.min_samples_leaf;
+}
+
+}  // namespace dml

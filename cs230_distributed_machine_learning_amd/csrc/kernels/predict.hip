@@ -1,0 +1,178 @@
+// predict.hip — batched forest inference and fused per-fit scoring (K6 + K10).
+//
+// The reference predicts once per fit and scores with sklearn metrics
+// (aws-prod/worker/worker.py:322-323 accuracy, :336-338 r2/mse, and inside
+// cross_val_score :326/:341).  Here one launch predicts the held-out rows of EVERY
+// fit of a batch (grid.y = fit), each thread walking all trees of its fit for one
+// row against the HBM-resident binned matrix; a second launch reduces per-fit score
+// statistics (correct count / SSE / sum y / sum y^2) so the host gets F x 4 doubles.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "forest_common.h"
+
+namespace dml {
+
+struct PredictArgs {
+  int64_t Xb, ld;
+  int64_t nodes, node_val, VC, is_reg, n_classes;
+  int64_t fit_tree_off;  // int32[F+1]: trees of fit f are [off[f], off[f+1]) (tree t's root = node t)
+  int64_t fit_row_off;   // int64[F+1]: rows of fit f in rows[] are [off[f], off[f+1])
+  int64_t rows;          // int32[]: row indices to predict
+  int64_t out_pred;      // int32 class id (cls) or float (reg), aligned with rows[]
+  int64_t out_proba;     // float [len(rows)][C] or 0
+  int64_t F, max_rows;
+};
+
+template <int MAXC>
+__global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
+  const int f = blockIdx.y;
+  const int32_t* toff = (const int32_t*)a.fit_tree_off;
+  const int64_t* roff = (const int64_t*)a.fit_row_off;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r0 = roff[f], nr = roff[f + 1] - r0;
+  if (i >= nr) return;
+  const int C = (int)a.n_classes;
+  const int32_t row = ((const int32_t*)a.rows)[r0 + i];
+  const uint8_t* xr = (const uint8_t*)a.Xb + (int64_t)row * a.ld;
+  const NodeRec* nodes = (const NodeRec*)a.nodes;
+  const double* val = (const double*)a.node_val;
+  float p[MAXC];
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) p[k] = 0.f;
+  for (int t = toff[f]; t < toff[f + 1]; ++t) {
+    int node = t;
+    NodeRec nr_ = nodes[node];
+    for (int steps = 0; nr_.split >= 0 && steps < 1 << 20; ++steps) {
+      const int b = xr[nr_.split >> 8];
+      node = nr_.left + (b > (nr_.split & 255) ? 1 : 0);
+      nr_ = nodes[node];
+    }
+    const double* v = val + (int64_t)node * a.VC;
+    double W = 0.0;
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k)
+      if (k < C) W += v[k];
+    if (W > 0.0) {
+      const double inv = 1.0 / W;
+#pragma unroll
+      for (int k = 0; k < MAXC; ++k)
+        if (k < C) p[k] += (float)(v[k] * inv);
+    }
+  }
+  int best = 0;
+  float bv = p[0];
+#pragma unroll
+  for (int k = 1; k < MAXC; ++k)
+    if (k < C && p[k] > bv) { bv = p[k]; best = k; }
+  ((int32_t*)a.out_pred)[r0 + i] = best;
+  if (a.out_proba) {
+    const float nt = (float)(toff[f + 1] - toff[f]);
+    float* op = (float*)a.out_proba + (r0 + i) * C;
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k)
+      if (k < C) op[k] = p[k] / nt;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_predict_reg(PredictArgs a) {
+  const int f = blockIdx.y;
+  const int32_t* toff = (const int32_t*)a.fit_tree_off;
+  const int64_t* roff = (const int64_t*)a.fit_row_off;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r0 = roff[f], nr = roff[f + 1] - r0;
+  if (i >= nr) return;
+  const int32_t row = ((const int32_t*)a.rows)[r0 + i];
+  const uint8_t* xr = (const uint8_t*)a.Xb + (int64_t)row * a.ld;
+  const NodeRec* nodes = (const NodeRec*)a.nodes;
+  const double* val = (const double*)a.node_val;
+  double acc = 0.0;
+  int nt = 0;
+  for (int t = toff[f]; t < toff[f + 1]; ++t) {
+    int node = t;
+    NodeRec nr_ = nodes[node];
+    for (int steps = 0; nr_.split >= 0 && steps < 1 << 20; ++steps) {
+      const int b = xr[nr_.split >> 8];
+      node = nr_.left + (b > (nr_.split & 255) ? 1 : 0);
+      nr_ = nodes[node];
+    }
+    const double* v = val + (int64_t)node * a.VC;
+    if (v[0] > 0.0) { acc += v[1] / v[0]; ++nt; }
+  }
+  ((float*)a.out_pred)[r0 + i] = nt ? (float)(acc / nt) : 0.f;
+}
+
+// per-fit score statistics: out[f] = {match_count or SSE, sum y, sum y^2, n}
+struct ScoreArgs {
+  int64_t rows;        // int32[] row ids
+  int64_t fit_row_off; // int64[F+1]
+  int64_t pred;        // int32 (cls) / float (reg)
+  int64_t ycls, yreg, is_reg;
+  int64_t out;         // double [F][4]
+  int64_t F;
+};
+
+__global__ __launch_bounds__(256) void k_scores(ScoreArgs a) {
+  const int f = blockIdx.x;
+  const int64_t* roff = (const int64_t*)a.fit_row_off;
+  const int64_t r0 = roff[f], r1 = roff[f + 1];
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  const int32_t* rows = (const int32_t*)a.rows;
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) {
+    const int32_t row = rows[i];
+    if (a.is_reg) {
+      const double y = ((const float*)a.yreg)[row];
+      const double e = (double)((const float*)a.pred)[i] - y;
+      s0 += e * e; s1 += y; s2 += y * y;
+    } else {
+      s0 += ((const int32_t*)a.pred)[i] == ((const int32_t*)a.ycls)[row] ? 1.0 : 0.0;
+    }
+  }
+  __shared__ double red[3][4];
+  for (int off = 32; off >= 1; off >>= 1) {
+    s0 += __shfl_xor(s0, off); s1 += __shfl_xor(s1, off); s2 += __shfl_xor(s2, off);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][w] = s0; red[1][w] = s1; red[2][w] = s2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double* o = (double*)a.out + 4 * f;
+    o[0] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    o[1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    o[2] = red[2][0] + red[2][1] + red[2][2] + red[2][3];
+    o[3] = (double)(r1 - r0);
+  }
+}
+
+}  // namespace dml
+
+using namespace dml;
+
+extern "C" {
+
+int dml_predict_sizeof_args() { return (int)sizeof(PredictArgs); }
+
+int dml_forest_predict(PredictArgs* a, hipStream_t st) {
+  if (a->F <= 0 || a->max_rows <= 0) return 0;
+  dim3 grid((unsigned)((a->max_rows + 255) / 256), (unsigned)a->F);
+  if (a->is_reg) {
+    k_predict_reg<<<grid, 256, 0, st>>>(*a);
+  } else {
+    const int C = (int)a->n_classes;
+    if (C <= 2) k_predict_cls<2><<<grid, 256, 0, st>>>(*a);
+    else if (C <= 4) k_predict_cls<4><<<grid, 256, 0, st>>>(*a);
+    else if (C <= 8) k_predict_cls<8><<<grid, 256, 0, st>>>(*a);
+    else if (C <= 16) k_predict_cls<16><<<grid, 256, 0, st>>>(*a);
+    else if (C <= 32) k_predict_cls<32><<<grid, 256, 0, st>>>(*a);
+    else if (C <= 64) k_predict_cls<64><<<grid, 256, 0, st>>>(*a);
+    else return 5;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+int dml_scores(ScoreArgs* a, hipStream_t st) {
+  if (a->F <= 0) return 0;
+  k_scores<<<(unsigned)a->F, 256, 0, st>>>(*a);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+}  // extern "C"

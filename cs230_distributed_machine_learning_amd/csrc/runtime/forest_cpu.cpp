@@ -1,0 +1,330 @@
+// forest_cpu.cpp — CPU random-forest builder/predictor (the plumbing/CI path).
+//
+// Grows exactly the trees the HIP builder (../kernels/forest.hip) grows: both take
+// every random decision (bootstrap weights, per-node feature order) and every split
+// score from forest_common.h, classification histograms are exact integers, and
+// ties break identically (earliest feature in visit order, then lowest bin).  The GPU
+// builds breadth-first with atomic node allocation; this builds depth-first with a
+// local counter; `dml_cpu_forest_export` renumbers into the GPU's pool layout (tree t's
+// root at index t, children in consecutive pairs) so predictions are comparable
+// element-for-element.
+//
+// Used when no GPU is present (BASELINE config 1: the iris plumbing job) and as the
+// oracle for the HIP kernels' tests.  Trees are built in parallel with OpenMP.
+#include <stdint.h>
+#include <string.h>
+#include <math.h>
+#include <vector>
+#include <algorithm>
+#include "../kernels/forest_common.h"
+
+namespace dml {
+
+struct CpuTree {
+  std::vector<NodeRec> nodes;   // local numbering, root = 0
+  std::vector<double> vals;     // [nodes][VC]
+};
+
+struct CpuForest {
+  int T = 0, VC = 0;
+  std::vector<CpuTree> trees;
+};
+
+struct Data {
+  const uint8_t* Xb; int64_t ld; int n, d, C, CH, VC, is_reg;
+  const int32_t* ycls; const float* yreg; const uint8_t* roles;
+};
+
+struct Job { int node, start, count, depth; uint64_t key; };
+
+static void build_tree(const Data& D, const TreeSpec& s, CpuTree& out) {
+  const uint8_t* role = D.roles + (int64_t)s.split * D.n;
+  std::vector<uint32_t> rows, tmp;
+  std::vector<uint32_t> wts;  // indexed by row id through a parallel array
+  rows.reserve(D.n);
+  std::vector<uint32_t> wrow(D.n, 0);
+  std::vector<double> root(D.VC, 0.0);
+  for (int r = 0; r < D.n; ++r) {
+    if (role[r] != 1) continue;
+    const uint32_t w = boot_weight(s, (uint32_t)r);
+    if (!w) continue;
+    rows.push_back((uint32_t)r);
+    wrow[r] = w;
+    if (D.is_reg) {
+      const double y = (double)D.yreg[r];
+      root[0] += (double)w; root[1] += (double)w * y; root[2] += (double)w * y * y;
+    } else {
+      root[D.ycls[r]] += (double)w;
+    }
+  }
+  tmp.resize(rows.size());
+  out.nodes.clear(); out.vals.clear();
+  NodeRec leaf{-1, -1};
+  out.nodes.push_back(leaf);
+  out.vals.insert(out.vals.end(), root.begin(), root.end());
+  double Wt = 0.0;
+  if (D.is_reg) Wt = root[0];
+  else for (int k = 0; k < D.C; ++k) Wt += root[k];
+
+  auto impurity_of = [&](const double* v) {
+    if (D.is_reg) return mse_impurity(v[0], v[1], v[2]);
+    ClsAcc a; a.init();
+    for (int k = 0; k < D.C; ++k) a.add(v[k]);
+    return cls_impurity(a, s.criterion);
+  };
+  auto visit = [&](int count, int depth, const double* v) {
+    return !(leaf_by_counts(s, count, depth) || impurity_of(v) <= kEps);
+  };
+
+  std::vector<Job> stack;
+  if (!rows.empty() && visit((int)rows.size(), 0, root.data())) stack.push_back({0, 0, (int)rows.size(), 0, root_key(s.seed)});
+  const int CH = D.CH;
+  std::vector<uint32_t> hu((size_t)CH * 256);
+  std::vector<float> hf((size_t)CH * 256);
+  std::vector<int16_t> perm(D.d);
+  std::vector<double> best_left(CH), cand_left(CH);
+  while (!stack.empty()) {
+    Job jb = stack.back();
+    stack.pop_back();
+    for (int i = 0; i < D.d; ++i) perm[i] = (int16_t)i;
+    int pos = 0, nonconst = 0, best_feat = -1, best_bin = -1;
+    double best_gain = -INFINITY;
+    const uint32_t* nr = rows.data() + jb.start;
+    while (nonconst < s.max_features && pos < D.d) {
+      const int t = perm_pick(jb.key, pos, D.d);
+      std::swap(perm[pos], perm[t]);
+      const int f = perm[pos];
+      ++pos;
+      double g_best = -INFINITY;
+      int b_best = -1;
+      bool nc = false;
+      if (!D.is_reg) {
+        std::fill(hu.begin(), hu.end(), 0u);
+        for (int i = 0; i < jb.count; ++i) {
+          const uint32_t r = nr[i];
+          const int b = D.Xb[(int64_t)r * D.ld + f];
+          hu[D.ycls[r] * 256 + b] += wrow[r];
+          hu[D.C * 256 + b] += 1u;
+        }
+        for (int ch = 0; ch < CH; ++ch)
+          for (int b = 1; b < 256; ++b) hu[ch * 256 + b] += hu[ch * 256 + b - 1];
+        const uint32_t tot_rows = hu[D.C * 256 + 255];
+        for (int b = 0; b < 255; ++b) {
+          const uint32_t rl = hu[D.C * 256 + b], rr = tot_rows - rl;
+          nc |= (rl > 0 && rr > 0);
+          if (rl < (uint32_t)s.min_samples_leaf || rr < (uint32_t)s.min_samples_leaf) continue;
+          ClsAcc L, R; L.init(); R.init();
+          for (int k = 0; k < D.C; ++k) {
+            const double lc = (double)hu[k * 256 + b], tc = (double)hu[k * 256 + 255];
+            L.add(lc); R.add(tc - lc);
+          }
+          const double g = cls_proxy(L, R, s.criterion);
+          if (g > g_best) { g_best = g; b_best = b; }
+        }
+        if (nc) {
+          ++nonconst;
+          if (b_best >= 0 && g_best > best_gain) {
+            best_gain = g_best; best_feat = f; best_bin = b_best;
+            for (int ch = 0; ch < CH; ++ch) best_left[ch] = (double)hu[ch * 256 + b_best];
+          }
+        }
+      } else {
+        std::fill(hf.begin(), hf.end(), 0.f);
+        for (int i = 0; i < jb.count; ++i) {
+          const uint32_t r = nr[i];
+          const int b = D.Xb[(int64_t)r * D.ld + f];
+          const float fw = (float)wrow[r], y = D.yreg[r], wy = fw * y;
+          hf[b] += fw; hf[256 + b] += wy; hf[512 + b] += wy * y; hf[768 + b] += 1.f;
+        }
+        for (int ch = 0; ch < CH; ++ch)
+          for (int b = 1; b < 256; ++b) hf[ch * 256 + b] += hf[ch * 256 + b - 1];
+        const float tot_rows = hf[768 + 255];
+        for (int b = 0; b < 255; ++b) {
+          const float rl = hf[768 + b], rr = tot_rows - rl;
+          nc |= (rl > 0.f && rr > 0.f);
+          if (rl < (float)s.min_samples_leaf || rr < (float)s.min_samples_leaf) continue;
+          const double l0 = hf[b], t0 = hf[255], l1 = hf[256 + b], t1 = hf[256 + 255];
+          const double g = mse_proxy(l0, l1, t0 - l0, t1 - l1);
+          if (g > g_best) { g_best = g; b_best = b; }
+        }
+        if (nc) {
+          ++nonconst;
+          if (b_best >= 0 && g_best > best_gain) {
+            best_gain = g_best; best_feat = f; best_bin = b_best;
+            for (int ch = 0; ch < CH; ++ch) best_left[ch] = (double)hf[ch * 256 + b_best];
+          }
+        }
+      }
+    }
+    if (best_feat < 0) continue;
+    // accept?
+    const double* pv = out.vals.data() + (size_t)jb.node * D.VC;
+    double impN, impL, impR, wN, wL, wR;
+    if (D.is_reg) {
+      wN = pv[0]; wL = best_left[0]; wR = pv[0] - best_left[0];
+      impN = mse_impurity(pv[0], pv[1], pv[2]);
+      impL = mse_impurity(best_left[0], best_left[1], best_left[2]);
+      impR = mse_impurity(pv[0] - best_left[0], pv[1] - best_left[1], pv[2] - best_left[2]);
+    } else {
+      ClsAcc N, L, R; N.init(); L.init(); R.init();
+      for (int k = 0; k < D.C; ++k) { N.add(pv[k]); L.add(best_left[k]); R.add(pv[k] - best_left[k]); }
+      wN = N.w; wL = L.w; wR = R.w;
+      impN = cls_impurity(N, s.criterion); impL = cls_impurity(L, s.criterion); impR = cls_impurity(R, s.criterion);
+    }
+    const double imp = improvement(Wt, wN, impN, wL, impL, wR, impR);
+    if (imp + kEps < (double)s.min_impurity_decrease) continue;
+    // split
+    const int base = (int)out.nodes.size();
+    out.nodes.push_back(leaf);
+    out.nodes.push_back(leaf);
+    out.vals.resize((size_t)(base + 2) * D.VC);
+    pv = out.vals.data() + (size_t)jb.node * D.VC;
+    double* lv = out.vals.data() + (size_t)base * D.VC;
+    double* rv = lv + D.VC;
+    for (int k = 0; k < D.VC; ++k) { lv[k] = best_left[k]; rv[k] = pv[k] - best_left[k]; }
+    out.nodes[jb.node].split = pack_split(best_feat, best_bin);
+    out.nodes[jb.node].left = base;
+    const int nl = (int)best_left[CH - 1];
+    // stable partition
+    uint32_t* nrw = rows.data() + jb.start;
+    int li = 0, ri = 0;
+    uint32_t* tw = tmp.data();
+    for (int i = 0; i < jb.count; ++i) {
+      const uint32_t r = nrw[i];
+      if (D.Xb[(int64_t)r * D.ld + best_feat] <= best_bin) nrw[li++] = r;
+      else tw[ri++] = r;
+    }
+    memcpy(nrw + li, tw, (size_t)ri * 4);
+    (void)nl;
+    const double* lvv = out.vals.data() + (size_t)base * D.VC;
+    const double* rvv = lvv + D.VC;
+    // push right first so the left subtree is processed first (depth-first, left-major)
+    if (visit(jb.count - li, jb.depth + 1, rvv))
+      stack.push_back({base + 1, jb.start + li, jb.count - li, jb.depth + 1, child_key(jb.key, 1)});
+    if (visit(li, jb.depth + 1, lvv))
+      stack.push_back({base, jb.start, li, jb.depth + 1, child_key(jb.key, 0)});
+  }
+}
+
+}  // namespace dml
+
+using namespace dml;
+
+extern "C" {
+
+int dml_cpu_sizeof_treespec() { return (int)sizeof(TreeSpec); }
+
+void* dml_cpu_forest_build(const uint8_t* Xb, int64_t ld, int64_t n, int64_t d, const int32_t* ycls,
+                           const float* yreg, int64_t n_classes, int64_t is_reg, const uint8_t* roles,
+                           const TreeSpec* specs, int64_t T) {
+  Data D;
+  D.Xb = Xb; D.ld = ld; D.n = (int)n; D.d = (int)d; D.is_reg = (int)is_reg;
+  D.C = is_reg ? 1 : (int)n_classes;
+  D.CH = is_reg ? 4 : (int)n_classes + 1;
+  D.VC = is_reg ? 3 : (int)n_classes;
+  D.ycls = ycls; D.yreg = yreg; D.roles = roles;
+  CpuForest* F = new CpuForest();
+  F->T = (int)T;
+  F->VC = D.VC;
+  F->trees.resize(T);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t t = 0; t < T; ++t) build_tree(D, specs[t], F->trees[t]);
+  return F;
+}
+
+int64_t dml_cpu_forest_num_nodes(void* h) {
+  CpuForest* F = (CpuForest*)h;
+  int64_t s = 0;
+  for (auto& t : F->trees) s += (int64_t)t.nodes.size();
+  return s;
+}
+
+// export into the GPU pool layout: root of tree t at index t, then each tree's
+// non-root nodes contiguously (children pairs stay adjacent).
+void dml_cpu_forest_export(void* h, NodeRec* nodes, double* vals) {
+  CpuForest* F = (CpuForest*)h;
+  int64_t next = F->T;
+  for (int t = 0; t < F->T; ++t) {
+    const CpuTree& tr = F->trees[t];
+    const int64_t base = next;
+    auto gidx = [&](int64_t local) { return local == 0 ? (int64_t)t : base + local - 1; };
+    for (size_t i = 0; i < tr.nodes.size(); ++i) {
+      NodeRec r = tr.nodes[i];
+      if (r.left >= 0) r.left = (int32_t)gidx(r.left);
+      const int64_t g = gidx((int64_t)i);
+      nodes[g] = r;
+      memcpy(vals + g * F->VC, tr.vals.data() + i * F->VC, sizeof(double) * F->VC);
+    }
+    next += (int64_t)tr.nodes.size() - 1;
+  }
+}
+
+void dml_cpu_forest_free(void* h) { delete (CpuForest*)h; }
+
+// predict rows (same accumulation order as predict.hip)
+void dml_cpu_forest_predict(const uint8_t* Xb, int64_t ld, const NodeRec* nodes, const double* val, int64_t VC,
+                            int64_t is_reg, int64_t C, const int32_t* fit_tree_off, const int64_t* fit_row_off,
+                            const int32_t* rows, int64_t F, int32_t* out_cls, float* out_reg, float* out_proba) {
+  for (int64_t f = 0; f < F; ++f) {
+    const int64_t r0 = fit_row_off[f], r1 = fit_row_off[f + 1];
+#pragma omp parallel for schedule(static)
+    for (int64_t i = r0; i < r1; ++i) {
+      const uint8_t* xr = Xb + (int64_t)rows[i] * ld;
+      std::vector<float> p(is_reg ? 1 : C, 0.f);
+      double acc = 0.0;
+      int nt = 0;
+      for (int t = fit_tree_off[f]; t < fit_tree_off[f + 1]; ++t) {
+        int node = t;
+        NodeRec nr = nodes[node];
+        while (nr.split >= 0) {
+          const int b = xr[nr.split >> 8];
+          node = nr.left + (b > (nr.split & 255) ? 1 : 0);
+          nr = nodes[node];
+        }
+        const double* v = val + (int64_t)node * VC;
+        if (is_reg) {
+          if (v[0] > 0.0) { acc += v[1] / v[0]; ++nt; }
+        } else {
+          double W = 0.0;
+          for (int k = 0; k < C; ++k) W += v[k];
+          if (W > 0.0) {
+            const double inv = 1.0 / W;
+            for (int k = 0; k < C; ++k) p[k] += (float)(v[k] * inv);
+          }
+        }
+      }
+      if (is_reg) {
+        out_reg[i] = nt ? (float)(acc / nt) : 0.f;
+      } else {
+        int best = 0;
+        float bv = p[0];
+        for (int k = 1; k < C; ++k)
+          if (p[k] > bv) { bv = p[k]; best = k; }
+        out_cls[i] = best;
+        if (out_proba) {
+          const float ntf = (float)(fit_tree_off[f + 1] - fit_tree_off[f]);
+          for (int k = 0; k < C; ++k) out_proba[i * C + k] = p[k] / ntf;
+        }
+      }
+    }
+  }
+}
+
+// bin X (row-major float32 [n,d]) with per-feature sorted edges [d][255] (+inf padded)
+void dml_cpu_bin(const float* X, int64_t n, int64_t d, const float* edges, uint8_t* out, int64_t ld) {
+#pragma omp parallel for schedule(static)
+  for (int64_t r = 0; r < n; ++r) {
+    for (int64_t f = 0; f < d; ++f) {
+      const float x = X[r * d + f];
+      const float* e = edges + f * 255;
+      int lo = 0, hi = 255;
+      while (lo < hi) {  // count of edges < x
+        const int mid = (lo + hi) >> 1;
+        if (e[mid] < x) lo = mid + 1; else hi = mid;
+      }
+      out[r * ld + f] = (uint8_t)lo;
+    }
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,237 @@
+"""Batched forest build / predict / score on GPU (HIP) or CPU (C++).
+
+The GPU entry points drive ``libdml_hip.so`` (csrc/kernels/forest.hip, predict.hip);
+the CPU ones drive ``libdml_cpu.so`` (csrc/runtime/forest_cpu.cpp).  Both consume the
+same ``TREESPEC_DTYPE`` records and produce the same pool layout:
+
+* ``nodes``  int32 [P, 2] — (feature*256 + bin | -1, left child | -1); right = left+1
+* ``vals``   float64 [P, VC] — class weight sums (classification) or (sum w, sum wy,
+  sum wy^2) (regression)
+* tree ``t`` of the batch has its root at node ``t``.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..utils import native
+
+GINI, ENTROPY, MSE = 0, 1, 2
+INT32_MAX = 2**31 - 1
+
+
+@dataclass
+class ForestTiers:
+    """Node-size tiers of the HIP builder (see forest.hip header)."""
+
+    wave_max: int = 256
+    block_max: int = 16384
+    chunk: int = 16384
+    kg_wave: int = 4
+    kg_block: int = 16
+    kg_large: int = 16
+    slack_wave: int = 0
+
+    def fitted(self, n_channels: int) -> "ForestTiers":
+        """Clamp feature-group sizes to the LDS budget for this channel count."""
+        per_feat = n_channels * 256 * 4
+        t = ForestTiers(**self.__dict__)
+        t.kg_wave = max(1, min(self.kg_wave, (24 * 1024) // per_feat))
+        t.kg_block = max(1, min(self.kg_block, (96 * 1024) // per_feat))
+        t.kg_large = max(1, min(self.kg_large, (96 * 1024) // per_feat, 64))
+        return t
+
+
+@dataclass
+class ForestBuild:
+    nodes: object  # torch.Tensor (cuda) or np.ndarray
+    vals: object
+    n_trees: int
+    VC: int
+    is_reg: bool
+    n_classes: int
+    stats: dict = field(default_factory=dict)
+
+    @property
+    def on_gpu(self) -> bool:
+        return isinstance(self.nodes, torch.Tensor) and self.nodes.is_cuda
+
+    def to_numpy(self) -> "ForestBuild":
+        if isinstance(self.nodes, torch.Tensor):
+            return ForestBuild(self.nodes.cpu().numpy(), self.vals.cpu().numpy(), self.n_trees, self.VC,
+                               self.is_reg, self.n_classes, dict(self.stats))
+        return self
+
+
+def make_specs(n: int) -> np.ndarray:
+    return np.zeros(n, dtype=native.TREESPEC_DTYPE)
+
+
+def _pool_bound(counts: np.ndarray, specs: np.ndarray) -> int:
+    msl = np.maximum(specs["min_samples_leaf"].astype(np.int64), 1)
+    leaves = np.maximum(counts // msl, 1)
+    depth = specs["max_depth"].astype(np.int64)
+    depth_cap = np.where(depth < 40, (np.int64(2) ** np.minimum(depth + 1, 40)) - 1, np.int64(2**62))
+    per = np.minimum(2 * leaves + 1, depth_cap)
+    return int(per.sum()) + 16
+
+
+def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,
+              specs: np.ndarray, n_classes: int, is_reg: bool, tiers: ForestTiers | None = None) -> ForestBuild:
+    lib = native.hip_lib()
+    dev = Xb.device
+    T = len(specs)
+    n, d = Xb.shape
+    CH = 4 if is_reg else n_classes + 1
+    VC = 3 if is_reg else n_classes
+    tiers = (tiers or ForestTiers()).fitted(CH)
+    stream = native.stream_handle(dev)
+    specs_dev = torch.from_numpy(specs.view(np.uint8).copy()).to(dev)
+    active = torch.zeros(T, dtype=torch.int32, device=dev)
+    a = native.ForestArgs()
+    a.Xb, a.ld, a.n, a.d = native.ptr(Xb), Xb.stride(0), n, d
+    a.ycls = native.ptr(ycls) if ycls is not None else 0
+    a.yreg = native.ptr(yreg) if yreg is not None else 0
+    a.n_classes, a.is_reg = (n_classes if not is_reg else 1), int(is_reg)
+    a.roles, a.n_splits = native.ptr(roles), roles.shape[0]
+    a.specs, a.T = native.ptr(specs_dev), T
+    a.active_count = native.ptr(active)
+    t0 = time.perf_counter()
+    rc = lib.dml_forest_count(ctypes.byref(a), stream)
+    if rc:
+        raise RuntimeError(f"dml_forest_count failed ({rc}): {native.hip_error(lib)}")
+    counts = active.cpu().numpy().astype(np.int64)
+    row_off = np.zeros(T + 1, dtype=np.int64)
+    np.cumsum(counts, out=row_off[1:])
+    row_off_dev = torch.from_numpy(row_off).to(dev)
+    a.row_off = native.ptr(row_off_dev)
+    a.rows_total = int(row_off[-1])
+    a.max_active = int(counts.max()) if T else 0
+    pool_cap = _pool_bound(counts, specs) + T
+    a.wave_max, a.block_max, a.chunk = tiers.wave_max, tiers.block_max, tiers.chunk
+    a.kg_wave, a.kg_block, a.kg_large, a.slack_wave = tiers.kg_wave, tiers.kg_block, tiers.kg_large, tiers.slack_wave
+    tree_W = torch.empty(T, dtype=torch.float64, device=dev)
+    a.tree_W = native.ptr(tree_W)
+    ws_bytes = lib.dml_forest_workspace_bytes(ctypes.byref(a))
+    workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    a.workspace, a.workspace_bytes = native.ptr(workspace), ws_bytes
+    for _attempt in range(4):
+        nodes = torch.empty((pool_cap, 2), dtype=torch.int32, device=dev)
+        vals = torch.empty((pool_cap, VC), dtype=torch.float64, device=dev)
+        a.nodes, a.node_val, a.pool_cap = native.ptr(nodes), native.ptr(vals), pool_cap
+        a.status_out = 0
+        rc = lib.dml_forest_build(ctypes.byref(a), stream)
+        if rc:
+            raise RuntimeError(f"dml_forest_build failed ({rc}): {native.hip_error(lib)}")
+        if a.status_out == 1:
+            pool_cap *= 2
+            continue
+        if a.status_out != 0:
+            raise RuntimeError(f"dml_forest_build status {a.status_out}")
+        break
+    else:
+        raise RuntimeError("forest node pool overflow")
+    P = int(a.n_nodes_out)
+    del workspace
+    stats = {"levels": int(a.levels_out), "large_rounds": int(a.large_rounds_out), "nodes": P,
+             "rows_total": int(a.rows_total), "build_s": time.perf_counter() - t0}
+    return ForestBuild(nodes[:P], vals[:P], T, VC, is_reg, n_classes, stats)
+
+
+def build_cpu(Xb: np.ndarray, ycls: Optional[np.ndarray], yreg: Optional[np.ndarray], roles: np.ndarray,
+              specs: np.ndarray, n_classes: int, is_reg: bool) -> ForestBuild:
+    lib = native.cpu_lib()
+    Xb = np.ascontiguousarray(Xb, dtype=np.uint8)
+    roles = np.ascontiguousarray(roles, dtype=np.uint8)
+    specs = np.ascontiguousarray(specs)
+    ycls = None if ycls is None else np.ascontiguousarray(ycls, dtype=np.int32)
+    yreg = None if yreg is None else np.ascontiguousarray(yreg, dtype=np.float32)
+    n, d = Xb.shape
+    T = len(specs)
+    VC = 3 if is_reg else n_classes
+    t0 = time.perf_counter()
+    h = lib.dml_cpu_forest_build(native.ptr(Xb), d, n, d, native.ptr(ycls), native.ptr(yreg),
+                                 (1 if is_reg else n_classes), int(is_reg), native.ptr(roles), native.ptr(specs), T)
+    try:
+        P = lib.dml_cpu_forest_num_nodes(h)
+        nodes = np.empty((P, 2), dtype=np.int32)
+        vals = np.empty((P, VC), dtype=np.float64)
+        lib.dml_cpu_forest_export(h, native.ptr(nodes), native.ptr(vals))
+    finally:
+        lib.dml_cpu_forest_free(h)
+    return ForestBuild(nodes, vals, T, VC, is_reg, n_classes, {"nodes": int(P), "build_s": time.perf_counter() - t0})
+
+
+def predict(fb: ForestBuild, Xb, fit_tree_off: np.ndarray, fit_row_off: np.ndarray, rows, want_proba: bool = False):
+    """Predict rows for F fits; trees of fit f are [fit_tree_off[f], fit_tree_off[f+1])."""
+    F = len(fit_tree_off) - 1
+    total = int(fit_row_off[-1])
+    C = fb.n_classes
+    if fb.on_gpu:
+        dev = Xb.device
+        lib = native.hip_lib()
+        toff = torch.from_numpy(np.asarray(fit_tree_off, dtype=np.int32)).to(dev)
+        roff = torch.from_numpy(np.asarray(fit_row_off, dtype=np.int64)).to(dev)
+        rows_t = rows if isinstance(rows, torch.Tensor) else torch.from_numpy(np.asarray(rows, np.int32)).to(dev)
+        out = torch.empty(total, dtype=torch.float32 if fb.is_reg else torch.int32, device=dev)
+        proba = torch.empty((total, C), dtype=torch.float32, device=dev) if (want_proba and not fb.is_reg) else None
+        p = native.PredictArgs()
+        p.Xb, p.ld = native.ptr(Xb), Xb.stride(0)
+        p.nodes, p.node_val, p.VC, p.is_reg, p.n_classes = native.ptr(fb.nodes), native.ptr(fb.vals), fb.VC, int(fb.is_reg), C
+        p.fit_tree_off, p.fit_row_off, p.rows = native.ptr(toff), native.ptr(roff), native.ptr(rows_t)
+        p.out_pred, p.out_proba = native.ptr(out), native.ptr(proba)
+        p.F = F
+        p.max_rows = int(np.max(np.diff(fit_row_off))) if F else 0
+        rc = lib.dml_forest_predict(ctypes.byref(p), native.stream_handle(dev))
+        if rc:
+            raise RuntimeError(f"dml_forest_predict failed ({rc})")
+        return (out, proba) if want_proba else out
+    lib = native.cpu_lib()
+    Xb = np.ascontiguousarray(Xb)
+    rows_np = np.ascontiguousarray(rows, dtype=np.int32)
+    toff = np.ascontiguousarray(fit_tree_off, dtype=np.int32)
+    roff = np.ascontiguousarray(fit_row_off, dtype=np.int64)
+    nodes = np.ascontiguousarray(fb.nodes, dtype=np.int32)
+    vals = np.ascontiguousarray(fb.vals, dtype=np.float64)
+    out_cls = np.empty(total, dtype=np.int32) if not fb.is_reg else None
+    out_reg = np.empty(total, dtype=np.float32) if fb.is_reg else None
+    proba = np.empty((total, C), dtype=np.float32) if (want_proba and not fb.is_reg) else None
+    lib.dml_cpu_forest_predict(native.ptr(Xb), Xb.shape[1], native.ptr(nodes), native.ptr(vals), fb.VC, int(fb.is_reg), C,
+                               native.ptr(toff), native.ptr(roff), native.ptr(rows_np), F, native.ptr(out_cls),
+                               native.ptr(out_reg), native.ptr(proba))
+    out = out_reg if fb.is_reg else out_cls
+    return (out, proba) if want_proba else out
+
+
+def score_stats(rows, fit_row_off: np.ndarray, pred, ycls=None, yreg=None, is_reg: bool = False) -> np.ndarray:
+    """[F, 4] = (correct | SSE, sum y, sum y^2, n) per fit — fused K10 kernel on GPU."""
+    F = len(fit_row_off) - 1
+    if isinstance(pred, torch.Tensor) and pred.is_cuda:
+        dev = pred.device
+        out = torch.empty((F, 4), dtype=torch.float64, device=dev)
+        roff = torch.from_numpy(np.asarray(fit_row_off, dtype=np.int64)).to(dev)
+        s = native.ScoreArgs()
+        s.rows, s.fit_row_off, s.pred = native.ptr(rows), native.ptr(roff), native.ptr(pred)
+        s.ycls, s.yreg, s.is_reg = native.ptr(ycls), native.ptr(yreg), int(is_reg)
+        s.out, s.F = native.ptr(out), F
+        rc = native.hip_lib().dml_scores(ctypes.byref(s), native.stream_handle(dev))
+        if rc:
+            raise RuntimeError("dml_scores failed")
+        return out.cpu().numpy()
+    rows = np.asarray(rows)
+    out = np.zeros((F, 4), dtype=np.float64)
+    for f in range(F):
+        r = rows[fit_row_off[f]:fit_row_off[f + 1]]
+        p = np.asarray(pred)[fit_row_off[f]:fit_row_off[f + 1]]
+        if is_reg:
+            y = np.asarray(yreg)[r].astype(np.float64)
+            out[f] = (np.sum((p.astype(np.float64) - y) ** 2), y.sum(), (y * y).sum(), len(r))
+        else:
+            out[f] = (np.sum(p == np.asarray(ycls)[r]), 0.0, 0.0, len(r))
+    return out

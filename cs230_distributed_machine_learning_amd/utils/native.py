@@ -1,0 +1,198 @@
+"""ctypes bindings for the in-tree native libraries.
+
+* ``libdml_hip.so`` — HIP kernels for gfx950 (forest build/predict, binning, scoring,
+  linear-model kernels).  Loaded only when a GPU path runs; if a GPU is present and the
+  library is missing or stale the import FAILS LOUDLY (there is no silent fallback).
+* ``libdml_cpu.so`` — C++ runtime (CPU forest builder used for the no-GPU plumbing
+  config and as the exactness oracle for the HIP builder; scheduler core; binning).
+
+Both are built by ``cs230_distributed_machine_learning_amd.build`` (``__graft_entry__.build``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+from .. import build as _build
+
+_lock = threading.Lock()
+_hip = None
+_cpu = None
+
+c_i64 = ctypes.c_int64
+c_i32 = ctypes.c_int32
+c_vp = ctypes.c_void_p
+
+POIS_TABLE = 12
+
+TREESPEC_DTYPE = np.dtype(
+    [
+        ("seed", "<u8"),
+        ("split", "<i4"),
+        ("fit", "<i4"),
+        ("max_depth", "<i4"),
+        ("min_samples_split", "<i4"),
+        ("min_samples_leaf", "<i4"),
+        ("max_features", "<i4"),
+        ("bootstrap", "<i4"),
+        ("criterion", "<i4"),
+        ("min_impurity_decrease", "<f4"),
+        ("pad0", "<f4"),
+        ("pois_cdf", "<u4", (POIS_TABLE,)),
+    ]
+)
+
+
+def _i64_struct(name: str, fields: list[str]):
+    return type(name, (ctypes.Structure,), {"_fields_": [(f, c_i64) for f in fields]})
+
+
+ForestArgs = _i64_struct(
+    "ForestArgs",
+    [
+        "Xb", "ld", "n", "d",
+        "ycls", "yreg", "n_classes", "is_reg",
+        "roles", "n_splits",
+        "specs", "T",
+        "active_count", "row_off", "rows_total", "max_active",
+        "nodes", "node_val", "pool_cap",
+        "tree_W",
+        "workspace", "workspace_bytes",
+        "wave_max", "block_max", "chunk",
+        "kg_wave", "kg_block", "kg_large", "slack_wave",
+        "n_nodes_out", "status_out", "levels_out", "large_rounds_out",
+    ],
+)
+
+PredictArgs = _i64_struct(
+    "PredictArgs",
+    ["Xb", "ld", "nodes", "node_val", "VC", "is_reg", "n_classes", "fit_tree_off", "fit_row_off", "rows",
+     "out_pred", "out_proba", "F", "max_rows"],
+)
+
+ScoreArgs = _i64_struct("ScoreArgs", ["rows", "fit_row_off", "pred", "ycls", "yreg", "is_reg", "out", "F"])
+
+
+def _load(path: str) -> ctypes.CDLL:
+    return ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
+def cpu_lib() -> ctypes.CDLL:
+    """Load (building if needed) the C++ runtime library."""
+    global _cpu
+    with _lock:
+        if _cpu is None:
+            path = _build.CPU_LIB
+            if not os.path.exists(path) or _build._stale(path, _cpu_sources()):
+                _build.build_cpu()
+            lib = _load(path)
+            lib.dml_cpu_sizeof_treespec.restype = c_i32
+            if lib.dml_cpu_sizeof_treespec() != TREESPEC_DTYPE.itemsize:
+                raise RuntimeError("TreeSpec layout mismatch between C++ and Python")
+            lib.dml_cpu_forest_build.restype = c_vp
+            lib.dml_cpu_forest_build.argtypes = [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64]
+            lib.dml_cpu_forest_num_nodes.restype = c_i64
+            lib.dml_cpu_forest_num_nodes.argtypes = [c_vp]
+            lib.dml_cpu_forest_export.argtypes = [c_vp, c_vp, c_vp]
+            lib.dml_cpu_forest_free.argtypes = [c_vp]
+            lib.dml_cpu_forest_predict.argtypes = [c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp,
+                                                   c_i64, c_vp, c_vp, c_vp]
+            lib.dml_cpu_bin.argtypes = [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64]
+            _cpu = lib
+        return _cpu
+
+
+def _cpu_sources():
+    import glob
+
+    return glob.glob(os.path.join(_build.CSRC, "runtime", "*.cpp")) + glob.glob(os.path.join(_build.CSRC, "kernels", "*.h"))
+
+
+def hip_lib() -> ctypes.CDLL:
+    """Load the HIP kernel library; raises if it is absent (no silent fallback)."""
+    global _hip
+    with _lock:
+        if _hip is None:
+            path = _build.HIP_LIB
+            if not os.path.exists(path):
+                raise RuntimeError(
+                    f"HIP kernel library {path} is missing: run `python -m cs230_distributed_machine_learning_amd.build`"
+                )
+            lib = _load(path)
+            lib.dml_forest_sizeof_treespec.restype = c_i32
+            lib.dml_forest_sizeof_args.restype = c_i32
+            if lib.dml_forest_sizeof_treespec() != TREESPEC_DTYPE.itemsize:
+                raise RuntimeError("TreeSpec layout mismatch between HIP library and Python")
+            if lib.dml_forest_sizeof_args() != ctypes.sizeof(ForestArgs):
+                raise RuntimeError("ForestArgs layout mismatch between HIP library and Python")
+            lib.dml_predict_sizeof_args.restype = c_i32
+            if lib.dml_predict_sizeof_args() != ctypes.sizeof(PredictArgs):
+                raise RuntimeError("PredictArgs layout mismatch between HIP library and Python")
+            lib.dml_forest_last_error.restype = ctypes.c_char_p
+            lib.dml_forest_last_error.argtypes = [ctypes.POINTER(c_i32)]
+            lib.dml_forest_workspace_bytes.restype = c_i64
+            lib.dml_forest_workspace_bytes.argtypes = [ctypes.POINTER(ForestArgs)]
+            lib.dml_forest_count.restype = c_i32
+            lib.dml_forest_count.argtypes = [ctypes.POINTER(ForestArgs), c_vp]
+            lib.dml_forest_build.restype = c_i32
+            lib.dml_forest_build.argtypes = [ctypes.POINTER(ForestArgs), c_vp]
+            lib.dml_forest_predict.restype = c_i32
+            lib.dml_forest_predict.argtypes = [ctypes.POINTER(PredictArgs), c_vp]
+            lib.dml_scores.restype = c_i32
+            lib.dml_scores.argtypes = [ctypes.POINTER(ScoreArgs), c_vp]
+            lib.dml_bin.restype = c_i32
+            lib.dml_bin.argtypes = [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]
+            _register_optional(lib)
+            _hip = lib
+        return _hip
+
+
+def _register_optional(lib) -> None:
+    """Signatures of kernels added in later files (absent symbols are skipped)."""
+    table = {
+        "dml_lr_softmax_grad": (c_i32, [c_vp] * 8 + [c_i64] * 5 + [c_vp]),
+    }
+    for name, (res, args) in table.items():
+        fn = getattr(lib, name, None)
+        if fn is not None:
+            fn.restype = res
+            fn.argtypes = args
+
+
+def hip_error(lib=None) -> str:
+    lib = lib or hip_lib()
+    line = c_i32(0)
+    msg = lib.dml_forest_last_error(ctypes.byref(line))
+    return f"{msg.decode() if msg else '?'} (forest.hip:{line.value})"
+
+
+def ptr(t) -> int:
+    """Device/host address of a torch tensor or numpy array (0 for None)."""
+    if t is None:
+        return 0
+    if isinstance(t, np.ndarray):
+        return int(t.ctypes.data)
+    return int(t.data_ptr())
+
+
+def stream_handle(device=None) -> int:
+    import torch
+
+    return int(torch.cuda.current_stream(device).cuda_stream)
+
+
+def poisson_cdf_table(lam: float) -> np.ndarray:
+    """Thresholds u >= T[j] => weight > j for u uniform on [0, 2^32)."""
+    import math
+
+    out = np.empty(POIS_TABLE, dtype=np.uint64)
+    p = math.exp(-lam)
+    cdf = 0.0
+    for j in range(POIS_TABLE):
+        cdf += p
+        p *= lam / (j + 1)
+        out[j] = min(int(cdf * 2.0**32), 0xFFFFFFFF)
+    return out.astype(np.uint32)

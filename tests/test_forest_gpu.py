@@ -1,0 +1,125 @@
+"""HIP forest builder vs the C++ CPU builder (exact tree equality) and vs sklearn."""
+import numpy as np
+import pytest
+import torch
+
+from cs230_distributed_machine_learning_amd.ops import binning, forest_ops
+from cs230_distributed_machine_learning_amd.search.cv import make_split_roles
+from cs230_distributed_machine_learning_amd.utils import native
+
+pytestmark = pytest.mark.gpu
+
+
+def _specs(n_fits, ntrees, d, **kw):
+    specs = forest_ops.make_specs(n_fits * ntrees)
+    for f in range(n_fits):
+        for t in range(ntrees):
+            s = specs[f * ntrees + t]
+            s["seed"] = 1000 + t
+            s["split"] = f
+            s["fit"] = f
+            s["max_depth"] = kw.get("max_depth", 2**31 - 1)
+            s["min_samples_split"] = kw.get("mss", 2)
+            s["min_samples_leaf"] = kw.get("msl", 1)
+            s["max_features"] = kw.get("k", max(1, int(np.sqrt(d))))
+            s["bootstrap"] = kw.get("bootstrap", 1)
+            s["criterion"] = kw.get("criterion", 0)
+            s["min_impurity_decrease"] = kw.get("mid", 0.0)
+            s["pois_cdf"] = native.poisson_cdf_table(1.0)
+    return specs
+
+
+def _canon(nodes, vals, T):
+    """Canonical pre-order encoding of each tree (independent of node numbering)."""
+    out = []
+    for t in range(T):
+        seq = []
+        stack = [t]
+        while stack:
+            i = stack.pop()
+            s, l = int(nodes[i, 0]), int(nodes[i, 1])
+            seq.append((s, tuple(np.round(vals[i], 6))))
+            if s >= 0:
+                stack.append(l + 1)
+                stack.append(l)
+        out.append(seq)
+    return out
+
+
+def _data(n, d, n_classes=2, seed=0):
+    from sklearn.datasets import make_classification
+
+    X, y = make_classification(n_samples=n, n_features=d, n_informative=max(2, d // 2), n_classes=n_classes,
+                               random_state=seed)
+    return X.astype(np.float32), y
+
+
+@pytest.mark.parametrize("n,d,C,kw", [
+    (3000, 12, 2, {}),
+    (20000, 20, 3, {"msl": 3}),
+    (60000, 16, 2, {"max_depth": 12, "k": 16, "bootstrap": 0}),
+    (5000, 30, 4, {"criterion": 0, "mss": 10}),
+])
+def test_gpu_trees_match_cpu(n, d, C, kw):
+    X, y = _data(n, d, C)
+    dev = torch.device("cuda:0")
+    Xt = torch.from_numpy(X).to(dev)
+    edges = binning.quantile_edges(Xt)
+    Xb = binning.bin_matrix(Xt, edges)
+    Xb_cpu = binning.bin_matrix(torch.from_numpy(X), edges.cpu()).numpy()
+    assert np.array_equal(Xb.cpu().numpy(), Xb_cpu)
+    roles, _ = make_split_roles(y, 3, True, holdout=False)
+    specs = _specs(3, 6, d, **kw)
+    ycls = y.astype(np.int32)
+    g = forest_ops.build_gpu(Xb, torch.from_numpy(ycls).to(dev), None, torch.from_numpy(roles).to(dev), specs, C, False,
+                             forest_ops.ForestTiers(wave_max=64, block_max=2048, chunk=1024))
+    c = forest_ops.build_cpu(Xb_cpu, ycls, None, roles, specs, C, False)
+    assert g.stats["nodes"] == c.stats["nodes"]
+    gc = _canon(g.nodes.cpu().numpy(), g.vals.cpu().numpy(), len(specs))
+    cc = _canon(c.nodes, c.vals, len(specs))
+    assert gc == cc
+    # predictions identical
+    rows, roff = [], [0]
+    for f in range(3):
+        r = np.nonzero(roles[f] == 2)[0]
+        rows.append(r)
+        roff.append(roff[-1] + len(r))
+    rows = np.concatenate(rows).astype(np.int32)
+    roff = np.array(roff)
+    toff = np.arange(4) * 6
+    pg = forest_ops.predict(g, Xb, toff, roff, torch.from_numpy(rows).to(dev)).cpu().numpy()
+    pc = forest_ops.predict(c, Xb_cpu, toff, roff, rows)
+    assert np.array_equal(pg, pc)
+    sg = forest_ops.score_stats(torch.from_numpy(rows).to(dev), roff, torch.from_numpy(pg).to(dev),
+                                ycls=torch.from_numpy(ycls).to(dev))
+    sc = forest_ops.score_stats(rows, roff, pc, ycls=ycls)
+    assert np.allclose(sg, sc)
+
+
+def test_gpu_regression_close_to_cpu():
+    from sklearn.datasets import make_regression
+
+    X, y = make_regression(n_samples=8000, n_features=10, noise=5.0, random_state=1)
+    X = X.astype(np.float32)
+    y = y.astype(np.float32)
+    dev = torch.device("cuda:0")
+    Xt = torch.from_numpy(X).to(dev)
+    edges = binning.quantile_edges(Xt)
+    Xb = binning.bin_matrix(Xt, edges)
+    roles, _ = make_split_roles(y, 3, False, holdout=False)
+    specs = _specs(3, 8, 10, k=10, criterion=2)
+    g = forest_ops.build_gpu(Xb, None, torch.from_numpy(y).to(dev), torch.from_numpy(roles).to(dev), specs, 1, True)
+    c = forest_ops.build_cpu(Xb.cpu().numpy(), None, y, roles, specs, 1, True)
+    rows, roff = [], [0]
+    for f in range(3):
+        r = np.nonzero(roles[f] == 2)[0]
+        rows.append(r)
+        roff.append(roff[-1] + len(r))
+    rows = np.concatenate(rows).astype(np.int32)
+    roff = np.array(roff)
+    toff = np.arange(4) * 8
+    pg = forest_ops.predict(g, Xb, toff, roff, torch.from_numpy(rows).to(dev)).cpu().numpy()
+    pc = forest_ops.predict(c, Xb.cpu().numpy(), toff, roff, rows)
+    r2 = lambda p: 1 - np.sum((p - y[rows]) ** 2) / np.sum((y[rows] - y[rows].mean()) ** 2)
+    assert abs(r2(pg) - r2(pc)) < 0.02
+    assert r2(pg) > 0.8
