@@ -1,0 +1,3 @@
+from .core import MLTaskManager
+
+__all__ = ["MLTaskManager"]

@@ -1,0 +1,93 @@
+"""Device-resident view of one dataset (the unit every fit of a job shares).
+
+The reference worker reloads and re-splits the whole CSV for every task
+(aws-prod/worker/worker.py:406-433, 302-303, 326).  Here a dataset is moved to the
+device once (H2D, or an RCCL broadcast/all-gather across ranks — parallel/data.py),
+its uint8 binned copy is built once on first tree use, and every CV/holdout split
+is a row of a ``uint8 [S, n]`` role tensor (search/cv.py).  Fits only ever read these
+resident buffers.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..search.cv import ROLE_TEST, ROLE_TRAIN
+
+
+class DeviceData:
+    def __init__(self, X, y, classification: bool, device: torch.device | str = "cpu",
+                 classes: Optional[np.ndarray] = None, name: str = ""):
+        self.device = torch.device(device)
+        self.name = name
+        if isinstance(X, torch.Tensor):
+            self.X = X.to(self.device, dtype=torch.float32).contiguous()
+        else:
+            self.X = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).to(self.device)
+        self.n, self.d = self.X.shape
+        self.classification = bool(classification)
+        y_np = y.cpu().numpy() if isinstance(y, torch.Tensor) else np.asarray(y)
+        self.y_host = y_np
+        if self.classification:
+            if classes is None:
+                classes, y_enc = np.unique(y_np, return_inverse=True)
+            else:
+                lookup = {c: i for i, c in enumerate(classes.tolist())}
+                y_enc = np.array([lookup[v] for v in y_np.tolist()], dtype=np.int64)
+            self.classes = classes
+            self.n_classes = len(classes)
+            self.y_enc = y_enc.astype(np.int32)
+            self.y_cls = torch.from_numpy(self.y_enc).to(self.device)
+            self.y_reg = self.y_cls.float()
+        else:
+            self.classes = None
+            self.n_classes = 1
+            self.y_enc = None
+            self.y_cls = None
+            self.y_reg = torch.from_numpy(y_np.astype(np.float32)).to(self.device)
+        self._Xb = None
+        self._edges = None
+        self.roles = None
+        self.split_names: List[str] = []
+        self.test_rows: List[torch.Tensor] = []
+        self.train_rows: List[torch.Tensor] = []
+        self._split_key = None
+
+    @property
+    def is_gpu(self) -> bool:
+        return self.device.type == "cuda"
+
+    # ---- binned copy (trees) -------------------------------------------------------
+    def binned(self):
+        if self._Xb is None:
+            from ..ops import binning
+
+            self._edges = binning.quantile_edges(self.X)
+            self._Xb = binning.bin_matrix(self.X, self._edges)
+        return self._Xb
+
+    @property
+    def edges(self):
+        self.binned()
+        return self._edges
+
+    # ---- splits --------------------------------------------------------------------
+    def set_splits(self, roles: np.ndarray, names: List[str], key=None) -> None:
+        if key is not None and key == self._split_key:
+            return
+        roles = np.ascontiguousarray(roles, dtype=np.uint8)
+        self.roles = torch.from_numpy(roles).to(self.device)
+        self.split_names = list(names)
+        self.test_rows = [torch.from_numpy(np.nonzero(r == ROLE_TEST)[0].astype(np.int32)).to(self.device) for r in roles]
+        self.train_rows = [torch.from_numpy(np.nonzero(r == ROLE_TRAIN)[0].astype(np.int32)).to(self.device) for r in roles]
+        self.train_counts = [int((r == ROLE_TRAIN).sum()) for r in roles]
+        self._split_key = key
+
+    def roles_np(self) -> np.ndarray:
+        return self.roles.cpu().numpy()
+
+    def sync(self):
+        if self.is_gpu:
+            torch.cuda.synchronize(self.device)

@@ -1,0 +1,580 @@
+"""Controller: the API operations of the reference master, over the new engine.
+
+Every route of aws-prod/master/master.py and the scheduler's
+membership routes (aws-prod/scheduler/scheduler.py:95-159) is a method here returning
+``(http_status, payload)``; ``gateway/app.py`` maps them onto HTTP and the client's
+in-process mode (``MLTaskManager(url=None)``) calls them directly, so both paths emit
+the same JSON.
+
+Jobs are expanded into J2 subtasks (search/grid.py, engine/jobs.py), recorded in the
+job table and handed to a *runner*: ``LocalRunner`` (this process, one device) or
+``parallel.runner.DistributedRunner`` (one rank per GPU over RCCL).
+"""
+from __future__ import annotations
+
+import glob
+import os
+import queue
+import threading
+import time
+import traceback
+import uuid
+from typing import Any, Dict, Iterator, List, Optional, Tuple
+
+import numpy as np
+
+from ..config import Config
+from ..data.preprocess import load_config, preprocess_frame
+from ..data.registry import DatasetRegistry
+from ..models.base import ParamError, family_of, is_classifier, supported_models
+from ..search.grid import expand_candidates
+from ..utils.log import get_logger
+from .jobs import Job, JobTable, json_safe, make_subtasks, now_iso, utc_iso
+from .model_store import ModelStore
+from .scheduler import Scheduler, Unit, chunk_units
+
+log = get_logger("dml.controller")
+
+Resp = Tuple[int, Any]
+
+
+def _cv_from(cv_params: Dict[str, Any]) -> int:
+    cv = cv_params.get("cv", 5)
+    if cv is None:
+        return 5
+    if isinstance(cv, bool):
+        raise ParamError("cv must be an int")
+    if isinstance(cv, (int, float)):
+        return int(cv)
+    if isinstance(cv, str):
+        digits = "".join(ch for ch in cv if ch.isdigit())
+        if cv.strip().isdigit():
+            return int(cv)
+        if "n_splits=" in cv and digits:
+            return int(cv.split("n_splits=")[1].split(",")[0].split(")")[0])
+    raise ParamError(f"unsupported cv specification {cv!r} (use an int)")
+
+
+def job_plan(request: Dict[str, Any]) -> Dict[str, Any]:
+    """Derive everything a worker needs from a J1 request."""
+    md = request.get("model_details") or {}
+    model_type = md.get("model_type")
+    if not model_type:
+        raise ParamError("model_details.model_type is required")
+    family_of(model_type)  # unsupported -> ParamError
+    hp = md.get("hyperparameters") or {}
+    tp = dict(request.get("train_params") or {})
+    search_type = md.get("search_type")
+    if search_type:
+        cvp = hp.get("cv_params") or {}
+        sp = hp.get("search_params") or {}
+        rs = sp.get("random_state", cvp.get("random_state"))
+        cands = expand_candidates(search_type, sp, random_state=rs)
+        cv = _cv_from(cvp)
+        scoring = cvp.get("scoring")
+        error_score = cvp.get("error_score", float("nan"))
+        refit = cvp.get("refit", True)
+    else:
+        cands = [{}]
+        cv = int(tp.get("cv", 5))   # the reference always runs cross_val_score(cv=5) (worker.py:326)
+        scoring = tp.get("scoring")
+        error_score = float("nan")
+        refit = True
+    if error_score is None:
+        error_score = float("nan")
+    return {
+        "model_type": model_type, "search_type": search_type, "candidates": cands, "cv": cv,
+        "scoring": scoring, "error_score": error_score, "refit": bool(refit) if not isinstance(refit, str) else True,
+        "test_size": tp.get("test_size", 0.2) if tp.get("test_size") is not None else 0.2,   # D2
+        "random_state": tp.get("random_state", 42) if tp.get("random_state") is not None else 42,
+        "holdout": bool(tp.get("holdout", True)),
+        "feature_columns": tp.get("feature_columns"), "target_column": tp.get("target_column"),
+    }
+
+
+class Controller:
+    def __init__(self, config: Optional[Config] = None, runner: Optional["Runner"] = None):
+        self.config = config or Config.from_env()
+        self.registry = DatasetRegistry(self.config.data_root)
+        self.models = ModelStore(self.config.models_dir)
+        self.table = JobTable(self.config.journal)
+        self.scheduler = Scheduler(self.config.dead_after_s, self.config.algo_weight)
+        self.runner = runner or LocalRunner(self)
+        if runner is not None:
+            runner.bind(self)
+        self._resumed = self._resume()
+
+    def _resume(self) -> int:
+        pending = self.table.replay()
+        for job in pending:
+            self.runner.submit(job)
+        return len(pending)
+
+    # ---- basic routes ------------------------------------------------------------------
+    def home(self) -> Resp:
+        return 200, {"message": "Distributed ML System API", "status": "running", "endpoints": [
+            "/health", "/create_session", "/download_data/<session_id>", "/check_data/<session_id>",
+            "/train/<session_id>", "/train_status/<session_id>", "/check_status/<session_id>/<job_id>",
+            "/metrics/<session_id>/<job_id>", "/download_model/<session_id>/<job_id>", "/preprocess/<session_id>",
+            "/workers", "/queues", "/subscribe", "/unsubscribe", "/heartbeat"],
+            "models": supported_models()}
+
+    def health(self) -> Resp:
+        return 200, {"status": "healthy", "timestamp": time.time(), **self.table.summary(),
+                     "workers": len(self.scheduler.alive_workers())}
+
+    def create_session(self) -> Resp:
+        return 201, {"message": "Session created", "session_id": self.table.create_session()}
+
+    def _bad_session(self, sid: str) -> Optional[Resp]:
+        if not self.table.has_session(sid):
+            return 404, {"error": "Invalid session ID"}
+        return None
+
+    # ---- data ---------------------------------------------------------------------------
+    def download_data(self, sid: str, body: Dict[str, Any]) -> Resp:
+        bad = self._bad_session(sid)
+        if bad:
+            return bad
+        body = body or {}
+        url, name, typ = body.get("dataset_url"), body.get("dataset_name"), body.get("dataset_type")
+        if not url or not name or not typ:
+            return 400, {"error": "Missing dataset parameters"}
+        ok, msg = self.registry.download(url, typ, name)
+        return (200, {"message": msg}) if ok else (500, {"error": msg})
+
+    def check_data(self, sid: str, dataset_name: Optional[str]) -> Resp:
+        bad = self._bad_session(sid)
+        if bad:
+            return bad
+        if not dataset_name:
+            return 400, {"error": "dataset_name is required"}
+        try:
+            path = self.registry.raw_file(dataset_name) or self.registry.find_file(dataset_name)
+        except ValueError as e:
+            return 400, {"error": str(e)}
+        if path:
+            return 200, {"status": f"Dataset {dataset_name} found at {path}"}
+        return 404, {"error": f"Dataset {dataset_name} not found, Please Use download_data function"}
+
+    def preprocess(self, sid: str, body: Dict[str, Any]) -> Resp:
+        bad = self._bad_session(sid)
+        if bad:
+            return bad
+        body = body or {}
+        name = body.get("dataset_id")
+        try:
+            path = self.registry.raw_file(name) if name else None
+        except ValueError as e:
+            return 400, {"error": str(e)}
+        if not path:
+            return 404, {"error": f"Dataset {name} not found"}
+        spec = body.get("yaml") or body.get("config") or body.get("yaml_url")
+        if not spec:
+            return 400, {"error": "Missing yaml parameters"}
+        try:
+            if isinstance(spec, str) and "\n" not in spec and not os.path.exists(spec):
+                # reference layout: CONFIG_PATH/<dataset>/*.yaml (master.py:361-377)
+                cands = sorted(glob.glob(os.path.join(self.registry.configs_dir, name, "*.yaml")))
+                base = os.path.basename(spec)
+                pick = [c for c in cands if os.path.basename(c) == base] or cands
+                if not pick:
+                    return 404, {"error": f"preprocessing config {spec!r} not found"}
+                spec = pick[0]
+            cfg = load_config(spec)
+            import pandas as pd
+
+            df = pd.read_csv(path)
+            out = preprocess_frame(df, cfg)
+            dest = self.registry.save_preprocessed(name, out)
+        except Exception as e:
+            return 500, {"error": f"{type(e).__name__}: {e}"}
+        return 200, {"message": f"Dataset successfully preprocessed and downloaded to {os.path.dirname(dest)}",
+                     "n_rows": int(len(out)), "n_cols": int(out.shape[1])}
+
+    # ---- training -----------------------------------------------------------------------
+    def _create_job(self, sid: str, body: Dict[str, Any]) -> Tuple[Optional[Job], Optional[Resp]]:
+        bad = self._bad_session(sid)
+        if bad:
+            return None, bad
+        body = dict(body or {})
+        body.setdefault("job_id", str(uuid.uuid4()))
+        body["session_id"] = sid
+        name = body.get("dataset_id")
+        try:
+            path = self.registry.find_file(name) if name else None
+        except ValueError as e:
+            return None, (400, {"error": str(e)})
+        if not path:
+            return None, (404, {"error": f"Dataset {name} not found, Please Use download_data function"})
+        try:
+            plan = job_plan(body)
+        except (ParamError, ValueError, TypeError) as e:
+            return None, (400, {"error": str(e)})
+        subtasks = make_subtasks(body, plan["candidates"], plan["cv"])
+        try:
+            job = self.table.create_job(body, subtasks, metadata=self.registry.metadata(name))   # D24
+        except ValueError as e:
+            return None, (409, {"error": str(e)})
+        self.runner.submit(job)
+        return job, None
+
+    def train(self, sid: str, body: Dict[str, Any]) -> Resp:
+        job, err = self._create_job(sid, body)
+        if err:
+            return err
+        return 200, {"status": "Model Training Started . . . .", "job_id": job.job_id, "total_subtasks": job.total}
+
+    def train_status(self, sid: str, body: Dict[str, Any]) -> Resp:
+        """SSE stream of J7 events (master.py:209-268)."""
+        job, err = self._create_job(sid, body)
+        if err:
+            return err
+
+        def stream() -> Iterator[str]:
+            import json
+
+            while True:
+                data = self.table.sse_json(job)
+                yield f"data: {json.dumps(data)}\n\n"
+                if job.finished:
+                    break
+                self.table.wait_finished(job.job_id, timeout=self.config.sse_interval_s)
+
+        return 200, stream()
+
+    def check_status(self, sid: str, jid: str) -> Resp:
+        bad = self._bad_session(sid)
+        if bad:
+            return bad
+        job = self.table.get(sid, jid)
+        if job is None:
+            return 404, {"error": f"Job {jid} not found."}
+        return 200, self.table.status_json(job)
+
+    def metrics(self, sid: str, jid: str, wait: bool = True, timeout: float = 3600.0) -> Resp:
+        """J8: one J3 record per subtask; waits for the job like the reference (bounded)."""
+        bad = self._bad_session(sid)
+        if bad:
+            return 404, {"error": "Invalid session"}
+        job = self.table.get(sid, jid)
+        if job is None:
+            return 404, {"error": "No subtasks found"}
+        if wait:
+            self.table.wait_finished(jid, timeout=timeout)
+        return 200, self.table.metrics_json(job)
+
+    def download_model(self, sid: str, jid: str, body: Dict[str, Any]) -> Resp:
+        bad = self._bad_session(sid)
+        if bad:
+            return bad
+        job = self.table.get(sid, jid)
+        if job is None:
+            return 404, {"error": f"Job {jid} not found."}
+        body = body or {}
+        path = self.models.resolve(body.get("model_path"), body.get("model_id"))
+        if path is None and job.result and job.result.get("best_result"):
+            best = job.result["best_result"]
+            path = self.models.resolve(best.get("model_path"), best.get("model_id"))
+        if path is None:
+            return 404, {"status": "error", "message": "Model file not found"}
+        return 200, {"__file__": path, "filename": os.path.basename(path)}
+
+    # ---- scheduler routes ------------------------------------------------------------------
+    def workers(self) -> Resp:
+        return 200, self.scheduler.workers_json()
+
+    def queues(self) -> Resp:
+        return 200, self.scheduler.queues()
+
+    def subscribe(self, body: Dict[str, Any]) -> Resp:
+        body = body or {}
+        wid = self.scheduler.register(body.get("host", "remote"), int(body.get("mem_capacity_mb", 0) or 0),
+                                      body.get("device", "cpu"))
+        return 200, {"status": "registered", "worker_id": wid}
+
+    def unsubscribe(self, body: Dict[str, Any]) -> Resp:
+        wid = str((body or {}).get("worker_id"))
+        units = self.scheduler.unsubscribe(wid)
+        self.runner.requeue(units)
+        return 200, {"status": "unsubscribed", "requeued": len(units)}
+
+    def heartbeat(self, body: Dict[str, Any]) -> Resp:
+        wid = str((body or {}).get("worker_id"))
+        if not self.scheduler.heartbeat(wid):
+            return 404, {"detail": "unknown worker; re-register"}
+        return 200, {"status": "ok"}
+
+    def shutdown(self) -> None:
+        self.runner.shutdown()
+
+
+# ======================================================================================
+# runners
+# ======================================================================================
+class Runner:
+    def bind(self, controller: Controller) -> None:
+        self.ctl = controller
+
+    def submit(self, job: Job) -> None:
+        raise NotImplementedError
+
+    def requeue(self, units: List[Unit]) -> None:
+        pass
+
+    def shutdown(self) -> None:
+        pass
+
+
+class DeviceCache:
+    """Resident DeviceData per (dataset file, columns, task type) on one device."""
+
+    def __init__(self, device: str, max_items: int = 4):
+        self.device = device
+        self.max_items = max_items
+        self._items: Dict[tuple, Any] = {}
+        self._order: List[tuple] = []
+
+    def get(self, ctl: Controller, plan: Dict[str, Any], dataset_id: str):
+        from ..data.device import DeviceData
+
+        ds = ctl.registry.load(dataset_id, plan["feature_columns"], plan["target_column"])
+        clf = is_classifier(plan["model_type"])
+        key = (ds.path, os.path.getmtime(ds.path) if ds.path else 0, tuple(ds.feature_names), ds.target_name, clf)
+        if key in self._items:
+            self._order.remove(key)
+            self._order.append(key)
+            return self._items[key]
+        dd = DeviceData(ds.X, ds.y, clf, self.device, name=dataset_id)
+        self._items[key] = dd
+        self._order.append(key)
+        while len(self._order) > self.max_items:
+            old = self._order.pop(0)
+            self._items.pop(old, None)
+        return dd
+
+
+class _Sampler:
+    """psutil CPU/mem sampling while a slice runs (reference worker.py:201-221), stopped in finally (D15)."""
+
+    def __init__(self, period: float = 0.5):
+        self.period = period
+        self.cpu: List[float] = []
+        self.mem: List[float] = []
+        self._stop = threading.Event()
+        self._t = None
+
+    def __enter__(self):
+        try:
+            import psutil
+
+            self._ps = psutil
+            psutil.cpu_percent(None)
+        except ImportError:
+            self._ps = None
+        self._t = threading.Thread(target=self._loop, daemon=True)
+        self._t.start()
+        return self
+
+    def _loop(self):
+        while not self._stop.wait(self.period):
+            if self._ps:
+                self.cpu.append(self._ps.cpu_percent(None))
+                self.mem.append(self._ps.virtual_memory().percent)
+
+    def __exit__(self, *a):
+        self._stop.set()
+        self._t.join(timeout=2)
+        if self._ps and not self.cpu:
+            self.cpu.append(self._ps.cpu_percent(None))
+            self.mem.append(self._ps.virtual_memory().percent)
+
+    def avg(self):
+        c = float(np.mean(self.cpu)) if self.cpu else 0.0
+        m = float(np.mean(self.mem)) if self.mem else 0.0
+        return c, m
+
+
+def candidate_costs(plan: Dict[str, Any], n_train: int, d: int, n_classes: int) -> List[float]:
+    fam = family_of(plan["model_type"])
+    out = []
+    for c in plan["candidates"]:
+        try:
+            rp = fam.resolve(plan["model_type"], c, n_train, d, n_classes)
+            splits = (plan["cv"] or 0) + (1 if plan["holdout"] else 0)
+            out.append(fam.cost(plan["model_type"], rp, n_train, d, n_classes) * max(1, splits))
+        except Exception:
+            out.append(1e-3)
+    return out
+
+
+def execute_plan_slice(ctl: Controller, job: Job, plan: Dict[str, Any], dd, cand_ids: List[int], worker_id: str,
+                       device_name: str, seed: int = 0):
+    """Run one slice of candidates on a device and return (results, J3 metrics per candidate)."""
+    from .executor import JobSpec, run_candidates
+
+    spec = JobSpec(model_type=plan["model_type"], candidates=[job.subtasks[i].spec["parameters"] for i in
+                                                               range(job.total)],
+                   cv=plan["cv"], scoring=plan["scoring"], holdout=plan["holdout"], test_size=plan["test_size"],
+                   random_state=plan["random_state"], error_score=plan["error_score"],
+                   keep_models="none", seed=seed)
+    received = utc_iso()
+    with _Sampler() as smp:
+        started = utc_iso()
+        t0 = time.perf_counter()
+        results = run_candidates(dd, spec, cand_ids)
+        wall = time.perf_counter() - t0
+    finished = utc_iso()
+    cpu, mem = smp.avg()
+    metrics = {}
+    for r in results:
+        metrics[r.candidate] = {
+            "worker_id": worker_id, "subtask_id": job.subtasks[r.candidate].subtask_id,
+            "status": "DONE" if r.ok else "FAILED", "received_at": received, "started_at": started,
+            "finished_at": finished, "cpu_percent_avg": cpu, "mem_percent_avg": mem, "algo": plan["model_type"],
+            "device": device_name, "fit_seconds": r.fit_seconds, "slice_wall_seconds": wall,
+            "n_fits": r.result.get("n_fits", 0) if r.ok else 0,
+        }
+    return results, metrics, wall
+
+
+def refit_best(ctl: Controller, job: Job, plan: Dict[str, Any], dd, best_idx: int) -> Optional[str]:
+    """sklearn refit=True: fit the best candidate on all rows and store the artefact."""
+    from .executor import JobSpec, run_candidates
+
+    spec = JobSpec(model_type=plan["model_type"], candidates=[job.subtasks[best_idx].spec["parameters"]], cv=0,
+                   holdout=False, keep_models="all", scoring=plan["scoring"])
+    # a single "full" split: train on every row; the executor scores nothing
+    from ..search.cv import ROLE_TRAIN
+
+    roles = np.full((1, dd.n), ROLE_TRAIN, dtype=np.uint8)
+    dd.set_splits(roles, ["full"], key=("full",))
+    from .executor import build_tasks
+
+    fam = family_of(plan["model_type"])
+    tasks, errors = build_tasks(dd, spec, [0])
+    if errors or not tasks:
+        return None
+    outs = fam.run(dd, tasks, keep_models=True)
+    if not outs or outs[0].model is None:
+        return None
+    model = outs[0].model
+    model["job_id"] = job.job_id
+    model["subtask_id"] = job.subtasks[best_idx].subtask_id
+    model["feature_names"] = list(ctl.registry.load(job.dataset_id, plan["feature_columns"],
+                                                    plan["target_column"]).feature_names)
+    return ctl.models.save(f"{job.subtasks[best_idx].subtask_id}_model", model)
+
+
+class LocalRunner(Runner):
+    """Runs jobs in this process on one device (``Config.device``), one job at a time.
+
+    Candidates are ordered LPT (most expensive first) and cut into slices of about
+    ``chunk_target_s`` estimated seconds so status/SSE progress streams while the
+    device stays batched.
+    """
+
+    def __init__(self, controller: Optional[Controller] = None):
+        self.q: "queue.Queue[Optional[Job]]" = queue.Queue()
+        self._thread: Optional[threading.Thread] = None
+        self.cache: Optional[DeviceCache] = None
+        if controller is not None:
+            self.bind(controller)
+
+    def bind(self, controller: Controller) -> None:
+        super().bind(controller)
+        self.device = controller.config.resolved_device()
+        self.cache = DeviceCache(self.device)
+        self.worker_id = controller.scheduler.register("local", 0, self.device)
+        self._hb_stop = threading.Event()
+
+    def submit(self, job: Job) -> None:
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._loop, name="dml-local-runner", daemon=True)
+            self._thread.start()
+        self.q.put(job)
+
+    def _loop(self):
+        while True:
+            job = self.q.get()
+            if job is None:
+                return
+            self.ctl.scheduler.heartbeat(self.worker_id)
+            try:
+                self.run_job(job)
+            except Exception as e:  # never leave a job hanging (D5)
+                traceback.print_exc()
+                for st in job.subtasks:
+                    if st.status not in ("completed", "failed"):
+                        self.ctl.table.finish_subtask(job.job_id, st.subtask_id, "failed",
+                                                      error=f"{type(e).__name__}: {e}")
+
+    def run_job(self, job: Job) -> None:
+        ctl = self.ctl
+        plan = job_plan(job.request)
+        dd = self.cache.get(ctl, plan, job.dataset_id)
+        todo = [st.index for st in job.subtasks if st.status not in ("completed", "failed")]
+        if not todo:
+            return
+        costs = candidate_costs(plan, int(dd.n * 0.8), dd.d, dd.n_classes)
+        order = sorted(todo, key=lambda i: -costs[i])
+        est = [ctl.scheduler.estimate(plan["model_type"], costs[i]) for i in order]
+        chunk_ids = chunk_units(est, ctl.config.chunk_target_s, 1)
+        slices: Dict[int, List[int]] = {}
+        for i, c in zip(order, chunk_ids):
+            slices.setdefault(int(c), []).append(i)
+        all_results = []
+        pending_final = None
+        for ci in sorted(slices):
+            ids = slices[ci]
+            ctl.table.mark_running(job.job_id, ids, self.worker_id)
+            results, metrics, wall = execute_plan_slice(ctl, job, plan, dd, ids, self.worker_id, self.device,
+                                                        seed=abs(hash(job.job_id)) & 0xFFFF)
+            unit = Unit(unit_id=f"{job.job_id}:{ci}", cost=sum(costs[i] for i in ids), algo=plan["model_type"])
+            ctl.scheduler.observe(self.worker_id, unit, wall)
+            ctl.scheduler.heartbeat(self.worker_id)
+            if ci == max(slices):
+                pending_final = (results, metrics)
+            else:
+                self._publish(job, results, metrics)
+            all_results.extend(results)
+        # refit + store the best model before the job turns "completed"
+        ok = [r for r in all_results if r.ok]
+        prev_ok = [st.result for st in job.subtasks if st.status == "completed" and st.result]
+        if ok and plan.get("refit", True) and ctl.config.keep_models != "none":
+            def score(r):
+                v = r.result.get("mean_cv_score")
+                return -np.inf if v is None or (isinstance(v, float) and np.isnan(v)) else v
+            best = max(ok, key=score)
+            better_prev = any(score_r(p) > score(best) for p in prev_ok)
+            if not better_prev:
+                try:
+                    path = refit_best(ctl, job, plan, dd, best.candidate)
+                    if path:
+                        best.result["model_path"] = path
+                except Exception:
+                    traceback.print_exc()
+        if pending_final:
+            self._publish(job, *pending_final)
+
+    def _publish(self, job: Job, results, metrics) -> None:
+        for r in results:
+            st = job.subtasks[r.candidate]
+            if r.ok:
+                R = dict(r.result)
+                R.setdefault("model_id", f"{st.subtask_id}_model")
+                R.setdefault("model_path", None)
+                self.ctl.table.finish_subtask(job.job_id, st.subtask_id, "completed", result=json_safe(R),
+                                              metrics=metrics.get(r.candidate))
+            else:
+                self.ctl.table.finish_subtask(job.job_id, st.subtask_id, "failed", error=r.error,
+                                              metrics=metrics.get(r.candidate))
+
+    def shutdown(self) -> None:
+        if self._thread is not None:
+            self.q.put(None)
+
+
+def score_r(R: Dict[str, Any]) -> float:
+    v = R.get("mean_cv_score")
+    return -np.inf if v is None or (isinstance(v, float) and np.isnan(v)) else v

@@ -1,0 +1,163 @@
+"""Estimator families: typed registry + the batched-fit interface.
+
+The reference instantiates estimators with ``exec``/``eval`` of
+``"{name}(**{parameters})"`` over a 15-name whitelist
+(aws-prod/worker/worker.py:36-57, :436-455; defect D19).  Here every supported name
+maps to a *family* object that (a) validates and resolves the sklearn-style parameter
+dict into numeric settings, (b) prices a fit for the scheduler, and (c) runs MANY fits
+(candidates x CV folds x holdout) in one batched device call.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence
+
+
+class ParamError(ValueError):
+    """Invalid estimator parameter (reported as a failed subtask, never a crash)."""
+
+
+@dataclass
+class FitTask:
+    task_id: int
+    candidate: int
+    split: int
+    model_type: str
+    params: Dict[str, Any]
+    seed: int = 0
+
+
+@dataclass
+class FitOutput:
+    task_id: int
+    pred: Any = None            # device tensor aligned with the split's test rows
+    proba: Any = None           # optional [n_test, C]
+    fit_seconds: float = 0.0    # amortised device time of this fit
+    error: Optional[str] = None
+    model: Any = None           # optional fitted model (when asked to keep it)
+    info: Dict[str, Any] = field(default_factory=dict)
+
+
+class Family:
+    model_types: Sequence[str] = ()
+    classifiers: Sequence[str] = ()
+
+    def is_classifier(self, model_type: str) -> bool:
+        return model_type in self.classifiers
+
+    def resolve(self, model_type: str, params: Dict[str, Any], n_train: int, n_features: int,
+                n_classes: int) -> Dict[str, Any]:
+        raise NotImplementedError
+
+    def cost(self, model_type: str, rp: Dict[str, Any], n_train: int, n_features: int, n_classes: int) -> float:
+        return 1.0
+
+    def run(self, data, tasks: List[FitTask], keep_models: bool = False) -> List[FitOutput]:
+        raise NotImplementedError
+
+
+_REGISTRY: Dict[str, Family] = {}
+
+
+def register(family: Family) -> Family:
+    for name in family.model_types:
+        _REGISTRY[name] = family
+    return family
+
+
+def family_of(model_type: str) -> Family:
+    _ensure_loaded()
+    try:
+        return _REGISTRY[model_type]
+    except KeyError:
+        raise ParamError(f"Unsupported model: {model_type}") from None
+
+
+def supported_models() -> List[str]:
+    _ensure_loaded()
+    return sorted(_REGISTRY)
+
+
+def is_classifier(model_type: str) -> bool:
+    return family_of(model_type).is_classifier(model_type)
+
+
+_loaded = False
+
+
+def _ensure_loaded():
+    global _loaded
+    if _loaded:
+        return
+    _loaded = True
+    from . import forest, linear, neighbors, boosting, svm, transformers  # noqa: F401
+
+
+# ---- common parameter helpers ---------------------------------------------------------
+def as_bool(v, name):
+    if isinstance(v, bool):
+        return v
+    if isinstance(v, (int,)) and v in (0, 1):
+        return bool(v)
+    if isinstance(v, str) and v.lower() in ("true", "false"):
+        return v.lower() == "true"
+    raise ParamError(f"{name} must be a bool, got {v!r}")
+
+
+def as_int(v, name, lo=None, hi=None, allow_none=False):
+    if v is None and allow_none:
+        return None
+    if isinstance(v, bool) or not isinstance(v, (int, float)) or (isinstance(v, float) and not v.is_integer()):
+        if isinstance(v, str):
+            try:
+                v = int(v)
+            except ValueError:
+                raise ParamError(f"{name} must be an int, got {v!r}") from None
+        else:
+            raise ParamError(f"{name} must be an int, got {v!r}")
+    v = int(v)
+    if lo is not None and v < lo:
+        raise ParamError(f"{name} must be >= {lo}, got {v}")
+    if hi is not None and v > hi:
+        raise ParamError(f"{name} must be <= {hi}, got {v}")
+    return v
+
+
+def as_float(v, name, lo=None, hi=None, allow_none=False):
+    if v is None and allow_none:
+        return None
+    if isinstance(v, bool):
+        raise ParamError(f"{name} must be a float, got {v!r}")
+    try:
+        v = float(v)
+    except (TypeError, ValueError):
+        raise ParamError(f"{name} must be a float, got {v!r}") from None
+    if math.isnan(v):
+        raise ParamError(f"{name} must not be NaN")
+    if lo is not None and v < lo:
+        raise ParamError(f"{name} must be >= {lo}, got {v}")
+    if hi is not None and v > hi:
+        raise ParamError(f"{name} must be <= {hi}, got {v}")
+    return v
+
+
+def seed_of(random_state) -> Optional[int]:
+    """random_state on the wire: int, None, or a str(RandomState) -> None."""
+    if random_state is None:
+        return None
+    if isinstance(random_state, bool):
+        return int(random_state)
+    if isinstance(random_state, (int,)):
+        return int(random_state) & 0xFFFFFFFFFFFF
+    if isinstance(random_state, float) and random_state.is_integer():
+        return int(random_state)
+    if isinstance(random_state, str):
+        try:
+            return int(random_state)
+        except ValueError:
+            return None
+    return None
+
+
+IGNORED_COMMON = {"n_jobs", "verbose", "warm_start", "copy_X", "positive_ignored"}

@@ -1,0 +1,287 @@
+"""RandomForest{Classifier,Regressor} family — batched over candidates x splits x trees.
+
+Parameter semantics follow sklearn's estimators the reference whitelists
+(aws-prod/worker/worker.py:38,45) and fits per task (:315, :326, :341).  All trees of
+all fits of a job slice are grown together by the HIP builder (ops/forest_ops.py,
+csrc/kernels/forest.hip) — or by the C++ builder on CPU — in memory-budgeted batches
+of whole fits, then every fit's held-out rows are predicted in one launch.
+
+Supported: n_estimators, criterion (gini/entropy/log_loss; squared_error; friedman_mse
+and absolute_error/poisson approximate with squared_error), max_depth,
+min_samples_split, min_samples_leaf (int or fraction), max_features (sqrt/log2/None/
+int/float), bootstrap, max_samples, min_impurity_decrease, random_state.  Parameters
+with no effect on the fitted function (n_jobs, verbose, warm_start, oob_score) are
+accepted and ignored; unsupported ones (class_weight != None, ccp_alpha > 0,
+max_leaf_nodes, min_weight_fraction_leaf > 0, monotonic_cst) are reported in the
+subtask's ``warnings``.
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Any, Dict, List
+
+import numpy as np
+import torch
+
+from ..ops import forest_ops
+from ..utils import native
+from .base import Family, FitOutput, FitTask, ParamError, as_bool, as_float, as_int, register, seed_of
+
+_CLS = "RandomForestClassifier"
+_REG = "RandomForestRegressor"
+
+_DEFAULTS = {
+    "n_estimators": 100, "criterion": None, "max_depth": None, "min_samples_split": 2, "min_samples_leaf": 1,
+    "min_weight_fraction_leaf": 0.0, "max_features": None, "max_leaf_nodes": None, "min_impurity_decrease": 0.0,
+    "bootstrap": True, "oob_score": False, "n_jobs": None, "random_state": None, "verbose": 0,
+    "warm_start": False, "class_weight": None, "ccp_alpha": 0.0, "max_samples": None, "monotonic_cst": None,
+}
+
+
+def _max_features(v, d, is_cls):
+    if v is None or v == "None":
+        v = "sqrt" if is_cls else 1.0
+    if isinstance(v, str):
+        if v == "sqrt" or v == "auto":
+            return max(1, int(math.sqrt(d)))
+        if v == "log2":
+            return max(1, int(math.log2(d)))
+        raise ParamError(f"max_features {v!r} not understood")
+    if isinstance(v, bool):
+        raise ParamError("max_features must not be a bool")
+    if isinstance(v, int) or (isinstance(v, float) and v > 1.0 and v.is_integer()):
+        return max(1, min(d, int(v)))
+    f = float(v)
+    if not 0.0 < f <= 1.0:
+        raise ParamError(f"max_features fraction must be in (0, 1], got {f}")
+    return max(1, int(f * d))
+
+
+def _count_param(v, n, name, lo_int):
+    if isinstance(v, float):
+        f = float(v)
+        if not 0.0 < f <= 1.0:
+            raise ParamError(f"{name} fraction must be in (0, 1], got {f}")
+        return max(lo_int, int(math.ceil(f * n)))
+    return as_int(v, name, lo=lo_int)
+
+
+class ForestFamily(Family):
+    model_types = (_CLS, _REG)
+    classifiers = (_CLS,)
+
+    def __init__(self):
+        self.tiers = forest_ops.ForestTiers()
+        self.hbm_budget_bytes = None  # None -> derived from free memory
+
+    def resolve(self, model_type, params, n_train, n_features, n_classes) -> Dict[str, Any]:
+        p = dict(_DEFAULTS)
+        p.update({k: v for k, v in params.items() if k in _DEFAULTS})
+        is_cls = model_type == _CLS
+        warn: List[str] = []
+        unknown = sorted(k for k in params if k not in _DEFAULTS)
+        if unknown:
+            warn.append(f"ignored unknown parameters {unknown}")
+        crit = p["criterion"] or ("gini" if is_cls else "squared_error")
+        if is_cls:
+            if crit not in ("gini", "entropy", "log_loss"):
+                raise ParamError(f"criterion {crit!r} invalid for {model_type}")
+            crit_id = forest_ops.GINI if crit == "gini" else forest_ops.ENTROPY
+        else:
+            if crit not in ("squared_error", "friedman_mse", "absolute_error", "poisson"):
+                raise ParamError(f"criterion {crit!r} invalid for {model_type}")
+            if crit != "squared_error":
+                warn.append(f"criterion={crit!r} approximated by squared_error")
+            crit_id = forest_ops.MSE
+        n_est = as_int(p["n_estimators"], "n_estimators", lo=1, hi=100000)
+        md = as_int(p["max_depth"], "max_depth", lo=1, allow_none=True)
+        mss = _count_param(p["min_samples_split"], n_train, "min_samples_split", 2)
+        msl = _count_param(p["min_samples_leaf"], n_train, "min_samples_leaf", 1)
+        k = _max_features(p["max_features"], n_features, is_cls)
+        boot = as_bool(p["bootstrap"], "bootstrap")
+        lam = 1.0
+        if p["max_samples"] is not None:
+            if not boot:
+                raise ParamError("`max_sample` cannot be set if `bootstrap=False`")
+            ms = p["max_samples"]
+            if isinstance(ms, float):
+                lam = float(ms)
+                if not 0.0 < lam <= 1.0:
+                    raise ParamError("max_samples fraction must be in (0, 1]")
+            else:
+                lam = min(1.0, as_int(ms, "max_samples", lo=1) / max(1, n_train))
+        mid = as_float(p["min_impurity_decrease"], "min_impurity_decrease", lo=0.0)
+        if p["class_weight"] not in (None, "None"):
+            warn.append("class_weight is not supported yet; fitted unweighted")
+        if as_float(p["ccp_alpha"], "ccp_alpha", lo=0.0) > 0:
+            warn.append("ccp_alpha pruning not supported; ignored")
+        if p["max_leaf_nodes"] not in (None, "None"):
+            warn.append("max_leaf_nodes not supported; ignored")
+        if as_float(p["min_weight_fraction_leaf"], "min_weight_fraction_leaf", lo=0.0, hi=0.5) > 0:
+            warn.append("min_weight_fraction_leaf not supported; ignored")
+        return {
+            "n_estimators": n_est, "criterion": crit_id, "max_depth": md if md is not None else forest_ops.INT32_MAX,
+            "min_samples_split": mss, "min_samples_leaf": msl, "max_features": k, "bootstrap": int(boot),
+            "lambda": lam, "min_impurity_decrease": mid, "seed": seed_of(p["random_state"]), "warnings": warn,
+        }
+
+    def cost(self, model_type, rp, n_train, n_features, n_classes) -> float:
+        """Relative device cost ~ trees x active rows x levels x features-per-node."""
+        active = 0.632 * n_train * rp["lambda"] if rp["bootstrap"] else n_train
+        leaves = max(1.0, active / rp["min_samples_leaf"] / max(1, rp["min_samples_split"] - 1))
+        depth = min(float(rp["max_depth"]), math.log2(leaves) * 1.6 + 1)
+        return rp["n_estimators"] * active * depth * rp["max_features"] * 1e-9 + 1e-3
+
+    # ------------------------------------------------------------------------------
+    def _tree_bytes(self, data, rp) -> float:
+        n_train = data.n
+        active = 0.632 * n_train if rp["bootstrap"] else n_train
+        VC = data.n_classes if data.classification else 3
+        pool = (2 * active / rp["min_samples_leaf"] + 1) * (8 + 8 * VC)
+        return active * 4 * 2 + pool + active * 24
+
+    def _budget(self, data) -> float:
+        if self.hbm_budget_bytes:
+            return float(self.hbm_budget_bytes)
+        if data.is_gpu:
+            free, _total = torch.cuda.mem_get_info(data.device)
+            return 0.55 * free
+        return 8e9
+
+    def run(self, data, tasks: List[FitTask], keep_models: bool = False) -> List[FitOutput]:
+        if not tasks:
+            return []
+        is_reg = not data.classification
+        Xb = data.binned()
+        budget = self._budget(data)
+        outs: Dict[int, FitOutput] = {}
+        # batches of whole fits under the memory budget
+        batches: List[List[FitTask]] = []
+        cur, cur_bytes = [], 0.0
+        for t in tasks:
+            b = self._tree_bytes(data, t.params) * t.params["n_estimators"]
+            if cur and cur_bytes + b > budget:
+                batches.append(cur)
+                cur, cur_bytes = [], 0.0
+            cur.append(t)
+            cur_bytes += b
+        if cur:
+            batches.append(cur)
+        for batch in batches:
+            for o in self._run_batch(data, Xb, batch, is_reg, keep_models):
+                outs[o.task_id] = o
+        return [outs[t.task_id] for t in tasks]
+
+    def _specs(self, batch: List[FitTask]) -> np.ndarray:
+        T = sum(t.params["n_estimators"] for t in batch)
+        specs = forest_ops.make_specs(T)
+        i = 0
+        for f, t in enumerate(batch):
+            rp = t.params
+            base = rp["seed"] if rp["seed"] is not None else t.seed
+            n = rp["n_estimators"]
+            sl = specs[i:i + n]
+            sl["seed"] = [native_seed(base, j) for j in range(n)]
+            sl["split"] = t.split
+            sl["fit"] = f
+            sl["max_depth"] = rp["max_depth"]
+            sl["min_samples_split"] = rp["min_samples_split"]
+            sl["min_samples_leaf"] = rp["min_samples_leaf"]
+            sl["max_features"] = rp["max_features"]
+            sl["bootstrap"] = rp["bootstrap"]
+            sl["criterion"] = rp["criterion"]
+            sl["min_impurity_decrease"] = rp["min_impurity_decrease"]
+            sl["pois_cdf"] = native.poisson_cdf_table(rp["lambda"])
+            i += n
+        return specs
+
+    def _run_batch(self, data, Xb, batch: List[FitTask], is_reg: bool, keep_models: bool) -> List[FitOutput]:
+        specs = self._specs(batch)
+        t0 = time.perf_counter()
+        if data.is_gpu:
+            fb = forest_ops.build_gpu(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
+                                      data.n_classes, is_reg, self.tiers)
+        else:
+            fb = forest_ops.build_cpu(Xb.numpy(), data.y_enc, None if not is_reg else data.y_reg.numpy(),
+                                      data.roles_np(), specs, data.n_classes, is_reg)
+        toff = np.zeros(len(batch) + 1, dtype=np.int64)
+        np.cumsum([t.params["n_estimators"] for t in batch], out=toff[1:])
+        rows = [data.test_rows[t.split] for t in batch]
+        roff = np.zeros(len(batch) + 1, dtype=np.int64)
+        np.cumsum([int(r.numel()) for r in rows], out=roff[1:])
+        if data.is_gpu:
+            rows_cat = torch.cat(rows) if rows else torch.empty(0, dtype=torch.int32, device=data.device)
+            pred = forest_ops.predict(fb, Xb, toff, roff, rows_cat)
+        else:
+            rows_cat = np.concatenate([r.numpy() for r in rows]) if rows else np.zeros(0, np.int32)
+            pred = forest_ops.predict(fb, Xb.numpy(), toff, roff, rows_cat)
+            pred = torch.from_numpy(pred)
+        if data.is_gpu:
+            torch.cuda.synchronize(data.device)
+        dt = time.perf_counter() - t0
+        total_trees = max(1, int(toff[-1]))
+        outs = []
+        for f, t in enumerate(batch):
+            share = t.params["n_estimators"] / total_trees
+            o = FitOutput(task_id=t.task_id, pred=pred[roff[f]:roff[f + 1]], fit_seconds=dt * share,
+                          info={"warnings": t.params.get("warnings", []), "batch_stats": dict(fb.stats)})
+            if keep_models:
+                o.model = extract_forest(fb, int(toff[f]), int(toff[f + 1]), data, t)
+            outs.append(o)
+        return outs
+
+
+def native_seed(base: int, tree: int) -> int:
+    x = (int(base) * 0x9E3779B97F4A7C15 + tree * 0xBF58476D1CE4E5B9 + 0x1234567) & 0xFFFFFFFFFFFFFFFF
+    x ^= x >> 31
+    return x
+
+
+def extract_forest(fb, t0: int, t1: int, data, task: FitTask) -> Dict[str, Any]:
+    """Renumber trees [t0, t1) of a batch pool into a standalone forest in pool layout.
+
+    Layout matches the kernels' contract: tree j's root is node j, every other node
+    follows, children pairs adjacent — so the saved model predicts with the same
+    HIP/C++ predictors (``roots`` is kept for readability).
+    """
+    nodes = fb.nodes.cpu().numpy() if isinstance(fb.nodes, torch.Tensor) else fb.nodes
+    vals = fb.vals.cpu().numpy() if isinstance(fb.vals, torch.Tensor) else fb.vals
+    T = t1 - t0
+    ids = {t: t - t0 for t in range(t0, t1)}
+    order = []
+    nxt = T
+    for t in range(t0, t1):
+        stack = [t]
+        while stack:
+            i = stack.pop()
+            order.append(i)
+            if nodes[i, 0] >= 0:
+                l = int(nodes[i, 1])
+                ids[l], ids[l + 1] = nxt, nxt + 1
+                nxt += 2
+                stack.append(l + 1)
+                stack.append(l)
+    nn = np.empty((nxt, 2), dtype=np.int32)
+    vv = np.empty((nxt, vals.shape[1]), dtype=np.float64)
+    for i in order:
+        j = ids[i]
+        nn[j, 0] = nodes[i, 0]
+        nn[j, 1] = ids[int(nodes[i, 1])] if nodes[i, 0] >= 0 else -1
+        vv[j] = vals[i]
+    return {
+        "kind": "forest",
+        "is_reg": bool(fb.is_reg),
+        "n_classes": int(fb.n_classes),
+        "classes": None if data.classes is None else np.asarray(data.classes).tolist(),
+        "nodes": nn,
+        "vals": vv,
+        "n_trees": T,
+        "edges": data.edges.cpu().numpy(),
+        "n_features": int(data.d),
+        "params": {k: v for k, v in task.params.items() if k != "warnings"},
+        "model_type": task.model_type,
+    }
+
+
+register(ForestFamily())

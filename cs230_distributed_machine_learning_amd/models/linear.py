@@ -1,0 +1,373 @@
+"""LogisticRegression and LinearRegression families — every fit of a job solved at once.
+
+Reference: both are whitelisted estimators fitted one (candidate, fold) at a time by
+sklearn on CPU (aws-prod/worker/worker.py:39,46 whitelist; :315, :326/:341 fits).
+
+LogisticRegression
+    Each fit (candidate x split) owns a block of columns of ONE weight matrix
+    ``W [d+1, M]`` (last row = intercept).  Per objective evaluation the whole batch
+    does: ``Z = X @ W`` (library GEMM) -> fused HIP link/loss/residual kernel
+    (``dml_lr_link_grad``, csrc/kernels/linear.hip) -> ``G = X^T R`` (library GEMM).
+    A batched L-BFGS (per-fit histories, per-fit Armijo steps, per-fit stopping on
+    ``max|grad| <= tol`` or ``max_iter``) minimises every fit's objective
+    ``mean(loss) + ||w||^2 / (2 C n)`` — the same optimum sklearn's lbfgs /
+    newton-cg / sag(a) / liblinear reach (liblinear: one-vs-rest, intercept
+    penalised via ``intercept_scaling``).  Binary problems use one sigmoid column,
+    multiclass the multinomial softmax (or OvR columns for liblinear / multi_class='ovr').
+LinearRegression
+    Normal equations per split (shared by every candidate on that split), solved by
+    pseudo-inverse (min-norm like sklearn's lstsq).
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Any, Dict, List
+
+import numpy as np
+import torch
+
+from ..utils import native
+from .base import Family, FitOutput, FitTask, ParamError, as_bool, as_float, as_int, register, seed_of
+
+KIND_BINARY, KIND_SOFTMAX, KIND_OVR = 0, 1, 2
+
+_LR_DEFAULTS = {
+    "penalty": "l2", "dual": False, "tol": 1e-4, "C": 1.0, "fit_intercept": True, "intercept_scaling": 1.0,
+    "class_weight": None, "random_state": None, "solver": "lbfgs", "max_iter": 100, "multi_class": "deprecated",
+    "verbose": 0, "warm_start": False, "n_jobs": None, "l1_ratio": None,
+}
+_SOLVERS = ("lbfgs", "liblinear", "newton-cg", "newton-cholesky", "sag", "saga")
+
+
+def link_grad_torch(Z: torch.Tensor, y: torch.Tensor, roles: torch.Tensor, col0, K, kind, split, scale):
+    """Reference (CPU) implementation of the fused kernel: returns (R, loss[F]).
+
+    Vectorised over fits sharing a (link kind, width) so a batch costs a handful of
+    tensor ops regardless of how many candidates x folds it holds.
+    """
+    n, M = Z.shape
+    F = len(col0)
+    R = torch.zeros_like(Z)
+    loss = torch.zeros(F, dtype=torch.float64, device=Z.device)
+    yl = y.long()
+    groups: Dict[tuple, List[int]] = {}
+    for f in range(F):
+        groups.setdefault((int(kind[f]), int(K[f])), []).append(f)
+    for (kd, k), fits in groups.items():
+        fi = torch.tensor(fits, dtype=torch.long, device=Z.device)
+        cols = (torch.tensor([int(col0[f]) for f in fits], device=Z.device).view(-1, 1)
+                + torch.arange(k, device=Z.device).view(1, -1))                      # [G, k]
+        z = Z[:, cols.flatten()].view(n, len(fits), k)                                 # [n, G, k]
+        m = (roles[torch.tensor([int(split[f]) for f in fits], device=Z.device)] == 1).t().to(Z.dtype)  # [n, G]
+        s = torch.tensor([float(scale[f]) for f in fits], dtype=Z.dtype, device=Z.device).view(1, -1)
+        if kd == KIND_SOFTMAX:
+            lse = torch.logsumexp(z, dim=2, keepdim=True)
+            onehot = torch.nn.functional.one_hot(yl, k).to(Z.dtype).unsqueeze(1)
+            r = torch.exp(z - lse) - onehot
+            l = lse.squeeze(2) - z.gather(2, yl.view(-1, 1, 1).expand(n, len(fits), 1)).squeeze(2)
+        else:
+            if kd == KIND_BINARY:
+                tgt = (yl == 1).to(Z.dtype).view(n, 1, 1).expand(n, len(fits), 1)
+            else:
+                tgt = torch.nn.functional.one_hot(yl, k).to(Z.dtype).unsqueeze(1).expand(n, len(fits), k)
+            r = torch.sigmoid(z) - tgt
+            l = torch.nn.functional.softplus(torch.where(tgt > 0.5, -z, z)).sum(2)
+        r = r * (m * s).unsqueeze(2)
+        R[:, cols.flatten()] = r.reshape(n, -1)
+        loss[fi] = (l.double() * m.double()).sum(0) * s.squeeze(0).double()
+    return R, loss
+
+
+class _Batch:
+    """Column layout of a batch of logistic fits."""
+
+    def __init__(self, data, tasks: List[FitTask]):
+        self.tasks = tasks
+        C = data.n_classes
+        col0, K, kind, split, scale, lam, icpt, pen_icpt, tol, max_iter = ([] for _ in range(10))
+        m = 0
+        for t in tasks:
+            rp = t.params
+            if C == 2:
+                k, kd = 1, KIND_BINARY
+            elif rp["ovr"]:
+                k, kd = C, KIND_OVR
+            else:
+                k, kd = C, KIND_SOFTMAX
+            n_f = max(1, data.train_counts[t.split])
+            col0.append(m); K.append(k); kind.append(kd); split.append(t.split)
+            scale.append(1.0 / n_f)
+            lam.append(0.0 if rp["C"] is None else 1.0 / (rp["C"] * n_f))
+            icpt.append(rp["intercept_scaling"] if rp["fit_intercept"] else 0.0)
+            pen_icpt.append(1.0 if rp["penalize_intercept"] else 0.0)
+            tol.append(rp["tol"]); max_iter.append(rp["max_iter"])
+            m += k
+        dev = data.device
+        self.M, self.F = m, len(tasks)
+        i32 = lambda v: torch.tensor(v, dtype=torch.int32, device=dev)
+        self.col0_l, self.K_l, self.kind_l, self.split_l = col0, K, kind, split
+        self.col0, self.K, self.kind, self.split = i32(col0), i32(K), i32(kind), i32(split)
+        self.scale = torch.tensor(scale, dtype=torch.float32, device=dev)
+        self.col_fit = torch.repeat_interleave(torch.arange(self.F, device=dev), torch.tensor(K, device=dev))
+        lam_t = torch.tensor(lam, dtype=torch.float32, device=dev)
+        self.lam_col = lam_t[self.col_fit]
+        self.icpt_col = torch.tensor(icpt, dtype=torch.float32, device=dev)[self.col_fit]
+        self.pen_icpt_col = torch.tensor(pen_icpt, dtype=torch.float32, device=dev)[self.col_fit]
+        self.tol = torch.tensor(tol, dtype=torch.float32, device=dev)
+        self.max_iter = torch.tensor(max_iter, dtype=torch.int64, device=dev)
+
+    def segsum(self, v: torch.Tensor) -> torch.Tensor:
+        out = torch.zeros(self.F, dtype=v.dtype, device=v.device)
+        return out.index_add_(0, self.col_fit, v)
+
+    def segmax(self, v: torch.Tensor) -> torch.Tensor:
+        out = torch.zeros(self.F, dtype=v.dtype, device=v.device)
+        return out.scatter_reduce_(0, self.col_fit, v, reduce="amax", include_self=True)
+
+
+class LogisticFamily(Family):
+    model_types = ("LogisticRegression",)
+    classifiers = ("LogisticRegression",)
+    history = 10
+
+    def resolve(self, model_type, params, n_train, n_features, n_classes):
+        p = dict(_LR_DEFAULTS)
+        p.update({k: v for k, v in params.items() if k in _LR_DEFAULTS})
+        warn = []
+        unknown = sorted(k for k in params if k not in _LR_DEFAULTS)
+        if unknown:
+            warn.append(f"ignored unknown parameters {unknown}")
+        solver = p["solver"] or "lbfgs"
+        if solver not in _SOLVERS:
+            raise ParamError(f"solver must be one of {_SOLVERS}, got {solver!r}")
+        penalty = p["penalty"]
+        if penalty in ("none", "None"):
+            penalty = None
+        if penalty not in ("l2", None, "l1", "elasticnet"):
+            raise ParamError(f"penalty {penalty!r} invalid")
+        if penalty in ("l1", "elasticnet"):
+            if penalty == "l1" and solver not in ("liblinear", "saga"):
+                raise ParamError(f"Solver {solver} supports only 'l2' or None penalties, got l1 penalty.")
+            raise ParamError(f"penalty={penalty!r} is not implemented on the device solver yet")
+        if penalty is None and solver == "liblinear":
+            raise ParamError("penalty=None is not supported for the liblinear solver")
+        C = as_float(p["C"], "C", lo=0.0)
+        if C <= 0:
+            raise ParamError("Penalty term must be positive")
+        mc = p["multi_class"]
+        ovr = solver == "liblinear" or mc == "ovr"
+        if p["class_weight"] not in (None, "None"):
+            warn.append("class_weight is not supported yet; fitted unweighted")
+        if as_bool(p["dual"], "dual"):
+            warn.append("dual=True solved in the primal (same optimum)")
+        return {
+            "C": None if penalty is None else C,
+            "tol": as_float(p["tol"], "tol", lo=0.0),
+            "max_iter": as_int(p["max_iter"], "max_iter", lo=0),
+            "fit_intercept": as_bool(p["fit_intercept"], "fit_intercept"),
+            "intercept_scaling": as_float(p["intercept_scaling"], "intercept_scaling", lo=0.0)
+            if solver == "liblinear" else 1.0,
+            "penalize_intercept": solver == "liblinear",
+            "ovr": ovr,
+            "solver": solver,
+            "seed": seed_of(p["random_state"]),
+            "warnings": warn,
+        }
+
+    def cost(self, model_type, rp, n_train, n_features, n_classes) -> float:
+        return max(1, rp["max_iter"]) * n_train * (n_features + 1) * max(1, n_classes - 1) * 4e-12 + 1e-3
+
+    # --------------------------------------------------------------------------------
+    def _objective(self, data, b: _Batch, W: torch.Tensor):
+        X = data.X
+        d = data.d
+        Z = torch.addmm(W[d] * b.icpt_col, X, W[:d])
+        if data.is_gpu:
+            R = torch.empty_like(Z)
+            loss = torch.empty(b.F, dtype=torch.float64, device=Z.device)
+            lib = native.hip_lib()
+            rc = lib.dml_lr_link_grad(native.ptr(Z), data.n, b.M, native.ptr(data.y_cls), native.ptr(data.roles),
+                                      native.ptr(b.col0), native.ptr(b.K), native.ptr(b.kind), native.ptr(b.split),
+                                      native.ptr(b.scale), b.F, native.ptr(R), native.ptr(loss),
+                                      native.stream_handle(data.device))
+            if rc:
+                raise RuntimeError("dml_lr_link_grad failed")
+        else:
+            R, loss = link_grad_torch(Z, data.y_cls, data.roles, b.col0_l, b.K_l, b.kind_l, b.split_l, b.scale.tolist())
+        G = torch.empty_like(W)
+        G[:d] = X.t() @ R
+        G[d] = R.sum(0) * b.icpt_col
+        reg = W * b.lam_col
+        reg[d] = reg[d] * b.pen_icpt_col
+        G += reg
+        f = loss + 0.5 * b.segsum((W * reg).sum(0)).double()
+        return f, G
+
+    def _solve(self, data, b: _Batch):
+        d, dev = data.d, data.device
+        W = torch.zeros((d + 1, b.M), dtype=torch.float32, device=dev)
+        f, G = self._objective(data, b, W)
+        hs, hy, hrho = [], [], []
+        iters = torch.zeros(b.F, dtype=torch.int64, device=dev)
+        stalled = torch.zeros(b.F, dtype=torch.bool, device=dev)
+        max_it = int(b.max_iter.max().item()) if b.F else 0
+        n_evals = 1
+        for it in range(max_it):
+            gmax = b.segmax(G.abs().amax(0))
+            active = (gmax > b.tol) & (iters < b.max_iter) & ~stalled
+            if not bool(active.any()):
+                break
+            act_col = active[b.col_fit].to(W.dtype)
+            q = G.clone()
+            alphas = []
+            for s, y, rho in zip(reversed(hs), reversed(hy), reversed(hrho)):
+                a = rho * b.segsum((s * q).sum(0))
+                q -= a[b.col_fit] * y
+                alphas.append(a)
+            if hs:
+                sy = b.segsum((hs[-1] * hy[-1]).sum(0))
+                yy = b.segsum((hy[-1] * hy[-1]).sum(0))
+                gamma = torch.where(yy > 0, sy / yy.clamp_min(1e-30), torch.ones_like(yy))
+            else:
+                gnorm = b.segsum((G * G).sum(0)).sqrt()
+                gamma = 1.0 / gnorm.clamp_min(1.0)
+            r = q * gamma[b.col_fit]
+            for (s, y, rho), a in zip(zip(hs, hy, hrho), reversed(alphas)):
+                bb = rho * b.segsum((y * r).sum(0))
+                r += (a - bb)[b.col_fit] * s
+            p = -r * act_col
+            gtp = b.segsum((G * p).sum(0))
+            bad = (gtp >= 0) & active
+            if bool(bad.any()):  # not a descent direction: restart from steepest descent
+                badc = bad[b.col_fit].to(W.dtype)
+                p = p * (1 - badc) - G * badc * act_col
+                gtp = b.segsum((G * p).sum(0))
+            step = torch.ones(b.F, dtype=torch.float32, device=dev)
+            for _ls in range(30):
+                Wt = W + p * step[b.col_fit]
+                ft, Gt = self._objective(data, b, Wt)
+                n_evals += 1
+                slack = 1e-7 * f.abs() + 1e-12  # float32 objective: tolerate round-off near the optimum
+                ok = (ft <= f + 1e-4 * step.double() * gtp.double() + slack) | ~active
+                if bool(ok.all()):
+                    break
+                step = torch.where(ok, step, step * 0.5)
+            else:
+                stalled |= ~ok
+                okc = ok[b.col_fit].to(W.dtype)
+                Wt = W + p * (step * ok.to(step.dtype))[b.col_fit]
+                ft, Gt = self._objective(data, b, Wt)
+                n_evals += 1
+            s_vec = Wt - W
+            y_vec = Gt - G
+            sy = b.segsum((s_vec * y_vec).sum(0))
+            rho = torch.where(sy > 1e-10, 1.0 / sy.clamp_min(1e-10), torch.zeros_like(sy))
+            hs.append(s_vec); hy.append(y_vec); hrho.append(rho)
+            if len(hs) > self.history:
+                hs.pop(0); hy.pop(0); hrho.pop(0)
+            W, f, G = Wt, ft, Gt
+            iters += active.to(torch.int64)
+        return W, iters, n_evals
+
+    def run(self, data, tasks: List[FitTask], keep_models: bool = False) -> List[FitOutput]:
+        if not tasks:
+            return []
+        if not data.classification:
+            raise ParamError("LogisticRegression needs a classification target")
+        t0 = time.perf_counter()
+        b = _Batch(data, tasks)
+        W, iters, n_evals = self._solve(data, b)
+        d = data.d
+        Z = torch.addmm(W[d] * b.icpt_col, data.X, W[:d])
+        outs = []
+        for f, t in enumerate(tasks):
+            c0, k = b.col0_l[f], b.K_l[f]
+            z = Z[data.test_rows[t.split].long(), c0:c0 + k]
+            if b.kind_l[f] == KIND_BINARY:
+                pred = (z[:, 0] > 0).to(torch.int32)
+                proba = torch.sigmoid(z[:, 0])
+                proba = torch.stack([1 - proba, proba], 1)
+            else:
+                pred = z.argmax(1).to(torch.int32)
+                proba = torch.softmax(z, 1) if b.kind_l[f] == KIND_SOFTMAX else None
+                if proba is None:
+                    pz = torch.sigmoid(z)
+                    proba = pz / pz.sum(1, keepdim=True).clamp_min(1e-30)
+            outs.append(FitOutput(task_id=t.task_id, pred=pred, proba=proba,
+                                  info={"warnings": t.params.get("warnings", []), "n_iter": int(iters[f].item())}))
+        if data.is_gpu:
+            torch.cuda.synchronize(data.device)
+        dt = time.perf_counter() - t0
+        for o in outs:
+            o.fit_seconds = dt / len(outs)
+            o.info["objective_evals"] = n_evals
+        if keep_models:
+            for f, (o, t) in enumerate(zip(outs, tasks)):
+                c0, k = b.col0_l[f], b.K_l[f]
+                o.model = {
+                    "kind": "linear_logistic", "coef": W[:d, c0:c0 + k].t().cpu().numpy(),
+                    "intercept": (W[d, c0:c0 + k] * b.icpt_col[c0:c0 + k]).cpu().numpy(),
+                    "link": b.kind_l[f], "classes": np.asarray(data.classes).tolist(),
+                    "model_type": t.model_type, "params": {k2: v for k2, v in t.params.items() if k2 != "warnings"},
+                }
+        return outs
+
+
+_LIN_DEFAULTS = {"fit_intercept": True, "copy_X": True, "n_jobs": None, "positive": False}
+
+
+class LinearRegressionFamily(Family):
+    model_types = ("LinearRegression",)
+    classifiers = ()
+
+    def resolve(self, model_type, params, n_train, n_features, n_classes):
+        p = dict(_LIN_DEFAULTS)
+        p.update({k: v for k, v in params.items() if k in _LIN_DEFAULTS})
+        warn = []
+        if as_bool(p["positive"], "positive"):
+            warn.append("positive=True not supported; unconstrained least squares used")
+        return {"fit_intercept": as_bool(p["fit_intercept"], "fit_intercept"), "warnings": warn}
+
+    def cost(self, model_type, rp, n_train, n_features, n_classes) -> float:
+        return n_train * n_features * n_features * 2e-12 + 1e-3
+
+    def run(self, data, tasks, keep_models=False):
+        t0 = time.perf_counter()
+        X, y = data.X, data.y_reg
+        cache: Dict[tuple, tuple] = {}
+        outs = []
+        for t in tasks:
+            key = (t.split, t.params["fit_intercept"])
+            if key not in cache:
+                tr = data.train_rows[t.split].long()
+                Xt, yt = X[tr].double(), y[tr].double()
+                if t.params["fit_intercept"]:
+                    xm, ym = Xt.mean(0), yt.mean()
+                    Xc, yc = Xt - xm, yt - ym
+                else:
+                    xm = torch.zeros(data.d, dtype=torch.float64, device=X.device)
+                    ym = torch.zeros((), dtype=torch.float64, device=X.device)
+                    Xc, yc = Xt, yt
+                A = Xc.t() @ Xc
+                w = torch.linalg.pinv(A, hermitian=True) @ (Xc.t() @ yc)
+                b0 = ym - xm @ w
+                cache[key] = (w, b0)
+            w, b0 = cache[key]
+            te = data.test_rows[t.split].long()
+            pred = (X[te].double() @ w + b0).float()
+            o = FitOutput(task_id=t.task_id, pred=pred, info={"warnings": t.params.get("warnings", [])})
+            if keep_models:
+                o.model = {"kind": "linear_regression", "coef": w.cpu().numpy(), "intercept": float(b0),
+                           "model_type": t.model_type, "params": {"fit_intercept": t.params["fit_intercept"]}}
+            outs.append(o)
+        if data.is_gpu:
+            torch.cuda.synchronize(data.device)
+        dt = time.perf_counter() - t0
+        for o in outs:
+            o.fit_seconds = dt / max(1, len(outs))
+        return outs
+
+
+register(LogisticFamily())
+register(LinearRegressionFamily())

@@ -1,0 +1,143 @@
+"""Scorers (``GridSearchCV(scoring=...)``) evaluated on-device from batched predictions.
+
+The reference hard-codes ``accuracy`` / ``r2`` and ignores the user's ``scoring``
+(aws-prod/worker/worker.py:326,341 vs master/task_handler.py:183; defect D6).  Here the
+common sklearn scorer names are honoured; all are "greater is better" like sklearn's
+(``neg_*`` for losses).  Inputs are encoded class ids (classification) or float
+targets, on whatever device the fit ran.
+"""
+from __future__ import annotations
+
+import math
+from typing import Callable, Dict, Optional
+
+import torch
+
+CLS_SCORERS = (
+    "accuracy", "balanced_accuracy", "f1", "f1_macro", "f1_micro", "f1_weighted", "precision", "precision_macro",
+    "precision_micro", "precision_weighted", "recall", "recall_macro", "recall_micro", "recall_weighted", "roc_auc",
+    "neg_log_loss", "jaccard", "jaccard_macro",
+)
+REG_SCORERS = (
+    "r2", "neg_mean_squared_error", "neg_mean_absolute_error", "neg_root_mean_squared_error", "explained_variance",
+    "max_error", "neg_median_absolute_error", "neg_mean_absolute_percentage_error",
+)
+
+
+def default_scoring(is_classifier: bool) -> str:
+    return "accuracy" if is_classifier else "r2"
+
+
+def validate_scoring(scoring, is_classifier: bool) -> str:
+    if scoring in (None, "None", ""):
+        return default_scoring(is_classifier)
+    if not isinstance(scoring, str):
+        raise ValueError(f"scoring must be a scorer name, got {scoring!r}")
+    allowed = CLS_SCORERS if is_classifier else REG_SCORERS
+    if scoring not in allowed:
+        raise ValueError(f"scoring {scoring!r} not supported for this estimator; choose from {allowed}")
+    return scoring
+
+
+def _confusion(y: torch.Tensor, p: torch.Tensor, C: int) -> torch.Tensor:
+    idx = y.long() * C + p.long()
+    return torch.bincount(idx, minlength=C * C).reshape(C, C).double()
+
+
+def _prf(cm: torch.Tensor, avg: str, what: str) -> float:
+    tp = torch.diag(cm)
+    pred_pos = cm.sum(0)
+    true_pos = cm.sum(1)
+    if avg == "micro":
+        return float(tp.sum() / cm.sum().clamp_min(1)) if what != "jaccard" else float(
+            tp.sum() / (pred_pos.sum() + true_pos.sum() - tp.sum()).clamp_min(1))
+    prec = torch.where(pred_pos > 0, tp / pred_pos.clamp_min(1), torch.zeros_like(tp))
+    rec = torch.where(true_pos > 0, tp / true_pos.clamp_min(1), torch.zeros_like(tp))
+    if what == "precision":
+        v = prec
+    elif what == "recall":
+        v = rec
+    elif what == "jaccard":
+        den = pred_pos + true_pos - tp
+        v = torch.where(den > 0, tp / den.clamp_min(1), torch.zeros_like(tp))
+    else:
+        den = prec + rec
+        v = torch.where(den > 0, 2 * prec * rec / den.clamp_min(1e-30), torch.zeros_like(tp))
+    if avg == "binary":
+        return float(v[1]) if v.numel() > 1 else 0.0
+    if avg == "weighted":
+        return float((v * true_pos).sum() / true_pos.sum().clamp_min(1))
+    return float(v.mean())
+
+
+def _auc(y: torch.Tensor, s: torch.Tensor) -> float:
+    y = y.double()
+    order = torch.argsort(s.double())
+    ss = s.double()[order]
+    ranks = torch.empty_like(ss)
+    # average ranks for ties
+    uniq, inv, counts = torch.unique_consecutive(ss, return_inverse=True, return_counts=True)
+    ends = torch.cumsum(counts, 0).double()
+    starts = ends - counts.double() + 1
+    avg = (starts + ends) / 2
+    ranks = avg[inv]
+    yo = y[order]
+    n1 = float(yo.sum())
+    n0 = float(len(yo) - n1)
+    if n1 == 0 or n0 == 0:
+        return float("nan")
+    return float((ranks[yo > 0.5].sum() - n1 * (n1 + 1) / 2) / (n1 * n0))
+
+
+def score(name: str, y_true: torch.Tensor, pred: torch.Tensor, n_classes: int = 2,
+          proba: Optional[torch.Tensor] = None) -> float:
+    """Scalar score for one fit (greater is better)."""
+    if y_true.numel() == 0:
+        return float("nan")
+    if name == "accuracy":
+        return float((pred.long() == y_true.long()).double().mean())
+    if name == "balanced_accuracy":
+        cm = _confusion(y_true, pred, n_classes)
+        tp, tot = torch.diag(cm), cm.sum(1)
+        m = tot > 0
+        return float((tp[m] / tot[m]).mean())
+    for what in ("precision", "recall", "f1", "jaccard"):
+        if name == what or name.startswith(what + "_"):
+            avg = name.split("_", 1)[1] if "_" in name else "binary"
+            if avg == "binary" and n_classes != 2:
+                raise ValueError(f"{name} needs a binary target; use {name}_macro")
+            return _prf(_confusion(y_true, pred, n_classes), avg, what)
+    if name == "roc_auc":
+        if proba is None or n_classes != 2:
+            raise ValueError("roc_auc needs probabilities of a binary classifier")
+        return _auc(y_true, proba[:, 1])
+    if name == "neg_log_loss":
+        if proba is None:
+            raise ValueError("neg_log_loss needs probabilities")
+        p = proba.double().clamp(1e-15, 1 - 1e-15)
+        p = p / p.sum(1, keepdim=True)
+        return float(torch.log(p.gather(1, y_true.long().view(-1, 1))).mean())
+    yt, yp = y_true.double(), pred.double()
+    err = yp - yt
+    if name == "r2":
+        ss_res = float((err * err).sum())
+        ss_tot = float(((yt - yt.mean()) ** 2).sum())
+        if ss_tot == 0.0:
+            return 1.0 if ss_res == 0.0 else 0.0
+        return 1.0 - ss_res / ss_tot
+    if name == "neg_mean_squared_error":
+        return -float((err * err).mean())
+    if name == "neg_root_mean_squared_error":
+        return -math.sqrt(float((err * err).mean()))
+    if name == "neg_mean_absolute_error":
+        return -float(err.abs().mean())
+    if name == "neg_median_absolute_error":
+        return -float(err.abs().median())
+    if name == "max_error":
+        return -float(err.abs().max())
+    if name == "explained_variance":
+        vt = float(yt.var(unbiased=False))
+        return 1.0 - float(err.var(unbiased=False)) / vt if vt > 0 else (1.0 if float(err.var()) == 0 else 0.0)
+    if name == "neg_mean_absolute_percentage_error":
+        return -float((err.abs() / yt.abs().clamp_min(torch.finfo(torch.float64).eps)).mean())
+    raise ValueError(f"unknown scorer {name!r}")

@@ -153,7 +153,9 @@ def hip_lib() -> ctypes.CDLL:
 def _register_optional(lib) -> None:
     """Signatures of kernels added in later files (absent symbols are skipped)."""
     table = {
-        "dml_lr_softmax_grad": (c_i32, [c_vp] * 8 + [c_i64] * 5 + [c_vp]),
+        "dml_lr_link_grad": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
+                                     c_vp]),
+        "dml_lr_predict": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     }
     for name, (res, args) in table.items():
         fn = getattr(lib, name, None)
