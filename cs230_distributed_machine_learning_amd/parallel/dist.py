@@ -1,0 +1,135 @@
+"""Process-group plumbing: one process per GPU, ``torch.distributed`` over RCCL/xGMI.
+
+Replaces the reference's transport layer (Kafka topics tasks/train/result/metrics,
+Redis, HTTP heartbeats) for the single-node design:
+* collectives (dataset all-gather/broadcast, score all-reduce) go over RCCL — the
+  ``nccl`` backend IS RCCL on ROCm — and ride the point-to-point xGMI links;
+* small control traffic (job announcements, work-claim counters, heartbeats) goes
+  through the rendezvous ``TCPStore`` (``store.add`` is an atomic counter).
+On a CPU box the same code runs on ``gloo`` (tests use world_size 2).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+
+    @property
+    def is_dist(self) -> bool:
+        return self.world > 1 and dist.is_initialized()
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+
+_INFO: Optional[DistInfo] = None
+
+
+def init(backend: Optional[str] = None, timeout_s: float = 1800.0, want_gpu: Optional[bool] = None) -> DistInfo:
+    """Initialise from torchrun env vars (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
+    global _INFO
+    if _INFO is not None:
+        return _INFO
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = torch.cuda.is_available() if want_gpu is None else want_gpu
+    if gpu:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    be = "none"
+    if world > 1:
+        be = backend or ("nccl" if gpu else "gloo")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
+        if be == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+    _INFO = DistInfo(rank, world, local, device, be)
+    return _INFO
+
+
+def info() -> DistInfo:
+    return _INFO or DistInfo()
+
+
+def barrier() -> None:
+    if info().is_dist:
+        if info().backend == "nccl":
+            dist.barrier(device_ids=[info().local_rank])
+        else:
+            dist.barrier()
+
+
+def broadcast(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    if info().is_dist:
+        dist.broadcast(t, src=src)
+    return t
+
+
+def all_gather_rows(shard: torch.Tensor) -> torch.Tensor:
+    """Concatenate equal-size row shards of every rank (rank order) on every rank."""
+    inf = info()
+    if not inf.is_dist:
+        return shard
+    shard = shard.contiguous()
+    out = torch.empty((shard.shape[0] * inf.world, *shard.shape[1:]), dtype=shard.dtype, device=shard.device)
+    if inf.backend == "nccl":
+        dist.all_gather_into_tensor(out, shard)
+    else:
+        parts = list(out.chunk(inf.world, 0))
+        dist.all_gather(parts, shard)
+    return out
+
+
+def all_reduce_sum(t: torch.Tensor) -> torch.Tensor:
+    if info().is_dist:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+
+
+def all_reduce_max(t: torch.Tensor) -> torch.Tensor:
+    if info().is_dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t
+
+
+def gather_objects(obj) -> List:
+    inf = info()
+    if not inf.is_dist:
+        return [obj]
+    out: List = [None] * inf.world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def store():
+    """The default group's TCPStore (None when not distributed)."""
+    if not info().is_dist:
+        return None
+    from torch.distributed.distributed_c10d import _get_default_store
+
+    return _get_default_store()
+
+
+def destroy() -> None:
+    global _INFO
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _INFO = None
