@@ -50,11 +50,13 @@ struct ForestArgs {
   int64_t wave_max, block_max, chunk;
   int64_t kg_wave, kg_block, kg_large;
   int64_t slack_wave;
+  int64_t sub_max, sub_cache_d;
   // outputs
   int64_t n_nodes_out, status_out, levels_out, large_rounds_out;
 };
 
-enum CounterSlot { kCntSets = 0 /*6*/, kPool = 6, kOverflow = 7, kNeedMore = 8, kOpenOvf = 9, kNumCounters = 16 };
+constexpr int kTiers = 4;  // 0 subtree, 1 wave, 2 block, 3 large
+enum CounterSlot { kCntSets = 0 /*8*/, kPool = 8, kOverflow = 9, kNeedMore = 10, kOpenOvf = 11, kNumCounters = 16 };
 
 struct LState {
   OpenNode on;
@@ -80,8 +82,8 @@ struct Ctx {
   double* node_val;
   int64_t pool_cap;
   double* tree_W;
-  OpenNode* open[2][3];
-  int64_t open_cap[3];
+  OpenNode* open[2][kTiers];
+  int64_t open_cap[kTiers];
   int32_t* counters;
   int32_t* cursors;      // [T]
   LState* lstate;
@@ -91,6 +93,7 @@ struct Ctx {
   int32_t* lcursor;      // [cap_large][2]
   int64_t large_cap;
   int32_t wave_max, block_max, chunk, kg_wave, kg_block, kg_large, slack_wave;
+  int32_t sub_max, sub_cache_d;
 };
 
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -125,8 +128,8 @@ __device__ void enqueue_or_leaf(const Ctx& c, int tree, int node, int start, int
   const TreeSpec& s = c.specs[tree];
   if (leaf_by_counts(s, count, depth)) return;
   if (node_impurity(c, node, s.criterion) <= kEps) return;
-  const int tier = count <= c.wave_max ? 0 : (count <= c.block_max ? 1 : 2);
-  const int idx = atomicAdd(&c.counters[set * 3 + tier], 1);
+  const int tier = count <= c.sub_max ? 0 : (count <= c.wave_max ? 1 : (count <= c.block_max ? 2 : 3));
+  const int idx = atomicAdd(&c.counters[set * kTiers + tier], 1);
   if (idx >= c.open_cap[tier]) {
     atomicOr(&c.counters[kOpenOvf], 1);
     return;
@@ -408,13 +411,215 @@ __global__ __launch_bounds__(NT) void k_nodes(Ctx c, int tier, int set_cur) {
 }
 
 // ------------------------------------------------------------------------------------
+// subtree tier: one wave grows the WHOLE subtree under a node with <= 64 rows
+// ------------------------------------------------------------------------------------
+// Each lane owns one row (bin row cached in LDS, class/target and bootstrap weight in
+// registers).  A node is a 64-bit lane mask; the subtree is walked depth-first with an
+// LDS stack.  A feature is evaluated by an in-wave bitonic sort of (bin, lane) keys
+// followed by wave prefix sums of the class weights — every candidate threshold is one
+// lane, no 256-bin histogram is cleared, scanned or flushed.  Candidates are only the
+// last lane of each run of equal bins, so the chosen split equals the CPU builder's
+// (cumulative sums at "bin <= b" are the same integers).
+struct SubEntry {
+  uint64_t mask;
+  uint64_t key;
+  int32_t node, depth;
+};
+
+__device__ __forceinline__ uint32_t bitonic64(uint32_t key, int lane) {
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const uint32_t other = __shfl_xor(key, j);
+      const bool up = (lane & k) == 0;
+      const bool lower = (lane & j) == 0;
+      const uint32_t mn = min(key, other), mx = max(key, other);
+      key = (lower == up) ? mn : mx;
+    }
+  }
+  return key;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const T o = __shfl_up(v, off);
+    if (lane >= off) v += o;
+  }
+  return v;
+}
+
+// evaluate one feature for the rows in `mask`; lane data: bin b (valid if in mask).
+// returns gain/bin via references (uniform across the wave) and whether non-constant.
+template <bool REG>
+__device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt, int lane, int my_bin, int my_cls,
+                         float my_w, float my_y, double& gain, int& bin, bool& nonconst) {
+  const bool act = (mask >> lane) & 1ull;
+  const uint32_t key = act ? ((uint32_t)my_bin << 6) | (uint32_t)lane : 0xFFFFFFFFu;
+  const uint32_t sk = bitonic64(key, lane);
+  const bool valid_row = lane < cnt;
+  const int src = (int)(sk & 63u);
+  const int b = valid_row ? (int)(sk >> 6) : 1024;
+  const int bnext = __shfl_down(b, 1);
+  const int blast = __shfl(b, cnt - 1);
+  const int bfirst = __shfl(b, 0);
+  nonconst = bfirst != blast;
+  const int lrows = lane + 1, rrows = cnt - lrows;
+  const bool cand = valid_row && lane < cnt - 1 && b != bnext && lrows >= s.min_samples_leaf &&
+                    rrows >= s.min_samples_leaf;
+  double g = -INFINITY;
+  if constexpr (!REG) {
+    // every shuffle runs with the full wave active (a shuffle inside a divergent branch
+    // would read lanes outside EXEC); select afterwards
+    const int ycls = __shfl(my_cls, src);
+    const float wsh = __shfl(my_w, src);
+    const uint32_t w = valid_row ? (uint32_t)wsh : 0u;
+    ClsAcc L, R;
+    L.init(); R.init();
+    for (int k = 0; k < c.C; ++k) {
+      const uint32_t v = (ycls == k) ? w : 0u;
+      const uint32_t pre = wave_incl_scan<uint32_t>(v, lane);
+      const uint32_t tot = __shfl(pre, cnt - 1);
+      L.add((double)pre);
+      R.add((double)(tot - pre));
+    }
+    if (cand) g = cls_proxy(L, R, s.criterion);
+  } else {
+    const float wsh = __shfl(my_w, src);
+    const float y = __shfl(my_y, src);
+    const float w = valid_row ? wsh : 0.f;
+    const float p0 = wave_incl_scan<float>(w, lane);
+    const float p1 = wave_incl_scan<float>(w * y, lane);
+    const float t0 = __shfl(p0, cnt - 1), t1 = __shfl(p1, cnt - 1);
+    if (cand) g = mse_proxy((double)p0, (double)p1, (double)(t0 - p0), (double)(t1 - p1));
+  }
+  int bl = cand ? lane : 64;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double og = __shfl_xor(g, off);
+    const int ol = __shfl_xor(bl, off);
+    if (og > g || (og == g && ol < bl)) { g = og; bl = ol; }
+  }
+  gain = g;
+  const int bsel = __shfl(b, bl & 63);
+  bin = bl < 64 ? bsel : -1;
+}
+
+template <bool REG>
+__global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const OpenNode on = c.open[set_cur][0][blockIdx.x];
+  const TreeSpec& s = c.specs[on.tree];
+  const int lane = threadIdx.x;
+  const int d = c.d;
+  const bool cache = c.sub_cache_d > 0;
+  const int dp = c.sub_cache_d;
+  const int perm_bytes = ((d * 2 + 15) / 16) * 16;
+  int16_t* perm = (int16_t*)smem;
+  SubEntry* stack = (SubEntry*)(smem + perm_bytes);
+  double* left_ch = (double*)(stack + 64);
+  uint8_t* xc = (uint8_t*)(left_ch + ((c.VC + 1) & ~1));
+  const int cnt0 = on.count;
+  const uint32_t* rows = c.rows_cur + c.row_off[on.tree] + on.start;
+  uint32_t row = 0;
+  int my_cls = 0;
+  float my_w = 0.f, my_y = 0.f;
+  if (lane < cnt0) {
+    row = rows[lane];
+    my_w = (float)boot_weight(s, row);
+    if constexpr (REG) my_y = c.yreg[row];
+    else my_cls = c.ycls[row];
+  }
+  const uint8_t* xg = c.Xb + (int64_t)row * c.ld;
+  if (cache && lane < cnt0)
+    for (int j = 0; j < d; ++j) xc[lane * dp + j] = xg[j];
+  if (lane == 0) {
+    SubEntry e;
+    e.mask = cnt0 >= 64 ? ~0ull : ((1ull << cnt0) - 1ull);
+    e.key = on.key; e.node = on.node; e.depth = on.depth;
+    stack[0] = e;
+  }
+  wave_lds_sync();
+  int sp = 1;
+  while (sp > 0) {
+    --sp;
+    const SubEntry e = stack[sp];
+    const int cnt = __popcll(e.mask);
+    // compact the node's lanes to 0..cnt-1 order is not needed: sub_eval sorts by (bin, lane)
+    for (int f = lane; f < d; f += 64) perm[f] = (int16_t)f;
+    wave_lds_sync();
+    int nonconst = 0, best_f = -1, best_b = -1;
+    double best_g = -INFINITY;
+    for (int pos = 0; nonconst < s.max_features && pos < d; ++pos) {
+      if (lane == 0) {
+        const int t = perm_pick(e.key, pos, d);
+        const int16_t tmp = perm[pos]; perm[pos] = perm[t]; perm[t] = tmp;
+      }
+      wave_lds_sync();
+      const int f = perm[pos];
+      const int my_bin = cache ? xc[lane * dp + f] : (lane < cnt0 ? xg[f] : 0);
+      double g;
+      int bb;
+      bool nc;
+      sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_y, g, bb, nc);
+      if (nc) {
+        ++nonconst;
+        if (bb >= 0 && g > best_g) { best_g = g; best_f = f; best_b = bb; }
+      }
+    }
+    if (best_f < 0) continue;
+    const int mybin = cache ? xc[lane * dp + best_f] : (lane < cnt0 ? xg[best_f] : 0);
+    const bool in = (e.mask >> lane) & 1ull;
+    const uint64_t lm = __ballot(in && mybin <= best_b) & e.mask;
+    const uint64_t rm = e.mask & ~lm;
+    // left child statistics (class weights / regression sums) by wave reductions
+    for (int k = 0; k < c.VC; ++k) {
+      double v;
+      const bool inl = (lm >> lane) & 1ull;
+      if constexpr (REG) {
+        v = !inl ? 0.0 : (k == 0 ? (double)my_w : (k == 1 ? (double)my_w * my_y : (double)my_w * my_y * my_y));
+      } else {
+        v = (inl && my_cls == k) ? (double)my_w : 0.0;
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0) left_ch[k] = v;
+    }
+    wave_lds_sync();
+    int base = -1;
+    if (lane == 0) {
+      if (accept_split(c, s, e.node, on.tree, left_ch)) base = make_children(c, e.node, best_f, best_b, left_ch);
+    }
+    base = __shfl(base, 0);
+    if (base < 0) continue;
+    const int nl = __popcll(lm), nr = cnt - nl;
+    // push right then left (left subtree first); leaf-by-count/purity children are not pushed
+    if (lane == 0) {
+      const int dep = e.depth + 1;
+      if (!leaf_by_counts(s, nr, dep) && node_impurity(c, base + 1, s.criterion) > kEps) {
+        SubEntry r; r.mask = rm; r.key = child_key(e.key, 1); r.node = base + 1; r.depth = dep;
+        stack[sp++] = r;
+      }
+      if (!leaf_by_counts(s, nl, dep) && node_impurity(c, base, s.criterion) > kEps) {
+        SubEntry l; l.mask = lm; l.key = child_key(e.key, 0); l.node = base; l.depth = dep;
+        stack[sp++] = l;
+      }
+    }
+    sp = __shfl(sp, 0);
+    wave_lds_sync();
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // large tier
 // ------------------------------------------------------------------------------------
 __global__ void k_large_prep(Ctx c, int set_cur, int nL) {
   const int slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= nL) return;
   LState st;
-  st.on = c.open[set_cur][2][slot];
+  st.on = c.open[set_cur][3][slot];
   const TreeSpec& s = c.specs[st.on.tree];
   int16_t* perm = c.lperm + (int64_t)slot * c.d;
   for (int i = 0; i < c.d; ++i) perm[i] = (int16_t)i;
@@ -649,8 +854,8 @@ __global__ void k_roots(Ctx c) {
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct Layout {
-  size_t rows_b, open[2][3], counters, cursors, lstate, lperm, lbest, ghist, lcursor, total;
-  int64_t open_cap[3], large_cap;
+  size_t rows_b, open[2][kTiers], counters, cursors, lstate, lperm, lbest, ghist, lcursor, total;
+  int64_t open_cap[kTiers], large_cap;
 };
 
 static Layout plan(const ForestArgs* a) {
@@ -659,15 +864,16 @@ static Layout plan(const ForestArgs* a) {
   const int64_t C = a->is_reg ? 3 : a->n_classes;
   const int64_t CH = a->is_reg ? 4 : a->n_classes + 1;
   L.open_cap[0] = R / 2 + T + 16;
-  L.open_cap[1] = R / (a->wave_max + 1) + T + 16;
-  L.open_cap[2] = R / (a->block_max + 1) + T + 16;
-  L.large_cap = L.open_cap[2];
+  L.open_cap[1] = R / (a->sub_max + 1) + T + 16;
+  L.open_cap[2] = R / (a->wave_max + 1) + T + 16;
+  L.open_cap[3] = R / (a->block_max + 1) + T + 16;
+  L.large_cap = L.open_cap[3];
   (void)C;
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
   L.rows_b = take((size_t)R * 4);
   for (int s = 0; s < 2; ++s)
-    for (int t = 0; t < 3; ++t) L.open[s][t] = take((size_t)L.open_cap[t] * sizeof(OpenNode));
+    for (int t = 0; t < kTiers; ++t) L.open[s][t] = take((size_t)L.open_cap[t] * sizeof(OpenNode));
   L.counters = take(kNumCounters * 4);
   L.cursors = take((size_t)T * 4);
   L.lstate = take((size_t)L.large_cap * sizeof(LState));
@@ -688,6 +894,13 @@ static size_t fused_lds(const ForestArgs* a, int KG) {
   return b;
 }
 
+static size_t sub_lds(const ForestArgs* a) {
+  const int VC = a->is_reg ? 3 : (int)a->n_classes;
+  size_t b = ((a->d * 2 + 15) / 16) * 16 + 64 * sizeof(SubEntry) + ((VC + 1) & ~1) * 8;
+  b += (size_t)64 * a->sub_cache_d + 16;
+  return b;
+}
+
 static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   Ctx c{};
   unsigned char* ws = (unsigned char*)a->workspace;
@@ -703,8 +916,8 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.tree_W = (double*)a->tree_W;
   c.rows_next = (uint32_t*)(ws + L.rows_b);
   for (int s = 0; s < 2; ++s)
-    for (int t = 0; t < 3; ++t) c.open[s][t] = (OpenNode*)(ws + L.open[s][t]);
-  for (int t = 0; t < 3; ++t) c.open_cap[t] = L.open_cap[t];
+    for (int t = 0; t < kTiers; ++t) c.open[s][t] = (OpenNode*)(ws + L.open[s][t]);
+  for (int t = 0; t < kTiers; ++t) c.open_cap[t] = L.open_cap[t];
   c.counters = (int32_t*)(ws + L.counters);
   c.cursors = (int32_t*)(ws + L.cursors);
   c.lstate = (LState*)(ws + L.lstate);
@@ -716,6 +929,8 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.wave_max = (int)a->wave_max; c.block_max = (int)a->block_max; c.chunk = (int)a->chunk;
   c.kg_wave = (int)a->kg_wave; c.kg_block = (int)a->kg_block; c.kg_large = (int)a->kg_large;
   c.slack_wave = (int)a->slack_wave;
+  c.sub_max = (int)a->sub_max;
+  c.sub_cache_d = (int)a->sub_cache_d;
   return c;
 }
 
@@ -742,7 +957,20 @@ static int32_t* pinned_counters() {
 
 using namespace dml;
 
+// kernel-level test hooks (tests/test_forest_gpu.py): in-wave sort and prefix scan
+__global__ void k_test_wave_prims(const uint32_t* in, uint32_t* sorted, uint32_t* scanned) {
+  const int lane = threadIdx.x;
+  const uint32_t v = in[blockIdx.x * 64 + lane];
+  sorted[blockIdx.x * 64 + lane] = bitonic64(v, lane);
+  scanned[blockIdx.x * 64 + lane] = wave_incl_scan<uint32_t>(v, lane);
+}
+
 extern "C" {
+
+int dml_test_wave_prims(const uint32_t* in, uint32_t* sorted, uint32_t* scanned, int64_t nblocks, hipStream_t st) {
+  k_test_wave_prims<<<(unsigned)nblocks, 64, 0, st>>>(in, sorted, scanned);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
 
 const char* dml_forest_last_error(int* line) {
   if (line) *line = g_last_err_line;
@@ -795,17 +1023,21 @@ int dml_forest_build(ForestArgs* a, hipStream_t st) {
   k_roots<<<(unsigned)((a->T + 255) / 256), 256, 0, st>>>(c);
   HIP_OK(hipGetLastError());
 
+  const size_t lds_s = sub_lds(a);
   const size_t lds_w = fused_lds(a, (int)a->kg_wave);
   const size_t lds_b = fused_lds(a, (int)a->kg_block);
   const int CH = c.CH;
   const size_t lds_hl = (size_t)a->kg_large * CH * 256 * 4;
   const size_t lds_sl = lds_hl + a->kg_large * 16 + 64;
   const size_t lds_max = 160 * 1024;
-  if (lds_w > lds_max || lds_b > lds_max || lds_sl > lds_max) return 7;
+  if (lds_w > lds_max || lds_b > lds_max || lds_sl > lds_max || lds_s > lds_max) return 7;
+  if (a->sub_max > 64) return 9;
   {
-    const int need = (int)std::max(lds_w, std::max(lds_b, lds_sl));
+    const int need = (int)std::max(std::max(lds_s, lds_w), std::max(lds_b, lds_sl));
     static int attr_set = 0;
     if (need > 64 * 1024 && need > attr_set) {
+      HIP_OK(hipFuncSetAttribute((const void*)k_subtree<false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_subtree<true>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_nodes<64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_nodes<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_nodes<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
@@ -823,17 +1055,21 @@ int dml_forest_build(ForestArgs* a, hipStream_t st) {
     HIP_OK(hipMemcpyAsync(h, c.counters, kNumCounters * 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     if (h[kOpenOvf]) { a->status_out = 4; break; }
-    const int nw = h[cur * 3 + 0], nb = h[cur * 3 + 1], nL = h[cur * 3 + 2];
-    if (nw + nb + nL == 0) break;
+    const int ns = h[cur * kTiers + 0], nw = h[cur * kTiers + 1], nb = h[cur * kTiers + 2], nL = h[cur * kTiers + 3];
+    if (ns + nw + nb + nL == 0) break;
     if (++levels > 1 << 20) return 8;
-    HIP_OK(hipMemsetAsync(c.counters + (1 - cur) * 3, 0, 12, st));
+    HIP_OK(hipMemsetAsync(c.counters + (1 - cur) * kTiers, 0, kTiers * 4, st));
+    if (ns) {
+      if (reg) k_subtree<true><<<ns, 64, lds_s, st>>>(c, cur);
+      else k_subtree<false><<<ns, 64, lds_s, st>>>(c, cur);
+    }
     if (nw) {
-      if (reg) k_nodes<64, true><<<nw, 64, lds_w, st>>>(c, 0, cur);
-      else k_nodes<64, false><<<nw, 64, lds_w, st>>>(c, 0, cur);
+      if (reg) k_nodes<64, true><<<nw, 64, lds_w, st>>>(c, 1, cur);
+      else k_nodes<64, false><<<nw, 64, lds_w, st>>>(c, 1, cur);
     }
     if (nb) {
-      if (reg) k_nodes<256, true><<<nb, 256, lds_b, st>>>(c, 1, cur);
-      else k_nodes<256, false><<<nb, 256, lds_b, st>>>(c, 1, cur);
+      if (reg) k_nodes<256, true><<<nb, 256, lds_b, st>>>(c, 2, cur);
+      else k_nodes<256, false><<<nb, 256, lds_b, st>>>(c, 2, cur);
     }
     if (nL) {
       k_large_prep<<<(nL + 63) / 64, 64, 0, st>>>(c, cur, nL);

@@ -30,6 +30,8 @@ INT32_MAX = 2**31 - 1
 class ForestTiers:
     """Node-size tiers of the HIP builder (see forest.hip header)."""
 
+    sub_max: int = 64          # <= 64 rows: one wave finishes the whole subtree (k_subtree)
+    sub_cache_max_d: int = 256  # cache the subtree's bin rows in LDS when d <= this
     wave_max: int = 256
     block_max: int = 16384
     chunk: int = 16384
@@ -67,6 +69,15 @@ class ForestBuild:
             return ForestBuild(self.nodes.cpu().numpy(), self.vals.cpu().numpy(), self.n_trees, self.VC,
                                self.is_reg, self.n_classes, dict(self.stats))
         return self
+
+
+def _sub_cache_stride(d: int) -> int:
+    """Row stride (bytes) of the subtree LDS cache: multiple of 4 with an odd word count
+    so 32 lanes reading the same feature hit 32 distinct banks."""
+    dp = (d + 3) // 4 * 4
+    if (dp // 4) % 2 == 0:
+        dp += 4
+    return dp
 
 
 def make_specs(n: int) -> np.ndarray:
@@ -116,6 +127,8 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     pool_cap = _pool_bound(counts, specs) + T
     a.wave_max, a.block_max, a.chunk = tiers.wave_max, tiers.block_max, tiers.chunk
     a.kg_wave, a.kg_block, a.kg_large, a.slack_wave = tiers.kg_wave, tiers.kg_block, tiers.kg_large, tiers.slack_wave
+    a.sub_max = tiers.sub_max
+    a.sub_cache_d = _sub_cache_stride(d) if d <= tiers.sub_cache_max_d else 0
     tree_W = torch.empty(T, dtype=torch.float64, device=dev)
     a.tree_W = native.ptr(tree_W)
     ws_bytes = lib.dml_forest_workspace_bytes(ctypes.byref(a))

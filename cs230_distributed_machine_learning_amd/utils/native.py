@@ -63,6 +63,7 @@ ForestArgs = _i64_struct(
         "workspace", "workspace_bytes",
         "wave_max", "block_max", "chunk",
         "kg_wave", "kg_block", "kg_large", "slack_wave",
+        "sub_max", "sub_cache_d",
         "n_nodes_out", "status_out", "levels_out", "large_rounds_out",
     ],
 )

@@ -54,13 +54,21 @@ def _data(n, d, n_classes=2, seed=0):
     return X.astype(np.float32), y
 
 
+TIERS = [
+    dict(sub_max=64, wave_max=256, block_max=2048, chunk=1024),
+    dict(sub_max=32, wave_max=200, block_max=1024, chunk=512),
+    dict(sub_max=0, wave_max=64, block_max=4096, chunk=2048),
+]
+
+
+@pytest.mark.parametrize("tiers", range(len(TIERS)))
 @pytest.mark.parametrize("n,d,C,kw", [
     (3000, 12, 2, {}),
     (20000, 20, 3, {"msl": 3}),
     (60000, 16, 2, {"max_depth": 12, "k": 16, "bootstrap": 0}),
     (5000, 30, 4, {"criterion": 0, "mss": 10}),
 ])
-def test_gpu_trees_match_cpu(n, d, C, kw):
+def test_gpu_trees_match_cpu(n, d, C, kw, tiers):
     X, y = _data(n, d, C)
     dev = torch.device("cuda:0")
     Xt = torch.from_numpy(X).to(dev)
@@ -72,7 +80,7 @@ def test_gpu_trees_match_cpu(n, d, C, kw):
     specs = _specs(3, 6, d, **kw)
     ycls = y.astype(np.int32)
     g = forest_ops.build_gpu(Xb, torch.from_numpy(ycls).to(dev), None, torch.from_numpy(roles).to(dev), specs, C, False,
-                             forest_ops.ForestTiers(wave_max=64, block_max=2048, chunk=1024))
+                             forest_ops.ForestTiers(**TIERS[tiers]))
     c = forest_ops.build_cpu(Xb_cpu, ycls, None, roles, specs, C, False)
     assert g.stats["nodes"] == c.stats["nodes"]
     gc = _canon(g.nodes.cpu().numpy(), g.vals.cpu().numpy(), len(specs))
@@ -123,3 +131,22 @@ def test_gpu_regression_close_to_cpu():
     r2 = lambda p: 1 - np.sum((p - y[rows]) ** 2) / np.sum((y[rows] - y[rows].mean()) ** 2)
     assert abs(r2(pg) - r2(pc)) < 0.02
     assert r2(pg) > 0.8
+
+
+def test_wave_primitives_sort_and_scan():
+    import ctypes
+
+    lib = native.hip_lib()
+    fn = lib.dml_test_wave_prims
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_void_p]
+    g = torch.Generator().manual_seed(0)
+    x = torch.randint(0, 1 << 14, (16, 64), generator=g, dtype=torch.int64).to(torch.int32)
+    x[3] = 7  # all equal
+    xd = x.cuda()
+    srt = torch.empty_like(xd)
+    scn = torch.empty_like(xd)
+    assert fn(xd.data_ptr(), srt.data_ptr(), scn.data_ptr(), 16, native.stream_handle()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(srt.cpu(), torch.sort(x, dim=1).values)
+    assert torch.equal(scn.cpu().long(), torch.cumsum(x.long(), dim=1))
