@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <stdio.h>
 #include "forest_common.h"
+#include "wave_ops.h"
 
 namespace dml {
 
@@ -53,6 +54,7 @@ struct ForestArgs {
   int64_t sub_max, sub_cache_d;
   // outputs
   int64_t n_nodes_out, status_out, levels_out, large_rounds_out;
+  int64_t tier_nodes_out[4];
 };
 
 constexpr int kTiers = 4;  // 0 subtree, 1 wave, 2 block, 3 large
@@ -63,6 +65,7 @@ struct LState {
   int32_t pos, nonconst, g, done;
   int32_t best_feat, best_bin, split, nl;
   double best_gain;
+  uint64_t last;   // rank of the last feature taken from the visiting order
 };
 
 struct Ctx {
@@ -163,31 +166,64 @@ __device__ int make_children(const Ctx& c, int node, int feat, int bin, const do
 }
 
 // ------------------------------------------------------------------------------------
-// histogram scan / evaluation — executed by ONE wave on one feature's [CH][256] image
+// histogram modes
 // ------------------------------------------------------------------------------------
+// MODE 0: classification, C class planes + 1 row-count plane of uint32 [CH][256]
+// MODE 1: binary classification, ONE uint64 plane: (w0 | w1 << 21 | rows << 42)
+// MODE 2: regression, float planes (sum w, sum wy, sum wy^2, rows) [4][256]
+template <int MODE> struct HT;
+template <> struct HT<0> { using T = uint32_t; };
+template <> struct HT<1> { using T = unsigned long long; };
+template <> struct HT<2> { using T = float; };
+
+__device__ __forceinline__ int hist_planes(int MODE, int CH) { return MODE == 1 ? 1 : CH; }
+
+// the next feature in the node's visiting order (see forest_common.h feature_rank):
+// min over f of rank(f) that is > `last` (or overall min when first).  ~0 if none.
+__device__ __forceinline__ uint64_t wave_next_feature(uint64_t node_key, int d, int lane, uint64_t last,
+                                                      bool first) {
+  uint64_t best = ~0ull;
+  for (int f = lane; f < d; f += 64) {
+    const uint64_t r = feature_rank(node_key, f);
+    if ((first || r > last) && r < best) best = r;
+  }
+  return wave::min_u64(best, lane);
+}
+
 template <typename CT>
 __device__ __forceinline__ void scan256(CT* p, int lane) {
   CT v0 = p[4 * lane], v1 = p[4 * lane + 1], v2 = p[4 * lane + 2], v3 = p[4 * lane + 3];
   v1 += v0; v2 += v1; v3 += v2;
-  CT t = v3;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    CT o = __shfl_up(t, off);
-    if (lane >= off) t += o;
-  }
-  CT ex = __shfl_up(t, 1);
-  if (lane == 0) ex = (CT)0;
+  CT t;
+  if constexpr (sizeof(CT) == 8) t = (CT)wave::incl_scan_u64((uint64_t)v3);
+  else t = wave::incl_scan<CT>(v3);
+  const CT ex = wave::excl_from_incl<CT>(t);
   p[4 * lane] = v0 + ex; p[4 * lane + 1] = v1 + ex; p[4 * lane + 2] = v2 + ex; p[4 * lane + 3] = v3 + ex;
 }
 
-template <bool REG>
-__device__ void eval_feature(typename std::conditional<REG, float, uint32_t>::type* h, int C, int CH,
-                             const TreeSpec& s, int lane, double* out_gain, int* out_bin, int* out_nc) {
-  using CT = typename std::conditional<REG, float, uint32_t>::type;
-  for (int ch = 0; ch < CH; ++ch) scan256<CT>(h + ch * 256, lane);
+// channel `ch` (CH layout: classes.., rows / s0,s1,s2,rows) of cumulative bin b
+template <int MODE>
+__device__ __forceinline__ double hist_chan(const typename HT<MODE>::T* h, int ch, int CH, int b) {
+  if constexpr (MODE == 1) {
+    const unsigned long long v = h[b];
+    return (double)(ch == 2 ? (v >> 42) : ((v >> (21 * ch)) & kPackMask21));
+  } else {
+    return (double)h[ch * 256 + b];
+  }
+}
+
+// ONE wave evaluates one feature's histogram: in-place scans, best bin, non-constant
+// flag, the best bin's cumulative channels (out_left[CH]); optionally zeroes the
+// histogram afterwards so the next feature group needs no clearing pass.
+template <int MODE>
+__device__ void eval_feature(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
+                             double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after) {
+  using CT = typename HT<MODE>::T;
+  const int planes = hist_planes(MODE, CH);
+  for (int ch = 0; ch < planes; ++ch) scan256<CT>(h + ch * 256, lane);
   wave_lds_sync();
-  const CT tot_rows = h[(CH - 1) * 256 + 255];
-  const CT msl = (CT)s.min_samples_leaf;
+  const double tot_rows = hist_chan<MODE>(h, CH - 1, CH, 255);
+  const double msl = (double)s.min_samples_leaf;
   double best = -INFINITY;
   int bb = -1;
   bool nc = false;
@@ -195,65 +231,62 @@ __device__ void eval_feature(typename std::conditional<REG, float, uint32_t>::ty
   for (int i = 0; i < 4; ++i) {
     const int b = lane * 4 + i;
     if (b == 255) break;
-    const CT rl = h[(CH - 1) * 256 + b];
-    const CT rr = tot_rows - rl;
-    nc |= (rl > (CT)0 && rr > (CT)0);
+    const double rl = hist_chan<MODE>(h, CH - 1, CH, b);
+    const double rr = tot_rows - rl;
+    nc |= (rl > 0.0 && rr > 0.0);
     if (rl < msl || rr < msl) continue;
     double g;
-    if constexpr (!REG) {
+    if constexpr (MODE == 2) {
+      const double l0 = (double)h[b], t0 = (double)h[255];
+      const double l1 = (double)h[256 + b], t1 = (double)h[256 + 255];
+      g = mse_proxy(l0, l1, t0 - l0, t1 - l1);
+    } else {
       ClsAcc L, R;
       L.init(); R.init();
       for (int k = 0; k < C; ++k) {
-        const double lc = (double)h[k * 256 + b];
-        const double tc = (double)h[k * 256 + 255];
+        const double lc = hist_chan<MODE>(h, k, CH, b);
+        const double tc = hist_chan<MODE>(h, k, CH, 255);
         L.add(lc);
         R.add(tc - lc);
       }
       g = cls_proxy(L, R, s.criterion);
-    } else {
-      const double l0 = (double)h[b], t0 = (double)h[255];
-      const double l1 = (double)h[256 + b], t1 = (double)h[256 + 255];
-      g = mse_proxy(l0, l1, t0 - l0, t1 - l1);
     }
     if (g > best) { best = g; bb = b; }
   }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double og = __shfl_xor(best, off);
-    const int ob = __shfl_xor(bb, off);
-    if (og > best || (og == best && ob >= 0 && (bb < 0 || ob < bb))) { best = og; bb = ob; }
-  }
+  wave::argmax(best, bb, lane);
   const bool any_nc = __ballot(nc) != 0ull;
+  if (lane < CH) out_left[lane] = bb >= 0 ? hist_chan<MODE>(h, lane, CH, bb) : 0.0;
   if (lane == 0) { *out_gain = best; *out_bin = bb; *out_nc = any_nc ? 1 : 0; }
+  if (zero_after) {
+    wave_lds_sync();
+    for (int ch = 0; ch < planes; ++ch) {
+      CT* p = h + ch * 256 + 4 * lane;
+      p[0] = (CT)0; p[1] = (CT)0; p[2] = (CT)0; p[3] = (CT)0;
+    }
+  }
 }
 
-// scratch block at the end of a fused kernel's LDS
-struct Scratch {
-  double best_gain;
-  int32_t best_feat, best_bin, nonconst, pos, g, base, nl, done;
-  int32_t wcnt[8];  // per-wave partition counts (L: 0..3, R: 4..7)
-  int32_t tile_base[2];
-};
-
-template <typename CT>
-__device__ __forceinline__ void hist_add_row(CT* hist, const Ctx& c, const int16_t* feats, int g, uint32_t row,
-                                             uint32_t w) {
+template <int MODE>
+__device__ __forceinline__ void hist_add_row(typename HT<MODE>::T* hist, const Ctx& c, const int16_t* feats, int g,
+                                             uint32_t row, uint32_t w, int span) {
   const uint8_t* xr = c.Xb + (int64_t)row * c.ld;
-  const int span = c.CH * 256;
-  if constexpr (std::is_same<CT, uint32_t>::value) {
+  if constexpr (MODE == 0) {
     const int y = c.ycls[row];
     for (int j = 0; j < g; ++j) {
       const int b = xr[feats[j]];
-      CT* hj = hist + j * span;
+      uint32_t* hj = hist + j * span;
       atomicAdd(&hj[y * 256 + b], w);
       atomicAdd(&hj[c.C * 256 + b], 1u);
     }
+  } else if constexpr (MODE == 1) {
+    const unsigned long long pv = pack_bin(c.ycls[row], w);
+    for (int j = 0; j < g; ++j) atomicAdd(&hist[j * span + xr[feats[j]]], pv);
   } else {
     const float yv = c.yreg[row];
     const float fw = (float)w, wy = fw * yv, wyy = wy * yv;
     for (int j = 0; j < g; ++j) {
       const int b = xr[feats[j]];
-      CT* hj = hist + j * span;
+      float* hj = hist + j * span;
       atomicAdd(&hj[b], fw);
       atomicAdd(&hj[256 + b], wy);
       atomicAdd(&hj[512 + b], wyy);
@@ -262,12 +295,10 @@ __device__ __forceinline__ void hist_add_row(CT* hist, const Ctx& c, const int16
   }
 }
 
-// serial selection over an evaluated group (thread 0). returns true when search is done.
-template <typename CT>
+// serial selection over an evaluated group, in visiting order (thread 0)
 __device__ void select_group(const Ctx& c, const TreeSpec& s, const int16_t* feats, int g, const double* rg,
-                             const int* rb, const int* rn, const CT* hist, double* best_left, int& nonconst,
+                             const int* rb, const int* rn, const double* rleft, double* best_left, int& nonconst,
                              double& best_gain, int& best_feat, int& best_bin) {
-  const int span = c.CH * 256;
   for (int j = 0; j < g; ++j) {
     if (!rn[j]) continue;
     ++nonconst;
@@ -275,7 +306,7 @@ __device__ void select_group(const Ctx& c, const TreeSpec& s, const int16_t* fea
       best_gain = rg[j];
       best_feat = feats[j];
       best_bin = rb[j];
-      for (int ch = 0; ch < c.CH; ++ch) best_left[ch] = (double)hist[j * span + ch * 256 + rb[j]];
+      for (int ch = 0; ch < c.CH; ++ch) best_left[ch] = rleft[j * c.CH + ch];
     }
     if (nonconst >= s.max_features) break;
   }
@@ -302,12 +333,40 @@ __device__ bool accept_split(const Ctx& c, const TreeSpec& s, int node, int tree
   return !(imp + kEps < (double)s.min_impurity_decrease);
 }
 
+// scratch block of the fused kernel
+struct Scratch {
+  uint64_t last;
+  double best_gain;
+  int32_t best_feat, best_bin, nonconst, pos, first, base, nl, pad;
+  int32_t wcnt[8];
+};
+
+struct FusedLayout {
+  size_t hist, feats, rg, rb, rn, rleft, best_left, sc, total;
+};
+
+__host__ __device__ inline FusedLayout fused_layout(int KG, int span, int elem, int CH) {
+  FusedLayout L;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off = (off + bytes + 15) / 16 * 16; return o; };
+  L.hist = take((size_t)KG * span * elem);
+  L.feats = take((size_t)KG * 2);
+  L.rg = take((size_t)KG * 8);
+  L.rb = take((size_t)KG * 4);
+  L.rn = take((size_t)KG * 4);
+  L.rleft = take((size_t)KG * CH * 8);
+  L.best_left = take((size_t)CH * 8);
+  L.sc = take(sizeof(Scratch));
+  L.total = off;
+  return L;
+}
+
 // ------------------------------------------------------------------------------------
 // fused per-node kernel (wave tier NT=64, block tier NT=256)
 // ------------------------------------------------------------------------------------
-template <int NT, bool REG>
+template <int NT, int MODE>
 __global__ __launch_bounds__(NT) void k_nodes(Ctx c, int tier, int set_cur) {
-  using CT = typename std::conditional<REG, float, uint32_t>::type;
+  using CT = typename HT<MODE>::T;
   constexpr int NW = NT / 64;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const OpenNode on = c.open[set_cur][tier][blockIdx.x];
@@ -316,21 +375,21 @@ __global__ __launch_bounds__(NT) void k_nodes(Ctx c, int tier, int set_cur) {
   const int d = c.d;
   const int KG = NT == 64 ? c.kg_wave : c.kg_block;
   const int slack = NT == 64 ? c.slack_wave : 0;
-  const int perm_bytes = ((d * 2 + 15) / 16) * 16;
-  int16_t* perm = (int16_t*)smem;
-  CT* hist = (CT*)(smem + perm_bytes);
-  const int span = c.CH * 256;
-  unsigned char* tail = smem + perm_bytes + (size_t)KG * span * sizeof(CT);
-  double* rg = (double*)tail;
-  int* rb = (int*)(rg + KG);
-  int* rn = rb + KG;
-  double* best_left = (double*)(((uintptr_t)(rn + KG) + 15) & ~(uintptr_t)15);
-  Scratch* sc = (Scratch*)(best_left + ((c.CH + 1) & ~1));
+  const int span = hist_planes(MODE, c.CH) * 256;
+  const FusedLayout FL = fused_layout(KG, span, (int)sizeof(CT), c.CH);
+  CT* hist = (CT*)(smem + FL.hist);
+  int16_t* feats = (int16_t*)(smem + FL.feats);
+  double* rg = (double*)(smem + FL.rg);
+  int* rb = (int*)(smem + FL.rb);
+  int* rn = (int*)(smem + FL.rn);
+  double* rleft = (double*)(smem + FL.rleft);
+  double* best_left = (double*)(smem + FL.best_left);
+  Scratch* sc = (Scratch*)(smem + FL.sc);
 
-  for (int i = tid; i < d; i += NT) perm[i] = (int16_t)i;
+  for (int i = tid; i < KG * span; i += NT) hist[i] = (CT)0;
   if (tid == 0) {
     sc->best_gain = -INFINITY; sc->best_feat = -1; sc->best_bin = -1;
-    sc->nonconst = 0; sc->pos = 0; sc->done = 0;
+    sc->nonconst = 0; sc->pos = 0; sc->first = 1; sc->last = 0;
   }
   __syncthreads();
   const uint32_t* rows = c.rows_cur + c.row_off[on.tree];
@@ -339,26 +398,29 @@ __global__ __launch_bounds__(NT) void k_nodes(Ctx c, int tier, int set_cur) {
     const int pos = sc->pos, nonconst = sc->nonconst;
     if (nonconst >= k || pos >= d) break;
     const int g = min(KG, min(k - nonconst + slack, d - pos));
-    if (tid == 0) {
-      for (int j = pos; j < pos + g; ++j) {
-        const int t = perm_pick(on.key, j, d);
-        const int16_t tmp = perm[j]; perm[j] = perm[t]; perm[t] = tmp;
+    if (wid == 0) {
+      uint64_t last = sc->last;
+      bool first = sc->first != 0;
+      for (int j = 0; j < g; ++j) {
+        last = wave_next_feature(on.key, d, lane, last, first);
+        first = false;
+        if (lane == 0) feats[j] = (int16_t)(uint32_t)last;
       }
+      if (lane == 0) { sc->last = last; sc->first = 0; }
     }
-    for (int i = tid; i < g * span; i += NT) hist[i] = (CT)0;
     __syncthreads();
-    const int16_t* feats = perm + pos;
     for (int r = tid; r < on.count; r += NT) {
       const uint32_t row = rows[on.start + r];
-      hist_add_row<CT>(hist, c, feats, g, row, boot_weight(s, row));
+      hist_add_row<MODE>(hist, c, feats, g, row, boot_weight(s, row), span);
     }
     __syncthreads();
-    for (int j = wid; j < g; j += NW) eval_feature<REG>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j);
+    for (int j = wid; j < g; j += NW)
+      eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, true);
     __syncthreads();
     if (tid == 0) {
       int nc = sc->nonconst, bf = sc->best_feat, bbin = sc->best_bin;
       double bg = sc->best_gain;
-      select_group<CT>(c, s, feats, g, rg, rb, rn, hist, best_left, nc, bg, bf, bbin);
+      select_group(c, s, feats, g, rg, rb, rn, rleft, best_left, nc, bg, bf, bbin);
       sc->nonconst = nc; sc->best_gain = bg; sc->best_feat = bf; sc->best_bin = bbin;
       sc->pos = pos + g;
     }
@@ -426,45 +488,19 @@ struct SubEntry {
   int32_t node, depth;
 };
 
-__device__ __forceinline__ uint32_t bitonic64(uint32_t key, int lane) {
-#pragma unroll
-  for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const uint32_t other = __shfl_xor(key, j);
-      const bool up = (lane & k) == 0;
-      const bool lower = (lane & j) == 0;
-      const uint32_t mn = min(key, other), mx = max(key, other);
-      key = (lower == up) ? mn : mx;
-    }
-  }
-  return key;
-}
-
-template <typename T>
-__device__ __forceinline__ T wave_incl_scan(T v, int lane) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const T o = __shfl_up(v, off);
-    if (lane >= off) v += o;
-  }
-  return v;
-}
-
 // evaluate one feature for the rows in `mask`; lane data: bin b (valid if in mask).
-// returns gain/bin via references (uniform across the wave) and whether non-constant.
 template <bool REG>
 __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt, int lane, int my_bin, int my_cls,
                          float my_w, float my_y, double& gain, int& bin, bool& nonconst) {
   const bool act = (mask >> lane) & 1ull;
   const uint32_t key = act ? ((uint32_t)my_bin << 6) | (uint32_t)lane : 0xFFFFFFFFu;
-  const uint32_t sk = bitonic64(key, lane);
+  const uint32_t sk = wave::bitonic64(key, lane);
   const bool valid_row = lane < cnt;
   const int src = (int)(sk & 63u);
   const int b = valid_row ? (int)(sk >> 6) : 1024;
-  const int bnext = __shfl_down(b, 1);
-  const int blast = __shfl(b, cnt - 1);
-  const int bfirst = __shfl(b, 0);
+  const int bnext = wave::shift_down1<int>(b, lane, 1024);
+  const int blast = wave::bcast<int>(b, cnt - 1);
+  const int bfirst = wave::bcast<int>(b, 0);
   nonconst = bfirst != blast;
   const int lrows = lane + 1, rrows = cnt - lrows;
   const bool cand = valid_row && lane < cnt - 1 && b != bnext && lrows >= s.min_samples_leaf &&
@@ -480,8 +516,8 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
     L.init(); R.init();
     for (int k = 0; k < c.C; ++k) {
       const uint32_t v = (ycls == k) ? w : 0u;
-      const uint32_t pre = wave_incl_scan<uint32_t>(v, lane);
-      const uint32_t tot = __shfl(pre, cnt - 1);
+      const uint32_t pre = wave::incl_scan<uint32_t>(v);
+      const uint32_t tot = wave::bcast<uint32_t>(pre, cnt - 1);
       L.add((double)pre);
       R.add((double)(tot - pre));
     }
@@ -490,20 +526,15 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
     const float wsh = __shfl(my_w, src);
     const float y = __shfl(my_y, src);
     const float w = valid_row ? wsh : 0.f;
-    const float p0 = wave_incl_scan<float>(w, lane);
-    const float p1 = wave_incl_scan<float>(w * y, lane);
-    const float t0 = __shfl(p0, cnt - 1), t1 = __shfl(p1, cnt - 1);
+    const float p0 = wave::incl_scan<float>(w);
+    const float p1 = wave::incl_scan<float>(w * y);
+    const float t0 = wave::bcast<float>(p0, cnt - 1), t1 = wave::bcast<float>(p1, cnt - 1);
     if (cand) g = mse_proxy((double)p0, (double)p1, (double)(t0 - p0), (double)(t1 - p1));
   }
   int bl = cand ? lane : 64;
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double og = __shfl_xor(g, off);
-    const int ol = __shfl_xor(bl, off);
-    if (og > g || (og == g && ol < bl)) { g = og; bl = ol; }
-  }
+  wave::argmax(g, bl, lane);
   gain = g;
-  const int bsel = __shfl(b, bl & 63);
+  const int bsel = wave::bcast<int>(b, bl & 63);
   bin = bl < 64 ? bsel : -1;
 }
 
@@ -516,9 +547,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   const int d = c.d;
   const bool cache = c.sub_cache_d > 0;
   const int dp = c.sub_cache_d;
-  const int perm_bytes = ((d * 2 + 15) / 16) * 16;
-  int16_t* perm = (int16_t*)smem;
-  SubEntry* stack = (SubEntry*)(smem + perm_bytes);
+  SubEntry* stack = (SubEntry*)smem;
   double* left_ch = (double*)(stack + 64);
   uint8_t* xc = (uint8_t*)(left_ch + ((c.VC + 1) & ~1));
   const int cnt0 = on.count;
@@ -547,18 +576,12 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     --sp;
     const SubEntry e = stack[sp];
     const int cnt = __popcll(e.mask);
-    // compact the node's lanes to 0..cnt-1 order is not needed: sub_eval sorts by (bin, lane)
-    for (int f = lane; f < d; f += 64) perm[f] = (int16_t)f;
-    wave_lds_sync();
     int nonconst = 0, best_f = -1, best_b = -1;
     double best_g = -INFINITY;
+    uint64_t last = 0;
     for (int pos = 0; nonconst < s.max_features && pos < d; ++pos) {
-      if (lane == 0) {
-        const int t = perm_pick(e.key, pos, d);
-        const int16_t tmp = perm[pos]; perm[pos] = perm[t]; perm[t] = tmp;
-      }
-      wave_lds_sync();
-      const int f = perm[pos];
+      last = wave_next_feature(e.key, d, lane, last, pos == 0);
+      const int f = (int)(uint32_t)last;
       const int my_bin = cache ? xc[lane * dp + f] : (lane < cnt0 ? xg[f] : 0);
       double g;
       int bb;
@@ -583,8 +606,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
       } else {
         v = (inl && my_cls == k) ? (double)my_w : 0.0;
       }
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+      v = wave::sum<double>(v, lane);
       if (lane == 0) left_ch[k] = v;
     }
     wave_lds_sync();
@@ -592,7 +614,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     if (lane == 0) {
       if (accept_split(c, s, e.node, on.tree, left_ch)) base = make_children(c, e.node, best_f, best_b, left_ch);
     }
-    base = __shfl(base, 0);
+    base = wave::bcast<int>(base, 0);
     if (base < 0) continue;
     const int nl = __popcll(lm), nr = cnt - nl;
     // push right then left (left subtree first); leaf-by-count/purity children are not pushed
@@ -607,7 +629,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
         stack[sp++] = l;
       }
     }
-    sp = __shfl(sp, 0);
+    sp = wave::bcast<int>(sp, 0);
     wave_lds_sync();
   }
 }
@@ -615,29 +637,32 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
 // ------------------------------------------------------------------------------------
 // large tier
 // ------------------------------------------------------------------------------------
-__global__ void k_large_prep(Ctx c, int set_cur, int nL) {
-  const int slot = blockIdx.x * blockDim.x + threadIdx.x;
-  if (slot >= nL) return;
+// one wave per large node: state + the first feature group of its visiting order
+__global__ __launch_bounds__(64) void k_large_prep(Ctx c, int set_cur, int nL) {
+  const int slot = blockIdx.x;
+  const int lane = threadIdx.x;
   LState st;
   st.on = c.open[set_cur][3][slot];
   const TreeSpec& s = c.specs[st.on.tree];
-  int16_t* perm = c.lperm + (int64_t)slot * c.d;
-  for (int i = 0; i < c.d; ++i) perm[i] = (int16_t)i;
+  int16_t* feats = c.lperm + (int64_t)slot * c.d;
+  st.g = min(c.kg_large, min(s.max_features, c.d));
+  uint64_t last = 0;
+  for (int j = 0; j < st.g; ++j) {
+    last = wave_next_feature(st.on.key, c.d, lane, last, j == 0);
+    if (lane == 0) feats[j] = (int16_t)(uint32_t)last;
+  }
+  if (lane != 0) return;
   st.pos = 0; st.nonconst = 0; st.done = 0; st.best_feat = -1; st.best_bin = -1; st.split = 0; st.nl = 0;
   st.best_gain = -INFINITY;
-  st.g = min(c.kg_large, min(s.max_features, c.d));
-  for (int j = 0; j < st.g; ++j) {
-    const int t = perm_pick(st.on.key, j, c.d);
-    const int16_t tmp = perm[j]; perm[j] = perm[t]; perm[t] = tmp;
-  }
+  st.last = last;
   c.lstate[slot] = st;
   c.lcursor[2 * slot] = 0;
   c.lcursor[2 * slot + 1] = 0;
 }
 
-template <bool REG>
+template <int MODE>
 __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
-  using CT = typename std::conditional<REG, float, uint32_t>::type;
+  using CT = typename HT<MODE>::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int slot = blockIdx.y;
   const LState& st = c.lstate[slot];
@@ -647,7 +672,7 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
   const int r1 = min(r0 + c.chunk, st.on.count);
   const TreeSpec& s = c.specs[st.on.tree];
   const int g = st.g;
-  const int span = c.CH * 256;
+  const int span = hist_planes(MODE, c.CH) * 256;
   __shared__ int16_t feats[64];
   CT* hist = (CT*)smem;
   const int16_t* perm = c.lperm + (int64_t)slot * c.d + st.pos;
@@ -657,19 +682,36 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
   const uint32_t* rows = c.rows_cur + c.row_off[st.on.tree] + st.on.start;
   for (int r = r0 + threadIdx.x; r < r1; r += 256) {
     const uint32_t row = rows[r];
-    hist_add_row<CT>(hist, c, feats, g, row, boot_weight(s, row));
+    hist_add_row<MODE>(hist, c, feats, g, row, boot_weight(s, row), span);
   }
   __syncthreads();
-  CT* gh = (CT*)c.ghist + (int64_t)slot * c.kg_large * span;
-  for (int i = threadIdx.x; i < g * span; i += 256) {
-    const CT v = hist[i];
-    if (v != (CT)0) atomicAdd(&gh[i], v);
+  // flush into the node's global histogram: always unpacked planes [CH][256]
+  const int gspan = c.CH * 256;
+  if constexpr (MODE == 1) {
+    uint32_t* gh = (uint32_t*)c.ghist + (int64_t)slot * c.kg_large * gspan;
+    for (int i = threadIdx.x; i < g * 256; i += 256) {
+      const unsigned long long v = hist[i];
+      if (!v) continue;
+      const int j = i >> 8, b = i & 255;
+      uint32_t* gj = gh + j * gspan;
+      const uint32_t w0 = (uint32_t)(v & kPackMask21), w1 = (uint32_t)((v >> 21) & kPackMask21);
+      if (w0) atomicAdd(&gj[b], w0);
+      if (w1) atomicAdd(&gj[256 + b], w1);
+      atomicAdd(&gj[512 + b], (uint32_t)(v >> 42));
+    }
+  } else {
+    CT* gh = (CT*)c.ghist + (int64_t)slot * c.kg_large * gspan;
+    for (int i = threadIdx.x; i < g * span; i += 256) {
+      const CT v = hist[i];
+      if (v != (CT)0) atomicAdd(&gh[i], v);
+    }
   }
 }
 
-template <bool REG>
+// evaluates the node's global histogram; MODE here is the GLOBAL layout (0 or 2)
+template <int MODE>
 __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
-  using CT = typename std::conditional<REG, float, uint32_t>::type;
+  using CT = typename HT<MODE>::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int slot = blockIdx.x;
   LState& st = c.lstate[slot];
@@ -681,31 +723,44 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   double* rg = (double*)(smem + (size_t)c.kg_large * span * sizeof(CT));
   int* rb = (int*)(rg + c.kg_large);
   int* rn = rb + c.kg_large;
+  double* rleft = (double*)(rn + c.kg_large + (c.kg_large & 1));
+  __shared__ int need_more;
   const CT* gh = (const CT*)c.ghist + (int64_t)slot * c.kg_large * span;
   for (int i = tid; i < g * span; i += 256) hist[i] = gh[i];
   __syncthreads();
-  for (int j = wid; j < g; j += 4) eval_feature<REG>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j);
+  for (int j = wid; j < g; j += 4)
+    eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, false);
   __syncthreads();
-  if (tid != 0) return;
   const int16_t* feats = c.lperm + (int64_t)slot * c.d + st.pos;
   double* best_left = c.lbest_left + (int64_t)slot * c.CH;
-  int nc = st.nonconst, bf = st.best_feat, bbin = st.best_bin;
-  double bg = st.best_gain;
-  select_group<CT>(c, s, feats, g, rg, rb, rn, hist, best_left, nc, bg, bf, bbin);
-  st.nonconst = nc; st.best_gain = bg; st.best_feat = bf; st.best_bin = bbin;
-  st.pos += g;
-  if (st.nonconst < s.max_features && st.pos < c.d) {
-    // need more features: extend the permutation lazily and ask the host for a round
-    const int g2 = min(c.kg_large, min(s.max_features - st.nonconst, c.d - st.pos));
-    int16_t* perm = c.lperm + (int64_t)slot * c.d;
-    for (int j = st.pos; j < st.pos + g2; ++j) {
-      const int t = perm_pick(st.on.key, j, c.d);
-      const int16_t tmp = perm[j]; perm[j] = perm[t]; perm[t] = tmp;
+  if (tid == 0) {
+    int nc = st.nonconst, bf = st.best_feat, bbin = st.best_bin;
+    double bg = st.best_gain;
+    select_group(c, s, feats, g, rg, rb, rn, rleft, best_left, nc, bg, bf, bbin);
+    st.nonconst = nc; st.best_gain = bg; st.best_feat = bf; st.best_bin = bbin;
+    st.pos += g;
+    need_more = (st.nonconst < s.max_features && st.pos < c.d) ? 1 : 0;
+  }
+  __syncthreads();
+  if (need_more) {
+    // extend the visiting order by the next feature group and ask the host for a round
+    if (wid == 0) {
+      const int g2 = min(c.kg_large, min(s.max_features - st.nonconst, c.d - st.pos));
+      int16_t* perm = c.lperm + (int64_t)slot * c.d;
+      uint64_t last = st.last;
+      for (int j = 0; j < g2; ++j) {
+        last = wave_next_feature(st.on.key, c.d, lane, last, false);
+        if (lane == 0) perm[st.pos + j] = (int16_t)(uint32_t)last;
+      }
+      if (lane == 0) {
+        st.last = last;
+        st.g = g2;
+        atomicOr(&c.counters[kNeedMore], 1);
+      }
     }
-    st.g = g2;
-    atomicOr(&c.counters[kNeedMore], 1);
     return;
   }
+  if (tid != 0) return;
   st.done = 1;
   int base = -1;
   if (st.best_feat >= 0 && accept_split(c, s, st.on.node, st.on.tree, best_left))
@@ -885,18 +940,20 @@ static Layout plan(const ForestArgs* a) {
   return L;
 }
 
+static int build_mode(const ForestArgs* a) { return a->is_reg ? 2 : (a->n_classes == 2 ? 1 : 0); }
+
+static size_t mode_elem(int mode) { return mode == 1 ? 8 : 4; }
+
 static size_t fused_lds(const ForestArgs* a, int KG) {
   const int CH = a->is_reg ? 4 : (int)a->n_classes + 1;
-  size_t perm_bytes = ((a->d * 2 + 15) / 16) * 16;
-  size_t b = perm_bytes + (size_t)KG * CH * 256 * 4;
-  b += KG * 8 + 2 * KG * 4;
-  b = align_up(b, 16) + ((CH + 1) & ~1) * 8 + sizeof(Scratch) + 16;
-  return b;
+  const int mode = build_mode(a);
+  const int span = (mode == 1 ? 1 : CH) * 256;
+  return fused_layout(KG, span, (int)mode_elem(mode), CH).total + 16;
 }
 
 static size_t sub_lds(const ForestArgs* a) {
   const int VC = a->is_reg ? 3 : (int)a->n_classes;
-  size_t b = ((a->d * 2 + 15) / 16) * 16 + 64 * sizeof(SubEntry) + ((VC + 1) & ~1) * 8;
+  size_t b = 64 * sizeof(SubEntry) + ((VC + 1) & ~1) * 8;
   b += (size_t)64 * a->sub_cache_d + 16;
   return b;
 }
@@ -945,6 +1002,28 @@ static hipError_t g_last_err = hipSuccess;
     }                                                   \
   } while (0)
 
+// side streams so the four node tiers of a level overlap (their tails otherwise
+// serialise: a level's few large nodes leave most CUs idle while small nodes wait)
+struct SideStreams {
+  hipStream_t s[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
+  bool ok = false;
+};
+
+static SideStreams* side_streams() {
+  static SideStreams ss;
+  if (!ss.ok) {
+    bool good = hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; i < 3 && good; ++i) {
+      good = hipStreamCreateWithFlags(&ss.s[i], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming) == hipSuccess;
+    }
+    ss.ok = good;
+    if (!good) return nullptr;
+  }
+  return &ss;
+}
+
 static int32_t* pinned_counters() {
   static int32_t* p = nullptr;
   if (!p) {
@@ -957,18 +1036,33 @@ static int32_t* pinned_counters() {
 
 using namespace dml;
 
-// kernel-level test hooks (tests/test_forest_gpu.py): in-wave sort and prefix scan
-__global__ void k_test_wave_prims(const uint32_t* in, uint32_t* sorted, uint32_t* scanned) {
+// kernel-level test hooks (tests/test_forest_gpu.py): wave primitives vs ds_bpermute
+// out layout per block of 64: [sorted | scan | xor1 | xor2 | xor4 | xor8 | xor16 | xor32 |
+//                             argmax idx | shift_down1 | min]
+__global__ void k_test_wave_prims(const uint32_t* in, uint32_t* out) {
   const int lane = threadIdx.x;
   const uint32_t v = in[blockIdx.x * 64 + lane];
-  sorted[blockIdx.x * 64 + lane] = bitonic64(v, lane);
-  scanned[blockIdx.x * 64 + lane] = wave_incl_scan<uint32_t>(v, lane);
+  uint32_t* o = out + (size_t)blockIdx.x * 64 * 11;
+  o[0 * 64 + lane] = wave::bitonic64(v, lane);
+  o[1 * 64 + lane] = wave::incl_scan<uint32_t>(v);
+  o[2 * 64 + lane] = wave::xor32<1>(v, lane);
+  o[3 * 64 + lane] = wave::xor32<2>(v, lane);
+  o[4 * 64 + lane] = wave::xor32<4>(v, lane);
+  o[5 * 64 + lane] = wave::xor32<8>(v, lane);
+  o[6 * 64 + lane] = wave::xor32<16>(v, lane);
+  o[7 * 64 + lane] = wave::xor32<32>(v, lane);
+  double g = (double)(v % 97u);
+  int idx = lane;
+  wave::argmax(g, idx, lane);
+  o[8 * 64 + lane] = (uint32_t)idx;
+  o[9 * 64 + lane] = (uint32_t)wave::shift_down1<int>((int)v, lane, -1);
+  o[10 * 64 + lane] = (uint32_t)wave::min_u64(((uint64_t)v << 32) | (uint32_t)lane, lane);
 }
 
 extern "C" {
 
-int dml_test_wave_prims(const uint32_t* in, uint32_t* sorted, uint32_t* scanned, int64_t nblocks, hipStream_t st) {
-  k_test_wave_prims<<<(unsigned)nblocks, 64, 0, st>>>(in, sorted, scanned);
+int dml_test_wave_prims(const uint32_t* in, uint32_t* out, int64_t nblocks, hipStream_t st) {
+  k_test_wave_prims<<<(unsigned)nblocks, 64, 0, st>>>(in, out);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -1000,8 +1094,13 @@ int dml_forest_count(ForestArgs* a, hipStream_t st) {
   return 0;
 }
 
-// phase 2: build every tree; status_out: 0 ok, 1 node-pool overflow, 4 open-list overflow
-int dml_forest_build(ForestArgs* a, hipStream_t st) {
+}  // extern "C"
+
+// level loop for one histogram mode (0 cls, 1 packed binary, 2 regression)
+template <int MODE>
+static int build_impl(ForestArgs* a, hipStream_t st) {
+  constexpr bool REG = MODE == 2;
+  constexpr int GM = MODE == 2 ? 2 : 0;  // global (large-tier) histogram layout
   Layout L = plan(a);
   if ((size_t)a->workspace_bytes < (size_t)dml_forest_workspace_bytes(a)) return 2;
   Ctx c = make_ctx(a, L);
@@ -1009,7 +1108,7 @@ int dml_forest_build(ForestArgs* a, hipStream_t st) {
   c.rows_cur = rows_a;
   int32_t* h = pinned_counters();
   if (!h) return 3;
-  const bool reg = a->is_reg != 0;
+  const bool reg = REG;
   if (!reg && (a->n_classes < 1 || a->n_classes > kMaxClasses)) return 5;
   if (a->d > 32767) return 6;
 
@@ -1027,30 +1126,26 @@ int dml_forest_build(ForestArgs* a, hipStream_t st) {
   const size_t lds_w = fused_lds(a, (int)a->kg_wave);
   const size_t lds_b = fused_lds(a, (int)a->kg_block);
   const int CH = c.CH;
-  const size_t lds_hl = (size_t)a->kg_large * CH * 256 * 4;
-  const size_t lds_sl = lds_hl + a->kg_large * 16 + 64;
+  const size_t lds_hl = (size_t)a->kg_large * (MODE == 1 ? 1 : CH) * 256 * mode_elem(MODE);
+  const size_t lds_sl = (size_t)a->kg_large * CH * 256 * 4 + a->kg_large * 16 + 16 + (size_t)a->kg_large * CH * 8 + 64;
   const size_t lds_max = 160 * 1024;
   if (lds_w > lds_max || lds_b > lds_max || lds_sl > lds_max || lds_s > lds_max) return 7;
   if (a->sub_max > 64) return 9;
   {
     const int need = (int)std::max(std::max(lds_s, lds_w), std::max(lds_b, lds_sl));
-    static int attr_set = 0;
-    if (need > 64 * 1024 && need > attr_set) {
-      HIP_OK(hipFuncSetAttribute((const void*)k_subtree<false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_subtree<true>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<256, true>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_hist_large<false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_hist_large<true>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_split_large<false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_split_large<true>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      attr_set = need;
+    static int attr_set[3] = {0, 0, 0};
+    if (need > 64 * 1024 && need > attr_set[MODE]) {
+      HIP_OK(hipFuncSetAttribute((const void*)k_subtree<REG>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<64, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<256, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_hist_large<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_split_large<GM>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      attr_set[MODE] = need;
     }
   }
   const unsigned nchunks = (unsigned)((a->max_active + a->chunk - 1) / a->chunk);
   int cur = 0, levels = 0, large_rounds = 0;
+  for (int i = 0; i < 4; ++i) a->tier_nodes_out[i] = 0;
   while (true) {
     HIP_OK(hipMemcpyAsync(h, c.counters, kNumCounters * 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
@@ -1059,37 +1154,38 @@ int dml_forest_build(ForestArgs* a, hipStream_t st) {
     if (ns + nw + nb + nL == 0) break;
     if (++levels > 1 << 20) return 8;
     HIP_OK(hipMemsetAsync(c.counters + (1 - cur) * kTiers, 0, kTiers * 4, st));
-    if (ns) {
-      if (reg) k_subtree<true><<<ns, 64, lds_s, st>>>(c, cur);
-      else k_subtree<false><<<ns, 64, lds_s, st>>>(c, cur);
+    a->tier_nodes_out[0] += ns; a->tier_nodes_out[1] += nw; a->tier_nodes_out[2] += nb; a->tier_nodes_out[3] += nL;
+    SideStreams* ss = side_streams();
+    const bool fork = ss != nullptr && ((ns > 0) + (nw > 0) + (nb > 0) + (nL > 0)) > 1;
+    hipStream_t s0 = st, s1 = st, s2 = st;
+    if (fork) {
+      HIP_OK(hipEventRecord(ss->fork, st));
+      for (int i = 0; i < 3; ++i) HIP_OK(hipStreamWaitEvent(ss->s[i], ss->fork, 0));
+      s0 = ss->s[0]; s1 = ss->s[1]; s2 = ss->s[2];
     }
-    if (nw) {
-      if (reg) k_nodes<64, true><<<nw, 64, lds_w, st>>>(c, 1, cur);
-      else k_nodes<64, false><<<nw, 64, lds_w, st>>>(c, 1, cur);
-    }
-    if (nb) {
-      if (reg) k_nodes<256, true><<<nb, 256, lds_b, st>>>(c, 2, cur);
-      else k_nodes<256, false><<<nb, 256, lds_b, st>>>(c, 2, cur);
-    }
+    if (ns) k_subtree<REG><<<ns, 64, lds_s, s0>>>(c, cur);
+    if (nw) k_nodes<64, MODE><<<nw, 64, lds_w, s1>>>(c, 1, cur);
+    if (nb) k_nodes<256, MODE><<<nb, 256, lds_b, s2>>>(c, 2, cur);
     if (nL) {
-      k_large_prep<<<(nL + 63) / 64, 64, 0, st>>>(c, cur, nL);
+      k_large_prep<<<nL, 64, 0, st>>>(c, cur, nL);
       while (true) {
         ++large_rounds;
         HIP_OK(hipMemsetAsync(c.ghist, 0, (size_t)nL * a->kg_large * CH * 256 * 4, st));
         HIP_OK(hipMemsetAsync(c.counters + kNeedMore, 0, 4, st));
         dim3 gh(nchunks, (unsigned)nL);
-        if (reg) {
-          k_hist_large<true><<<gh, 256, lds_hl, st>>>(c);
-          k_split_large<true><<<nL, 256, lds_sl, st>>>(c, cur);
-        } else {
-          k_hist_large<false><<<gh, 256, lds_hl, st>>>(c);
-          k_split_large<false><<<nL, 256, lds_sl, st>>>(c, cur);
-        }
+        k_hist_large<MODE><<<gh, 256, lds_hl, st>>>(c);
+        k_split_large<GM><<<nL, 256, lds_sl, st>>>(c, cur);
         HIP_OK(hipMemcpyAsync(h + 32, c.counters + kNeedMore, 4, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
         if (!h[32]) break;
       }
       k_partition_large<<<dim3(nchunks, (unsigned)nL), 256, 0, st>>>(c);
+    }
+    if (fork) {
+      for (int i = 0; i < 3; ++i) {
+        HIP_OK(hipEventRecord(ss->join[i], ss->s[i]));
+        HIP_OK(hipStreamWaitEvent(st, ss->join[i], 0));
+      }
     }
     HIP_OK(hipGetLastError());
     uint32_t* t = c.rows_cur; c.rows_cur = c.rows_next; c.rows_next = t;
@@ -1102,6 +1198,17 @@ int dml_forest_build(ForestArgs* a, hipStream_t st) {
   a->large_rounds_out = large_rounds;
   if (a->status_out != 4) a->status_out = h[kOverflow] ? 1 : (h[kOpenOvf] ? 4 : 0);
   return 0;
+}
+
+extern "C" {
+
+// phase 2: build every tree; status_out: 0 ok, 1 node-pool overflow, 4 open-list overflow
+int dml_forest_build(ForestArgs* a, hipStream_t st) {
+  switch (build_mode(a)) {
+    case 1: return build_impl<1>(a, st);
+    case 2: return build_impl<2>(a, st);
+    default: return build_impl<0>(a, st);
+  }
 }
 
 }  // extern "C"

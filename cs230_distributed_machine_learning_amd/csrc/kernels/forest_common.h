@@ -91,11 +91,23 @@ DML_HD uint64_t child_key(uint64_t parent, int side) {
   return splitmix64(parent * 0x9E3779B97F4A7C15ull + 0x51ED27ull + (uint64_t)side);
 }
 
-// swap target for position `pos` of the node's lazy Fisher-Yates feature permutation
-DML_HD int perm_pick(uint64_t node_key, int pos, int n_features) {
-  const uint32_t h = hash_u32(node_key, 0xFEA7ull + (uint64_t)pos);
-  const uint32_t span = (uint32_t)(n_features - pos);
-  return pos + (int)(((uint64_t)h * span) >> 32);
+// Per-node feature visiting order: features sorted by (hash(node_key, f), f).  iid
+// 32-bit keys give a uniformly random permutation (sklearn draws a random order too),
+// and the GPU can pull "the next feature" with one wave-wide min-reduction instead of
+// a serial Fisher-Yates walk over an LDS array.
+DML_HD uint32_t feature_key(uint64_t node_key, int f) { return hash_u32(node_key, 0xFEA7ull + (uint64_t)f); }
+
+DML_HD uint64_t feature_rank(uint64_t node_key, int f) {
+  return ((uint64_t)feature_key(node_key, f) << 32) | (uint32_t)f;
+}
+
+// binary classification: (w class0, w class1, rows) packed in one u64 so a histogram
+// update is ONE 64-bit LDS atomic.  Fields are 21/21/22 bits; a node or chunk must stay
+// under kPackMaxRows rows (weights <= kPoisTable).
+constexpr uint64_t kPackMask21 = (1ull << 21) - 1ull;
+constexpr int kPackMaxRows = 131072;
+DML_HD uint64_t pack_bin(int cls, uint32_t w) {
+  return (cls == 0 ? (uint64_t)w : ((uint64_t)w << 21)) | (1ull << 42);
 }
 
 // ---- impurity from channel sums ----------------------------------------------------
@@ -132,7 +144,7 @@ DML_HD double cls_impurity(const ClsAcc& a, int crit) {
 // proxy improvement (larger is better) ~ -(wl*imp_l + wr*imp_r) up to a constant
 DML_HD double cls_proxy(const ClsAcc& l, const ClsAcc& r, int crit) {
   if (crit == kEntropy) return (l.clogc - l.w * dlog2(l.w)) + (r.clogc - r.w * dlog2(r.w));
-  return l.sq / l.w + r.sq / r.w;
+  return (l.sq * r.w + r.sq * l.w) / (l.w * r.w);  // = l.sq/l.w + r.sq/r.w with one division
 }
 
 // regression: s0 = sum w, s1 = sum w*y, s2 = sum w*y^2

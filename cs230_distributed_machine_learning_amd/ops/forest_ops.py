@@ -153,7 +153,8 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     P = int(a.n_nodes_out)
     del workspace
     stats = {"levels": int(a.levels_out), "large_rounds": int(a.large_rounds_out), "nodes": P,
-             "rows_total": int(a.rows_total), "build_s": time.perf_counter() - t0}
+             "rows_total": int(a.rows_total), "build_s": time.perf_counter() - t0,
+             "tier_nodes": [int(a.tier0_nodes), int(a.tier1_nodes), int(a.tier2_nodes), int(a.tier3_nodes)]}
     return ForestBuild(nodes[:P], vals[:P], T, VC, is_reg, n_classes, stats)
 
 

@@ -65,6 +65,7 @@ ForestArgs = _i64_struct(
         "kg_wave", "kg_block", "kg_large", "slack_wave",
         "sub_max", "sub_cache_d",
         "n_nodes_out", "status_out", "levels_out", "large_rounds_out",
+        "tier0_nodes", "tier1_nodes", "tier2_nodes", "tier3_nodes",
     ],
 )
 

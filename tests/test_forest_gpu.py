@@ -134,19 +134,32 @@ def test_gpu_regression_close_to_cpu():
 
 
 def test_wave_primitives_sort_and_scan():
+    """DPP / permlane / readlane wave primitives (wave_ops.h) against numpy."""
     import ctypes
 
     lib = native.hip_lib()
     fn = lib.dml_test_wave_prims
     fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_void_p]
-    g = torch.Generator().manual_seed(0)
-    x = torch.randint(0, 1 << 14, (16, 64), generator=g, dtype=torch.int64).to(torch.int32)
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    rng = np.random.RandomState(0)
+    x = rng.randint(0, 1 << 14, size=(16, 64)).astype(np.uint32)
     x[3] = 7  # all equal
-    xd = x.cuda()
-    srt = torch.empty_like(xd)
-    scn = torch.empty_like(xd)
-    assert fn(xd.data_ptr(), srt.data_ptr(), scn.data_ptr(), 16, native.stream_handle()) == 0
+    x[4] = np.arange(64)[::-1]
+    xd = torch.from_numpy(x.astype(np.int32)).cuda()
+    out = torch.empty((16, 11, 64), dtype=torch.int32, device="cuda")
+    assert fn(xd.data_ptr(), out.data_ptr(), 16, native.stream_handle()) == 0
     torch.cuda.synchronize()
-    assert torch.equal(srt.cpu(), torch.sort(x, dim=1).values)
-    assert torch.equal(scn.cpu().long(), torch.cumsum(x.long(), dim=1))
+    o = out.cpu().numpy().view(np.uint32)
+    lanes = np.arange(64)
+    for bi in range(16):
+        v = x[bi]
+        assert np.array_equal(o[bi, 0], np.sort(v))
+        assert np.array_equal(o[bi, 1], np.cumsum(v.astype(np.uint64)).astype(np.uint32))
+        for k, m in enumerate((1, 2, 4, 8, 16, 32)):
+            assert np.array_equal(o[bi, 2 + k], v[lanes ^ m]), (bi, m)
+        g = v % 97
+        assert (o[bi, 8] == np.flatnonzero(g == g.max())[0]).all()
+        sd = np.concatenate([v[1:], [np.uint32(0xFFFFFFFF)]])
+        assert np.array_equal(o[bi, 9], sd)
+        mn = min((int(v[l]) << 32) | l for l in range(64))
+        assert (o[bi, 10] == np.uint32(mn & 0xFFFFFFFF)).all()
