@@ -112,7 +112,7 @@ __device__ double node_impurity(const Ctx& c, int node, int crit) {
   const double* v = c.node_val + (int64_t)node * c.VC;
   if (c.is_reg) return mse_impurity(v[0], v[1], v[2]);
   ClsAcc a;
-  a.init();
+  a.init(crit);
   for (int k = 0; k < c.C; ++k) a.add(v[k]);
   return cls_impurity(a, crit);
 }
@@ -190,6 +190,31 @@ __device__ __forceinline__ uint64_t wave_next_feature(uint64_t node_key, int d, 
   return wave::min_u64(best, lane);
 }
 
+// per-lane cache of the node's feature ranks (features lane + 64 i, i < 4): ranks are
+// hashed once per node instead of once per extracted feature (d <= 256; larger d falls
+// back to wave_next_feature).
+struct RankCache {
+  uint64_t r[4];
+  bool cached;
+  __device__ __forceinline__ void build(uint64_t node_key, int d, int lane) {
+    cached = d <= 256;
+    if (!cached) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = lane + 64 * i;
+      r[i] = f < d ? feature_rank(node_key, f) : ~0ull;
+    }
+  }
+  __device__ __forceinline__ uint64_t next(uint64_t node_key, int d, int lane, uint64_t last, bool first) const {
+    if (!cached) return wave_next_feature(node_key, d, lane, last, first);
+    uint64_t best = ~0ull;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if ((first || r[i] > last) && r[i] < best) best = r[i];
+    return wave::min_u64(best, lane);
+  }
+};
+
 template <typename CT>
 __device__ __forceinline__ void scan256(CT* p, int lane) {
   CT v0 = p[4 * lane], v1 = p[4 * lane + 1], v2 = p[4 * lane + 2], v3 = p[4 * lane + 3];
@@ -242,7 +267,7 @@ __device__ void eval_feature(typename HT<MODE>::T* h, int C, int CH, const TreeS
       g = mse_proxy(l0, l1, t0 - l0, t1 - l1);
     } else {
       ClsAcc L, R;
-      L.init(); R.init();
+      L.init(s.criterion); R.init(s.criterion);
       for (int k = 0; k < C; ++k) {
         const double lc = hist_chan<MODE>(h, k, CH, b);
         const double tc = hist_chan<MODE>(h, k, CH, 255);
@@ -324,7 +349,7 @@ __device__ bool accept_split(const Ctx& c, const TreeSpec& s, int node, int tree
     impR = mse_impurity(pv[0] - best_left[0], pv[1] - best_left[1], pv[2] - best_left[2]);
   } else {
     ClsAcc N, L, R;
-    N.init(); L.init(); R.init();
+    N.init(s.criterion); L.init(s.criterion); R.init(s.criterion);
     for (int k = 0; k < c.C; ++k) { N.add(pv[k]); L.add(best_left[k]); R.add(pv[k] - best_left[k]); }
     wN = N.w; wL = L.w; wR = R.w;
     impN = cls_impurity(N, s.criterion); impL = cls_impurity(L, s.criterion); impR = cls_impurity(R, s.criterion);
@@ -391,9 +416,23 @@ __global__ __launch_bounds__(NT) void k_nodes(Ctx c, int tier, int set_cur) {
     sc->best_gain = -INFINITY; sc->best_feat = -1; sc->best_bin = -1;
     sc->nonconst = 0; sc->pos = 0; sc->first = 1; sc->last = 0;
   }
+  RankCache rc;
+  if (wid == 0) rc.build(on.key, d, lane);
   __syncthreads();
   const uint32_t* rows = c.rows_cur + c.row_off[on.tree];
   const int k = s.max_features;
+  // wave tier: a node's <= 256 rows (ids + bootstrap weights) stay in registers across
+  // feature groups instead of being re-read and re-hashed per group
+  const bool reg_rows = NT == 64 && on.count <= 256;
+  uint32_t rrow[4], rw[4];
+  if (reg_rows) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = tid + 64 * i;
+      rrow[i] = r < on.count ? rows[on.start + r] : 0u;
+      rw[i] = r < on.count ? boot_weight(s, rrow[i]) : 0u;
+    }
+  }
   while (true) {
     const int pos = sc->pos, nonconst = sc->nonconst;
     if (nonconst >= k || pos >= d) break;
@@ -402,16 +441,22 @@ __global__ __launch_bounds__(NT) void k_nodes(Ctx c, int tier, int set_cur) {
       uint64_t last = sc->last;
       bool first = sc->first != 0;
       for (int j = 0; j < g; ++j) {
-        last = wave_next_feature(on.key, d, lane, last, first);
+        last = rc.next(on.key, d, lane, last, first);
         first = false;
         if (lane == 0) feats[j] = (int16_t)(uint32_t)last;
       }
       if (lane == 0) { sc->last = last; sc->first = 0; }
     }
     __syncthreads();
-    for (int r = tid; r < on.count; r += NT) {
-      const uint32_t row = rows[on.start + r];
-      hist_add_row<MODE>(hist, c, feats, g, row, boot_weight(s, row), span);
+    if (reg_rows) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (tid + 64 * i < on.count) hist_add_row<MODE>(hist, c, feats, g, rrow[i], rw[i], span);
+    } else {
+      for (int r = tid; r < on.count; r += NT) {
+        const uint32_t row = rows[on.start + r];
+        hist_add_row<MODE>(hist, c, feats, g, row, boot_weight(s, row), span);
+      }
     }
     __syncthreads();
     for (int j = wid; j < g; j += NW)
@@ -513,7 +558,7 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
     const float wsh = __shfl(my_w, src);
     const uint32_t w = valid_row ? (uint32_t)wsh : 0u;
     ClsAcc L, R;
-    L.init(); R.init();
+    L.init(s.criterion); R.init(s.criterion);
     for (int k = 0; k < c.C; ++k) {
       const uint32_t v = (ycls == k) ? w : 0u;
       const uint32_t pre = wave::incl_scan<uint32_t>(v);
@@ -579,8 +624,10 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     int nonconst = 0, best_f = -1, best_b = -1;
     double best_g = -INFINITY;
     uint64_t last = 0;
+    RankCache rc;
+    rc.build(e.key, d, lane);
     for (int pos = 0; nonconst < s.max_features && pos < d; ++pos) {
-      last = wave_next_feature(e.key, d, lane, last, pos == 0);
+      last = rc.next(e.key, d, lane, last, pos == 0);
       const int f = (int)(uint32_t)last;
       const int my_bin = cache ? xc[lane * dp + f] : (lane < cnt0 ? xg[f] : 0);
       double g;

@@ -124,13 +124,16 @@ DML_HD double dlog2(double x) {
 }
 
 // Accumulator for one side of a classification split, fed class sums in class order.
+// The entropy term (c log2 c) is only accumulated for the entropy criterion: for Gini
+// it would be dead work (a double log2 per class per candidate bin).
 struct ClsAcc {
   double w, sq, clogc;
-  DML_HDM void init() { w = 0.0; sq = 0.0; clogc = 0.0; }
+  bool ent;
+  DML_HDM void init(int crit) { w = 0.0; sq = 0.0; clogc = 0.0; ent = crit == kEntropy; }
   DML_HDM void add(double c) {
     w += c;
     sq += c * c;
-    if (c > 0.0) clogc += c * dlog2(c);
+    if (ent && c > 0.0) clogc += c * dlog2(c);
   }
 };
 

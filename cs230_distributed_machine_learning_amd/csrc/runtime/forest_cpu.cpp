@@ -68,7 +68,7 @@ static void build_tree(const Data& D, const TreeSpec& s, CpuTree& out) {
 
   auto impurity_of = [&](const double* v) {
     if (D.is_reg) return mse_impurity(v[0], v[1], v[2]);
-    ClsAcc a; a.init();
+    ClsAcc a; a.init(s.criterion);
     for (int k = 0; k < D.C; ++k) a.add(v[k]);
     return cls_impurity(a, s.criterion);
   };
@@ -112,7 +112,7 @@ static void build_tree(const Data& D, const TreeSpec& s, CpuTree& out) {
           const uint32_t rl = hu[D.C * 256 + b], rr = tot_rows - rl;
           nc |= (rl > 0 && rr > 0);
           if (rl < (uint32_t)s.min_samples_leaf || rr < (uint32_t)s.min_samples_leaf) continue;
-          ClsAcc L, R; L.init(); R.init();
+          ClsAcc L, R; L.init(s.criterion); R.init(s.criterion);
           for (int k = 0; k < D.C; ++k) {
             const double lc = (double)hu[k * 256 + b], tc = (double)hu[k * 256 + 255];
             L.add(lc); R.add(tc - lc);
@@ -165,7 +165,7 @@ static void build_tree(const Data& D, const TreeSpec& s, CpuTree& out) {
       impL = mse_impurity(best_left[0], best_left[1], best_left[2]);
       impR = mse_impurity(pv[0] - best_left[0], pv[1] - best_left[1], pv[2] - best_left[2]);
     } else {
-      ClsAcc N, L, R; N.init(); L.init(); R.init();
+      ClsAcc N, L, R; N.init(s.criterion); L.init(s.criterion); R.init(s.criterion);
       for (int k = 0; k < D.C; ++k) { N.add(pv[k]); L.add(best_left[k]); R.add(pv[k] - best_left[k]); }
       wN = N.w; wL = L.w; wR = R.w;
       impN = cls_impurity(N, s.criterion); impL = cls_impurity(L, s.criterion); impR = cls_impurity(R, s.criterion);
