@@ -408,16 +408,17 @@ def candidate_costs(plan: Dict[str, Any], n_train: int, d: int, n_classes: int) 
     return out
 
 
-def execute_plan_slice(ctl: Controller, job: Job, plan: Dict[str, Any], dd, cand_ids: List[int], worker_id: str,
-                       device_name: str, seed: int = 0):
-    """Run one slice of candidates on a device and return (results, J3 metrics per candidate)."""
+def run_slice(plan: Dict[str, Any], params: List[Dict[str, Any]], subtask_ids: List[str], dd, cand_ids: List[int],
+              worker_id: str, device_name: str, seed: int = 0):
+    """Run one slice of candidates on a device -> (results, J3 metrics per candidate, wall s).
+
+    Controller-free so every rank of the distributed runner executes exactly this.
+    """
     from .executor import JobSpec, run_candidates
 
-    spec = JobSpec(model_type=plan["model_type"], candidates=[job.subtasks[i].spec["parameters"] for i in
-                                                               range(job.total)],
-                   cv=plan["cv"], scoring=plan["scoring"], holdout=plan["holdout"], test_size=plan["test_size"],
-                   random_state=plan["random_state"], error_score=plan["error_score"],
-                   keep_models="none", seed=seed)
+    spec = JobSpec(model_type=plan["model_type"], candidates=params, cv=plan["cv"], scoring=plan["scoring"],
+                   holdout=plan["holdout"], test_size=plan["test_size"], random_state=plan["random_state"],
+                   error_score=plan["error_score"], keep_models="none", seed=seed)
     received = utc_iso()
     with _Sampler() as smp:
         started = utc_iso()
@@ -429,13 +430,49 @@ def execute_plan_slice(ctl: Controller, job: Job, plan: Dict[str, Any], dd, cand
     metrics = {}
     for r in results:
         metrics[r.candidate] = {
-            "worker_id": worker_id, "subtask_id": job.subtasks[r.candidate].subtask_id,
+            "worker_id": worker_id, "subtask_id": subtask_ids[r.candidate],
             "status": "DONE" if r.ok else "FAILED", "received_at": received, "started_at": started,
             "finished_at": finished, "cpu_percent_avg": cpu, "mem_percent_avg": mem, "algo": plan["model_type"],
             "device": device_name, "fit_seconds": r.fit_seconds, "slice_wall_seconds": wall,
             "n_fits": r.result.get("n_fits", 0) if r.ok else 0,
         }
     return results, metrics, wall
+
+
+def execute_plan_slice(ctl: Controller, job: Job, plan: Dict[str, Any], dd, cand_ids: List[int], worker_id: str,
+                       device_name: str, seed: int = 0):
+    params = [st.spec["parameters"] for st in job.subtasks]
+    sids = [st.subtask_id for st in job.subtasks]
+    return run_slice(plan, params, sids, dd, cand_ids, worker_id, device_name, seed)
+
+
+def plan_slices(ctl: Controller, plan: Dict[str, Any], todo: List[int], n_train: int, d: int, n_classes: int,
+                min_slices: int = 1) -> List[List[int]]:
+    """LPT order (most expensive first) cut into ~chunk_target_s slices."""
+    costs = candidate_costs(plan, n_train, d, n_classes)
+    order = sorted(todo, key=lambda i: -costs[i])
+    est = [ctl.scheduler.estimate(plan["model_type"], costs[i]) for i in order]
+    chunk_ids = chunk_units(est, ctl.config.chunk_target_s, min_slices)
+    slices: Dict[int, List[int]] = {}
+    for i, c in zip(order, chunk_ids):
+        slices.setdefault(int(c), []).append(i)
+    return [slices[k] for k in sorted(slices)]
+
+
+def publish_results(ctl: Controller, job: Job, results, metrics) -> None:
+    for r in results:
+        st = job.subtasks[r.candidate]
+        ok = r.ok if hasattr(r, "ok") else r["ok"]
+        if ok:
+            R = dict(r.result if hasattr(r, "result") else r["result"])
+            R.setdefault("model_id", f"{st.subtask_id}_model")
+            R.setdefault("model_path", None)
+            ctl.table.finish_subtask(job.job_id, st.subtask_id, "completed", result=json_safe(R),
+                                     metrics=metrics.get(r.candidate))
+        else:
+            ctl.table.finish_subtask(job.job_id, st.subtask_id, "failed",
+                                     error=r.error if hasattr(r, "error") else r.get("error"),
+                                     metrics=metrics.get(r.candidate))
 
 
 def refit_best(ctl: Controller, job: Job, plan: Dict[str, Any], dd, best_idx: int) -> Optional[str]:
@@ -516,63 +553,53 @@ class LocalRunner(Runner):
         todo = [st.index for st in job.subtasks if st.status not in ("completed", "failed")]
         if not todo:
             return
+        slices = plan_slices(ctl, plan, todo, int(dd.n * 0.8), dd.d, dd.n_classes)
         costs = candidate_costs(plan, int(dd.n * 0.8), dd.d, dd.n_classes)
-        order = sorted(todo, key=lambda i: -costs[i])
-        est = [ctl.scheduler.estimate(plan["model_type"], costs[i]) for i in order]
-        chunk_ids = chunk_units(est, ctl.config.chunk_target_s, 1)
-        slices: Dict[int, List[int]] = {}
-        for i, c in zip(order, chunk_ids):
-            slices.setdefault(int(c), []).append(i)
         all_results = []
         pending_final = None
-        for ci in sorted(slices):
-            ids = slices[ci]
+        for si, ids in enumerate(slices):
             ctl.table.mark_running(job.job_id, ids, self.worker_id)
             results, metrics, wall = execute_plan_slice(ctl, job, plan, dd, ids, self.worker_id, self.device,
-                                                        seed=abs(hash(job.job_id)) & 0xFFFF)
-            unit = Unit(unit_id=f"{job.job_id}:{ci}", cost=sum(costs[i] for i in ids), algo=plan["model_type"])
+                                                        seed=job_seed(job.job_id))
+            unit = Unit(unit_id=f"{job.job_id}:{si}", cost=sum(costs[i] for i in ids), algo=plan["model_type"])
             ctl.scheduler.observe(self.worker_id, unit, wall)
             ctl.scheduler.heartbeat(self.worker_id)
-            if ci == max(slices):
+            if si == len(slices) - 1:
                 pending_final = (results, metrics)
             else:
-                self._publish(job, results, metrics)
+                publish_results(ctl, job, results, metrics)
             all_results.extend(results)
-        # refit + store the best model before the job turns "completed"
-        ok = [r for r in all_results if r.ok]
-        prev_ok = [st.result for st in job.subtasks if st.status == "completed" and st.result]
-        if ok and plan.get("refit", True) and ctl.config.keep_models != "none":
-            def score(r):
-                v = r.result.get("mean_cv_score")
-                return -np.inf if v is None or (isinstance(v, float) and np.isnan(v)) else v
-            best = max(ok, key=score)
-            better_prev = any(score_r(p) > score(best) for p in prev_ok)
-            if not better_prev:
-                try:
-                    path = refit_best(ctl, job, plan, dd, best.candidate)
-                    if path:
-                        best.result["model_path"] = path
-                except Exception:
-                    traceback.print_exc()
+        finalize_job(ctl, job, plan, dd, all_results)
         if pending_final:
-            self._publish(job, *pending_final)
-
-    def _publish(self, job: Job, results, metrics) -> None:
-        for r in results:
-            st = job.subtasks[r.candidate]
-            if r.ok:
-                R = dict(r.result)
-                R.setdefault("model_id", f"{st.subtask_id}_model")
-                R.setdefault("model_path", None)
-                self.ctl.table.finish_subtask(job.job_id, st.subtask_id, "completed", result=json_safe(R),
-                                              metrics=metrics.get(r.candidate))
-            else:
-                self.ctl.table.finish_subtask(job.job_id, st.subtask_id, "failed", error=r.error,
-                                              metrics=metrics.get(r.candidate))
+            publish_results(ctl, job, *pending_final)
 
     def shutdown(self) -> None:
         if self._thread is not None:
             self.q.put(None)
+
+
+def job_seed(job_id: str) -> int:
+    import zlib
+
+    return zlib.crc32(job_id.encode()) & 0xFFFF
+
+
+def finalize_job(ctl: Controller, job: Job, plan: Dict[str, Any], dd, results) -> None:
+    """Refit the best candidate (sklearn refit=True) and attach its model path before
+    the last results are published, so "completed" always comes with the artefact."""
+    ok = [r for r in results if r.ok]
+    prev_ok = [st.result for st in job.subtasks if st.status == "completed" and st.result]
+    if not ok or not plan.get("refit", True) or ctl.config.keep_models == "none":
+        return
+    best = max(ok, key=lambda r: score_r(r.result))
+    if any(score_r(p) > score_r(best.result) for p in prev_ok):
+        return
+    try:
+        path = refit_best(ctl, job, plan, dd, best.candidate)
+        if path:
+            best.result["model_path"] = path
+    except Exception:
+        traceback.print_exc()
 
 
 def score_r(R: Dict[str, Any]) -> float:

@@ -1,0 +1,79 @@
+"""Dataset distribution across ranks (RCCL over xGMI), once per dataset.
+
+Reference: every worker re-reads the full CSV from NFS/EFS for every task
+(aws-prod/worker/worker.py:406-425; SURVEY §2.5 "the dominant data movement").  Here:
+
+* ``broadcast_table`` — rank 0 parses the file once, copies it to its GPU, and one
+  RCCL broadcast per tensor (X float32 [n, d], y) lands it in every rank's HBM;
+  the table then stays resident across every candidate and job (``DeviceCache``).
+* ``allgather_table`` — each rank holds a contiguous row shard (e.g. generated on the
+  device, data/synthetic.py) and one ``all_gather_into_tensor`` assembles the table.
+The uint8 binned copy is derived on each rank from edges broadcast by rank 0, so all
+ranks grow identical trees for identical seeds.
+"""
+from __future__ import annotations
+
+import json
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import dist
+
+
+def broadcast_table(X: Optional[np.ndarray], y: Optional[np.ndarray], device: torch.device, y_kind: str = "auto"):
+    """Rank 0 passes host arrays; every rank returns (X_dev, y_host_numpy)."""
+    inf = dist.info()
+    st = dist.store()
+    if not inf.is_dist:
+        return torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).to(device), np.asarray(y)
+    key = "dataset/meta"
+    if inf.rank == 0:
+        y = np.asarray(y)
+        # labels may be strings: ship a compact code array + the class table via the store
+        if y.dtype.kind in "OUS":
+            classes, codes = np.unique(y.astype(str), return_inverse=True)
+            meta = {"n": int(X.shape[0]), "d": int(X.shape[1]), "y": "codes", "classes": classes.tolist()}
+            y_num = codes.astype(np.float64)
+        else:
+            meta = {"n": int(X.shape[0]), "d": int(X.shape[1]), "y": str(y.dtype)}
+            y_num = y.astype(np.float64)
+        st.set(key, json.dumps(meta))
+        Xd = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).to(device)
+        yd = torch.from_numpy(y_num).to(device)
+    else:
+        st.wait([key])
+        meta = json.loads(st.get(key))
+        Xd = torch.empty((meta["n"], meta["d"]), dtype=torch.float32, device=device)
+        yd = torch.empty((meta["n"],), dtype=torch.float64, device=device)
+    dist.broadcast(Xd, 0)
+    dist.broadcast(yd, 0)
+    dist.barrier()
+    if inf.rank == 0:
+        st.delete_key(key)
+        return Xd, y
+    y_host = yd.cpu().numpy()
+    if meta["y"] == "codes":
+        y_host = np.asarray(meta["classes"], dtype=object)[y_host.astype(np.int64)]
+    else:
+        y_host = y_host.astype(np.dtype(meta["y"]))
+    return Xd, y_host
+
+
+def allgather_table(X_shard: torch.Tensor, y_shard: torch.Tensor):
+    return dist.all_gather_rows(X_shard), dist.all_gather_rows(y_shard)
+
+
+def share_bins(dd) -> None:
+    """Rank 0 computes quantile edges; all ranks bin with the same edges."""
+    from ..ops import binning
+
+    inf = dist.info()
+    if inf.rank == 0 or not inf.is_dist:
+        edges = binning.quantile_edges(dd.X)
+    else:
+        edges = torch.empty((dd.d, binning.MAX_EDGES), dtype=torch.float32, device=dd.X.device)
+    dist.broadcast(edges, 0)
+    dd._edges = edges
+    dd._Xb = binning.bin_matrix(dd.X, edges)

@@ -1,0 +1,109 @@
+"""Multi-process (gloo, world_size 2) runs of the distributed runtime on CPU.
+
+Exercises the same code the MI355X ranks run over RCCL: store-based job announcement,
+dataset broadcast, dynamic slice claiming, score all-reduce, result publication."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, root, outq):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), OMP_NUM_THREADS="2")
+    import threading
+
+    from cs230_distributed_machine_learning_amd.config import Config
+    from cs230_distributed_machine_learning_amd.parallel import dist
+    from cs230_distributed_machine_learning_amd.parallel.runner import DistributedRunner, WorkerCore, worker_loop
+
+    inf = dist.init(want_gpu=False, timeout_s=120)
+    core = WorkerCore(inf.device)
+    if rank == 0:
+        from cs230_distributed_machine_learning_amd.engine.service import Controller
+
+        cfg = Config.from_env(data_root=root, device="cpu", chunk_target_s=0.0)
+        runner = DistributedRunner(core)
+        ctl = Controller(cfg, runner=runner)
+
+        def drive():
+            try:
+                sid = ctl.create_session()[1]["session_id"]
+                ctl.download_data(sid, {"dataset_url": "iris", "dataset_name": "iris", "dataset_type": "sklearn"})
+                body = {"dataset_id": "iris", "train_params": {"test_size": 0.25, "random_state": 42,
+                                                               "target_column": "species"},
+                        "model_details": {"model_type": "LogisticRegression", "search_type": "GridSearchCV",
+                                          "hyperparameters": {"base_estimator_params": {},
+                                                              "search_params": {"param_grid": {
+                                                                  "C": [0.1, 1.0, 10.0, 100],
+                                                                  "solver": ["liblinear", "lbfgs"]}},
+                                                              "cv_params": {"cv": 5}}}}
+                st, resp = ctl.train(sid, body)
+                jid = resp["job_id"]
+                ctl.table.wait_finished(jid, timeout=300)
+                st, status = ctl.check_status(sid, jid)
+                body2 = dict(body, model_details={"model_type": "RandomForestClassifier",
+                                                  "search_type": "GridSearchCV",
+                                                  "hyperparameters": {"base_estimator_params": {"n_estimators": 10},
+                                                                      "search_params": {"param_grid": {
+                                                                          "max_depth": [2, 4, None]}},
+                                                                      "cv_params": {"cv": 3}}})
+                st, resp2 = ctl.train(sid, body2)
+                ctl.table.wait_finished(resp2["job_id"], timeout=300)
+                st, status2 = ctl.check_status(sid, resp2["job_id"])
+                metrics = ctl.metrics(sid, jid)[1]
+                outq.put(("ok", status, status2, metrics))
+            except Exception as e:  # pragma: no cover
+                import traceback
+
+                outq.put(("err", traceback.format_exc()))
+            finally:
+                runner.shutdown()
+
+        t = threading.Thread(target=drive, daemon=True)
+        t.start()
+        runner.serve_forever()
+        t.join()
+    else:
+        worker_loop(core)
+    dist.destroy()
+
+
+def test_two_rank_gridsearch_gloo():
+    root = tempfile.mkdtemp()
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, root, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        out = q.get(timeout=600)
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+            if p.is_alive():
+                p.kill()
+    assert out[0] == "ok", out[1]
+    status, status2, metrics = out[1], out[2], out[3]
+    assert status["job_status"] == "completed" and status["total_subtasks"] == 8
+    res = status["job_result"]["results"]
+    assert len(res) == 8
+    best = status["best_result"]
+    assert best["mean_cv_score"] >= 0.95
+    assert len(best["cv_scores"]) == 5
+    workers = {m["worker_id"] for m in metrics}
+    assert workers <= {"rank0", "rank1"} and len(metrics) == 8
+    assert status2["job_status"] == "completed" and len(status2["job_result"]["results"]) == 3
+    assert status2["best_result"]["mean_cv_score"] > 0.9
