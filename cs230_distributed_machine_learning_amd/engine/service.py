@@ -588,11 +588,12 @@ def finalize_job(ctl: Controller, job: Job, plan: Dict[str, Any], dd, results) -
     """Refit the best candidate (sklearn refit=True) and attach its model path before
     the last results are published, so "completed" always comes with the artefact."""
     ok = [r for r in results if r.ok]
-    prev_ok = [st.result for st in job.subtasks if st.status == "completed" and st.result]
     if not ok or not plan.get("refit", True) or ctl.config.keep_models == "none":
         return
-    best = max(ok, key=lambda r: score_r(r.result))
-    if any(score_r(p) > score_r(best.result) for p in prev_ok):
+    # same winner as jobs.aggregate_best: max mean_cv_score, ties -> lowest subtask index
+    best = max(ok, key=lambda r: (score_r(r.result), -r.candidate))
+    if any(st.status == "completed" and st.result and (score_r(st.result), -st.index) > (score_r(best.result), -best.candidate)
+           for st in job.subtasks):
         return
     try:
         path = refit_best(ctl, job, plan, dd, best.candidate)

@@ -5,20 +5,26 @@ scheduler's membership/introspection routes (aws-prod/scheduler/scheduler.py:95-
 so existing clients, the notebook prototype (``/train`` + ``/check_status``) and the
 0.2.6 SDK (``/train_status`` SSE + ``/metrics``) all talk to one process.
 """
-from __future__ import annotations
-
 from typing import Any, Optional
+
+from fastapi import FastAPI, Request   # module-level: FastAPI resolves route annotations from globals
 
 from ..engine.service import Controller
 
 
 def create_app(controller: Optional[Controller] = None):
-    from fastapi import FastAPI, Request
     from fastapi.middleware.cors import CORSMiddleware
     from fastapi.responses import FileResponse, JSONResponse, StreamingResponse
 
     ctl = controller or Controller()
-    app = FastAPI(title="distributed-ml (MI355X)")
+    from contextlib import asynccontextmanager
+
+    @asynccontextmanager
+    async def lifespan(_app):
+        yield
+        ctl.shutdown()
+
+    app = FastAPI(title="distributed-ml (MI355X)", lifespan=lifespan)
     app.add_middleware(CORSMiddleware, allow_origins=["*"], allow_methods=["*"], allow_headers=["*"])
     app.state.controller = ctl
 
@@ -107,10 +113,6 @@ def create_app(controller: Optional[Controller] = None):
     @app.post("/heartbeat")
     async def heartbeat(request: Request):
         return reply(ctl.heartbeat(await body_of(request)))
-
-    @app.on_event("shutdown")
-    def _shutdown():
-        ctl.shutdown()
 
     return app
 

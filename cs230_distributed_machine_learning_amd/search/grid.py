@@ -114,9 +114,10 @@ class ParameterGrid:
 def sample_without_replacement(n_population: int, n_samples: int, random_state=None) -> np.ndarray:
     """Same draws as ``sklearn.utils.random.sample_without_replacement(method="auto")``.
 
-    sklearn picks a permutation prefix when 0.01 < ratio < 0.99 and otherwise a
-    tracking-selection loop of ``randint`` rejections; both consume the RNG the same
-    way here, so the sampled candidate indices are identical.
+    sklearn picks a permutation prefix when 0.01 < ratio < 0.99, a tracking-selection
+    loop of ``randint`` rejections when ratio < 0.2, and reservoir sampling otherwise;
+    each branch consumes the RNG the same way here, so the sampled candidate indices
+    are identical.
     """
     if n_population < 0 or n_samples < 0 or n_samples > n_population:
         raise ValueError("invalid sample_without_replacement arguments")
@@ -125,6 +126,13 @@ def sample_without_replacement(n_population: int, n_samples: int, random_state=N
     if 0.01 < ratio < 0.99:
         return rng.permutation(n_population)[:n_samples]
     out = np.empty(n_samples, dtype=np.int64)
+    if ratio >= 0.2:
+        out[:] = np.arange(n_samples)
+        for i in range(n_samples, n_population):
+            j = rng.randint(0, i + 1)
+            if j < n_samples:
+                out[j] = i
+        return out
     selected = set()
     for i in range(n_samples):
         j = rng.randint(n_population)

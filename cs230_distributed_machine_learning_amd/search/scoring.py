@@ -132,7 +132,7 @@ def score(name: str, y_true: torch.Tensor, pred: torch.Tensor, n_classes: int = 
     if name == "neg_mean_absolute_error":
         return -float(err.abs().mean())
     if name == "neg_median_absolute_error":
-        return -float(err.abs().median())
+        return -float(torch.quantile(err.abs().double(), 0.5))  # numpy median (mean of middle pair)
     if name == "max_error":
         return -float(err.abs().max())
     if name == "explained_variance":
