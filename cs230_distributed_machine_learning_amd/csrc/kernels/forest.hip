@@ -55,6 +55,7 @@ struct ForestArgs {
   // outputs
   int64_t n_nodes_out, status_out, levels_out, large_rounds_out;
   int64_t tier_nodes_out[4];
+  int64_t ystride;       // >0: tree t regresses on yreg[specs[t].target * ystride + row] (boosting)
 };
 
 constexpr int kTiers = 4;  // 0 subtree, 1 wave, 2 block, 3 large
@@ -97,7 +98,13 @@ struct Ctx {
   int64_t large_cap;
   int32_t wave_max, block_max, chunk, kg_wave, kg_block, kg_large, slack_wave;
   int32_t sub_max, sub_cache_d;
+  int64_t ystride;
 };
+
+// target vector of a tree (shared y, or its own row of the boosting target matrix)
+__device__ __forceinline__ const float* tree_y(const Ctx& c, const TreeSpec& s) {
+  return c.ystride ? c.yreg + (int64_t)s.target * c.ystride : c.yreg;
+}
 
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
@@ -292,8 +299,8 @@ __device__ void eval_feature(typename HT<MODE>::T* h, int C, int CH, const TreeS
 }
 
 template <int MODE>
-__device__ __forceinline__ void hist_add_row(typename HT<MODE>::T* hist, const Ctx& c, const int16_t* feats, int g,
-                                             uint32_t row, uint32_t w, int span) {
+__device__ __forceinline__ void hist_add_row(typename HT<MODE>::T* hist, const Ctx& c, const float* ty,
+                                             const int16_t* feats, int g, uint32_t row, uint32_t w, int span) {
   const uint8_t* xr = c.Xb + (int64_t)row * c.ld;
   if constexpr (MODE == 0) {
     const int y = c.ycls[row];
@@ -307,7 +314,7 @@ __device__ __forceinline__ void hist_add_row(typename HT<MODE>::T* hist, const C
     const unsigned long long pv = pack_bin(c.ycls[row], w);
     for (int j = 0; j < g; ++j) atomicAdd(&hist[j * span + xr[feats[j]]], pv);
   } else {
-    const float yv = c.yreg[row];
+    const float yv = ty[row];
     const float fw = (float)w, wy = fw * yv, wyy = wy * yv;
     for (int j = 0; j < g; ++j) {
       const int b = xr[feats[j]];
@@ -451,11 +458,11 @@ __global__ __launch_bounds__(NT) void k_nodes(Ctx c, int tier, int set_cur) {
     if (reg_rows) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (tid + 64 * i < on.count) hist_add_row<MODE>(hist, c, feats, g, rrow[i], rw[i], span);
+        if (tid + 64 * i < on.count) hist_add_row<MODE>(hist, c, tree_y(c, s), feats, g, rrow[i], rw[i], span);
     } else {
       for (int r = tid; r < on.count; r += NT) {
         const uint32_t row = rows[on.start + r];
-        hist_add_row<MODE>(hist, c, feats, g, row, boot_weight(s, row), span);
+        hist_add_row<MODE>(hist, c, tree_y(c, s), feats, g, row, boot_weight(s, row), span);
       }
     }
     __syncthreads();
@@ -603,7 +610,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   if (lane < cnt0) {
     row = rows[lane];
     my_w = (float)boot_weight(s, row);
-    if constexpr (REG) my_y = c.yreg[row];
+    if constexpr (REG) my_y = tree_y(c, s)[row];
     else my_cls = c.ycls[row];
   }
   const uint8_t* xg = c.Xb + (int64_t)row * c.ld;
@@ -729,7 +736,7 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
   const uint32_t* rows = c.rows_cur + c.row_off[st.on.tree] + st.on.start;
   for (int r = r0 + threadIdx.x; r < r1; r += 256) {
     const uint32_t row = rows[r];
-    hist_add_row<MODE>(hist, c, feats, g, row, boot_weight(s, row), span);
+    hist_add_row<MODE>(hist, c, tree_y(c, s), feats, g, row, boot_weight(s, row), span);
   }
   __syncthreads();
   // flush into the node's global histogram: always unpacked planes [CH][256]
@@ -924,7 +931,7 @@ __global__ __launch_bounds__(256) void k_fill_active(Ctx c) {
     out[p++] = r;
     const double w = (double)wts[i];
     if constexpr (REG) {
-      const double y = (double)c.yreg[r];
+      const double y = (double)tree_y(c, s)[r];
       atomicAdd(&acc[0], w);
       atomicAdd(&acc[1], w * y);
       atomicAdd(&acc[2], w * y * y);
@@ -1014,6 +1021,7 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.CH = c.is_reg ? 4 : (int)a->n_classes + 1;
   c.VC = c.is_reg ? 3 : (int)a->n_classes;
   c.ycls = (const int32_t*)a->ycls; c.yreg = (const float*)a->yreg;
+  c.ystride = a->ystride;
   c.roles = (const uint8_t*)a->roles; c.specs = (const TreeSpec*)a->specs; c.T = (int)a->T;
   c.active_count = (int32_t*)a->active_count; c.row_off = (const int64_t*)a->row_off;
   c.nodes = (NodeRec*)a->nodes; c.node_val = (double*)a->node_val; c.pool_cap = a->pool_cap;

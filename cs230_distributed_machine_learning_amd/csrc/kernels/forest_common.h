@@ -49,10 +49,10 @@ struct TreeSpec {
   int32_t min_samples_split;
   int32_t min_samples_leaf;
   int32_t max_features;     // k (>=1, <= n_features)
-  int32_t bootstrap;        // 0/1
+  int32_t bootstrap;        // 0 all rows, 1 Poisson(lambda) bootstrap, 2 Bernoulli subsample (p = pois_cdf[0] / 2^32)
   int32_t criterion;        // Criterion
   float min_impurity_decrease;
-  float pad0;
+  int32_t target;           // row of the per-tree target matrix (ForestArgs.ystride > 0: boosting)
   uint32_t pois_cdf[kPoisTable];  // P(K<=j) * 2^32 (saturated), j = 0..11
 };
 
@@ -80,6 +80,7 @@ DML_HD uint32_t hash_u32(uint64_t key, uint64_t ctr) {
 DML_HD uint32_t boot_weight(const TreeSpec& t, uint32_t row) {
   if (!t.bootstrap) return 1u;
   const uint32_t u = hash_u32(t.seed, 0xB0075ull * 0x100000000ull + row);
+  if (t.bootstrap == 2) return u < t.pois_cdf[0] ? 1u : 0u;
   uint32_t k = 0;
   while (k < (uint32_t)kPoisTable && u >= t.pois_cdf[k]) ++k;
   return k;

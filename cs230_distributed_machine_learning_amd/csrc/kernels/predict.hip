@@ -143,11 +143,37 @@ __global__ __launch_bounds__(256) void k_scores(ScoreArgs a) {
   }
 }
 
+// leaf index of every row for every tree (boosting line search / raw-score update):
+// leaf[t * n + row]; trees t = t0 .. t0+T-1 have their roots at node t.
+__global__ __launch_bounds__(256) void k_apply(const uint8_t* __restrict__ Xb, int64_t ld, int64_t n,
+                                               const NodeRec* __restrict__ nodes, int32_t t0,
+                                               int32_t* __restrict__ leaf) {
+  const int t = blockIdx.y;
+  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (row >= n) return;
+  const uint8_t* xr = Xb + row * ld;
+  int node = t0 + t;
+  NodeRec nr = nodes[node];
+  for (int steps = 0; nr.split >= 0 && steps < 1 << 20; ++steps) {
+    node = nr.left + (xr[nr.split >> 8] > (nr.split & 255) ? 1 : 0);
+    nr = nodes[node];
+  }
+  leaf[(int64_t)t * n + row] = node;
+}
+
 }  // namespace dml
 
 using namespace dml;
 
 extern "C" {
+
+int dml_forest_apply(const uint8_t* Xb, int64_t ld, int64_t n, const dml::NodeRec* nodes, int32_t t0, int32_t T,
+                     int32_t* leaf, hipStream_t st) {
+  if (n <= 0 || T <= 0) return 0;
+  dim3 grid((unsigned)((n + 255) / 256), (unsigned)T);
+  dml::k_apply<<<grid, 256, 0, st>>>(Xb, ld, n, nodes, t0, leaf);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
 
 int dml_predict_sizeof_args() { return (int)sizeof(PredictArgs); }
 

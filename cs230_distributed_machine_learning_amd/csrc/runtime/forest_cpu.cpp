@@ -33,12 +33,14 @@ struct CpuForest {
 struct Data {
   const uint8_t* Xb; int64_t ld; int n, d, C, CH, VC, is_reg;
   const int32_t* ycls; const float* yreg; const uint8_t* roles;
+  int64_t ystride;
 };
 
 struct Job { int node, start, count, depth; uint64_t key; };
 
 static void build_tree(const Data& D, const TreeSpec& s, CpuTree& out) {
   const uint8_t* role = D.roles + (int64_t)s.split * D.n;
+  const float* Y = D.ystride ? D.yreg + (int64_t)s.target * D.ystride : D.yreg;
   std::vector<uint32_t> rows, tmp;
   std::vector<uint32_t> wts;  // indexed by row id through a parallel array
   rows.reserve(D.n);
@@ -51,7 +53,7 @@ static void build_tree(const Data& D, const TreeSpec& s, CpuTree& out) {
     rows.push_back((uint32_t)r);
     wrow[r] = w;
     if (D.is_reg) {
-      const double y = (double)D.yreg[r];
+      const double y = (double)Y[r];
       root[0] += (double)w; root[1] += (double)w * y; root[2] += (double)w * y * y;
     } else {
       root[D.ycls[r]] += (double)w;
@@ -132,7 +134,7 @@ static void build_tree(const Data& D, const TreeSpec& s, CpuTree& out) {
         for (int i = 0; i < jb.count; ++i) {
           const uint32_t r = nr[i];
           const int b = D.Xb[(int64_t)r * D.ld + f];
-          const float fw = (float)wrow[r], y = D.yreg[r], wy = fw * y;
+          const float fw = (float)wrow[r], y = Y[r], wy = fw * y;
           hf[b] += fw; hf[256 + b] += wy; hf[512 + b] += wy * y; hf[768 + b] += 1.f;
         }
         for (int ch = 0; ch < CH; ++ch)
@@ -215,8 +217,9 @@ int dml_cpu_sizeof_treespec() { return (int)sizeof(TreeSpec); }
 
 void* dml_cpu_forest_build(const uint8_t* Xb, int64_t ld, int64_t n, int64_t d, const int32_t* ycls,
                            const float* yreg, int64_t n_classes, int64_t is_reg, const uint8_t* roles,
-                           const TreeSpec* specs, int64_t T) {
+                           const TreeSpec* specs, int64_t T, int64_t ystride) {
   Data D;
+  D.ystride = ystride;
   D.Xb = Xb; D.ld = ld; D.n = (int)n; D.d = (int)d; D.is_reg = (int)is_reg;
   D.C = is_reg ? 1 : (int)n_classes;
   D.CH = is_reg ? 4 : (int)n_classes + 1;
@@ -256,6 +259,23 @@ void dml_cpu_forest_export(void* h, NodeRec* nodes, double* vals) {
     }
     next += (int64_t)tr.nodes.size() - 1;
   }
+}
+
+// leaf[t * n + row] for trees t0 .. t0+T-1 (roots at node t) over all n rows
+void dml_cpu_forest_apply(const uint8_t* Xb, int64_t ld, int64_t n, const NodeRec* nodes, int32_t t0, int32_t T,
+                          int32_t* leaf) {
+#pragma omp parallel for collapse(2) schedule(static)
+  for (int32_t t = 0; t < T; ++t)
+    for (int64_t r = 0; r < n; ++r) {
+      const uint8_t* xr = Xb + r * ld;
+      int node = t0 + t;
+      NodeRec nr = nodes[node];
+      while (nr.split >= 0) {
+        node = nr.left + (xr[nr.split >> 8] > (nr.split & 255) ? 1 : 0);
+        nr = nodes[node];
+      }
+      leaf[(int64_t)t * n + r] = node;
+    }
 }
 
 void dml_cpu_forest_free(void* h) { delete (CpuForest*)h; }

@@ -68,6 +68,12 @@ class DeviceData:
             self._Xb = binning.bin_matrix(self.X, self._edges)
         return self._Xb
 
+    def feature_major(self) -> torch.Tensor:
+        """``X^T`` [d, n] contiguous (coalesced per-feature streaming in the KNN/SVM kernels)."""
+        if getattr(self, "_XT", None) is None:
+            self._XT = self.X.t().contiguous()
+        return self._XT
+
     @property
     def edges(self):
         self.binned()

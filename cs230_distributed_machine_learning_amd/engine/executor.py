@@ -153,6 +153,11 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
             R: Dict[str, Any] = {}
             fit_s = sum((split_out[s][1].fit_seconds if split_out[s][1] else 0.0) for s in split_out)
             model = None
+            hold_out = split_out[hold_idx][1] if hold_idx is not None else None
+            if (hold_idx is not None and (hold_out is None or hold_out.error)) or (cv_idx and failed_fits == len(cv_idx)):
+                errs = [o.error for _t, o in split_out.values() if o is not None and o.error]
+                results.append(_failed(c, spec, errs[0] if errs else "fit failed"))
+                continue
             if hold_idx is not None:
                 t, o = split_out[hold_idx]
                 if clf:

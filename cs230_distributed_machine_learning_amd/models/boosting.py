@@ -1,1 +1,488 @@
-"""Placeholder: family registered later in the build."""
+"""GradientBoosting{Classifier,Regressor} — every fit of a job boosted in lock-step.
+
+Reference: both are whitelisted estimators (aws-prod/worker/worker.py:41,48) that
+sklearn fits one (candidate, fold) at a time: ``n_estimators`` sequential stages, each
+fitting ``K`` depth-``max_depth`` regression trees to the negative gradient and then
+re-solving the leaf values with one Newton / quantile step (sklearn
+``ensemble/_gb.py`` ``_fit_stage`` / ``_update_terminal_regions``).
+
+Here stage ``s`` of EVERY fit in the batch (candidates x CV folds x holdout x K
+classes) is one call of the batched histogram tree builder (csrc/kernels/forest.hip,
+regression mode) on a ``[fits*K, n]`` pseudo-residual matrix (``ForestArgs.ystride``:
+each tree reads its own target row), followed by one ``dml_forest_apply`` launch that
+maps every row to its leaf in every new tree.  Leaf line searches are segmented
+reductions over (tree, leaf) and the raw scores of all rows (train and held-out) are
+updated in place, so held-out predictions are ready when the last stage ends.
+
+Semantics kept from sklearn: losses log_loss (binomial / multinomial with the
+(K-1)/K factor), exponential, squared_error, absolute_error, huber, quantile; the
+DummyEstimator initial predictions; ``friedman_mse`` (same split ranking as
+squared_error for unit weights); learning_rate, subsample (exactly
+``int(subsample * n_train)`` in-bag rows per stage, drawn on-device), max_depth,
+min_samples_split/leaf, min_impurity_decrease, max_features.  Split thresholds come
+from the 256-bin quantisation shared with the forests (exact whenever a feature has
+<= 256 distinct values); early stopping (``n_iter_no_change``) is not implemented
+and is reported in the subtask's warnings.
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Any, Dict, List
+
+import numpy as np
+import torch
+
+from ..ops import forest_ops
+from ..utils import native
+from .base import Family, FitOutput, FitTask, ParamError, as_bool, as_float, as_int, register, seed_of
+from .forest import _count_param, native_seed
+
+_CLS = "GradientBoostingClassifier"
+_REG = "GradientBoostingRegressor"
+
+LOSS_SQ, LOSS_ABS, LOSS_HUBER, LOSS_QUANT, LOSS_LOG, LOSS_EXP = range(6)
+_CLS_LOSSES = {"log_loss": LOSS_LOG, "deviance": LOSS_LOG, "exponential": LOSS_EXP}
+_REG_LOSSES = {"squared_error": LOSS_SQ, "ls": LOSS_SQ, "absolute_error": LOSS_ABS, "lad": LOSS_ABS,
+               "huber": LOSS_HUBER, "quantile": LOSS_QUANT}
+
+_DEFAULTS = {
+    "loss": None, "learning_rate": 0.1, "n_estimators": 100, "subsample": 1.0, "criterion": "friedman_mse",
+    "min_samples_split": 2, "min_samples_leaf": 1, "min_weight_fraction_leaf": 0.0, "max_depth": 3,
+    "min_impurity_decrease": 0.0, "init": None, "random_state": None, "max_features": None, "alpha": 0.9,
+    "verbose": 0, "max_leaf_nodes": None, "warm_start": False, "validation_fraction": 0.1,
+    "n_iter_no_change": None, "tol": 1e-4, "ccp_alpha": 0.0,
+}
+_F32_EPS = float(np.finfo(np.float32).eps)
+
+
+def _max_features(v, d):
+    if v is None or v == "None":
+        return d
+    if isinstance(v, str):
+        if v in ("sqrt", "auto"):
+            return max(1, int(math.sqrt(d)))
+        if v == "log2":
+            return max(1, int(math.log2(d)))
+        raise ParamError(f"max_features {v!r} not understood")
+    if isinstance(v, bool):
+        raise ParamError("max_features must not be a bool")
+    if isinstance(v, int):
+        return max(1, min(d, v))
+    f = float(v)
+    if not 0.0 < f <= 1.0:
+        raise ParamError(f"max_features fraction must be in (0, 1], got {f}")
+    return max(1, int(f * d))
+
+
+# ---- percentiles (numpy 'linear' for the initial estimate, sklearn inverted-CDF in leaves) ----
+def _percentile_linear(v: torch.Tensor, q: float) -> torch.Tensor:
+    s, _ = torch.sort(v)
+    m = s.numel()
+    pos = q * (m - 1)
+    lo = int(math.floor(pos))
+    hi = min(lo + 1, m - 1)
+    return s[lo] + (s[hi] - s[lo]) * (pos - lo)
+
+
+def _percentile_icdf(v: torch.Tensor, q: float) -> torch.Tensor:
+    """sklearn ``_weighted_percentile`` with unit weights (lower value on ties)."""
+    s, _ = torch.sort(v)
+    m = s.numel()
+    i = max(0, min(m - 1, int(math.ceil(q * m - 1e-12)) - 1))
+    return s[i]
+
+
+def _segment_percentile(seg: torch.Tensor, val: torch.Tensor, n_seg: int, q: float) -> torch.Tensor:
+    """Inverted-CDF percentile of ``val`` within each segment id (unit weights); NaN if empty."""
+    out = torch.full((n_seg,), float("nan"), dtype=val.dtype, device=val.device)
+    if seg.numel() == 0:
+        return out
+    order = torch.argsort(val, stable=True)
+    seg_s = seg[order]
+    order2 = torch.argsort(seg_s, stable=True)
+    seg_sorted = seg_s[order2]
+    val_sorted = val[order][order2]
+    cnt = torch.bincount(seg_sorted, minlength=n_seg)
+    start = torch.cumsum(cnt, 0) - cnt
+    has = cnt > 0
+    k = torch.clamp(torch.ceil(q * cnt.double() - 1e-12).long() - 1, min=0)
+    k = torch.minimum(k, (cnt - 1).clamp_min(0))
+    idx = (start + k)[has]
+    out[has] = val_sorted[idx]
+    return out
+
+
+class GradientBoostingFamily(Family):
+    model_types = (_CLS, _REG)
+    classifiers = (_CLS,)
+
+    def __init__(self):
+        self.tiers = forest_ops.ForestTiers()
+
+    def resolve(self, model_type, params, n_train, n_features, n_classes) -> Dict[str, Any]:
+        p = dict(_DEFAULTS)
+        p.update({k: v for k, v in params.items() if k in _DEFAULTS})
+        is_cls = model_type == _CLS
+        warn: List[str] = []
+        unknown = sorted(k for k in params if k not in _DEFAULTS)
+        if unknown:
+            warn.append(f"ignored unknown parameters {unknown}")
+        loss_name = p["loss"] or ("log_loss" if is_cls else "squared_error")
+        table = _CLS_LOSSES if is_cls else _REG_LOSSES
+        if loss_name not in table:
+            raise ParamError(f"loss {loss_name!r} invalid for {model_type}")
+        loss = table[loss_name]
+        if loss == LOSS_EXP and n_classes > 2:
+            raise ParamError(f"ExponentialLoss requires 2 classes; got {n_classes} class(es).")
+        if p["criterion"] not in ("friedman_mse", "squared_error"):
+            raise ParamError(f"criterion {p['criterion']!r} invalid")
+        lr = as_float(p["learning_rate"], "learning_rate", lo=0.0)
+        sub = as_float(p["subsample"], "subsample", lo=0.0, hi=1.0)
+        if sub <= 0:
+            raise ParamError("subsample must be in (0, 1]")
+        init = p["init"]
+        if init not in (None, "zero", "None"):
+            raise ParamError("init must be None or 'zero' (custom init estimators are not supported)")
+        if p["n_iter_no_change"] is not None:
+            warn.append("n_iter_no_change early stopping not supported; all n_estimators stages fitted")
+        if p["max_leaf_nodes"] not in (None, "None"):
+            warn.append("max_leaf_nodes not supported; ignored")
+        if as_float(p["ccp_alpha"], "ccp_alpha", lo=0.0) > 0:
+            warn.append("ccp_alpha pruning not supported; ignored")
+        if as_float(p["min_weight_fraction_leaf"], "min_weight_fraction_leaf", lo=0.0, hi=0.5) > 0:
+            warn.append("min_weight_fraction_leaf not supported; ignored")
+        alpha = as_float(p["alpha"], "alpha", lo=0.0, hi=1.0)
+        if loss in (LOSS_HUBER, LOSS_QUANT) and not 0.0 < alpha < 1.0:
+            raise ParamError("alpha must be in (0, 1)")
+        md = as_int(p["max_depth"], "max_depth", lo=1, allow_none=True)
+        return {
+            "loss": loss, "learning_rate": lr, "n_estimators": as_int(p["n_estimators"], "n_estimators", lo=1,
+                                                                      hi=100000),
+            "subsample": sub, "max_depth": md if md is not None else forest_ops.INT32_MAX,
+            "min_samples_split": _count_param(p["min_samples_split"], n_train, "min_samples_split", 2),
+            "min_samples_leaf": _count_param(p["min_samples_leaf"], n_train, "min_samples_leaf", 1),
+            "min_impurity_decrease": as_float(p["min_impurity_decrease"], "min_impurity_decrease", lo=0.0),
+            "max_features": _max_features(p["max_features"], n_features), "alpha": alpha,
+            "init_zero": init == "zero", "seed": seed_of(p["random_state"]), "warnings": warn,
+        }
+
+    def cost(self, model_type, rp, n_train, n_features, n_classes) -> float:
+        K = n_classes if n_classes > 2 else 1
+        depth = min(rp["max_depth"], 12)
+        return rp["n_estimators"] * K * n_train * rp["subsample"] * depth * rp["max_features"] * 2e-9 + 1e-2
+
+    def run(self, data, tasks: List[FitTask], keep_models: bool = False) -> List[FitOutput]:
+        if not tasks:
+            return []
+        K = data.n_classes if (data.classification and data.n_classes > 2) else 1
+        per_fit = K * data.n * (8 + 4 + 4 + 1) * 1.5
+        budget = 0.4 * torch.cuda.mem_get_info(data.device)[0] if data.is_gpu else 4e9
+        cap = max(1, int(budget // max(1.0, per_fit)))
+        outs: List[FitOutput] = []
+        for i in range(0, len(tasks), cap):
+            outs.extend(self._boost(data, tasks[i:i + cap], K, keep_models))
+        return outs
+
+    # ------------------------------------------------------------------------------------
+    def _init_raw(self, data, t: FitTask, train: torch.Tensor, K: int) -> torch.Tensor:
+        rp = t.params
+        out = torch.zeros(K, dtype=torch.float64, device=data.device)
+        if rp["init_zero"]:
+            return out
+        loss = rp["loss"]
+        if loss in (LOSS_LOG, LOSS_EXP):
+            yc = data.y_cls[train].long()
+            if K == 1:
+                p = float((yc == 1).double().mean().clamp(_F32_EPS, 1 - _F32_EPS))
+                logit = math.log(p / (1 - p))
+                out[0] = logit if loss == LOSS_LOG else 0.5 * logit
+            else:
+                pr = torch.bincount(yc, minlength=K).double() / max(1, yc.numel())
+                lp = pr.clamp(_F32_EPS, 1 - _F32_EPS).log()
+                out[:] = lp - lp.mean()
+            return out
+        y = data.y_reg[train].double()
+        if loss == LOSS_SQ:
+            out[0] = y.mean()
+        elif loss in (LOSS_ABS, LOSS_HUBER):
+            out[0] = _percentile_linear(y, 0.5)
+        else:
+            out[0] = _percentile_linear(y, rp["alpha"])
+        return out
+
+    def _boost(self, data, batch: List[FitTask], K: int, keep_models: bool) -> List[FitOutput]:
+        t0 = time.perf_counter()
+        dev, n, gpu = data.device, data.n, data.is_gpu
+        F = len(batch)
+        Xb = data.binned()
+        Xb_host = None if gpu else Xb.numpy()
+        split_idx = torch.tensor([t.split for t in batch], device=dev)
+        train = data.roles[split_idx] == 1                                  # [F, n]
+        clf = data.classification
+        if clf:
+            ycls = data.y_cls.long()
+            Y = torch.nn.functional.one_hot(ycls, max(2, data.n_classes)).double().t()   # [C, n]
+            ybin = Y[1]
+        else:
+            yreg = data.y_reg.double()
+        raw = torch.stack([self._init_raw(data, t, train[f], K) for f, t in enumerate(batch)])   # [F, K]
+        init = raw.clone()
+        raw = raw[:, :, None].repeat(1, 1, n).contiguous()                 # [F, K, n]
+        lr = torch.tensor([t.params["learning_rate"] for t in batch], dtype=torch.float64, device=dev)
+        n_est = [t.params["n_estimators"] for t in batch]
+        seeds = [t.params["seed"] if t.params["seed"] is not None else t.seed for t in batch]
+        gens = [torch.Generator(device="cpu").manual_seed(int(s) & 0x7FFFFFFF) for s in seeds]
+        kept: List[List[Any]] = [[] for _ in range(F)]
+        train_idx = [torch.nonzero(train[f]).squeeze(1) for f in range(F)]
+        for stage in range(max(n_est)):
+            act = [f for f in range(F) if stage < n_est[f]]
+            A = len(act)
+            act_t = torch.tensor(act, device=dev)
+            R = raw[act_t]                                                 # [A, K, n]
+            loss = [batch[f].params["loss"] for f in act]
+            # --- negative gradient (pseudo-residuals) ------------------------------------
+            G = torch.empty_like(R)
+            hub_delta: Dict[int, float] = {}
+            for a, f in enumerate(act):
+                G[a], hub_delta[f] = self._neg_grad(batch[f].params, R[a], Y if clf else None,
+                                                    ybin if clf else None, None if clf else yreg, K, train[f])
+            # --- in-bag rows: the split's train rows, or a per-stage subsample of them ---
+            inbag = train[act_t]
+            sub_rows = []
+            for a, f in enumerate(act):
+                sub = batch[f].params["subsample"]
+                if sub < 1.0:
+                    tr = train_idx[f]
+                    m = max(1, int(sub * tr.numel()))
+                    pick = torch.randperm(tr.numel(), generator=gens[f])[:m].to(dev)
+                    row = torch.zeros(n, dtype=torch.bool, device=dev)
+                    row[tr[pick]] = True
+                    inbag[a] = row
+                    sub_rows.append(a)
+            # one role row per tree (roles = in-bag mask of its fit)
+            J = A * K
+            roles_t = inbag.repeat_interleave(K, dim=0).to(torch.uint8).contiguous()   # [J, n]
+            tgt = G.reshape(J, n).float().contiguous()
+            specs = forest_ops.make_specs(J)
+            for a, f in enumerate(act):
+                rp = batch[f].params
+                for k in range(K):
+                    j = a * K + k
+                    specs[j]["seed"] = native_seed(seeds[f], stage * K + k)
+                    specs[j]["split"] = j
+                    specs[j]["fit"] = j
+                    specs[j]["target"] = j
+                    specs[j]["max_depth"] = rp["max_depth"]
+                    specs[j]["min_samples_split"] = rp["min_samples_split"]
+                    specs[j]["min_samples_leaf"] = rp["min_samples_leaf"]
+                    specs[j]["max_features"] = rp["max_features"]
+                    specs[j]["bootstrap"] = 0
+                    specs[j]["criterion"] = forest_ops.MSE
+                    specs[j]["min_impurity_decrease"] = rp["min_impurity_decrease"]
+            if gpu:
+                fb = forest_ops.build_gpu(Xb, None, tgt, roles_t, specs, 1, True, self.tiers, ystride=n)
+                leaf = forest_ops.apply(fb, Xb).long()                     # [J, n]
+                vals = fb.vals
+            else:
+                fb = forest_ops.build_cpu(Xb_host, None, tgt.numpy(), roles_t.numpy(), specs, 1, True, ystride=n)
+                leaf = torch.from_numpy(forest_ops.apply(fb, Xb_host)).long()
+                vals = torch.from_numpy(fb.vals)
+            P = vals.shape[0]
+            # --- leaf values (line search) -----------------------------------------------
+            value = vals[:, 1] / vals[:, 0].clamp_min(1e-300)             # squared error: node mean
+            value = torch.where(vals[:, 0] > 0, value, torch.zeros_like(value))
+            m = roles_t.bool()
+            lf = leaf[m]
+            needs = {l for l in loss if l != LOSS_SQ}
+            if needs:
+                value = value.clone()
+                tree_of = torch.arange(J, device=dev).view(J, 1).expand(J, n)[m]
+                fit_of_tree = torch.tensor([act[j // K] for j in range(J)], device=dev)
+                loss_of_tree = torch.tensor([loss[j // K] for j in range(J)], device=dev)
+                g = G.reshape(J, n)[m]
+                node_loss = torch.full((P,), -1, dtype=torch.long, device=dev)
+                node_loss.scatter_(0, lf, loss_of_tree[tree_of])
+                if LOSS_LOG in needs or LOSS_EXP in needs:
+                    num = torch.zeros(P, dtype=torch.float64, device=dev).index_add_(0, lf, g)
+                    if K > 1:
+                        yk = Y[torch.arange(J, device=dev) % K].reshape(J, n)[m]
+                        prob = yk - g
+                        hess = prob * (1 - prob)
+                        num = num * (K - 1) / K
+                    else:
+                        yb = ybin.view(1, n).expand(J, n)[m]
+                        prob = yb - g
+                        hess_log = prob * (1 - prob)
+                        hess_exp = torch.where(yb > 0.5, g, -g)
+                        is_exp = loss_of_tree[tree_of] == LOSS_EXP
+                        hess = torch.where(is_exp, hess_exp, hess_log)
+                    den = torch.zeros(P, dtype=torch.float64, device=dev).index_add_(0, lf, hess)
+                    newton = torch.where(den.abs() < 1e-150, torch.where(num == 0, 0.0, torch.sign(num) * 1e150),
+                                         num / torch.where(den.abs() < 1e-150, torch.ones_like(den), den))
+                    sel = (node_loss == LOSS_LOG) | (node_loss == LOSS_EXP)
+                    value = torch.where(sel, newton, value)
+                if needs & {LOSS_ABS, LOSS_HUBER, LOSS_QUANT}:
+                    resid = (yreg.view(1, n) - R.reshape(J, n))[m]        # y - raw (K == 1 for regression)
+                    for lk in needs & {LOSS_ABS, LOSS_HUBER, LOSS_QUANT}:
+                        sel_rows = loss_of_tree[tree_of] == lk
+                        if lk == LOSS_QUANT:
+                            # per-tree alpha: group trees by alpha
+                            for alpha in sorted({batch[act[j // K]].params["alpha"] for j in range(J)
+                                                 if loss[j // K] == lk}):
+                                trees = torch.tensor([j for j in range(J) if loss[j // K] == lk and
+                                                      batch[act[j // K]].params["alpha"] == alpha], device=dev)
+                                rs = sel_rows & torch.isin(tree_of, trees)
+                                pv = _segment_percentile(lf[rs], resid[rs], P, alpha)
+                                value = torch.where(~torch.isnan(pv), pv, value)
+                            continue
+                        med = _segment_percentile(lf[sel_rows], resid[sel_rows], P, 0.5)
+                        if lk == LOSS_ABS:
+                            value = torch.where(~torch.isnan(med), med, value)
+                        else:
+                            delta = torch.zeros(J, dtype=torch.float64, device=dev)
+                            for j in range(J):
+                                if loss[j // K] == LOSS_HUBER:
+                                    delta[j] = hub_delta[act[j // K]]
+                            diff = resid[sel_rows] - med[lf[sel_rows]]
+                            dl = delta[tree_of[sel_rows]]
+                            term = torch.sign(diff) * torch.minimum(dl, diff.abs())
+                            s_ = torch.zeros(P, dtype=torch.float64, device=dev).index_add_(0, lf[sel_rows], term)
+                            c_ = torch.zeros(P, dtype=torch.float64, device=dev).index_add_(
+                                0, lf[sel_rows], torch.ones_like(term))
+                            hub = med + s_ / c_.clamp_min(1)
+                            value = torch.where(~torch.isnan(med), hub, value)
+            # --- raw-score update of every row (train and held-out) ------------------------
+            upd = value[leaf].view(A, K, n) * lr[act_t].view(A, 1, 1)
+            raw[act_t] += upd
+            if keep_models:
+                vals_np = value.cpu().numpy()
+                nodes_np = fb.nodes.cpu().numpy() if isinstance(fb.nodes, torch.Tensor) else fb.nodes
+                for a, f in enumerate(act):
+                    lr_f = float(lr[f])
+                    kept[f].append([_extract_tree(nodes_np, vals_np * lr_f, a * K + k) for k in range(K)])
+        if gpu:
+            torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        outs = []
+        for f, t in enumerate(batch):
+            rows = data.test_rows[t.split].long()
+            r = raw[f][:, rows]                                            # [K, m]
+            lossf = t.params["loss"]
+            proba = None
+            if not clf:
+                pred = r[0].float()
+            elif K == 1:
+                z = 2 * r[0] if lossf == LOSS_EXP else r[0]
+                p1 = torch.sigmoid(z)
+                proba = torch.stack([1 - p1, p1], 1)
+                pred = (r[0] >= 0).to(torch.int32)
+            else:
+                proba = torch.softmax(r.t(), 1)
+                pred = r.argmax(0).to(torch.int32)
+            o = FitOutput(task_id=t.task_id, pred=pred, proba=proba, fit_seconds=dt / F,
+                          info={"warnings": t.params.get("warnings", [])})
+            if keep_models:
+                o.model = _pack_model(kept[f], init[f].cpu().numpy(), t, data, K)
+            outs.append(o)
+        return outs
+
+    # negative gradient [K, n] of the fit's loss (+ huber delta, else 0)
+    @staticmethod
+    def _neg_grad(rp, r, Y, ybin, yreg, K, train_row):
+        loss = rp["loss"]
+        if loss == LOSS_LOG:
+            if K == 1:
+                return (ybin - torch.sigmoid(r[0])).view(1, -1), 0.0
+            return Y[:K] - torch.softmax(r, 0), 0.0
+        if loss == LOSS_EXP:
+            return (ybin * torch.exp(-r[0]) - (1 - ybin) * torch.exp(r[0])).view(1, -1), 0.0
+        diff = yreg - r[0]
+        if loss == LOSS_SQ:
+            return diff.view(1, -1), 0.0
+        if loss == LOSS_ABS:
+            return torch.sign(diff).view(1, -1), 0.0
+        if loss == LOSS_QUANT:
+            a = rp["alpha"]
+            return torch.where(diff >= 0, torch.full_like(diff, a), torch.full_like(diff, a - 1)).view(1, -1), 0.0
+        # huber: delta = alpha-percentile of |y - raw| over the fit's training rows (set_huber_delta)
+        delta = float(_percentile_icdf(diff[train_row].abs(), rp["alpha"]))
+        return torch.where(diff.abs() <= delta, diff, delta * torch.sign(diff)).view(1, -1), delta
+
+
+def _extract_tree(nodes: np.ndarray, values: np.ndarray, root: int):
+    """Standalone (nodes [m,2], value [m]) of the tree rooted at ``root`` (root first)."""
+    ids = {root: 0}
+    order = [root]
+    out_nodes, out_vals = [], []
+    i = 0
+    while i < len(order):
+        nd = order[i]
+        sp, left = int(nodes[nd, 0]), int(nodes[nd, 1])
+        if sp >= 0:
+            ids[left], ids[left + 1] = len(order), len(order) + 1
+            order.extend([left, left + 1])
+        i += 1
+    for nd in order:
+        sp, left = int(nodes[nd, 0]), int(nodes[nd, 1])
+        out_nodes.append((sp, ids[left] if sp >= 0 else -1))
+        out_vals.append(float(values[nd]))
+    return np.asarray(out_nodes, dtype=np.int32), np.asarray(out_vals, dtype=np.float64)
+
+
+def _pack_model(stages, init: np.ndarray, t: FitTask, data, K: int) -> Dict[str, Any]:
+    nodes, vals, roots = [], [], []
+    off = 0
+    for st in stages:
+        rr = []
+        for nd, vv in st:
+            nd = nd.copy()
+            nd[:, 1] = np.where(nd[:, 1] >= 0, nd[:, 1] + off, -1)
+            nodes.append(nd)
+            vals.append(vv)
+            rr.append(off)
+            off += len(nd)
+        roots.append(rr)
+    return {
+        "kind": "gbrt", "nodes": np.concatenate(nodes) if nodes else np.zeros((0, 2), np.int32),
+        "value": np.concatenate(vals) if vals else np.zeros(0), "roots": np.asarray(roots, dtype=np.int32),
+        "init": init, "K": K, "loss": int(t.params["loss"]), "edges": data.edges.cpu().numpy(),
+        "classes": None if data.classes is None else np.asarray(data.classes).tolist(),
+        "model_type": t.model_type, "params": {k: v for k, v in t.params.items() if k != "warnings"},
+    }
+
+
+def gbrt_raw_numpy(model: Dict[str, Any], X: np.ndarray) -> np.ndarray:
+    lib = native.cpu_lib()
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    edges = np.ascontiguousarray(model["edges"], dtype=np.float32)
+    Xb = np.empty(X.shape, dtype=np.uint8)
+    lib.dml_cpu_bin(native.ptr(X), X.shape[0], X.shape[1], native.ptr(edges), native.ptr(Xb), X.shape[1])
+    nodes, value, roots = model["nodes"], model["value"], np.asarray(model["roots"])
+    K = int(model["K"])
+    raw = np.tile(np.asarray(model["init"], dtype=np.float64), (X.shape[0], 1))
+    rows = np.arange(X.shape[0])
+    for s in range(roots.shape[0]):
+        for k in range(K):
+            node = np.full(X.shape[0], roots[s, k], dtype=np.int64)
+            while True:
+                sp = nodes[node, 0]
+                inner = sp >= 0
+                if not inner.any():
+                    break
+                feat, b = np.where(inner, sp >> 8, 0), np.where(inner, sp & 255, 0)
+                go = Xb[rows, feat] > b
+                node = np.where(inner, nodes[node, 1] + go, node)
+            raw[:, k] += value[node]
+    return raw
+
+
+def gbrt_predict_numpy(model: Dict[str, Any], X: np.ndarray) -> np.ndarray:
+    raw = gbrt_raw_numpy(model, X)
+    if model.get("classes") is None:
+        return raw[:, 0]
+    idx = (raw[:, 0] >= 0).astype(int) if raw.shape[1] == 1 else raw.argmax(1)
+    return np.asarray(model["classes"])[idx]
+
+
+register(GradientBoostingFamily())

@@ -1,1 +1,234 @@
-"""Placeholder: family registered later in the build."""
+"""KNeighborsClassifier / KNeighborsRegressor — one neighbour search per job, not per fit.
+
+Reference: both are whitelisted (aws-prod/worker/worker.py:42,49) and sklearn fits /
+predicts them once per (candidate, fold): a KD/ball tree build plus a query pass each
+time (sklearn ``neighbors/_kd_tree``, ``_ball_tree``, ``_pairwise_distances_reduction``).
+
+Here a KNN "fit" is only the choice of training rows (a role row of the split tensor),
+so for every metric the job uses ONE exact brute-force pass (HIP kernel ``dml_knn``,
+csrc/kernels/neighbors.hip; torch on CPU) finds the ``K_max`` nearest training rows of
+every test row of every split; each candidate (n_neighbors, weights) then votes from a
+prefix of those lists.  Neighbour search is exact, so predictions match sklearn's
+brute/kd/ball algorithms except where equal distances make the k-th neighbour
+ambiguous (ties resolved by lower row index here; parity unpinned for exact ties).
+``algorithm`` / ``leaf_size`` only pick sklearn's search structure and are accepted
+and ignored.
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Any, Dict, List, Tuple
+
+import numpy as np
+import torch
+
+from ..utils import native
+from .base import Family, FitOutput, FitTask, ParamError, as_int, as_float, register
+
+_DEFAULTS = {"n_neighbors": 5, "weights": "uniform", "algorithm": "auto", "leaf_size": 30, "p": 2,
+             "metric": "minkowski", "metric_params": None, "n_jobs": None}
+M_L2, M_L1, M_LINF, M_P = 0, 1, 2, 3
+KERNEL_KMAX = 64
+
+_METRICS = {"euclidean": (M_L2, 2.0), "l2": (M_L2, 2.0), "manhattan": (M_L1, 1.0), "cityblock": (M_L1, 1.0),
+            "l1": (M_L1, 1.0), "chebyshev": (M_LINF, math.inf), "infinity": (M_LINF, math.inf)}
+
+
+def metric_code(metric: str, p) -> Tuple[int, float]:
+    metric = str(metric).lower()
+    if metric == "minkowski":
+        p = as_float(p, "p", lo=0.0)
+        if p < 1:
+            raise ParamError("p must be >= 1 for the minkowski metric")
+        if p == 1:
+            return M_L1, 1.0
+        if p == 2:
+            return M_L2, 2.0
+        if math.isinf(p):
+            return M_LINF, math.inf
+        return M_P, p
+    if metric in _METRICS:
+        return _METRICS[metric]
+    raise ParamError(f"metric {metric!r} is not supported (minkowski/euclidean/manhattan/chebyshev)")
+
+
+def finish_distance(acc: torch.Tensor, metric: int, p: float) -> torch.Tensor:
+    """Kernel accumulators -> true distances (sqrt / p-th root)."""
+    if metric == M_L2:
+        return acc.clamp_min(0).sqrt()
+    if metric == M_P:
+        return acc.clamp_min(0).pow(1.0 / p)
+    return acc
+
+
+def _acc_torch(Q: torch.Tensor, R: torch.Tensor, metric: int, p: float) -> torch.Tensor:
+    """Accumulator-space distances [q, r] (same quantity the kernel ranks by)."""
+    diff = (Q[:, None, :] - R[None, :, :]).abs()
+    if metric == M_L2:
+        return (diff * diff).sum(2)
+    if metric == M_L1:
+        return diff.sum(2)
+    if metric == M_LINF:
+        return diff.amax(2)
+    return diff.pow(p).sum(2)
+
+
+def knn_search_torch(X: torch.Tensor, qrows: torch.Tensor, train_rows: torch.Tensor, K: int, metric: int, p: float):
+    """(acc distances [q, K], global row ids [q, K]) — ties broken by lower row id."""
+    out_d, out_i = [], []
+    R = X[train_rows.long()]
+    nr = R.shape[0]
+    K = min(K, nr)
+    step = max(1, (1 << 24) // max(1, nr * max(1, X.shape[1] // 8)))
+    for s in range(0, qrows.numel(), step):
+        Q = X[qrows[s:s + step].long()]
+        D = _acc_torch(Q, R, metric, p)
+        # stable sort over ascending row ids == (distance, row) order
+        Ds, idx = torch.sort(D, dim=1, stable=True)
+        out_d.append(Ds[:, :K])
+        out_i.append(train_rows.long()[idx[:, :K]])
+    if not out_d:
+        return (torch.empty((0, K), dtype=X.dtype, device=X.device),
+                torch.empty((0, K), dtype=torch.long, device=X.device))
+    return torch.cat(out_d), torch.cat(out_i)
+
+
+def knn_search_hip(data, splits: List[int], K: int, metric: int, p: float) -> Dict[int, Tuple[torch.Tensor, torch.Tensor]]:
+    """One kernel launch for all test rows of all ``splits``."""
+    lib = native.hip_lib()
+    qpw = int(lib.dml_knn_qpw())
+    dev = data.device
+    qr, qs, spans = [], [], {}
+    off = 0
+    for s in splits:
+        rows = data.test_rows[s].long()
+        m = rows.numel()
+        pad = (-m) % qpw
+        qr.append(torch.cat([rows, torch.full((pad,), -1, dtype=torch.long, device=dev)]))
+        qs.append(torch.full((m + pad,), s, dtype=torch.long, device=dev))
+        spans[s] = (off, m)
+        off += m + pad
+    qrow = torch.cat(qr).to(torch.int32).contiguous()
+    qsplit = torch.cat(qs).to(torch.int32).contiguous()
+    groups = qrow.numel() // qpw
+    out_d = torch.empty((qrow.numel(), K), dtype=torch.float32, device=dev)
+    out_i = torch.empty((qrow.numel(), K), dtype=torch.int32, device=dev)
+    XT = data.feature_major()
+    rc = lib.dml_knn(native.ptr(data.X), native.ptr(XT), data.n, data.d, native.ptr(data.roles), native.ptr(qrow),
+                     native.ptr(qsplit), groups, metric, float(p if math.isfinite(p) else 0.0), K, native.ptr(out_d),
+                     native.ptr(out_i), native.stream_handle(dev))
+    if rc:
+        raise RuntimeError(f"dml_knn failed (rc={rc})")
+    return {s: (out_d[o:o + m], out_i[o:o + m].long()) for s, (o, m) in spans.items()}
+
+
+def vote(dist: torch.Tensor, nb_y: torch.Tensor, k: int, weights: str, n_classes: int, classification: bool):
+    """Prediction from the first ``k`` neighbours (sklearn's uniform / distance rules)."""
+    d = dist[:, :k].double()
+    y = nb_y[:, :k]
+    if weights == "distance":
+        w = 1.0 / d                                      # 0-distance -> inf
+        inf = torch.isinf(w)
+        row_inf = inf.any(1, keepdim=True)
+        w = torch.where(row_inf, inf.double(), w)
+    else:
+        w = torch.ones_like(d)
+    if classification:
+        scores = torch.zeros((d.shape[0], n_classes), dtype=torch.float64, device=d.device)
+        scores.scatter_add_(1, y.long(), w)
+        pred = scores.argmax(1).to(torch.int32)          # first max = smallest class (sklearn mode)
+        proba = scores / scores.sum(1, keepdim=True).clamp_min(1e-300)
+        return pred, proba
+    yv = y.double()
+    return ((w * yv).sum(1) / w.sum(1)).float(), None
+
+
+class KNeighborsFamily(Family):
+    model_types = ("KNeighborsClassifier", "KNeighborsRegressor")
+    classifiers = ("KNeighborsClassifier",)
+
+    def resolve(self, model_type, params, n_train, n_features, n_classes):
+        p = dict(_DEFAULTS)
+        p.update({k: v for k, v in params.items() if k in _DEFAULTS})
+        warn = []
+        unknown = sorted(k for k in params if k not in _DEFAULTS)
+        if unknown:
+            warn.append(f"ignored unknown parameters {unknown}")
+        k = as_int(p["n_neighbors"], "n_neighbors", lo=1)
+        weights = p["weights"] if p["weights"] is not None else "uniform"
+        if weights not in ("uniform", "distance"):
+            raise ParamError("weights not recognized: should be 'uniform', 'distance'")
+        if p["algorithm"] not in ("auto", "ball_tree", "kd_tree", "brute"):
+            raise ParamError(f"algorithm {p['algorithm']!r} invalid")
+        as_int(p["leaf_size"], "leaf_size", lo=1)
+        if p["metric_params"]:
+            raise ParamError("metric_params is not supported")
+        metric, pp = metric_code(p["metric"], p["p"])
+        return {"n_neighbors": k, "weights": weights, "metric": metric, "p": pp, "warnings": warn}
+
+    def cost(self, model_type, rp, n_train, n_features, n_classes) -> float:
+        # one search per job is shared by every candidate; price a candidate at a share
+        return n_train * max(1.0, n_train / 4) * max(1, n_features) * 2e-13 + 1e-3
+
+    def run(self, data, tasks: List[FitTask], keep_models: bool = False) -> List[FitOutput]:
+        if not tasks:
+            return []
+        t0 = time.perf_counter()
+        clf = data.classification
+        y = data.y_cls if clf else data.y_reg
+        outs: Dict[int, FitOutput] = {}
+        groups: Dict[Tuple[int, float], List[FitTask]] = {}
+        for t in tasks:
+            groups.setdefault((t.params["metric"], t.params["p"]), []).append(t)
+        for (metric, p), ts in groups.items():
+            splits = sorted({t.split for t in ts})
+            for t in ts:
+                if t.params["n_neighbors"] > data.train_counts[t.split]:
+                    outs[t.task_id] = FitOutput(task_id=t.task_id, error=(
+                        f"Expected n_neighbors <= n_samples_fit, but n_neighbors = {t.params['n_neighbors']}, "
+                        f"n_samples_fit = {data.train_counts[t.split]}"))
+            ok = [t for t in ts if t.task_id not in outs]
+            if not ok:
+                continue
+            kmax = max(t.params["n_neighbors"] for t in ok)
+            if data.is_gpu and kmax <= KERNEL_KMAX:
+                nb = knn_search_hip(data, splits, kmax, metric, p)
+            else:
+                nb = {s: knn_search_torch(data.X, data.test_rows[s], data.train_rows[s], kmax, metric, p)
+                      for s in splits}
+            for t in ok:
+                acc, idx = nb[t.split]
+                dist = finish_distance(acc, metric, p)
+                pred, proba = vote(dist, y[idx], t.params["n_neighbors"], t.params["weights"], data.n_classes, clf)
+                o = FitOutput(task_id=t.task_id, pred=pred, proba=proba, info={"warnings": t.params["warnings"]})
+                if keep_models:
+                    tr = data.train_rows[t.split].long()
+                    o.model = {"kind": "knn", "X": data.X[tr].cpu().numpy(), "y": y[tr].cpu().numpy(),
+                               "classes": None if not clf else np.asarray(data.classes).tolist(),
+                               "n_neighbors": t.params["n_neighbors"], "weights": t.params["weights"],
+                               "metric": metric, "p": p, "model_type": t.model_type, "n_classes": data.n_classes}
+                outs[t.task_id] = o
+        data.sync()
+        dt = time.perf_counter() - t0
+        for o in outs.values():
+            o.fit_seconds = dt / max(1, len(outs))
+        return [outs[t.task_id] for t in tasks]
+
+
+def knn_predict_numpy(model: Dict[str, Any], X: np.ndarray) -> np.ndarray:
+    """Host prediction for a saved KNN artefact (the artefact stores its training rows)."""
+    Xtr = torch.from_numpy(np.asarray(model["X"], dtype=np.float32))
+    ytr = torch.from_numpy(np.asarray(model["y"]))
+    Q = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32))
+    allX = torch.cat([Xtr, Q])
+    n = Xtr.shape[0]
+    metric, p, k = int(model["metric"]), float(model["p"]), int(model["n_neighbors"])
+    acc, idx = knn_search_torch(allX, torch.arange(n, n + Q.shape[0]), torch.arange(n), k, metric, p)
+    clf = model.get("classes") is not None
+    pred, _ = vote(finish_distance(acc, metric, p), ytr[idx], k, model["weights"], int(model.get("n_classes", 1)), clf)
+    pred = pred.numpy()
+    return np.asarray(model["classes"])[pred] if clf else pred
+
+
+register(KNeighborsFamily())

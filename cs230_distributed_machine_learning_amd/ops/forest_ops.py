@@ -94,7 +94,10 @@ def _pool_bound(counts: np.ndarray, specs: np.ndarray) -> int:
 
 
 def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,
-              specs: np.ndarray, n_classes: int, is_reg: bool, tiers: ForestTiers | None = None) -> ForestBuild:
+              specs: np.ndarray, n_classes: int, is_reg: bool, tiers: ForestTiers | None = None,
+              ystride: int = 0) -> ForestBuild:
+    """``ystride > 0``: ``yreg`` is a [targets, ystride] matrix and tree t regresses on
+    row ``specs[t]['target']`` (gradient boosting's per-fit pseudo-residuals)."""
     lib = native.hip_lib()
     dev = Xb.device
     T = len(specs)
@@ -112,6 +115,7 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     a.n_classes, a.is_reg = (n_classes if not is_reg else 1), int(is_reg)
     a.roles, a.n_splits = native.ptr(roles), roles.shape[0]
     a.specs, a.T = native.ptr(specs_dev), T
+    a.ystride = int(ystride)
     a.active_count = native.ptr(active)
     t0 = time.perf_counter()
     rc = lib.dml_forest_count(ctypes.byref(a), stream)
@@ -159,7 +163,7 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
 
 
 def build_cpu(Xb: np.ndarray, ycls: Optional[np.ndarray], yreg: Optional[np.ndarray], roles: np.ndarray,
-              specs: np.ndarray, n_classes: int, is_reg: bool) -> ForestBuild:
+              specs: np.ndarray, n_classes: int, is_reg: bool, ystride: int = 0) -> ForestBuild:
     lib = native.cpu_lib()
     Xb = np.ascontiguousarray(Xb, dtype=np.uint8)
     roles = np.ascontiguousarray(roles, dtype=np.uint8)
@@ -171,7 +175,8 @@ def build_cpu(Xb: np.ndarray, ycls: Optional[np.ndarray], yreg: Optional[np.ndar
     VC = 3 if is_reg else n_classes
     t0 = time.perf_counter()
     h = lib.dml_cpu_forest_build(native.ptr(Xb), d, n, d, native.ptr(ycls), native.ptr(yreg),
-                                 (1 if is_reg else n_classes), int(is_reg), native.ptr(roles), native.ptr(specs), T)
+                                 (1 if is_reg else n_classes), int(is_reg), native.ptr(roles), native.ptr(specs), T,
+                                 int(ystride))
     try:
         P = lib.dml_cpu_forest_num_nodes(h)
         nodes = np.empty((P, 2), dtype=np.int32)
@@ -180,6 +185,24 @@ def build_cpu(Xb: np.ndarray, ycls: Optional[np.ndarray], yreg: Optional[np.ndar
     finally:
         lib.dml_cpu_forest_free(h)
     return ForestBuild(nodes, vals, T, VC, is_reg, n_classes, {"nodes": int(P), "build_s": time.perf_counter() - t0})
+
+
+def apply(fb: ForestBuild, Xb, t0: int = 0, T: Optional[int] = None):
+    """Leaf node index of every row for trees t0..t0+T-1: int32 [T, n]."""
+    T = fb.n_trees - t0 if T is None else T
+    n = Xb.shape[0]
+    if fb.on_gpu:
+        leaf = torch.empty((T, n), dtype=torch.int32, device=Xb.device)
+        rc = native.hip_lib().dml_forest_apply(native.ptr(Xb), Xb.stride(0), n, native.ptr(fb.nodes), t0, T,
+                                               native.ptr(leaf), native.stream_handle(Xb.device))
+        if rc:
+            raise RuntimeError("dml_forest_apply failed")
+        return leaf
+    Xb = np.ascontiguousarray(Xb)
+    nodes = np.ascontiguousarray(fb.nodes, dtype=np.int32)
+    leaf = np.empty((T, n), dtype=np.int32)
+    native.cpu_lib().dml_cpu_forest_apply(native.ptr(Xb), Xb.shape[1], n, native.ptr(nodes), t0, T, native.ptr(leaf))
+    return leaf
 
 
 def predict(fb: ForestBuild, Xb, fit_tree_off: np.ndarray, fit_row_off: np.ndarray, rows, want_proba: bool = False):

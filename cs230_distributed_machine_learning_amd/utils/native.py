@@ -40,7 +40,7 @@ TREESPEC_DTYPE = np.dtype(
         ("bootstrap", "<i4"),
         ("criterion", "<i4"),
         ("min_impurity_decrease", "<f4"),
-        ("pad0", "<f4"),
+        ("target", "<i4"),
         ("pois_cdf", "<u4", (POIS_TABLE,)),
     ]
 )
@@ -66,6 +66,7 @@ ForestArgs = _i64_struct(
         "sub_max", "sub_cache_d",
         "n_nodes_out", "status_out", "levels_out", "large_rounds_out",
         "tier0_nodes", "tier1_nodes", "tier2_nodes", "tier3_nodes",
+        "ystride",
     ],
 )
 
@@ -95,7 +96,9 @@ def cpu_lib() -> ctypes.CDLL:
             if lib.dml_cpu_sizeof_treespec() != TREESPEC_DTYPE.itemsize:
                 raise RuntimeError("TreeSpec layout mismatch between C++ and Python")
             lib.dml_cpu_forest_build.restype = c_vp
-            lib.dml_cpu_forest_build.argtypes = [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64]
+            lib.dml_cpu_forest_build.argtypes = [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64,
+                                                 c_i64]
+            lib.dml_cpu_forest_apply.argtypes = [c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp]
             lib.dml_cpu_forest_num_nodes.restype = c_i64
             lib.dml_cpu_forest_num_nodes.argtypes = [c_vp]
             lib.dml_cpu_forest_export.argtypes = [c_vp, c_vp, c_vp]
@@ -158,6 +161,10 @@ def _register_optional(lib) -> None:
         "dml_lr_link_grad": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                      c_vp]),
         "dml_lr_predict": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+        "dml_knn": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, ctypes.c_float, c_i32, c_vp,
+                            c_vp, c_vp]),
+        "dml_knn_qpw": (c_i32, []),
+        "dml_forest_apply": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp]),
     }
     for name, (res, args) in table.items():
         fn = getattr(lib, name, None)

@@ -1,0 +1,137 @@
+"""Estimator families on CPU vs scikit-learn (reference whitelist worker.py:36-57)."""
+import numpy as np
+import pytest
+
+from cs230_distributed_machine_learning_amd.data.device import DeviceData
+from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
+from cs230_distributed_machine_learning_amd.models.base import FitTask, family_of
+from cs230_distributed_machine_learning_amd.search.grid import ParameterGrid
+
+sk = pytest.importorskip("sklearn")
+from sklearn.datasets import load_iris, make_classification, make_regression  # noqa: E402
+from sklearn.model_selection import GridSearchCV  # noqa: E402
+
+
+def _ours(model, X, y, clf, grid, cv=5):
+    dd = DeviceData(X, y, clf, "cpu")
+    cands = list(ParameterGrid(grid))
+    res = run_candidates(dd, JobSpec(model, cands, cv=cv), range(len(cands)))
+    assert all(r.ok for r in res), [r.error for r in res if not r.ok]
+    return np.array([r.result["mean_cv_score"] for r in res])
+
+
+def _ref(est, X, y, grid, cv=5):
+    return GridSearchCV(est, grid, cv=cv).fit(X, y).cv_results_["mean_test_score"]
+
+
+def test_knn_classifier_matches_sklearn():
+    from sklearn.neighbors import KNeighborsClassifier
+
+    X, y = make_classification(600, 8, n_informative=5, n_classes=3, random_state=0)
+    grid = {"n_neighbors": [1, 3, 7, 15], "weights": ["uniform", "distance"], "p": [1, 2, 3]}
+    np.testing.assert_allclose(_ours("KNeighborsClassifier", X, y, True, grid),
+                               _ref(KNeighborsClassifier(), X, y, grid), atol=1e-12)
+
+
+def test_knn_regressor_matches_sklearn():
+    from sklearn.neighbors import KNeighborsRegressor
+
+    X, y = make_regression(500, 6, noise=5, random_state=1)
+    grid = {"n_neighbors": [2, 5, 9], "weights": ["uniform", "distance"], "metric": ["euclidean", "manhattan",
+                                                                                      "chebyshev"]}
+    np.testing.assert_allclose(_ours("KNeighborsRegressor", X, y, False, grid),
+                               _ref(KNeighborsRegressor(), X, y, grid), atol=1e-6)
+
+
+def test_knn_too_many_neighbors_is_a_failed_candidate():
+    X, y = load_iris(return_X_y=True)
+    dd = DeviceData(X, y, True, "cpu")
+    res = run_candidates(dd, JobSpec("KNeighborsClassifier", [{"n_neighbors": 500}, {"n_neighbors": 3}], cv=5),
+                         [0, 1])
+    assert not res[0].ok and "n_neighbors" in res[0].error
+    assert res[1].ok
+
+
+@pytest.mark.parametrize("loss,n_classes", [("log_loss", 2), ("exponential", 2), ("log_loss", 3)])
+def test_gbrt_classifier_full_fit_matches_sklearn(loss, n_classes):
+    """With every feature exactly binned, a GBRT fit reproduces sklearn's raw scores."""
+    from sklearn.ensemble import GradientBoostingClassifier
+
+    from cs230_distributed_machine_learning_amd.models.boosting import gbrt_raw_numpy
+
+    X, y = make_classification(300, 5, n_informative=4, n_redundant=0, n_classes=n_classes, random_state=3)
+    X = np.round(X, 1)
+    params = {"n_estimators": 8, "loss": loss, "max_depth": 2, "learning_rate": 0.3}
+    ref = GradientBoostingClassifier(random_state=0, **params).fit(X, y).decision_function(X)
+    dd = DeviceData(X, y, True, "cpu")
+    dd.set_splits(np.ones((1, len(y)), np.uint8), ["full"])
+    fam = family_of("GradientBoostingClassifier")
+    rp = fam.resolve("GradientBoostingClassifier", params, len(y), X.shape[1], n_classes)
+    out = fam.run(dd, [FitTask(0, 0, 0, "GradientBoostingClassifier", rp)], keep_models=True)[0]
+    raw = gbrt_raw_numpy(out.model, X)
+    raw = raw[:, 0] if ref.ndim == 1 else raw
+    np.testing.assert_allclose(raw, ref, atol=1e-9)
+
+
+@pytest.mark.parametrize("loss", ["squared_error", "absolute_error", "huber", "quantile"])
+def test_gbrt_regressor_full_fit_matches_sklearn(loss):
+    from sklearn.ensemble import GradientBoostingRegressor
+
+    from cs230_distributed_machine_learning_amd.models.boosting import gbrt_raw_numpy
+
+    X, y = make_regression(300, 4, noise=10, random_state=2)
+    X = np.round(X, 1)
+    y = np.round(y, 2)
+    params = {"n_estimators": 6, "loss": loss, "max_depth": 2}
+    ref = GradientBoostingRegressor(random_state=0, **params).fit(X, y).predict(X)
+    dd = DeviceData(X, y, False, "cpu")
+    dd.set_splits(np.ones((1, len(y)), np.uint8), ["full"])
+    fam = family_of("GradientBoostingRegressor")
+    rp = fam.resolve("GradientBoostingRegressor", params, len(y), X.shape[1], 1)
+    out = fam.run(dd, [FitTask(0, 0, 0, "GradientBoostingRegressor", rp)], keep_models=True)[0]
+    np.testing.assert_allclose(gbrt_raw_numpy(out.model, X)[:, 0], ref, rtol=1e-4, atol=1e-3)
+
+
+def test_gbrt_grid_close_to_sklearn():
+    from sklearn.ensemble import GradientBoostingClassifier
+
+    X, y = make_classification(400, 6, n_informative=4, random_state=0)
+    X = np.round(X, 1)
+    grid = {"n_estimators": [20, 50], "learning_rate": [0.1, 0.5]}
+    ours = _ours("GradientBoostingClassifier", X, y, True, grid)
+    ref = _ref(GradientBoostingClassifier(random_state=0), X, y, grid)
+    assert np.abs(ours - ref).max() < 0.03
+
+
+def test_gbrt_subsample_runs():
+    X, y = make_regression(300, 4, noise=10, random_state=2)
+    s = _ours("GradientBoostingRegressor", X, y, False, {"subsample": [0.5], "n_estimators": [30],
+                                                          "random_state": [0]})
+    assert s[0] > 0.5
+
+
+def test_logistic_matches_sklearn_iris():
+    from sklearn.linear_model import LogisticRegression
+
+    X, y = load_iris(return_X_y=True)
+    grid = {"C": [0.01, 0.1, 1.0, 10.0]}
+    ours = _ours("LogisticRegression", X, y, True, grid)
+    ref = _ref(LogisticRegression(max_iter=5000), X, y, grid)
+    assert np.abs(ours - ref).max() <= 0.0134
+
+
+def test_random_forest_close_to_sklearn():
+    from sklearn.ensemble import RandomForestClassifier
+
+    X, y = make_classification(500, 8, n_informative=5, random_state=4)
+    grid = {"n_estimators": [50], "max_depth": [3, None]}
+    ours = _ours("RandomForestClassifier", X, y, True, grid)
+    ref = _ref(RandomForestClassifier(random_state=0), X, y, grid)
+    assert np.abs(ours - ref).max() < 0.05
+
+
+def test_unsupported_model_is_rejected():
+    from cs230_distributed_machine_learning_amd.models.base import ParamError
+
+    with pytest.raises(ParamError):
+        family_of("MLPClassifier")

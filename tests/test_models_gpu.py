@@ -1,0 +1,118 @@
+"""HIP kernels of the non-forest families vs their plain-PyTorch fp32/fp64 references."""
+import numpy as np
+import pytest
+import torch
+
+from cs230_distributed_machine_learning_amd.data.device import DeviceData
+from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
+from cs230_distributed_machine_learning_amd.search.cv import make_split_roles
+from cs230_distributed_machine_learning_amd.search.grid import ParameterGrid
+
+pytestmark = pytest.mark.gpu
+
+
+def _dd(X, y, clf, dev, cv=5):
+    dd = DeviceData(X, y, clf, dev)
+    roles, names = make_split_roles(np.asarray(y), cv, clf, holdout=True, test_size=0.2, random_state=0)
+    dd.set_splits(roles, names)
+    return dd
+
+
+@pytest.mark.parametrize("metric,p", [(0, 2.0), (1, 1.0), (2, float("inf")), (3, 3.0)])
+@pytest.mark.parametrize("n,d,K", [(1000, 7, 5), (2053, 33, 64), (333, 3, 17)])
+def test_knn_kernel_matches_torch(metric, p, n, d, K):
+    from cs230_distributed_machine_learning_amd.models import neighbors as nb
+
+    rng = np.random.RandomState(n + d)
+    X = rng.randn(n, d).astype(np.float32)
+    y = rng.randint(0, 3, n)
+    dg = _dd(X, y, True, "cuda:0")
+    splits = list(range(len(dg.split_names)))
+    got = nb.knn_search_hip(dg, splits, K, metric, p)
+    for s in splits:
+        ref_d, ref_i = nb.knn_search_torch(dg.X.double(), dg.test_rows[s], dg.train_rows[s], K, metric, p)
+        gd, gi = got[s]
+        torch.testing.assert_close(gd.double(), ref_d, rtol=2e-5, atol=1e-5)
+        # neighbour sets agree except where two distances are within float32 round-off
+        mismatch = (gi != ref_i)
+        if mismatch.any():
+            close = (ref_d[mismatch] - gd.double()[mismatch]).abs() <= 1e-4 * ref_d[mismatch].abs().clamp_min(1)
+            assert bool(close.all())
+
+
+def test_knn_gpu_grid_matches_cpu():
+    rng = np.random.RandomState(0)
+    X = rng.randn(3000, 12).astype(np.float32)
+    y = (X[:, 0] + 0.5 * X[:, 1] > 0).astype(int)
+    grid = list(ParameterGrid({"n_neighbors": [1, 5, 31], "weights": ["uniform", "distance"]}))
+    out = {}
+    for dev in ("cpu", "cuda:0"):
+        dd = DeviceData(X, y, True, dev)
+        res = run_candidates(dd, JobSpec("KNeighborsClassifier", grid, cv=5), range(len(grid)))
+        out[dev] = np.array([r.result["mean_cv_score"] for r in res])
+    np.testing.assert_allclose(out["cuda:0"], out["cpu"], atol=1e-3)
+
+
+@pytest.mark.parametrize("model,clf,loss", [("GradientBoostingClassifier", True, "log_loss"),
+                                            ("GradientBoostingRegressor", False, "squared_error"),
+                                            ("GradientBoostingRegressor", False, "huber")])
+def test_gbrt_gpu_close_to_cpu(model, clf, loss):
+    rng = np.random.RandomState(1)
+    X = np.round(rng.randn(4000, 8), 1).astype(np.float32)
+    if clf:
+        y = (X[:, 0] * X[:, 1] + X[:, 2] > 0).astype(int)
+    else:
+        y = (X[:, 0] * 3 + X[:, 1] * X[:, 2] + rng.randn(4000) * 0.1).astype(np.float32)
+    grid = list(ParameterGrid({"n_estimators": [10, 40], "max_depth": [2, 4], "loss": [loss]}))
+    out = {}
+    for dev in ("cpu", "cuda:0"):
+        dd = DeviceData(X, y, clf, dev)
+        res = run_candidates(dd, JobSpec(model, grid, cv=3), range(len(grid)))
+        assert all(r.ok for r in res), [r.error for r in res]
+        out[dev] = np.array([r.result["mean_cv_score"] for r in res])
+    np.testing.assert_allclose(out["cuda:0"], out["cpu"], atol=5e-3)
+
+
+def test_lr_link_grad_kernel_matches_torch():
+    from cs230_distributed_machine_learning_amd.models import linear
+    from cs230_distributed_machine_learning_amd.utils import native
+
+    rng = np.random.RandomState(2)
+    n, C = 5000, 4
+    y = rng.randint(0, C, n).astype(np.int32)
+    dd = _dd(rng.randn(n, 6).astype(np.float32), y, True, "cuda:0")
+    S = len(dd.split_names)
+    # fits: softmax (K=C), OvR (K=C), binary (K=1) on assorted splits
+    kinds = [(linear.KIND_SOFTMAX, C), (linear.KIND_OVR, C), (linear.KIND_BINARY, 1)] * 3
+    col0, K, kind, split, scale = [], [], [], [], []
+    m = 0
+    for i, (kd, k) in enumerate(kinds):
+        col0.append(m); K.append(k); kind.append(kd); split.append(i % S); scale.append(1.0 / (i + 1))
+        m += k
+    Z = torch.randn(n, m, device="cuda:0")
+    i32 = lambda v: torch.tensor(v, dtype=torch.int32, device="cuda:0")
+    ycls = torch.from_numpy(y).cuda()
+    R = torch.empty_like(Z)
+    loss = torch.empty(len(kinds), dtype=torch.float64, device="cuda:0")
+    lib = native.hip_lib()
+    rc = lib.dml_lr_link_grad(native.ptr(Z), n, m, native.ptr(ycls), native.ptr(dd.roles), native.ptr(i32(col0)),
+                              native.ptr(i32(K)), native.ptr(i32(kind)), native.ptr(i32(split)),
+                              native.ptr(torch.tensor(scale, dtype=torch.float32, device="cuda:0")), len(kinds),
+                              native.ptr(R), native.ptr(loss), native.stream_handle())
+    assert rc == 0
+    Rr, lr = linear.link_grad_torch(Z.double(), ycls, dd.roles, col0, K, kind, split, scale)
+    torch.testing.assert_close(R.double(), Rr, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(loss, lr, rtol=1e-4, atol=1e-4)
+
+
+def test_lr_gpu_grid_matches_cpu():
+    rng = np.random.RandomState(3)
+    X = rng.randn(2000, 10).astype(np.float32)
+    y = (X @ rng.randn(10) + rng.randn(2000) > 0).astype(int)
+    grid = list(ParameterGrid({"C": [0.01, 1.0, 100.0], "solver": ["lbfgs", "liblinear"]}))
+    out = {}
+    for dev in ("cpu", "cuda:0"):
+        dd = DeviceData(X, y, True, dev)
+        res = run_candidates(dd, JobSpec("LogisticRegression", grid, cv=5), range(len(grid)))
+        out[dev] = np.array([r.result["mean_cv_score"] for r in res])
+    np.testing.assert_allclose(out["cuda:0"], out["cpu"], atol=2e-3)
