@@ -95,10 +95,12 @@ def test_lr_link_grad_kernel_matches_torch():
     R = torch.empty_like(Z)
     loss = torch.empty(len(kinds), dtype=torch.float64, device="cuda:0")
     lib = native.hip_lib()
-    rc = lib.dml_lr_link_grad(native.ptr(Z), n, m, native.ptr(ycls), native.ptr(dd.roles), native.ptr(i32(col0)),
-                              native.ptr(i32(K)), native.ptr(i32(kind)), native.ptr(i32(split)),
-                              native.ptr(torch.tensor(scale, dtype=torch.float32, device="cuda:0")), len(kinds),
-                              native.ptr(R), native.ptr(loss), native.stream_handle())
+    # keep every argument tensor alive across the asynchronous launch
+    args = [i32(col0), i32(K), i32(kind), i32(split), torch.tensor(scale, dtype=torch.float32, device="cuda:0")]
+    rc = lib.dml_lr_link_grad(native.ptr(Z), n, m, native.ptr(ycls), native.ptr(dd.roles),
+                              *[native.ptr(a) for a in args], len(kinds), native.ptr(R), native.ptr(loss),
+                              native.stream_handle())
+    torch.cuda.synchronize()
     assert rc == 0
     Rr, lr = linear.link_grad_torch(Z.double(), ycls, dd.roles, col0, K, kind, split, scale)
     torch.testing.assert_close(R.double(), Rr, rtol=1e-4, atol=1e-6)
