@@ -7,7 +7,8 @@ live in one shared model store as ``.npz`` (arrays + a JSON metadata string; loa
 with ``allow_pickle=False``, so downloading and loading a model executes nothing).
 
 Kinds: ``forest`` (pool layout of ops/forest_ops.py + bin edges),
-``linear_logistic``, ``linear_regression``, ``knn`` (training rows), ``gbrt``.
+``linear_logistic``, ``linear_regression``, ``knn`` (training rows), ``gbrt`` (stage trees),
+``svm`` (support vectors + dual coefficients per one-vs-one machine).
 """
 from __future__ import annotations
 
@@ -19,7 +20,7 @@ from typing import Any, Dict, Optional
 import numpy as np
 
 _ARRAY_KEYS = ("nodes", "vals", "edges", "coef", "intercept", "X", "y", "init", "stage_offsets", "scale", "mean",
-               "components", "var", "min", "max")
+               "components", "var", "min", "max", "value", "roots")
 
 
 def save_model(model: Dict[str, Any], path: str) -> str:
@@ -117,4 +118,8 @@ def predict(model: Dict[str, Any], X: np.ndarray) -> np.ndarray:
         from ..models.boosting import gbrt_predict_numpy
 
         return gbrt_predict_numpy(model, X)
+    if kind == "svm":
+        from ..models.svm import svm_predict_numpy
+
+        return svm_predict_numpy(model, X)
     raise ValueError(f"unknown model kind {kind!r}")

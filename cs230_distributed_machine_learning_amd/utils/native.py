@@ -106,6 +106,8 @@ def cpu_lib() -> ctypes.CDLL:
             lib.dml_cpu_forest_predict.argtypes = [c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp,
                                                    c_i64, c_vp, c_vp, c_vp]
             lib.dml_cpu_bin.argtypes = [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64]
+            lib.dml_cpu_svm_sizeof_prob.restype = c_i32
+            lib.dml_cpu_svm_smo.argtypes = [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]
             _cpu = lib
         return _cpu
 
@@ -165,6 +167,8 @@ def _register_optional(lib) -> None:
                             c_vp, c_vp]),
         "dml_knn_qpw": (c_i32, []),
         "dml_forest_apply": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp]),
+        "dml_svm_sizeof_prob": (c_i32, []),
+        "dml_svm_smo": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     }
     for name, (res, args) in table.items():
         fn = getattr(lib, name, None)

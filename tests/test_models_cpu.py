@@ -135,3 +135,47 @@ def test_unsupported_model_is_rejected():
 
     with pytest.raises(ParamError):
         family_of("MLPClassifier")
+
+
+def test_svc_matches_sklearn_iris():
+    from sklearn.svm import SVC
+
+    X, y = load_iris(return_X_y=True)
+    grid = {"C": [0.1, 1, 10], "kernel": ["rbf", "linear", "poly", "sigmoid"]}
+    np.testing.assert_allclose(_ours("SVC", X, y, True, grid), _ref(SVC(), X, y, grid), atol=1e-12)
+
+
+def test_svc_binary_class_weight_matches_sklearn():
+    from sklearn.svm import SVC
+
+    X, y = make_classification(300, 6, n_informative=4, weights=[0.7], random_state=0)
+    grid = {"C": [0.5, 5], "gamma": ["scale", 0.05], "class_weight": [None, "balanced"]}
+    np.testing.assert_allclose(_ours("SVC", X, y, True, grid), _ref(SVC(), X, y, grid), atol=1e-12)
+
+
+def test_svr_matches_sklearn():
+    from sklearn.svm import SVR
+
+    X, y = make_regression(200, 4, noise=10, random_state=2)
+    y = y / 50
+    grid = {"C": [1, 10], "epsilon": [0.05, 0.2], "kernel": ["rbf", "linear"]}
+    np.testing.assert_allclose(_ours("SVR", X, y, False, grid), _ref(SVR(), X, y, grid), atol=1e-4)
+
+
+def test_saved_models_predict_like_training(tmp_path):
+    """refit artefacts (.npz, no pickle) of every family predict on the host."""
+    from cs230_distributed_machine_learning_amd.engine.model_store import load_model, predict, save_model
+
+    X, y = load_iris(return_X_y=True)
+    for model, params in [("SVC", {"C": 3.0}), ("KNeighborsClassifier", {"n_neighbors": 3}),
+                          ("GradientBoostingClassifier", {"n_estimators": 5}),
+                          ("RandomForestClassifier", {"n_estimators": 5, "random_state": 0}),
+                          ("LogisticRegression", {"C": 1.0})]:
+        dd = DeviceData(X, y, True, "cpu")
+        dd.set_splits(np.ones((1, len(y)), np.uint8), ["full"])
+        fam = family_of(model)
+        rp = fam.resolve(model, params, len(y), 4, 3)
+        out = fam.run(dd, [FitTask(0, 0, 0, model, rp)], keep_models=True)[0]
+        path = save_model(out.model, str(tmp_path / f"{model}.npz"))
+        pred = predict(load_model(path), X)
+        assert (np.asarray(pred).astype(int) == y).mean() > 0.9, model

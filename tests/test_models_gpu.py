@@ -118,3 +118,25 @@ def test_lr_gpu_grid_matches_cpu():
         res = run_candidates(dd, JobSpec("LogisticRegression", grid, cv=5), range(len(grid)))
         out[dev] = np.array([r.result["mean_cv_score"] for r in res])
     np.testing.assert_allclose(out["cuda:0"], out["cpu"], atol=2e-3)
+
+
+@pytest.mark.parametrize("model,clf", [("SVC", True), ("SVR", False)])
+def test_svm_gpu_matches_cpu_solver(model, clf):
+    """The HIP SMO and the host SMO run the same algorithm: same dual solution."""
+    from cs230_distributed_machine_learning_amd.models.base import FitTask, family_of
+
+    rng = np.random.RandomState(5)
+    n = 900
+    X = rng.randn(n, 6).astype(np.float32)
+    if clf:
+        y = np.digitize(X[:, 0] + 0.5 * X[:, 1] ** 2 + 0.3 * rng.randn(n), [-0.5, 0.8])   # 3 classes
+    else:
+        y = (np.sin(X[:, 0]) + 0.3 * X[:, 1] + 0.1 * rng.randn(n)).astype(np.float32)
+    grid = list(ParameterGrid({"C": [0.3, 3.0], "kernel": ["rbf", "poly", "linear"]}))
+    out = {}
+    for dev in ("cpu", "cuda:0"):
+        dd = DeviceData(X, y, clf, dev)
+        res = run_candidates(dd, JobSpec(model, grid, cv=3), range(len(grid)))
+        assert all(r.ok for r in res), [r.error for r in res]
+        out[dev] = np.array([r.result["mean_cv_score"] for r in res])
+    np.testing.assert_allclose(out["cuda:0"], out["cpu"], atol=2e-3)
