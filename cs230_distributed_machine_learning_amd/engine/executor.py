@@ -89,6 +89,8 @@ def build_tasks(data, spec: JobSpec, candidate_ids: Sequence[int]):
 
 
 def _scores_for(data, task: FitTask, out: FitOutput, scorer: str):
+    if scorer == "score":
+        return float(out.info["score"])
     rows = data.test_rows[task.split].long()
     if data.classification:
         y = data.y_cls[rows]
@@ -101,9 +103,16 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
     """Run every split of the given candidates; returns one result per candidate."""
     names = prepare_splits(data, spec)
     clf = is_classifier(spec.model_type)
-    scorer = scoring_mod.validate_scoring(spec.scoring, clf)
-    tasks, errors = build_tasks(data, spec, candidate_ids)
     fam = family_of(spec.model_type)
+    self_scored = spec.model_type in getattr(fam, "self_scored", ())
+    if self_scored:
+        # estimators scored by their own ``score`` method (sklearn GridSearchCV with scoring=None)
+        if spec.scoring not in (None, "None", "", "score"):
+            raise ValueError(f"scoring {spec.scoring!r} needs predictions; {spec.model_type} only has score()")
+        scorer = "score"
+    else:
+        scorer = scoring_mod.validate_scoring(spec.scoring, clf)
+    tasks, errors = build_tasks(data, spec, candidate_ids)
     keep = spec.keep_models in ("all", "best")
     outputs: Dict[int, FitOutput] = {}
     if tasks:
@@ -160,7 +169,9 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
                 continue
             if hold_idx is not None:
                 t, o = split_out[hold_idx]
-                if clf:
+                if self_scored:
+                    R["score"] = _scores_for(data, t, o, "score")
+                elif clf:
                     R["accuracy"] = _scores_for(data, t, o, "accuracy")
                 else:
                     R["r2_score"] = _scores_for(data, t, o, "r2")
@@ -176,7 +187,7 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
                     float(np.mean(finite)) if finite and spec.error_score is None else float("nan"))
                 R["std_cv_score"] = float(np.std(cv_scores)) if finite else float("nan")
             else:
-                main = "accuracy" if clf else "r2_score"
+                main = "score" if self_scored else ("accuracy" if clf else "r2_score")
                 R["cv_scores"] = []
                 R["mean_cv_score"] = R.get(main, float("nan"))
             R["scoring"] = scorer

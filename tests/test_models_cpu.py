@@ -179,3 +179,27 @@ def test_saved_models_predict_like_training(tmp_path):
         path = save_model(out.model, str(tmp_path / f"{model}.npz"))
         pred = predict(load_model(path), X)
         assert (np.asarray(pred).astype(int) == y).mean() > 0.9, model
+
+
+@pytest.mark.parametrize("grid", [{"n_components": [1, 2, 3, 4]}, {"n_components": [0.9, 0.99, "mle", None]},
+                                  {"n_components": [2, 3], "whiten": [True]}])
+def test_pca_cv_log_likelihood_matches_sklearn(grid):
+    from sklearn.decomposition import PCA
+
+    rng = np.random.RandomState(0)
+    X = rng.randn(300, 6) @ rng.randn(6, 6) + rng.randn(300, 6) * 0.1
+    y = rng.randint(0, 2, 300)
+    dd = DeviceData(X, y, False, "cpu")
+    cands = list(ParameterGrid(grid))
+    res = run_candidates(dd, JobSpec("PCA", cands, cv=5), range(len(cands)))
+    assert all(r.ok for r in res), [r.error for r in res]
+    ours = np.array([r.result["mean_cv_score"] for r in res])
+    ref = GridSearchCV(PCA(), grid, cv=5).fit(X).cv_results_["mean_test_score"]
+    np.testing.assert_allclose(ours, ref, rtol=1e-5)
+
+
+def test_column_transformers_are_rejected_with_guidance():
+    X, y = load_iris(return_X_y=True)
+    dd = DeviceData(X, y, True, "cpu")
+    res = run_candidates(dd, JobSpec("StandardScaler", [{}], cv=3), [0])
+    assert not res[0].ok and "/preprocess" in res[0].error
