@@ -275,6 +275,28 @@ class LogisticFamily(Family):
             return []
         if not data.classification:
             raise ParamError("LogisticRegression needs a classification target")
+        # tiny lbfgs problems (iris-sized): a device launch per objective evaluation is pure
+        # latency, so they run on the host with scipy's L-BFGS-B on sklearn's exact float64
+        # objective -> same iterates as sklearn even where max_iter stops before convergence
+        small = [t for t in tasks if t.params["solver"] == "lbfgs" and
+                 data.train_counts[t.split] * (data.d + 1) * max(1, data.n_classes - 1) <= HOST_LBFGS_MAX_WORK]
+        if small:
+            done = {o.task_id: o for o in self._run_host_lbfgs(data, small, keep_models)}
+            rest = [t for t in tasks if t.task_id not in done]
+            if rest:
+                done.update({o.task_id: o for o in self.run(data, rest, keep_models)})
+            return [done[t.task_id] for t in tasks]
+        # memory-budgeted batches of whole fits: Z and R are [n, columns] and the L-BFGS
+        # history holds 2 x history [d+1, columns] matrices
+        width = 1 if data.n_classes == 2 else data.n_classes
+        per_col = 4.0 * (3 * data.n + (data.d + 1) * (2 * self.history + 6))
+        budget = 0.45 * torch.cuda.mem_get_info(data.device)[0] if data.is_gpu else 8e9
+        cap = max(1, int(budget // (per_col * width)))
+        if len(tasks) > cap:
+            outs: List[FitOutput] = []
+            for i in range(0, len(tasks), cap):
+                outs.extend(self.run(data, tasks[i:i + cap], keep_models))
+            return outs
         t0 = time.perf_counter()
         b = _Batch(data, tasks)
         W, iters, n_evals = self._solve(data, b)
@@ -313,6 +335,83 @@ class LogisticFamily(Family):
                 }
         return outs
 
+
+    def _run_host_lbfgs(self, data, tasks: List[FitTask], keep_models: bool) -> List[FitOutput]:
+        from scipy import optimize
+
+        t0 = time.perf_counter()
+        X = data.X.detach().double().cpu().numpy()
+        y = data.y_cls.cpu().numpy().astype(np.int64)
+        C_cls = data.n_classes
+        outs = []
+        for t in tasks:
+            rp = t.params
+            tr = data.train_rows[t.split].long().cpu().numpy()
+            te = data.test_rows[t.split].long().cpu().numpy()
+            Xt, yt = X[tr], y[tr]
+            n, d = Xt.shape
+            fi = rp["fit_intercept"]
+            lam = 0.0 if rp["C"] is None else 1.0 / (rp["C"] * n)
+            K = 1 if C_cls == 2 else C_cls
+            if K == 1:
+                tgt = (yt == 1).astype(np.float64)
+            else:
+                tgt = np.eye(K)[yt]
+
+            def fun(w):
+                W = w.reshape((K, d + int(fi)), order="F") if K > 1 else w.reshape(1, -1)
+                coef = W[:, :d]
+                Z = Xt @ coef.T + (W[:, d] if fi else 0.0)
+                if K == 1:
+                    z = Z[:, 0]
+                    loss = np.sum(np.logaddexp(0, z) - tgt * z) / n
+                    r = (1.0 / (1.0 + np.exp(-z)) - tgt)[:, None] / n
+                else:
+                    m = Z.max(1, keepdims=True)
+                    lse = m[:, 0] + np.log(np.exp(Z - m).sum(1))
+                    loss = np.sum(lse - (Z * tgt).sum(1)) / n
+                    r = (np.exp(Z - lse[:, None]) - tgt) / n
+                loss += 0.5 * lam * np.sum(coef * coef)
+                G = np.empty_like(W)
+                G[:, :d] = r.T @ Xt + lam * coef
+                if fi:
+                    G[:, d] = r.sum(0)
+                return loss, (G.ravel(order="F") if K > 1 else G.ravel())
+
+            w0 = np.zeros(K * (d + int(fi)))
+            res = optimize.minimize(fun, w0, method="L-BFGS-B", jac=True,
+                                    options={"maxiter": rp["max_iter"], "maxls": 50, "gtol": rp["tol"],
+                                             "ftol": 64 * np.finfo(float).eps})
+            W = res.x.reshape((K, d + int(fi)), order="F") if K > 1 else res.x.reshape(1, -1)
+            coef, b = W[:, :d], (W[:, d] if fi else np.zeros(K))
+            Z = X[te] @ coef.T + b
+            if K == 1:
+                pred = (Z[:, 0] > 0).astype(np.int32)
+                p1 = 1.0 / (1.0 + np.exp(-Z[:, 0]))
+                proba = np.stack([1 - p1, p1], 1)
+            else:
+                pred = Z.argmax(1).astype(np.int32)
+                e = np.exp(Z - Z.max(1, keepdims=True))
+                proba = e / e.sum(1, keepdims=True)
+            warn = list(rp.get("warnings", []))
+            if res.status != 0 and res.nit >= rp["max_iter"]:
+                warn.append("lbfgs failed to converge (status=1): STOP: TOTAL NO. OF ITERATIONS REACHED LIMIT.")
+            o = FitOutput(task_id=t.task_id, pred=torch.from_numpy(pred).to(data.device),
+                          proba=torch.from_numpy(proba).to(data.device),
+                          info={"warnings": warn, "n_iter": int(res.nit), "host_lbfgs": True})
+            if keep_models:
+                o.model = {"kind": "linear_logistic", "coef": coef, "intercept": b,
+                           "link": KIND_BINARY if K == 1 else KIND_SOFTMAX,
+                           "classes": np.asarray(data.classes).tolist(), "model_type": t.model_type,
+                           "params": {k2: v for k2, v in rp.items() if k2 != "warnings"}}
+            outs.append(o)
+        dt = time.perf_counter() - t0
+        for o in outs:
+            o.fit_seconds = dt / max(1, len(outs))
+        return outs
+
+
+HOST_LBFGS_MAX_WORK = 200_000   # n_train * (d+1) * (K-1): below this a fit runs on the host
 
 _LIN_DEFAULTS = {"fit_intercept": True, "copy_X": True, "n_jobs": None, "positive": False}
 

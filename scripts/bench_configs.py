@@ -1,0 +1,165 @@
+#!/usr/bin/env python3
+"""The five BASELINE.json configurations, one JSON line each (single process / 1 device).
+
+  1  LogisticRegression GridSearchCV cv=5 on iris through the client API (plumbing, CPU)
+  2  RandomForestClassifier 64-point grid, 1M x 100 synthetic, 1 GPU
+  3  the headline 256-point RF GridSearchCV is ``bench.py`` (1/2/4/8 GPUs)
+  4  RandomizedSearchCV LogisticRegression n_iter=512 cv=5 on --lr-rows x 1000 dense
+  5  mixed queue: concurrent RF + LR jobs from several sessions through the controller
+
+    python scripts/bench_configs.py --configs 1,2,4,5 [--lr-rows 10000000]
+
+Metric everywhere: CV fits per second of wall time (a candidate x fold fit counts 1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def _emit(cfg, fits, seconds, **extra):
+    print(json.dumps({"config": cfg, "cv_fits": fits, "seconds": round(seconds, 3),
+                      "cv_fits_per_s": round(fits / seconds, 4), **extra}), flush=True)
+
+
+def config1():
+    from sklearn.linear_model import LogisticRegression
+    from sklearn.model_selection import GridSearchCV
+
+    from cs230_distributed_machine_learning_amd.config import Config
+    from cs230_distributed_machine_learning_amd.engine.service import Controller
+    from distributed_ml import MLTaskManager
+
+    ctl = Controller(Config(data_root=tempfile.mkdtemp(), device="cpu"))
+    tm = MLTaskManager(controller=ctl)
+    tm.download_data("iris", "iris", "sklearn")
+    grid = {"C": [0.1, 1.0, 10.0, 100], "solver": ["liblinear", "lbfgs"]}
+    t0 = time.time()
+    out = tm.train(GridSearchCV(LogisticRegression(), grid, cv=5), "iris", {"target_column": "target"},
+                   wait_for_completion=True, polling_interval=0.02)
+    dt = time.time() - t0
+    best = out["best_result"]
+    _emit(1, 8 * 6, dt, best={k: best["parameters"][k] for k in ("C", "solver")},
+          best_mean_cv=round(best["mean_cv_score"], 4), note="48 fits = 8 candidates x (5 CV + 1 holdout)")
+    ctl.shutdown()
+
+
+def _synthetic(rows, d, dev, seed=0):
+    from cs230_distributed_machine_learning_amd.data import synthetic
+    from cs230_distributed_machine_learning_amd.data.device import DeviceData
+
+    X, y = synthetic.make_table(rows, d, informative=10, n_classes=2, noise=1.0, seed=seed, device=dev)
+    return DeviceData(X, y, classification=True, device=dev, name=f"synthetic-{rows}x{d}")
+
+
+def config2(dev):
+    from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
+    from cs230_distributed_machine_learning_amd.search.grid import expand_candidates
+
+    dd = _synthetic(1_000_000, 100, dev)
+    grid = {"n_estimators": [50, 100, 150, 200], "max_depth": [10, 20, 30, None], "min_samples_leaf": [1, 2, 4, 8]}
+    cands = expand_candidates("GridSearchCV", {"param_grid": grid})
+    spec = JobSpec("RandomForestClassifier", cands, cv=5, holdout=False, keep_models="none")
+    dd.binned()
+    torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    t0 = time.time()
+    done = 0
+    for i in range(0, len(cands), 4):   # 4 candidates (20 fits) per device batch
+        res = run_candidates(dd, spec, list(range(i, min(i + 4, len(cands)))))
+        assert all(r.ok for r in res)
+        done += 5 * len(res)
+    torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    _emit(2, done, time.time() - t0, grid_points=len(cands))
+
+
+def config4(dev, rows):
+    from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
+    from cs230_distributed_machine_learning_amd.search.grid import expand_candidates
+
+    dd = _synthetic(rows, 1000, dev, seed=1)
+    dist = {"C": {"dist": "loguniform", "a": 1e-3, "b": 1e2}, "solver": ["lbfgs", "liblinear"],
+            "max_iter": [100]}
+    cands = expand_candidates("RandomizedSearchCV", {"param_distributions": dist, "n_iter": 512, "random_state": 0})
+    spec = JobSpec("LogisticRegression", cands, cv=5, holdout=False, keep_models="none")
+    torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    t0 = time.time()
+    res = run_candidates(dd, spec, list(range(len(cands))))
+    torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    ok = [r for r in res if r.ok]
+    _emit(4, 5 * len(ok), time.time() - t0, rows=rows, features=1000, candidates=len(cands),
+          best_mean_cv=round(max(r.result["mean_cv_score"] for r in ok), 4))
+
+
+def config5(dev):
+    from cs230_distributed_machine_learning_amd.config import Config
+    from cs230_distributed_machine_learning_amd.engine.service import Controller
+    import pandas as pd
+
+    root = tempfile.mkdtemp()
+    rng = np.random.RandomState(0)
+    n, d = 200_000, 20
+    X = rng.randn(n, d).astype(np.float32)
+    y = (X[:, :5].sum(1) + rng.randn(n) > 0).astype(int)
+    df = pd.DataFrame(X, columns=[f"f{i}" for i in range(d)])
+    df["label"] = y
+    os.makedirs(os.path.join(root, "datasets", "mixed"), exist_ok=True)
+    df.to_csv(os.path.join(root, "datasets", "mixed", "mixed.csv"), index=False)
+    ctl = Controller(Config(data_root=root, device=str(dev)))
+    jobs = []
+    t0 = time.time()
+    for s in range(4):
+        sid = ctl.create_session()[1]["session_id"]
+        for kind in ("rf", "lr"):
+            if kind == "rf":
+                md = {"model_type": "RandomForestClassifier", "search_type": "GridSearchCV", "hyperparameters": {
+                    "base_estimator_params": {}, "cv_params": {"cv": 5},
+                    "search_params": {"param_grid": {"n_estimators": [50, 100], "max_depth": [10, None]}}}}
+            else:
+                md = {"model_type": "LogisticRegression", "search_type": "RandomizedSearchCV", "hyperparameters": {
+                    "base_estimator_params": {}, "cv_params": {"cv": 5}, "search_params": {
+                        "param_distributions": {"C": {"dist": "loguniform", "a": 1e-3, "b": 1e2}},
+                        "n_iter": 16, "random_state": s}}}
+            jid = f"{kind}-{s}"
+            st, _ = ctl.train(sid, {"job_id": jid, "dataset_id": "mixed", "model_details": md,
+                                    "train_params": {"target_column": "label"}})
+            assert st == 200
+            jobs.append((sid, jid))
+    fits = 0
+    for sid, jid in jobs:
+        ctl.table.wait_finished(jid, timeout=3600)
+        st = ctl.check_status(sid, jid)[1]
+        assert st["job_status"] == "completed", st
+        fits += st["total_subtasks"] * 6
+    _emit(5, fits, time.time() - t0, jobs=len(jobs), sessions=4)
+    ctl.shutdown()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="1,2,4,5")
+    ap.add_argument("--lr-rows", type=int, default=2_000_000)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0" if torch.cuda.is_available() else "cpu")
+    want = {int(c) for c in args.configs.split(",")}
+    if 1 in want:
+        config1()
+    if 2 in want:
+        config2(dev)
+    if 4 in want:
+        config4(dev, args.lr_rows)
+    if 5 in want:
+        config5(dev)
+
+
+if __name__ == "__main__":
+    main()

@@ -109,8 +109,8 @@ def test_lr_link_grad_kernel_matches_torch():
 
 def test_lr_gpu_grid_matches_cpu():
     rng = np.random.RandomState(3)
-    X = rng.randn(2000, 10).astype(np.float32)
-    y = (X @ rng.randn(10) + rng.randn(2000) > 0).astype(int)
+    X = rng.randn(40000, 10).astype(np.float32)          # large enough for the device solver
+    y = (X @ rng.randn(10) + rng.randn(40000) > 0).astype(int)
     grid = list(ParameterGrid({"C": [0.01, 1.0, 100.0], "solver": ["lbfgs", "liblinear"]}))
     out = {}
     for dev in ("cpu", "cuda:0"):
