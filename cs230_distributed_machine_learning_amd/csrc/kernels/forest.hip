@@ -28,6 +28,28 @@
 #include "forest_common.h"
 #include "wave_ops.h"
 
+#ifndef DML_RPT_BLOCK
+#define DML_RPT_BLOCK 1
+#endif
+#ifndef DML_NODES_WPE
+#define DML_NODES_WPE 4
+#endif
+#ifndef DML_KGMAX_WAVE
+#define DML_KGMAX_WAVE 4
+#endif
+
+// optional per-phase cycle accounting of the fused node kernel (-DDML_PHASE_PROF builds only)
+#ifdef DML_PHASE_PROF
+__device__ unsigned long long g_phase[3][8];
+#define PH_BEGIN uint64_t _pt = clock64(); uint64_t _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PH(i) if (threadIdx.x == 0) { const uint64_t _n = clock64(); _acc[i] += _n - _pt; _pt = _n; }
+#define PH_END(t) if (threadIdx.x == 0) { _acc[7] = 1; for (int _i = 0; _i < 8; ++_i) atomicAdd(&g_phase[t][_i], _acc[_i]); }
+#else
+#define PH_BEGIN
+#define PH(i)
+#define PH_END(t)
+#endif
+
 namespace dml {
 
 struct OpenNode {
@@ -248,8 +270,114 @@ __device__ __forceinline__ double hist_chan(const typename HT<MODE>::T* h, int c
 // flag, the best bin's cumulative channels (out_left[CH]); optionally zeroes the
 // histogram afterwards so the next feature group needs no clearing pass.
 template <int MODE>
+__device__ void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
+                                 double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after);
+
+// ONE wave evaluates one feature's histogram.  Binary (MODE 1) and regression (MODE 2)
+// histograms are read ONCE into registers (4 bins per lane), scanned with DPP, scored and
+// arg-maxed without writing the scan back to LDS; the histogram is cleared by the same
+// lanes right after the read.  Multiclass (MODE 0) keeps the LDS path (C+1 planes).
+template <int MODE>
 __device__ void eval_feature(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
                              double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after) {
+  if constexpr (MODE == 0) {
+    eval_feature_lds<MODE>(h, C, CH, s, lane, out_gain, out_bin, out_nc, out_left, zero_after);
+  } else {
+    using CT = typename HT<MODE>::T;
+    constexpr int NP = MODE == 1 ? 1 : 4;      // planes: packed u64 | (w, wy, wyy, rows) floats
+    CT v[NP][4];
+#pragma unroll
+    for (int q = 0; q < NP; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[q][i] = h[q * 256 + 4 * lane + i];
+    if (zero_after) {
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[q * 256 + 4 * lane + i] = (CT)0;
+    }
+    // in-lane prefix + wave exclusive offset -> cumulative value of bin 4*lane+i
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      v[q][1] += v[q][0]; v[q][2] += v[q][1]; v[q][3] += v[q][2];
+      CT t;
+      if constexpr (sizeof(CT) == 8) t = (CT)wave::incl_scan_u64((uint64_t)v[q][3]);
+      else t = wave::incl_scan<CT>(v[q][3]);
+      const CT ex = wave::excl_from_incl<CT>(t);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[q][i] += ex;
+    }
+    CT tot[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) tot[q] = wave::bcast<CT>(v[q][3], 63);
+    const double msl = (double)s.min_samples_leaf;
+    double best = -INFINITY;
+    int bb = -1;
+    bool nc = false;
+    double tot_rows;
+    if constexpr (MODE == 1) tot_rows = (double)((uint64_t)tot[0] >> 42);
+    else tot_rows = (double)tot[3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int b = lane * 4 + i;
+      double rl;
+      if constexpr (MODE == 1) rl = (double)((uint64_t)v[0][i] >> 42);
+      else rl = (double)v[3][i];
+      const double rr = tot_rows - rl;
+      if (b == 255) continue;
+      nc |= (rl > 0.0 && rr > 0.0);
+      if (rl < msl || rr < msl) continue;
+      double g;
+      if constexpr (MODE == 1) {
+        const uint64_t cv = (uint64_t)v[0][i], tv = (uint64_t)tot[0];
+        const double l0 = (double)(cv & kPackMask21), l1 = (double)((cv >> 21) & kPackMask21);
+        const double t0 = (double)(tv & kPackMask21), t1 = (double)((tv >> 21) & kPackMask21);
+        ClsAcc L, R;
+        L.init(s.criterion); R.init(s.criterion);
+        L.add(l0); L.add(l1);
+        R.add(t0 - l0); R.add(t1 - l1);
+        g = cls_proxy(L, R, s.criterion);
+      } else {
+        const double l0 = (double)v[0][i], l1 = (double)v[1][i];
+        g = mse_proxy(l0, l1, (double)tot[0] - l0, (double)tot[1] - l1);
+      }
+      if (g > best) { best = g; bb = b; }
+    }
+    wave::argmax(best, bb, lane);
+    const bool any_nc = __ballot(nc) != 0ull;
+    // the winning bin's cumulative channels, broadcast from its owner lane
+    const int src = bb >= 0 ? (bb >> 2) : 0, sel = bb >= 0 ? (bb & 3) : 0;
+    if constexpr (MODE == 1) {
+      uint64_t mine = (uint64_t)v[0][0];
+#pragma unroll
+      for (int i = 1; i < 4; ++i) if (sel == i) mine = (uint64_t)v[0][i];
+      const uint64_t cv = wave::bcast<uint64_t>(mine, src);
+      if (lane == 0) {
+        out_left[0] = bb >= 0 ? (double)(cv & kPackMask21) : 0.0;
+        out_left[1] = bb >= 0 ? (double)((cv >> 21) & kPackMask21) : 0.0;
+        out_left[2] = bb >= 0 ? (double)(cv >> 42) : 0.0;
+      }
+    } else {
+      float mine[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        mine[q] = v[q][0];
+#pragma unroll
+        for (int i = 1; i < 4; ++i) if (sel == i) mine[q] = v[q][i];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float cq = wave::bcast<float>(mine[q], src);
+        if (lane == 0) out_left[q] = bb >= 0 ? (double)cq : 0.0;
+      }
+    }
+    if (lane == 0) { *out_gain = best; *out_bin = bb; *out_nc = any_nc ? 1 : 0; }
+  }
+}
+
+template <int MODE>
+__device__ void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
+                                 double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after) {
   using CT = typename HT<MODE>::T;
   const int planes = hist_planes(MODE, CH);
   for (int ch = 0; ch < planes; ++ch) scan256<CT>(h + ch * 256, lane);
@@ -369,12 +497,13 @@ __device__ bool accept_split(const Ctx& c, const TreeSpec& s, int node, int tree
 struct Scratch {
   uint64_t last;
   double best_gain;
-  int32_t best_feat, best_bin, nonconst, pos, first, base, nl, pad;
-  int32_t wcnt[8];
+  double W;                 // tree weight (prefetched)
+  int32_t best_feat, best_bin, nonconst, pos, first, base, nl, best_j;
+  int32_t wcnt[32];         // partition: [2][RPT][NW] per-wave counts
 };
 
 struct FusedLayout {
-  size_t hist, feats, rg, rb, rn, rleft, best_left, sc, total;
+  size_t hist, feats, rg, rb, rn, rleft, best_left, pvs, rvs, sc, total;
 };
 
 __host__ __device__ inline FusedLayout fused_layout(int KG, int span, int elem, int CH) {
@@ -388,6 +517,8 @@ __host__ __device__ inline FusedLayout fused_layout(int KG, int span, int elem, 
   L.rn = take((size_t)KG * 4);
   L.rleft = take((size_t)KG * CH * 8);
   L.best_left = take((size_t)CH * 8);
+  L.pvs = take((size_t)CH * 8);
+  L.rvs = take((size_t)CH * 8);
   L.sc = take(sizeof(Scratch));
   L.total = off;
   return L;
@@ -396,16 +527,90 @@ __host__ __device__ inline FusedLayout fused_layout(int KG, int span, int elem, 
 // ------------------------------------------------------------------------------------
 // fused per-node kernel (wave tier NT=64, block tier NT=256)
 // ------------------------------------------------------------------------------------
+// accept_split / make_children / enqueue on values already held on-chip (LDS): the
+// parent's channel sums and the tree weight are prefetched at kernel start, so the
+// decision makes no dependent global round trips.
+__device__ bool accept_split_v(const Ctx& c, const TreeSpec& s, const double* pv, double Wt, const double* best_left) {
+  double impN, impL, impR, wN, wL, wR;
+  if (c.is_reg) {
+    wN = pv[0]; wL = best_left[0]; wR = pv[0] - best_left[0];
+    impN = mse_impurity(pv[0], pv[1], pv[2]);
+    impL = mse_impurity(best_left[0], best_left[1], best_left[2]);
+    impR = mse_impurity(pv[0] - best_left[0], pv[1] - best_left[1], pv[2] - best_left[2]);
+  } else {
+    ClsAcc N, L, R;
+    N.init(s.criterion); L.init(s.criterion); R.init(s.criterion);
+    for (int k = 0; k < c.C; ++k) { N.add(pv[k]); L.add(best_left[k]); R.add(pv[k] - best_left[k]); }
+    wN = N.w; wL = L.w; wR = R.w;
+    impN = cls_impurity(N, s.criterion); impL = cls_impurity(L, s.criterion); impR = cls_impurity(R, s.criterion);
+  }
+  const double imp = improvement(Wt, wN, impN, wL, impL, wR, impR);
+  return !(imp + kEps < (double)s.min_impurity_decrease);
+}
+
+__device__ double impurity_of_vals(const Ctx& c, const double* v, int crit) {
+  if (c.is_reg) return mse_impurity(v[0], v[1], v[2]);
+  ClsAcc a;
+  a.init(crit);
+  for (int k = 0; k < c.C; ++k) a.add(v[k]);
+  return cls_impurity(a, crit);
+}
+
+__device__ void enqueue_or_leaf_v(const Ctx& c, const TreeSpec& s, int tree, int node, int start, int count,
+                                  int depth, uint64_t key, int set, const double* vals) {
+  if (leaf_by_counts(s, count, depth)) return;
+  if (impurity_of_vals(c, vals, s.criterion) <= kEps) return;
+  const int tier = count <= c.sub_max ? 0 : (count <= c.wave_max ? 1 : (count <= c.block_max ? 2 : 3));
+  const int idx = atomicAdd(&c.counters[set * kTiers + tier], 1);
+  if (idx >= c.open_cap[tier]) {
+    atomicOr(&c.counters[kOpenOvf], 1);
+    return;
+  }
+  OpenNode on;
+  on.tree = tree; on.node = node; on.start = start; on.count = count; on.depth = depth; on.pad = 0;
+  on.key = key;
+  c.open[set][tier][idx] = on;
+}
+
+// histogram payload of one row: MODE 0 cls | w << 32, MODE 1 packed u64, MODE 2 (w, y) floats
+template <int MODE>
+__device__ __forceinline__ uint64_t row_payload(const Ctx& c, const float* ty, uint32_t row, uint32_t w) {
+  if constexpr (MODE == 0) return (uint64_t)(uint32_t)c.ycls[row] | ((uint64_t)w << 32);
+  else if constexpr (MODE == 1) return pack_bin(c.ycls[row], w);
+  else return (uint64_t)__builtin_bit_cast(uint32_t, (float)w) | ((uint64_t)__builtin_bit_cast(uint32_t, ty[row]) << 32);
+}
+
+template <int MODE>
+__device__ __forceinline__ void hist_add(typename HT<MODE>::T* hj, const Ctx& c, int b, uint64_t pl) {
+  if constexpr (MODE == 0) {
+    atomicAdd(&hj[(int)(uint32_t)pl * 256 + b], (uint32_t)(pl >> 32));
+    atomicAdd(&hj[c.C * 256 + b], 1u);
+  } else if constexpr (MODE == 1) {
+    atomicAdd(&hj[b], (unsigned long long)pl);
+  } else {
+    const float fw = __builtin_bit_cast(float, (uint32_t)pl), yv = __builtin_bit_cast(float, (uint32_t)(pl >> 32));
+    const float wy = fw * yv, wyy = wy * yv;
+    atomicAdd(&hj[b], fw);
+    atomicAdd(&hj[256 + b], wy);
+    atomicAdd(&hj[512 + b], wyy);
+    atomicAdd(&hj[768 + b], 1.0f);
+  }
+}
+
 template <int NT, int MODE>
-__global__ __launch_bounds__(NT) void k_nodes(Ctx c, int tier, int set_cur) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WPE, 8))) void k_nodes(Ctx c, int tier, int set_cur) {
   using CT = typename HT<MODE>::T;
   constexpr int NW = NT / 64;
+  constexpr int RPT = NT == 64 ? 4 : DML_RPT_BLOCK;   // rows per thread in registers (<= 4: packed u8 x 4)
+  static_assert(RPT >= 1 && RPT <= 4, "RPT");
+  constexpr int KGMAX = NT == 64 ? DML_KGMAX_WAVE : 16;   // feature-group bound (register-resident bins)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  PH_BEGIN
   const OpenNode on = c.open[set_cur][tier][blockIdx.x];
   const TreeSpec& s = c.specs[on.tree];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int d = c.d;
-  const int KG = NT == 64 ? c.kg_wave : c.kg_block;
+  const int KG = min(NT == 64 ? c.kg_wave : c.kg_block, KGMAX);
   const int slack = NT == 64 ? c.slack_wave : 0;
   const int span = hist_planes(MODE, c.CH) * 256;
   const FusedLayout FL = fused_layout(KG, span, (int)sizeof(CT), c.CH);
@@ -416,30 +621,44 @@ __global__ __launch_bounds__(NT) void k_nodes(Ctx c, int tier, int set_cur) {
   int* rn = (int*)(smem + FL.rn);
   double* rleft = (double*)(smem + FL.rleft);
   double* best_left = (double*)(smem + FL.best_left);
+  double* pvs = (double*)(smem + FL.pvs);       // parent channel sums
+  double* rvs = (double*)(smem + FL.rvs);       // right child channel sums
   Scratch* sc = (Scratch*)(smem + FL.sc);
 
   for (int i = tid; i < KG * span; i += NT) hist[i] = (CT)0;
+  if (tid < c.VC) pvs[tid] = c.node_val[(int64_t)on.node * c.VC + tid];
   if (tid == 0) {
     sc->best_gain = -INFINITY; sc->best_feat = -1; sc->best_bin = -1;
-    sc->nonconst = 0; sc->pos = 0; sc->first = 1; sc->last = 0;
+    sc->nonconst = 0; sc->pos = 0; sc->first = 1; sc->last = 0; sc->best_j = -1;
+    sc->W = c.tree_W[on.tree];
   }
   RankCache rc;
   if (wid == 0) rc.build(on.key, d, lane);
-  __syncthreads();
-  const uint32_t* rows = c.rows_cur + c.row_off[on.tree];
-  const int k = s.max_features;
-  // wave tier: a node's <= 256 rows (ids + bootstrap weights) stay in registers across
-  // feature groups instead of being re-read and re-hashed per group
-  const bool reg_rows = NT == 64 && on.count <= 256;
-  uint32_t rrow[4], rw[4];
-  if (reg_rows) {
+  const uint32_t* rows = c.rows_cur + c.row_off[on.tree] + on.start;
+  const float* ty = tree_y(c, s);
+  const int cnt = on.count;
+  // rows (+ bootstrap weight + label payload) of a <= NT*RPT-row node stay in registers
+  // for every feature group and the partition; larger nodes stream in NT*RPT chunks.
+  const bool reg_rows = cnt <= NT * RPT;
+  uint32_t rrow[RPT], rbin[RPT];
+  uint64_t rpl[RPT];
+  auto load_rows = [&](int base) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = tid + 64 * i;
-      rrow[i] = r < on.count ? rows[on.start + r] : 0u;
-      rw[i] = r < on.count ? boot_weight(s, rrow[i]) : 0u;
+    for (int u = 0; u < RPT; ++u) {
+      const int r = base + tid + NT * u;
+      rrow[u] = r < cnt ? rows[r] : 0xFFFFFFFFu;
     }
-  }
+#pragma unroll
+    for (int u = 0; u < RPT; ++u)
+      rpl[u] = rrow[u] != 0xFFFFFFFFu ? row_payload<MODE>(c, ty, rrow[u], boot_weight(s, rrow[u])) : 0ull;
+  };
+  if (reg_rows) load_rows(0);
+#pragma unroll
+  for (int u = 0; u < RPT; ++u) rbin[u] = 0;
+  __syncthreads();
+  PH(0)
+  const int k = s.max_features;
+  uint32_t pk[KGMAX];   // register rows: the group's bins packed 4 x u8 per feature (live across eval)
   while (true) {
     const int pos = sc->pos, nonconst = sc->nonconst;
     if (nonconst >= k || pos >= d) break;
@@ -455,73 +674,173 @@ __global__ __launch_bounds__(NT) void k_nodes(Ctx c, int tier, int set_cur) {
       if (lane == 0) { sc->last = last; sc->first = 0; }
     }
     __syncthreads();
-    if (reg_rows) {
+    PH(1)
+    for (int base = 0; base < cnt; base += NT * RPT) {
+      if (!reg_rows) load_rows(base);
+      // all g x RPT bin loads are issued before the first histogram atomic
+      uint32_t bins[KGMAX][RPT];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (tid + 64 * i < on.count) hist_add_row<MODE>(hist, c, tree_y(c, s), feats, g, rrow[i], rw[i], span);
-    } else {
-      for (int r = tid; r < on.count; r += NT) {
-        const uint32_t row = rows[on.start + r];
-        hist_add_row<MODE>(hist, c, tree_y(c, s), feats, g, row, boot_weight(s, row), span);
+      for (int j = 0; j < KGMAX; ++j) {
+        if (j < g) {
+          const int64_t f = feats[j];
+#pragma unroll
+          for (int u = 0; u < RPT; ++u)
+            bins[j][u] = rrow[u] != 0xFFFFFFFFu ? (uint32_t)c.Xb[(int64_t)rrow[u] * c.ld + f] : 0u;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < KGMAX; ++j) {
+        if (j < g) {
+          CT* hj = hist + j * span;
+#pragma unroll
+          for (int u = 0; u < RPT; ++u)
+            if (rrow[u] != 0xFFFFFFFFu) hist_add<MODE>(hj, c, (int)bins[j][u], rpl[u]);
+        }
+      }
+      if (reg_rows) {
+#pragma unroll
+        for (int j = 0; j < KGMAX; ++j)
+        {
+          uint32_t v = 0;
+#pragma unroll
+          for (int u = 0; u < RPT; ++u) v |= bins[j][u] << (8 * u);
+          pk[j] = j < g ? v : 0u;
+        }
       }
     }
     __syncthreads();
+    PH(2)
     for (int j = wid; j < g; j += NW)
       eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, true);
     __syncthreads();
-    if (tid == 0) {
-      int nc = sc->nonconst, bf = sc->best_feat, bbin = sc->best_bin;
-      double bg = sc->best_gain;
-      select_group(c, s, feats, g, rg, rb, rn, rleft, best_left, nc, bg, bf, bbin);
-      sc->nonconst = nc; sc->best_gain = bg; sc->best_feat = bf; sc->best_bin = bbin;
-      sc->pos = pos + g;
+    PH(3)
+    if (wid == 0) {
+      // wave-parallel form of select_group(): feature j counts if it is non-constant and
+      // among the first (k - nonconst) non-constant ones of the group; the first maximal
+      // gain among those replaces the running best if strictly better
+      const int nc0 = sc->nonconst;
+      const bool isnc = lane < g && rn[lane] != 0;
+      const uint64_t m = __ballot(isnc);
+      const bool considered = isnc && nc0 + lane_prefix(m) + 1 <= k;
+      const bool has = considered && rb[lane] >= 0;
+      double gj = has ? rg[lane] : -INFINITY;
+      int jj = has ? lane : 64;
+      wave::argmax(gj, jj, lane);
+      const bool upd = jj < 64 && gj > sc->best_gain;
+      if (upd && lane < c.CH) best_left[lane] = rleft[jj * c.CH + lane];
+      if (lane == 0) {
+        if (upd) { sc->best_gain = gj; sc->best_feat = feats[jj]; sc->best_bin = rb[jj]; }
+        sc->best_j = upd ? jj : -1;
+        sc->nonconst = min(nc0 + __popcll(m), k);
+        sc->pos = pos + g;
+      }
     }
     __syncthreads();
+    PH(4)
+    if (reg_rows) {
+      const int bj = sc->best_j;
+      uint32_t sel = 0;
+#pragma unroll
+      for (int j = 0; j < KGMAX; ++j)
+        if (j == bj) sel = pk[j];
+      if (bj >= 0)
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) rbin[u] = (sel >> (8 * u)) & 0xFFu;
+    }
   }
-  // ---- decision
+  // ---- decision (on-chip values only)
   if (tid == 0) {
     int base = -1;
-    if (sc->best_feat >= 0 && accept_split(c, s, on.node, on.tree, best_left))
-      base = make_children(c, on.node, sc->best_feat, sc->best_bin, best_left);
+    if (sc->best_feat >= 0 && accept_split_v(c, s, pvs, sc->W, best_left)) {
+      base = atomicAdd(&c.counters[kPool], 2);
+      if ((int64_t)base + 2 > c.pool_cap) {
+        atomicOr(&c.counters[kOverflow], 1);
+        base = -1;
+      } else {
+        NodeRec leaf; leaf.split = -1; leaf.left = -1;
+        c.nodes[base] = leaf;
+        c.nodes[base + 1] = leaf;
+        double* lv = c.node_val + (int64_t)base * c.VC;
+        for (int q = 0; q < c.VC; ++q) {
+          rvs[q] = pvs[q] - best_left[q];
+          lv[q] = best_left[q];
+          lv[c.VC + q] = rvs[q];
+        }
+        NodeRec rec; rec.split = pack_split(sc->best_feat, sc->best_bin); rec.left = base;
+        c.nodes[on.node] = rec;
+      }
+    }
     sc->base = base;
     sc->nl = base >= 0 ? (int)best_left[c.CH - 1] : 0;
   }
   __syncthreads();
+  PH(5)
   const int base = sc->base;
-  if (base < 0) return;
+  if (base < 0) { PH_END(NT == 64 ? 0 : 1) return; }
   const int feat = sc->best_feat, bin = sc->best_bin, nl = sc->nl;
+  constexpr int RT = NT > 64 ? 64 : 1;   // the right child is enqueued by another wave / lane
+  if (tid == 0)
+    enqueue_or_leaf_v(c, s, on.tree, base, on.start, nl, on.depth + 1, child_key(on.key, 0), 1 - set_cur, best_left);
+  if (tid == RT)
+    enqueue_or_leaf_v(c, s, on.tree, base + 1, on.start + nl, cnt - nl, on.depth + 1, child_key(on.key, 1),
+                      1 - set_cur, rvs);
+  // ---- stable partition: RPT ballot rounds per chunk, one block-level offset exchange
   uint32_t* out = c.rows_next + c.row_off[on.tree] + on.start;
   int baseL = 0, baseR = 0;
-  for (int t0 = 0; t0 < on.count; t0 += NT) {
-    const int r = t0 + tid;
-    const bool valid = r < on.count;
-    const uint32_t row = valid ? rows[on.start + r] : 0u;
-    const bool left = valid && c.Xb[(int64_t)row * c.ld + feat] <= bin;
-    const bool right = valid && !left;
-    const uint64_t ml = __ballot(left), mr = __ballot(right);
-    const int pl = lane_prefix(ml), pr = lane_prefix(mr);
-    int offL = 0, offR = 0, totL, totR;
+  for (int cb = 0; cb < cnt; cb += NT * RPT) {
+    if (!reg_rows) {
+      load_rows(cb);
+#pragma unroll
+      for (int u = 0; u < RPT; ++u)
+        rbin[u] = rrow[u] != 0xFFFFFFFFu ? (uint32_t)c.Xb[(int64_t)rrow[u] * c.ld + feat] : 0u;
+    }
+    uint64_t ml[RPT], mr[RPT];
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const bool valid = rrow[u] != 0xFFFFFFFFu;
+      const bool left = valid && (int)rbin[u] <= bin;
+      ml[u] = __ballot(left);
+      mr[u] = __ballot(valid && !left);
+    }
+    int offL[RPT], offR[RPT], totL = 0, totR = 0;
     if constexpr (NW == 1) {
-      totL = __popcll(ml); totR = __popcll(mr);
+#pragma unroll
+      for (int u = 0; u < RPT; ++u) {
+        offL[u] = totL; offR[u] = totR;
+        totL += __popcll(ml[u]); totR += __popcll(mr[u]);
+      }
     } else {
-      if (lane == 0) { sc->wcnt[wid] = __popcll(ml); sc->wcnt[4 + wid] = __popcll(mr); }
+      if (lane == 0)
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) {
+          sc->wcnt[u * NW + wid] = __popcll(ml[u]);
+          sc->wcnt[RPT * NW + u * NW + wid] = __popcll(mr[u]);
+        }
       __syncthreads();
-      totL = 0; totR = 0;
-      for (int w = 0; w < NW; ++w) {
-        if (w < wid) { offL += sc->wcnt[w]; offR += sc->wcnt[4 + w]; }
-        totL += sc->wcnt[w]; totR += sc->wcnt[4 + w];
+#pragma unroll
+      for (int u = 0; u < RPT; ++u) {
+        int l = 0, r = 0, lb = 0, rbb = 0;
+        for (int w = 0; w < NW; ++w) {
+          const int cl = sc->wcnt[u * NW + w], cr = sc->wcnt[RPT * NW + u * NW + w];
+          if (w < wid) { lb += cl; rbb += cr; }
+          l += cl; r += cr;
+        }
+        offL[u] = totL + lb; offR[u] = totR + rbb;
+        totL += l; totR += r;
       }
       __syncthreads();
     }
-    if (left) out[baseL + offL + pl] = row;
-    if (right) out[nl + baseR + offR + pr] = row;
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const bool valid = rrow[u] != 0xFFFFFFFFu;
+      if (!valid) continue;
+      if ((int)rbin[u] <= bin) out[baseL + offL[u] + lane_prefix(ml[u])] = rrow[u];
+      else out[nl + baseR + offR[u] + lane_prefix(mr[u])] = rrow[u];
+    }
     baseL += totL; baseR += totR;
   }
-  if (tid == 0) {
-    const int set_next = 1 - set_cur;
-    enqueue_or_leaf(c, on.tree, base, on.start, nl, on.depth + 1, child_key(on.key, 0), set_next);
-    enqueue_or_leaf(c, on.tree, base + 1, on.start + nl, on.count - nl, on.depth + 1, child_key(on.key, 1), set_next);
-  }
+  PH(6)
+  PH_END(NT == 64 ? 0 : 1)
 }
 
 // ------------------------------------------------------------------------------------
@@ -1115,6 +1434,18 @@ __global__ void k_test_wave_prims(const uint32_t* in, uint32_t* out) {
 }
 
 extern "C" {
+
+int dml_forest_phase_stats(unsigned long long* out) {
+#ifdef DML_PHASE_PROF
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 24) != hipSuccess) return 1;
+  unsigned long long z[24] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) != hipSuccess) return 1;
+  return 0;
+#else
+  (void)out;
+  return 2;
+#endif
+}
 
 int dml_test_wave_prims(const uint32_t* in, uint32_t* out, int64_t nblocks, hipStream_t st) {
   k_test_wave_prims<<<(unsigned)nblocks, 64, 0, st>>>(in, out);

@@ -81,8 +81,11 @@ DML_HD uint32_t boot_weight(const TreeSpec& t, uint32_t row) {
   if (!t.bootstrap) return 1u;
   const uint32_t u = hash_u32(t.seed, 0xB0075ull * 0x100000000ull + row);
   if (t.bootstrap == 2) return u < t.pois_cdf[0] ? 1u : 0u;
+  // inverse CDF: the table is non-decreasing, so "first j with u < T[j]" = #{j : u >= T[j]}
+  // (branch-free: 12 compares against wave-uniform table entries, no per-lane loop)
   uint32_t k = 0;
-  while (k < (uint32_t)kPoisTable && u >= t.pois_cdf[k]) ++k;
+#pragma unroll
+  for (int j = 0; j < kPoisTable; ++j) k += u >= t.pois_cdf[j] ? 1u : 0u;
   return k;
 }
 

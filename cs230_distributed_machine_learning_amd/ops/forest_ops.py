@@ -44,8 +44,8 @@ class ForestTiers:
         """Clamp feature-group sizes to the LDS budget for this channel count."""
         per_feat = n_channels * 256 * 4
         t = ForestTiers(**self.__dict__)
-        t.kg_wave = max(1, min(self.kg_wave, (24 * 1024) // per_feat))
-        t.kg_block = max(1, min(self.kg_block, (96 * 1024) // per_feat))
+        t.kg_wave = max(1, min(self.kg_wave, (24 * 1024) // per_feat, 4))     # k_nodes<64>: KGMAX 4
+        t.kg_block = max(1, min(self.kg_block, (96 * 1024) // per_feat, 16))  # k_nodes<256>: KGMAX 16
         t.kg_large = max(1, min(self.kg_large, (96 * 1024) // per_feat, 64))
         return t
 

@@ -123,7 +123,7 @@ def hip_lib() -> ctypes.CDLL:
     global _hip
     with _lock:
         if _hip is None:
-            path = _build.HIP_LIB
+            path = os.environ.get("DML_HIP_LIB") or _build.HIP_LIB   # override: A/B kernel variants
             if not os.path.exists(path):
                 raise RuntimeError(
                     f"HIP kernel library {path} is missing: run `python -m cs230_distributed_machine_learning_amd.build`"
