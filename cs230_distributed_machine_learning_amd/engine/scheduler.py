@@ -67,7 +67,7 @@ class Scheduler:
         self.algo_weight = {k.lower(): float(v) for k, v in (algo_weight or {}).items()}
         self.calib: Dict[str, float] = {}     # seconds per cost unit, per algorithm (EMA)
         self.ema = ema
-        self.assigned: Dict[str, Tuple[str, Unit]] = {}   # unit_id -> (worker, unit)
+        self.assigned: Dict[str, Tuple[str, Unit, float]] = {}   # unit_id -> (worker, unit, reserved seconds)
         self.held: List[Unit] = []
 
     # ---- membership ----------------------------------------------------------------------
@@ -94,7 +94,7 @@ class Scheduler:
             return self._orphan(w)
 
     def _orphan(self, w: WorkerState) -> List[Unit]:
-        units = [u for uid, (wid, u) in list(self.assigned.items()) if wid == w.worker_id]
+        units = [u for uid, (wid, u, _r) in list(self.assigned.items()) if wid == w.worker_id]
         for u in units:
             del self.assigned[u.unit_id]
         w.tasks_queue.clear()
@@ -166,10 +166,11 @@ class Scheduler:
                     continue
                 w = ws[j]
                 plan[w.worker_id].append(u)
-                w.load_seconds += costs[i] / w.speed_factor
+                reserved = costs[i] / w.speed_factor
+                w.load_seconds += reserved
                 w.mem_load_mb += u.mem_mb
                 w.tasks_queue.append(u.unit_id)
-                self.assigned[u.unit_id] = (w.worker_id, u)
+                self.assigned[u.unit_id] = (w.worker_id, u, reserved)
             return plan
 
     def complete(self, unit_id: str) -> None:
@@ -177,11 +178,10 @@ class Scheduler:
             item = self.assigned.pop(unit_id, None)
             if item is None:
                 return
-            wid, u = item
+            wid, u, reserved = item
             w = self.workers.get(wid)
             if w is not None:
-                est = self.estimate(u.algo, u.cost) / max(w.speed_factor, 1e-6)
-                w.load_seconds = max(0.0, w.load_seconds - est)   # release exactly what was reserved (D11)
+                w.load_seconds = max(0.0, w.load_seconds - reserved)   # release exactly what was reserved (D11)
                 w.mem_load_mb = max(0.0, w.mem_load_mb - u.mem_mb)
                 if unit_id in w.tasks_queue:
                     w.tasks_queue.remove(unit_id)
