@@ -28,6 +28,7 @@ class DeviceData:
             self.X = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).to(self.device)
         self.n, self.d = self.X.shape
         self.classification = bool(classification)
+        self.y_is_numeric = True
         y_np = y.cpu().numpy() if isinstance(y, torch.Tensor) else np.asarray(y)
         self.y_host = y_np
         if self.classification:
@@ -46,7 +47,15 @@ class DeviceData:
             self.n_classes = 1
             self.y_enc = None
             self.y_cls = None
-            self.y_reg = torch.from_numpy(y_np.astype(np.float32)).to(self.device)
+            try:
+                y_num = y_np.astype(np.float32)
+                self.y_is_numeric = True
+            except (ValueError, TypeError):
+                # non-numeric target under a regressor / unsupervised estimator: keep codes so
+                # unsupervised families (PCA) still run; regressors reject it (executor)
+                y_num = np.unique(y_np.astype(str), return_inverse=True)[1].astype(np.float32)
+                self.y_is_numeric = False
+            self.y_reg = torch.from_numpy(y_num).to(self.device)
         self._Xb = None
         self._edges = None
         self.roles = None

@@ -112,6 +112,8 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
         scorer = "score"
     else:
         scorer = scoring_mod.validate_scoring(spec.scoring, clf)
+    if not clf and not self_scored and not getattr(data, "y_is_numeric", True):
+        raise ValueError(f"{spec.model_type} needs a numeric target column; this target is categorical")
     tasks, errors = build_tasks(data, spec, candidate_ids)
     keep = spec.keep_models in ("all", "best")
     outputs: Dict[int, FitOutput] = {}

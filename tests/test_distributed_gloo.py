@@ -63,7 +63,19 @@ def _rank_main(rank, world, port, root, outq):
                 ctl.table.wait_finished(resp2["job_id"], timeout=300)
                 st, status2 = ctl.check_status(sid, resp2["job_id"])
                 metrics = ctl.metrics(sid, jid)[1]
-                outq.put(("ok", status, status2, metrics))
+                extra = []
+                for model, grid in [("SVC", {"C": [0.5, 5.0], "kernel": ["rbf", "linear"]}),
+                                    ("KNeighborsClassifier", {"n_neighbors": [3, 9], "weights": ["uniform", "distance"]}),
+                                    ("GradientBoostingClassifier", {"n_estimators": [10, 30]}),
+                                    ("PCA", {"n_components": [1, 2, 3]})]:
+                    b = dict(body, model_details={"model_type": model, "search_type": "GridSearchCV",
+                                                  "hyperparameters": {"base_estimator_params": {},
+                                                                      "search_params": {"param_grid": grid},
+                                                                      "cv_params": {"cv": 5}}})
+                    st, r = ctl.train(sid, b)
+                    ctl.table.wait_finished(r["job_id"], timeout=300)
+                    extra.append((model, ctl.check_status(sid, r["job_id"])[1]))
+                outq.put(("ok", status, status2, metrics, extra))
             except Exception as e:  # pragma: no cover
                 import traceback
 
@@ -107,3 +119,8 @@ def test_two_rank_gridsearch_gloo():
     assert workers <= {"rank0", "rank1"} and len(metrics) == 8
     assert status2["job_status"] == "completed" and len(status2["job_result"]["results"]) == 3
     assert status2["best_result"]["mean_cv_score"] > 0.9
+    for model, st in out[4]:
+        assert st["job_status"] == "completed", (model, st)
+        assert all("cv_scores" in r for r in st["job_result"]["results"]), model
+        if model != "PCA":
+            assert st["best_result"]["mean_cv_score"] > 0.9, (model, st["best_result"])
