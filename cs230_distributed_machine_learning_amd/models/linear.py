@@ -85,7 +85,7 @@ class _Batch:
     def __init__(self, data, tasks: List[FitTask]):
         self.tasks = tasks
         C = data.n_classes
-        col0, K, kind, split, scale, lam, icpt, pen_icpt, tol, max_iter = ([] for _ in range(10))
+        col0, K, kind, split, scale, lam, lam1, icpt, pen_icpt, tol, max_iter = ([] for _ in range(11))
         m = 0
         for t in tasks:
             rp = t.params
@@ -98,7 +98,10 @@ class _Batch:
             n_f = max(1, data.train_counts[t.split])
             col0.append(m); K.append(k); kind.append(kd); split.append(t.split)
             scale.append(1.0 / n_f)
-            lam.append(0.0 if rp["C"] is None else 1.0 / (rp["C"] * n_f))
+            strength = 0.0 if rp["C"] is None else 1.0 / (rp["C"] * n_f)
+            l1r = rp.get("l1_ratio", 0.0)
+            lam.append(strength * (1.0 - l1r))
+            lam1.append(strength * l1r)
             icpt.append(rp["intercept_scaling"] if rp["fit_intercept"] else 0.0)
             pen_icpt.append(1.0 if rp["penalize_intercept"] else 0.0)
             tol.append(rp["tol"]); max_iter.append(rp["max_iter"])
@@ -112,6 +115,8 @@ class _Batch:
         self.col_fit = torch.repeat_interleave(torch.arange(self.F, device=dev), torch.tensor(K, device=dev))
         lam_t = torch.tensor(lam, dtype=torch.float32, device=dev)
         self.lam_col = lam_t[self.col_fit]
+        self.l1_col = torch.tensor(lam1, dtype=torch.float32, device=dev)[self.col_fit]
+        self.has_l1 = any(v > 0 for v in lam1)
         self.icpt_col = torch.tensor(icpt, dtype=torch.float32, device=dev)[self.col_fit]
         self.pen_icpt_col = torch.tensor(pen_icpt, dtype=torch.float32, device=dev)[self.col_fit]
         self.tol = torch.tensor(tol, dtype=torch.float32, device=dev)
@@ -146,10 +151,17 @@ class LogisticFamily(Family):
             penalty = None
         if penalty not in ("l2", None, "l1", "elasticnet"):
             raise ParamError(f"penalty {penalty!r} invalid")
-        if penalty in ("l1", "elasticnet"):
-            if penalty == "l1" and solver not in ("liblinear", "saga"):
+        l1_ratio = 0.0
+        if penalty == "l1":
+            if solver not in ("liblinear", "saga"):
                 raise ParamError(f"Solver {solver} supports only 'l2' or None penalties, got l1 penalty.")
-            raise ParamError(f"penalty={penalty!r} is not implemented on the device solver yet")
+            l1_ratio = 1.0
+        elif penalty == "elasticnet":
+            if solver != "saga":
+                raise ParamError(f"Only 'saga' solver supports elasticnet penalty, got solver={solver}.")
+            if p["l1_ratio"] is None:
+                raise ParamError("l1_ratio must be specified when penalty is elasticnet.")
+            l1_ratio = as_float(p["l1_ratio"], "l1_ratio", lo=0.0, hi=1.0)
         if penalty is None and solver == "liblinear":
             raise ParamError("penalty=None is not supported for the liblinear solver")
         C = as_float(p["C"], "C", lo=0.0)
@@ -163,6 +175,7 @@ class LogisticFamily(Family):
             warn.append("dual=True solved in the primal (same optimum)")
         return {
             "C": None if penalty is None else C,
+            "l1_ratio": l1_ratio,
             "tol": as_float(p["tol"], "tol", lo=0.0),
             "max_iter": as_int(p["max_iter"], "max_iter", lo=0),
             "fit_intercept": as_bool(p["fit_intercept"], "fit_intercept"),
@@ -205,59 +218,92 @@ class LogisticFamily(Family):
         return f, G
 
     def _solve(self, data, b: _Batch):
+        """Batched L-BFGS; columns with an L1 term use OWL-QN (Andrew & Gao 2007):
+        pseudo-gradient, orthant-constrained direction and line search.  Columns without
+        L1 reduce exactly to plain L-BFGS."""
         d, dev = data.d, data.device
         W = torch.zeros((d + 1, b.M), dtype=torch.float32, device=dev)
         f, G = self._objective(data, b, W)
+        l1 = None
+        if b.has_l1:
+            l1 = b.l1_col.view(1, -1).repeat(d + 1, 1)
+            l1[d] = l1[d] * b.pen_icpt_col                     # intercept: L1 only when penalised (liblinear)
+            l1on = l1 > 0
+
+        def total(fv, Wv):
+            return fv if l1 is None else fv + b.segsum((l1 * Wv.abs()).sum(0)).double()
+
+        def pseudo(Wv, Gv):
+            if l1 is None:
+                return Gv
+            gp, gm = Gv + l1, Gv - l1
+            at0 = torch.where(gp < 0, gp, torch.where(gm > 0, gm, torch.zeros_like(Gv)))
+            return torch.where(Wv != 0, Gv + l1 * torch.sign(Wv), at0)
+
+        F = total(f, W)
+        PG = pseudo(W, G)
         hs, hy, hrho = [], [], []
         iters = torch.zeros(b.F, dtype=torch.int64, device=dev)
         stalled = torch.zeros(b.F, dtype=torch.bool, device=dev)
         max_it = int(b.max_iter.max().item()) if b.F else 0
         n_evals = 1
         for it in range(max_it):
-            gmax = b.segmax(G.abs().amax(0))
+            gmax = b.segmax(PG.abs().amax(0))
             active = (gmax > b.tol) & (iters < b.max_iter) & ~stalled
             if not bool(active.any()):
                 break
             act_col = active[b.col_fit].to(W.dtype)
-            q = G.clone()
+            q = PG.clone()
             alphas = []
-            for s, y, rho in zip(reversed(hs), reversed(hy), reversed(hrho)):
-                a = rho * b.segsum((s * q).sum(0))
-                q -= a[b.col_fit] * y
+            for s_, y_, rho in zip(reversed(hs), reversed(hy), reversed(hrho)):
+                a = rho * b.segsum((s_ * q).sum(0))
+                q -= a[b.col_fit] * y_
                 alphas.append(a)
             if hs:
                 sy = b.segsum((hs[-1] * hy[-1]).sum(0))
                 yy = b.segsum((hy[-1] * hy[-1]).sum(0))
                 gamma = torch.where(yy > 0, sy / yy.clamp_min(1e-30), torch.ones_like(yy))
             else:
-                gnorm = b.segsum((G * G).sum(0)).sqrt()
+                gnorm = b.segsum((PG * PG).sum(0)).sqrt()
                 gamma = 1.0 / gnorm.clamp_min(1.0)
             r = q * gamma[b.col_fit]
-            for (s, y, rho), a in zip(zip(hs, hy, hrho), reversed(alphas)):
-                bb = rho * b.segsum((y * r).sum(0))
-                r += (a - bb)[b.col_fit] * s
+            for (s_, y_, rho), a in zip(zip(hs, hy, hrho), reversed(alphas)):
+                bb = rho * b.segsum((y_ * r).sum(0))
+                r += (a - bb)[b.col_fit] * s_
             p = -r * act_col
-            gtp = b.segsum((G * p).sum(0))
+            if l1 is not None:   # keep the direction in the pseudo-gradient's orthant
+                p = torch.where(l1on & (p * PG >= 0), torch.zeros_like(p), p)
+            gtp = b.segsum((PG * p).sum(0))
             bad = (gtp >= 0) & active
             if bool(bad.any()):  # not a descent direction: restart from steepest descent
                 badc = bad[b.col_fit].to(W.dtype)
-                p = p * (1 - badc) - G * badc * act_col
-                gtp = b.segsum((G * p).sum(0))
+                p = p * (1 - badc) - PG * badc * act_col
+                gtp = b.segsum((PG * p).sum(0))
+            xi = None if l1 is None else torch.where(W != 0, torch.sign(W), torch.sign(-PG))
             step = torch.ones(b.F, dtype=torch.float32, device=dev)
+
+            def trial(stp):
+                Wt = W + p * stp[b.col_fit]
+                if xi is not None:   # orthant projection
+                    Wt = torch.where(l1on & (Wt * xi <= 0), torch.zeros_like(Wt), Wt)
+                return Wt
+
             for _ls in range(30):
-                Wt = W + p * step[b.col_fit]
+                Wt = trial(step)
                 ft, Gt = self._objective(data, b, Wt)
+                Ft = total(ft, Wt)
                 n_evals += 1
-                slack = 1e-7 * f.abs() + 1e-12  # float32 objective: tolerate round-off near the optimum
-                ok = (ft <= f + 1e-4 * step.double() * gtp.double() + slack) | ~active
+                slack = 1e-7 * F.abs() + 1e-12  # float32 objective: tolerate round-off near the optimum
+                dec = b.segsum((PG * (Wt - W)).sum(0)).double()
+                ok = (Ft <= F + 1e-4 * dec + slack) | ~active
                 if bool(ok.all()):
                     break
                 step = torch.where(ok, step, step * 0.5)
             else:
                 stalled |= ~ok
-                okc = ok[b.col_fit].to(W.dtype)
-                Wt = W + p * (step * ok.to(step.dtype))[b.col_fit]
+                Wt = trial(step * ok.to(step.dtype))
                 ft, Gt = self._objective(data, b, Wt)
+                Ft = total(ft, Wt)
                 n_evals += 1
             s_vec = Wt - W
             y_vec = Gt - G
@@ -266,7 +312,8 @@ class LogisticFamily(Family):
             hs.append(s_vec); hy.append(y_vec); hrho.append(rho)
             if len(hs) > self.history:
                 hs.pop(0); hy.pop(0); hrho.pop(0)
-            W, f, G = Wt, ft, Gt
+            W, f, G, F = Wt, ft, Gt, Ft
+            PG = pseudo(W, G)
             iters += active.to(torch.int64)
         return W, iters, n_evals
 

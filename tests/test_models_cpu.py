@@ -207,3 +207,15 @@ def test_column_transformers_are_rejected_with_guidance():
     dd = DeviceData(X, y, True, "cpu")
     res = run_candidates(dd, JobSpec("StandardScaler", [{}], cv=3), [0])
     assert not res[0].ok and "/preprocess" in res[0].error
+
+
+def test_logistic_l1_and_elasticnet_close_to_sklearn():
+    """OWL-QN on the device solver reaches sklearn's liblinear / saga optima."""
+    from sklearn.linear_model import LogisticRegression
+
+    X, y = make_classification(1500, 20, n_informative=6, random_state=0)
+    for grid in ({"C": [0.01, 0.1, 1.0], "penalty": ["l1"], "solver": ["liblinear", "saga"]},
+                 {"C": [0.05, 1.0], "penalty": ["elasticnet"], "solver": ["saga"], "l1_ratio": [0.2, 0.8]}):
+        ours = _ours("LogisticRegression", X, y, True, grid)
+        ref = _ref(LogisticRegression(max_iter=3000), X, y, grid)
+        assert np.abs(ours - ref).max() <= 0.004, (grid, ours, ref)
