@@ -32,6 +32,7 @@ __global__ __launch_bounds__(256) void k_lr_link_grad(const float* __restrict__ 
                                                       const int32_t* __restrict__ kind,
                                                       const int32_t* __restrict__ split,
                                                       const float* __restrict__ scale, int64_t F,
+                                                      const float* __restrict__ cw, int64_t cwC,
                                                       float* __restrict__ R, double* __restrict__ loss) {
   __shared__ double acc[kMaxFitsLds];
   const bool use_lds = F <= kMaxFitsLds;
@@ -51,7 +52,7 @@ __global__ __launch_bounds__(256) void k_lr_link_grad(const float* __restrict__ 
       continue;
     }
     const int yi = y[row];
-    const float s = scale[f];
+    const float s = cw ? scale[f] * cw[(int64_t)f * cwC + yi] : scale[f];   // class weights scale the row
     float l = 0.f;
     if (kind[f] == 1) {  // multinomial softmax over k columns
       float m = z[0];
@@ -105,12 +106,14 @@ extern "C" {
 
 int dml_lr_link_grad(const float* Z, int64_t n, int64_t M, const int32_t* y, const uint8_t* roles,
                      const int32_t* col0, const int32_t* K, const int32_t* kind, const int32_t* split,
-                     const float* scale, int64_t F, float* R, double* loss, hipStream_t st) {
+                     const float* scale, int64_t F, const float* cw, int64_t cwC, float* R, double* loss,
+                     hipStream_t st) {
   if (n <= 0 || F <= 0) return 0;
   if (hipMemsetAsync(loss, 0, F * sizeof(double), st) != hipSuccess) return 1;
   int64_t blocks = (n * F + 255) / 256;
   if (blocks > 256 * 32) blocks = 256 * 32;
-  k_lr_link_grad<<<(unsigned)blocks, 256, 0, st>>>(Z, n, M, y, roles, col0, K, kind, split, scale, F, R, loss);
+  k_lr_link_grad<<<(unsigned)blocks, 256, 0, st>>>(Z, n, M, y, roles, col0, K, kind, split, scale, F, cw, cwC, R,
+                                                   loss);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

@@ -40,7 +40,7 @@ _LR_DEFAULTS = {
 _SOLVERS = ("lbfgs", "liblinear", "newton-cg", "newton-cholesky", "sag", "saga")
 
 
-def link_grad_torch(Z: torch.Tensor, y: torch.Tensor, roles: torch.Tensor, col0, K, kind, split, scale):
+def link_grad_torch(Z: torch.Tensor, y: torch.Tensor, roles: torch.Tensor, col0, K, kind, split, scale, cw=None):
     """Reference (CPU) implementation of the fused kernel: returns (R, loss[F]).
 
     Vectorised over fits sharing a (link kind, width) so a batch costs a handful of
@@ -73,10 +73,29 @@ def link_grad_torch(Z: torch.Tensor, y: torch.Tensor, roles: torch.Tensor, col0,
                 tgt = torch.nn.functional.one_hot(yl, k).to(Z.dtype).unsqueeze(1).expand(n, len(fits), k)
             r = torch.sigmoid(z) - tgt
             l = torch.nn.functional.softplus(torch.where(tgt > 0.5, -z, z)).sum(2)
+        if cw is not None:   # per-row class weight of each fit (sample weights by class)
+            m = m * cw[fi][:, yl].t().to(Z.dtype)
         r = r * (m * s).unsqueeze(2)
         R[:, cols.flatten()] = r.reshape(n, -1)
         loss[fi] = (l.double() * m.double()).sum(0) * s.squeeze(0).double()
     return R, loss
+
+
+def class_weight_vector(data, split: int, cw):
+    """sklearn ``compute_class_weight`` on the split's training rows (None: unweighted)."""
+    if cw is None:
+        return None
+    C = data.n_classes
+    w = torch.ones(C, dtype=torch.float64, device=data.device)
+    if cw == "balanced":
+        yt = data.y_cls[data.train_rows[split].long()].long()
+        cnt = torch.bincount(yt, minlength=C).double()
+        return torch.where(cnt > 0, yt.numel() / (C * cnt.clamp_min(1)), w)
+    lookup = {str(c): i for i, c in enumerate(np.asarray(data.classes).tolist())}
+    for k, v in cw.items():
+        if str(k) in lookup:
+            w[lookup[str(k)]] = float(v)
+    return w
 
 
 class _Batch:
@@ -85,7 +104,8 @@ class _Batch:
     def __init__(self, data, tasks: List[FitTask]):
         self.tasks = tasks
         C = data.n_classes
-        col0, K, kind, split, scale, lam, lam1, icpt, pen_icpt, tol, max_iter = ([] for _ in range(11))
+        col0, K, kind, split, scale, lam, lam1, icpt, pen_icpt, tol, max_iter, cws = ([] for _ in range(12))
+        any_cw = False
         m = 0
         for t in tasks:
             rp = t.params
@@ -96,6 +116,11 @@ class _Batch:
             else:
                 k, kd = C, KIND_SOFTMAX
             n_f = max(1, data.train_counts[t.split])
+            cwv = class_weight_vector(data, t.split, rp.get("class_weight"))
+            if cwv is not None:
+                n_f = float(cwv[data.y_cls[data.train_rows[t.split].long()].long()].sum())   # sw_sum
+                any_cw = True
+            cws.append(cwv)
             col0.append(m); K.append(k); kind.append(kd); split.append(t.split)
             scale.append(1.0 / n_f)
             strength = 0.0 if rp["C"] is None else 1.0 / (rp["C"] * n_f)
@@ -117,6 +142,10 @@ class _Batch:
         self.lam_col = lam_t[self.col_fit]
         self.l1_col = torch.tensor(lam1, dtype=torch.float32, device=dev)[self.col_fit]
         self.has_l1 = any(v > 0 for v in lam1)
+        self.cw = None
+        if any_cw:
+            ones = torch.ones(C if C > 2 else 2, dtype=torch.float32, device=dev)
+            self.cw = torch.stack([ones if v is None else v.float() for v in cws]).contiguous()   # [F, C]
         self.icpt_col = torch.tensor(icpt, dtype=torch.float32, device=dev)[self.col_fit]
         self.pen_icpt_col = torch.tensor(pen_icpt, dtype=torch.float32, device=dev)[self.col_fit]
         self.tol = torch.tensor(tol, dtype=torch.float32, device=dev)
@@ -169,13 +198,17 @@ class LogisticFamily(Family):
             raise ParamError("Penalty term must be positive")
         mc = p["multi_class"]
         ovr = solver == "liblinear" or mc == "ovr"
-        if p["class_weight"] not in (None, "None"):
-            warn.append("class_weight is not supported yet; fitted unweighted")
+        cw = p["class_weight"]
+        if cw in ("None",):
+            cw = None
+        if cw is not None and cw != "balanced" and not isinstance(cw, dict):
+            raise ParamError("class_weight must be None, 'balanced' or a dict")
         if as_bool(p["dual"], "dual"):
             warn.append("dual=True solved in the primal (same optimum)")
         return {
             "C": None if penalty is None else C,
             "l1_ratio": l1_ratio,
+            "class_weight": cw,
             "tol": as_float(p["tol"], "tol", lo=0.0),
             "max_iter": as_int(p["max_iter"], "max_iter", lo=0),
             "fit_intercept": as_bool(p["fit_intercept"], "fit_intercept"),
@@ -202,12 +235,13 @@ class LogisticFamily(Family):
             lib = native.hip_lib()
             rc = lib.dml_lr_link_grad(native.ptr(Z), data.n, b.M, native.ptr(data.y_cls), native.ptr(data.roles),
                                       native.ptr(b.col0), native.ptr(b.K), native.ptr(b.kind), native.ptr(b.split),
-                                      native.ptr(b.scale), b.F, native.ptr(R), native.ptr(loss),
-                                      native.stream_handle(data.device))
+                                      native.ptr(b.scale), b.F, native.ptr(b.cw), int(b.cw.shape[1]) if b.cw is not None
+                                      else 0, native.ptr(R), native.ptr(loss), native.stream_handle(data.device))
             if rc:
                 raise RuntimeError("dml_lr_link_grad failed")
         else:
-            R, loss = link_grad_torch(Z, data.y_cls, data.roles, b.col0_l, b.K_l, b.kind_l, b.split_l, b.scale.tolist())
+            R, loss = link_grad_torch(Z, data.y_cls, data.roles, b.col0_l, b.K_l, b.kind_l, b.split_l, b.scale.tolist(),
+                                      b.cw)
         G = torch.empty_like(W)
         G[:d] = X.t() @ R
         G[d] = R.sum(0) * b.icpt_col
@@ -398,7 +432,10 @@ class LogisticFamily(Family):
             Xt, yt = X[tr], y[tr]
             n, d = Xt.shape
             fi = rp["fit_intercept"]
-            lam = 0.0 if rp["C"] is None else 1.0 / (rp["C"] * n)
+            cwv = class_weight_vector(data, t.split, rp.get("class_weight"))
+            sw = np.ones(n) if cwv is None else cwv.cpu().numpy()[yt]
+            sw_sum = float(sw.sum())
+            lam = 0.0 if rp["C"] is None else 1.0 / (rp["C"] * sw_sum)
             K = 1 if C_cls == 2 else C_cls
             if K == 1:
                 tgt = (yt == 1).astype(np.float64)
@@ -411,13 +448,13 @@ class LogisticFamily(Family):
                 Z = Xt @ coef.T + (W[:, d] if fi else 0.0)
                 if K == 1:
                     z = Z[:, 0]
-                    loss = np.sum(np.logaddexp(0, z) - tgt * z) / n
-                    r = (1.0 / (1.0 + np.exp(-z)) - tgt)[:, None] / n
+                    loss = np.sum(sw * (np.logaddexp(0, z) - tgt * z)) / sw_sum
+                    r = (sw * (1.0 / (1.0 + np.exp(-z)) - tgt))[:, None] / sw_sum
                 else:
                     m = Z.max(1, keepdims=True)
                     lse = m[:, 0] + np.log(np.exp(Z - m).sum(1))
-                    loss = np.sum(lse - (Z * tgt).sum(1)) / n
-                    r = (np.exp(Z - lse[:, None]) - tgt) / n
+                    loss = np.sum(sw * (lse - (Z * tgt).sum(1))) / sw_sum
+                    r = sw[:, None] * (np.exp(Z - lse[:, None]) - tgt) / sw_sum
                 loss += 0.5 * lam * np.sum(coef * coef)
                 G = np.empty_like(W)
                 G[:, :d] = r.T @ Xt + lam * coef

@@ -160,8 +160,8 @@ def hip_lib() -> ctypes.CDLL:
 def _register_optional(lib) -> None:
     """Signatures of kernels added in later files (absent symbols are skipped)."""
     table = {
-        "dml_lr_link_grad": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
-                                     c_vp]),
+        "dml_lr_link_grad": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
+                                     c_vp, c_vp, c_vp]),
         "dml_lr_predict": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
         "dml_knn": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, ctypes.c_float, c_i32, c_vp,
                             c_vp, c_vp]),

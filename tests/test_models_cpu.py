@@ -219,3 +219,13 @@ def test_logistic_l1_and_elasticnet_close_to_sklearn():
         ours = _ours("LogisticRegression", X, y, True, grid)
         ref = _ref(LogisticRegression(max_iter=3000), X, y, grid)
         assert np.abs(ours - ref).max() <= 0.004, (grid, ours, ref)
+
+
+def test_logistic_class_weight_matches_sklearn():
+    from sklearn.linear_model import LogisticRegression
+
+    X, y = make_classification(3000, 10, weights=[0.85], random_state=1)
+    for grid in ({"C": [0.1, 1.0], "class_weight": [None, "balanced", {0: 3.0, 1: 1.0}]},
+                 {"C": [0.1], "class_weight": ["balanced"], "solver": ["liblinear", "saga"]}):
+        np.testing.assert_allclose(_ours("LogisticRegression", X, y, True, grid),
+                                   _ref(LogisticRegression(max_iter=3000), X, y, grid), atol=1e-3)

@@ -98,7 +98,7 @@ def test_lr_link_grad_kernel_matches_torch():
     # keep every argument tensor alive across the asynchronous launch
     args = [i32(col0), i32(K), i32(kind), i32(split), torch.tensor(scale, dtype=torch.float32, device="cuda:0")]
     rc = lib.dml_lr_link_grad(native.ptr(Z), n, m, native.ptr(ycls), native.ptr(dd.roles),
-                              *[native.ptr(a) for a in args], len(kinds), native.ptr(R), native.ptr(loss),
+                              *[native.ptr(a) for a in args], len(kinds), 0, 0, native.ptr(R), native.ptr(loss),
                               native.stream_handle())
     torch.cuda.synchronize()
     assert rc == 0
