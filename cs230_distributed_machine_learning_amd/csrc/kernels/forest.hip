@@ -31,6 +31,9 @@
 #ifndef DML_RPT_BLOCK
 #define DML_RPT_BLOCK 1
 #endif
+#ifndef DML_BLOCK_NT
+#define DML_BLOCK_NT 256     // threads per block-tier node
+#endif
 #ifndef DML_NODES_WPE
 #define DML_NODES_WPE 4
 #endif
@@ -603,6 +606,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   constexpr int NW = NT / 64;
   constexpr int RPT = NT == 64 ? 4 : DML_RPT_BLOCK;   // rows per thread in registers (<= 4: packed u8 x 4)
   static_assert(RPT >= 1 && RPT <= 4, "RPT");
+  static_assert(2 * RPT * (NT / 64) <= 32, "Scratch::wcnt too small for this NT x RPT");
   constexpr int KGMAX = NT == 64 ? DML_KGMAX_WAVE : 16;   // feature-group bound (register-resident bins)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   PH_BEGIN
@@ -1523,7 +1527,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     if (need > 64 * 1024 && need > attr_set[MODE]) {
       HIP_OK(hipFuncSetAttribute((const void*)k_subtree<REG>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_nodes<64, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<256, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<DML_BLOCK_NT, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_hist_large<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_split_large<GM>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       attr_set[MODE] = need;
@@ -1551,7 +1555,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     }
     if (ns) k_subtree<REG><<<ns, 64, lds_s, s0>>>(c, cur);
     if (nw) k_nodes<64, MODE><<<nw, 64, lds_w, s1>>>(c, 1, cur);
-    if (nb) k_nodes<256, MODE><<<nb, 256, lds_b, s2>>>(c, 2, cur);
+    if (nb) k_nodes<DML_BLOCK_NT, MODE><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur);
     if (nL) {
       k_large_prep<<<nL, 64, 0, st>>>(c, cur, nL);
       while (true) {

@@ -161,11 +161,70 @@ __global__ __launch_bounds__(256) void k_apply(const uint8_t* __restrict__ Xb, i
   leaf[(int64_t)t * n + row] = node;
 }
 
+// ---- sklearn-style split thresholds -------------------------------------------------
+// A histogram split "bin <= b_lo" equals sklearn's "x <= (x_left_max + x_right_min) / 2"
+// on the training rows; held-out rows between the two values are routed like sklearn
+// only if the threshold sits at the midpoint.  For features whose bins are exact values
+// (<= 256 distinct), pass 1 finds b_hi = min bin among each internal node's right-going
+// in-bag training rows, pass 2 moves the split bin to the last bin value <= midpoint.
+__global__ __launch_bounds__(256) void k_refine_hi(const uint8_t* __restrict__ Xb, int64_t ld, int64_t n,
+                                                   const NodeRec* __restrict__ nodes,
+                                                   const TreeSpec* __restrict__ specs,
+                                                   const uint8_t* __restrict__ roles, uint32_t* hi) {
+  const int t = blockIdx.y;
+  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (row >= n) return;
+  const TreeSpec& s = specs[t];
+  if (roles[(int64_t)s.split * n + row] != 1 || boot_weight(s, (uint32_t)row) == 0) return;
+  const uint8_t* xr = Xb + row * ld;
+  int node = t;
+  NodeRec nr = nodes[node];
+  for (int steps = 0; nr.split >= 0 && steps < 1 << 20; ++steps) {
+    const uint32_t b = xr[nr.split >> 8];
+    if (b > (uint32_t)(nr.split & 255)) {
+      if (b < hi[node]) atomicMin(&hi[node], b);
+      node = nr.left + 1;
+    } else {
+      node = nr.left;
+    }
+    nr = nodes[node];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_refine_split(NodeRec* nodes, int64_t P, const uint32_t* __restrict__ hi,
+                                                      const float* __restrict__ vals, const uint8_t* __restrict__ exact) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= P) return;
+  const NodeRec nr = nodes[i];
+  if (nr.split < 0) return;
+  const int f = nr.split >> 8, blo = nr.split & 255;
+  const uint32_t bhi = hi[i];
+  if (!exact[f] || bhi > 255u || (int)bhi <= blo) return;
+  const float* v = vals + (int64_t)f * 256;
+  double m = (double)v[blo] / 2.0 + (double)v[bhi] / 2.0;
+  if (m == (double)v[bhi] || !(m == m)) m = (double)v[blo];
+  int b = blo;
+  while (b + 1 < (int)bhi && (double)v[b + 1] <= m) ++b;
+  nodes[i].split = f * 256 + b;
+}
+
 }  // namespace dml
 
 using namespace dml;
 
 extern "C" {
+
+int dml_forest_refine(const uint8_t* Xb, int64_t ld, int64_t n, NodeRec* nodes, int64_t P, const TreeSpec* specs,
+                      int32_t T, const uint8_t* roles, const float* vals, const uint8_t* exact, uint32_t* hi,
+                      hipStream_t st) {
+  if (P <= 0 || T <= 0) return 0;
+  if (hipMemsetAsync(hi, 0xFF, (size_t)P * 4, st) != hipSuccess) return 1;
+  dim3 g1((unsigned)((n + 255) / 256), (unsigned)T);
+  k_refine_hi<<<g1, 256, 0, st>>>(Xb, ld, n, nodes, specs, roles, hi);
+  k_refine_split<<<(unsigned)((P + 255) / 256), 256, 0, st>>>(nodes, P, hi, vals, exact);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 
 int dml_forest_apply(const uint8_t* Xb, int64_t ld, int64_t n, const dml::NodeRec* nodes, int32_t t0, int32_t T,
                      int32_t* leaf, hipStream_t st) {

@@ -278,6 +278,44 @@ void dml_cpu_forest_apply(const uint8_t* Xb, int64_t ld, int64_t n, const NodeRe
     }
 }
 
+// sklearn midpoint thresholds for exactly-binned features (same two passes as predict.hip)
+void dml_cpu_forest_refine(const uint8_t* Xb, int64_t ld, int64_t n, NodeRec* nodes, int64_t P, const TreeSpec* specs,
+                           int32_t T, const uint8_t* roles, const float* vals, const uint8_t* exact) {
+  std::vector<uint32_t> hi((size_t)P, 0xFFFFFFFFu);
+  for (int32_t t = 0; t < T; ++t) {
+    const TreeSpec& s = specs[t];
+    for (int64_t r = 0; r < n; ++r) {
+      if (roles[(int64_t)s.split * n + r] != 1 || boot_weight(s, (uint32_t)r) == 0) continue;
+      const uint8_t* xr = Xb + r * ld;
+      int node = t;
+      NodeRec nr = nodes[node];
+      while (nr.split >= 0) {
+        const uint32_t b = xr[nr.split >> 8];
+        if (b > (uint32_t)(nr.split & 255)) {
+          if (b < hi[node]) hi[node] = b;
+          node = nr.left + 1;
+        } else {
+          node = nr.left;
+        }
+        nr = nodes[node];
+      }
+    }
+  }
+  for (int64_t i = 0; i < P; ++i) {
+    const NodeRec nr = nodes[i];
+    if (nr.split < 0) continue;
+    const int f = nr.split >> 8, blo = nr.split & 255;
+    const uint32_t bhi = hi[i];
+    if (!exact[f] || bhi > 255u || (int)bhi <= blo) continue;
+    const float* v = vals + (int64_t)f * 256;
+    double m = (double)v[blo] / 2.0 + (double)v[bhi] / 2.0;
+    if (m == (double)v[bhi] || !(m == m)) m = (double)v[blo];
+    int b = blo;
+    while (b + 1 < (int)bhi && (double)v[b + 1] <= m) ++b;
+    nodes[i].split = f * 256 + b;
+  }
+}
+
 void dml_cpu_forest_free(void* h) { delete (CpuForest*)h; }
 
 // predict rows (same accumulation order as predict.hip)

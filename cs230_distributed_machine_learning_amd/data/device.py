@@ -83,6 +83,27 @@ class DeviceData:
             self._XT = self.X.t().contiguous()
         return self._XT
 
+    def bin_values(self):
+        """(values float32 [d, 256], exact uint8 [d]): the value each bin stands for, and
+        whether EVERY row's value equals its bin's value (features with <= 256 distinct
+        values).  Used to place split thresholds at sklearn's midpoints."""
+        if getattr(self, "_binvals", None) is None:
+            Xb = self.binned()
+            E = self._edges
+            finite = torch.isfinite(E)
+            k = finite.sum(1)                                          # finite edges per feature
+            V = torch.full((self.d, 256), float("inf"), dtype=torch.float32, device=self.device)
+            V[:, :255] = torch.where(finite, E, V[:, :255])
+            V[torch.arange(self.d, device=self.device), k] = self.X.max(0).values
+            exact = torch.ones(self.d, dtype=torch.bool, device=self.device)
+            step = max(1, (1 << 24) // max(1, self.d))
+            for s0 in range(0, self.n, step):
+                xb = Xb[s0:s0 + step].long()
+                got = torch.gather(V, 1, xb.t()).t()
+                exact &= (got == self.X[s0:s0 + step]).all(0)
+            self._binvals = (V.contiguous(), exact.to(torch.uint8).contiguous())
+        return self._binvals
+
     @property
     def edges(self):
         self.binned()

@@ -36,7 +36,7 @@ import torch
 from ..ops import forest_ops
 from ..utils import native
 from .base import Family, FitOutput, FitTask, ParamError, as_bool, as_float, as_int, register, seed_of
-from .forest import _count_param, native_seed
+from .forest import _count_param, _refine, native_seed
 
 _CLS = "GradientBoostingClassifier"
 _REG = "GradientBoostingRegressor"
@@ -282,10 +282,12 @@ class GradientBoostingFamily(Family):
                     specs[j]["min_impurity_decrease"] = rp["min_impurity_decrease"]
             if gpu:
                 fb = forest_ops.build_gpu(Xb, None, tgt, roles_t, specs, 1, True, self.tiers, ystride=n)
+                _refine(data, fb, Xb, specs, roles_t)
                 leaf = forest_ops.apply(fb, Xb).long()                     # [J, n]
                 vals = fb.vals
             else:
                 fb = forest_ops.build_cpu(Xb_host, None, tgt.numpy(), roles_t.numpy(), specs, 1, True, ystride=n)
+                _refine(data, fb, Xb, specs, roles_t)
                 leaf = torch.from_numpy(forest_ops.apply(fb, Xb_host)).long()
                 vals = torch.from_numpy(fb.vals)
             P = vals.shape[0]

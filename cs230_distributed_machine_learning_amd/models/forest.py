@@ -205,6 +205,7 @@ class ForestFamily(Family):
         else:
             fb = forest_ops.build_cpu(Xb.numpy(), data.y_enc, None if not is_reg else data.y_reg.numpy(),
                                       data.roles_np(), specs, data.n_classes, is_reg)
+        _refine(data, fb, Xb, specs, data.roles)
         toff = np.zeros(len(batch) + 1, dtype=np.int64)
         np.cumsum([t.params["n_estimators"] for t in batch], out=toff[1:])
         rows = [data.test_rows[t.split] for t in batch]
@@ -230,6 +231,18 @@ class ForestFamily(Family):
                 o.model = extract_forest(fb, int(toff[f]), int(toff[f + 1]), data, t)
             outs.append(o)
         return outs
+
+
+def _refine(data, fb, Xb, specs, roles) -> None:
+    """sklearn midpoint thresholds where the binning is exact (no-op on quantile-binned data)."""
+    vals, exact = data.bin_values()
+    if not bool(exact.any()):
+        return
+    if data.is_gpu:
+        forest_ops.refine_thresholds(fb, Xb, specs, roles, vals, exact)
+    else:
+        forest_ops.refine_thresholds(fb, Xb.numpy(), specs, roles.numpy() if isinstance(roles, torch.Tensor) else roles,
+                                     vals.numpy(), exact.numpy())
 
 
 def native_seed(base: int, tree: int) -> int:

@@ -187,6 +187,29 @@ def build_cpu(Xb: np.ndarray, ycls: Optional[np.ndarray], yreg: Optional[np.ndar
     return ForestBuild(nodes, vals, T, VC, is_reg, n_classes, {"nodes": int(P), "build_s": time.perf_counter() - t0})
 
 
+def refine_thresholds(fb: ForestBuild, Xb, specs: np.ndarray, roles, vals, exact) -> None:
+    """Move split bins to sklearn's midpoint thresholds on exactly-binned features (in place)."""
+    T = len(specs)
+    P = int(fb.nodes.shape[0])
+    if fb.on_gpu:
+        dev = Xb.device
+        specs_dev = torch.from_numpy(specs.view(np.uint8).copy()).to(dev)
+        hi = torch.empty(P, dtype=torch.int32, device=dev)
+        rc = native.hip_lib().dml_forest_refine(native.ptr(Xb), Xb.stride(0), Xb.shape[0], native.ptr(fb.nodes), P,
+                                                native.ptr(specs_dev), T, native.ptr(roles), native.ptr(vals),
+                                                native.ptr(exact), native.ptr(hi), native.stream_handle(dev))
+        if rc:
+            raise RuntimeError("dml_forest_refine failed")
+        torch.cuda.current_stream(dev).synchronize()   # keep specs_dev / hi alive until done
+        return
+    Xb_np = np.ascontiguousarray(Xb)
+    roles_np = np.ascontiguousarray(roles, dtype=np.uint8)
+    specs_c = np.ascontiguousarray(specs)
+    native.cpu_lib().dml_cpu_forest_refine(native.ptr(Xb_np), Xb_np.shape[1], Xb_np.shape[0], native.ptr(fb.nodes), P,
+                                           native.ptr(specs_c), T, native.ptr(roles_np), native.ptr(vals),
+                                           native.ptr(exact))
+
+
 def apply(fb: ForestBuild, Xb, t0: int = 0, T: Optional[int] = None):
     """Leaf node index of every row for trees t0..t0+T-1: int32 [T, n]."""
     T = fb.n_trees - t0 if T is None else T

@@ -99,6 +99,7 @@ def cpu_lib() -> ctypes.CDLL:
             lib.dml_cpu_forest_build.argtypes = [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64,
                                                  c_i64]
             lib.dml_cpu_forest_apply.argtypes = [c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp]
+            lib.dml_cpu_forest_refine.argtypes = [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp]
             lib.dml_cpu_forest_num_nodes.restype = c_i64
             lib.dml_cpu_forest_num_nodes.argtypes = [c_vp]
             lib.dml_cpu_forest_export.argtypes = [c_vp, c_vp, c_vp]
@@ -168,6 +169,7 @@ def _register_optional(lib) -> None:
         "dml_knn_qpw": (c_i32, []),
         "dml_forest_apply": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp]),
         "dml_svm_sizeof_prob": (c_i32, []),
+        "dml_forest_refine": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
         "dml_svm_smo": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     }
     for name, (res, args) in table.items():

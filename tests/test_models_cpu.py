@@ -100,7 +100,8 @@ def test_gbrt_grid_close_to_sklearn():
     grid = {"n_estimators": [20, 50], "learning_rate": [0.1, 0.5]}
     ours = _ours("GradientBoostingClassifier", X, y, True, grid)
     ref = _ref(GradientBoostingClassifier(random_state=0), X, y, grid)
-    assert np.abs(ours - ref).max() < 0.03
+    # exact-value bins + sklearn midpoint thresholds: only equal-gain feature ties differ
+    assert np.abs(ours - ref).max() < 0.01
 
 
 def test_gbrt_subsample_runs():
