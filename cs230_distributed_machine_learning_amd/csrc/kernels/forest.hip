@@ -920,11 +920,16 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   const TreeSpec& s = c.specs[on.tree];
   const int lane = threadIdx.x;
   const int d = c.d;
+  const int VC = c.VC;
   const bool cache = c.sub_cache_d > 0;
   const int dp = c.sub_cache_d;
+  // LDS: DFS stack, per-entry channel sums (no global re-reads of node stats), left
+  // child sums, row-bin cache
   SubEntry* stack = (SubEntry*)smem;
-  double* left_ch = (double*)(stack + 64);
-  uint8_t* xc = (uint8_t*)(left_ch + ((c.VC + 1) & ~1));
+  double* sstats = (double*)(stack + 64);            // [64][VC]
+  double* left_ch = sstats + 64 * VC;                // [VC]
+  double* right_ch = left_ch + VC;                   // [VC] (+ pad)
+  uint8_t* xc = (uint8_t*)(left_ch + ((2 * VC + 1) & ~1));
   const int cnt0 = on.count;
   const uint32_t* rows = c.rows_cur + c.row_off[on.tree] + on.start;
   uint32_t row = 0;
@@ -939,17 +944,38 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   const uint8_t* xg = c.Xb + (int64_t)row * c.ld;
   if (cache && lane < cnt0)
     for (int j = 0; j < d; ++j) xc[lane * dp + j] = xg[j];
+  // a subtree over cnt0 rows has at most cnt0 - 1 splits: reserve all node pairs with ONE
+  // pool atomic (unused pairs stay unreferenced)
+  int pool_base = 0;
+  int max_splits = cnt0 / max(1, s.min_samples_leaf) - 1;       // leaves <= rows / min_samples_leaf
+  {
+    const int levels_left = s.max_depth - on.depth;
+    if (levels_left < 30) max_splits = min(max_splits, (1 << max(0, levels_left)) - 1);
+    max_splits = max(0, max_splits);
+  }
   if (lane == 0) {
+    const int want = 2 * max_splits;
+    pool_base = want > 0 ? atomicAdd(&c.counters[kPool], want) : 0;
+    if (want > 0 && (int64_t)pool_base + want > c.pool_cap) {
+      atomicOr(&c.counters[kOverflow], 1);
+      pool_base = -1;
+    }
     SubEntry e;
     e.mask = cnt0 >= 64 ? ~0ull : ((1ull << cnt0) - 1ull);
     e.key = on.key; e.node = on.node; e.depth = on.depth;
     stack[0] = e;
   }
+  if (lane < VC) sstats[lane] = c.node_val[(int64_t)on.node * VC + lane];
+  const double Wt = c.tree_W[on.tree];
+  pool_base = wave::bcast<int>(pool_base, 0);
+  if (pool_base < 0) return;
+  int used = 0;
   wave_lds_sync();
   int sp = 1;
   while (sp > 0) {
     --sp;
     const SubEntry e = stack[sp];
+    const double* pv = sstats + sp * VC;
     const int cnt = __popcll(e.mask);
     int nonconst = 0, best_f = -1, best_b = -1;
     double best_g = -INFINITY;
@@ -975,7 +1001,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     const uint64_t lm = __ballot(in && mybin <= best_b) & e.mask;
     const uint64_t rm = e.mask & ~lm;
     // left child statistics (class weights / regression sums) by wave reductions
-    for (int k = 0; k < c.VC; ++k) {
+    for (int k = 0; k < VC; ++k) {
       double v;
       const bool inl = (lm >> lane) & 1ull;
       if constexpr (REG) {
@@ -984,31 +1010,51 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
         v = (inl && my_cls == k) ? (double)my_w : 0.0;
       }
       v = wave::sum<double>(v, lane);
-      if (lane == 0) left_ch[k] = v;
+      if (lane == 0) { left_ch[k] = v; right_ch[k] = pv[k] - v; }
     }
     wave_lds_sync();
     int base = -1;
-    if (lane == 0) {
-      if (accept_split(c, s, e.node, on.tree, left_ch)) base = make_children(c, e.node, best_f, best_b, left_ch);
+    if (lane == 0 && accept_split_v(c, s, pv, Wt, left_ch) && used < max_splits) {
+      base = pool_base + 2 * used;
+      NodeRec leaf; leaf.split = -1; leaf.left = -1;
+      c.nodes[base] = leaf;
+      c.nodes[base + 1] = leaf;
+      double* lv = c.node_val + (int64_t)base * VC;
+      for (int q = 0; q < VC; ++q) {
+        lv[q] = left_ch[q];
+        lv[VC + q] = right_ch[q];
+      }
+      NodeRec rec; rec.split = pack_split(best_f, best_b); rec.left = base;
+      c.nodes[e.node] = rec;
     }
     base = wave::bcast<int>(base, 0);
     if (base < 0) continue;
+    ++used;
     const int nl = __popcll(lm), nr = cnt - nl;
-    // push right then left (left subtree first); leaf-by-count/purity children are not pushed
+    // push right then left (left subtree first); leaf-by-count/purity children are not pushed.
+    // The popped entry's slot `sp` is reused: compute both children's sums before writing.
     if (lane == 0) {
       const int dep = e.depth + 1;
-      if (!leaf_by_counts(s, nr, dep) && node_impurity(c, base + 1, s.criterion) > kEps) {
+      const bool push_r = !leaf_by_counts(s, nr, dep) && impurity_of_vals(c, right_ch, s.criterion) > kEps;
+      const bool push_l = !leaf_by_counts(s, nl, dep) && impurity_of_vals(c, left_ch, s.criterion) > kEps;
+      if (push_r) {
         SubEntry r; r.mask = rm; r.key = child_key(e.key, 1); r.node = base + 1; r.depth = dep;
+        for (int q = 0; q < VC; ++q) sstats[sp * VC + q] = right_ch[q];
         stack[sp++] = r;
       }
-      if (!leaf_by_counts(s, nl, dep) && node_impurity(c, base, s.criterion) > kEps) {
+      if (push_l) {
         SubEntry l; l.mask = lm; l.key = child_key(e.key, 0); l.node = base; l.depth = dep;
+        for (int q = 0; q < VC; ++q) sstats[sp * VC + q] = left_ch[q];
         stack[sp++] = l;
       }
     }
     sp = wave::bcast<int>(sp, 0);
     wave_lds_sync();
   }
+  // reserved-but-unused node pairs become well-formed (unreferenced) leaves, so any
+  // pass over the whole pool sees valid records
+  const NodeRec leaf{-1, -1};
+  for (int i = 2 * used + lane; i < 2 * max_splits; i += 64) c.nodes[pool_base + i] = leaf;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1330,7 +1376,7 @@ static size_t fused_lds(const ForestArgs* a, int KG) {
 
 static size_t sub_lds(const ForestArgs* a) {
   const int VC = a->is_reg ? 3 : (int)a->n_classes;
-  size_t b = 64 * sizeof(SubEntry) + ((VC + 1) & ~1) * 8;
+  size_t b = 64 * sizeof(SubEntry) + (size_t)64 * VC * 8 + ((2 * VC + 1) & ~1) * 8;
   b += (size_t)64 * a->sub_cache_d + 16;
   return b;
 }

@@ -191,12 +191,12 @@ __global__ __launch_bounds__(256) void k_refine_hi(const uint8_t* __restrict__ X
   }
 }
 
-__global__ __launch_bounds__(256) void k_refine_split(NodeRec* nodes, int64_t P, const uint32_t* __restrict__ hi,
+__global__ __launch_bounds__(256) void k_refine_split(NodeRec* nodes, int64_t P, int64_t d, const uint32_t* __restrict__ hi,
                                                       const float* __restrict__ vals, const uint8_t* __restrict__ exact) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= P) return;
   const NodeRec nr = nodes[i];
-  if (nr.split < 0) return;
+  if (nr.split < 0 || (nr.split >> 8) >= d) return;
   const int f = nr.split >> 8, blo = nr.split & 255;
   const uint32_t bhi = hi[i];
   if (!exact[f] || bhi > 255u || (int)bhi <= blo) return;
@@ -214,14 +214,14 @@ using namespace dml;
 
 extern "C" {
 
-int dml_forest_refine(const uint8_t* Xb, int64_t ld, int64_t n, NodeRec* nodes, int64_t P, const TreeSpec* specs,
-                      int32_t T, const uint8_t* roles, const float* vals, const uint8_t* exact, uint32_t* hi,
-                      hipStream_t st) {
+int dml_forest_refine(const uint8_t* Xb, int64_t ld, int64_t n, int64_t d, NodeRec* nodes, int64_t P,
+                      const TreeSpec* specs, int32_t T, const uint8_t* roles, const float* vals, const uint8_t* exact,
+                      uint32_t* hi, hipStream_t st) {
   if (P <= 0 || T <= 0) return 0;
   if (hipMemsetAsync(hi, 0xFF, (size_t)P * 4, st) != hipSuccess) return 1;
   dim3 g1((unsigned)((n + 255) / 256), (unsigned)T);
   k_refine_hi<<<g1, 256, 0, st>>>(Xb, ld, n, nodes, specs, roles, hi);
-  k_refine_split<<<(unsigned)((P + 255) / 256), 256, 0, st>>>(nodes, P, hi, vals, exact);
+  k_refine_split<<<(unsigned)((P + 255) / 256), 256, 0, st>>>(nodes, P, d, hi, vals, exact);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

@@ -195,7 +195,8 @@ def refine_thresholds(fb: ForestBuild, Xb, specs: np.ndarray, roles, vals, exact
         dev = Xb.device
         specs_dev = torch.from_numpy(specs.view(np.uint8).copy()).to(dev)
         hi = torch.empty(P, dtype=torch.int32, device=dev)
-        rc = native.hip_lib().dml_forest_refine(native.ptr(Xb), Xb.stride(0), Xb.shape[0], native.ptr(fb.nodes), P,
+        rc = native.hip_lib().dml_forest_refine(native.ptr(Xb), Xb.stride(0), Xb.shape[0], Xb.shape[1],
+                                                native.ptr(fb.nodes), P,
                                                 native.ptr(specs_dev), T, native.ptr(roles), native.ptr(vals),
                                                 native.ptr(exact), native.ptr(hi), native.stream_handle(dev))
         if rc:

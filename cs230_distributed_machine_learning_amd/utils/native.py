@@ -169,7 +169,8 @@ def _register_optional(lib) -> None:
         "dml_knn_qpw": (c_i32, []),
         "dml_forest_apply": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp]),
         "dml_svm_sizeof_prob": (c_i32, []),
-        "dml_forest_refine": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+        "dml_forest_refine": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
+                                      c_vp]),
         "dml_svm_smo": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     }
     for name, (res, args) in table.items():

@@ -82,9 +82,11 @@ def test_gpu_trees_match_cpu(n, d, C, kw, tiers):
     g = forest_ops.build_gpu(Xb, torch.from_numpy(ycls).to(dev), None, torch.from_numpy(roles).to(dev), specs, C, False,
                              forest_ops.ForestTiers(**TIERS[tiers]))
     c = forest_ops.build_cpu(Xb_cpu, ycls, None, roles, specs, C, False)
-    assert g.stats["nodes"] == c.stats["nodes"]
+    # the GPU pool may hold unreferenced slots (subtree kernels reserve node pairs in bulk):
+    # compare the reachable trees
     gc = _canon(g.nodes.cpu().numpy(), g.vals.cpu().numpy(), len(specs))
     cc = _canon(c.nodes, c.vals, len(specs))
+    assert sum(map(len, gc)) == sum(map(len, cc)) == c.stats["nodes"]
     assert gc == cc
     # predictions identical
     rows, roff = [], [0]
