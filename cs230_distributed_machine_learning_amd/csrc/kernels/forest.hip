@@ -55,8 +55,12 @@ __device__ unsigned long long g_phase[3][8];
 
 namespace dml {
 
+// an open node: its rows are rows_cur[start, start + count) -- `start` is ABSOLUTE (tree
+// offset folded in at enqueue), so a node kernel's first dependent load is its rows
 struct OpenNode {
-  int32_t tree, node, start, count, depth, pad;
+  int32_t tree, node;
+  int64_t start;
+  int32_t count, depth;
   uint64_t key;
 };
 
@@ -158,7 +162,7 @@ __device__ double node_weight(const Ctx& c, int node) {
 }
 
 // decide whether a freshly created node is worth visiting; enqueue it into `set`
-__device__ void enqueue_or_leaf(const Ctx& c, int tree, int node, int start, int count, int depth,
+__device__ void enqueue_or_leaf(const Ctx& c, int tree, int node, int64_t start, int count, int depth,
                                 uint64_t key, int set) {
   const TreeSpec& s = c.specs[tree];
   if (leaf_by_counts(s, count, depth)) return;
@@ -170,7 +174,7 @@ __device__ void enqueue_or_leaf(const Ctx& c, int tree, int node, int start, int
     return;
   }
   OpenNode on;
-  on.tree = tree; on.node = node; on.start = start; on.count = count; on.depth = depth; on.pad = 0;
+  on.tree = tree; on.node = node; on.start = start; on.count = count; on.depth = depth;
   on.key = key;
   c.open[set][tier][idx] = on;
 }
@@ -559,7 +563,7 @@ __device__ double impurity_of_vals(const Ctx& c, const double* v, int crit) {
   return cls_impurity(a, crit);
 }
 
-__device__ void enqueue_or_leaf_v(const Ctx& c, const TreeSpec& s, int tree, int node, int start, int count,
+__device__ void enqueue_or_leaf_v(const Ctx& c, const TreeSpec& s, int tree, int node, int64_t start, int count,
                                   int depth, uint64_t key, int set, const double* vals) {
   if (leaf_by_counts(s, count, depth)) return;
   if (impurity_of_vals(c, vals, s.criterion) <= kEps) return;
@@ -570,7 +574,7 @@ __device__ void enqueue_or_leaf_v(const Ctx& c, const TreeSpec& s, int tree, int
     return;
   }
   OpenNode on;
-  on.tree = tree; on.node = node; on.start = start; on.count = count; on.depth = depth; on.pad = 0;
+  on.tree = tree; on.node = node; on.start = start; on.count = count; on.depth = depth;
   on.key = key;
   c.open[set][tier][idx] = on;
 }
@@ -601,7 +605,8 @@ __device__ __forceinline__ void hist_add(typename HT<MODE>::T* hj, const Ctx& c,
 }
 
 template <int NT, int MODE>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WPE, 8))) void k_nodes(Ctx c, int tier, int set_cur) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WPE, 8))) void k_nodes(Ctx c, int tier, int set_cur,
+                                                                                                   int pair_base) {
   using CT = typename HT<MODE>::T;
   constexpr int NW = NT / 64;
   constexpr int RPT = NT == 64 ? 4 : DML_RPT_BLOCK;   // rows per thread in registers (<= 4: packed u8 x 4)
@@ -638,7 +643,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   }
   RankCache rc;
   if (wid == 0) rc.build(on.key, d, lane);
-  const uint32_t* rows = c.rows_cur + c.row_off[on.tree] + on.start;
+  const uint32_t* rows = c.rows_cur + on.start;
   const float* ty = tree_y(c, s);
   const int cnt = on.count;
   // rows (+ bootstrap weight + label payload) of a <= NT*RPT-row node stay in registers
@@ -754,16 +759,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   }
   // ---- decision (on-chip values only)
   if (tid == 0) {
-    int base = -1;
-    if (sc->best_feat >= 0 && accept_split_v(c, s, pvs, sc->W, best_left)) {
-      base = atomicAdd(&c.counters[kPool], 2);
-      if ((int64_t)base + 2 > c.pool_cap) {
-        atomicOr(&c.counters[kOverflow], 1);
-        base = -1;
-      } else {
-        NodeRec leaf; leaf.split = -1; leaf.left = -1;
-        c.nodes[base] = leaf;
-        c.nodes[base + 1] = leaf;
+    // this node's child pair was reserved by the host for the whole level (no pool atomic)
+    int base = pair_base + 2 * (int)blockIdx.x;
+    NodeRec leaf; leaf.split = -1; leaf.left = -1;
+    c.nodes[base] = leaf;
+    c.nodes[base + 1] = leaf;
+    if (!(sc->best_feat >= 0 && accept_split_v(c, s, pvs, sc->W, best_left))) {
+      base = -1;   // the reserved pair stays as two unreferenced leaves
+    } else {
+      {
         double* lv = c.node_val + (int64_t)base * c.VC;
         for (int q = 0; q < c.VC; ++q) {
           rvs[q] = pvs[q] - best_left[q];
@@ -789,7 +793,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     enqueue_or_leaf_v(c, s, on.tree, base + 1, on.start + nl, cnt - nl, on.depth + 1, child_key(on.key, 1),
                       1 - set_cur, rvs);
   // ---- stable partition: RPT ballot rounds per chunk, one block-level offset exchange
-  uint32_t* out = c.rows_next + c.row_off[on.tree] + on.start;
+  uint32_t* out = c.rows_next + on.start;
   int baseL = 0, baseR = 0;
   for (int cb = 0; cb < cnt; cb += NT * RPT) {
     if (!reg_rows) {
@@ -931,7 +935,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   double* right_ch = left_ch + VC;                   // [VC] (+ pad)
   uint8_t* xc = (uint8_t*)(left_ch + ((2 * VC + 1) & ~1));
   const int cnt0 = on.count;
-  const uint32_t* rows = c.rows_cur + c.row_off[on.tree] + on.start;
+  const uint32_t* rows = c.rows_cur + on.start;
   uint32_t row = 0;
   int my_cls = 0;
   float my_w = 0.f, my_y = 0.f;
@@ -1102,7 +1106,7 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
   for (int j = threadIdx.x; j < g; j += 256) feats[j] = perm[j];
   for (int i = threadIdx.x; i < g * span; i += 256) hist[i] = (CT)0;
   __syncthreads();
-  const uint32_t* rows = c.rows_cur + c.row_off[st.on.tree] + st.on.start;
+  const uint32_t* rows = c.rows_cur + st.on.start;
   for (int r = r0 + threadIdx.x; r < r1; r += 256) {
     const uint32_t row = rows[r];
     hist_add_row<MODE>(hist, c, tree_y(c, s), feats, g, row, boot_weight(s, row), span);
@@ -1205,8 +1209,8 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
   if (r0 >= st.on.count) return;
   const int r1 = min(r0 + c.chunk, st.on.count);
   const int feat = st.best_feat, bin = st.best_bin, nl = st.nl;
-  const uint32_t* rows = c.rows_cur + c.row_off[st.on.tree] + st.on.start;
-  uint32_t* out = c.rows_next + c.row_off[st.on.tree] + st.on.start;
+  const uint32_t* rows = c.rows_cur + st.on.start;
+  uint32_t* out = c.rows_next + st.on.start;
   __shared__ int wcnt[8];
   __shared__ int tbase[2];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1323,7 +1327,7 @@ __global__ void k_roots(Ctx c) {
   c.tree_W[t] = node_weight(c, t);
   const int cnt = c.active_count[t];
   if (cnt == 0) return;
-  enqueue_or_leaf(c, t, t, 0, cnt, 0, root_key(c.specs[t].seed), 0);
+  enqueue_or_leaf(c, t, t, c.row_off[t], cnt, 0, root_key(c.specs[t].seed), 0);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1560,6 +1564,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
 
   const size_t lds_s = sub_lds(a);
   const size_t lds_w = fused_lds(a, (int)a->kg_wave);
+  int32_t* h_pool = h + 48;   // pinned slot for the per-level pool reservation (H2D)
   const size_t lds_b = fused_lds(a, (int)a->kg_block);
   const int CH = c.CH;
   const size_t lds_hl = (size_t)a->kg_large * (MODE == 1 ? 1 : CH) * 256 * mode_elem(MODE);
@@ -1590,6 +1595,13 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     if (ns + nw + nb + nL == 0) break;
     if (++levels > 1 << 20) return 8;
     HIP_OK(hipMemsetAsync(c.counters + (1 - cur) * kTiers, 0, kTiers * 4, st));
+    // reserve the child pairs of every wave/block-tier node of this level up front
+    const int64_t pair_w = h[kPool], pair_b = pair_w + 2LL * nw, pool_next = pair_b + 2LL * nb;
+    if (pool_next > a->pool_cap) { a->status_out = 1; return 0; }
+    if (nw + nb) {
+      *h_pool = (int32_t)pool_next;
+      HIP_OK(hipMemcpyAsync(c.counters + kPool, h_pool, 4, hipMemcpyHostToDevice, st));
+    }
     a->tier_nodes_out[0] += ns; a->tier_nodes_out[1] += nw; a->tier_nodes_out[2] += nb; a->tier_nodes_out[3] += nL;
     SideStreams* ss = side_streams();
     const bool fork = ss != nullptr && ((ns > 0) + (nw > 0) + (nb > 0) + (nL > 0)) > 1;
@@ -1600,8 +1612,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       s0 = ss->s[0]; s1 = ss->s[1]; s2 = ss->s[2];
     }
     if (ns) k_subtree<REG><<<ns, 64, lds_s, s0>>>(c, cur);
-    if (nw) k_nodes<64, MODE><<<nw, 64, lds_w, s1>>>(c, 1, cur);
-    if (nb) k_nodes<DML_BLOCK_NT, MODE><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur);
+    if (nw) k_nodes<64, MODE><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w);
+    if (nb) k_nodes<DML_BLOCK_NT, MODE><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b);
     if (nL) {
       k_large_prep<<<nL, 64, 0, st>>>(c, cur, nL);
       while (true) {

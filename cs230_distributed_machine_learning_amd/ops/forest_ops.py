@@ -138,6 +138,7 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     ws_bytes = lib.dml_forest_workspace_bytes(ctypes.byref(a))
     workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     a.workspace, a.workspace_bytes = native.ptr(workspace), ws_bytes
+    retries = 0
     for _attempt in range(4):
         nodes = torch.empty((pool_cap, 2), dtype=torch.int32, device=dev)
         vals = torch.empty((pool_cap, VC), dtype=torch.float64, device=dev)
@@ -148,6 +149,7 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
             raise RuntimeError(f"dml_forest_build failed ({rc}): {native.hip_error(lib)}")
         if a.status_out == 1:
             pool_cap *= 2
+            retries += 1
             continue
         if a.status_out != 0:
             raise RuntimeError(f"dml_forest_build status {a.status_out}")
@@ -157,7 +159,7 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     P = int(a.n_nodes_out)
     del workspace
     stats = {"levels": int(a.levels_out), "large_rounds": int(a.large_rounds_out), "nodes": P,
-             "rows_total": int(a.rows_total), "build_s": time.perf_counter() - t0,
+             "rows_total": int(a.rows_total), "build_s": time.perf_counter() - t0, "pool_retries": retries,
              "tier_nodes": [int(a.tier0_nodes), int(a.tier1_nodes), int(a.tier2_nodes), int(a.tier3_nodes)]}
     return ForestBuild(nodes[:P], vals[:P], T, VC, is_reg, n_classes, stats)
 

@@ -36,5 +36,6 @@ for g in grid:
         torch.cuda.synchronize(); t0 = time.time()
         fb = forest_ops.build_gpu(Xb, y, None, roles, specs, 2, False, tiers)
         torch.cuda.synchronize(); ts.append(time.time() - t0)
+        stats = fb.stats
         del fb
-    print(g, f"build {min(ts):.3f}s  ({T} trees)", flush=True)
+    print(g, f"build {min(ts):.3f}s  ({T} trees)", {k: stats[k] for k in ("levels", "pool_retries", "tier_nodes")}, flush=True)
