@@ -23,6 +23,33 @@ struct PredictArgs {
   int64_t F, max_rows;
 };
 
+// leaf of U consecutive trees [t0, t0 + u_n) for one row, walked in lock-step: the U
+// dependent node-load chains are independent, so U requests are in flight per thread
+// instead of one (tree traversal is latency-bound)
+constexpr int kPredU = 8;
+__device__ __forceinline__ void leaves_u(const NodeRec* __restrict__ nodes, const uint8_t* __restrict__ xr, int t0,
+                                         int u_n, int (&leaf)[kPredU]) {
+  NodeRec nr[kPredU];
+#pragma unroll
+  for (int u = 0; u < kPredU; ++u) {
+    leaf[u] = t0 + u;
+    nr[u] = u < u_n ? nodes[leaf[u]] : NodeRec{-1, -1};
+  }
+  for (int steps = 0; steps < 1 << 20; ++steps) {
+    bool any = false;
+#pragma unroll
+    for (int u = 0; u < kPredU; ++u) any |= nr[u].split >= 0;
+    if (!any) break;
+#pragma unroll
+    for (int u = 0; u < kPredU; ++u) {
+      if (nr[u].split >= 0) {
+        leaf[u] = nr[u].left + (xr[nr[u].split >> 8] > (nr[u].split & 255) ? 1 : 0);
+        nr[u] = nodes[leaf[u]];
+      }
+    }
+  }
+}
+
 template <int MAXC>
 __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
   const int f = blockIdx.y;
@@ -39,24 +66,26 @@ __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
   float p[MAXC];
 #pragma unroll
   for (int k = 0; k < MAXC; ++k) p[k] = 0.f;
-  for (int t = toff[f]; t < toff[f + 1]; ++t) {
-    int node = t;
-    NodeRec nr_ = nodes[node];
-    for (int steps = 0; nr_.split >= 0 && steps < 1 << 20; ++steps) {
-      const int b = xr[nr_.split >> 8];
-      node = nr_.left + (b > (nr_.split & 255) ? 1 : 0);
-      nr_ = nodes[node];
-    }
-    const double* v = val + (int64_t)node * a.VC;
-    double W = 0.0;
+  const int tend = toff[f + 1];
+  for (int t = toff[f]; t < tend; t += kPredU) {
+    int leaf[kPredU];
+    const int u_n = min(kPredU, tend - t);
+    leaves_u(nodes, xr, t, u_n, leaf);
+    // accumulate in tree order (bit-identical to the host predictor)
 #pragma unroll
-    for (int k = 0; k < MAXC; ++k)
-      if (k < C) W += v[k];
-    if (W > 0.0) {
-      const double inv = 1.0 / W;
+    for (int u = 0; u < kPredU; ++u) {
+      if (u >= u_n) break;
+      const double* v = val + (int64_t)leaf[u] * a.VC;
+      double W = 0.0;
 #pragma unroll
       for (int k = 0; k < MAXC; ++k)
-        if (k < C) p[k] += (float)(v[k] * inv);
+        if (k < C) W += v[k];
+      if (W > 0.0) {
+        const double inv = 1.0 / W;
+#pragma unroll
+        for (int k = 0; k < MAXC; ++k)
+          if (k < C) p[k] += (float)(v[k] * inv);
+      }
     }
   }
   int best = 0;
@@ -87,16 +116,17 @@ __global__ __launch_bounds__(256) void k_predict_reg(PredictArgs a) {
   const double* val = (const double*)a.node_val;
   double acc = 0.0;
   int nt = 0;
-  for (int t = toff[f]; t < toff[f + 1]; ++t) {
-    int node = t;
-    NodeRec nr_ = nodes[node];
-    for (int steps = 0; nr_.split >= 0 && steps < 1 << 20; ++steps) {
-      const int b = xr[nr_.split >> 8];
-      node = nr_.left + (b > (nr_.split & 255) ? 1 : 0);
-      nr_ = nodes[node];
+  const int tend = toff[f + 1];
+  for (int t = toff[f]; t < tend; t += kPredU) {
+    int leaf[kPredU];
+    const int u_n = min(kPredU, tend - t);
+    leaves_u(nodes, xr, t, u_n, leaf);
+#pragma unroll
+    for (int u = 0; u < kPredU; ++u) {
+      if (u >= u_n) break;
+      const double* v = val + (int64_t)leaf[u] * a.VC;
+      if (v[0] > 0.0) { acc += v[1] / v[0]; ++nt; }
     }
-    const double* v = val + (int64_t)node * a.VC;
-    if (v[0] > 0.0) { acc += v[1] / v[0]; ++nt; }
   }
   ((float*)a.out_pred)[r0 + i] = nt ? (float)(acc / nt) : 0.f;
 }
