@@ -684,6 +684,38 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     }
     __syncthreads();
     PH(1)
+    if (!reg_rows && RPT == 1) {
+      // large node, one row per thread per NT-row chunk: 2-deep software pipeline -- the
+      // next chunk's payload/bin loads and the row ids two chunks ahead are in flight while
+      // the current chunk's histogram atomics run
+      constexpr uint32_t INV = 0xFFFFFFFFu;
+      int fj[KGMAX];
+#pragma unroll
+      for (int j = 0; j < KGMAX; ++j) fj[j] = j < g ? (int)feats[j] : 0;
+      auto row_at = [&](int r) -> uint32_t { return r < cnt ? rows[r] : INV; };
+      uint32_t r0 = row_at(tid), r1 = row_at(NT + tid);
+      uint64_t pl0 = r0 != INV ? row_payload<MODE>(c, ty, r0, boot_weight(s, r0)) : 0ull;
+      uint32_t b0[KGMAX];
+#pragma unroll
+      for (int j = 0; j < KGMAX; ++j)
+        b0[j] = (j < g && r0 != INV) ? (uint32_t)c.Xb[(int64_t)r0 * c.ld + fj[j]] : 0u;
+      for (int base = 0; base < cnt; base += NT) {
+        const uint64_t pl1 = r1 != INV ? row_payload<MODE>(c, ty, r1, boot_weight(s, r1)) : 0ull;
+        uint32_t b1[KGMAX];
+#pragma unroll
+        for (int j = 0; j < KGMAX; ++j)
+          b1[j] = (j < g && r1 != INV) ? (uint32_t)c.Xb[(int64_t)r1 * c.ld + fj[j]] : 0u;
+        const uint32_t r2 = row_at(base + 2 * NT + tid);
+        if (r0 != INV) {
+#pragma unroll
+          for (int j = 0; j < KGMAX; ++j)
+            if (j < g) hist_add<MODE>(hist + j * span, c, (int)b0[j], pl0);
+        }
+        r0 = r1; r1 = r2; pl0 = pl1;
+#pragma unroll
+        for (int j = 0; j < KGMAX; ++j) b0[j] = b1[j];
+      }
+    } else
     for (int base = 0; base < cnt; base += NT * RPT) {
       if (!reg_rows) load_rows(base);
       // all g x RPT bin loads are issued before the first histogram atomic
