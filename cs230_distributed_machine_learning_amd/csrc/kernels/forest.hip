@@ -827,12 +827,28 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   // ---- stable partition: RPT ballot rounds per chunk, one block-level offset exchange
   uint32_t* out = c.rows_next + on.start;
   int baseL = 0, baseR = 0;
+  // streaming (large-node) partition: the split-feature bins of the next chunk and the row
+  // ids two chunks ahead are prefetched while the current chunk is ranked and written
+  constexpr uint32_t INVR = 0xFFFFFFFFu;
+  auto prow = [&](int r) -> uint32_t { return r < cnt ? rows[r] : INVR; };
+  auto pbin = [&](uint32_t r) -> uint32_t { return r != INVR ? (uint32_t)c.Xb[(int64_t)r * c.ld + feat] : 0u; };
+  uint32_t nrow = INVR, nbin = 0, frow = INVR;
+  if (!reg_rows && RPT == 1) {
+    rrow[0] = prow(tid);
+    rbin[0] = pbin(rrow[0]);
+    nrow = prow(NT + tid);
+  }
   for (int cb = 0; cb < cnt; cb += NT * RPT) {
     if (!reg_rows) {
-      load_rows(cb);
+      if constexpr (RPT == 1) {
+        nbin = pbin(nrow);
+        frow = prow(cb + 2 * NT + tid);
+      } else {
+        load_rows(cb);
 #pragma unroll
-      for (int u = 0; u < RPT; ++u)
-        rbin[u] = rrow[u] != 0xFFFFFFFFu ? (uint32_t)c.Xb[(int64_t)rrow[u] * c.ld + feat] : 0u;
+        for (int u = 0; u < RPT; ++u)
+          rbin[u] = rrow[u] != 0xFFFFFFFFu ? (uint32_t)c.Xb[(int64_t)rrow[u] * c.ld + feat] : 0u;
+      }
     }
     uint64_t ml[RPT], mr[RPT];
 #pragma unroll
@@ -878,6 +894,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
       else out[nl + baseR + offR[u] + lane_prefix(mr[u])] = rrow[u];
     }
     baseL += totL; baseR += totR;
+    if (!reg_rows && RPT == 1) { rrow[0] = nrow; rbin[0] = nbin; nrow = frow; }
   }
   PH(6)
   PH_END(NT == 64 ? 0 : 1)
