@@ -1156,9 +1156,40 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
   for (int i = threadIdx.x; i < g * span; i += 256) hist[i] = (CT)0;
   __syncthreads();
   const uint32_t* rows = c.rows_cur + st.on.start;
-  for (int r = r0 + threadIdx.x; r < r1; r += 256) {
-    const uint32_t row = rows[r];
-    hist_add_row<MODE>(hist, c, tree_y(c, s), feats, g, row, boot_weight(s, row), span);
+  const float* ty = tree_y(c, s);
+  constexpr int KGL = 16;
+  if (g <= KGL) {
+    // 2-deep software pipeline (see k_nodes): next row's bins/payload and the row id two
+    // steps ahead are in flight while this row's histogram atomics run
+    constexpr uint32_t INV = 0xFFFFFFFFu;
+    int fj[KGL];
+#pragma unroll
+    for (int j = 0; j < KGL; ++j) fj[j] = j < g ? (int)feats[j] : 0;
+    auto row_at = [&](int r) -> uint32_t { return r < r1 ? rows[r] : INV; };
+    const int t0 = r0 + (int)threadIdx.x;
+    uint32_t ra = row_at(t0), rbn = row_at(t0 + 256);
+    uint64_t pa = ra != INV ? row_payload<MODE>(c, ty, ra, boot_weight(s, ra)) : 0ull;
+    uint32_t ba[KGL];
+#pragma unroll
+    for (int j = 0; j < KGL; ++j) ba[j] = (j < g && ra != INV) ? (uint32_t)c.Xb[(int64_t)ra * c.ld + fj[j]] : 0u;
+    for (int r = t0; r < r1; r += 256) {
+      const uint64_t pb = rbn != INV ? row_payload<MODE>(c, ty, rbn, boot_weight(s, rbn)) : 0ull;
+      uint32_t bb[KGL];
+#pragma unroll
+      for (int j = 0; j < KGL; ++j) bb[j] = (j < g && rbn != INV) ? (uint32_t)c.Xb[(int64_t)rbn * c.ld + fj[j]] : 0u;
+      const uint32_t rc2 = row_at(r + 512);
+#pragma unroll
+      for (int j = 0; j < KGL; ++j)
+        if (j < g) hist_add<MODE>(hist + j * span, c, (int)ba[j], pa);
+      ra = rbn; rbn = rc2; pa = pb;
+#pragma unroll
+      for (int j = 0; j < KGL; ++j) ba[j] = bb[j];
+    }
+  } else {
+    for (int r = r0 + threadIdx.x; r < r1; r += 256) {
+      const uint32_t row = rows[r];
+      hist_add_row<MODE>(hist, c, ty, feats, g, row, boot_weight(s, row), span);
+    }
   }
   __syncthreads();
   // flush into the node's global histogram: always unpacked planes [CH][256]
