@@ -1282,6 +1282,9 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
 }
 
 __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
+  // pass 1 ranks the chunk's rows (split bins prefetched one step ahead, flags kept in LDS)
+  // and reserves the chunk's left/right ranges with ONE atomic pair; pass 2 writes the rows
+  // at ballot/prefix offsets (no global atomics per 256 rows)
   const int slot = blockIdx.y;
   const LState& st = c.lstate[slot];
   if (!st.split) return;
@@ -1291,31 +1294,65 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
   const int feat = st.best_feat, bin = st.best_bin, nl = st.nl;
   const uint32_t* rows = c.rows_cur + st.on.start;
   uint32_t* out = c.rows_next + st.on.start;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint64_t* lflag = (uint64_t*)smem;            // [chunk / 64] left-flag words (ballots)
   __shared__ int wcnt[8];
   __shared__ int tbase[2];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr uint32_t INV = 0xFFFFFFFFu;
+  auto row_at = [&](int r) -> uint32_t { return r < r1 ? rows[r] : INV; };
+  auto bin_of = [&](uint32_t row) -> int { return row != INV ? (int)c.Xb[(int64_t)row * c.ld + feat] : 0; };
+  int myL = 0;
+  {
+    uint32_t ra = row_at(r0 + tid);
+    int ba = bin_of(ra);
+    uint32_t rbn = row_at(r0 + tid + 256);
+    for (int t0 = r0; t0 < r1; t0 += 256) {
+      const int bb = bin_of(rbn);
+      const uint32_t rc2 = row_at(t0 + 512 + tid);
+      const bool left = ra != INV && ba <= bin;
+      const uint64_t ml = __ballot(left);
+      if (lane == 0) lflag[(t0 - r0) / 64 + wid] = ml;
+      myL += left ? 1 : 0;
+      ra = rbn; ba = bb; rbn = rc2;
+    }
+  }
+  // block totals -> one atomic pair for the whole chunk
+  for (int m = 32; m >= 1; m >>= 1) myL += __shfl_xor(myL, m);
+  if (lane == 0) wcnt[wid] = myL;
+  __syncthreads();
+  if (tid == 0) {
+    const int totL = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    const int totR = (r1 - r0) - totL;
+    tbase[0] = atomicAdd(&c.lcursor[2 * slot], totL);
+    tbase[1] = atomicAdd(&c.lcursor[2 * slot + 1], totR);
+  }
+  __syncthreads();
+  int baseL = tbase[0], baseR = tbase[1];
   for (int t0 = r0; t0 < r1; t0 += 256) {
     const int r = t0 + tid;
     const bool valid = r < r1;
     const uint32_t row = valid ? rows[r] : 0u;
-    const bool left = valid && c.Xb[(int64_t)row * c.ld + feat] <= bin;
-    const bool right = valid && !left;
-    const uint64_t ml = __ballot(left), mr = __ballot(right);
-    if (lane == 0) { wcnt[wid] = __popcll(ml); wcnt[4 + wid] = __popcll(mr); }
-    __syncthreads();
+    const int wi = (t0 - r0) / 64;
+    const uint64_t ml = lflag[wi + wid];
+    const uint64_t vm = valid ? ~0ull : 0ull;
+    const uint64_t mvalid = __ballot(valid);
+    const uint64_t mr = mvalid & ~ml;
     int offL = 0, offR = 0, totL = 0, totR = 0;
     for (int w = 0; w < 4; ++w) {
-      if (w < wid) { offL += wcnt[w]; offR += wcnt[4 + w]; }
-      totL += wcnt[w]; totR += wcnt[4 + w];
+      const uint64_t lw = lflag[wi + w];
+      const int nvw = max(0, min(64, r1 - (t0 + 64 * w)));
+      const uint64_t vw = nvw >= 64 ? ~0ull : ((1ull << nvw) - 1ull);
+      const int cl = __popcll(lw), cr = __popcll(vw & ~lw);
+      if (w < wid) { offL += cl; offR += cr; }
+      totL += cl; totR += cr;
     }
-    if (tid == 0) {
-      tbase[0] = atomicAdd(&c.lcursor[2 * slot], totL);
-      tbase[1] = atomicAdd(&c.lcursor[2 * slot + 1], totR);
+    (void)vm;
+    if (valid) {
+      if ((ml >> lane) & 1ull) out[baseL + offL + lane_prefix(ml)] = row;
+      else out[nl + baseR + offR + lane_prefix(mr)] = row;
     }
-    __syncthreads();
-    if (left) out[tbase[0] + offL + lane_prefix(ml)] = row;
-    if (right) out[nl + tbase[1] + offR + lane_prefix(mr)] = row;
-    __syncthreads();
+    baseL += totL; baseR += totR;
   }
 }
 
@@ -1707,7 +1744,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
         HIP_OK(hipStreamSynchronize(st));
         if (!h[32]) break;
       }
-      k_partition_large<<<dim3(nchunks, (unsigned)nL), 256, 0, st>>>(c);
+      k_partition_large<<<dim3(nchunks, (unsigned)nL), 256, (size_t)((a->chunk + 255) / 256) * 4 * 8, st>>>(c);
     }
     if (fork) {
       for (int i = 0; i < 3; ++i) {
