@@ -46,7 +46,8 @@
 __device__ unsigned long long g_phase[3][8];
 #define PH_BEGIN uint64_t _pt = clock64(); uint64_t _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define PH(i) if (threadIdx.x == 0) { const uint64_t _n = clock64(); _acc[i] += _n - _pt; _pt = _n; }
-#define PH_END(t) if (threadIdx.x == 0) { _acc[7] = 1; for (int _i = 0; _i < 8; ++_i) atomicAdd(&g_phase[t][_i], _acc[_i]); }
+#define PH_END(t) if (threadIdx.x == 0) { _acc[7] = 1; for (int _i = 0; _i < 8; ++_i) atomicAdd(&g_phase[t][_i], _acc[_i]); \
+                                            atomicAdd(&g_phase[2][t], (unsigned long long)on.count); }
 #else
 #define PH_BEGIN
 #define PH(i)

@@ -503,18 +503,33 @@ def refit_best(ctl: Controller, job: Job, plan: Dict[str, Any], dd, best_idx: in
     return ctl.models.save(f"{job.subtasks[best_idx].subtask_id}_model", model)
 
 
-class LocalRunner(Runner):
-    """Runs jobs in this process on one device (``Config.device``), one job at a time.
+class _JobRun:
+    """A job in flight on the local runner: its remaining LPT slices and partial results."""
 
-    Candidates are ordered LPT (most expensive first) and cut into slices of about
-    ``chunk_target_s`` estimated seconds so status/SSE progress streams while the
-    device stays batched.
+    def __init__(self, job: Job, plan: Dict[str, Any], dd, slices: List[List[int]], costs: List[float], seq: int):
+        self.job, self.plan, self.dd, self.costs, self.seq = job, plan, dd, costs, seq
+        self.slices = list(slices)
+        self.si = 0
+        self.results: List[Any] = []
+
+
+class LocalRunner(Runner):
+    """Runs jobs in this process on one device (``Config.device``) with session fair share.
+
+    Candidates of a job are ordered LPT (most expensive first) and cut into slices of about
+    ``chunk_target_s`` estimated seconds.  Between slices the runner picks the active job
+    of the session that has used the least device time so far (ties: arrival order), so a
+    small job submitted behind a large search finishes in seconds instead of waiting for
+    it (reference: one Kafka FIFO for all sessions).  Status/SSE progress
+    streams slice by slice while the device stays batched within each slice.
     """
 
     def __init__(self, controller: Optional[Controller] = None):
         self.q: "queue.Queue[Optional[Job]]" = queue.Queue()
         self._thread: Optional[threading.Thread] = None
         self.cache: Optional[DeviceCache] = None
+        self.session_used: Dict[str, float] = {}
+        self._seq = 0
         if controller is not None:
             self.bind(controller)
 
@@ -531,47 +546,83 @@ class LocalRunner(Runner):
             self._thread.start()
         self.q.put(job)
 
-    def _loop(self):
-        while True:
-            job = self.q.get()
-            if job is None:
-                return
-            self.ctl.scheduler.heartbeat(self.worker_id)
-            try:
-                self.run_job(job)
-            except Exception as e:  # never leave a job hanging (D5)
-                traceback.print_exc()
-                for st in job.subtasks:
-                    if st.status not in ("completed", "failed"):
-                        self.ctl.table.finish_subtask(job.job_id, st.subtask_id, "failed",
-                                                      error=f"{type(e).__name__}: {e}")
+    def _fail(self, job: Job, e: Exception) -> None:
+        traceback.print_exc()
+        for st in job.subtasks:
+            if st.status not in ("completed", "failed"):
+                self.ctl.table.finish_subtask(job.job_id, st.subtask_id, "failed", error=f"{type(e).__name__}: {e}")
 
-    def run_job(self, job: Job) -> None:
+    def _admit(self, job: Job) -> Optional[_JobRun]:
         ctl = self.ctl
         plan = job_plan(job.request)
         dd = self.cache.get(ctl, plan, job.dataset_id)
         todo = [st.index for st in job.subtasks if st.status not in ("completed", "failed")]
         if not todo:
-            return
+            return None
         slices = plan_slices(ctl, plan, todo, int(dd.n * 0.8), dd.d, dd.n_classes)
         costs = candidate_costs(plan, int(dd.n * 0.8), dd.d, dd.n_classes)
-        all_results = []
-        pending_final = None
-        for si, ids in enumerate(slices):
-            ctl.table.mark_running(job.job_id, ids, self.worker_id)
-            results, metrics, wall = execute_plan_slice(ctl, job, plan, dd, ids, self.worker_id, self.device,
-                                                        seed=job_seed(job.job_id))
-            unit = Unit(unit_id=f"{job.job_id}:{si}", cost=sum(costs[i] for i in ids), algo=plan["model_type"])
-            ctl.scheduler.observe(self.worker_id, unit, wall)
-            ctl.scheduler.heartbeat(self.worker_id)
-            if si == len(slices) - 1:
-                pending_final = (results, metrics)
-            else:
-                publish_results(ctl, job, results, metrics)
-            all_results.extend(results)
-        finalize_job(ctl, job, plan, dd, all_results)
-        if pending_final:
-            publish_results(ctl, job, *pending_final)
+        self._seq += 1
+        return _JobRun(job, plan, dd, slices, costs, self._seq)
+
+    def _loop(self):
+        active: List[_JobRun] = []
+        stop = False
+        while not stop or active:
+            # admit everything submitted so far (block only when idle)
+            while True:
+                try:
+                    job = self.q.get(block=not active and not stop)
+                except queue.Empty:
+                    break
+                if job is None:
+                    stop = True
+                    if not active:
+                        return
+                    continue
+                try:
+                    jr = self._admit(job)
+                    if jr is not None:
+                        active.append(jr)
+                        self.session_used.setdefault(job.session_id, 0.0)
+                except Exception as e:  # never leave a job hanging (D5)
+                    self._fail(job, e)
+            if not active:
+                continue
+            jr = min(active, key=lambda r: (self.session_used.get(r.job.session_id, 0.0), r.seq))
+            self.ctl.scheduler.heartbeat(self.worker_id)
+            try:
+                done = self._step(jr)
+            except Exception as e:
+                self._fail(jr.job, e)
+                done = True
+            if done:
+                active.remove(jr)
+
+    def _step(self, jr: _JobRun) -> bool:
+        """Run the job's next slice; returns True when the job is complete."""
+        ctl, job, plan, dd = self.ctl, jr.job, jr.plan, jr.dd
+        ids = jr.slices[jr.si]
+        ctl.table.mark_running(job.job_id, ids, self.worker_id)
+        results, metrics, wall = execute_plan_slice(ctl, job, plan, dd, ids, self.worker_id, self.device,
+                                                    seed=job_seed(job.job_id))
+        self.session_used[job.session_id] = self.session_used.get(job.session_id, 0.0) + wall
+        unit = Unit(unit_id=f"{job.job_id}:{jr.si}", cost=sum(jr.costs[i] for i in ids), algo=plan["model_type"])
+        ctl.scheduler.observe(self.worker_id, unit, wall)
+        jr.results.extend(results)
+        jr.si += 1
+        if jr.si < len(jr.slices):
+            publish_results(ctl, job, results, metrics)
+            return False
+        # last slice: refit the winner first, so "completed" always comes with the model
+        finalize_job(ctl, job, plan, dd, jr.results)
+        publish_results(ctl, job, results, metrics)
+        return True
+
+    def run_job(self, job: Job) -> None:
+        """Synchronously run one job to completion (used by tools and tests)."""
+        jr = self._admit(job)
+        while jr is not None and not self._step(jr):
+            pass
 
     def shutdown(self) -> None:
         if self._thread is not None:

@@ -13,4 +13,5 @@ for t, tn in enumerate(["wave(64)", "block(256)"]):
     v = out[t * 8:(t + 1) * 8].astype(float)
     n = v[7] or 1
     tot = v[:7].sum()
-    print(tn, f"nodes={int(v[7])} cycles/node={tot/n:.0f}", "  ".join(f"{names[i]}={v[i]/n:.0f} ({100*v[i]/tot:.0f}%)" for i in range(7)))
+    rows = float(out[16 + t])
+    print(tn, f"nodes={int(v[7])} rows/node={rows/n:.0f} cycles/node={tot/n:.0f}", "  ".join(f"{names[i]}={v[i]/n:.0f} ({100*v[i]/tot:.0f}%)" for i in range(7)))

@@ -309,3 +309,23 @@ def test_http_gateway_roundtrip(ctl):
     finally:
         server.should_exit = True
         time.sleep(0.3)
+
+
+def test_session_fair_share(tmp_path):
+    """A one-candidate job of session B overtakes a 20-candidate search of session A."""
+    cfg = Config(data_root=str(tmp_path / "d"), device="cpu", chunk_target_s=0.0)
+    c = Controller(cfg)
+    try:
+        sa = c.create_session()[1]["session_id"]
+        sb = c.create_session()[1]["session_id"]
+        c.download_data(sa, {"dataset_url": "iris", "dataset_name": "iris", "dataset_type": "sklearn"})
+        big = _j1("big", "RandomForestClassifier", {"n_estimators": [20, 30, 40, 50, 60], "max_depth": [2, 3, 4, None]})
+        assert c.train(sa, big)[0] == 200
+        assert c.train(sb, _j1("small", "LogisticRegression", {"C": [1.0]}))[0] == 200
+        assert c.table.wait_finished("small", timeout=120)
+        st_big = c.check_status(sa, "big")[1]
+        assert st_big["job_status"] != "completed" and st_big["tasks_pending"] > 0
+        assert c.table.wait_finished("big", timeout=300)
+        assert c.check_status(sa, "big")[1]["job_status"] == "completed"
+    finally:
+        c.shutdown()
