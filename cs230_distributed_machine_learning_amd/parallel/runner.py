@@ -221,6 +221,7 @@ class DistributedRunner(Runner):
         self.seq = 0
         self.stop = False
         self.dead: set = set()
+        self.session_used: Dict[str, float] = {}
 
     def bind(self, controller: Controller) -> None:
         super().bind(controller)
@@ -252,7 +253,11 @@ class DistributedRunner(Runner):
                         self._cv.wait(timeout=idle_poll_s)
                     if self.stop and not self.q:
                         break
-                    job = self.q.pop(0)
+                    # session fair share at job granularity: the next job comes from the
+                    # session that has used the least node time (ties: arrival order)
+                    k = min(range(len(self.q)), key=lambda i: (self.session_used.get(self.q[i].session_id, 0.0), i))
+                    job = self.q.pop(k)
+                t_job = time.time()
                 try:
                     self._run_job(job)
                 except Exception as e:
@@ -261,6 +266,7 @@ class DistributedRunner(Runner):
                         if sub.status not in ("completed", "failed"):
                             self.ctl.table.finish_subtask(job.job_id, sub.subtask_id, "failed",
                                                           error=f"{type(e).__name__}: {e}")
+                self.session_used[job.session_id] = self.session_used.get(job.session_id, 0.0) + time.time() - t_job
             st.set(f"job/{self.seq}", json.dumps({"shutdown": True}))
         finally:
             hb.stop()
