@@ -1,0 +1,409 @@
+// lr_mfma.hip — logistic-regression objective on the matrix cores (K7/K8, MFMA).
+//
+// Reference: LogisticRegression is fitted one (candidate, fold) at a time by sklearn on
+// CPU (aws-prod/worker/worker.py:39 whitelist; :315 fit, :326/:341 cross_val_score).
+// Here every fit of a batch is a block of columns of ONE weight matrix and one objective
+// evaluation of the whole batch is two GEMM-shaped passes on MFMA:
+//
+//   forward  Z = X W + b         A = X    [n x d]   B^T = W^T [M x d]
+//            -> fused epilogue: link (sigmoid / softmax / OvR), fold mask, class weights,
+//               per-fit loss, residual R = (P - Y) * s written TRANSPOSED (R^T [M x n])
+//   gradient G^T = R^T X         A = R^T  [M x n]   B^T = X^T [d+1 x n]  (split-K over n;
+//               X^T carries a row of ones, so the intercept gradient falls out of the GEMM)
+//
+// Numerics: fp32-equivalent "bf16x3".  Every fp32 operand is stored as hi = bf16(v) and
+// lo = bf16(v - hi) (|v - hi - lo| <= 2^-16 |v|) and a product is hi*hi + hi*lo + lo*hi,
+// accumulated in fp32 by v_mfma_f32_16x16x32_bf16: three bf16 MFMAs per product run at
+// 2.5 PF / 3 vs the 157 TF of the exact fp32 MFMA (no xf32 on gfx950), with a relative
+// error of ~1e-5 per dot product — far below the L-BFGS tolerances (1e-4 on max|grad|).
+//
+// Tiling (CDNA4, wave64): 256-thread workgroups own a 128 x 128 output tile; each wave a
+// 64 x 64 quadrant = 4 x 4 MFMA 16x16 tiles (16 fp32x4 accumulators).  K advances 32 at a
+// time through a double-buffered LDS stage (A hi/lo + B hi/lo, 64 KB), one barrier per
+// k-step, the next stage's global loads in flight while the current one is multiplied.
+// LDS rows are 64 B with the 16-B chunk index XOR-swizzled by bit 2 of the row, which makes
+// the ds_read_b128 fragment reads conflict-free under CDNA4's 4x16-lane b128 grouping.
+// Block ids are remapped XCD-aware (id % 8 = XCD): the column tiles of one row group (and,
+// in the gradient, every tile of one K slice) share an XCD, so X / R^T panels are fetched
+// from HBM once per XCD L2, not once per column tile.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int THREADS = 256;
+constexpr int PART = BM * BK;              // bf16 elements of one operand part of one stage
+constexpr int STAGE = 4 * PART;            // A hi, A lo, B hi, B lo
+constexpr int STAGE_BYTES = 2 * STAGE * 2; // two stages: 64 KB (also holds the fp32 Z tile)
+constexpr int LACC_BYTES = 2 * BN * 8;     // per-column loss partials (double)
+
+// ctypes-facing argument blocks (every field 8 bytes)
+struct FwdArgs {
+  int64_t xh, xl, ldx;           // X hi/lo [row_tiles*BM x Kp] bf16
+  int64_t wh, wl;                // W^T hi/lo [col_tiles*BN x Kp] bf16 (ld = ldx)
+  int64_t n, Kp, row_tiles, col_tiles, row_groups;
+  int64_t bias;                  // float [col_tiles*BN]
+  int64_t col_fit;               // int32 [col_tiles*BN]: fit owning the column, -1 = padding
+  int64_t fit_col0, fit_k, fit_kind, fit_split;   // int32 [F] (fit_col0 in padded columns)
+  int64_t scale;                 // float [F]
+  int64_t cw, cwC;               // float [F x cwC] class weights (0 = none)
+  int64_t y, roles;              // int32 [n], uint8 [S x n]
+  int64_t rh, rl, ldr;           // R^T hi/lo [col_tiles*BN x ldr] bf16
+  int64_t loss;                  // double [F] (accumulated; caller zeroes)
+};
+
+struct GradArgs {
+  int64_t rh, rl, ldr;           // R^T hi/lo [m_tiles*BM x ldr]
+  int64_t xth, xtl;              // X^T hi/lo [n_tiles*BN x ldr]
+  int64_t m_tiles, n_tiles, Kp;  // Kp = ldr (rows of the dataset, padded)
+  int64_t S, Kc;                 // K slices (multiple of 8) and slice length (multiple of BK)
+  int64_t out;                   // float [S x m_tiles*BM x n_tiles*BN] partial G^T slabs
+};
+
+struct Operands {
+  const uint16_t* ah;
+  const uint16_t* al;
+  int64_t lda;
+  const uint16_t* bh;
+  const uint16_t* bl;
+  int64_t ldb;
+};
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (((row >> 2) & 1) << 1); }
+
+// global -> registers: each of the 4 parts is 512 chunks of 16 B (128 rows x 4 chunks)
+__device__ __forceinline__ void load_stage(const Operands& op, int64_t row0, int64_t col0, int64_t k0, u32x4 (&r)[8],
+                                           int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = tid + i * THREADS;
+    const int row = q >> 2, c = (q & 3) * 8;
+    r[0 + i] = *(const u32x4*)(op.ah + (row0 + row) * op.lda + k0 + c);
+    r[2 + i] = *(const u32x4*)(op.al + (row0 + row) * op.lda + k0 + c);
+    r[4 + i] = *(const u32x4*)(op.bh + (col0 + row) * op.ldb + k0 + c);
+    r[6 + i] = *(const u32x4*)(op.bl + (col0 + row) * op.ldb + k0 + c);
+  }
+}
+
+__device__ __forceinline__ void store_stage(uint16_t* st, const u32x4 (&r)[8], int tid) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = tid + i * THREADS;
+      const int row = q >> 2, c = q & 3;
+      *(u32x4*)(st + p * PART + row * BK + swz(row, c) * 8) = r[p * 2 + i];
+    }
+}
+
+__device__ __forceinline__ bf16x8 frag(const uint16_t* part, int row, int chunk) {
+  return __builtin_bit_cast(bf16x8, *(const u32x4*)(part + row * BK + swz(row, chunk) * 8));
+}
+
+// one 32-deep k-step of the wave's 64 x 64 quadrant: 16 tiles x 3 bf16 MFMAs
+__device__ __forceinline__ void mma_stage(const uint16_t* st, f32x4 (&acc)[4][4], int wm, int wn, int lane) {
+  const int r = lane & 15, g = lane >> 4;
+  bf16x8 ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int arow = wm * 64 + i * 16 + r;
+    const int brow = wn * 64 + i * 16 + r;
+    ah[i] = frag(st + 0 * PART, arow, g);
+    al[i] = frag(st + 1 * PART, arow, g);
+    bh[i] = frag(st + 2 * PART, brow, g);
+    bl[i] = frag(st + 3 * PART, brow, g);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+    }
+}
+
+// C[row0:+128, col0:+128] = sum_{k in [kb, ke)} A[row, k] * B^T[col, k]  (bf16x3)
+// Ends with a barrier (the staging LDS is free afterwards).  kb >= ke gives zeros.
+__device__ __forceinline__ void gemm_tile(const Operands& op, int64_t row0, int64_t col0, int64_t kb, int64_t ke,
+                                          uint16_t* smem, f32x4 (&acc)[4][4], int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (kb >= ke) return;
+  const int lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  u32x4 r[8];
+  load_stage(op, row0, col0, kb, r, tid);
+  store_stage(smem, r, tid);
+  __syncthreads();
+  int cur = 0;
+  for (int64_t k = kb; k < ke; k += BK) {
+    const bool more = k + BK < ke;
+    if (more) load_stage(op, row0, col0, k + BK, r, tid);
+    mma_stage(smem + cur * STAGE, acc, wm, wn, lane);
+    if (more) store_stage(smem + (cur ^ 1) * STAGE, r, tid);
+    __syncthreads();
+    cur ^= 1;
+  }
+}
+
+__device__ __forceinline__ void put_hilo(uint16_t* hp, uint16_t* lp, float v) {
+  const __bf16 h = (__bf16)v;
+  const __bf16 l = (__bf16)(v - (float)h);
+  *hp = __builtin_bit_cast(uint16_t, h);
+  *lp = __builtin_bit_cast(uint16_t, l);
+}
+
+// 8 fp32 values -> 8 packed bf16 hi + 8 packed bf16 lo (one 16-B store each)
+__device__ __forceinline__ void split8(const float (&v)[8], u32x4& hv, u32x4& lv) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const __bf16 h0 = (__bf16)v[2 * q], h1 = (__bf16)v[2 * q + 1];
+    const __bf16 l0 = (__bf16)(v[2 * q] - (float)h0), l1 = (__bf16)(v[2 * q + 1] - (float)h1);
+    hv[q] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+    lv[q] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+  }
+}
+
+// Z tile element (row, col) at zs[row * BN + (col ^ (bit 2 of row) << 4)]: the accumulator
+// writes (32 lanes = two rows 4 apart x 16 columns) hit 32 distinct banks and the
+// epilogue's reads (64 consecutive columns of one row) 64 distinct banks.
+__device__ __forceinline__ int zidx(int row, int col) { return row * BN + (col ^ (((row >> 2) & 1) << 4)); }
+
+constexpr int YS_BYTES = BM * 4;   // the tile's labels, staged once per tile
+
+__global__ __launch_bounds__(THREADS, 2) void k_lr_fwd(FwdArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[STAGE_BYTES + LACC_BYTES + YS_BYTES];
+  uint16_t* smem = reinterpret_cast<uint16_t*>(smem_raw);
+  float* zs = reinterpret_cast<float*>(smem_raw);
+  double* lacc = reinterpret_cast<double*>(smem_raw + STAGE_BYTES);
+  int32_t* ys = reinterpret_cast<int32_t*>(smem_raw + STAGE_BYTES + LACC_BYTES);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+
+  // XCD-aware decomposition: the column tiles of one row group run on one XCD
+  const int64_t b = blockIdx.x, xcd = b & 7, local = b >> 3;
+  const int64_t ct = local % a.col_tiles;
+  const int64_t rg = (local / a.col_tiles) * 8 + xcd;
+  if (rg >= a.row_groups) return;   // grid-uniform (host sizes the grid exactly)
+
+  const int32_t* col_fit = reinterpret_cast<const int32_t*>(a.col_fit);
+  const float* bias = reinterpret_cast<const float*>(a.bias);
+  const int32_t* y = reinterpret_cast<const int32_t*>(a.y);
+  const uint8_t* roles = reinterpret_cast<const uint8_t*>(a.roles);
+  const Operands op{reinterpret_cast<const uint16_t*>(a.xh), reinterpret_cast<const uint16_t*>(a.xl), a.ldx,
+                    reinterpret_cast<const uint16_t*>(a.wh), reinterpret_cast<const uint16_t*>(a.wl), a.ldx};
+  const int64_t col0 = ct * BN;
+  const int wm = w >> 1, wn = w & 1;
+
+  // epilogue mapping: thread = (column c of the tile, 64-row half rh); the lead column of a
+  // fit owns the fit's k columns for its rows.  Everything about the fit is tile-invariant.
+  const int c = tid & (BN - 1), rh = tid >> 7;
+  const int f = col_fit[col0 + c];
+  const bool lead = f >= 0 && reinterpret_cast<const int32_t*>(a.fit_col0)[f] == col0 + c;
+  int k = 0, kind = 0;
+  int64_t role_off = 0;
+  float s0 = 0.f;
+  const float* cwf = nullptr;
+  if (lead) {
+    k = reinterpret_cast<const int32_t*>(a.fit_k)[f];
+    kind = reinterpret_cast<const int32_t*>(a.fit_kind)[f];
+    role_off = (int64_t)reinterpret_cast<const int32_t*>(a.fit_split)[f] * a.n;
+    s0 = reinterpret_cast<const float*>(a.scale)[f];
+    if (a.cw) cwf = reinterpret_cast<const float*>(a.cw) + (int64_t)f * a.cwC;
+  }
+  uint16_t* RH = reinterpret_cast<uint16_t*>(a.rh) + (col0 + c) * a.ldr;
+  uint16_t* RL = reinterpret_cast<uint16_t*>(a.rl) + (col0 + c) * a.ldr;
+  double lossacc = 0.0;
+
+  for (int64_t rt = rg; rt < a.row_tiles; rt += a.row_groups) {
+    const int64_t row0 = rt * BM;
+    f32x4 acc[4][4];
+    gemm_tile(op, row0, col0, 0, a.Kp, smem, acc, tid);
+    // accumulators (+ bias) -> fp32 Z tile in the (now free) staging LDS; labels -> LDS
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wn * 64 + j * 16 + (lane & 15);
+        const float bv = bias[col0 + col];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = wm * 64 + i * 16 + (lane >> 4) * 4 + e;
+          zs[zidx(row, col)] = acc[i][j][e] + bv;
+        }
+      }
+    if (tid < BM) ys[tid] = row0 + tid < a.n ? y[row0 + tid] : 0;
+    __syncthreads();
+    if (lead) {
+      float lsum = 0.f;
+      for (int rr = 0; rr < 64; rr += 8) {
+        const int lr0 = rh * 64 + rr;
+        const int64_t g0 = row0 + lr0;
+        float sc[8];
+        int yv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int64_t g = g0 + e;
+          yv[e] = ys[lr0 + e];
+          const bool tr = g < a.n && roles[role_off + g] == 1;
+          sc[e] = tr ? (cwf ? s0 * cwf[yv[e]] : s0) : 0.f;   // 0 also zeroes R of held-out rows
+        }
+        if (kind == 1) {   // multinomial softmax over k columns
+          float lse[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float m = zs[zidx(lr0 + e, c)];
+            for (int j = 1; j < k; ++j) m = fmaxf(m, zs[zidx(lr0 + e, c + j)]);
+            float se = 0.f;
+            for (int j = 0; j < k; ++j) se += __expf(zs[zidx(lr0 + e, c + j)] - m);
+            lse[e] = m + __logf(se);
+            lsum += sc[e] * (lse[e] - zs[zidx(lr0 + e, c + yv[e])]);
+          }
+          for (int j = 0; j < k; ++j) {
+            float r[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              r[e] = (__expf(zs[zidx(lr0 + e, c + j)] - lse[e]) - (yv[e] == j ? 1.f : 0.f)) * sc[e];
+            u32x4 hv, lv;
+            split8(r, hv, lv);
+            *(u32x4*)(RH + j * a.ldr + g0) = hv;
+            *(u32x4*)(RL + j * a.ldr + g0) = lv;
+          }
+        } else {           // 0: one sigmoid column (target y == 1); 2: OvR column j (target y == j)
+          for (int j = 0; j < k; ++j) {
+            float r[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float z = zs[zidx(lr0 + e, c + j)];
+              const bool pos = kind == 0 ? yv[e] == 1 : yv[e] == j;
+              const float ex = __expf(-fabsf(z));                    // one exp, one log, one rcp
+              const float inv = __builtin_amdgcn_rcpf(1.f + ex);
+              const float p = z >= 0.f ? inv : ex * inv;             // sigmoid(z)
+              const float t = pos ? -z : z;                          // loss = softplus(t), |t| = |z|
+              lsum += sc[e] * (fmaxf(t, 0.f) + __logf(1.f + ex));
+              r[e] = (p - (pos ? 1.f : 0.f)) * sc[e];
+            }
+            u32x4 hv, lv;
+            split8(r, hv, lv);
+            *(u32x4*)(RH + j * a.ldr + g0) = hv;
+            *(u32x4*)(RL + j * a.ldr + g0) = lv;
+          }
+        }
+      }
+      lossacc += (double)lsum;
+    }
+    __syncthreads();   // Z tile / label reads done before the next tile's staging writes
+  }
+  // the two row halves of a column combine in LDS; one atomic per fit per workgroup
+  if (rh == 1) lacc[c] = lossacc;
+  __syncthreads();
+  if (rh == 0 && lead) {
+    const double v = lossacc + lacc[c];
+    if (v != 0.0) atomicAdd(reinterpret_cast<double*>(a.loss) + f, v);
+  }
+}
+
+__global__ __launch_bounds__(THREADS, 2) void k_lr_grad(GradArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[STAGE_BYTES];
+  uint16_t* smem = reinterpret_cast<uint16_t*>(smem_raw);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // every output tile of one K slice runs on one XCD (shared R^T / X^T panels in its L2)
+  const int64_t b = blockIdx.x, xcd = b & 7, local = b >> 3;
+  const int64_t tiles = a.m_tiles * a.n_tiles;
+  const int64_t tile = local % tiles;
+  const int64_t s = (local / tiles) * 8 + xcd;
+  if (s >= a.S) return;
+  const int64_t mt = tile / a.n_tiles, nt = tile % a.n_tiles;
+  const int64_t kb = s * a.Kc;
+  const int64_t ke = kb + a.Kc < a.Kp ? kb + a.Kc : a.Kp;
+  const Operands op{reinterpret_cast<const uint16_t*>(a.rh), reinterpret_cast<const uint16_t*>(a.rl), a.ldr,
+                    reinterpret_cast<const uint16_t*>(a.xth), reinterpret_cast<const uint16_t*>(a.xtl), a.ldr};
+  f32x4 acc[4][4];
+  gemm_tile(op, mt * BM, nt * BN, kb, ke, smem, acc, tid);
+  const int64_t ldo = a.n_tiles * BN;
+  float* out = reinterpret_cast<float*>(a.out) + s * (a.m_tiles * BM) * ldo;
+  const int wm = w >> 1, wn = w & 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t col = nt * BN + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t row = mt * BM + wm * 64 + i * 16 + (lane >> 4) * 4 + e;
+        out[row * ldo + col] = acc[i][j][e];
+      }
+    }
+}
+
+// fp32 [rows x cols] (row-major, ld) -> bf16 hi/lo, written row-major or transposed into
+// zero-padded destinations; one-time operand preparation per dataset.
+// blockIdx.x walks 64-row tiles (rows can be ~10M), blockIdx.y 64-column tiles.
+__global__ __launch_bounds__(256) void k_split_hilo(const float* __restrict__ src, int64_t rows, int64_t cols,
+                                                     int64_t ld, uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
+                                                     int64_t ldd, int transpose) {
+  __shared__ float tile[64][65];
+  const int64_t r0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < rows && c < cols) ? src[r * ld + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    if (!transpose) {
+      const int64_t r = r0 + i, c = c0 + tx;
+      if (r < rows && c < cols) put_hilo(hi + r * ldd + c, lo + r * ldd + c, tile[i][tx]);
+    } else {   // destination [cols x rows]
+      const int64_t r = r0 + tx, c = c0 + i;
+      if (r < rows && c < cols) put_hilo(hi + c * ldd + r, lo + c * ldd + r, tile[tx][i]);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int dml_lr_mfma_tile() { return BM; }
+
+int dml_lr_mfma_fwd(const FwdArgs* a, hipStream_t st) {
+  if (a->row_tiles <= 0 || a->col_tiles <= 0) return 0;
+  if (a->Kp % BK || a->ldx % 8 || a->ldr % 8 || a->row_groups % 8 || a->row_groups <= 0) return 2;
+  if (a->Kp > a->ldx || a->row_tiles * BM > a->ldr) return 2;
+  const int64_t blocks = a->col_tiles * a->row_groups;
+  if (blocks > 0x7fffffff) return 2;
+  k_lr_fwd<<<(unsigned)blocks, THREADS, 0, st>>>(*a);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+int dml_lr_mfma_grad(const GradArgs* a, hipStream_t st) {
+  if (a->m_tiles <= 0 || a->n_tiles <= 0) return 0;
+  if (a->Kp % BK || a->Kc % BK || a->ldr % 8 || a->S % 8 || a->S <= 0 || a->S * a->Kc < a->Kp || a->Kp > a->ldr)
+    return 2;
+  const int64_t blocks = a->m_tiles * a->n_tiles * a->S;
+  if (blocks > 0x7fffffff) return 2;
+  k_lr_grad<<<(unsigned)blocks, THREADS, 0, st>>>(*a);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+int dml_split_hilo(const float* src, int64_t rows, int64_t cols, int64_t ld, uint16_t* hi, uint16_t* lo, int64_t ldd,
+                   int32_t transpose, hipStream_t st) {
+  if (rows <= 0 || cols <= 0) return 0;
+  dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((cols + 63) / 64));
+  if (grid.y > 65535) return 2;
+  k_split_hilo<<<grid, 256, 0, st>>>(src, rows, cols, ld, hi, lo, ldd, transpose);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+int dml_lr_sizeof_fwd_args() { return (int)sizeof(FwdArgs); }
+int dml_lr_sizeof_grad_args() { return (int)sizeof(GradArgs); }
+
+}  // extern "C"

@@ -20,7 +20,9 @@ LinearRegression
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
 import time
 from typing import Any, Dict, List
 
@@ -98,11 +100,135 @@ def class_weight_vector(data, split: int, cw):
     return w
 
 
+_TILE = 128   # output tile of csrc/kernels/lr_mfma.hip (dml_lr_mfma_tile)
+
+
+def _roundup(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def mfma_enabled(data) -> bool:
+    """The matrix-core objective runs for every device batch unless DML_LR_MFMA=0."""
+    return data.is_gpu and os.environ.get("DML_LR_MFMA", "1") != "0"
+
+
+class MfmaOperands:
+    """bf16 hi/lo operand copies of one dataset for the MFMA objective, built once and kept
+    resident next to the fp32 X (8 more bytes per element; 10M x 1000 -> 82 GB of the
+    288 GB HBM): ``X`` row-major with K padded to 32 (forward A operand) and ``X^T`` with
+    a row of ones appended (gradient B operand; the ones row yields the intercept gradient)."""
+
+    def __init__(self, data):
+        lib = native.hip_lib()
+        n, d, dev = data.n, data.d, data.device
+        self.npad = _roundup(n, _TILE)
+        self.Kp = _roundup(d, 32)
+        self.Dp = _roundup(d + 1, _TILE)
+        bf = torch.bfloat16
+        self.xh = torch.zeros((self.npad, self.Kp), dtype=bf, device=dev)
+        self.xl = torch.zeros_like(self.xh)
+        self.xth = torch.zeros((self.Dp, self.npad), dtype=bf, device=dev)
+        self.xtl = torch.zeros_like(self.xth)
+        st = native.stream_handle(dev)
+        for hi, lo, ldd, tr in ((self.xh, self.xl, self.Kp, 0), (self.xth, self.xtl, self.npad, 1)):
+            rc = lib.dml_split_hilo(native.ptr(data.X), n, d, d, native.ptr(hi), native.ptr(lo), ldd, tr, st)
+            if rc:
+                raise RuntimeError(f"dml_split_hilo failed ({rc})")
+        self.xth[d, :n] = 1.0
+
+
+def mfma_operands(data) -> MfmaOperands:
+    ops = getattr(data, "_lr_mfma_ops", None)
+    if ops is None:
+        ops = MfmaOperands(data)
+        data._lr_mfma_ops = ops
+    return ops
+
+
+class MfmaPlan:
+    """Buffers and launch blocks of one batch's matrix-core objective
+    (csrc/kernels/lr_mfma.hip): forward GEMM + fused link epilogue writing R^T, then the
+    split-K gradient GEMM into per-slice slabs (summed here in a fixed order)."""
+
+    def __init__(self, data, b: "_Batch"):
+        lib = native.hip_lib()
+        if lib.dml_lr_mfma_tile() != _TILE:
+            raise RuntimeError("lr_mfma tile mismatch")
+        self.ops = ops = mfma_operands(data)
+        dev = data.device
+        # padded column layout: no fit's column group straddles a 128-column tile
+        pcol0, m = [], 0
+        for k in b.K_l:
+            if (m % _TILE) + k > _TILE:
+                m = _roundup(m, _TILE)
+            pcol0.append(m)
+            m += k
+        self.Mp = _roundup(max(m, 1), _TILE)
+        col_tiles = self.Mp // _TILE
+        self.colmap = torch.tensor([c0 + j for c0, k in zip(pcol0, b.K_l) for j in range(k)], dtype=torch.long,
+                                   device=dev)
+        self.col_fit = torch.full((self.Mp,), -1, dtype=torch.int32, device=dev)
+        self.col_fit[self.colmap] = b.col_fit.to(torch.int32)
+        self.fit_col0 = torch.tensor(pcol0, dtype=torch.int32, device=dev)
+        bf = torch.bfloat16
+        self.wh = torch.zeros((self.Mp, ops.Kp), dtype=bf, device=dev)
+        self.wl = torch.zeros_like(self.wh)
+        self.bias = torch.zeros(self.Mp, dtype=torch.float32, device=dev)
+        self.rh = torch.zeros((self.Mp, ops.npad), dtype=bf, device=dev)   # rows >= n / pad columns stay 0
+        self.rl = torch.zeros_like(self.rh)
+        self.loss = torch.zeros(b.F, dtype=torch.float64, device=dev)
+        # forward: persistent, at most the resident workgroups (2 per CU), row groups % 8 == 0
+        row_tiles = ops.npad // _TILE
+        resident = 2 * torch.cuda.get_device_properties(dev).multi_processor_count
+        rg = max(8, (resident // col_tiles) // 8 * 8)
+        rg = min(rg, _roundup(row_tiles, 8))
+        # gradient: output tiles x K slices >= ~4 waves of workgroups; slices % 8 == 0
+        n_tiles = ops.Dp // _TILE
+        tiles = col_tiles * n_tiles
+        S = _roundup(-(-4 * resident // tiles), 8)
+        Kc = _roundup(-(-ops.npad // S), 32)
+        S = _roundup(-(-ops.npad // Kc), 8)
+        self.slabs = torch.empty((S, self.Mp, ops.Dp), dtype=torch.float32, device=dev)
+        p = native.ptr
+        self.fwd = native.LrFwdArgs(
+            xh=p(ops.xh), xl=p(ops.xl), ldx=ops.Kp, wh=p(self.wh), wl=p(self.wl), n=data.n, Kp=ops.Kp,
+            row_tiles=row_tiles, col_tiles=col_tiles, row_groups=rg, bias=p(self.bias), col_fit=p(self.col_fit),
+            fit_col0=p(self.fit_col0), fit_k=p(b.K), fit_kind=p(b.kind), fit_split=p(b.split), scale=p(b.scale),
+            cw=p(b.cw), cwC=int(b.cw.shape[1]) if b.cw is not None else 0, y=p(data.y_cls), roles=p(data.roles),
+            rh=p(self.rh), rl=p(self.rl), ldr=ops.npad, loss=p(self.loss))
+        self.grad = native.LrGradArgs(
+            rh=p(self.rh), rl=p(self.rl), ldr=ops.npad, xth=p(ops.xth), xtl=p(ops.xtl), m_tiles=col_tiles,
+            n_tiles=n_tiles, Kp=ops.npad, S=S, Kc=Kc, out=p(self.slabs))
+
+    def objective(self, data, b: "_Batch", W: torch.Tensor):
+        """(loss [F] float64, data gradient [d+1, M]) of the unregularised objective."""
+        d = data.d
+        Wt = W[:d].t()
+        hi = Wt.to(torch.bfloat16)
+        self.wh[self.colmap, :d] = hi
+        self.wl[self.colmap, :d] = (Wt - hi.float()).to(torch.bfloat16)
+        self.bias[self.colmap] = W[d] * b.icpt_col
+        self.loss.zero_()
+        lib = native.hip_lib()
+        st = native.stream_handle(data.device)
+        rc = lib.dml_lr_mfma_fwd(ctypes.byref(self.fwd), st)
+        if rc == 0:
+            rc = lib.dml_lr_mfma_grad(ctypes.byref(self.grad), st)
+        if rc:
+            raise RuntimeError(f"lr_mfma launch failed ({rc})")
+        GT = self.slabs.sum(0)
+        G = torch.empty_like(W)
+        G[:d] = GT[self.colmap, :d].t()
+        G[d] = GT[self.colmap, d] * b.icpt_col
+        return self.loss.clone(), G
+
+
 class _Batch:
     """Column layout of a batch of logistic fits."""
 
     def __init__(self, data, tasks: List[FitTask]):
         self.tasks = tasks
+        self.mf = None   # MfmaPlan when the matrix-core objective runs
         C = data.n_classes
         col0, K, kind, split, scale, lam, lam1, icpt, pen_icpt, tol, max_iter, cws = ([] for _ in range(12))
         any_cw = False
@@ -226,8 +352,14 @@ class LogisticFamily(Family):
 
     # --------------------------------------------------------------------------------
     def _objective(self, data, b: _Batch, W: torch.Tensor):
-        X = data.X
         d = data.d
+        if b.mf is not None:   # matrix cores: fused forward + split-K gradient (lr_mfma.hip)
+            loss, G = b.mf.objective(data, b, W)
+            reg = W * b.lam_col
+            reg[d] = reg[d] * b.pen_icpt_col
+            G += reg
+            return loss + 0.5 * b.segsum((W * reg).sum(0)).double(), G
+        X = data.X
         Z = torch.addmm(W[d] * b.icpt_col, X, W[:d])
         if data.is_gpu:
             R = torch.empty_like(Z)
@@ -327,7 +459,8 @@ class LogisticFamily(Family):
                 ft, Gt = self._objective(data, b, Wt)
                 Ft = total(ft, Wt)
                 n_evals += 1
-                slack = 1e-7 * F.abs() + 1e-12  # float32 objective: tolerate round-off near the optimum
+                # float32 (or bf16x3 on the matrix cores) objective: tolerate round-off near the optimum
+                slack = (4e-6 if b.mf is not None else 1e-7) * F.abs() + 1e-12
                 dec = b.segsum((PG * (Wt - W)).sum(0)).double()
                 ok = (Ft <= F + 1e-4 * dec + slack) | ~active
                 if bool(ok.all()):
@@ -370,7 +503,12 @@ class LogisticFamily(Family):
         # memory-budgeted batches of whole fits: Z and R are [n, columns] and the L-BFGS
         # history holds 2 x history [d+1, columns] matrices
         width = 1 if data.n_classes == 2 else data.n_classes
-        per_col = 4.0 * (3 * data.n + (data.d + 1) * (2 * self.history + 6))
+        use_mf = mfma_enabled(data)
+        if use_mf:   # resident bf16 operands first, so the budget below sees them
+            ops = mfma_operands(data)
+            per_col = 4.0 * (ops.npad + (data.d + 1) * (2 * self.history + 10) + 32 * ops.Dp)
+        else:
+            per_col = 4.0 * (3 * data.n + (data.d + 1) * (2 * self.history + 6))
         budget = 0.45 * torch.cuda.mem_get_info(data.device)[0] if data.is_gpu else 8e9
         cap = max(1, int(budget // (per_col * width)))
         if len(tasks) > cap:
@@ -380,13 +518,16 @@ class LogisticFamily(Family):
             return outs
         t0 = time.perf_counter()
         b = _Batch(data, tasks)
+        if use_mf:
+            b.mf = MfmaPlan(data, b)
         W, iters, n_evals = self._solve(data, b)
+        b.mf = None   # release R^T / slabs before the prediction GEMMs
         d = data.d
-        Z = torch.addmm(W[d] * b.icpt_col, data.X, W[:d])
+        Zte = self._test_logits(data, b, W)
         outs = []
         for f, t in enumerate(tasks):
-            c0, k = b.col0_l[f], b.K_l[f]
-            z = Z[data.test_rows[t.split].long(), c0:c0 + k]
+            k = b.K_l[f]
+            z = Zte[f]
             if b.kind_l[f] == KIND_BINARY:
                 pred = (z[:, 0] > 0).to(torch.int32)
                 proba = torch.sigmoid(z[:, 0])
@@ -416,6 +557,29 @@ class LogisticFamily(Family):
                 }
         return outs
 
+
+    @staticmethod
+    def _test_logits(data, b: _Batch, W: torch.Tensor) -> List[torch.Tensor]:
+        """Held-out logits of every fit: one GEMM per split over that split's test rows
+        only (row-chunked), never the full [n, M] product."""
+        d = data.d
+        bias = W[d] * b.icpt_col
+        by_split: Dict[int, List[int]] = {}
+        for f in range(b.F):
+            by_split.setdefault(b.split_l[f], []).append(f)
+        out: List[torch.Tensor] = [None] * b.F
+        for s, fits in by_split.items():
+            te = data.test_rows[s].long()
+            cols = torch.cat([torch.arange(b.col0_l[f], b.col0_l[f] + b.K_l[f]) for f in fits]).to(W.device)
+            Wc, bc = W[:d, cols], bias[cols]
+            step = max(1024, int(2e9 // (4 * (d + len(cols)))))
+            Z = torch.cat([torch.addmm(bc, data.X[te[i:i + step]], Wc) for i in range(0, len(te), step)]) \
+                if len(te) else torch.empty((0, len(cols)), dtype=W.dtype, device=W.device)
+            o = 0
+            for f in fits:
+                out[f] = Z[:, o:o + b.K_l[f]]
+                o += b.K_l[f]
+        return out
 
     def _run_host_lbfgs(self, data, tasks: List[FitTask], keep_models: bool) -> List[FitOutput]:
         from scipy import optimize

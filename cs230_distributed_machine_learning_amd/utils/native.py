@@ -78,6 +78,14 @@ PredictArgs = _i64_struct(
 
 ScoreArgs = _i64_struct("ScoreArgs", ["rows", "fit_row_off", "pred", "ycls", "yreg", "is_reg", "out", "F"])
 
+# csrc/kernels/lr_mfma.hip argument blocks (MFMA logistic-regression objective)
+LrFwdArgs = _i64_struct(
+    "LrFwdArgs",
+    ["xh", "xl", "ldx", "wh", "wl", "n", "Kp", "row_tiles", "col_tiles", "row_groups", "bias", "col_fit",
+     "fit_col0", "fit_k", "fit_kind", "fit_split", "scale", "cw", "cwC", "y", "roles", "rh", "rl", "ldr", "loss"],
+)
+LrGradArgs = _i64_struct("LrGradArgs", ["rh", "rl", "ldr", "xth", "xtl", "m_tiles", "n_tiles", "Kp", "S", "Kc", "out"])
+
 
 def _load(path: str) -> ctypes.CDLL:
     return ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
@@ -172,12 +180,22 @@ def _register_optional(lib) -> None:
         "dml_forest_refine": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
                                       c_vp]),
         "dml_svm_smo": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+        "dml_lr_mfma_tile": (c_i32, []),
+        "dml_lr_mfma_fwd": (c_i32, [ctypes.POINTER(LrFwdArgs), c_vp]),
+        "dml_lr_mfma_grad": (c_i32, [ctypes.POINTER(LrGradArgs), c_vp]),
+        "dml_split_hilo": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp]),
+        "dml_lr_sizeof_fwd_args": (c_i32, []),
+        "dml_lr_sizeof_grad_args": (c_i32, []),
     }
     for name, (res, args) in table.items():
         fn = getattr(lib, name, None)
         if fn is not None:
             fn.restype = res
             fn.argtypes = args
+    if getattr(lib, "dml_lr_sizeof_fwd_args", None) is not None:
+        if (lib.dml_lr_sizeof_fwd_args() != ctypes.sizeof(LrFwdArgs)
+                or lib.dml_lr_sizeof_grad_args() != ctypes.sizeof(LrGradArgs)):
+            raise RuntimeError("LR MFMA argument layout mismatch between HIP library and Python")
 
 
 def hip_error(lib=None) -> str:

@@ -107,6 +107,61 @@ def test_lr_link_grad_kernel_matches_torch():
     torch.testing.assert_close(loss, lr, rtol=1e-4, atol=1e-4)
 
 
+def _lr_batch(dd, specs):
+    from cs230_distributed_machine_learning_amd.models import linear
+    from cs230_distributed_machine_learning_amd.models.base import FitTask
+
+    fam = linear.LogisticFamily()
+    tasks = []
+    for i, (params, split) in enumerate(specs):
+        rp = fam.resolve("LogisticRegression", params, dd.n, dd.d, dd.n_classes)
+        tasks.append(FitTask(task_id=i, candidate=i, split=split, model_type="LogisticRegression", params=rp))
+    return fam, linear._Batch(dd, tasks)
+
+
+@pytest.mark.parametrize("C_cls,n,d", [(2, 3001, 70), (3, 2500, 45), (4, 700, 300)])
+def test_lr_mfma_objective_matches_fp32(C_cls, n, d):
+    """Matrix-core (bf16x3) objective vs the fp32 GEMM + link-kernel path: loss and gradient."""
+    from cs230_distributed_machine_learning_amd.models import linear
+
+    rng = np.random.RandomState(C_cls * 7 + d)
+    X = (rng.randn(n, d) * rng.uniform(0.1, 3.0, d)).astype(np.float32)
+    y = rng.randint(0, C_cls, n)
+    dd = _dd(X, y, True, "cuda:0")
+    S = len(dd.split_names)
+    specs = []
+    for i in range(40):   # softmax / OvR (liblinear) / class-weighted, assorted splits and C
+        p = {"C": float(10.0 ** rng.uniform(-2, 2)), "solver": ["lbfgs", "liblinear"][i % 2]}
+        if i % 5 == 0:
+            p["class_weight"] = "balanced"
+        specs.append((p, i % S))
+    fam, b = _lr_batch(dd, specs)
+    W = torch.randn((d + 1, b.M), device="cuda:0") * 0.05
+    f0, G0 = fam._objective(dd, b, W)
+    b.mf = linear.MfmaPlan(dd, b)
+    f1, G1 = fam._objective(dd, b, W)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(f1, f0, rtol=2e-5, atol=1e-6)
+    scale = G0.abs().amax(0, keepdim=True).clamp_min(1e-6)
+    assert float(((G1 - G0).abs() / scale).max()) < 2e-4
+
+
+def test_lr_mfma_fits_match_fp32_path(monkeypatch):
+    """Whole batched L-BFGS solves on the matrix cores reach the fp32 path's CV scores."""
+    rng = np.random.RandomState(5)
+    X = rng.randn(30000, 40).astype(np.float32)
+    y = (X @ rng.randn(40) + 2 * rng.randn(30000) > 0).astype(int)
+    grid = list(ParameterGrid({"C": [0.001, 0.1, 10.0], "solver": ["lbfgs", "liblinear"]}))
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("DML_LR_MFMA", flag)
+        dd = DeviceData(X, y, True, "cuda:0")
+        res = run_candidates(dd, JobSpec("LogisticRegression", grid, cv=5), range(len(grid)))
+        assert all(r.ok for r in res), [r.error for r in res]
+        out[flag] = np.array([r.result["mean_cv_score"] for r in res])
+    np.testing.assert_allclose(out["1"], out["0"], atol=1e-3)
+
+
 def test_lr_gpu_grid_matches_cpu():
     rng = np.random.RandomState(3)
     X = rng.randn(40000, 10).astype(np.float32)          # large enough for the device solver
