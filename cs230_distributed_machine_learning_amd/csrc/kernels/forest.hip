@@ -37,6 +37,14 @@
 #ifndef DML_NODES_WPE
 #define DML_NODES_WPE 4
 #endif
+// eval_feature is called with an LDS histogram (fused node kernels) and a global one
+// (large tier): inlined, each call site keeps its address space (ds_read / global_load);
+// out of line, every histogram access is a flat op that also counts on lgkmcnt.
+#ifndef DML_EVAL_NOINLINE
+#define DML_EVAL_ATTR __attribute__((always_inline))
+#else
+#define DML_EVAL_ATTR
+#endif
 #ifndef DML_KGMAX_WAVE
 #define DML_KGMAX_WAVE 4
 #endif
@@ -278,7 +286,7 @@ __device__ __forceinline__ double hist_chan(const typename HT<MODE>::T* h, int c
 // flag, the best bin's cumulative channels (out_left[CH]); optionally zeroes the
 // histogram afterwards so the next feature group needs no clearing pass.
 template <int MODE>
-__device__ void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
+__device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
                                  double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after);
 
 // ONE wave evaluates one feature's histogram.  Binary (MODE 1) and regression (MODE 2)
@@ -286,7 +294,7 @@ __device__ void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const T
 // arg-maxed without writing the scan back to LDS; the histogram is cleared by the same
 // lanes right after the read.  Multiclass (MODE 0) keeps the LDS path (C+1 planes).
 template <int MODE>
-__device__ void eval_feature(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
+__device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
                              double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after) {
   if constexpr (MODE == 0) {
     eval_feature_lds<MODE>(h, C, CH, s, lane, out_gain, out_bin, out_nc, out_left, zero_after);
@@ -384,7 +392,7 @@ __device__ void eval_feature(typename HT<MODE>::T* h, int C, int CH, const TreeS
 }
 
 template <int MODE>
-__device__ void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
+__device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
                                  double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after) {
   using CT = typename HT<MODE>::T;
   const int planes = hist_planes(MODE, CH);

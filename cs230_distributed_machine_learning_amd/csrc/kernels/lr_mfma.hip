@@ -23,6 +23,10 @@
 // k-step, the next stage's global loads in flight while the current one is multiplied.
 // LDS rows are 64 B with the 16-B chunk index XOR-swizzled by bit 2 of the row, which makes
 // the ds_read_b128 fragment reads conflict-free under CDNA4's 4x16-lane b128 grouping.
+// Every operand lives in HBM in a K-TILED layout, element (row, k) at
+// ((k / 32) * rows + row) * 32 + k % 32: one stage of one operand part (128 rows x 32 k) is
+// ONE contiguous 8-KB block.  (Row-major operands cost 2-3x here: a stage touched 128 rows
+// 64 B each, for R^T / X^T rows megabytes apart — measured 12.6 -> ~4 ms on the gradient.)
 // Block ids are remapped XCD-aware (id % 8 = XCD): the column tiles of one row group (and,
 // in the gradient, every tile of one K slice) share an XCD, so X / R^T panels are fetched
 // from HBM once per XCD L2, not once per column tile.
@@ -36,6 +40,10 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef LRM_PASSES
+#define LRM_PASSES 3   // A/B instrumentation: 1 = hi*hi only, 0 = no MFMA (never in production)
+#endif
+
 constexpr int BM = 128, BN = 128, BK = 32;
 constexpr int THREADS = 256;
 constexpr int PART = BM * BK;              // bf16 elements of one operand part of one stage
@@ -45,8 +53,8 @@ constexpr int LACC_BYTES = 2 * BN * 8;     // per-column loss partials (double)
 
 // ctypes-facing argument blocks (every field 8 bytes)
 struct FwdArgs {
-  int64_t xh, xl, ldx;           // X hi/lo [row_tiles*BM x Kp] bf16
-  int64_t wh, wl;                // W^T hi/lo [col_tiles*BN x Kp] bf16 (ld = ldx)
+  int64_t xh, xl, xrows;         // X hi/lo, K-tiled over xrows (= row_tiles*BM) rows, Kp deep
+  int64_t wh, wl;                // W^T hi/lo, K-tiled over col_tiles*BN rows, Kp deep
   int64_t n, Kp, row_tiles, col_tiles, row_groups;
   int64_t bias;                  // float [col_tiles*BN]
   int64_t col_fit;               // int32 [col_tiles*BN]: fit owning the column, -1 = padding
@@ -54,14 +62,14 @@ struct FwdArgs {
   int64_t scale;                 // float [F]
   int64_t cw, cwC;               // float [F x cwC] class weights (0 = none)
   int64_t y, roles;              // int32 [n], uint8 [S x n]
-  int64_t rh, rl, ldr;           // R^T hi/lo [col_tiles*BN x ldr] bf16
+  int64_t rh, rl, kr;            // R^T hi/lo, K-tiled over col_tiles*BN rows, kr (= xrows) deep
   int64_t loss;                  // double [F] (accumulated; caller zeroes)
 };
 
 struct GradArgs {
-  int64_t rh, rl, ldr;           // R^T hi/lo [m_tiles*BM x ldr]
-  int64_t xth, xtl;              // X^T hi/lo [n_tiles*BN x ldr]
-  int64_t m_tiles, n_tiles, Kp;  // Kp = ldr (rows of the dataset, padded)
+  int64_t rh, rl, unused;        // R^T hi/lo, K-tiled over m_tiles*BM rows, Kp deep
+  int64_t xth, xtl;              // X^T hi/lo (+ ones row), K-tiled over n_tiles*BN rows, Kp deep
+  int64_t m_tiles, n_tiles, Kp;  // Kp = rows of the dataset, padded
   int64_t S, Kc;                 // K slices (multiple of 8) and slice length (multiple of BK)
   int64_t out;                   // float [S x m_tiles*BM x n_tiles*BN] partial G^T slabs
 };
@@ -69,25 +77,35 @@ struct GradArgs {
 struct Operands {
   const uint16_t* ah;
   const uint16_t* al;
-  int64_t lda;
+  int64_t arows;   // rows of the K-tiled A operand (k-block stride = arows * 32)
   const uint16_t* bh;
   const uint16_t* bl;
-  int64_t ldb;
+  int64_t brows;
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (((row >> 2) & 1) << 1); }
 
-// global -> registers: each of the 4 parts is 512 chunks of 16 B (128 rows x 4 chunks)
+// operands arrive as integers (ctypes argument blocks): pin them to the GLOBAL address
+// space, otherwise hipcc emits flat loads, which also count on lgkmcnt and make every
+// LDS-fragment wait drain the next stage's prefetch
+typedef const __attribute__((address_space(1))) u32x4* gvec;
+typedef __attribute__((address_space(1))) u32x4* gvec_w;
+#define GPTR(T, v) ((T*)(__attribute__((address_space(1))) T*)(uintptr_t)(v))
+
+__device__ __forceinline__ u32x4 gload(const uint16_t* p) { return *(gvec)(uintptr_t)p; }
+
+// global -> registers: each of the 4 parts is one contiguous 8-KB block (128 rows x 32 k,
+// K-tiled layout): chunk q (16 B) = row q / 4, k chunk q % 4
 __device__ __forceinline__ void load_stage(const Operands& op, int64_t row0, int64_t col0, int64_t k0, u32x4 (&r)[8],
                                            int tid) {
+  const int64_t ab = ((k0 >> 5) * op.arows + row0) * BK, bb = ((k0 >> 5) * op.brows + col0) * BK;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int q = tid + i * THREADS;
-    const int row = q >> 2, c = (q & 3) * 8;
-    r[0 + i] = *(const u32x4*)(op.ah + (row0 + row) * op.lda + k0 + c);
-    r[2 + i] = *(const u32x4*)(op.al + (row0 + row) * op.lda + k0 + c);
-    r[4 + i] = *(const u32x4*)(op.bh + (col0 + row) * op.ldb + k0 + c);
-    r[6 + i] = *(const u32x4*)(op.bl + (col0 + row) * op.ldb + k0 + c);
+    r[0 + i] = gload(op.ah + ab + q * 8);
+    r[2 + i] = gload(op.al + ab + q * 8);
+    r[4 + i] = gload(op.bh + bb + q * 8);
+    r[6 + i] = gload(op.bl + bb + q * 8);
   }
 }
 
@@ -100,6 +118,28 @@ __device__ __forceinline__ void store_stage(uint16_t* st, const u32x4 (&r)[8], i
       const int row = q >> 2, c = q & 3;
       *(u32x4*)(st + p * PART + row * BK + swz(row, c) * 8) = r[p * 2 + i];
     }
+}
+
+// direct global -> LDS staging (global_load_lds_dwordx4, CDNA4): no staging registers, no
+// ds_write pass.  One wave-instruction fills 64 consecutive 16-B LDS slots (base + 16*lane);
+// the XOR swizzle is applied on the SOURCE side: the lane owning LDS slot p = 4*row + pc
+// fetches chunk pc ^ f(row) of that row, all inside the same contiguous 1 KB of HBM.
+__device__ __forceinline__ void glds_stage(const Operands& op, int64_t row0, int64_t col0, int64_t k0, uint16_t* st,
+                                           int tid) {
+  const int64_t ab = ((k0 >> 5) * op.arows + row0) * BK, bb = ((k0 >> 5) * op.brows + col0) * BK;
+  const int w = tid >> 6, lane = tid & 63;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int slot0 = (w * 2 + i) * 64;          // first LDS slot of this wave-instruction
+    const int p = slot0 + lane, row = p >> 2;
+    const int src = row * 4 + swz(row, p & 3);   // swz is an involution
+    const uint16_t* srcs[4] = {op.ah + ab, op.al + ab, op.bh + bb, op.bl + bb};
+#pragma unroll
+    for (int part = 0; part < 4; ++part)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(uintptr_t)(srcs[part] + src * 8),
+                                       (__attribute__((address_space(3))) void*)(st + part * PART + slot0 * 8), 16, 0,
+                                       0);
+  }
 }
 
 __device__ __forceinline__ bf16x8 frag(const uint16_t* part, int row, int chunk) {
@@ -123,9 +163,15 @@ __device__ __forceinline__ void mma_stage(const uint16_t* st, f32x4 (&acc)[4][4]
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+#if LRM_PASSES >= 3
       acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
       acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#endif
+#if LRM_PASSES >= 1
       acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#else
+      acc[i][j][0] += (float)ah[i][0] * (float)bh[j][0] + (float)al[i][1] * (float)bl[j][1];
+#endif
     }
 }
 
@@ -139,6 +185,17 @@ __device__ __forceinline__ void gemm_tile(const Operands& op, int64_t row0, int6
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (kb >= ke) return;
   const int lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+#ifndef LRM_REGSTAGE
+  glds_stage(op, row0, col0, kb, smem, tid);
+  __syncthreads();
+  int cur = 0;
+  for (int64_t k = kb; k < ke; k += BK) {
+    if (k + BK < ke) glds_stage(op, row0, col0, k + BK, smem + (cur ^ 1) * STAGE, tid);
+    mma_stage(smem + cur * STAGE, acc, wm, wn, lane);
+    __syncthreads();   // drains this wave's LDS-DMA (vmcnt(0)) and publishes the stage
+    cur ^= 1;
+  }
+#else   // register staging (A/B reference)
   u32x4 r[8];
   load_stage(op, row0, col0, kb, r, tid);
   store_stage(smem, r, tid);
@@ -146,12 +203,17 @@ __device__ __forceinline__ void gemm_tile(const Operands& op, int64_t row0, int6
   int cur = 0;
   for (int64_t k = kb; k < ke; k += BK) {
     const bool more = k + BK < ke;
+#ifndef LRM_NOLOAD
     if (more) load_stage(op, row0, col0, k + BK, r, tid);
+#endif
     mma_stage(smem + cur * STAGE, acc, wm, wn, lane);
+#ifndef LRM_NOSTORE
     if (more) store_stage(smem + (cur ^ 1) * STAGE, r, tid);
+#endif
     __syncthreads();
     cur ^= 1;
   }
+#endif
 }
 
 __device__ __forceinline__ void put_hilo(uint16_t* hp, uint16_t* lp, float v) {
@@ -193,12 +255,14 @@ __global__ __launch_bounds__(THREADS, 2) void k_lr_fwd(FwdArgs a) {
   const int64_t rg = (local / a.col_tiles) * 8 + xcd;
   if (rg >= a.row_groups) return;   // grid-uniform (host sizes the grid exactly)
 
-  const int32_t* col_fit = reinterpret_cast<const int32_t*>(a.col_fit);
-  const float* bias = reinterpret_cast<const float*>(a.bias);
-  const int32_t* y = reinterpret_cast<const int32_t*>(a.y);
-  const uint8_t* roles = reinterpret_cast<const uint8_t*>(a.roles);
-  const Operands op{reinterpret_cast<const uint16_t*>(a.xh), reinterpret_cast<const uint16_t*>(a.xl), a.ldx,
-                    reinterpret_cast<const uint16_t*>(a.wh), reinterpret_cast<const uint16_t*>(a.wl), a.ldx};
+  const auto col_fit = GPTR(const int32_t, a.col_fit);
+  const auto bias = GPTR(const float, a.bias);
+  const auto y = GPTR(const int32_t, a.y);
+  const auto roles = GPTR(const uint8_t, a.roles);
+  const Operands op{reinterpret_cast<const uint16_t*>(a.xh), reinterpret_cast<const uint16_t*>(a.xl), a.xrows,
+                    reinterpret_cast<const uint16_t*>(a.wh), reinterpret_cast<const uint16_t*>(a.wl),
+                    a.col_tiles * BN};
+  const int64_t Mp = a.col_tiles * BN;
   const int64_t col0 = ct * BN;
   const int wm = w >> 1, wn = w & 1;
 
@@ -216,10 +280,11 @@ __global__ __launch_bounds__(THREADS, 2) void k_lr_fwd(FwdArgs a) {
     kind = reinterpret_cast<const int32_t*>(a.fit_kind)[f];
     role_off = (int64_t)reinterpret_cast<const int32_t*>(a.fit_split)[f] * a.n;
     s0 = reinterpret_cast<const float*>(a.scale)[f];
-    if (a.cw) cwf = reinterpret_cast<const float*>(a.cw) + (int64_t)f * a.cwC;
+    if (a.cw) cwf = GPTR(const float, a.cw) + (int64_t)f * a.cwC;
   }
-  uint16_t* RH = reinterpret_cast<uint16_t*>(a.rh) + (col0 + c) * a.ldr;
-  uint16_t* RL = reinterpret_cast<uint16_t*>(a.rl) + (col0 + c) * a.ldr;
+  // R^T is K-tiled too: (column, row) at ((row / 32) * Mp + column) * 32 + row % 32
+  const auto RH = GPTR(uint16_t, a.rh) + (col0 + c) * BK;
+  const auto RL = GPTR(uint16_t, a.rl) + (col0 + c) * BK;
   double lossacc = 0.0;
 
   for (int64_t rt = rg; rt < a.row_tiles; rt += a.row_groups) {
@@ -273,8 +338,9 @@ __global__ __launch_bounds__(THREADS, 2) void k_lr_fwd(FwdArgs a) {
               r[e] = (__expf(zs[zidx(lr0 + e, c + j)] - lse[e]) - (yv[e] == j ? 1.f : 0.f)) * sc[e];
             u32x4 hv, lv;
             split8(r, hv, lv);
-            *(u32x4*)(RH + j * a.ldr + g0) = hv;
-            *(u32x4*)(RL + j * a.ldr + g0) = lv;
+            const int64_t off = ((g0 >> 5) * Mp + j) * BK + (g0 & (BK - 1));
+            *(gvec_w)(RH + off) = hv;
+            *(gvec_w)(RL + off) = lv;
           }
         } else {           // 0: one sigmoid column (target y == 1); 2: OvR column j (target y == j)
           for (int j = 0; j < k; ++j) {
@@ -292,8 +358,9 @@ __global__ __launch_bounds__(THREADS, 2) void k_lr_fwd(FwdArgs a) {
             }
             u32x4 hv, lv;
             split8(r, hv, lv);
-            *(u32x4*)(RH + j * a.ldr + g0) = hv;
-            *(u32x4*)(RL + j * a.ldr + g0) = lv;
+            const int64_t off = ((g0 >> 5) * Mp + j) * BK + (g0 & (BK - 1));
+            *(gvec_w)(RH + off) = hv;
+            *(gvec_w)(RL + off) = lv;
           }
         }
       }
@@ -323,12 +390,13 @@ __global__ __launch_bounds__(THREADS, 2) void k_lr_grad(GradArgs a) {
   const int64_t mt = tile / a.n_tiles, nt = tile % a.n_tiles;
   const int64_t kb = s * a.Kc;
   const int64_t ke = kb + a.Kc < a.Kp ? kb + a.Kc : a.Kp;
-  const Operands op{reinterpret_cast<const uint16_t*>(a.rh), reinterpret_cast<const uint16_t*>(a.rl), a.ldr,
-                    reinterpret_cast<const uint16_t*>(a.xth), reinterpret_cast<const uint16_t*>(a.xtl), a.ldr};
+  const Operands op{reinterpret_cast<const uint16_t*>(a.rh), reinterpret_cast<const uint16_t*>(a.rl),
+                    a.m_tiles * BM, reinterpret_cast<const uint16_t*>(a.xth), reinterpret_cast<const uint16_t*>(a.xtl),
+                    a.n_tiles * BN};
   f32x4 acc[4][4];
   gemm_tile(op, mt * BM, nt * BN, kb, ke, smem, acc, tid);
   const int64_t ldo = a.n_tiles * BN;
-  float* out = reinterpret_cast<float*>(a.out) + s * (a.m_tiles * BM) * ldo;
+  const auto out = GPTR(float, a.out) + s * (a.m_tiles * BM) * ldo;
   const int wm = w >> 1, wn = w & 1;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -343,12 +411,13 @@ __global__ __launch_bounds__(THREADS, 2) void k_lr_grad(GradArgs a) {
     }
 }
 
-// fp32 [rows x cols] (row-major, ld) -> bf16 hi/lo, written row-major or transposed into
-// zero-padded destinations; one-time operand preparation per dataset.
+// fp32 [rows x cols] (row-major, ld) -> bf16 hi/lo in the K-tiled operand layout with
+// `drows` operand rows: not transposed, operand (row r, k c); transposed, operand
+// (row c, k r).  One-time operand preparation per dataset (destinations pre-zeroed).
 // blockIdx.x walks 64-row tiles (rows can be ~10M), blockIdx.y 64-column tiles.
 __global__ __launch_bounds__(256) void k_split_hilo(const float* __restrict__ src, int64_t rows, int64_t cols,
                                                      int64_t ld, uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
-                                                     int64_t ldd, int transpose) {
+                                                     int64_t drows, int transpose) {
   __shared__ float tile[64][65];
   const int64_t r0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -360,10 +429,12 @@ __global__ __launch_bounds__(256) void k_split_hilo(const float* __restrict__ sr
   for (int i = ty; i < 64; i += 4) {
     if (!transpose) {
       const int64_t r = r0 + i, c = c0 + tx;
-      if (r < rows && c < cols) put_hilo(hi + r * ldd + c, lo + r * ldd + c, tile[i][tx]);
+      const int64_t o = ((c >> 5) * drows + r) * BK + (c & (BK - 1));
+      if (r < rows && c < cols) put_hilo(hi + o, lo + o, tile[i][tx]);
     } else {   // destination [cols x rows]
       const int64_t r = r0 + tx, c = c0 + i;
-      if (r < rows && c < cols) put_hilo(hi + c * ldd + r, lo + c * ldd + r, tile[tx][i]);
+      const int64_t o = ((r >> 5) * drows + c) * BK + (r & (BK - 1));
+      if (r < rows && c < cols) put_hilo(hi + o, lo + o, tile[tx][i]);
     }
   }
 }
@@ -376,8 +447,8 @@ int dml_lr_mfma_tile() { return BM; }
 
 int dml_lr_mfma_fwd(const FwdArgs* a, hipStream_t st) {
   if (a->row_tiles <= 0 || a->col_tiles <= 0) return 0;
-  if (a->Kp % BK || a->ldx % 8 || a->ldr % 8 || a->row_groups % 8 || a->row_groups <= 0) return 2;
-  if (a->Kp > a->ldx || a->row_tiles * BM > a->ldr) return 2;
+  if (a->Kp % BK || a->row_groups % 8 || a->row_groups <= 0) return 2;
+  if (a->xrows != a->row_tiles * BM || a->kr != a->xrows) return 2;
   const int64_t blocks = a->col_tiles * a->row_groups;
   if (blocks > 0x7fffffff) return 2;
   k_lr_fwd<<<(unsigned)blocks, THREADS, 0, st>>>(*a);
@@ -386,20 +457,19 @@ int dml_lr_mfma_fwd(const FwdArgs* a, hipStream_t st) {
 
 int dml_lr_mfma_grad(const GradArgs* a, hipStream_t st) {
   if (a->m_tiles <= 0 || a->n_tiles <= 0) return 0;
-  if (a->Kp % BK || a->Kc % BK || a->ldr % 8 || a->S % 8 || a->S <= 0 || a->S * a->Kc < a->Kp || a->Kp > a->ldr)
-    return 2;
+  if (a->Kp % BK || a->Kc % BK || a->S % 8 || a->S <= 0 || a->S * a->Kc < a->Kp) return 2;
   const int64_t blocks = a->m_tiles * a->n_tiles * a->S;
   if (blocks > 0x7fffffff) return 2;
   k_lr_grad<<<(unsigned)blocks, THREADS, 0, st>>>(*a);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
-int dml_split_hilo(const float* src, int64_t rows, int64_t cols, int64_t ld, uint16_t* hi, uint16_t* lo, int64_t ldd,
-                   int32_t transpose, hipStream_t st) {
+int dml_split_hilo(const float* src, int64_t rows, int64_t cols, int64_t ld, uint16_t* hi, uint16_t* lo,
+                   int64_t drows, int32_t transpose, hipStream_t st) {
   if (rows <= 0 || cols <= 0) return 0;
   dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((cols + 63) / 64));
   if (grid.y > 65535) return 2;
-  k_split_hilo<<<grid, 256, 0, st>>>(src, rows, cols, ld, hi, lo, ldd, transpose);
+  k_split_hilo<<<grid, 256, 0, st>>>(src, rows, cols, ld, hi, lo, drows, transpose);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

@@ -8,6 +8,9 @@
 // statistics (correct count / SSE / sum y / sum y^2) so the host gets F x 4 doubles.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+// int64 argument fields -> GLOBAL address-space pointers (flat loads otherwise)
+#define GPTR(T, v) ((T*)(__attribute__((address_space(1))) T*)(uintptr_t)(v))
 #include "forest_common.h"
 
 namespace dml {
@@ -53,16 +56,16 @@ __device__ __forceinline__ void leaves_u(const NodeRec* __restrict__ nodes, cons
 template <int MAXC>
 __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
   const int f = blockIdx.y;
-  const int32_t* toff = (const int32_t*)a.fit_tree_off;
-  const int64_t* roff = (const int64_t*)a.fit_row_off;
+  const int32_t* toff = GPTR(const int32_t, a.fit_tree_off);
+  const int64_t* roff = GPTR(const int64_t, a.fit_row_off);
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t r0 = roff[f], nr = roff[f + 1] - r0;
   if (i >= nr) return;
   const int C = (int)a.n_classes;
-  const int32_t row = ((const int32_t*)a.rows)[r0 + i];
-  const uint8_t* xr = (const uint8_t*)a.Xb + (int64_t)row * a.ld;
-  const NodeRec* nodes = (const NodeRec*)a.nodes;
-  const double* val = (const double*)a.node_val;
+  const int32_t row = (GPTR(const int32_t, a.rows))[r0 + i];
+  const uint8_t* xr = GPTR(const uint8_t, a.Xb) + (int64_t)row * a.ld;
+  const NodeRec* nodes = GPTR(const NodeRec, a.nodes);
+  const double* val = GPTR(const double, a.node_val);
   float p[MAXC];
 #pragma unroll
   for (int k = 0; k < MAXC; ++k) p[k] = 0.f;
@@ -93,10 +96,10 @@ __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
 #pragma unroll
   for (int k = 1; k < MAXC; ++k)
     if (k < C && p[k] > bv) { bv = p[k]; best = k; }
-  ((int32_t*)a.out_pred)[r0 + i] = best;
+  (GPTR(int32_t, a.out_pred))[r0 + i] = best;
   if (a.out_proba) {
     const float nt = (float)(toff[f + 1] - toff[f]);
-    float* op = (float*)a.out_proba + (r0 + i) * C;
+    float* op = GPTR(float, a.out_proba) + (r0 + i) * C;
 #pragma unroll
     for (int k = 0; k < MAXC; ++k)
       if (k < C) op[k] = p[k] / nt;
@@ -105,15 +108,15 @@ __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
 
 __global__ __launch_bounds__(256) void k_predict_reg(PredictArgs a) {
   const int f = blockIdx.y;
-  const int32_t* toff = (const int32_t*)a.fit_tree_off;
-  const int64_t* roff = (const int64_t*)a.fit_row_off;
+  const int32_t* toff = GPTR(const int32_t, a.fit_tree_off);
+  const int64_t* roff = GPTR(const int64_t, a.fit_row_off);
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t r0 = roff[f], nr = roff[f + 1] - r0;
   if (i >= nr) return;
-  const int32_t row = ((const int32_t*)a.rows)[r0 + i];
-  const uint8_t* xr = (const uint8_t*)a.Xb + (int64_t)row * a.ld;
-  const NodeRec* nodes = (const NodeRec*)a.nodes;
-  const double* val = (const double*)a.node_val;
+  const int32_t row = (GPTR(const int32_t, a.rows))[r0 + i];
+  const uint8_t* xr = GPTR(const uint8_t, a.Xb) + (int64_t)row * a.ld;
+  const NodeRec* nodes = GPTR(const NodeRec, a.nodes);
+  const double* val = GPTR(const double, a.node_val);
   double acc = 0.0;
   int nt = 0;
   const int tend = toff[f + 1];
@@ -128,7 +131,7 @@ __global__ __launch_bounds__(256) void k_predict_reg(PredictArgs a) {
       if (v[0] > 0.0) { acc += v[1] / v[0]; ++nt; }
     }
   }
-  ((float*)a.out_pred)[r0 + i] = nt ? (float)(acc / nt) : 0.f;
+  (GPTR(float, a.out_pred))[r0 + i] = nt ? (float)(acc / nt) : 0.f;
 }
 
 // per-fit score statistics: out[f] = {match_count or SSE, sum y, sum y^2, n}
@@ -143,18 +146,18 @@ struct ScoreArgs {
 
 __global__ __launch_bounds__(256) void k_scores(ScoreArgs a) {
   const int f = blockIdx.x;
-  const int64_t* roff = (const int64_t*)a.fit_row_off;
+  const int64_t* roff = GPTR(const int64_t, a.fit_row_off);
   const int64_t r0 = roff[f], r1 = roff[f + 1];
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-  const int32_t* rows = (const int32_t*)a.rows;
+  const int32_t* rows = GPTR(const int32_t, a.rows);
   for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) {
     const int32_t row = rows[i];
     if (a.is_reg) {
-      const double y = ((const float*)a.yreg)[row];
-      const double e = (double)((const float*)a.pred)[i] - y;
+      const double y = (GPTR(const float, a.yreg))[row];
+      const double e = (double)(GPTR(const float, a.pred))[i] - y;
       s0 += e * e; s1 += y; s2 += y * y;
     } else {
-      s0 += ((const int32_t*)a.pred)[i] == ((const int32_t*)a.ycls)[row] ? 1.0 : 0.0;
+      s0 += (GPTR(const int32_t, a.pred))[i] == (GPTR(const int32_t, a.ycls))[row] ? 1.0 : 0.0;
     }
   }
   __shared__ double red[3][4];
@@ -165,7 +168,7 @@ __global__ __launch_bounds__(256) void k_scores(ScoreArgs a) {
   if ((threadIdx.x & 63) == 0) { red[0][w] = s0; red[1][w] = s1; red[2][w] = s2; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double* o = (double*)a.out + 4 * f;
+    double* o = GPTR(double, a.out) + 4 * f;
     o[0] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
     o[1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
     o[2] = red[2][0] + red[2][1] + red[2][2] + red[2][3];

@@ -115,8 +115,9 @@ def mfma_enabled(data) -> bool:
 class MfmaOperands:
     """bf16 hi/lo operand copies of one dataset for the MFMA objective, built once and kept
     resident next to the fp32 X (8 more bytes per element; 10M x 1000 -> 82 GB of the
-    288 GB HBM): ``X`` row-major with K padded to 32 (forward A operand) and ``X^T`` with
-    a row of ones appended (gradient B operand; the ones row yields the intercept gradient)."""
+    288 GB HBM): ``X`` (forward A operand, K = features padded to 32) and ``X^T`` with a row
+    of ones appended (gradient B operand, K = rows; the ones row yields the intercept
+    gradient), both in the kernel's K-tiled layout ``[K/32, rows, 32]``."""
 
     def __init__(self, data):
         lib = native.hip_lib()
@@ -125,16 +126,18 @@ class MfmaOperands:
         self.Kp = _roundup(d, 32)
         self.Dp = _roundup(d + 1, _TILE)
         bf = torch.bfloat16
-        self.xh = torch.zeros((self.npad, self.Kp), dtype=bf, device=dev)
+        self.xh = torch.zeros((self.Kp // 32, self.npad, 32), dtype=bf, device=dev)
         self.xl = torch.zeros_like(self.xh)
-        self.xth = torch.zeros((self.Dp, self.npad), dtype=bf, device=dev)
+        self.xth = torch.zeros((self.npad // 32, self.Dp, 32), dtype=bf, device=dev)
         self.xtl = torch.zeros_like(self.xth)
         st = native.stream_handle(dev)
-        for hi, lo, ldd, tr in ((self.xh, self.xl, self.Kp, 0), (self.xth, self.xtl, self.npad, 1)):
-            rc = lib.dml_split_hilo(native.ptr(data.X), n, d, d, native.ptr(hi), native.ptr(lo), ldd, tr, st)
+        for hi, lo, drows, tr in ((self.xh, self.xl, self.npad, 0), (self.xth, self.xtl, self.Dp, 1)):
+            rc = lib.dml_split_hilo(native.ptr(data.X), n, d, d, native.ptr(hi), native.ptr(lo), drows, tr, st)
             if rc:
                 raise RuntimeError(f"dml_split_hilo failed ({rc})")
-        self.xth[d, :n] = 1.0
+        ones = torch.zeros(self.npad, dtype=bf, device=dev)
+        ones[:n] = 1.0
+        self.xth[:, d, :] = ones.view(-1, 32)
 
 
 def mfma_operands(data) -> MfmaOperands:
@@ -171,10 +174,11 @@ class MfmaPlan:
         self.col_fit[self.colmap] = b.col_fit.to(torch.int32)
         self.fit_col0 = torch.tensor(pcol0, dtype=torch.int32, device=dev)
         bf = torch.bfloat16
-        self.wh = torch.zeros((self.Mp, ops.Kp), dtype=bf, device=dev)
+        self.w_lin = torch.zeros((2, self.Mp, ops.Kp), dtype=bf, device=dev)     # hi/lo, row-major
+        self.wh = torch.zeros((ops.Kp // 32, self.Mp, 32), dtype=bf, device=dev)  # K-tiled copies
         self.wl = torch.zeros_like(self.wh)
         self.bias = torch.zeros(self.Mp, dtype=torch.float32, device=dev)
-        self.rh = torch.zeros((self.Mp, ops.npad), dtype=bf, device=dev)   # rows >= n / pad columns stay 0
+        self.rh = torch.zeros((ops.npad // 32, self.Mp, 32), dtype=bf, device=dev)   # pad columns stay 0
         self.rl = torch.zeros_like(self.rh)
         self.loss = torch.zeros(b.F, dtype=torch.float64, device=dev)
         # forward: persistent, at most the resident workgroups (2 per CU), row groups % 8 == 0
@@ -191,13 +195,13 @@ class MfmaPlan:
         self.slabs = torch.empty((S, self.Mp, ops.Dp), dtype=torch.float32, device=dev)
         p = native.ptr
         self.fwd = native.LrFwdArgs(
-            xh=p(ops.xh), xl=p(ops.xl), ldx=ops.Kp, wh=p(self.wh), wl=p(self.wl), n=data.n, Kp=ops.Kp,
+            xh=p(ops.xh), xl=p(ops.xl), xrows=ops.npad, wh=p(self.wh), wl=p(self.wl), n=data.n, Kp=ops.Kp,
             row_tiles=row_tiles, col_tiles=col_tiles, row_groups=rg, bias=p(self.bias), col_fit=p(self.col_fit),
             fit_col0=p(self.fit_col0), fit_k=p(b.K), fit_kind=p(b.kind), fit_split=p(b.split), scale=p(b.scale),
             cw=p(b.cw), cwC=int(b.cw.shape[1]) if b.cw is not None else 0, y=p(data.y_cls), roles=p(data.roles),
-            rh=p(self.rh), rl=p(self.rl), ldr=ops.npad, loss=p(self.loss))
+            rh=p(self.rh), rl=p(self.rl), kr=ops.npad, loss=p(self.loss))
         self.grad = native.LrGradArgs(
-            rh=p(self.rh), rl=p(self.rl), ldr=ops.npad, xth=p(ops.xth), xtl=p(ops.xtl), m_tiles=col_tiles,
+            rh=p(self.rh), rl=p(self.rl), unused=0, xth=p(ops.xth), xtl=p(ops.xtl), m_tiles=col_tiles,
             n_tiles=n_tiles, Kp=ops.npad, S=S, Kc=Kc, out=p(self.slabs))
 
     def objective(self, data, b: "_Batch", W: torch.Tensor):
@@ -205,8 +209,11 @@ class MfmaPlan:
         d = data.d
         Wt = W[:d].t()
         hi = Wt.to(torch.bfloat16)
-        self.wh[self.colmap, :d] = hi
-        self.wl[self.colmap, :d] = (Wt - hi.float()).to(torch.bfloat16)
+        self.w_lin[0, self.colmap, :d] = hi
+        self.w_lin[1, self.colmap, :d] = (Wt - hi.float()).to(torch.bfloat16)
+        kb = self.w_lin.shape[2] // 32
+        self.wh.copy_(self.w_lin[0].view(self.Mp, kb, 32).transpose(0, 1))
+        self.wl.copy_(self.w_lin[1].view(self.Mp, kb, 32).transpose(0, 1))
         self.bias[self.colmap] = W[d] * b.icpt_col
         self.loss.zero_()
         lib = native.hip_lib()

@@ -81,10 +81,10 @@ ScoreArgs = _i64_struct("ScoreArgs", ["rows", "fit_row_off", "pred", "ycls", "yr
 # csrc/kernels/lr_mfma.hip argument blocks (MFMA logistic-regression objective)
 LrFwdArgs = _i64_struct(
     "LrFwdArgs",
-    ["xh", "xl", "ldx", "wh", "wl", "n", "Kp", "row_tiles", "col_tiles", "row_groups", "bias", "col_fit",
-     "fit_col0", "fit_k", "fit_kind", "fit_split", "scale", "cw", "cwC", "y", "roles", "rh", "rl", "ldr", "loss"],
+    ["xh", "xl", "xrows", "wh", "wl", "n", "Kp", "row_tiles", "col_tiles", "row_groups", "bias", "col_fit",
+     "fit_col0", "fit_k", "fit_kind", "fit_split", "scale", "cw", "cwC", "y", "roles", "rh", "rl", "kr", "loss"],
 )
-LrGradArgs = _i64_struct("LrGradArgs", ["rh", "rl", "ldr", "xth", "xtl", "m_tiles", "n_tiles", "Kp", "S", "Kc", "out"])
+LrGradArgs = _i64_struct("LrGradArgs", ["rh", "rl", "unused", "xth", "xtl", "m_tiles", "n_tiles", "Kp", "S", "Kc", "out"])
 
 
 def _load(path: str) -> ctypes.CDLL:
