@@ -46,6 +46,7 @@ class JobSpec:
     return_train_score: bool = False
     keep_models: str = "best"                 # none | best | all
     seed: int = 0
+    raise_batch_errors: bool = False          # device errors propagate (the caller retries the batch)
 
     def split_key(self):
         return (self.cv, self.holdout, str(self.test_size), str(self.random_state), is_classifier(self.model_type))
@@ -125,6 +126,8 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
             for t in tasks:
                 errors.setdefault(t.candidate, f"ParamError: {e}")
         except Exception as e:  # device/kernel failure: every candidate of the batch fails
+            if spec.raise_batch_errors:
+                raise
             msg = f"{type(e).__name__}: {e}"
             for t in tasks:
                 errors.setdefault(t.candidate, msg)

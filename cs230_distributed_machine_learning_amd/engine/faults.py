@@ -1,0 +1,109 @@
+"""Fault injection and bounded retries for worker slices.
+
+The reference has no fault injection (only a commented-out 30-45 s sleep,
+aws-prod/worker/worker.py:308-311) and never retries a failed task: a failed subtask is
+reported once and the job hangs below 100 % (D5, master/task_handler.py:91).  Here:
+
+* a slice whose device batch raises (HIP error, OOM, injected fault) is retried up to
+  ``Config.max_retries`` times on the same rank before its candidates are failed with
+  the error (they then count as terminal and take ``error_score``);
+* ``DML_INJECT_FAIL_RATE`` (0..1) makes a deterministic fraction of slice *attempts*
+  raise ``InjectedFault`` — decided by a hash of (job seed, slice, attempt), so a test
+  can predict exactly which attempts fail;
+* ``DML_KILL_RANK_AFTER="<rank>:<k>"`` makes that rank hard-exit (``os._exit``) right
+  after claiming its (k+1)-th slice, i.e. with claimed-but-unpublished work — what a
+  crashed GPU process looks like to the controller, which must detect the silence and
+  re-queue the slice to the survivors.
+"""
+from __future__ import annotations
+
+import os
+import zlib
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+
+class InjectedFault(RuntimeError):
+    pass
+
+
+@dataclass(frozen=True)
+class FaultPlan:
+    fail_rate: float = 0.0
+    kill_rank: Optional[int] = None
+    kill_after: int = 0
+    max_retries: int = 2
+
+    @classmethod
+    def from_env(cls) -> "FaultPlan":
+        rate = float(os.environ.get("DML_INJECT_FAIL_RATE", "0") or 0.0)
+        kill = os.environ.get("DML_KILL_RANK_AFTER", "")
+        kr, ka = None, 0
+        if kill:
+            a, _, b = kill.partition(":")
+            kr, ka = int(a), int(b or 0)
+        retries = int(os.environ.get("DML_MAX_RETRIES", "2"))
+        return cls(min(max(rate, 0.0), 1.0), kr, ka, max(0, retries))
+
+    def should_fail(self, seed: int, slice_key: str, attempt: int) -> bool:
+        if self.fail_rate <= 0.0:
+            return False
+        h = zlib.crc32(f"{seed}:{slice_key}:{attempt}".encode()) & 0xFFFFFFFF
+        return h < self.fail_rate * 4294967296.0
+
+    def kill_now(self, rank: int, slices_done: int) -> bool:
+        return self.kill_rank is not None and rank == self.kill_rank and slices_done >= self.kill_after
+
+
+_PLAN: Optional[FaultPlan] = None
+
+
+def plan() -> FaultPlan:
+    global _PLAN
+    if _PLAN is None:
+        _PLAN = FaultPlan.from_env()
+    return _PLAN
+
+
+def reset() -> None:
+    """Re-read the environment (tests)."""
+    global _PLAN
+    _PLAN = None
+
+
+def maybe_inject(seed: int, slice_key: str, attempt: int) -> None:
+    if plan().should_fail(seed, slice_key, attempt):
+        raise InjectedFault(f"injected fault (slice {slice_key}, attempt {attempt})")
+
+
+def maybe_kill(rank: int, slices_done: int) -> None:
+    if plan().kill_now(rank, slices_done):
+        os._exit(17)
+
+
+def run_with_retries(fn, seed: int, slice_key: str, retries: Optional[int] = None) -> Tuple[object, int, Optional[BaseException]]:
+    """Call ``fn()`` with up to ``retries`` re-tries -> (value, attempts, last error).
+
+    ``value`` is None when every attempt raised."""
+    n = plan().max_retries if retries is None else retries
+    last: Optional[BaseException] = None
+    for attempt in range(n + 1):
+        try:
+            maybe_inject(seed, slice_key, attempt)
+            return fn(), attempt + 1, None
+        except (RuntimeError, OSError, MemoryError) as e:  # device / OOM / injected: retry the batch
+            last = e
+            _release_device_memory()
+        except Exception as e:  # deterministic (parameter / data) errors are not retried
+            return None, attempt + 1, e
+    return None, n + 1, last
+
+
+def _release_device_memory() -> None:
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+    except Exception:
+        pass

@@ -29,6 +29,7 @@ from ..data.registry import DatasetRegistry
 from ..models.base import ParamError, family_of, is_classifier, supported_models
 from ..search.grid import expand_candidates
 from ..utils.log import get_logger
+from ..utils import trace
 from .jobs import Job, JobTable, json_safe, make_subtasks, now_iso, utc_iso
 from .model_store import ModelStore
 from .scheduler import Scheduler, Unit, chunk_units
@@ -412,18 +413,26 @@ def run_slice(plan: Dict[str, Any], params: List[Dict[str, Any]], subtask_ids: L
               worker_id: str, device_name: str, seed: int = 0):
     """Run one slice of candidates on a device -> (results, J3 metrics per candidate, wall s).
 
-    Controller-free so every rank of the distributed runner executes exactly this.
+    Controller-free so every rank of the distributed runner executes exactly this.  A
+    batch that raises (device error, injected fault) is retried up to
+    ``DML_MAX_RETRIES`` times (engine/faults.py) before its candidates fail terminally.
     """
-    from .executor import JobSpec, run_candidates
+    from . import faults
+    from .executor import CandidateResult, JobSpec, run_candidates
 
     spec = JobSpec(model_type=plan["model_type"], candidates=params, cv=plan["cv"], scoring=plan["scoring"],
                    holdout=plan["holdout"], test_size=plan["test_size"], random_state=plan["random_state"],
-                   error_score=plan["error_score"], keep_models="none", seed=seed)
+                   error_score=plan["error_score"], keep_models="none", seed=seed, raise_batch_errors=True)
     received = utc_iso()
+    slice_key = ",".join(str(int(c)) for c in cand_ids)
     with _Sampler() as smp:
         started = utc_iso()
         t0 = time.perf_counter()
-        results = run_candidates(dd, spec, cand_ids)
+        with trace.range(f"slice {plan['model_type']} x{len(cand_ids)}"):
+            results, attempts, err = faults.run_with_retries(lambda: run_candidates(dd, spec, cand_ids), seed, slice_key)
+        if results is None:
+            results = [CandidateResult(candidate=c, ok=False, error=f"{type(err).__name__}: {err} "
+                                       f"(after {attempts} attempts)") for c in cand_ids]
         wall = time.perf_counter() - t0
     finished = utc_iso()
     cpu, mem = smp.avg()
@@ -434,7 +443,7 @@ def run_slice(plan: Dict[str, Any], params: List[Dict[str, Any]], subtask_ids: L
             "status": "DONE" if r.ok else "FAILED", "received_at": received, "started_at": started,
             "finished_at": finished, "cpu_percent_avg": cpu, "mem_percent_avg": mem, "algo": plan["model_type"],
             "device": device_name, "fit_seconds": r.fit_seconds, "slice_wall_seconds": wall,
-            "n_fits": r.result.get("n_fits", 0) if r.ok else 0,
+            "n_fits": r.result.get("n_fits", 0) if r.ok else 0, "attempts": attempts,
         }
     return results, metrics, wall
 

@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from ..utils import native
+from ..utils import trace
 
 GINI, ENTROPY, MSE = 0, 1, 2
 INT32_MAX = 2**31 - 1
@@ -144,7 +145,8 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
         vals = torch.empty((pool_cap, VC), dtype=torch.float64, device=dev)
         a.nodes, a.node_val, a.pool_cap = native.ptr(nodes), native.ptr(vals), pool_cap
         a.status_out = 0
-        rc = lib.dml_forest_build(ctypes.byref(a), stream)
+        with trace.range("forest_build"):   # host-side launch sequence of every tier
+            rc = lib.dml_forest_build(ctypes.byref(a), stream)
         if rc:
             raise RuntimeError(f"dml_forest_build failed ({rc}): {native.hip_error(lib)}")
         if a.status_out == 1:
@@ -251,7 +253,8 @@ def predict(fb: ForestBuild, Xb, fit_tree_off: np.ndarray, fit_row_off: np.ndarr
         p.out_pred, p.out_proba = native.ptr(out), native.ptr(proba)
         p.F = F
         p.max_rows = int(np.max(np.diff(fit_row_off))) if F else 0
-        rc = lib.dml_forest_predict(ctypes.byref(p), native.stream_handle(dev))
+        with trace.range("forest_predict"):
+            rc = lib.dml_forest_predict(ctypes.byref(p), native.stream_handle(dev))
         if rc:
             raise RuntimeError(f"dml_forest_predict failed ({rc})")
         return (out, proba) if want_proba else out

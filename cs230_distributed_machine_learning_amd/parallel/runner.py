@@ -32,6 +32,7 @@ from typing import Any, Dict, List, Optional
 import numpy as np
 import torch
 
+from ..engine import faults
 from ..engine.jobs import Job, json_safe
 from ..engine.service import (Controller, DeviceCache, Runner, candidate_costs, finalize_job, job_plan, job_seed,
                               plan_slices, publish_results, run_slice)
@@ -111,10 +112,12 @@ class _Heartbeat:
         self._t.start()
 
     def _loop(self):
-        while not self._stop.wait(HB_PERIOD_S):
+        while True:
             try:
                 self.store.set(f"hb/{self.rank}", str(time.time()))
             except Exception:
+                return
+            if self._stop.wait(HB_PERIOD_S):
                 return
 
     def stop(self):
@@ -172,33 +175,43 @@ class WorkerCore:
 
                 return [CandidateResult(candidate=c, ok=False, error=f"{type(e).__name__}: {e}") for c in ids], {}, 0.0
 
+        def publish(i, results, metrics, wall, local):
+            if local:
+                for res in results:
+                    if res.ok and n_cv:
+                        scores[res.candidate, :n_cv] = torch.tensor(
+                            [np.nan if v is None else v for v in res.result.get("cv_scores", [np.nan] * n_cv)],
+                            dtype=torch.float64)
+                        owned[res.candidate] = 1.0
+            st.set(f"job/{seq}/res/{i}", _enc_results(results, metrics))
+            st.set(f"job/{seq}/wall/{i}", str(wall))
+            if st.add(f"job/{seq}/first/{i}", 1) == 1:   # count each slice once (a re-queued
+                st.add(f"job/{seq}/done", 1)             # slice may finish twice)
+
+        n_done = 0
         while True:
             i = st.add(f"job/{seq}/next", 1) - 1
             if i >= len(slices):
                 break
             st.set(f"job/{seq}/claim/{i}", str(r))
-            ids = slices[i]
-            results, metrics, wall = exec_slice(ids)
-            for res in results:
-                if res.ok and n_cv:
-                    scores[res.candidate, :n_cv] = torch.tensor(
-                        [np.nan if v is None else v for v in res.result.get("cv_scores", [np.nan] * n_cv)],
-                        dtype=torch.float64)
-                    owned[res.candidate] = 1.0
-            st.set(f"job/{seq}/res/{i}", _enc_results(results, metrics))
-            st.set(f"job/{seq}/wall/{i}", str(wall))
-            st.add(f"job/{seq}/done", 1)
-        # requeued slices of a dead rank (rank 0 pushes them onto job/<seq>/rq)
-        while True:
-            j = st.add(f"job/{seq}/rq_next", 1) - 1
+            faults.maybe_kill(r, n_done)   # fault injection: die holding a claimed slice
+            results, metrics, wall = exec_slice(slices[i])
+            publish(i, results, metrics, wall, True)
+            n_done += 1
+        # Slices re-queued from a dead rank (rank 0's monitor appends them to job/<seq>/rq).
+        # Stay until every slice has a result: a rank that left before the death was
+        # detected would otherwise strand the re-queued work.  Each entry is claimed once.
+        j = 0
+        while int(st.add(f"job/{seq}/done", 0)) < len(slices):
             n_rq = int(st.add(f"job/{seq}/rq_len", 0))
-            if j >= n_rq:
-                break
-            i = int(st.get(f"job/{seq}/rq/{j}"))
-            ids = slices[i]
-            results, metrics, wall = exec_slice(ids)
-            st.set(f"job/{seq}/res/{i}", _enc_results(results, metrics))
-            st.add(f"job/{seq}/done", 1)
+            if j < n_rq:
+                if st.add(f"job/{seq}/rq_claim/{j}", 1) == 1:
+                    i = int(st.get(f"job/{seq}/rq/{j}"))
+                    results, metrics, wall = exec_slice(slices[i])
+                    publish(i, results, metrics, wall, False)   # not in this rank's RCCL share
+                j += 1
+                continue
+            time.sleep(0.02)
         # numeric result path: one RCCL all-reduce of the score matrix (when every rank is alive)
         st.add(f"job/{seq}/fin", 1)
         st.wait([f"job/{seq}/mode"])
@@ -221,6 +234,7 @@ class DistributedRunner(Runner):
         self.seq = 0
         self.stop = False
         self.dead: set = set()
+        self._hb_missing_since: Dict[int, float] = {}
         self.session_used: Dict[str, float] = {}
 
     def bind(self, controller: Controller) -> None:
@@ -386,9 +400,11 @@ class DistributedRunner(Runner):
             if r in self.dead:
                 continue
             try:
-                hb = float(st.get(f"hb/{r}")) if st.check([f"hb/{r}"]) else now
+                hb = float(st.get(f"hb/{r}")) if st.check([f"hb/{r}"]) else None
             except Exception:
                 hb = now
+            if hb is None:   # never beat: silent since we first looked
+                hb = self._hb_missing_since.setdefault(r, now)
             if now - hb > self.ctl.config.dead_after_s:
                 log.warning("rank %d missed heartbeats for %.1fs: re-queueing its slices", r, now - hb)
                 self.dead.add(r)
@@ -420,7 +436,8 @@ class DistributedRunner(Runner):
 
     def _cleanup(self, seq: int, n: int) -> None:
         st = self.core.store
-        for k in [f"job/{seq}"] + [f"job/{seq}/{s}/{i}" for s in ("res", "claim", "wall") for i in range(n)]:
+        for k in [f"job/{seq}"] + [f"job/{seq}/{s}/{i}" for s in ("res", "claim", "wall", "first", "rq_claim")
+                                   for i in range(n)]:
             try:
                 st.delete_key(k)
             except Exception:
@@ -439,8 +456,11 @@ def worker_loop(core: WorkerCore) -> None:
                 try:
                     st.wait([key], __import__("datetime").timedelta(seconds=60))
                     break
-                except Exception:
+                except TimeoutError:
                     continue  # idle longer than the store timeout: keep waiting
+                except Exception:   # the store (hosted by rank 0) is gone: the job server exited
+                    log.warning("rank %d lost the controller store; leaving", core.inf.rank)
+                    return
             msg = json.loads(st.get(key))
             if msg.get("shutdown"):
                 return

@@ -9,11 +9,29 @@ def kernel_stats(d):
     rows = []
     for f in glob.glob(f"{d}/**/*kernel_stats.csv", recursive=True):
         rows += list(csv.DictReader(open(f)))
+    if not rows:
+        return kernel_stats_db(d)
     tot = sum(float(r["TotalDurationNs"]) for r in rows) or 1
     out = []
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
         out.append(f"  {r['Name'][:60]:60s} calls={int(r['Calls']):6d} total_ms={float(r['TotalDurationNs'])/1e6:9.2f} "
                    f"{100*float(r['TotalDurationNs'])/tot:5.1f}%")
+    return out
+
+
+def kernel_stats_db(d):
+    """rocprofv3 >= ROCm 7 writes a rocpd SQLite database by default (``*_results.db``)."""
+    import sqlite3
+
+    out = []
+    for f in glob.glob(f"{d}/**/*.db", recursive=True):
+        c = sqlite3.connect(f)
+        for name, calls, tot_ns, avg_ns, pct in c.execute(
+                "select name, total_calls, total_duration, average, percentage from top_kernels"):
+            if pct < 0.01:
+                continue
+            out.append(f"  {name[:60]:60s} calls={int(calls):6d} total_ms={tot_ns/1e3:9.2f} avg_us={avg_ns:9.1f} "
+                       f"{pct:5.1f}%")
     return out
 
 

@@ -1,0 +1,169 @@
+"""Fault injection, bounded retries and kill-a-rank recovery.
+
+Reference behaviour being replaced: a failed task is reported once and never retried,
+and the job hangs (D5); a dead worker's queued tasks are re-sent through Kafka
+(scheduler_service.py:218-247).  Here a failing device batch is retried up to
+``DML_MAX_RETRIES`` times, and a rank that dies holding a claimed slice has that slice
+re-run by the survivors (store path), with the job still completing."""
+import os
+import socket
+import tempfile
+import time
+
+import pytest
+import torch.multiprocessing as mp
+
+from cs230_distributed_machine_learning_amd.config import Config
+from cs230_distributed_machine_learning_amd.engine import faults
+from cs230_distributed_machine_learning_amd.engine.service import Controller
+
+
+def _j1(job_id, model_type, grid, cv=3):
+    return {"job_id": job_id, "dataset_id": "iris", "model_details": {
+        "model_type": model_type, "search_type": "GridSearchCV", "hyperparameters": {
+            "base_estimator_params": {}, "search_params": {"param_grid": grid}, "cv_params": {"cv": cv}}},
+        "train_params": {"target_column": "target"}}
+
+
+@pytest.fixture
+def fault_env(monkeypatch):
+    def set_env(**kw):
+        for k, v in kw.items():
+            monkeypatch.setenv(k, str(v))
+        faults.reset()
+    yield set_env
+    faults.reset()
+
+
+def test_fault_plan_is_deterministic(fault_env):
+    fault_env(DML_INJECT_FAIL_RATE=0.5, DML_KILL_RANK_AFTER="3:2", DML_MAX_RETRIES=4)
+    p = faults.plan()
+    assert p.kill_rank == 3 and p.kill_after == 2 and p.max_retries == 4
+    draws = [p.should_fail(7, "1,2", a) for a in range(200)]
+    assert draws == [p.should_fail(7, "1,2", a) for a in range(200)]
+    assert 60 < sum(draws) < 140
+    assert not p.kill_now(3, 1) and p.kill_now(3, 2) and not p.kill_now(2, 5)
+
+
+def test_retry_recovers_and_exhaustion_fails(fault_env):
+    fault_env(DML_INJECT_FAIL_RATE=0.5, DML_MAX_RETRIES=8)
+    calls = []
+    val, attempts, err = faults.run_with_retries(lambda: calls.append(1) or "ok", seed=1, slice_key="a")
+    p = faults.plan()
+    assert val == "ok" and err is None and len(calls) == 1
+    assert all(p.should_fail(1, "a", k) for k in range(attempts - 1)) and not p.should_fail(1, "a", attempts - 1)
+    fault_env(DML_INJECT_FAIL_RATE=1.0, DML_MAX_RETRIES=2)
+    val, attempts, err = faults.run_with_retries(lambda: "never", seed=1, slice_key="a")
+    assert val is None and attempts == 3 and isinstance(err, faults.InjectedFault)
+    # deterministic errors are not retried
+    fault_env(DML_INJECT_FAIL_RATE=0.0)
+    val, attempts, err = faults.run_with_retries(lambda: (_ for _ in ()).throw(ValueError("bad")), 1, "b", retries=5)
+    assert val is None and attempts == 1 and isinstance(err, ValueError)
+
+
+def _run_job(tmp_path, grid):
+    c = Controller(Config(data_root=str(tmp_path / "data"), device="cpu", chunk_target_s=0.0))
+    try:
+        sid = c.create_session()[1]["session_id"]
+        c.download_data(sid, {"dataset_url": "iris", "dataset_name": "iris", "dataset_type": "sklearn"})
+        st, ack = c.train(sid, _j1("job-f", "LogisticRegression", grid))
+        assert st in (200, 202), ack
+        c.table.wait_finished(ack["job_id"], timeout=120)
+        return c.check_status(sid, ack["job_id"])[1], c.metrics(sid, ack["job_id"])[1]
+    finally:
+        c.shutdown()
+
+
+def test_local_job_survives_injected_faults(fault_env, tmp_path):
+    fault_env(DML_INJECT_FAIL_RATE=0.4, DML_MAX_RETRIES=10)
+    status, metrics = _run_job(tmp_path, {"C": [0.1, 1.0, 10.0, 100.0]})
+    assert status["job_status"] == "completed"
+    res = status["job_result"]["results"]
+    assert len(res) == 4 and all("cv_scores" in r for r in res)
+    assert max(m["attempts"] for m in metrics) > 1   # some slices really were retried
+
+
+def test_local_job_exhausted_retries_fail_terminally(fault_env, tmp_path):
+    fault_env(DML_INJECT_FAIL_RATE=1.0, DML_MAX_RETRIES=1)
+    status, metrics = _run_job(tmp_path, {"C": [0.1, 1.0]})
+    assert status["job_status"] == "failed"             # terminal, not stuck (D5)
+    assert all(m["status"] == "FAILED" and m["attempts"] == 2 for m in metrics)
+
+
+# ---- kill a rank mid-job (3 ranks, gloo) ------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, root, outq):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), OMP_NUM_THREADS="1", DML_KILL_RANK_AFTER="2:0", DML_DEAD_AFTER_S="3")
+    import threading
+
+    from cs230_distributed_machine_learning_amd.parallel import dist
+    from cs230_distributed_machine_learning_amd.parallel.runner import DistributedRunner, WorkerCore, worker_loop
+
+    inf = dist.init(want_gpu=False, timeout_s=60)
+    core = WorkerCore(inf.device)
+    if rank == 0:
+        cfg = Config.from_env(data_root=root, device="cpu", chunk_target_s=0.0)
+        runner = DistributedRunner(core)
+        ctl = Controller(cfg, runner=runner)
+
+        def drive():
+            try:
+                sid = ctl.create_session()[1]["session_id"]
+                ctl.download_data(sid, {"dataset_url": "iris", "dataset_name": "iris", "dataset_type": "sklearn"})
+                out = []
+                for jid, grid in (("j-kill", {"C": [0.01, 0.03, 0.1, 0.3, 1.0, 3.0, 10.0, 30.0, 100.0, 300.0, 1000.0, 3000.0]}),
+                                  ("j-after", {"C": [0.5, 5.0]})):
+                    st, ack = ctl.train(sid, _j1(jid, "LogisticRegression", grid))
+                    ctl.table.wait_finished(ack["job_id"], timeout=120)
+                    out.append((ctl.check_status(sid, ack["job_id"])[1], ctl.metrics(sid, ack["job_id"])[1]))
+                outq.put(("ok", out, sorted(runner.dead)))
+            except Exception:  # pragma: no cover
+                import traceback
+
+                outq.put(("err", traceback.format_exc()))
+            finally:
+                runner.shutdown()
+
+        t = threading.Thread(target=drive, daemon=True)
+        t.start()
+        runner.serve_forever()
+        t.join()
+        time.sleep(1.0)   # let rank 1 read the shutdown key before the store host exits
+    else:
+        worker_loop(core)
+    os._exit(0)   # a peer is dead: skip the collective teardown
+
+
+def test_killed_rank_slices_are_requeued():
+    root = tempfile.mkdtemp()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 3, port, root, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    try:
+        out = q.get(timeout=300)
+    finally:
+        deadline = time.time() + 60
+        for p in procs:
+            p.join(timeout=max(1, deadline - time.time()))
+            if p.is_alive():
+                p.kill()
+    assert out[0] == "ok", out[1]
+    (st1, m1), (st2, m2) = out[1]
+    assert out[2] == [2]                                   # rank 2 was declared dead
+    assert procs[2].exitcode == 17                         # ... because it crashed (injected)
+    assert st1["job_status"] == "completed" and len(st1["job_result"]["results"]) == 12
+    assert all("cv_scores" in r for r in st1["job_result"]["results"])
+    assert {m["worker_id"] for m in m1} <= {"rank0", "rank1", "rank2"}
+    assert st2["job_status"] == "completed" and len(st2["job_result"]["results"]) == 2
+    assert {m["worker_id"] for m in m2} <= {"rank0", "rank1"}
