@@ -71,6 +71,26 @@ def build_cpu(force: bool = False) -> str:
     return CPU_LIB
 
 
+SAN_EXE = os.path.join(LIB, "host_selftest_asan")
+
+
+def build_sanitized(force: bool = False) -> str:
+    """Host runtime + ``csrc/tests/host_selftest.cpp`` with AddressSanitizer and
+    UndefinedBehaviorSanitizer (host code only — GPU sanitizers are not used on MI355X
+    here).  Any report aborts the executable (``-fno-sanitize-recover=all``)."""
+    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))) + [os.path.join(CSRC, "tests", "host_selftest.cpp")]
+    deps = srcs + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
+    os.makedirs(LIB, exist_ok=True)
+    if force or _stale(SAN_EXE, deps):
+        cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
+        tmp = SAN_EXE + ".tmp"
+        _run([cxx, "-O1", "-g", "-std=c++17", "-fopenmp", "-ffp-contract=off", "-fsanitize=address,undefined",
+              "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-I", os.path.join(CSRC, "kernels"), *srcs,
+              "-o", tmp])
+        os.replace(tmp, SAN_EXE)
+    return SAN_EXE
+
+
 def build_all(force: bool = False) -> tuple[str, str]:
     return build_cpu(force), build_hip(force)
 
@@ -79,7 +99,10 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--cpu-only", action="store_true")
+    ap.add_argument("--sanitize", action="store_true", help="also build the ASan/UBSan host self-test")
     args = ap.parse_args()
+    if args.sanitize:
+        print(build_sanitized(args.force))
     print(build_cpu(args.force))
     if not args.cpu_only:
         print(build_hip(args.force))
