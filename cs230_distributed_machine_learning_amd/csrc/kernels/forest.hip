@@ -25,6 +25,7 @@
 #include <type_traits>
 #include <algorithm>
 #include <stdio.h>
+#include <stdlib.h>
 #include "forest_common.h"
 #include "wave_ops.h"
 
@@ -137,11 +138,26 @@ struct Ctx {
   int32_t wave_max, block_max, chunk, kg_wave, kg_block, kg_large, slack_wave;
   int32_t sub_max, sub_cache_d;
   int64_t ystride;
+  // row words: rows_cur/rows_next hold row | bootstrap weight << rbits | class << (rbits + 4)
+  // when `packed` (the weight and label travel with the row through every partition, so
+  // no kernel re-gathers ycls or re-hashes the bootstrap weight); else plain row ids
+  uint32_t rmask;
+  int32_t rbits, packed;
 };
 
 // target vector of a tree (shared y, or its own row of the boosting target matrix)
 __device__ __forceinline__ const float* tree_y(const Ctx& c, const TreeSpec& s) {
   return c.ystride ? c.yreg + (int64_t)s.target * c.ystride : c.yreg;
+}
+
+__device__ __forceinline__ uint32_t word_row(const Ctx& c, uint32_t wd) { return wd & c.rmask; }
+
+__device__ __forceinline__ uint32_t word_weight(const Ctx& c, const TreeSpec& s, uint32_t wd) {
+  return c.packed ? (wd >> c.rbits) & 15u : boot_weight(s, wd);
+}
+
+__device__ __forceinline__ int word_cls(const Ctx& c, uint32_t wd) {
+  return c.packed ? (int)(wd >> (c.rbits + 4)) : c.ycls[wd];
 }
 
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -597,6 +613,16 @@ __device__ __forceinline__ uint64_t row_payload(const Ctx& c, const float* ty, u
 }
 
 template <int MODE>
+__device__ __forceinline__ uint64_t word_payload(const Ctx& c, const TreeSpec& s, const float* ty, uint32_t wd) {
+  if (!c.packed) return row_payload<MODE>(c, ty, wd, boot_weight(s, wd));
+  const uint32_t w = (wd >> c.rbits) & 15u;
+  if constexpr (MODE == 0) return (uint64_t)(wd >> (c.rbits + 4)) | ((uint64_t)w << 32);
+  else if constexpr (MODE == 1) return pack_bin((int)(wd >> (c.rbits + 4)), w);
+  else return (uint64_t)__builtin_bit_cast(uint32_t, (float)w) |
+              ((uint64_t)__builtin_bit_cast(uint32_t, ty[wd & c.rmask]) << 32);
+}
+
+template <int MODE>
 __device__ __forceinline__ void hist_add(typename HT<MODE>::T* hj, const Ctx& c, int b, uint64_t pl) {
   if constexpr (MODE == 0) {
     atomicAdd(&hj[(int)(uint32_t)pl * 256 + b], (uint32_t)(pl >> 32));
@@ -668,7 +694,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     }
 #pragma unroll
     for (int u = 0; u < RPT; ++u)
-      rpl[u] = rrow[u] != 0xFFFFFFFFu ? row_payload<MODE>(c, ty, rrow[u], boot_weight(s, rrow[u])) : 0ull;
+      rpl[u] = rrow[u] != 0xFFFFFFFFu ? word_payload<MODE>(c, s, ty, rrow[u]) : 0ull;
   };
   if (reg_rows) load_rows(0);
 #pragma unroll
@@ -703,17 +729,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
       for (int j = 0; j < KGMAX; ++j) fj[j] = j < g ? (int)feats[j] : 0;
       auto row_at = [&](int r) -> uint32_t { return r < cnt ? rows[r] : INV; };
       uint32_t r0 = row_at(tid), r1 = row_at(NT + tid);
-      uint64_t pl0 = r0 != INV ? row_payload<MODE>(c, ty, r0, boot_weight(s, r0)) : 0ull;
+      uint64_t pl0 = r0 != INV ? word_payload<MODE>(c, s, ty, r0) : 0ull;
       uint32_t b0[KGMAX];
 #pragma unroll
       for (int j = 0; j < KGMAX; ++j)
-        b0[j] = (j < g && r0 != INV) ? (uint32_t)c.Xb[(int64_t)r0 * c.ld + fj[j]] : 0u;
+        b0[j] = (j < g && r0 != INV) ? (uint32_t)c.Xb[(int64_t)(r0 & c.rmask) * c.ld + fj[j]] : 0u;
       for (int base = 0; base < cnt; base += NT) {
-        const uint64_t pl1 = r1 != INV ? row_payload<MODE>(c, ty, r1, boot_weight(s, r1)) : 0ull;
+        const uint64_t pl1 = r1 != INV ? word_payload<MODE>(c, s, ty, r1) : 0ull;
         uint32_t b1[KGMAX];
 #pragma unroll
         for (int j = 0; j < KGMAX; ++j)
-          b1[j] = (j < g && r1 != INV) ? (uint32_t)c.Xb[(int64_t)r1 * c.ld + fj[j]] : 0u;
+          b1[j] = (j < g && r1 != INV) ? (uint32_t)c.Xb[(int64_t)(r1 & c.rmask) * c.ld + fj[j]] : 0u;
         const uint32_t r2 = row_at(base + 2 * NT + tid);
         if (r0 != INV) {
 #pragma unroll
@@ -735,7 +761,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
           const int64_t f = feats[j];
 #pragma unroll
           for (int u = 0; u < RPT; ++u)
-            bins[j][u] = rrow[u] != 0xFFFFFFFFu ? (uint32_t)c.Xb[(int64_t)rrow[u] * c.ld + f] : 0u;
+            bins[j][u] = rrow[u] != 0xFFFFFFFFu ? (uint32_t)c.Xb[(int64_t)(rrow[u] & c.rmask) * c.ld + f] : 0u;
         }
       }
 #pragma unroll
@@ -840,7 +866,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   // ids two chunks ahead are prefetched while the current chunk is ranked and written
   constexpr uint32_t INVR = 0xFFFFFFFFu;
   auto prow = [&](int r) -> uint32_t { return r < cnt ? rows[r] : INVR; };
-  auto pbin = [&](uint32_t r) -> uint32_t { return r != INVR ? (uint32_t)c.Xb[(int64_t)r * c.ld + feat] : 0u; };
+  auto pbin = [&](uint32_t r) -> uint32_t { return r != INVR ? (uint32_t)c.Xb[(int64_t)(r & c.rmask) * c.ld + feat] : 0u; };
   uint32_t nrow = INVR, nbin = 0, frow = INVR;
   if (!reg_rows && RPT == 1) {
     rrow[0] = prow(tid);
@@ -856,7 +882,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
         load_rows(cb);
 #pragma unroll
         for (int u = 0; u < RPT; ++u)
-          rbin[u] = rrow[u] != 0xFFFFFFFFu ? (uint32_t)c.Xb[(int64_t)rrow[u] * c.ld + feat] : 0u;
+          rbin[u] = rrow[u] != 0xFFFFFFFFu ? (uint32_t)c.Xb[(int64_t)(rrow[u] & c.rmask) * c.ld + feat] : 0u;
       }
     }
     uint64_t ml[RPT], mr[RPT];
@@ -998,10 +1024,11 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   int my_cls = 0;
   float my_w = 0.f, my_y = 0.f;
   if (lane < cnt0) {
-    row = rows[lane];
-    my_w = (float)boot_weight(s, row);
+    const uint32_t wd = rows[lane];
+    row = word_row(c, wd);
+    my_w = (float)word_weight(c, s, wd);
     if constexpr (REG) my_y = tree_y(c, s)[row];
-    else my_cls = c.ycls[row];
+    else my_cls = word_cls(c, wd);
   }
   const uint8_t* xg = c.Xb + (int64_t)row * c.ld;
   if (cache && lane < cnt0)
@@ -1177,15 +1204,15 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
     auto row_at = [&](int r) -> uint32_t { return r < r1 ? rows[r] : INV; };
     const int t0 = r0 + (int)threadIdx.x;
     uint32_t ra = row_at(t0), rbn = row_at(t0 + 256);
-    uint64_t pa = ra != INV ? row_payload<MODE>(c, ty, ra, boot_weight(s, ra)) : 0ull;
+    uint64_t pa = ra != INV ? word_payload<MODE>(c, s, ty, ra) : 0ull;
     uint32_t ba[KGL];
 #pragma unroll
-    for (int j = 0; j < KGL; ++j) ba[j] = (j < g && ra != INV) ? (uint32_t)c.Xb[(int64_t)ra * c.ld + fj[j]] : 0u;
+    for (int j = 0; j < KGL; ++j) ba[j] = (j < g && ra != INV) ? (uint32_t)c.Xb[(int64_t)(ra & c.rmask) * c.ld + fj[j]] : 0u;
     for (int r = t0; r < r1; r += 256) {
-      const uint64_t pb = rbn != INV ? row_payload<MODE>(c, ty, rbn, boot_weight(s, rbn)) : 0ull;
+      const uint64_t pb = rbn != INV ? word_payload<MODE>(c, s, ty, rbn) : 0ull;
       uint32_t bb[KGL];
 #pragma unroll
-      for (int j = 0; j < KGL; ++j) bb[j] = (j < g && rbn != INV) ? (uint32_t)c.Xb[(int64_t)rbn * c.ld + fj[j]] : 0u;
+      for (int j = 0; j < KGL; ++j) bb[j] = (j < g && rbn != INV) ? (uint32_t)c.Xb[(int64_t)(rbn & c.rmask) * c.ld + fj[j]] : 0u;
       const uint32_t rc2 = row_at(r + 512);
 #pragma unroll
       for (int j = 0; j < KGL; ++j)
@@ -1197,7 +1224,7 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
   } else {
     for (int r = r0 + threadIdx.x; r < r1; r += 256) {
       const uint32_t row = rows[r];
-      hist_add_row<MODE>(hist, c, ty, feats, g, row, boot_weight(s, row), span);
+      hist_add_row<MODE>(hist, c, ty, feats, g, word_row(c, row), word_weight(c, s, row), span);
     }
   }
   __syncthreads();
@@ -1310,7 +1337,7 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr uint32_t INV = 0xFFFFFFFFu;
   auto row_at = [&](int r) -> uint32_t { return r < r1 ? rows[r] : INV; };
-  auto bin_of = [&](uint32_t row) -> int { return row != INV ? (int)c.Xb[(int64_t)row * c.ld + feat] : 0; };
+  auto bin_of = [&](uint32_t row) -> int { return row != INV ? (int)c.Xb[(int64_t)(row & c.rmask) * c.ld + feat] : 0; };
   int myL = 0;
   {
     uint32_t ra = row_at(r0 + tid);
@@ -1427,7 +1454,12 @@ __global__ __launch_bounds__(256) void k_fill_active(Ctx c) {
   for (int i = 0; i < 4; ++i) {
     if (!act[i]) continue;
     const uint32_t r = (uint32_t)(r0 + tid * 4 + i);
-    out[p++] = r;
+    uint32_t wd = r;
+    if (c.packed) {
+      wd |= wts[i] << c.rbits;
+      if constexpr (!REG) wd |= (uint32_t)c.ycls[r] << (c.rbits + 4);
+    }
+    out[p++] = wd;
     const double w = (double)wts[i];
     if constexpr (REG) {
       const double y = (double)tree_y(c, s)[r];
@@ -1542,6 +1574,14 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.slack_wave = (int)a->slack_wave;
   c.sub_max = (int)a->sub_max;
   c.sub_cache_d = (int)a->sub_cache_d;
+  {
+    int cbits = 0;
+    if (!c.is_reg)
+      while ((1 << cbits) < c.C) ++cbits;
+    c.rbits = 28 - cbits;   // 4 weight bits (bootstrap weights <= kPoisTable = 12)
+    c.packed = (a->n < ((int64_t)1 << c.rbits) - 1) && getenv("DML_ROW_WORDS_OFF") == nullptr ? 1 : 0;
+    c.rmask = c.packed ? (uint32_t)((1u << c.rbits) - 1u) : 0xFFFFFFFFu;
+  }
   return c;
 }
 

@@ -61,6 +61,7 @@ TIERS = [
 ]
 
 
+@pytest.mark.parametrize("words", ["packed", "plain"])
 @pytest.mark.parametrize("tiers", range(len(TIERS)))
 @pytest.mark.parametrize("n,d,C,kw", [
     (3000, 12, 2, {}),
@@ -68,7 +69,9 @@ TIERS = [
     (60000, 16, 2, {"max_depth": 12, "k": 16, "bootstrap": 0}),
     (5000, 30, 4, {"criterion": 0, "mss": 10}),
 ])
-def test_gpu_trees_match_cpu(n, d, C, kw, tiers):
+def test_gpu_trees_match_cpu(n, d, C, kw, tiers, words, monkeypatch):
+    if words == "plain":   # row ids only (the path for tables too tall for packed row words)
+        monkeypatch.setenv("DML_ROW_WORDS_OFF", "1")
     X, y = _data(n, d, C)
     dev = torch.device("cuda:0")
     Xt = torch.from_numpy(X).to(dev)
@@ -106,9 +109,12 @@ def test_gpu_trees_match_cpu(n, d, C, kw, tiers):
     assert np.allclose(sg, sc)
 
 
-def test_gpu_regression_close_to_cpu():
+@pytest.mark.parametrize("words", ["packed", "plain"])
+def test_gpu_regression_close_to_cpu(words, monkeypatch):
     from sklearn.datasets import make_regression
 
+    if words == "plain":
+        monkeypatch.setenv("DML_ROW_WORDS_OFF", "1")
     X, y = make_regression(n_samples=8000, n_features=10, noise=5.0, random_state=1)
     X = X.astype(np.float32)
     y = y.astype(np.float32)
