@@ -78,6 +78,7 @@ def main() -> int:
     from cs230_distributed_machine_learning_amd.engine.service import candidate_costs
     from cs230_distributed_machine_learning_amd.ops import binning
     from cs230_distributed_machine_learning_amd.search.grid import expand_candidates
+    from cs230_distributed_machine_learning_amd.utils import trace
 
     inf = dist.init(want_gpu=not args.cpu)
     N, r = inf.world, inf.rank
@@ -123,7 +124,8 @@ def main() -> int:
 
     def step(s: int):
         mine = rank_step_cands(s)
-        res = run_candidates(dd, spec, mine)
+        with trace.range("step"):
+            res = run_candidates(dd, spec, mine)
         bad = [x.error for x in res if not x.ok]
         if bad:
             raise RuntimeError(f"rank {r}: failed fits: {bad[:2]}")
@@ -179,6 +181,7 @@ def main() -> int:
             "device": str(torch.cuda.get_device_name(dev)) if dev.type == "cuda" else "cpu",
         }
         line = json.dumps(out)
+        print("phases:", json.dumps(trace.summary()), file=sys.stderr, flush=True)
         print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:

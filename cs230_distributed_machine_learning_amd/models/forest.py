@@ -18,6 +18,7 @@ subtask's ``warnings``.
 from __future__ import annotations
 
 import math
+import os
 import time
 from typing import Any, Dict, List
 
@@ -25,7 +26,7 @@ import numpy as np
 import torch
 
 from ..ops import forest_ops
-from ..utils import native
+from ..utils import native, trace
 from .base import Family, FitOutput, FitTask, ParamError, as_bool, as_float, as_int, register, seed_of
 
 _CLS = "RandomForestClassifier"
@@ -144,9 +145,15 @@ class ForestFamily(Family):
     def _budget(self, data) -> float:
         if self.hbm_budget_bytes:
             return float(self.hbm_budget_bytes)
+        env = os.environ.get("DML_HBM_BUDGET_GB")   # Config.hbm_budget_gb
+        if env:
+            return float(env) * 1e9
         if data.is_gpu:
             free, _total = torch.cuda.mem_get_info(data.device)
-            return 0.55 * free
+            # blocks the caching allocator holds but nobody uses are free for this batch too
+            # (without this, the previous batch's freed pool makes the next batch split)
+            cached = torch.cuda.memory_reserved(data.device) - torch.cuda.memory_allocated(data.device)
+            return float(os.environ.get("DML_HBM_FRACTION", "0.55")) * (free + max(0, cached))
         return 8e9
 
     def run(self, data, tasks: List[FitTask], keep_models: bool = False) -> List[FitOutput]:
@@ -169,7 +176,9 @@ class ForestFamily(Family):
         if cur:
             batches.append(cur)
         for batch in batches:
-            for o in self._run_batch(data, Xb, batch, is_reg, keep_models):
+            with trace.range("forest_batch"):
+                out_b = self._run_batch(data, Xb, batch, is_reg, keep_models)
+            for o in out_b:
                 outs[o.task_id] = o
         return [outs[t.task_id] for t in tasks]
 
@@ -205,7 +214,8 @@ class ForestFamily(Family):
         else:
             fb = forest_ops.build_cpu(Xb.numpy(), data.y_enc, None if not is_reg else data.y_reg.numpy(),
                                       data.roles_np(), specs, data.n_classes, is_reg)
-        _refine(data, fb, Xb, specs, data.roles)
+        with trace.range("forest_refine"):
+            _refine(data, fb, Xb, specs, data.roles)
         toff = np.zeros(len(batch) + 1, dtype=np.int64)
         np.cumsum([t.params["n_estimators"] for t in batch], out=toff[1:])
         rows = [data.test_rows[t.split] for t in batch]

@@ -119,10 +119,11 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     a.ystride = int(ystride)
     a.active_count = native.ptr(active)
     t0 = time.perf_counter()
-    rc = lib.dml_forest_count(ctypes.byref(a), stream)
-    if rc:
-        raise RuntimeError(f"dml_forest_count failed ({rc}): {native.hip_error(lib)}")
-    counts = active.cpu().numpy().astype(np.int64)
+    with trace.range("forest_count"):
+        rc = lib.dml_forest_count(ctypes.byref(a), stream)
+        if rc:
+            raise RuntimeError(f"dml_forest_count failed ({rc}): {native.hip_error(lib)}")
+        counts = active.cpu().numpy().astype(np.int64)
     row_off = np.zeros(T + 1, dtype=np.int64)
     np.cumsum(counts, out=row_off[1:])
     row_off_dev = torch.from_numpy(row_off).to(dev)

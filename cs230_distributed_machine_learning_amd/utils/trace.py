@@ -9,7 +9,9 @@ slice / fit batch / kernel phase opens a named range that
 * accumulates host wall time per range name (``summary()``), which the bench scripts
   print as a phase breakdown.
 
-``DML_TRACE=0`` disables both (the ranges then cost one attribute check).
+``DML_TRACE=0`` disables both (the ranges then cost one attribute check);
+``DML_TRACE_SYNC=1`` synchronises the device at every range exit so host timers include
+the GPU work launched inside (debug attribution only: it serialises the pipeline).
 """
 from __future__ import annotations
 
@@ -21,6 +23,7 @@ import time
 from typing import Dict, Optional, Tuple
 
 _ENABLED = os.environ.get("DML_TRACE", "1") != "0"
+_SYNC = os.environ.get("DML_TRACE_SYNC", "0") == "1"
 _lib: Optional[ctypes.CDLL] = None
 _lib_tried = False
 _lock = threading.Lock()
@@ -68,6 +71,11 @@ def range(name: str):  # noqa: A001 - mirrors roctx naming
     try:
         yield
     finally:
+        if _SYNC:
+            import torch
+
+            if torch.cuda.is_available() and torch.cuda.is_initialized():
+                torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         if lib is not None:
             lib.roctxRangePop()
