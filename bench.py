@@ -10,11 +10,13 @@ cv=5, on 1M x 100 tabular data, 1/2/4/8 MI355X (one rank per GPU, RCCL over xGMI
 * Grid (256 = 4^4): n_estimators {50,100,150,200} x max_depth {10,20,30,None} x
   min_samples_split {2,5,10,20} x min_samples_leaf {1,2,4,8}; everything else at
   sklearn defaults (gini, max_features='sqrt', bootstrap).
-* Step (weak scaling): every rank runs ``--cands-per-rank`` candidates x cv folds.
-  Candidates are drawn one per cost quantile group so each rank-step has the same
-  cost profile whatever N is; after the fits each step all-gathers the per-candidate
-  CV scores over RCCL (the job's result path).  ``value`` = total CV fits / wall
-  seconds over exactly K timed steps (max over ranks).
+* Step (weak scaling): a step runs N x ``--cands-per-rank`` candidates x cv folds —
+  N candidates from each cost-quantile group, so the step's cost profile is the same
+  whatever N is — placed on the ranks by the engine's native LPT scheduler
+  (engine/scheduler.py ``lpt_assign``) with its analytic cost model; after the fits one
+  RCCL all-reduce gives every rank every candidate's CV scores (the job's result
+  path).  ``value`` = total CV fits / wall seconds over exactly K timed steps (max over
+  ranks).
 
 Run: ``python bench.py [--gpus N --steps K --warmup W]`` (N>1 under torchrun, or it
 re-launches itself through torch.distributed.run before touching the GPU).
@@ -111,16 +113,28 @@ def main() -> int:
     c = args.cands_per_rank
     groups = np.array_split(order, c)   # cost-quantile groups; a rank-step takes one candidate from each
 
+    from cs230_distributed_machine_learning_amd.engine.scheduler import lpt_assign
+
+    def step_pool(step: int):
+        return [int(g[(step * N + j) % len(g)]) for g in groups for j in range(N)]
+
     def rank_step_cands(step: int):
-        u = step * N + r
-        return [int(g[u % len(g)]) for g in groups]
+        # the step's pool: N candidates from every cost-quantile group (N x c candidates,
+        # N x c x cv fits), placed on the ranks by the native LPT scheduler with the same
+        # analytic cost model the engine uses, so the slowest rank (which sets the step
+        # time) is as close to the mean as the pool allows.  N=1: the rank takes the pool.
+        pool = step_pool(step)
+        if N == 1:
+            return pool
+        owner = lpt_assign([float(costs[i]) for i in pool], N)
+        return [cid for cid, o in zip(pool, owner) if int(o) == r]
 
     dist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     setup_s = time.perf_counter() - t_setup
 
-    score_buf = torch.zeros((N, c, args.cv), dtype=torch.float32, device=dev)
+    score_buf = torch.zeros((N * c, args.cv), dtype=torch.float32, device=dev)
 
     def step(s: int):
         mine = rank_step_cands(s)
@@ -129,9 +143,13 @@ def main() -> int:
         bad = [x.error for x in res if not x.ok]
         if bad:
             raise RuntimeError(f"rank {r}: failed fits: {bad[:2]}")
-        local = torch.tensor([x.result["cv_scores"] for x in res], dtype=torch.float32, device=dev)
-        allsc = dist.all_gather_rows(local.unsqueeze(0))   # RCCL: every rank's CV scores
-        score_buf.copy_(allsc)
+        # the job's result path: each rank fills its candidates' rows of the step's score
+        # table, one RCCL all-reduce gives every rank every candidate's CV scores
+        pos = {cid: i for i, cid in enumerate(step_pool(s))}
+        score_buf.zero_()
+        rows = torch.tensor([pos[cid] for cid in mine], dtype=torch.long, device=dev)
+        score_buf[rows] = torch.tensor([x.result["cv_scores"] for x in res], dtype=torch.float32, device=dev)
+        dist.all_reduce_sum(score_buf)
         return res
 
     for s in range(args.warmup):
