@@ -31,6 +31,10 @@ class Config:
     max_retries: int = 2
     chunk_target_s: float = 2.0            # progress granularity of a worker slice
     hbm_budget_gb: Optional[float] = None  # forest batch budget (default: 55% of free HBM)
+    # parallelism 'auto': a data-parallel-capable job runs row-sharded when its table is
+    # at least dp_min_cells cells AND (fewer candidates than ranks OR > dp_auto_gb of fp32)
+    dp_auto_gb: float = 48.0
+    dp_min_cells: int = 50_000_000
     algo_weight: Dict[str, float] = field(default_factory=dict)
     log_dir: Optional[str] = None
     deterministic: bool = True

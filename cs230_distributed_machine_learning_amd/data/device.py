@@ -121,6 +121,16 @@ class DeviceData:
         self.train_counts = [int((r == ROLE_TRAIN).sum()) for r in roles]
         self._split_key = key
 
+    def train_class_counts(self, split: int, C: int) -> torch.Tensor:
+        """Per-class counts (float64 [C]) of a split's training rows."""
+        yt = self.y_cls[self.train_rows[split].long()].long()
+        return torch.bincount(yt, minlength=C).double()
+
+    def test_targets(self, split: int) -> torch.Tensor:
+        """Targets of a split's held-out rows, in the order predictions come back."""
+        rows = self.test_rows[split].long()
+        return (self.y_cls if self.classification else self.y_reg)[rows]
+
     def roles_np(self) -> np.ndarray:
         return self.roles.cpu().numpy()
 

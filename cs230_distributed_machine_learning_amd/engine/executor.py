@@ -92,11 +92,7 @@ def build_tasks(data, spec: JobSpec, candidate_ids: Sequence[int]):
 def _scores_for(data, task: FitTask, out: FitOutput, scorer: str):
     if scorer == "score":
         return float(out.info["score"])
-    rows = data.test_rows[task.split].long()
-    if data.classification:
-        y = data.y_cls[rows]
-    else:
-        y = data.y_reg[rows]
+    y = data.test_targets(task.split)
     return scoring_mod.score(scorer, y, out.pred, data.n_classes, out.proba)
 
 
@@ -115,6 +111,9 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
         scorer = scoring_mod.validate_scoring(spec.scoring, clf)
     if not clf and not self_scored and not getattr(data, "y_is_numeric", True):
         raise ValueError(f"{spec.model_type} needs a numeric target column; this target is categorical")
+    sharded = getattr(data, "is_row_shard", False)
+    if sharded and not getattr(fam, "data_parallel", False):
+        raise ValueError(f"{spec.model_type} has no row-sharded (data-parallel) fit; run it task-parallel")
     tasks, errors = build_tasks(data, spec, candidate_ids)
     keep = spec.keep_models in ("all", "best")
     outputs: Dict[int, FitOutput] = {}
@@ -122,6 +121,8 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
         try:
             for o in fam.run(data, tasks, keep_models=keep):
                 outputs[o.task_id] = o
+            if sharded:   # rank-local held-out predictions -> the global prediction vectors
+                data.gather_outputs(tasks, outputs)
         except ParamError as e:
             for t in tasks:
                 errors.setdefault(t.candidate, f"ParamError: {e}")

@@ -83,6 +83,11 @@ def job_plan(request: Dict[str, Any]) -> Dict[str, Any]:
         refit = True
     if error_score is None:
         error_score = float("nan")
+    par = str(tp.get("parallelism") or "auto")
+    if par not in ("auto", "task", "data"):
+        raise ParamError(f"train_params.parallelism must be 'auto', 'task' or 'data', got {par!r}")
+    if par == "data" and not getattr(family_of(model_type), "data_parallel", False):
+        raise ParamError(f"{model_type} has no row-sharded (data-parallel) fit; use parallelism 'task'")
     return {
         "model_type": model_type, "search_type": search_type, "candidates": cands, "cv": cv,
         "scoring": scoring, "error_score": error_score, "refit": bool(refit) if not isinstance(refit, str) else True,
@@ -90,6 +95,7 @@ def job_plan(request: Dict[str, Any]) -> Dict[str, Any]:
         "random_state": tp.get("random_state", 42) if tp.get("random_state") is not None else 42,
         "holdout": bool(tp.get("holdout", True)),
         "feature_columns": tp.get("feature_columns"), "target_column": tp.get("target_column"),
+        "parallelism": par,
     }
 
 
@@ -484,19 +490,17 @@ def publish_results(ctl: Controller, job: Job, results, metrics) -> None:
                                      metrics=metrics.get(r.candidate))
 
 
-def refit_best(ctl: Controller, job: Job, plan: Dict[str, Any], dd, best_idx: int) -> Optional[str]:
-    """sklearn refit=True: fit the best candidate on all rows and store the artefact."""
-    from .executor import JobSpec, run_candidates
-
-    spec = JobSpec(model_type=plan["model_type"], candidates=[job.subtasks[best_idx].spec["parameters"]], cv=0,
-                   holdout=False, keep_models="all", scoring=plan["scoring"])
-    # a single "full" split: train on every row; the executor scores nothing
+def refit_model(plan: Dict[str, Any], params: Dict[str, Any], dd) -> Optional[Dict[str, Any]]:
+    """Fit one candidate on every row.  Under a RowShard every rank calls this in lock
+    step (the fit's reductions are collectives); only rank 0 keeps the model."""
     from ..search.cv import ROLE_TRAIN
+    from .executor import JobSpec, build_tasks
 
-    roles = np.full((1, dd.n), ROLE_TRAIN, dtype=np.uint8)
+    spec = JobSpec(model_type=plan["model_type"], candidates=[params], cv=0, holdout=False, keep_models="all",
+                   scoring=plan["scoring"])
+    # a single "full" split: train on every row; the executor scores nothing
+    roles = np.full((1, getattr(dd, "n_global", dd.n)), ROLE_TRAIN, dtype=np.uint8)
     dd.set_splits(roles, ["full"], key=("full",))
-    from .executor import build_tasks
-
     fam = family_of(plan["model_type"])
     tasks, errors = build_tasks(dd, spec, [0])
     if errors or not tasks:
@@ -504,7 +508,16 @@ def refit_best(ctl: Controller, job: Job, plan: Dict[str, Any], dd, best_idx: in
     outs = fam.run(dd, tasks, keep_models=True)
     if not outs or outs[0].model is None:
         return None
-    model = outs[0].model
+    return outs[0].model
+
+
+def refit_best(ctl: Controller, job: Job, plan: Dict[str, Any], dd, best_idx: int) -> Optional[str]:
+    """sklearn refit=True: fit the best candidate on all rows and store the artefact."""
+    from .executor import JobSpec, run_candidates
+
+    model = refit_model(plan, job.subtasks[best_idx].spec["parameters"], dd)
+    if model is None:
+        return None
     model["job_id"] = job.job_id
     model["subtask_id"] = job.subtasks[best_idx].subtask_id
     model["feature_names"] = list(ctl.registry.load(job.dataset_id, plan["feature_columns"],
@@ -647,13 +660,8 @@ def job_seed(job_id: str) -> int:
 def finalize_job(ctl: Controller, job: Job, plan: Dict[str, Any], dd, results) -> None:
     """Refit the best candidate (sklearn refit=True) and attach its model path before
     the last results are published, so "completed" always comes with the artefact."""
-    ok = [r for r in results if r.ok]
-    if not ok or not plan.get("refit", True) or ctl.config.keep_models == "none":
-        return
-    # same winner as jobs.aggregate_best: max mean_cv_score, ties -> lowest subtask index
-    best = max(ok, key=lambda r: (score_r(r.result), -r.candidate))
-    if any(st.status == "completed" and st.result and (score_r(st.result), -st.index) > (score_r(best.result), -best.candidate)
-           for st in job.subtasks):
+    best = pick_refit(ctl, job, plan, results)
+    if best is None:
         return
     try:
         path = refit_best(ctl, job, plan, dd, best.candidate)
@@ -661,6 +669,19 @@ def finalize_job(ctl: Controller, job: Job, plan: Dict[str, Any], dd, results) -
             best.result["model_path"] = path
     except Exception:
         traceback.print_exc()
+
+
+def pick_refit(ctl: Controller, job: Job, plan: Dict[str, Any], results):
+    """The result whose candidate gets refit on all rows, or None."""
+    ok = [r for r in results if r.ok]
+    if not ok or not plan.get("refit", True) or ctl.config.keep_models == "none":
+        return None
+    # same winner as jobs.aggregate_best: max mean_cv_score, ties -> lowest subtask index
+    best = max(ok, key=lambda r: (score_r(r.result), -r.candidate))
+    if any(st.status == "completed" and st.result and (score_r(st.result), -st.index) > (score_r(best.result), -best.candidate)
+           for st in job.subtasks):
+        return None
+    return best
 
 
 def score_r(R: Dict[str, Any]) -> float:

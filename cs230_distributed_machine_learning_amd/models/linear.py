@@ -90,9 +90,8 @@ def class_weight_vector(data, split: int, cw):
     C = data.n_classes
     w = torch.ones(C, dtype=torch.float64, device=data.device)
     if cw == "balanced":
-        yt = data.y_cls[data.train_rows[split].long()].long()
-        cnt = torch.bincount(yt, minlength=C).double()
-        return torch.where(cnt > 0, yt.numel() / (C * cnt.clamp_min(1)), w)
+        cnt = data.train_class_counts(split, C)      # global counts under a RowShard
+        return torch.where(cnt > 0, cnt.sum() / (C * cnt.clamp_min(1)), w)
     lookup = {str(c): i for i, c in enumerate(np.asarray(data.classes).tolist())}
     for k, v in cw.items():
         if str(k) in lookup:
@@ -101,6 +100,14 @@ def class_weight_vector(data, split: int, cw):
 
 
 _TILE = 128   # output tile of csrc/kernels/lr_mfma.hip (dml_lr_mfma_tile)
+
+
+def _dp_sum(data, t: torch.Tensor) -> torch.Tensor:
+    """Sum over the ranks of a row-sharded fit (parallel/data_parallel.py); identity otherwise."""
+    if getattr(data, "is_row_shard", False):
+        t = t.contiguous()
+        data.all_reduce(t)
+    return t
 
 
 def _roundup(x: int, m: int) -> int:
@@ -251,7 +258,7 @@ class _Batch:
             n_f = max(1, data.train_counts[t.split])
             cwv = class_weight_vector(data, t.split, rp.get("class_weight"))
             if cwv is not None:
-                n_f = float(cwv[data.y_cls[data.train_rows[t.split].long()].long()].sum())   # sw_sum
+                n_f = float(_dp_sum(data, cwv[data.y_cls[data.train_rows[t.split].long()].long()].sum()))   # sw_sum
                 any_cw = True
             cws.append(cwv)
             col0.append(m); K.append(k); kind.append(kd); split.append(t.split)
@@ -297,6 +304,7 @@ class LogisticFamily(Family):
     model_types = ("LogisticRegression",)
     classifiers = ("LogisticRegression",)
     history = 10
+    data_parallel = True   # loss + gradient all-reduced per objective evaluation under a RowShard
 
     def resolve(self, model_type, params, n_train, n_features, n_classes):
         p = dict(_LR_DEFAULTS)
@@ -362,6 +370,7 @@ class LogisticFamily(Family):
         d = data.d
         if b.mf is not None:   # matrix cores: fused forward + split-K gradient (lr_mfma.hip)
             loss, G = b.mf.objective(data, b, W)
+            loss, G = _dp_sum(data, loss), _dp_sum(data, G)
             reg = W * b.lam_col
             reg[d] = reg[d] * b.pen_icpt_col
             G += reg
@@ -384,6 +393,7 @@ class LogisticFamily(Family):
         G = torch.empty_like(W)
         G[:d] = X.t() @ R
         G[d] = R.sum(0) * b.icpt_col
+        loss, G = _dp_sum(data, loss), _dp_sum(data, G)
         reg = W * b.lam_col
         reg[d] = reg[d] * b.pen_icpt_col
         G += reg
@@ -499,7 +509,7 @@ class LogisticFamily(Family):
         # tiny lbfgs problems (iris-sized): a device launch per objective evaluation is pure
         # latency, so they run on the host with scipy's L-BFGS-B on sklearn's exact float64
         # objective -> same iterates as sklearn even where max_iter stops before convergence
-        small = [t for t in tasks if t.params["solver"] == "lbfgs" and
+        small = [t for t in tasks if t.params["solver"] == "lbfgs" and not getattr(data, "is_row_shard", False) and
                  data.train_counts[t.split] * (data.d + 1) * max(1, data.n_classes - 1) <= HOST_LBFGS_MAX_WORK]
         if small:
             done = {o.task_id: o for o in self._run_host_lbfgs(data, small, keep_models)}
@@ -674,6 +684,7 @@ _LIN_DEFAULTS = {"fit_intercept": True, "copy_X": True, "n_jobs": None, "positiv
 class LinearRegressionFamily(Family):
     model_types = ("LinearRegression",)
     classifiers = ()
+    data_parallel = True   # normal-equation moments all-reduced under a RowShard
 
     def resolve(self, model_type, params, n_train, n_features, n_classes):
         p = dict(_LIN_DEFAULTS)
@@ -696,17 +707,20 @@ class LinearRegressionFamily(Family):
             if key not in cache:
                 tr = data.train_rows[t.split].long()
                 Xt, yt = X[tr].double(), y[tr].double()
-                if t.params["fit_intercept"]:
+                if getattr(data, "is_row_shard", False):
+                    cache[key] = self._sharded_solve(data, Xt, yt, t.params["fit_intercept"])
+                elif t.params["fit_intercept"]:
                     xm, ym = Xt.mean(0), yt.mean()
                     Xc, yc = Xt - xm, yt - ym
                 else:
                     xm = torch.zeros(data.d, dtype=torch.float64, device=X.device)
                     ym = torch.zeros((), dtype=torch.float64, device=X.device)
                     Xc, yc = Xt, yt
-                A = Xc.t() @ Xc
-                w = torch.linalg.pinv(A, hermitian=True) @ (Xc.t() @ yc)
-                b0 = ym - xm @ w
-                cache[key] = (w, b0)
+                if key not in cache:
+                    A = Xc.t() @ Xc
+                    w = torch.linalg.pinv(A, hermitian=True) @ (Xc.t() @ yc)
+                    b0 = ym - xm @ w
+                    cache[key] = (w, b0)
             w, b0 = cache[key]
             te = data.test_rows[t.split].long()
             pred = (X[te].double() @ w + b0).float()
@@ -721,6 +735,28 @@ class LinearRegressionFamily(Family):
         for o in outs:
             o.fit_seconds = dt / max(1, len(outs))
         return outs
+
+    @staticmethod
+    def _sharded_solve(data, Xt: torch.Tensor, yt: torch.Tensor, fit_intercept: bool):
+        """Normal equations from all-reduced shard moments: one all-reduce of
+        [count, sum x, sum y, X^T X, X^T y] (float64), centred on the global means."""
+        d = Xt.shape[1]
+        m = torch.cat([torch.tensor([float(Xt.shape[0])], dtype=torch.float64, device=Xt.device), Xt.sum(0),
+                       yt.sum().view(1), (Xt.t() @ Xt).flatten(), Xt.t() @ yt])
+        _dp_sum(data, m)
+        cnt, sx, sy = m[0], m[1:1 + d], m[1 + d]
+        XX = m[2 + d:2 + d + d * d].view(d, d)
+        Xy = m[2 + d + d * d:]
+        if fit_intercept:
+            xm, ym = sx / cnt.clamp_min(1), sy / cnt.clamp_min(1)
+            A = XX - cnt * torch.outer(xm, xm)
+            bvec = Xy - cnt * xm * ym
+        else:
+            xm = torch.zeros(d, dtype=torch.float64, device=Xt.device)
+            ym = torch.zeros((), dtype=torch.float64, device=Xt.device)
+            A, bvec = XX, Xy
+        w = torch.linalg.pinv(A, hermitian=True) @ bvec
+        return w, ym - xm @ w
 
 
 register(LogisticFamily())

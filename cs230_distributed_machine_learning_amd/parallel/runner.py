@@ -36,7 +36,7 @@ from ..engine import faults
 from ..engine.jobs import Job, json_safe
 from ..engine.service import (Controller, DeviceCache, Runner, candidate_costs, finalize_job, job_plan, job_seed,
                               plan_slices, publish_results, run_slice)
-from ..models.base import is_classifier
+from ..models.base import family_of, is_classifier
 from ..utils.log import get_logger
 from . import data as pdata
 from . import dist
@@ -155,7 +155,51 @@ class WorkerCore:
         self.cache[key] = dd
         return dd
 
+    def dataset_dp(self, msg: Dict[str, Any], ctl: Optional[Controller]):
+        """Row shard of the job's table on this rank (one RCCL scatter; parallel/data_parallel.py)."""
+        from .data_parallel import RowShard, scatter_table
+
+        key = "dp:" + msg["dataset_key"]
+        if key in self.cache:
+            return self.cache[key]
+        plan = msg["plan"]
+        X = y = None
+        if self.inf.rank == 0:
+            ds = ctl.registry.load(msg["dataset_id"], plan["feature_columns"], plan["target_column"])
+            X, y = ds.X, ds.y
+        Xs, y_glob, r0 = scatter_table(X, y, self.device)
+        dd = RowShard(Xs, y_glob, r0, is_classifier(plan["model_type"]), self.device, name=msg["dataset_id"])
+        while len(self.cache) >= 4:
+            self.cache.pop(next(iter(self.cache)))
+        self.cache[key] = dd
+        return dd
+
+    def run_dp(self, seq: int, msg: Dict[str, Any], ctl: Optional[Controller] = None):
+        """Data-parallel job: every rank runs every slice in order on its row shard (the
+        fits' reductions are collectives, so the ranks move in lock step); rank 0
+        publishes the results, then all ranks refit the winner together."""
+        from ..engine.service import refit_model
+
+        st, r = self.store, self.inf.rank
+        plan = msg["plan"]
+        dd = self.dataset_dp(msg, ctl)
+        params, sids = msg["params"], msg["subtask_ids"]
+        for i, ids in enumerate(msg["slices"]):
+            results, metrics, wall = run_slice(plan, params, sids, dd, ids, "data-parallel", str(self.device),
+                                               seed=msg["seed"])
+            if r == 0:
+                st.set(f"job/{seq}/res/{i}", _enc_results(results, metrics))
+                st.set(f"job/{seq}/wall/{i}", str(wall))
+                st.add(f"job/{seq}/done", 1)
+        st.add(f"job/{seq}/fin", 1)
+        st.wait([f"job/{seq}/refit"])             # rank 0 picks the refit candidate (or -1)
+        best = int(st.get(f"job/{seq}/refit"))
+        model = refit_model(plan, params[best], dd) if best >= 0 else None
+        return dd, model
+
     def run(self, seq: int, msg: Dict[str, Any], ctl: Optional[Controller] = None, job: Optional[Job] = None):
+        if msg.get("mode") == "data":
+            return self.run_dp(seq, msg, ctl)
         st, r, world = self.store, self.inf.rank, self.inf.world
         plan = msg["plan"]
         dd = self.dataset(msg, ctl)
@@ -297,18 +341,24 @@ class DistributedRunner(Runner):
         if not todo:
             return
         world = dist.info().world
-        slices = plan_slices(ctl, plan, todo, int(n_rows * 0.8), max(1, int(meta.get("n_cols", 2)) - 1), 2,
-                             min_slices=min(len(todo), 2 * world))
+        n_feat = max(1, int(meta.get("n_cols", 2)) - 1)
+        data_par = self._data_parallel(plan, len(todo), n_rows, n_feat, world)
+        slices = plan_slices(ctl, plan, todo, int(n_rows * 0.8), n_feat, 2,
+                             min_slices=1 if data_par else min(len(todo), 2 * world))
         key = f"{ds_path}:{os.path.getmtime(ds_path)}:{plan['feature_columns']}:{plan['target_column']}:" \
               f"{is_classifier(plan['model_type'])}"
         seq = self.seq
         self.seq += 1
         msg = {"job_id": job.job_id, "dataset_id": job.dataset_id, "dataset_key": key, "plan": plan,
                "slices": slices, "params": [sub.spec["parameters"] for sub in job.subtasks],
-               "subtask_ids": [sub.subtask_id for sub in job.subtasks], "seed": job_seed(job.job_id)}
+               "subtask_ids": [sub.subtask_id for sub in job.subtasks], "seed": job_seed(job.job_id),
+               "mode": "data" if data_par else "task"}
         st.set(f"job/{seq}", json.dumps(json_safe(msg)))
         for ids in slices:
             ctl.table.mark_running(job.job_id, ids, "cluster")
+        if data_par:
+            self._run_job_dp(job, plan, seq, msg, slices)
+            return
         # progress publisher + liveness monitor while every rank (this one too) works
         done_evt = threading.Event()
         held: Dict[int, Any] = {}
@@ -328,6 +378,68 @@ class DistributedRunner(Runner):
         final = [held[i] for i in sorted(held)]
         finalize_job(ctl, job, plan, dd, results_all)
         for res, metrics in final:
+            publish_results(ctl, job, res, metrics)
+        self._cleanup(seq, len(slices))
+
+    def _data_parallel(self, plan, n_todo: int, n_rows: int, n_feat: int, world: int) -> bool:
+        """Row-sharded data parallelism (parallel/data_parallel.py) instead of task slices."""
+        par = plan.get("parallelism", "auto")
+        if par == "task" or world < 2 or not getattr(family_of(plan["model_type"]), "data_parallel", False):
+            return False
+        if par == "data":
+            return True
+        cfg = self.ctl.config
+        cells = n_rows * n_feat
+        return cells >= cfg.dp_min_cells and (n_todo < world or cells * 4 > cfg.dp_auto_gb * 2 ** 30)
+
+    def _run_job_dp(self, job: Job, plan, seq: int, msg, slices) -> None:
+        from ..engine.service import pick_refit, refit_model
+
+        ctl, st = self.ctl, self.core.store
+        done_evt = threading.Event()
+        held: Dict[int, Any] = {}
+        mon = threading.Thread(target=self._monitor, args=(job, seq, slices, done_evt, held), daemon=True)
+        mon.start()
+        # rank 0 runs the slices with everyone; the monitor publishes results as they land
+        results_all = []
+        refit_set, best = False, None
+        try:
+            dd = self.core.dataset_dp(msg, ctl)
+            params, sids = msg["params"], msg["subtask_ids"]
+            for i, ids in enumerate(slices):
+                results, metrics, wall = run_slice(plan, params, sids, dd, ids, "data-parallel", str(self.core.device),
+                                                   seed=msg["seed"])
+                st.set(f"job/{seq}/claim/{i}", "0")   # the monitor's wall-time observation reads it
+                st.set(f"job/{seq}/wall/{i}", str(wall))
+                st.set(f"job/{seq}/res/{i}", _enc_results(results, metrics))
+                st.add(f"job/{seq}/done", 1)
+                results_all.extend(results)
+            done_evt.set()
+            mon.join()
+            best = pick_refit(ctl, job, plan, results_all)
+            st.set(f"job/{seq}/refit", str(best.candidate if best is not None else -1))
+            refit_set = True
+            if best is not None:
+                try:
+                    model = refit_model(plan, params[best.candidate], dd)
+                    if model is not None:
+                        model["job_id"] = job.job_id
+                        model["subtask_id"] = job.subtasks[best.candidate].subtask_id
+                        model["feature_names"] = list(ctl.registry.load(job.dataset_id, plan["feature_columns"],
+                                                                        plan["target_column"]).feature_names)
+                        best.result["model_path"] = ctl.models.save(f"{job.subtasks[best.candidate].subtask_id}_model",
+                                                                    model)
+                except Exception:
+                    traceback.print_exc()
+        finally:
+            done_evt.set()
+            if not refit_set:
+                st.set(f"job/{seq}/refit", "-1")
+        path = best.result.get("model_path") if refit_set and best is not None else None
+        for res, metrics in [held[i] for i in sorted(held)]:
+            for x in res:
+                if path and x.candidate == best.candidate and x.ok:
+                    x.result["model_path"] = path
             publish_results(ctl, job, res, metrics)
         self._cleanup(seq, len(slices))
 

@@ -75,7 +75,14 @@ def _rank_main(rank, world, port, root, outq):
                     st, r = ctl.train(sid, b)
                     ctl.table.wait_finished(r["job_id"], timeout=300)
                     extra.append((model, ctl.check_status(sid, r["job_id"])[1]))
-                outq.put(("ok", status, status2, metrics, extra))
+                # the same LR grid row-sharded over both ranks (parallel/data_parallel.py)
+                b3 = dict(body, train_params=dict(body["train_params"], parallelism="data"))
+                st, r3 = ctl.train(sid, b3)
+                ctl.table.wait_finished(r3["job_id"], timeout=300)
+                status3 = ctl.check_status(sid, r3["job_id"])[1]
+                b3 = status3.get("best_result") or {}
+                status3["_resolved_model"] = ctl.models.resolve(b3.get("model_path"), b3.get("model_id"))
+                outq.put(("ok", status, status2, metrics, extra, status3))
             except Exception as e:  # pragma: no cover
                 import traceback
 
@@ -119,6 +126,16 @@ def test_two_rank_gridsearch_gloo():
     assert workers <= {"rank0", "rank1"} and len(metrics) == 8
     assert status2["job_status"] == "completed" and len(status2["job_result"]["results"]) == 3
     assert status2["best_result"]["mean_cv_score"] > 0.9
+    status3 = out[5]
+    assert status3["job_status"] == "completed" and len(status3["job_result"]["results"]) == 8
+    task_par = {(r["parameters"]["C"], r["parameters"]["solver"]): r for r in res}
+    for r in status3["job_result"]["results"]:
+        ref = task_par[(r["parameters"]["C"], r["parameters"]["solver"])]
+        assert len(r["cv_scores"]) == 5
+        if r["parameters"]["solver"] == "liblinear":   # same device solver, rows summed over 2 shards
+            assert np.allclose(r["cv_scores"], ref["cv_scores"], atol=0.034), (r, ref)
+    assert status3["best_result"]["mean_cv_score"] >= 0.95
+    assert status3["_resolved_model"] and os.path.exists(status3["_resolved_model"])
     for model, st in out[4]:
         assert st["job_status"] == "completed", (model, st)
         assert all("cv_scores" in r for r in st["job_result"]["results"]), model
