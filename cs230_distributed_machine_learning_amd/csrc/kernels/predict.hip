@@ -8,6 +8,7 @@
 // statistics (correct count / SSE / sum y / sum y^2) so the host gets F x 4 doubles.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 // int64 argument fields -> GLOBAL address-space pointers (flat loads otherwise)
 #define GPTR(T, v) ((T*)(__attribute__((address_space(1))) T*)(uintptr_t)(v))
@@ -29,7 +30,7 @@ struct PredictArgs {
 // leaf of U consecutive trees [t0, t0 + u_n) for one row, walked in lock-step: the U
 // dependent node-load chains are independent, so U requests are in flight per thread
 // instead of one (tree traversal is latency-bound)
-constexpr int kPredU = 8;
+template <int kPredU>
 __device__ __forceinline__ void leaves_u(const NodeRec* __restrict__ nodes, const uint8_t* __restrict__ xr, int t0,
                                          int u_n, int (&leaf)[kPredU]) {
   NodeRec nr[kPredU];
@@ -53,7 +54,7 @@ __device__ __forceinline__ void leaves_u(const NodeRec* __restrict__ nodes, cons
   }
 }
 
-template <int MAXC>
+template <int MAXC, int kPredU>
 __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
   const int f = blockIdx.y;
   const int32_t* toff = GPTR(const int32_t, a.fit_tree_off);
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
   for (int t = toff[f]; t < tend; t += kPredU) {
     int leaf[kPredU];
     const int u_n = min(kPredU, tend - t);
-    leaves_u(nodes, xr, t, u_n, leaf);
+    leaves_u<kPredU>(nodes, xr, t, u_n, leaf);
     // accumulate in tree order (bit-identical to the host predictor)
 #pragma unroll
     for (int u = 0; u < kPredU; ++u) {
@@ -106,6 +107,7 @@ __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
   }
 }
 
+template <int kPredU>
 __global__ __launch_bounds__(256) void k_predict_reg(PredictArgs a) {
   const int f = blockIdx.y;
   const int32_t* toff = GPTR(const int32_t, a.fit_tree_off);
@@ -123,7 +125,7 @@ __global__ __launch_bounds__(256) void k_predict_reg(PredictArgs a) {
   for (int t = toff[f]; t < tend; t += kPredU) {
     int leaf[kPredU];
     const int u_n = min(kPredU, tend - t);
-    leaves_u(nodes, xr, t, u_n, leaf);
+    leaves_u<kPredU>(nodes, xr, t, u_n, leaf);
 #pragma unroll
     for (int u = 0; u < kPredU; ++u) {
       if (u >= u_n) break;
@@ -241,6 +243,26 @@ __global__ __launch_bounds__(256) void k_refine_split(NodeRec* nodes, int64_t P,
   nodes[i].split = f * 256 + b;
 }
 
+// U trees walked in lock-step per thread (memory-level parallelism of the dependent
+// node-load chains); DML_PRED_U=4/16 select the other widths (A/B)
+template <int U>
+static int launch_predict(PredictArgs* a, hipStream_t st) {
+  dim3 grid((unsigned)((a->max_rows + 255) / 256), (unsigned)a->F);
+  if (a->is_reg) {
+    k_predict_reg<U><<<grid, 256, 0, st>>>(*a);
+  } else {
+    const int C = (int)a->n_classes;
+    if (C <= 2) k_predict_cls<2, U><<<grid, 256, 0, st>>>(*a);
+    else if (C <= 4) k_predict_cls<4, U><<<grid, 256, 0, st>>>(*a);
+    else if (C <= 8) k_predict_cls<8, U><<<grid, 256, 0, st>>>(*a);
+    else if (C <= 16) k_predict_cls<16, U><<<grid, 256, 0, st>>>(*a);
+    else if (C <= 32) k_predict_cls<32, U><<<grid, 256, 0, st>>>(*a);
+    else if (C <= 64) k_predict_cls<64, U><<<grid, 256, 0, st>>>(*a);
+    else return 5;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 }  // namespace dml
 
 using namespace dml;
@@ -271,20 +293,10 @@ int dml_predict_sizeof_args() { return (int)sizeof(PredictArgs); }
 
 int dml_forest_predict(PredictArgs* a, hipStream_t st) {
   if (a->F <= 0 || a->max_rows <= 0) return 0;
-  dim3 grid((unsigned)((a->max_rows + 255) / 256), (unsigned)a->F);
-  if (a->is_reg) {
-    k_predict_reg<<<grid, 256, 0, st>>>(*a);
-  } else {
-    const int C = (int)a->n_classes;
-    if (C <= 2) k_predict_cls<2><<<grid, 256, 0, st>>>(*a);
-    else if (C <= 4) k_predict_cls<4><<<grid, 256, 0, st>>>(*a);
-    else if (C <= 8) k_predict_cls<8><<<grid, 256, 0, st>>>(*a);
-    else if (C <= 16) k_predict_cls<16><<<grid, 256, 0, st>>>(*a);
-    else if (C <= 32) k_predict_cls<32><<<grid, 256, 0, st>>>(*a);
-    else if (C <= 64) k_predict_cls<64><<<grid, 256, 0, st>>>(*a);
-    else return 5;
-  }
-  return hipGetLastError() == hipSuccess ? 0 : 1;
+  static const int u = [] { const char* e = getenv("DML_PRED_U"); return e ? atoi(e) : 8; }();
+  if (u == 16) return launch_predict<16>(a, st);
+  if (u == 4) return launch_predict<4>(a, st);
+  return launch_predict<8>(a, st);
 }
 
 int dml_scores(ScoreArgs* a, hipStream_t st) {
