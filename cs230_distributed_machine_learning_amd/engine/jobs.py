@@ -92,6 +92,11 @@ class Job:
     started_ts: float = field(default_factory=time.time)
     finished_ts: Optional[float] = None
     error: Optional[str] = None
+    fits_done: int = 0                   # CV/holdout fits of completed subtasks (north-star counter)
+
+    def fits_per_s(self) -> float:
+        dt = (self.finished_ts or time.time()) - self.started_ts
+        return self.fits_done / dt if dt > 0 else 0.0
 
     @property
     def total(self) -> int:
@@ -114,6 +119,8 @@ class JobTable:
         self.jobs: Dict[str, Job] = {}
         self.journal_path = journal_path
         self._journal = None
+        self.node_fits = 0                    # fits completed by this controller since start
+        self.node_t0 = time.time()
         if journal_path:
             os.makedirs(os.path.dirname(os.path.abspath(journal_path)), exist_ok=True)
 
@@ -226,6 +233,9 @@ class JobTable:
         st.completed_at = now_iso()
         if st.status == "completed":
             job.n_done += 1
+            nf = int((result or {}).get("n_fits") or 0)
+            job.fits_done += nf
+            self.node_fits += nf
         else:
             job.n_failed += 1
         if log:
@@ -277,7 +287,8 @@ class JobTable:
         with self._lock:
             pending = sum(1 for st in job.subtasks if st.status not in TERMINAL)
             resp = {"session_id": job.session_id, "tasks_pending": pending, "job_id": job.job_id,
-                    "job_status": job.status, "total_subtasks": job.total}
+                    "job_status": job.status, "total_subtasks": job.total,
+                    "fits_done": job.fits_done, "fits_per_s": round(job.fits_per_s(), 4)}
             if job.finished and job.result is not None:
                 resp["job_result"] = job.result
                 if job.total > 1:
@@ -289,7 +300,8 @@ class JobTable:
         with self._lock:
             pending = sum(1 for st in job.subtasks if st.status not in TERMINAL)
             data = {"session_id": job.session_id, "job_id": job.job_id, "job_status": job.status,
-                    "tasks_pending": pending, "total_subtasks": job.total}
+                    "tasks_pending": pending, "total_subtasks": job.total,
+                    "fits_done": job.fits_done, "fits_per_s": round(job.fits_per_s(), 4)}
             if job.finished and job.result is not None:
                 data["job_result"] = job.result
             return json_safe(data)
@@ -305,6 +317,8 @@ class JobTable:
                 "sessions": len(self.sessions),
                 "jobs": len(self.jobs),
                 "running": sum(1 for j in self.jobs.values() if not j.finished),
+                "fits_done": self.node_fits,
+                "fits_per_s_since_start": round(self.node_fits / max(1e-9, time.time() - self.node_t0), 4),
             }
 
 

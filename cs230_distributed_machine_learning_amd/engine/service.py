@@ -431,6 +431,12 @@ def run_slice(plan: Dict[str, Any], params: List[Dict[str, Any]], subtask_ids: L
                    error_score=plan["error_score"], keep_models="none", seed=seed, raise_batch_errors=True)
     received = utc_iso()
     slice_key = ",".join(str(int(c)) for c in cand_ids)
+    gpu = dd.device.index if dd.is_gpu else None
+    if dd.is_gpu:
+        import torch
+
+        torch.cuda.reset_peak_memory_stats(dd.device)
+        hbm0 = torch.cuda.memory_allocated(dd.device)
     with _Sampler() as smp:
         started = utc_iso()
         t0 = time.perf_counter()
@@ -442,6 +448,10 @@ def run_slice(plan: Dict[str, Any], params: List[Dict[str, Any]], subtask_ids: L
         wall = time.perf_counter() - t0
     finished = utc_iso()
     cpu, mem = smp.avg()
+    hbm_peak = None
+    if dd.is_gpu:
+        hbm_peak = int(torch.cuda.max_memory_allocated(dd.device) - hbm0)   # slice working set above resident data
+    slice_fits = sum(int(r.result.get("n_fits", 0)) for r in results if r.ok)
     metrics = {}
     for r in results:
         metrics[r.candidate] = {
@@ -450,6 +460,9 @@ def run_slice(plan: Dict[str, Any], params: List[Dict[str, Any]], subtask_ids: L
             "finished_at": finished, "cpu_percent_avg": cpu, "mem_percent_avg": mem, "algo": plan["model_type"],
             "device": device_name, "fit_seconds": r.fit_seconds, "slice_wall_seconds": wall,
             "n_fits": r.result.get("n_fits", 0) if r.ok else 0, "attempts": attempts,
+            # GPU fields: device index, slice HBM working set, slice throughput
+            "gpu_id": gpu, "hbm_peak_bytes": hbm_peak, "slice_fits": slice_fits,
+            "slice_fits_per_s": round(slice_fits / wall, 4) if wall > 0 else None,
         }
     return results, metrics, wall
 

@@ -195,3 +195,22 @@ def test_svm_gpu_matches_cpu_solver(model, clf):
         assert all(r.ok for r in res), [r.error for r in res]
         out[dev] = np.array([r.result["mean_cv_score"] for r in res])
     np.testing.assert_allclose(out["cuda:0"], out["cpu"], atol=2e-3)
+
+
+def test_slice_metrics_report_gpu_fields():
+    """J3 records of a device slice carry the GPU index, the slice's HBM working set and
+    its fits/s (SURVEY §5.1/§5.5 observability fields)."""
+    from cs230_distributed_machine_learning_amd.engine.service import run_slice
+
+    rng = np.random.RandomState(5)
+    X = rng.randn(4000, 12).astype(np.float32)
+    y = (X[:, 0] + 0.3 * rng.randn(4000) > 0).astype(np.int64)
+    dd = DeviceData(X, y, True, "cuda:0")
+    plan = {"model_type": "RandomForestClassifier", "cv": 3, "scoring": None, "holdout": True, "test_size": 0.2,
+            "random_state": 0, "error_score": float("nan")}
+    params = [{"n_estimators": 8, "max_depth": 4}, {"n_estimators": 8, "max_depth": 8}]
+    results, metrics, wall = run_slice(plan, params, ["s-0", "s-1"], dd, [0, 1], "rank0", "cuda:0")
+    assert all(r.ok for r in results)
+    for m in metrics.values():
+        assert m["gpu_id"] == 0 and m["hbm_peak_bytes"] > 0
+        assert m["slice_fits"] == 8 and m["slice_fits_per_s"] > 0

@@ -84,9 +84,15 @@ def test_grid_job_contract(ctl):
         assert 0 <= r["mean_cv_score"] <= 1
     best = status["best_result"]
     assert best["mean_cv_score"] == max(r["mean_cv_score"] for r in res)
+    # north-star counters: 8 candidates x (5 CV + 1 holdout) fits, per job and per node
+    assert status["fits_done"] == 48 and status["fits_per_s"] > 0
+    health = ctl.health()[1]
+    assert health["fits_done"] >= 48 and health["fits_per_s_since_start"] > 0
     # J8 records: one per subtask with J2 ids
     st, recs = ctl.metrics(sid, "job-a")
     assert st == 200 and len(recs) == 8
+    for r in recs:   # GPU fields (None on this CPU controller) and slice throughput
+        assert "gpu_id" in r and "hbm_peak_bytes" in r and r["slice_fits"] >= r["n_fits"] > 0
     ids = sorted(r["subtask_id"] for r in recs)
     assert ids == sorted(f"job-a-subtask-{i}" for i in range(1, 9))
     assert all(r["status"] == "DONE" for r in recs)          # J3 (worker.py:233-244)
