@@ -3,7 +3,8 @@
 Replaces the three hard-coded ``config.py`` modules and scattered env vars of the
 reference (aws-prod/master/config.py:11-18, scheduler/config.py:12-19,
 worker/config.py:10-15, scheduler_service.py:29-37).  Values come from
-defaults < environment (``DML_*``) < explicit overrides / CLI flags.
+defaults < YAML file (``--config`` / ``DML_CONFIG``) < environment (``DML_*``) <
+explicit overrides / CLI flags.
 ``ALGO_WEIGHT_JSON`` is honoured for compatibility with the reference scheduler.
 """
 from __future__ import annotations
@@ -44,8 +45,11 @@ class Config:
         return os.path.join(os.path.abspath(self.data_root), "models")
 
     @classmethod
-    def from_env(cls, **overrides) -> "Config":
+    def from_env(cls, config_file: Optional[str] = None, **overrides) -> "Config":
         cfg = cls()
+        path = config_file or os.environ.get("DML_CONFIG")
+        if path:
+            cfg._apply_file(path)
         for f in fields(cls):
             env = os.environ.get("DML_" + f.name.upper())
             if env is None:
@@ -62,8 +66,29 @@ class Config:
                 setattr(cfg, k, v)
         return cfg
 
+    def _apply_file(self, path: str) -> None:
+        """YAML (or JSON) mapping of field names; unknown keys are an error."""
+        import yaml
+
+        with open(path) as f:
+            doc = yaml.safe_load(f) or {}
+        if not isinstance(doc, dict):
+            raise ValueError(f"config file {path} must hold a mapping")
+        known = {f.name: f for f in fields(self)}
+        bad = sorted(k for k in doc if k.replace("-", "_") not in known)
+        if bad:
+            raise ValueError(f"unknown config keys in {path}: {bad}")
+        for k, v in doc.items():
+            f = known[k.replace("-", "_")]
+            if isinstance(v, str) and "str" not in str(f.type):
+                v = _coerce(f.type, v)
+            if f.name == "algo_weight" and v is not None:
+                v = {str(a).lower(): float(w) for a, w in dict(v).items()}
+            setattr(self, f.name, v)
+
     @staticmethod
     def add_cli(ap: argparse.ArgumentParser) -> None:
+        ap.add_argument("--config", help="YAML config file (keys = Config fields)")
         ap.add_argument("--data-root")
         ap.add_argument("--journal")
         ap.add_argument("--device")
@@ -72,12 +97,17 @@ class Config:
         ap.add_argument("--keep-models", choices=["none", "best", "all"])
         ap.add_argument("--hbm-budget-gb", type=float)
         ap.add_argument("--log-dir")
+        ap.add_argument("--chunk-target-s", type=float)
+        ap.add_argument("--max-retries", type=int)
+        ap.add_argument("--dp-auto-gb", type=float)
+        ap.add_argument("--dp-min-cells", type=int)
 
     @classmethod
     def from_args(cls, ns: argparse.Namespace) -> "Config":
-        return cls.from_env(**{k: getattr(ns, k, None) for k in
+        return cls.from_env(config_file=getattr(ns, "config", None),
+                            **{k: getattr(ns, k, None) for k in
                                ("data_root", "journal", "device", "host", "port", "keep_models", "hbm_budget_gb",
-                                "log_dir")})
+                                "log_dir", "chunk_target_s", "max_retries", "dp_auto_gb", "dp_min_cells")})
 
     def resolved_device(self) -> str:
         if self.device != "auto":
