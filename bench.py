@@ -111,12 +111,19 @@ def main() -> int:
     costs = np.array(candidate_costs(plan, int(args.rows * (args.cv - 1) / args.cv), args.features, 2))
     order = np.argsort(-costs, kind="stable")
     c = args.cands_per_rank
-    groups = np.array_split(order, c)   # cost-quantile groups; a rank-step takes one candidate from each
+    groups = np.array_split(order, c)   # cost-quantile groups; a step takes N candidates from each
+    # Within a group, successive picks u = 0, 1, 2, ... visit positions in golden-ratio
+    # (low-discrepancy) order: any window of steps samples the group's cost range evenly
+    # (taking positions 0, 1, 2, ... would always pick each group's most expensive
+    # candidates first), and len(g) consecutive picks visit every candidate once, so
+    # ``--steps`` x N x c = 256 covers the whole grid exactly.
+    golden = [np.argsort(np.argsort(np.mod(np.arange(len(g)) * 0.6180339887498949, 1.0), kind="stable"),
+                         kind="stable") for g in groups]
 
     from cs230_distributed_machine_learning_amd.engine.scheduler import lpt_assign
 
     def step_pool(step: int):
-        return [int(g[(step * N + j) % len(g)]) for g in groups for j in range(N)]
+        return [int(g[gp[(step * N + j) % len(g)]]) for g, gp in zip(groups, golden) for j in range(N)]
 
     def rank_step_cands(step: int):
         # the step's pool: N candidates from every cost-quantile group (N x c candidates,

@@ -115,6 +115,10 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
     if sharded and not getattr(fam, "data_parallel", False):
         raise ValueError(f"{spec.model_type} has no row-sharded (data-parallel) fit; run it task-parallel")
     tasks, errors = build_tasks(data, spec, candidate_ids)
+    if data.is_gpu and not getattr(fam, "uses_forest_arena", False):
+        from ..ops import forest_ops
+
+        forest_ops.ARENA.clear(data.device)   # idle forest buffers back to the device for this family
     keep = spec.keep_models in ("all", "best")
     outputs: Dict[int, FitOutput] = {}
     if tasks:

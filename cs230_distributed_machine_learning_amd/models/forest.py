@@ -71,6 +71,7 @@ def _count_param(v, n, name, lo_int):
 class ForestFamily(Family):
     model_types = (_CLS, _REG)
     classifiers = (_CLS,)
+    uses_forest_arena = True   # batches reuse the device arena (ops/forest_ops.py ARENA)
 
     def __init__(self):
         self.tiers = forest_ops.ForestTiers()
@@ -153,7 +154,9 @@ class ForestFamily(Family):
             # blocks the caching allocator holds but nobody uses are free for this batch too
             # (without this, the previous batch's freed pool makes the next batch split)
             cached = torch.cuda.memory_reserved(data.device) - torch.cuda.memory_allocated(data.device)
-            return float(os.environ.get("DML_HBM_FRACTION", "0.55")) * (free + max(0, cached))
+            # ... and so are the idle forest arena slots this batch will reuse (ops/forest_ops.py)
+            arena = forest_ops.ARENA.held_bytes(data.device)
+            return float(os.environ.get("DML_HBM_FRACTION", "0.55")) * (free + max(0, cached) + arena)
         return 8e9
 
     def run(self, data, tasks: List[FitTask], keep_models: bool = False) -> List[FitOutput]:
@@ -210,37 +213,41 @@ class ForestFamily(Family):
         t0 = time.perf_counter()
         if data.is_gpu:
             fb = forest_ops.build_gpu(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
-                                      data.n_classes, is_reg, self.tiers)
+                                      data.n_classes, is_reg, self.tiers, reuse_pool=True)
         else:
             fb = forest_ops.build_cpu(Xb.numpy(), data.y_enc, None if not is_reg else data.y_reg.numpy(),
                                       data.roles_np(), specs, data.n_classes, is_reg)
-        with trace.range("forest_refine"):
-            _refine(data, fb, Xb, specs, data.roles)
-        toff = np.zeros(len(batch) + 1, dtype=np.int64)
-        np.cumsum([t.params["n_estimators"] for t in batch], out=toff[1:])
-        rows = [data.test_rows[t.split] for t in batch]
-        roff = np.zeros(len(batch) + 1, dtype=np.int64)
-        np.cumsum([int(r.numel()) for r in rows], out=roff[1:])
-        if data.is_gpu:
-            rows_cat = torch.cat(rows) if rows else torch.empty(0, dtype=torch.int32, device=data.device)
-            pred = forest_ops.predict(fb, Xb, toff, roff, rows_cat)
-        else:
-            rows_cat = np.concatenate([r.numpy() for r in rows]) if rows else np.zeros(0, np.int32)
-            pred = forest_ops.predict(fb, Xb.numpy(), toff, roff, rows_cat)
-            pred = torch.from_numpy(pred)
-        if data.is_gpu:
-            torch.cuda.synchronize(data.device)
-        dt = time.perf_counter() - t0
-        total_trees = max(1, int(toff[-1]))
-        outs = []
-        for f, t in enumerate(batch):
-            share = t.params["n_estimators"] / total_trees
-            o = FitOutput(task_id=t.task_id, pred=pred[roff[f]:roff[f + 1]], fit_seconds=dt * share,
-                          info={"warnings": t.params.get("warnings", []), "batch_stats": dict(fb.stats)})
-            if keep_models:
-                o.model = extract_forest(fb, int(toff[f]), int(toff[f + 1]), data, t)
-            outs.append(o)
-        return outs
+        try:
+            with trace.range("forest_refine"):
+                _refine(data, fb, Xb, specs, data.roles)
+            toff = np.zeros(len(batch) + 1, dtype=np.int64)
+            np.cumsum([t.params["n_estimators"] for t in batch], out=toff[1:])
+            rows = [data.test_rows[t.split] for t in batch]
+            roff = np.zeros(len(batch) + 1, dtype=np.int64)
+            np.cumsum([int(r.numel()) for r in rows], out=roff[1:])
+            if data.is_gpu:
+                rows_cat = torch.cat(rows) if rows else torch.empty(0, dtype=torch.int32, device=data.device)
+                pred = forest_ops.predict(fb, Xb, toff, roff, rows_cat)
+            else:
+                rows_cat = np.concatenate([r.numpy() for r in rows]) if rows else np.zeros(0, np.int32)
+                pred = forest_ops.predict(fb, Xb.numpy(), toff, roff, rows_cat)
+                pred = torch.from_numpy(pred)
+            if data.is_gpu:
+                with trace.range("forest_predict_wait"):   # refine + predict kernels drain here
+                    torch.cuda.synchronize(data.device)
+            dt = time.perf_counter() - t0
+            total_trees = max(1, int(toff[-1]))
+            outs = []
+            for f, t in enumerate(batch):
+                share = t.params["n_estimators"] / total_trees
+                o = FitOutput(task_id=t.task_id, pred=pred[roff[f]:roff[f + 1]], fit_seconds=dt * share,
+                              info={"warnings": t.params.get("warnings", []), "batch_stats": dict(fb.stats)})
+                if keep_models:
+                    o.model = extract_forest(fb, int(toff[f]), int(toff[f + 1]), data, t)
+                outs.append(o)
+            return outs
+        finally:   # the node pool is an arena slot: free it for the next batch
+            forest_ops.release_pool(fb)
 
 
 def _refine(data, fb, Xb, specs, roles) -> None:

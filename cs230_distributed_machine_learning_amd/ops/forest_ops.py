@@ -13,9 +13,10 @@ from __future__ import annotations
 
 import ctypes
 import math
+import threading
 import time
 from dataclasses import dataclass, field
-from typing import Optional
+from typing import Dict, Optional
 
 import numpy as np
 import torch
@@ -94,11 +95,73 @@ def _pool_bound(counts: np.ndarray, specs: np.ndarray) -> int:
     return int(per.sum()) + 16
 
 
+class _Arena:
+    """Per-device byte buffers reused by successive forest builds (grow-only).
+
+    A forest batch needs a workspace and a node pool of tens of GB whose sizes change
+    from batch to batch; fresh ``torch.empty`` calls of that size miss the caching
+    allocator and fall through to hipMalloc / release-and-retry, which measured ~1.1 s
+    per batch (a third of the bench step).  The arena keeps one buffer per slot and
+    device, grown with 1/8 headroom when a batch needs more, and hands out views.
+    Slot ``"ws"`` lives for one build; slot ``"pool"`` backs the returned node arrays
+    and is only used when the caller finishes with the ForestBuild before the next
+    build (the forest family; boosting keeps its trees and allocates its own)."""
+
+    def __init__(self):
+        self.bufs: Dict[tuple, torch.Tensor] = {}
+        self.busy: set = set()
+        self.lock = threading.Lock()
+
+    def take(self, dev: torch.device, slot: str, nbytes: int) -> Optional[torch.Tensor]:
+        key = (dev.index if dev.index is not None else torch.cuda.current_device(), slot)
+        with self.lock:
+            if key in self.busy:
+                return None              # another build on this device holds it: allocate fresh
+            buf = self.bufs.get(key)
+            if buf is None or buf.numel() < nbytes:
+                self.bufs.pop(key, None)
+                del buf
+                buf = torch.empty(int(nbytes + nbytes // 8), dtype=torch.uint8, device=dev)
+                self.bufs[key] = buf
+            self.busy.add(key)
+            return buf
+
+    def give(self, dev: torch.device, slot: str) -> None:
+        key = (dev.index if dev.index is not None else torch.cuda.current_device(), slot)
+        with self.lock:
+            self.busy.discard(key)
+
+    def clear(self, dev: torch.device) -> None:
+        """Return the idle slots of ``dev`` to the device (another family needs the HBM)."""
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        with self.lock:
+            drop = [k for k in self.bufs if k[0] == idx and k not in self.busy]
+            for k in drop:
+                del self.bufs[k]
+        if drop:
+            torch.cuda.empty_cache()
+
+    def held_bytes(self, dev: torch.device) -> int:
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        with self.lock:
+            return sum(int(b.numel()) for (i, _s), b in self.bufs.items() if i == idx and (i, _s) not in self.busy)
+
+
+ARENA = _Arena()
+
+
+def _carve(buf: torch.Tensor, off: int, shape, dtype) -> torch.Tensor:
+    n = int(np.prod(shape)) * torch.tensor([], dtype=dtype).element_size()
+    return buf[off:off + n].view(dtype).view(*shape)
+
+
 def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,
               specs: np.ndarray, n_classes: int, is_reg: bool, tiers: ForestTiers | None = None,
-              ystride: int = 0) -> ForestBuild:
+              ystride: int = 0, reuse_pool: bool = False) -> ForestBuild:
     """``ystride > 0``: ``yreg`` is a [targets, ystride] matrix and tree t regresses on
-    row ``specs[t]['target']`` (gradient boosting's per-fit pseudo-residuals)."""
+    row ``specs[t]['target']`` (gradient boosting's per-fit pseudo-residuals).
+    ``reuse_pool``: the node arrays live in the device arena and are valid until the
+    next ``reuse_pool`` build on this device (the caller must be done with them)."""
     lib = native.hip_lib()
     dev = Xb.device
     T = len(specs)
@@ -138,33 +201,71 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     tree_W = torch.empty(T, dtype=torch.float64, device=dev)
     a.tree_W = native.ptr(tree_W)
     ws_bytes = lib.dml_forest_workspace_bytes(ctypes.byref(a))
-    workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    with trace.range("forest_alloc"):
+        ws_buf = ARENA.take(dev, "ws", ws_bytes)
+        workspace = ws_buf[:ws_bytes] if ws_buf is not None else torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     a.workspace, a.workspace_bytes = native.ptr(workspace), ws_bytes
     retries = 0
-    for _attempt in range(4):
-        nodes = torch.empty((pool_cap, 2), dtype=torch.int32, device=dev)
-        vals = torch.empty((pool_cap, VC), dtype=torch.float64, device=dev)
-        a.nodes, a.node_val, a.pool_cap = native.ptr(nodes), native.ptr(vals), pool_cap
-        a.status_out = 0
-        with trace.range("forest_build"):   # host-side launch sequence of every tier
-            rc = lib.dml_forest_build(ctypes.byref(a), stream)
-        if rc:
-            raise RuntimeError(f"dml_forest_build failed ({rc}): {native.hip_error(lib)}")
-        if a.status_out == 1:
-            pool_cap *= 2
-            retries += 1
-            continue
-        if a.status_out != 0:
-            raise RuntimeError(f"dml_forest_build status {a.status_out}")
-        break
-    else:
-        raise RuntimeError("forest node pool overflow")
+    pool_held = False
+    try:
+        for _attempt in range(4):
+            with trace.range("forest_alloc"):
+                vals_off = (pool_cap * 8 + 255) // 256 * 256
+                pool_bytes = vals_off + pool_cap * VC * 8
+                pbuf = None
+                if reuse_pool:
+                    if pool_held:                      # a pool retry may need a bigger slot
+                        ARENA.give(dev, "pool")
+                        pool_held = False
+                    pbuf = ARENA.take(dev, "pool", pool_bytes)
+                    pool_held = pbuf is not None
+                if pbuf is not None:
+                    nodes = _carve(pbuf, 0, (pool_cap, 2), torch.int32)
+                    vals = _carve(pbuf, vals_off, (pool_cap, VC), torch.float64)
+                else:
+                    nodes = torch.empty((pool_cap, 2), dtype=torch.int32, device=dev)
+                    vals = torch.empty((pool_cap, VC), dtype=torch.float64, device=dev)
+            a.nodes, a.node_val, a.pool_cap = native.ptr(nodes), native.ptr(vals), pool_cap
+            a.status_out = 0
+            with trace.range("forest_build"):   # host-side launch sequence of every tier
+                rc = lib.dml_forest_build(ctypes.byref(a), stream)
+            if rc:
+                raise RuntimeError(f"dml_forest_build failed ({rc}): {native.hip_error(lib)}")
+            if a.status_out == 1:
+                pool_cap *= 2
+                retries += 1
+                continue
+            if a.status_out != 0:
+                raise RuntimeError(f"dml_forest_build status {a.status_out}")
+            break
+        else:
+            raise RuntimeError("forest node pool overflow")
+    except BaseException:
+        if pool_held:
+            ARENA.give(dev, "pool")
+        raise
+    finally:
+        # stream order keeps the next build's kernels behind this build's on the same stream
+        if ws_buf is not None:
+            ARENA.give(dev, "ws")
     P = int(a.n_nodes_out)
     del workspace
     stats = {"levels": int(a.levels_out), "large_rounds": int(a.large_rounds_out), "nodes": P,
              "rows_total": int(a.rows_total), "build_s": time.perf_counter() - t0, "pool_retries": retries,
              "tier_nodes": [int(a.tier0_nodes), int(a.tier1_nodes), int(a.tier2_nodes), int(a.tier3_nodes)]}
-    return ForestBuild(nodes[:P], vals[:P], T, VC, is_reg, n_classes, stats)
+    fb = ForestBuild(nodes[:P], vals[:P], T, VC, is_reg, n_classes, stats)
+    if pool_held:
+        fb.arena_dev = dev   # release_pool(fb) hands the arena slot back
+    return fb
+
+
+def release_pool(fb: ForestBuild) -> None:
+    """The caller is done with a ``reuse_pool`` build's node arrays."""
+    dev = getattr(fb, "arena_dev", None)
+    if dev is not None:
+        fb.nodes = fb.vals = None
+        fb.arena_dev = None
+        ARENA.give(dev, "pool")
 
 
 def build_cpu(Xb: np.ndarray, ycls: Optional[np.ndarray], yreg: Optional[np.ndarray], roles: np.ndarray,

@@ -52,11 +52,13 @@ def main():
     plan = {"model_type": "RandomForestClassifier", "candidates": cands, "cv": a.cv, "holdout": False}
     costs = np.array(candidate_costs(plan, int(a.rows * (a.cv - 1) / a.cv), a.features, 2))
     groups = np.array_split(np.argsort(-costs, kind="stable"), a.cands_per_rank)
+    golden = [np.argsort(np.argsort(np.mod(np.arange(len(g)) * 0.6180339887498949, 1.0), kind="stable"),
+                         kind="stable") for g in groups]   # same pick order as bench.py
 
     def lists(N, step, how):
         if how == "group":
             return [[int(g[(step * N + r) % len(g)]) for g in groups] for r in range(N)]
-        pool = [int(g[(step * N + j) % len(g)]) for g in groups for j in range(N)]
+        pool = [int(g[gp[(step * N + j) % len(g)]]) for g, gp in zip(groups, golden) for j in range(N)]
         owner = lpt_assign([float(costs[i]) for i in pool], N)
         return [[c for c, o in zip(pool, owner) if int(o) == r] for r in range(N)]
 
