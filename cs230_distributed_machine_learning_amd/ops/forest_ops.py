@@ -102,7 +102,7 @@ class _Arena:
     from batch to batch; fresh ``torch.empty`` calls of that size miss the caching
     allocator and fall through to hipMalloc / release-and-retry, which measured ~1.1 s
     per batch (a third of the bench step).  The arena keeps one buffer per slot and
-    device, grown with 1/8 headroom when a batch needs more, and hands out views.
+    device, grown with 50% headroom (capped by free HBM) when a batch needs more, and hands out views.
     Slot ``"ws"`` lives for one build; slot ``"pool"`` backs the returned node arrays
     and is only used when the caller finishes with the ForestBuild before the next
     build (the forest family; boosting keeps its trees and allocates its own)."""
@@ -121,7 +121,12 @@ class _Arena:
             if buf is None or buf.numel() < nbytes:
                 self.bufs.pop(key, None)
                 del buf
-                buf = torch.empty(int(nbytes + nbytes // 8), dtype=torch.uint8, device=dev)
+                # grow with 50% headroom (batch sizes vary; every regrowth is a slow
+                # hipMalloc), but never past 80% of what the device can still give
+                free, _ = torch.cuda.mem_get_info(dev)
+                spare = free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+                target = max(int(nbytes), min(int(nbytes * 3 // 2), int(0.8 * spare)))
+                buf = torch.empty(target, dtype=torch.uint8, device=dev)
                 self.bufs[key] = buf
             self.busy.add(key)
             return buf
