@@ -122,10 +122,11 @@ class _Arena:
                 self.bufs.pop(key, None)
                 del buf
                 # grow with 50% headroom (batch sizes vary; every regrowth is a slow
-                # hipMalloc), but never past 80% of what the device can still give
+                # hipMalloc), but never past 70% of what the device can still give (kernel scratch and
+                # runtime queues need the rest: a 0.8 budget fraction ran the queue out of resources)
                 free, _ = torch.cuda.mem_get_info(dev)
                 spare = free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
-                target = max(int(nbytes), min(int(nbytes * 3 // 2), int(0.8 * spare)))
+                target = max(int(nbytes), min(int(nbytes * 3 // 2), int(0.7 * spare)))
                 buf = torch.empty(target, dtype=torch.uint8, device=dev)
                 self.bufs[key] = buf
             self.busy.add(key)
