@@ -178,92 +178,12 @@ class ForestFamily(Family):
             cur_bytes += b
         if cur:
             batches.append(cur)
-        if data.is_gpu and not keep_models and len(batches) > 1 and os.environ.get("DML_FOREST_OVERLAP", "1") != "0":
-            got = self._run_batches_overlapped(data, Xb, batches, is_reg)
-            if got is not None:
-                for o in got:
-                    outs[o.task_id] = o
-                return [outs[t.task_id] for t in tasks]
         for batch in batches:
             with trace.range("forest_batch"):
                 out_b = self._run_batch(data, Xb, batch, is_reg, keep_models)
             for o in out_b:
                 outs[o.task_id] = o
         return [outs[t.task_id] for t in tasks]
-
-    def _run_batches_overlapped(self, data, Xb, batches: List[List[FitTask]], is_reg: bool):
-        """Several batches: batch k's held-out predict runs on a side stream while batch
-        k+1 builds on the main stream.  After refine, batch k's used nodes are copied into
-        the arena's ``pred`` slot (so the pool slot is free for the next build); the main
-        stream waits for predict k-1 before overwriting that slot, so the copy, the
-        predict and the next build stay ordered without any host sync."""
-        dev = data.device
-        main = torch.cuda.current_stream(dev)
-        side = _side_stream(dev)
-        prev_done = None
-        outs: List[FitOutput] = []
-        preds = []
-        t_run = time.perf_counter()
-        pred_buf = forest_ops.ARENA.take(dev, "pred", 1)
-        if pred_buf is None:   # slot held by another build on this device: sequential path
-            return None
-        try:
-            for batch in batches:
-                with trace.range("forest_batch"):
-                    specs = self._specs(batch)
-                    fb = forest_ops.build_gpu(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
-                                              data.n_classes, is_reg, self.tiers, reuse_pool=True)
-                    try:
-                        with trace.range("forest_refine"):
-                            _refine(data, fb, Xb, specs, data.roles)
-                        P, VC = int(fb.nodes.shape[0]), fb.VC
-                        voff = (P * 8 + 255) // 256 * 256
-                        if prev_done is not None:
-                            main.wait_event(prev_done)          # predict k-1 is done reading the slot
-                        if pred_buf is None or pred_buf.numel() < voff + P * VC * 8:
-                            forest_ops.ARENA.give(dev, "pred")
-                            pred_buf = forest_ops.ARENA.take(dev, "pred", voff + P * VC * 8)
-                        cn = forest_ops._carve(pred_buf, 0, (P, 2), torch.int32)
-                        cv = forest_ops._carve(pred_buf, voff, (P, VC), torch.float64)
-                        cn.copy_(fb.nodes)
-                        cv.copy_(fb.vals)
-                        stats = dict(fb.stats)
-                    finally:
-                        forest_ops.release_pool(fb)          # next build may reuse the pool slot
-                    fbc = forest_ops.ForestBuild(cn, cv, fb.n_trees, VC, is_reg, data.n_classes, stats)
-                    copied = torch.cuda.Event()
-                    copied.record(main)
-                    toff = np.zeros(len(batch) + 1, dtype=np.int64)
-                    np.cumsum([t.params["n_estimators"] for t in batch], out=toff[1:])
-                    rows = [data.test_rows[t.split] for t in batch]
-                    roff = np.zeros(len(batch) + 1, dtype=np.int64)
-                    np.cumsum([int(r.numel()) for r in rows], out=roff[1:])
-                    rows_cat = torch.cat(rows) if rows else torch.empty(0, dtype=torch.int32, device=dev)
-                    side.wait_event(copied)
-                    with torch.cuda.stream(side):
-                        pred = forest_ops.predict(fbc, Xb, toff, roff, rows_cat)
-                        done = torch.cuda.Event()
-                        done.record(side)
-                    rows_cat.record_stream(side)
-                    pred.record_stream(main)
-                    prev_done = done
-                    preds.append((batch, pred, roff, toff, stats))
-            if prev_done is not None:
-                with trace.range("forest_predict_wait"):
-                    main.wait_event(prev_done)
-                    torch.cuda.synchronize(dev)
-        finally:
-            if prev_done is not None:
-                prev_done.synchronize()
-            forest_ops.ARENA.give(dev, "pred")
-        dt = time.perf_counter() - t_run
-        total_trees = max(1, sum(int(tf[-1]) for _b, _p, _r, tf, _s in preds))
-        for batch, pred, roff, toff, stats in preds:
-            for f, t in enumerate(batch):
-                share = t.params["n_estimators"] / total_trees
-                outs.append(FitOutput(task_id=t.task_id, pred=pred[roff[f]:roff[f + 1]], fit_seconds=dt * share,
-                                      info={"warnings": t.params.get("warnings", []), "batch_stats": stats}))
-        return outs
 
     def _specs(self, batch: List[FitTask]) -> np.ndarray:
         T = sum(t.params["n_estimators"] for t in batch)
@@ -328,16 +248,6 @@ class ForestFamily(Family):
             return outs
         finally:   # the node pool is an arena slot: free it for the next batch
             forest_ops.release_pool(fb)
-
-
-_SIDE: Dict[int, "torch.cuda.Stream"] = {}
-
-
-def _side_stream(dev) -> "torch.cuda.Stream":
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    if idx not in _SIDE:
-        _SIDE[idx] = torch.cuda.Stream(device=dev)
-    return _SIDE[idx]
 
 
 def _refine(data, fb, Xb, specs, roles) -> None:

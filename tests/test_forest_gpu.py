@@ -171,33 +171,3 @@ def test_wave_primitives_sort_and_scan():
         assert np.array_equal(o[bi, 9], sd)
         mn = min((int(v[l]) << 32) | l for l in range(64))
         assert (o[bi, 10] == np.uint32(mn & 0xFFFFFFFF)).all()
-
-
-@pytest.mark.gpu
-def test_multi_batch_overlapped_predict_matches_sequential(monkeypatch):
-    """A memory budget that forces several forest batches: the overlapped path (predict
-    of batch k on a side stream while batch k+1 builds, node arrays copied out of the
-    arena pool) gives exactly the CV scores of the sequential path."""
-    from cs230_distributed_machine_learning_amd.data.device import DeviceData
-    from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
-    from cs230_distributed_machine_learning_amd.models.base import family_of
-
-    rng = np.random.RandomState(3)
-    X = rng.randn(20000, 16).astype(np.float32)
-    y = (X[:, 0] + X[:, 1] * X[:, 2] + 0.5 * rng.randn(20000) > 0).astype(np.int64)
-    dd = DeviceData(X, y, True, "cuda:0")
-    cands = [{"n_estimators": n, "max_depth": md, "min_samples_leaf": 1} for n in (6, 12) for md in (5, None)]
-    spec = JobSpec("RandomForestClassifier", cands, cv=3, holdout=True, test_size=0.2, random_state=0,
-                   keep_models="none")
-    fam = family_of("RandomForestClassifier")
-    per_fit = fam._tree_bytes(dd, {"bootstrap": True, "lambda": 1.0, "min_samples_leaf": 1}) * 12
-    monkeypatch.setattr(fam, "hbm_budget_bytes", per_fit * 2.5)    # ~2 fits per batch -> many batches
-    monkeypatch.setenv("DML_FOREST_OVERLAP", "0")
-    seq = run_candidates(dd, spec, range(len(cands)))
-    monkeypatch.setenv("DML_FOREST_OVERLAP", "1")
-    ovl = run_candidates(dd, spec, range(len(cands)))
-    assert all(r.ok for r in seq + ovl)
-    for a, b in zip(seq, ovl):
-        assert a.result["cv_scores"] == b.result["cv_scores"] and a.result["accuracy"] == b.result["accuracy"]
-    stats = [r for r in seq]
-    assert len(stats) == len(cands)
