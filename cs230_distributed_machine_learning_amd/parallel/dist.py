@@ -47,6 +47,11 @@ def init(backend: Optional[str] = None, timeout_s: float = 1800.0, want_gpu: Opt
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # multi-rank rehearsal on a one-GPU box: every rank shares device 0 and the
+    # collectives go over gloo (RCCL refuses two ranks on one device)
+    if os.environ.get("DML_SHARE_DEVICE") == "1":
+        local = 0
+    backend = backend or os.environ.get("DML_DIST_BACKEND") or None
     gpu = torch.cuda.is_available() if want_gpu is None else want_gpu
     if gpu:
         torch.cuda.set_device(local)
