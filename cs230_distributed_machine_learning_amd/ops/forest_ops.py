@@ -34,8 +34,8 @@ class ForestTiers:
 
     sub_max: int = 64          # <= 64 rows: one wave finishes the whole subtree (k_subtree)
     sub_cache_max_d: int = 256  # cache the subtree's bin rows in LDS when d <= this
-    wave_max: int = 256
-    block_max: int = 16384
+    wave_max: int = 512         # sweeps (profiles/r1_forest_ab_experiments.md): 512 / 131072 best
+    block_max: int = 131072
     chunk: int = 16384
     kg_wave: int = 4
     kg_block: int = 16
