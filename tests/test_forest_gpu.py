@@ -171,3 +171,28 @@ def test_wave_primitives_sort_and_scan():
         assert np.array_equal(o[bi, 9], sd)
         mn = min((int(v[l]) << 32) | l for l in range(64))
         assert (o[bi, 10] == np.uint32(mn & 0xFFFFFFFF)).all()
+
+
+@pytest.mark.gpu
+def test_gpu_family_scores_match_host_path():
+    """The whole forest family path on the GPU (build, refine, batched predict, fused
+    scoring) gives the C++ host builder + predictor's CV and holdout scores, and exported
+    models keep plain leaf records."""
+    from cs230_distributed_machine_learning_amd.data.device import DeviceData
+    from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
+
+    rng = np.random.RandomState(11)
+    X = rng.randn(6000, 12).astype(np.float32)
+    y = (X[:, 0] - X[:, 3] * X[:, 4] + 0.7 * rng.randn(6000) > 0).astype(np.int64)
+    cands = [{"n_estimators": 9, "max_depth": md, "min_samples_leaf": msl} for md in (4, None) for msl in (1, 5)]
+    spec = JobSpec("RandomForestClassifier", cands, cv=3, holdout=True, test_size=0.25, random_state=1,
+                   keep_models="all")
+    gpu = run_candidates(DeviceData(X, y, True, "cuda:0"), spec, range(len(cands)))
+    cpu = run_candidates(DeviceData(X, y, True, "cpu"), spec, range(len(cands)))
+    for g, c in zip(gpu, cpu):
+        assert g.ok and c.ok
+        # identical predictions; the two scoring paths may round the mean in the last ulp
+        assert np.allclose(g.result["cv_scores"], c.result["cv_scores"], rtol=0, atol=1e-12)
+        assert abs(g.result["accuracy"] - c.result["accuracy"]) <= 1e-12
+        nodes = np.asarray(g.model["nodes"])
+        assert set(np.unique(nodes[nodes[:, 0] < 0, 0]).tolist()) == {-1}
