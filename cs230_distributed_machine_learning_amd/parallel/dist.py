@@ -62,6 +62,10 @@ def init(backend: Optional[str] = None, timeout_s: float = 1800.0, want_gpu: Opt
     if world > 1:
         be = backend or ("nccl" if gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # RCCL watchdog: a collective that outlives the timeout (a peer rank
+        # died mid-job) tears the communicator down and raises instead of hanging the rank
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        timeout_s = float(os.environ.get("DML_COLLECTIVE_TIMEOUT_S", timeout_s))
         kw = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kw["device_id"] = device
