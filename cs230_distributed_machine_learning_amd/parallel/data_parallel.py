@@ -109,9 +109,9 @@ class RowShard(DeviceData):
         self.r0, self.n_global = int(r0), int(len(y_global))
         self.y_host = y_global            # split construction (stratified folds) sees the global labels
         self.group = group
-        if self.classification:
-            lookup = {c: i for i, c in enumerate(classes.tolist())}
-            self._y_glob = torch.tensor([lookup[v] for v in y_global.tolist()], dtype=torch.int32, device=self.device)
+        if self.classification:   # classes come sorted from np.unique: codes by binary search
+            codes = np.searchsorted(classes, y_global).astype(np.int32)
+            self._y_glob = torch.from_numpy(codes).to(self.device)
         else:
             self._y_glob = torch.from_numpy(np.asarray(y_global, dtype=np.float32)).to(self.device)
         self._test_glob: List[torch.Tensor] = []
