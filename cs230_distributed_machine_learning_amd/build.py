@@ -39,6 +39,27 @@ def _stale(target: str, sources: list[str]) -> bool:
     return any(os.path.getmtime(s) > t for s in sources)
 
 
+def _src_hash(sources: list[str], flags: list[str]) -> str:
+    import hashlib
+
+    h = hashlib.sha256(" ".join(flags).encode())
+    for s in sorted(sources):
+        with open(s, "rb") as f:
+            h.update(s.encode() + b"\0" + f.read())
+    return h.hexdigest()
+
+
+def _stale_by_hash(target: str, sources: list[str], flags: list[str]) -> bool:
+    """Content-keyed staleness (a fresh checkout gives every file a new mtime, so an
+    mtime test can pick a stale executable): the build stores the hash of its sources
+    and flags next to the target."""
+    stamp = target + ".srchash"
+    if not os.path.exists(target) or not os.path.exists(stamp):
+        return True
+    with open(stamp) as f:
+        return f.read().strip() != _src_hash(sources, flags)
+
+
 def _run(cmd: list[str]) -> None:
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
@@ -81,13 +102,15 @@ def build_sanitized(force: bool = False) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))) + [os.path.join(CSRC, "tests", "host_selftest.cpp")]
     deps = srcs + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
     os.makedirs(LIB, exist_ok=True)
-    if force or _stale(SAN_EXE, deps):
-        cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
+    cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
+    flags = [cxx, "-O1", "-g", "-std=c++17", "-fopenmp", "-ffp-contract=off", "-fsanitize=address,undefined",
+             "-fno-sanitize-recover=all", "-fno-omit-frame-pointer"]
+    if force or _stale_by_hash(SAN_EXE, deps, flags):
         tmp = SAN_EXE + ".tmp"
-        _run([cxx, "-O1", "-g", "-std=c++17", "-fopenmp", "-ffp-contract=off", "-fsanitize=address,undefined",
-              "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-I", os.path.join(CSRC, "kernels"), *srcs,
-              "-o", tmp])
+        _run([*flags, "-I", os.path.join(CSRC, "kernels"), *srcs, "-o", tmp])
         os.replace(tmp, SAN_EXE)
+        with open(SAN_EXE + ".srchash", "w") as f:
+            f.write(_src_hash(deps, flags))
     return SAN_EXE
 
 
