@@ -107,6 +107,15 @@ def main() -> int:
     spec = JobSpec("RandomForestClassifier", cands, cv=args.cv, holdout=False, random_state=0, keep_models="none",
                    seed=args.seed)
     prepare_splits(dd, spec)
+    if dev.type == "cuda":
+        # job setup: the device arena is sized once for the largest step batch this grid
+        # can form, so no timed step pays a multi-GB hipMalloc (the engine does the same
+        # per job: engine/service.py)
+        from cs230_distributed_machine_learning_amd.models.base import family_of
+
+        fam = family_of(spec.model_type)
+        rps = [fam.resolve(spec.model_type, p, dd.train_counts[0], dd.d, dd.n_classes) for p in cands]
+        fam.presize(dd, rps, args.cands_per_rank, args.cv)
     plan = {"model_type": "RandomForestClassifier", "candidates": cands, "cv": args.cv, "holdout": False}
     costs = np.array(candidate_costs(plan, int(args.rows * (args.cv - 1) / args.cv), args.features, 2))
     order = np.argsort(-costs, kind="stable")

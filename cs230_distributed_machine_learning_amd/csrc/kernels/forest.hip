@@ -49,6 +49,19 @@
 #ifndef DML_KGMAX_WAVE
 #define DML_KGMAX_WAVE 4
 #endif
+// large-tier grids: node index fastest (1) so chunk c of EVERY large node is in flight at
+// once -- at the top levels the rows behind chunk c of all trees of a fold are nearly the
+// same rows, so those table lines are served from the XCD's L2 -- or chunk fastest (0)
+#ifndef DML_LARGE_NODE_FAST
+#define DML_LARGE_NODE_FAST 1
+#endif
+#if DML_LARGE_NODE_FAST
+#define DML_LSLOT ((int)blockIdx.x)
+#define DML_LCHUNK ((int)blockIdx.y)
+#else
+#define DML_LSLOT ((int)blockIdx.y)
+#define DML_LCHUNK ((int)blockIdx.x)
+#endif
 
 // optional per-phase cycle accounting of the fused node kernel (-DDML_PHASE_PROF builds only)
 #ifdef DML_PHASE_PROF
@@ -1176,10 +1189,10 @@ template <int MODE>
 __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
   using CT = typename HT<MODE>::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int slot = blockIdx.y;
+  const int slot = DML_LSLOT;
   const LState& st = c.lstate[slot];
   if (st.done) return;
-  const int r0 = blockIdx.x * c.chunk;
+  const int r0 = DML_LCHUNK * c.chunk;
   if (r0 >= st.on.count) return;
   const int r1 = min(r0 + c.chunk, st.on.count);
   const TreeSpec& s = c.specs[st.on.tree];
@@ -1321,10 +1334,10 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
   // pass 1 ranks the chunk's rows (split bins prefetched one step ahead, flags kept in LDS)
   // and reserves the chunk's left/right ranges with ONE atomic pair; pass 2 writes the rows
   // at ballot/prefix offsets (no global atomics per 256 rows)
-  const int slot = blockIdx.y;
+  const int slot = DML_LSLOT;
   const LState& st = c.lstate[slot];
   if (!st.split) return;
-  const int r0 = blockIdx.x * c.chunk;
+  const int r0 = DML_LCHUNK * c.chunk;
   if (r0 >= st.on.count) return;
   const int r1 = min(r0 + c.chunk, st.on.count);
   const int feat = st.best_feat, bin = st.best_bin, nl = st.nl;
@@ -1786,14 +1799,15 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
         ++large_rounds;
         HIP_OK(hipMemsetAsync(c.ghist, 0, (size_t)nL * a->kg_large * CH * 256 * 4, st));
         HIP_OK(hipMemsetAsync(c.counters + kNeedMore, 0, 4, st));
-        dim3 gh(nchunks, (unsigned)nL);
+        const dim3 gh = DML_LARGE_NODE_FAST ? dim3((unsigned)nL, nchunks) : dim3(nchunks, (unsigned)nL);
         k_hist_large<MODE><<<gh, 256, lds_hl, st>>>(c);
         k_split_large<GM><<<nL, 256, lds_sl, st>>>(c, cur);
         HIP_OK(hipMemcpyAsync(h + 32, c.counters + kNeedMore, 4, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
         if (!h[32]) break;
       }
-      k_partition_large<<<dim3(nchunks, (unsigned)nL), 256, (size_t)((a->chunk + 255) / 256) * 4 * 8, st>>>(c);
+      const dim3 gp = DML_LARGE_NODE_FAST ? dim3((unsigned)nL, nchunks) : dim3(nchunks, (unsigned)nL);
+      k_partition_large<<<gp, 256, (size_t)((a->chunk + 255) / 256) * 4 * 8, st>>>(c);
     }
     if (fork) {
       for (int i = 0; i < 3; ++i) {

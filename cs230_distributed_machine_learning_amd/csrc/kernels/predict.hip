@@ -25,6 +25,8 @@ struct PredictArgs {
   int64_t out_pred;      // int32 class id (cls) or float (reg), aligned with rows[]
   int64_t out_proba;     // float [len(rows)][C] or 0
   int64_t F, max_rows;
+  int64_t d;          // features (bins per row actually read)
+  int64_t lds_pitch;  // set by dml_forest_predict: LDS row stride, 0 = no staging
 };
 
 // leaf of U consecutive trees [t0, t0 + u_n) for one row, walked in lock-step: the U
@@ -54,17 +56,45 @@ __device__ __forceinline__ void leaves_u(const NodeRec* __restrict__ nodes, cons
   }
 }
 
+// The block's 256 rows are staged in LDS once (dword stride odd -> a wave whose lanes
+// read the same feature hits distinct banks), so the ~25 bin reads per tree walk are LDS
+// reads and the only vector-memory traffic of the walk is the node-record chain.
+// PredictArgs.lds_pitch = row stride in bytes (multiple of 4, <= ld), 0 = read bins from HBM.
+__device__ __forceinline__ const uint8_t* stage_rows(const PredictArgs& a, uint8_t* xs, int64_t r0, int64_t nr) {
+  const int P = (int)a.lds_pitch, W = P >> 2;
+  const int64_t b0 = (int64_t)blockIdx.x * 256;
+  __shared__ int32_t srow[256];
+  const int64_t i = b0 + threadIdx.x;
+  srow[threadIdx.x] = i < nr ? (GPTR(const int32_t, a.rows))[r0 + i] : -1;
+  __syncthreads();
+  const uint8_t* X = GPTR(const uint8_t, a.Xb);
+  for (int k = threadIdx.x; k < 256 * W; k += 256) {
+    const int r = k / W, w = k - r * W;
+    const int32_t row = srow[r];
+    if (row >= 0) ((uint32_t*)xs)[k] = *(const uint32_t*)(X + (int64_t)row * a.ld + 4 * w);
+  }
+  __syncthreads();
+  return xs + threadIdx.x * P;
+}
+
 template <int MAXC, int kPredU>
 __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
   const int f = blockIdx.y;
   const int32_t* toff = GPTR(const int32_t, a.fit_tree_off);
   const int64_t* roff = GPTR(const int64_t, a.fit_row_off);
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t r0 = roff[f], nr = roff[f + 1] - r0;
-  if (i >= nr) return;
+  if ((int64_t)blockIdx.x * 256 >= nr) return;
+  const uint8_t* xr;
+  if (a.lds_pitch) {
+    xr = stage_rows(a, xs_lds, r0, nr);
+    if (i >= nr) return;
+  } else {
+    if (i >= nr) return;
+    xr = GPTR(const uint8_t, a.Xb) + (int64_t)(GPTR(const int32_t, a.rows))[r0 + i] * a.ld;
+  }
   const int C = (int)a.n_classes;
-  const int32_t row = (GPTR(const int32_t, a.rows))[r0 + i];
-  const uint8_t* xr = GPTR(const uint8_t, a.Xb) + (int64_t)row * a.ld;
   const NodeRec* nodes = GPTR(const NodeRec, a.nodes);
   const double* val = GPTR(const double, a.node_val);
   float p[MAXC];
@@ -109,14 +139,21 @@ __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
 
 template <int kPredU>
 __global__ __launch_bounds__(256) void k_predict_reg(PredictArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
   const int f = blockIdx.y;
   const int32_t* toff = GPTR(const int32_t, a.fit_tree_off);
   const int64_t* roff = GPTR(const int64_t, a.fit_row_off);
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t r0 = roff[f], nr = roff[f + 1] - r0;
-  if (i >= nr) return;
-  const int32_t row = (GPTR(const int32_t, a.rows))[r0 + i];
-  const uint8_t* xr = GPTR(const uint8_t, a.Xb) + (int64_t)row * a.ld;
+  if ((int64_t)blockIdx.x * 256 >= nr) return;
+  const uint8_t* xr;
+  if (a.lds_pitch) {
+    xr = stage_rows(a, xs_lds, r0, nr);
+    if (i >= nr) return;
+  } else {
+    if (i >= nr) return;
+    xr = GPTR(const uint8_t, a.Xb) + (int64_t)(GPTR(const int32_t, a.rows))[r0 + i] * a.ld;
+  }
   const NodeRec* nodes = GPTR(const NodeRec, a.nodes);
   const double* val = GPTR(const double, a.node_val);
   double acc = 0.0;
@@ -245,19 +282,31 @@ __global__ __launch_bounds__(256) void k_refine_split(NodeRec* nodes, int64_t P,
 
 // U trees walked in lock-step per thread (memory-level parallelism of the dependent
 // node-load chains); DML_PRED_U=4/16 select the other widths (A/B)
+// LDS row stride for staged predict rows: whole dwords, odd dword count (conflict-free
+// when the lanes of a wave read the same feature), within the row pitch; 0 disables
+static int64_t predict_pitch(const PredictArgs* a) {
+  static const bool off = getenv("DML_PRED_NO_STAGE") != nullptr;
+  int64_t w = (a->d + 3) / 4;
+  if ((w & 1) == 0) ++w;
+  if (off || a->d <= 0 || 4 * ((a->d + 3) / 4) > a->ld || (a->ld & 3) || 256 * 4 * w > 64 * 1024) return 0;
+  return 4 * w;
+}
+
 template <int U>
 static int launch_predict(PredictArgs* a, hipStream_t st) {
   dim3 grid((unsigned)((a->max_rows + 255) / 256), (unsigned)a->F);
+  a->lds_pitch = predict_pitch(a);
+  const size_t lds = (size_t)a->lds_pitch * 256;
   if (a->is_reg) {
-    k_predict_reg<U><<<grid, 256, 0, st>>>(*a);
+    k_predict_reg<U><<<grid, 256, lds, st>>>(*a);
   } else {
     const int C = (int)a->n_classes;
-    if (C <= 2) k_predict_cls<2, U><<<grid, 256, 0, st>>>(*a);
-    else if (C <= 4) k_predict_cls<4, U><<<grid, 256, 0, st>>>(*a);
-    else if (C <= 8) k_predict_cls<8, U><<<grid, 256, 0, st>>>(*a);
-    else if (C <= 16) k_predict_cls<16, U><<<grid, 256, 0, st>>>(*a);
-    else if (C <= 32) k_predict_cls<32, U><<<grid, 256, 0, st>>>(*a);
-    else if (C <= 64) k_predict_cls<64, U><<<grid, 256, 0, st>>>(*a);
+    if (C <= 2) k_predict_cls<2, U><<<grid, 256, lds, st>>>(*a);
+    else if (C <= 4) k_predict_cls<4, U><<<grid, 256, lds, st>>>(*a);
+    else if (C <= 8) k_predict_cls<8, U><<<grid, 256, lds, st>>>(*a);
+    else if (C <= 16) k_predict_cls<16, U><<<grid, 256, lds, st>>>(*a);
+    else if (C <= 32) k_predict_cls<32, U><<<grid, 256, lds, st>>>(*a);
+    else if (C <= 64) k_predict_cls<64, U><<<grid, 256, lds, st>>>(*a);
     else return 5;
   }
   return hipGetLastError() == hipSuccess ? 0 : 1;

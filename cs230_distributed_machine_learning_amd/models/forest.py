@@ -143,6 +143,42 @@ class ForestFamily(Family):
         pool = (2 * active / rp["min_samples_leaf"] + 1) * (8 + 8 * VC)
         return active * 4 * 2 + pool + active * 24
 
+    def footprint(self, data, rp) -> tuple:
+        """(active rows over the fit's trees, node-pool bound) of one fit -- the
+        quantities the device workspace and node pool are sized from (forest_ops)."""
+        n_train = max(data.train_counts) if getattr(data, "train_counts", None) else data.n
+        if rp["bootstrap"]:
+            lam = rp["lambda"]
+            active = n_train * (1.0 - math.exp(-lam)) * 1.01 + 64   # Poisson(lam) weight > 0
+        else:
+            active = float(n_train)
+        T = rp["n_estimators"]
+        per_tree = 2 * active / max(1, rp["min_samples_leaf"]) + 1
+        if rp["max_depth"] < 40:
+            per_tree = min(per_tree, 2.0 ** (rp["max_depth"] + 1) - 1)
+        return T * active, T * per_tree + T
+
+    def presize(self, data, rps: List[Dict[str, Any]], cands_per_batch: int, n_splits: int) -> None:
+        """Grow the device arena at job setup to the largest batch this job can form
+        (its ``cands_per_batch`` largest candidates x ``n_splits`` splits), so no batch
+        of the job regrows it mid-run.  ``rps``: resolved parameters per candidate."""
+        if not data.is_gpu or not rps:
+            return
+        foot = sorted((self.footprint(data, rp) + (rp["n_estimators"],) for rp in rps), reverse=True)
+        top = foot[:max(1, cands_per_batch)]
+        rows = int(n_splits * sum(f[0] for f in top))
+        pool = int(n_splits * sum(f[1] for f in top)) + 16
+        T = int(n_splits * sum(f[2] for f in top))
+        budget = self._budget(data)
+        ws = forest_ops.workspace_bytes(rows, T, data.d, data.n_classes, not data.classification, self.tiers)
+        VC = data.n_classes if data.classification else 3
+        pb = forest_ops.pool_bytes(pool, VC)
+        if ws + pb > budget:            # such a batch would be split anyway: reserve the budget's share
+            scale = budget / float(ws + pb)
+            ws, pb = int(ws * scale), int(pb * scale)
+        forest_ops.ARENA.reserve(data.device, "ws", ws)
+        forest_ops.ARENA.reserve(data.device, "pool", pb)
+
     def _budget(self, data) -> float:
         if self.hbm_budget_bytes:
             return float(self.hbm_budget_bytes)

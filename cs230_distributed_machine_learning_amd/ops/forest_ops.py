@@ -132,6 +132,27 @@ class _Arena:
             self.busy.add(key)
             return buf
 
+    def reserve(self, dev: torch.device, slot: str, nbytes: int) -> int:
+        """Grow an idle slot to ``nbytes`` now (job setup), so the batches of the job never
+        regrow it mid-run (each regrowth is a multi-GB hipMalloc).  Capped at 70% of
+        what the device can still give; returns the slot's size."""
+        key = (dev.index if dev.index is not None else torch.cuda.current_device(), slot)
+        with self.lock:
+            if key in self.busy:
+                return 0
+            buf = self.bufs.get(key)
+            if buf is not None and buf.numel() >= nbytes:
+                return int(buf.numel())
+            if buf is not None:
+                self.bufs.pop(key)
+                del buf
+                torch.cuda.empty_cache()
+            free, _ = torch.cuda.mem_get_info(dev)
+            spare = free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+            target = int(min(int(nbytes), int(0.7 * spare)))
+            self.bufs[key] = torch.empty(target, dtype=torch.uint8, device=dev)
+            return target
+
     def give(self, dev: torch.device, slot: str) -> None:
         key = (dev.index if dev.index is not None else torch.cuda.current_device(), slot)
         with self.lock:
@@ -154,6 +175,24 @@ class _Arena:
 
 
 ARENA = _Arena()
+
+
+def workspace_bytes(rows_total: int, T: int, d: int, n_classes: int, is_reg: bool,
+                    tiers: "ForestTiers | None" = None) -> int:
+    """Device workspace of a build with ``rows_total`` active rows over ``T`` trees
+    (the C++ planner's own layout, csrc/kernels/forest.hip ``plan``)."""
+    CH = 4 if is_reg else n_classes + 1
+    t = (tiers or ForestTiers()).fitted(CH)
+    a = native.ForestArgs()
+    a.d, a.n_classes, a.is_reg, a.T = d, (n_classes if not is_reg else 1), int(is_reg), T
+    a.rows_total = int(rows_total)
+    a.wave_max, a.block_max, a.chunk = t.wave_max, t.block_max, t.chunk
+    a.kg_wave, a.kg_block, a.kg_large, a.slack_wave, a.sub_max = t.kg_wave, t.kg_block, t.kg_large, t.slack_wave, t.sub_max
+    return int(native.hip_lib().dml_forest_workspace_bytes(ctypes.byref(a)))
+
+
+def pool_bytes(pool_cap: int, VC: int) -> int:
+    return (pool_cap * 8 + 255) // 256 * 256 + pool_cap * VC * 8
 
 
 def _carve(buf: torch.Tensor, off: int, shape, dtype) -> torch.Tensor:
@@ -217,13 +256,13 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
         for _attempt in range(4):
             with trace.range("forest_alloc"):
                 vals_off = (pool_cap * 8 + 255) // 256 * 256
-                pool_bytes = vals_off + pool_cap * VC * 8
+                pbytes = pool_bytes(pool_cap, VC)
                 pbuf = None
                 if reuse_pool:
                     if pool_held:                      # a pool retry may need a bigger slot
                         ARENA.give(dev, "pool")
                         pool_held = False
-                    pbuf = ARENA.take(dev, "pool", pool_bytes)
+                    pbuf = ARENA.take(dev, "pool", pbytes)
                     pool_held = pbuf is not None
                 if pbuf is not None:
                     nodes = _carve(pbuf, 0, (pool_cap, 2), torch.int32)
@@ -360,6 +399,7 @@ def predict(fb: ForestBuild, Xb, fit_tree_off: np.ndarray, fit_row_off: np.ndarr
         p.fit_tree_off, p.fit_row_off, p.rows = native.ptr(toff), native.ptr(roff), native.ptr(rows_t)
         p.out_pred, p.out_proba = native.ptr(out), native.ptr(proba)
         p.F = F
+        p.d = int(Xb.shape[1])
         p.max_rows = int(np.max(np.diff(fit_row_off))) if F else 0
         with trace.range("forest_predict"):
             rc = lib.dml_forest_predict(ctypes.byref(p), native.stream_handle(dev))
