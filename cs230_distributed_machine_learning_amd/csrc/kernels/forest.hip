@@ -252,43 +252,6 @@ template <> struct HT<2> { using T = float; };
 
 __device__ __forceinline__ int hist_planes(int MODE, int CH) { return MODE == 1 ? 1 : CH; }
 
-// the next feature in the node's visiting order (see forest_common.h feature_rank):
-// min over f of rank(f) that is > `last` (or overall min when first).  ~0 if none.
-__device__ __forceinline__ uint64_t wave_next_feature(uint64_t node_key, int d, int lane, uint64_t last,
-                                                      bool first) {
-  uint64_t best = ~0ull;
-  for (int f = lane; f < d; f += 64) {
-    const uint64_t r = feature_rank(node_key, f);
-    if ((first || r > last) && r < best) best = r;
-  }
-  return wave::min_u64(best, lane);
-}
-
-// per-lane cache of the node's feature ranks (features lane + 64 i, i < 4): ranks are
-// hashed once per node instead of once per extracted feature (d <= 256; larger d falls
-// back to wave_next_feature).
-struct RankCache {
-  uint64_t r[4];
-  bool cached;
-  __device__ __forceinline__ void build(uint64_t node_key, int d, int lane) {
-    cached = d <= 256;
-    if (!cached) return;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = lane + 64 * i;
-      r[i] = f < d ? feature_rank(node_key, f) : ~0ull;
-    }
-  }
-  __device__ __forceinline__ uint64_t next(uint64_t node_key, int d, int lane, uint64_t last, bool first) const {
-    if (!cached) return wave_next_feature(node_key, d, lane, last, first);
-    uint64_t best = ~0ull;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if ((first || r[i] > last) && r[i] < best) best = r[i];
-    return wave::min_u64(best, lane);
-  }
-};
-
 template <typename CT>
 __device__ __forceinline__ void scan256(CT* p, int lane) {
   CT v0 = p[4 * lane], v1 = p[4 * lane + 1], v2 = p[4 * lane + 2], v3 = p[4 * lane + 3];
@@ -689,8 +652,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     sc->nonconst = 0; sc->pos = 0; sc->first = 1; sc->last = 0; sc->best_j = -1;
     sc->W = c.tree_W[on.tree];
   }
-  RankCache rc;
-  if (wid == 0) rc.build(on.key, d, lane);
+  const FeatPerm fp = feat_perm(on.key, d);   // node's feature visiting order (forest_common.h)
   const uint32_t* rows = c.rows_cur + on.start;
   const float* ty = tree_y(c, s);
   const int cnt = on.count;
@@ -720,16 +682,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     const int pos = sc->pos, nonconst = sc->nonconst;
     if (nonconst >= k || pos >= d) break;
     const int g = min(KG, min(k - nonconst + slack, d - pos));
-    if (wid == 0) {
-      uint64_t last = sc->last;
-      bool first = sc->first != 0;
-      for (int j = 0; j < g; ++j) {
-        last = rc.next(on.key, d, lane, last, first);
-        first = false;
-        if (lane == 0) feats[j] = (int16_t)(uint32_t)last;
-      }
-      if (lane == 0) { sc->last = last; sc->first = 0; }
-    }
+    if (tid < g) feats[tid] = (int16_t)feature_at(fp, pos + tid, d);   // one visiting position per lane
     __syncthreads();
     PH(1)
     if (!reg_rows && RPT == 1) {
@@ -1081,12 +1034,9 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     const int cnt = __popcll(e.mask);
     int nonconst = 0, best_f = -1, best_b = -1;
     double best_g = -INFINITY;
-    uint64_t last = 0;
-    RankCache rc;
-    rc.build(e.key, d, lane);
+    const FeatPerm fp = feat_perm(e.key, d);
     for (int pos = 0; nonconst < s.max_features && pos < d; ++pos) {
-      last = rc.next(e.key, d, lane, last, pos == 0);
-      const int f = (int)(uint32_t)last;
+      const int f = feature_at(fp, pos, d);
       const int my_bin = cache ? xc[lane * dp + f] : (lane < cnt0 ? xg[f] : 0);
       double g;
       int bb;
@@ -1171,15 +1121,12 @@ __global__ __launch_bounds__(64) void k_large_prep(Ctx c, int set_cur, int nL) {
   const TreeSpec& s = c.specs[st.on.tree];
   int16_t* feats = c.lperm + (int64_t)slot * c.d;
   st.g = min(c.kg_large, min(s.max_features, c.d));
-  uint64_t last = 0;
-  for (int j = 0; j < st.g; ++j) {
-    last = wave_next_feature(st.on.key, c.d, lane, last, j == 0);
-    if (lane == 0) feats[j] = (int16_t)(uint32_t)last;
-  }
+  const FeatPerm fp = feat_perm(st.on.key, c.d);
+  for (int j = lane; j < st.g; j += 64) feats[j] = (int16_t)feature_at(fp, j, c.d);
   if (lane != 0) return;
   st.pos = 0; st.nonconst = 0; st.done = 0; st.best_feat = -1; st.best_bin = -1; st.split = 0; st.nl = 0;
   st.best_gain = -INFINITY;
-  st.last = last;
+  st.last = 0;
   c.lstate[slot] = st;
   c.lcursor[2 * slot] = 0;
   c.lcursor[2 * slot + 1] = 0;
@@ -1303,13 +1250,9 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
     if (wid == 0) {
       const int g2 = min(c.kg_large, min(s.max_features - st.nonconst, c.d - st.pos));
       int16_t* perm = c.lperm + (int64_t)slot * c.d;
-      uint64_t last = st.last;
-      for (int j = 0; j < g2; ++j) {
-        last = wave_next_feature(st.on.key, c.d, lane, last, false);
-        if (lane == 0) perm[st.pos + j] = (int16_t)(uint32_t)last;
-      }
+      const FeatPerm fp = feat_perm(st.on.key, c.d);
+      for (int j = lane; j < g2; j += 64) perm[st.pos + j] = (int16_t)feature_at(fp, st.pos + j, c.d);
       if (lane == 0) {
-        st.last = last;
         st.g = g2;
         atomicOr(&c.counters[kNeedMore], 1);
       }

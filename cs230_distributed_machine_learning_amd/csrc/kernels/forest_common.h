@@ -95,14 +95,46 @@ DML_HD uint64_t child_key(uint64_t parent, int side) {
   return splitmix64(parent * 0x9E3779B97F4A7C15ull + 0x51ED27ull + (uint64_t)side);
 }
 
-// Per-node feature visiting order: features sorted by (hash(node_key, f), f).  iid
-// 32-bit keys give a uniformly random permutation (sklearn draws a random order too),
-// and the GPU can pull "the next feature" with one wave-wide min-reduction instead of
-// a serial Fisher-Yates walk over an LDS array.
-DML_HD uint32_t feature_key(uint64_t node_key, int f) { return hash_u32(node_key, 0xFEA7ull + (uint64_t)f); }
+// Per-node feature visiting order: a keyed pseudo-random permutation of [0, d) that is
+// evaluated POSITION BY POSITION -- feature_at(key, k, d) is the k-th feature visited --
+// so a GPU lane can compute its own position's feature with no wave-wide min-search
+// (each lane of a wave takes one position; sklearn draws a random order too).  The
+// permutation is a 3-round keyed bijection on [0, 2^b) (odd multiply + add, xor-shift:
+// each step is invertible mod 2^b) restricted to [0, d) by cycle walking.
+struct FeatPerm {
+  uint32_t m1, a1, m2, a2, m3, a3, mask, sh;
+};
 
-DML_HD uint64_t feature_rank(uint64_t node_key, int f) {
-  return ((uint64_t)feature_key(node_key, f) << 32) | (uint32_t)f;
+DML_HD FeatPerm feat_perm(uint64_t node_key, int d) {
+  FeatPerm p;
+  int b = 1;
+  while ((1 << b) < d) ++b;
+  p.mask = (1u << b) - 1u;
+  p.sh = (uint32_t)((b + 1) >> 1);
+  const uint64_t h1 = splitmix64(node_key ^ 0xFEA7FEA7ull), h2 = splitmix64(h1);
+  const uint64_t h3 = splitmix64(h2);
+  p.m1 = ((uint32_t)h1 | 1u) & p.mask; p.a1 = (uint32_t)(h1 >> 32) & p.mask;
+  p.m2 = ((uint32_t)h2 | 1u) & p.mask; p.a2 = (uint32_t)(h2 >> 32) & p.mask;
+  p.m3 = ((uint32_t)h3 | 1u) & p.mask; p.a3 = (uint32_t)(h3 >> 32) & p.mask;
+  if (p.mask == 1u) { p.m1 = p.m2 = p.m3 = 1u; }
+  return p;
+}
+
+DML_HD uint32_t feat_perm_step(const FeatPerm& p, uint32_t x) {
+  x = (x * p.m1 + p.a1) & p.mask;
+  x ^= x >> p.sh;
+  x = (x * p.m2 + p.a2) & p.mask;
+  x ^= x >> p.sh;
+  x = (x * p.m3 + p.a3) & p.mask;
+  x ^= x >> p.sh;
+  return x;
+}
+
+// k-th feature of the node's visiting order (k < d)
+DML_HD int feature_at(const FeatPerm& p, int k, int d) {
+  uint32_t x = feat_perm_step(p, (uint32_t)k);
+  while (x >= (uint32_t)d) x = feat_perm_step(p, x);   // cycle walk: stays a permutation of [0, d)
+  return (int)x;
 }
 
 // binary classification: (w class0, w class1, rows) packed in one u64 so a histogram

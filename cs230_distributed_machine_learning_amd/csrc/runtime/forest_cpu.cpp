@@ -83,18 +83,16 @@ static void build_tree(const Data& D, const TreeSpec& s, CpuTree& out) {
   const int CH = D.CH;
   std::vector<uint32_t> hu((size_t)CH * 256);
   std::vector<float> hf((size_t)CH * 256);
-  std::vector<uint64_t> rank(D.d);
   std::vector<double> best_left(CH), cand_left(CH);
   while (!stack.empty()) {
     Job jb = stack.back();
     stack.pop_back();
-    for (int f = 0; f < D.d; ++f) rank[f] = feature_rank(jb.key, f);
-    std::sort(rank.begin(), rank.end());
+    const FeatPerm fp = feat_perm(jb.key, D.d);
     int pos = 0, nonconst = 0, best_feat = -1, best_bin = -1;
     double best_gain = -INFINITY;
     const uint32_t* nr = rows.data() + jb.start;
     while (nonconst < s.max_features && pos < D.d) {
-      const int f = (int)(uint32_t)rank[pos];
+      const int f = feature_at(fp, pos, D.d);
       ++pos;
       double g_best = -INFINITY;
       int b_best = -1;
