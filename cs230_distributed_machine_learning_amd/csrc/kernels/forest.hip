@@ -49,6 +49,9 @@
 #ifndef DML_KGMAX_WAVE
 #define DML_KGMAX_WAVE 4
 #endif
+#ifndef DML_WAVE_PREFETCH
+#define DML_WAVE_PREFETCH 12   // wave tier: visiting positions whose bins are gathered up front
+#endif
 // large-tier grids: node index fastest (1) so chunk c of EVERY large node is in flight at
 // once -- at the top levels the rows behind chunk c of all trees of a fold are nearly the
 // same rows, so those table lines are served from the XCD's L2 -- or chunk fastest (0)
@@ -678,6 +681,32 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   PH(0)
   const int k = s.max_features;
   uint32_t pk[KGMAX];   // register rows: the group's bins packed 4 x u8 per feature (live across eval)
+  // wave tier, register rows: the bins of the first KPRE visiting positions are gathered
+  // ONCE, all in flight together, before the first feature group -- the later groups
+  // (KG histograms at a time fit LDS) then start without another gather round trip
+  constexpr int KPRE = (NT == 64 && RPT == 4) ? DML_WAVE_PREFETCH : 0;
+  uint32_t pre[KPRE > 0 ? KPRE : 1];
+  int npre = 0;
+  if constexpr (KPRE > 0) {
+    if (reg_rows) {
+      npre = min(KPRE, min(k + slack, d));
+      uint32_t raw[KPRE][RPT];
+#pragma unroll
+      for (int q = 0; q < KPRE; ++q) {
+        const int64_t f = q < npre ? feature_at(fp, q, d) : 0;
+#pragma unroll
+        for (int u = 0; u < RPT; ++u)
+          raw[q][u] = (q < npre && rrow[u] != 0xFFFFFFFFu) ? (uint32_t)c.Xb[(int64_t)(rrow[u] & c.rmask) * c.ld + f] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < KPRE; ++q) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) v |= raw[q][u] << (8 * u);
+        pre[q] = v;
+      }
+    }
+  }
   while (true) {
     const int pos = sc->pos, nonconst = sc->nonconst;
     if (nonconst >= k || pos >= d) break;
@@ -685,6 +714,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     if (tid < g) feats[tid] = (int16_t)feature_at(fp, pos + tid, d);   // one visiting position per lane
     __syncthreads();
     PH(1)
+    if (KPRE > 0 && reg_rows && pos + g <= npre) {
+      // prefetched group: histogram atomics straight from the packed register bins
+#pragma unroll
+      for (int q = 0; q < (KPRE > 0 ? KPRE : 1); ++q) {
+        if (q >= pos && q < pos + g) {
+          CT* hj = hist + (q - pos) * span;
+#pragma unroll
+          for (int u = 0; u < RPT; ++u)
+            if (rrow[u] != 0xFFFFFFFFu) hist_add<MODE>(hj, c, (int)((pre[q] >> (8 * u)) & 0xFFu), rpl[u]);
+        }
+      }
+    } else
     if (!reg_rows && RPT == 1) {
       // large node, one row per thread per NT-row chunk: 2-deep software pipeline -- the
       // next chunk's payload/bin loads and the row ids two chunks ahead are in flight while
@@ -782,9 +823,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     if (reg_rows) {
       const int bj = sc->best_j;
       uint32_t sel = 0;
+      if (KPRE > 0 && pos + g <= npre) {
 #pragma unroll
-      for (int j = 0; j < KGMAX; ++j)
-        if (j == bj) sel = pk[j];
+        for (int q = 0; q < (KPRE > 0 ? KPRE : 1); ++q)
+          if (q == pos + bj) sel = pre[q];
+      } else {
+#pragma unroll
+        for (int j = 0; j < KGMAX; ++j)
+          if (j == bj) sel = pk[j];
+      }
       if (bj >= 0)
 #pragma unroll
         for (int u = 0; u < RPT; ++u) rbin[u] = (sel >> (8 * u)) & 0xFFu;
@@ -967,6 +1014,119 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
   bin = bl < 64 ? bsel : -1;
 }
 
+// ---- segmented evaluation of small subtree nodes (classification) -------------------
+// A node with cnt <= WD rows (WD = 8/16/32) is evaluated on 64 / WD features at once: the
+// wave is cut into WD-lane segments, each segment holds the node's rows compacted into
+// its first cnt lanes and evaluates one feature of the node's visiting order (in-segment
+// bitonic sort, segment-relative prefix sums, in-segment argmax).  The candidates, their
+// scores and the tie-break (lowest bin, then visiting order) are exactly those of the
+// one-feature-per-wave path, so the split found is identical -- most subtree nodes are
+// tiny, and this replaces 64-lane sorts of 2-8 valid rows.
+template <int WD>
+__device__ __forceinline__ uint32_t bitonic_seg(uint32_t key, int j, int lane) {
+#define DML_SEG_STEP(K, J)                                      \
+  {                                                             \
+    const uint32_t other = wave::xor32<J>(key, lane);           \
+    const bool up = (K) == WD ? true : ((j & (K)) == 0);        \
+    const bool lower = (j & (J)) == 0;                          \
+    const uint32_t mn = key < other ? key : other;              \
+    const uint32_t mx = key < other ? other : key;              \
+    key = (lower == up) ? mn : mx;                              \
+  }
+  DML_SEG_STEP(2, 1)
+  DML_SEG_STEP(4, 2) DML_SEG_STEP(4, 1)
+  DML_SEG_STEP(8, 4) DML_SEG_STEP(8, 2) DML_SEG_STEP(8, 1)
+  if constexpr (WD >= 16) { DML_SEG_STEP(16, 8) DML_SEG_STEP(16, 4) DML_SEG_STEP(16, 2) DML_SEG_STEP(16, 1) }
+  if constexpr (WD >= 32) {
+    DML_SEG_STEP(32, 16) DML_SEG_STEP(32, 8) DML_SEG_STEP(32, 4) DML_SEG_STEP(32, 2) DML_SEG_STEP(32, 1)
+  }
+#undef DML_SEG_STEP
+  return key;
+}
+
+template <int WD>
+__device__ __forceinline__ void argmax_seg(double& g, int& idx, int lane) {
+#define DML_SEG_ARG(M)                                               \
+  {                                                                  \
+    const double og = wave::shfl_xor<M>(g, lane);                    \
+    const int oi = wave::shfl_xor<M>(idx, lane);                     \
+    if (og > g || (og == g && (unsigned)oi < (unsigned)idx)) {       \
+      g = og;                                                        \
+      idx = oi;                                                      \
+    }                                                                \
+  }
+  if constexpr (WD >= 32) DML_SEG_ARG(16)
+  if constexpr (WD >= 16) DML_SEG_ARG(8)
+  DML_SEG_ARG(4) DML_SEG_ARG(2) DML_SEG_ARG(1)
+#undef DML_SEG_ARG
+}
+
+// evaluates the node whose rows are the compact indices [0, cnt) (src lane of compact
+// row j: `src`); updates the running (nonconst, best) in visiting order exactly like the
+// per-feature loop.  xc: LDS row-bin cache (stride dp); cls_j / w_j: class and weight of
+// compact row j (valid in every segment's lane j).
+template <int WD>
+__device__ void sub_node_seg(const Ctx& c, const TreeSpec& s, const FeatPerm& fp, int cnt, int lane, int src,
+                             int cls_j, uint32_t w_j, const uint8_t* xc, int dp, int& nonconst, double& best_g,
+                             int& best_f, int& best_b) {
+  constexpr int S = 64 / WD;
+  const int d = c.d;
+  const int seg = lane / WD, j = lane & (WD - 1);
+  const bool valid_row = j < cnt;
+  for (int pos = 0; nonconst < s.max_features && pos < d; pos += S) {
+    const bool has_f = pos + seg < d;
+    const int f = has_f ? feature_at(fp, pos + seg, d) : 0;
+    const int my_bin = (valid_row && has_f) ? (int)xc[src * dp + f] : 0;
+    const uint32_t key = valid_row ? ((uint32_t)my_bin << 6) | (uint32_t)j : 0xFFFFFFFFu;
+    const uint32_t sk = bitonic_seg<WD>(key, j, lane);
+    const int jj = (int)(sk & 63u);
+    const int b = valid_row ? (int)(sk >> 6) : 1024;
+    const int bnext = wave::shift_down1<int>(b, lane, 1024);
+    // class / weight of the sorted row (compact row jj lives in lane seg*WD + jj of every segment)
+    const int srcl = seg * WD + (valid_row ? jj : 0);
+    const int ycls = __shfl(cls_j, srcl);
+    const uint32_t wsh = (uint32_t)__shfl((int)w_j, srcl);
+    const uint32_t w = valid_row ? wsh : 0u;
+    const bool cand = valid_row && j < cnt - 1 && b != bnext && j + 1 >= s.min_samples_leaf &&
+                      cnt - j - 1 >= s.min_samples_leaf;
+    const bool ncl = valid_row && j < cnt - 1 && b != bnext;
+    ClsAcc L, R;
+    L.init(s.criterion); R.init(s.criterion);
+    for (int k = 0; k < c.C; ++k) {
+      const uint32_t v = (ycls == k) ? w : 0u;
+      uint32_t pre = wave::incl_scan<uint32_t>(v);
+      // segment-relative: subtract the inclusive total of the preceding segments
+      uint32_t base = 0, tot = 0;
+#pragma unroll
+      for (int q = 0; q < S; ++q) {
+        const uint32_t bq = q ? (uint32_t)__builtin_amdgcn_readlane((int)pre, q * WD - 1) : 0u;
+        const uint32_t eq = (uint32_t)__builtin_amdgcn_readlane((int)pre, q * WD + cnt - 1);
+        if (seg == q) { base = bq; tot = eq - bq; }
+      }
+      pre -= base;
+      L.add((double)pre);
+      R.add((double)(tot - pre));
+    }
+    double g = cand ? cls_proxy(L, R, s.criterion) : -INFINITY;
+    int bl = cand ? j : 64;
+    argmax_seg<WD>(g, bl, lane);
+    const int bsel = __shfl(b, seg * WD + (bl & (WD - 1)));
+    const uint64_t ncm = __ballot(ncl);
+    // serial selection over the S evaluated features, in visiting order
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+      if (pos + q >= d || nonconst >= s.max_features) break;
+      const bool nc = ((ncm >> (q * WD)) & ((WD == 64 ? ~0ull : ((1ull << WD) - 1ull)))) != 0ull;
+      if (!nc) continue;
+      ++nonconst;
+      const double gq = wave::bcast<double>(g, q * WD);
+      const int blq = wave::bcast<int>(bl, q * WD);
+      const int bq = wave::bcast<int>(bsel, q * WD);
+      if (blq < 64 && gq > best_g) { best_g = gq; best_f = feature_at(fp, pos + q, d); best_b = bq; }
+    }
+  }
+}
+
 template <bool REG>
 __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -984,6 +1144,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   double* left_ch = sstats + 64 * VC;                // [VC]
   double* right_ch = left_ch + VC;                   // [VC] (+ pad)
   uint8_t* xc = (uint8_t*)(left_ch + ((2 * VC + 1) & ~1));
+  int32_t* cidx = (int32_t*)(xc + ((64 * c.sub_cache_d + 15) & ~15));   // [64] compaction map
   const int cnt0 = on.count;
   const uint32_t* rows = c.rows_cur + on.start;
   uint32_t row = 0;
@@ -1035,6 +1196,20 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     int nonconst = 0, best_f = -1, best_b = -1;
     double best_g = -INFINITY;
     const FeatPerm fp = feat_perm(e.key, d);
+    if (!REG && cache && cnt <= 32) {
+      // compact the node's rows: compact row j <- lane of the j-th set bit of the mask
+      const bool in = (e.mask >> lane) & 1ull;
+      if (in) cidx[lane_prefix(e.mask)] = lane;
+      wave_lds_sync();
+      const int jx = cnt <= 8 ? (lane & 7) : (cnt <= 16 ? (lane & 15) : (lane & 31));
+      const int src = jx < cnt ? cidx[jx] : 0;
+      const int cls_j = __shfl(my_cls, src);
+      const uint32_t w_j = (uint32_t)__shfl((int)(uint32_t)my_w, src);
+      if (cnt <= 8) sub_node_seg<8>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b);
+      else if (cnt <= 16) sub_node_seg<16>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b);
+      else sub_node_seg<32>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b);
+      wave_lds_sync();   // cidx is rewritten by the next node
+    } else
     for (int pos = 0; nonconst < s.max_features && pos < d; ++pos) {
       const int f = feature_at(fp, pos, d);
       const int my_bin = cache ? xc[lane * dp + f] : (lane < cnt0 ? xg[f] : 0);
@@ -1495,7 +1670,7 @@ static size_t fused_lds(const ForestArgs* a, int KG) {
 static size_t sub_lds(const ForestArgs* a) {
   const int VC = a->is_reg ? 3 : (int)a->n_classes;
   size_t b = 64 * sizeof(SubEntry) + (size_t)64 * VC * 8 + ((2 * VC + 1) & ~1) * 8;
-  b += (size_t)64 * a->sub_cache_d + 16;
+  b += (size_t)((64 * a->sub_cache_d + 15) & ~15) + 64 * 4 + 16;   // row-bin cache + compaction map
   return b;
 }
 
