@@ -159,6 +159,11 @@ struct Ctx {
   // no kernel re-gathers ycls or re-hashes the bootstrap weight); else plain row ids
   uint32_t rmask;
   int32_t rbits, packed;
+  // block tier, streamed nodes: the feature group's bins of every row, 16 B per row
+  // position (positions of rows_cur), written by the histogram pass so the partition
+  // reads the split feature's bin with 16-B-strided coalesced loads instead of
+  // re-gathering a 128-B table line per row
+  uint8_t* bscr;
 };
 
 // target vector of a tree (shared y, or its own row of the boosting target matrix)
@@ -749,6 +754,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
           b1[j] = (j < g && r1 != INV) ? (uint32_t)c.Xb[(int64_t)(r1 & c.rmask) * c.ld + fj[j]] : 0u;
         const uint32_t r2 = row_at(base + 2 * NT + tid);
         if (r0 != INV) {
+          if constexpr (NT == 256 && KGMAX == 16) {
+            uint4 v;
+            v.x = b0[0] | b0[1] << 8 | b0[2] << 16 | b0[3] << 24;
+            v.y = b0[4] | b0[5] << 8 | b0[6] << 16 | b0[7] << 24;
+            v.z = b0[8] | b0[9] << 8 | b0[10] << 16 | b0[11] << 24;
+            v.w = b0[12] | b0[13] << 8 | b0[14] << 16 | b0[15] << 24;
+            *(uint4*)(c.bscr + (on.start + base + tid) * 16) = v;
+          }
 #pragma unroll
           for (int j = 0; j < KGMAX; ++j)
             if (j < g) hist_add<MODE>(hist + j * span, c, (int)b0[j], pl0);
@@ -879,17 +892,24 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   // ids two chunks ahead are prefetched while the current chunk is ranked and written
   constexpr uint32_t INVR = 0xFFFFFFFFu;
   auto prow = [&](int r) -> uint32_t { return r < cnt ? rows[r] : INVR; };
-  auto pbin = [&](uint32_t r) -> uint32_t { return r != INVR ? (uint32_t)c.Xb[(int64_t)(r & c.rmask) * c.ld + feat] : 0u; };
+  // the split feature's bin at row position p: from the histogram pass's scratch when the
+  // final feature group (the one the scratch holds) produced the best split, else gathered
+  const int bj_scr = (NT == 256 && KGMAX == 16 && !reg_rows) ? sc->best_j : -1;
+  auto pbin = [&](int p, uint32_t r) -> uint32_t {
+    if (r == INVR) return 0u;
+    if (bj_scr >= 0) return (uint32_t)c.bscr[(on.start + p) * 16 + bj_scr];
+    return (uint32_t)c.Xb[(int64_t)(r & c.rmask) * c.ld + feat];
+  };
   uint32_t nrow = INVR, nbin = 0, frow = INVR;
   if (!reg_rows && RPT == 1) {
     rrow[0] = prow(tid);
-    rbin[0] = pbin(rrow[0]);
+    rbin[0] = pbin(tid, rrow[0]);
     nrow = prow(NT + tid);
   }
   for (int cb = 0; cb < cnt; cb += NT * RPT) {
     if (!reg_rows) {
       if constexpr (RPT == 1) {
-        nbin = pbin(nrow);
+        nbin = pbin(cb + NT + tid, nrow);
         frow = prow(cb + 2 * NT + tid);
       } else {
         load_rows(cb);
@@ -1625,7 +1645,7 @@ __global__ void k_roots(Ctx c) {
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct Layout {
-  size_t rows_b, open[2][kTiers], counters, cursors, lstate, lperm, lbest, ghist, lcursor, total;
+  size_t rows_b, open[2][kTiers], counters, cursors, lstate, lperm, lbest, ghist, lcursor, bscr, total;
   int64_t open_cap[kTiers], large_cap;
 };
 
@@ -1652,6 +1672,7 @@ static Layout plan(const ForestArgs* a) {
   L.lbest = take((size_t)L.large_cap * CH * 8);
   L.ghist = take((size_t)L.large_cap * a->kg_large * CH * 256 * 4);
   L.lcursor = take((size_t)L.large_cap * 8);
+  L.bscr = take((size_t)R * 16);
   L.total = off;
   return L;
 }
@@ -1699,6 +1720,7 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.lbest_left = (double*)(ws + L.lbest);
   c.ghist = (void*)(ws + L.ghist);
   c.lcursor = (int32_t*)(ws + L.lcursor);
+  c.bscr = ws + L.bscr;
   c.large_cap = L.large_cap;
   c.wave_max = (int)a->wave_max; c.block_max = (int)a->block_max; c.chunk = (int)a->chunk;
   c.kg_wave = (int)a->kg_wave; c.kg_block = (int)a->kg_block; c.kg_large = (int)a->kg_large;
