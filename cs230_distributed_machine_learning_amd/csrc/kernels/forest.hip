@@ -121,7 +121,8 @@ struct LState {
   int32_t pos, nonconst, g, done;
   int32_t best_feat, best_bin, split, nl;
   double best_gain;
-  uint64_t last;   // rank of the last feature taken from the visiting order
+  int32_t best_j;  // index of the best feature in the LAST round's group (its bins are in Ctx::bscr), else -1
+  int32_t pad_;
 };
 
 struct Ctx {
@@ -474,7 +475,8 @@ __device__ __forceinline__ void hist_add_row(typename HT<MODE>::T* hist, const C
 // serial selection over an evaluated group, in visiting order (thread 0)
 __device__ void select_group(const Ctx& c, const TreeSpec& s, const int16_t* feats, int g, const double* rg,
                              const int* rb, const int* rn, const double* rleft, double* best_left, int& nonconst,
-                             double& best_gain, int& best_feat, int& best_bin) {
+                             double& best_gain, int& best_feat, int& best_bin, int& upd_j) {
+  upd_j = -1;
   for (int j = 0; j < g; ++j) {
     if (!rn[j]) continue;
     ++nonconst;
@@ -482,6 +484,7 @@ __device__ void select_group(const Ctx& c, const TreeSpec& s, const int16_t* fea
       best_gain = rg[j];
       best_feat = feats[j];
       best_bin = rb[j];
+      upd_j = j;
       for (int ch = 0; ch < c.CH; ++ch) best_left[ch] = rleft[j * c.CH + ch];
     }
     if (nonconst >= s.max_features) break;
@@ -1321,7 +1324,7 @@ __global__ __launch_bounds__(64) void k_large_prep(Ctx c, int set_cur, int nL) {
   if (lane != 0) return;
   st.pos = 0; st.nonconst = 0; st.done = 0; st.best_feat = -1; st.best_bin = -1; st.split = 0; st.nl = 0;
   st.best_gain = -INFINITY;
-  st.last = 0;
+  st.best_j = -1;
   c.lstate[slot] = st;
   c.lcursor[2 * slot] = 0;
   c.lcursor[2 * slot + 1] = 0;
@@ -1369,6 +1372,14 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
 #pragma unroll
       for (int j = 0; j < KGL; ++j) bb[j] = (j < g && rbn != INV) ? (uint32_t)c.Xb[(int64_t)(rbn & c.rmask) * c.ld + fj[j]] : 0u;
       const uint32_t rc2 = row_at(r + 512);
+      if (ra != INV) {   // the group's bins of this row position for the partition (Ctx::bscr)
+        uint4 v;
+        v.x = ba[0] | ba[1] << 8 | ba[2] << 16 | ba[3] << 24;
+        v.y = ba[4] | ba[5] << 8 | ba[6] << 16 | ba[7] << 24;
+        v.z = ba[8] | ba[9] << 8 | ba[10] << 16 | ba[11] << 24;
+        v.w = ba[12] | ba[13] << 8 | ba[14] << 16 | ba[15] << 24;
+        *(uint4*)(c.bscr + (st.on.start + r) * 16) = v;
+      }
 #pragma unroll
       for (int j = 0; j < KGL; ++j)
         if (j < g) hist_add<MODE>(hist + j * span, c, (int)ba[j], pa);
@@ -1434,8 +1445,12 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   if (tid == 0) {
     int nc = st.nonconst, bf = st.best_feat, bbin = st.best_bin;
     double bg = st.best_gain;
-    select_group(c, s, feats, g, rg, rb, rn, rleft, best_left, nc, bg, bf, bbin);
+    int uj;
+    select_group(c, s, feats, g, rg, rb, rn, rleft, best_left, nc, bg, bf, bbin, uj);
     st.nonconst = nc; st.best_gain = bg; st.best_feat = bf; st.best_bin = bbin;
+    // this round's scratch holds the best feature's bins only if it was updated now (and the
+    // histogram pass took the <= 16-feature path that writes the scratch)
+    st.best_j = g <= 16 ? uj : -1;
     st.pos += g;
     need_more = (st.nonconst < s.max_features && st.pos < c.d) ? 1 : 0;
   }
@@ -1488,14 +1503,21 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr uint32_t INV = 0xFFFFFFFFu;
   auto row_at = [&](int r) -> uint32_t { return r < r1 ? rows[r] : INV; };
-  auto bin_of = [&](uint32_t row) -> int { return row != INV ? (int)c.Xb[(int64_t)(row & c.rmask) * c.ld + feat] : 0; };
+  // split bin at row position p: from the histogram pass's scratch if the final round's
+  // group produced the best split (st.best_j >= 0), else gathered from the table
+  const int bj = st.best_j;
+  auto bin_of = [&](int p, uint32_t row) -> int {
+    if (row == INV) return 0;
+    if (bj >= 0) return (int)c.bscr[(st.on.start + p) * 16 + bj];
+    return (int)c.Xb[(int64_t)(row & c.rmask) * c.ld + feat];
+  };
   int myL = 0;
   {
     uint32_t ra = row_at(r0 + tid);
-    int ba = bin_of(ra);
+    int ba = bin_of(r0 + tid, ra);
     uint32_t rbn = row_at(r0 + tid + 256);
     for (int t0 = r0; t0 < r1; t0 += 256) {
-      const int bb = bin_of(rbn);
+      const int bb = bin_of(t0 + 256 + tid, rbn);
       const uint32_t rc2 = row_at(t0 + 512 + tid);
       const bool left = ra != INV && ba <= bin;
       const uint64_t ml = __ballot(left);
