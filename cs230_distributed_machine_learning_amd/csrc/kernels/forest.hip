@@ -121,8 +121,8 @@ struct LState {
   int32_t pos, nonconst, g, done;
   int32_t best_feat, best_bin, split, nl;
   double best_gain;
-  int32_t best_j;  // index of the best feature in the LAST round's group (its bins are in Ctx::bscr), else -1
-  int32_t pad_;
+  int32_t best_pos; // visiting position of the best split's feature
+  int32_t scr_n;    // positions [0, scr_n) have their bins in Ctx::bscr (round 0, <= 16 features)
 };
 
 struct Ctx {
@@ -518,6 +518,8 @@ struct Scratch {
   double best_gain;
   double W;                 // tree weight (prefetched)
   int32_t best_feat, best_bin, nonconst, pos, first, base, nl, best_j;
+  int32_t best_pos;         // visiting position of the best split's feature
+  int32_t scr_n;            // streamed nodes: positions [0, scr_n) have their bins in Ctx::bscr
   int32_t wcnt[32];         // partition: [2][RPT][NW] per-wave counts
 };
 
@@ -661,6 +663,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   if (tid == 0) {
     sc->best_gain = -INFINITY; sc->best_feat = -1; sc->best_bin = -1;
     sc->nonconst = 0; sc->pos = 0; sc->first = 1; sc->last = 0; sc->best_j = -1;
+    sc->best_pos = 1 << 30; sc->scr_n = 0;
     sc->W = c.tree_W[on.tree];
   }
   const FeatPerm fp = feat_perm(on.key, d);   // node's feature visiting order (forest_common.h)
@@ -757,7 +760,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
           b1[j] = (j < g && r1 != INV) ? (uint32_t)c.Xb[(int64_t)(r1 & c.rmask) * c.ld + fj[j]] : 0u;
         const uint32_t r2 = row_at(base + 2 * NT + tid);
         if (r0 != INV) {
-          if constexpr (NT == 256 && KGMAX == 16) {
+          if (NT == 256 && KGMAX == 16 && pos == 0) {
             uint4 v;
             v.x = b0[0] | b0[1] << 8 | b0[2] << 16 | b0[3] << 24;
             v.y = b0[4] | b0[5] << 8 | b0[6] << 16 | b0[7] << 24;
@@ -796,6 +799,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
             if (rrow[u] != 0xFFFFFFFFu) hist_add<MODE>(hj, c, (int)bins[j][u], rpl[u]);
         }
       }
+      if (NT == 64 && !reg_rows && pos < 16) {
+        // streamed wave-tier node: this group's bins at byte (visiting position) of the slot
+#pragma unroll
+        for (int u = 0; u < RPT; ++u)
+          if (rrow[u] != 0xFFFFFFFFu) {
+            uint8_t* slot = c.bscr + (on.start + base + tid + NT * u) * 16;
+#pragma unroll
+            for (int j = 0; j < KGMAX; ++j)
+              if (j < g && pos + j < 16) slot[pos + j] = (uint8_t)bins[j][u];
+          }
+      }
       if (reg_rows) {
 #pragma unroll
         for (int j = 0; j < KGMAX; ++j)
@@ -828,8 +842,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
       const bool upd = jj < 64 && gj > sc->best_gain;
       if (upd && lane < c.CH) best_left[lane] = rleft[jj * c.CH + lane];
       if (lane == 0) {
-        if (upd) { sc->best_gain = gj; sc->best_feat = feats[jj]; sc->best_bin = rb[jj]; }
+        if (upd) { sc->best_gain = gj; sc->best_feat = feats[jj]; sc->best_bin = rb[jj]; sc->best_pos = pos + jj; }
         sc->best_j = upd ? jj : -1;
+        // bscr slots: byte q of a row's 16-B slot = visiting position q (written by the
+        // streamed histogram passes: the block tier's first group, the wave tier's groups)
+        if (!reg_rows) sc->scr_n = NT == 256 ? (pos == 0 ? min(g, 16) : sc->scr_n) : min(16, pos + g);
         sc->nonconst = min(nc0 + __popcll(m), k);
         sc->pos = pos + g;
       }
@@ -897,7 +914,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   auto prow = [&](int r) -> uint32_t { return r < cnt ? rows[r] : INVR; };
   // the split feature's bin at row position p: from the histogram pass's scratch when the
   // final feature group (the one the scratch holds) produced the best split, else gathered
-  const int bj_scr = (NT == 256 && KGMAX == 16 && !reg_rows) ? sc->best_j : -1;
+  const int bj_scr = (!reg_rows && sc->best_pos < sc->scr_n) ? sc->best_pos : -1;
   auto pbin = [&](int p, uint32_t r) -> uint32_t {
     if (r == INVR) return 0u;
     if (bj_scr >= 0) return (uint32_t)c.bscr[(on.start + p) * 16 + bj_scr];
@@ -918,7 +935,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
         load_rows(cb);
 #pragma unroll
         for (int u = 0; u < RPT; ++u)
-          rbin[u] = rrow[u] != 0xFFFFFFFFu ? (uint32_t)c.Xb[(int64_t)(rrow[u] & c.rmask) * c.ld + feat] : 0u;
+          rbin[u] = rrow[u] == 0xFFFFFFFFu ? 0u
+                  : bj_scr >= 0 ? (uint32_t)c.bscr[(on.start + cb + tid + NT * u) * 16 + bj_scr]
+                                : (uint32_t)c.Xb[(int64_t)(rrow[u] & c.rmask) * c.ld + feat];
       }
     }
     uint64_t ml[RPT], mr[RPT];
@@ -1324,7 +1343,8 @@ __global__ __launch_bounds__(64) void k_large_prep(Ctx c, int set_cur, int nL) {
   if (lane != 0) return;
   st.pos = 0; st.nonconst = 0; st.done = 0; st.best_feat = -1; st.best_bin = -1; st.split = 0; st.nl = 0;
   st.best_gain = -INFINITY;
-  st.best_j = -1;
+  st.best_pos = 1 << 30;
+  st.scr_n = st.g <= 16 ? st.g : 0;
   c.lstate[slot] = st;
   c.lcursor[2 * slot] = 0;
   c.lcursor[2 * slot + 1] = 0;
@@ -1372,7 +1392,7 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
 #pragma unroll
       for (int j = 0; j < KGL; ++j) bb[j] = (j < g && rbn != INV) ? (uint32_t)c.Xb[(int64_t)(rbn & c.rmask) * c.ld + fj[j]] : 0u;
       const uint32_t rc2 = row_at(r + 512);
-      if (ra != INV) {   // the group's bins of this row position for the partition (Ctx::bscr)
+      if (ra != INV && st.pos == 0) {   // round 0: bins of visiting positions 0..15 (Ctx::bscr)
         uint4 v;
         v.x = ba[0] | ba[1] << 8 | ba[2] << 16 | ba[3] << 24;
         v.y = ba[4] | ba[5] << 8 | ba[6] << 16 | ba[7] << 24;
@@ -1448,9 +1468,7 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
     int uj;
     select_group(c, s, feats, g, rg, rb, rn, rleft, best_left, nc, bg, bf, bbin, uj);
     st.nonconst = nc; st.best_gain = bg; st.best_feat = bf; st.best_bin = bbin;
-    // this round's scratch holds the best feature's bins only if it was updated now (and the
-    // histogram pass took the <= 16-feature path that writes the scratch)
-    st.best_j = g <= 16 ? uj : -1;
+    if (uj >= 0) st.best_pos = st.pos + uj;
     st.pos += g;
     need_more = (st.nonconst < s.max_features && st.pos < c.d) ? 1 : 0;
   }
@@ -1505,7 +1523,7 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
   auto row_at = [&](int r) -> uint32_t { return r < r1 ? rows[r] : INV; };
   // split bin at row position p: from the histogram pass's scratch if the final round's
   // group produced the best split (st.best_j >= 0), else gathered from the table
-  const int bj = st.best_j;
+  const int bj = st.best_pos < st.scr_n ? st.best_pos : -1;
   auto bin_of = [&](int p, uint32_t row) -> int {
     if (row == INV) return 0;
     if (bj >= 0) return (int)c.bscr[(st.on.start + p) * 16 + bj];
