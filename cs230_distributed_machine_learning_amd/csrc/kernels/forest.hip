@@ -111,6 +111,7 @@ struct ForestArgs {
   int64_t n_nodes_out, status_out, levels_out, large_rounds_out;
   int64_t tier_nodes_out[4];
   int64_t ystride;       // >0: tree t regresses on yreg[specs[t].target * ystride + row] (boosting)
+  int64_t XbT;           // optional feature-major copy of the bins, uint8 [d][n] (0 = none)
 };
 
 constexpr int kTiers = 4;  // 0 subtree, 1 wave, 2 block, 3 large
@@ -165,6 +166,10 @@ struct Ctx {
   // reads the split feature's bin with 16-B-strided coalesced loads instead of
   // re-gathering a 128-B table line per row
   uint8_t* bscr;
+  // feature-major bins [d][n] (optional): the large tier's nodes hold a dense, sorted
+  // share of the table's rows, so a 64-lane gather of one feature from the feature-major
+  // copy touches a couple of lines instead of 64 row lines
+  const uint8_t* XbT;
 };
 
 // target vector of a tree (shared y, or its own row of the boosting target matrix)
@@ -1350,6 +1355,11 @@ __global__ __launch_bounds__(64) void k_large_prep(Ctx c, int set_cur, int nL) {
   c.lcursor[2 * slot + 1] = 0;
 }
 
+__device__ __forceinline__ uint32_t large_bin(const Ctx& c, uint32_t wd, int f) {
+  const uint32_t row = wd & c.rmask;
+  return c.XbT ? (uint32_t)c.XbT[(int64_t)f * c.n + row] : (uint32_t)c.Xb[(int64_t)row * c.ld + f];
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
   using CT = typename HT<MODE>::T;
@@ -1385,12 +1395,12 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
     uint64_t pa = ra != INV ? word_payload<MODE>(c, s, ty, ra) : 0ull;
     uint32_t ba[KGL];
 #pragma unroll
-    for (int j = 0; j < KGL; ++j) ba[j] = (j < g && ra != INV) ? (uint32_t)c.Xb[(int64_t)(ra & c.rmask) * c.ld + fj[j]] : 0u;
+    for (int j = 0; j < KGL; ++j) ba[j] = (j < g && ra != INV) ? large_bin(c, ra, fj[j]) : 0u;
     for (int r = t0; r < r1; r += 256) {
       const uint64_t pb = rbn != INV ? word_payload<MODE>(c, s, ty, rbn) : 0ull;
       uint32_t bb[KGL];
 #pragma unroll
-      for (int j = 0; j < KGL; ++j) bb[j] = (j < g && rbn != INV) ? (uint32_t)c.Xb[(int64_t)(rbn & c.rmask) * c.ld + fj[j]] : 0u;
+      for (int j = 0; j < KGL; ++j) bb[j] = (j < g && rbn != INV) ? large_bin(c, rbn, fj[j]) : 0u;
       const uint32_t rc2 = row_at(r + 512);
       if (ra != INV && st.pos == 0) {   // round 0: bins of visiting positions 0..15 (Ctx::bscr)
         uint4 v;
@@ -1761,6 +1771,7 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.ghist = (void*)(ws + L.ghist);
   c.lcursor = (int32_t*)(ws + L.lcursor);
   c.bscr = ws + L.bscr;
+  c.XbT = (const uint8_t*)a->XbT;
   c.large_cap = L.large_cap;
   c.wave_max = (int)a->wave_max; c.block_max = (int)a->block_max; c.chunk = (int)a->chunk;
   c.kg_wave = (int)a->kg_wave; c.kg_block = (int)a->kg_block; c.kg_large = (int)a->kg_large;

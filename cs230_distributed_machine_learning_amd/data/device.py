@@ -77,6 +77,14 @@ class DeviceData:
             self._Xb = binning.bin_matrix(self.X, self._edges)
         return self._Xb
 
+    def binned_feature_major(self):
+        """Feature-major copy of the bins, uint8 [d, n] (the forest builder's large tier
+        gathers one feature of a dense sorted row set from it: coalesced)."""
+        if getattr(self, "_XbT", None) is None:
+            Xb = self.binned()
+            self._XbT = Xb[:, :self.d].t().contiguous()
+        return self._XbT
+
     def feature_major(self) -> torch.Tensor:
         """``X^T`` [d, n] contiguous (coalesced per-feature streaming in the KNN/SVM kernels)."""
         if getattr(self, "_XT", None) is None:

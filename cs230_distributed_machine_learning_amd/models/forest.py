@@ -249,7 +249,8 @@ class ForestFamily(Family):
         t0 = time.perf_counter()
         if data.is_gpu:
             fb = forest_ops.build_gpu(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
-                                      data.n_classes, is_reg, self.tiers, reuse_pool=True)
+                                      data.n_classes, is_reg, self.tiers, reuse_pool=True,
+                                      XbT=data.binned_feature_major())
         else:
             fb = forest_ops.build_cpu(Xb.numpy(), data.y_enc, None if not is_reg else data.y_reg.numpy(),
                                       data.roles_np(), specs, data.n_classes, is_reg)

@@ -202,7 +202,7 @@ def _carve(buf: torch.Tensor, off: int, shape, dtype) -> torch.Tensor:
 
 def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,
               specs: np.ndarray, n_classes: int, is_reg: bool, tiers: ForestTiers | None = None,
-              ystride: int = 0, reuse_pool: bool = False) -> ForestBuild:
+              ystride: int = 0, reuse_pool: bool = False, XbT: Optional[torch.Tensor] = None) -> ForestBuild:
     """``ystride > 0``: ``yreg`` is a [targets, ystride] matrix and tree t regresses on
     row ``specs[t]['target']`` (gradient boosting's per-fit pseudo-residuals).
     ``reuse_pool``: the node arrays live in the device arena and are valid until the
@@ -225,6 +225,9 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     a.roles, a.n_splits = native.ptr(roles), roles.shape[0]
     a.specs, a.T = native.ptr(specs_dev), T
     a.ystride = int(ystride)
+    if XbT is not None:
+        assert XbT.shape == (d, n) and XbT.dtype == torch.uint8 and XbT.is_contiguous() and XbT.device == dev
+    a.XbT = native.ptr(XbT) if XbT is not None else 0
     a.active_count = native.ptr(active)
     t0 = time.perf_counter()
     with trace.range("forest_count"):

@@ -66,7 +66,7 @@ ForestArgs = _i64_struct(
         "sub_max", "sub_cache_d",
         "n_nodes_out", "status_out", "levels_out", "large_rounds_out",
         "tier0_nodes", "tier1_nodes", "tier2_nodes", "tier3_nodes",
-        "ystride",
+        "ystride", "XbT",
     ],
 )
 

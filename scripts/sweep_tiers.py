@@ -10,6 +10,8 @@ dev = torch.device('cuda:0')
 X, y = synthetic.make_table(1_000_000, 100, informative=10, n_classes=2, noise=1.0, seed=0, device=dev)
 y = y.to(torch.int32)
 edges = binning.quantile_edges(X); Xb = binning.bin_matrix(X, edges)
+import os
+XbT = None if os.environ.get("DML_NO_XBT") else Xb[:, :X.shape[1]].t().contiguous()
 roles, _ = make_split_roles(y.cpu().numpy(), 5, True, holdout=False)
 roles = torch.from_numpy(roles).to(dev)
 # 4 candidates spanning the grid's cost range
@@ -34,7 +36,7 @@ for g in grid:
     ts = []
     for rep in range(2):
         torch.cuda.synchronize(); t0 = time.time()
-        fb = forest_ops.build_gpu(Xb, y, None, roles, specs, 2, False, tiers)
+        fb = forest_ops.build_gpu(Xb, y, None, roles, specs, 2, False, tiers, XbT=XbT)
         torch.cuda.synchronize(); ts.append(time.time() - t0)
         stats = fb.stats
         del fb
