@@ -4,9 +4,11 @@ The reference has no fault injection (only a commented-out 30-45 s sleep,
 aws-prod/worker/worker.py:308-311) and never retries a failed task: a failed subtask is
 reported once and the job hangs below 100 % (D5, master/task_handler.py:91).  Here:
 
-* a slice whose device batch raises (HIP error, OOM, injected fault) is retried up to
-  ``Config.max_retries`` times on the same rank before its candidates are failed with
-  the error (they then count as terminal and take ``error_score``);
+* a slice whose device batch raises a transient error (OOM, injected fault) is retried
+  up to ``Config.max_retries`` times on the same rank before its candidates are failed
+  with the error (they then count as terminal and take ``error_score``); a sticky device
+  fault (HIP error) is not retried in-process under the distributed runner: the worker
+  exits and the dispatcher re-queues its slice on a survivor (parallel/runner.py);
 * ``DML_INJECT_FAIL_RATE`` (0..1) makes a deterministic fraction of slice *attempts*
   raise ``InjectedFault`` — decided by a hash of (job seed, slice, attempt), so a test
   can predict exactly which attempts fail;
@@ -81,17 +83,21 @@ def maybe_kill(rank: int, slices_done: int) -> None:
         os._exit(17)
 
 
-def run_with_retries(fn, seed: int, slice_key: str, retries: Optional[int] = None) -> Tuple[object, int, Optional[BaseException]]:
+def run_with_retries(fn, seed: int, slice_key: str, retries: Optional[int] = None,
+                     reraise=None) -> Tuple[object, int, Optional[BaseException]]:
     """Call ``fn()`` with up to ``retries`` re-tries -> (value, attempts, last error).
 
-    ``value`` is None when every attempt raised."""
+    ``value`` is None when every attempt raised.  ``reraise(e) -> bool`` marks errors that
+    must not be retried in this process (a sticky device fault): they propagate."""
     n = plan().max_retries if retries is None else retries
     last: Optional[BaseException] = None
     for attempt in range(n + 1):
         try:
             maybe_inject(seed, slice_key, attempt)
             return fn(), attempt + 1, None
-        except (RuntimeError, OSError, MemoryError) as e:  # device / OOM / injected: retry the batch
+        except (RuntimeError, OSError, MemoryError) as e:  # OOM / injected / transient: retry the batch
+            if reraise is not None and reraise(e):
+                raise
             last = e
             _release_device_memory()
         except Exception as e:  # deterministic (parameter / data) errors are not retried

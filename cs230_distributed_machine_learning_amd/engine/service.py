@@ -302,9 +302,10 @@ class Controller:
 
     def unsubscribe(self, body: Dict[str, Any]) -> Resp:
         wid = str((body or {}).get("worker_id"))
+        left = self.runner.leave(wid)
         units = self.scheduler.unsubscribe(wid)
         self.runner.requeue(units)
-        return 200, {"status": "unsubscribed", "requeued": len(units)}
+        return 200, {"status": "unsubscribed", "requeued": len(units), "left": left}
 
     def heartbeat(self, body: Dict[str, Any]) -> Resp:
         wid = str((body or {}).get("worker_id"))
@@ -328,6 +329,10 @@ class Runner:
 
     def requeue(self, units: List[Unit]) -> None:
         pass
+
+    def leave(self, worker_id: str) -> bool:
+        """A worker unsubscribed: stop giving it work (runners with membership)."""
+        return False
 
     def shutdown(self) -> None:
         pass
@@ -416,19 +421,28 @@ def candidate_costs(plan: Dict[str, Any], n_train: int, d: int, n_classes: int) 
 
 
 def run_slice(plan: Dict[str, Any], params: List[Dict[str, Any]], subtask_ids: List[str], dd, cand_ids: List[int],
-              worker_id: str, device_name: str, seed: int = 0):
+              worker_id: str, device_name: str, seed: int = 0, keep_models: str = "none",
+              models_root: Optional[str] = None, fault_exit: bool = False, retries: Optional[int] = None):
     """Run one slice of candidates on a device -> (results, J3 metrics per candidate, wall s).
 
     Controller-free so every rank of the distributed runner executes exactly this.  A
-    batch that raises (device error, injected fault) is retried up to
+    batch that raises a transient error (injected fault, OOM) is retried up to
     ``DML_MAX_RETRIES`` times (engine/faults.py) before its candidates fail terminally.
+    With ``fault_exit`` a device fault is re-raised instead: a poisoned HIP context
+    cannot recover in-process, so the worker exits and the dispatcher re-queues the
+    slice on a survivor.  ``retries=0`` for row-sharded slices (a one-rank retry would
+    pair collectives wrongly with its peers).  ``keep_models="all"``: every candidate's
+    holdout model is written to ``models_root`` and its ``model_path`` / ``model_id``
+    returned in the result (reference worker.py:351-361).
     """
     from . import faults
     from .executor import CandidateResult, JobSpec, run_candidates
 
+    keep_all = keep_models == "all" and models_root is not None and bool(plan["holdout"])
     spec = JobSpec(model_type=plan["model_type"], candidates=params, cv=plan["cv"], scoring=plan["scoring"],
                    holdout=plan["holdout"], test_size=plan["test_size"], random_state=plan["random_state"],
-                   error_score=plan["error_score"], keep_models="none", seed=seed, raise_batch_errors=True)
+                   error_score=plan["error_score"], keep_models="all" if keep_all else "none", seed=seed,
+                   raise_batch_errors=True)
     received = utc_iso()
     slice_key = ",".join(str(int(c)) for c in cand_ids)
     gpu = dd.device.index if dd.is_gpu else None
@@ -441,12 +455,25 @@ def run_slice(plan: Dict[str, Any], params: List[Dict[str, Any]], subtask_ids: L
         started = utc_iso()
         t0 = time.perf_counter()
         with trace.range(f"slice {plan['model_type']} x{len(cand_ids)}"):
-            results, attempts, err = faults.run_with_retries(lambda: run_candidates(dd, spec, cand_ids), seed, slice_key)
+            results, attempts, err = faults.run_with_retries(lambda: run_candidates(dd, spec, cand_ids), seed, slice_key,
+                                                             retries=retries,
+                                                             reraise=_device_fault if fault_exit else None)
         if results is None:
             results = [CandidateResult(candidate=c, ok=False, error=f"{type(err).__name__}: {err} "
                                        f"(after {attempts} attempts)") for c in cand_ids]
         wall = time.perf_counter() - t0
     finished = utc_iso()
+    if keep_all:
+        store = ModelStore(models_root)
+        for r in results:
+            if r.ok and r.model is not None:
+                try:
+                    r.model["subtask_id"] = subtask_ids[r.candidate]
+                    r.result["model_id"] = f"{subtask_ids[r.candidate]}_model"
+                    r.result["model_path"] = store.save(r.result["model_id"], r.model)
+                except Exception:
+                    traceback.print_exc()
+                r.model = None
     cpu, mem = smp.avg()
     hbm_peak = None
     if dd.is_gpu:
@@ -467,11 +494,18 @@ def run_slice(plan: Dict[str, Any], params: List[Dict[str, Any]], subtask_ids: L
     return results, metrics, wall
 
 
+def _device_fault(e: BaseException) -> bool:
+    from ..parallel.runner import is_device_fault
+
+    return is_device_fault(e)
+
+
 def execute_plan_slice(ctl: Controller, job: Job, plan: Dict[str, Any], dd, cand_ids: List[int], worker_id: str,
                        device_name: str, seed: int = 0):
     params = [st.spec["parameters"] for st in job.subtasks]
     sids = [st.subtask_id for st in job.subtasks]
-    return run_slice(plan, params, sids, dd, cand_ids, worker_id, device_name, seed)
+    return run_slice(plan, params, sids, dd, cand_ids, worker_id, device_name, seed,
+                     keep_models=ctl.config.keep_models, models_root=ctl.models.root)
 
 
 def plan_slices(ctl: Controller, plan: Dict[str, Any], todo: List[int], n_train: int, d: int, n_classes: int,

@@ -77,3 +77,40 @@ def share_bins(dd) -> None:
     dist.broadcast(edges, 0)
     dd._edges = edges
     dd._Xb = binning.bin_matrix(dd.X, edges)
+
+
+# ---- host-staged transport (no collective) ------------------------------------------------
+# Used when a collective over the whole process group is impossible or not wanted: a rank
+# died (the default group can no longer broadcast), or a worker joined after launch (it is
+# not in the process group at all).  Rank 0 parses the table once and writes it to a
+# host file (tmpfs by default); every rank memory-maps it and copies it to its own GPU over
+# its own PCIe link -- no rank waits for another.
+def stage_host(X: np.ndarray, y: np.ndarray, path: str) -> str:
+    import os
+
+    y = np.asarray(y)
+    meta = {"n": int(X.shape[0]), "d": int(X.shape[1])}
+    if y.dtype.kind in "OUS":
+        classes, codes = np.unique(y.astype(str), return_inverse=True)
+        meta.update(y="codes", classes=classes.tolist())
+        y_arr = codes.astype(np.int64)
+    else:
+        meta["y"] = str(y.dtype)
+        y_arr = y
+    tmp = path + ".tmp.npz"
+    np.savez(tmp, X=np.ascontiguousarray(X, dtype=np.float32), y=y_arr, meta=np.array(json.dumps(meta)))
+    os.replace(tmp, path)
+    return path
+
+
+def load_staged(path: str, device: torch.device):
+    """(X on ``device``, y host array) from a file written by ``stage_host``."""
+    with np.load(path, allow_pickle=False) as z:
+        meta = json.loads(str(z["meta"]))
+        X = torch.from_numpy(np.ascontiguousarray(z["X"])).to(device)
+        y = z["y"]
+    if meta["y"] == "codes":
+        y = np.asarray(meta["classes"], dtype=object)[y.astype(np.int64)]
+    else:
+        y = y.astype(np.dtype(meta["y"]))
+    return X, y

@@ -29,7 +29,8 @@ class DistInfo:
 
     @property
     def is_dist(self) -> bool:
-        return self.world > 1 and dist.is_initialized()
+        """A process group exists (world > 1, or DML_FORCE_PG=1 at world 1): collectives run."""
+        return self.backend != "none" and dist.is_initialized()
 
     @property
     def is_root(self) -> bool:
@@ -59,11 +60,20 @@ def init(backend: Optional[str] = None, timeout_s: float = 1800.0, want_gpu: Opt
     else:
         device = torch.device("cpu")
     be = "none"
-    if world > 1:
+    # DML_FORCE_PG=1: build the process group even for one rank, so the RCCL code path
+    # (communicator setup, every collective the runner and bench use) runs on a one-GPU box
+    force = os.environ.get("DML_FORCE_PG") == "1"
+    if world > 1 or force:
         be = backend or ("nccl" if gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         # RCCL watchdog: a collective that outlives the timeout (a peer rank
-        # died mid-job) tears the communicator down and raises instead of hanging the rank
+        # died mid-job) is caught by the watchdog, which aborts the communicator and ends
+        # THIS process (mode 1, TearDown) instead of leaving it hung forever; the runner
+        # avoids collectives once a peer is known dead (parallel/runner.py), so this only
+        # fires for a death in the middle of a collective epoch
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         timeout_s = float(os.environ.get("DML_COLLECTIVE_TIMEOUT_S", timeout_s))
         kw = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
@@ -135,6 +145,22 @@ def store():
     from torch.distributed.distributed_c10d import _get_default_store
 
     return _get_default_store()
+
+
+def service_store():
+    """The runner's control-plane store: the rendezvous TCPStore under the fixed prefix
+    ``dml`` -- the same view whether a process is a member of the process group (walks
+    past the group's own key prefixes) or joined later with just the host and port
+    (``parallel/runner.py join_cluster``)."""
+    from torch.distributed import PrefixStore
+
+    st = store()
+    if st is None:
+        return None
+    raw = st
+    while getattr(raw, "underlying_store", None) is not None:
+        raw = raw.underlying_store
+    return PrefixStore("dml", raw)
 
 
 def destroy() -> None:

@@ -1,41 +1,61 @@
-"""Distributed job runner: one rank per GPU, rank 0 = controller + gateway + worker.
+"""Distributed job runner: one rank per GPU; rank 0 = controller + gateway + dispatcher + worker.
 
 Replaces the reference's scheduler/worker tiers and their Kafka/HTTP plumbing
-(aws-prod/scheduler/scheduler_service.py:197-351 ingress/status loops,
+(aws-prod/scheduler/scheduler_service.py:173-191 placement, :197-351 ingress/status
+loops, :205-247 heartbeat monitor + requeue; scheduler.py:105-139 subscribe/unsubscribe;
 worker/worker.py:156-286 consume loop):
 
-job announcement   rank 0 writes ``job/<seq>`` (the J1 request) into the TCPStore; the
-                   other ranks block on that key (no spinning poll loops, D13)
-dataset            rank 0 parses once; RCCL broadcast into every rank's HBM, then the
-                   uint8 binned copy is derived from rank-0 edges (parallel/data.py);
-                   cached per dataset for later jobs
-work               candidates in LPT order (most expensive first), cut into slices;
-                   every rank claims slices with ``store.add`` on one counter — dynamic
-                   self-scheduling that also absorbs speed differences (work stealing)
-results            per-slice result JSON through the store (rank 0 publishes progress
-                   while ranks still run: streaming status/SSE), and at the end one RCCL
-                   all-reduce of the [candidates x CV-folds] score matrix — the numeric
-                   result path — checked against the store copy
-liveness           every rank refreshes ``hb/<rank>``; rank 0's monitor re-queues the
-                   claimed-but-unfinished slices of a rank that went silent, and the
-                   job then finishes on the store path only (a dead rank cannot join a
-                   collective)
+jobs               every submitted job is admitted at once and cut into LPT slices
+                   (most expensive first); the cluster runs the slices of ALL active jobs
+                   concurrently, like the reference scheduler interleaving every job's
+                   tasks across every worker
+dispatch           rank 0's dispatcher hands each idle worker its next slice through the
+                   rendezvous TCPStore (``asg/<worker>/<k>`` -> ``res/<worker>/<k>``); the
+                   slice comes from the active job of the session that has used the least
+                   node time so far (slice-level fair share, the same policy as the local
+                   runner), so a one-candidate job overtakes a running 256-candidate search
+dataset            once per dataset per worker.  While the whole process group is alive the
+                   dispatcher runs a *collective epoch*: it drains the workers and every rank
+                   receives the table by ONE RCCL broadcast over xGMI (parallel/data.py).
+                   Once a rank has died (the default group can no longer run collectives) or
+                   for a worker that joined after launch, rank 0 stages the table in a host
+                   file and each worker copies it to its own GPU over its own PCIe link
+results            per-slice result JSON through the store; rank 0 publishes progress as
+                   slices land (status / SSE stream) and holds each job's last slice until
+                   the best candidate is refit, so "completed" always carries the model
+liveness           every worker refreshes ``hb/<worker>``; a worker silent for
+                   ``dead_after_s`` is declared dead, its in-flight slice goes back to the
+                   front of its job's queue and the survivors finish the job.  A slice that
+                   hits a device fault makes its worker exit (a poisoned HIP context cannot
+                   retry in-process); the dispatcher re-queues it the same way
+membership         processes outside the launch world can join at any time
+                   (``join_cluster``; /subscribe): they get a worker id, heartbeat, and
+                   receive slices with host-staged datasets; they leave by unsubscribing or
+                   by dying (reference scheduler.py:105-139 elastic join/leave)
+data parallel      row-sharded jobs (parallel/data_parallel.py) run as an exclusive epoch on
+                   every rank of the process group, only while it is whole; otherwise they
+                   fall back to task-parallel slices
 """
 from __future__ import annotations
 
+import collections
 import json
+import os
+import tempfile
 import threading
 import time
 import traceback
-from typing import Any, Dict, List, Optional
+import zlib
+from dataclasses import dataclass, field
+from typing import Any, Deque, Dict, List, Optional, Set
 
 import numpy as np
 import torch
 
 from ..engine import faults
 from ..engine.jobs import Job, json_safe
-from ..engine.service import (Controller, DeviceCache, Runner, candidate_costs, finalize_job, job_plan, job_seed,
-                              plan_slices, publish_results, run_slice)
+from ..engine.service import (Controller, Runner, candidate_costs, job_plan, job_seed, pick_refit, plan_slices,
+                              publish_results, refit_model, run_slice)
 from ..models.base import family_of, is_classifier
 from ..utils.log import get_logger
 from . import data as pdata
@@ -44,12 +64,14 @@ from . import dist
 log = get_logger("dml.runner")
 
 HB_PERIOD_S = 1.0
+POLL_S = 0.003
+MAX_WORKERS = 4096
 
 
 class LockedStore:
-    """Thread-safe view of the TCPStore for rank 0 (main loop + monitor threads).
-
-    ``wait`` polls ``check`` so a blocked waiter never holds the lock."""
+    """Thread-safe view of a TCPStore client (rank 0's dispatcher, its worker thread and
+    the heartbeat share one client); ``wait`` polls ``check`` so a waiter never holds
+    the lock."""
 
     def __init__(self, store):
         self._s = store
@@ -73,16 +95,19 @@ class LockedStore:
 
     def delete_key(self, k):
         with self._lock:
-            return self._s.delete_key(k)
+            try:
+                return self._s.delete_key(k)
+            except Exception:
+                return False
 
-    def wait(self, ks, timeout=None):
+    def wait(self, ks, timeout=None, poll_s: float = 0.002):
         t0 = time.time()
         while True:
             if self.check(ks):
                 return
-            if timeout is not None and time.time() - t0 > timeout.total_seconds():
+            if timeout is not None and time.time() - t0 > timeout:
                 raise TimeoutError(ks)
-            time.sleep(0.002)
+            time.sleep(poll_s)
 
 
 class _Res:
@@ -96,25 +121,25 @@ class _Res:
         self.fit_seconds = float(d.get("fit_seconds", 0.0))
 
 
-def _enc_results(results, metrics) -> str:
+def _enc_results(results, metrics) -> List[Dict[str, Any]]:
     out = []
     for r in results:
         out.append({"candidate": r.candidate, "ok": r.ok, "result": json_safe(r.result), "error": r.error,
                     "fit_seconds": r.fit_seconds, "metrics": json_safe(metrics.get(r.candidate))})
-    return json.dumps(out)
+    return out
 
 
 class _Heartbeat:
-    def __init__(self, store, rank: int):
-        self.store, self.rank = store, rank
+    def __init__(self, store, wid: int):
+        self.store, self.wid = store, wid
         self._stop = threading.Event()
-        self._t = threading.Thread(target=self._loop, daemon=True, name=f"dml-hb-{rank}")
+        self._t = threading.Thread(target=self._loop, daemon=True, name=f"dml-hb-{wid}")
         self._t.start()
 
     def _loop(self):
         while True:
             try:
-                self.store.set(f"hb/{self.rank}", str(time.time()))
+                self.store.set(f"hb/{self.wid}", str(time.time()))
             except Exception:
                 return
             if self._stop.wait(HB_PERIOD_S):
@@ -124,23 +149,78 @@ class _Heartbeat:
         self._stop.set()
 
 
+_DEVICE_FAULT_MARKERS = ("HIP error", "hipError", "CUDA error", "device-side assert", "HSA_STATUS",
+                         "illegal memory access", "GPU fault", "unspecified launch failure", "memory access fault")
+
+
+def is_device_fault(e: BaseException) -> bool:
+    """A sticky device fault poisons the process's HIP context: nothing more can run here."""
+    if isinstance(e, faults.InjectedFault) or isinstance(e, torch.cuda.OutOfMemoryError):
+        return False
+    msg = f"{type(e).__name__}: {e}"
+    return isinstance(e, RuntimeError) and any(m in msg for m in _DEVICE_FAULT_MARKERS)
+
+
+def dataset_key(registry, dataset_id: str, plan: Dict[str, Any]) -> str:
+    path = registry.find_file(dataset_id)
+    mt = os.path.getmtime(path) if path and os.path.exists(path) else 0
+    return f"{path}:{mt}:{plan['feature_columns']}:{plan['target_column']}:{is_classifier(plan['model_type'])}"
+
+
+def _needs_bins(plan) -> bool:
+    return plan["model_type"].startswith("RandomForest") or plan["model_type"].startswith("GradientBoosting")
+
+
 class WorkerCore:
-    """What every rank does for one job (rank 0 also bookkeeps)."""
+    """What a worker does with an assignment (every rank; rank 0 also has the controller)."""
 
-    def __init__(self, device: torch.device):
+    def __init__(self, device: torch.device, wid: Optional[int] = None, store=None, in_group: bool = True):
         self.inf = dist.info()
-        self.store = LockedStore(dist.store())
+        self.wid = self.inf.rank if wid is None else wid
+        self.store = store if store is not None else LockedStore(dist.service_store())
         self.device = device
-        self.cache: Dict[str, Any] = {}
-        self.collectives_ok = True
+        self.in_group = in_group
+        self.cache: "collections.OrderedDict[str, Any]" = collections.OrderedDict()
+        self.msgs: Dict[int, Dict[str, Any]] = {}
+        self.slices_done = 0
 
-    # dataset: broadcast once, keep resident
-    def dataset(self, msg: Dict[str, Any], ctl: Optional[Controller]):
+    # ---- job messages and datasets ------------------------------------------------------
+    def job_msg(self, seq: int) -> Dict[str, Any]:
+        m = self.msgs.get(seq)
+        if m is None:
+            m = json.loads(self.store.get(f"job/{seq}"))
+            self.msgs[seq] = m
+            while len(self.msgs) > 64:
+                self.msgs.pop(next(iter(self.msgs)))
+        return m
+
+    def _keep(self, key: str, dd) -> None:
+        self.cache[key] = dd
+        self.cache.move_to_end(key)
+        while len(self.cache) > 4:
+            self.cache.popitem(last=False)
+
+    def dataset(self, msg: Dict[str, Any], ctl: Optional[Controller] = None):
+        """The job's resident table; loaded from the host-staged file when absent."""
         from ..data.device import DeviceData
 
         key = msg["dataset_key"]
-        if key in self.cache:
-            return self.cache[key]
+        dd = self.cache.get(key)
+        if dd is not None:
+            self.cache.move_to_end(key)
+            return dd
+        path = msg.get("staged")
+        if not path:
+            raise RuntimeError(f"dataset {msg['dataset_id']!r} is not resident on worker {self.wid} and not staged")
+        X, y = pdata.load_staged(path, self.device)
+        dd = DeviceData(X, y, is_classifier(msg["plan"]["model_type"]), self.device, name=msg["dataset_id"])
+        self._keep(key, dd)
+        return dd
+
+    def load_collective(self, msg: Dict[str, Any], ctl: Optional[Controller]):
+        """Collective epoch: every rank receives the table by one broadcast (RCCL on GPU)."""
+        from ..data.device import DeviceData
+
         plan = msg["plan"]
         X = y = None
         if self.inf.rank == 0:
@@ -148,20 +228,49 @@ class WorkerCore:
             X, y = ds.X, ds.y
         Xd, y_host = pdata.broadcast_table(X, y, self.device)
         dd = DeviceData(Xd, y_host, is_classifier(plan["model_type"]), self.device, name=msg["dataset_id"])
-        if plan["model_type"].startswith("RandomForest") or plan["model_type"].startswith("GradientBoosting"):
+        if _needs_bins(plan):
             pdata.share_bins(dd)
-        while len(self.cache) >= 4:
-            self.cache.pop(next(iter(self.cache)))
-        self.cache[key] = dd
+        self._keep(msg["dataset_key"], dd)
         return dd
 
-    def dataset_dp(self, msg: Dict[str, Any], ctl: Optional[Controller]):
-        """Row shard of the job's table on this rank (one RCCL scatter; parallel/data_parallel.py)."""
+    # ---- assignments ----------------------------------------------------------------------
+    def execute(self, a: Dict[str, Any], ctl: Optional[Controller]) -> Dict[str, Any]:
+        kind = a["kind"]
+        if kind == "slice":
+            return self._slice(a, ctl)
+        if kind == "load":
+            msg = self.job_msg(a["seq"])
+            t0 = time.perf_counter()
+            self.load_collective(msg, ctl)
+            return {"loaded": msg["dataset_key"], "wall": time.perf_counter() - t0, "cache": list(self.cache.keys())}
+        if kind == "dp":
+            return self._dp(a, ctl)
+        if kind == "refit":
+            return self._refit(a, ctl)
+        raise ValueError(f"unknown assignment kind {kind!r}")
+
+    def _slice(self, a, ctl) -> Dict[str, Any]:
+        msg = self.job_msg(a["seq"])
+        faults.maybe_kill(self.wid, self.slices_done)   # fault injection: die holding an assigned slice
+        t_load = time.perf_counter()
+        dd = self.dataset(msg, ctl)
+        load_s = time.perf_counter() - t_load
+        results, metrics, wall = run_slice(msg["plan"], msg["params"], msg["subtask_ids"], dd, a["ids"],
+                                           f"rank{self.wid}", str(self.device), seed=msg["seed"],
+                                           keep_models=msg.get("keep_models", "none"),
+                                           models_root=msg.get("models_root"), fault_exit=True)
+        self.slices_done += 1
+        return {"results": _enc_results(results, metrics), "wall": wall, "load_s": load_s,
+                "cache": list(self.cache.keys())}
+
+    def _dp(self, a, ctl) -> Dict[str, Any]:
+        """Data-parallel job on the whole process group: every rank runs every slice in
+        order on its row shard (the fits' reductions are collectives), then all ranks
+        refit the winner together; rank 0 decides the winner and keeps the model."""
         from .data_parallel import RowShard, scatter_table
 
-        key = "dp:" + msg["dataset_key"]
-        if key in self.cache:
-            return self.cache[key]
+        seq = a["seq"]
+        msg = self.job_msg(seq)
         plan = msg["plan"]
         X = y = None
         if self.inf.rank == 0:
@@ -169,127 +278,177 @@ class WorkerCore:
             X, y = ds.X, ds.y
         Xs, y_glob, r0 = scatter_table(X, y, self.device)
         dd = RowShard(Xs, y_glob, r0, is_classifier(plan["model_type"]), self.device, name=msg["dataset_id"])
-        while len(self.cache) >= 4:
-            self.cache.pop(next(iter(self.cache)))
-        self.cache[key] = dd
-        return dd
+        out: List[Dict[str, Any]] = []
+        results_all = []
+        for ids in msg["slices"]:
+            results, metrics, wall = run_slice(plan, msg["params"], msg["subtask_ids"], dd, ids, "data-parallel",
+                                               str(self.device), seed=msg["seed"], retries=0)
+            results_all.extend(results)
+            out.append({"results": _enc_results(results, metrics), "wall": wall})
+        # the winner is chosen by rank 0 (it owns the job table) and announced to every rank
+        if self.inf.rank == 0:
+            job = ctl.table.get(msg["session_id"], msg["job_id"])
+            best = pick_refit(ctl, job, plan, results_all)
+            self.store.set(f"job/{seq}/refit", str(best.candidate if best is not None else -1))
+        self.store.wait([f"job/{seq}/refit"])
+        best_i = int(self.store.get(f"job/{seq}/refit"))
+        model_path = None
+        if best_i >= 0:
+            model = refit_model(plan, msg["params"][best_i], dd)
+            if self.inf.rank == 0 and model is not None:
+                model_path = _save_model(ctl, msg, best_i, model)
+        return {"dp_slices": out, "refit": best_i, "model_path": model_path}
 
-    def run_dp(self, seq: int, msg: Dict[str, Any], ctl: Optional[Controller] = None):
-        """Data-parallel job: every rank runs every slice in order on its row shard (the
-        fits' reductions are collectives, so the ranks move in lock step); rank 0
-        publishes the results, then all ranks refit the winner together."""
-        from ..engine.service import refit_model
-
-        st, r = self.store, self.inf.rank
-        plan = msg["plan"]
-        dd = self.dataset_dp(msg, ctl)
-        params, sids = msg["params"], msg["subtask_ids"]
-        for i, ids in enumerate(msg["slices"]):
-            results, metrics, wall = run_slice(plan, params, sids, dd, ids, "data-parallel", str(self.device),
-                                               seed=msg["seed"])
-            if r == 0:
-                st.set(f"job/{seq}/res/{i}", _enc_results(results, metrics))
-                st.set(f"job/{seq}/wall/{i}", str(wall))
-                st.add(f"job/{seq}/done", 1)
-        st.add(f"job/{seq}/fin", 1)
-        st.wait([f"job/{seq}/refit"])             # rank 0 picks the refit candidate (or -1)
-        best = int(st.get(f"job/{seq}/refit"))
-        model = refit_model(plan, params[best], dd) if best >= 0 else None
-        return dd, model
-
-    def run(self, seq: int, msg: Dict[str, Any], ctl: Optional[Controller] = None, job: Optional[Job] = None):
-        if msg.get("mode") == "data":
-            return self.run_dp(seq, msg, ctl)
-        st, r, world = self.store, self.inf.rank, self.inf.world
-        plan = msg["plan"]
+    def _refit(self, a, ctl) -> Dict[str, Any]:
+        msg = self.job_msg(a["seq"])
         dd = self.dataset(msg, ctl)
-        slices: List[List[int]] = msg["slices"]
-        params, sids = msg["params"], msg["subtask_ids"]
-        n_cand = len(params)
-        n_cv = int(plan["cv"] or 0)
-        scores = torch.zeros((n_cand, max(1, n_cv)), dtype=torch.float64, device=self.device)
-        owned = torch.zeros((n_cand,), dtype=torch.float64, device=self.device)
-        worker_id = f"rank{r}"
-        def exec_slice(ids):
-            try:
-                return run_slice(plan, params, sids, dd, ids, worker_id, str(self.device), seed=msg["seed"])
-            except Exception as e:  # a failing slice must not desert the job's collectives
-                traceback.print_exc()
-                from ..engine.executor import CandidateResult
+        t0 = time.perf_counter()
+        model = refit_model(msg["plan"], msg["params"][a["candidate"]], dd)
+        path = _save_model(ctl, msg, a["candidate"], model) if model is not None else None
+        return {"model_path": path, "wall": time.perf_counter() - t0}
 
-                return [CandidateResult(candidate=c, ok=False, error=f"{type(e).__name__}: {e}") for c in ids], {}, 0.0
 
-        def publish(i, results, metrics, wall, local):
-            if local:
-                for res in results:
-                    if res.ok and n_cv:
-                        scores[res.candidate, :n_cv] = torch.tensor(
-                            [np.nan if v is None else v for v in res.result.get("cv_scores", [np.nan] * n_cv)],
-                            dtype=torch.float64)
-                        owned[res.candidate] = 1.0
-            st.set(f"job/{seq}/res/{i}", _enc_results(results, metrics))
-            st.set(f"job/{seq}/wall/{i}", str(wall))
-            if st.add(f"job/{seq}/first/{i}", 1) == 1:   # count each slice once (a re-queued
-                st.add(f"job/{seq}/done", 1)             # slice may finish twice)
+def _save_model(ctl, msg, cand: int, model) -> Optional[str]:
+    try:
+        model["job_id"] = msg["job_id"]
+        model["subtask_id"] = msg["subtask_ids"][cand]
+        if ctl is not None:
+            model["feature_names"] = list(ctl.registry.load(msg["dataset_id"], msg["plan"]["feature_columns"],
+                                                            msg["plan"]["target_column"]).feature_names)
+            return ctl.models.save(f"{msg['subtask_ids'][cand]}_model", model)
+        from ..engine.model_store import ModelStore
 
-        n_done = 0
+        return ModelStore(msg["models_root"]).save(f"{msg['subtask_ids'][cand]}_model", model)
+    except Exception:
+        traceback.print_exc()
+        return None
+
+
+def worker_loop(core: WorkerCore, ctl: Optional[Controller] = None, heartbeat: bool = True) -> None:
+    """A worker's life: wait for its next assignment, execute it, post the result.
+
+    A device fault poisons this process's HIP context: the worker posts the error and
+    exits non-zero; the dispatcher re-queues its slice to the survivors."""
+    st, wid = core.store, core.wid
+    hb = _Heartbeat(st, wid) if heartbeat else None
+    k = 0
+    try:
         while True:
-            i = st.add(f"job/{seq}/next", 1) - 1
-            if i >= len(slices):
-                break
-            st.set(f"job/{seq}/claim/{i}", str(r))
-            faults.maybe_kill(r, n_done)   # fault injection: die holding a claimed slice
-            results, metrics, wall = exec_slice(slices[i])
-            publish(i, results, metrics, wall, True)
-            n_done += 1
-        # Slices re-queued from a dead rank (rank 0's monitor appends them to job/<seq>/rq).
-        # Stay until every slice has a result: a rank that left before the death was
-        # detected would otherwise strand the re-queued work.  Each entry is claimed once.
-        j = 0
-        while int(st.add(f"job/{seq}/done", 0)) < len(slices):
-            n_rq = int(st.add(f"job/{seq}/rq_len", 0))
-            if j < n_rq:
-                if st.add(f"job/{seq}/rq_claim/{j}", 1) == 1:
-                    i = int(st.get(f"job/{seq}/rq/{j}"))
-                    results, metrics, wall = exec_slice(slices[i])
-                    publish(i, results, metrics, wall, False)   # not in this rank's RCCL share
-                j += 1
-                continue
-            time.sleep(0.02)
-        # numeric result path: one RCCL all-reduce of the score matrix (when every rank is alive)
-        st.add(f"job/{seq}/fin", 1)
-        st.wait([f"job/{seq}/mode"])
-        mode = st.get(f"job/{seq}/mode").decode()
-        if mode == "collective" and self.collectives_ok:
-            dist.all_reduce_sum(scores)
-            dist.all_reduce_sum(owned)
-        else:
-            self.collectives_ok = False
-        return dd, scores, owned, mode
+            key = f"asg/{wid}/{k}"
+            try:
+                st.wait([key], poll_s=0.002)
+            except Exception:   # the store (hosted by rank 0) is gone: the service exited
+                log.warning("worker %d lost the controller store; leaving", wid)
+                return
+            a = json.loads(st.get(key))
+            st.delete_key(key)
+            if a["kind"] == "stop":
+                return
+            try:
+                out = core.execute(a, ctl)
+            except Exception as e:
+                traceback.print_exc()
+                if is_device_fault(e):
+                    st.set(f"res/{wid}/{k}", json.dumps({"fatal": f"{type(e).__name__}: {e}"}))
+                    log.error("worker %d: device fault, exiting: %s", wid, e)
+                    os._exit(3)
+                out = {"error": f"{type(e).__name__}: {e}"}
+            st.set(f"res/{wid}/{k}", json.dumps(json_safe(out)))
+            k += 1
+    finally:
+        if hb is not None:
+            hb.stop()
+
+
+def join_cluster(host: str, port: int, device: torch.device, mem_mb: int = 0, timeout_s: float = 60.0) -> int:
+    """Join a running service as an extra worker (not a member of its process group): get
+    a worker id from the dispatcher's store, announce it, and serve assignments until the
+    service stops.  Datasets arrive host-staged; collectives are never asked of a joiner."""
+    import datetime
+
+    from torch.distributed import PrefixStore, TCPStore
+
+    raw = TCPStore(host, port, is_master=False, timeout=datetime.timedelta(seconds=timeout_s))
+    st = LockedStore(PrefixStore("dml", raw))   # the service's control plane (dist.service_store)
+    n = int(st.add("join/n", 1))
+    wid = MAX_WORKERS + n - 1
+    st.set(f"join/{n - 1}", json.dumps({"wid": wid, "device": str(device), "mem_mb": mem_mb, "pid": os.getpid()}))
+    core = WorkerCore(device, wid=wid, store=st, in_group=False)
+    worker_loop(core, None)
+    return wid
+
+
+# ---------------------------------------------------------------------------------------
+# rank 0: dispatcher
+# ---------------------------------------------------------------------------------------
+@dataclass
+class _JobState:
+    job: Job
+    plan: Dict[str, Any]
+    seq: int
+    msg: Dict[str, Any]
+    slices: List[List[int]]
+    est: List[float]                        # estimated seconds per slice
+    queue: Deque[int] = field(default_factory=collections.deque)
+    inflight: Set[int] = field(default_factory=set)
+    done: Dict[int, Any] = field(default_factory=dict)   # slice -> list[_Res]
+    metrics: Dict[int, Dict[int, Any]] = field(default_factory=dict)
+    mode: str = "task"                      # task | data
+    transport: str = "rccl"                 # rccl (collective epoch) | staged (host file)
+    staged_ready: bool = False
+    held: Optional[int] = None              # the last slice, published after the refit
+    refit_pending: bool = False
+    refit_inflight: bool = False
+    refit_candidate: int = -1
+    best: Any = None
+    finished: bool = False
+
+
+@dataclass
+class _Worker:
+    wid: int
+    in_group: bool
+    next_k: int = 0
+    busy: Optional[Dict[str, Any]] = None   # the in-flight assignment
+    sent_at: float = 0.0
+    est: float = 0.0
+    loaded: Set[str] = field(default_factory=set)
+    alive: bool = True
+    joined_at: float = 0.0
 
 
 class DistributedRunner(Runner):
-    """Rank-0 side: turns controller jobs into store announcements and publishes results."""
+    """Rank 0's dispatcher (runs in the main thread; the gateway serves from a thread and
+    rank 0's own worker runs in another)."""
 
     def __init__(self, core: WorkerCore):
         self.core = core
-        self.q: List[Job] = []
+        self.st = core.store
+        self.pending: List[Job] = []
         self._cv = threading.Condition()
         self.seq = 0
         self.stop = False
-        self.dead: set = set()
-        self._hb_missing_since: Dict[int, float] = {}
+        self.jobs: List[_JobState] = []
+        inf = dist.info()
+        self.world = inf.world
+        self.workers: Dict[int, _Worker] = {r: _Worker(r, True) for r in range(self.world)}
+        self.dead: Set[int] = set()
         self.session_used: Dict[str, float] = {}
+        self.epoch: Optional[Dict[str, Any]] = None     # a collective epoch waiting for / holding the group
+        self.epoch_queue: List[Dict[str, Any]] = []
+        self._hb_missing_since: Dict[int, float] = {}
+        self._joined = 0
+        self._stage_dir = os.environ.get("DML_STAGE_DIR") or (
+            tempfile.mkdtemp(prefix="dml_stage_", dir="/dev/shm") if os.path.isdir("/dev/shm") else tempfile.mkdtemp())
+        self._t0 = time.time()
 
     def bind(self, controller: Controller) -> None:
         super().bind(controller)
-        self.worker_ids = {}
-        for r in range(dist.info().world):
-            self.worker_ids[r] = controller.scheduler.register(f"rank{r}", 0, f"cuda:{r}")
+        self.worker_ids = {r: controller.scheduler.register(f"rank{r}", 0, f"cuda:{r}") for r in range(self.world)}
 
     def submit(self, job: Job) -> None:
         with self._cv:
-            self.q.append(job)
+            self.pending.append(job)
             self._cv.notify_all()
 
     def requeue(self, units) -> None:
@@ -300,287 +459,417 @@ class DistributedRunner(Runner):
             self.stop = True
             self._cv.notify_all()
 
-    # rank 0 main loop (runs in the main thread; the gateway serves from a thread)
-    def serve_forever(self, idle_poll_s: float = 0.5) -> None:
-        st = self.core.store
-        hb = _Heartbeat(st, 0)
+    # ---- main loop ---------------------------------------------------------------------
+    def serve_forever(self, idle_poll_s: float = 0.05) -> None:
+        w0 = threading.Thread(target=worker_loop, args=(self.core, self.ctl, False), daemon=True,
+                              name="dml-rank0-worker")
+        w0.start()
         try:
             while True:
                 with self._cv:
-                    while not self.q and not self.stop:
-                        self._cv.wait(timeout=idle_poll_s)
-                    if self.stop and not self.q:
-                        break
-                    # session fair share at job granularity: the next job comes from the
-                    # session that has used the least node time (ties: arrival order)
-                    k = min(range(len(self.q)), key=lambda i: (self.session_used.get(self.q[i].session_id, 0.0), i))
-                    job = self.q.pop(k)
-                t_job = time.time()
-                try:
-                    self._run_job(job)
-                except Exception as e:
-                    traceback.print_exc()
-                    for sub in job.subtasks:
-                        if sub.status not in ("completed", "failed"):
-                            self.ctl.table.finish_subtask(job.job_id, sub.subtask_id, "failed",
-                                                          error=f"{type(e).__name__}: {e}")
-                self.session_used[job.session_id] = self.session_used.get(job.session_id, 0.0) + time.time() - t_job
-            st.set(f"job/{self.seq}", json.dumps({"shutdown": True}))
+                    new = self.pending
+                    self.pending = []
+                    stopping = self.stop
+                for job in new:
+                    self._admit(job)
+                busy = self._poll_results()
+                self._membership()
+                self._liveness()
+                self._dispatch()
+                active = any(not js.finished for js in self.jobs) or any(
+                    w.busy is not None for w in self.workers.values() if w.alive)
+                if stopping and not active:
+                    break
+                if not active and not busy:
+                    with self._cv:
+                        if not self.pending and not self.stop:
+                            self._cv.wait(timeout=idle_poll_s)
+                else:
+                    time.sleep(POLL_S)
         finally:
-            hb.stop()
+            for w in self.workers.values():
+                if w.alive:
+                    self._assign(w, {"kind": "stop"})
+            w0.join(timeout=30)
+            self._cleanup_stage()
 
-    def _run_job(self, job: Job) -> None:
-        ctl, st = self.ctl, self.core.store
-        plan = job_plan(job.request)
-        ds_path = ctl.registry.find_file(job.dataset_id)
-        import os
+    # ---- admission -----------------------------------------------------------------------
+    def _admit(self, job: Job) -> None:
+        ctl = self.ctl
+        try:
+            plan = job_plan(job.request)
+            meta = ctl.registry.metadata(job.dataset_id)
+            n_rows = int(meta.get("n_rows", 1000))
+            n_feat = max(1, int(meta.get("n_cols", 2)) - 1)
+            todo = [sub.index for sub in job.subtasks if sub.status not in ("completed", "failed")]
+            if not todo:
+                return
+            data_par = self._data_parallel(plan, len(todo), n_rows, n_feat)
+            slices = plan_slices(ctl, plan, todo, int(n_rows * 0.8), n_feat, 2,
+                                 min_slices=1 if data_par else min(len(todo), 2 * self._n_alive()))
+            costs = candidate_costs(plan, int(n_rows * 0.8), n_feat, 2)
+            est = [ctl.scheduler.estimate(plan["model_type"], sum(costs[i] for i in ids)) for ids in slices]
+            seq = self.seq
+            self.seq += 1
+            msg = {"job_id": job.job_id, "session_id": job.session_id, "dataset_id": job.dataset_id,
+                   "dataset_key": dataset_key(ctl.registry, job.dataset_id, plan), "plan": plan,
+                   "slices": slices, "params": [sub.spec["parameters"] for sub in job.subtasks],
+                   "subtask_ids": [sub.subtask_id for sub in job.subtasks], "seed": job_seed(job.job_id),
+                   "keep_models": ctl.config.keep_models, "models_root": ctl.models.root}
+            js = _JobState(job, plan, seq, msg, slices, est, mode="data" if data_par else "task")
+            js.queue.extend(range(len(slices)))
+            # datasets travel by collective broadcast while the whole group is alive and
+            # nobody joined from outside it; otherwise host-staged
+            js.transport = "rccl" if (dist.info().is_dist and not self.dead) else "staged"
+            if js.transport == "staged" or self._joiners_alive():
+                self._stage(js)
+            self._publish_msg(js)
+            for ids in slices:
+                ctl.table.mark_running(job.job_id, ids, "cluster")
+            self.jobs.append(js)
+            self.session_used.setdefault(job.session_id, 0.0)
+            if js.mode == "data":
+                self.epoch_queue.append({"kind": "dp", "job": js})
+        except Exception as e:
+            traceback.print_exc()
+            self._fail_job(job, e)
 
-        meta = ctl.registry.metadata(job.dataset_id)
-        n_rows = int(meta.get("n_rows", 1000))
-        todo = [sub.index for sub in job.subtasks if sub.status not in ("completed", "failed")]
-        if not todo:
+    def _publish_msg(self, js: _JobState) -> None:
+        self.st.set(f"job/{js.seq}", json.dumps(json_safe(js.msg)))
+
+    def _stage(self, js: _JobState) -> None:
+        if js.staged_ready:
             return
-        world = dist.info().world
-        n_feat = max(1, int(meta.get("n_cols", 2)) - 1)
-        data_par = self._data_parallel(plan, len(todo), n_rows, n_feat, world)
-        slices = plan_slices(ctl, plan, todo, int(n_rows * 0.8), n_feat, 2,
-                             min_slices=1 if data_par else min(len(todo), 2 * world))
-        key = f"{ds_path}:{os.path.getmtime(ds_path)}:{plan['feature_columns']}:{plan['target_column']}:" \
-              f"{is_classifier(plan['model_type'])}"
-        seq = self.seq
-        self.seq += 1
-        msg = {"job_id": job.job_id, "dataset_id": job.dataset_id, "dataset_key": key, "plan": plan,
-               "slices": slices, "params": [sub.spec["parameters"] for sub in job.subtasks],
-               "subtask_ids": [sub.subtask_id for sub in job.subtasks], "seed": job_seed(job.job_id),
-               "mode": "data" if data_par else "task"}
-        st.set(f"job/{seq}", json.dumps(json_safe(msg)))
-        for ids in slices:
-            ctl.table.mark_running(job.job_id, ids, "cluster")
-        if data_par:
-            self._run_job_dp(job, plan, seq, msg, slices)
-            return
-        # progress publisher + liveness monitor while every rank (this one too) works
-        done_evt = threading.Event()
-        held: Dict[int, Any] = {}
-        mon = threading.Thread(target=self._monitor, args=(job, seq, slices, done_evt, held), daemon=True)
-        mon.start()
-        dd, scores, owned, mode = self._participate(seq, msg)
-        done_evt.set()
-        mon.join()
-        # collect everything not yet published
-        results_all = []
-        for i in range(len(slices)):
-            raw = st.get(f"job/{seq}/res/{i}")
-            for d in json.loads(raw):
-                results_all.append(_Res(d))
-        if mode == "collective":
-            self._check_scores(results_all, scores, owned, int(plan["cv"] or 0))
-        final = [held[i] for i in sorted(held)]
-        finalize_job(ctl, job, plan, dd, results_all)
-        for res, metrics in final:
-            publish_results(ctl, job, res, metrics)
-        self._cleanup(seq, len(slices))
+        ds = self.ctl.registry.load(js.job.dataset_id, js.plan["feature_columns"], js.plan["target_column"])
+        name = f"{zlib.crc32(js.msg['dataset_key'].encode()) & 0xFFFFFFFF:08x}.npz"
+        path = os.path.join(self._stage_dir, name)
+        if not os.path.exists(path):
+            pdata.stage_host(ds.X, ds.y, path)
+        js.msg["staged"] = path
+        js.staged_ready = True
+        self._publish_msg(js)
 
-    def _data_parallel(self, plan, n_todo: int, n_rows: int, n_feat: int, world: int) -> bool:
-        """Row-sharded data parallelism (parallel/data_parallel.py) instead of task slices."""
+    def _cleanup_stage(self) -> None:
+        import shutil
+
+        if not os.environ.get("DML_STAGE_DIR"):
+            shutil.rmtree(self._stage_dir, ignore_errors=True)
+
+    def _data_parallel(self, plan, n_todo: int, n_rows: int, n_feat: int) -> bool:
+        """Row-sharded data parallelism needs every rank of the group: never once one died."""
         par = plan.get("parallelism", "auto")
-        if par == "task" or world < 2 or not getattr(family_of(plan["model_type"]), "data_parallel", False):
+        if par == "task" or not dist.info().is_dist or self.dead or \
+                not getattr(family_of(plan["model_type"]), "data_parallel", False):
             return False
         if par == "data":
             return True
         cfg = self.ctl.config
         cells = n_rows * n_feat
-        return cells >= cfg.dp_min_cells and (n_todo < world or cells * 4 > cfg.dp_auto_gb * 2 ** 30)
+        return cells >= cfg.dp_min_cells and (n_todo < self.world or cells * 4 > cfg.dp_auto_gb * 2 ** 30)
 
-    def _run_job_dp(self, job: Job, plan, seq: int, msg, slices) -> None:
-        from ..engine.service import pick_refit, refit_model
+    def _fail_job(self, job: Job, e: Exception) -> None:
+        for sub in job.subtasks:
+            if sub.status not in ("completed", "failed"):
+                self.ctl.table.finish_subtask(job.job_id, sub.subtask_id, "failed", error=f"{type(e).__name__}: {e}")
 
-        ctl, st = self.ctl, self.core.store
-        done_evt = threading.Event()
-        held: Dict[int, Any] = {}
-        mon = threading.Thread(target=self._monitor, args=(job, seq, slices, done_evt, held), daemon=True)
-        mon.start()
-        # rank 0 runs the slices with everyone; the monitor publishes results as they land
-        results_all = []
-        refit_set, best = False, None
-        try:
-            dd = self.core.dataset_dp(msg, ctl)
-            params, sids = msg["params"], msg["subtask_ids"]
-            for i, ids in enumerate(slices):
-                results, metrics, wall = run_slice(plan, params, sids, dd, ids, "data-parallel", str(self.core.device),
-                                                   seed=msg["seed"])
-                st.set(f"job/{seq}/claim/{i}", "0")   # the monitor's wall-time observation reads it
-                st.set(f"job/{seq}/wall/{i}", str(wall))
-                st.set(f"job/{seq}/res/{i}", _enc_results(results, metrics))
-                st.add(f"job/{seq}/done", 1)
-                results_all.extend(results)
-            done_evt.set()
-            mon.join()
-            best = pick_refit(ctl, job, plan, results_all)
-            st.set(f"job/{seq}/refit", str(best.candidate if best is not None else -1))
-            refit_set = True
-            if best is not None:
-                try:
-                    model = refit_model(plan, params[best.candidate], dd)
-                    if model is not None:
-                        model["job_id"] = job.job_id
-                        model["subtask_id"] = job.subtasks[best.candidate].subtask_id
-                        model["feature_names"] = list(ctl.registry.load(job.dataset_id, plan["feature_columns"],
-                                                                        plan["target_column"]).feature_names)
-                        best.result["model_path"] = ctl.models.save(f"{job.subtasks[best.candidate].subtask_id}_model",
-                                                                    model)
-                except Exception:
-                    traceback.print_exc()
-        finally:
-            done_evt.set()
-            if not refit_set:
-                st.set(f"job/{seq}/refit", "-1")
-        path = best.result.get("model_path") if refit_set and best is not None else None
-        for res, metrics in [held[i] for i in sorted(held)]:
-            for x in res:
-                if path and x.candidate == best.candidate and x.ok:
-                    x.result["model_path"] = path
-            publish_results(ctl, job, res, metrics)
-        self._cleanup(seq, len(slices))
+    # ---- assignments -----------------------------------------------------------------------
+    def _n_alive(self) -> int:
+        return sum(1 for w in self.workers.values() if w.alive)
 
-    def _participate(self, seq, msg):
-        # decide collective vs store-only once every live rank has finished its claims
-        st = self.core.store
-        t = threading.Thread(target=self._decide_mode, args=(seq,), daemon=True)
-        t.start()
-        out = self.core.run(seq, msg, self.ctl)
-        t.join()
-        return out
+    def _joiners_alive(self) -> bool:
+        return any(w.alive and not w.in_group for w in self.workers.values())
 
-    def _decide_mode(self, seq):
-        st = self.core.store
-        world = dist.info().world
-        while True:
-            fin = int(st.add(f"job/{seq}/fin", 0))
-            alive = world - len(self.dead)
-            if fin >= alive:
-                break
-            time.sleep(0.05)
-        st.set(f"job/{seq}/mode", "collective" if not self.dead and self.core.collectives_ok else "store")
+    def _assign(self, w: _Worker, a: Dict[str, Any], est: float = 0.0) -> None:
+        k = w.next_k
+        w.next_k += 1
+        if a["kind"] != "stop":
+            w.busy = dict(a, k=k)
+            w.sent_at = time.time()
+            w.est = est
+        self.st.set(f"asg/{w.wid}/{k}", json.dumps(a))
 
-    def _monitor(self, job: Job, seq: int, slices, done_evt: threading.Event, held: Dict[int, Any]):
-        st, ctl = self.core.store, self.ctl
-        published = set()
-        world = dist.info().world
-        last = len(slices) - 1
-        while True:
-            finished = done_evt.is_set()
-            for i in range(len(slices)):
-                if i in published:
-                    continue
-                try:
-                    if not st.check([f"job/{seq}/res/{i}"]):
-                        continue
-                    raw = st.get(f"job/{seq}/res/{i}")
-                except Exception:
-                    continue
-                items = json.loads(raw)
-                res = [_Res(d) for d in items]
-                metrics = {d["candidate"]: d.get("metrics") for d in items}
-                published.add(i)
-                if i == last:
-                    held[i] = (res, metrics)   # published after the best model is refit
-                else:
-                    publish_results(ctl, job, res, metrics)
-                try:
-                    wall = float(st.get(f"job/{seq}/wall/{i}"))
-                    claim = int(st.get(f"job/{seq}/claim/{i}"))
-                    from ..engine.scheduler import Unit
-
-                    ctl.scheduler.observe(self.worker_ids.get(claim, "1"),
-                                          Unit(unit_id=f"{job.job_id}:{i}", cost=1.0, algo=job.model_type), wall)
-                except Exception:
-                    pass
-            self._liveness(seq, slices, published)
-            if finished and len(published) >= len(slices):
+    def _dispatch(self) -> None:
+        # a collective epoch owns the process group until every rank has answered
+        if self.epoch is not None:
+            return
+        if self.epoch_queue:
+            ep = self.epoch_queue[0]
+            js = ep["job"]
+            group = [w for w in self.workers.values() if w.in_group]
+            if self.dead or any(not w.alive for w in group):
+                # the group is broken: a data-parallel job runs task-parallel instead
+                self.epoch_queue.pop(0)
+                if ep["kind"] == "dp":
+                    js.mode = "task"
+                    if js.transport == "rccl":
+                        js.transport = "staged"
+                        self._stage(js)
                 return
-            if finished:
-                time.sleep(0.01)
-            else:
-                time.sleep(0.05)
+            if all(w.busy is None for w in group):
+                self.epoch_queue.pop(0)
+                self.epoch = {"kind": ep["kind"], "job": js, "waiting": {w.wid for w in group}}
+                for w in group:
+                    self._assign(w, {"kind": ep["kind"], "seq": js.seq})
+                return
+            return   # drain: no new slices until the group is idle
+        # refits go to rank 0 (it owns the controller and saves the artefact)
+        w0 = self.workers[0]
+        for js in self.jobs:
+            if js.refit_pending and w0.busy is None:
+                key = js.msg["dataset_key"]
+                if key not in w0.loaded and js.transport == "rccl":
+                    self._request_load(js)
+                    return
+                self._assign(w0, {"kind": "refit", "seq": js.seq, "candidate": js.refit_candidate})
+                js.refit_pending = False
+                js.refit_inflight = True
+        for w in sorted(self.workers.values(), key=lambda w: w.wid):
+            if not w.alive or w.busy is not None:
+                continue
+            js, i = self._next_slice(w)
+            if js is None:
+                if self.epoch_queue:
+                    return
+                continue
+            js.queue.remove(i)
+            js.inflight.add(i)
+            est = js.est[i]
+            self.session_used[js.job.session_id] = self.session_used.get(js.job.session_id, 0.0) + est
+            self._assign(w, {"kind": "slice", "seq": js.seq, "slice": i, "ids": js.slices[i]}, est)
 
-    def _liveness(self, seq, slices, published):
-        st = self.core.store
+    def _next_slice(self, w: _Worker):
+        """Fair share: the next slice comes from the job of the least-served session (ties:
+        admission order) among the jobs this worker can run now."""
+        cands = []
+        for js in self.jobs:
+            if js.finished or js.mode != "task" or not js.queue:
+                continue
+            key = js.msg["dataset_key"]
+            if key not in w.loaded:
+                if js.transport == "rccl" and w.in_group:
+                    self._request_load(js)
+                    continue
+                if not js.staged_ready:
+                    self._stage(js)
+            cands.append(js)
+        if not cands:
+            return None, None
+        js = min(cands, key=lambda j: (self.session_used.get(j.job.session_id, 0.0), j.seq))
+        return js, js.queue[0]
+
+    def _request_load(self, js: _JobState) -> None:
+        if not any(ep["kind"] == "load" and ep["job"].msg["dataset_key"] == js.msg["dataset_key"]
+                   for ep in self.epoch_queue):
+            self.epoch_queue.append({"kind": "load", "job": js})
+
+    # ---- results ----------------------------------------------------------------------------
+    def _poll_results(self) -> bool:
+        got = False
+        for w in list(self.workers.values()):
+            if w.busy is None:
+                continue
+            key = f"res/{w.wid}/{w.busy['k']}"
+            if not self.st.check([key]):
+                continue
+            out = json.loads(self.st.get(key))
+            self.st.delete_key(key)
+            a = w.busy
+            w.busy = None
+            got = True
+            if "fatal" in out:
+                log.error("worker %d reported a device fault (%s): re-queueing its work", w.wid, out["fatal"])
+                self._declare_dead(w, a)
+                continue
+            self._on_result(w, a, out)
+        return got
+
+    def _on_result(self, w: _Worker, a: Dict[str, Any], out: Dict[str, Any]) -> None:
+        kind = a["kind"]
+        js = self._job(a.get("seq"))
+        if kind == "load":
+            if "cache" in out:
+                w.loaded = set(out["cache"])
+            if "error" in out and js is not None and js.transport == "rccl":
+                log.error("collective load of %s failed on worker %d (%s): host-staging it", js.job.dataset_id,
+                          w.wid, out["error"])
+                js.transport = "staged"
+                self._stage(js)
+            self._epoch_answer(w)
+            return
+        if kind == "dp":
+            self._epoch_answer(w)
+            if w.wid == 0 and js is not None:
+                self._finish_dp(js, out)
+            return
+        if js is None:
+            return
+        if kind == "refit":
+            js.refit_inflight = False
+            self._finish_job(js, out.get("model_path"))
+            return
+        # slice
+        i = a["slice"]
+        js.inflight.discard(i)
+        if "cache" in out:
+            w.loaded = set(out["cache"])
+        if "error" in out:   # the whole slice raised outside the executor: its candidates fail
+            res = [_Res({"candidate": c, "ok": False, "error": out["error"]}) for c in a["ids"]]
+            metrics = {}
+        else:
+            res = [_Res(d) for d in out["results"]]
+            metrics = {d["candidate"]: d.get("metrics") for d in out["results"]}
+        wall = float(out.get("wall", 0.0))
+        sid = js.job.session_id
+        self.session_used[sid] = self.session_used.get(sid, 0.0) - w.est + wall
+        try:
+            from ..engine.scheduler import Unit
+
+            self.ctl.scheduler.observe(self.worker_ids.get(w.wid, f"rank{w.wid}"),
+                                       Unit(unit_id=f"{js.job.job_id}:{i}", cost=1.0, algo=js.job.model_type), wall)
+        except Exception:
+            pass
+        if i in js.done:   # a re-queued slice finished twice: count it once
+            return
+        js.done[i] = res
+        js.metrics[i] = metrics
+        if len(js.done) < len(js.slices):
+            publish_results(self.ctl, js.job, res, metrics)
+            return
+        js.held = i
+        self._complete(js)
+
+    def _complete(self, js: _JobState) -> None:
+        """Every slice is in: refit the winner (on rank 0), then publish the held slice."""
+        results_all = [r for i in sorted(js.done) for r in js.done[i]]
+        best = pick_refit(self.ctl, js.job, js.plan, results_all)
+        js.best = best
+        if best is None:
+            self._finish_job(js, None)
+            return
+        js.refit_candidate = best.candidate
+        js.refit_pending = True
+
+    def _finish_job(self, js: _JobState, model_path: Optional[str]) -> None:
+        best = getattr(js, "best", None)
+        if best is not None and model_path:
+            best.result["model_path"] = model_path
+        if js.held is not None:
+            publish_results(self.ctl, js.job, js.done[js.held], js.metrics.get(js.held, {}))
+        js.finished = True
+        self._cleanup_job(js)
+
+    def _finish_dp(self, js: _JobState, out: Dict[str, Any]) -> None:
+        if "error" in out:
+            self._fail_job(js.job, RuntimeError(out["error"]))
+            js.finished = True
+            return
+        slices = out.get("dp_slices", [])
+        best_i, path = out.get("refit", -1), out.get("model_path")
+        for n, sl in enumerate(slices):
+            res = [_Res(d) for d in sl["results"]]
+            metrics = {d["candidate"]: d.get("metrics") for d in sl["results"]}
+            if path:
+                for x in res:
+                    if x.candidate == best_i and x.ok:
+                        x.result["model_path"] = path
+            js.done[n] = res
+            publish_results(self.ctl, js.job, res, metrics)
+        js.finished = True
+        self._cleanup_job(js)
+
+    def _epoch_answer(self, w: _Worker) -> None:
+        if self.epoch is None:
+            return
+        self.epoch["waiting"].discard(w.wid)
+        if not self.epoch["waiting"]:
+            self.epoch = None
+
+    def _job(self, seq) -> Optional[_JobState]:
+        if seq is None:
+            return None
+        for js in self.jobs:
+            if js.seq == seq:
+                return js
+        return None
+
+    def _cleanup_job(self, js: _JobState) -> None:
+        self.st.delete_key(f"job/{js.seq}")
+        self.st.delete_key(f"job/{js.seq}/refit")
+        self.jobs = [j for j in self.jobs if not j.finished]
+
+    # ---- membership and liveness ------------------------------------------------------------
+    def _membership(self) -> None:
+        """Workers that joined from outside the process group (join_cluster)."""
+        try:
+            n = int(self.st.add("join/n", 0))
+        except Exception:
+            return
+        while self._joined < n:
+            key = f"join/{self._joined}"
+            if not self.st.check([key]):
+                return
+            info = json.loads(self.st.get(key))
+            wid = int(info["wid"])
+            self.workers[wid] = _Worker(wid, False, joined_at=time.time())
+            self.worker_ids[wid] = self.ctl.scheduler.register(f"rank{wid}", int(info.get("mem_mb", 0)),
+                                                               info.get("device", "cpu"))
+            log.info("worker %d joined (%s)", wid, info.get("device"))
+            self._joined += 1
+            for js in self.jobs:   # joiners read host-staged datasets
+                if not js.finished and not js.staged_ready:
+                    self._stage(js)
+
+    def leave(self, worker_id: str) -> bool:
+        for wid, sid in list(self.worker_ids.items()):
+            if sid == worker_id:
+                return self.remove_worker(wid)
+        return False
+
+    def remove_worker(self, wid: int) -> bool:
+        """Graceful leave (/unsubscribe): finish the current assignment, get no more."""
+        w = self.workers.get(wid)
+        if w is None or not w.alive or w.in_group:
+            return False
+        self._assign(w, {"kind": "stop"})
+        w.alive = False
+        return True
+
+    def _liveness(self) -> None:
         now = time.time()
-        world = dist.info().world
-        for r in range(1, world):
-            if r in self.dead:
+        for w in list(self.workers.values()):
+            if w.wid == 0 or not w.alive:
                 continue
             try:
-                hb = float(st.get(f"hb/{r}")) if st.check([f"hb/{r}"]) else None
+                hb = float(self.st.get(f"hb/{w.wid}")) if self.st.check([f"hb/{w.wid}"]) else None
             except Exception:
                 hb = now
             if hb is None:   # never beat: silent since we first looked
-                hb = self._hb_missing_since.setdefault(r, now)
+                hb = self._hb_missing_since.setdefault(w.wid, now)
             if now - hb > self.ctl.config.dead_after_s:
-                log.warning("rank %d missed heartbeats for %.1fs: re-queueing its slices", r, now - hb)
-                self.dead.add(r)
-                self.ctl.scheduler.unsubscribe(self.worker_ids.get(r, ""))
-                for i in range(len(slices)):
-                    if i in published:
-                        continue
-                    try:
-                        if st.check([f"job/{seq}/claim/{i}"]) and int(st.get(f"job/{seq}/claim/{i}")) == r:
-                            j = int(st.add(f"job/{seq}/rq_len", 1)) - 1
-                            st.set(f"job/{seq}/rq/{j}", str(i))
-                    except Exception:
-                        pass
+                log.warning("worker %d missed heartbeats for %.1fs: declared dead", w.wid, now - hb)
+                self._declare_dead(w, w.busy)
             else:
-                self.ctl.scheduler.heartbeat(self.worker_ids.get(r, ""))
+                self.ctl.scheduler.heartbeat(self.worker_ids.get(w.wid, ""))
         self.ctl.scheduler.heartbeat(self.worker_ids.get(0, ""))
 
-    @staticmethod
-    def _check_scores(results, scores, owned, n_cv):
-        if not n_cv:
-            return
-        sc = scores.cpu().numpy()
-        for r in results:
-            if not r.ok:
-                continue
-            mine = np.array([np.nan if v is None else v for v in r.result.get("cv_scores", [])], dtype=np.float64)
-            if mine.size and not np.allclose(mine, sc[r.candidate, :mine.size], equal_nan=True, atol=1e-9):
-                log.error("RCCL score matrix disagrees with store results for candidate %d", r.candidate)
-
-    def _cleanup(self, seq: int, n: int) -> None:
-        st = self.core.store
-        for k in [f"job/{seq}"] + [f"job/{seq}/{s}/{i}" for s in ("res", "claim", "wall", "first", "rq_claim")
-                                   for i in range(n)]:
-            try:
-                st.delete_key(k)
-            except Exception:
-                pass
-
-
-def worker_loop(core: WorkerCore) -> None:
-    """Ranks 1..N-1: wait for job announcements and run them until shutdown."""
-    st = core.store
-    hb = _Heartbeat(st, core.inf.rank)
-    seq = 0
-    try:
-        while True:
-            key = f"job/{seq}"
-            while True:
-                try:
-                    st.wait([key], __import__("datetime").timedelta(seconds=60))
-                    break
-                except TimeoutError:
-                    continue  # idle longer than the store timeout: keep waiting
-                except Exception:   # the store (hosted by rank 0) is gone: the job server exited
-                    log.warning("rank %d lost the controller store; leaving", core.inf.rank)
-                    return
-            msg = json.loads(st.get(key))
-            if msg.get("shutdown"):
-                return
-            try:
-                core.run(seq, msg, None)
-            except Exception:
-                traceback.print_exc()
-                st.add(f"job/{seq}/fin", 1)
-            seq += 1
-    finally:
-        hb.stop()
+    def _declare_dead(self, w: _Worker, a: Optional[Dict[str, Any]]) -> None:
+        w.alive = False
+        w.busy = None
+        if w.in_group:
+            self.dead.add(w.wid)
+        self.ctl.scheduler.unsubscribe(self.worker_ids.get(w.wid, ""))
+        if a is not None and a["kind"] == "slice":
+            js = self._job(a["seq"])
+            if js is not None and a["slice"] not in js.done:
+                js.inflight.discard(a["slice"])
+                js.queue.appendleft(a["slice"])   # re-queued first: it has waited longest
+        if self.epoch is not None:
+            # a collective cannot complete without this rank: the survivors of the epoch time
+            # out (DML_COLLECTIVE_TIMEOUT_S); the dispatcher stops waiting for the dead one
+            self._epoch_answer(w)
+        # the group is broken for good: pending collectives become host-staged / task-parallel
+        if w.in_group:
+            for js in self.jobs:
+                if not js.finished and js.transport == "rccl":
+                    js.transport = "staged"
+                    self._stage(js)

@@ -1,35 +1,98 @@
 """Launcher: ``python -m cs230_distributed_machine_learning_amd.serve --gpus 8 --port 5001``.
 
 One process per GPU (torch.distributed over RCCL).  Rank 0 runs the controller, the
-HTTP gateway (same routes as the reference master + scheduler) and is itself a worker;
-ranks 1..N-1 are workers.  With ``--gpus 1`` (or no GPU) everything runs in one
-process with the local runner.  Replaces the reference's docker-compose topology of
-master + scheduler + 4 workers + Kafka + Redis (aws-prod/docker-compose.yml).
+HTTP gateway (same routes as the reference master + scheduler), the dispatcher, and is
+itself a worker; ranks 1..N-1 are workers.  With ``--gpus 1`` (or no GPU) everything
+runs in one process with the local runner.  Replaces the reference's docker-compose
+topology of master + scheduler + 4 workers + Kafka + Redis (aws-prod/docker-compose.yml).
+
+The parent process (which never touches a GPU) starts the ranks as its own children
+and supervises them: a worker rank that dies is reported and NOT restarted -- the
+dispatcher on rank 0 re-queues its work to the survivors -- and rank 0 (the service)
+keeps running; only rank 0 exiting ends the service.  (torchrun's elastic agent would
+instead tear the whole group down, controller included, when any worker exits.)
+
+Extra capacity can join a running service at any time (elastic membership, reference
+aws-prod/scheduler/scheduler.py:105-117):
+``python -m cs230_distributed_machine_learning_amd.serve --join 127.0.0.1:29541 --device cuda:3``
 """
 from __future__ import annotations
 
 import argparse
 import os
+import signal
 import subprocess
 import sys
+import time
+
+
+def _supervise(args, argv) -> int:
+    """Start one child per rank (before any GPU call here) and supervise them."""
+    env0 = dict(os.environ)
+    env0.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env0.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(args.master_port), WORLD_SIZE=str(args.gpus))
+    procs = []
+    for r in range(args.gpus):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, "-m", "cs230_distributed_machine_learning_amd.serve"] + argv,
+                                      env=env))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+
+    signal.signal(signal.SIGTERM, stop)
+    reported = set()
+    try:
+        while True:
+            rc0 = procs[0].poll()
+            if rc0 is not None:          # the service (rank 0) ended: stop the workers
+                stop()
+                deadline = time.time() + 30
+                for p in procs[1:]:
+                    try:
+                        p.wait(timeout=max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                return rc0
+            for r, p in enumerate(procs[1:], start=1):
+                rc = p.poll()
+                if rc is not None and r not in reported:
+                    reported.add(r)
+                    print(f"[serve] rank {r} exited with code {rc}; rank 0 re-queues its work to the survivors",
+                          file=sys.stderr, flush=True)
+            time.sleep(0.5)
+    except KeyboardInterrupt:
+        stop()
+        return 130
 
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description="distributed-ml (MI355X) service")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--master-port", type=int, default=29541)
+    ap.add_argument("--join", default=None, metavar="HOST:PORT",
+                    help="join a running service (its --master-port) as an extra worker")
     from .config import Config
 
     Config.add_cli(ap)
+    argv = list(argv if argv is not None else sys.argv[1:])
     args = ap.parse_args(argv)
+    if args.join:
+        from .parallel.runner import join_cluster
+        import torch
+
+        host, _, port = args.join.rpartition(":")
+        dev = torch.device(args.device if args.device not in (None, "auto") else
+                           ("cuda:0" if torch.cuda.is_available() else "cpu"))
+        if dev.type == "cuda":
+            torch.cuda.set_device(dev)
+        wid = join_cluster(host or "127.0.0.1", int(port), dev)
+        print(f"[serve] worker {wid} left the cluster", file=sys.stderr)
+        return 0
     if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
-        # re-launch one rank per GPU before touching the GPU in this process
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-               "--master-addr", "127.0.0.1", "--master-port", str(args.master_port), "-m",
-               "cs230_distributed_machine_learning_amd.serve"] + (argv if argv is not None else sys.argv[1:])
-        env = dict(os.environ)
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        return subprocess.call(cmd, env=env)
+        return _supervise(args, argv)
 
     cfg = Config.from_args(args)
     from .utils.log import get_logger
@@ -61,6 +124,8 @@ def main(argv=None) -> int:
             runner.serve_forever()
         except KeyboardInterrupt:
             runner.shutdown()
+        if runner.dead:
+            os._exit(0)   # a peer is gone: the process-group teardown would wait for it
     else:
         worker_loop(core)
     dist.destroy()

@@ -124,6 +124,15 @@ def _rank_main(rank, world, port, root, outq):
                     st, ack = ctl.train(sid, _j1(jid, "LogisticRegression", grid))
                     ctl.table.wait_finished(ack["job_id"], timeout=120)
                     out.append((ctl.check_status(sid, ack["job_id"])[1], ctl.metrics(sid, ack["job_id"])[1]))
+                # a NEW dataset after the death: the group can no longer broadcast, so the
+                # table is host-staged to the survivors; must finish well inside 60 s
+                ctl.download_data(sid, {"dataset_url": "wine", "dataset_name": "wine", "dataset_type": "sklearn"})
+                t0 = time.time()
+                body = _j1("j-newdata", "LogisticRegression", {"C": [0.1, 1.0, 10.0]})
+                body["dataset_id"] = "wine"
+                st, ack = ctl.train(sid, body)
+                ctl.table.wait_finished(ack["job_id"], timeout=120)
+                out.append((ctl.check_status(sid, ack["job_id"])[1], time.time() - t0))
                 outq.put(("ok", out, sorted(runner.dead)))
             except Exception:  # pragma: no cover
                 import traceback
@@ -159,7 +168,7 @@ def test_killed_rank_slices_are_requeued():
             if p.is_alive():
                 p.kill()
     assert out[0] == "ok", out[1]
-    (st1, m1), (st2, m2) = out[1]
+    (st1, m1), (st2, m2), (st3, t3) = out[1]
     assert out[2] == [2]                                   # rank 2 was declared dead
     assert procs[2].exitcode == 17                         # ... because it crashed (injected)
     assert st1["job_status"] == "completed" and len(st1["job_result"]["results"]) == 12
@@ -167,3 +176,6 @@ def test_killed_rank_slices_are_requeued():
     assert {m["worker_id"] for m in m1} <= {"rank0", "rank1", "rank2"}
     assert st2["job_status"] == "completed" and len(st2["job_result"]["results"]) == 2
     assert {m["worker_id"] for m in m2} <= {"rank0", "rank1"}
+    # recovery: a job on a dataset no survivor holds yet completes on the survivors
+    assert st3["job_status"] == "completed" and len(st3["job_result"]["results"]) == 3, st3
+    assert t3 < 60, t3

@@ -1,0 +1,99 @@
+"""The RCCL path on one MI355X: a real ``nccl`` (= RCCL) process group at world size 1.
+
+The multi-GPU bench and the cluster runner call RCCL at N=8 on the driver's node; this
+test makes every one of those calls execute on the one GPU we have (``DML_FORCE_PG=1``
+builds the group even for one rank): ``all_gather_into_tensor``, ``broadcast``,
+``all_reduce`` SUM/MAX, ``barrier(device_ids=...)``, the dataset broadcast + shared
+bin edges, the row scatter of a data-parallel job, and then the DistributedRunner +
+worker loop end to end (RF and LR grid searches, one row-sharded LR job) on that group.
+Reference channels replaced: aws-prod/scheduler/scheduler_service.py:268-273 (Kafka
+`train` routing), aws-prod/worker/worker.py:253 (Kafka `result`).
+"""
+import os
+import socket
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from cs230_distributed_machine_learning_amd.config import Config
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _job(model, grid, cv=3, par=None):
+    tp = {"target_column": "species", "test_size": 0.25, "random_state": 0}
+    if par:
+        tp["parallelism"] = par
+    return {"dataset_id": "iris", "train_params": tp,
+            "model_details": {"model_type": model, "search_type": "GridSearchCV",
+                              "hyperparameters": {"base_estimator_params": {}, "search_params": {"param_grid": grid},
+                                                  "cv_params": {"cv": cv}}}}
+
+
+@pytest.mark.gpu
+def test_rccl_world1_collectives_and_cluster_runner(tmp_path, monkeypatch):
+    for k, v in dict(DML_FORCE_PG="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
+                     WORLD_SIZE="1", LOCAL_RANK="0").items():
+        monkeypatch.setenv(k, v)
+    from cs230_distributed_machine_learning_amd.engine.service import Controller
+    from cs230_distributed_machine_learning_amd.parallel import data as pdata
+    from cs230_distributed_machine_learning_amd.parallel import dist
+    from cs230_distributed_machine_learning_amd.parallel.runner import DistributedRunner, WorkerCore
+
+    dist.destroy()
+    inf = dist.init(want_gpu=True, timeout_s=300)
+    try:
+        assert inf.backend == "nccl" and inf.is_dist and inf.device.type == "cuda"
+        dev = inf.device
+        x = torch.arange(24, dtype=torch.float32, device=dev).reshape(6, 4)
+        assert torch.equal(dist.all_gather_rows(x), x)                 # all_gather_into_tensor
+        b = x.clone()
+        dist.broadcast(b, 0)
+        assert torch.equal(b, x)
+        s = x.clone()
+        dist.all_reduce_sum(s)
+        assert torch.equal(s, x)
+        m = x.clone()
+        dist.all_reduce_max(m)
+        assert torch.equal(m, x)
+        dist.barrier()                                                 # barrier(device_ids=[0])
+        Xd, yh = pdata.broadcast_table(np.arange(40, dtype=np.float32).reshape(10, 4), np.arange(10), dev)
+        assert Xd.device == dev and float(Xd.sum()) == float(np.arange(40).sum()) and len(yh) == 10
+        torch.cuda.synchronize()
+
+        core = WorkerCore(dev)
+        runner = DistributedRunner(core)
+        ctl = Controller(Config(data_root=str(tmp_path), device="cuda:0", chunk_target_s=0.0), runner=runner)
+        t = threading.Thread(target=runner.serve_forever, daemon=True)
+        t.start()
+        try:
+            sid = ctl.create_session()[1]["session_id"]
+            assert ctl.download_data(sid, {"dataset_url": "iris", "dataset_name": "iris",
+                                           "dataset_type": "sklearn"})[0] == 200
+            out = {}
+            for name, body in (("rf", _job("RandomForestClassifier", {"n_estimators": [10], "max_depth": [3, None]})),
+                               ("lr", _job("LogisticRegression", {"C": [0.1, 1.0, 10.0]})),
+                               ("lr_dp", _job("LogisticRegression", {"C": [1.0, 10.0]}, par="data"))):
+                st, ack = ctl.train(sid, body)
+                assert st in (200, 202), ack
+                assert ctl.table.wait_finished(ack["job_id"], timeout=300)
+                out[name] = (ctl.check_status(sid, ack["job_id"])[1], ctl.metrics(sid, ack["job_id"])[1])
+        finally:
+            runner.shutdown()
+            t.join(timeout=120)
+        for name, (status, metrics) in out.items():
+            assert status["job_status"] == "completed", (name, status)
+            assert status["best_result"]["mean_cv_score"] > 0.85, (name, status["best_result"])
+        assert {m["worker_id"] for m in out["rf"][1]} == {"rank0"}
+        assert {m["worker_id"] for m in out["lr_dp"][1]} == {"data-parallel"}
+        assert all(js.transport == "rccl" for js in runner.jobs) and not runner.dead
+    finally:
+        dist.destroy()
