@@ -7,7 +7,8 @@ per GPU and at least one slice per rank.  Data-parallel mode covers the other tw
 cases — a table larger than one GPU wants to hold, or fewer fits than ranks:
 
 * ``scatter_table``: rank 0 parses the table once; every rank receives only its
-  contiguous row block ``[r0, r1)`` (one RCCL scatter per tensor).  Labels are tiny
+  contiguous row block ``[r0, r1)`` (chunked RCCL point-to-point sends; rank 0's device
+  holds its own block plus one chunk).  Labels are tiny
   and are broadcast whole, so every rank builds the SAME global CV/holdout split roles.
 * ``RowShard``: a ``DeviceData`` over the local rows whose split bookkeeping is global:
   local ``roles``/``train_rows``/``test_rows`` index the shard, ``train_counts`` and
@@ -37,6 +38,9 @@ from ..search.cv import ROLE_TEST, ROLE_TRAIN
 from . import dist
 
 
+SCATTER_CHUNK_BYTES = 256 << 20
+
+
 def shard_bounds(n: int, world: int, rank: int):
     """Contiguous row block of ``rank``: sizes differ by at most one row."""
     base, rem = divmod(n, world)
@@ -47,8 +51,9 @@ def shard_bounds(n: int, world: int, rank: int):
 def scatter_table(X: Optional[np.ndarray], y: Optional[np.ndarray], device: torch.device):
     """Rank 0 passes host arrays; every rank returns (X_shard_dev, y_global_host, r0).
 
-    X moves as one scatter (each rank receives only its rows, padded to the largest
-    block); y (n values) is broadcast to every rank."""
+    X moves by chunked point-to-point sends from rank 0 (each rank receives only its
+    rows; rank 0 holds its own block plus one chunk); y (n values) is broadcast to
+    every rank."""
     inf = dist.info()
     if not inf.is_dist:
         return torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).to(device), np.asarray(y), 0
@@ -68,31 +73,37 @@ def scatter_table(X: Optional[np.ndarray], y: Optional[np.ndarray], device: torc
         st.wait([key])
         meta = json.loads(st.get(key))
     n, d, world = meta["n"], meta["d"], inf.world
-    blk = shard_bounds(n, world, 0)[1]
     r0, r1 = shard_bounds(n, world, inf.rank)
-    recv = torch.empty((blk, d), dtype=torch.float32, device=device)
-    parts = None
+    recv = torch.empty((r1 - r0, d), dtype=torch.float32, device=device)
+    # rank 0 keeps only its own block resident: every other rank's rows leave in
+    # row chunks of <= SCATTER_CHUNK_BYTES, one point-to-point send at a time, so rank 0's
+    # device never holds more than its block plus one chunk (a table larger than one GPU
+    # wants to hold is exactly what this mode is for)
+    ch = max(1, SCATTER_CHUNK_BYTES // max(1, 4 * d))
     if inf.rank == 0:
         Xt = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32))
-        parts = []
-        for k in range(world):
+        recv.copy_(Xt[r0:r1])
+        for k in range(1, world):
             a, b = shard_bounds(n, world, k)
-            p = torch.zeros((blk, d), dtype=torch.float32)
-            p[:b - a] = Xt[a:b]
-            parts.append(p.to(device))
-    torch.distributed.scatter(recv, parts, src=0)
+            for c0 in range(a, b, ch):
+                c1 = min(b, c0 + ch)
+                torch.distributed.send(Xt[c0:c1].to(device), dst=k)
+    else:
+        for c0 in range(r0, r1, ch):
+            c1 = min(r1, c0 + ch)
+            torch.distributed.recv(recv[c0 - r0:c1 - r0], src=0)
     yd = torch.from_numpy(y_num).to(device) if inf.rank == 0 else torch.empty((n,), dtype=torch.float64, device=device)
     dist.broadcast(yd, 0)
     dist.barrier()
     if inf.rank == 0:
         st.delete_key(key)
-        return recv[:r1 - r0].contiguous(), y, r0
+        return recv, y, r0
     y_host = yd.cpu().numpy()
     if meta["y"] == "codes":
         y_host = np.asarray(meta["classes"], dtype=object)[y_host.astype(np.int64)]
     else:
         y_host = y_host.astype(np.dtype(meta["y"]))
-    return recv[:r1 - r0].contiguous(), y_host, r0
+    return recv, y_host, r0
 
 
 class RowShard(DeviceData):
