@@ -100,12 +100,9 @@ def config4(dev, rows):
           best_mean_cv=round(max(r.result["mean_cv_score"] for r in ok), 4))
 
 
-def config5(dev):
-    from cs230_distributed_machine_learning_amd.config import Config
-    from cs230_distributed_machine_learning_amd.engine.service import Controller
+def _config5_data(root):
     import pandas as pd
 
-    root = tempfile.mkdtemp()
     rng = np.random.RandomState(0)
     n, d = 200_000, 20
     X = rng.randn(n, d).astype(np.float32)
@@ -114,7 +111,9 @@ def config5(dev):
     df["label"] = y
     os.makedirs(os.path.join(root, "datasets", "mixed"), exist_ok=True)
     df.to_csv(os.path.join(root, "datasets", "mixed", "mixed.csv"), index=False)
-    ctl = Controller(Config(data_root=root, device=str(dev)))
+
+
+def _config5_drive(ctl, runner_name):
     jobs = []
     t0 = time.time()
     for s in range(4):
@@ -135,12 +134,55 @@ def config5(dev):
             assert st == 200
             jobs.append((sid, jid))
     fits = 0
+    workers = set()
     for sid, jid in jobs:
         ctl.table.wait_finished(jid, timeout=3600)
         st = ctl.check_status(sid, jid)[1]
         assert st["job_status"] == "completed", st
         fits += st["total_subtasks"] * 6
-    _emit(5, fits, time.time() - t0, jobs=len(jobs), sessions=4)
+        workers |= {m.get("worker_id") for m in ctl.metrics(sid, jid)[1]}
+    _emit(5, fits, time.time() - t0, jobs=len(jobs), sessions=4, runner=runner_name, workers=sorted(workers))
+
+
+def config5(dev):
+    """Mixed queue through the controller: the local runner on one process, or -- under
+    torchrun / DML_FORCE_PG=1 -- the cluster DistributedRunner (rank 0 dispatches, every
+    rank works), the path BASELINE config 5 names for 8 GPUs."""
+    from cs230_distributed_machine_learning_amd.config import Config
+    from cs230_distributed_machine_learning_amd.engine.service import Controller
+
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("DML_FORCE_PG") == "1":
+        import threading
+
+        from cs230_distributed_machine_learning_amd.parallel import dist
+        from cs230_distributed_machine_learning_amd.parallel.runner import DistributedRunner, WorkerCore, worker_loop
+
+        inf = dist.init(want_gpu=dev.type == "cuda")
+        core = WorkerCore(inf.device)
+        if inf.rank == 0:
+            root = tempfile.mkdtemp()
+            _config5_data(root)
+            runner = DistributedRunner(core)
+            ctl = Controller(Config(data_root=root, device=str(inf.device)), runner=runner)
+
+            def drive():
+                try:
+                    _config5_drive(ctl, f"distributed x{inf.world}")
+                finally:
+                    runner.shutdown()
+
+            t = threading.Thread(target=drive, daemon=True)
+            t.start()
+            runner.serve_forever()
+            t.join()
+        else:
+            worker_loop(core)
+        dist.destroy()
+        return
+    root = tempfile.mkdtemp()
+    _config5_data(root)
+    ctl = Controller(Config(data_root=root, device=str(dev)))
+    _config5_drive(ctl, "local")
     ctl.shutdown()
 
 
@@ -148,7 +190,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="1,2,4,5")
     ap.add_argument("--lr-rows", type=int, default=2_000_000)
+    ap.add_argument("--gpus", type=int, default=1, help="config 5 on N ranks (relaunches under torchrun)")
     args = ap.parse_args()
+    if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        import subprocess
+
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", "29571", os.path.abspath(__file__),
+               "--configs", "5"]
+        return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
     dev = torch.device("cuda:0" if torch.cuda.is_available() else "cpu")
     want = {int(c) for c in args.configs.split(",")}
     if 1 in want:
@@ -162,4 +212,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
