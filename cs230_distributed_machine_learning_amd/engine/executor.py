@@ -120,6 +120,10 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
 
         forest_ops.ARENA.clear(data.device)   # idle forest buffers back to the device for this family
     keep = spec.keep_models in ("all", "best")
+    if keep and "holdout" in names:   # only the holdout fit's model is reported (J4 model_path)
+        hold = names.index("holdout")
+        for t in tasks:
+            t.keep = t.split == hold
     outputs: Dict[int, FitOutput] = {}
     if tasks:
         try:

@@ -26,6 +26,7 @@ class FitTask:
     model_type: str
     params: Dict[str, Any]
     seed: int = 0
+    keep: bool = True           # with keep_models: this fit's model is wanted (holdout fits only, when there is one)
 
 
 @dataclass

@@ -361,6 +361,8 @@ class GradientBoostingFamily(Family):
                 vals_np = value.cpu().numpy()
                 nodes_np = fb.nodes.cpu().numpy() if isinstance(fb.nodes, torch.Tensor) else fb.nodes
                 for a, f in enumerate(act):
+                    if not batch[f].keep:
+                        continue
                     lr_f = float(lr[f])
                     kept[f].append([_extract_tree(nodes_np, vals_np * lr_f, a * K + k) for k in range(K)])
         if gpu:
@@ -384,7 +386,7 @@ class GradientBoostingFamily(Family):
                 pred = r.argmax(0).to(torch.int32)
             o = FitOutput(task_id=t.task_id, pred=pred, proba=proba, fit_seconds=dt / F,
                           info={"warnings": t.params.get("warnings", [])})
-            if keep_models:
+            if keep_models and t.keep:
                 o.model = _pack_model(kept[f], init[f].cpu().numpy(), t, data, K)
             outs.append(o)
         return outs

@@ -279,7 +279,7 @@ class ForestFamily(Family):
                 share = t.params["n_estimators"] / total_trees
                 o = FitOutput(task_id=t.task_id, pred=pred[roff[f]:roff[f + 1]], fit_seconds=dt * share,
                               info={"warnings": t.params.get("warnings", []), "batch_stats": dict(fb.stats)})
-                if keep_models:
+                if keep_models and t.keep:
                     o.model = extract_forest(fb, int(toff[f]), int(toff[f + 1]), data, t)
                 outs.append(o)
             return outs
@@ -309,33 +309,33 @@ def extract_forest(fb, t0: int, t1: int, data, task: FitTask) -> Dict[str, Any]:
     """Renumber trees [t0, t1) of a batch pool into a standalone forest in pool layout.
 
     Layout matches the kernels' contract: tree j's root is node j, every other node
-    follows, children pairs adjacent — so the saved model predicts with the same
-    HIP/C++ predictors (``roots`` is kept for readability).
+    follows, children pairs adjacent -- so the saved model predicts with the same
+    HIP/C++ predictors (``roots`` is kept for readability).  The renumbering is
+    breadth-first and vectorised level by level on the pool's own device (a full-depth
+    forest on 1M rows has ~10^8 nodes: a per-node host loop would take minutes), and only
+    the extracted nodes leave the device.
     """
-    nodes = fb.nodes.cpu().numpy() if isinstance(fb.nodes, torch.Tensor) else fb.nodes
-    vals = fb.vals.cpu().numpy() if isinstance(fb.vals, torch.Tensor) else fb.vals
+    nodes = fb.nodes if isinstance(fb.nodes, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(fb.nodes))
+    vals = fb.vals if isinstance(fb.vals, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(fb.vals))
+    dev = nodes.device
     T = t1 - t0
-    ids = {t: t - t0 for t in range(t0, t1)}
-    order = []
+    order, lefts = [], []
+    fo = torch.arange(t0, t1, dtype=torch.int64, device=dev)
     nxt = T
-    for t in range(t0, t1):
-        stack = [t]
-        while stack:
-            i = stack.pop()
-            order.append(i)
-            if nodes[i, 0] >= 0:
-                l = int(nodes[i, 1])
-                ids[l], ids[l + 1] = nxt, nxt + 1
-                nxt += 2
-                stack.append(l + 1)
-                stack.append(l)
-    nn = np.empty((nxt, 2), dtype=np.int32)
-    vv = np.empty((nxt, vals.shape[1]), dtype=np.float64)
-    for i in order:
-        j = ids[i]
-        nn[j, 0] = nodes[i, 0]
-        nn[j, 1] = ids[int(nodes[i, 1])] if nodes[i, 0] >= 0 else -1
-        vv[j] = vals[i]
+    while fo.numel():
+        rec = nodes[fo]
+        internal = rec[:, 0] >= 0
+        k = int(internal.sum())
+        left_new = torch.full((fo.numel(),), -1, dtype=torch.int32, device=dev)
+        left_new[internal] = (nxt + 2 * torch.arange(k, device=dev)).to(torch.int32)
+        order.append(fo)
+        lefts.append(left_new)
+        l_old = rec[internal, 1].to(torch.int64)
+        fo = torch.stack([l_old, l_old + 1], 1).reshape(-1)   # children pairs stay adjacent
+        nxt += 2 * k
+    old = torch.cat(order)
+    nn = torch.stack([nodes[old, 0], torch.cat(lefts)], 1).cpu().numpy().astype(np.int32)
+    vv = vals[old].cpu().numpy().astype(np.float64)
     return {
         "kind": "forest",
         "is_reg": bool(fb.is_reg),

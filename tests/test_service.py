@@ -335,3 +335,33 @@ def test_session_fair_share(tmp_path):
         assert c.check_status(sa, "big")[1]["job_status"] == "completed"
     finally:
         c.shutdown()
+
+
+def test_keep_models_all_returns_every_candidate_model(tmp_path):
+    """``keep_models="all"``: every candidate's holdout model is stored and its J4 result
+    carries ``model_path``/``model_id`` (reference worker.py:351-361); the client downloads a
+    NON-best candidate's model by that path (core.py:201-206)."""
+    cfg = Config(data_root=str(tmp_path / "data"), device="cpu", keep_models="all")
+    c = Controller(cfg)
+    try:
+        sid = c.create_session()[1]["session_id"]
+        c.download_data(sid, {"dataset_url": "iris", "dataset_name": "iris", "dataset_type": "sklearn"})
+        st, ack = c.train(sid, _j1("job-k", "RandomForestClassifier", {"max_depth": [1, 3, None]}, cv=3))
+        assert st in (200, 202), ack
+        status = _wait(c, sid, "job-k")
+        assert status["job_status"] == "completed"
+        res = status["job_result"]["results"]
+        assert len(res) == 3 and all(r.get("model_path") and r.get("model_id") for r in res)
+        best = status["best_result"]
+        other = [r for r in res if r["model_path"] != best["model_path"]][0]
+        st, f = c.download_model(sid, "job-k", {"model_path": other["model_path"], "model_id": other["model_id"]})
+        assert st == 200 and f["__file__"].endswith(".npz")
+        m = load_model(f["__file__"])
+        assert m["kind"] == "forest" and m["params"]["max_depth"] == (other["parameters"]["max_depth"] or 2**31 - 1)
+        from sklearn.datasets import load_iris
+
+        iris = load_iris()
+        names = np.asarray(iris.target_names)[iris.target]
+        assert (np.asarray(predict(m, iris.data)).astype(str) == names).mean() > 0.6
+    finally:
+        c.shutdown()
