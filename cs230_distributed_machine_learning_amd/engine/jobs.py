@@ -157,6 +157,13 @@ class JobTable:
                         if job:
                             self._finish_subtask(job, ev["subtask_id"], ev["status"], ev.get("result"),
                                                  ev.get("error"), ev.get("metrics"), log=False)
+                    elif kind == "model":
+                        job = self.jobs.get(ev["job_id"])
+                        idx = _subtask_index(ev["subtask_id"])
+                        if job and idx is not None and idx < job.total and job.subtasks[idx].result is not None:
+                            job.subtasks[idx].result = dict(job.subtasks[idx].result, model_path=ev["model_path"])
+                            if job.finished:
+                                self._complete(job)
             return [j for j in self.jobs.values() if not j.finished]
 
     # ---- sessions ----------------------------------------------------------------------
@@ -243,6 +250,22 @@ class JobTable:
                        "result": result, "error": error, "metrics": metrics})
         if job.n_done + job.n_failed == job.total:
             self._complete(job)
+
+    def attach_model(self, job_id: str, subtask_id: str, model_path: str) -> None:
+        """Record the refit model's path on a completed subtask (before the job completes)."""
+        with self._lock:
+            job = self.jobs.get(job_id)
+            if job is None:
+                return
+            idx = _subtask_index(subtask_id)
+            if idx is None or idx >= job.total:
+                return
+            st = job.subtasks[idx]
+            if st.result is not None:
+                st.result = dict(st.result, model_path=model_path)
+                self._log({"event": "model", "job_id": job_id, "subtask_id": subtask_id, "model_path": model_path})
+                if job.finished and job.result is not None:
+                    self._complete(job)
 
     def _complete(self, job: Job) -> None:
         ok = [st.result for st in job.subtasks if st.status == "completed" and st.result is not None]

@@ -508,6 +508,21 @@ def execute_plan_slice(ctl: Controller, job: Job, plan: Dict[str, Any], dd, cand
                      keep_models=ctl.config.keep_models, models_root=ctl.models.root)
 
 
+def presize_for_job(plan: Dict[str, Any], params: List[Dict[str, Any]], dd, slices: List[List[int]]) -> None:
+    """Job setup on a worker: families with a device arena (the forest builder) size it
+    once for the largest slice this job can hand the worker, so no slice pays a multi-GB
+    hipMalloc mid-job."""
+    fam = family_of(plan["model_type"])
+    if not getattr(dd, "is_gpu", False) or not hasattr(fam, "presize") or not slices:
+        return
+    try:
+        n_splits = (plan["cv"] or 0) + (1 if plan["holdout"] else 0)
+        rps = [fam.resolve(plan["model_type"], p, int(dd.n * 0.8), dd.d, dd.n_classes) for p in params]
+        fam.presize(dd, rps, max(len(s) for s in slices), max(1, n_splits))
+    except Exception:
+        traceback.print_exc()
+
+
 def plan_slices(ctl: Controller, plan: Dict[str, Any], todo: List[int], n_train: int, d: int, n_classes: int,
                 min_slices: int = 1) -> List[List[int]]:
     """LPT order (most expensive first) cut into ~chunk_target_s slices."""
@@ -630,6 +645,7 @@ class LocalRunner(Runner):
             return None
         slices = plan_slices(ctl, plan, todo, int(dd.n * 0.8), dd.d, dd.n_classes)
         costs = candidate_costs(plan, int(dd.n * 0.8), dd.d, dd.n_classes)
+        presize_for_job(plan, [st.spec["parameters"] for st in job.subtasks], dd, slices)
         self._seq += 1
         return _JobRun(job, plan, dd, slices, costs, self._seq)
 
@@ -683,7 +699,7 @@ class LocalRunner(Runner):
             publish_results(ctl, job, results, metrics)
             return False
         # last slice: refit the winner first, so "completed" always comes with the model
-        finalize_job(ctl, job, plan, dd, jr.results)
+        finalize_job(ctl, job, plan, dd, results)   # the earlier slices are already in the table
         publish_results(ctl, job, results, metrics)
         return True
 
@@ -705,30 +721,45 @@ def job_seed(job_id: str) -> int:
 
 
 def finalize_job(ctl: Controller, job: Job, plan: Dict[str, Any], dd, results) -> None:
-    """Refit the best candidate (sklearn refit=True) and attach its model path before
-    the last results are published, so "completed" always comes with the artefact."""
+    """Refit the best candidate (sklearn refit=True) and attach its model path before the
+    last results are published, so "completed" always comes with the artefact."""
     best = pick_refit(ctl, job, plan, results)
     if best is None:
         return
     try:
-        path = refit_best(ctl, job, plan, dd, best.candidate)
+        path = refit_best(ctl, job, plan, dd, best)
         if path:
-            best.result["model_path"] = path
+            attach_model(ctl, job, results, best, path)
     except Exception:
         traceback.print_exc()
 
 
-def pick_refit(ctl: Controller, job: Job, plan: Dict[str, Any], results):
-    """The result whose candidate gets refit on all rows, or None."""
-    ok = [r for r in results if r.ok]
-    if not ok or not plan.get("refit", True) or ctl.config.keep_models == "none":
+def pick_refit(ctl: Controller, job: Job, plan: Dict[str, Any], results) -> Optional[int]:
+    """Index of the candidate to refit on all rows -- the job's best by mean CV score over
+    every result so far (already published subtasks + ``results``), ties to the lowest
+    index like jobs.aggregate_best -- or None (refit=False, keep_models='none', no success)."""
+    if not plan.get("refit", True) or ctl.config.keep_models == "none":
         return None
-    # same winner as jobs.aggregate_best: max mean_cv_score, ties -> lowest subtask index
-    best = max(ok, key=lambda r: (score_r(r.result), -r.candidate))
-    if any(st.status == "completed" and st.result and (score_r(st.result), -st.index) > (score_r(best.result), -best.candidate)
-           for st in job.subtasks):
+    pool: Dict[int, float] = {}
+    for st in job.subtasks:
+        if st.status == "completed" and st.result:
+            pool[st.index] = score_r(st.result)
+    for r in results:
+        if r.ok:
+            pool[r.candidate] = score_r(r.result)
+    if not pool:
         return None
-    return best
+    return max(pool, key=lambda i: (pool[i], -i))
+
+
+def attach_model(ctl: Controller, job: Job, results, cand: int, path: str) -> None:
+    """The refit model's path goes on the winner's J4 result: in the not-yet-published
+    ``results`` when it is there, else on its already-published subtask."""
+    for r in results:
+        if r.candidate == cand and r.ok:
+            r.result["model_path"] = path
+            return
+    ctl.table.attach_model(job.job_id, job.subtasks[cand].subtask_id, path)
 
 
 def score_r(R: Dict[str, Any]) -> float:

@@ -54,8 +54,8 @@ import torch
 
 from ..engine import faults
 from ..engine.jobs import Job, json_safe
-from ..engine.service import (Controller, Runner, candidate_costs, job_plan, job_seed, pick_refit, plan_slices,
-                              publish_results, refit_model, run_slice)
+from ..engine.service import (Controller, Runner, attach_model, candidate_costs, job_plan, job_seed, pick_refit,
+                              plan_slices, presize_for_job, publish_results, refit_model, run_slice)
 from ..models.base import family_of, is_classifier
 from ..utils.log import get_logger
 from . import data as pdata
@@ -182,6 +182,7 @@ class WorkerCore:
         self.in_group = in_group
         self.cache: "collections.OrderedDict[str, Any]" = collections.OrderedDict()
         self.msgs: Dict[int, Dict[str, Any]] = {}
+        self.presized: Set[int] = set()
         self.slices_done = 0
 
     # ---- job messages and datasets ------------------------------------------------------
@@ -254,6 +255,9 @@ class WorkerCore:
         faults.maybe_kill(self.wid, self.slices_done)   # fault injection: die holding an assigned slice
         t_load = time.perf_counter()
         dd = self.dataset(msg, ctl)
+        if a["seq"] not in self.presized:   # job setup on this worker: size the device arena once
+            self.presized.add(a["seq"])
+            presize_for_job(msg["plan"], msg["params"], dd, msg["slices"])
         load_s = time.perf_counter() - t_load
         results, metrics, wall = run_slice(msg["plan"], msg["params"], msg["subtask_ids"], dd, a["ids"],
                                            f"rank{self.wid}", str(self.device), seed=msg["seed"],
@@ -289,7 +293,7 @@ class WorkerCore:
         if self.inf.rank == 0:
             job = ctl.table.get(msg["session_id"], msg["job_id"])
             best = pick_refit(ctl, job, plan, results_all)
-            self.store.set(f"job/{seq}/refit", str(best.candidate if best is not None else -1))
+            self.store.set(f"job/{seq}/refit", str(best if best is not None else -1))
         self.store.wait([f"job/{seq}/refit"])
         best_i = int(self.store.get(f"job/{seq}/refit"))
         model_path = None
@@ -400,7 +404,6 @@ class _JobState:
     refit_pending: bool = False
     refit_inflight: bool = False
     refit_candidate: int = -1
-    best: Any = None
     finished: bool = False
 
 
@@ -740,19 +743,16 @@ class DistributedRunner(Runner):
 
     def _complete(self, js: _JobState) -> None:
         """Every slice is in: refit the winner (on rank 0), then publish the held slice."""
-        results_all = [r for i in sorted(js.done) for r in js.done[i]]
-        best = pick_refit(self.ctl, js.job, js.plan, results_all)
-        js.best = best
+        best = pick_refit(self.ctl, js.job, js.plan, js.done[js.held])
         if best is None:
             self._finish_job(js, None)
             return
-        js.refit_candidate = best.candidate
+        js.refit_candidate = best
         js.refit_pending = True
 
     def _finish_job(self, js: _JobState, model_path: Optional[str]) -> None:
-        best = getattr(js, "best", None)
-        if best is not None and model_path:
-            best.result["model_path"] = model_path
+        if model_path and js.refit_candidate >= 0:
+            attach_model(self.ctl, js.job, js.done.get(js.held, []), js.refit_candidate, model_path)
         if js.held is not None:
             publish_results(self.ctl, js.job, js.done[js.held], js.metrics.get(js.held, {}))
         js.finished = True

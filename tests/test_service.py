@@ -84,6 +84,7 @@ def test_grid_job_contract(ctl):
         assert 0 <= r["mean_cv_score"] <= 1
     best = status["best_result"]
     assert best["mean_cv_score"] == max(r["mean_cv_score"] for r in res)
+    assert best.get("model_path"), best     # refit of the job's best, whichever slice it ran in
     # north-star counters: 8 candidates x (5 CV + 1 holdout) fits, per job and per node
     assert status["fits_done"] == 48 and status["fits_per_s"] > 0
     health = ctl.health()[1]
@@ -363,5 +364,23 @@ def test_keep_models_all_returns_every_candidate_model(tmp_path):
         iris = load_iris()
         names = np.asarray(iris.target_names)[iris.target]
         assert (np.asarray(predict(m, iris.data)).astype(str) == names).mean() > 0.6
+    finally:
+        c.shutdown()
+
+
+def test_refit_attaches_model_when_best_ran_in_an_early_slice(tmp_path):
+    """One candidate per slice: the winner's result is published long before the job ends,
+    and the refit model path must still land on it (J5 best_result.model_path)."""
+    c = Controller(Config(data_root=str(tmp_path / "data"), device="cpu", chunk_target_s=0.0))
+    try:
+        sid = c.create_session()[1]["session_id"]
+        c.download_data(sid, {"dataset_url": "iris", "dataset_name": "iris", "dataset_type": "sklearn"})
+        # the most expensive (first-run, LPT) candidates are the best ones here
+        grid = {"n_estimators": [1, 2, 3, 40], "max_depth": [1, None]}
+        c.train(sid, _j1("job-r", "RandomForestClassifier", grid, cv=3))
+        status = _wait(c, sid, "job-r")
+        best = status["best_result"]
+        assert status["job_status"] == "completed" and best.get("model_path"), best
+        assert os.path.exists(best["model_path"])
     finally:
         c.shutdown()
