@@ -279,9 +279,16 @@ def run_e2e(args) -> int:
         assert st in (200, 202), ack
         ctl.table.wait_finished(ack["job_id"], timeout=7200)
         wall = time.perf_counter() - t2
+        t_end = time.time()
         status = ctl.check_status(sid, ack["job_id"])[1]
         metrics = ctl.metrics(sid, ack["job_id"])[1]
-        last_slice_end = max(m.get("finished_at") or "" for m in metrics)
+        from datetime import datetime
+
+        def _ts(x):
+            return datetime.fromisoformat(x.replace("Z", "").replace("+00:00", "") + "+00:00").timestamp()
+
+        last_slice_end = max(_ts(m["finished_at"]) for m in metrics if m.get("finished_at"))
+        out["tail_s"] = t_end - last_slice_end   # refit of the best candidate + model store + publish
         out.update(status=status, wall=wall, t_reg=t_reg, t_load=t_load, workers=sorted({m["worker_id"] for m in metrics}),
                    last=last_slice_end, slices=len({(m.get("worker_id"), m.get("started_at")) for m in metrics}))
 
@@ -338,6 +345,7 @@ def run_e2e(args) -> int:
         "dataset_first_load_s": round(out["t_load"], 2), "workers": out["workers"],
         "best_mean_cv": round(status["best_result"]["mean_cv_score"], 4),
         "best_model_stored": bool(status["best_result"].get("model_path")),
+        "refit_and_publish_s": round(out["tail_s"], 2),
     }
     print(json.dumps(line), flush=True)
     if args.json_out:

@@ -518,7 +518,9 @@ def presize_for_job(plan: Dict[str, Any], params: List[Dict[str, Any]], dd, slic
     try:
         n_splits = (plan["cv"] or 0) + (1 if plan["holdout"] else 0)
         rps = [fam.resolve(plan["model_type"], p, int(dd.n * 0.8), dd.d, dd.n_classes) for p in params]
-        fam.presize(dd, rps, max(len(s) for s in slices), max(1, n_splits))
+        # slices are re-cut once the first one calibrates the cost model: size for the
+        # larger of the planned slices and a typical re-cut one (capped by the HBM budget)
+        fam.presize(dd, rps, max(max(len(s) for s in slices), min(len(params), 8)), max(1, n_splits))
     except Exception:
         traceback.print_exc()
 
@@ -594,6 +596,7 @@ class _JobRun:
         self.job, self.plan, self.dd, self.costs, self.seq = job, plan, dd, costs, seq
         self.slices = list(slices)
         self.si = 0
+        self.rechunked = False
         self.results: List[Any] = []
 
 
@@ -695,6 +698,13 @@ class LocalRunner(Runner):
         ctl.scheduler.observe(self.worker_id, unit, wall)
         jr.results.extend(results)
         jr.si += 1
+        if not jr.rechunked and jr.si < len(jr.slices):
+            # the job was cut with the device's prior seconds-per-cost; the first slice
+            # calibrated it: re-cut the rest so slices are ~chunk_target_s of real work (a
+            # GPU batch of one candidate leaves most of the chip idle at the top levels)
+            jr.rechunked = True
+            rest = [i for sl in jr.slices[jr.si:] for i in sl]
+            jr.slices = jr.slices[:jr.si] + plan_slices(ctl, plan, rest, int(dd.n * 0.8), dd.d, dd.n_classes)
         if jr.si < len(jr.slices):
             publish_results(ctl, job, results, metrics)
             return False

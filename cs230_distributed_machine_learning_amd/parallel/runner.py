@@ -405,6 +405,11 @@ class _JobState:
     refit_inflight: bool = False
     refit_candidate: int = -1
     finished: bool = False
+    cand_costs: List[float] = field(default_factory=list)
+    n_train: int = 0
+    n_feat: int = 1
+    rechunked: bool = False
+    retired: Set[int] = field(default_factory=set)   # queued slices replaced by a re-cut
 
 
 @dataclass
@@ -519,7 +524,8 @@ class DistributedRunner(Runner):
                    "slices": slices, "params": [sub.spec["parameters"] for sub in job.subtasks],
                    "subtask_ids": [sub.subtask_id for sub in job.subtasks], "seed": job_seed(job.job_id),
                    "keep_models": ctl.config.keep_models, "models_root": ctl.models.root}
-            js = _JobState(job, plan, seq, msg, slices, est, mode="data" if data_par else "task")
+            js = _JobState(job, plan, seq, msg, slices, est, mode="data" if data_par else "task",
+                           cand_costs=costs, n_train=int(n_rows * 0.8), n_feat=n_feat)
             js.queue.extend(range(len(slices)))
             # datasets travel by collective broadcast while the whole group is alive and
             # nobody joined from outside it; otherwise host-staged
@@ -727,19 +733,39 @@ class DistributedRunner(Runner):
         try:
             from ..engine.scheduler import Unit
 
+            cost = sum(js.cand_costs[c] for c in a["ids"]) if js.cand_costs else 1.0
             self.ctl.scheduler.observe(self.worker_ids.get(w.wid, f"rank{w.wid}"),
-                                       Unit(unit_id=f"{js.job.job_id}:{i}", cost=1.0, algo=js.job.model_type), wall)
+                                       Unit(unit_id=f"{js.job.job_id}:{i}", cost=cost, algo=js.job.model_type), wall)
         except Exception:
             pass
+        if not js.rechunked and "error" not in out:
+            self._rechunk(js)
         if i in js.done:   # a re-queued slice finished twice: count it once
             return
         js.done[i] = res
         js.metrics[i] = metrics
-        if len(js.done) < len(js.slices):
+        if len(js.done) + len(js.retired) < len(js.slices):
             publish_results(self.ctl, js.job, res, metrics)
             return
         js.held = i
         self._complete(js)
+
+    def _rechunk(self, js: _JobState) -> None:
+        """The job was cut with the prior seconds-per-cost; its first slice calibrated the
+        cost model: re-cut the still-queued candidates into ~chunk_target_s slices (a
+        one-candidate GPU batch leaves most of the chip idle at the top levels)."""
+        js.rechunked = True
+        queued = list(js.queue)
+        if len(queued) < 2:
+            return
+        ids = [c for q in queued for c in js.slices[q]]
+        new = plan_slices(self.ctl, js.plan, ids, js.n_train, js.n_feat, 2, min_slices=min(len(ids), self._n_alive()))
+        base = len(js.slices)
+        js.slices.extend(new)
+        js.est.extend(self.ctl.scheduler.estimate(js.plan["model_type"], sum(js.cand_costs[c] for c in sl))
+                      for sl in new)
+        js.retired.update(queued)
+        js.queue = collections.deque(range(base, base + len(new)))
 
     def _complete(self, js: _JobState) -> None:
         """Every slice is in: refit the winner (on rank 0), then publish the held slice."""
