@@ -112,6 +112,7 @@ struct ForestArgs {
   int64_t tier_nodes_out[4];
   int64_t ystride;       // >0: tree t regresses on yreg[specs[t].target * ystride + row] (boosting)
   int64_t XbT;           // optional feature-major copy of the bins, uint8 [d][n] (0 = none)
+  int64_t cw;            // class-weight table double [T][C] (0 = no class weights in this build)
 };
 
 constexpr int kTiers = 4;  // 0 subtree, 1 wave, 2 block, 3 large
@@ -170,6 +171,10 @@ struct Ctx {
   // share of the table's rows, so a 64-lane gather of one feature from the feature-major
   // copy touches a couple of lines instead of 64 row lines
   const uint8_t* XbT;
+  // class weights (sklearn class_weight): row t of a [T][C] table multiplies tree t's
+  // integer class sums wherever they become doubles (histogram scans, root and child
+  // statistics); rows of balanced_subsample trees are filled by k_roots
+  const double* cw;
 };
 
 // target vector of a tree (shared y, or its own row of the boosting target matrix)
@@ -186,6 +191,12 @@ __device__ __forceinline__ uint32_t word_weight(const Ctx& c, const TreeSpec& s,
 __device__ __forceinline__ int word_cls(const Ctx& c, uint32_t wd) {
   return c.packed ? (int)(wd >> (c.rbits + 4)) : c.ycls[wd];
 }
+
+// class-weight row of a tree (nullptr: every weight is 1)
+__device__ __forceinline__ const double* tree_cw(const Ctx& c, int tree) {
+  return (c.cw && c.specs[tree].cw_mode) ? c.cw + (int64_t)tree * c.C : nullptr;
+}
+__device__ __forceinline__ double cwk(const double* cw, int k) { return cw ? cw[k] : 1.0; }
 
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
@@ -293,7 +304,8 @@ __device__ __forceinline__ double hist_chan(const typename HT<MODE>::T* h, int c
 // histogram afterwards so the next feature group needs no clearing pass.
 template <int MODE>
 __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
-                                 double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after);
+                                 double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after,
+                                 const double* cw);
 
 // ONE wave evaluates one feature's histogram.  Binary (MODE 1) and regression (MODE 2)
 // histograms are read ONCE into registers (4 bins per lane), scanned with DPP, scored and
@@ -301,9 +313,10 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
 // lanes right after the read.  Multiclass (MODE 0) keeps the LDS path (C+1 planes).
 template <int MODE>
 __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
-                             double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after) {
+                             double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after,
+                             const double* cw = nullptr) {
   if constexpr (MODE == 0) {
-    eval_feature_lds<MODE>(h, C, CH, s, lane, out_gain, out_bin, out_nc, out_left, zero_after);
+    eval_feature_lds<MODE>(h, C, CH, s, lane, out_gain, out_bin, out_nc, out_left, zero_after, cw);
   } else {
     using CT = typename HT<MODE>::T;
     constexpr int NP = MODE == 1 ? 1 : 4;      // planes: packed u64 | (w, wy, wyy, rows) floats
@@ -333,6 +346,7 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
 #pragma unroll
     for (int q = 0; q < NP; ++q) tot[q] = wave::bcast<CT>(v[q][3], 63);
     const double msl = (double)s.min_samples_leaf;
+    const double cw0 = cwk(cw, 0), cw1 = cwk(cw, 1);
     double best = -INFINITY;
     int bb = -1;
     bool nc = false;
@@ -352,8 +366,8 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
       double g;
       if constexpr (MODE == 1) {
         const uint64_t cv = (uint64_t)v[0][i], tv = (uint64_t)tot[0];
-        const double l0 = (double)(cv & kPackMask21), l1 = (double)((cv >> 21) & kPackMask21);
-        const double t0 = (double)(tv & kPackMask21), t1 = (double)((tv >> 21) & kPackMask21);
+        const double l0 = (double)(cv & kPackMask21) * cw0, l1 = (double)((cv >> 21) & kPackMask21) * cw1;
+        const double t0 = (double)(tv & kPackMask21) * cw0, t1 = (double)((tv >> 21) & kPackMask21) * cw1;
         ClsAcc L, R;
         L.init(s.criterion); R.init(s.criterion);
         L.add(l0); L.add(l1);
@@ -375,8 +389,8 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
       for (int i = 1; i < 4; ++i) if (sel == i) mine = (uint64_t)v[0][i];
       const uint64_t cv = wave::bcast<uint64_t>(mine, src);
       if (lane == 0) {
-        out_left[0] = bb >= 0 ? (double)(cv & kPackMask21) : 0.0;
-        out_left[1] = bb >= 0 ? (double)((cv >> 21) & kPackMask21) : 0.0;
+        out_left[0] = bb >= 0 ? (double)(cv & kPackMask21) * cw0 : 0.0;
+        out_left[1] = bb >= 0 ? (double)((cv >> 21) & kPackMask21) * cw1 : 0.0;
         out_left[2] = bb >= 0 ? (double)(cv >> 42) : 0.0;
       }
     } else {
@@ -399,7 +413,8 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
 
 template <int MODE>
 __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
-                                 double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after) {
+                                 double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after,
+                                 const double* cw) {
   using CT = typename HT<MODE>::T;
   const int planes = hist_planes(MODE, CH);
   for (int ch = 0; ch < planes; ++ch) scan256<CT>(h + ch * 256, lane);
@@ -426,8 +441,8 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
       ClsAcc L, R;
       L.init(s.criterion); R.init(s.criterion);
       for (int k = 0; k < C; ++k) {
-        const double lc = hist_chan<MODE>(h, k, CH, b);
-        const double tc = hist_chan<MODE>(h, k, CH, 255);
+        const double lc = hist_chan<MODE>(h, k, CH, b) * cwk(cw, k);
+        const double tc = hist_chan<MODE>(h, k, CH, 255) * cwk(cw, k);
         L.add(lc);
         R.add(tc - lc);
       }
@@ -437,7 +452,7 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
   }
   wave::argmax(best, bb, lane);
   const bool any_nc = __ballot(nc) != 0ull;
-  if (lane < CH) out_left[lane] = bb >= 0 ? hist_chan<MODE>(h, lane, CH, bb) : 0.0;
+  if (lane < CH) out_left[lane] = bb >= 0 ? hist_chan<MODE>(h, lane, CH, bb) * (lane < C ? cwk(cw, lane) : 1.0) : 0.0;
   if (lane == 0) { *out_gain = best; *out_bin = bb; *out_nc = any_nc ? 1 : 0; }
   if (zero_after) {
     wave_lds_sync();
@@ -829,7 +844,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     __syncthreads();
     PH(2)
     for (int j = wid; j < g; j += NW)
-      eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, true);
+      eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, true,
+                         tree_cw(c, on.tree));
     __syncthreads();
     PH(3)
     if (wid == 0) {
@@ -1014,7 +1030,7 @@ struct SubEntry {
 // evaluate one feature for the rows in `mask`; lane data: bin b (valid if in mask).
 template <bool REG>
 __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt, int lane, int my_bin, int my_cls,
-                         float my_w, float my_y, double& gain, int& bin, bool& nonconst) {
+                         float my_w, float my_y, double& gain, int& bin, bool& nonconst, const double* cw) {
   const bool act = (mask >> lane) & 1ull;
   const uint32_t key = act ? ((uint32_t)my_bin << 6) | (uint32_t)lane : 0xFFFFFFFFu;
   const uint32_t sk = wave::bitonic64(key, lane);
@@ -1041,8 +1057,9 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
       const uint32_t v = (ycls == k) ? w : 0u;
       const uint32_t pre = wave::incl_scan<uint32_t>(v);
       const uint32_t tot = wave::bcast<uint32_t>(pre, cnt - 1);
-      L.add((double)pre);
-      R.add((double)(tot - pre));
+      const double lw = (double)pre * cwk(cw, k), tw = (double)tot * cwk(cw, k);
+      L.add(lw);
+      R.add(tw - lw);
     }
     if (cand) g = cls_proxy(L, R, s.criterion);
   } else {
@@ -1115,7 +1132,7 @@ __device__ __forceinline__ void argmax_seg(double& g, int& idx, int lane) {
 template <int WD>
 __device__ void sub_node_seg(const Ctx& c, const TreeSpec& s, const FeatPerm& fp, int cnt, int lane, int src,
                              int cls_j, uint32_t w_j, const uint8_t* xc, int dp, int& nonconst, double& best_g,
-                             int& best_f, int& best_b) {
+                             int& best_f, int& best_b, const double* cw) {
   constexpr int S = 64 / WD;
   const int d = c.d;
   const int seg = lane / WD, j = lane & (WD - 1);
@@ -1151,8 +1168,9 @@ __device__ void sub_node_seg(const Ctx& c, const TreeSpec& s, const FeatPerm& fp
         if (seg == q) { base = bq; tot = eq - bq; }
       }
       pre -= base;
-      L.add((double)pre);
-      R.add((double)(tot - pre));
+      const double lw = (double)pre * cwk(cw, k), tw = (double)tot * cwk(cw, k);
+      L.add(lw);
+      R.add(tw - lw);
     }
     double g = cand ? cls_proxy(L, R, s.criterion) : -INFINITY;
     int bl = cand ? j : 64;
@@ -1230,6 +1248,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   }
   if (lane < VC) sstats[lane] = c.node_val[(int64_t)on.node * VC + lane];
   const double Wt = c.tree_W[on.tree];
+  const double* tcw = REG ? nullptr : tree_cw(c, on.tree);
   pool_base = wave::bcast<int>(pool_base, 0);
   if (pool_base < 0) return;
   int used = 0;
@@ -1252,9 +1271,9 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
       const int src = jx < cnt ? cidx[jx] : 0;
       const int cls_j = __shfl(my_cls, src);
       const uint32_t w_j = (uint32_t)__shfl((int)(uint32_t)my_w, src);
-      if (cnt <= 8) sub_node_seg<8>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b);
-      else if (cnt <= 16) sub_node_seg<16>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b);
-      else sub_node_seg<32>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b);
+      if (cnt <= 8) sub_node_seg<8>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw);
+      else if (cnt <= 16) sub_node_seg<16>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw);
+      else sub_node_seg<32>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw);
       wave_lds_sync();   // cidx is rewritten by the next node
     } else
     for (int pos = 0; nonconst < s.max_features && pos < d; ++pos) {
@@ -1263,7 +1282,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
       double g;
       int bb;
       bool nc;
-      sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_y, g, bb, nc);
+      sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_y, g, bb, nc, tcw);
       if (nc) {
         ++nonconst;
         if (bb >= 0 && g > best_g) { best_g = g; best_f = f; best_b = bb; }
@@ -1283,7 +1302,8 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
       } else {
         v = (inl && my_cls == k) ? (double)my_w : 0.0;
       }
-      v = wave::sum<double>(v, lane);
+      v = wave::sum<double>(v, lane);     // integer-valued: exact in any order
+      if constexpr (!REG) v *= cwk(tcw, k);
       if (lane == 0) { left_ch[k] = v; right_ch[k] = pv[k] - v; }
     }
     wave_lds_sync();
@@ -1468,7 +1488,8 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   for (int i = tid; i < g * span; i += 256) hist[i] = gh[i];
   __syncthreads();
   for (int j = wid; j < g; j += 4)
-    eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, false);
+    eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, false,
+                       tree_cw(c, st.on.tree));
   __syncthreads();
   const int16_t* feats = c.lperm + (int64_t)slot * c.d + st.pos;
   double* best_left = c.lbest_left + (int64_t)slot * c.CH;
@@ -1683,6 +1704,12 @@ __global__ void k_roots(Ctx c) {
   if (t >= c.T) return;
   NodeRec leaf; leaf.split = -1; leaf.left = -1;
   c.nodes[t] = leaf;
+  if (!c.is_reg && c.cw && c.specs[t].cw_mode) {
+    double* row = const_cast<double*>(c.cw) + (int64_t)t * c.C;
+    double* v = c.node_val + (int64_t)t * c.VC;
+    if (c.specs[t].cw_mode == 2) balanced_weights(v, c.C, row);   // from this tree's bootstrap counts
+    for (int k = 0; k < c.C; ++k) v[k] *= row[k];
+  }
   c.tree_W[t] = node_weight(c, t);
   const int cnt = c.active_count[t];
   if (cnt == 0) return;
@@ -1772,6 +1799,7 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.lcursor = (int32_t*)(ws + L.lcursor);
   c.bscr = ws + L.bscr;
   c.XbT = (const uint8_t*)a->XbT;
+  c.cw = (const double*)a->cw;
   c.large_cap = L.large_cap;
   c.wave_max = (int)a->wave_max; c.block_max = (int)a->block_max; c.chunk = (int)a->chunk;
   c.kg_wave = (int)a->kg_wave; c.kg_block = (int)a->kg_block; c.kg_large = (int)a->kg_large;

@@ -54,7 +54,22 @@ struct TreeSpec {
   float min_impurity_decrease;
   int32_t target;           // row of the per-tree target matrix (ForestArgs.ystride > 0: boosting)
   uint32_t pois_cdf[kPoisTable];  // P(K<=j) * 2^32 (saturated), j = 0..11
+  int32_t cw_mode;          // class weights: 0 none, 1 fixed row of the cw table (dict / "balanced"),
+                            // 2 "balanced_subsample" (row computed from this tree's bootstrap counts)
+  int32_t reserved;
 };
+
+// sklearn class_weight="balanced_subsample" for one tree from its root class counts
+// (bootstrap-weighted): n_samples / (n_present_classes * count_k); absent classes get 1.
+DML_HD void balanced_weights(const double* counts, int C, double* out) {
+  double total = 0.0;
+  int present = 0;
+  for (int k = 0; k < C; ++k) {
+    total += counts[k];
+    present += counts[k] > 0.0 ? 1 : 0;
+  }
+  for (int k = 0; k < C; ++k) out[k] = counts[k] > 0.0 ? total / ((double)present * counts[k]) : 1.0;
+}
 
 // node record written by both builders
 struct NodeRec {
@@ -208,6 +223,99 @@ constexpr double kEps = 1e-7;  // sklearn EPSILON for purity / min_impurity_decr
 // leaf-by-counts rule (before any split search)
 DML_HD bool leaf_by_counts(const TreeSpec& t, int count, int depth) {
   return depth >= t.max_depth || count < t.min_samples_split || count < 2 * t.min_samples_leaf;
+}
+
+// ---- max_leaf_nodes: best-first selection on a grown tree ---------------------------
+// sklearn grows a max_leaf_nodes tree best-first (BestFirstTreeBuilder): it always
+// expands the frontier node of largest impurity improvement and stops after L-1
+// expansions.  Every node's split here is a function of the node alone (keyed feature
+// permutation, same rows), so that tree is exactly the top of the depth-first tree this
+// builder grows: replay the best-first order over the grown tree and turn the internal
+// nodes still on the frontier into leaves (their stored sums are their leaf values).
+// One routine for the HIP kernel (one lane per tree) and the C++ builder: same order,
+// same doubles, identical trees.
+
+DML_HD double val_impurity(const double* v, int C, bool is_reg, int crit, double& w) {
+  if (is_reg) { w = v[0]; return mse_impurity(v[0], v[1], v[2]); }
+  ClsAcc a;
+  a.init(crit);
+  for (int k = 0; k < C; ++k) a.add(v[k]);
+  w = a.w;
+  return cls_impurity(a, crit);
+}
+
+DML_HD double split_priority(const NodeRec* nodes, const double* vals, int64_t VC, int C, bool is_reg, int crit,
+                             double Wt, int node) {
+  double wN, wL, wR;
+  const int l = nodes[node].left;
+  const double iN = val_impurity(vals + (int64_t)node * VC, C, is_reg, crit, wN);
+  const double iL = val_impurity(vals + (int64_t)l * VC, C, is_reg, crit, wL);
+  const double iR = val_impurity(vals + (int64_t)(l + 1) * VC, C, is_reg, crit, wR);
+  return improvement(Wt, wN, iN, wL, iL, wR, iR);
+}
+
+struct FrontierEnt {
+  double pri;
+  int32_t node, pad;
+};
+
+// max-heap order: larger improvement first, then the smaller node id (deterministic ties)
+DML_HD bool frontier_before(const FrontierEnt& a, const FrontierEnt& b) {
+  return a.pri > b.pri || (a.pri == b.pri && a.node < b.node);
+}
+
+DML_HDM void frontier_push(FrontierEnt* h, int& n, FrontierEnt e) {
+  int i = n++;
+  while (i > 0) {
+    const int p = (i - 1) >> 1;
+    if (!frontier_before(e, h[p])) break;
+    h[i] = h[p];
+    i = p;
+  }
+  h[i] = e;
+}
+
+DML_HDM FrontierEnt frontier_pop(FrontierEnt* h, int& n) {
+  const FrontierEnt top = h[0];
+  const FrontierEnt last = h[--n];
+  int i = 0;
+  for (;;) {
+    const int l = 2 * i + 1;
+    if (l >= n) break;
+    const int m = (l + 1 < n && frontier_before(h[l + 1], h[l])) ? l + 1 : l;
+    if (!frontier_before(h[m], last)) break;
+    h[i] = h[m];
+    i = m;
+  }
+  if (n > 0) h[i] = last;
+  return top;
+}
+
+// Keep the best-first top of the tree rooted at ``root`` with at most L leaves.
+// ``heap``: scratch for at least L entries (the frontier never holds more).
+// Returns the number of leaves of the kept tree.
+DML_HDM int best_first_prune(NodeRec* nodes, const double* vals, int64_t VC, int C, bool is_reg, int crit, int root,
+                             int L, FrontierEnt* heap) {
+  if (nodes[root].split < 0) return 1;
+  double Wt;
+  val_impurity(vals + (int64_t)root * VC, C, is_reg, crit, Wt);
+  int n = 0, leaves = 1, budget = L - 1;
+  frontier_push(heap, n, FrontierEnt{split_priority(nodes, vals, VC, C, is_reg, crit, Wt, root), root, 0});
+  while (n > 0) {
+    const FrontierEnt e = frontier_pop(heap, n);
+    if (budget <= 0) {   // out of expansions: this frontier node stays a leaf
+      nodes[e.node].split = -1;
+      nodes[e.node].left = -1;
+      continue;
+    }
+    --budget;
+    ++leaves;
+    const int l = nodes[e.node].left;
+    for (int s = 0; s < 2; ++s)
+      if (nodes[l + s].split >= 0)
+        frontier_push(heap, n, FrontierEnt{split_priority(nodes, vals, VC, C, is_reg, crit, Wt, l + s), l + s, 0});
+  }
+  return leaves;
 }
 
 }  // namespace dml

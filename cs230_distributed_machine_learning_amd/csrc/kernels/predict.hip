@@ -312,11 +312,36 @@ static int launch_predict(PredictArgs* a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// max_leaf_nodes: one lane per limited tree replays sklearn's best-first order over the
+// grown tree (forest_common.h best_first_prune); the frontier heap lives in global
+// scratch, ``cap`` entries per lane.  Trees with limit 0 are left alone.
+__global__ void k_prune_best_first(NodeRec* nodes, const double* vals, int64_t VC, int C, int is_reg,
+                                   const TreeSpec* specs, const int32_t* limit, int32_t t0, int32_t T,
+                                   FrontierEnt* heap, int64_t cap, int32_t* leaves) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= T) return;
+  const int t = t0 + i;   // tree t's root is pool node t
+  const int L = limit[t];
+  if (L <= 0 || L > cap) { if (leaves) leaves[t] = -1; return; }
+  const int n = best_first_prune(nodes, vals, VC, C, is_reg != 0, specs[t].criterion, t, L, heap + (int64_t)i * cap);
+  if (leaves) leaves[t] = n;
+}
+
 }  // namespace dml
 
 using namespace dml;
 
 extern "C" {
+
+int dml_forest_prune(NodeRec* nodes, const double* vals, int64_t VC, int32_t C, int32_t is_reg,
+                     const TreeSpec* specs, const int32_t* limit, int32_t t0, int32_t T, void* heap, int64_t cap,
+                     int32_t* leaves, hipStream_t st) {
+  if (T <= 0) return 0;
+  if (cap <= 0 || heap == nullptr) return 2;
+  k_prune_best_first<<<(unsigned)((T + 63) / 64), 64, 0, st>>>(nodes, vals, VC, C, is_reg, specs, limit, t0, T,
+                                                               static_cast<FrontierEnt*>(heap), cap, leaves);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
 
 int dml_forest_refine(const uint8_t* Xb, int64_t ld, int64_t n, int64_t d, NodeRec* nodes, int64_t P,
                       const TreeSpec* specs, int32_t T, const uint8_t* roles, const float* vals, const uint8_t* exact,

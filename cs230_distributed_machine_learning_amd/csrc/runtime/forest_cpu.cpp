@@ -34,11 +34,12 @@ struct Data {
   const uint8_t* Xb; int64_t ld; int n, d, C, CH, VC, is_reg;
   const int32_t* ycls; const float* yreg; const uint8_t* roles;
   int64_t ystride;
+  const double* cw;   // class-weight table [T][C] (rows of cw_mode 1 trees), or null
 };
 
 struct Job { int node, start, count, depth; uint64_t key; };
 
-static void build_tree(const Data& D, const TreeSpec& s, CpuTree& out) {
+static void build_tree(const Data& D, const TreeSpec& s, int64_t t, CpuTree& out) {
   const uint8_t* role = D.roles + (int64_t)s.split * D.n;
   const float* Y = D.ystride ? D.yreg + (int64_t)s.target * D.ystride : D.yreg;
   std::vector<uint32_t> rows, tmp;
@@ -60,6 +61,14 @@ static void build_tree(const Data& D, const TreeSpec& s, CpuTree& out) {
     }
   }
   tmp.resize(rows.size());
+  // class weights multiply the (integer) class sums: root statistics here, every
+  // histogram channel below -- exactly where the HIP builder applies them
+  std::vector<double> cwv(D.is_reg ? 0 : D.C, 1.0);
+  if (!D.is_reg && s.cw_mode != 0) {
+    if (s.cw_mode == 2) balanced_weights(root.data(), D.C, cwv.data());
+    else if (D.cw) for (int k = 0; k < D.C; ++k) cwv[k] = D.cw[t * D.C + k];
+    for (int k = 0; k < D.C; ++k) root[k] *= cwv[k];
+  }
   out.nodes.clear(); out.vals.clear();
   NodeRec leaf{-1, -1};
   out.nodes.push_back(leaf);
@@ -114,7 +123,7 @@ static void build_tree(const Data& D, const TreeSpec& s, CpuTree& out) {
           if (rl < (uint32_t)s.min_samples_leaf || rr < (uint32_t)s.min_samples_leaf) continue;
           ClsAcc L, R; L.init(s.criterion); R.init(s.criterion);
           for (int k = 0; k < D.C; ++k) {
-            const double lc = (double)hu[k * 256 + b], tc = (double)hu[k * 256 + 255];
+            const double lc = (double)hu[k * 256 + b] * cwv[k], tc = (double)hu[k * 256 + 255] * cwv[k];
             L.add(lc); R.add(tc - lc);
           }
           const double g = cls_proxy(L, R, s.criterion);
@@ -124,7 +133,7 @@ static void build_tree(const Data& D, const TreeSpec& s, CpuTree& out) {
           ++nonconst;
           if (b_best >= 0 && g_best > best_gain) {
             best_gain = g_best; best_feat = f; best_bin = b_best;
-            for (int ch = 0; ch < CH; ++ch) best_left[ch] = (double)hu[ch * 256 + b_best];
+            for (int ch = 0; ch < CH; ++ch) best_left[ch] = (double)hu[ch * 256 + b_best] * (ch < D.C ? cwv[ch] : 1.0);
           }
         }
       } else {
@@ -215,9 +224,10 @@ int dml_cpu_sizeof_treespec() { return (int)sizeof(TreeSpec); }
 
 void* dml_cpu_forest_build(const uint8_t* Xb, int64_t ld, int64_t n, int64_t d, const int32_t* ycls,
                            const float* yreg, int64_t n_classes, int64_t is_reg, const uint8_t* roles,
-                           const TreeSpec* specs, int64_t T, int64_t ystride) {
+                           const TreeSpec* specs, int64_t T, int64_t ystride, const double* cw) {
   Data D;
   D.ystride = ystride;
+  D.cw = cw;
   D.Xb = Xb; D.ld = ld; D.n = (int)n; D.d = (int)d; D.is_reg = (int)is_reg;
   D.C = is_reg ? 1 : (int)n_classes;
   D.CH = is_reg ? 4 : (int)n_classes + 1;
@@ -228,7 +238,7 @@ void* dml_cpu_forest_build(const uint8_t* Xb, int64_t ld, int64_t n, int64_t d, 
   F->VC = D.VC;
   F->trees.resize(T);
 #pragma omp parallel for schedule(dynamic, 1)
-  for (int64_t t = 0; t < T; ++t) build_tree(D, specs[t], F->trees[t]);
+  for (int64_t t = 0; t < T; ++t) build_tree(D, specs[t], t, F->trees[t]);
   return F;
 }
 
@@ -274,6 +284,22 @@ void dml_cpu_forest_apply(const uint8_t* Xb, int64_t ld, int64_t n, const NodeRe
       }
       leaf[(int64_t)t * n + r] = node;
     }
+}
+
+// max_leaf_nodes: best-first top of each limited tree (forest_common.h, the routine the
+// HIP kernel k_prune_best_first runs); limit[t] <= 0 leaves tree t alone
+void dml_cpu_forest_prune(NodeRec* nodes, const double* vals, int64_t VC, int32_t C, int32_t is_reg,
+                          const TreeSpec* specs, const int32_t* limit, int32_t T, int32_t* leaves) {
+  std::vector<FrontierEnt> heap;
+  for (int32_t t = 0; t < T; ++t) {
+    if (limit[t] <= 0) {
+      if (leaves) leaves[t] = -1;
+      continue;
+    }
+    heap.resize((size_t)limit[t]);
+    const int n = best_first_prune(nodes, vals, VC, C, is_reg != 0, specs[t].criterion, t, limit[t], heap.data());
+    if (leaves) leaves[t] = n;
+  }
 }
 
 // sklearn midpoint thresholds for exactly-binned features (same two passes as predict.hip)

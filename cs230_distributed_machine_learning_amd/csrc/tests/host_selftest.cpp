@@ -18,7 +18,7 @@ using namespace dml;
 
 extern "C" {
 void* dml_cpu_forest_build(const uint8_t*, int64_t, int64_t, int64_t, const int32_t*, const float*, int64_t, int64_t,
-                           const uint8_t*, const TreeSpec*, int64_t, int64_t);
+                           const uint8_t*, const TreeSpec*, int64_t, int64_t, const double*);
 int64_t dml_cpu_forest_num_nodes(void*);
 void dml_cpu_forest_export(void*, NodeRec*, double*);
 void dml_cpu_forest_apply(const uint8_t*, int64_t, int64_t, const NodeRec*, int32_t, int32_t, int32_t*);
@@ -84,8 +84,10 @@ static void forest_case(bool is_reg, int crit) {
   for (int t = 0; t < T; ++t)
     specs.push_back(make_spec(0x9e37ull * (t + 1), t / 4, t % 2 ? 6 : std::numeric_limits<int32_t>::max(),
                               2 + t % 3, 1 + t % 2, t % 3 == 0 ? (int)d : 4, t % 4 == 3 ? 0 : 1, crit));
+  if (!is_reg)   // class_weight="balanced_subsample" on some trees (weights from the bootstrap counts)
+    for (int t = 4; t < T; t += 5) specs[t].cw_mode = 2;
   void* h = dml_cpu_forest_build(Xb.data(), d, n, d, is_reg ? nullptr : ycls.data(), is_reg ? yreg.data() : nullptr,
-                                 C, is_reg, roles.data(), specs.data(), T, 0);
+                                 C, is_reg, roles.data(), specs.data(), T, 0, nullptr);
   CHECK(h != nullptr);
   const int64_t P = dml_cpu_forest_num_nodes(h);
   CHECK(P >= T);

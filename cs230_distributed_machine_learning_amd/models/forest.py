@@ -9,11 +9,14 @@ of whole fits, then every fit's held-out rows are predicted in one launch.
 Supported: n_estimators, criterion (gini/entropy/log_loss; squared_error; friedman_mse
 and absolute_error/poisson approximate with squared_error), max_depth,
 min_samples_split, min_samples_leaf (int or fraction), max_features (sqrt/log2/None/
-int/float), bootstrap, max_samples, min_impurity_decrease, random_state.  Parameters
+int/float), bootstrap, max_samples, min_impurity_decrease, max_leaf_nodes (sklearn's
+best-first tree: the grown tree is cut to its best-first top, ops/forest_ops.py
+prune_max_leaves), random_state.  Parameters
 with no effect on the fitted function (n_jobs, verbose, warm_start, oob_score) are
-accepted and ignored; unsupported ones (class_weight != None, ccp_alpha > 0,
-max_leaf_nodes, min_weight_fraction_leaf > 0, monotonic_cst) are reported in the
-subtask's ``warnings``.
+accepted and ignored; class_weight (dict / "balanced" / "balanced_subsample") scales
+the per-class sums inside the builder exactly where sklearn's sample weights would;
+unsupported ones (ccp_alpha > 0, min_weight_fraction_leaf > 0, monotonic_cst) are
+reported in the subtask's ``warnings``.
 """
 from __future__ import annotations
 
@@ -32,17 +35,21 @@ from .base import Family, FitOutput, FitTask, ParamError, as_bool, as_float, as_
 _CLS = "RandomForestClassifier"
 _REG = "RandomForestRegressor"
 
+_DEFAULT = object()   # "parameter not given"
+
 _DEFAULTS = {
     "n_estimators": 100, "criterion": None, "max_depth": None, "min_samples_split": 2, "min_samples_leaf": 1,
-    "min_weight_fraction_leaf": 0.0, "max_features": None, "max_leaf_nodes": None, "min_impurity_decrease": 0.0,
+    "min_weight_fraction_leaf": 0.0, "max_features": _DEFAULT, "max_leaf_nodes": None, "min_impurity_decrease": 0.0,
     "bootstrap": True, "oob_score": False, "n_jobs": None, "random_state": None, "verbose": 0,
     "warm_start": False, "class_weight": None, "ccp_alpha": 0.0, "max_samples": None, "monotonic_cst": None,
 }
 
 
 def _max_features(v, d, is_cls):
-    if v is None or v == "None":
+    if v is _DEFAULT:        # sklearn's defaults: "sqrt" (classifier), 1.0 (regressor)
         v = "sqrt" if is_cls else 1.0
+    if v is None or v == "None":   # an explicit None means every feature
+        return d
     if isinstance(v, str):
         if v == "sqrt" or v == "auto":
             return max(1, int(math.sqrt(d)))
@@ -114,18 +121,30 @@ class ForestFamily(Family):
             else:
                 lam = min(1.0, as_int(ms, "max_samples", lo=1) / max(1, n_train))
         mid = as_float(p["min_impurity_decrease"], "min_impurity_decrease", lo=0.0)
-        if p["class_weight"] not in (None, "None"):
-            warn.append("class_weight is not supported yet; fitted unweighted")
+        cw = p["class_weight"]
+        if cw in ("None",):
+            cw = None
+        if cw is not None:
+            if not is_cls:
+                raise ParamError("class_weight is only valid for classifiers")
+            if isinstance(cw, str):
+                if cw not in ("balanced", "balanced_subsample"):
+                    raise ParamError(f"class_weight {cw!r} must be a dict, 'balanced' or 'balanced_subsample'")
+            elif isinstance(cw, dict):
+                cw = {str(k): as_float(v, "class_weight value", lo=0.0) for k, v in cw.items()}
+            else:
+                raise ParamError("class_weight must be a dict, 'balanced', 'balanced_subsample' or None")
         if as_float(p["ccp_alpha"], "ccp_alpha", lo=0.0) > 0:
             warn.append("ccp_alpha pruning not supported; ignored")
-        if p["max_leaf_nodes"] not in (None, "None"):
-            warn.append("max_leaf_nodes not supported; ignored")
+        mln = as_int(p["max_leaf_nodes"] if p["max_leaf_nodes"] != "None" else None, "max_leaf_nodes", lo=2,
+                     allow_none=True)
         if as_float(p["min_weight_fraction_leaf"], "min_weight_fraction_leaf", lo=0.0, hi=0.5) > 0:
             warn.append("min_weight_fraction_leaf not supported; ignored")
         return {
             "n_estimators": n_est, "criterion": crit_id, "max_depth": md if md is not None else forest_ops.INT32_MAX,
             "min_samples_split": mss, "min_samples_leaf": msl, "max_features": k, "bootstrap": int(boot),
             "lambda": lam, "min_impurity_decrease": mid, "seed": seed_of(p["random_state"]), "warnings": warn,
+            "class_weight": cw, "max_leaf_nodes": mln or 0,
         }
 
     def cost(self, model_type, rp, n_train, n_features, n_classes) -> float:
@@ -241,20 +260,61 @@ class ForestFamily(Family):
             sl["criterion"] = rp["criterion"]
             sl["min_impurity_decrease"] = rp["min_impurity_decrease"]
             sl["pois_cdf"] = native.poisson_cdf_table(rp["lambda"])
+            cw = rp.get("class_weight")
+            sl["cw_mode"] = 0 if cw is None else (2 if cw == "balanced_subsample" else 1)
             i += n
         return specs
 
+    @staticmethod
+    def class_weight_table(data, batch: List[FitTask], specs: np.ndarray):
+        """[T, C] class weights per tree (sklearn semantics) or None when no fit uses them.
+        ``balanced``: n_train / (n_classes_present * n_k) over the fit's training rows;
+        a dict maps class labels to weights (missing classes 1); ``balanced_subsample``
+        rows are computed per tree on the device from its bootstrap counts."""
+        if not any(t.params.get("class_weight") is not None for t in batch) or not data.classification:
+            return None
+        C = data.n_classes
+        tab = np.ones((len(specs), C), dtype=np.float64)
+        roles = data.roles_np()
+        labels = [str(c) for c in np.asarray(data.classes).tolist()]
+        i = 0
+        for t in batch:
+            n = t.params["n_estimators"]
+            cw = t.params.get("class_weight")
+            row = np.ones(C, dtype=np.float64)
+            if cw == "balanced":
+                from ..search.cv import ROLE_TRAIN
+
+                y_tr = data.y_enc[roles[t.split] == ROLE_TRAIN]
+                cnt = np.bincount(y_tr, minlength=C).astype(np.float64)
+                present = max(1, int((cnt > 0).sum()))
+                row = np.where(cnt > 0, len(y_tr) / (present * np.maximum(cnt, 1)), 1.0)
+            elif isinstance(cw, dict):
+                for k, lab in enumerate(labels):
+                    if lab in cw:
+                        row[k] = float(cw[lab])
+                    elif lab.lstrip("-").isdigit() and str(int(lab)) in cw:
+                        row[k] = float(cw[str(int(lab))])
+            tab[i:i + n] = row
+            i += n
+        return tab
+
     def _run_batch(self, data, Xb, batch: List[FitTask], is_reg: bool, keep_models: bool) -> List[FitOutput]:
         specs = self._specs(batch)
+        cw = self.class_weight_table(data, batch, specs)
         t0 = time.perf_counter()
         if data.is_gpu:
             fb = forest_ops.build_gpu(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
                                       data.n_classes, is_reg, self.tiers, reuse_pool=True,
-                                      XbT=data.binned_feature_major())
+                                      XbT=data.binned_feature_major(), cw=cw)
         else:
             fb = forest_ops.build_cpu(Xb.numpy(), data.y_enc, None if not is_reg else data.y_reg.numpy(),
-                                      data.roles_np(), specs, data.n_classes, is_reg)
+                                      data.roles_np(), specs, data.n_classes, is_reg, cw=cw)
         try:
+            if any(t.params.get("max_leaf_nodes") for t in batch):
+                with trace.range("forest_prune"):
+                    forest_ops.prune_max_leaves(fb, specs, np.repeat(
+                        [t.params.get("max_leaf_nodes", 0) for t in batch], [t.params["n_estimators"] for t in batch]))
             with trace.range("forest_refine"):
                 _refine(data, fb, Xb, specs, data.roles)
             toff = np.zeros(len(batch) + 1, dtype=np.int64)

@@ -202,7 +202,8 @@ def _carve(buf: torch.Tensor, off: int, shape, dtype) -> torch.Tensor:
 
 def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,
               specs: np.ndarray, n_classes: int, is_reg: bool, tiers: ForestTiers | None = None,
-              ystride: int = 0, reuse_pool: bool = False, XbT: Optional[torch.Tensor] = None) -> ForestBuild:
+              ystride: int = 0, reuse_pool: bool = False, XbT: Optional[torch.Tensor] = None,
+              cw: Optional[np.ndarray] = None) -> ForestBuild:
     """``ystride > 0``: ``yreg`` is a [targets, ystride] matrix and tree t regresses on
     row ``specs[t]['target']`` (gradient boosting's per-fit pseudo-residuals).
     ``reuse_pool``: the node arrays live in the device arena and are valid until the
@@ -228,6 +229,11 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     if XbT is not None:
         assert XbT.shape == (d, n) and XbT.dtype == torch.uint8 and XbT.is_contiguous() and XbT.device == dev
     a.XbT = native.ptr(XbT) if XbT is not None else 0
+    # class-weight table [T, C] float64 (rows of cw_mode 2 trees are filled by the kernel)
+    cw_dev = None
+    if cw is not None and not is_reg:
+        cw_dev = torch.from_numpy(np.ascontiguousarray(cw, dtype=np.float64).reshape(T, n_classes)).to(dev)
+    a.cw = native.ptr(cw_dev) if cw_dev is not None else 0
     a.active_count = native.ptr(active)
     t0 = time.perf_counter()
     with trace.range("forest_count"):
@@ -317,7 +323,8 @@ def release_pool(fb: ForestBuild) -> None:
 
 
 def build_cpu(Xb: np.ndarray, ycls: Optional[np.ndarray], yreg: Optional[np.ndarray], roles: np.ndarray,
-              specs: np.ndarray, n_classes: int, is_reg: bool, ystride: int = 0) -> ForestBuild:
+              specs: np.ndarray, n_classes: int, is_reg: bool, ystride: int = 0,
+              cw: Optional[np.ndarray] = None) -> ForestBuild:
     lib = native.cpu_lib()
     Xb = np.ascontiguousarray(Xb, dtype=np.uint8)
     roles = np.ascontiguousarray(roles, dtype=np.uint8)
@@ -328,9 +335,10 @@ def build_cpu(Xb: np.ndarray, ycls: Optional[np.ndarray], yreg: Optional[np.ndar
     T = len(specs)
     VC = 3 if is_reg else n_classes
     t0 = time.perf_counter()
+    cw = None if (cw is None or is_reg) else np.ascontiguousarray(cw, dtype=np.float64).reshape(T, n_classes)
     h = lib.dml_cpu_forest_build(native.ptr(Xb), d, n, d, native.ptr(ycls), native.ptr(yreg),
                                  (1 if is_reg else n_classes), int(is_reg), native.ptr(roles), native.ptr(specs), T,
-                                 int(ystride))
+                                 int(ystride), native.ptr(cw))
     try:
         P = lib.dml_cpu_forest_num_nodes(h)
         nodes = np.empty((P, 2), dtype=np.int32)
@@ -339,6 +347,46 @@ def build_cpu(Xb: np.ndarray, ycls: Optional[np.ndarray], yreg: Optional[np.ndar
     finally:
         lib.dml_cpu_forest_free(h)
     return ForestBuild(nodes, vals, T, VC, is_reg, n_classes, {"nodes": int(P), "build_s": time.perf_counter() - t0})
+
+
+PRUNE_SCRATCH_BYTES = 256 << 20
+
+
+def prune_max_leaves(fb: ForestBuild, specs: np.ndarray, limit: np.ndarray) -> np.ndarray:
+    """max_leaf_nodes: keep each limited tree's best-first top (sklearn's
+    BestFirstTreeBuilder order; csrc/kernels/forest_common.h best_first_prune), in place.
+    ``limit``: int32 [T], 0 = unlimited.  Returns the leaf count per tree (-1 = untouched)."""
+    T = len(specs)
+    limit = np.ascontiguousarray(limit, dtype=np.int32)
+    lim_trees = np.nonzero(limit > 0)[0]
+    if lim_trees.size == 0:
+        return np.full(T, -1, dtype=np.int32)
+    VC, C = int(fb.VC), (1 if fb.is_reg else int(fb.n_classes))
+    if not fb.on_gpu:
+        leaves = np.empty(T, dtype=np.int32)
+        specs_c = np.ascontiguousarray(specs)
+        native.cpu_lib().dml_cpu_forest_prune(native.ptr(fb.nodes), native.ptr(fb.vals), VC, C, int(fb.is_reg),
+                                              native.ptr(specs_c), native.ptr(limit), T, native.ptr(leaves))
+        return leaves
+    dev = fb.nodes.device
+    lib = native.hip_lib()
+    specs_dev = torch.from_numpy(specs.view(np.uint8).copy()).to(dev)
+    lim_dev = torch.from_numpy(limit).to(dev)
+    leaves = torch.full((T,), -1, dtype=torch.int32, device=dev)
+    cap = int(limit.max())
+    per = max(1, PRUNE_SCRATCH_BYTES // (16 * cap))
+    t, t_end = int(lim_trees[0]), int(lim_trees[-1]) + 1
+    heap = torch.empty(min(per, t_end - t) * cap * 16, dtype=torch.uint8, device=dev)
+    stream = native.stream_handle(dev)
+    while t < t_end:
+        n = min(per, t_end - t)
+        rc = lib.dml_forest_prune(native.ptr(fb.nodes), native.ptr(fb.vals), VC, C, int(fb.is_reg),
+                                  native.ptr(specs_dev), native.ptr(lim_dev), t, n, native.ptr(heap), cap,
+                                  native.ptr(leaves), stream)
+        if rc:
+            raise RuntimeError(f"dml_forest_prune failed ({rc})")
+        t += n
+    return leaves.cpu().numpy()   # also keeps specs_dev / heap alive until the kernels are done
 
 
 def refine_thresholds(fb: ForestBuild, Xb, specs: np.ndarray, roles, vals, exact) -> None:

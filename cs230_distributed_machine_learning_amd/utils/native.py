@@ -42,6 +42,8 @@ TREESPEC_DTYPE = np.dtype(
         ("min_impurity_decrease", "<f4"),
         ("target", "<i4"),
         ("pois_cdf", "<u4", (POIS_TABLE,)),
+        ("cw_mode", "<i4"),
+        ("reserved", "<i4"),
     ]
 )
 
@@ -66,7 +68,7 @@ ForestArgs = _i64_struct(
         "sub_max", "sub_cache_d",
         "n_nodes_out", "status_out", "levels_out", "large_rounds_out",
         "tier0_nodes", "tier1_nodes", "tier2_nodes", "tier3_nodes",
-        "ystride", "XbT",
+        "ystride", "XbT", "cw",
     ],
 )
 
@@ -105,9 +107,10 @@ def cpu_lib() -> ctypes.CDLL:
                 raise RuntimeError("TreeSpec layout mismatch between C++ and Python")
             lib.dml_cpu_forest_build.restype = c_vp
             lib.dml_cpu_forest_build.argtypes = [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64,
-                                                 c_i64]
+                                                 c_i64, c_vp]
             lib.dml_cpu_forest_apply.argtypes = [c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp]
             lib.dml_cpu_forest_refine.argtypes = [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp]
+            lib.dml_cpu_forest_prune.argtypes = [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp]
             lib.dml_cpu_forest_num_nodes.restype = c_i64
             lib.dml_cpu_forest_num_nodes.argtypes = [c_vp]
             lib.dml_cpu_forest_export.argtypes = [c_vp, c_vp, c_vp]
@@ -176,6 +179,7 @@ def _register_optional(lib) -> None:
                             c_vp, c_vp]),
         "dml_knn_qpw": (c_i32, []),
         "dml_forest_apply": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp]),
+        "dml_forest_prune": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp]),
         "dml_svm_sizeof_prob": (c_i32, []),
         "dml_forest_refine": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
                                       c_vp]),

@@ -109,6 +109,69 @@ def test_gpu_trees_match_cpu(n, d, C, kw, tiers, words, monkeypatch):
     assert np.allclose(sg, sc)
 
 
+@pytest.mark.parametrize("tiers", range(len(TIERS)))
+@pytest.mark.parametrize("n,d,C", [(4000, 12, 2), (30000, 16, 3)])
+def test_gpu_class_weighted_trees_match_cpu(n, d, C, tiers):
+    """class_weight: dict weights (cw_mode 1) and balanced_subsample (cw_mode 2, weights
+    computed by the root kernel from each tree's bootstrap counts) give identical trees."""
+    X, y = _data(n, d, C, seed=3)
+    y = np.where(np.random.RandomState(0).rand(n) < 0.6, 0, y)       # imbalanced
+    dev = torch.device("cuda:0")
+    edges = binning.quantile_edges(torch.from_numpy(X).to(dev))
+    Xb = binning.bin_matrix(torch.from_numpy(X).to(dev), edges)
+    Xb_cpu = Xb.cpu().numpy()
+    roles, _ = make_split_roles(y, 3, True, holdout=False)
+    specs = _specs(3, 6, d, msl=2)
+    T = len(specs)
+    cw = np.ones((T, C))
+    for t in range(T):
+        specs[t]["cw_mode"] = (0, 1, 2)[t % 3]
+        if t % 3 == 1:
+            cw[t] = 1.0 + np.arange(C) * 2.5
+    ycls = y.astype(np.int32)
+    g = forest_ops.build_gpu(Xb, torch.from_numpy(ycls).to(dev), None, torch.from_numpy(roles).to(dev), specs, C, False,
+                             forest_ops.ForestTiers(**TIERS[tiers]), cw=cw.copy())
+    c = forest_ops.build_cpu(Xb_cpu, ycls, None, roles, specs, C, False, cw=cw.copy())
+    gc = _canon(g.nodes.cpu().numpy(), g.vals.cpu().numpy(), T)
+    cc = _canon(c.nodes, c.vals, T)
+    assert gc == cc
+
+
+@pytest.mark.parametrize("is_reg", [False, True])
+def test_gpu_max_leaf_prune_matches_cpu(is_reg):
+    """max_leaf_nodes: the HIP best-first pass (one lane per tree) keeps the same nodes as
+    the C++ one, and every limited tree ends with at most L leaves."""
+    n, d, C = 20000, 16, 3
+    X, y = _data(n, d, C, seed=4)
+    dev = torch.device("cuda:0")
+    Xb = binning.bin_matrix(torch.from_numpy(X).to(dev), binning.quantile_edges(torch.from_numpy(X).to(dev)))
+    Xb_cpu = Xb.cpu().numpy()
+    roles, _ = make_split_roles(y, 3, True, holdout=False)
+    specs = _specs(3, 8, d, criterion=2 if is_reg else 1)
+    T = len(specs)
+    limit = np.array([(0, 2, 7, 40, 3000)[t % 5] for t in range(T)], dtype=np.int32)
+    if is_reg:
+        yr = (X[:, 0] * 2 + X[:, 1] ** 2).astype(np.float32)
+        g = forest_ops.build_gpu(Xb, None, torch.from_numpy(yr).to(dev), torch.from_numpy(roles).to(dev), specs, 1, True)
+        c = forest_ops.build_cpu(Xb_cpu, None, yr, roles, specs, 1, True)
+    else:
+        ycls = y.astype(np.int32)
+        g = forest_ops.build_gpu(Xb, torch.from_numpy(ycls).to(dev), None, torch.from_numpy(roles).to(dev), specs, C,
+                                 False)
+        c = forest_ops.build_cpu(Xb_cpu, ycls, None, roles, specs, C, False)
+    lg = forest_ops.prune_max_leaves(g, specs, limit)
+    lc = forest_ops.prune_max_leaves(c, specs, limit)
+    for lv in (lg, lc):
+        assert all(lv[t] == -1 if limit[t] == 0 else 1 <= lv[t] <= limit[t] for t in range(T))
+    gn = g.nodes.cpu().numpy()
+    for t in range(T):   # the reported leaf count is the reachable one
+        if limit[t]:
+            assert sum(1 for s, _ in _canon(gn, g.vals.cpu().numpy(), t + 1)[t] if s < 0) == lg[t]
+    if not is_reg:   # (regression sums are float atomics on the GPU: trees equal only up to rounding)
+        assert np.array_equal(lg, lc)
+        assert _canon(gn, g.vals.cpu().numpy(), T) == _canon(c.nodes, c.vals, T)
+
+
 @pytest.mark.parametrize("words", ["packed", "plain"])
 def test_gpu_regression_close_to_cpu(words, monkeypatch):
     from sklearn.datasets import make_regression
