@@ -166,12 +166,36 @@ DML_HD uint64_t pack_bin(int cls, uint32_t w) {
 #pragma clang fp contract(off)
 #endif
 
+// log2 for the entropy criterion, written out in IEEE +,-,*,/ (no FMA contraction in this
+// header) so host and device round identically: the device libm's log2 and glibc's can
+// differ by an ulp, enough to flip an entropy tie between two splits and make the HIP and
+// C++ builders grow different trees.  x = m 2^e with m in [sqrt(1/2), sqrt(2));
+// ln m = 2 atanh(s), s = (m-1)/(m+1), |s| < 0.1716: the series to s^21 is below 1e-18.
 DML_HD double dlog2(double x) {
+  int e;
 #if defined(__HIP_DEVICE_COMPILE__)
-  return ::log2(x);
+  double m = ::frexp(x, &e);
 #else
-  return log2(x);
+  double m = frexp(x, &e);
 #endif
+  if (m < 0.70710678118654752440) {
+    m = m * 2.0;
+    e -= 1;
+  }
+  const double s = (m - 1.0) / (m + 1.0);
+  const double s2 = s * s;
+  double p = 1.0 / 21.0;
+  p = p * s2 + 1.0 / 19.0;
+  p = p * s2 + 1.0 / 17.0;
+  p = p * s2 + 1.0 / 15.0;
+  p = p * s2 + 1.0 / 13.0;
+  p = p * s2 + 1.0 / 11.0;
+  p = p * s2 + 1.0 / 9.0;
+  p = p * s2 + 1.0 / 7.0;
+  p = p * s2 + 1.0 / 5.0;
+  p = p * s2 + 1.0 / 3.0;
+  p = p * s2 + 1.0;
+  return (double)e + (2.0 * s * p) * 1.44269504088896340736;
 }
 
 // Accumulator for one side of a classification split, fed class sums in class order.

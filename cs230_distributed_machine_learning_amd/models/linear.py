@@ -401,10 +401,21 @@ class LogisticFamily(Family):
         return f, G
 
     def _solve(self, data, b: _Batch):
-        """Batched L-BFGS; columns with an L1 term use OWL-QN (Andrew & Gao 2007):
-        pseudo-gradient, orthant-constrained direction and line search.  Columns without
-        L1 reduce exactly to plain L-BFGS."""
+        """Batched L-BFGS that stays on the device; columns with an L1 term use OWL-QN
+        (Andrew & Gao 2007): pseudo-gradient, orthant-constrained direction and line
+        search.  Columns without L1 reduce exactly to plain L-BFGS.
+
+        Every fit runs its own L-BFGS state machine, advanced by masked tensor ops: one
+        global step = one batched objective evaluation at every fit's current trial point,
+        after which each fit independently accepts its trial (Armijo; history push into
+        its slot of a ring buffer, new two-loop direction, step 1) or backtracks (halve its
+        step).  A fit that backtracks therefore never holds the others back, and nothing on
+        the way needs the host: the only device->host read is the "any fit still active"
+        flag, once every ``sync_every`` steps (``last_solve_stats['host_syncs']``).  Each
+        fit's iterates are the ones a lock-step L-BFGS would produce for it alone."""
         d, dev = data.d, data.device
+        H, Fn = self.history, b.F
+        col = b.col_fit
         W = torch.zeros((d + 1, b.M), dtype=torch.float32, device=dev)
         f, G = self._objective(data, b, W)
         l1 = None
@@ -423,82 +434,120 @@ class LogisticFamily(Family):
             at0 = torch.where(gp < 0, gp, torch.where(gm > 0, gm, torch.zeros_like(Gv)))
             return torch.where(Wv != 0, Gv + l1 * torch.sign(Wv), at0)
 
-        F = total(f, W)
-        PG = pseudo(W, G)
-        hs, hy, hrho = [], [], []
-        iters = torch.zeros(b.F, dtype=torch.int64, device=dev)
-        stalled = torch.zeros(b.F, dtype=torch.bool, device=dev)
-        max_it = int(b.max_iter.max().item()) if b.F else 0
-        n_evals = 1
-        for it in range(max_it):
-            gmax = b.segmax(PG.abs().amax(0))
-            active = (gmax > b.tol) & (iters < b.max_iter) & ~stalled
-            if not bool(active.any()):
-                break
-            act_col = active[b.col_fit].to(W.dtype)
-            q = PG.clone()
-            alphas = []
-            for s_, y_, rho in zip(reversed(hs), reversed(hy), reversed(hrho)):
-                a = rho * b.segsum((s_ * q).sum(0))
-                q -= a[b.col_fit] * y_
-                alphas.append(a)
-            if hs:
-                sy = b.segsum((hs[-1] * hy[-1]).sum(0))
-                yy = b.segsum((hy[-1] * hy[-1]).sum(0))
-                gamma = torch.where(yy > 0, sy / yy.clamp_min(1e-30), torch.ones_like(yy))
-            else:
-                gnorm = b.segsum((PG * PG).sum(0)).sqrt()
-                gamma = 1.0 / gnorm.clamp_min(1.0)
-            r = q * gamma[b.col_fit]
-            for (s_, y_, rho), a in zip(zip(hs, hy, hrho), reversed(alphas)):
-                bb = rho * b.segsum((y_ * r).sum(0))
-                r += (a - bb)[b.col_fit] * s_
+        S = torch.zeros((H, d + 1, b.M), dtype=W.dtype, device=dev)   # ring buffers of (s, y) pairs
+        Y = torch.zeros_like(S)
+        RHO = torch.zeros((H, Fn), dtype=torch.float32, device=dev)
+        hcount = torch.zeros(Fn, dtype=torch.int64, device=dev)       # pairs pushed per fit
+        iters = torch.zeros(Fn, dtype=torch.int64, device=dev)
+        stalled = torch.zeros(Fn, dtype=torch.bool, device=dev)
+        ls = torch.zeros(Fn, dtype=torch.int32, device=dev)           # trials of the current iteration
+        step = torch.ones(Fn, dtype=torch.float32, device=dev)
+        hidx = torch.arange(H, device=dev)
+
+        def direction(PGv, Wv, act):
+            """Two-loop recursion over each fit's own newest-first history; returns the
+            search direction and (OWL-QN) the orthant signs of the line search."""
+            q = PGv.clone()
+            n_hist = hcount.clamp(max=H)
+            slots, alphas = [], []
+            for i in range(H):
+                slot = (hcount - 1 - i) % H                            # [F]
+                valid = (i < n_hist).to(RHO.dtype)
+                sl_col = slot[col].view(1, 1, -1).expand(1, d + 1, b.M)
+                Si, Yi = S.gather(0, sl_col)[0], Y.gather(0, sl_col)[0]
+                rho_i = RHO.gather(0, slot.view(1, -1))[0] * valid
+                a_i = rho_i * b.segsum((Si * q).sum(0))
+                q -= a_i[col] * Yi
+                slots.append((Si, Yi, rho_i))
+                alphas.append(a_i)
+            S0, Y0, _ = slots[0]
+            sy = b.segsum((S0 * Y0).sum(0))
+            yy = b.segsum((Y0 * Y0).sum(0))
+            gamma_h = torch.where(yy > 0, sy / yy.clamp_min(1e-30), torch.ones_like(yy))
+            gnorm = b.segsum((PGv * PGv).sum(0)).sqrt()
+            gamma = torch.where(hcount > 0, gamma_h, 1.0 / gnorm.clamp_min(1.0))
+            r = q * gamma[col]
+            for i in reversed(range(H)):
+                Si, Yi, rho_i = slots[i]
+                bb = rho_i * b.segsum((Yi * r).sum(0))
+                r += (alphas[i] - bb)[col] * Si
+            act_col = act[col].to(Wv.dtype)
             p = -r * act_col
             if l1 is not None:   # keep the direction in the pseudo-gradient's orthant
-                p = torch.where(l1on & (p * PG >= 0), torch.zeros_like(p), p)
-            gtp = b.segsum((PG * p).sum(0))
-            bad = (gtp >= 0) & active
-            if bool(bad.any()):  # not a descent direction: restart from steepest descent
-                badc = bad[b.col_fit].to(W.dtype)
-                p = p * (1 - badc) - PG * badc * act_col
-                gtp = b.segsum((PG * p).sum(0))
-            xi = None if l1 is None else torch.where(W != 0, torch.sign(W), torch.sign(-PG))
-            step = torch.ones(b.F, dtype=torch.float32, device=dev)
+                p = torch.where(l1on & (p * PGv >= 0), torch.zeros_like(p), p)
+            gtp = b.segsum((PGv * p).sum(0))
+            bad = ((gtp >= 0) & act)[col].unsqueeze(0)               # not a descent direction:
+            p = torch.where(bad, -PGv * act_col, p)                  # restart from steepest descent
+            xi = None if l1 is None else torch.where(Wv != 0, torch.sign(Wv), torch.sign(-PGv))
+            return p, xi
 
-            def trial(stp):
-                Wt = W + p * stp[b.col_fit]
-                if xi is not None:   # orthant projection
-                    Wt = torch.where(l1on & (Wt * xi <= 0), torch.zeros_like(Wt), Wt)
-                return Wt
+        def trial(Wv, p, xi, stp, act):
+            Wt = Wv + p * stp[col]
+            if xi is not None:   # orthant projection
+                Wt = torch.where(l1on & (Wt * xi <= 0), torch.zeros_like(Wt), Wt)
+            return torch.where(act[col].unsqueeze(0), Wt, Wv)
 
-            for _ls in range(30):
-                Wt = trial(step)
-                ft, Gt = self._objective(data, b, Wt)
-                Ft = total(ft, Wt)
-                n_evals += 1
-                # float32 (or bf16x3 on the matrix cores) objective: tolerate round-off near the optimum
-                slack = (4e-6 if b.mf is not None else 1e-7) * F.abs() + 1e-12
-                dec = b.segsum((PG * (Wt - W)).sum(0)).double()
-                ok = (Ft <= F + 1e-4 * dec + slack) | ~active
-                if bool(ok.all()):
-                    break
-                step = torch.where(ok, step, step * 0.5)
-            else:
-                stalled |= ~ok
-                Wt = trial(step * ok.to(step.dtype))
-                ft, Gt = self._objective(data, b, Wt)
-                Ft = total(ft, Wt)
-                n_evals += 1
+        Ftot = total(f, W)
+        PG = pseudo(W, G)
+        active = (b.segmax(PG.abs().amax(0)) > b.tol) & (iters < b.max_iter)
+        P, XI = direction(PG, W, active)
+        Wt = trial(W, P, XI, step, active)
+        max_it = max((t.params["max_iter"] for t in b.tasks), default=0)
+        sync_every = max(1, int(os.environ.get("DML_LR_SYNC_EVERY", "4")))
+        n_evals, host_syncs, steps = 1, 0, 0
+        if max_it > 0:
+            host_syncs += 1
+            running = bool(active.any())
+        else:
+            running = False
+        max_steps = max_it * 31
+        while running and steps < max_steps:
+            ft, Gt = self._objective(data, b, Wt)
+            Ft = total(ft, Wt)
+            n_evals += 1
+            steps += 1
+            # float32 (or bf16x3 on the matrix cores) objective: tolerate round-off near the optimum
+            slack = (4e-6 if b.mf is not None else 1e-7) * Ftot.abs() + 1e-12
+            dec = b.segsum((PG * (Wt - W)).sum(0)).double()
+            ok = Ft <= Ftot + 1e-4 * dec + slack
+            acc = ok & active
+            rej = active & ~ok
+            ls = ls + rej.to(ls.dtype)
+            fail = rej & (ls >= 30)                                  # line search exhausted
+            stalled |= fail
+            # accepted fits push (s, y) into their next ring slot and move to the trial point
+            acc_c = acc[col].unsqueeze(0)
             s_vec = Wt - W
             y_vec = Gt - G
             sy = b.segsum((s_vec * y_vec).sum(0))
             rho = torch.where(sy > 1e-10, 1.0 / sy.clamp_min(1e-10), torch.zeros_like(sy))
-            hs.append(s_vec); hy.append(y_vec); hrho.append(rho)
-            if len(hs) > self.history:
-                hs.pop(0); hy.pop(0); hrho.pop(0)
-            W, f, G, F = Wt, ft, Gt, Ft
+            slot = hcount % H
+            put = (hidx.view(-1, 1) == slot.view(1, -1)) & acc.view(1, -1)     # [H, F]
+            put_c = put[:, col].unsqueeze(1)                                    # [H, 1, M]
+            S = torch.where(put_c, s_vec.unsqueeze(0), S)
+            Y = torch.where(put_c, y_vec.unsqueeze(0), Y)
+            RHO = torch.where(put, rho.view(1, -1), RHO)
+            hcount = hcount + acc.to(hcount.dtype)
+            W = torch.where(acc_c, Wt, W)
+            G = torch.where(acc_c, Gt, G)
+            Ftot = torch.where(acc, Ft, Ftot)
+            iters = iters + (acc | fail).to(iters.dtype)
             PG = pseudo(W, G)
-            iters += active.to(torch.int64)
+            active = (b.segmax(PG.abs().amax(0)) > b.tol) & (iters < b.max_iter) & ~stalled
+            # accepted fits: new direction at step 1; rejected ones: halve their step
+            fresh = acc & active
+            Pn, XIn = direction(PG, W, fresh)
+            fresh_c = fresh[col].unsqueeze(0)
+            P = torch.where(fresh_c, Pn, P)
+            if XI is not None:
+                XI = torch.where(fresh_c, XIn, XI)
+            step = torch.where(fresh, torch.ones_like(step), torch.where(rej, step * 0.5, step))
+            ls = torch.where(fresh, torch.zeros_like(ls), ls)
+            Wt = trial(W, P, XI, step, active)
+            if steps % sync_every == 0:
+                host_syncs += 1
+                running = bool(active.any())
+        self.last_solve_stats = {"host_syncs": host_syncs, "steps": steps, "sync_every": sync_every}
         return W, iters, n_evals
 
     def run(self, data, tasks: List[FitTask], keep_models: bool = False) -> List[FitOutput]:
@@ -541,6 +590,8 @@ class LogisticFamily(Family):
         b.mf = None   # release R^T / slabs before the prediction GEMMs
         d = data.d
         Zte = self._test_logits(data, b, W)
+        iters_h = iters.cpu().tolist()
+        self.last_solve_stats["iterations_max"] = max(iters_h, default=0)
         outs = []
         for f, t in enumerate(tasks):
             k = b.K_l[f]
@@ -556,7 +607,7 @@ class LogisticFamily(Family):
                     pz = torch.sigmoid(z)
                     proba = pz / pz.sum(1, keepdim=True).clamp_min(1e-30)
             outs.append(FitOutput(task_id=t.task_id, pred=pred, proba=proba,
-                                  info={"warnings": t.params.get("warnings", []), "n_iter": int(iters[f].item())}))
+                                  info={"warnings": t.params.get("warnings", []), "n_iter": int(iters_h[f])}))
         if data.is_gpu:
             torch.cuda.synchronize(data.device)
         dt = time.perf_counter() - t0

@@ -17,6 +17,7 @@ and ignored.
 from __future__ import annotations
 
 import math
+import os
 import time
 from typing import Any, Dict, List, Tuple
 
@@ -94,11 +95,39 @@ def knn_search_torch(X: torch.Tensor, qrows: torch.Tensor, train_rows: torch.Ten
     return torch.cat(out_d), torch.cat(out_i)
 
 
+MFMA_KMAX = 32   # the matrix-core path re-ranks 64 candidates: keep >= 32 rows of margin
+
+
+def mfma_operands(data):
+    """bf16 hi/lo planes of X in the MFMA K-step layout [2][KS][npad][16] plus the squared
+    row norms (csrc/kernels/neighbors.hip ``dml_knn_l2_mfma``); built once per dataset."""
+    ops = getattr(data, "_knn_mfma_ops", None)
+    if ops is None:
+        X = data.X
+        n, d = X.shape
+        ks = -(-d // 16)
+        if ks <= 8:
+            ks = 1 << (ks - 1).bit_length()   # register-resident query operand: 1/2/4/8 K-steps
+        npad = -(-n // 128) * 128
+        Xp = torch.zeros((npad, ks * 16), dtype=torch.float32, device=X.device)
+        Xp[:n, :d] = X
+        hi = Xp.to(torch.bfloat16)
+        lo = (Xp - hi.float()).to(torch.bfloat16)
+        xhl = torch.stack([hi, lo]).view(2, npad, ks, 16).transpose(1, 2).contiguous()
+        rn = (X.double() ** 2).sum(1).float().contiguous()
+        ops = (xhl, npad, ks, rn)
+        data._knn_mfma_ops = ops
+    return ops
+
+
 def knn_search_hip(data, splits: List[int], K: int, metric: int, p: float) -> Dict[int, Tuple[torch.Tensor, torch.Tensor]]:
-    """One kernel launch for all test rows of all ``splits``."""
+    """One kernel launch for all test rows of all ``splits``: squared L2 with K <= 32 on the
+    matrix cores (exact re-rank of an MFMA-selected top-64), every other metric on the
+    scalar streaming kernel."""
     lib = native.hip_lib()
     qpw = int(lib.dml_knn_qpw())
     dev = data.device
+    use_mfma = metric == M_L2 and K <= MFMA_KMAX and os.environ.get("DML_KNN_MFMA", "1") != "0"
     qr, qs, spans = [], [], {}
     off = 0
     for s in splits:
@@ -109,15 +138,25 @@ def knn_search_hip(data, splits: List[int], K: int, metric: int, p: float) -> Di
         qs.append(torch.full((m + pad,), s, dtype=torch.long, device=dev))
         spans[s] = (off, m)
         off += m + pad
+    if use_mfma:   # whole workgroups of 4 query groups
+        pad = (-off) % (4 * qpw)
+        qr.append(torch.full((pad,), -1, dtype=torch.long, device=dev))
+        qs.append(torch.full((pad,), splits[-1], dtype=torch.long, device=dev))
     qrow = torch.cat(qr).to(torch.int32).contiguous()
     qsplit = torch.cat(qs).to(torch.int32).contiguous()
     groups = qrow.numel() // qpw
     out_d = torch.empty((qrow.numel(), K), dtype=torch.float32, device=dev)
     out_i = torch.empty((qrow.numel(), K), dtype=torch.int32, device=dev)
-    XT = data.feature_major()
-    rc = lib.dml_knn(native.ptr(data.X), native.ptr(XT), data.n, data.d, native.ptr(data.roles), native.ptr(qrow),
-                     native.ptr(qsplit), groups, metric, float(p if math.isfinite(p) else 0.0), K, native.ptr(out_d),
-                     native.ptr(out_i), native.stream_handle(dev))
+    if use_mfma:
+        xhl, npad, ks, rn = mfma_operands(data)
+        rc = lib.dml_knn_l2_mfma(native.ptr(xhl), npad, ks, native.ptr(rn), native.ptr(data.X), data.n, data.d,
+                                 native.ptr(data.roles), native.ptr(qrow), native.ptr(qsplit), groups, K,
+                                 native.ptr(out_d), native.ptr(out_i), native.stream_handle(dev))
+    else:
+        XT = data.feature_major()
+        rc = lib.dml_knn(native.ptr(data.X), native.ptr(XT), data.n, data.d, native.ptr(data.roles), native.ptr(qrow),
+                         native.ptr(qsplit), groups, metric, float(p if math.isfinite(p) else 0.0), K,
+                         native.ptr(out_d), native.ptr(out_i), native.stream_handle(dev))
     if rc:
         raise RuntimeError(f"dml_knn failed (rc={rc})")
     return {s: (out_d[o:o + m], out_i[o:o + m].long()) for s, (o, m) in spans.items()}

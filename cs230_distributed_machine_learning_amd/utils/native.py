@@ -175,6 +175,8 @@ def _register_optional(lib) -> None:
         "dml_lr_link_grad": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
                                      c_vp, c_vp, c_vp]),
         "dml_lr_predict": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+        "dml_knn_l2_mfma": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp,
+                                    c_vp, c_vp]),
         "dml_knn": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, ctypes.c_float, c_i32, c_vp,
                             c_vp, c_vp]),
         "dml_knn_qpw": (c_i32, []),

@@ -68,6 +68,7 @@ TIERS = [
     (20000, 20, 3, {"msl": 3}),
     (60000, 16, 2, {"max_depth": 12, "k": 16, "bootstrap": 0}),
     (5000, 30, 4, {"criterion": 0, "mss": 10}),
+    (8000, 14, 3, {"criterion": 1}),            # entropy: host/device-identical log2 (forest_common.h)
 ])
 def test_gpu_trees_match_cpu(n, d, C, kw, tiers, words, monkeypatch):
     if words == "plain":   # row ids only (the path for tables too tall for packed row words)

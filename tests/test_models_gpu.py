@@ -40,6 +40,27 @@ def test_knn_kernel_matches_torch(metric, p, n, d, K):
             assert bool(close.all())
 
 
+@pytest.mark.parametrize("n,d,K", [(1000, 7, 5), (5003, 33, 32), (2000, 150, 1), (3000, 20, 9)])
+def test_knn_mfma_l2_equals_scalar_kernel(n, d, K, monkeypatch):
+    """The matrix-core squared-L2 search (bf16x3 selection + exact re-rank) returns the
+    scalar kernel's neighbours and distances bit for bit -- duplicate rows (exact ties)
+    included."""
+    from cs230_distributed_machine_learning_amd.models import neighbors as nb
+
+    rng = np.random.RandomState(n + d)
+    X = rng.randn(n, d).astype(np.float32) * rng.uniform(0.1, 10, d).astype(np.float32)
+    X[n // 2:n // 2 + 50] = X[:50]                      # duplicates -> equal distances
+    y = rng.randint(0, 3, n)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DML_KNN_MFMA", mode)
+        dg = _dd(X, y, True, "cuda:0")
+        out[mode] = nb.knn_search_hip(dg, list(range(len(dg.split_names))), K, 0, 2.0)
+    for s in out["0"]:
+        assert torch.equal(out["1"][s][1], out["0"][s][1])
+        assert torch.equal(out["1"][s][0], out["0"][s][0])
+
+
 def test_knn_gpu_grid_matches_cpu():
     rng = np.random.RandomState(0)
     X = rng.randn(3000, 12).astype(np.float32)
