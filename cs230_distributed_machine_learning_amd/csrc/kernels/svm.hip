@@ -42,6 +42,8 @@ struct SvmProb {
   int64_t iters;     // in/out: iterations done so far
   int64_t status;    // in/out: 0 running, 1 optimal, 2 iteration limit
   int64_t svr;       // 1: variable t uses row t mod nrows
+  int64_t coff;      // split solver: kernel-column cache, S * nrows floats at coff
+  int64_t moff;      // split solver: per-workgroup cache maps, B * (nrows + 2 S) ints at moff
 };
 
 __device__ __forceinline__ float kfun(int kernel, double gamma, double coef0, int degree, float acc) {
@@ -267,6 +269,416 @@ __global__ __launch_bounds__(NT) void k_smo(const float* __restrict__ X, int64_t
   }
 }
 
+// ======================================================================================
+// Split SMO: B workgroups per dual problem + an LRU kernel-column cache in HBM.
+//
+// One workgroup per problem leaves most of the 256 CUs idle (a job has tens of problems)
+// and recomputes two kernel columns per iteration.  Here workgroup w of problem p owns
+// the row slice [r0, r1) (and, for epsilon-SVR, the variables of those rows): the
+// selection sweeps, the kernel-column slices and the gradient update are slice-local, and
+// per SMO iteration the B workgroups exchange only two small records (the slice's best i
+// candidate with its G / alpha; the best j candidate with its G / alpha and max y G).
+// Each record word is a 64-bit agent-scope atomic carrying (sequence tag << 32 | 32
+// payload bits), so a reader spins until every word of a record shows the current tag:
+// no grid barrier, no cache-wide fences.  Every workgroup then reduces the B records in
+// the same order and runs the same two-variable update, so all of them take identical
+// decisions (libsvm's selection, update and stopping rules, as k_smo).
+//
+// Kernel columns go through an LRU cache of S columns per problem (libsvm's Kernel
+// cache, here S * nrows floats in HBM): the slot map (row -> slot) and the slot stamps
+// are replicated per workgroup -- every replica sees the same i/j sequence, so all make
+// the same hit/miss/victim decisions with no shared writes -- and each workgroup fills or
+// reads only its own slice of a slot.
+//
+// Co-residency: a record spin needs all B workgroups of its problem running; the host
+// keeps the grid within the occupancy bound (checked in dml_svm_smo_split) and every spin
+// gives up after kSpinLimit polls (status 3: the host reports an error, no hang).
+constexpr int kRecW = 10;                 // 64-bit words per record
+constexpr int kMaxB = 24;                 // workgroups per problem (B * kRecW <= NT readers)
+constexpr int kMaxSlots = 1 << 16;        // cache slots per problem
+constexpr uint64_t kSpinLimit = 1ull << 22;  // ~5 s of polling: a stuck peer ends the launch, not the GPU
+
+__device__ __forceinline__ void rec_put(uint64_t* w, uint32_t tag, uint32_t payload) {
+  __hip_atomic_store(w, ((uint64_t)tag << 32) | payload, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t lo32(double v) { return (uint32_t)__builtin_bit_cast(uint64_t, v); }
+__device__ __forceinline__ uint32_t hi32(double v) { return (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32); }
+__device__ __forceinline__ double mkd(uint32_t lo, uint32_t hi) {
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+struct SplitCtx {
+  int B, w, S;
+  int64_t r0, r1;
+};
+
+// publish this workgroup's record (payload words v[0..n)) and gather all B records of the
+// exchange into pay[B][kRecW]; returns false if a spin gave up
+__device__ bool exchange(uint64_t* rec, const SplitCtx& sc, uint32_t seq, const uint32_t* v, int n,
+                         uint32_t* pay, int* abort_flag) {
+  uint64_t* mine = rec + ((int64_t)(seq & 1) * sc.B + sc.w) * kRecW;
+  if (threadIdx.x < n) rec_put(mine + threadIdx.x, seq, v[threadIdx.x]);
+  const int total = sc.B * kRecW;
+  if (threadIdx.x < total && (threadIdx.x % kRecW) < n) {
+    const uint64_t* src = rec + (int64_t)(seq & 1) * sc.B * kRecW + threadIdx.x;
+    uint64_t x;
+    uint64_t spins = 0;
+    while (true) {
+      x = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)(x >> 32) == seq) break;
+      if (++spins > kSpinLimit) { *abort_flag = 1; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    pay[threadIdx.x] = (uint32_t)x;
+  }
+  __syncthreads();
+  return *abort_flag == 0;
+}
+
+// kernel value of rowset rows (a, b) -- the same arithmetic as kernel_column's entry
+__device__ float kernel_pair(const SvmProb& p, const float* X, int64_t d, int64_t a, int64_t b) {
+  const float* base = X + p.xoff;
+  float acc = 0.f;
+  if (p.kernel == KRBF) {
+    for (int64_t f = 0; f < d; ++f) {
+      const float t = base[f * p.nrows + a] - base[f * p.nrows + b];
+      acc = __builtin_fmaf(t, t, acc);
+    }
+  } else {
+    for (int64_t f = 0; f < d; ++f) acc = __builtin_fmaf(base[f * p.nrows + a], base[f * p.nrows + b], acc);
+  }
+  return kfun((int)p.kernel, p.gamma, p.coef0, (int)p.degree, acc);
+}
+
+// column of rowset row `src`, rows [r0, r1) only.  Each thread carries 4 rows (stride NT)
+// through an unrolled feature loop so 4 x 4 independent loads are in flight (a one-row
+// fma chain waits out one memory latency per feature); the per-row arithmetic (feature
+// order, fmaf chain) is kernel_column's.
+__device__ void column_slice(const SvmProb& p, const float* __restrict__ X, int64_t d, int64_t src, float* xs,
+                             float* __restrict__ col, int64_t r0, int64_t r1) {
+  const bool lds = d <= kMaxLdsD;
+  const float* base = X + p.xoff;
+  if (lds) {
+    for (int64_t f = threadIdx.x; f < d; f += NT) xs[f] = base[f * p.nrows + src];
+    __syncthreads();
+  }
+  const int kernel = (int)p.kernel;
+  const int64_t nr = p.nrows;
+  for (int64_t rb = r0 + threadIdx.x; rb < r1; rb += 4 * NT) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int64_t rr[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) rr[k] = min(rb + k * NT, r1 - 1);   // clamped: the tail recomputes a valid row
+#pragma unroll 4
+    for (int64_t f = 0; f < d; ++f) {
+      const float a = lds ? xs[f] : base[f * nr + src];
+      const float* xf = base + f * nr;
+      if (kernel == KRBF) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float t = a - xf[rr[k]];
+          acc[k] = __builtin_fmaf(t, t, acc[k]);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] = __builtin_fmaf(a, xf[rr[k]], acc[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (rb + k * NT < r1) col[rb + k * NT] = kfun(kernel, p.gamma, p.coef0, (int)p.degree, acc[k]);
+  }
+  __syncthreads();
+}
+
+// LRU-style lookup of the column of `row` in this workgroup's replica of the cache map;
+// fills the slice on a miss.  Victim: the least recently used of 256 slots sampled by a
+// hash of the tick (all slots when S <= 256, i.e. exact LRU) -- O(1) per miss for any S
+// and the same choice in every replica.  Returns the slot's column base.
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+
+__device__ float* cache_column(const SvmProb& p, const float* X, int64_t d, float* kc, int32_t* slot_of,
+                               int32_t* row_of, uint32_t* stamp, uint32_t tick, int64_t row, const SplitCtx& sc,
+                               float* xs, int* s_slot, int* s_red) {
+  if (threadIdx.x == 0) *s_slot = slot_of[row];
+  __syncthreads();
+  int slot = *s_slot;
+  const bool hit = slot >= 0;
+  if (!hit) {
+    const uint32_t cand = sc.S <= NT ? (uint32_t)threadIdx.x : mix32(tick * 2654435761U + threadIdx.x) % (uint32_t)sc.S;
+    uint64_t best = cand < (uint32_t)sc.S ? (((uint64_t)stamp[cand] << 32) | cand) : ~0ull;
+    for (int m = 32; m >= 1; m >>= 1) {
+      const uint64_t o = __shfl_xor(best, m);
+      best = o < best ? o : best;
+    }
+    if ((threadIdx.x & 63) == 0) reinterpret_cast<uint64_t*>(s_red)[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t bb = reinterpret_cast<uint64_t*>(s_red)[0];
+      for (int q = 1; q < NT / 64; ++q) {
+        const uint64_t o = reinterpret_cast<uint64_t*>(s_red)[q];
+        bb = o < bb ? o : bb;
+      }
+      const int v = (int)(uint32_t)bb;
+      const int old = row_of[v];
+      if (old >= 0) slot_of[old] = -1;
+      slot_of[row] = v;
+      row_of[v] = (int32_t)row;
+      *s_slot = v;
+    }
+    __syncthreads();
+    slot = *s_slot;
+  }
+  if (threadIdx.x == 0) stamp[slot] = tick;
+  float* col = kc + p.coff + (int64_t)slot * p.nrows;
+  if (!hit) column_slice(p, X, d, row, xs, col, sc.r0, sc.r1);
+  __syncthreads();
+  return col;
+}
+
+__global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, int64_t d, const SvmProb* probs,
+                                                  int B, int S, const float* __restrict__ yv,
+                                                  const double* __restrict__ Cv, const float* __restrict__ qd,
+                                                  double* __restrict__ alpha, double* __restrict__ G,
+                                                  float* __restrict__ kc, int32_t* __restrict__ meta,
+                                                  uint64_t* __restrict__ recs, int64_t* __restrict__ out_state,
+                                                  int64_t chunk, int64_t* __restrict__ prof) {
+  // prof (optional, workgroup 0 only): wall-clock ticks per phase + cache misses
+  int64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tph = wall_clock64();
+  const bool do_prof = prof != nullptr && blockIdx.x == 0;
+#define SVM_PH(k) if (do_prof) { const uint64_t t_ = wall_clock64(); ph[k] += (int64_t)(t_ - tph); tph = t_; }
+  const int pid = blockIdx.x / B;
+  const SvmProb p = probs[pid];
+  if (p.status != 0) return;
+  __shared__ float xs[kMaxLdsD];
+  __shared__ Cand red[NT / 64];
+  __shared__ double redd[NT / 64];
+  __shared__ uint32_t pay[kMaxB * kRecW];
+  __shared__ int s_slot, s_abort;
+  __shared__ uint32_t vals[kRecW];
+  __shared__ int s_red[2 * (NT / 64)];
+  SplitCtx sc;
+  sc.B = B;
+  sc.w = blockIdx.x - pid * B;
+  sc.S = S;
+  const int64_t nr = p.nrows, L = p.L;
+  sc.r0 = nr * sc.w / B;
+  sc.r1 = nr * (sc.w + 1) / B;
+  const float* y = yv + p.voff;
+  const double* C = Cv + p.voff;
+  double* a = alpha + p.voff;
+  double* g = G + p.voff;
+  const float* QD = qd + p.roff;
+  uint64_t* rec = recs + (int64_t)pid * 2 * B * kRecW;
+  int32_t* my_meta = meta + p.moff + (int64_t)sc.w * (nr + 2 * S);
+  int32_t* slot_of = my_meta;                 // [nr]
+  int32_t* row_of = my_meta + nr;             // [S]
+  uint32_t* stamp = reinterpret_cast<uint32_t*>(my_meta + nr + S);   // [S]
+  if (threadIdx.x == 0) s_abort = 0;
+  __syncthreads();
+  auto rowof = [&](int64_t t) { return (p.svr && t >= nr) ? t - nr : t; };
+  const int nseg = p.svr ? 2 : 1;             // this slice's variables: [r0,r1) (+ nr for SVR)
+
+  int64_t it = p.iters;
+  int status = 0;
+  uint32_t seq = 0;
+  const int64_t stop_at = min(p.max_iter, it + chunk);
+  auto local_i = [&]() {
+    Cand ci{-kInf, -1};
+    for (int sgi = 0; sgi < nseg; ++sgi)
+      for (int64_t t = sc.r0 + sgi * nr + threadIdx.x; t < sc.r1 + sgi * nr; t += NT) {
+        const double yt = y[t];
+        const bool up = yt > 0 ? !is_upper(a[t], C[t]) : !is_lower(a[t]);
+        if (up) {
+          const double v = -yt * g[t];
+          if (better<true>(v, (int)t, ci.v, ci.idx)) { ci.v = v; ci.idx = (int)t; }
+        }
+      }
+    return ci;
+  };
+  Cand ci = local_i();
+  while (true) {
+    if (it >= stop_at) { status = it >= p.max_iter ? 2 : 0; break; }
+    // ---- exchange 1: i = argmax over I_up of -y G (with G_i, alpha_i) ----
+    const Cand bi_l = block_reduce<true>(ci, red);
+    if (threadIdx.x == 0) {
+      const int t = bi_l.idx;
+      vals[0] = lo32(bi_l.v); vals[1] = hi32(bi_l.v); vals[2] = (uint32_t)t;
+      const double gi = t >= 0 ? g[t] : 0.0, ai = t >= 0 ? a[t] : 0.0;
+      vals[3] = lo32(gi); vals[4] = hi32(gi); vals[5] = lo32(ai); vals[6] = hi32(ai);
+    }
+    __syncthreads();
+    SVM_PH(0)
+    if (!exchange(rec, sc, ++seq, vals, 7, pay, &s_abort)) { status = 3; break; }
+    SVM_PH(1)
+    double Gmax = -kInf, gi = 0.0, ai_old = 0.0;
+    int i = -1;
+    for (int q = 0; q < B; ++q) {
+      const uint32_t* r = pay + q * kRecW;
+      const int idx = (int)r[2];
+      const double v = mkd(r[0], r[1]);
+      if (better<true>(v, idx, Gmax, i)) { Gmax = v; i = idx; gi = mkd(r[3], r[4]); ai_old = mkd(r[5], r[6]); }
+    }
+    __syncthreads();
+    if (i < 0) { status = 1; break; }
+    const double yi = y[i];
+    const int64_t ri = rowof(i);
+    const uint32_t tick = (uint32_t)(2 * (it + 1));
+    if (do_prof && threadIdx.x == 0 && slot_of[ri] < 0) ph[7] += 1;
+    const float* Ki = cache_column(p, X, d, kc, slot_of, row_of, stamp, tick, ri, sc, xs, &s_slot, s_red);
+    SVM_PH(2)
+    // ---- local j candidates (second-order gain) + max over I_low of y G ----
+    // 4 variables per thread per step, every load issued before any use (latency-bound
+    // sweep); selection ties break by index, so the visiting order does not matter
+    Cand cj{kInf, -1};
+    double gmax2 = -kInf;
+    const double QDi = QD[ri];
+    for (int sgi = 0; sgi < nseg; ++sgi) {
+      const int64_t lo = sc.r0 + sgi * nr, hi = sc.r1 + sgi * nr;
+      for (int64_t tb = lo + threadIdx.x; tb < hi; tb += 4 * NT) {
+        double yk[4], ak[4], Ck[4], gk[4], kk[4], qk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t t = min(tb + k * NT, hi - 1);
+          const int64_t rt = rowof(t);
+          yk[k] = y[t]; ak[k] = a[t]; Ck[k] = C[t]; gk[k] = g[t]; kk[k] = (double)Ki[rt]; qk[k] = QD[rt];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t t = tb + k * NT;
+          if (t >= hi) break;
+          const double yt = yk[k];
+          if (yt > 0) {
+            if (!is_lower(ak[k])) {
+              const double gd = Gmax + gk[k];
+              gmax2 = fmax(gmax2, gk[k]);
+              if (gd > 0) {
+                double qc = QDi + qk[k] - 2.0 * yi * (yi * yt * kk[k]);
+                const double od = qc > 0 ? -(gd * gd) / qc : -(gd * gd) / kTau;
+                if (better<false>(od, (int)t, cj.v, cj.idx)) { cj.v = od; cj.idx = (int)t; }
+              }
+            }
+          } else {
+            if (!is_upper(ak[k], Ck[k])) {
+              const double gd = Gmax - gk[k];
+              gmax2 = fmax(gmax2, -gk[k]);
+              if (gd > 0) {
+                double qc = QDi + qk[k] + 2.0 * yi * (yi * yt * kk[k]);
+                const double od = qc > 0 ? -(gd * gd) / qc : -(gd * gd) / kTau;
+                if (better<false>(od, (int)t, cj.v, cj.idx)) { cj.v = od; cj.idx = (int)t; }
+              }
+            }
+          }
+        }
+      }
+    }
+    const Cand bj_l = block_reduce<false>(cj, red);
+    const double gm2_l = block_max(gmax2, redd);
+    if (threadIdx.x == 0) {
+      const int t = bj_l.idx;
+      vals[0] = lo32(bj_l.v); vals[1] = hi32(bj_l.v); vals[2] = (uint32_t)t;
+      const double gj = t >= 0 ? g[t] : 0.0, aj = t >= 0 ? a[t] : 0.0;
+      vals[3] = lo32(gj); vals[4] = hi32(gj); vals[5] = lo32(aj); vals[6] = hi32(aj);
+      vals[7] = lo32(gm2_l); vals[8] = hi32(gm2_l);
+    }
+    __syncthreads();
+    SVM_PH(3)
+    // ---- exchange 2 ----
+    if (!exchange(rec, sc, ++seq, vals, 9, pay, &s_abort)) { status = 3; break; }
+    SVM_PH(4)
+    double bjv = kInf, gj = 0.0, aj_old = 0.0, Gmax2 = -kInf;
+    int j = -1;
+    for (int q = 0; q < B; ++q) {
+      const uint32_t* r = pay + q * kRecW;
+      const int idx = (int)r[2];
+      const double v = mkd(r[0], r[1]);
+      if (better<false>(v, idx, bjv, j)) { bjv = v; j = idx; gj = mkd(r[3], r[4]); aj_old = mkd(r[5], r[6]); }
+      Gmax2 = fmax(Gmax2, mkd(r[7], r[8]));
+    }
+    __syncthreads();
+    if (Gmax + Gmax2 < p.eps || j < 0) { status = 1; break; }
+    const double yj = y[j];
+    const int64_t rj = rowof(j);
+    if (do_prof && threadIdx.x == 0 && slot_of[rj] < 0) ph[7] += 1;
+    const float* Kj = cache_column(p, X, d, kc, slot_of, row_of, stamp, tick + 1, rj, sc, xs, &s_slot, s_red);
+    SVM_PH(5)
+    // ---- two-variable update: every workgroup computes the same values ----
+    const double Ci = C[i], Cj = C[j];
+    const double Qij = yi * yj * (double)kernel_pair(p, X, d, ri, rj);
+    const double QDj = QD[rj];
+    double ai = ai_old, aj = aj_old;
+    if (yi != yj) {
+      double qc = QDi + QDj + 2.0 * Qij;
+      if (qc <= 0) qc = kTau;
+      const double delta = (-gi - gj) / qc;
+      const double diff = ai - aj;
+      ai += delta; aj += delta;
+      if (diff > 0) { if (aj < 0) { aj = 0; ai = diff; } }
+      else { if (ai < 0) { ai = 0; aj = -diff; } }
+      if (diff > Ci - Cj) { if (ai > Ci) { ai = Ci; aj = Ci - diff; } }
+      else { if (aj > Cj) { aj = Cj; ai = Cj + diff; } }
+    } else {
+      double qc = QDi + QDj - 2.0 * Qij;
+      if (qc <= 0) qc = kTau;
+      const double delta = (gi - gj) / qc;
+      const double sum = ai + aj;
+      ai -= delta; aj += delta;
+      if (sum > Ci) { if (ai > Ci) { ai = Ci; aj = sum - Ci; } }
+      else { if (aj < 0) { aj = 0; ai = sum; } }
+      if (sum > Cj) { if (aj > Cj) { aj = Cj; ai = sum - Cj; } }
+      else { if (ai < 0) { ai = 0; aj = sum; } }
+    }
+    const double dai = ai - ai_old, daj = aj - aj_old;
+    auto owns = [&](int t) { const int64_t r = rowof(t); return r >= sc.r0 && r < sc.r1; };
+    if (threadIdx.x == 0) {
+      if (owns(i)) a[i] = ai;
+      if (owns(j)) a[j] = aj;
+    }
+    __syncthreads();
+    // gradient update of this slice fused with its next i candidates (4 per thread per step)
+    ci = Cand{-kInf, -1};
+    for (int sgi = 0; sgi < nseg; ++sgi) {
+      const int64_t lo = sc.r0 + sgi * nr, hi = sc.r1 + sgi * nr;
+      for (int64_t tb = lo + threadIdx.x; tb < hi; tb += 4 * NT) {
+        double yk[4], ak[4], Ck[4], gk[4], kik[4], kjk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t t = min(tb + k * NT, hi - 1);
+          const int64_t rt = rowof(t);
+          yk[k] = y[t]; ak[k] = a[t]; Ck[k] = C[t]; gk[k] = g[t]; kik[k] = (double)Ki[rt]; kjk[k] = (double)Kj[rt];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t t = tb + k * NT;
+          if (t >= hi) break;
+          const double yt = yk[k];
+          const double gt = gk[k] + yt * (yi * kik[k] * dai + yj * kjk[k] * daj);
+          g[t] = gt;
+          const bool up = yt > 0 ? !is_upper(ak[k], Ck[k]) : !is_lower(ak[k]);
+          if (up) {
+            const double v = -yt * gt;
+            if (better<true>(v, (int)t, ci.v, ci.idx)) { ci.v = v; ci.idx = (int)t; }
+          }
+        }
+      }
+    }
+    ++it;
+    __syncthreads();
+    SVM_PH(6)
+  }
+#undef SVM_PH
+  if (do_prof && threadIdx.x == 0)
+    for (int k = 0; k < 8; ++k) prof[k] += ph[k];
+  if (threadIdx.x == 0 && sc.w == 0) {
+    out_state[2 * pid] = it;
+    out_state[2 * pid + 1] = status;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -279,6 +691,38 @@ int dml_svm_smo(const float* X, int64_t d, void* probs, int64_t nprob, const flo
   if (nprob <= 0) return 0;
   k_smo<<<(unsigned)nprob, NT, 0, st>>>(X, d, (SvmProb*)probs, y, C, qd, alpha, G, kbuf, chunk);
   return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// Split solver: probs (device, read-only) x B workgroups each; S cache slots per problem
+// (2 <= S <= 1024); kc: cache columns (coff per problem); meta: per-problem per-workgroup
+// maps (moff; slot_of = -1, row_of = -1, stamp = 0 initially); recs: nprob * 2 * B * 10
+// zeroed words; out_state: [nprob][2] (iterations, status) written by workgroup 0.
+int dml_svm_smo_split(const float* X, int64_t d, const void* probs, int64_t nprob, int32_t B, int32_t S,
+                      const float* y, const double* C, const float* qd, double* alpha, double* G, float* kc,
+                      int32_t* meta, uint64_t* recs, int64_t* out_state, int64_t chunk, int64_t* prof,
+                      hipStream_t st) {
+  if (nprob <= 0) return 0;
+  if (B < 1 || B > kMaxB || S < 2 || S > kMaxSlots) return 2;
+  if (B > 1) {   // every workgroup of the grid must be resident at once (record spins)
+    int per_cu = 0, dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 3;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_smo_split, NT, 0) != hipSuccess) return 3;
+    if ((int64_t)nprob * B > (int64_t)per_cu * prop.multiProcessorCount / 2) return 4;
+  }
+  k_smo_split<<<(unsigned)(nprob * B), NT, 0, st>>>(X, d, (const SvmProb*)probs, B, S, y, C, qd, alpha, G, kc, meta,
+                                                     recs, out_state, chunk, prof);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+int dml_svm_split_limits(int32_t* max_b, int32_t* max_slots) {
+  *max_b = kMaxB;
+  *max_slots = kMaxSlots;
+  int per_cu = 0, dev = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_smo_split, NT, 0) != hipSuccess) return -1;
+  return per_cu * prop.multiProcessorCount / 2;   // workgroups the host may launch at once
 }
 
 }  // extern "C"

@@ -20,6 +20,7 @@ struct SvmProb {
   int64_t xoff, roff, nrows, L, voff, koff, kernel, degree;
   double gamma, coef0, eps;
   int64_t max_iter, iters, status, svr;
+  int64_t coff, moff;   // GPU split solver only (svm.hip)
 };
 
 float kfun(int kernel, double gamma, double coef0, int degree, float acc) {

@@ -17,7 +17,9 @@ affect libsvm's speed and are accepted and ignored; ``probability=True`` does no
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
 import time
 from typing import Any, Dict, List, Tuple
 
@@ -40,8 +42,13 @@ _SVR_DEFAULTS = {"kernel": "rbf", "degree": 3, "gamma": "scale", "coef0": 0.0, "
 
 PROB_DTYPE = np.dtype([("xoff", "<i8"), ("roff", "<i8"), ("nrows", "<i8"), ("L", "<i8"), ("voff", "<i8"),
                        ("koff", "<i8"), ("kernel", "<i8"), ("degree", "<i8"), ("gamma", "<f8"), ("coef0", "<f8"),
-                       ("eps", "<f8"), ("max_iter", "<i8"), ("iters", "<i8"), ("status", "<i8"), ("svr", "<i8")])
+                       ("eps", "<f8"), ("max_iter", "<i8"), ("iters", "<i8"), ("status", "<i8"), ("svr", "<i8"),
+                       ("coff", "<i8"), ("moff", "<i8")])
 CHUNK_ITERS = 20000
+SPLIT_CHUNK_ITERS = 50000
+CACHE_FRACTION = 0.25        # of free HBM for the kernel-column caches (libsvm cache_size analogue) ...
+CACHE_MAX_GB = 24.0          # ... and at most this much (DML_SVM_CACHE_GB)
+MIN_ROWS_PER_WG = 1024       # split a problem over workgroups only down to this slice size
 
 
 class SVMFamily(Family):
@@ -150,7 +157,7 @@ class SVMFamily(Family):
                 qd = self._diag(norm2[key], rp["kernel"], gamma, rp["coef0"], rp["degree"])
                 mi = rp["max_iter"] if rp["max_iter"] > 0 else max(10_000_000, 100 * L)
                 probs.append((xoff[key], roff, nr, L, voff, koff, rp["kernel"], rp["degree"], gamma, rp["coef0"],
-                              rp["tol"], mi, 0, 0, int(svr)))
+                              rp["tol"], mi, 0, 0, int(svr), 0, 0))
                 prob_of.append((ti, pi, key))
                 ys.append(y_t.float()); Cs.append(C_t); Gs.append(G0); qds.append(qd.float())
                 voff += L; roff += nr; koff += 2 * nr
@@ -220,6 +227,8 @@ class SVMFamily(Family):
             lib = native.hip_lib()
             if lib.dml_svm_sizeof_prob() != PROB_DTYPE.itemsize:
                 raise RuntimeError("SvmProb layout mismatch")
+            if os.environ.get("DML_SVM_SPLIT", "1") != "0" and self._solve_split(data, lib, P, Xrs, y, C, qd, alpha, G):
+                return
             kbuf = torch.empty(max(1, kbuf_len), dtype=torch.float32, device=data.device)
             Pd = torch.from_numpy(P.view(np.uint8).copy()).to(data.device)
             while True:
@@ -231,12 +240,91 @@ class SVMFamily(Family):
                 P[:] = Pd.cpu().numpy().view(PROB_DTYPE)
                 if (P["status"] != 0).all():
                     break
+            self.last_solve_stats = {"solver": "one workgroup per problem", "problems": len(P),
+                                     "iterations_max": int(P["iters"].max())}
         else:
             lib = native.cpu_lib()
             if lib.dml_cpu_svm_sizeof_prob() != PROB_DTYPE.itemsize:
                 raise RuntimeError("SvmProb layout mismatch")
             lib.dml_cpu_svm_smo(native.ptr(Xrs), data.d, native.ptr(P), len(P), native.ptr(y), native.ptr(C),
                                 native.ptr(qd), native.ptr(alpha), native.ptr(G))
+
+    def _solve_split(self, data, lib, P, Xrs, y, C, qd, alpha, G) -> bool:
+        """B workgroups per problem + per-problem LRU kernel-column caches
+        (csrc/kernels/svm.hip ``k_smo_split``).  Every launch (a chunk of SMO iterations)
+        re-splits the still-running problems over the resident workgroups, so the last
+        hard problems (large C) end up with the most workgroups.  False: the split solver
+        cannot run here (the caller uses the one-workgroup kernel)."""
+        dev = data.device
+        nprob = len(P)
+        max_b, max_slots = ctypes.c_int32(0), ctypes.c_int32(0)
+        resident = int(lib.dml_svm_split_limits(ctypes.byref(max_b), ctypes.byref(max_slots)))
+        nr = P["nrows"].astype(np.int64)
+        if resident <= 0 or nprob == 0:
+            return False
+        MB = int(max_b.value)
+        free = torch.cuda.mem_get_info(dev)[0]
+        cache_bytes = min(CACHE_FRACTION * free, float(os.environ.get("DML_SVM_CACHE_GB", CACHE_MAX_GB)) * 1e9)
+        S = int(min(max_slots.value, int(nr.max()), cache_bytes // max(1, 4 * int(nr.sum()))))
+        if os.environ.get("DML_SVM_CACHE_SLOTS"):   # tests: force evictions
+            S = min(S, int(os.environ["DML_SVM_CACHE_SLOTS"]))
+        if S < 2:
+            return False
+        P["coff"] = np.concatenate([[0], np.cumsum(nr * S)[:-1]])
+        rep = nr + 2 * S                               # one workgroup's map: slot_of [nr], row_of [S], stamp [S]
+        P["moff"] = np.concatenate([[0], np.cumsum(MB * rep)[:-1]])
+        meta_np = np.full(int((MB * rep).sum()), -1, dtype=np.int32)
+        for p in range(nprob):   # stamps start at 0: unused slots are the first victims
+            for w in range(MB):
+                st = int(P["moff"][p]) + w * int(rep[p]) + int(nr[p]) + S
+                meta_np[st:st + S] = 0
+        meta = torch.from_numpy(meta_np).to(dev)
+        kc = torch.empty(int((nr * S).sum()), dtype=torch.float32, device=dev)
+        prof = torch.zeros(8, dtype=torch.int64, device=dev) if os.environ.get("DML_SVM_PROFILE") else None
+        launches, B_prev, B_hist = 0, 0, []
+        while True:
+            run = np.nonzero(P["status"] == 0)[0]
+            if run.size == 0:
+                break
+            B = int(min(MB, max(1, resident // run.size), max(1, int(nr[run].max()) // MIN_ROWS_PER_WG)))
+            if run.size * B > resident:
+                B = 1   # no cross-workgroup waits at B = 1: any grid size is safe
+            if launches and B != B_prev:
+                # every replica of a problem's cache map is identical and every cached column
+                # is complete (the old slices covered all rows): copy replica 0 to the new ones
+                for p in run:
+                    o, r_ = int(P["moff"][p]), int(rep[p])
+                    view = meta[o:o + MB * r_].view(MB, r_)
+                    view[1:B] = view[0]
+            Pr = np.ascontiguousarray(P[run])
+            Pd = torch.from_numpy(Pr.view(np.uint8).copy()).to(dev)
+            recs = torch.zeros(run.size * 2 * B * 10, dtype=torch.int64, device=dev)
+            out_state = torch.zeros(2 * run.size, dtype=torch.int64, device=dev)
+            rc = lib.dml_svm_smo_split(native.ptr(Xrs), data.d, native.ptr(Pd), run.size, B, S, native.ptr(y),
+                                       native.ptr(C), native.ptr(qd), native.ptr(alpha), native.ptr(G), native.ptr(kc),
+                                       native.ptr(meta), native.ptr(recs), native.ptr(out_state), SPLIT_CHUNK_ITERS,
+                                       native.ptr(prof), native.stream_handle(dev))
+            if rc == 4 and launches == 0:
+                return False
+            if rc:
+                raise RuntimeError(f"dml_svm_smo_split failed ({rc})")
+            launches += 1
+            B_prev = B
+            B_hist.append(B)
+            st = out_state.view(run.size, 2).cpu().numpy()
+            P["iters"][run] = st[:, 0]
+            P["status"][run] = st[:, 1]
+            if (P["status"] == 3).any():
+                raise RuntimeError("SMO workgroups of a problem lost contact (not co-resident?)")
+        self.last_solve_stats = {"solver": "split", "problems": nprob, "workgroups_per_problem": max(B_hist),
+                                 "workgroups_per_launch": B_hist, "cache_slots": S, "launches": launches,
+                                 "iterations_max": int(P["iters"].max()), "iterations_sum": int(P["iters"].sum())}
+        if prof is not None:   # first running problem, workgroup 0: 100 MHz ticks -> microseconds per phase
+            pr = prof.cpu().numpy()
+            names = ("i_reduce", "xchg_i", "col_i", "j_sweep", "xchg_j", "col_j_update", "g_sweep")
+            self.last_solve_stats["phase_us"] = {k: round(float(pr[q]) / 100.0, 1) for q, k in enumerate(names)}
+            self.last_solve_stats["cache_misses"] = int(pr[7])
+        return True
 
     @staticmethod
     def _gamma(data, t: FitTask, gamma, cache: Dict[int, float]) -> float:

@@ -185,6 +185,9 @@ def _register_optional(lib) -> None:
         "dml_svm_sizeof_prob": (c_i32, []),
         "dml_forest_refine": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
                                       c_vp]),
+        "dml_svm_smo_split": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                      c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+        "dml_svm_split_limits": (c_i32, [c_vp, c_vp]),
         "dml_svm_smo": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
         "dml_lr_mfma_tile": (c_i32, []),
         "dml_lr_mfma_fwd": (c_i32, [ctypes.POINTER(LrFwdArgs), c_vp]),

@@ -218,6 +218,34 @@ def test_svm_gpu_matches_cpu_solver(model, clf):
     np.testing.assert_allclose(out["cuda:0"], out["cpu"], atol=2e-3)
 
 
+@pytest.mark.parametrize("model,slots", [("SVC", 4), ("SVC", 1024), ("SVR", 8)])
+def test_svm_split_solver_equals_single_workgroup_solver(model, slots, monkeypatch):
+    """Several workgroups per problem exchanging atomic records + the LRU column cache
+    (evicting at 4 / 8 slots) take exactly the single-workgroup solver's SMO steps."""
+    from cs230_distributed_machine_learning_amd.models.base import family_of
+
+    rng = np.random.RandomState(7)
+    n = 7000
+    X = rng.randn(n, 9).astype(np.float32)
+    clf = model == "SVC"
+    y = (X[:, 0] + 0.4 * X[:, 1] ** 2 + 0.5 * rng.randn(n) > 0.3).astype(int) if clf else \
+        (np.sin(X[:, 0]) + 0.2 * rng.randn(n)).astype(np.float32)
+    grid = list(ParameterGrid({"C": [0.5, 5.0], "gamma": ["scale"]}))
+    out, stats = {}, {}
+    fam = family_of(model)
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DML_SVM_SPLIT", mode)
+        monkeypatch.setenv("DML_SVM_CACHE_SLOTS", str(slots))
+        dd = DeviceData(X, y, clf, "cuda:0")
+        res = run_candidates(dd, JobSpec(model, grid, cv=3, holdout=False), range(len(grid)))
+        assert all(r.ok for r in res), [r.error for r in res]
+        out[mode] = [r.result["cv_scores"] for r in res]
+        stats[mode] = dict(fam.last_solve_stats)
+    assert stats["1"]["solver"] == "split" and stats["1"]["workgroups_per_problem"] > 1, stats
+    assert stats["1"]["iterations_max"] == stats["0"]["iterations_max"], stats
+    assert out["1"] == out["0"]
+
+
 def test_slice_metrics_report_gpu_fields():
     """J3 records of a device slice carry the GPU index, the slice's HBM working set and
     its fits/s (SURVEY §5.1/§5.5 observability fields)."""
