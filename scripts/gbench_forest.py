@@ -1,4 +1,4 @@
-import numpy as np, torch, time, sys
+import numpy as np, torch, time, sys, os
 sys.path.insert(0, '/root/repo')
 from cs230_distributed_machine_learning_amd.ops import binning, forest_ops
 from cs230_distributed_machine_learning_amd.utils import native
@@ -19,7 +19,8 @@ for f in range(nfits):
         s['max_features']=int(np.sqrt(d)); s['bootstrap']=1; s['criterion']=0; s['pois_cdf']=native.poisson_cdf_table(1.0)
 for rep in range(2):
     torch.cuda.synchronize(); t0=time.time()
-    fb = forest_ops.build_gpu(Xb, y, None, roles, specs, 2, False)
+    XbT = None if os.environ.get('DML_NO_XBT') else Xb[:, :d].t().contiguous()   # the family path's feature-major copy
+    fb = forest_ops.build_gpu(Xb, y, None, roles, specs, 2, False, XbT=XbT)
     torch.cuda.synchronize(); t1=time.time()
     print('build', t1-t0, fb.stats, 'per-tree ms', (t1-t0)/len(specs)*1e3)
 rows=[]; roff=[0]
