@@ -365,7 +365,8 @@ def run_e2e(args) -> int:
 
     def drive(ctl):
         sid = ctl.create_session()[1]["session_id"]
-        spec = f"classification?n={args.rows}&d={args.features}&informative=10&noise=1.0&seed={args.seed}"
+        # the bench's own generator (data/synthetic.py), so the e2e job fits the same table
+        spec = f"classification?n={args.rows}&d={args.features}&informative=10&noise=1.0&seed={args.seed}&gen=blocks"
         t0 = time.perf_counter()
         st, msg = ctl.download_data(sid, {"dataset_url": spec, "dataset_name": "synth", "dataset_type": "synthetic"})
         assert st == 200, msg
@@ -397,6 +398,13 @@ def run_e2e(args) -> int:
 
         last_slice_end = max(_ts(m["finished_at"]) for m in metrics if m.get("finished_at"))
         out["tail_s"] = t_end - last_slice_end   # refit of the best candidate + model store + publish
+        # slice-level accounting: device time inside slices vs the job's wall time
+        sl = {}
+        for m in metrics:
+            key = (m.get("worker_id"), m.get("started_at"))
+            sl[key] = (m.get("slice_wall_seconds") or 0.0, m.get("slice_fits") or 0)
+        out["slice_wall_sum_s"] = sum(w for w, _ in sl.values())
+        out["fits_per_slice_mean"] = sum(f for _, f in sl.values()) / max(1, len(sl))
         out.update(status=status, wall=wall, t_reg=t_reg, t_load=t_load, workers=sorted({m["worker_id"] for m in metrics}),
                    last=last_slice_end, slices=len({(m.get("worker_id"), m.get("started_at")) for m in metrics}))
 
@@ -454,7 +462,12 @@ def run_e2e(args) -> int:
         "best_mean_cv": round(status["best_result"]["mean_cv_score"], 4),
         "best_model_stored": bool(status["best_result"].get("model_path")),
         "refit_and_publish_s": round(out["tail_s"], 2),
+        "slices": out["slices"], "fits_per_slice_mean": round(out["fits_per_slice_mean"], 1),
+        "slice_wall_sum_s": round(out["slice_wall_sum_s"], 2),
     }
+    from cs230_distributed_machine_learning_amd.utils import trace
+
+    print("phases:", json.dumps(trace.summary()), file=sys.stderr, flush=True)
     print(json.dumps(line), flush=True)
     if args.json_out:
         with open(args.json_out, "w") as f:

@@ -225,14 +225,27 @@ def load_table(path: str, name: str, feature_columns=None, target_column=None) -
 
 
 def synthetic_table(spec: str, seed_default: int = 0):
-    """``classification?n=..&d=..&classes=..&informative=..&seed=..`` or ``regression?...``."""
+    """``classification?n=..&d=..&classes=..&informative=..&seed=..`` or ``regression?...``;
+    ``&gen=blocks`` uses the block generator of data/synthetic.py (n a multiple of 15625)."""
     kind, _, q = spec.partition("?")
     args = {k: v[0] for k, v in parse_qs(q).items()}
     n = int(args.get("n", 1000))
     d = int(args.get("d", 20))
     seed = int(args.get("seed", seed_default))
-    X, y = synthetic_arrays(kind, n, d, int(args.get("classes", 2)), int(args.get("informative", min(d, 10))), seed,
-                            float(args.get("noise", 0.5)))
+    if args.get("gen") == "blocks":
+        # the block generator of data/synthetic.py (what bench.py makes on the device):
+        # same weights and noise model, so bench --e2e fits the bench's table shape AND
+        # difficulty (tree sizes follow the label noise)
+        from . import synthetic as _syn
+
+        reg = not kind.startswith("class")
+        Xt, yt = _syn.make_table(n, d, informative=int(args.get("informative", min(d, 10))),
+                                 n_classes=int(args.get("classes", 2)), noise=float(args.get("noise", 1.0)), seed=seed,
+                                 device="cpu", regression=reg)
+        X, y = Xt.numpy(), (yt.numpy() if reg else yt.numpy().astype(np.int64))
+    else:
+        X, y = synthetic_arrays(kind, n, d, int(args.get("classes", 2)), int(args.get("informative", min(d, 10))),
+                                seed, float(args.get("noise", 0.5)))
     cols = [f"x{i}" for i in range(d)] + ["target"]
     return X, y, cols
 

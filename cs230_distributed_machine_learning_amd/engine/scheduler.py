@@ -65,7 +65,8 @@ class Scheduler:
         self._next_id = 1
         self.dead_after_s = dead_after_s
         self.algo_weight = {k.lower(): float(v) for k, v in (algo_weight or {}).items()}
-        self.calib: Dict[str, float] = {}     # seconds per cost unit, per algorithm (EMA)
+        self.calib: Dict[str, float] = {}     # seconds per cost unit, per algorithm
+        self._calib_sums: Dict[str, Tuple[float, float]] = {}   # decayed (seconds, cost) sums
         self.ema = ema
         self.assigned: Dict[str, Tuple[str, Unit, float]] = {}   # unit_id -> (worker, unit, reserved seconds)
         self.held: List[Unit] = []
@@ -124,14 +125,21 @@ class Scheduler:
         return cost_units * self.calib.get(a, 1.0) * self.algo_weight.get(a, 1.0)
 
     def observe(self, worker_id: str, unit: Unit, seconds: float) -> None:
-        """Feedback: calibrate seconds/cost for the algorithm and the worker speed (EMA)."""
+        """Feedback: calibrate seconds/cost for the algorithm and the worker speed.
+
+        The calibration is a decayed ratio estimator, sum(seconds) / sum(cost units) over
+        recent slices, not an average of per-slice ratios: a slice's weight is its cost, so
+        a tiny warm-up job whose wall time is all fixed overhead (a per-slice ratio 100x
+        the real one) cannot mis-price the next search, and one real slice corrects it."""
         with self._lock:
             a = unit.algo.lower()
             if unit.cost > 0 and seconds > 0:
                 w = self.workers.get(str(worker_id))
-                speed = w.speed_factor if w else 1.0
-                obs = seconds * speed / unit.cost
-                self.calib[a] = obs if a not in self.calib else (1 - self.ema) * self.calib[a] + self.ema * obs
+                ss, sc = self._calib_sums.get(a, (0.0, 0.0))
+                ss = (1 - self.ema) * ss + seconds
+                sc = (1 - self.ema) * sc + unit.cost
+                self._calib_sums[a] = (ss, sc)
+                self.calib[a] = ss / sc
                 if w is not None:
                     pred = self.estimate(unit.algo, unit.cost)
                     ratio = pred / seconds if seconds > 0 else 1.0

@@ -538,6 +538,22 @@ def plan_slices(ctl: Controller, plan: Dict[str, Any], todo: List[int], n_train:
     return [slices[k] for k in sorted(slices)]
 
 
+def should_recut(ctl: Controller, plan: Dict[str, Any], queued: List[List[int]], costs: List[float]) -> bool:
+    """True when the queued slices, priced with the CURRENT calibration, are far from
+    ``chunk_target_s``: the median is under half the target, or over twice it while some
+    slice still holds several candidates.  A job is cut with the prior seconds-per-cost
+    and the first slices (cold caches, lazy device copies) can mis-calibrate it; slices of
+    one candidate leave most of the GPU idle at the top tree levels."""
+    if len(queued) < 2:
+        return False
+    T = ctl.config.chunk_target_s
+    if T <= 0:
+        return False
+    est = sorted(ctl.scheduler.estimate(plan["model_type"], sum(costs[c] for c in sl)) for sl in queued)
+    med = est[len(est) // 2]
+    return med < 0.5 * T or (med > 2.0 * T and any(len(sl) > 1 for sl in queued))
+
+
 def publish_results(ctl: Controller, job: Job, results, metrics) -> None:
     for r in results:
         st = job.subtasks[r.candidate]
@@ -597,6 +613,7 @@ class _JobRun:
         self.slices = list(slices)
         self.si = 0
         self.rechunked = False
+        self.recuts = 0
         self.results: List[Any] = []
 
 
@@ -698,11 +715,12 @@ class LocalRunner(Runner):
         ctl.scheduler.observe(self.worker_id, unit, wall)
         jr.results.extend(results)
         jr.si += 1
-        if not jr.rechunked and jr.si < len(jr.slices):
-            # the job was cut with the device's prior seconds-per-cost; the first slice
+        if jr.si < len(jr.slices) and (not jr.rechunked or should_recut(ctl, plan, jr.slices[jr.si:], jr.costs)):
+            # the job was cut with the device's prior seconds-per-cost; the slices so far
             # calibrated it: re-cut the rest so slices are ~chunk_target_s of real work (a
             # GPU batch of one candidate leaves most of the chip idle at the top levels)
             jr.rechunked = True
+            jr.recuts += 1
             rest = [i for sl in jr.slices[jr.si:] for i in sl]
             jr.slices = jr.slices[:jr.si] + plan_slices(ctl, plan, rest, int(dd.n * 0.8), dd.d, dd.n_classes)
         if jr.si < len(jr.slices):

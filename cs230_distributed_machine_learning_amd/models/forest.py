@@ -177,24 +177,36 @@ class ForestFamily(Family):
             per_tree = min(per_tree, 2.0 ** (rp["max_depth"] + 1) - 1)
         return T * active, T * per_tree + T
 
+    def _need(self, data, rows: float, T: int, pool: float) -> int:
+        """Real device bytes of a batch: the builder's workspace layout + the node pool."""
+        VC = data.n_classes if data.classification else 3
+        return (forest_ops.workspace_bytes(int(rows), int(T), data.d, data.n_classes, not data.classification,
+                                           self.tiers) + forest_ops.pool_bytes(int(pool) + 16, VC))
+
     def presize(self, data, rps: List[Dict[str, Any]], cands_per_batch: int, n_splits: int) -> None:
-        """Grow the device arena at job setup to the largest batch this job can form
-        (its ``cands_per_batch`` largest candidates x ``n_splits`` splits), so no batch
-        of the job regrows it mid-run.  ``rps``: resolved parameters per candidate."""
+        """Grow the device arena at job setup to the largest batch this job can form, so no
+        batch regrows it mid-run (a regrowth frees and maps 100+ GB: 2.6-4.5 s each,
+        measured).  The largest batch is the budget-bounded greedy batch of the job's most
+        expensive fits -- exactly how ``run`` forms batches -- whatever the slicing, since
+        the runner re-cuts slices as it calibrates.  ``rps``: resolved parameters per
+        candidate; ``cands_per_batch`` is accepted for the runner's API (not a bound)."""
         if not data.is_gpu or not rps:
             return
-        foot = sorted((self.footprint(data, rp) + (rp["n_estimators"],) for rp in rps), reverse=True)
-        top = foot[:max(1, cands_per_batch)]
-        rows = int(n_splits * sum(f[0] for f in top))
-        pool = int(n_splits * sum(f[1] for f in top)) + 16
-        T = int(n_splits * sum(f[2] for f in top))
         budget = self._budget(data)
-        ws = forest_ops.workspace_bytes(rows, T, data.d, data.n_classes, not data.classification, self.tiers)
+        fits = []
+        for rp in rps:
+            rows, pool = self.footprint(data, rp)
+            fits.extend([(rows, rp["n_estimators"], pool)] * max(1, n_splits))
+        fits.sort(reverse=True)
+        rows = pool = 0.0
+        T = 0
+        for fr, ft, fp in fits:
+            if T and self._need(data, rows + fr, T + ft, pool + fp) > budget:
+                break
+            rows, T, pool = rows + fr, T + ft, pool + fp
+        ws = forest_ops.workspace_bytes(int(rows), T, data.d, data.n_classes, not data.classification, self.tiers)
         VC = data.n_classes if data.classification else 3
-        pb = forest_ops.pool_bytes(pool, VC)
-        if ws + pb > budget:            # such a batch would be split anyway: reserve the budget's share
-            scale = budget / float(ws + pb)
-            ws, pb = int(ws * scale), int(pb * scale)
+        pb = forest_ops.pool_bytes(int(pool) + 16, VC)
         forest_ops.ARENA.reserve(data.device, "ws", ws)
         forest_ops.ARENA.reserve(data.device, "pool", pb)
 
@@ -221,10 +233,22 @@ class ForestFamily(Family):
         Xb = data.binned()
         budget = self._budget(data)
         outs: Dict[int, FitOutput] = {}
-        # batches of whole fits under the memory budget
+        # batches of whole fits under the memory budget (on the device: the builder's real
+        # workspace + node-pool bytes, the same rule ``presize`` sizes the arena with)
         batches: List[List[FitTask]] = []
         cur, cur_bytes = [], 0.0
+        rows = pool = 0.0
+        T = 0
         for t in tasks:
+            if data.is_gpu:
+                fr, fp = self.footprint(data, t.params)
+                ft = t.params["n_estimators"]
+                if cur and self._need(data, rows + fr, T + ft, pool + fp) > budget:
+                    batches.append(cur)
+                    cur, rows, T, pool = [], 0.0, 0, 0.0
+                cur.append(t)
+                rows, T, pool = rows + fr, T + ft, pool + fp
+                continue
             b = self._tree_bytes(data, t.params) * t.params["n_estimators"]
             if cur and cur_bytes + b > budget:
                 batches.append(cur)

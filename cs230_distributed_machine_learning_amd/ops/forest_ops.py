@@ -12,11 +12,13 @@ same ``TREESPEC_DTYPE`` records and produce the same pool layout:
 from __future__ import annotations
 
 import ctypes
+import os
+import sys
 import math
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Dict, Optional
+from typing import Dict, List, Optional
 
 import numpy as np
 import torch
@@ -110,15 +112,20 @@ class _Arena:
     def __init__(self):
         self.bufs: Dict[tuple, torch.Tensor] = {}
         self.busy: set = set()
+        self.grows: List[tuple] = []   # (slot, old bytes, new bytes, seconds) of every mid-run regrowth
         self.lock = threading.Lock()
 
     def take(self, dev: torch.device, slot: str, nbytes: int) -> Optional[torch.Tensor]:
         key = (dev.index if dev.index is not None else torch.cuda.current_device(), slot)
         with self.lock:
             if key in self.busy:
+                if os.environ.get("DML_ARENA_LOG"):
+                    print(f"[arena] {slot} busy: fresh allocation of {nbytes / 1e9:.2f} GB", file=sys.stderr, flush=True)
                 return None              # another build on this device holds it: allocate fresh
             buf = self.bufs.get(key)
             if buf is None or buf.numel() < nbytes:
+                t_grow = time.perf_counter()
+                old = 0 if buf is None else int(buf.numel())
                 self.bufs.pop(key, None)
                 del buf
                 # grow with 50% headroom (batch sizes vary; every regrowth is a slow
@@ -129,6 +136,10 @@ class _Arena:
                 target = max(int(nbytes), min(int(nbytes * 3 // 2), int(0.7 * spare)))
                 buf = torch.empty(target, dtype=torch.uint8, device=dev)
                 self.bufs[key] = buf
+                self.grows.append((slot, old, target, time.perf_counter() - t_grow))
+                if os.environ.get("DML_ARENA_LOG"):
+                    print(f"[arena] grow {slot}: {old / 1e9:.2f} -> {target / 1e9:.2f} GB (need {nbytes / 1e9:.2f}) "
+                          f"{self.grows[-1][3]:.3f}s", file=sys.stderr, flush=True)
             self.busy.add(key)
             return buf
 

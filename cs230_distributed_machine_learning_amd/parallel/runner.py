@@ -55,7 +55,8 @@ import torch
 from ..engine import faults
 from ..engine.jobs import Job, json_safe
 from ..engine.service import (Controller, Runner, attach_model, candidate_costs, job_plan, job_seed, pick_refit,
-                              plan_slices, presize_for_job, publish_results, refit_model, run_slice)
+                              plan_slices, presize_for_job, publish_results, refit_model, run_slice,
+                              should_recut)
 from ..models.base import family_of, is_classifier
 from ..utils.log import get_logger
 from . import data as pdata
@@ -738,7 +739,8 @@ class DistributedRunner(Runner):
                                        Unit(unit_id=f"{js.job.job_id}:{i}", cost=cost, algo=js.job.model_type), wall)
         except Exception:
             pass
-        if not js.rechunked and "error" not in out:
+        if "error" not in out and (not js.rechunked or should_recut(
+                self.ctl, js.plan, [js.slices[q] for q in js.queue], js.cand_costs)):
             self._rechunk(js)
         if i in js.done:   # a re-queued slice finished twice: count it once
             return
@@ -751,9 +753,11 @@ class DistributedRunner(Runner):
         self._complete(js)
 
     def _rechunk(self, js: _JobState) -> None:
-        """The job was cut with the prior seconds-per-cost; its first slice calibrated the
+        """The job was cut with the prior seconds-per-cost; its first slices calibrated the
         cost model: re-cut the still-queued candidates into ~chunk_target_s slices (a
-        one-candidate GPU batch leaves most of the chip idle at the top levels)."""
+        one-candidate GPU batch leaves most of the chip idle at the top levels).  Runs
+        after the first slice and again whenever the queue, priced with the current
+        calibration, drifts far from the target (``should_recut``)."""
         js.rechunked = True
         queued = list(js.queue)
         if len(queued) < 2:
