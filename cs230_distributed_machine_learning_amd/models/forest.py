@@ -185,11 +185,11 @@ class ForestFamily(Family):
 
     def presize(self, data, rps: List[Dict[str, Any]], cands_per_batch: int, n_splits: int) -> None:
         """Grow the device arena at job setup to the largest batch this job can form, so no
-        batch regrows it mid-run (a regrowth frees and maps 100+ GB: 2.6-4.5 s each,
-        measured).  The largest batch is the budget-bounded greedy batch of the job's most
-        expensive fits -- exactly how ``run`` forms batches -- whatever the slicing, since
-        the runner re-cuts slices as it calibrates.  ``rps``: resolved parameters per
-        candidate; ``cands_per_batch`` is accepted for the runner's API (not a bound)."""
+        batch regrows it mid-run (a regrowth frees and maps 100+ GB: 2.6-4.7 s each,
+        measured).  Workspace and node pool share one slot (ops/forest_ops.py), and every
+        batch is formed under the same budget by ``_need``, so one slot of
+        min(budget, the job's largest greedy batch) fits all of them.  ``rps``: resolved
+        parameters per candidate; ``cands_per_batch`` is accepted for the runner's API."""
         if not data.is_gpu or not rps:
             return
         budget = self._budget(data)
@@ -200,15 +200,19 @@ class ForestFamily(Family):
         fits.sort(reverse=True)
         rows = pool = 0.0
         T = 0
+        need = 0
         for fr, ft, fp in fits:
-            if T and self._need(data, rows + fr, T + ft, pool + fp) > budget:
+            nxt = self._need(data, rows + fr, T + ft, pool + fp)
+            if T and nxt > budget:
                 break
-            rows, T, pool = rows + fr, T + ft, pool + fp
-        ws = forest_ops.workspace_bytes(int(rows), T, data.d, data.n_classes, not data.classification, self.tiers)
-        VC = data.n_classes if data.classification else 3
-        pb = forest_ops.pool_bytes(int(pool) + 16, VC)
-        forest_ops.ARENA.reserve(data.device, "ws", ws)
-        forest_ops.ARENA.reserve(data.device, "pool", pb)
+            rows, T, pool, need = rows + fr, T + ft, pool + fp, nxt
+        need = int(min(budget, need * 1.02) + (1 << 20))    # alignment slack of the carve
+        if os.environ.get("DML_ARENA_LOG"):
+            import sys
+
+            print(f"[arena] presize: budget {budget / 1e9:.1f} GB, {len(fits)} fits, batch rows {rows:.3g} T {T} -> "
+                  f"slot {need / 1e9:.1f} GB", file=sys.stderr, flush=True)
+        forest_ops.ARENA.reserve(data.device, "forest", need)
 
     def _budget(self, data) -> float:
         if self.hbm_budget_bytes:
@@ -257,6 +261,11 @@ class ForestFamily(Family):
             cur_bytes += b
         if cur:
             batches.append(cur)
+        if os.environ.get("DML_ARENA_LOG") and data.is_gpu:
+            import sys
+
+            print(f"[arena] run: budget {budget / 1e9:.1f} GB, {len(tasks)} fits -> {len(batches)} batches "
+                  f"{[len(b) for b in batches]}", file=sys.stderr, flush=True)
         for batch in batches:
             with trace.range("forest_batch"):
                 out_b = self._run_batch(data, Xb, batch, is_reg, keep_models)

@@ -105,9 +105,10 @@ class _Arena:
     allocator and fall through to hipMalloc / release-and-retry, which measured ~1.1 s
     per batch (a third of the bench step).  The arena keeps one buffer per slot and
     device, grown with 50% headroom (capped by free HBM) when a batch needs more, and hands out views.
-    Slot ``"ws"`` lives for one build; slot ``"pool"`` backs the returned node arrays
-    and is only used when the caller finishes with the ForestBuild before the next
-    build (the forest family; boosting keeps its trees and allocates its own)."""
+    Slot ``"forest"`` holds a build's workspace AND node pool and stays taken until the
+    caller's ``release_pool`` (the forest family, which is done with a batch's trees
+    before the next build; ``ForestFamily.presize`` sizes it once per job).  Slot
+    ``"ws"`` is a workspace-only slot for builds whose trees outlive the call (boosting)."""
 
     def __init__(self):
         self.bufs: Dict[tuple, torch.Tensor] = {}
@@ -266,30 +267,40 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     tree_W = torch.empty(T, dtype=torch.float64, device=dev)
     a.tree_W = native.ptr(tree_W)
     ws_bytes = lib.dml_forest_workspace_bytes(ctypes.byref(a))
-    with trace.range("forest_alloc"):
-        ws_buf = ARENA.take(dev, "ws", ws_bytes)
-        workspace = ws_buf[:ws_bytes] if ws_buf is not None else torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-    a.workspace, a.workspace_bytes = native.ptr(workspace), ws_bytes
+    ws_span = (ws_bytes + 255) // 256 * 256
+    # reuse_pool (the forest family): workspace and node pool share ONE arena slot,
+    # "forest", held until release_pool -- any batch under the family's HBM budget fits
+    # the presized slot whatever its split between rows (workspace) and nodes (pool).
+    # Otherwise (boosting keeps its trees): arena workspace + freshly allocated pool.
+    slot = None
+    ws_buf = None
+    if not reuse_pool:
+        with trace.range("forest_alloc"):
+            ws_buf = ARENA.take(dev, "ws", ws_bytes)
+            workspace = ws_buf[:ws_bytes] if ws_buf is not None else torch.empty(ws_bytes, dtype=torch.uint8,
+                                                                                  device=dev)
     retries = 0
-    pool_held = False
     try:
         for _attempt in range(4):
             with trace.range("forest_alloc"):
                 vals_off = (pool_cap * 8 + 255) // 256 * 256
                 pbytes = pool_bytes(pool_cap, VC)
-                pbuf = None
                 if reuse_pool:
-                    if pool_held:                      # a pool retry may need a bigger slot
-                        ARENA.give(dev, "pool")
-                        pool_held = False
-                    pbuf = ARENA.take(dev, "pool", pbytes)
-                    pool_held = pbuf is not None
-                if pbuf is not None:
-                    nodes = _carve(pbuf, 0, (pool_cap, 2), torch.int32)
-                    vals = _carve(pbuf, vals_off, (pool_cap, VC), torch.float64)
+                    if slot is not None:               # a pool retry needs a bigger slot
+                        ARENA.give(dev, slot)
+                        slot = None
+                    buf = ARENA.take(dev, "forest", ws_span + pbytes)
+                    if buf is not None:
+                        slot = "forest"
+                    else:
+                        buf = torch.empty(ws_span + pbytes, dtype=torch.uint8, device=dev)
+                    workspace = buf[:ws_bytes]
+                    nodes = _carve(buf, ws_span, (pool_cap, 2), torch.int32)
+                    vals = _carve(buf, ws_span + vals_off, (pool_cap, VC), torch.float64)
                 else:
                     nodes = torch.empty((pool_cap, 2), dtype=torch.int32, device=dev)
                     vals = torch.empty((pool_cap, VC), dtype=torch.float64, device=dev)
+            a.workspace, a.workspace_bytes = native.ptr(workspace), ws_bytes
             a.nodes, a.node_val, a.pool_cap = native.ptr(nodes), native.ptr(vals), pool_cap
             a.status_out = 0
             with trace.range("forest_build"):   # host-side launch sequence of every tier
@@ -306,8 +317,8 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
         else:
             raise RuntimeError("forest node pool overflow")
     except BaseException:
-        if pool_held:
-            ARENA.give(dev, "pool")
+        if slot is not None:
+            ARENA.give(dev, slot)
         raise
     finally:
         # stream order keeps the next build's kernels behind this build's on the same stream
@@ -319,8 +330,9 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
              "rows_total": int(a.rows_total), "build_s": time.perf_counter() - t0, "pool_retries": retries,
              "tier_nodes": [int(a.tier0_nodes), int(a.tier1_nodes), int(a.tier2_nodes), int(a.tier3_nodes)]}
     fb = ForestBuild(nodes[:P], vals[:P], T, VC, is_reg, n_classes, stats)
-    if pool_held:
+    if slot is not None:
         fb.arena_dev = dev   # release_pool(fb) hands the arena slot back
+        fb.arena_slot = slot
     return fb
 
 
@@ -330,7 +342,7 @@ def release_pool(fb: ForestBuild) -> None:
     if dev is not None:
         fb.nodes = fb.vals = None
         fb.arena_dev = None
-        ARENA.give(dev, "pool")
+        ARENA.give(dev, getattr(fb, "arena_slot", "forest"))
 
 
 def build_cpu(Xb: np.ndarray, ycls: Optional[np.ndarray], yreg: Optional[np.ndarray], roles: np.ndarray,
