@@ -295,7 +295,18 @@ class Controller:
         return 200, self.scheduler.queues()
 
     def subscribe(self, body: Dict[str, Any]) -> Resp:
+        """Reference scheduler.py:105-117.  Under the cluster runner the answer tells the
+        new worker where to join: it connects to the rendezvous store with
+        ``serve --join HOST:PORT`` (``parallel/runner.py`` ``join_cluster``), gets a worker
+        id from the dispatcher and starts receiving slices; the store, not this REST
+        call, is its work channel.  Without a cluster runner the worker is bookkeeping
+        only (single-process service)."""
         body = body or {}
+        join = self.runner.join_info()
+        if join is not None:
+            return 200, {"status": "join", "join": join,
+                         "command": f"python -m cs230_distributed_machine_learning_amd.serve --join "
+                                    f"{join['host']}:{join['port']} --device {body.get('device', 'cuda:0')}"}
         wid = self.scheduler.register(body.get("host", "remote"), int(body.get("mem_capacity_mb", 0) or 0),
                                       body.get("device", "cpu"))
         return 200, {"status": "registered", "worker_id": wid}
@@ -333,6 +344,10 @@ class Runner:
     def leave(self, worker_id: str) -> bool:
         """A worker unsubscribed: stop giving it work (runners with membership)."""
         return False
+
+    def join_info(self) -> Optional[Dict[str, Any]]:
+        """Where an extra worker joins this runner (None: no elastic membership)."""
+        return None
 
     def shutdown(self) -> None:
         pass

@@ -849,6 +849,11 @@ class DistributedRunner(Runner):
                 if not js.finished and not js.staged_ready:
                     self._stage(js)
 
+    def join_info(self) -> Optional[Dict[str, Any]]:
+        """The rendezvous store a ``join_cluster`` worker connects to (/subscribe answer)."""
+        return {"host": os.environ.get("MASTER_ADDR", "127.0.0.1"), "port": int(os.environ.get("MASTER_PORT", "0")),
+                "workers": sum(1 for w in self.workers.values() if w.alive)}
+
     def leave(self, worker_id: str) -> bool:
         for wid, sid in list(self.worker_ids.items()):
             if sid == worker_id:

@@ -150,6 +150,8 @@ def _drive_join(ctl, runner):
     metrics = ctl.metrics(sid, a["job_id"])[1]
     joined = [w for w in runner.workers.values() if not w.in_group]
     sched_id = runner.worker_ids[joined[0].wid]
+    sub = ctl.subscribe({"host": "newbox", "device": "cpu"})[1]   # the REST answer points at the store
+    assert sub["status"] == "join" and sub["join"]["port"] > 0 and "--join" in sub["command"], sub
     left = ctl.unsubscribe({"worker_id": sched_id})[1]
     return status, metrics, joined[0].wid, left
 
