@@ -16,7 +16,9 @@ LogisticRegression
     multiclass the multinomial softmax (or OvR columns for liblinear / multi_class='ovr').
 LinearRegression
     Normal equations per split (shared by every candidate on that split), solved by
-    pseudo-inverse (min-norm like sklearn's lstsq).
+    pseudo-inverse (min-norm like sklearn's lstsq).  On the GPU every split's moments
+    come from one fused pass over X (``dml_split_moments``: f64 MFMA tiles, split
+    masks from the role rows, shifted by the column means for an accurate centring).
 """
 from __future__ import annotations
 
@@ -24,7 +26,7 @@ import ctypes
 import math
 import os
 import time
-from typing import Any, Dict, List
+from typing import Any, Dict, List, Tuple
 
 import numpy as np
 import torch
@@ -752,6 +754,9 @@ class LinearRegressionFamily(Family):
         t0 = time.perf_counter()
         X, y = data.X, data.y_reg
         cache: Dict[tuple, tuple] = {}
+        if (data.is_gpu and not getattr(data, "is_row_shard", False)
+                and os.environ.get("DML_LINREG_KERNEL", "1") != "0"):
+            cache = self._solve_from_moments(data, tasks)
         outs = []
         for t in tasks:
             key = (t.split, t.params["fit_intercept"])
@@ -786,6 +791,54 @@ class LinearRegressionFamily(Family):
         for o in outs:
             o.fit_seconds = dt / max(1, len(outs))
         return outs
+
+    @staticmethod
+    def split_moments(data, splits: List[int]) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(M [len(splits), d+2, d+2] float64, shift [d+1]): every split's train-row moments
+        of z = [x - c_x, 1, y - c_y] from ONE pass over X (csrc/kernels/linear.hip
+        ``dml_split_moments``, f64 MFMA), c = the column means over all rows."""
+        X, y = data.X.contiguous(), data.y_reg.float().contiguous()
+        n, d = X.shape
+        dev = X.device
+        shift = torch.cat([torch.mean(X, 0, dtype=torch.float64), torch.mean(y, dtype=torch.float64).view(1)])
+        Dp = _roundup(d + 2, 16)
+        roles = data.roles[torch.tensor(splits, dtype=torch.long, device=dev)].contiguous()
+        out = torch.zeros((len(splits), Dp, Dp), dtype=torch.float64, device=dev)
+        lib = native.hip_lib()
+        for g0 in range(0, len(splits), 8):
+            g1 = min(len(splits), g0 + 8)
+            rc = lib.dml_split_moments(native.ptr(X), X.stride(0), native.ptr(y), native.ptr(shift),
+                                       native.ptr(roles[g0:g1]), n, d, g1 - g0, native.ptr(out[g0:g1]), Dp,
+                                       native.stream_handle(dev))
+            if rc:
+                raise RuntimeError(f"dml_split_moments failed ({rc})")
+        M = torch.triu(out) + torch.triu(out, 1).transpose(1, 2)   # the kernel fills ti <= tj tiles
+        return M[:, :d + 2, :d + 2], shift
+
+    def _solve_from_moments(self, data, tasks) -> Dict[tuple, tuple]:
+        """(split, fit_intercept) -> (w, b0) for every task, from the fused moments."""
+        d = data.d
+        splits = sorted({t.split for t in tasks})
+        M, shift = self.split_moments(data, splits)
+        cx, cy = shift[:d], shift[d]
+        out: Dict[tuple, tuple] = {}
+        for i, sp in enumerate(splits):
+            m = M[i]
+            cnt, Sx, Sy = m[d, d], m[:d, d], m[d + 1, d]
+            XX, Xy = m[:d, :d], m[:d, d + 1]
+            for fi in sorted({t.params["fit_intercept"] for t in tasks if t.split == sp}):
+                if fi:
+                    xm, ym = Sx / cnt.clamp_min(1), Sy / cnt.clamp_min(1)
+                    A = XX - cnt * torch.outer(xm, xm)
+                    b = Xy - cnt * xm * ym
+                    w = torch.linalg.pinv(A, hermitian=True) @ b
+                    out[(sp, fi)] = (w, (ym + cy) - (xm + cx) @ w)
+                else:   # moments about the origin: x = z + c_x, y = z_y + c_y
+                    XX0 = XX + torch.outer(Sx, cx) + torch.outer(cx, Sx) + cnt * torch.outer(cx, cx)
+                    Xy0 = Xy + Sx * cy + cx * Sy + cnt * cx * cy
+                    w = torch.linalg.pinv(XX0, hermitian=True) @ Xy0
+                    out[(sp, fi)] = (w, torch.zeros((), dtype=torch.float64, device=w.device))
+        return out
 
     @staticmethod
     def _sharded_solve(data, Xt: torch.Tensor, yt: torch.Tensor, fit_intercept: bool):

@@ -189,6 +189,7 @@ def _register_optional(lib) -> None:
                                       c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
         "dml_svm_split_limits": (c_i32, [c_vp, c_vp]),
         "dml_svm_smo": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+        "dml_split_moments": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp]),
         "dml_lr_mfma_tile": (c_i32, []),
         "dml_lr_mfma_fwd": (c_i32, [ctypes.POINTER(LrFwdArgs), c_vp]),
         "dml_lr_mfma_grad": (c_i32, [ctypes.POINTER(LrGradArgs), c_vp]),

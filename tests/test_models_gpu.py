@@ -263,3 +263,36 @@ def test_slice_metrics_report_gpu_fields():
     for m in metrics.values():
         assert m["gpu_id"] == 0 and m["hbm_peak_bytes"] > 0
         assert m["slice_fits"] == 8 and m["slice_fits_per_s"] > 0
+
+
+@pytest.mark.parametrize("n,d,offset", [(5000, 7, 0.0), (40000, 33, 500.0), (3000, 130, 3.0)])
+def test_linreg_fused_moments_match_float64_torch(n, d, offset, monkeypatch):
+    """LinearRegression's one-pass f64-MFMA split moments (dml_split_moments) give the
+    float64 torch solution: same coefficients / predictions, with and without intercept,
+    on data far from the origin (the shift keeps the centring exact)."""
+    from cs230_distributed_machine_learning_amd.models import linear
+
+    rng = np.random.RandomState(d)
+    X = (rng.randn(n, d) + offset).astype(np.float32)
+    y = (X @ rng.randn(d) + 0.1 * rng.randn(n) + 2.0).astype(np.float32)
+    dg = _dd(X, y, False, "cuda:0")
+    splits = list(range(len(dg.split_names)))
+    M, shift = linear.LinearRegressionFamily.split_moments(dg, splits)
+    Z = torch.cat([torch.from_numpy(X).double() - shift[:d].cpu(), torch.ones(n, 1, dtype=torch.float64),
+                   torch.from_numpy(y).double().view(-1, 1) - shift[d].cpu()], 1)
+    for i, s in enumerate(splits):
+        m = torch.from_numpy((dg.roles[s] == 1).cpu().numpy()).double()
+        ref = (Z * m[:, None]).t() @ Z
+        torch.testing.assert_close(M[i].cpu(), ref, rtol=1e-10, atol=1e-7 * float(ref.abs().max()))
+    fam = linear.LinearRegressionFamily()
+    tasks = []
+    from cs230_distributed_machine_learning_amd.models.base import FitTask
+    for fi in (True, False):
+        for s in splits:
+            tasks.append(FitTask(task_id=len(tasks), candidate=0, split=s, model_type="LinearRegression",
+                                 params=fam.resolve("LinearRegression", {"fit_intercept": fi}, n, d, 1)))
+    got = fam.run(dg, tasks)
+    monkeypatch.setenv("DML_LINREG_KERNEL", "0")
+    ref = fam.run(dg, tasks)
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a.pred.double(), b.pred.double(), rtol=1e-5, atol=1e-4)
