@@ -797,10 +797,13 @@ class LinearRegressionFamily(Family):
         """(M [len(splits), d+2, d+2] float64, shift [d+1]): every split's train-row moments
         of z = [x - c_x, 1, y - c_y] from ONE pass over X (csrc/kernels/linear.hip
         ``dml_split_moments``, f64 MFMA), c = the column means over all rows."""
-        X, y = data.X.contiguous(), data.y_reg.float().contiguous()
+        X = data.X.contiguous()
+        y = data.y_reg.float().contiguous() if getattr(data, "y_reg", None) is not None else None
         n, d = X.shape
         dev = X.device
-        shift = torch.cat([torch.mean(X, 0, dtype=torch.float64), torch.mean(y, dtype=torch.float64).view(1)])
+        ymean = torch.mean(y, dtype=torch.float64).view(1) if y is not None else torch.zeros(1, dtype=torch.float64,
+                                                                                               device=dev)
+        shift = torch.cat([torch.mean(X, 0, dtype=torch.float64), ymean])
         Dp = _roundup(d + 2, 16)
         roles = data.roles[torch.tensor(splits, dtype=torch.long, device=dev)].contiguous()
         out = torch.zeros((len(splits), Dp, Dp), dtype=torch.float64, device=dev)

@@ -22,6 +22,7 @@ Here:
 from __future__ import annotations
 
 import math
+import os
 import time
 from typing import Any, Dict, List
 
@@ -106,14 +107,28 @@ class PCAFamily(Family):
         d = data.d
         eig: Dict[int, Any] = {}
         outs = []
+        fused = {}
+        if data.is_gpu and not getattr(data, "is_row_shard", False) and os.environ.get("DML_LINREG_KERNEL", "1") != "0":
+            # every split's covariance from one pass over X (the LinearRegression moments kernel)
+            from .linear import LinearRegressionFamily
+
+            splits = sorted({t.split for t in tasks})
+            M, shift = LinearRegressionFamily.split_moments(data, splits)
+            for i, sp in enumerate(splits):
+                cnt, Sx, XX = M[i][d, d], M[i][:d, d], M[i][:d, :d]
+                dm = Sx / cnt.clamp_min(1)
+                fused[sp] = (shift[:d] + dm, (XX - cnt * torch.outer(dm, dm)) / max(1.0, float(cnt) - 1), int(cnt))
         for t in tasks:
             if t.split not in eig:
-                tr = data.train_rows[t.split].long()
-                Xt = X[tr].double()
-                mean = Xt.mean(0)
-                Xc = Xt - mean
-                n = Xt.shape[0]
-                cov = Xc.t() @ Xc / max(1, n - 1)
+                if t.split in fused:
+                    mean, cov, n = fused[t.split]
+                else:
+                    tr = data.train_rows[t.split].long()
+                    Xt = X[tr].double()
+                    mean = Xt.mean(0)
+                    Xc = Xt - mean
+                    n = Xt.shape[0]
+                    cov = Xc.t() @ Xc / max(1, n - 1)
                 lam, V = torch.linalg.eigh(cov)                       # ascending
                 lam, V = lam.flip(0).clamp_min(0), V.flip(1)
                 te = data.test_rows[t.split].long()

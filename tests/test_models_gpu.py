@@ -296,3 +296,19 @@ def test_linreg_fused_moments_match_float64_torch(n, d, offset, monkeypatch):
     ref = fam.run(dg, tasks)
     for a, b in zip(got, ref):
         torch.testing.assert_close(a.pred.double(), b.pred.double(), rtol=1e-5, atol=1e-4)
+
+
+def test_pca_gpu_fused_covariance_matches_cpu():
+    """PCA on the GPU takes every split's covariance from the fused moments kernel; the
+    CV log-likelihood scores match the host float64 path."""
+    rng = np.random.RandomState(3)
+    X = (rng.randn(6000, 12) @ rng.randn(12, 12) + 40.0).astype(np.float32)
+    y = rng.randint(0, 2, 6000)
+    grid = list(ParameterGrid({"n_components": [1, 3, 6, 11], "whiten": [False, True]}))
+    out = {}
+    for dev in ("cpu", "cuda:0"):
+        dd = DeviceData(X, y, True, dev)
+        res = run_candidates(dd, JobSpec("PCA", grid, cv=5), range(len(grid)))
+        assert all(r.ok for r in res), [r.error for r in res]
+        out[dev] = np.array([r.result["mean_cv_score"] for r in res])
+    np.testing.assert_allclose(out["cuda:0"], out["cpu"], rtol=1e-6, atol=1e-6)
