@@ -58,3 +58,32 @@ def test_held_when_no_workers_and_requeue_on_death():
 def test_algo_weight_scales_estimates():
     s = Scheduler(algo_weight={"SVC": 3.0})
     assert s.estimate("svc", 2.0) == 6.0 and s.estimate("LogisticRegression", 2.0) == 2.0
+
+
+def test_calibration_is_cost_weighted_so_a_warmup_job_cannot_misprice_a_search():
+    """A tiny warm-up slice (all fixed overhead: 0.3 s for 0.001 cost units) followed by
+    one real slice (1.5 s for 30 units): the estimate for a 15-unit candidate must be
+    near the real 0.05 s/unit, not the warm-up's 300 s/unit."""
+    s = Scheduler()
+    wid = s.register("local")
+    s.observe(wid, Unit("warm", 0.001, algo="RandomForestClassifier"), 0.3)
+    s.observe(wid, Unit("real", 30.0, algo="RandomForestClassifier"), 1.5)
+    est = s.estimate("RandomForestClassifier", 15.0)
+    assert 0.6 < est < 1.2, est
+
+
+def test_should_recut_when_queue_far_from_target():
+    from types import SimpleNamespace
+
+    from cs230_distributed_machine_learning_amd.engine.service import should_recut
+
+    sched = Scheduler()
+    ctl = SimpleNamespace(config=SimpleNamespace(chunk_target_s=2.0), scheduler=sched)
+    plan = {"model_type": "RandomForestClassifier"}
+    costs = [1.0] * 10
+    sched.calib["randomforestclassifier"] = 0.1                    # 0.1 s per candidate
+    assert should_recut(ctl, plan, [[i] for i in range(10)], costs)           # 0.1 s slices << 2 s
+    assert not should_recut(ctl, plan, [list(range(0, 5)) * 4, list(range(5, 10)) * 4], costs)   # 2 s slices
+    sched.calib["randomforestclassifier"] = 5.0
+    assert should_recut(ctl, plan, [[0, 1], [2, 3], [4, 5]], costs)            # 10 s slices of 2
+    assert not should_recut(ctl, plan, [[0], [1], [2]], costs)                 # single candidates: nothing to split
