@@ -36,8 +36,8 @@ class ForestTiers:
 
     sub_max: int = 64          # <= 64 rows: one wave finishes the whole subtree (k_subtree)
     sub_cache_max_d: int = 256  # cache the subtree's bin rows in LDS when d <= this
-    wave_max: int = 512         # sweeps (profiles/r1_forest_ab_experiments.md): 512 / 131072 best
-    block_max: int = 131072
+    wave_max: int = 512         # sweeps: profiles/r1_forest_ab_experiments.md, r2_tier_sweep.txt
+    block_max: int = 32768      # r2 kernels (XbT large tier): 32768 beats 131072 by 4 %
     chunk: int = 16384
     kg_wave: int = 4
     kg_block: int = 16
