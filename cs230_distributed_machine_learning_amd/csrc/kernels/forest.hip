@@ -32,6 +32,11 @@
 #ifndef DML_RPT_BLOCK
 #define DML_RPT_BLOCK 1
 #endif
+#if DML_RPT_BLOCK != 1
+// measured round 2 (profiles/r2_compile_variants.log): RPT 2 grows wrong trees with the
+// block tier's bin scratch (bscr) -- the host-builder equality tests catch it
+#error "DML_RPT_BLOCK != 1 is not supported (block-tier bin scratch assumes one row per thread)"
+#endif
 #ifndef DML_BLOCK_NT
 #define DML_BLOCK_NT 256     // threads per block-tier node
 #endif
