@@ -36,6 +36,9 @@ class Config:
     # at least dp_min_cells cells AND (fewer candidates than ranks OR > dp_auto_gb of fp32)
     dp_auto_gb: float = 48.0
     dp_min_cells: int = 50_000_000
+    # tree jobs on a table whose float32 copy exceeds this fraction of the device's free
+    # HBM keep only the uint8 bins resident (DeviceData binned_only: streamed binning)
+    stream_binned_fraction: float = 0.5
     algo_weight: Dict[str, float] = field(default_factory=dict)
     log_dir: Optional[str] = None
     deterministic: bool = True

@@ -17,16 +17,36 @@ import torch
 from ..search.cv import ROLE_TEST, ROLE_TRAIN
 
 
+STREAM_CHUNK_ROWS = 1 << 20
+
+
 class DeviceData:
+    """``binned_only=True``: the float32 table never becomes resident.  It is streamed
+    from host memory (numpy array or ``np.memmap``) in row chunks through two pinned
+    buffers, with the H2D copy on a side stream overlapping the binning kernel of the
+    previous chunk; only the uint8 bins stay in HBM (4x smaller: a 400 GB float32 table
+    trains as 100 GB of bins).  The quantile edges come from the same 200k-row sample the
+    resident path draws (ops/binning.py), so the bins -- and every tree -- are identical.
+    Only tree families run on such a table (``Family.binned_ok``)."""
+
     def __init__(self, X, y, classification: bool, device: torch.device | str = "cpu",
-                 classes: Optional[np.ndarray] = None, name: str = ""):
+                 classes: Optional[np.ndarray] = None, name: str = "", binned_only: bool = False,
+                 chunk_rows: int = STREAM_CHUNK_ROWS):
         self.device = torch.device(device)
         self.name = name
-        if isinstance(X, torch.Tensor):
+        self.binned_only = bool(binned_only)
+        self._Xb = None
+        self._edges = None
+        if self.binned_only:
+            self.X = None
+            Xh = X.cpu().numpy() if isinstance(X, torch.Tensor) else X
+            self.n, self.d = Xh.shape
+        elif isinstance(X, torch.Tensor):
             self.X = X.to(self.device, dtype=torch.float32).contiguous()
+            self.n, self.d = self.X.shape
         else:
             self.X = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).to(self.device)
-        self.n, self.d = self.X.shape
+            self.n, self.d = self.X.shape
         self.classification = bool(classification)
         self.y_is_numeric = True
         y_np = y.cpu().numpy() if isinstance(y, torch.Tensor) else np.asarray(y)
@@ -56,8 +76,8 @@ class DeviceData:
                 y_num = np.unique(y_np.astype(str), return_inverse=True)[1].astype(np.float32)
                 self.y_is_numeric = False
             self.y_reg = torch.from_numpy(y_num).to(self.device)
-        self._Xb = None
-        self._edges = None
+        if self.binned_only:
+            self._stream_bin(Xh, chunk_rows)
         self.roles = None
         self.split_names: List[str] = []
         self.test_rows: List[torch.Tensor] = []
@@ -69,6 +89,56 @@ class DeviceData:
         return self.device.type == "cuda"
 
     # ---- binned copy (trees) -------------------------------------------------------
+    def _stream_bin(self, Xh, chunk_rows: int) -> None:
+        from ..ops import binning
+        from ..utils import native
+
+        n, d, dev = self.n, self.d, self.device
+        sample = 200_000                                  # binning.quantile_edges' sample
+        if n > sample:
+            idx = np.sort(np.random.RandomState(0).choice(n, sample, replace=False))
+            Xs = np.array(Xh[idx], dtype=np.float32, order="C")
+        else:
+            Xs = np.array(Xh, dtype=np.float32, order="C")
+        Xs_t = torch.from_numpy(Xs).to(dev)
+        self._edges = binning.quantile_edges(Xs_t)
+        self._sample_max = Xs_t.max(0).values
+        del Xs_t
+        if not self.is_gpu:
+            self._Xb = torch.empty((n, d), dtype=torch.uint8)
+            for r0 in range(0, n, chunk_rows):
+                r1 = min(n, r0 + chunk_rows)
+                self._Xb[r0:r1] = binning.bin_matrix(torch.from_numpy(np.array(Xh[r0:r1], np.float32, order="C")),
+                                                     self._edges)
+            return
+        ld = binning.row_pitch(d)
+        buf = torch.zeros((n, ld), dtype=torch.uint8, device=dev)
+        chunk = max(1, min(chunk_rows, n))
+        pins = [torch.empty((chunk, d), dtype=torch.float32, pin_memory=True) for _ in range(2)]
+        devb = [torch.empty((chunk, d), dtype=torch.float32, device=dev) for _ in range(2)]
+        copy_stream = torch.cuda.Stream(dev)
+        compute = torch.cuda.current_stream(dev)
+        done = [None, None]
+        lib = native.hip_lib()
+        for i, r0 in enumerate(range(0, n, chunk)):
+            b, m = i % 2, min(chunk, n - r0)
+            if done[b] is not None:
+                done[b].synchronize()                 # the chunk that last used buffer b is binned
+            np.copyto(pins[b][:m].numpy(), Xh[r0:r0 + m], casting="same_kind")
+            with torch.cuda.stream(copy_stream):
+                devb[b][:m].copy_(pins[b][:m], non_blocking=True)
+                copied = torch.cuda.Event()
+                copied.record(copy_stream)
+            compute.wait_event(copied)
+            rc = lib.dml_bin(native.ptr(devb[b]), m, d, native.ptr(self._edges), native.ptr(buf[r0:r0 + m]), ld,
+                             native.stream_handle(dev))
+            if rc != 0:
+                raise RuntimeError(f"dml_bin failed ({rc})")
+            done[b] = torch.cuda.Event()
+            done[b].record(compute)
+        torch.cuda.synchronize(dev)
+        self._Xb = buf[:, :d]
+
     def binned(self):
         if self._Xb is None:
             from ..ops import binning
@@ -87,6 +157,8 @@ class DeviceData:
 
     def feature_major(self) -> torch.Tensor:
         """``X^T`` [d, n] contiguous (coalesced per-feature streaming in the KNN/SVM kernels)."""
+        if self.X is None:
+            raise ValueError("binned-only table: the float32 rows are not resident")
         if getattr(self, "_XT", None) is None:
             self._XT = self.X.t().contiguous()
         return self._XT
@@ -95,6 +167,15 @@ class DeviceData:
         """(values float32 [d, 256], exact uint8 [d]): the value each bin stands for, and
         whether EVERY row's value equals its bin's value (features with <= 256 distinct
         values).  Used to place split thresholds at sklearn's midpoints."""
+        if getattr(self, "_binvals", None) is None and self.X is None:
+            # binned-only: no rows to check exactness against -> thresholds stay at bin
+            # boundaries (the midpoint refinement is skipped)
+            E = self._edges
+            finite = torch.isfinite(E)
+            V = torch.full((self.d, 256), float("inf"), dtype=torch.float32, device=self.device)
+            V[:, :255] = torch.where(finite, E, V[:, :255])
+            V[torch.arange(self.d, device=self.device), finite.sum(1)] = self._sample_max
+            self._binvals = (V.contiguous(), torch.zeros(self.d, dtype=torch.uint8, device=self.device))
         if getattr(self, "_binvals", None) is None:
             Xb = self.binned()
             E = self._edges

@@ -356,6 +356,15 @@ class Runner:
 class DeviceCache:
     """Resident DeviceData per (dataset file, columns, task type) on one device."""
 
+    def _binned_only(self, ctl: Controller, plan: Dict[str, Any], X) -> bool:
+        """Tree jobs on a table too large for HBM as float32 keep only its bins resident."""
+        if not str(self.device).startswith("cuda") or not getattr(family_of(plan["model_type"]), "binned_ok", False):
+            return False
+        import torch
+
+        free = torch.cuda.mem_get_info(torch.device(self.device))[0]
+        return float(np.asarray(X).shape[0]) * np.asarray(X).shape[1] * 4 > ctl.config.stream_binned_fraction * free
+
     def __init__(self, device: str, max_items: int = 4):
         self.device = device
         self.max_items = max_items
@@ -367,12 +376,14 @@ class DeviceCache:
 
         ds = ctl.registry.load(dataset_id, plan["feature_columns"], plan["target_column"])
         clf = is_classifier(plan["model_type"])
-        key = (ds.path, os.path.getmtime(ds.path) if ds.path else 0, tuple(ds.feature_names), ds.target_name, clf)
+        binned = self._binned_only(ctl, plan, ds.X)
+        key = (ds.path, os.path.getmtime(ds.path) if ds.path else 0, tuple(ds.feature_names), ds.target_name, clf,
+               binned)
         if key in self._items:
             self._order.remove(key)
             self._order.append(key)
             return self._items[key]
-        dd = DeviceData(ds.X, ds.y, clf, self.device, name=dataset_id)
+        dd = DeviceData(ds.X, ds.y, clf, self.device, name=dataset_id, binned_only=binned)
         self._items[key] = dd
         self._order.append(key)
         while len(self._order) > self.max_items:

@@ -117,6 +117,8 @@ class GradientBoostingFamily(Family):
     model_types = (_CLS, _REG)
     classifiers = (_CLS,)
 
+    binned_ok = True   # the stages only read the uint8 bins (DeviceData binned_only tables)
+
     def __init__(self):
         self.tiers = forest_ops.ForestTiers()
 

@@ -79,6 +79,7 @@ class ForestFamily(Family):
     model_types = (_CLS, _REG)
     classifiers = (_CLS,)
     uses_forest_arena = True   # batches reuse the device arena (ops/forest_ops.py ARENA)
+    binned_ok = True           # fits only read the uint8 bins (DeviceData binned_only tables)
 
     def __init__(self):
         self.tiers = forest_ops.ForestTiers()
