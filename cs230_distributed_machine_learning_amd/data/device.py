@@ -31,7 +31,7 @@ class DeviceData:
 
     def __init__(self, X, y, classification: bool, device: torch.device | str = "cpu",
                  classes: Optional[np.ndarray] = None, name: str = "", binned_only: bool = False,
-                 chunk_rows: int = STREAM_CHUNK_ROWS):
+                 chunk_rows: int = STREAM_CHUNK_ROWS, _bins=None):
         self.device = torch.device(device)
         self.name = name
         self.binned_only = bool(binned_only)
@@ -76,7 +76,10 @@ class DeviceData:
                 y_num = np.unique(y_np.astype(str), return_inverse=True)[1].astype(np.float32)
                 self.y_is_numeric = False
             self.y_reg = torch.from_numpy(y_num).to(self.device)
-        if self.binned_only:
+        if self.binned_only and _bins is not None:   # received bins (parallel/data.py broadcast_binned)
+            self._Xb_full, self._edges, self._sample_max = _bins
+            self._Xb = self._Xb_full[:, :self.d]
+        elif self.binned_only:
             self._stream_bin(Xh, chunk_rows)
         self.roles = None
         self.split_names: List[str] = []
@@ -105,7 +108,7 @@ class DeviceData:
         self._sample_max = Xs_t.max(0).values
         del Xs_t
         if not self.is_gpu:
-            self._Xb = torch.empty((n, d), dtype=torch.uint8)
+            self._Xb = self._Xb_full = torch.empty((n, d), dtype=torch.uint8)
             for r0 in range(0, n, chunk_rows):
                 r1 = min(n, r0 + chunk_rows)
                 self._Xb[r0:r1] = binning.bin_matrix(torch.from_numpy(np.array(Xh[r0:r1], np.float32, order="C")),
@@ -137,7 +140,17 @@ class DeviceData:
             done[b] = torch.cuda.Event()
             done[b].record(compute)
         torch.cuda.synchronize(dev)
+        self._Xb_full = buf
         self._Xb = buf[:, :d]
+
+    @classmethod
+    def from_bins(cls, Xb_full: torch.Tensor, d: int, edges: torch.Tensor, sample_max: torch.Tensor, y,
+                  classification: bool, device, name: str = "") -> "DeviceData":
+        """A binned-only table from bins built elsewhere (a broadcast from rank 0)."""
+        n = Xb_full.shape[0]
+        shape_only = np.lib.stride_tricks.as_strided(np.zeros(1, np.float32), (n, d), (0, 0))
+        return cls(shape_only, y, classification, device, name=name, binned_only=True,
+                   _bins=(Xb_full, edges, sample_max))
 
     def binned(self):
         if self._Xb is None:

@@ -61,6 +61,41 @@ def broadcast_table(X: Optional[np.ndarray], y: Optional[np.ndarray], device: to
     return Xd, y_host
 
 
+def broadcast_binned(X: Optional[np.ndarray], y: Optional[np.ndarray], classification: bool, device: torch.device,
+                     name: str = ""):
+    """Binned-only distribution of a table too large for HBM as float32 (tree jobs):
+    rank 0 streams its host rows through the binning kernel (DeviceData binned_only),
+    then ONE RCCL broadcast of the uint8 bins (+ edges) lands them on every rank -- a
+    quarter of the float32 bytes over xGMI, and no rank ever holds the float32 table."""
+    from ..data.device import DeviceData
+
+    inf = dist.info()
+    if not inf.is_dist:
+        return DeviceData(X, y, classification, device, name=name, binned_only=True)
+    st = dist.store()
+    key = "dataset/binmeta"
+    if inf.rank == 0:
+        _, y_host = broadcast_table(np.zeros((len(y), 0), dtype=np.float32), y, device)
+        dd = DeviceData(X, y_host, classification, device, name=name, binned_only=True)
+        buf, edges, smax = dd._Xb_full.contiguous(), dd._edges.contiguous(), dd._sample_max.contiguous().float()
+        st.set(key, json.dumps({"n": int(buf.shape[0]), "ld": int(buf.shape[1]), "d": int(dd.d)}))
+    else:
+        _, y_host = broadcast_table(None, None, device)
+        st.wait([key])
+        meta = json.loads(st.get(key))
+        buf = torch.empty((meta["n"], meta["ld"]), dtype=torch.uint8, device=device)
+        edges = torch.empty((meta["d"], 255), dtype=torch.float32, device=device)
+        smax = torch.empty((meta["d"],), dtype=torch.float32, device=device)
+    dist.broadcast(buf, 0)
+    dist.broadcast(edges, 0)
+    dist.broadcast(smax, 0)
+    dist.barrier()
+    if inf.rank == 0:
+        st.delete_key(key)
+        return dd
+    return DeviceData.from_bins(buf, meta["d"], edges, smax, y_host, classification, device, name=name)
+
+
 def allgather_table(X_shard: torch.Tensor, y_shard: torch.Tensor):
     return dist.all_gather_rows(X_shard), dist.all_gather_rows(y_shard)
 

@@ -224,16 +224,33 @@ class WorkerCore:
         from ..data.device import DeviceData
 
         plan = msg["plan"]
+        clf = is_classifier(plan["model_type"])
         X = y = None
+        mode_key = "dataset/mode"
         if self.inf.rank == 0:
             ds = ctl.registry.load(msg["dataset_id"], plan["feature_columns"], plan["target_column"])
             X, y = ds.X, ds.y
-        Xd, y_host = pdata.broadcast_table(X, y, self.device)
-        dd = DeviceData(Xd, y_host, is_classifier(plan["model_type"]), self.device, name=msg["dataset_id"])
-        if _needs_bins(plan):
-            pdata.share_bins(dd)
+            binned = ctl is not None and _binned_only_table(ctl, plan, X, self.device)
+            self.store_raw().set(mode_key, "binned" if binned else "full")
+        else:
+            self.store_raw().wait([mode_key])
+            binned = self.store_raw().get(mode_key).decode() == "binned"
+        if binned:   # tree job on a table too large for HBM as float32: bins only
+            dd = pdata.broadcast_binned(X, y, clf, self.device, name=msg["dataset_id"])
+        else:
+            Xd, y_host = pdata.broadcast_table(X, y, self.device)
+            dd = DeviceData(Xd, y_host, clf, self.device, name=msg["dataset_id"])
+            if _needs_bins(plan):
+                pdata.share_bins(dd)
+        dist.barrier()
+        if self.inf.rank == 0:
+            self.store_raw().delete_key(mode_key)
         self._keep(msg["dataset_key"], dd)
         return dd
+
+    @staticmethod
+    def store_raw():
+        return dist.store()
 
     # ---- assignments ----------------------------------------------------------------------
     def execute(self, a: Dict[str, Any], ctl: Optional[Controller]) -> Dict[str, Any]:
@@ -363,6 +380,14 @@ def worker_loop(core: WorkerCore, ctl: Optional[Controller] = None, heartbeat: b
     finally:
         if hb is not None:
             hb.stop()
+
+
+def _binned_only_table(ctl: Controller, plan: Dict[str, Any], X, device) -> bool:
+    """Same rule as the local device cache (engine/service.py DeviceCache._binned_only)."""
+    if getattr(device, "type", str(device)) != "cuda" or not getattr(family_of(plan["model_type"]), "binned_ok", False):
+        return False
+    free = torch.cuda.mem_get_info(device)[0]
+    return float(np.asarray(X).shape[0]) * np.asarray(X).shape[1] * 4 > ctl.config.stream_binned_fraction * free
 
 
 def join_cluster(host: str, port: int, device: torch.device, mem_mb: int = 0, timeout_s: float = 60.0) -> int:

@@ -51,3 +51,48 @@ def test_binned_only_cpu_matches_resident(tmp_path):
 def test_binned_only_gpu_streaming_matches_resident(tmp_path):
     # > 200k rows: the edge sample path; small chunks: the pinned double-buffer pipeline
     _check("cuda:0", 260_000, 17, 50_000, tmp_path)
+
+
+def _bcast_rank(rank, world, port, q):
+    import os
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), OMP_NUM_THREADS="1")
+    from cs230_distributed_machine_learning_amd.parallel import data as pdata
+    from cs230_distributed_machine_learning_amd.parallel import dist
+
+    dist.init(want_gpu=False, timeout_s=120)
+    try:
+        X, y = _table(3000, 7, seed=5) if rank == 0 else (None, None)
+        dd = pdata.broadcast_binned(X, y, True, torch.device("cpu"), name="t")
+        q.put((rank, dd.binned().numpy().copy(), dd.edges.numpy().copy(), list(dd.y_host[:20]),
+               _scores(dd, "RandomForestClassifier", {"n_estimators": [6], "max_depth": [3, None]})))
+    finally:
+        dist.destroy()
+
+
+def test_broadcast_binned_two_ranks_gloo():
+    """The cluster runner's binned-only load: rank 0 bins, one broadcast of the bins."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_bcast_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict((r[0], r[1:]) for r in (q.get(timeout=180) for _ in range(2)))
+    for p in ps:
+        p.join(timeout=60)
+    X, y = _table(3000, 7, seed=5)
+    ref = DeviceData(X, y, True, "cpu")
+    for r in (0, 1):
+        Xb, E, y20, sc = out[r]
+        assert np.array_equal(Xb, ref.binned().numpy()) and np.array_equal(E, ref.edges.numpy())
+        assert list(y20) == list(y[:20])
+    assert out[0][3] == out[1][3]
