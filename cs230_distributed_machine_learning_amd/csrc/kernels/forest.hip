@@ -32,10 +32,8 @@
 #ifndef DML_RPT_BLOCK
 #define DML_RPT_BLOCK 1
 #endif
-#if DML_RPT_BLOCK != 1
-// measured round 2 (profiles/r2_compile_variants.log): RPT 2 grows wrong trees with the
-// block tier's bin scratch (bscr) -- the host-builder equality tests catch it
-#error "DML_RPT_BLOCK != 1 is not supported (block-tier bin scratch assumes one row per thread)"
+#if DML_RPT_BLOCK < 1 || DML_RPT_BLOCK > 4
+#error "DML_RPT_BLOCK must be 1..4"
 #endif
 #ifndef DML_BLOCK_NT
 #define DML_BLOCK_NT 256     // threads per block-tier node
@@ -823,6 +821,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
           for (int u = 0; u < RPT; ++u)
             if (rrow[u] != 0xFFFFFFFFu) hist_add<MODE>(hj, c, (int)bins[j][u], rpl[u]);
         }
+      }
+      if (NT == 256 && !reg_rows && pos == 0) {
+        // streamed block-tier node, RPT rows per thread: the first group's bins (<= 16
+        // visiting positions) into each row's scratch slot, as the one-row pipeline does
+#pragma unroll
+        for (int u = 0; u < RPT; ++u)
+          if (rrow[u] != 0xFFFFFFFFu) {
+            uint32_t w4[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < KGMAX && j < 16; ++j)
+              if (j < g) w4[j >> 2] |= (bins[j][u] & 0xFFu) << (8 * (j & 3));
+            *(uint4*)(c.bscr + (on.start + base + tid + NT * u) * 16) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+          }
       }
       if (NT == 64 && !reg_rows && pos < 16) {
         // streamed wave-tier node: this group's bins at byte (visiting position) of the slot
