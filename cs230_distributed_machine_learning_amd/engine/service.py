@@ -242,9 +242,12 @@ class Controller:
             import json
 
             while True:
+                # read ``finished`` BEFORE the snapshot: a job finishing between the two
+                # would otherwise end the stream on a non-final event
+                fin = job.finished
                 data = self.table.sse_json(job)
                 yield f"data: {json.dumps(data)}\n\n"
-                if job.finished:
+                if fin:
                     break
                 self.table.wait_finished(job.job_id, timeout=self.config.sse_interval_s)
 

@@ -80,6 +80,8 @@ class ForestFamily(Family):
     classifiers = (_CLS,)
     uses_forest_arena = True   # batches reuse the device arena (ops/forest_ops.py ARENA)
     binned_ok = True           # fits only read the uint8 bins (DeviceData binned_only tables)
+    data_parallel = True       # row-sharded fit: per-level histogram all-reduce (ops/forest_dp.py)
+    dp_when_few = False        # "auto" picks the row-sharded fit for tables too large to replicate only
 
     def __init__(self):
         self.tiers = forest_ops.ForestTiers()
@@ -191,7 +193,7 @@ class ForestFamily(Family):
         batch is formed under the same budget by ``_need``, so one slot of
         min(budget, the job's largest greedy batch) fits all of them.  ``rps``: resolved
         parameters per candidate; ``cands_per_batch`` is accepted for the runner's API."""
-        if not data.is_gpu or not rps:
+        if not data.is_gpu or not rps or getattr(data, "is_row_shard", False):
             return
         budget = self._budget(data)
         fits = []
@@ -236,7 +238,10 @@ class ForestFamily(Family):
             return []
         is_reg = not data.classification
         Xb = data.binned()
+        sharded = getattr(data, "is_row_shard", False)
         budget = self._budget(data)
+        if sharded:   # every rank must form the SAME batches: the smallest budget of the group
+            budget = float(data.all_reduce(torch.tensor([budget], dtype=torch.float64, device=data.device), "min")[0])
         outs: Dict[int, FitOutput] = {}
         # batches of whole fits under the memory budget (on the device: the builder's real
         # workspace + node-pool bytes, the same rule ``presize`` sizes the arena with)
@@ -245,6 +250,14 @@ class ForestFamily(Family):
         rows = pool = 0.0
         T = 0
         for t in tasks:
+            if sharded:
+                b = self._dp_bytes(data, t.params)
+                if cur and cur_bytes + b > budget:
+                    batches.append(cur)
+                    cur, cur_bytes = [], 0.0
+                cur.append(t)
+                cur_bytes += b
+                continue
             if data.is_gpu:
                 fr, fp = self.footprint(data, t.params)
                 ft = t.params["n_estimators"]
@@ -273,6 +286,15 @@ class ForestFamily(Family):
             for o in out_b:
                 outs[o.task_id] = o
         return [outs[t.task_id] for t in tasks]
+
+    def _dp_bytes(self, data, rp) -> float:
+        """Device bytes of one fit under the row-sharded builder: the (tree, row) weight
+        table and the sorted pair arrays of the local rows (3 int32 + sort scratch), and
+        the fit's share of the replicated node pool (ops/forest_dp.py)."""
+        T = rp["n_estimators"]
+        _rows, pool = self.footprint(data, rp)
+        VC = data.n_classes if data.classification else 3
+        return T * data.n * (1 + 0.632 * 40) + pool * (8 + 8 * VC) * 2
 
     def _specs(self, batch: List[FitTask]) -> np.ndarray:
         T = sum(t.params["n_estimators"] for t in batch)
@@ -309,20 +331,16 @@ class ForestFamily(Family):
             return None
         C = data.n_classes
         tab = np.ones((len(specs), C), dtype=np.float64)
-        roles = data.roles_np()
         labels = [str(c) for c in np.asarray(data.classes).tolist()]
         i = 0
         for t in batch:
             n = t.params["n_estimators"]
             cw = t.params.get("class_weight")
             row = np.ones(C, dtype=np.float64)
-            if cw == "balanced":
-                from ..search.cv import ROLE_TRAIN
-
-                y_tr = data.y_enc[roles[t.split] == ROLE_TRAIN]
-                cnt = np.bincount(y_tr, minlength=C).astype(np.float64)
+            if cw == "balanced":   # global counts under a row shard (an all-reduce)
+                cnt = data.train_class_counts(t.split, C).cpu().numpy().astype(np.float64)
                 present = max(1, int((cnt > 0).sum()))
-                row = np.where(cnt > 0, len(y_tr) / (present * np.maximum(cnt, 1)), 1.0)
+                row = np.where(cnt > 0, float(cnt.sum()) / (present * np.maximum(cnt, 1)), 1.0)
             elif isinstance(cw, dict):
                 for k, lab in enumerate(labels):
                     if lab in cw:
@@ -337,7 +355,13 @@ class ForestFamily(Family):
         specs = self._specs(batch)
         cw = self.class_weight_table(data, batch, specs)
         t0 = time.perf_counter()
-        if data.is_gpu:
+        sharded = getattr(data, "is_row_shard", False)
+        if sharded:
+            from ..ops import forest_dp
+
+            fb = forest_dp.build_dp(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
+                                    data.n_classes, is_reg, data.r0, reduce=data.all_reduce, cw=cw)
+        elif data.is_gpu:
             fb = forest_ops.build_gpu(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
                                       data.n_classes, is_reg, self.tiers, reuse_pool=True,
                                       XbT=data.binned_feature_major(), cw=cw)
@@ -350,7 +374,14 @@ class ForestFamily(Family):
                     forest_ops.prune_max_leaves(fb, specs, np.repeat(
                         [t.params.get("max_leaf_nodes", 0) for t in batch], [t.params["n_estimators"] for t in batch]))
             with trace.range("forest_refine"):
-                _refine(data, fb, Xb, specs, data.roles)
+                if sharded:
+                    from ..ops import forest_dp
+
+                    vals, exact = data.bin_values()
+                    if bool(exact.any()):   # already the AND over ranks: the same answer on every rank
+                        forest_dp.refine_dp(fb, Xb, data.roles, specs, data.r0, vals, exact, reduce=data.all_reduce)
+                else:
+                    _refine(data, fb, Xb, specs, data.roles)
             toff = np.zeros(len(batch) + 1, dtype=np.int64)
             np.cumsum([t.params["n_estimators"] for t in batch], out=toff[1:])
             rows = [data.test_rows[t.split] for t in batch]

@@ -129,11 +129,61 @@ class RowShard(DeviceData):
         self._test_counts: List[np.ndarray] = []
 
     # ---- collectives ------------------------------------------------------------------
-    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
-        """In-place sum over ranks (RCCL on GPU, gloo on CPU); identical result on every rank."""
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        """In-place sum / min / max over ranks (RCCL on GPU, gloo on CPU); identical
+        result on every rank."""
         if dist.info().is_dist:
-            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.group)
+            ro = {"sum": torch.distributed.ReduceOp.SUM, "min": torch.distributed.ReduceOp.MIN,
+                  "max": torch.distributed.ReduceOp.MAX}[op]
+            torch.distributed.all_reduce(t, op=ro, group=self.group)
         return t
+
+    def _world_bounds(self):
+        world = dist.info().world if dist.info().is_dist else 1
+        return [shard_bounds(self.n_global, world, k) for k in range(world)] if world > 1 else [(0, self.n_global)]
+
+    # ---- binned copy (row-sharded forests) --------------------------------------------
+    def binned(self):
+        """Bins of the local rows with the GLOBAL quantile edges: the 200k-row edge sample
+        of ops/binning.py is drawn over global row ids, every rank contributes its sampled
+        rows and one all-gather assembles the sample in global row order -- so the edges,
+        and every tree, equal the single-GPU ones."""
+        if self._Xb is None:
+            from ..ops import binning
+
+            sample = 200_000
+            if self.n_global > sample:
+                idx = np.sort(np.random.RandomState(0).choice(self.n_global, sample, replace=False))
+            else:
+                idx = np.arange(self.n_global)
+            loc = idx[(idx >= self.r0) & (idx < self.r0 + self.n)] - self.r0
+            Xs = self.X[torch.from_numpy(loc).to(self.device)]
+            counts = np.array([int(((idx >= a) & (idx < b)).sum()) for a, b in self._world_bounds()], dtype=np.int64)
+            Xs = self._gather_rows(Xs, counts)
+            self._edges = binning.quantile_edges(Xs)
+            self._Xb = binning.bin_matrix(self.X, self._edges)
+        return self._Xb
+
+    def bin_values(self):
+        """``DeviceData.bin_values`` over the global table: the top bin's value is the
+        global column max, and a feature is exactly binned only if it is on every rank."""
+        if getattr(self, "_binvals", None) is None:
+            Xb = self.binned()
+            E = self._edges
+            finite = torch.isfinite(E)
+            k = finite.sum(1)
+            V = torch.full((self.d, 256), float("inf"), dtype=torch.float32, device=self.device)
+            V[:, :255] = torch.where(finite, E, V[:, :255])
+            mx = self.X.max(0).values if self.n else torch.full((self.d,), float("-inf"), device=self.device)
+            V[torch.arange(self.d, device=self.device), k] = self.all_reduce(mx.contiguous(), "max")
+            exact = torch.ones(self.d, dtype=torch.bool, device=self.device)
+            step = max(1, (1 << 24) // max(1, self.d))
+            for s0 in range(0, self.n, step):
+                got = torch.gather(V, 1, Xb[s0:s0 + step].long().t()).t()
+                exact &= (got == self.X[s0:s0 + step]).all(0)
+            ex = self.all_reduce(exact.to(torch.int32), "min")
+            self._binvals = (V.contiguous(), ex.to(torch.uint8).contiguous())
+        return self._binvals
 
     def _gather_rows(self, t: torch.Tensor, counts: np.ndarray) -> torch.Tensor:
         if not dist.info().is_dist:
@@ -158,7 +208,7 @@ class RowShard(DeviceData):
         self.train_counts = [int((r == ROLE_TRAIN).sum()) for r in roles]          # global
         self._test_glob = [torch.from_numpy(np.nonzero(r == ROLE_TEST)[0].astype(np.int64)).to(self.device)
                            for r in roles]
-        bounds = [shard_bounds(self.n_global, world, k) for k in range(world)] if world > 1 else [(0, self.n_global)]
+        bounds = self._world_bounds()
         self._test_counts = [np.array([int((r[a:b] == ROLE_TEST).sum()) for a, b in bounds], dtype=np.int64)
                              for r in roles]
         if world > 1 and bounds[dist.info().rank] != (self.r0, self.r0 + n_loc):

@@ -600,7 +600,10 @@ class DistributedRunner(Runner):
             return True
         cfg = self.ctl.config
         cells = n_rows * n_feat
-        return cells >= cfg.dp_min_cells and (n_todo < self.world or cells * 4 > cfg.dp_auto_gb * 2 ** 30)
+        # forests: only for tables too large to replicate (a per-level all-reduce costs more
+        # than it saves while every rank can hold the table and run whole fits)
+        few = n_todo < self.world and getattr(family_of(plan["model_type"]), "dp_when_few", True)
+        return cells >= cfg.dp_min_cells and (few or cells * 4 > cfg.dp_auto_gb * 2 ** 30)
 
     def _fail_job(self, job: Job, e: Exception) -> None:
         for sub in job.subtasks:

@@ -120,6 +120,9 @@ def cpu_lib() -> ctypes.CDLL:
             lib.dml_cpu_bin.argtypes = [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64]
             lib.dml_cpu_svm_sizeof_prob.restype = c_i32
             lib.dml_cpu_svm_smo.argtypes = [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]
+            lib.dml_cpu_dp_sizeof_args.restype = c_i32
+            lib.dml_cpu_dp_step.restype = c_i32
+            lib.dml_cpu_dp_step.argtypes = [c_vp, c_i32]
             _cpu = lib
         return _cpu
 
@@ -196,6 +199,9 @@ def _register_optional(lib) -> None:
         "dml_split_hilo": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp]),
         "dml_lr_sizeof_fwd_args": (c_i32, []),
         "dml_lr_sizeof_grad_args": (c_i32, []),
+        "dml_dp_sizeof_args": (c_i32, []),
+        "dml_dp_sizeof_slot": (c_i32, []),
+        "dml_dp_step": (c_i32, [c_vp, c_i32, c_vp]),
     }
     for name, (res, args) in table.items():
         fn = getattr(lib, name, None)

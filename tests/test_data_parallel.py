@@ -12,6 +12,11 @@ import torch.multiprocessing as mp
 
 from cs230_distributed_machine_learning_amd.parallel.data_parallel import shard_bounds
 
+# row-sharded forests: per-level histogram all-reduce (ops/forest_dp.py)
+RF_GRID = [{"n_estimators": 8, "max_depth": md, "min_samples_leaf": msl, "class_weight": cw, "random_state": 5}
+           for md, msl, cw in ((None, 1, None), (6, 3, "balanced"), (None, 2, "balanced_subsample"))] + \
+          [{"n_estimators": 6, "criterion": "entropy", "max_features": 0.5, "random_state": 2}]
+RFR_GRID = [{"n_estimators": 5, "max_depth": 8, "random_state": 1}, {"n_estimators": 4, "min_samples_leaf": 5}]
 LR_GRID = [{"C": c, "solver": s, "class_weight": cw, "max_iter": 200}
            for c in (0.05, 1.0) for s in ("liblinear", "newton-cg") for cw in (None, "balanced")]
 
@@ -65,12 +70,14 @@ def _rank(rank, world, port, outq):
         a, b = shard_bounds(len(X), world, rank)
         shr = RowShard(X[a:b], y_reg, a, False, inf.device)
         lin = _run(shr, X, y_reg, "LinearRegression", [{"fit_intercept": True}, {"fit_intercept": False}], cv=3)
+        rf = _run(sh, X, yg, "RandomForestClassifier", RF_GRID, cv=3)
+        rfr = _run(shr, X, y_reg, "RandomForestRegressor", RFR_GRID, cv=3)
         err = None
         try:
-            _run(sh, X, yg, "RandomForestClassifier", [{"n_estimators": 2}])
+            _run(sh, X, yg, "KNeighborsClassifier", [{"n_neighbors": 3}])
         except ValueError as e:
             err = str(e)
-        outq.put(("ok", rank, lr, lin, err))
+        outq.put(("ok", rank, lr, lin, err, rf, rfr))
         dist.destroy()
     except Exception:  # pragma: no cover
         import traceback
@@ -110,6 +117,15 @@ def test_row_sharded_fits_match_single_process():
     for (cv_s, hold), (cv_r, hold_r) in zip(o0[3], ref_lin):
         assert np.allclose(cv_s, cv_r, atol=1e-9) and abs(hold - hold_r) < 1e-9
     assert o0[4] and "row-sharded" in o0[4]
+    # classification forests are the SAME forests the one-process builder grows (integer
+    # histograms summed over ranks): identical scores; regression sums floats in another
+    # order, so near-tie splits may differ
+    ref_rf = _run(DeviceData(X, y_cls, True), X, y_cls, "RandomForestClassifier", RF_GRID, cv=3)
+    assert o0[5] == o1[5] and o0[6] == o1[6]
+    assert o0[5] == ref_rf, (o0[5], ref_rf)
+    ref_rfr = _run(DeviceData(X, y_reg, False), X, y_reg, "RandomForestRegressor", RFR_GRID, cv=3)
+    for (cv_s, hold), (cv_r, hold_r) in zip(o0[6], ref_rfr):
+        assert np.allclose(cv_s, cv_r, atol=0.02) and abs(hold - hold_r) < 0.02, (cv_s, cv_r)
 
 
 def test_shard_bounds_cover_rows():

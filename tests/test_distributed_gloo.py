@@ -55,7 +55,7 @@ def _rank_main(rank, world, port, root, outq):
                 st, status = ctl.check_status(sid, jid)
                 body2 = dict(body, model_details={"model_type": "RandomForestClassifier",
                                                   "search_type": "GridSearchCV",
-                                                  "hyperparameters": {"base_estimator_params": {"n_estimators": 10},
+                                                  "hyperparameters": {"base_estimator_params": {"n_estimators": 10, "random_state": 7},
                                                                       "search_params": {"param_grid": {
                                                                           "max_depth": [2, 4, None]}},
                                                                       "cv_params": {"cv": 3}}})
@@ -82,7 +82,14 @@ def _rank_main(rank, world, port, root, outq):
                 status3 = ctl.check_status(sid, r3["job_id"])[1]
                 b3 = status3.get("best_result") or {}
                 status3["_resolved_model"] = ctl.models.resolve(b3.get("model_path"), b3.get("model_id"))
-                outq.put(("ok", status, status2, metrics, extra, status3))
+                # the RF grid row-sharded too (per-level histogram all-reduce, ops/forest_dp.py)
+                b4 = dict(body2, train_params=dict(body2["train_params"], parallelism="data"))
+                st, r4 = ctl.train(sid, b4)
+                ctl.table.wait_finished(r4["job_id"], timeout=300)
+                status4 = ctl.check_status(sid, r4["job_id"])[1]
+                b4 = status4.get("best_result") or {}
+                status4["_resolved_model"] = ctl.models.resolve(b4.get("model_path"), b4.get("model_id"))
+                outq.put(("ok", status, status2, metrics, extra, status3, status4))
             except Exception as e:  # pragma: no cover
                 import traceback
 
@@ -136,6 +143,14 @@ def test_two_rank_gridsearch_gloo():
             assert np.allclose(r["cv_scores"], ref["cv_scores"], atol=0.034), (r, ref)
     assert status3["best_result"]["mean_cv_score"] >= 0.95
     assert status3["_resolved_model"] and os.path.exists(status3["_resolved_model"])
+    # row-sharded forests grow the task-parallel job's trees: identical CV and holdout scores
+    status4 = out[6]
+    assert status4["job_status"] == "completed", status4
+    rf_task = {str(r["parameters"]["max_depth"]): r for r in status2["job_result"]["results"]}
+    for r in status4["job_result"]["results"]:
+        ref = rf_task[str(r["parameters"]["max_depth"])]
+        assert r["cv_scores"] == ref["cv_scores"] and r.get("accuracy") == ref.get("accuracy"), (r, ref)
+    assert status4["_resolved_model"] and os.path.exists(status4["_resolved_model"])
     for model, st in out[4]:
         assert st["job_status"] == "completed", (model, st)
         assert all("cv_scores" in r for r in st["job_result"]["results"]), model
