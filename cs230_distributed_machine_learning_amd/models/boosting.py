@@ -148,8 +148,7 @@ class GradientBoostingFamily(Family):
             raise ParamError("init must be None or 'zero' (custom init estimators are not supported)")
         if p["n_iter_no_change"] is not None:
             warn.append("n_iter_no_change early stopping not supported; all n_estimators stages fitted")
-        if as_float(p["ccp_alpha"], "ccp_alpha", lo=0.0) > 0:
-            warn.append("ccp_alpha pruning not supported; ignored")
+        ccp = as_float(p["ccp_alpha"], "ccp_alpha", lo=0.0)
         if as_float(p["min_weight_fraction_leaf"], "min_weight_fraction_leaf", lo=0.0, hi=0.5) > 0:
             warn.append("min_weight_fraction_leaf not supported; ignored")
         alpha = as_float(p["alpha"], "alpha", lo=0.0, hi=1.0)
@@ -165,6 +164,7 @@ class GradientBoostingFamily(Family):
             "min_impurity_decrease": as_float(p["min_impurity_decrease"], "min_impurity_decrease", lo=0.0),
             "max_features": _max_features(p["max_features"], n_features), "alpha": alpha,
             "init_zero": init == "zero", "seed": seed_of(p["random_state"]), "warnings": warn,
+            "ccp_alpha": ccp,
             "max_leaf_nodes": as_int(p["max_leaf_nodes"] if p["max_leaf_nodes"] != "None" else None, "max_leaf_nodes",
                                      lo=2, allow_none=True) or 0,
         }
@@ -283,10 +283,13 @@ class GradientBoostingFamily(Family):
                     specs[j]["criterion"] = forest_ops.MSE
                     specs[j]["min_impurity_decrease"] = rp["min_impurity_decrease"]
             limit = np.repeat([batch[f].params.get("max_leaf_nodes", 0) for f in act], K)
+            ccp = np.repeat([batch[f].params.get("ccp_alpha", 0.0) for f in act], K)
             if gpu:
                 fb = forest_ops.build_gpu(Xb, None, tgt, roles_t, specs, 1, True, self.tiers, ystride=n)
                 if limit.any():   # sklearn's best-first tree (friedman_mse and squared_error rank splits alike)
                     forest_ops.prune_max_leaves(fb, specs, limit)
+                if ccp.any():     # minimal cost-complexity pruning of each stage tree (variance impurity)
+                    forest_ops.prune_ccp(fb, specs, ccp)
                 _refine(data, fb, Xb, specs, roles_t)
                 leaf = forest_ops.apply(fb, Xb).long()                     # [J, n]
                 vals = fb.vals
@@ -294,6 +297,8 @@ class GradientBoostingFamily(Family):
                 fb = forest_ops.build_cpu(Xb_host, None, tgt.numpy(), roles_t.numpy(), specs, 1, True, ystride=n)
                 if limit.any():
                     forest_ops.prune_max_leaves(fb, specs, limit)
+                if ccp.any():
+                    forest_ops.prune_ccp(fb, specs, ccp)
                 _refine(data, fb, Xb, specs, roles_t)
                 leaf = torch.from_numpy(forest_ops.apply(fb, Xb_host)).long()
                 vals = torch.from_numpy(fb.vals)

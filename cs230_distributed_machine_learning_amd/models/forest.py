@@ -15,8 +15,9 @@ prune_max_leaves), random_state.  Parameters
 with no effect on the fitted function (n_jobs, verbose, warm_start, oob_score) are
 accepted and ignored; class_weight (dict / "balanced" / "balanced_subsample") scales
 the per-class sums inside the builder exactly where sklearn's sample weights would;
-unsupported ones (ccp_alpha > 0, min_weight_fraction_leaf > 0, monotonic_cst) are
-reported in the subtask's ``warnings``.
+ccp_alpha > 0 prunes every grown tree to its minimal cost-complexity subtree
+(ops/forest_ops.py prune_ccp); unsupported ones (min_weight_fraction_leaf > 0,
+monotonic_cst) are reported in the subtask's ``warnings``.
 """
 from __future__ import annotations
 
@@ -137,8 +138,7 @@ class ForestFamily(Family):
                 cw = {str(k): as_float(v, "class_weight value", lo=0.0) for k, v in cw.items()}
             else:
                 raise ParamError("class_weight must be a dict, 'balanced', 'balanced_subsample' or None")
-        if as_float(p["ccp_alpha"], "ccp_alpha", lo=0.0) > 0:
-            warn.append("ccp_alpha pruning not supported; ignored")
+        ccp = as_float(p["ccp_alpha"], "ccp_alpha", lo=0.0)
         mln = as_int(p["max_leaf_nodes"] if p["max_leaf_nodes"] != "None" else None, "max_leaf_nodes", lo=2,
                      allow_none=True)
         if as_float(p["min_weight_fraction_leaf"], "min_weight_fraction_leaf", lo=0.0, hi=0.5) > 0:
@@ -147,7 +147,7 @@ class ForestFamily(Family):
             "n_estimators": n_est, "criterion": crit_id, "max_depth": md if md is not None else forest_ops.INT32_MAX,
             "min_samples_split": mss, "min_samples_leaf": msl, "max_features": k, "bootstrap": int(boot),
             "lambda": lam, "min_impurity_decrease": mid, "seed": seed_of(p["random_state"]), "warnings": warn,
-            "class_weight": cw, "max_leaf_nodes": mln or 0,
+            "class_weight": cw, "max_leaf_nodes": mln or 0, "ccp_alpha": ccp,
         }
 
     def cost(self, model_type, rp, n_train, n_features, n_classes) -> float:
@@ -373,6 +373,10 @@ class ForestFamily(Family):
                 with trace.range("forest_prune"):
                     forest_ops.prune_max_leaves(fb, specs, np.repeat(
                         [t.params.get("max_leaf_nodes", 0) for t in batch], [t.params["n_estimators"] for t in batch]))
+            if any(t.params.get("ccp_alpha", 0.0) > 0 for t in batch):
+                with trace.range("forest_ccp"):   # sklearn prunes after growing (and after best-first)
+                    forest_ops.prune_ccp(fb, specs, np.repeat(
+                        [t.params.get("ccp_alpha", 0.0) for t in batch], [t.params["n_estimators"] for t in batch]))
             with trace.range("forest_refine"):
                 if sharded:
                     from ..ops import forest_dp

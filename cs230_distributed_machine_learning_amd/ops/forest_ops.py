@@ -412,6 +412,68 @@ def prune_max_leaves(fb: ForestBuild, specs: np.ndarray, limit: np.ndarray) -> n
     return leaves.cpu().numpy()   # also keeps specs_dev / heap alive until the kernels are done
 
 
+def prune_ccp(fb: ForestBuild, specs: np.ndarray, alpha: np.ndarray) -> np.ndarray:
+    """Minimal cost-complexity pruning (sklearn ``ccp_alpha``), in place, on the device.
+
+    sklearn prunes the weakest link (smallest effective alpha
+    ``g(t) = (R(t) - R(T_t)) / (|leaves(T_t)| - 1)``) while ``g <= ccp_alpha``, with
+    ``R(t) = W_t / W_root * impurity(t)``.  That sequence ends in the smallest subtree
+    minimising ``R(T) + alpha * |leaves(T)|`` (Breiman et al.), which is one bottom-up
+    pass: a node becomes a leaf when ``R(t) + alpha <= the best cost of its subtree``.
+    The pass runs level by level from the leaves up, vectorised over every tree of the
+    batch (breadth-first levels of the pool, as ``extract_forest`` walks them).
+    ``alpha``: float64 [T] (0 = leave the tree alone).  Returns leaves per tree."""
+    T = len(specs)
+    on_np = not isinstance(fb.nodes, torch.Tensor)
+    nodes = torch.from_numpy(fb.nodes) if on_np else fb.nodes
+    vals = torch.from_numpy(fb.vals) if on_np else fb.vals
+    dev = nodes.device
+    a = torch.from_numpy(np.ascontiguousarray(alpha, dtype=np.float64)).to(dev)
+    crit = torch.from_numpy(np.ascontiguousarray(specs["criterion"], dtype=np.int64)).to(dev)
+    v = vals.double()
+    if fb.is_reg:
+        w = v[:, 0]
+        m = v[:, 1] / w.clamp_min(1e-300)
+        imp = torch.where(w > 0, v[:, 2] / w.clamp_min(1e-300) - m * m, torch.zeros_like(w))
+    else:
+        w = v.sum(1)
+        p = v / w.clamp_min(1e-300).unsqueeze(1)
+        gini = 1.0 - (p * p).sum(1)
+        ent = -(torch.where(p > 0, p * torch.log2(p.clamp_min(1e-300)), torch.zeros_like(p))).sum(1)
+    levels = []
+    fo = torch.arange(T, dtype=torch.int64, device=dev)
+    tr = fo.clone()
+    while fo.numel():
+        levels.append((fo, tr))
+        rec = nodes[fo]
+        internal = rec[:, 0] >= 0
+        l = rec[internal, 1].to(torch.int64)
+        tr = tr[internal].repeat_interleave(2)
+        fo = torch.stack([l, l + 1], 1).reshape(-1)
+    W_root = w[:T]
+    cost = torch.zeros(nodes.shape[0], dtype=torch.float64, device=dev)
+    leaves = torch.zeros(nodes.shape[0], dtype=torch.int64, device=dev)
+    for fo, tr in reversed(levels):
+        if fb.is_reg:
+            im = imp[fo]
+        else:
+            im = torch.where(crit[tr] == ENTROPY, ent[fo], gini[fo])
+        R = w[fo] / W_root[tr] * im
+        leaf_cost = R + a[tr]
+        rec = nodes[fo]
+        internal = rec[:, 0] >= 0
+        l = rec[:, 1].clamp_min(0).to(torch.int64)
+        sub = torch.where(internal, cost[l] + cost[l + 1], leaf_cost)
+        nl = torch.where(internal, leaves[l] + leaves[l + 1], torch.ones_like(l))
+        cut = internal & (a[tr] > 0) & (leaf_cost <= sub)
+        cost[fo] = torch.where(cut | ~internal, leaf_cost, sub)
+        leaves[fo] = torch.where(cut, torch.ones_like(nl), nl)
+        if bool(cut.any()):
+            idx = fo[cut]
+            nodes[idx] = torch.tensor([-1, -1], dtype=nodes.dtype, device=dev)
+    return leaves[:T].cpu().numpy()
+
+
 def refine_thresholds(fb: ForestBuild, Xb, specs: np.ndarray, roles, vals, exact) -> None:
     """Move split bins to sklearn's midpoint thresholds on exactly-binned features (in place)."""
     T = len(specs)
