@@ -360,7 +360,7 @@ class ForestFamily(Family):
             from ..ops import forest_dp
 
             fb = forest_dp.build_dp(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
-                                    data.n_classes, is_reg, data.r0, reduce=data.all_reduce, cw=cw)
+                                    data.n_classes, is_reg, data.r0, reduce=data.all_reduce, cw=cw, comm=data)
         elif data.is_gpu:
             fb = forest_ops.build_gpu(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
                                       data.n_classes, is_reg, self.tiers, reuse_pool=True,

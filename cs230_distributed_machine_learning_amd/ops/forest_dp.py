@@ -7,11 +7,13 @@ of a batch grow level-synchronously on ALL ranks at once:
 1. each rank histograms the open nodes of the level over its own rows
    (``csrc/kernels/forest_dp.hip``: LDS-privatised tiles for large nodes, global atomics
    for small ones; the C++ twin ``csrc/runtime/forest_dp_cpu.cpp`` on CPU);
-2. ONE all-reduce per level-round sums the ``[nodes, positions, channels, 256]`` histogram
-   tensor over the ranks (RCCL over xGMI; gloo on CPU);
-3. every rank evaluates the identical global histograms with the same code
-   (``forest_dp.h``), so every rank holds the same node pool, and partitions only its own
-   (tree, row) pairs, which are re-sorted by node for the next level.
+2. ONE reduce-scatter per level-round sums the ``[nodes, positions, channels, 256]``
+   histogram tensor over the ranks, split by node (RCCL over xGMI; gloo on CPU): each
+   rank owns 1/N of the nodes' global histograms;
+3. each rank evaluates its own nodes with the shared code (``forest_dp.h``) and one
+   all-gather of the 64-B decision records gives every rank every decision, so every rank
+   holds the same node pool; each partitions only its own (tree, row) pairs, which are
+   re-sorted by node for the next level.
 
 The reference has no counterpart: its workers each re-read the whole CSV and fit one
 candidate alone (aws-prod/worker/worker.py:406-425, :315).  Decisions follow the one-GPU
@@ -90,9 +92,16 @@ def _p(t) -> int:
 
 def build_dp(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,
              specs: np.ndarray, n_classes: int, is_reg: bool, r0: int, reduce: Reducer = _no_reduce,
-             cw: Optional[np.ndarray] = None, hist_budget: int = HIST_BUDGET) -> ForestBuild:
+             cw: Optional[np.ndarray] = None, hist_budget: int = HIST_BUDGET, comm=None) -> ForestBuild:
     """Grow the ``specs`` trees over the row shard ``Xb`` (global rows ``r0 ..``);
-    ``reduce`` sums / mins tensors over the ranks.  Every rank returns the same pool."""
+    ``reduce`` sums / mins tensors over the ranks.  Every rank returns the same pool.
+
+    ``comm`` (world > 1; ``RowShard`` provides it): ``reduce_scatter_rows`` /
+    ``all_gather_equal`` / ``rank`` / ``world``.  Each level-round's histograms are then
+    REDUCE-SCATTERED by node: rank k receives the global sums of 1/N of the searching
+    nodes only, evaluates just those, and one all-gather of the (64 B slot + best-left
+    sums) records makes every rank's decisions identical again.  Over a ring that moves
+    half the bytes of an all-reduce, and the split evaluation is divided by N."""
     dev = Xb.device
     L = _Lib(dev)
     t0 = time.perf_counter()
@@ -141,6 +150,8 @@ def build_dp(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torc
     del pair
     P, lvl_lo, lvl_n = T, 0, T
     hist_dtype = torch.float32 if is_reg else torch.int32
+    world = int(getattr(comm, "world", 1)) if comm is not None else 1
+    scatter = world > 1
     lds_feats = LDS_BYTES // (CH * 1024)
 
     while slots.shape[0]:
@@ -168,7 +179,8 @@ def build_dp(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torc
                 sub = srch[c0:c0 + chunk].contiguous()
                 Sc = int(sub.numel())
                 feats = torch.empty((Sc, KR), dtype=torch.int32, device=dev)
-                hist = torch.zeros((Sc, KR, CH, 256), dtype=hist_dtype, device=dev)
+                q = -(-Sc // world)                          # nodes owned per rank (reduce-scatter)
+                hist = torch.zeros((q * world if scatter else Sc, KR, CH, 256), dtype=hist_dtype, device=dev)
                 a.srch, a.S, a.KR, a.feats, a.hist = _p(sub), Sc, KR, _p(feats), _p(hist)
                 L.step(a, 3)
                 th = time.perf_counter()
@@ -195,11 +207,33 @@ def build_dp(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torc
                         torch.cuda.current_stream(dev).synchronize()
                 tr = time.perf_counter()
                 stats["hist_s"] += tr - th
-                with trace.range("forest_dp_allreduce"):
-                    reduce(hist, "sum")
-                stats["reduce_s"] += time.perf_counter() - tr
-                stats["allreduce_bytes"] += hist.numel() * 4
-                L.step(a, 5)
+                if scatter:
+                    # owner-computes: the global sums of this rank's 1/N of the nodes
+                    with trace.range("forest_dp_reduce_scatter"):
+                        own = comm.reduce_scatter_rows(hist)
+                    stats["reduce_s"] += time.perf_counter() - tr
+                    stats["allreduce_bytes"] += hist.numel() * 4 // 2     # ring: half of an all-reduce
+                    lo = min(Sc, comm.rank * q)
+                    hi = min(Sc, lo + q)
+                    own_srch = sub[lo:hi].contiguous()
+                    a.srch, a.S, a.hist, a.feats = _p(own_srch), hi - lo, _p(own), _p(feats[lo:hi])
+                    L.step(a, 5)
+                    idx = own_srch.long()
+                    rec = torch.zeros((q, SLOT_BYTES + 8 * CH), dtype=torch.uint8, device=dev)
+                    rec[:hi - lo, :SLOT_BYTES] = slots[idx]
+                    rec[:hi - lo, SLOT_BYTES:] = best_left[idx].view(torch.uint8)
+                    with trace.range("forest_dp_gather_decisions"):
+                        rec = comm.all_gather_equal(rec)[:Sc]
+                    sl_all = sub.long()
+                    slots[sl_all] = rec[:, :SLOT_BYTES]
+                    best_left[sl_all] = rec[:, SLOT_BYTES:].contiguous().view(torch.float64)
+                    a.srch, a.S, a.hist, a.feats = _p(sub), Sc, _p(hist), _p(feats)
+                else:
+                    with trace.range("forest_dp_allreduce"):
+                        reduce(hist, "sum")
+                    stats["reduce_s"] += time.perf_counter() - tr
+                    stats["allreduce_bytes"] += hist.numel() * 4
+                    L.step(a, 5)
                 stats["rounds"] += 1
                 del feats, hist, tile_s, tile_off, small
         # ---- accept, children, partition ------------------------------------------------

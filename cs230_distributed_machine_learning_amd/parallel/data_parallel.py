@@ -138,6 +138,43 @@ class RowShard(DeviceData):
             torch.distributed.all_reduce(t, op=ro, group=self.group)
         return t
 
+    # reduce-scatter / all-gather over equal row blocks (row-sharded forests: each rank
+    # owns 1/N of a level's node histograms, evaluates them, and shares the decisions)
+    @property
+    def world(self) -> int:
+        return dist.info().world if dist.info().is_dist else 1
+
+    @property
+    def rank(self) -> int:
+        return dist.info().rank if dist.info().is_dist else 0
+
+    def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """Sum over ranks of ``t`` [world * q, ...]; this rank gets rows [rank*q, rank*q+q)."""
+        w = self.world
+        if w == 1:
+            return t
+        q = t.shape[0] // w
+        if dist.info().backend == "nccl":
+            out = torch.empty((q,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            torch.distributed.reduce_scatter_tensor(out, t.contiguous(), group=self.group)
+            return out
+        torch.distributed.all_reduce(t, group=self.group)    # gloo: no reduce-scatter
+        return t[self.rank * q:(self.rank + 1) * q]
+
+    def all_gather_equal(self, t: torch.Tensor) -> torch.Tensor:
+        """Rank-ordered concatenation of every rank's equal-size ``t``."""
+        w = self.world
+        if w == 1:
+            return t
+        t = t.contiguous()
+        if dist.info().backend == "nccl":
+            out = torch.empty((w * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            torch.distributed.all_gather_into_tensor(out, t, group=self.group)
+            return out
+        parts = [torch.empty_like(t) for _ in range(w)]
+        torch.distributed.all_gather(parts, t, group=self.group)
+        return torch.cat(parts)
+
     def _world_bounds(self):
         world = dist.info().world if dist.info().is_dist else 1
         return [shard_bounds(self.n_global, world, k) for k in range(world)] if world > 1 else [(0, self.n_global)]
