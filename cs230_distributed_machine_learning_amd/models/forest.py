@@ -6,8 +6,8 @@ all fits of a job slice are grown together by the HIP builder (ops/forest_ops.py
 csrc/kernels/forest.hip) — or by the C++ builder on CPU — in memory-budgeted batches
 of whole fits, then every fit's held-out rows are predicted in one launch.
 
-Supported: n_estimators, criterion (gini/entropy/log_loss; squared_error; friedman_mse
-and absolute_error/poisson approximate with squared_error), max_depth,
+Supported: n_estimators, criterion (gini/entropy/log_loss; squared_error; friedman_mse, whose splits are
+squared_error's; absolute_error/poisson approximate with squared_error), max_depth,
 min_samples_split, min_samples_leaf (int or fraction), max_features (sqrt/log2/None/
 int/float), bootstrap, max_samples, min_impurity_decrease, max_leaf_nodes (sklearn's
 best-first tree: the grown tree is cut to its best-first top, ops/forest_ops.py
@@ -104,7 +104,15 @@ class ForestFamily(Family):
         else:
             if crit not in ("squared_error", "friedman_mse", "absolute_error", "poisson"):
                 raise ParamError(f"criterion {crit!r} invalid for {model_type}")
-            if crit != "squared_error":
+            # friedman_mse ranks splits exactly like squared_error: its proxy
+            # w_l w_r (m_l - m_r)^2 is W_node x (the squared-error proxy - a node constant),
+            # so the chosen splits are the same; only min_impurity_decrease, which it scales
+            # by the node weight, differs
+            if crit == "friedman_mse":
+                if float(p["min_impurity_decrease"] or 0.0) > 0:
+                    warn.append("criterion='friedman_mse' with min_impurity_decrease > 0: the decrease is "
+                                "tested on the squared_error scale")
+            elif crit != "squared_error":
                 warn.append(f"criterion={crit!r} approximated by squared_error")
             crit_id = forest_ops.MSE
         n_est = as_int(p["n_estimators"], "n_estimators", lo=1, hi=100000)

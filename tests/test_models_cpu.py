@@ -238,3 +238,21 @@ def test_logistic_class_weight_matches_sklearn():
                  {"C": [0.1], "class_weight": ["balanced"], "solver": ["liblinear", "saga"]}):
         np.testing.assert_allclose(_ours("LogisticRegression", X, y, True, grid),
                                    _ref(LogisticRegression(max_iter=3000), X, y, grid), atol=1e-3)
+
+
+def test_rf_friedman_mse_is_squared_error_split_for_split():
+    """friedman_mse's proxy is W_node x (squared-error proxy - const): same trees, no warning."""
+    from sklearn.datasets import make_regression
+
+    X, y = make_regression(400, 6, noise=5, random_state=1)
+    fam = family_of("RandomForestRegressor")
+    outs = []
+    for crit in ("squared_error", "friedman_mse"):
+        dd = DeviceData(X, y, False, "cpu")
+        dd.set_splits(np.ones((1, len(y)), np.uint8), ["full"])
+        rp = fam.resolve("RandomForestRegressor", {"criterion": crit, "n_estimators": 5, "random_state": 3},
+                         len(y), X.shape[1], 1)
+        assert rp["warnings"] == []
+        o = fam.run(dd, [FitTask(0, 0, 0, "RandomForestRegressor", rp)], keep_models=True)[0]
+        outs.append(o.model)
+    assert np.array_equal(outs[0]["nodes"], outs[1]["nodes"])
