@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include "forest_dp.h"
+#include "wave_ops.h"
 
 namespace dml {
 
@@ -209,6 +210,94 @@ __global__ void k_dp_split(DpArgs a) {
   dp_ptr<DpSlot>(a.slots)[slot] = sl;
 }
 
+// classification: one WAVE per searching slot, each lane owning 4 bins.  Integer prefix
+// sums by DPP wave scan (exact, so the same sums as the sequential loop), the same
+// per-bin gain code, and an argmax ordered (gain desc, bin asc) -- the sequential loop's
+// "first strictly-better bin" -- so the decisions equal dp_eval_slot's.
+template <int CHMAX>
+__global__ void __launch_bounds__(kDpBlock) k_dp_split_wave(DpArgs a) {
+  const int s = (int)(((int64_t)blockIdx.x * kDpBlock + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  if (s >= a.S) return;
+  const int slot = dp_ptr<const int32_t>(a.srch)[s];
+  DpSlot sl = dp_ptr<const DpSlot>(a.slots)[slot];
+  const TreeSpec& sp = dp_ptr<const TreeSpec>(a.specs)[sl.tree];
+  const int C = (int)a.C, CH = (int)a.CH, KR = (int)a.KR, d = (int)a.d;
+  const double* cwv = dp_cwv(a, sl.tree);
+  double* bl = dp_ptr<double>(a.best_left) + (int64_t)slot * CH;
+  const uint32_t* h = dp_ptr<const uint32_t>(a.hist) + (int64_t)s * KR * CH * 256;
+  const int32_t* fs = dp_ptr<const int32_t>(a.feats) + (int64_t)s * KR;
+  const uint32_t msl = (uint32_t)sp.min_samples_leaf;
+  for (int k = 0; k < KR && !sl.done; ++k) {
+    const int feat = fs[k];
+    if (feat < 0) {
+      sl.done = 1;
+      break;
+    }
+    sl.pos += 1;
+    uint32_t pre[CHMAX][4], tot[CHMAX];
+#pragma unroll
+    for (int ch = 0; ch < CHMAX; ++ch) {
+      if (ch >= CH) break;
+      const uint4 v = ((const uint4*)(h + ((int64_t)k * CH + ch) * 256))[lane];
+      const uint32_t c0 = v.x, c1 = c0 + v.y, c2 = c1 + v.z, c3 = c2 + v.w;
+      const uint32_t incl = wave::incl_scan<uint32_t>(c3), ex = incl - c3;
+      pre[ch][0] = ex + c0; pre[ch][1] = ex + c1; pre[ch][2] = ex + c2; pre[ch][3] = ex + c3;
+      tot[ch] = wave::bcast<uint32_t>(incl, 63);
+    }
+    double best = -INFINITY;
+    int bb = -1;
+    bool nc = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int b = lane * 4 + i;
+      if (b == 255) break;
+      uint32_t rl = 0, rt = 0;
+#pragma unroll
+      for (int ch = 0; ch < CHMAX; ++ch)
+        if (ch == C) { rl = pre[ch][i]; rt = tot[ch]; }
+      const uint32_t rr = rt - rl;
+      nc |= (rl > 0 && rr > 0);
+      if (rl < msl || rr < msl) continue;
+      ClsAcc L, R;
+      L.init(sp.criterion);
+      R.init(sp.criterion);
+#pragma unroll
+      for (int c = 0; c < CHMAX; ++c) {
+        if (c >= C) break;
+        const double cw = cwv ? cwv[c] : 1.0;
+        const double lc = (double)pre[c][i] * cw, tc = (double)tot[c] * cw;
+        L.add(lc);
+        R.add(tc - lc);
+      }
+      const double g = cls_proxy(L, R, sp.criterion);
+      if (g > best) {
+        best = g;
+        bb = b;
+      }
+    }
+    wave::argmax(best, bb, lane);
+    if (__ballot(nc) != 0ull) {
+      sl.nonconst += 1;
+      if (bb >= 0 && best > sl.best_gain) {
+        sl.best_gain = best;
+        sl.best_feat = feat;
+        sl.best_bin = bb;
+        const int src = bb >> 2, sel = bb & 3;
+#pragma unroll
+        for (int ch = 0; ch < CHMAX; ++ch) {
+          if (ch >= CH) break;
+          const uint32_t mine = sel == 0 ? pre[ch][0] : sel == 1 ? pre[ch][1] : sel == 2 ? pre[ch][2] : pre[ch][3];
+          const uint32_t cv = wave::bcast<uint32_t>(mine, src);
+          if (lane == 0) bl[ch] = (double)cv * ((ch < C && cwv) ? cwv[ch] : 1.0);
+        }
+      }
+    }
+    if (sl.nonconst >= sp.max_features || sl.pos >= d) sl.done = 1;
+  }
+  if (lane == 0) dp_ptr<DpSlot>(a.slots)[slot] = sl;
+}
+
 __global__ void k_dp_accept(DpArgs a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.S_open) return;
@@ -302,7 +391,10 @@ int dml_dp_step(const DpArgs* a, int step, hipStream_t st) {
       break;
     }
     case 5:
-      if (a->S > 0) k_dp_split<<<blocks(a->S, 64), 64, 0, st>>>(*a);
+      if (a->S <= 0) break;
+      if (!a->is_reg && a->CH <= 3) k_dp_split_wave<3><<<blocks(a->S * 64, kDpBlock), kDpBlock, 0, st>>>(*a);
+      else if (!a->is_reg && a->CH <= 9) k_dp_split_wave<9><<<blocks(a->S * 64, kDpBlock), kDpBlock, 0, st>>>(*a);
+      else k_dp_split<<<blocks(a->S, 64), 64, 0, st>>>(*a);   // regression (fp32 bin order) / many classes
       break;
     case 6:
       if (a->S_open > 0) k_dp_accept<<<blocks(a->S_open, 64), 64, 0, st>>>(*a);

@@ -30,6 +30,7 @@ task-parallel path stays the fast one when every rank can hold the table.
 from __future__ import annotations
 
 import ctypes
+import os
 import time
 from typing import Callable, Optional
 
@@ -153,6 +154,7 @@ def build_dp(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torc
     world = int(getattr(comm, "world", 1)) if comm is not None else 1
     scatter = world > 1
     lds_feats = LDS_BYTES // (CH * 1024)
+    timing = os.environ.get("DML_DP_TIMING") == "1"
 
     while slots.shape[0]:
         S_open = int(slots.shape[0])
@@ -203,7 +205,7 @@ def build_dp(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torc
                 a.small_s, a.n_small, a.lds_feats = _p(small), int(small.numel()), max(1, min(lds_feats, KR))
                 with trace.range("forest_dp_hist"):
                     L.step(a, 4)
-                    if L.gpu:
+                    if L.gpu and timing:   # per-phase timing only: the collective orders itself
                         torch.cuda.current_stream(dev).synchronize()
                 tr = time.perf_counter()
                 stats["hist_s"] += tr - th
