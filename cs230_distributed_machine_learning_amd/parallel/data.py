@@ -3,9 +3,9 @@
 Reference: every worker re-reads the full CSV from NFS/EFS for every task
 (aws-prod/worker/worker.py:406-425; SURVEY §2.5 "the dominant data movement").  Here:
 
-* ``broadcast_table`` — rank 0 parses the file once; its rows go host -> pinned ->
-  HBM -> every rank in 256 MB chunks with the memcpy, the H2D copy and the RCCL
-  broadcast of consecutive chunks overlapped (``_pipelined_broadcast``); the table then
+* ``broadcast_table`` — rank 0 parses the file once; its rows go host -> HBM -> every
+  rank in 256 MB chunks, the H2D copy of chunk k overlapping the RCCL broadcast of chunk
+  k-1 (``_pipelined_broadcast``); the table then
   stays resident across every candidate and job (``DeviceCache``).
 * ``allgather_table`` — each rank holds a contiguous row shard (e.g. generated on the
   device, data/synthetic.py) and one ``all_gather_into_tensor`` assembles the table.
@@ -65,14 +65,14 @@ BCAST_CHUNK_BYTES = 256 << 20
 
 
 def _pipelined_broadcast(X: Optional[np.ndarray], Xd: torch.Tensor, chunk_bytes: Optional[int] = None) -> None:
-    """Root's host rows -> every rank's ``Xd``, in row chunks, three stages overlapped.
+    """Root's host rows -> every rank's ``Xd``, in row chunks, H2D and broadcast overlapped.
 
-    One ``Tensor.to(device)`` of a pageable 40 GB table is a single host-staged copy, and
-    only then does the broadcast start.  Here, for chunk k, rank 0 memcpy's the rows into
-    one of two pinned buffers while chunk k-1 is copied H2D on a side stream and chunk k-2
-    is broadcast by RCCL over xGMI.  Each stage waits only on events; the host never waits
-    on the collective.  The other ranks post one broadcast per chunk straight into their
-    slice of ``Xd``."""
+    Rank 0 copies chunk k host -> HBM on a side stream (the pageable copy path runs at
+    ~55 GB/s on MI355X, measured: profiles/r2_bcast_bench.log; staging through our own
+    pinned buffers was slower, 25 GB/s, bound by the host memcpy) while RCCL broadcasts
+    chunk k-1 over xGMI; the broadcast of a chunk waits only on that chunk's copy event.
+    A single ``.to(device)`` followed by one broadcast would serialise the two.  The other
+    ranks post one broadcast per chunk straight into their slice of ``Xd``."""
     n, d = Xd.shape
     if n == 0 or d == 0:
         return
@@ -80,29 +80,21 @@ def _pipelined_broadcast(X: Optional[np.ndarray], Xd: torch.Tensor, chunk_bytes:
     root = dist.info().rank == 0
     gpu = Xd.is_cuda
     if root and gpu:
-        pins = [torch.empty((min(rows, n), d), dtype=torch.float32, pin_memory=True) for _ in range(2)]
         copy_stream = torch.cuda.Stream(Xd.device)
         compute = torch.cuda.current_stream(Xd.device)
-        done = [None, None]
-    for i, r0 in enumerate(range(0, n, rows)):
+    for r0 in range(0, n, rows):
         r1 = min(n, r0 + rows)
         if root:
-            src = np.ascontiguousarray(X[r0:r1], dtype=np.float32)
+            src = torch.from_numpy(np.ascontiguousarray(X[r0:r1], dtype=np.float32))
             if gpu:
-                b = i % 2
-                if done[b] is not None:
-                    done[b].synchronize()          # the H2D that last read pinned buffer b is done
-                np.copyto(pins[b][:r1 - r0].numpy(), src)
                 with torch.cuda.stream(copy_stream):
-                    Xd[r0:r1].copy_(pins[b][:r1 - r0], non_blocking=True)
-                    done[b] = torch.cuda.Event()
-                    done[b].record(copy_stream)
-                compute.wait_event(done[b])        # the broadcast of this chunk follows its copy
+                    Xd[r0:r1].copy_(src)
+                    ev = torch.cuda.Event()
+                    ev.record(copy_stream)
+                compute.wait_event(ev)             # this chunk's broadcast follows its copy only
             else:
-                Xd[r0:r1].copy_(torch.from_numpy(src))
+                Xd[r0:r1].copy_(src)
         dist.broadcast(Xd[r0:r1], 0)
-    if root and gpu:
-        torch.cuda.current_stream(Xd.device).synchronize()   # pinned buffers are freed after this
 
 
 def broadcast_binned(X: Optional[np.ndarray], y: Optional[np.ndarray], classification: bool, device: torch.device,

@@ -1,5 +1,5 @@
-"""Root-table distribution: one pageable ``.to(device)`` + broadcast vs the pipelined
-pinned-chunk broadcast (parallel/data.py ``_pipelined_broadcast``), on an RCCL group.
+"""Root-table distribution: one pageable ``.to(device)`` + broadcast vs the chunked,
+copy/broadcast-overlapped path (parallel/data.py ``_pipelined_broadcast``), on an RCCL group.
 
     python scripts/bcast_bench.py [GB]
 
