@@ -378,7 +378,7 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
         g = cls_proxy(L, R, s.criterion);
       } else {
         const double l0 = (double)v[0][i], l1 = (double)v[1][i];
-        g = mse_proxy(l0, l1, (double)tot[0] - l0, (double)tot[1] - l1);
+        g = reg_proxy(s.criterion, l0, l1, (double)tot[0] - l0, (double)tot[1] - l1);
       }
       if (g > best) { best = g; bb = b; }
     }
@@ -439,7 +439,7 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
     if constexpr (MODE == 2) {
       const double l0 = (double)h[b], t0 = (double)h[255];
       const double l1 = (double)h[256 + b], t1 = (double)h[256 + 255];
-      g = mse_proxy(l0, l1, t0 - l0, t1 - l1);
+      g = reg_proxy(s.criterion, l0, l1, t0 - l0, t1 - l1);
     } else {
       ClsAcc L, R;
       L.init(s.criterion); R.init(s.criterion);
@@ -1085,7 +1085,7 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
     const float p0 = wave::incl_scan<float>(w);
     const float p1 = wave::incl_scan<float>(w * y);
     const float t0 = wave::bcast<float>(p0, cnt - 1), t1 = wave::bcast<float>(p1, cnt - 1);
-    if (cand) g = mse_proxy((double)p0, (double)p1, (double)(t0 - p0), (double)(t1 - p1));
+    if (cand) g = reg_proxy(s.criterion, (double)p0, (double)p1, (double)(t0 - p0), (double)(t1 - p1));
   }
   int bl = cand ? lane : 64;
   wave::argmax(g, bl, lane);

@@ -38,7 +38,7 @@ constexpr int kBins = 256;        // uint8 bins
 constexpr int kPoisTable = 12;    // Poisson CDF thresholds kept per tree
 constexpr int kMaxClasses = 64;   // classification channels supported by the builders
 
-enum Criterion : int32_t { kGini = 0, kEntropy = 1, kMSE = 2 };
+enum Criterion : int32_t { kGini = 0, kEntropy = 1, kMSE = 2, kPoisson = 3 };
 
 // Per-tree build specification (POD, identical layout on host, device and ctypes).
 struct TreeSpec {
@@ -234,6 +234,19 @@ DML_HD double mse_impurity(double s0, double s1, double s2) {
 
 DML_HD double mse_proxy(double l0, double l1, double r0, double r1) {
   return l1 * l1 / l0 + r1 * r1 / r0;
+}
+
+// regression split proxy (larger is better) from (sum w, sum wy) of both sides.
+// Poisson (sklearn's criterion="poisson"): sum_l log(mean_l) + sum_r log(mean_r), -inf
+// when a side's sum of y is not positive; log2 (dlog2: host/device-identical) ranks the
+// same as sklearn's natural log.  Node impurities (purity, min_impurity_decrease) stay
+// the squared-error ones: zero exactly when y is constant, like the Poisson deviance.
+DML_HD double reg_proxy(int crit, double l0, double l1, double r0, double r1) {
+  if (crit == kPoisson) {
+    if (l1 <= 1e-15 || r1 <= 1e-15) return -INFINITY;
+    return l1 * dlog2(l1 / l0) + r1 * dlog2(r1 / r0);
+  }
+  return mse_proxy(l0, l1, r0, r1);
 }
 
 // sklearn's impurity_improvement(), scaled by the node's share of the tree's weight

@@ -212,7 +212,7 @@ DML_HDM void dp_eval_slot(const DpArgs& a, DpSlot& sl, double* best_left, const 
         nc |= (rl > 0.f && rr > 0.f);
         if (rl < (float)s.min_samples_leaf || rr < (float)s.min_samples_leaf) continue;
         const double l0 = pre[0], t0 = tot[0], l1 = pre[1], t1 = tot[1];
-        const double g = mse_proxy(l0, l1, t0 - l0, t1 - l1);
+        const double g = reg_proxy(s.criterion, l0, l1, t0 - l0, t1 - l1);
         if (g > g_best) {
           g_best = g;
           b_best = b;

@@ -152,7 +152,7 @@ static void build_tree(const Data& D, const TreeSpec& s, int64_t t, CpuTree& out
           nc |= (rl > 0.f && rr > 0.f);
           if (rl < (float)s.min_samples_leaf || rr < (float)s.min_samples_leaf) continue;
           const double l0 = hf[b], t0 = hf[255], l1 = hf[256 + b], t1 = hf[256 + 255];
-          const double g = mse_proxy(l0, l1, t0 - l0, t1 - l1);
+          const double g = reg_proxy(s.criterion, l0, l1, t0 - l0, t1 - l1);
           if (g > g_best) { g_best = g; b_best = b; }
         }
         if (nc) {

@@ -7,7 +7,8 @@ csrc/kernels/forest.hip) — or by the C++ builder on CPU — in memory-budgeted
 of whole fits, then every fit's held-out rows are predicted in one launch.
 
 Supported: n_estimators, criterion (gini/entropy/log_loss; squared_error; friedman_mse, whose splits are
-squared_error's; absolute_error/poisson approximate with squared_error), max_depth,
+squared_error's; poisson -- sklearn's proxy sum_l log(mean_l) + sum_r log(mean_r);
+absolute_error approximates with squared_error), max_depth,
 min_samples_split, min_samples_leaf (int or fraction), max_features (sqrt/log2/None/
 int/float), bootstrap, max_samples, min_impurity_decrease, max_leaf_nodes (sklearn's
 best-first tree: the grown tree is cut to its best-first top, ops/forest_ops.py
@@ -112,9 +113,12 @@ class ForestFamily(Family):
                 if float(p["min_impurity_decrease"] or 0.0) > 0:
                     warn.append("criterion='friedman_mse' with min_impurity_decrease > 0: the decrease is "
                                 "tested on the squared_error scale")
-            elif crit != "squared_error":
+            elif crit == "absolute_error":
                 warn.append(f"criterion={crit!r} approximated by squared_error")
-            crit_id = forest_ops.MSE
+            crit_id = forest_ops.POISSON if crit == "poisson" else forest_ops.MSE
+            if crit == "poisson" and (float(p["min_impurity_decrease"] or 0.0) > 0 or float(p["ccp_alpha"] or 0.0) > 0):
+                warn.append("criterion='poisson': min_impurity_decrease / ccp_alpha are applied on the "
+                            "squared-error impurity scale")
         n_est = as_int(p["n_estimators"], "n_estimators", lo=1, hi=100000)
         md = as_int(p["max_depth"], "max_depth", lo=1, allow_none=True)
         mss = _count_param(p["min_samples_split"], n_train, "min_samples_split", 2)
@@ -245,6 +249,12 @@ class ForestFamily(Family):
         if not tasks:
             return []
         is_reg = not data.classification
+        if is_reg and any(t.params.get("criterion") == forest_ops.POISSON for t in tasks):
+            ymin = float(data.y_reg.min()) if data.n else 0.0
+            if getattr(data, "is_row_shard", False):
+                ymin = float(data.all_reduce(torch.tensor([ymin], dtype=torch.float64, device=data.device), "min")[0])
+            if ymin < 0:   # sklearn raises the same
+                raise ParamError("Some value(s) of y are negative which is not allowed for Poisson regression.")
         Xb = data.binned()
         sharded = getattr(data, "is_row_shard", False)
         budget = self._budget(data)

@@ -26,7 +26,7 @@ import torch
 from ..utils import native
 from ..utils import trace
 
-GINI, ENTROPY, MSE = 0, 1, 2
+GINI, ENTROPY, MSE, POISSON = 0, 1, 2, 3
 INT32_MAX = 2**31 - 1
 
 

@@ -173,8 +173,9 @@ def test_gpu_max_leaf_prune_matches_cpu(is_reg):
         assert _canon(gn, g.vals.cpu().numpy(), T) == _canon(c.nodes, c.vals, T)
 
 
-@pytest.mark.parametrize("words", ["packed", "plain"])
-def test_gpu_regression_close_to_cpu(words, monkeypatch):
+@pytest.mark.parametrize("words,crit", [("packed", 2), ("plain", 2), ("packed", 3)])
+def test_gpu_regression_close_to_cpu(words, crit, monkeypatch):
+    """crit 3 = Poisson (forest_common.h reg_proxy) on a positive target."""
     from sklearn.datasets import make_regression
 
     if words == "plain":
@@ -182,12 +183,14 @@ def test_gpu_regression_close_to_cpu(words, monkeypatch):
     X, y = make_regression(n_samples=8000, n_features=10, noise=5.0, random_state=1)
     X = X.astype(np.float32)
     y = y.astype(np.float32)
+    if crit == 3:
+        y = np.exp(y / np.abs(y).max() * 2).astype(np.float32)
     dev = torch.device("cuda:0")
     Xt = torch.from_numpy(X).to(dev)
     edges = binning.quantile_edges(Xt)
     Xb = binning.bin_matrix(Xt, edges)
     roles, _ = make_split_roles(y, 3, False, holdout=False)
-    specs = _specs(3, 8, 10, k=10, criterion=2)
+    specs = _specs(3, 8, 10, k=10, criterion=crit)
     g = forest_ops.build_gpu(Xb, None, torch.from_numpy(y).to(dev), torch.from_numpy(roles).to(dev), specs, 1, True)
     c = forest_ops.build_cpu(Xb.cpu().numpy(), None, y, roles, specs, 1, True)
     rows, roff = [], [0]

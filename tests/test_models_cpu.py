@@ -256,3 +256,40 @@ def test_rf_friedman_mse_is_squared_error_split_for_split():
         o = fam.run(dd, [FitTask(0, 0, 0, "RandomForestRegressor", rp)], keep_models=True)[0]
         outs.append(o.model)
     assert np.array_equal(outs[0]["nodes"], outs[1]["nodes"])
+
+
+def test_rf_poisson_criterion_matches_sklearn():
+    """criterion='poisson': sklearn's proxy (sum_l log mean_l + sum_r log mean_r); on
+    exactly binned columns, no bootstrap and every feature, the tree is sklearn's."""
+    from sklearn.ensemble import RandomForestRegressor
+
+    from cs230_distributed_machine_learning_amd.engine.service import refit_model
+
+    rng = np.random.default_rng(2)
+    X = rng.integers(0, 8, size=(500, 4)).astype(np.float32)
+    y = rng.poisson(np.exp(0.3 * X[:, 0] - 0.2 * X[:, 1])).astype(np.float64)
+    # equal-gain ties between features go by the visiting order (sklearn's RNG vs our keyed
+    # order: squared_error trees differ from sklearn's on some seeds for the same reason);
+    # these seeds have no such tie
+    for seed in (1, 2):
+        params = {"n_estimators": 1, "bootstrap": False, "max_features": None, "criterion": "poisson",
+                  "min_samples_leaf": 5, "random_state": seed}
+        m = refit_model({"model_type": "RandomForestRegressor", "scoring": None}, params, DeviceData(X, y, False))
+        sk = RandomForestRegressor(**params).fit(X, y).estimators_[0].tree_
+        nodes, vals = np.asarray(m["nodes"]), np.asarray(m["vals"])
+        leaves = nodes[:, 0] < 0
+        ours = np.sort(vals[leaves, 1] / vals[leaves, 0])
+        ref = np.sort(sk.value[sk.children_left == -1][:, 0, 0])
+        assert len(ours) == len(ref)
+        np.testing.assert_allclose(ours, ref, rtol=1e-9)
+    # ...and it is a different tree from squared_error's
+    m2 = refit_model({"model_type": "RandomForestRegressor", "scoring": None}, dict(params, criterion="squared_error"),
+                     DeviceData(X, y, False))
+    assert not np.array_equal(np.asarray(m2["nodes"]), nodes)
+    # negative targets are refused like sklearn
+    fam = family_of("RandomForestRegressor")
+    rp = fam.resolve("RandomForestRegressor", params, 500, 4, 1)
+    dd = DeviceData(X, y - 3.0, False, "cpu")
+    dd.set_splits(np.ones((1, len(y)), np.uint8), ["full"])
+    with pytest.raises(Exception, match="negative"):
+        fam.run(dd, [FitTask(0, 0, 0, "RandomForestRegressor", rp)])
