@@ -232,6 +232,7 @@ __device__ void enqueue_or_leaf(const Ctx& c, int tree, int node, int64_t start,
                                 uint64_t key, int set) {
   const TreeSpec& s = c.specs[tree];
   if (leaf_by_counts(s, count, depth)) return;
+  if (leaf_by_weight(s, node_weight(c, node))) return;
   if (node_impurity(c, node, s.criterion) <= kEps) return;
   const int tier = count <= c.sub_max ? 0 : (count <= c.wave_max ? 1 : (count <= c.block_max ? 2 : 3));
   const int idx = atomicAdd(&c.counters[set * kTiers + tier], 1);
@@ -375,9 +376,11 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
         L.init(s.criterion); R.init(s.criterion);
         L.add(l0); L.add(l1);
         R.add(t0 - l0); R.add(t1 - l1);
+        if (side_too_light(s, L.w, R.w)) continue;
         g = cls_proxy(L, R, s.criterion);
       } else {
         const double l0 = (double)v[0][i], l1 = (double)v[1][i];
+        if (side_too_light(s, l0, (double)tot[0] - l0)) continue;
         g = reg_proxy(s.criterion, l0, l1, (double)tot[0] - l0, (double)tot[1] - l1);
       }
       if (g > best) { best = g; bb = b; }
@@ -439,6 +442,7 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
     if constexpr (MODE == 2) {
       const double l0 = (double)h[b], t0 = (double)h[255];
       const double l1 = (double)h[256 + b], t1 = (double)h[256 + 255];
+      if (side_too_light(s, l0, t0 - l0)) continue;
       g = reg_proxy(s.criterion, l0, l1, t0 - l0, t1 - l1);
     } else {
       ClsAcc L, R;
@@ -449,6 +453,7 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
         L.add(lc);
         R.add(tc - lc);
       }
+      if (side_too_light(s, L.w, R.w)) continue;
       g = cls_proxy(L, R, s.criterion);
     }
     if (g > best) { best = g; bb = b; }
@@ -603,6 +608,7 @@ __device__ double impurity_of_vals(const Ctx& c, const double* v, int crit) {
 __device__ void enqueue_or_leaf_v(const Ctx& c, const TreeSpec& s, int tree, int node, int64_t start, int count,
                                   int depth, uint64_t key, int set, const double* vals) {
   if (leaf_by_counts(s, count, depth)) return;
+  if (leaf_by_weight(s, vals_weight(vals, c.C, c.is_reg))) return;
   if (impurity_of_vals(c, vals, s.criterion) <= kEps) return;
   const int tier = count <= c.sub_max ? 0 : (count <= c.wave_max ? 1 : (count <= c.block_max ? 2 : 3));
   const int idx = atomicAdd(&c.counters[set * kTiers + tier], 1);
@@ -1077,7 +1083,7 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
       L.add(lw);
       R.add(tw - lw);
     }
-    if (cand) g = cls_proxy(L, R, s.criterion);
+    if (cand && !side_too_light(s, L.w, R.w)) g = cls_proxy(L, R, s.criterion);
   } else {
     const float wsh = __shfl(my_w, src);
     const float y = __shfl(my_y, src);
@@ -1085,7 +1091,8 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
     const float p0 = wave::incl_scan<float>(w);
     const float p1 = wave::incl_scan<float>(w * y);
     const float t0 = wave::bcast<float>(p0, cnt - 1), t1 = wave::bcast<float>(p1, cnt - 1);
-    if (cand) g = reg_proxy(s.criterion, (double)p0, (double)p1, (double)(t0 - p0), (double)(t1 - p1));
+    if (cand && !side_too_light(s, (double)p0, (double)(t0 - p0)))
+      g = reg_proxy(s.criterion, (double)p0, (double)p1, (double)(t0 - p0), (double)(t1 - p1));
   }
   int bl = cand ? lane : 64;
   wave::argmax(g, bl, lane);
@@ -1345,8 +1352,10 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     // The popped entry's slot `sp` is reused: compute both children's sums before writing.
     if (lane == 0) {
       const int dep = e.depth + 1;
-      const bool push_r = !leaf_by_counts(s, nr, dep) && impurity_of_vals(c, right_ch, s.criterion) > kEps;
-      const bool push_l = !leaf_by_counts(s, nl, dep) && impurity_of_vals(c, left_ch, s.criterion) > kEps;
+      const bool push_r = !leaf_by_counts(s, nr, dep) && !leaf_by_weight(s, vals_weight(right_ch, c.C, c.is_reg)) &&
+                          impurity_of_vals(c, right_ch, s.criterion) > kEps;
+      const bool push_l = !leaf_by_counts(s, nl, dep) && !leaf_by_weight(s, vals_weight(left_ch, c.C, c.is_reg)) &&
+                          impurity_of_vals(c, left_ch, s.criterion) > kEps;
       if (push_r) {
         SubEntry r; r.mask = rm; r.key = child_key(e.key, 1); r.node = base + 1; r.depth = dep;
         for (int q = 0; q < VC; ++q) sstats[sp * VC + q] = right_ch[q];
@@ -1727,6 +1736,10 @@ __global__ void k_roots(Ctx c) {
     for (int k = 0; k < c.C; ++k) v[k] *= row[k];
   }
   c.tree_W[t] = node_weight(c, t);
+  {   // min_weight_fraction_leaf -> absolute weight, read by every later kernel of the build
+    TreeSpec& sm = const_cast<TreeSpec&>(c.specs[t]);
+    sm.min_weight_leaf = sm.min_weight_frac * c.tree_W[t];
+  }
   const int cnt = c.active_count[t];
   if (cnt == 0) return;
   enqueue_or_leaf(c, t, t, c.row_off[t], cnt, 0, root_key(c.specs[t].seed), 0);

@@ -57,6 +57,8 @@ struct TreeSpec {
   int32_t cw_mode;          // class weights: 0 none, 1 fixed row of the cw table (dict / "balanced"),
                             // 2 "balanced_subsample" (row computed from this tree's bootstrap counts)
   int32_t reserved;
+  double min_weight_frac;   // sklearn min_weight_fraction_leaf
+  double min_weight_leaf;   // = min_weight_frac x the tree's total weight; set by each builder at the root
 };
 
 // sklearn class_weight="balanced_subsample" for one tree from its root class counts
@@ -260,6 +262,25 @@ constexpr double kEps = 1e-7;  // sklearn EPSILON for purity / min_impurity_decr
 // leaf-by-counts rule (before any split search)
 DML_HD bool leaf_by_counts(const TreeSpec& t, int count, int depth) {
   return depth >= t.max_depth || count < t.min_samples_split || count < 2 * t.min_samples_leaf;
+}
+
+// min_weight_fraction_leaf (sklearn): a node lighter than 2 x min_weight_leaf is a leaf,
+// and a split leaving either side lighter than min_weight_leaf is not a candidate.
+// Weights include bootstrap counts and class weights (sklearn's sample weights).
+DML_HD bool leaf_by_weight(const TreeSpec& t, double w_node) {
+  return t.min_weight_leaf > 0.0 && w_node < 2.0 * t.min_weight_leaf;
+}
+
+DML_HD bool side_too_light(const TreeSpec& t, double wl, double wr) {
+  return t.min_weight_leaf > 0.0 && (wl < t.min_weight_leaf || wr < t.min_weight_leaf);
+}
+
+// total weight of a node value vector (class sums | (sum w, sum wy, sum wy^2))
+DML_HD double vals_weight(const double* v, int C, int is_reg) {
+  if (is_reg) return v[0];
+  double w = 0.0;
+  for (int k = 0; k < C; ++k) w += v[k];
+  return w;
 }
 
 // ---- max_leaf_nodes: best-first selection on a grown tree ---------------------------

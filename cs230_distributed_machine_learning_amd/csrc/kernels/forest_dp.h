@@ -93,7 +93,8 @@ DML_HD double dp_impurity(const double* v, int C, int is_reg, int crit) {
 
 // the builders' "grow this node?" rule (forest_cpu.cpp visit())
 DML_HD bool dp_visit(const TreeSpec& t, double count, int depth, const double* v, int C, int is_reg) {
-  return !(leaf_by_counts(t, (int)count, depth) || dp_impurity(v, C, is_reg, t.criterion) <= kEps);
+  return !(leaf_by_counts(t, (int)count, depth) || leaf_by_weight(t, vals_weight(v, C, is_reg)) ||
+           dp_impurity(v, C, is_reg, t.criterion) <= kEps);
 }
 
 // Root of tree ``t`` from its all-reduced statistics: class weights (balanced_subsample
@@ -120,6 +121,7 @@ DML_HD int dp_root_one(const DpArgs& a, int t, DpSlot* slot) {
     }
   }
   dp_ptr<double>(a.tree_W)[t] = W;
+  dp_ptr<TreeSpec>(a.specs)[t].min_weight_leaf = s.min_weight_frac * W;   // read by every later step
   const double count = st[CH - 1];
   slot->key = root_key(s.seed);
   slot->best_gain = -INFINITY;
@@ -181,6 +183,7 @@ DML_HDM void dp_eval_slot(const DpArgs& a, DpSlot& sl, double* best_left, const 
           L.add(lc);
           R.add(tc - lc);
         }
+        if (side_too_light(s, L.w, R.w)) continue;
         const double g = cls_proxy(L, R, s.criterion);
         if (g > g_best) {
           g_best = g;
@@ -212,6 +215,7 @@ DML_HDM void dp_eval_slot(const DpArgs& a, DpSlot& sl, double* best_left, const 
         nc |= (rl > 0.f && rr > 0.f);
         if (rl < (float)s.min_samples_leaf || rr < (float)s.min_samples_leaf) continue;
         const double l0 = pre[0], t0 = tot[0], l1 = pre[1], t1 = tot[1];
+        if (side_too_light(s, l0, t0 - l0)) continue;
         const double g = reg_proxy(s.criterion, l0, l1, t0 - l0, t1 - l1);
         if (g > g_best) {
           g_best = g;

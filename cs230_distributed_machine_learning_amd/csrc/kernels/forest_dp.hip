@@ -270,6 +270,7 @@ __global__ void __launch_bounds__(kDpBlock) k_dp_split_wave(DpArgs a) {
         L.add(lc);
         R.add(tc - lc);
       }
+      if (side_too_light(sp, L.w, R.w)) continue;
       const double g = cls_proxy(L, R, sp.criterion);
       if (g > best) {
         best = g;

@@ -39,7 +39,8 @@ struct Data {
 
 struct Job { int node, start, count, depth; uint64_t key; };
 
-static void build_tree(const Data& D, const TreeSpec& s, int64_t t, CpuTree& out) {
+static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& out) {
+  TreeSpec s = s_in;   // min_weight_leaf is set once the tree's total weight is known
   const uint8_t* role = D.roles + (int64_t)s.split * D.n;
   const float* Y = D.ystride ? D.yreg + (int64_t)s.target * D.ystride : D.yreg;
   std::vector<uint32_t> rows, tmp;
@@ -76,6 +77,7 @@ static void build_tree(const Data& D, const TreeSpec& s, int64_t t, CpuTree& out
   double Wt = 0.0;
   if (D.is_reg) Wt = root[0];
   else for (int k = 0; k < D.C; ++k) Wt += root[k];
+  s.min_weight_leaf = s.min_weight_frac * Wt;
 
   auto impurity_of = [&](const double* v) {
     if (D.is_reg) return mse_impurity(v[0], v[1], v[2]);
@@ -84,7 +86,8 @@ static void build_tree(const Data& D, const TreeSpec& s, int64_t t, CpuTree& out
     return cls_impurity(a, s.criterion);
   };
   auto visit = [&](int count, int depth, const double* v) {
-    return !(leaf_by_counts(s, count, depth) || impurity_of(v) <= kEps);
+    return !(leaf_by_counts(s, count, depth) || leaf_by_weight(s, vals_weight(v, D.C, D.is_reg)) ||
+             impurity_of(v) <= kEps);
   };
 
   std::vector<Job> stack;
@@ -126,6 +129,7 @@ static void build_tree(const Data& D, const TreeSpec& s, int64_t t, CpuTree& out
             const double lc = (double)hu[k * 256 + b] * cwv[k], tc = (double)hu[k * 256 + 255] * cwv[k];
             L.add(lc); R.add(tc - lc);
           }
+          if (side_too_light(s, L.w, R.w)) continue;
           const double g = cls_proxy(L, R, s.criterion);
           if (g > g_best) { g_best = g; b_best = b; }
         }
@@ -152,6 +156,7 @@ static void build_tree(const Data& D, const TreeSpec& s, int64_t t, CpuTree& out
           nc |= (rl > 0.f && rr > 0.f);
           if (rl < (float)s.min_samples_leaf || rr < (float)s.min_samples_leaf) continue;
           const double l0 = hf[b], t0 = hf[255], l1 = hf[256 + b], t1 = hf[256 + 255];
+          if (side_too_light(s, l0, t0 - l0)) continue;
           const double g = reg_proxy(s.criterion, l0, l1, t0 - l0, t1 - l1);
           if (g > g_best) { g_best = g; b_best = b; }
         }

@@ -149,8 +149,7 @@ class GradientBoostingFamily(Family):
         if p["n_iter_no_change"] is not None:
             warn.append("n_iter_no_change early stopping not supported; all n_estimators stages fitted")
         ccp = as_float(p["ccp_alpha"], "ccp_alpha", lo=0.0)
-        if as_float(p["min_weight_fraction_leaf"], "min_weight_fraction_leaf", lo=0.0, hi=0.5) > 0:
-            warn.append("min_weight_fraction_leaf not supported; ignored")
+        mwf = as_float(p["min_weight_fraction_leaf"], "min_weight_fraction_leaf", lo=0.0, hi=0.5)
         alpha = as_float(p["alpha"], "alpha", lo=0.0, hi=1.0)
         if loss in (LOSS_HUBER, LOSS_QUANT) and not 0.0 < alpha < 1.0:
             raise ParamError("alpha must be in (0, 1)")
@@ -164,7 +163,7 @@ class GradientBoostingFamily(Family):
             "min_impurity_decrease": as_float(p["min_impurity_decrease"], "min_impurity_decrease", lo=0.0),
             "max_features": _max_features(p["max_features"], n_features), "alpha": alpha,
             "init_zero": init == "zero", "seed": seed_of(p["random_state"]), "warnings": warn,
-            "ccp_alpha": ccp,
+            "ccp_alpha": ccp, "min_weight_fraction_leaf": mwf,
             "max_leaf_nodes": as_int(p["max_leaf_nodes"] if p["max_leaf_nodes"] != "None" else None, "max_leaf_nodes",
                                      lo=2, allow_none=True) or 0,
         }
@@ -282,6 +281,7 @@ class GradientBoostingFamily(Family):
                     specs[j]["bootstrap"] = 0
                     specs[j]["criterion"] = forest_ops.MSE
                     specs[j]["min_impurity_decrease"] = rp["min_impurity_decrease"]
+                    specs[j]["min_weight_frac"] = rp.get("min_weight_fraction_leaf", 0.0)
             limit = np.repeat([batch[f].params.get("max_leaf_nodes", 0) for f in act], K)
             ccp = np.repeat([batch[f].params.get("ccp_alpha", 0.0) for f in act], K)
             if gpu:

@@ -17,8 +17,9 @@ with no effect on the fitted function (n_jobs, verbose, warm_start, oob_score) a
 accepted and ignored; class_weight (dict / "balanced" / "balanced_subsample") scales
 the per-class sums inside the builder exactly where sklearn's sample weights would;
 ccp_alpha > 0 prunes every grown tree to its minimal cost-complexity subtree
-(ops/forest_ops.py prune_ccp); unsupported ones (min_weight_fraction_leaf > 0,
-monotonic_cst) are reported in the subtask's ``warnings``.
+(ops/forest_ops.py prune_ccp); min_weight_fraction_leaf bounds every side's weight
+(bootstrap counts x class weights, as sklearn's sample weights) inside the builders;
+monotonic_cst is unsupported and reported in the subtask's ``warnings``.
 """
 from __future__ import annotations
 
@@ -153,13 +154,14 @@ class ForestFamily(Family):
         ccp = as_float(p["ccp_alpha"], "ccp_alpha", lo=0.0)
         mln = as_int(p["max_leaf_nodes"] if p["max_leaf_nodes"] != "None" else None, "max_leaf_nodes", lo=2,
                      allow_none=True)
-        if as_float(p["min_weight_fraction_leaf"], "min_weight_fraction_leaf", lo=0.0, hi=0.5) > 0:
-            warn.append("min_weight_fraction_leaf not supported; ignored")
+        mwf = as_float(p["min_weight_fraction_leaf"], "min_weight_fraction_leaf", lo=0.0, hi=0.5)
+        if p["monotonic_cst"] not in (None, "None"):
+            warn.append("monotonic_cst not supported; ignored")
         return {
             "n_estimators": n_est, "criterion": crit_id, "max_depth": md if md is not None else forest_ops.INT32_MAX,
             "min_samples_split": mss, "min_samples_leaf": msl, "max_features": k, "bootstrap": int(boot),
             "lambda": lam, "min_impurity_decrease": mid, "seed": seed_of(p["random_state"]), "warnings": warn,
-            "class_weight": cw, "max_leaf_nodes": mln or 0, "ccp_alpha": ccp,
+            "class_weight": cw, "max_leaf_nodes": mln or 0, "ccp_alpha": ccp, "min_weight_fraction_leaf": mwf,
         }
 
     def cost(self, model_type, rp, n_train, n_features, n_classes) -> float:
@@ -333,6 +335,7 @@ class ForestFamily(Family):
             sl["bootstrap"] = rp["bootstrap"]
             sl["criterion"] = rp["criterion"]
             sl["min_impurity_decrease"] = rp["min_impurity_decrease"]
+            sl["min_weight_frac"] = rp.get("min_weight_fraction_leaf", 0.0)
             sl["pois_cdf"] = native.poisson_cdf_table(rp["lambda"])
             cw = rp.get("class_weight")
             sl["cw_mode"] = 0 if cw is None else (2 if cw == "balanced_subsample" else 1)

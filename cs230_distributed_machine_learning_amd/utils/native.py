@@ -44,6 +44,8 @@ TREESPEC_DTYPE = np.dtype(
         ("pois_cdf", "<u4", (POIS_TABLE,)),
         ("cw_mode", "<i4"),
         ("reserved", "<i4"),
+        ("min_weight_frac", "<f8"),
+        ("min_weight_leaf", "<f8"),
     ]
 )
 

@@ -25,6 +25,7 @@ def _specs(n_fits, ntrees, d, **kw):
             s["bootstrap"] = kw.get("bootstrap", 1)
             s["criterion"] = kw.get("criterion", 0)
             s["min_impurity_decrease"] = kw.get("mid", 0.0)
+            s["min_weight_frac"] = kw.get("mwf", 0.0)
             s["pois_cdf"] = native.poisson_cdf_table(1.0)
     return specs
 
@@ -69,6 +70,8 @@ TIERS = [
     (60000, 16, 2, {"max_depth": 12, "k": 16, "bootstrap": 0}),
     (5000, 30, 4, {"criterion": 0, "mss": 10}),
     (8000, 14, 3, {"criterion": 1}),            # entropy: host/device-identical log2 (forest_common.h)
+    (20000, 16, 2, {"mwf": 0.002}),              # min_weight_fraction_leaf in every tier
+    (6000, 12, 3, {"mwf": 0.02, "criterion": 1}),
 ])
 def test_gpu_trees_match_cpu(n, d, C, kw, tiers, words, monkeypatch):
     if words == "plain":   # row ids only (the path for tables too tall for packed row words)

@@ -293,3 +293,40 @@ def test_rf_poisson_criterion_matches_sklearn():
     dd.set_splits(np.ones((1, len(y)), np.uint8), ["full"])
     with pytest.raises(Exception, match="negative"):
         fam.run(dd, [FitTask(0, 0, 0, "RandomForestRegressor", rp)])
+
+
+@pytest.mark.parametrize("model,kw", [
+    ("RandomForestClassifier", {}),
+    ("RandomForestClassifier", {"class_weight": {"0": 1.0, "1": 3.0}}),
+    ("RandomForestRegressor", {}),
+])
+def test_rf_min_weight_fraction_leaf_matches_sklearn(model, kw):
+    """min_weight_fraction_leaf: no side lighter than frac x total weight (class weights
+    included), nodes lighter than twice that are leaves -- sklearn's tree on exact bins."""
+    from sklearn import ensemble
+
+    from cs230_distributed_machine_learning_amd.engine.service import refit_model
+
+    rng = np.random.default_rng(7)
+    X = rng.integers(0, 6, size=(400, 3)).astype(np.float32)
+    reg = model.endswith("Regressor")
+    y = (X[:, 0] * 1.5 + X[:, 1] + rng.normal(size=400)) if reg else \
+        ((X[:, 0] + X[:, 1] + rng.integers(0, 3, 400)) > 6).astype(np.int64)
+    skw = dict(kw)
+    if "class_weight" in skw:
+        skw["class_weight"] = {int(k): v for k, v in skw["class_weight"].items()}
+    for frac in (0.0, 0.03, 0.12):
+        params = {"n_estimators": 1, "bootstrap": False, "max_features": None, "random_state": 1,
+                  "min_weight_fraction_leaf": frac}
+        m = refit_model({"model_type": model, "scoring": None}, dict(params, **kw), DeviceData(X, y, not reg))
+        t = getattr(ensemble, model)(**params, **skw).fit(X, y).estimators_[0].tree_
+        nodes, vals = np.asarray(m["nodes"]), np.asarray(m["vals"])
+        lv = nodes[:, 0] < 0
+        assert lv.sum() == t.n_leaves, (frac, lv.sum(), t.n_leaves)
+        if reg:
+            ours = np.sort(vals[lv, 1] / vals[lv, 0])
+            ref = np.sort(t.value[t.children_left == -1][:, 0, 0])
+        else:
+            ours = np.sort(vals[lv].sum(1))
+            ref = np.sort(t.weighted_n_node_samples[t.children_left == -1])
+        np.testing.assert_allclose(ours, ref, rtol=1e-4 if reg else 1e-9)   # targets are float32 here
