@@ -1067,6 +1067,7 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
   const bool cand = valid_row && lane < cnt - 1 && b != bnext && lrows >= s.min_samples_leaf &&
                     rrows >= s.min_samples_leaf;
   double g = -INFINITY;
+  bool ok = cand;   // cand and both sides at least min_weight_leaf heavy
   if constexpr (!REG) {
     // every shuffle runs with the full wave active (a shuffle inside a divergent branch
     // would read lanes outside EXEC); select afterwards
@@ -1083,7 +1084,8 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
       L.add(lw);
       R.add(tw - lw);
     }
-    if (cand && !side_too_light(s, L.w, R.w)) g = cls_proxy(L, R, s.criterion);
+    ok = cand && !side_too_light(s, L.w, R.w);
+    if (ok) g = cls_proxy(L, R, s.criterion);
   } else {
     const float wsh = __shfl(my_w, src);
     const float y = __shfl(my_y, src);
@@ -1091,10 +1093,10 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
     const float p0 = wave::incl_scan<float>(w);
     const float p1 = wave::incl_scan<float>(w * y);
     const float t0 = wave::bcast<float>(p0, cnt - 1), t1 = wave::bcast<float>(p1, cnt - 1);
-    if (cand && !side_too_light(s, (double)p0, (double)(t0 - p0)))
-      g = reg_proxy(s.criterion, (double)p0, (double)p1, (double)(t0 - p0), (double)(t1 - p1));
+    ok = cand && !side_too_light(s, (double)p0, (double)(t0 - p0));
+    if (ok) g = reg_proxy(s.criterion, (double)p0, (double)p1, (double)(t0 - p0), (double)(t1 - p1));
   }
-  int bl = cand ? lane : 64;
+  int bl = ok ? lane : 64;
   wave::argmax(g, bl, lane);
   gain = g;
   const int bsel = wave::bcast<int>(b, bl & 63);
@@ -1195,8 +1197,9 @@ __device__ void sub_node_seg(const Ctx& c, const TreeSpec& s, const FeatPerm& fp
       L.add(lw);
       R.add(tw - lw);
     }
-    double g = cand ? cls_proxy(L, R, s.criterion) : -INFINITY;
-    int bl = cand ? j : 64;
+    const bool ok = cand && !side_too_light(s, L.w, R.w);
+    double g = ok ? cls_proxy(L, R, s.criterion) : -INFINITY;
+    int bl = ok ? j : 64;
     argmax_seg<WD>(g, bl, lane);
     const int bsel = __shfl(b, seg * WD + (bl & (WD - 1)));
     const uint64_t ncm = __ballot(ncl);

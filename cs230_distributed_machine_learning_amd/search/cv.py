@@ -84,6 +84,55 @@ def holdout_indices(n: int, test_size=0.2, random_state=None):
     return perm[n_test : n_test + n_train], perm[:n_test]
 
 
+def _approximate_mode(class_counts: np.ndarray, n_draws: int, rng) -> np.ndarray:
+    """sklearn.utils.extmath._approximate_mode: per-class draws closest to the class
+    proportions, ties among equal remainders broken by ``rng``."""
+    continuous = class_counts / class_counts.sum() * n_draws
+    floored = np.floor(continuous)
+    need = int(n_draws - floored.sum())
+    if need > 0:
+        remainder = continuous - floored
+        for value in np.sort(np.unique(remainder))[::-1]:
+            (inds,) = np.where(remainder == value)
+            add_now = min(len(inds), need)
+            inds = rng.choice(inds, size=add_now, replace=False)
+            floored[inds] += 1
+            need -= add_now
+            if need == 0:
+                break
+    return floored.astype(int)
+
+
+def stratified_holdout_indices(y: np.ndarray, test_size=0.1, random_state=None):
+    """(train_idx, test_idx) exactly as ``train_test_split(..., stratify=y)``
+    (StratifiedShuffleSplit's first split; GradientBoosting's early-stopping split)."""
+    y = np.asarray(y)
+    n = len(y)
+    n_test = math.ceil(float(test_size) * n) if np.asarray(test_size).dtype.kind == "f" else int(test_size)
+    n_train = n - n_test
+    classes, y_idx = np.unique(y, return_inverse=True)
+    counts = np.bincount(y_idx)
+    if counts.min() < 2:
+        raise ValueError("The least populated class in y has only 1 member, which is too few.")
+    if n_train < len(classes) or n_test < len(classes):
+        raise ValueError("train/test size should be greater or equal to the number of classes")
+    class_indices = np.split(np.argsort(y_idx, kind="mergesort"), np.cumsum(counts)[:-1])
+    if random_state is None:
+        rng = np.random.mtrand._rand
+    elif isinstance(random_state, np.random.RandomState):
+        rng = random_state
+    else:
+        rng = np.random.RandomState(int(random_state))
+    n_i = _approximate_mode(counts, n_train, rng)
+    t_i = _approximate_mode(counts - n_i, n_test, rng)
+    train, test = [], []
+    for i in range(len(classes)):
+        perm = class_indices[i].take(rng.permutation(counts[i]), mode="clip")
+        train.extend(perm[:n_i[i]])
+        test.extend(perm[n_i[i]:n_i[i] + t_i[i]])
+    return rng.permutation(train), rng.permutation(test)
+
+
 def make_split_roles(
     y: np.ndarray,
     cv: int,
