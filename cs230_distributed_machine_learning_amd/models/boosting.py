@@ -21,7 +21,8 @@ squared_error for unit weights); learning_rate, subsample (exactly
 ``int(subsample * n_train)`` in-bag rows per stage, drawn on-device), max_depth,
 min_samples_split/leaf, min_impurity_decrease, max_features.  Split thresholds come
 from the 256-bin quantisation shared with the forests (exact whenever a feature has
-<= 256 distinct values); early stopping (``n_iter_no_change``) is not implemented
+<= 256 distinct values); early stopping (``n_iter_no_change``) holds out sklearn's
+validation split and stops on sklearn's rule
 and is reported in the subtask's warnings.
 """
 from __future__ import annotations
@@ -34,6 +35,7 @@ import numpy as np
 import torch
 
 from ..ops import forest_ops
+from ..search import cv as cv_mod
 from ..utils import native
 from .base import Family, FitOutput, FitTask, ParamError, as_bool, as_float, as_int, register, seed_of
 from .forest import _count_param, _refine, native_seed
@@ -146,8 +148,12 @@ class GradientBoostingFamily(Family):
         init = p["init"]
         if init not in (None, "zero", "None"):
             raise ParamError("init must be None or 'zero' (custom init estimators are not supported)")
-        if p["n_iter_no_change"] is not None:
-            warn.append("n_iter_no_change early stopping not supported; all n_estimators stages fitted")
+        nic = as_int(p["n_iter_no_change"], "n_iter_no_change", lo=1, allow_none=True)
+        vf = as_float(p["validation_fraction"], "validation_fraction", lo=0.0, hi=1.0)
+        if nic is not None and not 0.0 < vf < 1.0:
+            raise ParamError("validation_fraction must be in (0, 1)")
+        rs = p["random_state"]
+        rs = int(rs) if isinstance(rs, (int, np.integer)) or (isinstance(rs, str) and rs.lstrip("-").isdigit()) else None
         ccp = as_float(p["ccp_alpha"], "ccp_alpha", lo=0.0)
         mwf = as_float(p["min_weight_fraction_leaf"], "min_weight_fraction_leaf", lo=0.0, hi=0.5)
         alpha = as_float(p["alpha"], "alpha", lo=0.0, hi=1.0)
@@ -164,6 +170,8 @@ class GradientBoostingFamily(Family):
             "max_features": _max_features(p["max_features"], n_features), "alpha": alpha,
             "init_zero": init == "zero", "seed": seed_of(p["random_state"]), "warnings": warn,
             "ccp_alpha": ccp, "min_weight_fraction_leaf": mwf,
+            "n_iter_no_change": nic, "validation_fraction": vf, "tol": as_float(p["tol"], "tol", lo=0.0),
+            "random_state_int": rs,
             "max_leaf_nodes": as_int(p["max_leaf_nodes"] if p["max_leaf_nodes"] != "None" else None, "max_leaf_nodes",
                                      lo=2, allow_none=True) or 0,
         }
@@ -221,6 +229,27 @@ class GradientBoostingFamily(Family):
         split_idx = torch.tensor([t.split for t in batch], device=dev)
         train = data.roles[split_idx] == 1                                  # [F, n]
         clf = data.classification
+        # early stopping (n_iter_no_change): sklearn holds out validation_fraction of the
+        # fit's training rows (train_test_split, stratified for classifiers, seeded by
+        # random_state) and stops when the validation loss has not improved by tol over
+        # the last n_iter_no_change stages; the stage that triggers the stop is kept
+        val_rows: Dict[int, torch.Tensor] = {}
+        hist: Dict[int, np.ndarray] = {}
+        for f, t in enumerate(batch):
+            nic = t.params.get("n_iter_no_change")
+            if not nic:
+                continue
+            tr = torch.nonzero(train[f]).squeeze(1).cpu().numpy()
+            rs = t.params.get("random_state_int")
+            rs = rs if rs is not None else int(t.seed) & 0x7FFFFFFF
+            if clf:
+                _, va = cv_mod.stratified_holdout_indices(data.y_enc[tr], t.params["validation_fraction"], rs)
+            else:
+                _, va = cv_mod.holdout_indices(len(tr), t.params["validation_fraction"], rs)
+            vr = torch.from_numpy(tr[np.sort(va)]).to(dev)
+            train[f, vr] = False
+            val_rows[f] = vr
+            hist[f] = np.full(int(nic), np.inf)
         if clf:
             ycls = data.y_cls.long()
             Y = torch.nn.functional.one_hot(ycls, max(2, data.n_classes)).double().t()   # [C, n]
@@ -238,6 +267,8 @@ class GradientBoostingFamily(Family):
         train_idx = [torch.nonzero(train[f]).squeeze(1) for f in range(F)]
         for stage in range(max(n_est)):
             act = [f for f in range(F) if stage < n_est[f]]
+            if not act:
+                break
             A = len(act)
             act_t = torch.tensor(act, device=dev)
             R = raw[act_t]                                                 # [A, K, n]
@@ -369,6 +400,14 @@ class GradientBoostingFamily(Family):
             # --- raw-score update of every row (train and held-out) ------------------------
             upd = value[leaf].view(A, K, n) * lr[act_t].view(A, 1, 1)
             raw[act_t] += upd
+            for a, f in enumerate(act):
+                if f in val_rows:
+                    vl = self._val_loss(batch[f].params, raw[f][:, val_rows[f]], val_rows[f], data, K, hub_delta.get(f))
+                    h = hist[f]
+                    if np.any(vl + batch[f].params["tol"] < h):
+                        h[stage % len(h)] = vl
+                    else:
+                        n_est[f] = stage + 1     # this stage is the fit's last (sklearn keeps it)
             if keep_models:
                 vals_np = value.cpu().numpy()
                 nodes_np = fb.nodes.cpu().numpy() if isinstance(fb.nodes, torch.Tensor) else fb.nodes
@@ -402,6 +441,32 @@ class GradientBoostingFamily(Family):
                 o.model = _pack_model(kept[f], init[f].cpu().numpy(), t, data, K)
             outs.append(o)
         return outs
+
+    @staticmethod
+    def _val_loss(rp, r, rows, data, K, delta) -> float:
+        """sklearn's ``self._loss(y_val, raw_val)``: mean of the half-losses GradientBoosting
+        uses (HalfBinomial / HalfMultinomial / Exponential / HalfSquared / Absolute / Pinball /
+        Huber at the stage's delta) over the validation rows."""
+        loss = rp["loss"]
+        if loss in (LOSS_LOG, LOSS_EXP):
+            y = data.y_cls[rows].long()
+            if loss == LOSS_EXP:
+                return float(torch.exp(-(2.0 * y.double() - 1.0) * r[0]).mean())
+            if K == 1:
+                z = r[0]
+                return float((torch.nn.functional.softplus(z) - y.double() * z).mean())
+            return float((torch.logsumexp(r, 0) - r.gather(0, y.view(1, -1))[0]).mean())
+        d = data.y_reg[rows].double() - r[0]
+        if loss == LOSS_SQ:
+            return float((0.5 * d * d).mean())
+        if loss == LOSS_ABS:
+            return float(d.abs().mean())
+        if loss == LOSS_QUANT:
+            a = rp["alpha"]
+            return float(torch.where(d >= 0, a * d, (a - 1.0) * d).mean())
+        dl = float(delta or 0.0)
+        ad = d.abs()
+        return float(torch.where(ad <= dl, 0.5 * d * d, dl * (ad - 0.5 * dl)).mean())
 
     # negative gradient [K, n] of the fit's loss (+ huber delta, else 0)
     @staticmethod

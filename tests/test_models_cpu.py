@@ -330,3 +330,38 @@ def test_rf_min_weight_fraction_leaf_matches_sklearn(model, kw):
             ours = np.sort(vals[lv].sum(1))
             ref = np.sort(t.weighted_n_node_samples[t.children_left == -1])
         np.testing.assert_allclose(ours, ref, rtol=1e-4 if reg else 1e-9)   # targets are float32 here
+
+
+@pytest.mark.parametrize("model,loss", [("GradientBoostingRegressor", "squared_error"),
+                                        ("GradientBoostingClassifier", "log_loss")])
+def test_gbrt_early_stopping_matches_sklearn(model, loss):
+    """n_iter_no_change: sklearn's validation split (stratified for classifiers), its loss,
+    its stopping rule -- the same number of stages and the same raw scores."""
+    from sklearn import ensemble
+    from sklearn.datasets import make_classification, make_regression
+
+    from cs230_distributed_machine_learning_amd.models.boosting import gbrt_raw_numpy
+
+    reg = model.endswith("Regressor")
+    if reg:
+        X, y = make_regression(400, 4, noise=25, random_state=4)
+        y = np.round(y, 2)
+    else:
+        X, y = make_classification(400, 5, n_informative=3, n_redundant=0, flip_y=0.2, random_state=4)
+    X = np.round(X, 1)
+    params = {"n_estimators": 300, "loss": loss, "max_depth": 3, "learning_rate": 0.3, "n_iter_no_change": 4,
+              "validation_fraction": 0.2, "random_state": 11}
+    sk = getattr(ensemble, model)(**params).fit(X, y)
+    assert sk.n_estimators_ < 300
+    ref = sk.predict(X) if reg else sk.decision_function(X)
+    dd = DeviceData(X, y, not reg, "cpu")
+    dd.set_splits(np.ones((1, len(y)), np.uint8), ["full"])
+    fam = family_of(model)
+    rp = fam.resolve(model, params, len(y), X.shape[1], 1 if reg else 2)
+    out = fam.run(dd, [FitTask(0, 0, 0, model, rp)], keep_models=True)[0]
+    assert len(out.model["roots"]) == sk.n_estimators_
+    got = gbrt_raw_numpy(out.model, X)[:, 0]
+    # equal-gain ties between features go by the visiting order (sklearn's RNG vs ours),
+    # so a deep stage can pick another of the tied splits for a few rows
+    close = np.isclose(got, ref, rtol=1e-4, atol=1e-3)
+    assert close.mean() >= 0.97, close.mean()
