@@ -178,3 +178,18 @@ def test_validate_scoring():
     assert dsc.validate_scoring(None, False) == "r2"
     with pytest.raises(ValueError):
         dsc.validate_scoring("r2", True)
+
+
+def test_stratified_holdout_matches_sklearn():
+    """GradientBoosting's early-stopping split: train_test_split(..., stratify=y)."""
+    from sklearn.model_selection import train_test_split
+
+    from cs230_distributed_machine_learning_amd.search.cv import stratified_holdout_indices
+
+    for seed in range(6):
+        rng = np.random.default_rng(seed)
+        y = rng.integers(0, 3 + seed % 3, size=97 + seed * 13)
+        idx = np.arange(len(y))
+        a, b = train_test_split(idx, test_size=0.1 + 0.05 * seed, random_state=seed, stratify=y)
+        c, d = stratified_holdout_indices(y, 0.1 + 0.05 * seed, seed)
+        assert np.array_equal(a, c) and np.array_equal(b, d)
