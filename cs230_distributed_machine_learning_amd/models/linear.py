@@ -729,6 +729,24 @@ class LogisticFamily(Family):
         return outs
 
 
+def _ls_solve(A: torch.Tensor, b: torch.Tensor, positive: bool) -> torch.Tensor:
+    """Least squares from the normal equations ``A = X^T X``, ``b = X^T y``: the
+    minimum-norm solution (sklearn's lstsq), or with ``positive`` the non-negative one
+    (sklearn's scipy ``nnls``).  NNLS needs only a factor R with R^T R = A and R^T z = b:
+    ||X w - y||^2 = ||R w - z||^2 + const, so the d x d system stands in for the rows."""
+    if not positive:
+        return torch.linalg.pinv(A, hermitian=True) @ b
+    from scipy.optimize import nnls
+
+    lam, V = np.linalg.eigh(A.cpu().numpy())
+    keep = lam > lam.max() * A.shape[0] * np.finfo(np.float64).eps if lam.size else lam > 0
+    Vk, lk = V[:, keep], lam[keep]
+    R = np.sqrt(lk)[:, None] * Vk.T                      # k x d, R^T R = A on its range
+    z = (Vk.T @ b.cpu().numpy()) / np.sqrt(lk)           # R^T z = b
+    w, _ = nnls(R, z, maxiter=50 * max(1, A.shape[0]))
+    return torch.from_numpy(w).to(device=A.device, dtype=torch.float64)
+
+
 HOST_LBFGS_MAX_WORK = 200_000   # n_train * (d+1) * (K-1): below this a fit runs on the host
 
 _LIN_DEFAULTS = {"fit_intercept": True, "copy_X": True, "n_jobs": None, "positive": False}
@@ -742,10 +760,8 @@ class LinearRegressionFamily(Family):
     def resolve(self, model_type, params, n_train, n_features, n_classes):
         p = dict(_LIN_DEFAULTS)
         p.update({k: v for k, v in params.items() if k in _LIN_DEFAULTS})
-        warn = []
-        if as_bool(p["positive"], "positive"):
-            warn.append("positive=True not supported; unconstrained least squares used")
-        return {"fit_intercept": as_bool(p["fit_intercept"], "fit_intercept"), "warnings": warn}
+        return {"fit_intercept": as_bool(p["fit_intercept"], "fit_intercept"),
+                "positive": as_bool(p["positive"], "positive"), "warnings": []}
 
     def cost(self, model_type, rp, n_train, n_features, n_classes) -> float:
         return n_train * n_features * n_features * 2e-12 + 1e-3
@@ -759,12 +775,13 @@ class LinearRegressionFamily(Family):
             cache = self._solve_from_moments(data, tasks)
         outs = []
         for t in tasks:
-            key = (t.split, t.params["fit_intercept"])
+            pos = bool(t.params.get("positive", False))
+            key = (t.split, t.params["fit_intercept"], pos)
             if key not in cache:
                 tr = data.train_rows[t.split].long()
                 Xt, yt = X[tr].double(), y[tr].double()
                 if getattr(data, "is_row_shard", False):
-                    cache[key] = self._sharded_solve(data, Xt, yt, t.params["fit_intercept"])
+                    cache[key] = self._sharded_solve(data, Xt, yt, t.params["fit_intercept"], pos)
                 elif t.params["fit_intercept"]:
                     xm, ym = Xt.mean(0), yt.mean()
                     Xc, yc = Xt - xm, yt - ym
@@ -773,8 +790,7 @@ class LinearRegressionFamily(Family):
                     ym = torch.zeros((), dtype=torch.float64, device=X.device)
                     Xc, yc = Xt, yt
                 if key not in cache:
-                    A = Xc.t() @ Xc
-                    w = torch.linalg.pinv(A, hermitian=True) @ (Xc.t() @ yc)
+                    w = _ls_solve(Xc.t() @ Xc, Xc.t() @ yc, pos)
                     b0 = ym - xm @ w
                     cache[key] = (w, b0)
             w, b0 = cache[key]
@@ -783,7 +799,8 @@ class LinearRegressionFamily(Family):
             o = FitOutput(task_id=t.task_id, pred=pred, info={"warnings": t.params.get("warnings", [])})
             if keep_models:
                 o.model = {"kind": "linear_regression", "coef": w.cpu().numpy(), "intercept": float(b0),
-                           "model_type": t.model_type, "params": {"fit_intercept": t.params["fit_intercept"]}}
+                           "model_type": t.model_type, "params": {"fit_intercept": t.params["fit_intercept"],
+                                                                  "positive": pos}}
             outs.append(o)
         if data.is_gpu:
             torch.cuda.synchronize(data.device)
@@ -829,22 +846,23 @@ class LinearRegressionFamily(Family):
             m = M[i]
             cnt, Sx, Sy = m[d, d], m[:d, d], m[d + 1, d]
             XX, Xy = m[:d, :d], m[:d, d + 1]
-            for fi in sorted({t.params["fit_intercept"] for t in tasks if t.split == sp}):
+            for fi, pos in sorted({(t.params["fit_intercept"], bool(t.params.get("positive", False)))
+                                   for t in tasks if t.split == sp}):
                 if fi:
                     xm, ym = Sx / cnt.clamp_min(1), Sy / cnt.clamp_min(1)
                     A = XX - cnt * torch.outer(xm, xm)
                     b = Xy - cnt * xm * ym
-                    w = torch.linalg.pinv(A, hermitian=True) @ b
-                    out[(sp, fi)] = (w, (ym + cy) - (xm + cx) @ w)
+                    w = _ls_solve(A, b, pos)
+                    out[(sp, fi, pos)] = (w, (ym + cy) - (xm + cx) @ w)
                 else:   # moments about the origin: x = z + c_x, y = z_y + c_y
                     XX0 = XX + torch.outer(Sx, cx) + torch.outer(cx, Sx) + cnt * torch.outer(cx, cx)
                     Xy0 = Xy + Sx * cy + cx * Sy + cnt * cx * cy
-                    w = torch.linalg.pinv(XX0, hermitian=True) @ Xy0
-                    out[(sp, fi)] = (w, torch.zeros((), dtype=torch.float64, device=w.device))
+                    w = _ls_solve(XX0, Xy0, pos)
+                    out[(sp, fi, pos)] = (w, torch.zeros((), dtype=torch.float64, device=w.device))
         return out
 
     @staticmethod
-    def _sharded_solve(data, Xt: torch.Tensor, yt: torch.Tensor, fit_intercept: bool):
+    def _sharded_solve(data, Xt: torch.Tensor, yt: torch.Tensor, fit_intercept: bool, positive: bool = False):
         """Normal equations from all-reduced shard moments: one all-reduce of
         [count, sum x, sum y, X^T X, X^T y] (float64), centred on the global means."""
         d = Xt.shape[1]
@@ -862,7 +880,7 @@ class LinearRegressionFamily(Family):
             xm = torch.zeros(d, dtype=torch.float64, device=Xt.device)
             ym = torch.zeros((), dtype=torch.float64, device=Xt.device)
             A, bvec = XX, Xy
-        w = torch.linalg.pinv(A, hermitian=True) @ bvec
+        w = _ls_solve(A, bvec, positive)
         return w, ym - xm @ w
 
 

@@ -365,3 +365,22 @@ def test_gbrt_early_stopping_matches_sklearn(model, loss):
     # so a deep stage can pick another of the tied splits for a few rows
     close = np.isclose(got, ref, rtol=1e-4, atol=1e-3)
     assert close.mean() >= 0.97, close.mean()
+
+
+@pytest.mark.parametrize("fit_intercept", [True, False])
+def test_linear_regression_positive_matches_sklearn(fit_intercept):
+    """positive=True: non-negative least squares from the normal equations (NNLS on a
+    Gram factor) = sklearn's nnls on the rows."""
+    from sklearn.linear_model import LinearRegression
+
+    from cs230_distributed_machine_learning_amd.engine.service import refit_model
+
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(300, 6))
+    y = X @ np.array([1.5, -2.0, 0.7, 0.0, -0.3, 2.2]) + 0.5 + 0.1 * rng.normal(size=300)
+    params = {"positive": True, "fit_intercept": fit_intercept}
+    m = refit_model({"model_type": "LinearRegression", "scoring": None}, params, DeviceData(X, y, False))
+    sk = LinearRegression(**params).fit(X, y)
+    assert (m["coef"] >= 0).all()
+    np.testing.assert_allclose(m["coef"], sk.coef_, atol=2e-5)
+    assert abs(m["intercept"] - sk.intercept_) < 2e-5
