@@ -48,6 +48,12 @@ SMALL_SEG = 1024         # pairs: below this a node's histogram goes straight to
 TILE_ROWS = 4096         # pairs per LDS tile of a large node
 LDS_BYTES = 65536        # LDS per workgroup for the tile histograms
 HIST_BUDGET = 1 << 30    # bytes of histogram per all-reduce chunk
+# classification nodes of <= this many global rows exchange sparse histograms: a row adds
+# at most 2 x KR non-zero (index, count) int32 pairs (8 B each) against the node's dense
+# KR x channels x 1 KiB reduce-scatter share.  Swept on a 2-rank gloo build (60k x 20,
+# 8 full-depth trees): exchanged bytes 0.38 GB dense -> 0.20 / 0.135 / 0.121 GB at
+# 16 / 48 / 96 rows (profiles/r2_forest_dp_sparse_sweep.log)
+SPARSE_ROWS = 96
 
 
 class DpArgs(ctypes.Structure):
@@ -177,67 +183,95 @@ def build_dp(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torc
             left_pos = int((d - sv[sl, F_POS]).max())
             KR = max(1, min(left_pos, need + max(1, need // 4)))
             chunk = max(1, hist_budget // (KR * CH * 1024))
-            for c0 in range(0, S, chunk):
-                sub = srch[c0:c0 + chunk].contiguous()
-                Sc = int(sub.numel())
-                feats = torch.empty((Sc, KR), dtype=torch.int32, device=dev)
-                q = -(-Sc // world)                          # nodes owned per rank (reduce-scatter)
-                hist = torch.zeros((q * world if scatter else Sc, KR, CH, 256), dtype=hist_dtype, device=dev)
-                a.srch, a.S, a.KR, a.feats, a.hist = _p(sub), Sc, KR, _p(feats), _p(hist)
-                L.step(a, 3)
-                th = time.perf_counter()
-                cnt = seg_cnt[sub.long()]
-                if L.gpu and lds_feats > 0:
-                    big = cnt >= SMALL_SEG
-                    bi = torch.nonzero(big).flatten()
-                    nt = (cnt[bi] + TILE_ROWS - 1) // TILE_ROWS
-                    n_tiles = int(nt.sum()) if bi.numel() else 0
-                    tile_s = torch.repeat_interleave(bi.to(torch.int32), nt, output_size=n_tiles)
-                    first = torch.cumsum(nt, 0) - nt
-                    tile_off = (torch.arange(n_tiles, device=dev) -
-                                torch.repeat_interleave(first, nt, output_size=n_tiles)) * TILE_ROWS
-                    small = torch.nonzero((~big) & (cnt > 0)).flatten().to(torch.int32)
-                else:
-                    tile_s = tile_off = None
-                    n_tiles = 0
-                    small = torch.nonzero(cnt > 0).flatten().to(torch.int32)
-                a.tile_s, a.tile_off, a.n_tiles, a.tile_rows = _p(tile_s), _p(tile_off), n_tiles, TILE_ROWS
-                a.small_s, a.n_small, a.lds_feats = _p(small), int(small.numel()), max(1, min(lds_feats, KR))
-                with trace.range("forest_dp_hist"):
-                    L.step(a, 4)
-                    if L.gpu and timing:   # per-phase timing only: the collective orders itself
-                        torch.cuda.current_stream(dev).synchronize()
-                tr = time.perf_counter()
-                stats["hist_s"] += tr - th
-                if scatter:
-                    # owner-computes: the global sums of this rank's 1/N of the nodes
-                    with trace.range("forest_dp_reduce_scatter"):
-                        own = comm.reduce_scatter_rows(hist)
-                    stats["reduce_s"] += time.perf_counter() - tr
-                    stats["allreduce_bytes"] += hist.numel() * 4 // 2     # ring: half of an all-reduce
-                    lo = min(Sc, comm.rank * q)
-                    hi = min(Sc, lo + q)
-                    own_srch = sub[lo:hi].contiguous()
-                    a.srch, a.S, a.hist, a.feats = _p(own_srch), hi - lo, _p(own), _p(feats[lo:hi])
-                    L.step(a, 5)
-                    idx = own_srch.long()
-                    rec = torch.zeros((q, SLOT_BYTES + 8 * CH), dtype=torch.uint8, device=dev)
-                    rec[:hi - lo, :SLOT_BYTES] = slots[idx]
-                    rec[:hi - lo, SLOT_BYTES:] = best_left[idx].view(torch.uint8)
-                    with trace.range("forest_dp_gather_decisions"):
-                        rec = comm.all_gather_equal(rec)[:Sc]
-                    sl_all = sub.long()
-                    slots[sl_all] = rec[:, :SLOT_BYTES]
-                    best_left[sl_all] = rec[:, SLOT_BYTES:].contiguous().view(torch.float64)
-                    a.srch, a.S, a.hist, a.feats = _p(sub), Sc, _p(hist), _p(feats)
-                else:
-                    with trace.range("forest_dp_allreduce"):
-                        reduce(hist, "sum")
-                    stats["reduce_s"] += time.perf_counter() - tr
-                    stats["allreduce_bytes"] += hist.numel() * 4
-                    L.step(a, 5)
-                stats["rounds"] += 1
-                del feats, hist, tile_s, tile_off, small
+            # small nodes of a classification forest exchange sparse local histograms
+            # (non-zero (index, count) pairs) instead of dense 256-bin tensors
+            groups = [(srch, False)]
+            if scatter and not is_reg:
+                small_n = slots.view(torch.float64)[sl, 2] <= SPARSE_ROWS
+                groups = [(srch[~small_n].contiguous(), False), (srch[small_n].contiguous(), True)]
+            for grp, sparse in groups:
+                Sg = int(grp.numel())
+                for c0 in range(0, Sg, chunk):
+                    sub = grp[c0:c0 + chunk].contiguous()
+                    Sc = int(sub.numel())
+                    feats = torch.empty((Sc, KR), dtype=torch.int32, device=dev)
+                    q = -(-Sc // world)                          # nodes owned per rank (reduce-scatter)
+                    rs = scatter and not sparse
+                    hist = torch.zeros((q * world if rs else Sc, KR, CH, 256), dtype=hist_dtype, device=dev)
+                    a.srch, a.S, a.KR, a.feats, a.hist = _p(sub), Sc, KR, _p(feats), _p(hist)
+                    L.step(a, 3)
+                    th = time.perf_counter()
+                    cnt = seg_cnt[sub.long()]
+                    if L.gpu and lds_feats > 0:
+                        big = cnt >= SMALL_SEG
+                        bi = torch.nonzero(big).flatten()
+                        nt = (cnt[bi] + TILE_ROWS - 1) // TILE_ROWS
+                        n_tiles = int(nt.sum()) if bi.numel() else 0
+                        tile_s = torch.repeat_interleave(bi.to(torch.int32), nt, output_size=n_tiles)
+                        first = torch.cumsum(nt, 0) - nt
+                        tile_off = (torch.arange(n_tiles, device=dev) -
+                                    torch.repeat_interleave(first, nt, output_size=n_tiles)) * TILE_ROWS
+                        small = torch.nonzero((~big) & (cnt > 0)).flatten().to(torch.int32)
+                    else:
+                        tile_s = tile_off = None
+                        n_tiles = 0
+                        small = torch.nonzero(cnt > 0).flatten().to(torch.int32)
+                    a.tile_s, a.tile_off, a.n_tiles, a.tile_rows = _p(tile_s), _p(tile_off), n_tiles, TILE_ROWS
+                    a.small_s, a.n_small, a.lds_feats = _p(small), int(small.numel()), max(1, min(lds_feats, KR))
+                    with trace.range("forest_dp_hist"):
+                        L.step(a, 4)
+                        if L.gpu and timing:   # per-phase timing only: the collective orders itself
+                            torch.cuda.current_stream(dev).synchronize()
+                    tr = time.perf_counter()
+                    stats["hist_s"] += tr - th
+                    if sparse:
+                        # every rank sums the same gathered (index, count) pairs: integer
+                        # sums, identical on every rank, so every rank evaluates these nodes
+                        with trace.range("forest_dp_sparse_gather"):
+                            flat = hist.view(-1)
+                            nz = torch.nonzero(flat).flatten()
+                            pairs = torch.stack([nz.to(torch.int32), flat[nz].to(torch.int32)], 1)   # < 2^28 bins
+                            cnts = comm.all_gather_equal(torch.tensor([pairs.shape[0]], dtype=torch.int64, device=dev))
+                            m = int(cnts.max())
+                            pad = torch.zeros((m, 2), dtype=torch.int32, device=dev)
+                            pad[:pairs.shape[0]] = pairs
+                            allp = comm.all_gather_equal(pad)
+                            keep = torch.cat([torch.arange(m, device=dev) < int(c) for c in cnts.tolist()])
+                            allp = allp[keep]
+                            flat.zero_()
+                            flat.index_add_(0, allp[:, 0].long(), allp[:, 1].to(hist_dtype))
+                        stats["reduce_s"] += time.perf_counter() - tr
+                        stats["allreduce_bytes"] += int(cnts.sum()) * 8
+                        L.step(a, 5)
+                    elif scatter:
+                        # owner-computes: the global sums of this rank's 1/N of the nodes
+                        with trace.range("forest_dp_reduce_scatter"):
+                            own = comm.reduce_scatter_rows(hist)
+                        stats["reduce_s"] += time.perf_counter() - tr
+                        stats["allreduce_bytes"] += hist.numel() * 4 // 2     # ring: half of an all-reduce
+                        lo = min(Sc, comm.rank * q)
+                        hi = min(Sc, lo + q)
+                        own_srch = sub[lo:hi].contiguous()
+                        a.srch, a.S, a.hist, a.feats = _p(own_srch), hi - lo, _p(own), _p(feats[lo:hi])
+                        L.step(a, 5)
+                        idx = own_srch.long()
+                        rec = torch.zeros((q, SLOT_BYTES + 8 * CH), dtype=torch.uint8, device=dev)
+                        rec[:hi - lo, :SLOT_BYTES] = slots[idx]
+                        rec[:hi - lo, SLOT_BYTES:] = best_left[idx].view(torch.uint8)
+                        with trace.range("forest_dp_gather_decisions"):
+                            rec = comm.all_gather_equal(rec)[:Sc]
+                        sl_all = sub.long()
+                        slots[sl_all] = rec[:, :SLOT_BYTES]
+                        best_left[sl_all] = rec[:, SLOT_BYTES:].contiguous().view(torch.float64)
+                        a.srch, a.S, a.hist, a.feats = _p(sub), Sc, _p(hist), _p(feats)
+                    else:
+                        with trace.range("forest_dp_allreduce"):
+                            reduce(hist, "sum")
+                        stats["reduce_s"] += time.perf_counter() - tr
+                        stats["allreduce_bytes"] += hist.numel() * 4
+                        L.step(a, 5)
+                    stats["rounds"] += 1
+                    del feats, hist, tile_s, tile_off, small
         # ---- accept, children, partition ------------------------------------------------
         L.step(a, 6)
         split = sv[:, F_SPLIT]
