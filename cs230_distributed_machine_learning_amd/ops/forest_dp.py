@@ -232,14 +232,15 @@ def build_dp(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torc
                             nz = torch.nonzero(flat).flatten()
                             pairs = torch.stack([nz.to(torch.int32), flat[nz].to(torch.int32)], 1)   # < 2^28 bins
                             cnts = comm.all_gather_equal(torch.tensor([pairs.shape[0]], dtype=torch.int64, device=dev))
-                            m = int(cnts.max())
-                            pad = torch.zeros((m, 2), dtype=torch.int32, device=dev)
-                            pad[:pairs.shape[0]] = pairs
-                            allp = comm.all_gather_equal(pad)
-                            keep = torch.cat([torch.arange(m, device=dev) < int(c) for c in cnts.tolist()])
-                            allp = allp[keep]
-                            flat.zero_()
-                            flat.index_add_(0, allp[:, 0].long(), allp[:, 1].to(hist_dtype))
+                            m = int(cnts.max())          # the same on every rank
+                            if m > 0:
+                                pad = torch.zeros((m, 2), dtype=torch.int32, device=dev)
+                                pad[:pairs.shape[0]] = pairs
+                                allp = comm.all_gather_equal(pad)
+                                keep = torch.cat([torch.arange(m, device=dev) < int(c) for c in cnts.tolist()])
+                                allp = allp[keep]
+                                flat.zero_()
+                                flat.index_add_(0, allp[:, 0].long(), allp[:, 1].to(hist_dtype))
                         stats["reduce_s"] += time.perf_counter() - tr
                         stats["allreduce_bytes"] += int(cnts.sum()) * 8
                         L.step(a, 5)
