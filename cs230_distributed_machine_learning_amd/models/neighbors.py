@@ -183,9 +183,60 @@ def vote(dist: torch.Tensor, nb_y: torch.Tensor, k: int, weights: str, n_classes
     return ((w * yv).sum(1) / w.sum(1)).float(), None
 
 
+def _merge_topk(d_parts: torch.Tensor, i_parts: torch.Tensor, y_parts: torch.Tensor, K: int):
+    """[W, q, K] per-rank candidates -> the global top-K per query in (distance, row id)
+    order: the order a one-process stable sort over ascending row ids gives."""
+    W, q, k = d_parts.shape
+    d = d_parts.permute(1, 0, 2).reshape(q, W * k)
+    i = i_parts.permute(1, 0, 2).reshape(q, W * k)
+    y = y_parts.permute(1, 0, 2).reshape(q, W * k)
+    _, o1 = torch.sort(i, dim=1, stable=True)                  # ascending row id ...
+    d, i, y = d.gather(1, o1), i.gather(1, o1), y.gather(1, o1)
+    _, o2 = torch.sort(d, dim=1, stable=True)                  # ... then distance (stable)
+    return d.gather(1, o2)[:, :K], y.gather(1, o2)[:, :K]
+
+
+def knn_search_sharded(data, splits: List[int], K: int, metric: int, p: float, y: torch.Tensor):
+    """Row-sharded search (parallel/data_parallel.py RowShard): every rank searches ALL
+    of a split's held-out rows (one all-gather of their features) against its OWN training
+    rows, one all-gather of the per-rank top-K (distance, global row id, target) and an
+    exact merge give the global neighbours; each rank keeps its own queries' rows.
+    Distances are computed element for element like the one-process search, so ties break
+    the same way (lower global row id)."""
+    out = {}
+    world, rank = data.world, data.rank
+    for s in splits:
+        cnt = data._test_counts[s]
+        Q = data._gather_rows(data.X[data.test_rows[s].long()], cnt)          # [m_glob, d]
+        tr = data.train_rows[s].long()
+        R = data.X[tr]
+        m = Q.shape[0]
+        k_loc = min(K, R.shape[0])
+        big = torch.finfo(torch.float32).max
+        dd = torch.full((m, K), big, dtype=torch.float32, device=Q.device)
+        ii = torch.full((m, K), 2 ** 62, dtype=torch.long, device=Q.device)
+        yy = torch.zeros((m, K), dtype=y.dtype, device=Q.device)
+        if k_loc > 0 and m > 0:
+            step = max(1, (1 << 24) // max(1, R.shape[0] * max(1, data.d // 8)))
+            for q0 in range(0, m, step):
+                D = _acc_torch(Q[q0:q0 + step], R, metric, p)
+                Ds, idx = torch.sort(D, dim=1, stable=True)
+                dd[q0:q0 + step, :k_loc] = Ds[:, :k_loc].float()
+                ii[q0:q0 + step, :k_loc] = tr[idx[:, :k_loc]] + data.r0
+                yy[q0:q0 + step, :k_loc] = y[tr[idx[:, :k_loc]]]
+        acc, nb_y = _merge_topk(data.all_gather_equal(dd).view(world, m, K),
+                                data.all_gather_equal(ii).view(world, m, K),
+                                data.all_gather_equal(yy).view(world, m, K), K)
+        o = int(cnt[:rank].sum())
+        out[s] = (acc[o:o + int(cnt[rank])], nb_y[o:o + int(cnt[rank])])
+    return out
+
+
 class KNeighborsFamily(Family):
     model_types = ("KNeighborsClassifier", "KNeighborsRegressor")
     classifiers = ("KNeighborsClassifier",)
+    data_parallel = True   # row-sharded search: per-rank top-K + exact merge (knn_search_sharded)
+    dp_when_few = False    # a replicated table is always faster when it fits
 
     def resolve(self, model_type, params, n_train, n_features, n_classes):
         p = dict(_DEFAULTS)
@@ -231,19 +282,25 @@ class KNeighborsFamily(Family):
             if not ok:
                 continue
             kmax = max(t.params["n_neighbors"] for t in ok)
-            if data.is_gpu and kmax <= KERNEL_KMAX:
-                nb = knn_search_hip(data, splits, kmax, metric, p)
+            if getattr(data, "is_row_shard", False):
+                nb = knn_search_sharded(data, splits, kmax, metric, p, y)
+            elif data.is_gpu and kmax <= KERNEL_KMAX:
+                nb = {s: (a, y[i]) for s, (a, i) in knn_search_hip(data, splits, kmax, metric, p).items()}
             else:
-                nb = {s: knn_search_torch(data.X, data.test_rows[s], data.train_rows[s], kmax, metric, p)
-                      for s in splits}
+                nb = {s: (a, y[i]) for s, (a, i) in ((s, knn_search_torch(data.X, data.test_rows[s], data.train_rows[s],
+                                                                          kmax, metric, p)) for s in splits)}
             for t in ok:
-                acc, idx = nb[t.split]
+                acc, nb_y = nb[t.split]
                 dist = finish_distance(acc, metric, p)
-                pred, proba = vote(dist, y[idx], t.params["n_neighbors"], t.params["weights"], data.n_classes, clf)
+                pred, proba = vote(dist, nb_y, t.params["n_neighbors"], t.params["weights"], data.n_classes, clf)
                 o = FitOutput(task_id=t.task_id, pred=pred, proba=proba, info={"warnings": t.params["warnings"]})
                 if keep_models:
                     tr = data.train_rows[t.split].long()
-                    o.model = {"kind": "knn", "X": data.X[tr].cpu().numpy(), "y": y[tr].cpu().numpy(),
+                    Xtr, ytr = data.X[tr], y[tr]
+                    if getattr(data, "is_row_shard", False):   # the fitted model holds every rank's rows
+                        cnt = data.all_gather_equal(torch.tensor([tr.numel()], device=data.device)).cpu().numpy()
+                        Xtr, ytr = data._gather_rows(Xtr, cnt), data._gather_rows(ytr, cnt)
+                    o.model = {"kind": "knn", "X": Xtr.cpu().numpy(), "y": ytr.cpu().numpy(),
                                "classes": None if not clf else np.asarray(data.classes).tolist(),
                                "n_neighbors": t.params["n_neighbors"], "weights": t.params["weights"],
                                "metric": metric, "p": p, "model_type": t.model_type, "n_classes": data.n_classes}

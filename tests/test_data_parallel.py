@@ -16,6 +16,8 @@ from cs230_distributed_machine_learning_amd.parallel.data_parallel import shard_
 RF_GRID = [{"n_estimators": 8, "max_depth": md, "min_samples_leaf": msl, "class_weight": cw, "random_state": 5}
            for md, msl, cw in ((None, 1, None), (6, 3, "balanced"), (None, 2, "balanced_subsample"))] + \
           [{"n_estimators": 6, "criterion": "entropy", "max_features": 0.5, "random_state": 2}]
+KNN_GRID = [{"n_neighbors": k, "weights": w, "metric": m} for k, w, m in
+            ((5, "uniform", "minkowski"), (9, "distance", "manhattan"), (3, "uniform", "chebyshev"))]
 RFR_GRID = [{"n_estimators": 5, "max_depth": 8, "random_state": 1}, {"n_estimators": 4, "min_samples_leaf": 5}]
 LR_GRID = [{"C": c, "solver": s, "class_weight": cw, "max_iter": 200}
            for c in (0.05, 1.0) for s in ("liblinear", "newton-cg") for cw in (None, "balanced")]
@@ -78,12 +80,14 @@ def _rank(rank, world, port, outq):
         lin = _run(shr, X, y_reg, "LinearRegression", [{"fit_intercept": True}, {"fit_intercept": False}], cv=3)
         rf = _run(sh, X, yg, "RandomForestClassifier", RF_GRID, cv=3)
         rfr = _run(shr, X, y_reg, "RandomForestRegressor", RFR_GRID, cv=3)
+        knn = _run(sh, X, yg, "KNeighborsClassifier", KNN_GRID, cv=3)
+        knr = _run(shr, X, y_reg, "KNeighborsRegressor", KNN_GRID[:2], cv=3)
         err = None
         try:
-            _run(sh, X, yg, "KNeighborsClassifier", [{"n_neighbors": 3}])
+            _run(sh, X, yg, "SVC", [{"C": 1.0}])
         except ValueError as e:
             err = str(e)
-        outq.put(("ok", rank, lr, lin, err, rf, rfr))
+        outq.put(("ok", rank, lr, lin, err, rf, rfr, knn, knr))
         dist.destroy()
     except Exception:  # pragma: no cover
         import traceback
@@ -129,6 +133,12 @@ def test_row_sharded_fits_match_single_process():
     ref_rf = _run(DeviceData(X, y_cls, True), X, y_cls, "RandomForestClassifier", RF_GRID, cv=3)
     assert o0[5] == o1[5] and o0[6] == o1[6]
     assert o0[5] == ref_rf, (o0[5], ref_rf)
+    # row-sharded KNN: per-rank top-K + exact merge = the one-process neighbours
+    assert o0[7] == o1[7] and o0[8] == o1[8]
+    assert o0[7] == _run(DeviceData(X, y_cls, True), X, y_cls, "KNeighborsClassifier", KNN_GRID, cv=3)
+    ref_knr = _run(DeviceData(X, y_reg, False), X, y_reg, "KNeighborsRegressor", KNN_GRID[:2], cv=3)
+    for (cv_s, hold), (cv_r, hold_r) in zip(o0[8], ref_knr):
+        assert np.allclose(cv_s, cv_r, atol=1e-9) and abs(hold - hold_r) < 1e-9
     ref_rfr = _run(DeviceData(X, y_reg, False), X, y_reg, "RandomForestRegressor", RFR_GRID, cv=3)
     for (cv_s, hold), (cv_r, hold_r) in zip(o0[6], ref_rfr):
         assert np.allclose(cv_s, cv_r, atol=0.02) and abs(hold - hold_r) < 0.02, (cv_s, cv_r)
