@@ -80,6 +80,8 @@ class PCAFamily(Family):
     model_types = ("PCA",)
     classifiers = ()
     self_scored = ("PCA",)
+    data_parallel = True   # row-sharded: [count, sum x, X^T X] and the test log-likelihood sums all-reduced
+    dp_when_few = False
 
     def resolve(self, model_type, params, n_train, n_features, n_classes) -> Dict[str, Any]:
         p = dict(_PCA_DEFAULTS)
@@ -118,10 +120,19 @@ class PCAFamily(Family):
                 cnt, Sx, XX = M[i][d, d], M[i][:d, d], M[i][:d, :d]
                 dm = Sx / cnt.clamp_min(1)
                 fused[sp] = (shift[:d] + dm, (XX - cnt * torch.outer(dm, dm)) / max(1.0, float(cnt) - 1), int(cnt))
+        sharded = getattr(data, "is_row_shard", False)
         for t in tasks:
             if t.split not in eig:
                 if t.split in fused:
                     mean, cov, n = fused[t.split]
+                elif sharded:   # global moments: one all-reduce of [count, sum x, X^T X] (float64)
+                    Xt = X[data.train_rows[t.split].long()].double()
+                    m = torch.cat([torch.tensor([float(Xt.shape[0])], dtype=torch.float64, device=X.device),
+                                   Xt.sum(0), (Xt.t() @ Xt).flatten()])
+                    data.all_reduce(m)
+                    n = int(m[0])
+                    mean = m[1:1 + d] / max(1, n)
+                    cov = (m[1 + d:].view(d, d) - n * torch.outer(mean, mean)) / max(1, n - 1)
                 else:
                     tr = data.train_rows[t.split].long()
                     Xt = X[tr].double()
@@ -154,7 +165,12 @@ class PCAFamily(Family):
                 score = -math.inf
             else:
                 ll = -0.5 * ((Z * Z) / lam_d).sum(1) - 0.5 * (d * math.log(2 * math.pi) + torch.log(lam_d).sum())
-                score = float(ll.mean())
+                if sharded:   # mean over the GLOBAL held-out rows
+                    acc = data.all_reduce(torch.stack([ll.sum(), torch.tensor(float(ll.numel()), dtype=ll.dtype,
+                                                                              device=ll.device)]))
+                    score = float(acc[0] / acc[1].clamp_min(1))
+                else:
+                    score = float(ll.mean())
             o = FitOutput(task_id=t.task_id, info={"score": score, "n_components": k,
                                                    "warnings": t.params["warnings"]})
             if keep_models:

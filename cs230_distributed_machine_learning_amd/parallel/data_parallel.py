@@ -264,7 +264,7 @@ class RowShard(DeviceData):
         global row order).  Every rank holds the same tasks, so the collectives match."""
         for t in sorted(tasks, key=lambda t: t.task_id):
             o = outputs.get(t.task_id)
-            if o is None:
+            if o is None or o.pred is None:   # self-scored families (PCA) reduce their own score
                 continue
             cnt = self._test_counts[t.split]
             o.pred = self._gather_rows(o.pred, cnt)

@@ -18,6 +18,7 @@ RF_GRID = [{"n_estimators": 8, "max_depth": md, "min_samples_leaf": msl, "class_
           [{"n_estimators": 6, "criterion": "entropy", "max_features": 0.5, "random_state": 2}]
 KNN_GRID = [{"n_neighbors": k, "weights": w, "metric": m} for k, w, m in
             ((5, "uniform", "minkowski"), (9, "distance", "manhattan"), (3, "uniform", "chebyshev"))]
+PCA_GRID = [{"n_components": k} for k in (2, 5, "mle")] + [{"n_components": 4, "whiten": True}]
 RFR_GRID = [{"n_estimators": 5, "max_depth": 8, "random_state": 1}, {"n_estimators": 4, "min_samples_leaf": 5}]
 LR_GRID = [{"C": c, "solver": s, "class_weight": cw, "max_iter": 200}
            for c in (0.05, 1.0) for s in ("liblinear", "newton-cg") for cw in (None, "balanced")]
@@ -87,7 +88,8 @@ def _rank(rank, world, port, outq):
             _run(sh, X, yg, "SVC", [{"C": 1.0}])
         except ValueError as e:
             err = str(e)
-        outq.put(("ok", rank, lr, lin, err, rf, rfr, knn, knr))
+        pca = _run(shr, X, y_reg, "PCA", PCA_GRID, cv=3)
+        outq.put(("ok", rank, lr, lin, err, rf, rfr, knn, knr, pca))
         dist.destroy()
     except Exception:  # pragma: no cover
         import traceback
@@ -139,6 +141,11 @@ def test_row_sharded_fits_match_single_process():
     ref_knr = _run(DeviceData(X, y_reg, False), X, y_reg, "KNeighborsRegressor", KNN_GRID[:2], cv=3)
     for (cv_s, hold), (cv_r, hold_r) in zip(o0[8], ref_knr):
         assert np.allclose(cv_s, cv_r, atol=1e-9) and abs(hold - hold_r) < 1e-9
+    # row-sharded PCA: all-reduced moments and held-out log-likelihood sums
+    assert o0[9] == o1[9]
+    ref_pca = _run(DeviceData(X, y_reg, False), X, y_reg, "PCA", PCA_GRID, cv=3)
+    for (cv_s, hold), (cv_r, hold_r) in zip(o0[9], ref_pca):
+        assert np.allclose(cv_s, cv_r, rtol=1e-9, atol=1e-9), (cv_s, cv_r)
     ref_rfr = _run(DeviceData(X, y_reg, False), X, y_reg, "RandomForestRegressor", RFR_GRID, cv=3)
     for (cv_s, hold), (cv_r, hold_r) in zip(o0[6], ref_rfr):
         assert np.allclose(cv_s, cv_r, atol=0.02) and abs(hold - hold_r) < 0.02, (cv_s, cv_r)
