@@ -174,7 +174,9 @@ def _gpu_rank(rank, world, port, outq):
         X, y_cls, _ = _table(n=40000, d=48, seed=1)
         a, b = shard_bounds(len(X), world, rank)
         sh = RowShard(X[a:b], y_cls, a, True, inf.device)
-        outq.put(("ok", rank, _run(sh, X, y_cls, "LogisticRegression", GPU_GRID)))
+        lr = _run(sh, X, y_cls, "LogisticRegression", GPU_GRID)
+        knn = _run(sh, X, y_cls, "KNeighborsClassifier", KNN_GRID[:2], cv=3)
+        outq.put(("ok", rank, lr, knn))
         dist.destroy()
     except Exception:  # pragma: no cover
         import traceback
@@ -216,3 +218,9 @@ def test_row_sharded_lr_on_gpu_matches_single_process():
     for (cv_s, hold), (cv_r, hold_r) in zip(o0[2], ref):
         assert np.allclose(cv_s, cv_r, atol=2e-3), (cv_s, cv_r)
         assert abs(hold - hold_r) <= 2e-3
+    # row-sharded KNN (torch distances per shard + exact merge) vs the one-GPU HIP search
+    assert o0[3] == o1[3]
+    ref_knn = _run(DeviceData(X, y_cls, True, torch.device("cuda:0")), X, y_cls, "KNeighborsClassifier",
+                   KNN_GRID[:2], cv=3)
+    for (cv_s, hold), (cv_r, hold_r) in zip(o0[3], ref_knn):
+        assert np.allclose(cv_s, cv_r, atol=1e-3), (cv_s, cv_r)
