@@ -77,10 +77,17 @@ struct DpArgs {
   int64_t slot_of, lvl_lo, lvl_n;    // int32 [lvl_n]: slot of node lvl_lo + i (-1 none)
   // threshold refinement
   int64_t hi, binvals, exact, P_total;
+  int64_t ystride;                   // > 0: yreg is [targets][ystride], tree t regresses on row specs[t].target
 };
 
 template <typename T>
 DML_HD T* dp_ptr(int64_t v) { return (T*)(uintptr_t)v; }
+
+// regression target of (tree, local row): gradient boosting gives every tree its own row
+DML_HD float dp_target(const DpArgs& a, int tree, int64_t r) {
+  const float* y = dp_ptr<const float>(a.yreg);
+  return a.ystride ? y[(int64_t)dp_ptr<const TreeSpec>(a.specs)[tree].target * a.ystride + r] : y[r];
+}
 
 // impurity of a node's value vector
 DML_HD double dp_impurity(const double* v, int C, int is_reg, int crit) {

@@ -65,7 +65,7 @@ __global__ void k_dp_root_stats(DpArgs a) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += stride) {
     const uint32_t w = w8[r];
     if (!w) continue;
-    const double y = (double)dp_ptr<const float>(a.yreg)[r];
+    const double y = (double)dp_target(a, t, r);
     atomicAdd(&acc[0], (double)w);
     atomicAdd(&acc[1], (double)w * y);
     atomicAdd(&acc[2], (double)w * y * y);
@@ -100,7 +100,7 @@ __device__ __forceinline__ void dp_row(const DpArgs& a, int64_t p, int32_t& r, u
   r = dp_ptr<const int32_t>(a.act_row)[p];
   const int t = dp_ptr<const int32_t>(a.act_tree)[p];
   w = boot_weight(dp_ptr<const TreeSpec>(a.specs)[t], (uint32_t)(a.r0 + r));
-  if (kReg) fy = dp_ptr<const float>(a.yreg)[r];
+  if (kReg) fy = dp_target(a, t, r);
   else y = dp_ptr<const int32_t>(a.ycls)[r];
 }
 

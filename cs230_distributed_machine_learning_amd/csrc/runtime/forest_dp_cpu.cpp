@@ -43,7 +43,7 @@ static void dp_root_stats(const DpArgs& a) {
       double acc[4] = {0.0, 0.0, 0.0, 0.0};
       for (int64_t r = 0; r < a.n; ++r) {
         if (!w8[r]) continue;
-        const double w = (double)w8[r], y = (double)dp_ptr<const float>(a.yreg)[r];
+        const double w = (double)w8[r], y = (double)dp_target(a, (int)t, r);
         acc[0] += w; acc[1] += w * y; acc[2] += w * y * y; acc[3] += 1.0;
       }
       for (int c = 0; c < 4; ++c) out[c] += acc[c];
@@ -76,7 +76,7 @@ static void dp_hist(const DpArgs& a) {
           hu[(k * CH + C) * 256 + b] += 1u;
         }
       } else {
-        const float fw = (float)w, y = dp_ptr<const float>(a.yreg)[r], wy = fw * y;
+        const float fw = (float)w, y = dp_target(a, t, r), wy = fw * y;
         for (int k = 0; k < KR && fs[k] >= 0; ++k) {
           float* h = hf + (k * 4) * 256 + xr[fs[k]];
           h[0] += fw; h[256] += wy; h[512] += wy * y; h[768] += 1.f;

@@ -120,6 +120,8 @@ class GradientBoostingFamily(Family):
     classifiers = (_CLS,)
 
     binned_ok = True   # the stages only read the uint8 bins (DeviceData binned_only tables)
+    data_parallel = True   # row-sharded stages: ops/forest_dp.py trees + all-reduced line searches
+    dp_when_few = False
 
     def __init__(self):
         self.tiers = forest_ops.ForestTiers()
@@ -187,6 +189,8 @@ class GradientBoostingFamily(Family):
         K = data.n_classes if (data.classification and data.n_classes > 2) else 1
         per_fit = K * data.n * (8 + 4 + 4 + 1) * 1.5
         budget = 0.4 * torch.cuda.mem_get_info(data.device)[0] if data.is_gpu else 4e9
+        if getattr(data, "is_row_shard", False):   # every rank must cut the same batches
+            budget = float(data.all_reduce(torch.tensor([budget], dtype=torch.float64, device=data.device), "min")[0])
         cap = max(1, int(budget // max(1.0, per_fit)))
         outs: List[FitOutput] = []
         for i in range(0, len(tasks), cap):
@@ -200,6 +204,24 @@ class GradientBoostingFamily(Family):
         if rp["init_zero"]:
             return out
         loss = rp["loss"]
+        if getattr(data, "is_row_shard", False):   # global class priors / mean from summed counts
+            if loss in (LOSS_LOG, LOSS_EXP):
+                yc = data.y_cls[train].long()
+                cnt = data.all_reduce(torch.bincount(yc, minlength=max(2, K)).double())
+                pr = cnt / cnt.sum().clamp_min(1)
+                if K == 1:
+                    p = float(pr[1].clamp(_F32_EPS, 1 - _F32_EPS))
+                    logit = math.log(p / (1 - p))
+                    out[0] = logit if loss == LOSS_LOG else 0.5 * logit
+                else:
+                    lp = pr.clamp(_F32_EPS, 1 - _F32_EPS).log()
+                    out[:] = lp - lp.mean()
+                return out
+            y = data.y_reg[train].double()
+            acc = data.all_reduce(torch.stack([y.sum(), torch.tensor(float(y.numel()), dtype=torch.float64,
+                                                                     device=y.device)]))
+            out[0] = acc[0] / acc[1].clamp_min(1)
+            return out
         if loss in (LOSS_LOG, LOSS_EXP):
             yc = data.y_cls[train].long()
             if K == 1:
@@ -229,6 +251,13 @@ class GradientBoostingFamily(Family):
         split_idx = torch.tensor([t.split for t in batch], device=dev)
         train = data.roles[split_idx] == 1                                  # [F, n]
         clf = data.classification
+        sharded = getattr(data, "is_row_shard", False)
+        if sharded:
+            bad = [t for t in batch if t.params["loss"] in (LOSS_ABS, LOSS_HUBER, LOSS_QUANT) or
+                   t.params.get("n_iter_no_change")]
+            if bad:   # leaf percentiles / the held-out split are not sums over ranks
+                raise ParamError("row-sharded GradientBoosting supports squared_error, log_loss and exponential "
+                                 "losses without n_iter_no_change; run this job task-parallel")
         # early stopping (n_iter_no_change): sklearn holds out validation_fraction of the
         # fit's training rows (train_test_split, stratified for classifiers, seeded by
         # random_state) and stops when the validation loss has not improved by tol over
@@ -265,6 +294,9 @@ class GradientBoostingFamily(Family):
         gens = [torch.Generator(device="cpu").manual_seed(int(s) & 0x7FFFFFFF) for s in seeds]
         kept: List[List[Any]] = [[] for _ in range(F)]
         train_idx = [torch.nonzero(train[f]).squeeze(1) for f in range(F)]
+        if sharded:   # the global training rows (ascending), for subsample draws equal on every rank
+            cnts = [data.all_gather_equal(torch.tensor([int(ti.numel())], device=dev)).cpu().numpy() for ti in train_idx]
+            gtrain = [data._gather_rows(ti + data.r0, c) for ti, c in zip(train_idx, cnts)]
         for stage in range(max(n_est)):
             act = [f for f in range(F) if stage < n_est[f]]
             if not act:
@@ -285,11 +317,15 @@ class GradientBoostingFamily(Family):
             for a, f in enumerate(act):
                 sub = batch[f].params["subsample"]
                 if sub < 1.0:
-                    tr = train_idx[f]
+                    tr = gtrain[f] if sharded else train_idx[f]
                     m = max(1, int(sub * tr.numel()))
                     pick = torch.randperm(tr.numel(), generator=gens[f])[:m].to(dev)
                     row = torch.zeros(n, dtype=torch.bool, device=dev)
-                    row[tr[pick]] = True
+                    sel = tr[pick]
+                    if sharded:   # this rank's share of the global draw
+                        sel = sel - data.r0
+                        sel = sel[(sel >= 0) & (sel < n)]
+                    row[sel] = True
                     inbag[a] = row
                     sub_rows.append(a)
             # one role row per tree (roles = in-bag mask of its fit)
@@ -315,7 +351,25 @@ class GradientBoostingFamily(Family):
                     specs[j]["min_weight_frac"] = rp.get("min_weight_fraction_leaf", 0.0)
             limit = np.repeat([batch[f].params.get("max_leaf_nodes", 0) for f in act], K)
             ccp = np.repeat([batch[f].params.get("ccp_alpha", 0.0) for f in act], K)
-            if gpu:
+            if sharded:   # level-synchronous trees over the row shards (ops/forest_dp.py)
+                from ..ops import forest_dp
+
+                fb = forest_dp.build_dp(Xb, None, tgt, roles_t, specs, 1, True, data.r0, reduce=data.all_reduce,
+                                        comm=data, ystride=n)
+                if not gpu:
+                    fb = fb.to_numpy()
+                if limit.any():
+                    forest_ops.prune_max_leaves(fb, specs, limit)
+                if ccp.any():
+                    forest_ops.prune_ccp(fb, specs, ccp)
+                bv, ex = data.bin_values()
+                if bool(ex.any()):
+                    nodes_t = fb.nodes if gpu else torch.from_numpy(fb.nodes)
+                    fbt = forest_ops.ForestBuild(nodes_t, fb.vals, fb.n_trees, fb.VC, True, 1)
+                    forest_dp.refine_dp(fbt, Xb, roles_t, specs, data.r0, bv, ex, reduce=data.all_reduce)
+                leaf = forest_ops.apply(fb, Xb).long() if gpu else torch.from_numpy(forest_ops.apply(fb, Xb_host)).long()
+                vals = fb.vals if gpu else torch.from_numpy(fb.vals)
+            elif gpu:
                 fb = forest_ops.build_gpu(Xb, None, tgt, roles_t, specs, 1, True, self.tiers, ystride=n)
                 if limit.any():   # sklearn's best-first tree (friedman_mse and squared_error rank splits alike)
                     forest_ops.prune_max_leaves(fb, specs, limit)
@@ -363,6 +417,8 @@ class GradientBoostingFamily(Family):
                         is_exp = loss_of_tree[tree_of] == LOSS_EXP
                         hess = torch.where(is_exp, hess_exp, hess_log)
                     den = torch.zeros(P, dtype=torch.float64, device=dev).index_add_(0, lf, hess)
+                    if sharded:   # leaf sums over every rank's rows
+                        num, den = data.all_reduce(num), data.all_reduce(den)
                     newton = torch.where(den.abs() < 1e-150, torch.where(num == 0, 0.0, torch.sign(num) * 1e150),
                                          num / torch.where(den.abs() < 1e-150, torch.ones_like(den), den))
                     sel = (node_loss == LOSS_LOG) | (node_loss == LOSS_EXP)

@@ -61,7 +61,7 @@ class DpArgs(ctypes.Structure):
         "Xb ld n d r0 ycls yreg C CH VC is_reg roles specs T cw tree_W root wts "
         "act_row act_tree act_node A new_node slots best_left S_open seg_start seg_cnt "
         "srch S KR feats hist tile_s tile_off n_tiles tile_rows small_s n_small lds_feats "
-        "nodes vals P child_base next next_open slot_of lvl_lo lvl_n hi binvals exact P_total").split()]
+        "nodes vals P child_base next next_open slot_of lvl_lo lvl_n hi binvals exact P_total ystride").split()]
 
 
 Reducer = Callable[[torch.Tensor, str], torch.Tensor]   # (tensor, "sum" | "min" | "max") -> in place
@@ -99,7 +99,8 @@ def _p(t) -> int:
 
 def build_dp(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,
              specs: np.ndarray, n_classes: int, is_reg: bool, r0: int, reduce: Reducer = _no_reduce,
-             cw: Optional[np.ndarray] = None, hist_budget: int = HIST_BUDGET, comm=None) -> ForestBuild:
+             cw: Optional[np.ndarray] = None, hist_budget: int = HIST_BUDGET, comm=None,
+             ystride: int = 0) -> ForestBuild:
     """Grow the ``specs`` trees over the row shard ``Xb`` (global rows ``r0 ..``);
     ``reduce`` sums / mins tensors over the ranks.  Every rank returns the same pool.
 
@@ -118,7 +119,7 @@ def build_dp(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torc
     CH, VC = (4, 3) if is_reg else (C + 1, C)
     a = DpArgs()
     a.Xb, a.ld, a.n, a.d, a.r0 = _p(Xb), Xb.stride(0), n, d, int(r0)
-    a.ycls, a.yreg = _p(ycls), _p(yreg)
+    a.ycls, a.yreg, a.ystride = _p(ycls), _p(yreg), int(ystride)
     a.C, a.CH, a.VC, a.is_reg = C, CH, VC, int(is_reg)
     roles = roles.contiguous()
     a.roles = _p(roles)

@@ -18,6 +18,8 @@ RF_GRID = [{"n_estimators": 8, "max_depth": md, "min_samples_leaf": msl, "class_
           [{"n_estimators": 6, "criterion": "entropy", "max_features": 0.5, "random_state": 2}]
 KNN_GRID = [{"n_neighbors": k, "weights": w, "metric": m} for k, w, m in
             ((5, "uniform", "minkowski"), (9, "distance", "manhattan"), (3, "uniform", "chebyshev"))]
+GB_GRID = [{"n_estimators": 12, "max_depth": 3, "learning_rate": 0.3, "random_state": 1},
+           {"n_estimators": 8, "max_depth": 2, "subsample": 0.7, "random_state": 2}]
 PCA_GRID = [{"n_components": k} for k in (2, 5, "mle")] + [{"n_components": 4, "whiten": True}]
 RFR_GRID = [{"n_estimators": 5, "max_depth": 8, "random_state": 1}, {"n_estimators": 4, "min_samples_leaf": 5}]
 LR_GRID = [{"C": c, "solver": s, "class_weight": cw, "max_iter": 200}
@@ -89,7 +91,14 @@ def _rank(rank, world, port, outq):
         except ValueError as e:
             err = str(e)
         pca = _run(shr, X, y_reg, "PCA", PCA_GRID, cv=3)
-        outq.put(("ok", rank, lr, lin, err, rf, rfr, knn, knr, pca))
+        gbc = _run(sh, X, yg, "GradientBoostingClassifier", GB_GRID, cv=3)
+        gbr = _run(shr, X, y_reg, "GradientBoostingRegressor", GB_GRID[:1], cv=3)
+        gb_err = None
+        try:
+            _run(shr, X, y_reg, "GradientBoostingRegressor", [{"loss": "huber", "n_estimators": 3}], cv=3)
+        except AssertionError as e:
+            gb_err = str(e)
+        outq.put(("ok", rank, lr, lin, err, rf, rfr, knn, knr, pca, gbc, gbr, gb_err))
         dist.destroy()
     except Exception:  # pragma: no cover
         import traceback
@@ -146,6 +155,16 @@ def test_row_sharded_fits_match_single_process():
     ref_pca = _run(DeviceData(X, y_reg, False), X, y_reg, "PCA", PCA_GRID, cv=3)
     for (cv_s, hold), (cv_r, hold_r) in zip(o0[9], ref_pca):
         assert np.allclose(cv_s, cv_r, rtol=1e-9, atol=1e-9), (cv_s, cv_r)
+    # row-sharded boosting: regression stage trees over fp32 histograms summed across ranks
+    # (near-tie splits may differ), all-reduced Newton leaf sums, global subsample draws
+    assert o0[10] == o1[10] and o0[11] == o1[11]
+    ref_gbc = _run(DeviceData(X, y_cls, True), X, y_cls, "GradientBoostingClassifier", GB_GRID, cv=3)
+    for (cv_s, hold), (cv_r, hold_r) in zip(o0[10], ref_gbc):
+        assert np.allclose(cv_s, cv_r, atol=0.02) and abs(hold - hold_r) <= 0.02, (cv_s, cv_r)
+    ref_gbr = _run(DeviceData(X, y_reg, False), X, y_reg, "GradientBoostingRegressor", GB_GRID[:1], cv=3)
+    for (cv_s, hold), (cv_r, hold_r) in zip(o0[11], ref_gbr):
+        assert np.allclose(cv_s, cv_r, atol=0.02) and abs(hold - hold_r) <= 0.02, (cv_s, cv_r)
+    assert o0[12] and "row-sharded GradientBoosting" in o0[12]
     ref_rfr = _run(DeviceData(X, y_reg, False), X, y_reg, "RandomForestRegressor", RFR_GRID, cv=3)
     for (cv_s, hold), (cv_r, hold_r) in zip(o0[6], ref_rfr):
         assert np.allclose(cv_s, cv_r, atol=0.02) and abs(hold - hold_r) < 0.02, (cv_s, cv_r)
