@@ -170,7 +170,7 @@ def _gpu_rank(rank, world, port, outq):
         X, y = _gpu_table()
         a, b = shard_bounds(len(X), world, rank)
         sh = RowShard(X[a:b], y, a, True, inf.device)
-        outq.put(("ok", rank, _run_rf(sh)))
+        outq.put(("ok", rank, _run_rf(sh), _run_rf(sh, "GradientBoostingClassifier", GB_GRID)))
         dist.destroy()
     except Exception:  # pragma: no cover
         import traceback
@@ -189,12 +189,14 @@ RF_GRID = [{"n_estimators": 6, "max_depth": md, "class_weight": cw, "random_stat
            for md, cw in ((None, None), (9, "balanced"))]
 
 
-def _run_rf(data):
+GB_GRID = [{"n_estimators": 10, "max_depth": 3, "learning_rate": 0.3, "subsample": 0.8, "random_state": 4}]
+
+
+def _run_rf(data, model="RandomForestClassifier", grid=RF_GRID):
     from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
 
-    spec = JobSpec("RandomForestClassifier", RF_GRID, cv=3, holdout=True, test_size=0.2, random_state=1,
-                   keep_models="none")
-    res = run_candidates(data, spec, range(len(RF_GRID)))
+    spec = JobSpec(model, grid, cv=3, holdout=True, test_size=0.2, random_state=1, keep_models="none")
+    res = run_candidates(data, spec, range(len(grid)))
     assert all(r.ok for r in res), [r.error for r in res if not r.ok]
     return [(r.result["cv_scores"], r.result.get("accuracy")) for r in res]
 
@@ -224,6 +226,11 @@ def test_row_sharded_forest_two_ranks_on_gpu():
     for o in outs:
         assert o[0] == "ok", o[2]
     X, y = _gpu_table()
-    ref = _run_rf(DeviceData(X, y, True, torch.device("cuda:0")))
+    dd = DeviceData(X, y, True, torch.device("cuda:0"))
+    ref = _run_rf(dd)
     o0, o1 = sorted(outs, key=lambda o: o[1])
     assert o0[2] == o1[2] == ref, (o0[2], ref)
+    # row-sharded boosting (fp32 stage histograms summed across ranks): close to one GPU
+    assert o0[3] == o1[3]
+    for (cv_s, hold), (cv_r, hold_r) in zip(o0[3], _run_rf(dd, "GradientBoostingClassifier", GB_GRID)):
+        assert np.allclose(cv_s, cv_r, atol=0.02) and abs(hold - hold_r) <= 0.02, (cv_s, cv_r)
