@@ -13,7 +13,8 @@ matrix x coefficient products (library GEMM).  Supported: C, kernel
 (linear/poly/rbf/sigmoid), degree, gamma ('scale'/'auto'/float), coef0, tol, max_iter,
 class_weight (dict / 'balanced'), epsilon (SVR).  ``shrinking`` / ``cache_size`` only
 affect libsvm's speed and are accepted and ignored; ``probability=True`` does not change
-``predict`` and is ignored (reported), ``break_ties=True`` is reported.
+``predict`` and is ignored (reported); ``break_ties=True`` predicts the argmax of
+sklearn's one-vs-rest decision function (votes + squashed summed confidences).
 """
 from __future__ import annotations
 
@@ -51,6 +52,24 @@ CACHE_MAX_GB = 24.0          # ... and at most this much (DML_SVM_CACHE_GB)
 MIN_ROWS_PER_WG = 1024       # split a problem over workgroups only down to this slice size
 
 
+
+def _ovr_argmax(dec, ti, pairs, m, C, dev) -> torch.Tensor:
+    """sklearn SVC(break_ties=True): argmax of the one-vs-rest decision function built from
+    the one-vs-one values (sklearn.utils.multiclass._ovr_decision_function: votes plus
+    summed confidences squashed into (-1/3, 1/3))."""
+    votes = torch.zeros((m, C), dtype=torch.float64, device=dev)
+    conf = torch.zeros((m, C), dtype=torch.float64, device=dev)
+    for pi, (a_, b_) in enumerate(pairs):
+        dv = dec.get((ti, pi))
+        if dv is None:
+            continue
+        dv = dv.double()
+        conf[:, a_] += dv
+        conf[:, b_] -= dv
+        votes[:, a_] += (dv >= 0).double()
+        votes[:, b_] += (dv < 0).double()
+    return (votes + conf / (3 * (conf.abs() + 1))).argmax(1).to(torch.int32)
+
 class SVMFamily(Family):
     model_types = (_SVC, _SVR)
     classifiers = (_SVC,)
@@ -87,8 +106,9 @@ class SVMFamily(Family):
             out["class_weight"] = cw
             if as_bool(p["probability"], "probability"):
                 warn.append("probability=True: Platt scaling not computed (predict is unaffected)")
-            if as_bool(p["break_ties"], "break_ties"):
-                warn.append("break_ties=True not supported; one-vs-one vote ties go to the lower class")
+            out["break_ties"] = as_bool(p["break_ties"], "break_ties")
+            if out["break_ties"] and p["decision_function_shape"] == "ovo":
+                raise ParamError("break_ties must be False when decision_function_shape is 'ovo'")
         return out
 
     def cost(self, model_type, rp, n_train, n_features, n_classes) -> float:
@@ -211,6 +231,8 @@ class SVMFamily(Family):
                     votes[:, a_] += (dv > 0).int()
                     votes[:, b_] += (dv <= 0).int()
                 pred = votes.argmax(1).to(torch.int32)      # first max = lowest class (libsvm vote)
+                if t.params.get("break_ties") and C_cls > 2:
+                    pred = _ovr_argmax(dec, ti, pairs, te.numel(), C_cls, dev)
             o = FitOutput(task_id=t.task_id, pred=pred, fit_seconds=dt / len(tasks),
                           info={"warnings": t.params["warnings"]})
             if keep_models:

@@ -384,3 +384,22 @@ def test_linear_regression_positive_matches_sklearn(fit_intercept):
     assert (m["coef"] >= 0).all()
     np.testing.assert_allclose(m["coef"], sk.coef_, atol=2e-5)
     assert abs(m["intercept"] - sk.intercept_) < 2e-5
+
+
+def test_svc_break_ties_matches_sklearn():
+    """break_ties=True: argmax of sklearn's one-vs-rest decision function."""
+    from sklearn.datasets import make_blobs
+    from sklearn.svm import SVC
+
+    from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
+
+    X, y = make_blobs(240, 3, centers=4, cluster_std=3.0, random_state=2)
+    grid = [{"C": 0.5, "break_ties": True}, {"C": 0.5, "break_ties": False}]
+    spec = JobSpec("SVC", grid, cv=3, holdout=False, keep_models="none")
+    res = run_candidates(DeviceData(X, y, True, "cpu"), spec, range(2))
+    assert all(r.ok for r in res), [r.error for r in res]
+    from sklearn.model_selection import StratifiedKFold, cross_val_score
+
+    for r, g in zip(res, grid):
+        ref = cross_val_score(SVC(**g), X, y, cv=StratifiedKFold(3))
+        assert np.allclose(r.result["cv_scores"], ref, atol=1e-12), (g, r.result["cv_scores"], ref)
