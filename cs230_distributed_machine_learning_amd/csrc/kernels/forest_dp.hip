@@ -173,29 +173,27 @@ __global__ void __launch_bounds__(kDpBlock) k_dp_hist_small(DpArgs a) {
   const int32_t* fs = dp_ptr<const int32_t>(a.feats) + (int64_t)s * KR;
   const uint8_t* Xb = dp_ptr<const uint8_t>(a.Xb);
   uint32_t* gh = dp_ptr<uint32_t>(a.hist) + (int64_t)s * KR * CH * 256;
-  // lanes over (pair, position): a node of m pairs keeps min(64, m x KR) lanes busy (one
-  // lane per pair would leave most of the wave idle on the few-row nodes of deep levels)
-  int kv = KR;
-  while (kv > 0 && fs[kv - 1] < 0) --kv;            // positions past d carry no feature
-  const int64_t work = cnt * kv;
-  for (int64_t j = lane; j < work; j += 64) {
-    const int64_t i = j / kv;
-    const int k = (int)(j - i * kv);
+  for (int64_t i = lane; i < cnt; i += 64) {
     int32_t r, y = 0;
     uint32_t w;
     float fy = 0.f;
     dp_row<kReg>(a, seg0 + i, r, w, y, fy);
-    const int b = Xb[(int64_t)r * a.ld + fs[k]];
-    if (kReg) {
-      const float fw = (float)w, wy = fw * fy;
-      float* h = (float*)gh + (k * 4) * 256 + b;
-      atomicAdd(h, fw);
-      atomicAdd(h + 256, wy);
-      atomicAdd(h + 512, wy * fy);
-      atomicAdd(h + 768, 1.f);
-    } else {
-      atomicAdd(&gh[(k * CH + y) * 256 + b], w);
-      atomicAdd(&gh[(k * CH + C) * 256 + b], 1u);
+    const uint8_t* xr = Xb + (int64_t)r * a.ld;
+    for (int k = 0; k < KR; ++k) {
+      const int f = fs[k];
+      if (f < 0) break;
+      const int b = xr[f];
+      if (kReg) {
+        const float fw = (float)w, wy = fw * fy;
+        float* h = (float*)gh + (k * 4) * 256 + b;
+        atomicAdd(h, fw);
+        atomicAdd(h + 256, wy);
+        atomicAdd(h + 512, wy * fy);
+        atomicAdd(h + 768, 1.f);
+      } else {
+        atomicAdd(&gh[(k * CH + y) * 256 + b], w);
+        atomicAdd(&gh[(k * CH + C) * 256 + b], 1u);
+      }
     }
   }
 }
