@@ -234,3 +234,66 @@ def test_row_sharded_forest_two_ranks_on_gpu():
     assert o0[3] == o1[3]
     for (cv_s, hold), (cv_r, hold_r) in zip(o0[3], _run_rf(dd, "GradientBoostingClassifier", GB_GRID)):
         assert np.allclose(cv_s, cv_r, atol=0.02) and abs(hold - hold_r) <= 0.02, (cv_s, cv_r)
+
+
+def _w3_data():
+    rng = np.random.default_rng(5)
+    X = rng.normal(size=(7001, 9)).astype(np.float32)
+    X[:, 2] = rng.integers(0, 3, 7001)
+    y = ((X[:, 0] + X[:, 2] + rng.normal(size=7001)) > 0.7).astype(np.int64) + (X[:, 1] > 1)
+    return X, y
+
+
+def _w3_rank(rank, world, port, outq):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), OMP_NUM_THREADS="2")
+    try:
+        from cs230_distributed_machine_learning_amd.parallel import dist
+        from cs230_distributed_machine_learning_amd.parallel.data_parallel import RowShard, shard_bounds
+
+        inf = dist.init(want_gpu=False, timeout_s=120)
+        X, y = _w3_data()
+        a, b = shard_bounds(len(X), world, rank)
+        sh = RowShard(X[a:b], y, a, True, inf.device)
+        sh.set_splits(np.ones((1, len(X)), np.uint8), ["full"])
+        specs = _specs(5, 9, crit=1, mf=3)
+        specs["split"] = 0
+        fb = forest_dp.build_dp(sh.binned(), sh.y_cls, None, sh.roles, specs, 3, False, sh.r0, reduce=sh.all_reduce,
+                                comm=sh)
+        outq.put(("ok", rank, canon(fb, 5)))
+        dist.destroy()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        outq.put(("err", rank, traceback.format_exc()))
+
+
+def test_dp_builder_three_ranks_gloo():
+    """Odd world size: node ownership padded to a multiple of 3, sparse small-node gathers
+    of unequal length -- every rank grows the one-process trees."""
+    import torch.multiprocessing as mp
+
+    from cs230_distributed_machine_learning_amd.data.device import DeviceData
+
+    X, y = _w3_data()
+    dd = DeviceData(X, y, True)
+    specs = _specs(5, 9, crit=1, mf=3)
+    specs["split"] = 0
+    ref = canon(forest_ops.build_cpu(dd.binned().numpy(), dd.y_enc, None, np.ones((1, len(X)), np.uint8), specs, 3,
+                                     False), 5)
+    world, port = 3, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_w3_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        outs = [q.get(timeout=300) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for o in outs:
+        assert o[0] == "ok", o[2]
+        assert o[2] == ref
