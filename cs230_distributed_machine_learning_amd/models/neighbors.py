@@ -196,6 +196,29 @@ def _merge_topk(d_parts: torch.Tensor, i_parts: torch.Tensor, y_parts: torch.Ten
     return d.gather(1, o2)[:, :K], y.gather(1, o2)[:, :K]
 
 
+class _QueryTable:
+    """This rank's rows followed by the gathered held-out rows of every split, as one table
+    for ``knn_search_hip``: candidates are this rank's training rows (role 1), queries are
+    the appended rows (role 0), so the HIP kernels search other ranks' queries unchanged."""
+
+    def __init__(self, data, Qs: Dict[int, torch.Tensor]):
+        self.device, self.d, n = data.device, data.d, data.n
+        self.X = torch.cat([data.X] + [Qs[s] for s in sorted(Qs)]).contiguous()
+        self.n = int(self.X.shape[0])
+        self.roles = torch.zeros((data.roles.shape[0], self.n), dtype=torch.uint8, device=self.device)
+        self.roles[:, :n] = data.roles
+        self.test_rows, off = {}, n
+        for s in sorted(Qs):
+            m = int(Qs[s].shape[0])
+            self.test_rows[s] = torch.arange(off, off + m, dtype=torch.int32, device=self.device)
+            off += m
+
+    def feature_major(self) -> torch.Tensor:
+        if getattr(self, "_XT", None) is None:
+            self._XT = self.X.t().contiguous()
+        return self._XT
+
+
 def knn_search_sharded(data, splits: List[int], K: int, metric: int, p: float, y: torch.Tensor):
     """Row-sharded search (parallel/data_parallel.py RowShard): every rank searches ALL
     of a split's held-out rows (one all-gather of their features) against its OWN training
@@ -205,9 +228,14 @@ def knn_search_sharded(data, splits: List[int], K: int, metric: int, p: float, y
     the same way (lower global row id)."""
     out = {}
     world, rank = data.world, data.rank
+    Qs = {s: data._gather_rows(data.X[data.test_rows[s].long()], data._test_counts[s]) for s in splits}
+    hip = None
+    # the HIP search (MFMA for L2) needs K candidates on this rank for every split
+    if data.is_gpu and K <= KERNEL_KMAX and all(int(data.train_rows[s].numel()) >= K for s in splits):
+        hip = knn_search_hip(_QueryTable(data, Qs), splits, K, metric, p)
     for s in splits:
         cnt = data._test_counts[s]
-        Q = data._gather_rows(data.X[data.test_rows[s].long()], cnt)          # [m_glob, d]
+        Q = Qs[s]                                                              # [m_glob, d]
         tr = data.train_rows[s].long()
         R = data.X[tr]
         m = Q.shape[0]
@@ -216,7 +244,10 @@ def knn_search_sharded(data, splits: List[int], K: int, metric: int, p: float, y
         dd = torch.full((m, K), big, dtype=torch.float32, device=Q.device)
         ii = torch.full((m, K), 2 ** 62, dtype=torch.long, device=Q.device)
         yy = torch.zeros((m, K), dtype=y.dtype, device=Q.device)
-        if k_loc > 0 and m > 0:
+        if hip is not None:   # indices < data.n: this rank's rows
+            acc, idx = hip[s]
+            dd, ii, yy = acc.float(), idx + data.r0, y[idx]
+        elif k_loc > 0 and m > 0:
             step = max(1, (1 << 24) // max(1, R.shape[0] * max(1, data.d // 8)))
             for q0 in range(0, m, step):
                 D = _acc_torch(Q[q0:q0 + step], R, metric, p)
