@@ -262,6 +262,9 @@ class ForestFamily(Family):
         budget = self._budget(data)
         if sharded:   # every rank must form the SAME batches: the smallest budget of the group
             budget = float(data.all_reduce(torch.tensor([budget], dtype=torch.float64, device=data.device), "min")[0])
+            # trees per level-synchronous build: the (tree, row) pair arrays take ~26 B per
+            # tree and local row (ops/forest_dp.py build_dp tree_chunk)
+            self._dp_tree_chunk = max(1, int(budget // max(1.0, data.n * 26.0)))
         outs: Dict[int, FitOutput] = {}
         # batches of whole fits under the memory budget (on the device: the builder's real
         # workspace + node-pool bytes, the same rule ``presize`` sizes the arena with)
@@ -381,7 +384,8 @@ class ForestFamily(Family):
             from ..ops import forest_dp
 
             fb = forest_dp.build_dp(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
-                                    data.n_classes, is_reg, data.r0, reduce=data.all_reduce, cw=cw, comm=data)
+                                    data.n_classes, is_reg, data.r0, reduce=data.all_reduce, cw=cw, comm=data,
+                                    tree_chunk=getattr(self, "_dp_tree_chunk", None))
         elif data.is_gpu:
             fb = forest_ops.build_gpu(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
                                       data.n_classes, is_reg, self.tiers, reuse_pool=True,

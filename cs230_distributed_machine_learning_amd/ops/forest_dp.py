@@ -97,19 +97,12 @@ def _p(t) -> int:
     return 0 if t is None else int(t.data_ptr())
 
 
-def build_dp(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,
-             specs: np.ndarray, n_classes: int, is_reg: bool, r0: int, reduce: Reducer = _no_reduce,
-             cw: Optional[np.ndarray] = None, hist_budget: int = HIST_BUDGET, comm=None,
-             ystride: int = 0) -> ForestBuild:
-    """Grow the ``specs`` trees over the row shard ``Xb`` (global rows ``r0 ..``);
-    ``reduce`` sums / mins tensors over the ranks.  Every rank returns the same pool.
-
-    ``comm`` (world > 1; ``RowShard`` provides it): ``reduce_scatter_rows`` /
-    ``all_gather_equal`` / ``rank`` / ``world``.  Each level-round's histograms are then
-    REDUCE-SCATTERED by node: rank k receives the global sums of 1/N of the searching
-    nodes only, evaluates just those, and one all-gather of the (64 B slot + best-left
-    sums) records makes every rank's decisions identical again.  Over a ring that moves
-    half the bytes of an all-reduce, and the split evaluation is divided by N."""
+def _build_chunk(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,
+                 specs: np.ndarray, n_classes: int, is_reg: bool, r0: int, reduce: Reducer = _no_reduce,
+                 cw: Optional[np.ndarray] = None, hist_budget: int = HIST_BUDGET, comm=None,
+                 ystride: int = 0) -> ForestBuild:
+    """One level-synchronous build of every tree of ``specs`` (``build_dp`` documents the
+    arguments and the collectives)."""
     dev = Xb.device
     L = _Lib(dev)
     t0 = time.perf_counter()
@@ -311,6 +304,68 @@ def build_dp(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torc
     stats.update(nodes=P, build_s=time.perf_counter() - t0)
     fb = ForestBuild(nodes[:P], vals[:P], T, VC, is_reg, int(n_classes), stats)
     fb.dp_specs_dev = specs_dev
+    return fb
+
+
+def build_dp(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,
+             specs: np.ndarray, n_classes: int, is_reg: bool, r0: int, reduce: Reducer = _no_reduce,
+             cw: Optional[np.ndarray] = None, hist_budget: int = HIST_BUDGET, comm=None,
+             ystride: int = 0, tree_chunk: Optional[int] = None) -> ForestBuild:
+    """Grow the ``specs`` trees over the row shard ``Xb`` (global rows ``r0 ..``);
+    ``reduce`` sums / mins tensors over the ranks.  Every rank returns the same pool.
+
+    ``comm`` (world > 1; ``RowShard`` provides it): ``reduce_scatter_rows`` /
+    ``all_gather_equal`` / ``rank`` / ``world``.  Each level-round's histograms are then
+    REDUCE-SCATTERED by node: rank k receives the global sums of 1/N of the searching
+    nodes only, evaluates just those, and one all-gather of the (64 B slot + best-left
+    sums) records makes every rank's decisions identical again.  Over a ring that moves
+    half the bytes of an all-reduce, and the split evaluation is divided by N.
+
+    ``tree_chunk``: grow at most this many trees at a time (the (tree, row) pair arrays
+    cost ~26 B per tree and local row: a 1000-tree fit on a 25M-row shard would need
+    650 GB at once); the chunks' pools are concatenated into the one-build layout."""
+    T = len(specs)
+    tc = T if not tree_chunk else max(1, min(T, int(tree_chunk)))
+    if tc >= T:
+        return _build_chunk(Xb, ycls, yreg, roles, specs, n_classes, is_reg, r0, reduce, cw, hist_budget, comm,
+                            ystride)
+    parts = []
+    for t0 in range(0, T, tc):
+        t1 = min(T, t0 + tc)
+        parts.append(_build_chunk(Xb, ycls, yreg, roles, specs[t0:t1], n_classes, is_reg, r0, reduce,
+                                  None if cw is None else np.ascontiguousarray(cw[t0:t1]), hist_budget, comm,
+                                  ystride))
+    return _concat_pools(parts, T)
+
+
+def _concat_pools(parts, T: int) -> ForestBuild:
+    """Pools of consecutive tree chunks -> one pool in the builders' layout (tree t's root
+    at node t, every other node after the roots, child pairs adjacent)."""
+    dev = parts[0].nodes.device
+    P_total = T + sum(int(p.nodes.shape[0]) - p.n_trees for p in parts)
+    nodes = torch.empty((P_total, 2), dtype=torch.int32, device=dev)
+    vals = torch.empty((P_total, parts[0].VC), dtype=torch.float64, device=dev)
+    root_base, rest = 0, T
+    stats = {}
+    for p in parts:
+        Pc, Tc = int(p.nodes.shape[0]), p.n_trees
+        m = torch.empty(Pc, dtype=torch.int64, device=dev)
+        m[:Tc] = torch.arange(root_base, root_base + Tc, device=dev)
+        m[Tc:] = torch.arange(rest, rest + Pc - Tc, device=dev)
+        nd = p.nodes.clone()
+        internal = nd[:, 1] >= 0
+        nd[internal, 1] = m[nd[internal, 1].long()].to(torch.int32)
+        nodes[m] = nd
+        vals[m] = p.vals
+        root_base += Tc
+        rest += Pc - Tc
+        for k, v in p.stats.items():
+            if isinstance(v, (int, float)):
+                stats[k] = stats.get(k, 0) + v
+    stats["nodes"] = P_total
+    stats["tree_chunks"] = len(parts)
+    fb = ForestBuild(nodes, vals, T, parts[0].VC, parts[0].is_reg, parts[0].n_classes, stats)
+    fb.dp_specs_dev = None
     return fb
 
 

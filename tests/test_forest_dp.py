@@ -297,3 +297,21 @@ def test_dp_builder_three_ranks_gloo():
     for o in outs:
         assert o[0] == "ok", o[2]
         assert o[2] == ref
+
+
+def test_dp_builder_tree_chunks_concatenate_to_one_pool():
+    """tree_chunk: trees grown a few at a time land in the one-build pool layout."""
+    Xb, y, _, roles = _data(n=1500)
+    T = 7
+    specs = _specs(T, Xb.shape[1], cw_mode=2)
+    cw = np.ones((T, 3))
+    ref = forest_ops.build_cpu(Xb.numpy(), y, None, roles, specs, 3, False, cw=cw.copy())
+    dp = forest_dp.build_dp(Xb, torch.from_numpy(y), None, torch.from_numpy(roles), specs, 3, False, 0,
+                            cw=cw.copy(), tree_chunk=3)
+    assert dp.stats["tree_chunks"] == 3
+    assert canon(ref, T) == canon(dp, T)
+    n = Xb.shape[0]
+    rows = np.arange(n, dtype=np.int32)
+    toff, roff = np.array([0, 3, T]), np.array([0, n // 2, n])
+    assert np.array_equal(forest_ops.predict(ref, Xb.numpy(), toff, roff, rows),
+                          forest_ops.predict(dp.to_numpy(), Xb.numpy(), toff, roff, rows))
