@@ -262,9 +262,9 @@ class ForestFamily(Family):
         budget = self._budget(data)
         if sharded:   # every rank must form the SAME batches: the smallest budget of the group
             budget = float(data.all_reduce(torch.tensor([budget], dtype=torch.float64, device=data.device), "min")[0])
-            # trees per level-synchronous build: the (tree, row) pair arrays take ~26 B per
-            # tree and local row (ops/forest_dp.py build_dp tree_chunk)
-            self._dp_tree_chunk = max(1, int(budget // max(1.0, data.n * 26.0)))
+        # row shard: trees per level-synchronous build -- the (tree, row) pair arrays take
+        # ~26 B per tree and local row (ops/forest_dp.py build_dp tree_chunk)
+        tree_chunk = max(1, int(budget // max(1.0, data.n * 26.0))) if sharded else None
         outs: Dict[int, FitOutput] = {}
         # batches of whole fits under the memory budget (on the device: the builder's real
         # workspace + node-pool bytes, the same rule ``presize`` sizes the arena with)
@@ -305,7 +305,7 @@ class ForestFamily(Family):
                   f"{[len(b) for b in batches]}", file=sys.stderr, flush=True)
         for batch in batches:
             with trace.range("forest_batch"):
-                out_b = self._run_batch(data, Xb, batch, is_reg, keep_models)
+                out_b = self._run_batch(data, Xb, batch, is_reg, keep_models, tree_chunk)
             for o in out_b:
                 outs[o.task_id] = o
         return [outs[t.task_id] for t in tasks]
@@ -375,7 +375,8 @@ class ForestFamily(Family):
             i += n
         return tab
 
-    def _run_batch(self, data, Xb, batch: List[FitTask], is_reg: bool, keep_models: bool) -> List[FitOutput]:
+    def _run_batch(self, data, Xb, batch: List[FitTask], is_reg: bool, keep_models: bool,
+                   tree_chunk: int | None = None) -> List[FitOutput]:
         specs = self._specs(batch)
         cw = self.class_weight_table(data, batch, specs)
         t0 = time.perf_counter()
@@ -385,7 +386,7 @@ class ForestFamily(Family):
 
             fb = forest_dp.build_dp(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
                                     data.n_classes, is_reg, data.r0, reduce=data.all_reduce, cw=cw, comm=data,
-                                    tree_chunk=getattr(self, "_dp_tree_chunk", None))
+                                    tree_chunk=tree_chunk)
         elif data.is_gpu:
             fb = forest_ops.build_gpu(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
                                       data.n_classes, is_reg, self.tiers, reuse_pool=True,
