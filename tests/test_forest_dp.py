@@ -315,3 +315,24 @@ def test_dp_builder_tree_chunks_concatenate_to_one_pool():
     toff, roff = np.array([0, 3, T]), np.array([0, n // 2, n])
     assert np.array_equal(forest_ops.predict(ref, Xb.numpy(), toff, roff, rows),
                           forest_ops.predict(dp.to_numpy(), Xb.numpy(), toff, roff, rows))
+
+
+@pytest.mark.gpu
+def test_dp_builder_gpu_regression_and_poisson():
+    """Regression (fp32 LDS tiles + atomics, sequential-bin split kernel) and Poisson on the
+    GPU vs the C++ builder: float sums in another order, so predictions agree closely."""
+    Xb, _, yr, roles = _data(n=50000, d=20, seed=3)
+    X, E = _data.last
+    dev = torch.device("cuda:0")
+    Xg = binning.bin_matrix(torch.from_numpy(X).to(dev), E.to(dev))
+    n = Xb.shape[0]
+    rows = np.arange(n, dtype=np.int32)
+    for crit, y in ((2, yr), (3, np.exp(yr / np.abs(yr).max()).astype(np.float32))):
+        specs = _specs(4, 20, crit=crit, mf=10, msl=3)
+        ref = forest_ops.build_cpu(Xb.numpy(), None, y, roles, specs, 1, True)
+        dp = forest_dp.build_dp(Xg, None, torch.from_numpy(y).to(dev), torch.from_numpy(roles).to(dev), specs, 1,
+                                True, 0)
+        pr = forest_ops.predict(ref, Xb.numpy(), np.array([0, 4]), np.array([0, n]), rows)
+        pd = forest_ops.predict(dp, Xg, np.array([0, 4]), np.array([0, n]), torch.from_numpy(rows).to(dev)).cpu().numpy()
+        r2 = 1 - np.sum((pd - pr) ** 2) / np.sum((pr - pr.mean()) ** 2)
+        assert r2 > 0.99, (crit, r2)
