@@ -11,6 +11,7 @@ every test row of every split; each candidate (n_neighbors, weights) then votes 
 prefix of those lists.  Neighbour search is exact, so predictions match sklearn's
 brute/kd/ball algorithms except where equal distances make the k-th neighbour
 ambiguous (ties resolved by lower row index here; parity unpinned for exact ties).
+``metric="cosine"`` is a library GEMM over unit rows (sklearn's cosine_distances).
 ``algorithm`` / ``leaf_size`` only pick sklearn's search structure and are accepted
 and ignored.
 """
@@ -29,11 +30,12 @@ from .base import Family, FitOutput, FitTask, ParamError, as_int, as_float, regi
 
 _DEFAULTS = {"n_neighbors": 5, "weights": "uniform", "algorithm": "auto", "leaf_size": 30, "p": 2,
              "metric": "minkowski", "metric_params": None, "n_jobs": None}
-M_L2, M_L1, M_LINF, M_P = 0, 1, 2, 3
+M_L2, M_L1, M_LINF, M_P, M_COS = 0, 1, 2, 3, 4
 KERNEL_KMAX = 64
 
 _METRICS = {"euclidean": (M_L2, 2.0), "l2": (M_L2, 2.0), "manhattan": (M_L1, 1.0), "cityblock": (M_L1, 1.0),
-            "l1": (M_L1, 1.0), "chebyshev": (M_LINF, math.inf), "infinity": (M_LINF, math.inf)}
+            "l1": (M_L1, 1.0), "chebyshev": (M_LINF, math.inf), "infinity": (M_LINF, math.inf),
+            "cosine": (M_COS, 0.0)}
 
 
 def metric_code(metric: str, p) -> Tuple[int, float]:
@@ -51,7 +53,7 @@ def metric_code(metric: str, p) -> Tuple[int, float]:
         return M_P, p
     if metric in _METRICS:
         return _METRICS[metric]
-    raise ParamError(f"metric {metric!r} is not supported (minkowski/euclidean/manhattan/chebyshev)")
+    raise ParamError(f"metric {metric!r} is not supported (minkowski/euclidean/manhattan/chebyshev/cosine)")
 
 
 def finish_distance(acc: torch.Tensor, metric: int, p: float) -> torch.Tensor:
@@ -63,8 +65,15 @@ def finish_distance(acc: torch.Tensor, metric: int, p: float) -> torch.Tensor:
     return acc
 
 
+def _unit_rows(A: torch.Tensor) -> torch.Tensor:
+    n = torch.linalg.vector_norm(A, dim=1, keepdim=True)
+    return A / torch.where(n > 0, n, torch.ones_like(n))     # zero rows stay zero (sklearn normalize)
+
+
 def _acc_torch(Q: torch.Tensor, R: torch.Tensor, metric: int, p: float) -> torch.Tensor:
     """Accumulator-space distances [q, r] (same quantity the kernel ranks by)."""
+    if metric == M_COS:   # sklearn cosine_distances: clip(1 - <q/|q|, r/|r|>, 0, 2); a library GEMM
+        return (1.0 - _unit_rows(Q) @ _unit_rows(R).t()).clamp(0.0, 2.0)
     diff = (Q[:, None, :] - R[None, :, :]).abs()
     if metric == M_L2:
         return (diff * diff).sum(2)
@@ -231,7 +240,8 @@ def knn_search_sharded(data, splits: List[int], K: int, metric: int, p: float, y
     Qs = {s: data._gather_rows(data.X[data.test_rows[s].long()], data._test_counts[s]) for s in splits}
     hip = None
     # the HIP search (MFMA for L2) needs K candidates on this rank for every split
-    if data.is_gpu and K <= KERNEL_KMAX and all(int(data.train_rows[s].numel()) >= K for s in splits):
+    if (data.is_gpu and K <= KERNEL_KMAX and metric != M_COS
+            and all(int(data.train_rows[s].numel()) >= K for s in splits)):
         hip = knn_search_hip(_QueryTable(data, Qs), splits, K, metric, p)
     for s in splits:
         cnt = data._test_counts[s]
@@ -315,7 +325,7 @@ class KNeighborsFamily(Family):
             kmax = max(t.params["n_neighbors"] for t in ok)
             if getattr(data, "is_row_shard", False):
                 nb = knn_search_sharded(data, splits, kmax, metric, p, y)
-            elif data.is_gpu and kmax <= KERNEL_KMAX:
+            elif data.is_gpu and kmax <= KERNEL_KMAX and metric != M_COS:
                 nb = {s: (a, y[i]) for s, (a, i) in knn_search_hip(data, splits, kmax, metric, p).items()}
             else:
                 nb = {s: (a, y[i]) for s, (a, i) in ((s, knn_search_torch(data.X, data.test_rows[s], data.train_rows[s],

@@ -403,3 +403,22 @@ def test_svc_break_ties_matches_sklearn():
     for r, g in zip(res, grid):
         ref = cross_val_score(SVC(**g), X, y, cv=StratifiedKFold(3))
         assert np.allclose(r.result["cv_scores"], ref, atol=1e-12), (g, r.result["cv_scores"], ref)
+
+
+def test_knn_cosine_matches_sklearn():
+    from sklearn.model_selection import StratifiedKFold, cross_val_score
+    from sklearn.neighbors import KNeighborsClassifier
+
+    from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
+
+    rng = np.random.default_rng(8)
+    X = rng.normal(size=(300, 6))
+    X[:5] = 0.0                                      # zero rows: cosine distance 1 to everything
+    y = (X[:, 0] * X[:, 1] > 0).astype(np.int64)
+    grid = [{"n_neighbors": k, "metric": "cosine", "weights": w} for k, w in ((5, "uniform"), (7, "distance"))]
+    res = run_candidates(DeviceData(X, y, True, "cpu"), JobSpec("KNeighborsClassifier", grid, cv=3, holdout=False,
+                                                                keep_models="none"), range(2))
+    assert all(r.ok for r in res), [r.error for r in res]
+    for r, g in zip(res, grid):
+        ref = cross_val_score(KNeighborsClassifier(**g), X.astype(np.float32), y, cv=StratifiedKFold(3))
+        assert np.allclose(r.result["cv_scores"], ref, atol=1e-12), (g, r.result["cv_scores"], ref)
