@@ -118,6 +118,9 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
     if sharded and not getattr(fam, "data_parallel", False):
         raise ValueError(f"{spec.model_type} has no row-sharded (data-parallel) fit; run it task-parallel")
     tasks, errors = build_tasks(data, spec, candidate_ids)
+    if scoring_mod.needs_proba(scorer):   # families that only predict labels by default add probabilities
+        for t in tasks:
+            t.need_proba = True
     if data.is_gpu and not getattr(fam, "uses_forest_arena", False):
         from ..ops import forest_ops
 

@@ -27,6 +27,7 @@ class FitTask:
     params: Dict[str, Any]
     seed: int = 0
     keep: bool = True           # with keep_models: this fit's model is wanted (holdout fits only, when there is one)
+    need_proba: bool = False    # the job's scorer reads class probabilities (roc_auc, neg_log_loss, ...)
 
 
 @dataclass

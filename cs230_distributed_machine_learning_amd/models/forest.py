@@ -417,13 +417,17 @@ class ForestFamily(Family):
             rows = [data.test_rows[t.split] for t in batch]
             roff = np.zeros(len(batch) + 1, dtype=np.int64)
             np.cumsum([int(r.numel()) for r in rows], out=roff[1:])
+            want_proba = (not is_reg) and any(t.need_proba for t in batch)
+            proba = None
             if data.is_gpu:
                 rows_cat = torch.cat(rows) if rows else torch.empty(0, dtype=torch.int32, device=data.device)
-                pred = forest_ops.predict(fb, Xb, toff, roff, rows_cat)
+                pred = forest_ops.predict(fb, Xb, toff, roff, rows_cat, want_proba=want_proba)
             else:
                 rows_cat = np.concatenate([r.numpy() for r in rows]) if rows else np.zeros(0, np.int32)
-                pred = forest_ops.predict(fb, Xb.numpy(), toff, roff, rows_cat)
-                pred = torch.from_numpy(pred)
+                pred = forest_ops.predict(fb, Xb.numpy(), toff, roff, rows_cat, want_proba=want_proba)
+                pred = (torch.from_numpy(pred[0]), torch.from_numpy(pred[1])) if want_proba else torch.from_numpy(pred)
+            if want_proba:   # sklearn predict_proba: the mean of the trees' leaf class fractions
+                pred, proba = pred
             if data.is_gpu:
                 with trace.range("forest_predict_wait"):   # refine + predict kernels drain here
                     torch.cuda.synchronize(data.device)
@@ -433,6 +437,7 @@ class ForestFamily(Family):
             for f, t in enumerate(batch):
                 share = t.params["n_estimators"] / total_trees
                 o = FitOutput(task_id=t.task_id, pred=pred[roff[f]:roff[f + 1]], fit_seconds=dt * share,
+                              proba=None if proba is None else proba[roff[f]:roff[f + 1]],
                               info={"warnings": t.params.get("warnings", []), "batch_stats": dict(fb.stats)})
                 if keep_models and t.keep:
                     o.model = extract_forest(fb, int(toff[f]), int(toff[f + 1]), data, t)

@@ -16,12 +16,24 @@ import torch
 CLS_SCORERS = (
     "accuracy", "balanced_accuracy", "f1", "f1_macro", "f1_micro", "f1_weighted", "precision", "precision_macro",
     "precision_micro", "precision_weighted", "recall", "recall_macro", "recall_micro", "recall_weighted", "roc_auc",
-    "neg_log_loss", "jaccard", "jaccard_macro",
+    "neg_log_loss", "jaccard", "jaccard_macro", "jaccard_micro", "jaccard_weighted", "matthews_corrcoef",
+    "average_precision", "neg_brier_score", "roc_auc_ovr", "roc_auc_ovr_weighted", "roc_auc_ovo",
+    "roc_auc_ovo_weighted",
 )
 REG_SCORERS = (
     "r2", "neg_mean_squared_error", "neg_mean_absolute_error", "neg_root_mean_squared_error", "explained_variance",
-    "max_error", "neg_median_absolute_error", "neg_mean_absolute_percentage_error",
+    "max_error", "neg_median_absolute_error", "neg_mean_absolute_percentage_error", "neg_mean_squared_log_error",
+    "neg_root_mean_squared_log_error", "neg_mean_poisson_deviance", "neg_mean_gamma_deviance",
+    "d2_absolute_error_score",
 )
+
+
+PROBA_SCORERS = ("roc_auc", "neg_log_loss", "average_precision", "neg_brier_score", "roc_auc_ovr",
+                 "roc_auc_ovr_weighted", "roc_auc_ovo", "roc_auc_ovo_weighted")
+
+
+def needs_proba(name) -> bool:
+    return name in PROBA_SCORERS
 
 
 def default_scoring(is_classifier: bool) -> str:
@@ -89,6 +101,58 @@ def _auc(y: torch.Tensor, s: torch.Tensor) -> float:
     return float((ranks[yo > 0.5].sum() - n1 * (n1 + 1) / 2) / (n1 * n0))
 
 
+def _average_precision(y: torch.Tensor, s: torch.Tensor) -> float:
+    """sklearn average_precision_score (binary): sum over distinct thresholds, descending,
+    of (R_n - R_{n-1}) P_n; equal scores form one threshold."""
+    order = torch.argsort(s.double(), descending=True, stable=True)
+    ss, yo = s.double()[order], y.double()[order]
+    tps = torch.cumsum(yo, 0)
+    fps = torch.cumsum(1.0 - yo, 0)
+    last = torch.ones_like(ss, dtype=torch.bool)
+    last[:-1] = ss[1:] != ss[:-1]                  # the last position of each distinct score
+    tps, fps = tps[last], fps[last]
+    P = float(tps[-1]) if tps.numel() else 0.0
+    if P == 0:
+        return float("nan")
+    prec = tps / (tps + fps)
+    rec = tps / P
+    drec = torch.diff(torch.cat([torch.zeros(1, dtype=rec.dtype, device=rec.device), rec]))
+    return float((drec * prec).sum())
+
+
+def _mcc(cm: torch.Tensor) -> float:
+    """sklearn matthews_corrcoef (multiclass form from the confusion matrix)."""
+    t_sum, p_sum = cm.sum(1), cm.sum(0)
+    n_correct, n = float(torch.diag(cm).sum()), float(cm.sum())
+    cov_ytyp = n_correct * n - float(t_sum @ p_sum)
+    cov_ypyp = n * n - float(p_sum @ p_sum)
+    cov_ytyt = n * n - float(t_sum @ t_sum)
+    if cov_ypyp * cov_ytyt == 0:
+        return 0.0
+    return cov_ytyp / math.sqrt(cov_ytyt * cov_ypyp)
+
+
+def _multiclass_auc(y: torch.Tensor, proba: torch.Tensor, C: int, kind: str, weighted: bool) -> float:
+    """sklearn roc_auc_score(multi_class="ovr" | "ovo", average="macro" | "weighted")."""
+    y = y.long()
+    prev = torch.bincount(y, minlength=C).double()
+    if kind == "ovr":
+        aucs = torch.tensor([_auc((y == k).double(), proba[:, k]) for k in range(C)], dtype=torch.float64)
+        return float((aucs * prev.cpu()).sum() / prev.sum().cpu()) if weighted else float(aucs.mean())
+    vals, wts = [], []
+    for a in range(C):
+        for b in range(a + 1, C):
+            m = (y == a) | (y == b)
+            ya, yb = (y[m] == a).double(), (y[m] == b).double()
+            vals.append((_auc(ya, proba[m, a]) + _auc(yb, proba[m, b])) / 2.0)
+            wts.append(float(m.sum()))
+    v = torch.tensor(vals, dtype=torch.float64)
+    if weighted:   # Hand & Till with prevalence weights: pair weight = share of its samples
+        w = torch.tensor(wts, dtype=torch.float64)
+        return float((v * w).sum() / w.sum())
+    return float(v.mean())
+
+
 def score(name: str, y_true: torch.Tensor, pred: torch.Tensor, n_classes: int = 2,
           proba: Optional[torch.Tensor] = None) -> float:
     """Scalar score for one fit (greater is better)."""
@@ -111,11 +175,30 @@ def score(name: str, y_true: torch.Tensor, pred: torch.Tensor, n_classes: int = 
         if proba is None or n_classes != 2:
             raise ValueError("roc_auc needs probabilities of a binary classifier")
         return _auc(y_true, proba[:, 1])
+    if name.startswith("roc_auc_ov"):
+        if proba is None:
+            raise ValueError(f"{name} needs probabilities")
+        kind = name[8:11]
+        return _multiclass_auc(y_true, proba.double(), proba.shape[1], kind, name.endswith("_weighted"))
+    if name == "average_precision":
+        if proba is None or n_classes != 2:
+            raise ValueError("average_precision needs probabilities of a binary classifier")
+        return _average_precision(y_true, proba[:, 1])
+    if name == "neg_brier_score":
+        if proba is None:
+            raise ValueError("neg_brier_score needs probabilities")
+        onehot = torch.nn.functional.one_hot(y_true.long(), proba.shape[1]).double()
+        d = proba.double() - onehot
+        if proba.shape[1] == 2:   # binary: the positive class's squared error
+            return -float((d[:, 1] ** 2).mean())
+        return -float((d * d).sum(1).mean())
+    if name == "matthews_corrcoef":
+        return _mcc(_confusion(y_true, pred, n_classes))
     if name == "neg_log_loss":
         if proba is None:
             raise ValueError("neg_log_loss needs probabilities")
-        p = proba.double().clamp(1e-15, 1 - 1e-15)
-        p = p / p.sum(1, keepdim=True)
+        eps = float(torch.finfo(torch.float64).eps)   # sklearn: the float64 predict_proba's eps
+        p = proba.double().clamp(eps, 1 - eps)
         return float(torch.log(p.gather(1, y_true.long().view(-1, 1))).mean())
     yt, yp = y_true.double(), pred.double()
     err = yp - yt
@@ -140,4 +223,27 @@ def score(name: str, y_true: torch.Tensor, pred: torch.Tensor, n_classes: int = 
         return 1.0 - float(err.var(unbiased=False)) / vt if vt > 0 else (1.0 if float(err.var()) == 0 else 0.0)
     if name == "neg_mean_absolute_percentage_error":
         return -float((err.abs() / yt.abs().clamp_min(torch.finfo(torch.float64).eps)).mean())
+    if name in ("neg_mean_squared_log_error", "neg_root_mean_squared_log_error"):
+        if bool((yt <= -1).any()) or bool((yp <= -1).any()):
+            raise ValueError("Mean Squared Logarithmic Error cannot be used when targets contain values less "
+                             "than or equal to -1.")
+        msle = float(((torch.log1p(yt) - torch.log1p(yp)) ** 2).mean())
+        return -msle if name == "neg_mean_squared_log_error" else -math.sqrt(msle)
+    if name == "neg_mean_poisson_deviance":
+        if bool((yt < 0).any()) or bool((yp <= 0).any()):
+            raise ValueError("Mean Tweedie deviance error with power=1 can only be used on non-negative y and "
+                             "strictly positive y_pred.")
+        xlogy = torch.where(yt > 0, yt * torch.log(yt / yp), torch.zeros_like(yt))
+        return -float((2.0 * (xlogy - yt + yp)).mean())
+    if name == "neg_mean_gamma_deviance":
+        if bool((yt <= 0).any()) or bool((yp <= 0).any()):
+            raise ValueError("Mean Tweedie deviance error with power=2 can only be used on strictly positive y "
+                             "and y_pred.")
+        return -float((2.0 * (torch.log(yp / yt) + yt / yp - 1.0)).mean())
+    if name == "d2_absolute_error_score":
+        num = float(err.abs().sum())
+        den = float((yt - torch.quantile(yt, 0.5)).abs().sum())
+        if den == 0.0:
+            return 1.0 if num == 0.0 else 0.0
+        return 1.0 - num / den
     raise ValueError(f"unknown scorer {name!r}")

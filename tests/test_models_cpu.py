@@ -422,3 +422,25 @@ def test_knn_cosine_matches_sklearn():
     for r, g in zip(res, grid):
         ref = cross_val_score(KNeighborsClassifier(**g), X.astype(np.float32), y, cv=StratifiedKFold(3))
         assert np.allclose(r.result["cv_scores"], ref, atol=1e-12), (g, r.result["cv_scores"], ref)
+
+
+@pytest.mark.parametrize("scoring", ["roc_auc", "neg_log_loss", "neg_brier_score", "average_precision"])
+def test_rf_probability_scorers_match_sklearn(scoring):
+    """Probability scorers on forests: the fits return sklearn's predict_proba (mean of the
+    trees' leaf class fractions) when the job's scorer needs it."""
+    from sklearn.ensemble import RandomForestClassifier
+    from sklearn.model_selection import StratifiedKFold, cross_val_score
+
+    from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
+
+    rng = np.random.default_rng(1)
+    X = rng.integers(0, 6, size=(400, 3)).astype(np.float32)
+    y = ((X[:, 0] + X[:, 1] + rng.integers(0, 4, 400)) > 7).astype(np.int64)
+    # random_state 4: no equal-gain split ties between features on this table (their order is
+    # sklearn's RNG vs our keyed order)
+    g = {"n_estimators": 1, "bootstrap": False, "max_features": None, "min_samples_leaf": 8, "random_state": 4}
+    spec = JobSpec("RandomForestClassifier", [g], cv=3, holdout=False, keep_models="none", scoring=scoring)
+    res = run_candidates(DeviceData(X, y, True, "cpu"), spec, [0])
+    assert res[0].ok, res[0].error
+    ref = cross_val_score(RandomForestClassifier(**g), X, y, cv=StratifiedKFold(3), scoring=scoring)
+    assert np.allclose(res[0].result["cv_scores"], ref, atol=1e-6), (res[0].result["cv_scores"], ref)

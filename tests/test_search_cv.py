@@ -193,3 +193,57 @@ def test_stratified_holdout_matches_sklearn():
         a, b = train_test_split(idx, test_size=0.1 + 0.05 * seed, random_state=seed, stratify=y)
         c, d = stratified_holdout_indices(y, 0.1 + 0.05 * seed, seed)
         assert np.array_equal(a, c) and np.array_equal(b, d)
+
+
+@pytest.mark.parametrize("C", [2, 4])
+@pytest.mark.parametrize("name", ["matthews_corrcoef", "jaccard_micro", "jaccard_weighted", "neg_brier_score",
+                                  "average_precision", "roc_auc_ovr", "roc_auc_ovr_weighted", "roc_auc_ovo",
+                                  "roc_auc_ovo_weighted"])
+def test_more_classification_scorers_match_sklearn(name, C):
+    """Scorer strings a GridSearchCV user passes, through sklearn's own scorer objects."""
+    from sklearn.metrics import get_scorer
+
+    if C == 2 and name.startswith("roc_auc_ov"):
+        pytest.skip("multiclass-only scorer")
+    if C > 2 and name in ("average_precision",):
+        pytest.skip("binary-only scorer")
+    rng = np.random.RandomState(5 + C)
+    y = rng.randint(0, C, 500)
+    logits = rng.randn(500, C) + 1.5 * np.eye(C)[y]
+    logits = np.round(logits, 1)                    # some tied scores
+    proba = np.exp(logits) / np.exp(logits).sum(1, keepdims=True)
+    pred = proba.argmax(1)
+
+    from sklearn.base import BaseEstimator, ClassifierMixin
+
+    class _Fixed(ClassifierMixin, BaseEstimator):
+        classes_ = np.arange(C)
+
+        def predict(self, X):
+            return pred
+
+        def predict_proba(self, X):
+            return proba
+
+    ref = get_scorer(name)(_Fixed(), np.zeros((500, 1)), y)
+    got = dsc.score(name, torch.from_numpy(y), torch.from_numpy(pred), C, torch.from_numpy(proba))
+    assert got == pytest.approx(ref, rel=1e-9, abs=1e-12), (name, got, ref)
+
+
+@pytest.mark.parametrize("name", ["neg_mean_squared_log_error", "neg_root_mean_squared_log_error",
+                                  "neg_mean_poisson_deviance", "neg_mean_gamma_deviance", "d2_absolute_error_score",
+                                  "neg_mean_absolute_percentage_error"])
+def test_more_regression_scorers_match_sklearn(name):
+    from sklearn.metrics import get_scorer
+
+    rng = np.random.RandomState(3)
+    y = np.abs(rng.randn(200) * 3) + 0.5
+    p = np.abs(y + rng.randn(200) * 0.5) + 0.05
+
+    class _Fixed:
+        def predict(self, X):
+            return p
+
+    ref = get_scorer(name)(_Fixed(), np.zeros((200, 1)), y)
+    got = dsc.score(name, torch.from_numpy(y), torch.from_numpy(p))
+    assert got == pytest.approx(ref, rel=1e-9, abs=1e-12), (name, got, ref)
