@@ -266,3 +266,33 @@ def test_gpu_family_scores_match_host_path():
         assert abs(g.result["accuracy"] - c.result["accuracy"]) <= 1e-12
         nodes = np.asarray(g.model["nodes"])
         assert set(np.unique(nodes[nodes[:, 0] < 0, 0]).tolist()) == {-1}
+
+
+@pytest.mark.gpu
+def test_gpu_predict_proba_matches_cpu():
+    """predict_proba (probability scorers): the HIP predict kernel's class fractions equal
+    the C++ predictor's for the same trees."""
+    X, y = _data(20000, 12, 3)
+    dev = torch.device("cuda:0")
+    Xt = torch.from_numpy(X).to(dev)
+    edges = binning.quantile_edges(Xt)
+    Xb = binning.bin_matrix(Xt, edges)
+    Xb_cpu = binning.bin_matrix(torch.from_numpy(X), edges.cpu()).numpy()
+    roles, _ = make_split_roles(y, 3, True, holdout=False)
+    specs = _specs(3, 6, 12, msl=4)
+    ycls = y.astype(np.int32)
+    c = forest_ops.build_cpu(Xb_cpu, ycls, None, roles, specs, 3, False)
+    g = forest_ops.ForestBuild(torch.from_numpy(c.nodes).to(dev), torch.from_numpy(c.vals).to(dev), c.n_trees, c.VC,
+                               False, 3)
+    rows, roff = [], [0]
+    for f in range(3):
+        r = np.nonzero(roles[f] == 2)[0]
+        rows.append(r)
+        roff.append(roff[-1] + len(r))
+    rows = np.concatenate(rows).astype(np.int32)
+    roff, toff = np.array(roff), np.arange(4) * 6
+    pg, qg = forest_ops.predict(g, Xb, toff, roff, torch.from_numpy(rows).to(dev), want_proba=True)
+    pc, qc = forest_ops.predict(c, Xb_cpu, toff, roff, rows, want_proba=True)
+    assert np.array_equal(pg.cpu().numpy(), pc)
+    assert np.allclose(qg.cpu().numpy(), qc, atol=1e-6)
+    assert np.allclose(qc.sum(1), 1.0, atol=1e-5)
