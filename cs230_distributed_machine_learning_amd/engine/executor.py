@@ -93,7 +93,7 @@ def _scores_for(data, task: FitTask, out: FitOutput, scorer: str):
     if scorer == "score":
         return float(out.info["score"])
     y = data.test_targets(task.split)
-    return scoring_mod.score(scorer, y, out.pred, data.n_classes, out.proba)
+    return scoring_mod.score(scorer, y, out.pred, data.n_classes, out.proba, decision=out.decision)
 
 
 def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[CandidateResult]:

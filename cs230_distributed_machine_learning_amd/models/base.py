@@ -35,6 +35,7 @@ class FitOutput:
     task_id: int
     pred: Any = None            # device tensor aligned with the split's test rows
     proba: Any = None           # optional [n_test, C]
+    decision: Any = None        # optional binary decision_function [n_test] (SVC: roc_auc / average_precision)
     fit_seconds: float = 0.0    # amortised device time of this fit
     error: Optional[str] = None
     model: Any = None           # optional fitted model (when asked to keep it)

@@ -235,6 +235,8 @@ class SVMFamily(Family):
                     pred = _ovr_argmax(dec, ti, pairs, te.numel(), C_cls, dev)
             o = FitOutput(task_id=t.task_id, pred=pred, fit_seconds=dt / len(tasks),
                           info={"warnings": t.params["warnings"]})
+            if not svr and C_cls == 2 and (ti, 0) in dec:
+                o.decision = -dec[(ti, 0)]   # sklearn's binary decision_function: positive -> classes_[1]
             if keep_models:
                 rp = t.params
                 o.model = {"kind": "svm", "svr": svr, "machines": models.get(ti, []), "kernel": rp["kernel"],

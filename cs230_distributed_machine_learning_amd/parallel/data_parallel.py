@@ -270,3 +270,5 @@ class RowShard(DeviceData):
             o.pred = self._gather_rows(o.pred, cnt)
             if o.proba is not None:
                 o.proba = self._gather_rows(o.proba, cnt)
+            if getattr(o, "decision", None) is not None:
+                o.decision = self._gather_rows(o.decision, cnt)

@@ -154,8 +154,10 @@ def _multiclass_auc(y: torch.Tensor, proba: torch.Tensor, C: int, kind: str, wei
 
 
 def score(name: str, y_true: torch.Tensor, pred: torch.Tensor, n_classes: int = 2,
-          proba: Optional[torch.Tensor] = None) -> float:
-    """Scalar score for one fit (greater is better)."""
+          proba: Optional[torch.Tensor] = None, decision: Optional[torch.Tensor] = None) -> float:
+    """Scalar score for one fit (greater is better).  ``decision``: a binary classifier's
+    decision_function, which sklearn's threshold scorers (roc_auc, average_precision) use
+    when the estimator has no predict_proba (SVC)."""
     if y_true.numel() == 0:
         return float("nan")
     if name == "accuracy":
@@ -172,18 +174,18 @@ def score(name: str, y_true: torch.Tensor, pred: torch.Tensor, n_classes: int = 
                 raise ValueError(f"{name} needs a binary target; use {name}_macro")
             return _prf(_confusion(y_true, pred, n_classes), avg, what)
     if name == "roc_auc":
-        if proba is None or n_classes != 2:
-            raise ValueError("roc_auc needs probabilities of a binary classifier")
-        return _auc(y_true, proba[:, 1])
+        if (proba is None and decision is None) or n_classes != 2:
+            raise ValueError("roc_auc needs probabilities or decision values of a binary classifier")
+        return _auc(y_true, proba[:, 1] if proba is not None else decision)
     if name.startswith("roc_auc_ov"):
         if proba is None:
             raise ValueError(f"{name} needs probabilities")
         kind = name[8:11]
         return _multiclass_auc(y_true, proba.double(), proba.shape[1], kind, name.endswith("_weighted"))
     if name == "average_precision":
-        if proba is None or n_classes != 2:
-            raise ValueError("average_precision needs probabilities of a binary classifier")
-        return _average_precision(y_true, proba[:, 1])
+        if (proba is None and decision is None) or n_classes != 2:
+            raise ValueError("average_precision needs probabilities or decision values of a binary classifier")
+        return _average_precision(y_true, proba[:, 1] if proba is not None else decision)
     if name == "neg_brier_score":
         if proba is None:
             raise ValueError("neg_brier_score needs probabilities")

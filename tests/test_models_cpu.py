@@ -444,3 +444,22 @@ def test_rf_probability_scorers_match_sklearn(scoring):
     assert res[0].ok, res[0].error
     ref = cross_val_score(RandomForestClassifier(**g), X, y, cv=StratifiedKFold(3), scoring=scoring)
     assert np.allclose(res[0].result["cv_scores"], ref, atol=1e-6), (res[0].result["cv_scores"], ref)
+
+
+@pytest.mark.parametrize("scoring", ["roc_auc", "average_precision"])
+def test_svc_threshold_scorers_use_decision_function(scoring):
+    """sklearn's roc_auc / average_precision read SVC's decision_function (no predict_proba)."""
+    from sklearn.model_selection import StratifiedKFold, cross_val_score
+    from sklearn.svm import SVC
+
+    from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
+
+    rng = np.random.default_rng(4)
+    X = rng.normal(size=(240, 4))
+    y = (X[:, 0] + 0.8 * rng.normal(size=240) > 0).astype(np.int64)
+    g = {"C": 0.7, "gamma": 0.3}
+    res = run_candidates(DeviceData(X, y, True, "cpu"), JobSpec("SVC", [g], cv=3, holdout=False, keep_models="none",
+                                                                scoring=scoring), [0])
+    assert res[0].ok, res[0].error
+    ref = cross_val_score(SVC(**g), X.astype(np.float32), y, cv=StratifiedKFold(3), scoring=scoring)
+    assert np.allclose(res[0].result["cv_scores"], ref, atol=1e-9), (res[0].result["cv_scores"], ref)
