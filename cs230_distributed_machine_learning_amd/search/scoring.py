@@ -18,7 +18,7 @@ CLS_SCORERS = (
     "precision_micro", "precision_weighted", "recall", "recall_macro", "recall_micro", "recall_weighted", "roc_auc",
     "neg_log_loss", "jaccard", "jaccard_macro", "jaccard_micro", "jaccard_weighted", "matthews_corrcoef",
     "average_precision", "neg_brier_score", "roc_auc_ovr", "roc_auc_ovr_weighted", "roc_auc_ovo",
-    "roc_auc_ovo_weighted",
+    "roc_auc_ovo_weighted", "top_k_accuracy",
 )
 REG_SCORERS = (
     "r2", "neg_mean_squared_error", "neg_mean_absolute_error", "neg_root_mean_squared_error", "explained_variance",
@@ -29,7 +29,7 @@ REG_SCORERS = (
 
 
 PROBA_SCORERS = ("roc_auc", "neg_log_loss", "average_precision", "neg_brier_score", "roc_auc_ovr",
-                 "roc_auc_ovr_weighted", "roc_auc_ovo", "roc_auc_ovo_weighted")
+                 "roc_auc_ovr_weighted", "roc_auc_ovo", "roc_auc_ovo_weighted", "top_k_accuracy")
 
 
 def needs_proba(name) -> bool:
@@ -194,6 +194,13 @@ def score(name: str, y_true: torch.Tensor, pred: torch.Tensor, n_classes: int = 
         if proba.shape[1] == 2:   # binary: the positive class's squared error
             return -float((d[:, 1] ** 2).mean())
         return -float((d * d).sum(1).mean())
+    if name == "top_k_accuracy":   # sklearn default k=2; ties: the higher class index ranks first
+        if proba is None:
+            raise ValueError("top_k_accuracy needs probabilities")
+        if proba.shape[1] <= 2:
+            return 1.0
+        order = torch.argsort(proba.double(), dim=1, stable=True).flip(1)[:, :2]
+        return float((order == y_true.long().view(-1, 1)).any(1).double().mean())
     if name == "matthews_corrcoef":
         return _mcc(_confusion(y_true, pred, n_classes))
     if name == "neg_log_loss":

@@ -198,7 +198,7 @@ def test_stratified_holdout_matches_sklearn():
 @pytest.mark.parametrize("C", [2, 4])
 @pytest.mark.parametrize("name", ["matthews_corrcoef", "jaccard_micro", "jaccard_weighted", "neg_brier_score",
                                   "average_precision", "roc_auc_ovr", "roc_auc_ovr_weighted", "roc_auc_ovo",
-                                  "roc_auc_ovo_weighted"])
+                                  "roc_auc_ovo_weighted", "top_k_accuracy"])
 def test_more_classification_scorers_match_sklearn(name, C):
     """Scorer strings a GridSearchCV user passes, through sklearn's own scorer objects."""
     from sklearn.metrics import get_scorer
