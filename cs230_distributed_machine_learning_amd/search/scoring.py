@@ -18,13 +18,16 @@ CLS_SCORERS = (
     "precision_micro", "precision_weighted", "recall", "recall_macro", "recall_micro", "recall_weighted", "roc_auc",
     "neg_log_loss", "jaccard", "jaccard_macro", "jaccard_micro", "jaccard_weighted", "matthews_corrcoef",
     "average_precision", "neg_brier_score", "roc_auc_ovr", "roc_auc_ovr_weighted", "roc_auc_ovo",
-    "roc_auc_ovo_weighted", "top_k_accuracy",
+    "roc_auc_ovo_weighted", "top_k_accuracy", "positive_likelihood_ratio", "neg_negative_likelihood_ratio",
+    # label-agreement (clustering) scores of the predictions against the targets
+    "rand_score", "adjusted_rand_score", "fowlkes_mallows_score", "mutual_info_score",
+    "normalized_mutual_info_score", "homogeneity_score", "completeness_score", "v_measure_score",
 )
 REG_SCORERS = (
     "r2", "neg_mean_squared_error", "neg_mean_absolute_error", "neg_root_mean_squared_error", "explained_variance",
     "max_error", "neg_median_absolute_error", "neg_mean_absolute_percentage_error", "neg_mean_squared_log_error",
     "neg_root_mean_squared_log_error", "neg_mean_poisson_deviance", "neg_mean_gamma_deviance",
-    "d2_absolute_error_score",
+    "d2_absolute_error_score", "neg_max_error",
 )
 
 
@@ -153,6 +156,62 @@ def _multiclass_auc(y: torch.Tensor, proba: torch.Tensor, C: int, kind: str, wei
     return float(v.mean())
 
 
+_CLUSTER = ("rand_score", "adjusted_rand_score", "fowlkes_mallows_score", "mutual_info_score",
+            "normalized_mutual_info_score", "homogeneity_score", "completeness_score", "v_measure_score")
+
+
+def _cluster_score(name: str, y: torch.Tensor, p: torch.Tensor) -> float:
+    """sklearn.metrics.cluster scores from the contingency table of (targets, predictions)."""
+    _, yi = torch.unique(y.long(), return_inverse=True)
+    _, pi = torch.unique(p.long(), return_inverse=True)
+    R, K = int(yi.max()) + 1, int(pi.max()) + 1
+    cont = torch.bincount(yi * K + pi, minlength=R * K).reshape(R, K).double()
+    n = float(cont.sum())
+    a, b = cont.sum(1), cont.sum(0)
+    if name in ("rand_score", "adjusted_rand_score", "fowlkes_mallows_score"):
+        comb = lambda x: x * (x - 1) / 2.0   # noqa: E731
+        s_ij, s_a, s_b = float(comb(cont).sum()), float(comb(a).sum()), float(comb(b).sum())
+        if name == "fowlkes_mallows_score":
+            tk = float((cont * cont).sum()) - n
+            pk, qk = float((a * a).sum()) - n, float((b * b).sum()) - n
+            return math.sqrt(tk / pk) * math.sqrt(tk / qk) if tk != 0.0 else 0.0
+        total = comb(n)
+        if name == "rand_score":
+            if total == 0:
+                return 1.0
+            return (total + 2 * s_ij - s_a - s_b) / total
+        if R == K == 1 or R == K == n or total == 0:   # sklearn's special cases
+            return 1.0
+        expected = s_a * s_b / total
+        return (s_ij - expected) / ((s_a + s_b) / 2.0 - expected)
+
+    def ent(c):
+        c = c[c > 0]
+        t = float(c.sum())
+        return float(-((c / t) * (torch.log(c) - math.log(t))).sum()) if t > 0 else 0.0
+
+    nz = cont > 0
+    pij = cont[nz]
+    outer = (a.view(-1, 1) * b.view(1, -1))[nz]
+    mi = float(((pij / n) * (torch.log(pij) - math.log(n)) + (pij / n) * (math.log(n) * 2 - torch.log(outer))).sum())
+    mi = max(mi, 0.0)
+    if name == "mutual_info_score":
+        return mi
+    hy, hp = ent(a), ent(b)
+    if name == "normalized_mutual_info_score":   # average_method="arithmetic"
+        if R == K == 1 or (R == 1 and K == 1):
+            return 1.0
+        den = (hy + hp) / 2.0
+        return mi / den if den > 0 else 1.0
+    hom = 1.0 if hy == 0 else mi / hy
+    com = 1.0 if hp == 0 else mi / hp
+    if name == "homogeneity_score":
+        return hom
+    if name == "completeness_score":
+        return com
+    return 0.0 if hom + com == 0 else 2.0 * hom * com / (hom + com)
+
+
 def score(name: str, y_true: torch.Tensor, pred: torch.Tensor, n_classes: int = 2,
           proba: Optional[torch.Tensor] = None, decision: Optional[torch.Tensor] = None) -> float:
     """Scalar score for one fit (greater is better).  ``decision``: a binary classifier's
@@ -201,6 +260,16 @@ def score(name: str, y_true: torch.Tensor, pred: torch.Tensor, n_classes: int = 
             return 1.0
         order = torch.argsort(proba.double(), dim=1, stable=True).flip(1)[:, :2]
         return float((order == y_true.long().view(-1, 1)).any(1).double().mean())
+    if name in ("positive_likelihood_ratio", "neg_negative_likelihood_ratio"):
+        if n_classes != 2:
+            raise ValueError(f"{name} needs a binary target")
+        cm = _confusion(y_true, pred, 2)
+        tn, fp, fn, tp = (float(v) for v in cm.flatten())
+        if name == "positive_likelihood_ratio":   # sensitivity / (1 - specificity)
+            return (tp / (tp + fn)) / (fp / (fp + tn)) if fp > 0 and tp + fn > 0 else float("nan")
+        return -((fn / (tp + fn)) / (tn / (fp + tn))) if tn > 0 and tp + fn > 0 else float("nan")
+    if name in _CLUSTER:
+        return _cluster_score(name, y_true, pred)
     if name == "matthews_corrcoef":
         return _mcc(_confusion(y_true, pred, n_classes))
     if name == "neg_log_loss":
@@ -225,7 +294,7 @@ def score(name: str, y_true: torch.Tensor, pred: torch.Tensor, n_classes: int = 
         return -float(err.abs().mean())
     if name == "neg_median_absolute_error":
         return -float(torch.quantile(err.abs().double(), 0.5))  # numpy median (mean of middle pair)
-    if name == "max_error":
+    if name in ("max_error", "neg_max_error"):   # sklearn >= 1.6 names it neg_max_error
         return -float(err.abs().max())
     if name == "explained_variance":
         vt = float(yt.var(unbiased=False))

@@ -230,7 +230,7 @@ def test_more_classification_scorers_match_sklearn(name, C):
     assert got == pytest.approx(ref, rel=1e-9, abs=1e-12), (name, got, ref)
 
 
-@pytest.mark.parametrize("name", ["neg_mean_squared_log_error", "neg_root_mean_squared_log_error",
+@pytest.mark.parametrize("name", ["neg_max_error", "neg_mean_squared_log_error", "neg_root_mean_squared_log_error",
                                   "neg_mean_poisson_deviance", "neg_mean_gamma_deviance", "d2_absolute_error_score",
                                   "neg_mean_absolute_percentage_error"])
 def test_more_regression_scorers_match_sklearn(name):
@@ -246,4 +246,27 @@ def test_more_regression_scorers_match_sklearn(name):
 
     ref = get_scorer(name)(_Fixed(), np.zeros((200, 1)), y)
     got = dsc.score(name, torch.from_numpy(y), torch.from_numpy(p))
+    assert got == pytest.approx(ref, rel=1e-9, abs=1e-12), (name, got, ref)
+
+
+@pytest.mark.parametrize("name", ["positive_likelihood_ratio", "neg_negative_likelihood_ratio", "rand_score",
+                                  "adjusted_rand_score", "fowlkes_mallows_score", "mutual_info_score",
+                                  "normalized_mutual_info_score", "homogeneity_score", "completeness_score",
+                                  "v_measure_score"])
+@pytest.mark.parametrize("C", [2, 3])
+def test_label_agreement_scorers_match_sklearn(name, C):
+    from sklearn.metrics import get_scorer
+
+    if C > 2 and "likelihood" in name:
+        pytest.skip("binary-only scorer")
+    rng = np.random.RandomState(11 + C)
+    y = rng.randint(0, C, 300)
+    pred = np.where(rng.rand(300) < 0.7, y, rng.randint(0, C, 300))
+
+    class _Fixed:
+        def predict(self, X):
+            return pred
+
+    ref = get_scorer(name)(_Fixed(), np.zeros((300, 1)), y)
+    got = dsc.score(name, torch.from_numpy(y), torch.from_numpy(pred), C)
     assert got == pytest.approx(ref, rel=1e-9, abs=1e-12), (name, got, ref)
