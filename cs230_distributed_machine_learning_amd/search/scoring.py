@@ -11,6 +11,7 @@ from __future__ import annotations
 import math
 from typing import Callable, Dict, Optional
 
+import numpy as np
 import torch
 
 CLS_SCORERS = (
@@ -22,6 +23,7 @@ CLS_SCORERS = (
     # label-agreement (clustering) scores of the predictions against the targets
     "rand_score", "adjusted_rand_score", "fowlkes_mallows_score", "mutual_info_score",
     "normalized_mutual_info_score", "homogeneity_score", "completeness_score", "v_measure_score",
+    "adjusted_mutual_info_score",
 )
 REG_SCORERS = (
     "r2", "neg_mean_squared_error", "neg_mean_absolute_error", "neg_root_mean_squared_error", "explained_variance",
@@ -157,7 +159,30 @@ def _multiclass_auc(y: torch.Tensor, proba: torch.Tensor, C: int, kind: str, wei
 
 
 _CLUSTER = ("rand_score", "adjusted_rand_score", "fowlkes_mallows_score", "mutual_info_score",
-            "normalized_mutual_info_score", "homogeneity_score", "completeness_score", "v_measure_score")
+            "normalized_mutual_info_score", "homogeneity_score", "completeness_score", "v_measure_score",
+            "adjusted_mutual_info_score")
+
+
+def _expected_mi(a: np.ndarray, b: np.ndarray, n: int) -> float:
+    """Expected mutual information of two labelings with marginals a, b (hypergeometric
+    model; sklearn.metrics.cluster._expected_mutual_info_fast), vectorised per cell."""
+    from scipy.special import gammaln
+
+    if a.size == 1 or b.size == 1:
+        return 0.0
+    emi = 0.0
+    base = gammaln(n + 1)
+    for ai in a:
+        for bj in b:
+            lo, hi = max(1, ai + bj - n), min(ai, bj)
+            if lo > hi:
+                continue
+            nij = np.arange(lo, hi + 1, dtype=np.float64)
+            term2 = np.log(n) + np.log(nij) - np.log(ai) - np.log(bj)
+            gln = (gammaln(ai + 1) + gammaln(bj + 1) + gammaln(n - ai + 1) + gammaln(n - bj + 1) - base
+                   - gammaln(nij + 1) - gammaln(ai - nij + 1) - gammaln(bj - nij + 1) - gammaln(n - ai - bj + nij + 1))
+            emi += float((nij / n * term2 * np.exp(gln)).sum())
+    return emi
 
 
 def _cluster_score(name: str, y: torch.Tensor, p: torch.Tensor) -> float:
@@ -198,6 +223,14 @@ def _cluster_score(name: str, y: torch.Tensor, p: torch.Tensor) -> float:
     if name == "mutual_info_score":
         return mi
     hy, hp = ent(a), ent(b)
+    if name == "adjusted_mutual_info_score":   # average_method="arithmetic"
+        if R == K == 1:
+            return 1.0
+        emi = _expected_mi(a.cpu().numpy().astype(np.int64), b.cpu().numpy().astype(np.int64), int(n))
+        den = (hy + hp) / 2.0 - emi
+        eps = float(np.finfo(np.float64).eps)
+        den = min(den, -eps) if den < 0 else max(den, eps)
+        return (mi - emi) / den
     if name == "normalized_mutual_info_score":   # average_method="arithmetic"
         if R == K == 1 or (R == 1 and K == 1):
             return 1.0

@@ -252,7 +252,7 @@ def test_more_regression_scorers_match_sklearn(name):
 @pytest.mark.parametrize("name", ["positive_likelihood_ratio", "neg_negative_likelihood_ratio", "rand_score",
                                   "adjusted_rand_score", "fowlkes_mallows_score", "mutual_info_score",
                                   "normalized_mutual_info_score", "homogeneity_score", "completeness_score",
-                                  "v_measure_score"])
+                                  "v_measure_score", "adjusted_mutual_info_score"])
 @pytest.mark.parametrize("C", [2, 3])
 def test_label_agreement_scorers_match_sklearn(name, C):
     from sklearn.metrics import get_scorer
