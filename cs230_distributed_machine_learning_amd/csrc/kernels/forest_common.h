@@ -38,7 +38,9 @@ constexpr int kBins = 256;        // uint8 bins
 constexpr int kPoisTable = 12;    // Poisson CDF thresholds kept per tree
 constexpr int kMaxClasses = 64;   // classification channels supported by the builders
 
-enum Criterion : int32_t { kGini = 0, kEntropy = 1, kMSE = 2, kPoisson = 3 };
+// kMAE (sklearn "absolute_error") is grown by the host builder only (forest_cpu.cpp):
+// its split search needs per-node weighted medians, not histogram sums
+enum Criterion : int32_t { kGini = 0, kEntropy = 1, kMSE = 2, kPoisson = 3, kMAE = 4 };
 
 // Per-tree build specification (POD, identical layout on host, device and ctypes).
 struct TreeSpec {

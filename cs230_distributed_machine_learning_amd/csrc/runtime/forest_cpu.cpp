@@ -39,6 +39,36 @@ struct Data {
 
 struct Job { int node, start, count, depth; uint64_t key; };
 
+// Fenwick tree over the y-ranks of one node's rows: weights and weighted targets
+struct Fenwick {
+  int m = 0;
+  std::vector<double> w, s;
+  void reset(int m_) { m = m_; w.assign(m + 1, 0.0); s.assign(m + 1, 0.0); }
+  void fill(const double* ws, const double* ys) {   // every rank present: linear build
+    for (int i = 1; i <= m; ++i) { w[i] = ws[i - 1]; s[i] = ws[i - 1] * ys[i - 1]; }
+    for (int i = 1; i <= m; ++i) {
+      const int j = i + (i & -i);
+      if (j <= m) { w[j] += w[i]; s[j] += s[i]; }
+    }
+  }
+  void add(int r, double dw, double ds) {
+    for (int i = r + 1; i <= m; i += i & -i) { w[i] += dw; s[i] += ds; }
+  }
+  // sum w |y - median| of the set (total weight W, weighted sum S): the deviation is the
+  // same for every median of the set, so take the lowest rank whose prefix reaches W/2
+  double absdev(double W, double S, const double* ys) const {
+    int pos = 0, step = 1;
+    while (step * 2 <= m) step *= 2;
+    double cw = 0.0, cs = 0.0;
+    for (; step; step >>= 1)
+      if (pos + step <= m && cw + w[pos + step] < W * 0.5) { pos += step; cw += w[pos]; cs += s[pos]; }
+    const double med = ys[pos];   // rank pos (0-based) is the first with prefix >= W/2
+    double wle = 0.0, sle = 0.0;
+    for (int i = pos + 1; i > 0; i -= i & -i) { wle += w[i]; sle += s[i]; }
+    return med * wle - sle + (S - sle) - med * (W - wle);
+  }
+};
+
 static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& out) {
   TreeSpec s = s_in;   // min_weight_leaf is set once the tree's total weight is known
   const uint8_t* role = D.roles + (int64_t)s.split * D.n;
@@ -62,6 +92,37 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     }
   }
   tmp.resize(rows.size());
+  // criterion="absolute_error" (sklearn MAE): node value = weighted median, impurity =
+  // sum w |y - median| / W.  Node values are stored as {W, W*median, abs + W*median^2}
+  // so that v1/v0 is the median (what predict reads) and mse_impurity(v) is the MAE
+  // impurity (what max_leaf_nodes / ccp_alpha pruning read); the exact abs sums of the
+  // nodes are kept aside for the purity and acceptance tests
+  const bool mae = D.is_reg && s.criterion == kMAE;
+  std::vector<double> nabs;
+  std::vector<uint32_t> ord;
+  std::vector<double> ys, ws;
+  std::vector<int32_t> rank_of(mae ? D.n : 0);
+  Fenwick fl, fr;
+  auto sort_rows = [&](int start, int count) {   // node rows by (y, row id)
+    ord.assign(rows.begin() + start, rows.begin() + start + count);
+    std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return Y[a] < Y[b] || (Y[a] == Y[b] && a < b); });
+    ys.resize(count); ws.resize(count);
+    for (int k = 0; k < count; ++k) { ys[k] = (double)Y[ord[k]]; ws[k] = (double)wrow[ord[k]]; rank_of[ord[k]] = k; }
+  };
+  auto mae_node = [&](int start, int count, double* v) {   // sklearn WeightedMedianCalculator
+    sort_rows(start, count);
+    double W = 0.0;
+    for (int k = 0; k < count; ++k) W += ws[k];
+    double c = 0.0;
+    int k = 0;
+    while (k < count && c < W * 0.5) c += ws[k++];
+    const double med = (c == W * 0.5 && k < count) ? (ys[k - 1] + ys[k]) / 2.0 : ys[k > 0 ? k - 1 : 0];
+    double ab = 0.0;
+    for (int i = 0; i < count; ++i) ab += ws[i] * fabs(ys[i] - med);
+    v[0] = W; v[1] = W * med; v[2] = ab + W * med * med;
+    return ab;
+  };
+  if (mae && !rows.empty()) nabs.push_back(mae_node(0, (int)rows.size(), root.data()));
   // class weights multiply the (integer) class sums: root statistics here, every
   // histogram channel below -- exactly where the HIP builder applies them
   std::vector<double> cwv(D.is_reg ? 0 : D.C, 1.0);
@@ -85,13 +146,14 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     for (int k = 0; k < D.C; ++k) a.add(v[k]);
     return cls_impurity(a, s.criterion);
   };
-  auto visit = [&](int count, int depth, const double* v) {
-    return !(leaf_by_counts(s, count, depth) || leaf_by_weight(s, vals_weight(v, D.C, D.is_reg)) ||
-             impurity_of(v) <= kEps);
+  auto node_imp = [&](int node, const double* v) { return mae ? nabs[node] / v[0] : impurity_of(v); };
+  auto visit = [&](int count, int depth, const double* v, double imp) {
+    return !(leaf_by_counts(s, count, depth) || leaf_by_weight(s, vals_weight(v, D.C, D.is_reg)) || imp <= kEps);
   };
 
   std::vector<Job> stack;
-  if (!rows.empty() && visit((int)rows.size(), 0, root.data())) stack.push_back({0, 0, (int)rows.size(), 0, root_key(s.seed)});
+  if (!rows.empty() && visit((int)rows.size(), 0, root.data(), node_imp(0, root.data())))
+    stack.push_back({0, 0, (int)rows.size(), 0, root_key(s.seed)});
   const int CH = D.CH;
   std::vector<uint32_t> hu((size_t)CH * 256);
   std::vector<float> hf((size_t)CH * 256);
@@ -103,13 +165,58 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     int pos = 0, nonconst = 0, best_feat = -1, best_bin = -1;
     double best_gain = -INFINITY;
     const uint32_t* nr = rows.data() + jb.start;
+    double mae_l = 0.0, mae_r = 0.0;   // abs sums of the best split's sides
+    double Wn = 0.0, Sn = 0.0;
+    int bcnt[256];
+    if (mae) {
+      sort_rows(jb.start, jb.count);
+      for (int k = 0; k < jb.count; ++k) { Wn += ws[k]; Sn += ws[k] * ys[k]; }
+    }
     while (nonconst < s.max_features && pos < D.d) {
       const int f = feature_at(fp, pos, D.d);
       ++pos;
       double g_best = -INFINITY;
       int b_best = -1;
       bool nc = false;
-      if (!D.is_reg) {
+      if (mae) {
+        // exact MAE sweep: rows enter the left set bin by bin; the medians and abs
+        // deviations of both sides come from Fenwick trees over the node's y-ranks
+        std::fill(bcnt, bcnt + 256, 0);
+        for (int i = 0; i < jb.count; ++i) ++bcnt[D.Xb[(int64_t)nr[i] * D.ld + f]];
+        std::vector<int> boff(257, 0);
+        for (int b = 0; b < 256; ++b) boff[b + 1] = boff[b] + bcnt[b];
+        std::vector<uint32_t> byb(jb.count);
+        { std::vector<int> cur(boff.begin(), boff.end() - 1);
+          for (int i = 0; i < jb.count; ++i) byb[cur[D.Xb[(int64_t)nr[i] * D.ld + f]]++] = nr[i]; }
+        fl.reset(jb.count); fr.reset(jb.count); fr.fill(ws.data(), ys.data());
+        double Wl = 0.0, Sl = 0.0;
+        int nl = 0;
+        for (int b = 0; b < 255; ++b) {
+          if (!bcnt[b]) continue;
+          for (int i = boff[b]; i < boff[b + 1]; ++i) {
+            const int k = rank_of[byb[i]];
+            const double w = ws[k], wy = w * ys[k];
+            fl.add(k, w, wy); fr.add(k, -w, -wy);
+            Wl += w; Sl += wy;
+          }
+          nl += bcnt[b];
+          const int nrr = jb.count - nl;
+          if (nrr == 0) break;
+          nc = true;
+          if (nl < s.min_samples_leaf || nrr < s.min_samples_leaf) continue;
+          if (side_too_light(s, Wl, Wn - Wl)) continue;
+          const double al = fl.absdev(Wl, Sl, ys.data()), ar = fr.absdev(Wn - Wl, Sn - Sl, ys.data());
+          const double g = -(al + ar);
+          if (g > g_best) {
+            g_best = g; b_best = b;
+            if (g > best_gain) { mae_l = al; mae_r = ar; best_left[0] = Wl; }
+          }
+        }
+        if (nc) {
+          ++nonconst;
+          if (b_best >= 0 && g_best > best_gain) { best_gain = g_best; best_feat = f; best_bin = b_best; }
+        }
+      } else if (!D.is_reg) {
         std::fill(hu.begin(), hu.end(), 0u);
         for (int i = 0; i < jb.count; ++i) {
           const uint32_t r = nr[i];
@@ -173,7 +280,10 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     // accept?
     const double* pv = out.vals.data() + (size_t)jb.node * D.VC;
     double impN, impL, impR, wN, wL, wR;
-    if (D.is_reg) {
+    if (mae) {
+      wN = pv[0]; wL = best_left[0]; wR = pv[0] - best_left[0];
+      impN = nabs[jb.node] / wN; impL = mae_l / wL; impR = mae_r / wR;
+    } else if (D.is_reg) {
       wN = pv[0]; wL = best_left[0]; wR = pv[0] - best_left[0];
       impN = mse_impurity(pv[0], pv[1], pv[2]);
       impL = mse_impurity(best_left[0], best_left[1], best_left[2]);
@@ -194,7 +304,8 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     pv = out.vals.data() + (size_t)jb.node * D.VC;
     double* lv = out.vals.data() + (size_t)base * D.VC;
     double* rv = lv + D.VC;
-    for (int k = 0; k < D.VC; ++k) { lv[k] = best_left[k]; rv[k] = pv[k] - best_left[k]; }
+    if (!mae)
+      for (int k = 0; k < D.VC; ++k) { lv[k] = best_left[k]; rv[k] = pv[k] - best_left[k]; }
     out.nodes[jb.node].split = pack_split(best_feat, best_bin);
     out.nodes[jb.node].left = base;
     const int nl = (int)best_left[CH - 1];
@@ -209,12 +320,17 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     }
     memcpy(nrw + li, tw, (size_t)ri * 4);
     (void)nl;
+    if (mae) {
+      nabs.resize(base + 2);
+      nabs[base] = mae_node(jb.start, li, lv);
+      nabs[base + 1] = mae_node(jb.start + li, jb.count - li, rv);
+    }
     const double* lvv = out.vals.data() + (size_t)base * D.VC;
     const double* rvv = lvv + D.VC;
     // push right first so the left subtree is processed first (depth-first, left-major)
-    if (visit(jb.count - li, jb.depth + 1, rvv))
+    if (visit(jb.count - li, jb.depth + 1, rvv, node_imp(base + 1, rvv)))
       stack.push_back({base + 1, jb.start + li, jb.count - li, jb.depth + 1, child_key(jb.key, 1)});
-    if (visit(li, jb.depth + 1, lvv))
+    if (visit(li, jb.depth + 1, lvv, node_imp(base, lvv)))
       stack.push_back({base, jb.start, li, jb.depth + 1, child_key(jb.key, 0)});
   }
 }

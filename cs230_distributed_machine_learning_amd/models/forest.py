@@ -8,7 +8,7 @@ of whole fits, then every fit's held-out rows are predicted in one launch.
 
 Supported: n_estimators, criterion (gini/entropy/log_loss; squared_error; friedman_mse, whose splits are
 squared_error's; poisson -- sklearn's proxy sum_l log(mean_l) + sum_r log(mean_r);
-absolute_error approximates with squared_error), max_depth,
+absolute_error: exact, on the host builder), max_depth,
 min_samples_split, min_samples_leaf (int or fraction), max_features (sqrt/log2/None/
 int/float), bootstrap, max_samples, min_impurity_decrease, max_leaf_nodes (sklearn's
 best-first tree: the grown tree is cut to its best-first top, ops/forest_ops.py
@@ -114,9 +114,7 @@ class ForestFamily(Family):
                 if float(p["min_impurity_decrease"] or 0.0) > 0:
                     warn.append("criterion='friedman_mse' with min_impurity_decrease > 0: the decrease is "
                                 "tested on the squared_error scale")
-            elif crit == "absolute_error":
-                warn.append(f"criterion={crit!r} approximated by squared_error")
-            crit_id = forest_ops.POISSON if crit == "poisson" else forest_ops.MSE
+            crit_id = {"poisson": forest_ops.POISSON, "absolute_error": forest_ops.MAE}.get(crit, forest_ops.MSE)
             if crit == "poisson" and (float(p["min_impurity_decrease"] or 0.0) > 0 or float(p["ccp_alpha"] or 0.0) > 0):
                 warn.append("criterion='poisson': min_impurity_decrease / ccp_alpha are applied on the "
                             "squared-error impurity scale")
@@ -259,6 +257,15 @@ class ForestFamily(Family):
                 raise ParamError("Some value(s) of y are negative which is not allowed for Poisson regression.")
         Xb = data.binned()
         sharded = getattr(data, "is_row_shard", False)
+        if sharded and any(t.params.get("criterion") == forest_ops.MAE for t in tasks):
+            for t in tasks:   # the row-sharded builder sums histograms; medians need every row
+                if t.params.get("criterion") == forest_ops.MAE:
+                    t.params["criterion"] = forest_ops.MSE
+                    t.params.setdefault("warnings", []).append(
+                        "criterion='absolute_error' under a row shard: grown with squared_error")
+        # absolute_error trees grow on the host builder (forest_cpu.cpp): batch them apart
+        tasks_in = tasks
+        tasks = sorted(tasks, key=lambda t: t.params.get("criterion") == forest_ops.MAE)
         budget = self._budget(data)
         if sharded:   # every rank must form the SAME batches: the smallest budget of the group
             budget = float(data.all_reduce(torch.tensor([budget], dtype=torch.float64, device=data.device), "min")[0])
@@ -273,6 +280,9 @@ class ForestFamily(Family):
         rows = pool = 0.0
         T = 0
         for t in tasks:
+            if cur and (t.params.get("criterion") == forest_ops.MAE) != (cur[-1].params.get("criterion") == forest_ops.MAE):
+                batches.append(cur)
+                cur, cur_bytes, rows, T, pool = [], 0.0, 0.0, 0, 0.0
             if sharded:
                 b = self._dp_bytes(data, t.params)
                 if cur and cur_bytes + b > budget:
@@ -308,7 +318,7 @@ class ForestFamily(Family):
                 out_b = self._run_batch(data, Xb, batch, is_reg, keep_models, tree_chunk)
             for o in out_b:
                 outs[o.task_id] = o
-        return [outs[t.task_id] for t in tasks]
+        return [outs[t.task_id] for t in tasks_in]
 
     def _dp_bytes(self, data, rp) -> float:
         """Device bytes of one fit under the row-sharded builder: the (tree, row) weight
@@ -387,6 +397,14 @@ class ForestFamily(Family):
             fb = forest_dp.build_dp(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
                                     data.n_classes, is_reg, data.r0, reduce=data.all_reduce, cw=cw, comm=data,
                                     tree_chunk=tree_chunk)
+        elif is_reg and batch[0].params.get("criterion") == forest_ops.MAE:
+            # exact absolute_error: per-node weighted medians on the host builder; the
+            # pruning / refine / predict steps below run where the data lives
+            fb = forest_ops.build_cpu(Xb.cpu().numpy(), None, data.y_reg.cpu().numpy(), data.roles_np(), specs,
+                                      data.n_classes, is_reg)
+            if data.is_gpu:
+                fb.nodes = torch.from_numpy(fb.nodes).to(data.device)
+                fb.vals = torch.from_numpy(fb.vals).to(data.device)
         elif data.is_gpu:
             fb = forest_ops.build_gpu(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
                                       data.n_classes, is_reg, self.tiers, reuse_pool=True,

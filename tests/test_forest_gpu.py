@@ -296,3 +296,26 @@ def test_gpu_predict_proba_matches_cpu():
     assert np.array_equal(pg.cpu().numpy(), pc)
     assert np.allclose(qg.cpu().numpy(), qc, atol=1e-6)
     assert np.allclose(qc.sum(1), 1.0, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_gpu_absolute_error_family_matches_host_path():
+    """criterion='absolute_error' on device-resident data: the host builder grows the
+    trees (per-node medians), then pruning, refine and the HIP predict + scoring run on
+    the GPU -- the same CV scores as the all-host path, and a mixed MAE / squared_error
+    grid keeps each candidate's own criterion."""
+    from cs230_distributed_machine_learning_amd.data.device import DeviceData
+    from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
+
+    rng = np.random.RandomState(5)
+    X = rng.randint(0, 16, size=(3000, 6)).astype(np.float32)
+    y = X[:, 0] - 0.5 * X[:, 2] + rng.standard_t(2, 3000)
+    cands = [{"n_estimators": 4, "criterion": c, "max_depth": 6, "ccp_alpha": a}
+             for c in ("absolute_error", "squared_error") for a in (0.0, 0.01)]
+    spec = JobSpec("RandomForestRegressor", cands, cv=3, holdout=False, random_state=1)
+    gpu = run_candidates(DeviceData(X, y, False, "cuda:0"), spec, range(len(cands)))
+    cpu = run_candidates(DeviceData(X, y, False, "cpu"), spec, range(len(cands)))
+    for g, c in zip(gpu, cpu):
+        assert g.ok and c.ok
+        assert np.allclose(g.result["cv_scores"], c.result["cv_scores"], rtol=1e-6, atol=1e-9)
+    assert not np.allclose(cpu[0].result["cv_scores"], cpu[2].result["cv_scores"])

@@ -295,6 +295,36 @@ def test_rf_poisson_criterion_matches_sklearn():
         fam.run(dd, [FitTask(0, 0, 0, "RandomForestRegressor", rp)])
 
 
+@pytest.mark.parametrize("extra,seeds", [({}, (1, 3, 6)), ({"max_depth": 4}, (1, 2)),
+                                         ({"max_leaf_nodes": 12}, (1, 2)), ({"ccp_alpha": 0.05}, (1, 2))])
+def test_rf_absolute_error_matches_sklearn(extra, seeds):
+    """criterion='absolute_error': weighted-median leaves and exact abs-deviation splits
+    (forest_cpu.cpp Fenwick sweep); sklearn's tree on exactly binned columns, also
+    through best-first (max_leaf_nodes) and ccp_alpha pruning, which read the MAE
+    impurity.  Full-depth trees on other seeds hit equal-gain ties between features."""
+    from sklearn.ensemble import RandomForestRegressor
+
+    from cs230_distributed_machine_learning_amd.engine.service import refit_model
+
+    rng = np.random.default_rng(3)
+    X = rng.integers(0, 8, size=(400, 4)).astype(np.float32)
+    y = np.round((1.5 * X[:, 0] - X[:, 1] + rng.standard_t(2, 400)) * 8) / 8
+    for seed in seeds:
+        params = {"n_estimators": 1, "bootstrap": False, "max_features": None, "criterion": "absolute_error",
+                  "min_samples_leaf": 3, "random_state": seed, **extra}
+        m = refit_model({"model_type": "RandomForestRegressor", "scoring": None}, params, DeviceData(X, y, False))
+        sk = RandomForestRegressor(**params).fit(X, y).estimators_[0].tree_
+        nodes, vals = np.asarray(m["nodes"]), np.asarray(m["vals"])
+        leaves = nodes[:, 0] < 0
+        ours = np.sort(vals[leaves, 1] / vals[leaves, 0])
+        ref = np.sort(sk.value[sk.children_left == -1][:, 0, 0])
+        assert len(ours) == len(ref)
+        np.testing.assert_allclose(ours, ref, rtol=1e-9)
+    fam = family_of("RandomForestRegressor")
+    rp = fam.resolve("RandomForestRegressor", params, 400, 4, 1)
+    assert rp["warnings"] == []
+
+
 @pytest.mark.parametrize("model,kw", [
     ("RandomForestClassifier", {}),
     ("RandomForestClassifier", {"class_weight": {"0": 1.0, "1": 3.0}}),
@@ -463,3 +493,23 @@ def test_svc_threshold_scorers_use_decision_function(scoring):
     assert res[0].ok, res[0].error
     ref = cross_val_score(SVC(**g), X.astype(np.float32), y, cv=StratifiedKFold(3), scoring=scoring)
     assert np.allclose(res[0].result["cv_scores"], ref, atol=1e-9), (res[0].result["cv_scores"], ref)
+
+
+def test_rf_mixed_criteria_batches_keep_task_order():
+    """A grid mixing absolute_error (host builder) and squared_error candidates is
+    batched apart, and every output still belongs to its own task."""
+    from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
+
+    rng = np.random.default_rng(0)
+    X = rng.integers(0, 8, size=(600, 4)).astype(np.float32)
+    y = X[:, 0] - X[:, 1] + rng.standard_normal(600)
+    cands = [{"n_estimators": 3, "criterion": c, "max_depth": 4, "random_state": 5}
+             for c in ("absolute_error", "squared_error", "absolute_error", "poisson")]
+    yp = y - y.min()
+    spec = JobSpec("RandomForestRegressor", cands, cv=3, holdout=False, random_state=2)
+    mixed = run_candidates(DeviceData(X, yp, False, "cpu"), spec, range(4))
+    for i, c in enumerate(cands):
+        alone = run_candidates(DeviceData(X, yp, False, "cpu"), JobSpec("RandomForestRegressor", [c], cv=3,
+                                                                         holdout=False, random_state=2), [0])[0]
+        assert mixed[i].result["cv_scores"] == alone.result["cv_scores"]
+    assert mixed[0].result["cv_scores"] == mixed[2].result["cv_scores"]
