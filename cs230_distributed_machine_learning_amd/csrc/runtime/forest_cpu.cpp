@@ -35,9 +35,11 @@ struct Data {
   const int32_t* ycls; const float* yreg; const uint8_t* roles;
   int64_t ystride;
   const double* cw;   // class-weight table [T][C] (rows of cw_mode 1 trees), or null
+  const int8_t* mono; // monotonic_cst table [fits][d] (+1 / -1 / 0; binary classifiers'
+                      // rows already constrain the class-0 fraction), or null
 };
 
-struct Job { int node, start, count, depth; uint64_t key; };
+struct Job { int node, start, count, depth; uint64_t key; double lo, hi; };
 
 // Fenwick tree over the y-ranks of one node's rows: weights and weighted targets
 struct Fenwick {
@@ -146,6 +148,15 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     for (int k = 0; k < D.C; ++k) a.add(v[k]);
     return cls_impurity(a, s.criterion);
   };
+  // monotonic_cst (sklearn >= 1.4): a constrained feature's split must keep the children's
+  // values ordered and inside the node's bounds; the children's bounds meet at the mean of
+  // the two values (sklearn's middle_value rounding); every node value is clipped to its bounds once the tree is grown
+  const int8_t* mono = D.mono ? D.mono + (int64_t)s.fit * D.d : nullptr;
+  std::vector<double> nlo(1, -INFINITY), nhi(1, INFINITY);
+  auto side_value = [&](double w, double a) { return w > 0.0 ? a / w : 0.0; };
+  auto mono_ok = [&](int m, double lo, double hi, double vl, double vr) {
+    return vl >= lo && vr >= lo && vl <= hi && vr <= hi && (vl - vr) * m <= 0.0;
+  };
   auto node_imp = [&](int node, const double* v) { return mae ? nabs[node] / v[0] : impurity_of(v); };
   auto visit = [&](int count, int depth, const double* v, double imp) {
     return !(leaf_by_counts(s, count, depth) || leaf_by_weight(s, vals_weight(v, D.C, D.is_reg)) || imp <= kEps);
@@ -153,7 +164,7 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
 
   std::vector<Job> stack;
   if (!rows.empty() && visit((int)rows.size(), 0, root.data(), node_imp(0, root.data())))
-    stack.push_back({0, 0, (int)rows.size(), 0, root_key(s.seed)});
+    stack.push_back({0, 0, (int)rows.size(), 0, root_key(s.seed), -INFINITY, INFINITY});
   const int CH = D.CH;
   std::vector<uint32_t> hu((size_t)CH * 256);
   std::vector<float> hf((size_t)CH * 256);
@@ -166,6 +177,7 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     double best_gain = -INFINITY;
     const uint32_t* nr = rows.data() + jb.start;
     double mae_l = 0.0, mae_r = 0.0;   // abs sums of the best split's sides
+    double best_mid = 0.0;             // mean of the best split's two side values
     double Wn = 0.0, Sn = 0.0;
     int bcnt[256];
     if (mae) {
@@ -237,8 +249,14 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
             L.add(lc); R.add(tc - lc);
           }
           if (side_too_light(s, L.w, R.w)) continue;
+          const double l0 = (double)hu[b] * cwv[0], t0c = (double)hu[255] * cwv[0];
+          const double vl = side_value(L.w, l0), vr = side_value(R.w, t0c - l0);
+          if (mono && mono[f] && !mono_ok(mono[f], jb.lo, jb.hi, vl, vr)) continue;
           const double g = cls_proxy(L, R, s.criterion);
-          if (g > g_best) { g_best = g; b_best = b; }
+          if (g > g_best) {
+            g_best = g; b_best = b;
+            if (g > best_gain) best_mid = l0 / (2.0 * L.w) + (t0c - l0) / (2.0 * R.w);
+          }
         }
         if (nc) {
           ++nonconst;
@@ -264,8 +282,13 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
           if (rl < (float)s.min_samples_leaf || rr < (float)s.min_samples_leaf) continue;
           const double l0 = hf[b], t0 = hf[255], l1 = hf[256 + b], t1 = hf[256 + 255];
           if (side_too_light(s, l0, t0 - l0)) continue;
+          const double vl = side_value(l0, l1), vr = side_value(t0 - l0, t1 - l1);
+          if (mono && mono[f] && !mono_ok(mono[f], jb.lo, jb.hi, vl, vr)) continue;
           const double g = reg_proxy(s.criterion, l0, l1, t0 - l0, t1 - l1);
-          if (g > g_best) { g_best = g; b_best = b; }
+          if (g > g_best) {
+            g_best = g; b_best = b;
+            if (g > best_gain) best_mid = l1 / (2.0 * l0) + (t1 - l1) / (2.0 * (t0 - l0));
+          }
         }
         if (nc) {
           ++nonconst;
@@ -320,6 +343,11 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     }
     memcpy(nrw + li, tw, (size_t)ri * 4);
     (void)nl;
+    const int mc = mono ? mono[best_feat] : 0;
+    const double llo = mc < 0 ? best_mid : jb.lo, lhi = mc > 0 ? best_mid : jb.hi;
+    const double rlo = mc > 0 ? best_mid : jb.lo, rhi = mc < 0 ? best_mid : jb.hi;
+    nlo.resize(base + 2); nhi.resize(base + 2);
+    nlo[base] = llo; nhi[base] = lhi; nlo[base + 1] = rlo; nhi[base + 1] = rhi;
     if (mae) {
       nabs.resize(base + 2);
       nabs[base] = mae_node(jb.start, li, lv);
@@ -329,9 +357,25 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     const double* rvv = lvv + D.VC;
     // push right first so the left subtree is processed first (depth-first, left-major)
     if (visit(jb.count - li, jb.depth + 1, rvv, node_imp(base + 1, rvv)))
-      stack.push_back({base + 1, jb.start + li, jb.count - li, jb.depth + 1, child_key(jb.key, 1)});
+      stack.push_back({base + 1, jb.start + li, jb.count - li, jb.depth + 1, child_key(jb.key, 1), rlo, rhi});
     if (visit(li, jb.depth + 1, lvv, node_imp(base, lvv)))
-      stack.push_back({base, jb.start, li, jb.depth + 1, child_key(jb.key, 0)});
+      stack.push_back({base, jb.start, li, jb.depth + 1, child_key(jb.key, 0), llo, lhi});
+  }
+  if (mono) {   // clip every node's value to its bounds (sklearn clip_node_value)
+    for (size_t i = 0; i < out.nodes.size(); ++i) {
+      double* v = out.vals.data() + i * D.VC;
+      if (D.is_reg) {   // the mean moves, the squared-error impurity stays
+        if (v[0] <= 0.0) continue;
+        const double m = v[1] / v[0], c = std::min(std::max(m, nlo[i]), nhi[i]);
+        v[2] += v[0] * (c * c - m * m);
+        v[1] = v[0] * c;
+      } else {          // binary: the class-0 fraction is clipped, class 1 takes the rest
+        const double W = v[0] + v[1];
+        if (W <= 0.0) continue;
+        const double c = std::min(std::max(v[0] / W, nlo[i]), nhi[i]);
+        v[0] = W * c; v[1] = W * (1.0 - c);
+      }
+    }
   }
 }
 
@@ -343,10 +387,12 @@ extern "C" {
 
 int dml_cpu_sizeof_treespec() { return (int)sizeof(TreeSpec); }
 
-void* dml_cpu_forest_build(const uint8_t* Xb, int64_t ld, int64_t n, int64_t d, const int32_t* ycls,
-                           const float* yreg, int64_t n_classes, int64_t is_reg, const uint8_t* roles,
-                           const TreeSpec* specs, int64_t T, int64_t ystride, const double* cw) {
+void* dml_cpu_forest_build_mono(const uint8_t* Xb, int64_t ld, int64_t n, int64_t d, const int32_t* ycls,
+                                const float* yreg, int64_t n_classes, int64_t is_reg, const uint8_t* roles,
+                                const TreeSpec* specs, int64_t T, int64_t ystride, const double* cw,
+                                const int8_t* mono) {
   Data D;
+  D.mono = mono;
   D.ystride = ystride;
   D.cw = cw;
   D.Xb = Xb; D.ld = ld; D.n = (int)n; D.d = (int)d; D.is_reg = (int)is_reg;
@@ -361,6 +407,13 @@ void* dml_cpu_forest_build(const uint8_t* Xb, int64_t ld, int64_t n, int64_t d, 
 #pragma omp parallel for schedule(dynamic, 1)
   for (int64_t t = 0; t < T; ++t) build_tree(D, specs[t], t, F->trees[t]);
   return F;
+}
+
+void* dml_cpu_forest_build(const uint8_t* Xb, int64_t ld, int64_t n, int64_t d, const int32_t* ycls,
+                           const float* yreg, int64_t n_classes, int64_t is_reg, const uint8_t* roles,
+                           const TreeSpec* specs, int64_t T, int64_t ystride, const double* cw) {
+  return dml_cpu_forest_build_mono(Xb, ld, n, d, ycls, yreg, n_classes, is_reg, roles, specs, T, ystride, cw,
+                                   nullptr);
 }
 
 int64_t dml_cpu_forest_num_nodes(void* h) {

@@ -19,7 +19,8 @@ the per-class sums inside the builder exactly where sklearn's sample weights wou
 ccp_alpha > 0 prunes every grown tree to its minimal cost-complexity subtree
 (ops/forest_ops.py prune_ccp); min_weight_fraction_leaf bounds every side's weight
 (bootstrap counts x class weights, as sklearn's sample weights) inside the builders;
-monotonic_cst is unsupported and reported in the subtask's ``warnings``.
+monotonic_cst (regression and binary classification, sklearn's bounds and clipping) and
+criterion="absolute_error" grow on the C++ host builder.
 """
 from __future__ import annotations
 
@@ -153,13 +154,33 @@ class ForestFamily(Family):
         mln = as_int(p["max_leaf_nodes"] if p["max_leaf_nodes"] != "None" else None, "max_leaf_nodes", lo=2,
                      allow_none=True)
         mwf = as_float(p["min_weight_fraction_leaf"], "min_weight_fraction_leaf", lo=0.0, hi=0.5)
-        if p["monotonic_cst"] not in (None, "None"):
-            warn.append("monotonic_cst not supported; ignored")
+        mono = p["monotonic_cst"]
+        if mono in (None, "None"):
+            mono = None
+        else:   # sklearn's checks and messages
+            try:
+                mono = [int(v) for v in mono]
+            except (TypeError, ValueError):
+                raise ParamError("monotonic_cst must be None or an array-like of -1, 0 or 1")
+            if len(mono) != n_features:
+                raise ParamError(f"monotonic_cst has shape {len(mono)} but the input data X has {n_features} features.")
+            if any(v not in (-1, 0, 1) for v in mono):
+                raise ParamError("monotonic_cst must be None or an array-like of -1, 0 or 1.")
+            if is_cls and n_classes > 2:
+                raise ParamError("Monotonicity constraints are not supported with multiclass classification")
+            if crit == "absolute_error":
+                warn.append("monotonic_cst with criterion='absolute_error' is not supported; ignored")
+                mono = None
+            elif not any(mono):
+                mono = None
+            elif ccp > 0 or mln:
+                warn.append("monotonic_cst with ccp_alpha / max_leaf_nodes: pruning reads the clipped node values")
         return {
             "n_estimators": n_est, "criterion": crit_id, "max_depth": md if md is not None else forest_ops.INT32_MAX,
             "min_samples_split": mss, "min_samples_leaf": msl, "max_features": k, "bootstrap": int(boot),
             "lambda": lam, "min_impurity_decrease": mid, "seed": seed_of(p["random_state"]), "warnings": warn,
             "class_weight": cw, "max_leaf_nodes": mln or 0, "ccp_alpha": ccp, "min_weight_fraction_leaf": mwf,
+            "monotonic_cst": mono,
         }
 
     def cost(self, model_type, rp, n_train, n_features, n_classes) -> float:
@@ -257,15 +278,19 @@ class ForestFamily(Family):
                 raise ParamError("Some value(s) of y are negative which is not allowed for Poisson regression.")
         Xb = data.binned()
         sharded = getattr(data, "is_row_shard", False)
-        if sharded and any(t.params.get("criterion") == forest_ops.MAE for t in tasks):
+        if sharded:
             for t in tasks:   # the row-sharded builder sums histograms; medians need every row
                 if t.params.get("criterion") == forest_ops.MAE:
                     t.params["criterion"] = forest_ops.MSE
                     t.params.setdefault("warnings", []).append(
                         "criterion='absolute_error' under a row shard: grown with squared_error")
-        # absolute_error trees grow on the host builder (forest_cpu.cpp): batch them apart
+                if t.params.get("monotonic_cst") is not None:
+                    t.params["monotonic_cst"] = None
+                    t.params.setdefault("warnings", []).append("monotonic_cst under a row shard: ignored")
+        # absolute_error and monotonic_cst trees grow on the host builder (forest_cpu.cpp):
+        # batch them apart
         tasks_in = tasks
-        tasks = sorted(tasks, key=lambda t: t.params.get("criterion") == forest_ops.MAE)
+        tasks = sorted(tasks, key=_host_only)
         budget = self._budget(data)
         if sharded:   # every rank must form the SAME batches: the smallest budget of the group
             budget = float(data.all_reduce(torch.tensor([budget], dtype=torch.float64, device=data.device), "min")[0])
@@ -280,7 +305,7 @@ class ForestFamily(Family):
         rows = pool = 0.0
         T = 0
         for t in tasks:
-            if cur and (t.params.get("criterion") == forest_ops.MAE) != (cur[-1].params.get("criterion") == forest_ops.MAE):
+            if cur and _host_only(t) != _host_only(cur[-1]):
                 batches.append(cur)
                 cur, cur_bytes, rows, T, pool = [], 0.0, 0.0, 0, 0.0
             if sharded:
@@ -397,11 +422,19 @@ class ForestFamily(Family):
             fb = forest_dp.build_dp(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
                                     data.n_classes, is_reg, data.r0, reduce=data.all_reduce, cw=cw, comm=data,
                                     tree_chunk=tree_chunk)
-        elif is_reg and batch[0].params.get("criterion") == forest_ops.MAE:
-            # exact absolute_error: per-node weighted medians on the host builder; the
-            # pruning / refine / predict steps below run where the data lives
-            fb = forest_ops.build_cpu(Xb.cpu().numpy(), None, data.y_reg.cpu().numpy(), data.roles_np(), specs,
-                                      data.n_classes, is_reg)
+        elif _host_only(batch[0]):
+            # exact absolute_error (per-node weighted medians) and monotonic_cst (bounded
+            # node values) grow on the host builder; the pruning / refine / predict steps
+            # below run where the data lives
+            mono = None
+            if any(t.params.get("monotonic_cst") is not None for t in batch):
+                mono = np.zeros((len(batch), Xb.shape[1]), dtype=np.int8)
+                for f, t in enumerate(batch):
+                    if t.params.get("monotonic_cst") is not None:   # classifiers: class-0 fraction
+                        mono[f] = np.asarray(t.params["monotonic_cst"], dtype=np.int8) * (1 if is_reg else -1)
+            ycls = None if is_reg else np.asarray(data.y_enc, dtype=np.int32)
+            fb = forest_ops.build_cpu(Xb.cpu().numpy(), ycls, None if not is_reg else data.y_reg.cpu().numpy(),
+                                      data.roles_np(), specs, data.n_classes, is_reg, cw=cw, mono=mono)
             if data.is_gpu:
                 fb.nodes = torch.from_numpy(fb.nodes).to(data.device)
                 fb.vals = torch.from_numpy(fb.vals).to(data.device)
@@ -463,6 +496,10 @@ class ForestFamily(Family):
             return outs
         finally:   # the node pool is an arena slot: free it for the next batch
             forest_ops.release_pool(fb)
+
+
+def _host_only(t: FitTask) -> bool:
+    return t.params.get("criterion") == forest_ops.MAE or t.params.get("monotonic_cst") is not None
 
 
 def _refine(data, fb, Xb, specs, roles) -> None:

@@ -347,7 +347,9 @@ def release_pool(fb: ForestBuild) -> None:
 
 def build_cpu(Xb: np.ndarray, ycls: Optional[np.ndarray], yreg: Optional[np.ndarray], roles: np.ndarray,
               specs: np.ndarray, n_classes: int, is_reg: bool, ystride: int = 0,
-              cw: Optional[np.ndarray] = None) -> ForestBuild:
+              cw: Optional[np.ndarray] = None, mono: Optional[np.ndarray] = None) -> ForestBuild:
+    """The C++ host builder.  ``mono``: int8 [fits, d] monotonic constraints indexed by
+    the specs' ``fit`` (classifier rows constrain the class-0 fraction), or None."""
     lib = native.cpu_lib()
     Xb = np.ascontiguousarray(Xb, dtype=np.uint8)
     roles = np.ascontiguousarray(roles, dtype=np.uint8)
@@ -359,9 +361,10 @@ def build_cpu(Xb: np.ndarray, ycls: Optional[np.ndarray], yreg: Optional[np.ndar
     VC = 3 if is_reg else n_classes
     t0 = time.perf_counter()
     cw = None if (cw is None or is_reg) else np.ascontiguousarray(cw, dtype=np.float64).reshape(T, n_classes)
-    h = lib.dml_cpu_forest_build(native.ptr(Xb), d, n, d, native.ptr(ycls), native.ptr(yreg),
-                                 (1 if is_reg else n_classes), int(is_reg), native.ptr(roles), native.ptr(specs), T,
-                                 int(ystride), native.ptr(cw))
+    mono = None if mono is None else np.ascontiguousarray(mono, dtype=np.int8)
+    h = lib.dml_cpu_forest_build_mono(native.ptr(Xb), d, n, d, native.ptr(ycls), native.ptr(yreg),
+                                      (1 if is_reg else n_classes), int(is_reg), native.ptr(roles), native.ptr(specs),
+                                      T, int(ystride), native.ptr(cw), native.ptr(mono))
     try:
         P = lib.dml_cpu_forest_num_nodes(h)
         nodes = np.empty((P, 2), dtype=np.int32)

@@ -319,3 +319,22 @@ def test_gpu_absolute_error_family_matches_host_path():
         assert g.ok and c.ok
         assert np.allclose(g.result["cv_scores"], c.result["cv_scores"], rtol=1e-6, atol=1e-9)
     assert not np.allclose(cpu[0].result["cv_scores"], cpu[2].result["cv_scores"])
+
+
+@pytest.mark.gpu
+def test_gpu_monotonic_cst_family_matches_host_path():
+    """monotonic_cst candidates on device-resident data grow on the host builder and are
+    predicted / scored by the HIP kernels: the CV scores of the all-host path."""
+    from cs230_distributed_machine_learning_amd.data.device import DeviceData
+    from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
+
+    rng = np.random.RandomState(2)
+    X = rng.randint(0, 16, size=(3000, 5)).astype(np.float32)
+    y = (X[:, 0] - 0.5 * X[:, 1] + 3 * rng.randn(3000) > 4).astype(np.int64)
+    cands = [{"n_estimators": 4, "max_depth": 7, "monotonic_cst": c} for c in ([1, -1, 0, 0, 0], None)]
+    spec = JobSpec("RandomForestClassifier", cands, cv=3, holdout=False, random_state=1)
+    gpu = run_candidates(DeviceData(X, y, True, "cuda:0"), spec, range(len(cands)))
+    cpu = run_candidates(DeviceData(X, y, True, "cpu"), spec, range(len(cands)))
+    for g, c in zip(gpu, cpu):
+        assert g.ok and c.ok
+        assert np.allclose(g.result["cv_scores"], c.result["cv_scores"], rtol=0, atol=1e-12)

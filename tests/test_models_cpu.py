@@ -513,3 +513,54 @@ def test_rf_mixed_criteria_batches_keep_task_order():
                                                                          holdout=False, random_state=2), [0])[0]
         assert mixed[i].result["cv_scores"] == alone.result["cv_scores"]
     assert mixed[0].result["cv_scores"] == mixed[2].result["cv_scores"]
+
+
+@pytest.mark.parametrize("model", ["RandomForestRegressor", "RandomForestClassifier"])
+@pytest.mark.parametrize("extra", [{"max_depth": 5}, {"min_samples_leaf": 10}, {}])
+def test_rf_monotonic_cst_matches_sklearn(model, extra):
+    """monotonic_cst (sklearn >= 1.4): constrained splits keep the children's values
+    ordered and inside the node's bounds, bounds meet at sklearn's middle value, node
+    values are clipped -- sklearn's trees on exactly binned columns (regression at any
+    depth; binary classification to the depths tested: its full-depth trees meet
+    equal-gini ties between features)."""
+    from sklearn.ensemble import RandomForestClassifier, RandomForestRegressor
+
+    from cs230_distributed_machine_learning_amd.engine.service import refit_model
+
+    is_cls = model == "RandomForestClassifier"
+    if is_cls and not extra:
+        pytest.skip("full-depth classification trees: equal-gain ties")
+    rng = np.random.default_rng(3)
+    X = rng.integers(0, 8, size=(500, 4)).astype(np.float32)
+    y = np.round((0.5 * X[:, 0] - 0.3 * X[:, 1] + np.sin(X[:, 2]) + rng.standard_normal(500)) * 8) / 8
+    if is_cls:
+        y = (y > np.median(y)).astype(np.int64)
+    Est = RandomForestClassifier if is_cls else RandomForestRegressor
+    for cst in ([1, -1, 0, 0], [1, 0, -1, 1]):
+        params = {"n_estimators": 1, "bootstrap": False, "max_features": None, "monotonic_cst": cst,
+                  "random_state": 1, "min_samples_leaf": 2, **extra}
+        m = refit_model({"model_type": model, "scoring": None}, params, DeviceData(X, y, is_cls))
+        sk = Est(**params).fit(X, y).estimators_[0].tree_
+        nodes, vals = np.asarray(m["nodes"]), np.asarray(m["vals"])
+        leaves = nodes[:, 0] < 0
+        ours = vals[leaves, 0] / vals[leaves].sum(1) if is_cls else vals[leaves, 1] / vals[leaves, 0]
+        v = sk.value[sk.children_left == -1][:, 0, :]
+        ref = v[:, 0] / v.sum(1) if is_cls else v[:, 0]
+        assert len(ours) == len(ref)
+        np.testing.assert_allclose(np.sort(ours), np.sort(ref), rtol=1e-9, atol=1e-12)
+    rp = family_of(model).resolve(model, {"monotonic_cst": [1, -1, 0, 0]}, 500, 4, 2)
+    assert rp["monotonic_cst"] == [1, -1, 0, 0] and rp["warnings"] == []
+
+
+def test_rf_monotonic_cst_param_errors():
+    from cs230_distributed_machine_learning_amd.models.base import ParamError
+
+    fam = family_of("RandomForestClassifier")
+    with pytest.raises(ParamError, match="multiclass"):
+        fam.resolve("RandomForestClassifier", {"monotonic_cst": [1, 0]}, 100, 2, 3)
+    with pytest.raises(ParamError, match="features"):
+        fam.resolve("RandomForestClassifier", {"monotonic_cst": [1, 0, 0]}, 100, 2, 2)
+    with pytest.raises(ParamError, match="-1, 0 or 1"):
+        fam.resolve("RandomForestRegressor", {"monotonic_cst": [2, 0]}, 100, 2, 1)
+    rp = fam.resolve("RandomForestRegressor", {"monotonic_cst": [0, 0]}, 100, 2, 1)
+    assert rp["monotonic_cst"] is None
