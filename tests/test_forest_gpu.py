@@ -315,9 +315,13 @@ def test_gpu_absolute_error_family_matches_host_path():
     spec = JobSpec("RandomForestRegressor", cands, cv=3, holdout=False, random_state=1)
     gpu = run_candidates(DeviceData(X, y, False, "cuda:0"), spec, range(len(cands)))
     cpu = run_candidates(DeviceData(X, y, False, "cpu"), spec, range(len(cands)))
-    for g, c in zip(gpu, cpu):
+    for i, (g, c) in enumerate(zip(gpu, cpu)):
         assert g.ok and c.ok
-        assert np.allclose(g.result["cv_scores"], c.result["cv_scores"], rtol=1e-6, atol=1e-9)
+        # absolute_error: the same host-built trees, predicted by the HIP kernel; the
+        # squared_error candidates come from the GPU builder, whose float histogram sums
+        # make trees close to, not equal to, the host's (test_gpu_regression_close_to_cpu)
+        tol = 1e-6 if cands[i]["criterion"] == "absolute_error" else 2e-2
+        assert np.allclose(g.result["cv_scores"], c.result["cv_scores"], rtol=0, atol=tol), (i, g.result, c.result)
     assert not np.allclose(cpu[0].result["cv_scores"], cpu[2].result["cv_scores"])
 
 
