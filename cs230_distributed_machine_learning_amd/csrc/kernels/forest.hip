@@ -536,7 +536,7 @@ __device__ bool accept_split(const Ctx& c, const TreeSpec& s, int node, int tree
     wN = N.w; wL = L.w; wR = R.w;
     impN = cls_impurity(N, s.criterion); impL = cls_impurity(L, s.criterion); impR = cls_impurity(R, s.criterion);
   }
-  const double imp = improvement(Wt, wN, impN, wL, impL, wR, impR);
+  const double imp = accept_improvement(s, c.is_reg != 0, pv, best_left, Wt, wN, impN, wL, impL, wR, impR);
   return !(imp + kEps < (double)s.min_impurity_decrease);
 }
 
@@ -593,7 +593,7 @@ __device__ bool accept_split_v(const Ctx& c, const TreeSpec& s, const double* pv
     wN = N.w; wL = L.w; wR = R.w;
     impN = cls_impurity(N, s.criterion); impL = cls_impurity(L, s.criterion); impR = cls_impurity(R, s.criterion);
   }
-  const double imp = improvement(Wt, wN, impN, wL, impL, wR, impR);
+  const double imp = accept_improvement(s, c.is_reg != 0, pv, best_left, Wt, wN, impN, wL, impL, wR, impR);
   return !(imp + kEps < (double)s.min_impurity_decrease);
 }
 

@@ -40,7 +40,9 @@ constexpr int kMaxClasses = 64;   // classification channels supported by the bu
 
 // kMAE (sklearn "absolute_error") is grown by the host builder only (forest_cpu.cpp):
 // its split search needs per-node weighted medians, not histogram sums
-enum Criterion : int32_t { kGini = 0, kEntropy = 1, kMSE = 2, kPoisson = 3, kMAE = 4 };
+// kFriedman (sklearn "friedman_mse") grows exactly like kMSE (its split proxy ranks
+// candidates the same way); only the min_impurity_decrease test differs (accept_improvement)
+enum Criterion : int32_t { kGini = 0, kEntropy = 1, kMSE = 2, kPoisson = 3, kMAE = 4, kFriedman = 5 };
 
 // Per-tree build specification (POD, identical layout on host, device and ctypes).
 struct TreeSpec {
@@ -260,6 +262,19 @@ DML_HD double improvement(double W_tree, double W_node, double imp_node, double 
 }
 
 constexpr double kEps = 1e-7;  // sklearn EPSILON for purity / min_impurity_decrease tests
+
+// the improvement the min_impurity_decrease test reads: sklearn's impurity_improvement(),
+// or for friedman_mse FriedmanMSE.impurity_improvement = (w_r s_l - w_l s_r)^2 /
+// (w_l w_r W_node), which is not scaled by the tree weight.  pv / bl: the node's and the
+// left side's regression sums {w, w y, ...}
+DML_HD double accept_improvement(const TreeSpec& s, bool is_reg, const double* pv, const double* bl, double Wt,
+                                 double wN, double impN, double wL, double impL, double wR, double impR) {
+  if (is_reg && s.criterion == kFriedman) {
+    const double wl = bl[0], wr = pv[0] - bl[0], diff = wr * bl[1] - wl * (pv[1] - bl[1]);
+    return diff * diff / (wl * wr * pv[0]);
+  }
+  return improvement(Wt, wN, impN, wL, impL, wR, impR);
+}
 
 // leaf-by-counts rule (before any split search)
 DML_HD bool leaf_by_counts(const TreeSpec& t, int count, int depth) {

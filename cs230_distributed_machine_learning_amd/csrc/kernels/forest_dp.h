@@ -267,7 +267,7 @@ DML_HD int dp_accept_one(const DpArgs& a, const DpSlot& sl, const double* best_l
     impN = cls_impurity(N, s.criterion); impL = cls_impurity(L, s.criterion); impR = cls_impurity(R, s.criterion);
   }
   const double Wt = dp_ptr<const double>(a.tree_W)[sl.tree];
-  const double imp = improvement(Wt, wN, impN, wL, impL, wR, impR);
+  const double imp = accept_improvement(s, a.is_reg != 0, pv, best_left, Wt, wN, impN, wL, impL, wR, impR);
   return (imp + kEps < (double)s.min_impurity_decrease) ? 0 : 1;
 }
 

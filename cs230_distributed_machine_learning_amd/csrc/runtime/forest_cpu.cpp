@@ -317,7 +317,8 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
       wN = N.w; wL = L.w; wR = R.w;
       impN = cls_impurity(N, s.criterion); impL = cls_impurity(L, s.criterion); impR = cls_impurity(R, s.criterion);
     }
-    const double imp = improvement(Wt, wN, impN, wL, impL, wR, impR);
+    const double imp = mae ? improvement(Wt, wN, impN, wL, impL, wR, impR)
+                           : accept_improvement(s, D.is_reg != 0, pv, best_left.data(), Wt, wN, impN, wL, impL, wR, impR);
     if (imp + kEps < (double)s.min_impurity_decrease) continue;
     // split
     const int base = (int)out.nodes.size();

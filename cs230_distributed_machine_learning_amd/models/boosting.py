@@ -172,6 +172,7 @@ class GradientBoostingFamily(Family):
             "max_features": _max_features(p["max_features"], n_features), "alpha": alpha,
             "init_zero": init == "zero", "seed": seed_of(p["random_state"]), "warnings": warn,
             "ccp_alpha": ccp, "min_weight_fraction_leaf": mwf,
+            "criterion": forest_ops.FRIEDMAN if p["criterion"] == "friedman_mse" else forest_ops.MSE,
             "n_iter_no_change": nic, "validation_fraction": vf, "tol": as_float(p["tol"], "tol", lo=0.0),
             "random_state_int": rs,
             "max_leaf_nodes": as_int(p["max_leaf_nodes"] if p["max_leaf_nodes"] != "None" else None, "max_leaf_nodes",
@@ -346,7 +347,7 @@ class GradientBoostingFamily(Family):
                     specs[j]["min_samples_leaf"] = rp["min_samples_leaf"]
                     specs[j]["max_features"] = rp["max_features"]
                     specs[j]["bootstrap"] = 0
-                    specs[j]["criterion"] = forest_ops.MSE
+                    specs[j]["criterion"] = rp.get("criterion", forest_ops.MSE)
                     specs[j]["min_impurity_decrease"] = rp["min_impurity_decrease"]
                     specs[j]["min_weight_frac"] = rp.get("min_weight_fraction_leaf", 0.0)
             limit = np.repeat([batch[f].params.get("max_leaf_nodes", 0) for f in act], K)

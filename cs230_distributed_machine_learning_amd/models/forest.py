@@ -109,13 +109,10 @@ class ForestFamily(Family):
                 raise ParamError(f"criterion {crit!r} invalid for {model_type}")
             # friedman_mse ranks splits exactly like squared_error: its proxy
             # w_l w_r (m_l - m_r)^2 is W_node x (the squared-error proxy - a node constant),
-            # so the chosen splits are the same; only min_impurity_decrease, which it scales
-            # by the node weight, differs
-            if crit == "friedman_mse":
-                if float(p["min_impurity_decrease"] or 0.0) > 0:
-                    warn.append("criterion='friedman_mse' with min_impurity_decrease > 0: the decrease is "
-                                "tested on the squared_error scale")
-            crit_id = {"poisson": forest_ops.POISSON, "absolute_error": forest_ops.MAE}.get(crit, forest_ops.MSE)
+            # so the chosen splits are the same; min_impurity_decrease reads sklearn's
+            # FriedmanMSE improvement (forest_common.h accept_improvement)
+            crit_id = {"poisson": forest_ops.POISSON, "absolute_error": forest_ops.MAE,
+                       "friedman_mse": forest_ops.FRIEDMAN}.get(crit, forest_ops.MSE)
             if crit == "poisson" and (float(p["min_impurity_decrease"] or 0.0) > 0 or float(p["ccp_alpha"] or 0.0) > 0):
                 warn.append("criterion='poisson': min_impurity_decrease / ccp_alpha are applied on the "
                             "squared-error impurity scale")

@@ -26,7 +26,7 @@ import torch
 from ..utils import native
 from ..utils import trace
 
-GINI, ENTROPY, MSE, POISSON, MAE = 0, 1, 2, 3, 4   # MAE: host builder only (build_cpu)
+GINI, ENTROPY, MSE, POISSON, MAE, FRIEDMAN = 0, 1, 2, 3, 4, 5   # MAE: host builder only (build_cpu)
 INT32_MAX = 2**31 - 1
 
 

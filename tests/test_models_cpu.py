@@ -258,6 +258,38 @@ def test_rf_friedman_mse_is_squared_error_split_for_split():
     assert np.array_equal(outs[0]["nodes"], outs[1]["nodes"])
 
 
+@pytest.mark.parametrize("mid", [0.5, 2.0, 8.0])
+def test_friedman_mse_min_impurity_decrease_matches_sklearn(mid):
+    """min_impurity_decrease under friedman_mse reads sklearn's FriedmanMSE improvement
+    (w_r s_l - w_l s_r)^2 / (w_l w_r W_node), not the tree-weight-scaled squared-error one
+    (forest_common.h accept_improvement): sklearn's trees for both criteria."""
+    from sklearn.ensemble import GradientBoostingRegressor, RandomForestRegressor
+
+    from cs230_distributed_machine_learning_amd.engine.service import refit_model
+
+    rng = np.random.default_rng(3)
+    X = rng.integers(0, 8, size=(500, 4)).astype(np.float32)
+    y = np.round((0.5 * X[:, 0] - 0.3 * X[:, 1] + np.sin(X[:, 2]) + rng.standard_normal(500)) * 8) / 8
+    for crit in ("friedman_mse", "squared_error"):
+        params = {"n_estimators": 1, "bootstrap": False, "max_features": None, "criterion": crit,
+                  "min_impurity_decrease": mid, "random_state": 1}
+        m = refit_model({"model_type": "RandomForestRegressor", "scoring": None}, params, DeviceData(X, y, False))
+        sk = RandomForestRegressor(**params).fit(X, y).estimators_[0].tree_
+        nodes, vals = np.asarray(m["nodes"]), np.asarray(m["vals"])
+        lv = nodes[:, 0] < 0
+        ref = np.sort(sk.value[sk.children_left == -1][:, 0, 0])
+        assert lv.sum() == len(ref)
+        np.testing.assert_allclose(np.sort(vals[lv, 1] / vals[lv, 0]), ref, rtol=1e-9)
+    # GradientBoosting's default criterion is friedman_mse: the same leaf counts per stage
+    params = {"n_estimators": 3, "max_depth": None, "min_impurity_decrease": mid / 4, "random_state": 0}
+    m = refit_model({"model_type": "GradientBoostingRegressor", "scoring": None}, params, DeviceData(X, y, False))
+    sk = GradientBoostingRegressor(**params).fit(X, y)
+    Xq = X[:50].astype(np.float64)
+    from cs230_distributed_machine_learning_amd.models.boosting import gbrt_predict_numpy
+
+    np.testing.assert_allclose(gbrt_predict_numpy(m, Xq), sk.predict(Xq), rtol=1e-5, atol=1e-4)
+
+
 def test_rf_poisson_criterion_matches_sklearn():
     """criterion='poisson': sklearn's proxy (sum_l log mean_l + sum_r log mean_r); on
     exactly binned columns, no bootstrap and every feature, the tree is sklearn's."""
