@@ -176,9 +176,10 @@ def test_gpu_max_leaf_prune_matches_cpu(is_reg):
         assert _canon(gn, g.vals.cpu().numpy(), T) == _canon(c.nodes, c.vals, T)
 
 
-@pytest.mark.parametrize("words,crit", [("packed", 2), ("plain", 2), ("packed", 3)])
+@pytest.mark.parametrize("words,crit", [("packed", 2), ("plain", 2), ("packed", 3), ("packed", 5)])
 def test_gpu_regression_close_to_cpu(words, crit, monkeypatch):
-    """crit 3 = Poisson (forest_common.h reg_proxy) on a positive target."""
+    """crit 3 = Poisson (forest_common.h reg_proxy) on a positive target; crit 5 =
+    friedman_mse with min_impurity_decrease (forest_common.h accept_improvement)."""
     from sklearn.datasets import make_regression
 
     if words == "plain":
@@ -194,6 +195,8 @@ def test_gpu_regression_close_to_cpu(words, crit, monkeypatch):
     Xb = binning.bin_matrix(Xt, edges)
     roles, _ = make_split_roles(y, 3, False, holdout=False)
     specs = _specs(3, 8, 10, k=10, criterion=crit)
+    if crit == 5:
+        specs["min_impurity_decrease"] = 200.0
     g = forest_ops.build_gpu(Xb, None, torch.from_numpy(y).to(dev), torch.from_numpy(roles).to(dev), specs, 1, True)
     c = forest_ops.build_cpu(Xb.cpu().numpy(), None, y, roles, specs, 1, True)
     rows, roff = [], [0]
@@ -209,6 +212,10 @@ def test_gpu_regression_close_to_cpu(words, crit, monkeypatch):
     r2 = lambda p: 1 - np.sum((p - y[rows]) ** 2) / np.sum((y[rows] - y[rows].mean()) ** 2)
     assert abs(r2(pg) - r2(pc)) < 0.02
     assert r2(pg) > 0.8
+    if crit == 5:   # the decrease test cut the trees, on both builders alike
+        full = forest_ops.build_cpu(Xb.cpu().numpy(), None, y, roles, _specs(3, 8, 10, k=10, criterion=2), 1, True)
+        assert len(c.nodes) < 0.9 * len(full.nodes)
+        assert abs(len(g.nodes) - len(c.nodes)) <= 0.05 * len(c.nodes)
 
 
 def test_wave_primitives_sort_and_scan():
