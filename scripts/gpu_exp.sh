@@ -1,24 +1,59 @@
-# One parameterised GPU experiment command (replaces the round-1 one-off files).
+# The one GPU command file: every gpurun experiment is a preset of this script.
 #   gpurun -- bash scripts/gpu_exp.sh <kind> [args...]
+# Each GPU step has its own time limit and steps are chained with &&, so the first
+# failure (fault, abort, timeout) ends the call. Logs land in gpurun_out/.
 # kinds:
-#   bench [bench.py args]        headline bench, JSON line to gpurun_out/exp_bench.log
-#   prof  [bench.py args]        rocprofv3 kernel stats of bench.py  -> gpurun_out/exp_prof/
-#   pmc   "<counters>" [gbench args]   one PMC pass on scripts/gbench_forest.py -> gpurun_out/exp_pmc/
-#   sweep [sweep_tiers.py args]  forest tier sweep
+#   tests   [pytest args]             GPU test tier                     -> exp_tests.log
+#   smoke                             __graft_entry__.smoke()           -> exp_smoke.log
+#   check                             tests + smoke + short bench + rocprof kernel stats
+#   bench   [bench.py args]           headline bench, JSON line         -> exp_bench.log
+#   prof    [bench.py args]           rocprofv3 kernel stats of bench.py -> exp_prof/
+#   pmc     "<counters>" [gbench args]  one PMC pass on gbench_forest.py -> exp_pmc/
+#   roofline [gbench args]            kernel trace + the four PMC passes of the roofline table
+#   phase                             per-phase k_nodes cycles (needs lib/libdml_hip_phase.so)
+#   sweep   [sweep_tiers.py args]     forest tier sweep
 #   configs [bench_configs.py args]   BASELINE configs 1/2/4/5
-#   gbench [gbench_forest.py args]    forest builder micro-bench
+#   gbench  [gbench_forest.py args]   forest builder micro-bench
+#   e2e                               bench.py --e2e local and over a world-1 process group
+#   rccl                              world-1 RCCL tests + bench over the process group + rocprof
+#   rehearse                          bench.py --gpus 2/4 sharing the one GPU over gloo
+#   scaling                           scaling_sim.py at 2/4/8 ranks
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+PYT="python -u -m pytest -x -q --timeout 240 --timeout-method thread"
+GB="scripts/gbench_forest.py"
 kind=$1; shift
 case "$kind" in
+  tests)   timeout -k 10 900 $PYT tests -m gpu "$@" > gpurun_out/exp_tests.log 2>&1; rc=$?; tail -3 gpurun_out/exp_tests.log; exit $rc ;;
+  smoke)   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/exp_smoke.log 2>&1 && tail -1 gpurun_out/exp_smoke.log ;;
+  check)   timeout -k 10 900 $PYT tests -m gpu > gpurun_out/exp_tests.log 2>&1 && tail -1 gpurun_out/exp_tests.log && \
+           timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/exp_smoke.log 2>&1 && tail -1 gpurun_out/exp_smoke.log && \
+           timeout -k 10 400 python bench.py --steps 8 --warmup 2 > gpurun_out/exp_bench.log 2>&1 && tail -1 gpurun_out/exp_bench.log && \
+           timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/exp_prof -o run -- python3 bench.py --steps 3 --warmup 1 > gpurun_out/exp_prof.log 2>&1 && echo PROF_OK ;;
   bench)   timeout -k 10 900 python -u bench.py "$@" > gpurun_out/exp_bench.log 2>&1 && tail -1 gpurun_out/exp_bench.log ;;
   prof)    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/exp_prof -o run -- python3 bench.py "$@" > gpurun_out/exp_prof.log 2>&1 && echo PROF_OK ;;
   pmc)     ctrs=$1; shift; args=${*:-1000000 100 100 5}
-           timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv -d gpurun_out/exp_pmc -o p -- python3 scripts/gbench_forest.py $args > gpurun_out/exp_pmc.log 2>&1 && echo PMC_OK ;;
+           timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv -d gpurun_out/exp_pmc -o p -- python3 $GB $args > gpurun_out/exp_pmc.log 2>&1 && echo PMC_OK ;;
+  roofline) args=${*:-1000000 100 100 5}
+           timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rf_kt -o p -- python3 $GB $args > gpurun_out/rf_kt.log 2>&1 && echo KT_OK && \
+           timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/rf_a -o p -- python3 $GB $args > gpurun_out/rf_a.log 2>&1 && echo PA_OK && \
+           timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/rf_b -o p -- python3 $GB $args > gpurun_out/rf_b.log 2>&1 && echo PB_OK && \
+           timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/rf_c -o p -- python3 $GB $args > gpurun_out/rf_c.log 2>&1 && echo PC_OK && \
+           timeout -s KILL 120 rocprofv3 --pmc TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum TD_TD_BUSY_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/rf_d -o p -- python3 $GB $args > gpurun_out/rf_d.log 2>&1 && echo PD_OK ;;
+  phase)   DML_HIP_LIB=cs230_distributed_machine_learning_amd/lib/libdml_hip_phase.so timeout -k 10 300 python -u scripts/phase_prof.py > gpurun_out/exp_phase.log 2>&1 && tail -3 gpurun_out/exp_phase.log ;;
   sweep)   timeout -k 10 900 python -u scripts/sweep_tiers.py "$@" > gpurun_out/exp_sweep.log 2>&1 && cat gpurun_out/exp_sweep.log ;;
   configs) timeout -k 10 900 python -u scripts/bench_configs.py "$@" > gpurun_out/exp_configs.log 2>&1 && cat gpurun_out/exp_configs.log ;;
-  gbench)  timeout -k 10 600 python -u scripts/gbench_forest.py "$@" > gpurun_out/exp_gbench.log 2>&1 && cat gpurun_out/exp_gbench.log ;;
+  gbench)  timeout -k 10 600 python -u $GB "$@" > gpurun_out/exp_gbench.log 2>&1 && cat gpurun_out/exp_gbench.log ;;
+  e2e)     timeout -k 10 900 python -u bench.py --e2e > gpurun_out/exp_e2e_local.log 2>&1 && tail -1 gpurun_out/exp_e2e_local.log && \
+           DML_FORCE_PG=1 MASTER_PORT=29601 timeout -k 10 900 python -u bench.py --e2e > gpurun_out/exp_e2e_dist.log 2>&1 && tail -1 gpurun_out/exp_e2e_dist.log ;;
+  rccl)    timeout -k 10 300 $PYT tests/test_rccl_gpu.py > gpurun_out/exp_rccl_test.log 2>&1 && tail -1 gpurun_out/exp_rccl_test.log && \
+           DML_FORCE_PG=1 MASTER_PORT=29581 timeout -k 10 300 python bench.py --steps 5 --warmup 2 > gpurun_out/exp_rccl_bench.log 2>&1 && tail -1 gpurun_out/exp_rccl_bench.log | cut -c1-160 && \
+           DML_FORCE_PG=1 MASTER_PORT=29582 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/exp_rccl_prof -o run -- python3 bench.py --steps 2 --warmup 1 > gpurun_out/exp_rccl_prof.log 2>&1 && echo PROF_OK ;;
+  rehearse) export DML_SHARE_DEVICE=1 DML_DIST_BACKEND=gloo DML_HBM_BUDGET_GB=40
+           timeout -k 10 400 python bench.py --gpus 2 --rows 250000 --steps 2 --warmup 1 --master-port 29611 > gpurun_out/exp_rh2.log 2>&1 && tail -1 gpurun_out/exp_rh2.log | cut -c1-330 && \
+           timeout -k 10 400 python bench.py --gpus 4 --rows 250000 --steps 1 --warmup 1 --master-port 29612 > gpurun_out/exp_rh4.log 2>&1 && tail -1 gpurun_out/exp_rh4.log | cut -c1-330 ;;
+  scaling) timeout -k 10 600 python -u scripts/scaling_sim.py --world 2,4,8 --steps 2 > gpurun_out/exp_scaling.log 2>&1 && cat gpurun_out/exp_scaling.log ;;
   *) echo "unknown kind $kind"; exit 2 ;;
 esac
