@@ -67,16 +67,30 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"build failed: {' '.join(cmd)}")
 
 
-def build_hip(force: bool = False) -> str:
+def build_hip(force: bool = False, out: str = HIP_LIB, extra_flags: tuple = ()) -> str:
+    """``out`` / ``extra_flags``: A/B variants of the kernel library (e.g. ``-DDML_PHASE_PROF``
+    into ``lib/libdml_hip_phase.so``, loaded through ``DML_HIP_LIB``)."""
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     deps = srcs + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
     os.makedirs(LIB, exist_ok=True)
+    if out != HIP_LIB:
+        force = True
     if force or _stale(HIP_LIB, deps):
-        tmp = HIP_LIB + ".tmp"
-        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-Wno-unused-result", "-I", os.path.join(CSRC, "kernels"), *srcs, "-o", tmp])
-        os.replace(tmp, HIP_LIB)
-    return HIP_LIB
+        # one hipcc per translation unit, in parallel (forest.hip alone is most of the
+        # build), then one link
+        from concurrent.futures import ThreadPoolExecutor
+
+        objdir = os.path.join(LIB, "obj", os.path.basename(out)[:-3])
+        os.makedirs(objdir, exist_ok=True)
+        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result",
+                 "-I", os.path.join(CSRC, "kernels"), *extra_flags]
+        objs = [os.path.join(objdir, os.path.basename(s)[:-4] + ".o") for s in srcs]
+        with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+            list(ex.map(lambda so: _run([_hipcc(), *flags, "-c", so[0], "-o", so[1]]), zip(srcs, objs)))
+        tmp = out + ".tmp"
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", *objs, "-o", tmp])
+        os.replace(tmp, out)
+    return out
 
 
 def build_cpu(force: bool = False) -> str:
@@ -123,7 +137,12 @@ if __name__ == "__main__":
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--cpu-only", action="store_true")
     ap.add_argument("--sanitize", action="store_true", help="also build the ASan/UBSan host self-test")
+    ap.add_argument("--variant", help="build an A/B kernel library lib/libdml_hip_<variant>.so instead")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="preprocessor define for --variant")
     args = ap.parse_args()
+    if args.variant:
+        print(build_hip(True, os.path.join(LIB, f"libdml_hip_{args.variant}.so"), tuple("-D" + d for d in args.defines)))
+        sys.exit(0)
     if args.sanitize:
         print(build_sanitized(args.force))
     print(build_cpu(args.force))

@@ -41,7 +41,9 @@ class Config:
     stream_binned_fraction: float = 0.5
     algo_weight: Dict[str, float] = field(default_factory=dict)
     log_dir: Optional[str] = None
-    deterministic: bool = True
+    # (no "deterministic" switch: every tree builder is deterministic by construction --
+    # classification histograms are integer counts, regression histograms exact 64-bit
+    # fixed-point sums, forest_common.h -- so there is no faster non-deterministic mode)
 
     @property
     def models_dir(self) -> str:

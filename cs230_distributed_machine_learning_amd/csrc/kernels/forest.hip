@@ -116,6 +116,7 @@ struct ForestArgs {
   int64_t ystride;       // >0: tree t regresses on yreg[specs[t].target * ystride + row] (boosting)
   int64_t XbT;           // optional feature-major copy of the bins, uint8 [d][n] (0 = none)
   int64_t cw;            // class-weight table double [T][C] (0 = no class weights in this build)
+  int64_t yq_e1, yq_e2;  // regression fixed-point exponents (forest_common.h reg_exponents)
 };
 
 constexpr int kTiers = 4;  // 0 subtree, 1 wave, 2 block, 3 large
@@ -178,6 +179,9 @@ struct Ctx {
   // integer class sums wherever they become doubles (histogram scans, root and child
   // statistics); rows of balanced_subsample trees are filled by k_roots
   const double* cw;
+  // regression: exact integer histogram sums of w, w yq, w y2q (forest_common.h)
+  RegScale rq;
+  unsigned long long* rsum;   // [T][3] integer root sums (k_fill_active -> k_roots)
 };
 
 // target vector of a tree (shared y, or its own row of the boosting target matrix)
@@ -277,9 +281,29 @@ __device__ int make_children(const Ctx& c, int node, int feat, int bin, const do
 template <int MODE> struct HT;
 template <> struct HT<0> { using T = uint32_t; };
 template <> struct HT<1> { using T = unsigned long long; };
-template <> struct HT<2> { using T = float; };
+template <> struct HT<2> { using T = unsigned long long; };
 
-__device__ __forceinline__ int hist_planes(int MODE, int CH) { return MODE == 1 ? 1 : CH; }
+// planes of one feature's histogram: MODE 1 one packed plane, MODE 2 three integer planes
+// (w | rows << 32, sum w yq, sum w y2q), MODE 0 the CH class/row planes
+__host__ __device__ __forceinline__ int hist_planes(int MODE, int CH) { return MODE == 1 ? 1 : (MODE == 2 ? 3 : CH); }
+
+// histogram payload of one row: MODE 0 cls | w << 32, MODE 1 packed u64, MODE 2 the
+// row's three integer regression terms
+struct RegPL {
+  unsigned long long wr, wy, wyy;   // w | 1 << 32, w yq, w y2q (two's complement)
+};
+template <int MODE> struct PLT { using T = uint64_t; };
+template <> struct PLT<2> { using T = RegPL; };
+
+__device__ __forceinline__ RegPL reg_payload(const Ctx& c, uint32_t w, float y) {
+  int64_t yq, y2q;
+  reg_quantize(y, c.rq, yq, y2q);
+  RegPL p;
+  p.wr = (unsigned long long)w | (1ull << 32);
+  p.wy = (unsigned long long)((int64_t)w * yq);
+  p.wyy = (unsigned long long)((int64_t)w * y2q);
+  return p;
+}
 
 template <typename CT>
 __device__ __forceinline__ void scan256(CT* p, int lane) {
@@ -318,12 +342,12 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
 template <int MODE>
 __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
                              double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after,
-                             const double* cw = nullptr) {
+                             const double* cw = nullptr, const RegScale* rq = nullptr) {
   if constexpr (MODE == 0) {
     eval_feature_lds<MODE>(h, C, CH, s, lane, out_gain, out_bin, out_nc, out_left, zero_after, cw);
   } else {
     using CT = typename HT<MODE>::T;
-    constexpr int NP = MODE == 1 ? 1 : 4;      // planes: packed u64 | (w, wy, wyy, rows) floats
+    constexpr int NP = MODE == 1 ? 1 : 3;      // planes: packed u64 | (w | rows << 32, w yq, w y2q) integers
     CT v[NP][4];
 #pragma unroll
     for (int q = 0; q < NP; ++q)
@@ -356,13 +380,13 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
     bool nc = false;
     double tot_rows;
     if constexpr (MODE == 1) tot_rows = (double)((uint64_t)tot[0] >> 42);
-    else tot_rows = (double)tot[3];
+    else tot_rows = reg_rows(tot[0]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int b = lane * 4 + i;
       double rl;
       if constexpr (MODE == 1) rl = (double)((uint64_t)v[0][i] >> 42);
-      else rl = (double)v[3][i];
+      else rl = reg_rows(v[0][i]);
       const double rr = tot_rows - rl;
       if (b == 255) continue;
       nc |= (rl > 0.0 && rr > 0.0);
@@ -378,10 +402,10 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
         R.add(t0 - l0); R.add(t1 - l1);
         if (side_too_light(s, L.w, R.w)) continue;
         g = cls_proxy(L, R, s.criterion);
-      } else {
-        const double l0 = (double)v[0][i], l1 = (double)v[1][i];
-        if (side_too_light(s, l0, (double)tot[0] - l0)) continue;
-        g = reg_proxy(s.criterion, l0, l1, (double)tot[0] - l0, (double)tot[1] - l1);
+      } else {   // the host builder's formula (forest_cpu.cpp), on the same integers
+        const double l0 = reg_w(v[0][i]), t0 = reg_w(tot[0]), l1 = reg_s1(v[1][i], *rq), t1 = reg_s1(tot[1], *rq);
+        if (side_too_light(s, l0, t0 - l0)) continue;
+        g = reg_proxy(s.criterion, l0, l1, t0 - l0, t1 - l1);
       }
       if (g > best) { best = g; bb = b; }
     }
@@ -400,17 +424,21 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
         out_left[2] = bb >= 0 ? (double)(cv >> 42) : 0.0;
       }
     } else {
-      float mine[4];
+      uint64_t mine[3];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < 3; ++q) {
         mine[q] = v[q][0];
 #pragma unroll
         for (int i = 1; i < 4; ++i) if (sel == i) mine[q] = v[q][i];
       }
+      uint64_t cq[3];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float cq = wave::bcast<float>(mine[q], src);
-        if (lane == 0) out_left[q] = bb >= 0 ? (double)cq : 0.0;
+      for (int q = 0; q < 3; ++q) cq[q] = wave::bcast<uint64_t>(mine[q], src);
+      if (lane == 0) {   // channels {w, w y, w y^2, rows}
+        out_left[0] = bb >= 0 ? reg_w(cq[0]) : 0.0;
+        out_left[1] = bb >= 0 ? reg_s1(cq[1], *rq) : 0.0;
+        out_left[2] = bb >= 0 ? reg_s2(cq[2], *rq) : 0.0;
+        out_left[3] = bb >= 0 ? reg_rows(cq[0]) : 0.0;
       }
     }
     if (lane == 0) { *out_gain = best; *out_bin = bb; *out_nc = any_nc ? 1 : 0; }
@@ -422,6 +450,7 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
                                  double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after,
                                  const double* cw) {
   using CT = typename HT<MODE>::T;
+  static_assert(MODE == 0, "binary and regression histograms are evaluated in registers (eval_feature)");
   const int planes = hist_planes(MODE, CH);
   for (int ch = 0; ch < planes; ++ch) scan256<CT>(h + ch * 256, lane);
   wave_lds_sync();
@@ -439,12 +468,7 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
     nc |= (rl > 0.0 && rr > 0.0);
     if (rl < msl || rr < msl) continue;
     double g;
-    if constexpr (MODE == 2) {
-      const double l0 = (double)h[b], t0 = (double)h[255];
-      const double l1 = (double)h[256 + b], t1 = (double)h[256 + 255];
-      if (side_too_light(s, l0, t0 - l0)) continue;
-      g = reg_proxy(s.criterion, l0, l1, t0 - l0, t1 - l1);
-    } else {
+    {
       ClsAcc L, R;
       L.init(s.criterion); R.init(s.criterion);
       for (int k = 0; k < C; ++k) {
@@ -487,15 +511,13 @@ __device__ __forceinline__ void hist_add_row(typename HT<MODE>::T* hist, const C
     const unsigned long long pv = pack_bin(c.ycls[row], w);
     for (int j = 0; j < g; ++j) atomicAdd(&hist[j * span + xr[feats[j]]], pv);
   } else {
-    const float yv = ty[row];
-    const float fw = (float)w, wy = fw * yv, wyy = wy * yv;
+    const RegPL p = reg_payload(c, w, ty[row]);
     for (int j = 0; j < g; ++j) {
       const int b = xr[feats[j]];
-      float* hj = hist + j * span;
-      atomicAdd(&hj[b], fw);
-      atomicAdd(&hj[256 + b], wy);
-      atomicAdd(&hj[512 + b], wyy);
-      atomicAdd(&hj[768 + b], 1.0f);
+      unsigned long long* hj = hist + j * span;
+      atomicAdd(&hj[b], p.wr);
+      atomicAdd(&hj[256 + b], p.wy);
+      atomicAdd(&hj[512 + b], p.wyy);
     }
   }
 }
@@ -622,38 +644,40 @@ __device__ void enqueue_or_leaf_v(const Ctx& c, const TreeSpec& s, int tree, int
   c.open[set][tier][idx] = on;
 }
 
-// histogram payload of one row: MODE 0 cls | w << 32, MODE 1 packed u64, MODE 2 (w, y) floats
+// histogram payload of one row (PLT above)
 template <int MODE>
-__device__ __forceinline__ uint64_t row_payload(const Ctx& c, const float* ty, uint32_t row, uint32_t w) {
+__device__ __forceinline__ typename PLT<MODE>::T row_payload(const Ctx& c, const float* ty, uint32_t row, uint32_t w) {
   if constexpr (MODE == 0) return (uint64_t)(uint32_t)c.ycls[row] | ((uint64_t)w << 32);
   else if constexpr (MODE == 1) return pack_bin(c.ycls[row], w);
-  else return (uint64_t)__builtin_bit_cast(uint32_t, (float)w) | ((uint64_t)__builtin_bit_cast(uint32_t, ty[row]) << 32);
+  else return reg_payload(c, w, ty[row]);
 }
 
 template <int MODE>
-__device__ __forceinline__ uint64_t word_payload(const Ctx& c, const TreeSpec& s, const float* ty, uint32_t wd) {
+__device__ __forceinline__ typename PLT<MODE>::T word_payload(const Ctx& c, const TreeSpec& s, const float* ty,
+                                                              uint32_t wd) {
   if (!c.packed) return row_payload<MODE>(c, ty, wd, boot_weight(s, wd));
   const uint32_t w = (wd >> c.rbits) & 15u;
   if constexpr (MODE == 0) return (uint64_t)(wd >> (c.rbits + 4)) | ((uint64_t)w << 32);
   else if constexpr (MODE == 1) return pack_bin((int)(wd >> (c.rbits + 4)), w);
-  else return (uint64_t)__builtin_bit_cast(uint32_t, (float)w) |
-              ((uint64_t)__builtin_bit_cast(uint32_t, ty[wd & c.rmask]) << 32);
+  else return reg_payload(c, w, ty[wd & c.rmask]);
 }
 
 template <int MODE>
-__device__ __forceinline__ void hist_add(typename HT<MODE>::T* hj, const Ctx& c, int b, uint64_t pl) {
+__device__ __forceinline__ void hist_add(typename HT<MODE>::T* hj, const Ctx& c, int b, const typename PLT<MODE>::T& pl) {
+#ifdef DML_X2_ATOMIC   // sensitivity build: every histogram atomic issued twice (the second adds 0)
+  if constexpr (MODE == 1) atomicAdd(&hj[b], (unsigned long long)(pl * (uint64_t)((uint32_t)c.n >> 31)));
+#endif
+  if constexpr (MODE == 2) {
+    atomicAdd(&hj[b], pl.wr);
+    atomicAdd(&hj[256 + b], pl.wy);
+    atomicAdd(&hj[512 + b], pl.wyy);
+    return;
+  }
   if constexpr (MODE == 0) {
     atomicAdd(&hj[(int)(uint32_t)pl * 256 + b], (uint32_t)(pl >> 32));
     atomicAdd(&hj[c.C * 256 + b], 1u);
   } else if constexpr (MODE == 1) {
     atomicAdd(&hj[b], (unsigned long long)pl);
-  } else {
-    const float fw = __builtin_bit_cast(float, (uint32_t)pl), yv = __builtin_bit_cast(float, (uint32_t)(pl >> 32));
-    const float wy = fw * yv, wyy = wy * yv;
-    atomicAdd(&hj[b], fw);
-    atomicAdd(&hj[256 + b], wy);
-    atomicAdd(&hj[512 + b], wyy);
-    atomicAdd(&hj[768 + b], 1.0f);
   }
 }
 
@@ -703,7 +727,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   // for every feature group and the partition; larger nodes stream in NT*RPT chunks.
   const bool reg_rows = cnt <= NT * RPT;
   uint32_t rrow[RPT], rbin[RPT];
-  uint64_t rpl[RPT];
+  using PL = typename PLT<MODE>::T;
+  PL rpl[RPT];
   auto load_rows = [&](int base) {
 #pragma unroll
     for (int u = 0; u < RPT; ++u) {
@@ -712,7 +737,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     }
 #pragma unroll
     for (int u = 0; u < RPT; ++u)
-      rpl[u] = rrow[u] != 0xFFFFFFFFu ? word_payload<MODE>(c, s, ty, rrow[u]) : 0ull;
+      rpl[u] = rrow[u] != 0xFFFFFFFFu ? word_payload<MODE>(c, s, ty, rrow[u]) : PL{};
   };
   if (reg_rows) load_rows(0);
 #pragma unroll
@@ -737,6 +762,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
 #pragma unroll
         for (int u = 0; u < RPT; ++u)
           raw[q][u] = (q < npre && rrow[u] != 0xFFFFFFFFu) ? (uint32_t)c.Xb[(int64_t)(rrow[u] & c.rmask) * c.ld + f] : 0u;
+#ifdef DML_X2_GATHER   // sensitivity build: every bin gathered twice
+#pragma unroll
+      for (int u = 0; u < RPT; ++u)
+        raw[q][u] |= (q < npre && rrow[u] != 0xFFFFFFFFu) ? (uint32_t)c.Xb[(int64_t)(rrow[u] & c.rmask) * c.ld + f + ((uint32_t)c.n >> 31)] : 0u;
+#endif
       }
 #pragma unroll
       for (int q = 0; q < KPRE; ++q) {
@@ -776,17 +806,22 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
       for (int j = 0; j < KGMAX; ++j) fj[j] = j < g ? (int)feats[j] : 0;
       auto row_at = [&](int r) -> uint32_t { return r < cnt ? rows[r] : INV; };
       uint32_t r0 = row_at(tid), r1 = row_at(NT + tid);
-      uint64_t pl0 = r0 != INV ? word_payload<MODE>(c, s, ty, r0) : 0ull;
+      PL pl0 = r0 != INV ? word_payload<MODE>(c, s, ty, r0) : PL{};
       uint32_t b0[KGMAX];
 #pragma unroll
       for (int j = 0; j < KGMAX; ++j)
         b0[j] = (j < g && r0 != INV) ? (uint32_t)c.Xb[(int64_t)(r0 & c.rmask) * c.ld + fj[j]] : 0u;
       for (int base = 0; base < cnt; base += NT) {
-        const uint64_t pl1 = r1 != INV ? word_payload<MODE>(c, s, ty, r1) : 0ull;
+        const PL pl1 = r1 != INV ? word_payload<MODE>(c, s, ty, r1) : PL{};
         uint32_t b1[KGMAX];
 #pragma unroll
         for (int j = 0; j < KGMAX; ++j)
           b1[j] = (j < g && r1 != INV) ? (uint32_t)c.Xb[(int64_t)(r1 & c.rmask) * c.ld + fj[j]] : 0u;
+#ifdef DML_X2_GATHER
+#pragma unroll
+        for (int j = 0; j < KGMAX; ++j)
+          b1[j] |= (j < g && r1 != INV) ? (uint32_t)c.Xb[(int64_t)(r1 & c.rmask) * c.ld + fj[j] + ((uint32_t)c.n >> 31)] : 0u;
+#endif
         const uint32_t r2 = row_at(base + 2 * NT + tid);
         if (r0 != INV) {
           if (NT == 256 && KGMAX == 16 && pos == 0) {
@@ -865,9 +900,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     }
     __syncthreads();
     PH(2)
-    for (int j = wid; j < g; j += NW)
+    for (int j = wid; j < g; j += NW) {
+#ifdef DML_X2_EVAL   // sensitivity build: every feature evaluated twice (the first keeps the histogram)
+      eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, false,
+                         tree_cw(c, on.tree), &c.rq);
+      wave_lds_sync();
+#endif
       eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, true,
-                         tree_cw(c, on.tree));
+                         tree_cw(c, on.tree), &c.rq);
+    }
     __syncthreads();
     PH(3)
     if (wid == 0) {
@@ -949,6 +990,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     enqueue_or_leaf_v(c, s, on.tree, base + 1, on.start + nl, cnt - nl, on.depth + 1, child_key(on.key, 1),
                       1 - set_cur, rvs);
   // ---- stable partition: RPT ballot rounds per chunk, one block-level offset exchange
+#ifdef DML_X2_PART   // sensitivity build: the (idempotent) partition pass runs twice
+  for (int rep_ = 0; rep_ < 2; ++rep_) {
+#endif
   uint32_t* out = c.rows_next + on.start;
   int baseL = 0, baseR = 0;
   // streaming (large-node) partition: the split-feature bins of the next chunk and the row
@@ -1029,6 +1073,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     baseL += totL; baseR += totR;
     if (!reg_rows && RPT == 1) { rrow[0] = nrow; rbin[0] = nbin; nrow = frow; }
   }
+#ifdef DML_X2_PART
+  }
+#endif
   PH(6)
   PH_END(NT == 64 ? 0 : 1)
 }
@@ -1052,7 +1099,7 @@ struct SubEntry {
 // evaluate one feature for the rows in `mask`; lane data: bin b (valid if in mask).
 template <bool REG>
 __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt, int lane, int my_bin, int my_cls,
-                         float my_w, float my_y, double& gain, int& bin, bool& nonconst, const double* cw) {
+                         float my_w, int64_t my_yq, double& gain, int& bin, bool& nonconst, const double* cw) {
   const bool act = (mask >> lane) & 1ull;
   const uint32_t key = act ? ((uint32_t)my_bin << 6) | (uint32_t)lane : 0xFFFFFFFFu;
   const uint32_t sk = wave::bitonic64(key, lane);
@@ -1087,14 +1134,19 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
     ok = cand && !side_too_light(s, L.w, R.w);
     if (ok) g = cls_proxy(L, R, s.criterion);
   } else {
-    const float wsh = __shfl(my_w, src);
-    const float y = __shfl(my_y, src);
-    const float w = valid_row ? wsh : 0.f;
-    const float p0 = wave::incl_scan<float>(w);
-    const float p1 = wave::incl_scan<float>(w * y);
-    const float t0 = wave::bcast<float>(p0, cnt - 1), t1 = wave::bcast<float>(p1, cnt - 1);
-    ok = cand && !side_too_light(s, (double)p0, (double)(t0 - p0));
-    if (ok) g = reg_proxy(s.criterion, (double)p0, (double)p1, (double)(t0 - p0), (double)(t1 - p1));
+    // integer prefix sums of w and w yq in (bin, lane) order: at the last lane of a bin
+    // run they are the host builder's histogram prefix sums (forest_common.h)
+    const uint32_t wsh = (uint32_t)__shfl((int)(uint32_t)my_w, src);
+    const uint32_t ylo = (uint32_t)__shfl((int)(uint32_t)(uint64_t)my_yq, src);
+    const uint32_t yhi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)my_yq >> 32), src);
+    const int64_t yq = (int64_t)(((uint64_t)yhi << 32) | ylo);
+    const uint64_t w = valid_row ? (uint64_t)wsh : 0ull;
+    const uint64_t wy = valid_row ? (uint64_t)((int64_t)wsh * yq) : 0ull;
+    const uint64_t p0 = wave::incl_scan_u64(w), p1 = wave::incl_scan_u64(wy);
+    const uint64_t t0 = wave::bcast<uint64_t>(p0, cnt - 1), t1 = wave::bcast<uint64_t>(p1, cnt - 1);
+    const double l0 = (double)p0, tt0 = (double)t0, l1 = reg_s1(p1, c.rq), tt1 = reg_s1(t1, c.rq);
+    ok = cand && !side_too_light(s, l0, tt0 - l0);
+    if (ok) g = reg_proxy(s.criterion, l0, l1, tt0 - l0, tt1 - l1);
   }
   int bl = ok ? lane : 64;
   wave::argmax(g, bl, lane);
@@ -1240,17 +1292,41 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   const uint32_t* rows = c.rows_cur + on.start;
   uint32_t row = 0;
   int my_cls = 0;
-  float my_w = 0.f, my_y = 0.f;
+  float my_w = 0.f;
+  int64_t my_yq = 0, my_y2q = 0;   // regression: the row's fixed-point y, y^2
   if (lane < cnt0) {
     const uint32_t wd = rows[lane];
     row = word_row(c, wd);
     my_w = (float)word_weight(c, s, wd);
-    if constexpr (REG) my_y = tree_y(c, s)[row];
+    if constexpr (REG) reg_quantize(tree_y(c, s)[row], c.rq, my_yq, my_y2q);
     else my_cls = word_cls(c, wd);
   }
   const uint8_t* xg = c.Xb + (int64_t)row * c.ld;
-  if (cache && lane < cnt0)
-    for (int j = 0; j < d; ++j) xc[lane * dp + j] = xg[j];
+  if (cache && lane < cnt0) {
+    // the row's bins, ONE 16-B load per 16 features (a byte loop costs the vector memory
+    // pipeline one address per feature per row: 100 instead of 7 at d = 100) and one
+    // 4-B LDS store per 4 features (dp is a multiple of 4)
+    if ((c.ld & 15) == 0 && c.ld >= ((d + 15) & ~15)) {
+      const uint4* src = (const uint4*)xg;
+      uint32_t* dst = (uint32_t*)(xc + lane * dp);
+      const int nw = dp >> 2, nseg = (d + 15) >> 4;
+      for (int q0 = 0; q0 < nseg; q0 += 8) {   // 8 loads in flight before the first store
+        uint4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = q0 + i < nseg ? src[q0 + i] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int w0 = 4 * (q0 + i);
+          if (w0 + 0 < nw) dst[w0 + 0] = v[i].x;
+          if (w0 + 1 < nw) dst[w0 + 1] = v[i].y;
+          if (w0 + 2 < nw) dst[w0 + 2] = v[i].z;
+          if (w0 + 3 < nw) dst[w0 + 3] = v[i].w;
+        }
+      }
+    } else {
+      for (int j = 0; j < d; ++j) xc[lane * dp + j] = xg[j];
+    }
+  }
   // a subtree over cnt0 rows has at most cnt0 - 1 splits: reserve all node pairs with ONE
   // pool atomic (unused pairs stay unreferenced)
   int pool_base = 0;
@@ -1308,7 +1384,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
       double g;
       int bb;
       bool nc;
-      sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_y, g, bb, nc, tcw);
+      sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_yq, g, bb, nc, tcw);
       if (nc) {
         ++nonconst;
         if (bb >= 0 && g > best_g) { best_g = g; best_f = f; best_b = bb; }
@@ -1323,13 +1399,16 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     for (int k = 0; k < VC; ++k) {
       double v;
       const bool inl = (lm >> lane) & 1ull;
-      if constexpr (REG) {
-        v = !inl ? 0.0 : (k == 0 ? (double)my_w : (k == 1 ? (double)my_w * my_y : (double)my_w * my_y * my_y));
+      if constexpr (REG) {   // integer sums (exact in any order), then the double channels
+        const int64_t wi = (int64_t)my_w;
+        uint64_t q = !inl ? 0ull : (uint64_t)(k == 0 ? wi : (k == 1 ? wi * my_yq : wi * my_y2q));
+        q = wave::sum<uint64_t>(q, lane);
+        v = k == 0 ? (double)q : (k == 1 ? reg_s1(q, c.rq) : reg_s2(q, c.rq));
       } else {
         v = (inl && my_cls == k) ? (double)my_w : 0.0;
+        v = wave::sum<double>(v, lane);     // integer-valued: exact in any order
+        v *= cwk(tcw, k);
       }
-      v = wave::sum<double>(v, lane);     // integer-valued: exact in any order
-      if constexpr (!REG) v *= cwk(tcw, k);
       if (lane == 0) { left_ch[k] = v; right_ch[k] = pv[k] - v; }
     }
     wave_lds_sync();
@@ -1440,12 +1519,13 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
     auto row_at = [&](int r) -> uint32_t { return r < r1 ? rows[r] : INV; };
     const int t0 = r0 + (int)threadIdx.x;
     uint32_t ra = row_at(t0), rbn = row_at(t0 + 256);
-    uint64_t pa = ra != INV ? word_payload<MODE>(c, s, ty, ra) : 0ull;
+    using PL = typename PLT<MODE>::T;
+    PL pa = ra != INV ? word_payload<MODE>(c, s, ty, ra) : PL{};
     uint32_t ba[KGL];
 #pragma unroll
     for (int j = 0; j < KGL; ++j) ba[j] = (j < g && ra != INV) ? large_bin(c, ra, fj[j]) : 0u;
     for (int r = t0; r < r1; r += 256) {
-      const uint64_t pb = rbn != INV ? word_payload<MODE>(c, s, ty, rbn) : 0ull;
+      const PL pb = rbn != INV ? word_payload<MODE>(c, s, ty, rbn) : PL{};
       uint32_t bb[KGL];
 #pragma unroll
       for (int j = 0; j < KGL; ++j) bb[j] = (j < g && rbn != INV) ? large_bin(c, rbn, fj[j]) : 0u;
@@ -1472,8 +1552,9 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
     }
   }
   __syncthreads();
-  // flush into the node's global histogram: always unpacked planes [CH][256]
-  const int gspan = c.CH * 256;
+  // flush into the node's global histogram: unpacked planes [CH][256] (u32) for
+  // classification, the three integer planes (u64) for regression
+  const int gspan = hist_planes(MODE == 1 ? 0 : MODE, c.CH) * 256;
   if constexpr (MODE == 1) {
     uint32_t* gh = (uint32_t*)c.ghist + (int64_t)slot * c.kg_large * gspan;
     for (int i = threadIdx.x; i < g * 256; i += 256) {
@@ -1504,7 +1585,7 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   LState& st = c.lstate[slot];
   if (st.done) return;
   const TreeSpec& s = c.specs[st.on.tree];
-  const int g = st.g, span = c.CH * 256;
+  const int g = st.g, span = hist_planes(MODE, c.CH) * 256;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   CT* hist = (CT*)smem;
   double* rg = (double*)(smem + (size_t)c.kg_large * span * sizeof(CT));
@@ -1517,7 +1598,7 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   __syncthreads();
   for (int j = wid; j < g; j += 4)
     eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, false,
-                       tree_cw(c, st.on.tree));
+                       tree_cw(c, st.on.tree), &c.rq);
   __syncthreads();
   const int16_t* feats = c.lperm + (int64_t)slot * c.d + st.pos;
   double* best_left = c.lbest_left + (int64_t)slot * c.CH;
@@ -1674,7 +1755,9 @@ __global__ __launch_bounds__(256) void k_fill_active(Ctx c) {
   __shared__ int wcnt[16];
   __shared__ int base_s;
   __shared__ double acc[kMaxClasses];
+  __shared__ unsigned long long racc[3];   // regression: integer sums w, w yq, w y2q
   for (int k = tid; k < kMaxClasses; k += 256) acc[k] = 0.0;
+  if (tid < 3) racc[tid] = 0ull;
   const int r0 = blockIdx.x * 1024;
   uint32_t wts[4];
   bool act[4];
@@ -1710,19 +1793,22 @@ __global__ __launch_bounds__(256) void k_fill_active(Ctx c) {
       if constexpr (!REG) wd |= (uint32_t)c.ycls[r] << (c.rbits + 4);
     }
     out[p++] = wd;
-    const double w = (double)wts[i];
     if constexpr (REG) {
-      const double y = (double)tree_y(c, s)[r];
-      atomicAdd(&acc[0], w);
-      atomicAdd(&acc[1], w * y);
-      atomicAdd(&acc[2], w * y * y);
+      const RegPL q = reg_payload(c, wts[i], tree_y(c, s)[r]);
+      atomicAdd(&racc[0], (unsigned long long)wts[i]);
+      atomicAdd(&racc[1], q.wy);
+      atomicAdd(&racc[2], q.wyy);
     } else {
-      atomicAdd(&acc[c.ycls[r]], w);
+      atomicAdd(&acc[c.ycls[r]], (double)wts[i]);
     }
   }
   __syncthreads();
-  for (int k = tid; k < c.VC; k += 256)
-    if (acc[k] != 0.0) atomicAdd(&c.node_val[(int64_t)t * c.VC + k], acc[k]);
+  if constexpr (REG) {
+    if (tid < 3 && racc[tid]) atomicAdd(&c.rsum[(int64_t)t * 3 + tid], racc[tid]);
+  } else {
+    for (int k = tid; k < c.VC; k += 256)
+      if (acc[k] != 0.0) atomicAdd(&c.node_val[(int64_t)t * c.VC + k], acc[k]);
+  }
 }
 
 __global__ void k_init_counters(Ctx c) { c.counters[kPool] = c.T; }
@@ -1732,6 +1818,11 @@ __global__ void k_roots(Ctx c) {
   if (t >= c.T) return;
   NodeRec leaf; leaf.split = -1; leaf.left = -1;
   c.nodes[t] = leaf;
+  if (c.is_reg) {   // integer root sums -> the double channels (forest_common.h)
+    const unsigned long long* q = c.rsum + (int64_t)t * 3;
+    double* v = c.node_val + (int64_t)t * c.VC;
+    v[0] = (double)q[0]; v[1] = reg_s1(q[1], c.rq); v[2] = reg_s2(q[2], c.rq);
+  }
   if (!c.is_reg && c.cw && c.specs[t].cw_mode) {
     double* row = const_cast<double*>(c.cw) + (int64_t)t * c.C;
     double* v = c.node_val + (int64_t)t * c.VC;
@@ -1754,9 +1845,17 @@ __global__ void k_roots(Ctx c) {
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct Layout {
-  size_t rows_b, open[2][kTiers], counters, cursors, lstate, lperm, lbest, ghist, lcursor, bscr, total;
+  size_t rows_b, open[2][kTiers], counters, cursors, lstate, lperm, lbest, ghist, lcursor, bscr, rsum, total;
   int64_t open_cap[kTiers], large_cap;
 };
+
+static int build_mode(const ForestArgs* a) { return a->is_reg ? 2 : (a->n_classes == 2 ? 1 : 0); }
+
+static size_t mode_elem(int mode) { return mode == 0 ? 4 : 8; }
+
+// bytes of one feature's large-tier GLOBAL histogram: u32 [CH][256] (classification,
+// binary unpacked), u64 [3][256] (regression integer planes)
+static size_t ghist_feat_bytes(int mode, int CH) { return mode == 2 ? (size_t)3 * 256 * 8 : (size_t)CH * 256 * 4; }
 
 static Layout plan(const ForestArgs* a) {
   Layout L{};
@@ -1779,21 +1878,18 @@ static Layout plan(const ForestArgs* a) {
   L.lstate = take((size_t)L.large_cap * sizeof(LState));
   L.lperm = take((size_t)L.large_cap * a->d * 2);
   L.lbest = take((size_t)L.large_cap * CH * 8);
-  L.ghist = take((size_t)L.large_cap * a->kg_large * CH * 256 * 4);
+  L.ghist = take((size_t)L.large_cap * a->kg_large * ghist_feat_bytes(build_mode(a), (int)CH));
   L.lcursor = take((size_t)L.large_cap * 8);
   L.bscr = take((size_t)R * 16);
+  L.rsum = take((size_t)T * 3 * 8);
   L.total = off;
   return L;
 }
 
-static int build_mode(const ForestArgs* a) { return a->is_reg ? 2 : (a->n_classes == 2 ? 1 : 0); }
-
-static size_t mode_elem(int mode) { return mode == 1 ? 8 : 4; }
-
 static size_t fused_lds(const ForestArgs* a, int KG) {
   const int CH = a->is_reg ? 4 : (int)a->n_classes + 1;
   const int mode = build_mode(a);
-  const int span = (mode == 1 ? 1 : CH) * 256;
+  const int span = hist_planes(mode, CH) * 256;
   return fused_layout(KG, span, (int)mode_elem(mode), CH).total + 16;
 }
 
@@ -1830,6 +1926,8 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.ghist = (void*)(ws + L.ghist);
   c.lcursor = (int32_t*)(ws + L.lcursor);
   c.bscr = ws + L.bscr;
+  c.rsum = (unsigned long long*)(ws + L.rsum);
+  c.rq = reg_scale((int)a->yq_e1, (int)a->yq_e2);
   c.XbT = (const uint8_t*)a->XbT;
   c.cw = (const double*)a->cw;
   c.large_cap = L.large_cap;
@@ -1985,6 +2083,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   HIP_OK(hipMemsetAsync(c.counters, 0, kNumCounters * 4, st));
   HIP_OK(hipMemsetAsync(c.cursors, 0, a->T * 4, st));
   HIP_OK(hipMemsetAsync(c.node_val, 0, (size_t)a->T * c.VC * 8, st));
+  if (reg) HIP_OK(hipMemsetAsync(c.rsum, 0, (size_t)a->T * 3 * 8, st));
   k_init_counters<<<1, 1, 0, st>>>(c);
   dim3 gfill((unsigned)((a->n + 1023) / 1024), (unsigned)a->T);
   if (reg) k_fill_active<true><<<gfill, 256, 0, st>>>(c);
@@ -1997,8 +2096,9 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   int32_t* h_pool = h + 48;   // pinned slot for the per-level pool reservation (H2D)
   const size_t lds_b = fused_lds(a, (int)a->kg_block);
   const int CH = c.CH;
-  const size_t lds_hl = (size_t)a->kg_large * (MODE == 1 ? 1 : CH) * 256 * mode_elem(MODE);
-  const size_t lds_sl = (size_t)a->kg_large * CH * 256 * 4 + a->kg_large * 16 + 16 + (size_t)a->kg_large * CH * 8 + 64;
+  const size_t lds_hl = (size_t)a->kg_large * hist_planes(MODE, CH) * 256 * mode_elem(MODE);
+  const size_t lds_sl = (size_t)a->kg_large * ghist_feat_bytes(MODE, CH) + a->kg_large * 16 + 16 +
+                        (size_t)a->kg_large * CH * 8 + 64;
   const size_t lds_max = 160 * 1024;
   if (lds_w > lds_max || lds_b > lds_max || lds_sl > lds_max || lds_s > lds_max) return 7;
   if (a->sub_max > 64) return 9;
@@ -2034,7 +2134,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     }
     a->tier_nodes_out[0] += ns; a->tier_nodes_out[1] += nw; a->tier_nodes_out[2] += nb; a->tier_nodes_out[3] += nL;
     SideStreams* ss = side_streams();
-    const bool fork = ss != nullptr && ((ns > 0) + (nw > 0) + (nb > 0) + (nL > 0)) > 1;
+    static const bool serial_tiers = getenv("DML_SERIAL_TIERS") != nullptr;   // profiling: tiers one after another
+    const bool fork = !serial_tiers && ss != nullptr && ((ns > 0) + (nw > 0) + (nb > 0) + (nL > 0)) > 1;
     hipStream_t s0 = st, s1 = st, s2 = st;
     if (fork) {
       HIP_OK(hipEventRecord(ss->fork, st));
@@ -2048,7 +2149,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       k_large_prep<<<nL, 64, 0, st>>>(c, cur, nL);
       while (true) {
         ++large_rounds;
-        HIP_OK(hipMemsetAsync(c.ghist, 0, (size_t)nL * a->kg_large * CH * 256 * 4, st));
+        HIP_OK(hipMemsetAsync(c.ghist, 0, (size_t)nL * a->kg_large * ghist_feat_bytes(MODE, CH), st));
         HIP_OK(hipMemsetAsync(c.counters + kNeedMore, 0, 4, st));
         const dim3 gh = DML_LARGE_NODE_FAST ? dim3((unsigned)nL, nchunks) : dim3(nchunks, (unsigned)nL);
         k_hist_large<MODE><<<gh, 256, lds_hl, st>>>(c);

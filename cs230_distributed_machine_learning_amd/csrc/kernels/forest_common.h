@@ -231,6 +231,66 @@ DML_HD double cls_proxy(const ClsAcc& l, const ClsAcc& r, int crit) {
   return (l.sq * r.w + r.sq * l.w) / (l.w * r.w);  // = l.sq/l.w + r.sq/r.w with one division
 }
 
+// ---- regression sums: exact, order-independent fixed point --------------------------
+// Regression histograms (both builders, every tier) accumulate per bin, in 64-bit INTEGER
+// arithmetic: sum w and the row count packed as (w | rows << 32), sum w*yq and sum w*y2q,
+// with yq = rint(y 2^e1), y2q = rint(y^2 2^e2).  e1 / e2 are chosen per build (host side,
+// `reg_exponents`) so that no sum over a tree's rows can exceed 2^62 in magnitude.
+// Integer sums are exact in ANY order: GPU atomics no longer make a regression tree
+// depend on arrival order, and the C++ builder, doing the same integer sums, grows the
+// identical tree (sklearn accumulates these sums in float64; the fixed-point grid is
+// max|y| 2^-38 at a million rows, below fp32 y's own resolution for all but tiny y).
+// Doubles are formed from the integer sums only for scoring:
+//   channel 0: (double)(sum w), 1: (double)sum(w yq) 2^-e1, 2: (double)sum(w y2q) 2^-e2,
+//   3: rows (regression best_left / node layout {w, wy, wyy} + rows, as before).
+struct RegScale {
+  double s1, s2, i1, i2;   // 2^e1, 2^e2, 2^-e1, 2^-e2
+};
+
+DML_HD RegScale reg_scale(int e1, int e2) {
+  RegScale q;
+  q.s1 = ldexp(1.0, e1); q.s2 = ldexp(1.0, e2);
+  q.i1 = ldexp(1.0, -e1); q.i2 = ldexp(1.0, -e2);
+  return q;
+}
+
+// exponents of a build: every |sum| <= 15 n max|y| 2^e1 < 2^61 (bootstrap weights <= 15),
+// likewise y^2 for e2 (ops/forest_ops.py `reg_exponents` mirrors this rule exactly)
+DML_HD void reg_exponents(double max_abs_y, int64_t n, int& e1, int& e2) {
+  e1 = 0; e2 = 0;
+  if (!(max_abs_y > 0.0) || n <= 0) return;
+  int kw, k;
+  frexp(15.0 * (double)n, &kw);   // 15 n < 2^kw
+  frexp(max_abs_y, &k);           // max|y| < 2^k
+  e1 = 61 - kw - k;
+  e2 = 61 - kw - 2 * k;
+  e1 = e1 < -1000 ? -1000 : (e1 > 1000 ? 1000 : e1);
+  e2 = e2 < -1000 ? -1000 : (e2 > 1000 ? 1000 : e2);
+}
+
+// round half to even, identically on host (llrint, default rounding mode) and device
+DML_HD int64_t reg_round(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (int64_t)__double2ll_rn(v);
+#else
+  return (int64_t)llrint(v);
+#endif
+}
+
+// a row's fixed-point target and squared target (y*y is exact in double: 48-bit product)
+DML_HD void reg_quantize(float y, const RegScale& q, int64_t& yq, int64_t& y2q) {
+  const double yd = (double)y;
+  yq = reg_round(yd * q.s1);
+  y2q = reg_round((yd * yd) * q.s2);
+}
+
+constexpr uint64_t kRegLo32 = 0xFFFFFFFFull;
+// the double channels of integer sums (w | rows << 32, sum w yq, sum w y2q)
+DML_HD double reg_w(uint64_t wr) { return (double)(wr & kRegLo32); }
+DML_HD double reg_rows(uint64_t wr) { return (double)(wr >> 32); }
+DML_HD double reg_s1(uint64_t v, const RegScale& q) { return (double)(int64_t)v * q.i1; }
+DML_HD double reg_s2(uint64_t v, const RegScale& q) { return (double)(int64_t)v * q.i2; }
+
 // regression: s0 = sum w, s1 = sum w*y, s2 = sum w*y^2
 DML_HD double mse_impurity(double s0, double s1, double s2) {
   if (s0 <= 0.0) return 0.0;

@@ -55,7 +55,8 @@ struct DpArgs {
   int64_t specs, T;                  // TreeSpec [T]
   int64_t cw;                        // double [T][C] class weights (cls) or 0
   int64_t tree_W;                    // double [T]
-  int64_t root;                      // double [T][CH] root statistics (all-reduced)
+  int64_t root;                      // [T][CH] root statistics (all-reduced): double (cls) |
+                                     // int64 {sum w, sum w yq, sum w y2q, rows} (reg)
   int64_t wts;                       // uint8 [T][n] bootstrap weight of (tree, local row) (init only)
   // (tree, row) pairs of every open node, sorted by node
   int64_t act_row, act_tree, act_node, A;
@@ -66,7 +67,8 @@ struct DpArgs {
   // one search round
   int64_t srch, S, KR;               // int32 [S] slot ids being searched; KR positions each
   int64_t feats;                     // int32 [S][KR] feature of each position (-1 past d)
-  int64_t hist;                      // [S][KR][CH][256] uint32 (cls) | float (reg)
+  int64_t hist;                      // [S][KR][CH][256] uint32 (cls) | [S][KR][3][256] uint64 (reg:
+                                     // w | rows << 32, sum w yq, sum w y2q -- exact, see forest_common.h)
   int64_t tile_s, tile_off, n_tiles, tile_rows;  // LDS tiles: search index, pair offset in the segment
   int64_t small_s, n_small;          // search indices of small segments (global atomics)
   int64_t lds_feats;                 // positions per LDS pass (hist tiles)
@@ -78,10 +80,14 @@ struct DpArgs {
   // threshold refinement
   int64_t hi, binvals, exact, P_total;
   int64_t ystride;                   // > 0: yreg is [targets][ystride], tree t regresses on row specs[t].target
+  int64_t yq_e1, yq_e2;              // regression fixed point (forest_common.h), global over the ranks
 };
 
 template <typename T>
 DML_HD T* dp_ptr(int64_t v) { return (T*)(uintptr_t)v; }
+
+// 32-bit words of one searching slot's histogram block
+DML_HD int64_t dp_hist_words(const DpArgs& a) { return a.is_reg ? a.KR * 3 * 256 * 2 : a.KR * a.CH * 256; }
 
 // regression target of (tree, local row): gradient boosting gives every tree its own row
 DML_HD float dp_target(const DpArgs& a, int tree, int64_t r) {
@@ -112,13 +118,17 @@ DML_HD int dp_root_one(const DpArgs& a, int t, DpSlot* slot) {
   const int C = (int)a.C, CH = (int)a.CH, VC = (int)a.VC;
   const double* st = dp_ptr<const double>(a.root) + (int64_t)t * CH;
   double* v = dp_ptr<double>(a.vals) + (int64_t)t * VC;
+  double count;
   int32_t* nd = dp_ptr<int32_t>(a.nodes) + 2 * (int64_t)t;
   nd[0] = -1;
   nd[1] = -1;
   double W = 0.0;
-  if (a.is_reg) {
-    v[0] = st[0]; v[1] = st[1]; v[2] = st[2];
-    W = st[0];
+  if (a.is_reg) {   // exact integer sums over every rank's rows
+    const RegScale q = reg_scale((int)a.yq_e1, (int)a.yq_e2);
+    const uint64_t* si = dp_ptr<const uint64_t>(a.root) + (int64_t)t * CH;
+    v[0] = (double)si[0]; v[1] = reg_s1(si[1], q); v[2] = reg_s2(si[2], q);
+    W = v[0];
+    count = (double)si[3];
   } else {
     double* cwv = a.cw ? dp_ptr<double>(a.cw) + (int64_t)t * C : nullptr;
     if (cwv && s.cw_mode == 2) balanced_weights(st, C, cwv);
@@ -126,10 +136,10 @@ DML_HD int dp_root_one(const DpArgs& a, int t, DpSlot* slot) {
       v[k] = (cwv && s.cw_mode != 0) ? st[k] * cwv[k] : st[k];
       W += v[k];
     }
+    count = st[CH - 1];
   }
   dp_ptr<double>(a.tree_W)[t] = W;
   dp_ptr<TreeSpec>(a.specs)[t].min_weight_leaf = s.min_weight_frac * W;   // read by every later step
-  const double count = st[CH - 1];
   slot->key = root_key(s.seed);
   slot->best_gain = -INFINITY;
   slot->count = count;
@@ -211,17 +221,18 @@ DML_HDM void dp_eval_slot(const DpArgs& a, DpSlot& sl, double* best_left, const 
         }
       }
     } else {
-      // float prefix sums in bin order: the CPU builder's in-place cumsum
-      const float* hf = (const float*)h + (int64_t)k * 4 * 256;
-      float tot[4] = {0.f, 0.f, 0.f, 0.f}, pre[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int ch = 0; ch < 4; ++ch)
-        for (int b = 0; b < 256; ++b) tot[ch] += hf[ch * 256 + b];
+      // integer prefix sums in bin order: forest_cpu.cpp's regression histogram scan
+      const RegScale q = reg_scale((int)a.yq_e1, (int)a.yq_e2);
+      const uint64_t* hr = (const uint64_t*)h + (int64_t)k * 3 * 256;
+      uint64_t tot[3] = {0ull, 0ull, 0ull}, pre[3] = {0ull, 0ull, 0ull};
+      for (int ch = 0; ch < 3; ++ch)
+        for (int b = 0; b < 256; ++b) tot[ch] += hr[ch * 256 + b];
       for (int b = 0; b < 255; ++b) {
-        for (int ch = 0; ch < 4; ++ch) pre[ch] += hf[ch * 256 + b];
-        const float rl = pre[3], rr = tot[3] - rl;
-        nc |= (rl > 0.f && rr > 0.f);
-        if (rl < (float)s.min_samples_leaf || rr < (float)s.min_samples_leaf) continue;
-        const double l0 = pre[0], t0 = tot[0], l1 = pre[1], t1 = tot[1];
+        for (int ch = 0; ch < 3; ++ch) pre[ch] += hr[ch * 256 + b];
+        const uint32_t rl = (uint32_t)(pre[0] >> 32), rr = (uint32_t)(tot[0] >> 32) - rl;
+        nc |= (rl > 0 && rr > 0);
+        if (rl < (uint32_t)s.min_samples_leaf || rr < (uint32_t)s.min_samples_leaf) continue;
+        const double l0 = reg_w(pre[0]), t0 = reg_w(tot[0]), l1 = reg_s1(pre[1], q), t1 = reg_s1(tot[1], q);
         if (side_too_light(s, l0, t0 - l0)) continue;
         const double g = reg_proxy(s.criterion, l0, l1, t0 - l0, t1 - l1);
         if (g > g_best) {
@@ -235,11 +246,11 @@ DML_HDM void dp_eval_slot(const DpArgs& a, DpSlot& sl, double* best_left, const 
           sl.best_gain = g_best;
           sl.best_feat = feat;
           sl.best_bin = b_best;
-          for (int ch = 0; ch < 4; ++ch) {
-            float acc = 0.f;
-            for (int b = 0; b <= b_best; ++b) acc += hf[ch * 256 + b];
-            best_left[ch] = (double)acc;
-          }
+          uint64_t acc[3] = {0ull, 0ull, 0ull};
+          for (int ch = 0; ch < 3; ++ch)
+            for (int b = 0; b <= b_best; ++b) acc[ch] += hr[ch * 256 + b];
+          best_left[0] = reg_w(acc[0]); best_left[1] = reg_s1(acc[1], q); best_left[2] = reg_s2(acc[2], q);
+          best_left[3] = reg_rows(acc[0]);
         }
       }
     }

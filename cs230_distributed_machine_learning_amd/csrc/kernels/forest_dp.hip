@@ -39,11 +39,8 @@ __global__ void k_dp_weights(DpArgs a) {
 
 // local root statistics [T][CH] (doubles; classification sums are integers, exact)
 __global__ void k_dp_root_stats(DpArgs a) {
-  __shared__ double acc[kMaxClasses + 1];
   const int t = blockIdx.y;
   const int CH = (int)a.CH;
-  for (int c = threadIdx.x; c < CH; c += blockDim.x) acc[c] = 0.0;
-  __syncthreads();
   const uint8_t* w8 = dp_ptr<const uint8_t>(a.wts) + (int64_t)t * a.n;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   if (!a.is_reg) {
@@ -62,18 +59,24 @@ __global__ void k_dp_root_stats(DpArgs a) {
       if (cnt[c]) atomicAdd(dp_ptr<double>(a.root) + (int64_t)t * CH + c, (double)cnt[c]);
     return;
   }
+  // regression: exact integer sums {w, w yq, w y2q, rows} (forest_common.h)
+  __shared__ unsigned long long racc[4];
+  if (threadIdx.x < 4) racc[threadIdx.x] = 0ull;
+  __syncthreads();
+  const RegScale q = reg_scale((int)a.yq_e1, (int)a.yq_e2);
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += stride) {
     const uint32_t w = w8[r];
     if (!w) continue;
-    const double y = (double)dp_target(a, t, r);
-    atomicAdd(&acc[0], (double)w);
-    atomicAdd(&acc[1], (double)w * y);
-    atomicAdd(&acc[2], (double)w * y * y);
-    atomicAdd(&acc[3], 1.0);
+    int64_t yq, y2q;
+    reg_quantize(dp_target(a, t, r), q, yq, y2q);
+    atomicAdd(&racc[0], (unsigned long long)w);
+    atomicAdd(&racc[1], (unsigned long long)((int64_t)w * yq));
+    atomicAdd(&racc[2], (unsigned long long)((int64_t)w * y2q));
+    atomicAdd(&racc[3], 1ull);
   }
   __syncthreads();
   for (int c = threadIdx.x; c < 4; c += blockDim.x)
-    if (acc[c] != 0.0) atomicAdd(dp_ptr<double>(a.root) + (int64_t)t * 4 + c, acc[c]);
+    if (racc[c]) atomicAdd(dp_ptr<unsigned long long>(a.root) + (int64_t)t * 4 + c, racc[c]);
 }
 
 __global__ void k_dp_roots(DpArgs a) {
@@ -93,6 +96,20 @@ __global__ void k_dp_feats(DpArgs a) {
   const DpSlot& sl = dp_ptr<const DpSlot>(a.slots)[dp_ptr<const int32_t>(a.srch)[s]];
   const int p = sl.pos + k;
   dp_ptr<int32_t>(a.feats)[idx] = p < a.d ? feature_at(feat_perm(sl.key, (int)a.d), p, (int)a.d) : -1;
+}
+
+// a regression row's three integer histogram terms
+struct DpRegRow {
+  unsigned long long wr, wy, wyy;
+};
+__device__ __forceinline__ DpRegRow dp_reg_row(const DpArgs& a, uint32_t w, float fy) {
+  int64_t yq, y2q;
+  reg_quantize(fy, reg_scale((int)a.yq_e1, (int)a.yq_e2), yq, y2q);
+  DpRegRow t;
+  t.wr = (unsigned long long)w | (1ull << 32);
+  t.wy = (unsigned long long)((int64_t)w * yq);
+  t.wyy = (unsigned long long)((int64_t)w * y2q);
+  return t;
 }
 
 template <bool kReg>
@@ -117,11 +134,11 @@ __global__ void __launch_bounds__(kDpBlock) k_dp_hist_tiles(DpArgs a) {
   const int CH = (int)a.CH, C = (int)a.C, KR = (int)a.KR, G = (int)a.lds_feats;
   const int32_t* fs = dp_ptr<const int32_t>(a.feats) + (int64_t)s * KR;
   const uint8_t* Xb = dp_ptr<const uint8_t>(a.Xb);
-  uint32_t* gh = dp_ptr<uint32_t>(a.hist) + (int64_t)s * KR * CH * 256;
-  float* ldf = (float*)lds;
+  uint32_t* gh = dp_ptr<uint32_t>(a.hist) + (int64_t)s * dp_hist_words(a);
+  unsigned long long* ldr = (unsigned long long*)lds;   // regression: [ng][3][256] u64
   for (int g0 = 0; g0 < KR; g0 += G) {
     const int ng = min(G, KR - g0);
-    const int words = ng * CH * 256;
+    const int words = kReg ? ng * 3 * 256 * 2 : ng * CH * 256;
     for (int j = threadIdx.x; j < words; j += kDpBlock) lds[j] = 0u;
     __syncthreads();
     for (int64_t i = threadIdx.x; i < cnt; i += kDpBlock) {
@@ -130,17 +147,17 @@ __global__ void __launch_bounds__(kDpBlock) k_dp_hist_tiles(DpArgs a) {
       float fy = 0.f;
       dp_row<kReg>(a, seg0 + i, r, w, y, fy);
       const uint8_t* xr = Xb + (int64_t)r * a.ld;
+      DpRegRow q{};
+      if (kReg) q = dp_reg_row(a, w, fy);
       for (int k = 0; k < ng; ++k) {
         const int f = fs[g0 + k];
         if (f < 0) break;
         const int b = xr[f];
         if (kReg) {
-          const float fw = (float)w, wy = fw * fy;
-          float* h = ldf + (k * 4) * 256 + b;
-          atomicAdd(h, fw);
-          atomicAdd(h + 256, wy);
-          atomicAdd(h + 512, wy * fy);
-          atomicAdd(h + 768, 1.f);
+          unsigned long long* h = ldr + (k * 3) * 256 + b;
+          atomicAdd(h, q.wr);
+          atomicAdd(h + 256, q.wy);
+          atomicAdd(h + 512, q.wyy);
         } else {
           atomicAdd(&lds[(k * CH + y) * 256 + b], w);
           atomicAdd(&lds[(k * CH + C) * 256 + b], 1u);
@@ -148,12 +165,16 @@ __global__ void __launch_bounds__(kDpBlock) k_dp_hist_tiles(DpArgs a) {
       }
     }
     __syncthreads();
-    uint32_t* dst = gh + (int64_t)g0 * CH * 256;
-    for (int j = threadIdx.x; j < words; j += kDpBlock) {
-      const uint32_t v = lds[j];
-      if (!v) continue;
-      if (kReg) atomicAdd((float*)dst + j, __uint_as_float(v));
-      else atomicAdd(dst + j, v);
+    if (kReg) {
+      unsigned long long* dst = (unsigned long long*)gh + (int64_t)g0 * 3 * 256;
+      for (int j = threadIdx.x; j < ng * 3 * 256; j += kDpBlock)
+        if (ldr[j]) atomicAdd(dst + j, ldr[j]);
+    } else {
+      uint32_t* dst = gh + (int64_t)g0 * CH * 256;
+      for (int j = threadIdx.x; j < words; j += kDpBlock) {
+        const uint32_t v = lds[j];
+        if (v) atomicAdd(dst + j, v);
+      }
     }
     __syncthreads();
   }
@@ -172,24 +193,24 @@ __global__ void __launch_bounds__(kDpBlock) k_dp_hist_small(DpArgs a) {
   const int CH = (int)a.CH, C = (int)a.C, KR = (int)a.KR;
   const int32_t* fs = dp_ptr<const int32_t>(a.feats) + (int64_t)s * KR;
   const uint8_t* Xb = dp_ptr<const uint8_t>(a.Xb);
-  uint32_t* gh = dp_ptr<uint32_t>(a.hist) + (int64_t)s * KR * CH * 256;
+  uint32_t* gh = dp_ptr<uint32_t>(a.hist) + (int64_t)s * dp_hist_words(a);
   for (int64_t i = lane; i < cnt; i += 64) {
     int32_t r, y = 0;
     uint32_t w;
     float fy = 0.f;
     dp_row<kReg>(a, seg0 + i, r, w, y, fy);
     const uint8_t* xr = Xb + (int64_t)r * a.ld;
+    DpRegRow q{};
+    if (kReg) q = dp_reg_row(a, w, fy);
     for (int k = 0; k < KR; ++k) {
       const int f = fs[k];
       if (f < 0) break;
       const int b = xr[f];
       if (kReg) {
-        const float fw = (float)w, wy = fw * fy;
-        float* h = (float*)gh + (k * 4) * 256 + b;
-        atomicAdd(h, fw);
-        atomicAdd(h + 256, wy);
-        atomicAdd(h + 512, wy * fy);
-        atomicAdd(h + 768, 1.f);
+        unsigned long long* h = (unsigned long long*)gh + (k * 3) * 256 + b;
+        atomicAdd(h, q.wr);
+        atomicAdd(h + 256, q.wy);
+        atomicAdd(h + 512, q.wyy);
       } else {
         atomicAdd(&gh[(k * CH + y) * 256 + b], w);
         atomicAdd(&gh[(k * CH + C) * 256 + b], 1u);
@@ -204,7 +225,7 @@ __global__ void k_dp_split(DpArgs a) {
   if (s >= a.S) return;
   const int slot = dp_ptr<const int32_t>(a.srch)[s];
   DpSlot sl = dp_ptr<DpSlot>(a.slots)[slot];
-  const int64_t hw = a.KR * a.CH * 256;
+  const int64_t hw = dp_hist_words(a);
   dp_eval_slot(a, sl, dp_ptr<double>(a.best_left) + (int64_t)slot * a.CH, dp_ptr<const uint32_t>(a.hist) + s * hw,
                dp_ptr<const int32_t>(a.feats) + (int64_t)s * a.KR);
   dp_ptr<DpSlot>(a.slots)[slot] = sl;
@@ -378,7 +399,7 @@ int dml_dp_step(const DpArgs* a, int step, hipStream_t st) {
       if (a->S * a->KR > 0) k_dp_feats<<<blocks(a->S * a->KR, kDpBlock), kDpBlock, 0, st>>>(*a);
       break;
     case 4: {
-      const size_t lds = (size_t)a->lds_feats * a->CH * 256 * 4;
+      const size_t lds = (size_t)a->lds_feats * 256 * (a->is_reg ? 3 * 8 : a->CH * 4);
       if (a->n_tiles > 0) {
         if (a->lds_feats <= 0 || lds > 65536) return 2;
         if (a->is_reg) k_dp_hist_tiles<true><<<(unsigned)a->n_tiles, kDpBlock, lds, st>>>(*a);

@@ -37,6 +37,9 @@ struct Data {
   const double* cw;   // class-weight table [T][C] (rows of cw_mode 1 trees), or null
   const int8_t* mono; // monotonic_cst table [fits][d] (+1 / -1 / 0; binary classifiers'
                       // rows already constrain the class-0 fraction), or null
+  RegScale rq;        // regression fixed point (forest_common.h)
+  const int64_t* yq;  // per (target, row): rint(y 2^e1), rint(y^2 2^e2) -- computed once per build
+  const int64_t* y2q;
 };
 
 struct Job { int node, start, count, depth; uint64_t key; double lo, hi; };
@@ -75,11 +78,14 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
   TreeSpec s = s_in;   // min_weight_leaf is set once the tree's total weight is known
   const uint8_t* role = D.roles + (int64_t)s.split * D.n;
   const float* Y = D.ystride ? D.yreg + (int64_t)s.target * D.ystride : D.yreg;
+  const int64_t* YQ = D.is_reg ? D.yq + (D.ystride ? (int64_t)s.target * D.ystride : 0) : nullptr;
+  const int64_t* Y2Q = D.is_reg ? D.y2q + (D.ystride ? (int64_t)s.target * D.ystride : 0) : nullptr;
   std::vector<uint32_t> rows, tmp;
   std::vector<uint32_t> wts;  // indexed by row id through a parallel array
   rows.reserve(D.n);
   std::vector<uint32_t> wrow(D.n, 0);
   std::vector<double> root(D.VC, 0.0);
+  uint64_t rw = 0, ry = 0, ryy = 0;   // regression root sums (integer, see forest_common.h)
   for (int r = 0; r < D.n; ++r) {
     if (role[r] != 1) continue;
     const uint32_t w = boot_weight(s, (uint32_t)r);
@@ -87,12 +93,12 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     rows.push_back((uint32_t)r);
     wrow[r] = w;
     if (D.is_reg) {
-      const double y = (double)Y[r];
-      root[0] += (double)w; root[1] += (double)w * y; root[2] += (double)w * y * y;
+      rw += w; ry += (uint64_t)((int64_t)w * YQ[r]); ryy += (uint64_t)((int64_t)w * Y2Q[r]);
     } else {
       root[D.ycls[r]] += (double)w;
     }
   }
+  if (D.is_reg) { root[0] = (double)rw; root[1] = reg_s1(ry, D.rq); root[2] = reg_s2(ryy, D.rq); }
   tmp.resize(rows.size());
   // criterion="absolute_error" (sklearn MAE): node value = weighted median, impurity =
   // sum w |y - median| / W.  Node values are stored as {W, W*median, abs + W*median^2}
@@ -167,7 +173,7 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     stack.push_back({0, 0, (int)rows.size(), 0, root_key(s.seed), -INFINITY, INFINITY});
   const int CH = D.CH;
   std::vector<uint32_t> hu((size_t)CH * 256);
-  std::vector<float> hf((size_t)CH * 256);
+  std::vector<uint64_t> hr((size_t)3 * 256);   // regression: (w | rows << 32), sum w yq, sum w y2q
   std::vector<double> best_left(CH), cand_left(CH);
   while (!stack.empty()) {
     Job jb = stack.back();
@@ -266,21 +272,22 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
           }
         }
       } else {
-        std::fill(hf.begin(), hf.end(), 0.f);
+        std::fill(hr.begin(), hr.end(), 0ull);
         for (int i = 0; i < jb.count; ++i) {
           const uint32_t r = nr[i];
           const int b = D.Xb[(int64_t)r * D.ld + f];
-          const float fw = (float)wrow[r], y = Y[r], wy = fw * y;
-          hf[b] += fw; hf[256 + b] += wy; hf[512 + b] += wy * y; hf[768 + b] += 1.f;
+          const int64_t w = wrow[r];
+          hr[b] += (uint64_t)w | (1ull << 32); hr[256 + b] += (uint64_t)(w * YQ[r]); hr[512 + b] += (uint64_t)(w * Y2Q[r]);
         }
-        for (int ch = 0; ch < CH; ++ch)
-          for (int b = 1; b < 256; ++b) hf[ch * 256 + b] += hf[ch * 256 + b - 1];
-        const float tot_rows = hf[768 + 255];
+        for (int ch = 0; ch < 3; ++ch)
+          for (int b = 1; b < 256; ++b) hr[ch * 256 + b] += hr[ch * 256 + b - 1];
+        const uint32_t tot_rows = (uint32_t)(hr[255] >> 32);
         for (int b = 0; b < 255; ++b) {
-          const float rl = hf[768 + b], rr = tot_rows - rl;
-          nc |= (rl > 0.f && rr > 0.f);
-          if (rl < (float)s.min_samples_leaf || rr < (float)s.min_samples_leaf) continue;
-          const double l0 = hf[b], t0 = hf[255], l1 = hf[256 + b], t1 = hf[256 + 255];
+          const uint32_t rl = (uint32_t)(hr[b] >> 32), rr = tot_rows - rl;
+          nc |= (rl > 0 && rr > 0);
+          if (rl < (uint32_t)s.min_samples_leaf || rr < (uint32_t)s.min_samples_leaf) continue;
+          const double l0 = reg_w(hr[b]), t0 = reg_w(hr[255]), l1 = reg_s1(hr[256 + b], D.rq),
+                       t1 = reg_s1(hr[256 + 255], D.rq);
           if (side_too_light(s, l0, t0 - l0)) continue;
           const double vl = side_value(l0, l1), vr = side_value(t0 - l0, t1 - l1);
           if (mono && mono[f] && !mono_ok(mono[f], jb.lo, jb.hi, vl, vr)) continue;
@@ -294,7 +301,9 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
           ++nonconst;
           if (b_best >= 0 && g_best > best_gain) {
             best_gain = g_best; best_feat = f; best_bin = b_best;
-            for (int ch = 0; ch < CH; ++ch) best_left[ch] = (double)hf[ch * 256 + b_best];
+            const uint64_t* h = hr.data() + b_best;
+            best_left[0] = reg_w(h[0]); best_left[1] = reg_s1(h[256], D.rq); best_left[2] = reg_s2(h[512], D.rq);
+            best_left[3] = reg_rows(h[0]);
           }
         }
       }
@@ -391,8 +400,22 @@ int dml_cpu_sizeof_treespec() { return (int)sizeof(TreeSpec); }
 void* dml_cpu_forest_build_mono(const uint8_t* Xb, int64_t ld, int64_t n, int64_t d, const int32_t* ycls,
                                 const float* yreg, int64_t n_classes, int64_t is_reg, const uint8_t* roles,
                                 const TreeSpec* specs, int64_t T, int64_t ystride, const double* cw,
-                                const int8_t* mono) {
+                                const int8_t* mono, int64_t e1, int64_t e2) {
   Data D;
+  // regression: every (target, row) quantised once (forest_common.h fixed point)
+  std::vector<int64_t> yq, y2q;
+  D.rq = reg_scale((int)e1, (int)e2);
+  D.yq = D.y2q = nullptr;
+  if (is_reg) {
+    int64_t targets = 1;
+    if (ystride > 0)
+      for (int64_t t = 0; t < T; ++t) targets = std::max<int64_t>(targets, (int64_t)specs[t].target + 1);
+    const int64_t len = ystride > 0 ? (targets - 1) * ystride + n : n;
+    yq.resize(len); y2q.resize(len);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < len; ++i) reg_quantize(yreg[i], D.rq, yq[i], y2q[i]);
+    D.yq = yq.data(); D.y2q = y2q.data();
+  }
   D.mono = mono;
   D.ystride = ystride;
   D.cw = cw;
@@ -413,8 +436,24 @@ void* dml_cpu_forest_build_mono(const uint8_t* Xb, int64_t ld, int64_t n, int64_
 void* dml_cpu_forest_build(const uint8_t* Xb, int64_t ld, int64_t n, int64_t d, const int32_t* ycls,
                            const float* yreg, int64_t n_classes, int64_t is_reg, const uint8_t* roles,
                            const TreeSpec* specs, int64_t T, int64_t ystride, const double* cw) {
+  int e1 = 0, e2 = 0;
+  if (is_reg) {   // exponents from the data (entry point of the host self-test)
+    double m = 0.0;
+    int64_t targets = 1;
+    if (ystride > 0)
+      for (int64_t t = 0; t < T; ++t) targets = std::max<int64_t>(targets, (int64_t)specs[t].target + 1);
+    const int64_t len = ystride > 0 ? (targets - 1) * ystride + n : n;
+    for (int64_t i = 0; i < len; ++i) m = std::max(m, fabs((double)yreg[i]));
+    reg_exponents(m, n, e1, e2);
+  }
   return dml_cpu_forest_build_mono(Xb, ld, n, d, ycls, yreg, n_classes, is_reg, roles, specs, T, ystride, cw,
-                                   nullptr);
+                                   nullptr, e1, e2);
+}
+
+void dml_reg_exponents(double max_abs_y, int64_t n, int32_t* out) {
+  int e1, e2;
+  reg_exponents(max_abs_y, n, e1, e2);
+  out[0] = e1; out[1] = e2;
 }
 
 int64_t dml_cpu_forest_num_nodes(void* h) {

@@ -39,14 +39,18 @@ static void dp_root_stats(const DpArgs& a) {
         cnt[CH - 1] += 1;
       }
       for (int c = 0; c < CH; ++c) out[c] += (double)cnt[c];
-    } else {
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    } else {   // exact integer sums {w, w yq, w y2q, rows} (forest_common.h)
+      const RegScale q = reg_scale((int)a.yq_e1, (int)a.yq_e2);
+      uint64_t acc[4] = {0ull, 0ull, 0ull, 0ull};
       for (int64_t r = 0; r < a.n; ++r) {
         if (!w8[r]) continue;
-        const double w = (double)w8[r], y = (double)dp_target(a, (int)t, r);
-        acc[0] += w; acc[1] += w * y; acc[2] += w * y * y; acc[3] += 1.0;
+        int64_t yq, y2q;
+        reg_quantize(dp_target(a, (int)t, r), q, yq, y2q);
+        const int64_t w = w8[r];
+        acc[0] += (uint64_t)w; acc[1] += (uint64_t)(w * yq); acc[2] += (uint64_t)(w * y2q); acc[3] += 1ull;
       }
-      for (int c = 0; c < 4; ++c) out[c] += acc[c];
+      uint64_t* outi = dp_ptr<uint64_t>(a.root) + t * CH;
+      for (int c = 0; c < 4; ++c) outi[c] += acc[c];
     }
   }
 }
@@ -60,8 +64,9 @@ static void dp_hist(const DpArgs& a) {
     const int slot = dp_ptr<const int32_t>(a.srch)[s];
     const int64_t seg0 = dp_ptr<const int64_t>(a.seg_start)[slot], cnt = dp_ptr<const int64_t>(a.seg_cnt)[slot];
     const int32_t* fs = dp_ptr<const int32_t>(a.feats) + s * KR;
-    uint32_t* hu = dp_ptr<uint32_t>(a.hist) + s * KR * CH * 256;
-    float* hf = (float*)hu;
+    uint32_t* hu = dp_ptr<uint32_t>(a.hist) + s * dp_hist_words(a);
+    uint64_t* hr = (uint64_t*)hu;
+    const RegScale q = reg_scale((int)a.yq_e1, (int)a.yq_e2);
     for (int64_t i = 0; i < cnt; ++i) {
       const int64_t p = seg0 + i;
       const int32_t r = dp_ptr<const int32_t>(a.act_row)[p];
@@ -76,10 +81,12 @@ static void dp_hist(const DpArgs& a) {
           hu[(k * CH + C) * 256 + b] += 1u;
         }
       } else {
-        const float fw = (float)w, y = dp_target(a, t, r), wy = fw * y;
+        int64_t yq, y2q;
+        reg_quantize(dp_target(a, t, r), q, yq, y2q);
+        const uint64_t wr = (uint64_t)w | (1ull << 32), wy = (uint64_t)((int64_t)w * yq), wyy = (uint64_t)((int64_t)w * y2q);
         for (int k = 0; k < KR && fs[k] >= 0; ++k) {
-          float* h = hf + (k * 4) * 256 + xr[fs[k]];
-          h[0] += fw; h[256] += wy; h[512] += wy * y; h[768] += 1.f;
+          uint64_t* h = hr + (k * 3) * 256 + xr[fs[k]];
+          h[0] += wr; h[256] += wy; h[512] += wyy;
         }
       }
     }
@@ -149,7 +156,7 @@ int dml_cpu_dp_step(const DpArgs* ap, int step) {
         const int slot = dp_ptr<const int32_t>(a.srch)[s];
         DpSlot& sl = dp_ptr<DpSlot>(a.slots)[slot];
         dp_eval_slot(a, sl, dp_ptr<double>(a.best_left) + (int64_t)slot * a.CH,
-                     dp_ptr<const uint32_t>(a.hist) + s * a.KR * a.CH * 256, dp_ptr<const int32_t>(a.feats) + s * a.KR);
+                     dp_ptr<const uint32_t>(a.hist) + s * dp_hist_words(a), dp_ptr<const int32_t>(a.feats) + s * a.KR);
       }
       break;
     case 6:

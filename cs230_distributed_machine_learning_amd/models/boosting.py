@@ -236,7 +236,9 @@ class GradientBoostingFamily(Family):
             return out
         y = data.y_reg[train].double()
         if loss == LOSS_SQ:
-            out[0] = y.mean()
+            # correctly rounded mean (math.fsum) -- the same double on every device, so a
+            # squared-error ensemble is the same on the GPU as on the host builder
+            out[0] = math.fsum(y.cpu().numpy().tolist()) / max(1, y.numel())
         elif loss in (LOSS_ABS, LOSS_HUBER):
             out[0] = _percentile_linear(y, 0.5)
         else:

@@ -38,7 +38,7 @@ import numpy as np
 import torch
 
 from ..utils import native, trace
-from .forest_ops import ForestBuild
+from .forest_ops import reg_exponents_of, ForestBuild
 
 SLOT_BYTES = 64
 # int32 column of each DpSlot field (forest_dp.h): key 0-1, best_gain 2-3, count 4-5
@@ -61,7 +61,7 @@ class DpArgs(ctypes.Structure):
         "Xb ld n d r0 ycls yreg C CH VC is_reg roles specs T cw tree_W root wts "
         "act_row act_tree act_node A new_node slots best_left S_open seg_start seg_cnt "
         "srch S KR feats hist tile_s tile_off n_tiles tile_rows small_s n_small lds_feats "
-        "nodes vals P child_base next next_open slot_of lvl_lo lvl_n hi binvals exact P_total ystride").split()]
+        "nodes vals P child_base next next_open slot_of lvl_lo lvl_n hi binvals exact P_total ystride yq_e1 yq_e2").split()]
 
 
 Reducer = Callable[[torch.Tensor, str], torch.Tensor]   # (tensor, "sum" | "min" | "max") -> in place
@@ -125,11 +125,19 @@ def _build_chunk(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[
     mf = torch.from_numpy(np.ascontiguousarray(specs["max_features"], dtype=np.int32)).to(dev)
     stats = {"levels": 0, "rounds": 0, "allreduce_bytes": 0, "hist_s": 0.0, "reduce_s": 0.0}
 
+    if is_reg:
+        # the fixed-point exponents of the ONE-GPU build of the whole table: max|y| and
+        # the row count over every rank (forest_common.h reg_exponents)
+        mt = torch.tensor([float(yreg.abs().max()) if yreg.numel() else 0.0, float(n)], dtype=torch.float64,
+                          device=dev)
+        m_all, n_all = reduce(mt[:1].clone(), "max"), reduce(mt[1:].clone(), "sum")
+        a.yq_e1, a.yq_e2 = reg_exponents_of(float(m_all[0]), int(n_all[0]))
     # ---- roots: local bootstrap statistics, summed over the ranks ----------------------
     wts = torch.empty((T, n), dtype=torch.uint8, device=dev)
     a.wts = _p(wts)
     L.step(a, 0)
-    root = torch.zeros((T, CH), dtype=torch.float64, device=dev)
+    # regression roots are exact integer sums {w, w yq, w y2q, rows}
+    root = torch.zeros((T, CH), dtype=torch.int64 if is_reg else torch.float64, device=dev)
     a.root = _p(root)
     L.step(a, 1)
     reduce(root, "sum")
@@ -150,10 +158,13 @@ def _build_chunk(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[
     act_node = act_tree.clone()           # tree t's root is node t; pairs already sorted by node
     del pair
     P, lvl_lo, lvl_n = T, 0, T
-    hist_dtype = torch.float32 if is_reg else torch.int32
+    # regression: three integer planes (w | rows << 32, w yq, w y2q), u64 as int64
+    hist_dtype = torch.int64 if is_reg else torch.int32
+    HP = 3 if is_reg else CH
+    pos_bytes = HP * 256 * (8 if is_reg else 4)      # histogram bytes of one visiting position
     world = int(getattr(comm, "world", 1)) if comm is not None else 1
     scatter = world > 1
-    lds_feats = LDS_BYTES // (CH * 1024)
+    lds_feats = LDS_BYTES // pos_bytes
     timing = os.environ.get("DML_DP_TIMING") == "1"
 
     while slots.shape[0]:
@@ -176,7 +187,7 @@ def _build_chunk(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[
             need = int((mf[sv[sl, F_TREE].long()] - sv[sl, F_NONCONST]).max())
             left_pos = int((d - sv[sl, F_POS]).max())
             KR = max(1, min(left_pos, need + max(1, need // 4)))
-            chunk = max(1, hist_budget // (KR * CH * 1024))
+            chunk = max(1, hist_budget // (KR * pos_bytes))
             # small nodes of a classification forest exchange sparse local histograms
             # (non-zero (index, count) pairs) instead of dense 256-bin tensors
             groups = [(srch, False)]
@@ -191,7 +202,7 @@ def _build_chunk(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[
                     feats = torch.empty((Sc, KR), dtype=torch.int32, device=dev)
                     q = -(-Sc // world)                          # nodes owned per rank (reduce-scatter)
                     rs = scatter and not sparse
-                    hist = torch.zeros((q * world if rs else Sc, KR, CH, 256), dtype=hist_dtype, device=dev)
+                    hist = torch.zeros((q * world if rs else Sc, KR, HP, 256), dtype=hist_dtype, device=dev)
                     a.srch, a.S, a.KR, a.feats, a.hist = _p(sub), Sc, KR, _p(feats), _p(hist)
                     L.step(a, 3)
                     th = time.perf_counter()
@@ -243,7 +254,7 @@ def _build_chunk(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[
                         with trace.range("forest_dp_reduce_scatter"):
                             own = comm.reduce_scatter_rows(hist)
                         stats["reduce_s"] += time.perf_counter() - tr
-                        stats["allreduce_bytes"] += hist.numel() * 4 // 2     # ring: half of an all-reduce
+                        stats["allreduce_bytes"] += hist.numel() * hist.element_size() // 2   # ring: half an all-reduce
                         lo = min(Sc, comm.rank * q)
                         hi = min(Sc, lo + q)
                         own_srch = sub[lo:hi].contiguous()
@@ -263,7 +274,7 @@ def _build_chunk(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[
                         with trace.range("forest_dp_allreduce"):
                             reduce(hist, "sum")
                         stats["reduce_s"] += time.perf_counter() - tr
-                        stats["allreduce_bytes"] += hist.numel() * 4
+                        stats["allreduce_bytes"] += hist.numel() * hist.element_size()
                         L.step(a, 5)
                     stats["rounds"] += 1
                     del feats, hist, tile_s, tile_off, small

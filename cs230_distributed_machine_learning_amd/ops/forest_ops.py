@@ -212,6 +212,32 @@ def _carve(buf: torch.Tensor, off: int, shape, dtype) -> torch.Tensor:
     return buf[off:off + n].view(dtype).view(*shape)
 
 
+def reg_exponents(yreg, n: int) -> tuple[int, int]:
+    """Fixed-point exponents (e1, e2) of a regression build: forest_common.h
+    ``reg_exponents`` on max|y| over the whole target array, so the HIP and the C++
+    builders quantise identically (checked against the C rule in the tests)."""
+    if yreg is None or n <= 0:
+        return 0, 0
+    if torch.is_tensor(yreg):
+        m = float(yreg.abs().max()) if yreg.numel() else 0.0
+    else:
+        a = np.asarray(yreg, dtype=np.float32)
+        m = float(np.abs(a).max()) if a.size else 0.0
+    return reg_exponents_of(m, n)
+
+
+def reg_exponents_of(max_abs_y: float, n: int) -> tuple[int, int]:
+    """The exponent rule itself (forest_common.h ``reg_exponents``): every integer sum
+    over a tree's rows stays below 2^61 in magnitude (weights <= 15, n rows)."""
+    if not math.isfinite(max_abs_y):
+        raise ValueError("regression target contains NaN or infinity")
+    if max_abs_y <= 0.0 or n <= 0:
+        return 0, 0
+    kw, k = math.frexp(15.0 * n)[1], math.frexp(max_abs_y)[1]
+    clamp = lambda e: max(-1000, min(1000, e))
+    return clamp(61 - kw - k), clamp(61 - kw - 2 * k)
+
+
 def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,
               specs: np.ndarray, n_classes: int, is_reg: bool, tiers: ForestTiers | None = None,
               ystride: int = 0, reuse_pool: bool = False, XbT: Optional[torch.Tensor] = None,
@@ -235,6 +261,7 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     a.ycls = native.ptr(ycls) if ycls is not None else 0
     a.yreg = native.ptr(yreg) if yreg is not None else 0
     a.n_classes, a.is_reg = (n_classes if not is_reg else 1), int(is_reg)
+    a.yq_e1, a.yq_e2 = reg_exponents(yreg, n) if is_reg else (0, 0)
     a.roles, a.n_splits = native.ptr(roles), roles.shape[0]
     a.specs, a.T = native.ptr(specs_dev), T
     a.ystride = int(ystride)
@@ -362,9 +389,10 @@ def build_cpu(Xb: np.ndarray, ycls: Optional[np.ndarray], yreg: Optional[np.ndar
     t0 = time.perf_counter()
     cw = None if (cw is None or is_reg) else np.ascontiguousarray(cw, dtype=np.float64).reshape(T, n_classes)
     mono = None if mono is None else np.ascontiguousarray(mono, dtype=np.int8)
+    e1, e2 = reg_exponents(yreg, n) if is_reg else (0, 0)
     h = lib.dml_cpu_forest_build_mono(native.ptr(Xb), d, n, d, native.ptr(ycls), native.ptr(yreg),
                                       (1 if is_reg else n_classes), int(is_reg), native.ptr(roles), native.ptr(specs),
-                                      T, int(ystride), native.ptr(cw), native.ptr(mono))
+                                      T, int(ystride), native.ptr(cw), native.ptr(mono), e1, e2)
     try:
         P = lib.dml_cpu_forest_num_nodes(h)
         nodes = np.empty((P, 2), dtype=np.int32)

@@ -71,6 +71,7 @@ ForestArgs = _i64_struct(
         "n_nodes_out", "status_out", "levels_out", "large_rounds_out",
         "tier0_nodes", "tier1_nodes", "tier2_nodes", "tier3_nodes",
         "ystride", "XbT", "cw",
+        "yq_e1", "yq_e2",
     ],
 )
 
@@ -112,7 +113,8 @@ def cpu_lib() -> ctypes.CDLL:
                                                  c_i64, c_vp]
             lib.dml_cpu_forest_build_mono.restype = c_vp
             lib.dml_cpu_forest_build_mono.argtypes = [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
-                                                      c_i64, c_i64, c_vp, c_vp]
+                                                      c_i64, c_i64, c_vp, c_vp, c_i64, c_i64]
+            lib.dml_reg_exponents.argtypes = [ctypes.c_double, c_i64, c_vp]
             lib.dml_cpu_forest_apply.argtypes = [c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp]
             lib.dml_cpu_forest_refine.argtypes = [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp]
             lib.dml_cpu_forest_prune.argtypes = [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp]

@@ -3,7 +3,7 @@
 # Each GPU step has its own time limit and steps are chained with &&, so the first
 # failure (fault, abort, timeout) ends the call. Logs land in gpurun_out/.
 # kinds:
-#   tests   [pytest args]             GPU test tier                     -> exp_tests.log
+#   tests   [test paths]              GPU test tier (default: all of tests/) -> exp_tests.log
 #   smoke                             __graft_entry__.smoke()           -> exp_smoke.log
 #   check                             tests + smoke + short bench + rocprof kernel stats
 #   bench   [bench.py args]           headline bench, JSON line         -> exp_bench.log
@@ -26,7 +26,7 @@ PYT="python -u -m pytest -x -q --timeout 240 --timeout-method thread"
 GB="scripts/gbench_forest.py"
 kind=$1; shift
 case "$kind" in
-  tests)   timeout -k 10 900 $PYT tests -m gpu "$@" > gpurun_out/exp_tests.log 2>&1; rc=$?; tail -3 gpurun_out/exp_tests.log; exit $rc ;;
+  tests)   timeout -k 10 900 $PYT -m gpu ${@:-tests} > gpurun_out/exp_tests.log 2>&1; rc=$?; tail -3 gpurun_out/exp_tests.log; exit $rc ;;
   smoke)   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/exp_smoke.log 2>&1 && tail -1 gpurun_out/exp_smoke.log ;;
   check)   timeout -k 10 900 $PYT tests -m gpu > gpurun_out/exp_tests.log 2>&1 && tail -1 gpurun_out/exp_tests.log && \
            timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/exp_smoke.log 2>&1 && tail -1 gpurun_out/exp_smoke.log && \

@@ -109,7 +109,9 @@ def test_dp_builder_regression_one_rank():
     rows = np.arange(n, dtype=np.int32)
     pr = forest_ops.predict(ref, Xb.numpy(), np.array([0, 4]), np.array([0, n]), rows)
     pd = forest_ops.predict(dp.to_numpy(), Xb.numpy(), np.array([0, 4]), np.array([0, n]), rows)
-    assert np.allclose(pr, pd, atol=1e-4)
+    # exact integer regression sums (forest_common.h): the same trees, node for node
+    assert canon(ref, 4) == canon(dp, 4)
+    assert np.array_equal(pr, pd)
 
 
 def test_dp_refine_matches_host_refine():
@@ -244,6 +246,10 @@ def _w3_data():
     return X, y
 
 
+def _w3_yreg(X):
+    return (X[:, 0] * 3 + X[:, 1] * X[:, 3] + 0.25 * X[:, 2]).astype(np.float32)
+
+
 def _w3_rank(rank, world, port, outq):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), OMP_NUM_THREADS="2")
@@ -260,7 +266,14 @@ def _w3_rank(rank, world, port, outq):
         specs["split"] = 0
         fb = forest_dp.build_dp(sh.binned(), sh.y_cls, None, sh.roles, specs, 3, False, sh.r0, reduce=sh.all_reduce,
                                 comm=sh)
-        outq.put(("ok", rank, canon(fb, 5)))
+        # regression: integer histogram / root sums summed over the ranks (exact)
+        shr = RowShard(X[a:b], _w3_yreg(X), a, False, inf.device)
+        shr.set_splits(np.ones((1, len(X)), np.uint8), ["full"])
+        rspecs = _specs(4, 9, crit=2, mf=4, msl=2)
+        rspecs["split"] = 0
+        fr = forest_dp.build_dp(shr.binned(), None, shr.y_reg, shr.roles, rspecs, 1, True, shr.r0,
+                                reduce=shr.all_reduce, comm=shr)
+        outq.put(("ok", rank, canon(fb, 5), canon(fr, 4)))
         dist.destroy()
     except Exception:  # pragma: no cover
         import traceback
@@ -281,6 +294,10 @@ def test_dp_builder_three_ranks_gloo():
     specs["split"] = 0
     ref = canon(forest_ops.build_cpu(dd.binned().numpy(), dd.y_enc, None, np.ones((1, len(X)), np.uint8), specs, 3,
                                      False), 5)
+    rspecs = _specs(4, 9, crit=2, mf=4, msl=2)
+    rspecs["split"] = 0
+    rref = canon(forest_ops.build_cpu(dd.binned().numpy(), None, _w3_yreg(X), np.ones((1, len(X)), np.uint8), rspecs,
+                                      1, True), 4)
     world, port = 3, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -297,6 +314,7 @@ def test_dp_builder_three_ranks_gloo():
     for o in outs:
         assert o[0] == "ok", o[2]
         assert o[2] == ref
+        assert o[3] == rref   # row-sharded regression trees == the one-process trees
 
 
 def test_dp_builder_tree_chunks_concatenate_to_one_pool():
@@ -319,8 +337,8 @@ def test_dp_builder_tree_chunks_concatenate_to_one_pool():
 
 @pytest.mark.gpu
 def test_dp_builder_gpu_regression_and_poisson():
-    """Regression (fp32 LDS tiles + atomics, sequential-bin split kernel) and Poisson on the
-    GPU vs the C++ builder: float sums in another order, so predictions agree closely."""
+    """Regression (integer LDS tiles + 64-bit atomics, sequential-bin split kernel) and
+    Poisson on the GPU vs the C++ builder: exact integer sums, identical trees."""
     Xb, _, yr, roles = _data(n=50000, d=20, seed=3)
     X, E = _data.last
     dev = torch.device("cuda:0")
@@ -334,5 +352,5 @@ def test_dp_builder_gpu_regression_and_poisson():
                                 True, 0)
         pr = forest_ops.predict(ref, Xb.numpy(), np.array([0, 4]), np.array([0, n]), rows)
         pd = forest_ops.predict(dp, Xg, np.array([0, 4]), np.array([0, n]), torch.from_numpy(rows).to(dev)).cpu().numpy()
-        r2 = 1 - np.sum((pd - pr) ** 2) / np.sum((pr - pr.mean()) ** 2)
-        assert r2 > 0.99, (crit, r2)
+        assert canon(ref, 4) == canon(dp, 4), crit
+        assert np.array_equal(pd, pr), crit

@@ -91,7 +91,11 @@ def test_gbrt_gpu_close_to_cpu(model, clf, loss):
         res = run_candidates(dd, JobSpec(model, grid, cv=3), range(len(grid)))
         assert all(r.ok for r in res), [r.error for r in res]
         out[dev] = np.array([r.result["mean_cv_score"] for r in res])
-    np.testing.assert_allclose(out["cuda:0"], out["cpu"], atol=5e-3)
+    if loss == "squared_error":
+        # exact integer regression histograms + a correctly rounded init: identical ensembles
+        np.testing.assert_allclose(out["cuda:0"], out["cpu"], rtol=0, atol=1e-9)
+    else:   # sigmoid / percentile / float64 index_add leaf updates differ in the last bits by device
+        np.testing.assert_allclose(out["cuda:0"], out["cpu"], atol=5e-3)
 
 
 def test_lr_link_grad_kernel_matches_torch():
