@@ -166,11 +166,22 @@ def main() -> int:
     setup_s = time.perf_counter() - t_setup
 
     score_buf = torch.zeros((N * c, args.cv), dtype=torch.float32, device=dev)
+    busy: dict = {}          # timed step -> this rank's own fit seconds (before the collective)
+    lpt_imb: dict = {}       # timed step -> LPT-predicted max / mean rank cost of the step's pool
 
     def step(s: int):
         mine = rank_step_cands(s)
+        if N > 1:
+            pool = step_pool(s)
+            owner = lpt_assign([float(costs[i]) for i in pool], N)
+            per = np.zeros(N)
+            for cid, o in zip(pool, owner):
+                per[int(o)] += costs[cid]
+            lpt_imb[s] = float(per.max() / max(per.mean(), 1e-12))
+        t_s = time.perf_counter()
         with trace.range("step"):
             res = run_candidates(dd, spec, mine)
+        busy[s] = time.perf_counter() - t_s   # results are on the host: the fits are done
         bad = [x.error for x in res if not x.ok]
         if bad:
             raise RuntimeError(f"rank {r}: failed fits: {bad[:2]}")
@@ -201,6 +212,11 @@ def main() -> int:
 
     fits_per_step = N * c * args.cv
     value = args.steps * fits_per_step / elapsed
+    # per-rank step times (N > 1 diagnosis: a poor curve says whether the placement or the
+    # ranks' speed is to blame)
+    timed = list(range(args.warmup, args.warmup + args.steps))
+    bt = torch.tensor([busy.get(s, 0.0) for s in timed], dtype=torch.float64, device=dev)
+    all_bt = dist.all_gather_rows(bt.view(1, -1)).cpu().numpy()          # [N, steps]
     if r == 0:
         mean_cv = float(score_buf.mean().item())
         out = {
@@ -227,6 +243,11 @@ def main() -> int:
             },
             "setup_s": round(setup_s, 2),
             "mean_cv_accuracy_last_step": round(mean_cv, 4),
+            "per_rank_fit_ms_per_step": {"min": round(1000 * float(all_bt.mean(1).min()), 1),
+                                         "mean": round(1000 * float(all_bt.mean(1).mean()), 1),
+                                         "max": round(1000 * float(all_bt.mean(1).max()), 1)},
+            "measured_step_imbalance": round(float(np.mean(all_bt.max(0) / np.maximum(all_bt.mean(0), 1e-12))), 3),
+            "lpt_predicted_imbalance": round(float(np.mean([lpt_imb[s] for s in timed])), 3) if N > 1 else 1.0,
             "device": str(torch.cuda.get_device_name(dev)) if dev.type == "cuda" else "cpu",
         }
         line = json.dumps(out)

@@ -157,6 +157,11 @@ class JobTable:
                         if job:
                             self._finish_subtask(job, ev["subtask_id"], ev["status"], ev.get("result"),
                                                  ev.get("error"), ev.get("metrics"), log=False)
+                    elif kind == "result_update":
+                        job = self.jobs.get(ev["job_id"])
+                        idx = _subtask_index(ev["subtask_id"])
+                        if job and idx is not None and idx < job.total and job.subtasks[idx].result is not None:
+                            job.subtasks[idx].result = dict(job.subtasks[idx].result, **ev.get("fields", {}))
                     elif kind == "model":
                         job = self.jobs.get(ev["job_id"])
                         idx = _subtask_index(ev["subtask_id"])
@@ -250,6 +255,22 @@ class JobTable:
                        "result": result, "error": error, "metrics": metrics})
         if job.n_done + job.n_failed == job.total:
             self._complete(job)
+
+    def update_result(self, job_id: str, subtask_id: str, fields: Dict[str, Any]) -> None:
+        """Overwrite fields of a completed subtask's result (the cluster runner's scores
+        epoch replaces the progress copies with the all-gathered ones) before the job
+        completes; journaled so a resumed job reads the same record."""
+        with self._lock:
+            job = self.jobs.get(job_id)
+            if job is None:
+                return
+            idx = _subtask_index(subtask_id)
+            if idx is None or idx >= job.total:
+                return
+            st = job.subtasks[idx]
+            if st.result is not None:
+                st.result = dict(st.result, **fields)
+                self._log({"event": "result_update", "job_id": job_id, "subtask_id": subtask_id, "fields": fields})
 
     def attach_model(self, job_id: str, subtask_id: str, model_path: str) -> None:
         """Record the refit model's path on a completed subtask (before the job completes)."""

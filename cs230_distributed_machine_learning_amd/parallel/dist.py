@@ -163,6 +163,20 @@ def service_store():
     return PrefixStore("dml", raw)
 
 
+def service_client(timeout_s: float = 300.0):
+    """A NEW connection to the control-plane store (same ``dml`` view as service_store):
+    a thread that blocks in ``TCPStore.wait`` on its own client never holds up the
+    threads sharing the main one (parallel/runner.py)."""
+    import datetime
+
+    from torch.distributed import PrefixStore, TCPStore
+
+    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = int(os.environ.get("MASTER_PORT", "29500"))
+    raw = TCPStore(host, port, is_master=False, timeout=datetime.timedelta(seconds=timeout_s))
+    return PrefixStore("dml", raw)
+
+
 def destroy() -> None:
     global _INFO
     if dist.is_initialized():

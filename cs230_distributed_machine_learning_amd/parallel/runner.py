@@ -20,9 +20,16 @@ dataset            once per dataset per worker.  While the whole process group i
                    Once a rank has died (the default group can no longer run collectives) or
                    for a worker that joined after launch, rank 0 stages the table in a host
                    file and each worker copies it to its own GPU over its own PCIe link
-results            per-slice result JSON through the store; rank 0 publishes progress as
-                   slices land (status / SSE stream) and holds each job's last slice until
-                   the best candidate is refit, so "completed" always carries the model
+results            every rank keeps the score rows of the candidates it ran; when a job's last
+                   slice lands, a *scores epoch* all-gathers them over RCCL
+                   (all_gather_into_tensor of a [candidates, width] float64 tensor) and rank
+                   0 builds the job's final records (J5) from that tensor -- the reference's
+                   Kafka ``result`` channel (worker.py:247-254 -> task_handler.py:18-50).  The
+                   per-slice store message is the control / progress copy (status and SSE
+                   stream as slices land; the fallback once the group is broken or for a
+                   joined worker, whose rows no collective can reach).  Rank 0 holds each
+                   job's last slice until the best candidate is refit, so "completed"
+                   always carries the model
 liveness           every worker refreshes ``hb/<worker>``; a worker silent for
                    ``dead_after_s`` is declared dead, its in-flight slice goes back to the
                    front of its job's queue and the survivors finish the job.  A slice that
@@ -71,37 +78,58 @@ MAX_WORKERS = 4096
 
 class LockedStore:
     """Thread-safe view of a TCPStore client (rank 0's dispatcher, its worker thread and
-    the heartbeat share one client); ``wait`` polls ``check`` so a waiter never holds
-    the lock."""
+    the heartbeat share one client).  ``wait`` blocks server-side (``TCPStore.wait``) on a
+    PRIVATE client when one is given (``waiter``: no lock held, no polling), else polls
+    ``check``.  ``ops`` counts the store operations this view issued (control-plane load,
+    profiles/r3_cluster_8rank_gloo.log)."""
 
-    def __init__(self, store):
+    def __init__(self, store, waiter=None):
         self._s = store
         self._lock = threading.Lock()
+        self._waiter = waiter
+        self.ops = 0
 
     def add(self, k, v):
         with self._lock:
+            self.ops += 1
             return self._s.add(k, v)
 
     def set(self, k, v):
         with self._lock:
+            self.ops += 1
             return self._s.set(k, v)
 
     def get(self, k):
         with self._lock:
+            self.ops += 1
             return self._s.get(k)
 
     def check(self, ks):
         with self._lock:
+            self.ops += 1
             return self._s.check(ks)
 
     def delete_key(self, k):
         with self._lock:
+            self.ops += 1
             try:
                 return self._s.delete_key(k)
             except Exception:
                 return False
 
     def wait(self, ks, timeout=None, poll_s: float = 0.002):
+        if self._waiter is not None:
+            import datetime
+
+            t = 24 * 3600.0 if timeout is None else max(0.001, float(timeout))
+            self.ops += 1
+            try:
+                self._waiter.wait(ks, datetime.timedelta(seconds=t))
+            except Exception as e:   # DistStoreError: timeout, or the store is gone
+                if "timeout" in str(e).lower() or "timed out" in str(e).lower():
+                    raise TimeoutError(ks) from e
+                raise
+            return
         t0 = time.time()
         while True:
             if self.check(ks):
@@ -109,6 +137,22 @@ class LockedStore:
             if timeout is not None and time.time() - t0 > timeout:
                 raise TimeoutError(ks)
             time.sleep(poll_s)
+
+
+SCORE_HEAD = 4   # score row: [ok, mean_cv_score, std_cv_score, n_cv, cv_0 .. cv_{n_cv-1}]
+
+
+def score_row(ok: bool, result: Dict[str, Any], width: int) -> np.ndarray:
+    """A candidate's numeric result as one float64 row (NaN padded) for the scores epoch."""
+    row = np.full(width, np.nan, dtype=np.float64)
+    row[0] = 1.0 if ok else 0.0
+    if ok:
+        cvs = list(result.get("cv_scores") or [])[:width - SCORE_HEAD]
+        row[1] = float(result.get("mean_cv_score", np.nan))
+        row[2] = float(result.get("std_cv_score", np.nan))
+        row[3] = len(cvs)
+        row[SCORE_HEAD:SCORE_HEAD + len(cvs)] = [np.nan if v is None else float(v) for v in cvs]
+    return row
 
 
 class _Res:
@@ -178,13 +222,20 @@ class WorkerCore:
     def __init__(self, device: torch.device, wid: Optional[int] = None, store=None, in_group: bool = True):
         self.inf = dist.info()
         self.wid = self.inf.rank if wid is None else wid
-        self.store = store if store is not None else LockedStore(dist.service_store())
+        if store is None:   # the shared client + a private one this worker blocks on
+            store = LockedStore(dist.service_store(), waiter=_private_client())
+        self.store = store
         self.device = device
         self.in_group = in_group
         self.cache: "collections.OrderedDict[str, Any]" = collections.OrderedDict()
         self.msgs: Dict[int, Dict[str, Any]] = {}
         self.presized: Set[int] = set()
         self.slices_done = 0
+        # scores epoch: this rank's score rows per job (seq -> candidate -> row) until the
+        # job's all-gather; rank 0's merged [candidates, width + 1] table per job after it
+        self.score_rows: Dict[int, Dict[int, np.ndarray]] = {}
+        self.gathered: Dict[int, Any] = {}
+        self.score_width = 64
 
     # ---- job messages and datasets ------------------------------------------------------
     def job_msg(self, seq: int) -> Dict[str, Any]:
@@ -266,7 +317,32 @@ class WorkerCore:
             return self._dp(a, ctl)
         if kind == "refit":
             return self._refit(a, ctl)
+        if kind == "scores":
+            return self._scores(a)
         raise ValueError(f"unknown assignment kind {kind!r}")
+
+    def _scores(self, a) -> Dict[str, Any]:
+        """Scores epoch of one job (every rank of the group): each rank contributes the score
+        rows of the candidates it ran, ONE all_gather_into_tensor (RCCL over xGMI; gloo on
+        CPU) assembles them, rank 0 keeps the merged table for the dispatcher."""
+        seq, n, W = int(a["seq"]), int(a["n"]), int(a["width"])
+        mine = self.score_rows.pop(seq, {})
+        dev = self.inf.device if self.inf.is_dist else self.device
+        t = torch.full((n, W + 1), float("nan"), dtype=torch.float64)
+        t[:, W] = 0.0
+        for c, row in mine.items():
+            if 0 <= c < n:
+                t[c, :W] = torch.from_numpy(row[:W])
+                t[c, W] = 1.0
+        allt = dist.all_gather_rows(t.to(dev)).cpu().numpy().reshape(-1, n, W + 1)
+        if self.inf.rank == 0:
+            merged = np.full((n, W + 1), np.nan)
+            merged[:, W] = 0.0
+            for r in range(allt.shape[0]):          # a re-run slice: the first rank's row wins
+                take = (allt[r, :, W] > 0) & (merged[:, W] == 0)
+                merged[take] = allt[r, take]
+            self.gathered[seq] = (merged, self.inf.backend)
+        return {"scores": seq, "rows": len(mine), "backend": self.inf.backend}
 
     def _slice(self, a, ctl) -> Dict[str, Any]:
         msg = self.job_msg(a["seq"])
@@ -282,6 +358,10 @@ class WorkerCore:
                                            keep_models=msg.get("keep_models", "none"),
                                            models_root=msg.get("models_root"), fault_exit=True)
         self.slices_done += 1
+        if self.in_group:   # kept for the job's scores epoch (parallel/runner.py header)
+            rows = self.score_rows.setdefault(a["seq"], {})
+            for r in results:
+                rows[r.candidate] = score_row(r.ok, r.result or {}, self.score_width)
         return {"results": _enc_results(results, metrics), "wall": wall, "load_s": load_s,
                 "cache": list(self.cache.keys())}
 
@@ -346,8 +426,31 @@ def _save_model(ctl, msg, cand: int, model) -> Optional[str]:
         return None
 
 
+def _private_client():
+    """A second store connection for blocking waits (None: fall back to polling)."""
+    try:
+        return dist.service_client()
+    except Exception:
+        return None
+
+
+def post_wake(st: LockedStore) -> None:
+    """Wake rank 0's dispatcher: ``wake/count`` numbers the events, ``wake/<n>`` is the key
+    the dispatcher blocks on for the n-th one (TCPStore.wait, no timeout, no polling)."""
+    n = int(st.add("wake/count", 1))
+    st.set(f"wake/{n}", "1")
+
+
+def post_result(st: LockedStore, wid: int, k: int, out: Dict[str, Any]) -> None:
+    """Post a worker's answer: ``res/count`` numbers the answers (the dispatcher reads one
+    counter instead of checking every busy worker's key), then wake the dispatcher."""
+    st.set(f"res/{wid}/{k}", json.dumps(json_safe(out)))
+    st.add("res/count", 1)
+    post_wake(st)
+
+
 def worker_loop(core: WorkerCore, ctl: Optional[Controller] = None, heartbeat: bool = True) -> None:
-    """A worker's life: wait for its next assignment, execute it, post the result.
+    """A worker's life: block until its next assignment, execute it, post the result.
 
     A device fault poisons this process's HIP context: the worker posts the error and
     exits non-zero; the dispatcher re-queues its slice to the survivors."""
@@ -358,7 +461,12 @@ def worker_loop(core: WorkerCore, ctl: Optional[Controller] = None, heartbeat: b
         while True:
             key = f"asg/{wid}/{k}"
             try:
-                st.wait([key], poll_s=0.002)
+                while True:
+                    try:
+                        st.wait([key], timeout=3600.0)
+                        break
+                    except TimeoutError:
+                        continue
             except Exception:   # the store (hosted by rank 0) is gone: the service exited
                 log.warning("worker %d lost the controller store; leaving", wid)
                 return
@@ -371,11 +479,12 @@ def worker_loop(core: WorkerCore, ctl: Optional[Controller] = None, heartbeat: b
             except Exception as e:
                 traceback.print_exc()
                 if is_device_fault(e):
-                    st.set(f"res/{wid}/{k}", json.dumps({"fatal": f"{type(e).__name__}: {e}"}))
+                    post_result(st, wid, k, {"fatal": f"{type(e).__name__}: {e}"})
                     log.error("worker %d: device fault, exiting: %s", wid, e)
                     os._exit(3)
                 out = {"error": f"{type(e).__name__}: {e}"}
-            st.set(f"res/{wid}/{k}", json.dumps(json_safe(out)))
+            out["t_post"] = time.time()
+            post_result(st, wid, k, out)
             k += 1
     finally:
         if hb is not None:
@@ -399,7 +508,8 @@ def join_cluster(host: str, port: int, device: torch.device, mem_mb: int = 0, ti
     from torch.distributed import PrefixStore, TCPStore
 
     raw = TCPStore(host, port, is_master=False, timeout=datetime.timedelta(seconds=timeout_s))
-    st = LockedStore(PrefixStore("dml", raw))   # the service's control plane (dist.service_store)
+    waiter = PrefixStore("dml", TCPStore(host, port, is_master=False, timeout=datetime.timedelta(seconds=timeout_s)))
+    st = LockedStore(PrefixStore("dml", raw), waiter=waiter)   # the service's control plane (dist.service_store)
     n = int(st.add("join/n", 1))
     wid = MAX_WORKERS + n - 1
     st.set(f"join/{n - 1}", json.dumps({"wid": wid, "device": str(device), "mem_mb": mem_mb, "pid": os.getpid()}))
@@ -436,6 +546,8 @@ class _JobState:
     n_feat: int = 1
     rechunked: bool = False
     retired: Set[int] = field(default_factory=set)   # queued slices replaced by a re-cut
+    scores_pending: bool = False            # waiting for the job's scores epoch (RCCL all-gather)
+    scores_via: str = "store"               # where the final records' scores came from
 
 
 @dataclass
@@ -472,6 +584,14 @@ class DistributedRunner(Runner):
         self.epoch_queue: List[Dict[str, Any]] = []
         self._hb_missing_since: Dict[int, float] = {}
         self._joined = 0
+        self._res_seen = 0                                 # answers consumed (res/count)
+        self._wake_seen = 0                                # wake events consumed (wake/count)
+        self._waiting = False                              # the dispatcher is blocked on a wake key
+        self._next_liveness = self._next_membership = 0.0
+        self._waiter = LockedStore(self.st._s, waiter=_private_client()) if isinstance(self.st, LockedStore) else None
+        # control-plane accounting: dispatcher loop turns, answer -> next assignment latency
+        self.stats: Dict[str, Any] = {"loops": 0, "answers": 0, "dispatch_latency_s": []}
+        self._t_answer: Dict[int, float] = {}
         self._stage_dir = os.environ.get("DML_STAGE_DIR") or (
             tempfile.mkdtemp(prefix="dml_stage_", dir="/dev/shm") if os.path.isdir("/dev/shm") else tempfile.mkdtemp())
         self._t0 = time.time()
@@ -484,6 +604,21 @@ class DistributedRunner(Runner):
         with self._cv:
             self.pending.append(job)
             self._cv.notify_all()
+        self._poke()
+
+    def _poke(self) -> None:
+        """Wake the dispatcher if it is blocked on the store (new job, shutdown, timer)."""
+        if self._waiting:
+            try:
+                post_wake(self.st)
+            except Exception:
+                pass
+
+    def _ticker(self) -> None:
+        """Liveness / membership deadlines while the dispatcher blocks: one wake per 0.5 s."""
+        while not self.stop:
+            time.sleep(0.5)
+            self._poke()
 
     def requeue(self, units) -> None:
         pass
@@ -492,12 +627,14 @@ class DistributedRunner(Runner):
         with self._cv:
             self.stop = True
             self._cv.notify_all()
+        self._poke()
 
     # ---- main loop ---------------------------------------------------------------------
     def serve_forever(self, idle_poll_s: float = 0.05) -> None:
         w0 = threading.Thread(target=worker_loop, args=(self.core, self.ctl, False), daemon=True,
                               name="dml-rank0-worker")
         w0.start()
+        threading.Thread(target=self._ticker, daemon=True, name="dml-dispatch-ticker").start()
         try:
             while True:
                 with self._cv:
@@ -506,9 +643,15 @@ class DistributedRunner(Runner):
                     stopping = self.stop
                 for job in new:
                     self._admit(job)
+                self.stats["loops"] += 1
                 busy = self._poll_results()
-                self._membership()
-                self._liveness()
+                now = time.time()
+                if now >= self._next_membership:
+                    self._next_membership = now + 0.25
+                    self._membership()
+                if now >= self._next_liveness:
+                    self._next_liveness = now + 0.5
+                    self._liveness()
                 self._dispatch()
                 active = any(not js.finished for js in self.jobs) or any(
                     w.busy is not None for w in self.workers.values() if w.alive)
@@ -518,8 +661,8 @@ class DistributedRunner(Runner):
                     with self._cv:
                         if not self.pending and not self.stop:
                             self._cv.wait(timeout=idle_poll_s)
-                else:
-                    time.sleep(POLL_S)
+                elif not busy:
+                    self._wait_answer(idle_poll_s)
         finally:
             for w in self.workers.values():
                 if w.alive:
@@ -620,6 +763,12 @@ class DistributedRunner(Runner):
     def _assign(self, w: _Worker, a: Dict[str, Any], est: float = 0.0) -> None:
         k = w.next_k
         w.next_k += 1
+        t_ans = self._t_answer.pop(w.wid, None)
+        if t_ans is not None and a["kind"] == "slice":   # the worker's answer -> its next slice
+            lat = self.stats["dispatch_latency_s"]
+            lat.append(time.time() - t_ans)
+            if len(lat) > 100000:
+                del lat[:50000]
         if a["kind"] != "stop":
             w.busy = dict(a, k=k)
             w.sent_at = time.time()
@@ -642,12 +791,18 @@ class DistributedRunner(Runner):
                     if js.transport == "rccl":
                         js.transport = "staged"
                         self._stage(js)
+                elif ep["kind"] == "scores":   # no collective any more: the store copies stand
+                    js.scores_pending = False
+                    self._complete(js)
                 return
             if all(w.busy is None for w in group):
                 self.epoch_queue.pop(0)
                 self.epoch = {"kind": ep["kind"], "job": js, "waiting": {w.wid for w in group}}
+                payload = {"kind": ep["kind"], "seq": js.seq}
+                if ep["kind"] == "scores":
+                    payload.update(n=len(js.job.subtasks), width=self.core.score_width)
                 for w in group:
-                    self._assign(w, {"kind": ep["kind"], "seq": js.seq})
+                    self._assign(w, payload)
                 return
             return   # drain: no new slices until the group is idle
         # refits go to rank 0 (it owns the controller and saves the artefact)
@@ -701,7 +856,39 @@ class DistributedRunner(Runner):
             self.epoch_queue.append({"kind": "load", "job": js})
 
     # ---- results ----------------------------------------------------------------------------
+    def _wait_answer(self, timeout: float) -> None:
+        """Block (server-side, on a private store client) until the next wake event: a
+        worker answer, a submitted job, shutdown, or the 0.5 s liveness ticker -- no busy
+        polling of every worker's result key."""
+        if self._waiter is None or self._waiter._waiter is None:
+            time.sleep(POLL_S)
+            return
+        self._waiting = True
+        try:
+            with self._cv:
+                if self.pending or self.stop:
+                    return
+            self._waiter.wait([f"wake/{self._wake_seen + 1}"], timeout=30.0)
+        except TimeoutError:
+            pass
+        except Exception:
+            time.sleep(POLL_S)
+        finally:
+            self._waiting = False
+            m = int(self.st.add("wake/count", 0))
+            for i in range(self._wake_seen + 1, m + 1):
+                self.st.delete_key(f"wake/{i}")
+            self._wake_seen = m
+
+    def store_ops(self) -> int:
+        """Store operations issued by rank 0's clients (dispatcher, its worker, heartbeat)."""
+        return int(getattr(self.st, "ops", 0)) + int(getattr(self._waiter, "ops", 0))
+
     def _poll_results(self) -> bool:
+        n = int(self.st.add("res/count", 0))
+        if n == self._res_seen:
+            return False
+        self._res_seen = n
         got = False
         for w in list(self.workers.values()):
             if w.busy is None:
@@ -714,6 +901,8 @@ class DistributedRunner(Runner):
             a = w.busy
             w.busy = None
             got = True
+            self.stats["answers"] += 1
+            self._t_answer[w.wid] = float(out.get("t_post", time.time()))
             if "fatal" in out:
                 log.error("worker %d reported a device fault (%s): re-queueing its work", w.wid, out["fatal"])
                 self._declare_dead(w, a)
@@ -738,6 +927,16 @@ class DistributedRunner(Runner):
             self._epoch_answer(w)
             if w.wid == 0 and js is not None:
                 self._finish_dp(js, out)
+            return
+        if kind == "scores":
+            self._epoch_answer(w)
+            if w.wid == 0 and js is not None:
+                if "error" in out:
+                    log.error("scores epoch of job %s failed (%s): the store copies stand", js.job.job_id, out["error"])
+                else:
+                    self._merge_scores(js)
+                js.scores_pending = False
+                self._complete(js)
             return
         if js is None:
             return
@@ -799,8 +998,50 @@ class DistributedRunner(Runner):
         js.retired.update(queued)
         js.queue = collections.deque(range(base, base + len(new)))
 
+    def _collective_scores(self, js: _JobState) -> bool:
+        """The job's scores can travel by collective: the whole launch group is alive and
+        every slice ran inside it."""
+        return (js.transport == "rccl" and dist.info().is_dist and not self.dead and js.scores_via == "store"
+                and all(w.alive for w in self.workers.values() if w.in_group))
+
+    def _merge_scores(self, js: _JobState) -> None:
+        """The final records' scores from the all-gathered table: the held slice's results
+        before they are published, the already-published subtasks in the job table."""
+        got = self.core.gathered.pop(js.seq, None)
+        if got is None:
+            return
+        tab, backend = got
+        via = "rccl" if backend == "nccl" else str(backend)   # nccl IS RCCL on ROCm
+        W = tab.shape[1] - 1
+        mismatch = 0
+        for i, res in js.done.items():
+            for r in res:
+                row = tab[r.candidate] if 0 <= r.candidate < tab.shape[0] else None
+                if row is None or row[W] == 0 or not r.ok or row[0] != 1.0:
+                    continue
+                ncv = int(row[3])
+                upd = {"mean_cv_score": float(row[1]), "std_cv_score": float(row[2]),
+                       "cv_scores": [float(v) for v in row[SCORE_HEAD:SCORE_HEAD + ncv]], "scores_via": via}
+                old = r.result or {}
+                if any(json.dumps(json_safe(old.get(k))) != json.dumps(json_safe(v))
+                       for k, v in upd.items() if k != "scores_via"):
+                    mismatch += 1
+                r.result = dict(old, **upd)
+                if i != js.held:
+                    self.ctl.table.update_result(js.job.job_id, js.job.subtasks[r.candidate].subtask_id, upd)
+        js.scores_via = via
+        if mismatch:
+            log.error("job %s: %d candidates' collective scores differ from their store copies", js.job.job_id,
+                      mismatch)
+
     def _complete(self, js: _JobState) -> None:
-        """Every slice is in: refit the winner (on rank 0), then publish the held slice."""
+        """Every slice is in: all-gather the scores (scores epoch), refit the winner (on
+        rank 0), then publish the held slice."""
+        if self._collective_scores(js):
+            if not js.scores_pending:
+                js.scores_pending = True
+                self.epoch_queue.append({"kind": "scores", "job": js})
+            return
         best = pick_refit(self.ctl, js.job, js.plan, js.done[js.held])
         if best is None:
             self._finish_job(js, None)

@@ -126,6 +126,10 @@ def test_two_rank_gridsearch_gloo():
     assert status["job_status"] == "completed" and status["total_subtasks"] == 8
     res = status["job_result"]["results"]
     assert len(res) == 8
+    # the final records' scores came from the job's scores epoch (all_gather over the
+    # group: gloo here, RCCL on the MI355X ranks), not from the per-slice store copies
+    assert all(r.get("scores_via") == "gloo" for r in res), [r.get("scores_via") for r in res]
+    assert all(r.get("scores_via") == "gloo" for r in status2["job_result"]["results"])
     best = status["best_result"]
     assert best["mean_cv_score"] >= 0.95
     assert len(best["cv_scores"]) == 5
