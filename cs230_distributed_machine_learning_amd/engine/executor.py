@@ -212,6 +212,9 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
                 R["mean_cv_score"] = R.get(main, float("nan"))
             R["scoring"] = scorer
             R["fit_time_total"] = fit_s
+            its = [split_out[s][1].info.get("n_iter") for s in cv_idx if split_out[s][1] is not None]
+            if its and all(i is not None for i in its):   # iterative solvers: per-fold n_iter (sklearn n_iter_)
+                R["n_iter"] = [int(i) for i in its]
             R["n_fits"] = len(split_out)
             if failed_fits:
                 R["failed_fits"] = failed_fits

@@ -92,6 +92,11 @@ def test_rccl_world1_collectives_and_cluster_runner(tmp_path, monkeypatch):
         for name, (status, metrics) in out.items():
             assert status["job_status"] == "completed", (name, status)
             assert status["best_result"]["mean_cv_score"] > 0.85, (name, status["best_result"])
+        # task-parallel jobs: the final records' scores came from the job's scores epoch,
+        # an all_gather_into_tensor on the RCCL group (parallel/runner.py), not the store copies
+        for name in ("rf", "lr"):
+            res = out[name][0]["job_result"]["results"]
+            assert res and all(r.get("scores_via") == "rccl" for r in res), (name, [r.get("scores_via") for r in res])
         assert {m["worker_id"] for m in out["rf"][1]} == {"rank0"}
         assert {m["worker_id"] for m in out["lr_dp"][1]} == {"data-parallel"}
         assert all(js.transport == "rccl" for js in runner.jobs) and not runner.dead
