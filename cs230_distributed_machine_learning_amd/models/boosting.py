@@ -406,7 +406,7 @@ class GradientBoostingFamily(Family):
                 node_loss = torch.full((P,), -1, dtype=torch.long, device=dev)
                 node_loss.scatter_(0, lf, loss_of_tree[tree_of])
                 if LOSS_LOG in needs or LOSS_EXP in needs:
-                    num = torch.zeros(P, dtype=torch.float64, device=dev).index_add_(0, lf, g)
+                    num = leaf_sum(lf, g, P)
                     if K > 1:
                         yk = Y[torch.arange(J, device=dev) % K].reshape(J, n)[m]
                         prob = yk - g
@@ -419,7 +419,7 @@ class GradientBoostingFamily(Family):
                         hess_exp = torch.where(yb > 0.5, g, -g)
                         is_exp = loss_of_tree[tree_of] == LOSS_EXP
                         hess = torch.where(is_exp, hess_exp, hess_log)
-                    den = torch.zeros(P, dtype=torch.float64, device=dev).index_add_(0, lf, hess)
+                    den = leaf_sum(lf, hess, P)
                     if sharded:   # leaf sums over every rank's rows
                         num, den = data.all_reduce(num), data.all_reduce(den)
                     newton = torch.where(den.abs() < 1e-150, torch.where(num == 0, 0.0, torch.sign(num) * 1e150),
@@ -451,9 +451,8 @@ class GradientBoostingFamily(Family):
                             diff = resid[sel_rows] - med[lf[sel_rows]]
                             dl = delta[tree_of[sel_rows]]
                             term = torch.sign(diff) * torch.minimum(dl, diff.abs())
-                            s_ = torch.zeros(P, dtype=torch.float64, device=dev).index_add_(0, lf[sel_rows], term)
-                            c_ = torch.zeros(P, dtype=torch.float64, device=dev).index_add_(
-                                0, lf[sel_rows], torch.ones_like(term))
+                            s_ = leaf_sum(lf[sel_rows], term, P)
+                            c_ = torch.bincount(lf[sel_rows], minlength=P).to(torch.float64)
                             hub = med + s_ / c_.clamp_min(1)
                             value = torch.where(~torch.isnan(med), hub, value)
             # --- raw-score update of every row (train and held-out) ------------------------
@@ -568,6 +567,27 @@ def _extract_tree(nodes: np.ndarray, values: np.ndarray, root: int):
         out_nodes.append((sp, ids[left] if sp >= 0 else -1))
         out_vals.append(float(values[nd]))
     return np.asarray(out_nodes, dtype=np.int32), np.asarray(out_vals, dtype=np.float64)
+
+
+def leaf_sum(leaf: torch.Tensor, v: torch.Tensor, P: int) -> torch.Tensor:
+    """Per-leaf float64 sums of ``v`` (leaf ids in [0, P)).  A plain ``index_add_`` sends a
+    whole stage's rows -- fits x trees x 800k -- into the few leaves of depth-3..5 trees:
+    every add hits one of a handful of addresses and the float64 atomics serialise (82 of
+    88 s of the config-6 GBRT grid, profiles/r3_gbrt_config6.md).  Here each row
+    adds into its own copy of the leaf vector (C x P addresses, rows interleaved over the
+    copies), and the copies are summed."""
+    n = int(leaf.numel())
+    if n == 0:
+        return torch.zeros(P, dtype=torch.float64, device=v.device)
+    C = int(max(1, min(n // 4096, 1024, (64 << 20) // max(1, P))))
+    if C == 1:
+        return torch.zeros(P, dtype=torch.float64, device=v.device).index_add_(0, leaf, v.to(torch.float64))
+    # interleaved copies: consecutive rows (one tree, one or two leaves) go to different
+    # copies, so a wave's 64 adds land on 64 addresses instead of queueing on one
+    chunk = torch.arange(n, device=leaf.device, dtype=torch.int64) % C
+    part = torch.zeros(C * P, dtype=torch.float64, device=v.device)
+    part.index_add_(0, chunk * P + leaf.to(torch.int64), v.to(torch.float64))
+    return part.view(C, P).sum(0)
 
 
 def _pack_model(stages, init: np.ndarray, t: FitTask, data, K: int) -> Dict[str, Any]:

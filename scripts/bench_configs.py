@@ -6,6 +6,8 @@
   3  the headline 256-point RF GridSearchCV is ``bench.py`` (1/2/4/8 GPUs)
   4  RandomizedSearchCV LogisticRegression n_iter=512 cv=5 on --lr-rows x 1000 dense
   5  mixed queue: concurrent RF + LR jobs from several sessions through the controller
+  6  GradientBoostingClassifier GridSearchCV n_estimators {100, 200} x max_depth {3, 5},
+     cv=5, 1M x 100 synthetic, 1 GPU (every fit of the grid boosted in one stage loop)
 
     python scripts/bench_configs.py --configs 1,2,4,5 [--lr-rows 10000000]
 
@@ -186,6 +188,27 @@ def config5(dev):
     ctl.shutdown()
 
 
+def config6(dev):
+    from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
+    from cs230_distributed_machine_learning_amd.search.grid import expand_candidates
+    from cs230_distributed_machine_learning_amd.utils import trace
+
+    dd = _synthetic(1_000_000, 100, dev)
+    grid = {"n_estimators": [100, 200], "max_depth": [3, 5]}
+    cands = expand_candidates("GridSearchCV", {"param_grid": grid})
+    spec = JobSpec("GradientBoostingClassifier", cands, cv=5, holdout=False, keep_models="none")
+    dd.binned()
+    torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    trace.summary(reset=True)
+    t0 = time.time()
+    res = run_candidates(dd, spec, list(range(len(cands))))
+    torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    dt = time.time() - t0
+    assert all(r.ok for r in res), [r.error for r in res if not r.ok]
+    _emit(6, 5 * len(res), dt, grid_points=len(cands), stages_total=5 * sum(int(c["n_estimators"]) for c in cands),
+          best_mean_cv=round(max(r.result["mean_cv_score"] for r in res), 4), phases=trace.summary())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="1,2,4,5")
@@ -209,6 +232,8 @@ def main():
         config4(dev, args.lr_rows)
     if 5 in want:
         config5(dev)
+    if 6 in want:
+        config6(dev)
 
 
 if __name__ == "__main__":

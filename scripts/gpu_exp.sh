@@ -18,6 +18,8 @@
 #   rccl                              world-1 RCCL tests + bench over the process group + rocprof
 #   rehearse                          bench.py --gpus 2/4 sharing the one GPU over gloo
 #   scaling                           scaling_sim.py at 2/4/8 ranks
+#   gbrt                              BASELINE-style GBRT grid (bench_configs.py config 6) + its kernel trace
+#   rccljob                           kernel trace of the world-1 RCCL cluster-runner test (RCCL kernels of real jobs)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -55,5 +57,10 @@ case "$kind" in
            timeout -k 10 400 python bench.py --gpus 2 --rows 250000 --steps 2 --warmup 1 --master-port 29611 > gpurun_out/exp_rh2.log 2>&1 && tail -1 gpurun_out/exp_rh2.log | cut -c1-330 && \
            timeout -k 10 400 python bench.py --gpus 4 --rows 250000 --steps 1 --warmup 1 --master-port 29612 > gpurun_out/exp_rh4.log 2>&1 && tail -1 gpurun_out/exp_rh4.log | cut -c1-330 ;;
   scaling) timeout -k 10 600 python -u scripts/scaling_sim.py --world 2,4,8 --steps 2 > gpurun_out/exp_scaling.log 2>&1 && cat gpurun_out/exp_scaling.log ;;
+  gbrt)    timeout -k 10 600 python -u scripts/bench_configs.py --configs 6 > gpurun_out/exp_gbrt.log 2>&1 && tail -1 gpurun_out/exp_gbrt.log | cut -c1-300 && \
+           timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/exp_gbrt_prof -o run -- python3 scripts/bench_configs.py --configs 6 > gpurun_out/exp_gbrt_prof.log 2>&1 && \
+           python scripts/timeline.py gpurun_out/exp_gbrt_prof > gpurun_out/exp_gbrt_busy.txt && rm -f gpurun_out/exp_gbrt_prof/*kernel_trace.csv && head -3 gpurun_out/exp_gbrt_busy.txt ;;
+  rccljob) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/exp_rccljob -o run -- python3 -m pytest -x -q tests/test_rccl_gpu.py > gpurun_out/exp_rccljob.log 2>&1 && \
+           rm -f gpurun_out/exp_rccljob/*kernel_trace.csv && grep -i -c "nccl\|rccl" gpurun_out/exp_rccljob/run_kernel_stats.csv ;;
   *) echo "unknown kind $kind"; exit 2 ;;
 esac
