@@ -23,13 +23,16 @@ import torch
 from . import dist
 
 
-def broadcast_table(X: Optional[np.ndarray], y: Optional[np.ndarray], device: torch.device, y_kind: str = "auto"):
-    """Rank 0 passes host arrays; every rank returns (X_dev, y_host_numpy)."""
+def broadcast_table(X: Optional[np.ndarray], y: Optional[np.ndarray], device: torch.device, y_kind: str = "auto",
+                    group=None, tag: str = ""):
+    """Rank 0 passes host arrays; every rank returns (X_dev, y_host_numpy).  ``group`` /
+    ``tag``: the communicator and a key suffix unique to this load (concurrent loads on
+    the runner's side group)."""
     inf = dist.info()
     st = dist.store()
     if not inf.is_dist:
         return torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).to(device), np.asarray(y)
-    key = "dataset/meta"
+    key = "dataset/meta" + tag
     if inf.rank == 0:
         y = np.asarray(y)
         # labels may be strings: ship a compact code array + the class table via the store
@@ -47,9 +50,9 @@ def broadcast_table(X: Optional[np.ndarray], y: Optional[np.ndarray], device: to
         meta = json.loads(st.get(key))
         yd = torch.empty((meta["n"],), dtype=torch.float64, device=device)
     Xd = torch.empty((meta["n"], meta["d"]), dtype=torch.float32, device=device)
-    _pipelined_broadcast(X if inf.rank == 0 else None, Xd)
-    dist.broadcast(yd, 0)
-    dist.barrier()
+    _pipelined_broadcast(X if inf.rank == 0 else None, Xd, group=group)
+    dist.broadcast(yd, 0, group=group)
+    dist.barrier(group=group)
     if inf.rank == 0:
         st.delete_key(key)
         return Xd, y
@@ -64,7 +67,8 @@ def broadcast_table(X: Optional[np.ndarray], y: Optional[np.ndarray], device: to
 BCAST_CHUNK_BYTES = 256 << 20
 
 
-def _pipelined_broadcast(X: Optional[np.ndarray], Xd: torch.Tensor, chunk_bytes: Optional[int] = None) -> None:
+def _pipelined_broadcast(X: Optional[np.ndarray], Xd: torch.Tensor, chunk_bytes: Optional[int] = None,
+                         group=None) -> None:
     """Root's host rows -> every rank's ``Xd``, in row chunks, H2D and broadcast overlapped.
 
     Rank 0 copies chunk k host -> HBM on a side stream (the pageable copy path runs at
@@ -94,11 +98,11 @@ def _pipelined_broadcast(X: Optional[np.ndarray], Xd: torch.Tensor, chunk_bytes:
                 compute.wait_event(ev)             # this chunk's broadcast follows its copy only
             else:
                 Xd[r0:r1].copy_(src)
-        dist.broadcast(Xd[r0:r1], 0)
+        dist.broadcast(Xd[r0:r1], 0, group=group)
 
 
 def broadcast_binned(X: Optional[np.ndarray], y: Optional[np.ndarray], classification: bool, device: torch.device,
-                     name: str = ""):
+                     name: str = "", group=None, tag: str = ""):
     """Binned-only distribution of a table too large for HBM as float32 (tree jobs):
     rank 0 streams its host rows through the binning kernel (DeviceData binned_only),
     then ONE RCCL broadcast of the uint8 bins (+ edges) lands them on every rank -- a
@@ -109,23 +113,23 @@ def broadcast_binned(X: Optional[np.ndarray], y: Optional[np.ndarray], classific
     if not inf.is_dist:
         return DeviceData(X, y, classification, device, name=name, binned_only=True)
     st = dist.store()
-    key = "dataset/binmeta"
+    key = "dataset/binmeta" + tag
     if inf.rank == 0:
-        _, y_host = broadcast_table(np.zeros((len(y), 0), dtype=np.float32), y, device)
+        _, y_host = broadcast_table(np.zeros((len(y), 0), dtype=np.float32), y, device, group=group, tag=tag)
         dd = DeviceData(X, y_host, classification, device, name=name, binned_only=True)
         buf, edges, smax = dd._Xb_full.contiguous(), dd._edges.contiguous(), dd._sample_max.contiguous().float()
         st.set(key, json.dumps({"n": int(buf.shape[0]), "ld": int(buf.shape[1]), "d": int(dd.d)}))
     else:
-        _, y_host = broadcast_table(None, None, device)
+        _, y_host = broadcast_table(None, None, device, group=group, tag=tag)
         st.wait([key])
         meta = json.loads(st.get(key))
         buf = torch.empty((meta["n"], meta["ld"]), dtype=torch.uint8, device=device)
         edges = torch.empty((meta["d"], 255), dtype=torch.float32, device=device)
         smax = torch.empty((meta["d"],), dtype=torch.float32, device=device)
-    dist.broadcast(buf, 0)
-    dist.broadcast(edges, 0)
-    dist.broadcast(smax, 0)
-    dist.barrier()
+    dist.broadcast(buf, 0, group=group)
+    dist.broadcast(edges, 0, group=group)
+    dist.broadcast(smax, 0, group=group)
+    dist.barrier(group=group)
     if inf.rank == 0:
         st.delete_key(key)
         return dd
@@ -136,7 +140,7 @@ def allgather_table(X_shard: torch.Tensor, y_shard: torch.Tensor):
     return dist.all_gather_rows(X_shard), dist.all_gather_rows(y_shard)
 
 
-def share_bins(dd) -> None:
+def share_bins(dd, group=None) -> None:
     """Rank 0 computes quantile edges; all ranks bin with the same edges."""
     from ..ops import binning
 
@@ -145,7 +149,7 @@ def share_bins(dd) -> None:
         edges = binning.quantile_edges(dd.X)
     else:
         edges = torch.empty((dd.d, binning.MAX_EDGES), dtype=torch.float32, device=dd.X.device)
-    dist.broadcast(edges, 0)
+    dist.broadcast(edges, 0, group=group)
     dd._edges = edges
     dd._Xb = binning.bin_matrix(dd.X, edges)
 

@@ -88,21 +88,37 @@ def info() -> DistInfo:
     return _INFO or DistInfo()
 
 
-def barrier() -> None:
+_SIDE = None
+
+
+def side_group():
+    """A second communicator over every rank (created collectively, at WorkerCore setup):
+    the cluster runner's collective thread broadcasts new datasets and all-gathers job
+    scores on it WHILE the worker threads run slices on the default stream -- no rank is
+    drained for a collective (parallel/runner.py).  None when not distributed."""
+    global _SIDE
+    if not info().is_dist:
+        return None
+    if _SIDE is None:
+        _SIDE = dist.new_group(ranks=list(range(info().world)), backend=info().backend)
+    return _SIDE
+
+
+def barrier(group=None) -> None:
     if info().is_dist:
         if info().backend == "nccl":
-            dist.barrier(device_ids=[info().local_rank])
+            dist.barrier(group=group, device_ids=[info().local_rank])
         else:
-            dist.barrier()
+            dist.barrier(group=group)
 
 
-def broadcast(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+def broadcast(t: torch.Tensor, src: int = 0, group=None) -> torch.Tensor:
     if info().is_dist:
-        dist.broadcast(t, src=src)
+        dist.broadcast(t, src=src, group=group)
     return t
 
 
-def all_gather_rows(shard: torch.Tensor) -> torch.Tensor:
+def all_gather_rows(shard: torch.Tensor, group=None) -> torch.Tensor:
     """Concatenate equal-size row shards of every rank (rank order) on every rank."""
     inf = info()
     if not inf.is_dist:
@@ -110,10 +126,10 @@ def all_gather_rows(shard: torch.Tensor) -> torch.Tensor:
     shard = shard.contiguous()
     out = torch.empty((shard.shape[0] * inf.world, *shard.shape[1:]), dtype=shard.dtype, device=shard.device)
     if inf.backend == "nccl":
-        dist.all_gather_into_tensor(out, shard)
+        dist.all_gather_into_tensor(out, shard, group=group)
     else:
         parts = list(out.chunk(inf.world, 0))
-        dist.all_gather(parts, shard)
+        dist.all_gather(parts, shard, group=group)
     return out
 
 
@@ -178,7 +194,8 @@ def service_client(timeout_s: float = 300.0):
 
 
 def destroy() -> None:
-    global _INFO
+    global _INFO, _SIDE
+    _SIDE = None
     if dist.is_initialized():
         dist.destroy_process_group()
     _INFO = None

@@ -14,14 +14,16 @@ dispatch           rank 0's dispatcher hands each idle worker its next slice thr
                    slice comes from the active job of the session that has used the least
                    node time so far (slice-level fair share, the same policy as the local
                    runner), so a one-candidate job overtakes a running 256-candidate search
-dataset            once per dataset per worker.  While the whole process group is alive the
-                   dispatcher runs a *collective epoch*: it drains the workers and every rank
-                   receives the table by ONE RCCL broadcast over xGMI (parallel/data.py).
+dataset            once per dataset per worker.  While the whole process group is alive every
+                   rank receives the table by ONE RCCL broadcast over xGMI (parallel/data.py)
+                   issued by the rank's *collective thread* on a second communicator
+                   (dist.side_group) and its own HIP stream: the worker threads keep running
+                   slices of resident datasets meanwhile -- nothing is drained for a load.
                    Once a rank has died (the default group can no longer run collectives) or
                    for a worker that joined after launch, rank 0 stages the table in a host
                    file and each worker copies it to its own GPU over its own PCIe link
 results            every rank keeps the score rows of the candidates it ran; when a job's last
-                   slice lands, a *scores epoch* all-gathers them over RCCL
+                   slice lands, the collective threads all-gather them over RCCL (side group)
                    (all_gather_into_tensor of a [candidates, width] float64 tensor) and rank
                    0 builds the job's final records (J5) from that tensor -- the reference's
                    Kafka ``result`` channel (worker.py:247-254 -> task_handler.py:18-50).  The
@@ -236,33 +238,48 @@ class WorkerCore:
         self.score_rows: Dict[int, Dict[int, np.ndarray]] = {}
         self.gathered: Dict[int, Any] = {}
         self.score_width = 64
+        self.cache_lock = threading.RLock()   # the worker and the collective thread share the cache
+        # the side communicator (collective with every rank: built here, by every in-group rank)
+        self.side = dist.side_group() if (in_group and self.inf.is_dist) else None
 
     # ---- job messages and datasets ------------------------------------------------------
     def job_msg(self, seq: int) -> Dict[str, Any]:
         m = self.msgs.get(seq)
         if m is None:
             m = json.loads(self.store.get(f"job/{seq}"))
+            m["_seq"] = seq
             self.msgs[seq] = m
             while len(self.msgs) > 64:
                 self.msgs.pop(next(iter(self.msgs)))
         return m
 
     def _keep(self, key: str, dd) -> None:
-        self.cache[key] = dd
-        self.cache.move_to_end(key)
-        while len(self.cache) > 4:
-            self.cache.popitem(last=False)
+        with self.cache_lock:
+            self.cache[key] = dd
+            self.cache.move_to_end(key)
+            while len(self.cache) > 4:
+                self.cache.popitem(last=False)
+
+    def cache_keys(self) -> List[str]:
+        with self.cache_lock:
+            return list(self.cache.keys())
 
     def dataset(self, msg: Dict[str, Any], ctl: Optional[Controller] = None):
         """The job's resident table; loaded from the host-staged file when absent."""
         from ..data.device import DeviceData
 
         key = msg["dataset_key"]
-        dd = self.cache.get(key)
-        if dd is not None:
-            self.cache.move_to_end(key)
-            return dd
+        with self.cache_lock:
+            dd = self.cache.get(key)
+            if dd is not None:
+                self.cache.move_to_end(key)
+                return dd
         path = msg.get("staged")
+        if not path and "_seq" in msg:   # cached before the dispatcher host-staged the table
+            fresh = json.loads(self.store.get(f"job/{msg['_seq']}"))
+            fresh["_seq"] = msg["_seq"]
+            self.msgs[msg["_seq"]] = fresh
+            path = fresh.get("staged")
         if not path:
             raise RuntimeError(f"dataset {msg['dataset_id']!r} is not resident on worker {self.wid} and not staged")
         X, y = pdata.load_staged(path, self.device)
@@ -270,14 +287,15 @@ class WorkerCore:
         self._keep(key, dd)
         return dd
 
-    def load_collective(self, msg: Dict[str, Any], ctl: Optional[Controller]):
-        """Collective epoch: every rank receives the table by one broadcast (RCCL on GPU)."""
+    def load_collective(self, msg: Dict[str, Any], ctl: Optional[Controller], group=None, tag: str = ""):
+        """Every rank receives the table by one broadcast (RCCL on GPU); on the side group
+        (``group``, key suffix ``tag``) when the collective thread runs it."""
         from ..data.device import DeviceData
 
         plan = msg["plan"]
         clf = is_classifier(plan["model_type"])
         X = y = None
-        mode_key = "dataset/mode"
+        mode_key = "dataset/mode" + tag
         if self.inf.rank == 0:
             ds = ctl.registry.load(msg["dataset_id"], plan["feature_columns"], plan["target_column"])
             X, y = ds.X, ds.y
@@ -287,13 +305,13 @@ class WorkerCore:
             self.store_raw().wait([mode_key])
             binned = self.store_raw().get(mode_key).decode() == "binned"
         if binned:   # tree job on a table too large for HBM as float32: bins only
-            dd = pdata.broadcast_binned(X, y, clf, self.device, name=msg["dataset_id"])
+            dd = pdata.broadcast_binned(X, y, clf, self.device, name=msg["dataset_id"], group=group, tag=tag)
         else:
-            Xd, y_host = pdata.broadcast_table(X, y, self.device)
+            Xd, y_host = pdata.broadcast_table(X, y, self.device, group=group, tag=tag)
             dd = DeviceData(Xd, y_host, clf, self.device, name=msg["dataset_id"])
             if _needs_bins(plan):
-                pdata.share_bins(dd)
-        dist.barrier()
+                pdata.share_bins(dd, group=group)
+        dist.barrier(group=group)
         if self.inf.rank == 0:
             self.store_raw().delete_key(mode_key)
         self._keep(msg["dataset_key"], dd)
@@ -312,7 +330,7 @@ class WorkerCore:
             msg = self.job_msg(a["seq"])
             t0 = time.perf_counter()
             self.load_collective(msg, ctl)
-            return {"loaded": msg["dataset_key"], "wall": time.perf_counter() - t0, "cache": list(self.cache.keys())}
+            return {"loaded": msg["dataset_key"], "wall": time.perf_counter() - t0, "cache": self.cache_keys()}
         if kind == "dp":
             return self._dp(a, ctl)
         if kind == "refit":
@@ -321,7 +339,26 @@ class WorkerCore:
             return self._scores(a)
         raise ValueError(f"unknown assignment kind {kind!r}")
 
-    def _scores(self, a) -> Dict[str, Any]:
+    def collective(self, a: Dict[str, Any], ctl: Optional[Controller], stream=None) -> Dict[str, Any]:
+        """A task of the collective thread (side group, own stream): a dataset broadcast or
+        a job's scores all-gather.  Every in-group rank runs the tasks in the same order."""
+        t0 = time.perf_counter()
+        ctx = torch.cuda.stream(stream) if stream is not None else _null_ctx()
+        with ctx:
+            if a["kind"] == "load":
+                msg = self.job_msg(a["seq"])
+                self.load_collective(msg, ctl, group=self.side, tag=f"/c{a['i']}")
+                out = {"loaded": msg["dataset_key"], "cache": self.cache_keys()}
+            elif a["kind"] == "scores":
+                out = self._scores(a, group=self.side)
+            else:
+                raise ValueError(f"unknown collective task {a['kind']!r}")
+            if stream is not None:
+                stream.synchronize()   # the table is complete before any slice may use it
+        out["wall"] = time.perf_counter() - t0
+        return out
+
+    def _scores(self, a, group=None) -> Dict[str, Any]:
         """Scores epoch of one job (every rank of the group): each rank contributes the score
         rows of the candidates it ran, ONE all_gather_into_tensor (RCCL over xGMI; gloo on
         CPU) assembles them, rank 0 keeps the merged table for the dispatcher."""
@@ -334,7 +371,7 @@ class WorkerCore:
             if 0 <= c < n:
                 t[c, :W] = torch.from_numpy(row[:W])
                 t[c, W] = 1.0
-        allt = dist.all_gather_rows(t.to(dev)).cpu().numpy().reshape(-1, n, W + 1)
+        allt = dist.all_gather_rows(t.to(dev), group=group).cpu().numpy().reshape(-1, n, W + 1)
         if self.inf.rank == 0:
             merged = np.full((n, W + 1), np.nan)
             merged[:, W] = 0.0
@@ -363,7 +400,7 @@ class WorkerCore:
             for r in results:
                 rows[r.candidate] = score_row(r.ok, r.result or {}, self.score_width)
         return {"results": _enc_results(results, metrics), "wall": wall, "load_s": load_s,
-                "cache": list(self.cache.keys())}
+                "cache": self.cache_keys()}
 
     def _dp(self, a, ctl) -> Dict[str, Any]:
         """Data-parallel job on the whole process group: every rank runs every slice in
@@ -434,6 +471,54 @@ def _private_client():
         return None
 
 
+class _null_ctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def collective_loop(core: WorkerCore, ctl: Optional[Controller] = None) -> None:
+    """An in-group rank's collective thread: runs the dispatcher's collective tasks
+    (``coll/<i>``: dataset broadcasts, job score gathers) in order on the side group and
+    its own stream while the worker thread keeps running slices.  A failed collective
+    means the group is broken: the thread reports it and stops."""
+    st = LockedStore(core.store._s, waiter=_private_client())
+    stream = None
+    if core.device.type == "cuda":
+        torch.cuda.set_device(core.device)
+        stream = torch.cuda.Stream(core.device)
+    i = 0
+    while True:
+        key = f"coll/{i}"
+        try:
+            while True:
+                try:
+                    st.wait([key], timeout=3600.0)
+                    break
+                except TimeoutError:
+                    continue
+            a = json.loads(st.get(key))
+        except Exception:
+            return
+        if a["kind"] == "stop":
+            return
+        a["i"] = i
+        failed = False
+        try:
+            out = core.collective(a, ctl, stream)
+        except Exception as e:
+            traceback.print_exc()
+            out, failed = {"error": f"{type(e).__name__}: {e}"}, True
+        st.set(f"colldone/{core.wid}/{i}", json.dumps(json_safe(out)))
+        st.add("coll/count", 1)
+        post_wake(st)
+        i += 1
+        if failed:
+            return
+
+
 def post_wake(st: LockedStore) -> None:
     """Wake rank 0's dispatcher: ``wake/count`` numbers the events, ``wake/<n>`` is the key
     the dispatcher blocks on for the n-th one (TCPStore.wait, no timeout, no polling)."""
@@ -456,6 +541,8 @@ def worker_loop(core: WorkerCore, ctl: Optional[Controller] = None, heartbeat: b
     exits non-zero; the dispatcher re-queues its slice to the survivors."""
     st, wid = core.store, core.wid
     hb = _Heartbeat(st, wid) if heartbeat else None
+    if core.side is not None:   # this rank's collective thread (side group)
+        threading.Thread(target=collective_loop, args=(core, ctl), daemon=True, name=f"dml-coll-{wid}").start()
     k = 0
     try:
         while True:
@@ -586,11 +673,16 @@ class DistributedRunner(Runner):
         self._joined = 0
         self._res_seen = 0                                 # answers consumed (res/count)
         self._wake_seen = 0                                # wake events consumed (wake/count)
+        # collective tasks run by every in-group rank's collective thread (side group)
+        self.coll_seq = 0
+        self.coll_pending: Dict[int, Dict[str, Any]] = {}
+        self._coll_seen = 0
         self._waiting = False                              # the dispatcher is blocked on a wake key
         self._next_liveness = self._next_membership = 0.0
         self._waiter = LockedStore(self.st._s, waiter=_private_client()) if isinstance(self.st, LockedStore) else None
         # control-plane accounting: dispatcher loop turns, answer -> next assignment latency
-        self.stats: Dict[str, Any] = {"loops": 0, "answers": 0, "dispatch_latency_s": []}
+        self.stats: Dict[str, Any] = {"loops": 0, "answers": 0, "dispatch_latency_s": [], "max_drain_wait_s": 0.0}
+        self._drain_since: Optional[float] = None        # an epoch is draining the group since
         self._t_answer: Dict[int, float] = {}
         self._stage_dir = os.environ.get("DML_STAGE_DIR") or (
             tempfile.mkdtemp(prefix="dml_stage_", dir="/dev/shm") if os.path.isdir("/dev/shm") else tempfile.mkdtemp())
@@ -645,6 +737,7 @@ class DistributedRunner(Runner):
                     self._admit(job)
                 self.stats["loops"] += 1
                 busy = self._poll_results()
+                busy = self._poll_coll() or busy
                 now = time.time()
                 if now >= self._next_membership:
                     self._next_membership = now + 0.25
@@ -664,6 +757,11 @@ class DistributedRunner(Runner):
                 elif not busy:
                     self._wait_answer(idle_poll_s)
         finally:
+            if any(w.in_group for w in self.workers.values()) and self.core.side is not None:
+                try:
+                    self.st.set(f"coll/{self.coll_seq}", json.dumps({"kind": "stop"}))
+                except Exception:
+                    pass
             for w in self.workers.values():
                 if w.alive:
                     self._assign(w, {"kind": "stop"})
@@ -796,6 +894,10 @@ class DistributedRunner(Runner):
                     self._complete(js)
                 return
             if all(w.busy is None for w in group):
+                if self._drain_since is not None:
+                    self.stats["max_drain_wait_s"] = max(self.stats["max_drain_wait_s"],
+                                                         time.time() - self._drain_since)
+                    self._drain_since = None
                 self.epoch_queue.pop(0)
                 self.epoch = {"kind": ep["kind"], "job": js, "waiting": {w.wid for w in group}}
                 payload = {"kind": ep["kind"], "seq": js.seq}
@@ -804,6 +906,8 @@ class DistributedRunner(Runner):
                 for w in group:
                     self._assign(w, payload)
                 return
+            if self._drain_since is None and any(w.busy is None for w in group):
+                self._drain_since = time.time()   # idle ranks wait for the epoch from here
             return   # drain: no new slices until the group is idle
         # refits go to rank 0 (it owns the controller and saves the artefact)
         w0 = self.workers[0]
@@ -851,9 +955,58 @@ class DistributedRunner(Runner):
         return js, js.queue[0]
 
     def _request_load(self, js: _JobState) -> None:
-        if not any(ep["kind"] == "load" and ep["job"].msg["dataset_key"] == js.msg["dataset_key"]
-                   for ep in self.epoch_queue):
-            self.epoch_queue.append({"kind": "load", "job": js})
+        """Broadcast the job's table to every in-group rank -- a collective task of the
+        ranks' collective threads, so no rank is drained for it."""
+        key = js.msg["dataset_key"]
+        if any(t["kind"] == "load" and t["dkey"] == key for t in self.coll_pending.values()):
+            return
+        self._post_coll({"kind": "load", "seq": js.seq}, js, dkey=key)
+
+    def _post_coll(self, task: Dict[str, Any], js: _JobState, dkey: str = "") -> None:
+        i = self.coll_seq
+        self.coll_seq += 1
+        self.st.set(f"coll/{i}", json.dumps(task))
+        self.coll_pending[i] = {"kind": task["kind"], "job": js, "dkey": dkey, "t0": time.time(),
+                                "waiting": {w.wid for w in self.workers.values() if w.in_group and w.alive}}
+
+    def _poll_coll(self) -> bool:
+        """Answers of the collective threads (``colldone/<worker>/<task>``)."""
+        n = int(self.st.add("coll/count", 0))
+        if n == self._coll_seen:
+            return False
+        self._coll_seen = n
+        for i, t in list(self.coll_pending.items()):
+            for wid in list(t["waiting"]):
+                key = f"colldone/{wid}/{i}"
+                if not self.st.check([key]):
+                    continue
+                out = json.loads(self.st.get(key))
+                self.st.delete_key(key)
+                t["waiting"].discard(wid)
+                self._on_coll(t, wid, out)
+            if not t["waiting"]:
+                self.coll_pending.pop(i, None)
+                self.st.delete_key(f"coll/{i}")
+        return True
+
+    def _on_coll(self, t: Dict[str, Any], wid: int, out: Dict[str, Any]) -> None:
+        js, w = t["job"], self.workers.get(wid)
+        if t["kind"] == "load":
+            if w is not None and "cache" in out:
+                w.loaded = set(out["cache"])
+            if "error" in out and js.transport == "rccl":
+                log.error("collective load of %s failed on worker %d (%s): host-staging it", js.job.dataset_id, wid,
+                          out["error"])
+                js.transport = "staged"
+                self._stage(js)
+            return
+        if t["kind"] == "scores" and wid == 0 and js.scores_pending:
+            if "error" in out:
+                log.error("scores gather of job %s failed (%s): the store copies stand", js.job.job_id, out["error"])
+            else:
+                self._merge_scores(js)
+            js.scores_pending = False
+            self._complete(js)
 
     # ---- results ----------------------------------------------------------------------------
     def _wait_answer(self, timeout: float) -> None:
@@ -1040,7 +1193,8 @@ class DistributedRunner(Runner):
         if self._collective_scores(js):
             if not js.scores_pending:
                 js.scores_pending = True
-                self.epoch_queue.append({"kind": "scores", "job": js})
+                self._post_coll({"kind": "scores", "seq": js.seq, "n": len(js.job.subtasks),
+                                 "width": self.core.score_width}, js)
             return
         best = pick_refit(self.ctl, js.job, js.plan, js.done[js.held])
         if best is None:
@@ -1171,6 +1325,16 @@ class DistributedRunner(Runner):
             # a collective cannot complete without this rank: the survivors of the epoch time
             # out (DML_COLLECTIVE_TIMEOUT_S); the dispatcher stops waiting for the dead one
             self._epoch_answer(w)
+        if w.in_group:
+            # pending side-group collectives can no longer complete: loads fall back to
+            # host staging (below), score gathers to the per-slice store copies
+            for i, t in list(self.coll_pending.items()):
+                self.coll_pending.pop(i, None)
+                js = t["job"]
+                if t["kind"] == "scores" and js.scores_pending:
+                    js.scores_pending = False
+                    js.scores_via = "store-fallback"
+                    self._complete(js)
         # the group is broken for good: pending collectives become host-staged / task-parallel
         if w.in_group:
             for js in self.jobs:

@@ -112,6 +112,7 @@ def _rank_main(rank, world, port, root, kill, outq):
             outq.put(("ok", {"world": world, "killed": kill, "dead": sorted(runner.dead), "wall_s": round(wall, 2),
                              "jobs": jobs, "dispatcher_loops": runner.stats["loops"],
                              "answers": runner.stats["answers"], "rank0_store_ops": ops,
+                             "max_drain_wait_s": round(runner.stats["max_drain_wait_s"], 3),
                              "rank0_store_ops_per_s": round(ops / max(wall, 1e-9), 1),
                              "dispatch_latency_ms": {"p50": pct(0.5), "p90": pct(0.9), "p99": pct(0.99),
                                                      "max": pct(1.0), "n": len(lat)}}))

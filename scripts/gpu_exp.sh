@@ -19,6 +19,7 @@
 #   rehearse                          bench.py --gpus 2/4 sharing the one GPU over gloo
 #   scaling                           scaling_sim.py at 2/4/8 ranks
 #   gbrt                              BASELINE-style GBRT grid (bench_configs.py config 6) + its kernel trace
+#   cluster                           world-1 RCCL runner test + config 5 and bench --e2e through the cluster runner
 #   rccljob                           kernel trace of the world-1 RCCL cluster-runner test (RCCL kernels of real jobs)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -60,6 +61,9 @@ case "$kind" in
   gbrt)    timeout -k 10 600 python -u scripts/bench_configs.py --configs 6 > gpurun_out/exp_gbrt.log 2>&1 && tail -1 gpurun_out/exp_gbrt.log | cut -c1-300 && \
            timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/exp_gbrt_prof -o run -- python3 scripts/bench_configs.py --configs 6 > gpurun_out/exp_gbrt_prof.log 2>&1 && \
            python scripts/timeline.py gpurun_out/exp_gbrt_prof > gpurun_out/exp_gbrt_busy.txt && rm -f gpurun_out/exp_gbrt_prof/*kernel_trace.csv && head -3 gpurun_out/exp_gbrt_busy.txt ;;
+  cluster) timeout -k 10 300 $PYT tests/test_rccl_gpu.py > gpurun_out/exp_rccl_test.log 2>&1 && tail -1 gpurun_out/exp_rccl_test.log && \
+           DML_FORCE_PG=1 MASTER_PORT=29602 timeout -k 10 600 python -u scripts/bench_configs.py --configs 5 > gpurun_out/exp_cfg5_dist.log 2>&1 && tail -1 gpurun_out/exp_cfg5_dist.log | cut -c1-300 && \
+           DML_FORCE_PG=1 MASTER_PORT=29601 timeout -k 10 900 python -u bench.py --e2e > gpurun_out/exp_e2e_dist.log 2>&1 && tail -1 gpurun_out/exp_e2e_dist.log | cut -c1-300 ;;
   rccljob) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/exp_rccljob -o run -- python3 -m pytest -x -q tests/test_rccl_gpu.py > gpurun_out/exp_rccljob.log 2>&1 && \
            rm -f gpurun_out/exp_rccljob/*kernel_trace.csv && grep -i -c "nccl\|rccl" gpurun_out/exp_rccljob/run_kernel_stats.csv ;;
   *) echo "unknown kind $kind"; exit 2 ;;
