@@ -379,13 +379,19 @@ class DeviceCache:
 
         ds = ctl.registry.load(dataset_id, plan["feature_columns"], plan["target_column"])
         clf = is_classifier(plan["model_type"])
+        base = (ds.path, os.path.getmtime(ds.path) if ds.path else 0, tuple(ds.feature_names), ds.target_name, clf)
+        # a resident float32 entry serves every job on this table (a tree job reads its bins
+        # too), so the free-HBM test below never caches the same table twice; a bins-only
+        # entry serves the tree jobs it was made for
+        full = base + (False,)
+        tree_ok = getattr(family_of(plan["model_type"]), "binned_ok", False)
+        for key in ((full, base + (True,)) if tree_ok else (full,)):
+            if key in self._items:
+                self._order.remove(key)
+                self._order.append(key)
+                return self._items[key]
         binned = self._binned_only(ctl, plan, ds.X)
-        key = (ds.path, os.path.getmtime(ds.path) if ds.path else 0, tuple(ds.feature_names), ds.target_name, clf,
-               binned)
-        if key in self._items:
-            self._order.remove(key)
-            self._order.append(key)
-            return self._items[key]
+        key = base + (binned,)
         dd = DeviceData(ds.X, ds.y, clf, self.device, name=dataset_id, binned_only=binned)
         self._items[key] = dd
         self._order.append(key)
