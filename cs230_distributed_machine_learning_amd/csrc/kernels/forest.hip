@@ -117,6 +117,8 @@ struct ForestArgs {
   int64_t XbT;           // optional feature-major copy of the bins, uint8 [d][n] (0 = none)
   int64_t cw;            // class-weight table double [T][C] (0 = no class weights in this build)
   int64_t yq_e1, yq_e2;  // regression fixed-point exponents (forest_common.h reg_exponents)
+  int64_t mono;          // int8 [fits][d] monotonic_cst rows (binary classifiers negated), 0 = none
+  int64_t nbound;        // double [pool_cap][2] node bounds (lo, hi) when mono != 0
 };
 
 constexpr int kTiers = 4;  // 0 subtree, 1 wave, 2 block, 3 large
@@ -129,6 +131,7 @@ struct LState {
   double best_gain;
   int32_t best_pos; // visiting position of the best split's feature
   int32_t scr_n;    // positions [0, scr_n) have their bins in Ctx::bscr (round 0, <= 16 features)
+  double best_mid;  // monotonic_cst: middle value of the best split
 };
 
 struct Ctx {
@@ -182,7 +185,29 @@ struct Ctx {
   // regression: exact integer histogram sums of w, w yq, w y2q (forest_common.h)
   RegScale rq;
   unsigned long long* rsum;   // [T][3] integer root sums (k_fill_active -> k_roots)
+  // monotonic_cst: per-fit constraint rows and every pool node's value bounds [lo, hi]
+  // (forest_common.h mono_*); null when no tree of the build is constrained
+  const int8_t* mono;
+  double* nbound;
 };
+
+// the constraint of feature f for the tree's fit (0: unconstrained or no table)
+__device__ __forceinline__ int mono_of(const Ctx& c, const TreeSpec& s, int f) {
+  return c.mono ? (int)c.mono[(int64_t)s.fit * c.d + f] : 0;
+}
+
+// children's bounds from the parent's and the chosen split (every child of a build with a
+// constraint table gets bounds, unconstrained splits pass the parent's through)
+__device__ __forceinline__ void mono_children(const Ctx& c, int node, int left, int m, double mid) {
+  if (!c.nbound) return;
+  const double lo = c.nbound[2 * (int64_t)node], hi = c.nbound[2 * (int64_t)node + 1];
+  for (int side = 0; side < 2; ++side) {
+    double clo, chi;
+    mono_child_bounds(m, lo, hi, mid, side, clo, chi);
+    c.nbound[2 * (int64_t)(left + side)] = clo;
+    c.nbound[2 * (int64_t)(left + side) + 1] = chi;
+  }
+}
 
 // target vector of a tree (shared y, or its own row of the boosting target matrix)
 __device__ __forceinline__ const float* tree_y(const Ctx& c, const TreeSpec& s) {
@@ -330,10 +355,16 @@ __device__ __forceinline__ double hist_chan(const typename HT<MODE>::T* h, int c
 // ONE wave evaluates one feature's histogram: in-place scans, best bin, non-constant
 // flag, the best bin's cumulative channels (out_left[CH]); optionally zeroes the
 // histogram afterwards so the next feature group needs no clearing pass.
+// monotonic_cst of one evaluated feature: its constraint m (0 = none) and the node's bounds
+struct MonoQ {
+  int m;
+  double lo, hi;
+};
+
 template <int MODE>
 __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
                                  double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after,
-                                 const double* cw);
+                                 const double* cw, MonoQ mq, double* out_mid);
 
 // ONE wave evaluates one feature's histogram.  Binary (MODE 1) and regression (MODE 2)
 // histograms are read ONCE into registers (4 bins per lane), scanned with DPP, scored and
@@ -342,9 +373,10 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
 template <int MODE>
 __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
                              double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after,
-                             const double* cw = nullptr, const RegScale* rq = nullptr) {
+                             const double* cw = nullptr, const RegScale* rq = nullptr, MonoQ mq = MonoQ{0, 0.0, 0.0},
+                             double* out_mid = nullptr) {
   if constexpr (MODE == 0) {
-    eval_feature_lds<MODE>(h, C, CH, s, lane, out_gain, out_bin, out_nc, out_left, zero_after, cw);
+    eval_feature_lds<MODE>(h, C, CH, s, lane, out_gain, out_bin, out_nc, out_left, zero_after, cw, mq, out_mid);
   } else {
     using CT = typename HT<MODE>::T;
     constexpr int NP = MODE == 1 ? 1 : 3;      // planes: packed u64 | (w | rows << 32, w yq, w y2q) integers
@@ -375,7 +407,7 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
     for (int q = 0; q < NP; ++q) tot[q] = wave::bcast<CT>(v[q][3], 63);
     const double msl = (double)s.min_samples_leaf;
     const double cw0 = cwk(cw, 0), cw1 = cwk(cw, 1);
-    double best = -INFINITY;
+    double best = -INFINITY, bmid = 0.0;
     int bb = -1;
     bool nc = false;
     double tot_rows;
@@ -391,7 +423,7 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
       if (b == 255) continue;
       nc |= (rl > 0.0 && rr > 0.0);
       if (rl < msl || rr < msl) continue;
-      double g;
+      double g, mid = 0.0;
       if constexpr (MODE == 1) {
         const uint64_t cv = (uint64_t)v[0][i], tv = (uint64_t)tot[0];
         const double l0 = (double)(cv & kPackMask21) * cw0, l1 = (double)((cv >> 21) & kPackMask21) * cw1;
@@ -401,13 +433,21 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
         L.add(l0); L.add(l1);
         R.add(t0 - l0); R.add(t1 - l1);
         if (side_too_light(s, L.w, R.w)) continue;
+        if (mq.m) {   // monotonic_cst on the class-0 fraction (forest_cpu.cpp)
+          if (!mono_ok(mq.m, mq.lo, mq.hi, side_value(L.w, l0), side_value(R.w, t0 - l0))) continue;
+          mid = mono_mid(L.w, l0, R.w, t0 - l0);
+        }
         g = cls_proxy(L, R, s.criterion);
       } else {   // the host builder's formula (forest_cpu.cpp), on the same integers
         const double l0 = reg_w(v[0][i]), t0 = reg_w(tot[0]), l1 = reg_s1(v[1][i], *rq), t1 = reg_s1(tot[1], *rq);
         if (side_too_light(s, l0, t0 - l0)) continue;
+        if (mq.m) {
+          if (!mono_ok(mq.m, mq.lo, mq.hi, side_value(l0, l1), side_value(t0 - l0, t1 - l1))) continue;
+          mid = mono_mid(l0, l1, t0 - l0, t1 - l1);
+        }
         g = reg_proxy(s.criterion, l0, l1, t0 - l0, t1 - l1);
       }
-      if (g > best) { best = g; bb = b; }
+      if (g > best) { best = g; bb = b; bmid = mid; }
     }
     wave::argmax(best, bb, lane);
     const bool any_nc = __ballot(nc) != 0ull;
@@ -441,6 +481,10 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
         out_left[3] = bb >= 0 ? reg_rows(cq[0]) : 0.0;
       }
     }
+    if (out_mid) {   // the winning bin's middle value, from its owner lane
+      const double m = wave::bcast<double>(bmid, bb >= 0 ? (bb >> 2) : 0);
+      if (lane == 0) *out_mid = m;
+    }
     if (lane == 0) { *out_gain = best; *out_bin = bb; *out_nc = any_nc ? 1 : 0; }
   }
 }
@@ -448,7 +492,7 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
 template <int MODE>
 __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
                                  double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after,
-                                 const double* cw) {
+                                 const double* cw, MonoQ mq, double* out_mid) {
   using CT = typename HT<MODE>::T;
   static_assert(MODE == 0, "binary and regression histograms are evaluated in registers (eval_feature)");
   const int planes = hist_planes(MODE, CH);
@@ -456,7 +500,7 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
   wave_lds_sync();
   const double tot_rows = hist_chan<MODE>(h, CH - 1, CH, 255);
   const double msl = (double)s.min_samples_leaf;
-  double best = -INFINITY;
+  double best = -INFINITY, bmid = 0.0;
   int bb = -1;
   bool nc = false;
 #pragma unroll
@@ -467,22 +511,32 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
     const double rr = tot_rows - rl;
     nc |= (rl > 0.0 && rr > 0.0);
     if (rl < msl || rr < msl) continue;
-    double g;
+    double g, mid = 0.0;
     {
       ClsAcc L, R;
       L.init(s.criterion); R.init(s.criterion);
+      double l0 = 0.0, t0 = 0.0;
       for (int k = 0; k < C; ++k) {
         const double lc = hist_chan<MODE>(h, k, CH, b) * cwk(cw, k);
         const double tc = hist_chan<MODE>(h, k, CH, 255) * cwk(cw, k);
+        if (k == 0) { l0 = lc; t0 = tc; }
         L.add(lc);
         R.add(tc - lc);
       }
       if (side_too_light(s, L.w, R.w)) continue;
+      if (mq.m) {   // binary monotonic_cst (class-0 fraction)
+        if (!mono_ok(mq.m, mq.lo, mq.hi, side_value(L.w, l0), side_value(R.w, t0 - l0))) continue;
+        mid = mono_mid(L.w, l0, R.w, t0 - l0);
+      }
       g = cls_proxy(L, R, s.criterion);
     }
-    if (g > best) { best = g; bb = b; }
+    if (g > best) { best = g; bb = b; bmid = mid; }
   }
   wave::argmax(best, bb, lane);
+  if (out_mid) {
+    const double m = wave::bcast<double>(bmid, bb >= 0 ? (bb >> 2) : 0);
+    if (lane == 0) *out_mid = m;
+  }
   const bool any_nc = __ballot(nc) != 0ull;
   if (lane < CH) out_left[lane] = bb >= 0 ? hist_chan<MODE>(h, lane, CH, bb) * (lane < C ? cwk(cw, lane) : 1.0) : 0.0;
   if (lane == 0) { *out_gain = best; *out_bin = bb; *out_nc = any_nc ? 1 : 0; }
@@ -571,10 +625,12 @@ struct Scratch {
   int32_t best_pos;         // visiting position of the best split's feature
   int32_t scr_n;            // streamed nodes: positions [0, scr_n) have their bins in Ctx::bscr
   int32_t wcnt[32];         // partition: [2][RPT][NW] per-wave counts
+  double best_mid;          // monotonic_cst: middle value of the best split
+  double lo, hi;            // monotonic_cst: this node's bounds
 };
 
 struct FusedLayout {
-  size_t hist, feats, rg, rb, rn, rleft, best_left, pvs, rvs, sc, total;
+  size_t hist, feats, rg, rb, rn, rleft, rmid, best_left, pvs, rvs, sc, total;
 };
 
 __host__ __device__ inline FusedLayout fused_layout(int KG, int span, int elem, int CH) {
@@ -587,6 +643,7 @@ __host__ __device__ inline FusedLayout fused_layout(int KG, int span, int elem, 
   L.rb = take((size_t)KG * 4);
   L.rn = take((size_t)KG * 4);
   L.rleft = take((size_t)KG * CH * 8);
+  L.rmid = take((size_t)KG * 8);
   L.best_left = take((size_t)CH * 8);
   L.pvs = take((size_t)CH * 8);
   L.rvs = take((size_t)CH * 8);
@@ -706,6 +763,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   int* rb = (int*)(smem + FL.rb);
   int* rn = (int*)(smem + FL.rn);
   double* rleft = (double*)(smem + FL.rleft);
+  double* rmid = (double*)(smem + FL.rmid);     // monotonic_cst: each feature's best middle value
   double* best_left = (double*)(smem + FL.best_left);
   double* pvs = (double*)(smem + FL.pvs);       // parent channel sums
   double* rvs = (double*)(smem + FL.rvs);       // right child channel sums
@@ -718,6 +776,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     sc->nonconst = 0; sc->pos = 0; sc->first = 1; sc->last = 0; sc->best_j = -1;
     sc->best_pos = 1 << 30; sc->scr_n = 0;
     sc->W = c.tree_W[on.tree];
+    sc->best_mid = 0.0;
+    sc->lo = c.nbound ? c.nbound[2 * (int64_t)on.node] : -INFINITY;
+    sc->hi = c.nbound ? c.nbound[2 * (int64_t)on.node + 1] : INFINITY;
   }
   const FeatPerm fp = feat_perm(on.key, d);   // node's feature visiting order (forest_common.h)
   const uint32_t* rows = c.rows_cur + on.start;
@@ -903,11 +964,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     for (int j = wid; j < g; j += NW) {
 #ifdef DML_X2_EVAL   // sensitivity build: every feature evaluated twice (the first keeps the histogram)
       eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, false,
-                         tree_cw(c, on.tree), &c.rq);
+                         tree_cw(c, on.tree), &c.rq, MonoQ{mono_of(c, s, feats[j]), sc->lo, sc->hi}, rmid + j);
       wave_lds_sync();
 #endif
       eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, true,
-                         tree_cw(c, on.tree), &c.rq);
+                         tree_cw(c, on.tree), &c.rq, MonoQ{mono_of(c, s, feats[j]), sc->lo, sc->hi}, rmid + j);
     }
     __syncthreads();
     PH(3)
@@ -926,7 +987,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
       const bool upd = jj < 64 && gj > sc->best_gain;
       if (upd && lane < c.CH) best_left[lane] = rleft[jj * c.CH + lane];
       if (lane == 0) {
-        if (upd) { sc->best_gain = gj; sc->best_feat = feats[jj]; sc->best_bin = rb[jj]; sc->best_pos = pos + jj; }
+        if (upd) {
+          sc->best_gain = gj; sc->best_feat = feats[jj]; sc->best_bin = rb[jj]; sc->best_pos = pos + jj;
+          sc->best_mid = rmid[jj];
+        }
         sc->best_j = upd ? jj : -1;
         // bscr slots: byte q of a row's 16-B slot = visiting position q (written by the
         // streamed histogram passes: the block tier's first group, the wave tier's groups)
@@ -973,6 +1037,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
         }
         NodeRec rec; rec.split = pack_split(sc->best_feat, sc->best_bin); rec.left = base;
         c.nodes[on.node] = rec;
+        mono_children(c, on.node, base, mono_of(c, s, sc->best_feat), sc->best_mid);
       }
     }
     sc->base = base;
@@ -1094,12 +1159,14 @@ struct SubEntry {
   uint64_t mask;
   uint64_t key;
   int32_t node, depth;
+  double lo, hi;   // monotonic_cst bounds of the node
 };
 
 // evaluate one feature for the rows in `mask`; lane data: bin b (valid if in mask).
 template <bool REG>
 __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt, int lane, int my_bin, int my_cls,
-                         float my_w, int64_t my_yq, double& gain, int& bin, bool& nonconst, const double* cw) {
+                         float my_w, int64_t my_yq, double& gain, int& bin, bool& nonconst, const double* cw,
+                         MonoQ mq, double& mid) {
   const bool act = (mask >> lane) & 1ull;
   const uint32_t key = act ? ((uint32_t)my_bin << 6) | (uint32_t)lane : 0xFFFFFFFFu;
   const uint32_t sk = wave::bitonic64(key, lane);
@@ -1113,7 +1180,7 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
   const int lrows = lane + 1, rrows = cnt - lrows;
   const bool cand = valid_row && lane < cnt - 1 && b != bnext && lrows >= s.min_samples_leaf &&
                     rrows >= s.min_samples_leaf;
-  double g = -INFINITY;
+  double g = -INFINITY, mid_l = 0.0;
   bool ok = cand;   // cand and both sides at least min_weight_leaf heavy
   if constexpr (!REG) {
     // every shuffle runs with the full wave active (a shuffle inside a divergent branch
@@ -1123,15 +1190,21 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
     const uint32_t w = valid_row ? (uint32_t)wsh : 0u;
     ClsAcc L, R;
     L.init(s.criterion); R.init(s.criterion);
+    double l0 = 0.0, t0 = 0.0;
     for (int k = 0; k < c.C; ++k) {
       const uint32_t v = (ycls == k) ? w : 0u;
       const uint32_t pre = wave::incl_scan<uint32_t>(v);
       const uint32_t tot = wave::bcast<uint32_t>(pre, cnt - 1);
       const double lw = (double)pre * cwk(cw, k), tw = (double)tot * cwk(cw, k);
+      if (k == 0) { l0 = lw; t0 = tw; }
       L.add(lw);
       R.add(tw - lw);
     }
     ok = cand && !side_too_light(s, L.w, R.w);
+    if (ok && mq.m) {   // monotonic_cst (class-0 fraction)
+      ok = mono_ok(mq.m, mq.lo, mq.hi, side_value(L.w, l0), side_value(R.w, t0 - l0));
+      mid_l = mono_mid(L.w, l0, R.w, t0 - l0);
+    }
     if (ok) g = cls_proxy(L, R, s.criterion);
   } else {
     // integer prefix sums of w and w yq in (bin, lane) order: at the last lane of a bin
@@ -1146,10 +1219,15 @@ __device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt
     const uint64_t t0 = wave::bcast<uint64_t>(p0, cnt - 1), t1 = wave::bcast<uint64_t>(p1, cnt - 1);
     const double l0 = (double)p0, tt0 = (double)t0, l1 = reg_s1(p1, c.rq), tt1 = reg_s1(t1, c.rq);
     ok = cand && !side_too_light(s, l0, tt0 - l0);
+    if (ok && mq.m) {
+      ok = mono_ok(mq.m, mq.lo, mq.hi, side_value(l0, l1), side_value(tt0 - l0, tt1 - l1));
+      mid_l = mono_mid(l0, l1, tt0 - l0, tt1 - l1);
+    }
     if (ok) g = reg_proxy(s.criterion, l0, l1, tt0 - l0, tt1 - l1);
   }
   int bl = ok ? lane : 64;
   wave::argmax(g, bl, lane);
+  mid = wave::bcast<double>(mid_l, bl & 63);
   gain = g;
   const int bsel = wave::bcast<int>(b, bl & 63);
   bin = bl < 64 ? bsel : -1;
@@ -1346,6 +1424,8 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     SubEntry e;
     e.mask = cnt0 >= 64 ? ~0ull : ((1ull << cnt0) - 1ull);
     e.key = on.key; e.node = on.node; e.depth = on.depth;
+    e.lo = c.nbound ? c.nbound[2 * (int64_t)on.node] : -INFINITY;
+    e.hi = c.nbound ? c.nbound[2 * (int64_t)on.node + 1] : INFINITY;
     stack[0] = e;
   }
   if (lane < VC) sstats[lane] = c.node_val[(int64_t)on.node * VC + lane];
@@ -1362,9 +1442,9 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     const double* pv = sstats + sp * VC;
     const int cnt = __popcll(e.mask);
     int nonconst = 0, best_f = -1, best_b = -1;
-    double best_g = -INFINITY;
+    double best_g = -INFINITY, best_mid = 0.0;
     const FeatPerm fp = feat_perm(e.key, d);
-    if (!REG && cache && cnt <= 32) {
+    if (!REG && cache && cnt <= 32 && !c.mono) {
       // compact the node's rows: compact row j <- lane of the j-th set bit of the mask
       const bool in = (e.mask >> lane) & 1ull;
       if (in) cidx[lane_prefix(e.mask)] = lane;
@@ -1381,13 +1461,14 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     for (int pos = 0; nonconst < s.max_features && pos < d; ++pos) {
       const int f = feature_at(fp, pos, d);
       const int my_bin = cache ? xc[lane * dp + f] : (lane < cnt0 ? xg[f] : 0);
-      double g;
+      double g, mid;
       int bb;
       bool nc;
-      sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_yq, g, bb, nc, tcw);
+      sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_yq, g, bb, nc, tcw,
+                    MonoQ{mono_of(c, s, f), e.lo, e.hi}, mid);
       if (nc) {
         ++nonconst;
-        if (bb >= 0 && g > best_g) { best_g = g; best_f = f; best_b = bb; }
+        if (bb >= 0 && g > best_g) { best_g = g; best_f = f; best_b = bb; best_mid = mid; }
       }
     }
     if (best_f < 0) continue;
@@ -1425,6 +1506,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
       }
       NodeRec rec; rec.split = pack_split(best_f, best_b); rec.left = base;
       c.nodes[e.node] = rec;
+      mono_children(c, e.node, base, mono_of(c, s, best_f), best_mid);
     }
     base = wave::bcast<int>(base, 0);
     if (base < 0) continue;
@@ -1438,13 +1520,16 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
                           impurity_of_vals(c, right_ch, s.criterion) > kEps;
       const bool push_l = !leaf_by_counts(s, nl, dep) && !leaf_by_weight(s, vals_weight(left_ch, c.C, c.is_reg)) &&
                           impurity_of_vals(c, left_ch, s.criterion) > kEps;
+      const int mbest = mono_of(c, s, best_f);
       if (push_r) {
         SubEntry r; r.mask = rm; r.key = child_key(e.key, 1); r.node = base + 1; r.depth = dep;
+        mono_child_bounds(mbest, e.lo, e.hi, best_mid, 1, r.lo, r.hi);
         for (int q = 0; q < VC; ++q) sstats[sp * VC + q] = right_ch[q];
         stack[sp++] = r;
       }
       if (push_l) {
         SubEntry l; l.mask = lm; l.key = child_key(e.key, 0); l.node = base; l.depth = dep;
+        mono_child_bounds(mbest, e.lo, e.hi, best_mid, 0, l.lo, l.hi);
         for (int q = 0; q < VC; ++q) sstats[sp * VC + q] = left_ch[q];
         stack[sp++] = l;
       }
@@ -1475,6 +1560,7 @@ __global__ __launch_bounds__(64) void k_large_prep(Ctx c, int set_cur, int nL) {
   if (lane != 0) return;
   st.pos = 0; st.nonconst = 0; st.done = 0; st.best_feat = -1; st.best_bin = -1; st.split = 0; st.nl = 0;
   st.best_gain = -INFINITY;
+  st.best_mid = 0.0;
   st.best_pos = 1 << 30;
   st.scr_n = st.g <= 16 ? st.g : 0;
   c.lstate[slot] = st;
@@ -1592,15 +1678,18 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   int* rb = (int*)(rg + c.kg_large);
   int* rn = rb + c.kg_large;
   double* rleft = (double*)(rn + c.kg_large + (c.kg_large & 1));
+  double* rmid = rleft + (int64_t)c.kg_large * c.CH;   // monotonic_cst middle values
   __shared__ int need_more;
   const CT* gh = (const CT*)c.ghist + (int64_t)slot * c.kg_large * span;
   for (int i = tid; i < g * span; i += 256) hist[i] = gh[i];
+  const int16_t* feats = c.lperm + (int64_t)slot * c.d + st.pos;
+  const double nlo = c.nbound ? c.nbound[2 * (int64_t)st.on.node] : -INFINITY;
+  const double nhi = c.nbound ? c.nbound[2 * (int64_t)st.on.node + 1] : INFINITY;
   __syncthreads();
   for (int j = wid; j < g; j += 4)
     eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, false,
-                       tree_cw(c, st.on.tree), &c.rq);
+                       tree_cw(c, st.on.tree), &c.rq, MonoQ{mono_of(c, s, feats[j]), nlo, nhi}, rmid + j);
   __syncthreads();
-  const int16_t* feats = c.lperm + (int64_t)slot * c.d + st.pos;
   double* best_left = c.lbest_left + (int64_t)slot * c.CH;
   if (tid == 0) {
     int nc = st.nonconst, bf = st.best_feat, bbin = st.best_bin;
@@ -1608,7 +1697,7 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
     int uj;
     select_group(c, s, feats, g, rg, rb, rn, rleft, best_left, nc, bg, bf, bbin, uj);
     st.nonconst = nc; st.best_gain = bg; st.best_feat = bf; st.best_bin = bbin;
-    if (uj >= 0) st.best_pos = st.pos + uj;
+    if (uj >= 0) { st.best_pos = st.pos + uj; st.best_mid = rmid[uj]; }
     st.pos += g;
     need_more = (st.nonconst < s.max_features && st.pos < c.d) ? 1 : 0;
   }
@@ -1633,6 +1722,7 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   if (st.best_feat >= 0 && accept_split(c, s, st.on.node, st.on.tree, best_left))
     base = make_children(c, st.on.node, st.best_feat, st.best_bin, best_left);
   if (base < 0) return;
+  mono_children(c, st.on.node, base, mono_of(c, s, st.best_feat), st.best_mid);
   st.split = 1;
   st.nl = (int)best_left[c.CH - 1];
   const int set_next = 1 - set_cur;
@@ -1813,6 +1903,14 @@ __global__ __launch_bounds__(256) void k_fill_active(Ctx c) {
 
 __global__ void k_init_counters(Ctx c) { c.counters[kPool] = c.T; }
 
+// monotonic_cst: clip every node's value to its bounds once the trees are grown (the host
+// builder clips every node of a build that has a constraint table, forest_cpu.cpp)
+__global__ void k_mono_clip(Ctx c, int64_t P) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  mono_clip(c.node_val + i * c.VC, c.is_reg, c.nbound[2 * i], c.nbound[2 * i + 1]);
+}
+
 __global__ void k_roots(Ctx c) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= c.T) return;
@@ -1927,6 +2025,8 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.lcursor = (int32_t*)(ws + L.lcursor);
   c.bscr = ws + L.bscr;
   c.rsum = (unsigned long long*)(ws + L.rsum);
+  c.mono = (const int8_t*)a->mono;
+  c.nbound = a->mono ? (double*)a->nbound : nullptr;
   c.rq = reg_scale((int)a->yq_e1, (int)a->yq_e2);
   c.XbT = (const uint8_t*)a->XbT;
   c.cw = (const double*)a->cw;
@@ -2098,7 +2198,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   const int CH = c.CH;
   const size_t lds_hl = (size_t)a->kg_large * hist_planes(MODE, CH) * 256 * mode_elem(MODE);
   const size_t lds_sl = (size_t)a->kg_large * ghist_feat_bytes(MODE, CH) + a->kg_large * 16 + 16 +
-                        (size_t)a->kg_large * CH * 8 + 64;
+                        (size_t)a->kg_large * CH * 8 + (size_t)a->kg_large * 8 + 64;
   const size_t lds_max = 160 * 1024;
   if (lds_w > lds_max || lds_b > lds_max || lds_sl > lds_max || lds_s > lds_max) return 7;
   if (a->sub_max > 64) return 9;
@@ -2174,6 +2274,11 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   HIP_OK(hipMemcpyAsync(h, c.counters, kNumCounters * 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
   a->n_nodes_out = h[kPool];
+  if (c.mono && c.nbound && h[kPool] > 0) {
+    const int64_t P = std::min<int64_t>(h[kPool], a->pool_cap);
+    k_mono_clip<<<(unsigned)((P + 255) / 256), 256, 0, st>>>(c, P);
+    HIP_OK(hipGetLastError());
+  }
   a->levels_out = levels;
   a->large_rounds_out = large_rounds;
   if (a->status_out != 4) a->status_out = h[kOverflow] ? 1 : (h[kOpenOvf] ? 4 : 0);

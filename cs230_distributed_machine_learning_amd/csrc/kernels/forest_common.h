@@ -336,6 +336,47 @@ DML_HD double accept_improvement(const TreeSpec& s, bool is_reg, const double* p
   return improvement(Wt, wN, impN, wL, impL, wR, impR);
 }
 
+// ---- monotonic_cst (sklearn >= 1.4) --------------------------------------------------
+// A split on a constrained feature (m = +1 increasing, -1 decreasing; binary classifiers
+// constrain the class-0 fraction, so their rows arrive negated) must keep both children's
+// values inside the node's [lo, hi] and ordered; the children's bounds meet at the mean of
+// the two values (sklearn's middle_value), and every node value is clipped to its bounds
+// once the tree is grown.  Shared by the host builder and every HIP tier.
+DML_HD double side_value(double w, double a) { return w > 0.0 ? a / w : 0.0; }
+
+DML_HD bool mono_ok(int m, double lo, double hi, double vl, double vr) {
+  return vl >= lo && vr >= lo && vl <= hi && vr <= hi && (vl - vr) * m <= 0.0;
+}
+
+// the children's bound: mean of the two side values, from (left weight, left value sum,
+// right weight, right value sum)
+DML_HD double mono_mid(double lw, double la, double rw, double ra) { return la / (2.0 * lw) + ra / (2.0 * rw); }
+
+// a child's [lo, hi] from the parent's and the split's middle value
+DML_HD void mono_child_bounds(int m, double lo, double hi, double mid, int side, double& clo, double& chi) {
+  if (side == 0) { clo = m < 0 ? mid : lo; chi = m > 0 ? mid : hi; }
+  else { clo = m > 0 ? mid : lo; chi = m < 0 ? mid : hi; }
+}
+
+// clip a grown node's value to its bounds (regression: the mean moves, the squared-error
+// impurity stays; binary: the class-0 fraction is clipped, class 1 takes the rest)
+DML_HD void mono_clip(double* v, int is_reg, double lo, double hi) {
+  if (is_reg) {
+    if (v[0] <= 0.0) return;
+    const double m = v[1] / v[0];
+    const double c = m < lo ? lo : (m > hi ? hi : m);
+    v[2] += v[0] * (c * c - m * m);
+    v[1] = v[0] * c;
+  } else {
+    const double W = v[0] + v[1];
+    if (W <= 0.0) return;
+    const double f = v[0] / W;
+    const double c = f < lo ? lo : (f > hi ? hi : f);
+    v[0] = W * c;
+    v[1] = W * (1.0 - c);
+  }
+}
+
 // leaf-by-counts rule (before any split search)
 DML_HD bool leaf_by_counts(const TreeSpec& t, int count, int depth) {
   return depth >= t.max_depth || count < t.min_samples_split || count < 2 * t.min_samples_leaf;

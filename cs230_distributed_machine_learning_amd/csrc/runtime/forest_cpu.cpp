@@ -158,11 +158,7 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
   // values ordered and inside the node's bounds; the children's bounds meet at the mean of
   // the two values (sklearn's middle_value rounding); every node value is clipped to its bounds once the tree is grown
   const int8_t* mono = D.mono ? D.mono + (int64_t)s.fit * D.d : nullptr;
-  std::vector<double> nlo(1, -INFINITY), nhi(1, INFINITY);
-  auto side_value = [&](double w, double a) { return w > 0.0 ? a / w : 0.0; };
-  auto mono_ok = [&](int m, double lo, double hi, double vl, double vr) {
-    return vl >= lo && vr >= lo && vl <= hi && vr <= hi && (vl - vr) * m <= 0.0;
-  };
+  std::vector<double> nlo(1, -INFINITY), nhi(1, INFINITY);   // (helpers: forest_common.h)
   auto node_imp = [&](int node, const double* v) { return mae ? nabs[node] / v[0] : impurity_of(v); };
   auto visit = [&](int count, int depth, const double* v, double imp) {
     return !(leaf_by_counts(s, count, depth) || leaf_by_weight(s, vals_weight(v, D.C, D.is_reg)) || imp <= kEps);
@@ -261,7 +257,7 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
           const double g = cls_proxy(L, R, s.criterion);
           if (g > g_best) {
             g_best = g; b_best = b;
-            if (g > best_gain) best_mid = l0 / (2.0 * L.w) + (t0c - l0) / (2.0 * R.w);
+            if (g > best_gain) best_mid = mono_mid(L.w, l0, R.w, t0c - l0);
           }
         }
         if (nc) {
@@ -294,7 +290,7 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
           const double g = reg_proxy(s.criterion, l0, l1, t0 - l0, t1 - l1);
           if (g > g_best) {
             g_best = g; b_best = b;
-            if (g > best_gain) best_mid = l1 / (2.0 * l0) + (t1 - l1) / (2.0 * (t0 - l0));
+            if (g > best_gain) best_mid = mono_mid(l0, l1, t0 - l0, t1 - l1);
           }
         }
         if (nc) {
@@ -354,8 +350,9 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     memcpy(nrw + li, tw, (size_t)ri * 4);
     (void)nl;
     const int mc = mono ? mono[best_feat] : 0;
-    const double llo = mc < 0 ? best_mid : jb.lo, lhi = mc > 0 ? best_mid : jb.hi;
-    const double rlo = mc > 0 ? best_mid : jb.lo, rhi = mc < 0 ? best_mid : jb.hi;
+    double llo, lhi, rlo, rhi;
+    mono_child_bounds(mc, jb.lo, jb.hi, best_mid, 0, llo, lhi);
+    mono_child_bounds(mc, jb.lo, jb.hi, best_mid, 1, rlo, rhi);
     nlo.resize(base + 2); nhi.resize(base + 2);
     nlo[base] = llo; nhi[base] = lhi; nlo[base + 1] = rlo; nhi[base + 1] = rhi;
     if (mae) {
@@ -371,22 +368,8 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     if (visit(li, jb.depth + 1, lvv, node_imp(base, lvv)))
       stack.push_back({base, jb.start, li, jb.depth + 1, child_key(jb.key, 0), llo, lhi});
   }
-  if (mono) {   // clip every node's value to its bounds (sklearn clip_node_value)
-    for (size_t i = 0; i < out.nodes.size(); ++i) {
-      double* v = out.vals.data() + i * D.VC;
-      if (D.is_reg) {   // the mean moves, the squared-error impurity stays
-        if (v[0] <= 0.0) continue;
-        const double m = v[1] / v[0], c = std::min(std::max(m, nlo[i]), nhi[i]);
-        v[2] += v[0] * (c * c - m * m);
-        v[1] = v[0] * c;
-      } else {          // binary: the class-0 fraction is clipped, class 1 takes the rest
-        const double W = v[0] + v[1];
-        if (W <= 0.0) continue;
-        const double c = std::min(std::max(v[0] / W, nlo[i]), nhi[i]);
-        v[0] = W * c; v[1] = W * (1.0 - c);
-      }
-    }
-  }
+  if (mono)   // clip every node's value to its bounds (sklearn clip_node_value)
+    for (size_t i = 0; i < out.nodes.size(); ++i) mono_clip(out.vals.data() + i * D.VC, D.is_reg, nlo[i], nhi[i]);
 }
 
 }  // namespace dml

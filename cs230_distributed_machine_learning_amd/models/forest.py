@@ -19,8 +19,9 @@ the per-class sums inside the builder exactly where sklearn's sample weights wou
 ccp_alpha > 0 prunes every grown tree to its minimal cost-complexity subtree
 (ops/forest_ops.py prune_ccp); min_weight_fraction_leaf bounds every side's weight
 (bootstrap counts x class weights, as sklearn's sample weights) inside the builders;
-monotonic_cst (regression and binary classification, sklearn's bounds and clipping) and
-criterion="absolute_error" grow on the C++ host builder.
+monotonic_cst (regression and binary classification, sklearn's bounds and clipping) grows
+on the HIP builder in every tier (per-node bounds, identical to the host builder's trees);
+criterion="absolute_error" grows on the C++ host builder.
 """
 from __future__ import annotations
 
@@ -284,8 +285,7 @@ class ForestFamily(Family):
                 if t.params.get("monotonic_cst") is not None:
                     t.params["monotonic_cst"] = None
                     t.params.setdefault("warnings", []).append("monotonic_cst under a row shard: ignored")
-        # absolute_error and monotonic_cst trees grow on the host builder (forest_cpu.cpp):
-        # batch them apart
+        # absolute_error trees grow on the host builder (forest_cpu.cpp): batch them apart
         tasks_in = tasks
         tasks = sorted(tasks, key=_host_only)
         budget = self._budget(data)
@@ -420,15 +420,9 @@ class ForestFamily(Family):
                                     data.n_classes, is_reg, data.r0, reduce=data.all_reduce, cw=cw, comm=data,
                                     tree_chunk=tree_chunk)
         elif _host_only(batch[0]):
-            # exact absolute_error (per-node weighted medians) and monotonic_cst (bounded
-            # node values) grow on the host builder; the pruning / refine / predict steps
-            # below run where the data lives
-            mono = None
-            if any(t.params.get("monotonic_cst") is not None for t in batch):
-                mono = np.zeros((len(batch), Xb.shape[1]), dtype=np.int8)
-                for f, t in enumerate(batch):
-                    if t.params.get("monotonic_cst") is not None:   # classifiers: class-0 fraction
-                        mono[f] = np.asarray(t.params["monotonic_cst"], dtype=np.int8) * (1 if is_reg else -1)
+            # exact absolute_error (per-node weighted medians) grows on the host builder;
+            # the pruning / refine / predict steps below run where the data lives
+            mono = _mono_table(batch, Xb.shape[1], is_reg)
             ycls = None if is_reg else np.asarray(data.y_enc, dtype=np.int32)
             fb = forest_ops.build_cpu(Xb.cpu().numpy(), ycls, None if not is_reg else data.y_reg.cpu().numpy(),
                                       data.roles_np(), specs, data.n_classes, is_reg, cw=cw, mono=mono)
@@ -436,12 +430,15 @@ class ForestFamily(Family):
                 fb.nodes = torch.from_numpy(fb.nodes).to(data.device)
                 fb.vals = torch.from_numpy(fb.vals).to(data.device)
         elif data.is_gpu:
+            # monotonic_cst grows on the HIP builder too (per-node bounds in every tier)
             fb = forest_ops.build_gpu(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
                                       data.n_classes, is_reg, self.tiers, reuse_pool=True,
-                                      XbT=data.binned_feature_major(), cw=cw)
+                                      XbT=data.binned_feature_major(), cw=cw,
+                                      mono=_mono_table(batch, Xb.shape[1], is_reg))
         else:
             fb = forest_ops.build_cpu(Xb.numpy(), data.y_enc, None if not is_reg else data.y_reg.numpy(),
-                                      data.roles_np(), specs, data.n_classes, is_reg, cw=cw)
+                                      data.roles_np(), specs, data.n_classes, is_reg, cw=cw,
+                                      mono=_mono_table(batch, Xb.shape[1], is_reg))
         try:
             if any(t.params.get("max_leaf_nodes") for t in batch):
                 with trace.range("forest_prune"):
@@ -496,7 +493,20 @@ class ForestFamily(Family):
 
 
 def _host_only(t: FitTask) -> bool:
-    return t.params.get("criterion") == forest_ops.MAE or t.params.get("monotonic_cst") is not None
+    """absolute_error trees grow on the host builder (per-node weighted medians)."""
+    return t.params.get("criterion") == forest_ops.MAE
+
+
+def _mono_table(batch, d: int, is_reg: bool):
+    """int8 [fits][d] monotonic_cst rows of a batch (None: no fit is constrained);
+    classifier rows constrain the class-0 fraction, so they are negated."""
+    if not any(t.params.get("monotonic_cst") is not None for t in batch):
+        return None
+    mono = np.zeros((len(batch), d), dtype=np.int8)
+    for f, t in enumerate(batch):
+        if t.params.get("monotonic_cst") is not None:
+            mono[f] = np.asarray(t.params["monotonic_cst"], dtype=np.int8) * (1 if is_reg else -1)
+    return mono
 
 
 def _refine(data, fb, Xb, specs, roles) -> None:

@@ -241,7 +241,7 @@ def reg_exponents_of(max_abs_y: float, n: int) -> tuple[int, int]:
 def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,
               specs: np.ndarray, n_classes: int, is_reg: bool, tiers: ForestTiers | None = None,
               ystride: int = 0, reuse_pool: bool = False, XbT: Optional[torch.Tensor] = None,
-              cw: Optional[np.ndarray] = None) -> ForestBuild:
+              cw: Optional[np.ndarray] = None, mono: Optional[np.ndarray] = None) -> ForestBuild:
     """``ystride > 0``: ``yreg`` is a [targets, ystride] matrix and tree t regresses on
     row ``specs[t]['target']`` (gradient boosting's per-fit pseudo-residuals).
     ``reuse_pool``: the node arrays live in the device arena and are valid until the
@@ -273,6 +273,13 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     if cw is not None and not is_reg:
         cw_dev = torch.from_numpy(np.ascontiguousarray(cw, dtype=np.float64).reshape(T, n_classes)).to(dev)
     a.cw = native.ptr(cw_dev) if cw_dev is not None else 0
+    # monotonic_cst: int8 [fits][d] rows indexed by the specs' "fit" (classifier rows
+    # constrain the class-0 fraction, i.e. arrive negated) + per-node bounds
+    mono_dev = None
+    if mono is not None and np.any(mono):
+        mono_dev = torch.from_numpy(np.ascontiguousarray(mono, dtype=np.int8)).to(dev)
+    a.mono = native.ptr(mono_dev) if mono_dev is not None else 0
+    a.nbound = 0
     a.active_count = native.ptr(active)
     t0 = time.perf_counter()
     with trace.range("forest_count"):
@@ -329,6 +336,11 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
                     vals = torch.empty((pool_cap, VC), dtype=torch.float64, device=dev)
             a.workspace, a.workspace_bytes = native.ptr(workspace), ws_bytes
             a.nodes, a.node_val, a.pool_cap = native.ptr(nodes), native.ptr(vals), pool_cap
+            if mono_dev is not None:   # every pool slot starts unbounded
+                nbound = torch.empty((pool_cap, 2), dtype=torch.float64, device=dev)
+                nbound[:, 0] = -math.inf
+                nbound[:, 1] = math.inf
+                a.nbound = native.ptr(nbound)
             a.status_out = 0
             with trace.range("forest_build"):   # host-side launch sequence of every tier
                 rc = lib.dml_forest_build(ctypes.byref(a), stream)

@@ -339,9 +339,48 @@ def test_gpu_absolute_error_family_matches_host_path():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("tiers", range(len(TIERS)))
+@pytest.mark.parametrize("is_reg", [False, True])
+def test_gpu_monotonic_cst_trees_match_cpu(is_reg, tiers):
+    """monotonic_cst on the HIP builder: the constrained-split rejection, the children's
+    middle-value bounds and the final clip in every tier (subtree / wave / block / large)
+    give the host builder's trees node for node (regression and binary classification)."""
+    rng = np.random.RandomState(7)
+    n, d = 12000, 8
+    X = rng.randn(n, d).astype(np.float32)
+    if is_reg:
+        y = (2 * X[:, 0] - X[:, 1] + np.sin(3 * X[:, 2]) + 0.5 * rng.randn(n)).astype(np.float32)
+    else:
+        y = (X[:, 0] - 0.7 * X[:, 1] + rng.randn(n) > 0).astype(np.int32)
+    dev = torch.device("cuda:0")
+    Xb = binning.bin_matrix(torch.from_numpy(X).to(dev), binning.quantile_edges(torch.from_numpy(X).to(dev)))
+    Xb_cpu = Xb.cpu().numpy()
+    roles, _ = make_split_roles(y, 3, not is_reg, holdout=False)
+    specs = _specs(3, 5, d, k=4, criterion=2 if is_reg else 0, msl=2)
+    T = len(specs)
+    # fit 0: +1 / -1 constraints; fit 1: unconstrained row of a constrained build; fit 2: +1 only
+    mono = np.zeros((3, d), dtype=np.int8)
+    mono[0, :2] = (1, -1)
+    mono[2, 0] = 1
+    if not is_reg:
+        mono = -mono   # classifiers constrain the class-0 fraction (models/forest.py _mono_table)
+    tier = forest_ops.ForestTiers(**TIERS[tiers])
+    if is_reg:
+        g = forest_ops.build_gpu(Xb, None, torch.from_numpy(y).to(dev), torch.from_numpy(roles).to(dev), specs, 1,
+                                 True, tier, mono=mono)
+        c = forest_ops.build_cpu(Xb_cpu, None, y, roles, specs, 1, True, mono=mono)
+    else:
+        g = forest_ops.build_gpu(Xb, torch.from_numpy(y).to(dev), None, torch.from_numpy(roles).to(dev), specs, 2,
+                                 False, tier, mono=mono)
+        c = forest_ops.build_cpu(Xb_cpu, y, None, roles, specs, 2, False, mono=mono)
+    gc = _canon(g.nodes.cpu().numpy(), g.vals.cpu().numpy(), T)
+    cc = _canon(c.nodes, c.vals, T)
+    assert gc == cc
+
+
 def test_gpu_monotonic_cst_family_matches_host_path():
-    """monotonic_cst candidates on device-resident data grow on the host builder and are
-    predicted / scored by the HIP kernels: the CV scores of the all-host path."""
+    """monotonic_cst candidates on device-resident data grow on the HIP builder and score
+    exactly what the all-host path scores."""
     from cs230_distributed_machine_learning_amd.data.device import DeviceData
     from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
 
