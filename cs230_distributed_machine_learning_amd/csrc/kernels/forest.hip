@@ -52,6 +52,9 @@
 #ifndef DML_KGMAX_WAVE
 #define DML_KGMAX_WAVE 4
 #endif
+#ifndef DML_GINI_PF
+#define DML_GINI_PF 1          // binary Gini: fp32 pre-filter of candidate bins (eval_feature)
+#endif
 #ifndef DML_WAVE_PREFETCH
 #define DML_WAVE_PREFETCH 12   // wave tier: visiting positions whose bins are gathered up front
 #endif
@@ -91,6 +94,9 @@ struct OpenNode {
   int64_t start;
   int32_t count, depth;
   uint64_t key;
+  int32_t pool_base;   // subtree tier: first pool slot of the subtree's reserved pairs (-1: k_subtree
+                       // reserves them itself, -2: pool overflow already flagged)
+  int32_t tier;        // child staging slot: the child's tier, -1 = no open child
 };
 
 // ctypes-facing argument block: every field is 8 bytes (pointers as int64).
@@ -153,6 +159,11 @@ struct Ctx {
   double* tree_W;
   OpenNode* open[2][kTiers];
   int64_t open_cap[kTiers];
+  // child staging: the wave/block-tier parent at level position i writes its two children to
+  // stage[2 i + side] (no atomics); k_compact buckets them into the next level's open lists
+  // with one atomic per workgroup and tier -- a per-child returning atomic on one counter
+  // address per tier serialised ~60 M times per bench build (+0.56 s for one extra per child)
+  OpenNode* stage;
   int32_t* counters;
   int32_t* cursors;      // [T]
   LState* lstate;
@@ -271,8 +282,17 @@ __device__ void enqueue_or_leaf(const Ctx& c, int tree, int node, int64_t start,
   }
   OpenNode on;
   on.tree = tree; on.node = node; on.start = start; on.count = count; on.depth = depth;
-  on.key = key;
+  on.key = key; on.pool_base = -1; on.tier = tier;
   c.open[set][tier][idx] = on;
+}
+
+// node pairs a subtree-tier node reserves: a subtree over cnt0 rows has at most
+// cnt0 / min_samples_leaf - 1 splits, and at most 2^levels_left - 1 under max_depth
+__device__ __forceinline__ int subtree_max_splits(const TreeSpec& s, int cnt0, int depth) {
+  int max_splits = cnt0 / max(1, s.min_samples_leaf) - 1;
+  const int levels_left = s.max_depth - depth;
+  if (levels_left < 30) max_splits = min(max_splits, (1 << max(0, levels_left)) - 1);
+  return max(0, max_splits);
 }
 
 // allocate two children, write parent record and children stats. returns left index or -1.
@@ -413,6 +433,58 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
     double tot_rows;
     if constexpr (MODE == 1) tot_rows = (double)((uint64_t)tot[0] >> 42);
     else tot_rows = reg_rows(tot[0]);
+    // binary Gini: fp32 pre-filter.  Every candidate bin is scored in fp32 (relative error
+    // < 2^-19: all terms are sums and products of non-negative values), and only the bins
+    // within 2^-14 of the wave's fp32 maximum -- a set that provably holds every bin whose
+    // fp64 score equals the fp64 maximum -- are re-scored in fp64 with the exact formula of
+    // the generic path below.  The split chosen is therefore the one the full fp64 sweep
+    // (and the host builder) chooses, at ~1 fp64 score per lane instead of 4.
+    bool pf = false;
+    if constexpr (MODE == 1 && DML_GINI_PF)
+      pf = s.criterion == kGini && mq.m == 0 && cw0 >= 0x1p-20 && cw0 <= 0x1p20 && cw1 >= 0x1p-20 && cw1 <= 0x1p20;
+    if (MODE == 1 && pf) {
+      const uint64_t tv = (uint64_t)tot[0];
+      const uint32_t trows = (uint32_t)(tv >> 42), t0i = (uint32_t)(tv & kPackMask21),
+                     t1i = (uint32_t)((tv >> 21) & kPackMask21);
+      const uint32_t mslu = (uint32_t)s.min_samples_leaf;
+      const float cw0f = (float)cw0, cw1f = (float)cw1;
+      const double t0 = (double)t0i * cw0, t1 = (double)t1i * cw1;
+      const bool mwl = s.min_weight_leaf > 0.0;
+      float q[4];
+      float qmax = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint64_t cv = (uint64_t)v[0][i];
+        const uint32_t rl = (uint32_t)(cv >> 42), rr = trows - rl;
+        const uint32_t l0i = (uint32_t)(cv & kPackMask21), l1i = (uint32_t)((cv >> 21) & kPackMask21);
+        nc |= (rl > 0u && rr > 0u);
+        bool ok = (lane * 4 + i) != 255 && rl >= mslu && rr >= mslu;
+        if (mwl) {   // the generic path's side weights, same doubles
+          const double l0 = (double)l0i * cw0, l1 = (double)l1i * cw1;
+          ok = ok && !side_too_light(s, l0 + l1, (t0 - l0) + (t1 - l1));
+        }
+        const float a0 = (float)l0i * cw0f, a1 = (float)l1i * cw1f;
+        const float r0 = (float)(t0i - l0i) * cw0f, r1 = (float)(t1i - l1i) * cw1f;
+        const float wl = a0 + a1, wr = r0 + r1;
+        const float num = (a0 * a0 + a1 * a1) * wr + (r0 * r0 + r1 * r1) * wl;
+        q[i] = ok ? num * __builtin_amdgcn_rcpf(wl * wr) : -INFINITY;
+        qmax = fmaxf(qmax, q[i]);
+      }
+      qmax = wave::max_f32(qmax, lane);
+      const float thr = qmax - qmax * 0x1p-14f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (!(q[i] >= thr) || q[i] == -INFINITY) continue;
+        const uint64_t cv = (uint64_t)v[0][i];
+        const double l0 = (double)(cv & kPackMask21) * cw0, l1 = (double)((cv >> 21) & kPackMask21) * cw1;
+        ClsAcc L, R;
+        L.init(s.criterion); R.init(s.criterion);
+        L.add(l0); L.add(l1);
+        R.add(t0 - l0); R.add(t1 - l1);
+        const double g = cls_proxy(L, R, s.criterion);
+        if (g > best) { best = g; bb = lane * 4 + i; }
+      }
+    } else
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int b = lane * 4 + i;
@@ -449,7 +521,18 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
       }
       if (g > best) { best = g; bb = b; bmid = mid; }
     }
-    wave::argmax(best, bb, lane);
+    {
+      // one lane holding a candidate (the usual outcome of the fp32 pre-filter): its pair
+      // is the wave's argmax, no reduction needed
+      const uint64_t cm = __ballot(bb >= 0);
+      if (__popcll(cm) == 1) {
+        const int src = (int)__builtin_ctzll(cm);
+        best = wave::bcast<double>(best, src);
+        bb = wave::bcast<int>(bb, src);
+      } else {
+        wave::argmax(best, bb, lane);
+      }
+    }
     const bool any_nc = __ballot(nc) != 0ull;
     // the winning bin's cumulative channels, broadcast from its owner lane
     const int src = bb >= 0 ? (bb >> 2) : 0, sel = bb >= 0 ? (bb & 3) : 0;
@@ -684,21 +767,17 @@ __device__ double impurity_of_vals(const Ctx& c, const double* v, int crit) {
   return cls_impurity(a, crit);
 }
 
-__device__ void enqueue_or_leaf_v(const Ctx& c, const TreeSpec& s, int tree, int node, int64_t start, int count,
-                                  int depth, uint64_t key, int set, const double* vals) {
-  if (leaf_by_counts(s, count, depth)) return;
-  if (leaf_by_weight(s, vals_weight(vals, c.C, c.is_reg))) return;
-  if (impurity_of_vals(c, vals, s.criterion) <= kEps) return;
-  const int tier = count <= c.sub_max ? 0 : (count <= c.wave_max ? 1 : (count <= c.block_max ? 2 : 3));
-  const int idx = atomicAdd(&c.counters[set * kTiers + tier], 1);
-  if (idx >= c.open_cap[tier]) {
-    atomicOr(&c.counters[kOpenOvf], 1);
-    return;
-  }
+// a wave/block-tier child into its staging slot (k_compact enqueues it): tier -1 = leaf
+__device__ void stage_child(const Ctx& c, const TreeSpec& s, int tree, int node, int64_t start, int count, int depth,
+                            uint64_t key, int64_t slot, const double* vals) {
+  int tier = -1;
+  if (!leaf_by_counts(s, count, depth) && !leaf_by_weight(s, vals_weight(vals, c.C, c.is_reg)) &&
+      impurity_of_vals(c, vals, s.criterion) > kEps)
+    tier = count <= c.sub_max ? 0 : (count <= c.wave_max ? 1 : (count <= c.block_max ? 2 : 3));
   OpenNode on;
   on.tree = tree; on.node = node; on.start = start; on.count = count; on.depth = depth;
-  on.key = key;
-  c.open[set][tier][idx] = on;
+  on.key = key; on.pool_base = -1; on.tier = tier;
+  c.stage[slot] = on;
 }
 
 // histogram payload of one row (PLT above)
@@ -740,7 +819,7 @@ __device__ __forceinline__ void hist_add(typename HT<MODE>::T* hj, const Ctx& c,
 
 template <int NT, int MODE>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WPE, 8))) void k_nodes(Ctx c, int tier, int set_cur,
-                                                                                                   int pair_base) {
+                                                                                                   int pair_base, int stage_base) {
   using CT = typename HT<MODE>::T;
   constexpr int NW = NT / 64;
   constexpr int RPT = NT == 64 ? 4 : DML_RPT_BLOCK;   // rows per thread in registers (<= 4: packed u8 x 4)
@@ -1027,6 +1106,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     c.nodes[base + 1] = leaf;
     if (!(sc->best_feat >= 0 && accept_split_v(c, s, pvs, sc->W, best_left))) {
       base = -1;   // the reserved pair stays as two unreferenced leaves
+      c.stage[2 * (stage_base + (int64_t)blockIdx.x)].tier = -1;
+      c.stage[2 * (stage_base + (int64_t)blockIdx.x) + 1].tier = -1;
     } else {
       {
         double* lv = c.node_val + (int64_t)base * c.VC;
@@ -1050,10 +1131,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   const int feat = sc->best_feat, bin = sc->best_bin, nl = sc->nl;
   constexpr int RT = NT > 64 ? 64 : 1;   // the right child is enqueued by another wave / lane
   if (tid == 0)
-    enqueue_or_leaf_v(c, s, on.tree, base, on.start, nl, on.depth + 1, child_key(on.key, 0), 1 - set_cur, best_left);
+    stage_child(c, s, on.tree, base, on.start, nl, on.depth + 1, child_key(on.key, 0),
+                2 * (stage_base + (int64_t)blockIdx.x), best_left);
   if (tid == RT)
-    enqueue_or_leaf_v(c, s, on.tree, base + 1, on.start + nl, cnt - nl, on.depth + 1, child_key(on.key, 1),
-                      1 - set_cur, rvs);
+    stage_child(c, s, on.tree, base + 1, on.start + nl, cnt - nl, on.depth + 1, child_key(on.key, 1),
+                2 * (stage_base + (int64_t)blockIdx.x) + 1, rvs);
   // ---- stable partition: RPT ballot rounds per chunk, one block-level offset exchange
 #ifdef DML_X2_PART   // sensitivity build: the (idempotent) partition pass runs twice
   for (int rep_ = 0; rep_ < 2; ++rep_) {
@@ -1405,21 +1487,21 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
       for (int j = 0; j < d; ++j) xc[lane * dp + j] = xg[j];
     }
   }
-  // a subtree over cnt0 rows has at most cnt0 - 1 splits: reserve all node pairs with ONE
-  // pool atomic (unused pairs stay unreferenced)
-  int pool_base = 0;
-  int max_splits = cnt0 / max(1, s.min_samples_leaf) - 1;       // leaves <= rows / min_samples_leaf
-  {
-    const int levels_left = s.max_depth - on.depth;
-    if (levels_left < 30) max_splits = min(max_splits, (1 << max(0, levels_left)) - 1);
-    max_splits = max(0, max_splits);
-  }
+  // a subtree over cnt0 rows has at most cnt0 - 1 splits: all its node pairs are reserved at
+  // once -- by k_compact for staged nodes (on.pool_base), else with ONE pool atomic here
+  // (unused pairs stay unreferenced)
+  int pool_base = on.pool_base;
+  const int max_splits = subtree_max_splits(s, cnt0, on.depth);
   if (lane == 0) {
     const int want = 2 * max_splits;
-    pool_base = want > 0 ? atomicAdd(&c.counters[kPool], want) : 0;
-    if (want > 0 && (int64_t)pool_base + want > c.pool_cap) {
-      atomicOr(&c.counters[kOverflow], 1);
-      pool_base = -1;
+    if (pool_base == -1) {
+      pool_base = want > 0 ? atomicAdd(&c.counters[kPool], want) : 0;
+      if (want > 0 && (int64_t)pool_base + want > c.pool_cap) {
+        atomicOr(&c.counters[kOverflow], 1);
+        pool_base = -1;
+      }
+    } else if (pool_base < 0) {
+      pool_base = -1;   // k_compact flagged the overflow
     }
     SubEntry e;
     e.mask = cnt0 >= 64 ? ~0ull : ((1ull << cnt0) - 1ull);
@@ -1903,6 +1985,81 @@ __global__ __launch_bounds__(256) void k_fill_active(Ctx c) {
 
 __global__ void k_init_counters(Ctx c) { c.counters[kPool] = c.T; }
 
+// Buckets one level's staged wave/block-tier children into the next level's open lists.
+// 1024 staging slots per workgroup; each tier's positions come from wave scans and ONE atomic
+// per tier per workgroup, and the subtree tier's node pairs (subtree_max_splits) are reserved
+// here the same way (one pool atomic per workgroup) and handed over in OpenNode::pool_base.
+// Open-list order within a workgroup follows the staging order; across workgroups it is the
+// atomics' order (node numbering was never order-independent; tree shapes are).
+__global__ __launch_bounds__(256) void k_compact(Ctx c, int set, int64_t n) {
+  constexpr int NQ = kTiers + 1;   // per-tier entries + subtree pool slots
+  __shared__ int wtot[4][NQ];
+  __shared__ int gbase[NQ];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t i0 = (int64_t)blockIdx.x * 1024 + tid * 4;
+  OpenNode e[4];
+  int want[4];
+  int cnt[NQ] = {0, 0, 0, 0, 0};
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    want[u] = 0;
+    e[u].tier = -1;
+    if (i0 + u < n) e[u] = c.stage[i0 + u];
+    const int t = e[u].tier;
+    if (t < 0) continue;
+    ++cnt[t];
+    if (t == 0) {
+      want[u] = 2 * subtree_max_splits(c.specs[e[u].tree], e[u].count, e[u].depth);
+      cnt[kTiers] += want[u];
+    }
+  }
+  int off[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int inc = wave::incl_scan<int>(cnt[q]);
+    off[q] = inc - cnt[q];
+    if (lane == 63) wtot[wid][q] = inc;
+  }
+  __syncthreads();
+  if (tid < NQ) {
+    int tot = 0;
+    for (int w = 0; w < 4; ++w) {
+      const int v = wtot[w][tid];
+      wtot[w][tid] = tot;
+      tot += v;
+    }
+    int* ctr = tid < kTiers ? &c.counters[set * kTiers + tid] : &c.counters[kPool];
+    gbase[tid] = tot ? atomicAdd(ctr, tot) : 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) off[q] += gbase[q] + wtot[wid][q];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = e[u].tier;
+    if (t < 0) continue;
+    int idx = 0;
+#pragma unroll
+    for (int q = 0; q < kTiers; ++q)
+      if (q == t) idx = off[q]++;
+    if (t == 0) {
+      const int pb = off[kTiers];
+      off[kTiers] += want[u];
+      if (want[u] > 0 && (int64_t)pb + want[u] > c.pool_cap) {
+        atomicOr(&c.counters[kOverflow], 1);
+        e[u].pool_base = -2;
+      } else {
+        e[u].pool_base = pb;
+      }
+    }
+    if (idx >= c.open_cap[t]) {
+      atomicOr(&c.counters[kOpenOvf], 1);
+      continue;
+    }
+    c.open[set][t][idx] = e[u];
+  }
+}
+
 // monotonic_cst: clip every node's value to its bounds once the trees are grown (the host
 // builder clips every node of a build that has a constraint table, forest_cpu.cpp)
 __global__ void k_mono_clip(Ctx c, int64_t P) {
@@ -1943,7 +2100,8 @@ __global__ void k_roots(Ctx c) {
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct Layout {
-  size_t rows_b, open[2][kTiers], counters, cursors, lstate, lperm, lbest, ghist, lcursor, bscr, rsum, total;
+  size_t rows_b, open[2][kTiers], stage, counters, cursors, lstate, lperm, lbest, ghist, lcursor, bscr, rsum, total;
+  int64_t stage_cap;
   int64_t open_cap[kTiers], large_cap;
 };
 
@@ -1960,17 +2118,21 @@ static Layout plan(const ForestArgs* a) {
   const int64_t R = a->rows_total, T = a->T;
   const int64_t C = a->is_reg ? 3 : a->n_classes;
   const int64_t CH = a->is_reg ? 4 : a->n_classes + 1;
-  L.open_cap[0] = R / 2 + T + 16;
+  // a level's nodes hold disjoint rows: <= R / (smallest node of the tier) of each tier.
+  // Subtree-tier nodes are roots or children of the previous level's wave/block/large nodes.
   L.open_cap[1] = R / (a->sub_max + 1) + T + 16;
   L.open_cap[2] = R / (a->wave_max + 1) + T + 16;
   L.open_cap[3] = R / (a->block_max + 1) + T + 16;
+  L.open_cap[0] = 2 * (L.open_cap[1] + L.open_cap[2] + L.open_cap[3]) + T + 16;
   L.large_cap = L.open_cap[3];
+  L.stage_cap = 2 * (L.open_cap[1] + L.open_cap[2]);
   (void)C;
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
   L.rows_b = take((size_t)R * 4);
   for (int s = 0; s < 2; ++s)
     for (int t = 0; t < kTiers; ++t) L.open[s][t] = take((size_t)L.open_cap[t] * sizeof(OpenNode));
+  L.stage = take((size_t)L.stage_cap * sizeof(OpenNode));
   L.counters = take(kNumCounters * 4);
   L.cursors = take((size_t)T * 4);
   L.lstate = take((size_t)L.large_cap * sizeof(LState));
@@ -2016,6 +2178,7 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   for (int s = 0; s < 2; ++s)
     for (int t = 0; t < kTiers; ++t) c.open[s][t] = (OpenNode*)(ws + L.open[s][t]);
   for (int t = 0; t < kTiers; ++t) c.open_cap[t] = L.open_cap[t];
+  c.stage = (OpenNode*)(ws + L.stage);
   c.counters = (int32_t*)(ws + L.counters);
   c.cursors = (int32_t*)(ws + L.cursors);
   c.lstate = (LState*)(ws + L.lstate);
@@ -2243,8 +2406,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       s0 = ss->s[0]; s1 = ss->s[1]; s2 = ss->s[2];
     }
     if (ns) k_subtree<REG><<<ns, 64, lds_s, s0>>>(c, cur);
-    if (nw) k_nodes<64, MODE><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w);
-    if (nb) k_nodes<DML_BLOCK_NT, MODE><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b);
+    if (nw) k_nodes<64, MODE><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w, 0);
+    if (nb) k_nodes<DML_BLOCK_NT, MODE><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, nw);
     if (nL) {
       k_large_prep<<<nL, 64, 0, st>>>(c, cur, nL);
       while (true) {
@@ -2266,6 +2429,10 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
         HIP_OK(hipEventRecord(ss->join[i], ss->s[i]));
         HIP_OK(hipStreamWaitEvent(st, ss->join[i], 0));
       }
+    }
+    if (nw + nb) {   // the staged children of the wave/block tiers -> next level's open lists
+      const int64_t nst = 2LL * (nw + nb);
+      k_compact<<<(unsigned)((nst + 1023) / 1024), 256, 0, st>>>(c, 1 - cur, nst);
     }
     HIP_OK(hipGetLastError());
     uint32_t* t = c.rows_cur; c.rows_cur = c.rows_next; c.rows_next = t;

@@ -181,6 +181,13 @@ __device__ __forceinline__ uint64_t min_u64(uint64_t v, int lane) {
   return v;
 }
 
+// float max over the wave (every lane ends with it)
+__device__ __forceinline__ float max_f32(float v, int lane) {
+  v = fmaxf(v, shfl_xor<32>(v, lane)); v = fmaxf(v, shfl_xor<16>(v, lane)); v = fmaxf(v, shfl_xor<8>(v, lane));
+  v = fmaxf(v, shfl_xor<4>(v, lane)); v = fmaxf(v, shfl_xor<2>(v, lane)); v = fmaxf(v, shfl_xor<1>(v, lane));
+  return v;
+}
+
 template <typename T>
 __device__ __forceinline__ T sum(T v, int lane) {
   v += shfl_xor<32>(v, lane); v += shfl_xor<16>(v, lane); v += shfl_xor<8>(v, lane);
