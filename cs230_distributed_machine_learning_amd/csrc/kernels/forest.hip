@@ -125,6 +125,8 @@ struct ForestArgs {
   int64_t yq_e1, yq_e2;  // regression fixed-point exponents (forest_common.h reg_exponents)
   int64_t mono;          // int8 [fits][d] monotonic_cst rows (binary classifiers negated), 0 = none
   int64_t nbound;        // double [pool_cap][2] node bounds (lo, hi) when mono != 0
+  int64_t fast_crit;     // 1 + the single criterion of a build with no class weights, monotonic
+                         // constraints or min_weight_fraction_leaf (node kernels specialised on it); 0 = generic
 };
 
 constexpr int kTiers = 4;  // 0 subtree, 1 wave, 2 block, 3 large
@@ -202,15 +204,28 @@ struct Ctx {
   double* nbound;
 };
 
+// The TreeSpec fields the kernels read, as scalars (a by-value TreeSpec would live in
+// scratch memory: it embeds the Poisson table, which stays behind a pointer here).
+struct NodeSpec {
+  uint64_t seed;
+  const uint32_t* pois_cdf;
+  int32_t split, fit, max_depth, min_samples_split, min_samples_leaf, max_features, bootstrap, criterion, target,
+      cw_mode;
+  float min_impurity_decrease;
+  double min_weight_leaf;
+};
 // the constraint of feature f for the tree's fit (0: unconstrained or no table)
-__device__ __forceinline__ int mono_of(const Ctx& c, const TreeSpec& s, int f) {
+template <int FC = -1>
+__device__ __forceinline__ int mono_of(const Ctx& c, const NodeSpec& s, int f) {
+  if constexpr (FC >= 0) return 0;
   return c.mono ? (int)c.mono[(int64_t)s.fit * c.d + f] : 0;
 }
 
 // children's bounds from the parent's and the chosen split (every child of a build with a
 // constraint table gets bounds, unconstrained splits pass the parent's through)
+template <int FC = -1>
 __device__ __forceinline__ void mono_children(const Ctx& c, int node, int left, int m, double mid) {
-  if (!c.nbound) return;
+  if (FC >= 0 || !c.nbound) return;
   const double lo = c.nbound[2 * (int64_t)node], hi = c.nbound[2 * (int64_t)node + 1];
   for (int side = 0; side < 2; ++side) {
     double clo, chi;
@@ -220,14 +235,30 @@ __device__ __forceinline__ void mono_children(const Ctx& c, int node, int left, 
   }
 }
 
+// Node kernels specialised on one criterion (FC >= 0): the build has no class weights, no
+// monotonic constraints and no min_weight_fraction_leaf, so those branches and every other
+// criterion's scoring (entropy log2 series, Poisson) compile out of the kernel (spec_of here,
+// and tree_cw / mono_of / mono_children / the node-bound reads return their neutral values).
+template <int FC>
+__device__ __forceinline__ NodeSpec spec_of(const Ctx& c, int tree) {
+  const TreeSpec& t = c.specs[tree];
+  NodeSpec s;
+  s.seed = t.seed; s.pois_cdf = t.pois_cdf; s.split = t.split; s.fit = t.fit; s.max_depth = t.max_depth;
+  s.min_samples_split = t.min_samples_split; s.min_samples_leaf = t.min_samples_leaf;
+  s.max_features = t.max_features; s.bootstrap = t.bootstrap; s.criterion = t.criterion; s.target = t.target;
+  s.cw_mode = t.cw_mode; s.min_impurity_decrease = t.min_impurity_decrease; s.min_weight_leaf = t.min_weight_leaf;
+  if constexpr (FC >= 0) { s.criterion = FC; s.min_weight_leaf = 0.0; }
+  return s;
+}
+
 // target vector of a tree (shared y, or its own row of the boosting target matrix)
-__device__ __forceinline__ const float* tree_y(const Ctx& c, const TreeSpec& s) {
+__device__ __forceinline__ const float* tree_y(const Ctx& c, const NodeSpec& s) {
   return c.ystride ? c.yreg + (int64_t)s.target * c.ystride : c.yreg;
 }
 
 __device__ __forceinline__ uint32_t word_row(const Ctx& c, uint32_t wd) { return wd & c.rmask; }
 
-__device__ __forceinline__ uint32_t word_weight(const Ctx& c, const TreeSpec& s, uint32_t wd) {
+__device__ __forceinline__ uint32_t word_weight(const Ctx& c, const NodeSpec& s, uint32_t wd) {
   return c.packed ? (wd >> c.rbits) & 15u : boot_weight(s, wd);
 }
 
@@ -236,7 +267,9 @@ __device__ __forceinline__ int word_cls(const Ctx& c, uint32_t wd) {
 }
 
 // class-weight row of a tree (nullptr: every weight is 1)
+template <int FC = -1>
 __device__ __forceinline__ const double* tree_cw(const Ctx& c, int tree) {
+  if constexpr (FC >= 0) return nullptr;
   return (c.cw && c.specs[tree].cw_mode) ? c.cw + (int64_t)tree * c.C : nullptr;
 }
 __device__ __forceinline__ double cwk(const double* cw, int k) { return cw ? cw[k] : 1.0; }
@@ -270,7 +303,7 @@ __device__ double node_weight(const Ctx& c, int node) {
 // decide whether a freshly created node is worth visiting; enqueue it into `set`
 __device__ void enqueue_or_leaf(const Ctx& c, int tree, int node, int64_t start, int count, int depth,
                                 uint64_t key, int set) {
-  const TreeSpec& s = c.specs[tree];
+  const NodeSpec s = spec_of<-1>(c, tree);
   if (leaf_by_counts(s, count, depth)) return;
   if (leaf_by_weight(s, node_weight(c, node))) return;
   if (node_impurity(c, node, s.criterion) <= kEps) return;
@@ -288,7 +321,8 @@ __device__ void enqueue_or_leaf(const Ctx& c, int tree, int node, int64_t start,
 
 // node pairs a subtree-tier node reserves: a subtree over cnt0 rows has at most
 // cnt0 / min_samples_leaf - 1 splits, and at most 2^levels_left - 1 under max_depth
-__device__ __forceinline__ int subtree_max_splits(const TreeSpec& s, int cnt0, int depth) {
+template <class TS>
+__device__ __forceinline__ int subtree_max_splits(const TS& s, int cnt0, int depth) {
   int max_splits = cnt0 / max(1, s.min_samples_leaf) - 1;
   const int levels_left = s.max_depth - depth;
   if (levels_left < 30) max_splits = min(max_splits, (1 << max(0, levels_left)) - 1);
@@ -382,7 +416,7 @@ struct MonoQ {
 };
 
 template <int MODE>
-__device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
+__device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const NodeSpec& s, int lane,
                                  double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after,
                                  const double* cw, MonoQ mq, double* out_mid);
 
@@ -391,7 +425,7 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
 // arg-maxed without writing the scan back to LDS; the histogram is cleared by the same
 // lanes right after the read.  Multiclass (MODE 0) keeps the LDS path (C+1 planes).
 template <int MODE>
-__device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
+__device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int CH, const NodeSpec& s, int lane,
                              double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after,
                              const double* cw = nullptr, const RegScale* rq = nullptr, MonoQ mq = MonoQ{0, 0.0, 0.0},
                              double* out_mid = nullptr) {
@@ -573,7 +607,7 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
 }
 
 template <int MODE>
-__device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const TreeSpec& s, int lane,
+__device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, int CH, const NodeSpec& s, int lane,
                                  double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after,
                                  const double* cw, MonoQ mq, double* out_mid) {
   using CT = typename HT<MODE>::T;
@@ -660,7 +694,7 @@ __device__ __forceinline__ void hist_add_row(typename HT<MODE>::T* hist, const C
 }
 
 // serial selection over an evaluated group, in visiting order (thread 0)
-__device__ void select_group(const Ctx& c, const TreeSpec& s, const int16_t* feats, int g, const double* rg,
+__device__ void select_group(const Ctx& c, const NodeSpec& s, const int16_t* feats, int g, const double* rg,
                              const int* rb, const int* rn, const double* rleft, double* best_left, int& nonconst,
                              double& best_gain, int& best_feat, int& best_bin, int& upd_j) {
   upd_j = -1;
@@ -679,7 +713,7 @@ __device__ void select_group(const Ctx& c, const TreeSpec& s, const int16_t* fea
 }
 
 // final split decision given the best candidate; returns true if node splits
-__device__ bool accept_split(const Ctx& c, const TreeSpec& s, int node, int tree, const double* best_left) {
+__device__ bool accept_split(const Ctx& c, const NodeSpec& s, int node, int tree, const double* best_left) {
   const double* pv = c.node_val + (int64_t)node * c.VC;
   const double Wt = c.tree_W[tree];
   double impN, impL, impR, wN, wL, wR;
@@ -741,7 +775,7 @@ __host__ __device__ inline FusedLayout fused_layout(int KG, int span, int elem, 
 // accept_split / make_children / enqueue on values already held on-chip (LDS): the
 // parent's channel sums and the tree weight are prefetched at kernel start, so the
 // decision makes no dependent global round trips.
-__device__ bool accept_split_v(const Ctx& c, const TreeSpec& s, const double* pv, double Wt, const double* best_left) {
+__device__ __forceinline__ bool accept_split_v(const Ctx& c, const NodeSpec& s, const double* pv, double Wt, const double* best_left) {
   double impN, impL, impR, wN, wL, wR;
   if (c.is_reg) {
     wN = pv[0]; wL = best_left[0]; wR = pv[0] - best_left[0];
@@ -759,7 +793,7 @@ __device__ bool accept_split_v(const Ctx& c, const TreeSpec& s, const double* pv
   return !(imp + kEps < (double)s.min_impurity_decrease);
 }
 
-__device__ double impurity_of_vals(const Ctx& c, const double* v, int crit) {
+__device__ __forceinline__ double impurity_of_vals(const Ctx& c, const double* v, int crit) {
   if (c.is_reg) return mse_impurity(v[0], v[1], v[2]);
   ClsAcc a;
   a.init(crit);
@@ -768,7 +802,7 @@ __device__ double impurity_of_vals(const Ctx& c, const double* v, int crit) {
 }
 
 // a wave/block-tier child into its staging slot (k_compact enqueues it): tier -1 = leaf
-__device__ void stage_child(const Ctx& c, const TreeSpec& s, int tree, int node, int64_t start, int count, int depth,
+__device__ __forceinline__ void stage_child(const Ctx& c, const NodeSpec& s, int tree, int node, int64_t start, int count, int depth,
                             uint64_t key, int64_t slot, const double* vals) {
   int tier = -1;
   if (!leaf_by_counts(s, count, depth) && !leaf_by_weight(s, vals_weight(vals, c.C, c.is_reg)) &&
@@ -789,7 +823,7 @@ __device__ __forceinline__ typename PLT<MODE>::T row_payload(const Ctx& c, const
 }
 
 template <int MODE>
-__device__ __forceinline__ typename PLT<MODE>::T word_payload(const Ctx& c, const TreeSpec& s, const float* ty,
+__device__ __forceinline__ typename PLT<MODE>::T word_payload(const Ctx& c, const NodeSpec& s, const float* ty,
                                                               uint32_t wd) {
   if (!c.packed) return row_payload<MODE>(c, ty, wd, boot_weight(s, wd));
   const uint32_t w = (wd >> c.rbits) & 15u;
@@ -817,7 +851,7 @@ __device__ __forceinline__ void hist_add(typename HT<MODE>::T* hj, const Ctx& c,
   }
 }
 
-template <int NT, int MODE>
+template <int NT, int MODE, int FC>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WPE, 8))) void k_nodes(Ctx c, int tier, int set_cur,
                                                                                                    int pair_base, int stage_base) {
   using CT = typename HT<MODE>::T;
@@ -829,7 +863,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   PH_BEGIN
   const OpenNode on = c.open[set_cur][tier][blockIdx.x];
-  const TreeSpec& s = c.specs[on.tree];
+  const NodeSpec s = spec_of<FC>(c, on.tree);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int d = c.d;
   const int KG = min(NT == 64 ? c.kg_wave : c.kg_block, KGMAX);
@@ -856,8 +890,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     sc->best_pos = 1 << 30; sc->scr_n = 0;
     sc->W = c.tree_W[on.tree];
     sc->best_mid = 0.0;
-    sc->lo = c.nbound ? c.nbound[2 * (int64_t)on.node] : -INFINITY;
-    sc->hi = c.nbound ? c.nbound[2 * (int64_t)on.node + 1] : INFINITY;
+    sc->lo = (FC < 0 && c.nbound) ? c.nbound[2 * (int64_t)on.node] : -INFINITY;
+    sc->hi = (FC < 0 && c.nbound) ? c.nbound[2 * (int64_t)on.node + 1] : INFINITY;
   }
   const FeatPerm fp = feat_perm(on.key, d);   // node's feature visiting order (forest_common.h)
   const uint32_t* rows = c.rows_cur + on.start;
@@ -1043,11 +1077,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     for (int j = wid; j < g; j += NW) {
 #ifdef DML_X2_EVAL   // sensitivity build: every feature evaluated twice (the first keeps the histogram)
       eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, false,
-                         tree_cw(c, on.tree), &c.rq, MonoQ{mono_of(c, s, feats[j]), sc->lo, sc->hi}, rmid + j);
+                         tree_cw<FC>(c, on.tree), &c.rq, MonoQ{mono_of<FC>(c, s, feats[j]), sc->lo, sc->hi}, rmid + j);
       wave_lds_sync();
 #endif
       eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, true,
-                         tree_cw(c, on.tree), &c.rq, MonoQ{mono_of(c, s, feats[j]), sc->lo, sc->hi}, rmid + j);
+                         tree_cw<FC>(c, on.tree), &c.rq, MonoQ{mono_of<FC>(c, s, feats[j]), sc->lo, sc->hi}, rmid + j);
     }
     __syncthreads();
     PH(3)
@@ -1118,7 +1152,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
         }
         NodeRec rec; rec.split = pack_split(sc->best_feat, sc->best_bin); rec.left = base;
         c.nodes[on.node] = rec;
-        mono_children(c, on.node, base, mono_of(c, s, sc->best_feat), sc->best_mid);
+        mono_children<FC>(c, on.node, base, mono_of<FC>(c, s, sc->best_feat), sc->best_mid);
       }
     }
     sc->base = base;
@@ -1246,7 +1280,7 @@ struct SubEntry {
 
 // evaluate one feature for the rows in `mask`; lane data: bin b (valid if in mask).
 template <bool REG>
-__device__ void sub_eval(const Ctx& c, const TreeSpec& s, uint64_t mask, int cnt, int lane, int my_bin, int my_cls,
+__device__ __forceinline__ void sub_eval(const Ctx& c, const NodeSpec& s, uint64_t mask, int cnt, int lane, int my_bin, int my_cls,
                          float my_w, int64_t my_yq, double& gain, int& bin, bool& nonconst, const double* cw,
                          MonoQ mq, double& mid) {
   const bool act = (mask >> lane) & 1ull;
@@ -1367,7 +1401,7 @@ __device__ __forceinline__ void argmax_seg(double& g, int& idx, int lane) {
 // per-feature loop.  xc: LDS row-bin cache (stride dp); cls_j / w_j: class and weight of
 // compact row j (valid in every segment's lane j).
 template <int WD>
-__device__ void sub_node_seg(const Ctx& c, const TreeSpec& s, const FeatPerm& fp, int cnt, int lane, int src,
+__device__ __forceinline__ void sub_node_seg(const Ctx& c, const NodeSpec& s, const FeatPerm& fp, int cnt, int lane, int src,
                              int cls_j, uint32_t w_j, const uint8_t* xc, int dp, int& nonconst, double& best_g,
                              int& best_f, int& best_b, const double* cw) {
   constexpr int S = 64 / WD;
@@ -1430,11 +1464,11 @@ __device__ void sub_node_seg(const Ctx& c, const TreeSpec& s, const FeatPerm& fp
   }
 }
 
-template <bool REG>
+template <bool REG, int FC>
 __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const OpenNode on = c.open[set_cur][0][blockIdx.x];
-  const TreeSpec& s = c.specs[on.tree];
+  const NodeSpec s = spec_of<FC>(c, on.tree);
   const int lane = threadIdx.x;
   const int d = c.d;
   const int VC = c.VC;
@@ -1506,13 +1540,13 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     SubEntry e;
     e.mask = cnt0 >= 64 ? ~0ull : ((1ull << cnt0) - 1ull);
     e.key = on.key; e.node = on.node; e.depth = on.depth;
-    e.lo = c.nbound ? c.nbound[2 * (int64_t)on.node] : -INFINITY;
-    e.hi = c.nbound ? c.nbound[2 * (int64_t)on.node + 1] : INFINITY;
+    e.lo = (FC < 0 && c.nbound) ? c.nbound[2 * (int64_t)on.node] : -INFINITY;
+    e.hi = (FC < 0 && c.nbound) ? c.nbound[2 * (int64_t)on.node + 1] : INFINITY;
     stack[0] = e;
   }
   if (lane < VC) sstats[lane] = c.node_val[(int64_t)on.node * VC + lane];
   const double Wt = c.tree_W[on.tree];
-  const double* tcw = REG ? nullptr : tree_cw(c, on.tree);
+  const double* tcw = REG ? nullptr : tree_cw<FC>(c, on.tree);
   pool_base = wave::bcast<int>(pool_base, 0);
   if (pool_base < 0) return;
   int used = 0;
@@ -1526,7 +1560,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     int nonconst = 0, best_f = -1, best_b = -1;
     double best_g = -INFINITY, best_mid = 0.0;
     const FeatPerm fp = feat_perm(e.key, d);
-    if (!REG && cache && cnt <= 32 && !c.mono) {
+    if (!REG && cache && cnt <= 32 && (FC >= 0 || !c.mono)) {
       // compact the node's rows: compact row j <- lane of the j-th set bit of the mask
       const bool in = (e.mask >> lane) & 1ull;
       if (in) cidx[lane_prefix(e.mask)] = lane;
@@ -1547,7 +1581,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
       int bb;
       bool nc;
       sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_yq, g, bb, nc, tcw,
-                    MonoQ{mono_of(c, s, f), e.lo, e.hi}, mid);
+                    MonoQ{mono_of<FC>(c, s, f), e.lo, e.hi}, mid);
       if (nc) {
         ++nonconst;
         if (bb >= 0 && g > best_g) { best_g = g; best_f = f; best_b = bb; best_mid = mid; }
@@ -1588,7 +1622,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
       }
       NodeRec rec; rec.split = pack_split(best_f, best_b); rec.left = base;
       c.nodes[e.node] = rec;
-      mono_children(c, e.node, base, mono_of(c, s, best_f), best_mid);
+      mono_children<FC>(c, e.node, base, mono_of<FC>(c, s, best_f), best_mid);
     }
     base = wave::bcast<int>(base, 0);
     if (base < 0) continue;
@@ -1602,7 +1636,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
                           impurity_of_vals(c, right_ch, s.criterion) > kEps;
       const bool push_l = !leaf_by_counts(s, nl, dep) && !leaf_by_weight(s, vals_weight(left_ch, c.C, c.is_reg)) &&
                           impurity_of_vals(c, left_ch, s.criterion) > kEps;
-      const int mbest = mono_of(c, s, best_f);
+      const int mbest = mono_of<FC>(c, s, best_f);
       if (push_r) {
         SubEntry r; r.mask = rm; r.key = child_key(e.key, 1); r.node = base + 1; r.depth = dep;
         mono_child_bounds(mbest, e.lo, e.hi, best_mid, 1, r.lo, r.hi);
@@ -1634,7 +1668,7 @@ __global__ __launch_bounds__(64) void k_large_prep(Ctx c, int set_cur, int nL) {
   const int lane = threadIdx.x;
   LState st;
   st.on = c.open[set_cur][3][slot];
-  const TreeSpec& s = c.specs[st.on.tree];
+  const NodeSpec s = spec_of<-1>(c, st.on.tree);
   int16_t* feats = c.lperm + (int64_t)slot * c.d;
   st.g = min(c.kg_large, min(s.max_features, c.d));
   const FeatPerm fp = feat_perm(st.on.key, c.d);
@@ -1665,7 +1699,7 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
   const int r0 = DML_LCHUNK * c.chunk;
   if (r0 >= st.on.count) return;
   const int r1 = min(r0 + c.chunk, st.on.count);
-  const TreeSpec& s = c.specs[st.on.tree];
+  const NodeSpec s = spec_of<-1>(c, st.on.tree);
   const int g = st.g;
   const int span = hist_planes(MODE, c.CH) * 256;
   __shared__ int16_t feats[64];
@@ -1752,7 +1786,7 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   const int slot = blockIdx.x;
   LState& st = c.lstate[slot];
   if (st.done) return;
-  const TreeSpec& s = c.specs[st.on.tree];
+  const NodeSpec s = spec_of<-1>(c, st.on.tree);
   const int g = st.g, span = hist_planes(MODE, c.CH) * 256;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   CT* hist = (CT*)smem;
@@ -1900,7 +1934,7 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_count_active(Ctx c) {
   const int t = blockIdx.y;
-  const TreeSpec& s = c.specs[t];
+  const NodeSpec s = spec_of<-1>(c, t);
   const uint8_t* role = c.roles + (int64_t)s.split * c.n;
   int cnt = 0;
   const int r0 = blockIdx.x * 1024;
@@ -1921,7 +1955,7 @@ __global__ __launch_bounds__(256) void k_count_active(Ctx c) {
 template <bool REG>
 __global__ __launch_bounds__(256) void k_fill_active(Ctx c) {
   const int t = blockIdx.y;
-  const TreeSpec& s = c.specs[t];
+  const NodeSpec s = spec_of<-1>(c, t);
   const uint8_t* role = c.roles + (int64_t)s.split * c.n;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   __shared__ int wcnt[16];
@@ -2332,6 +2366,9 @@ template <int MODE>
 static int build_impl(ForestArgs* a, hipStream_t st) {
   constexpr bool REG = MODE == 2;
   constexpr int GM = MODE == 2 ? 2 : 0;  // global (large-tier) histogram layout
+  // the criterion the node kernels are specialised on (gini / squared_error builds)
+  constexpr int FCX = REG ? kMSE : kGini;
+  const bool fast = a->fast_crit == FCX + 1;
   Layout L = plan(a);
   if ((size_t)a->workspace_bytes < (size_t)dml_forest_workspace_bytes(a)) return 2;
   Ctx c = make_ctx(a, L);
@@ -2369,9 +2406,12 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     const int need = (int)std::max(std::max(lds_s, lds_w), std::max(lds_b, lds_sl));
     static int attr_set[3] = {0, 0, 0};
     if (need > 64 * 1024 && need > attr_set[MODE]) {
-      HIP_OK(hipFuncSetAttribute((const void*)k_subtree<REG>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<64, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<DML_BLOCK_NT, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_subtree<REG, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_subtree<REG, FCX>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<64, MODE, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<64, MODE, FCX>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<DML_BLOCK_NT, MODE, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<DML_BLOCK_NT, MODE, FCX>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_hist_large<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_split_large<GM>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       attr_set[MODE] = need;
@@ -2405,9 +2445,15 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       for (int i = 0; i < 3; ++i) HIP_OK(hipStreamWaitEvent(ss->s[i], ss->fork, 0));
       s0 = ss->s[0]; s1 = ss->s[1]; s2 = ss->s[2];
     }
-    if (ns) k_subtree<REG><<<ns, 64, lds_s, s0>>>(c, cur);
-    if (nw) k_nodes<64, MODE><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w, 0);
-    if (nb) k_nodes<DML_BLOCK_NT, MODE><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, nw);
+    if (fast) {
+      if (ns) k_subtree<REG, FCX><<<ns, 64, lds_s, s0>>>(c, cur);
+      if (nw) k_nodes<64, MODE, FCX><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w, 0);
+      if (nb) k_nodes<DML_BLOCK_NT, MODE, FCX><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, nw);
+    } else {
+      if (ns) k_subtree<REG, -1><<<ns, 64, lds_s, s0>>>(c, cur);
+      if (nw) k_nodes<64, MODE, -1><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w, 0);
+      if (nb) k_nodes<DML_BLOCK_NT, MODE, -1><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, nw);
+    }
     if (nL) {
       k_large_prep<<<nL, 64, 0, st>>>(c, cur, nL);
       while (true) {

@@ -97,8 +97,10 @@ DML_HD uint32_t hash_u32(uint64_t key, uint64_t ctr) {
   return (uint32_t)(splitmix64(key ^ splitmix64(ctr + 0x632BE59BD9B4E019ull)) >> 32);
 }
 
-// bootstrap weight of `row` for the tree
-DML_HD uint32_t boot_weight(const TreeSpec& t, uint32_t row) {
+// bootstrap weight of `row` for the tree (TS: TreeSpec, or any view with its fields --
+// the HIP node kernels pass a register-resident NodeSpec)
+template <class TS>
+DML_HD uint32_t boot_weight(const TS& t, uint32_t row) {
   if (!t.bootstrap) return 1u;
   const uint32_t u = hash_u32(t.seed, 0xB0075ull * 0x100000000ull + row);
   if (t.bootstrap == 2) return u < t.pois_cdf[0] ? 1u : 0u;
@@ -327,7 +329,8 @@ constexpr double kEps = 1e-7;  // sklearn EPSILON for purity / min_impurity_decr
 // or for friedman_mse FriedmanMSE.impurity_improvement = (w_r s_l - w_l s_r)^2 /
 // (w_l w_r W_node), which is not scaled by the tree weight.  pv / bl: the node's and the
 // left side's regression sums {w, w y, ...}
-DML_HD double accept_improvement(const TreeSpec& s, bool is_reg, const double* pv, const double* bl, double Wt,
+template <class TS>
+DML_HD double accept_improvement(const TS& s, bool is_reg, const double* pv, const double* bl, double Wt,
                                  double wN, double impN, double wL, double impL, double wR, double impR) {
   if (is_reg && s.criterion == kFriedman) {
     const double wl = bl[0], wr = pv[0] - bl[0], diff = wr * bl[1] - wl * (pv[1] - bl[1]);
@@ -378,18 +381,21 @@ DML_HD void mono_clip(double* v, int is_reg, double lo, double hi) {
 }
 
 // leaf-by-counts rule (before any split search)
-DML_HD bool leaf_by_counts(const TreeSpec& t, int count, int depth) {
+template <class TS>
+DML_HD bool leaf_by_counts(const TS& t, int count, int depth) {
   return depth >= t.max_depth || count < t.min_samples_split || count < 2 * t.min_samples_leaf;
 }
 
 // min_weight_fraction_leaf (sklearn): a node lighter than 2 x min_weight_leaf is a leaf,
 // and a split leaving either side lighter than min_weight_leaf is not a candidate.
 // Weights include bootstrap counts and class weights (sklearn's sample weights).
-DML_HD bool leaf_by_weight(const TreeSpec& t, double w_node) {
+template <class TS>
+DML_HD bool leaf_by_weight(const TS& t, double w_node) {
   return t.min_weight_leaf > 0.0 && w_node < 2.0 * t.min_weight_leaf;
 }
 
-DML_HD bool side_too_light(const TreeSpec& t, double wl, double wr) {
+template <class TS>
+DML_HD bool side_too_light(const TS& t, double wl, double wr) {
   return t.min_weight_leaf > 0.0 && (wl < t.min_weight_leaf || wr < t.min_weight_leaf);
 }
 

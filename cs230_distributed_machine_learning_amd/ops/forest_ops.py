@@ -280,6 +280,11 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
         mono_dev = torch.from_numpy(np.ascontiguousarray(mono, dtype=np.int8)).to(dev)
     a.mono = native.ptr(mono_dev) if mono_dev is not None else 0
     a.nbound = 0
+    # one criterion, no class weights / monotonic constraints / min_weight_fraction_leaf: the
+    # HIP node kernels specialised on that criterion run (forest.hip spec_of / specialise)
+    crits = np.unique(specs["criterion"]) if T else np.zeros(0)
+    a.fast_crit = (int(crits[0]) + 1 if len(crits) == 1 and cw_dev is None and mono_dev is None
+                   and not np.any(specs["min_weight_frac"] > 0) else 0)
     a.active_count = native.ptr(active)
     t0 = time.perf_counter()
     with trace.range("forest_count"):

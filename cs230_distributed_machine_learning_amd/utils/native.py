@@ -72,7 +72,7 @@ ForestArgs = _i64_struct(
         "tier0_nodes", "tier1_nodes", "tier2_nodes", "tier3_nodes",
         "ystride", "XbT", "cw",
         "yq_e1", "yq_e2",
-        "mono", "nbound",
+        "mono", "nbound", "fast_crit",
     ],
 )
 
