@@ -258,12 +258,15 @@ __device__ __forceinline__ const float* tree_y(const Ctx& c, const NodeSpec& s) 
 
 __device__ __forceinline__ uint32_t word_row(const Ctx& c, uint32_t wd) { return wd & c.rmask; }
 
+// PK: the kernel is specialised on packed row words (FC >= 0 builds are launched only then)
+template <bool PK = false>
 __device__ __forceinline__ uint32_t word_weight(const Ctx& c, const NodeSpec& s, uint32_t wd) {
-  return c.packed ? (wd >> c.rbits) & 15u : boot_weight(s, wd);
+  return (PK || c.packed) ? (wd >> c.rbits) & 15u : boot_weight(s, wd);
 }
 
+template <bool PK = false>
 __device__ __forceinline__ int word_cls(const Ctx& c, uint32_t wd) {
-  return c.packed ? (int)(wd >> (c.rbits + 4)) : c.ycls[wd];
+  return (PK || c.packed) ? (int)(wd >> (c.rbits + 4)) : c.ycls[wd];
 }
 
 // class-weight row of a tree (nullptr: every weight is 1)
@@ -822,10 +825,10 @@ __device__ __forceinline__ typename PLT<MODE>::T row_payload(const Ctx& c, const
   else return reg_payload(c, w, ty[row]);
 }
 
-template <int MODE>
+template <int MODE, bool PK = false>
 __device__ __forceinline__ typename PLT<MODE>::T word_payload(const Ctx& c, const NodeSpec& s, const float* ty,
                                                               uint32_t wd) {
-  if (!c.packed) return row_payload<MODE>(c, ty, wd, boot_weight(s, wd));
+  if (!PK && !c.packed) return row_payload<MODE>(c, ty, wd, boot_weight(s, wd));
   const uint32_t w = (wd >> c.rbits) & 15u;
   if constexpr (MODE == 0) return (uint64_t)(wd >> (c.rbits + 4)) | ((uint64_t)w << 32);
   else if constexpr (MODE == 1) return pack_bin((int)(wd >> (c.rbits + 4)), w);
@@ -855,6 +858,7 @@ template <int NT, int MODE, int FC>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WPE, 8))) void k_nodes(Ctx c, int tier, int set_cur,
                                                                                                    int pair_base, int stage_base) {
   using CT = typename HT<MODE>::T;
+  constexpr bool PK = FC >= 0;   // specialised builds have packed row words
   constexpr int NW = NT / 64;
   constexpr int RPT = NT == 64 ? 4 : DML_RPT_BLOCK;   // rows per thread in registers (<= 4: packed u8 x 4)
   static_assert(RPT >= 1 && RPT <= 4, "RPT");
@@ -911,7 +915,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     }
 #pragma unroll
     for (int u = 0; u < RPT; ++u)
-      rpl[u] = rrow[u] != 0xFFFFFFFFu ? word_payload<MODE>(c, s, ty, rrow[u]) : PL{};
+      rpl[u] = rrow[u] != 0xFFFFFFFFu ? word_payload<MODE, PK>(c, s, ty, rrow[u]) : PL{};
   };
   if (reg_rows) load_rows(0);
 #pragma unroll
@@ -930,12 +934,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     if (reg_rows) {
       npre = min(KPRE, min(k + slack, d));
       uint32_t raw[KPRE][RPT];
+      // row lines of the lane's rows (an absent row reads row 0: every load is unconditional)
+      const uint8_t* xr[RPT];
+#pragma unroll
+      for (int u = 0; u < RPT; ++u) xr[u] = c.Xb + (int64_t)(rrow[u] != 0xFFFFFFFFu ? (rrow[u] & c.rmask) : 0u) * c.ld;
 #pragma unroll
       for (int q = 0; q < KPRE; ++q) {
-        const int64_t f = q < npre ? feature_at(fp, q, d) : 0;
+        const int f = __builtin_amdgcn_readfirstlane(q < npre ? feature_at(fp, q, d) : 0);
 #pragma unroll
-        for (int u = 0; u < RPT; ++u)
-          raw[q][u] = (q < npre && rrow[u] != 0xFFFFFFFFu) ? (uint32_t)c.Xb[(int64_t)(rrow[u] & c.rmask) * c.ld + f] : 0u;
+        for (int u = 0; u < RPT; ++u) raw[q][u] = q < npre ? (uint32_t)xr[u][f] : 0u;
 #ifdef DML_X2_GATHER   // sensitivity build: every bin gathered twice
 #pragma unroll
       for (int u = 0; u < RPT; ++u)
@@ -952,7 +959,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     }
   }
   while (true) {
-    const int pos = sc->pos, nonconst = sc->nonconst;
+    // wave-uniform loop state in SGPRs: the per-group bounds (g) are then scalar branches, not
+    // exec masks (a masked load merges into a phi whose copies force vmcnt(0) waits)
+    const int pos = __builtin_amdgcn_readfirstlane(sc->pos), nonconst = __builtin_amdgcn_readfirstlane(sc->nonconst);
     if (nonconst >= k || pos >= d) break;
     const int g = min(KG, min(k - nonconst + slack, d - pos));
     if (tid < g) feats[tid] = (int16_t)feature_at(fp, pos + tid, d);   // one visiting position per lane
@@ -971,48 +980,74 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
       }
     } else
     if (!reg_rows && RPT == 1) {
-      // large node, one row per thread per NT-row chunk: 2-deep software pipeline -- the
-      // next chunk's payload/bin loads and the row ids two chunks ahead are in flight while
-      // the current chunk's histogram atomics run
+      // large node, one row per thread per NT-row chunk, software-pipelined over chunks with
+      // two register sets (A: even chunks, B: odd chunks) that swap roles without copies: per
+      // chunk, the row id two chunks ahead is loaded first, then the next chunk's bins are
+      // gathered, then this chunk's histogram atomics run -- so waiting for this chunk's bins
+      // never waits for the next chunk's (vmcnt retires in issue order, and a register copy of
+      // a pending load would force exactly that wait)
+      // Every load of a chunk is issued unconditionally and their number is a compile-time G = g:
+      // with a conditional or variable count the compiler cannot count outstanding loads and
+      // waits for all of them (vmcnt(0)), which would drain the next chunk's gathers too.
       constexpr uint32_t INV = 0xFFFFFFFFu;
-      int fj[KGMAX];
+      auto run = [&](auto Gc) {
+        constexpr int G = decltype(Gc)::value;
+        int fj[G];
 #pragma unroll
-      for (int j = 0; j < KGMAX; ++j) fj[j] = j < g ? (int)feats[j] : 0;
-      auto row_at = [&](int r) -> uint32_t { return r < cnt ? rows[r] : INV; };
-      uint32_t r0 = row_at(tid), r1 = row_at(NT + tid);
-      PL pl0 = r0 != INV ? word_payload<MODE>(c, s, ty, r0) : PL{};
-      uint32_t b0[KGMAX];
+        for (int j = 0; j < G; ++j) fj[j] = __builtin_amdgcn_readfirstlane((int)feats[j < g ? j : 0]);
+        auto row_at = [&](int r) -> uint32_t {
+          const uint32_t v = rows[min(r, cnt - 1)];
+          return r < cnt ? v : INV;
+        };
+        auto gather = [&](uint32_t r, uint32_t* b) {
+          const uint8_t* xr = c.Xb + (int64_t)(r != INV ? (r & c.rmask) : 0u) * c.ld;
 #pragma unroll
-      for (int j = 0; j < KGMAX; ++j)
-        b0[j] = (j < g && r0 != INV) ? (uint32_t)c.Xb[(int64_t)(r0 & c.rmask) * c.ld + fj[j]] : 0u;
-      for (int base = 0; base < cnt; base += NT) {
-        const PL pl1 = r1 != INV ? word_payload<MODE>(c, s, ty, r1) : PL{};
-        uint32_t b1[KGMAX];
-#pragma unroll
-        for (int j = 0; j < KGMAX; ++j)
-          b1[j] = (j < g && r1 != INV) ? (uint32_t)c.Xb[(int64_t)(r1 & c.rmask) * c.ld + fj[j]] : 0u;
+          for (int j = 0; j < G; ++j) b[j] = (uint32_t)xr[fj[j]];
 #ifdef DML_X2_GATHER
 #pragma unroll
-        for (int j = 0; j < KGMAX; ++j)
-          b1[j] |= (j < g && r1 != INV) ? (uint32_t)c.Xb[(int64_t)(r1 & c.rmask) * c.ld + fj[j] + ((uint32_t)c.n >> 31)] : 0u;
+          for (int j = 0; j < G; ++j) b[j] |= (uint32_t)xr[fj[j] + ((uint32_t)c.n >> 31)];
 #endif
-        const uint32_t r2 = row_at(base + 2 * NT + tid);
-        if (r0 != INV) {
-          if (NT == 256 && KGMAX == 16 && pos == 0) {
-            uint4 v;
-            v.x = b0[0] | b0[1] << 8 | b0[2] << 16 | b0[3] << 24;
-            v.y = b0[4] | b0[5] << 8 | b0[6] << 16 | b0[7] << 24;
-            v.z = b0[8] | b0[9] << 8 | b0[10] << 16 | b0[11] << 24;
-            v.w = b0[12] | b0[13] << 8 | b0[14] << 16 | b0[15] << 24;
-            *(uint4*)(c.bscr + (on.start + base + tid) * 16) = v;
+        };
+        auto consume = [&](int base, bool valid, const uint32_t* b, const PL& pl) {
+          if (NT == 256 && pos == 0 && valid) {
+            uint32_t w4[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < G && j < 16; ++j) w4[j >> 2] |= (j < g ? b[j] & 0xFFu : 0u) << (8 * (j & 3));
+            *(uint4*)(c.bscr + (on.start + base + tid) * 16) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
           }
+          if (valid) {
 #pragma unroll
-          for (int j = 0; j < KGMAX; ++j)
-            if (j < g) hist_add<MODE>(hist + j * span, c, (int)b0[j], pl0);
+            for (int j = 0; j < G; ++j)
+              if (j < g) hist_add<MODE>(hist + j * span, c, (int)b[j], pl);
+          }
+        };
+        uint32_t rA = row_at(tid), rB = row_at(NT + tid);
+        uint32_t bA[G], bB[G];
+        gather(rA, bA);
+        bool vA = rA != INV, vB = false;
+        PL pA = vA ? word_payload<MODE, PK>(c, s, ty, rA) : PL{}, pB{};
+        for (int base = 0; base < cnt; base += 2 * NT) {
+          rA = row_at(base + 2 * NT + tid);       // chunk k+2's row id
+          gather(rB, bB);                         // chunk k+1's bins
+          vB = rB != INV;
+          pB = vB ? word_payload<MODE, PK>(c, s, ty, rB) : PL{};
+          consume(base, vA, bA, pA);              // chunk k
+          rB = row_at(base + 3 * NT + tid);       // chunk k+3's row id
+          gather(rA, bA);                         // chunk k+2's bins
+          vA = rA != INV;
+          pA = vA ? word_payload<MODE, PK>(c, s, ty, rA) : PL{};
+          consume(base + NT, vB, bB, pB);         // chunk k+1
         }
-        r0 = r1; r1 = r2; pl0 = pl1;
-#pragma unroll
-        for (int j = 0; j < KGMAX; ++j) b0[j] = b1[j];
+      };
+      // one instantiation per group size: an extra load per row is an extra cache-line lookup,
+      // and the gathers are lookup-bound (one line per CU clock)
+      switch (g) {
+#define DML_G_CASE(N) case N: run(std::integral_constant<int, (N < KGMAX ? N : KGMAX)>{}); break;
+        DML_G_CASE(1) DML_G_CASE(2) DML_G_CASE(3) DML_G_CASE(4) DML_G_CASE(5) DML_G_CASE(6) DML_G_CASE(7)
+        DML_G_CASE(8) DML_G_CASE(9) DML_G_CASE(10) DML_G_CASE(11) DML_G_CASE(12) DML_G_CASE(13) DML_G_CASE(14)
+        DML_G_CASE(15)
+#undef DML_G_CASE
+        default: run(std::integral_constant<int, KGMAX>{}); break;
       }
     } else
     for (int base = 0; base < cnt; base += NT * RPT) {
@@ -2368,10 +2403,10 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   constexpr int GM = MODE == 2 ? 2 : 0;  // global (large-tier) histogram layout
   // the criterion the node kernels are specialised on (gini / squared_error builds)
   constexpr int FCX = REG ? kMSE : kGini;
-  const bool fast = a->fast_crit == FCX + 1;
   Layout L = plan(a);
   if ((size_t)a->workspace_bytes < (size_t)dml_forest_workspace_bytes(a)) return 2;
   Ctx c = make_ctx(a, L);
+  const bool fast = a->fast_crit == FCX + 1 && c.packed;   // PK kernels assume packed row words
   uint32_t* rows_a = (uint32_t*)(((unsigned char*)a->workspace) + L.total);
   c.rows_cur = rows_a;
   int32_t* h = pinned_counters();
