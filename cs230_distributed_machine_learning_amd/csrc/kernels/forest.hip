@@ -1319,11 +1319,15 @@ __device__ __forceinline__ void sub_eval(const Ctx& c, const NodeSpec& s, uint64
                          float my_w, int64_t my_yq, double& gain, int& bin, bool& nonconst, const double* cw,
                          MonoQ mq, double& mid) {
   const bool act = (mask >> lane) & 1ull;
-  const uint32_t key = act ? ((uint32_t)my_bin << 6) | (uint32_t)lane : 0xFFFFFFFFu;
+  // classification: the row's class and weight ride in the key's low bits (bin << 10 | cls << 4
+  // | w), so the sorted lanes hold their rows' payload without shuffles (equal keys are
+  // interchangeable rows); regression keeps (bin, lane) keys and shuffles its 64-bit targets
+  const uint32_t key = !act ? 0xFFFFFFFFu
+                            : (REG ? ((uint32_t)my_bin << 6) | (uint32_t)lane
+                                   : ((uint32_t)my_bin << 10) | ((uint32_t)my_cls << 4) | ((uint32_t)my_w & 15u));
   const uint32_t sk = wave::bitonic64(key, lane);
   const bool valid_row = lane < cnt;
-  const int src = (int)(sk & 63u);
-  const int b = valid_row ? (int)(sk >> 6) : 1024;
+  const int b = valid_row ? (int)(sk >> (REG ? 6 : 10)) : 1024;
   const int bnext = wave::shift_down1<int>(b, lane, 1024);
   const int blast = wave::bcast<int>(b, cnt - 1);
   const int bfirst = wave::bcast<int>(b, 0);
@@ -1334,22 +1338,31 @@ __device__ __forceinline__ void sub_eval(const Ctx& c, const NodeSpec& s, uint64
   double g = -INFINITY, mid_l = 0.0;
   bool ok = cand;   // cand and both sides at least min_weight_leaf heavy
   if constexpr (!REG) {
-    // every shuffle runs with the full wave active (a shuffle inside a divergent branch
-    // would read lanes outside EXEC); select afterwards
-    const int ycls = __shfl(my_cls, src);
-    const float wsh = __shfl(my_w, src);
-    const uint32_t w = valid_row ? (uint32_t)wsh : 0u;
+    const int ycls = (int)((sk >> 4) & 63u);
+    const uint32_t w = valid_row ? (sk & 15u) : 0u;
     ClsAcc L, R;
     L.init(s.criterion); R.init(s.criterion);
     double l0 = 0.0, t0 = 0.0;
-    for (int k = 0; k < c.C; ++k) {
-      const uint32_t v = (ycls == k) ? w : 0u;
-      const uint32_t pre = wave::incl_scan<uint32_t>(v);
+    if (c.C == 2) {
+      // binary: ONE scan of (w | w [class 1] << 16) carries both channels (<= 64 rows weigh < 2^16)
+      const uint32_t pre = wave::incl_scan<uint32_t>(w | (ycls == 1 ? w << 16 : 0u));
       const uint32_t tot = wave::bcast<uint32_t>(pre, cnt - 1);
-      const double lw = (double)pre * cwk(cw, k), tw = (double)tot * cwk(cw, k);
-      if (k == 0) { l0 = lw; t0 = tw; }
-      L.add(lw);
-      R.add(tw - lw);
+      const uint32_t p1 = pre >> 16, p0 = (pre & 0xFFFFu) - p1, q1 = tot >> 16, q0 = (tot & 0xFFFFu) - q1;
+      const double lw0 = (double)p0 * cwk(cw, 0), tw0 = (double)q0 * cwk(cw, 0);
+      const double lw1 = (double)p1 * cwk(cw, 1), tw1 = (double)q1 * cwk(cw, 1);
+      l0 = lw0; t0 = tw0;
+      L.add(lw0); R.add(tw0 - lw0);
+      L.add(lw1); R.add(tw1 - lw1);
+    } else {
+      for (int k = 0; k < c.C; ++k) {
+        const uint32_t v = (ycls == k) ? w : 0u;
+        const uint32_t pre = wave::incl_scan<uint32_t>(v);
+        const uint32_t tot = wave::bcast<uint32_t>(pre, cnt - 1);
+        const double lw = (double)pre * cwk(cw, k), tw = (double)tot * cwk(cw, k);
+        if (k == 0) { l0 = lw; t0 = tw; }
+        L.add(lw);
+        R.add(tw - lw);
+      }
     }
     ok = cand && !side_too_light(s, L.w, R.w);
     if (ok && mq.m) {   // monotonic_cst (class-0 fraction)
@@ -1360,6 +1373,7 @@ __device__ __forceinline__ void sub_eval(const Ctx& c, const NodeSpec& s, uint64
   } else {
     // integer prefix sums of w and w yq in (bin, lane) order: at the last lane of a bin
     // run they are the host builder's histogram prefix sums (forest_common.h)
+    const int src = (int)(sk & 63u);
     const uint32_t wsh = (uint32_t)__shfl((int)(uint32_t)my_w, src);
     const uint32_t ylo = (uint32_t)__shfl((int)(uint32_t)(uint64_t)my_yq, src);
     const uint32_t yhi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)my_yq >> 32), src);
@@ -1376,8 +1390,22 @@ __device__ __forceinline__ void sub_eval(const Ctx& c, const NodeSpec& s, uint64
     }
     if (ok) g = reg_proxy(s.criterion, l0, l1, tt0 - l0, tt1 - l1);
   }
-  int bl = ok ? lane : 64;
-  wave::argmax(g, bl, lane);
+  int bl;
+  if (!REG && s.criterion == kGini && !mq.m) {
+    // Gini gains of candidates are positive doubles, whose bit patterns order like the
+    // values: a u64 max, then the first lane holding it (the lowest candidate bin)
+    uint64_t gb = ok ? __builtin_bit_cast(uint64_t, g) : 0ull;
+    uint64_t mx = gb;
+#define DML_MAXU64_STEP(M) { const uint64_t o = wave::shfl_xor<M>(mx, lane); mx = o > mx ? o : mx; }
+    DML_MAXU64_STEP(32) DML_MAXU64_STEP(16) DML_MAXU64_STEP(8) DML_MAXU64_STEP(4) DML_MAXU64_STEP(2) DML_MAXU64_STEP(1)
+#undef DML_MAXU64_STEP
+    const uint64_t hit = __ballot(ok && gb == mx);
+    bl = hit ? (int)__builtin_ctzll(hit) : 64;
+    g = hit ? __builtin_bit_cast(double, mx) : -INFINITY;
+  } else {
+    bl = ok ? lane : 64;
+    wave::argmax(g, bl, lane);
+  }
   mid = wave::bcast<double>(mid_l, bl & 63);
   gain = g;
   const int bsel = wave::bcast<int>(b, bl & 63);
@@ -1443,30 +1471,30 @@ __device__ __forceinline__ void sub_node_seg(const Ctx& c, const NodeSpec& s, co
   const int d = c.d;
   const int seg = lane / WD, j = lane & (WD - 1);
   const bool valid_row = j < cnt;
+  // the row's class and weight ride in the low bits of its sort key (bin << 10 | cls << 4 | w):
+  // after the sort every lane holds its sorted row's payload, no shuffles (rows of equal
+  // keys are interchangeable: the sums at the end of a bin run are the same)
+  const uint32_t pay = ((uint32_t)cls_j << 4) | (w_j & 15u);
   for (int pos = 0; nonconst < s.max_features && pos < d; pos += S) {
     const bool has_f = pos + seg < d;
     const int f = has_f ? feature_at(fp, pos + seg, d) : 0;
     const int my_bin = (valid_row && has_f) ? (int)xc[src * dp + f] : 0;
-    const uint32_t key = valid_row ? ((uint32_t)my_bin << 6) | (uint32_t)j : 0xFFFFFFFFu;
+    const uint32_t key = valid_row ? ((uint32_t)my_bin << 10) | pay : 0xFFFFFFFFu;
     const uint32_t sk = bitonic_seg<WD>(key, j, lane);
-    const int jj = (int)(sk & 63u);
-    const int b = valid_row ? (int)(sk >> 6) : 1024;
+    const int b = valid_row ? (int)(sk >> 10) : 1024;
     const int bnext = wave::shift_down1<int>(b, lane, 1024);
-    // class / weight of the sorted row (compact row jj lives in lane seg*WD + jj of every segment)
-    const int srcl = seg * WD + (valid_row ? jj : 0);
-    const int ycls = __shfl(cls_j, srcl);
-    const uint32_t wsh = (uint32_t)__shfl((int)w_j, srcl);
-    const uint32_t w = valid_row ? wsh : 0u;
+    const int ycls = (int)((sk >> 4) & 63u);
+    const uint32_t w = valid_row ? (sk & 15u) : 0u;
     const bool cand = valid_row && j < cnt - 1 && b != bnext && j + 1 >= s.min_samples_leaf &&
                       cnt - j - 1 >= s.min_samples_leaf;
     const bool ncl = valid_row && j < cnt - 1 && b != bnext;
     ClsAcc L, R;
     L.init(s.criterion); R.init(s.criterion);
-    for (int k = 0; k < c.C; ++k) {
-      const uint32_t v = (ycls == k) ? w : 0u;
-      uint32_t pre = wave::incl_scan<uint32_t>(v);
-      // segment-relative: subtract the inclusive total of the preceding segments
-      uint32_t base = 0, tot = 0;
+    // segment-relative inclusive prefix: subtract the inclusive total of the preceding segments
+    auto seg_scan = [&](uint32_t v, uint32_t& pre, uint32_t& tot) {
+      pre = wave::incl_scan<uint32_t>(v);
+      uint32_t base = 0;
+      tot = 0;
 #pragma unroll
       for (int q = 0; q < S; ++q) {
         const uint32_t bq = q ? (uint32_t)__builtin_amdgcn_readlane((int)pre, q * WD - 1) : 0u;
@@ -1474,9 +1502,25 @@ __device__ __forceinline__ void sub_node_seg(const Ctx& c, const NodeSpec& s, co
         if (seg == q) { base = bq; tot = eq - bq; }
       }
       pre -= base;
-      const double lw = (double)pre * cwk(cw, k), tw = (double)tot * cwk(cw, k);
-      L.add(lw);
-      R.add(tw - lw);
+    };
+    if (c.C == 2) {
+      // binary: ONE scan of (w | w [class 1] << 16) carries both channels (a node of <= 32
+      // rows weighs < 2^16)
+      uint32_t pre, tot;
+      seg_scan(w | (ycls == 1 ? w << 16 : 0u), pre, tot);
+      const uint32_t l1 = pre >> 16, l0 = (pre & 0xFFFFu) - l1, t1 = tot >> 16, t0 = (tot & 0xFFFFu) - t1;
+      const double lw0 = (double)l0 * cwk(cw, 0), tw0 = (double)t0 * cwk(cw, 0);
+      const double lw1 = (double)l1 * cwk(cw, 1), tw1 = (double)t1 * cwk(cw, 1);
+      L.add(lw0); R.add(tw0 - lw0);
+      L.add(lw1); R.add(tw1 - lw1);
+    } else {
+      for (int k = 0; k < c.C; ++k) {
+        uint32_t pre, tot;
+        seg_scan((ycls == k) ? w : 0u, pre, tot);
+        const double lw = (double)pre * cwk(cw, k), tw = (double)tot * cwk(cw, k);
+        L.add(lw);
+        R.add(tw - lw);
+      }
     }
     const bool ok = cand && !side_too_light(s, L.w, R.w);
     double g = ok ? cls_proxy(L, R, s.criterion) : -INFINITY;
@@ -1484,17 +1528,36 @@ __device__ __forceinline__ void sub_node_seg(const Ctx& c, const NodeSpec& s, co
     argmax_seg<WD>(g, bl, lane);
     const int bsel = __shfl(b, seg * WD + (bl & (WD - 1)));
     const uint64_t ncm = __ballot(ncl);
-    // serial selection over the S evaluated features, in visiting order
+    // selection over the S features in visiting order, vectorised: segment q counts when its
+    // feature is non-constant and among the first (max_features - nonconst) such; the first
+    // maximal gain among the counted ones replaces the running best if strictly better --
+    // exactly the sequential loop's outcome
+    uint32_t ncs = 0;   // bit q: segment q's feature is non-constant (and exists)
 #pragma unroll
-    for (int q = 0; q < S; ++q) {
-      if (pos + q >= d || nonconst >= s.max_features) break;
-      const bool nc = ((ncm >> (q * WD)) & ((WD == 64 ? ~0ull : ((1ull << WD) - 1ull)))) != 0ull;
-      if (!nc) continue;
-      ++nonconst;
-      const double gq = wave::bcast<double>(g, q * WD);
-      const int blq = wave::bcast<int>(bl, q * WD);
-      const int bq = wave::bcast<int>(bsel, q * WD);
-      if (blq < 64 && gq > best_g) { best_g = gq; best_f = feature_at(fp, pos + q, d); best_b = bq; }
+    for (int q = 0; q < S; ++q)
+      if (pos + q < d && ((ncm >> (q * WD)) & (WD == 64 ? ~0ull : ((1ull << WD) - 1ull))) != 0ull) ncs |= 1u << q;
+    const int room = s.max_features - nonconst;
+    const bool counted = ((ncs >> seg) & 1u) && __popc(ncs & ((1u << seg) - 1u)) < room;
+    double gq = (counted && bl < 64) ? g : -INFINITY;
+    int qi = (counted && bl < 64) ? seg : 64;
+    if constexpr (S >= 2) {
+      auto step = [&](auto Mc) {
+        constexpr int M = decltype(Mc)::value;
+        const double og = wave::shfl_xor<M>(gq, lane);
+        const int oi = wave::shfl_xor<M>(qi, lane);
+        if (og > gq || (og == gq && oi < qi)) { gq = og; qi = oi; }
+      };
+      if constexpr (WD <= 32) step(std::integral_constant<int, 32>{});
+      if constexpr (WD <= 16) step(std::integral_constant<int, 16>{});
+      if constexpr (WD <= 8) step(std::integral_constant<int, 8>{});
+    }
+    nonconst = min(s.max_features, nonconst + __popc(ncs));
+    gq = wave::bcast<double>(gq, 0);
+    qi = wave::bcast<int>(qi, 0);
+    if (qi < 64 && gq > best_g) {
+      best_g = gq;
+      best_f = feature_at(fp, pos + qi, d);
+      best_b = __builtin_amdgcn_readlane(bsel, qi * WD);
     }
   }
 }
@@ -1604,6 +1667,16 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
       const int src = jx < cnt ? cidx[jx] : 0;
       const int cls_j = __shfl(my_cls, src);
       const uint32_t w_j = (uint32_t)__shfl((int)(uint32_t)my_w, src);
+#ifdef DML_X2_SUB   // sensitivity build: every segmented evaluation twice (the first into copies)
+      {
+        int nc2 = nonconst, bf2 = best_f, bb2 = best_b;
+        double bg2 = best_g;
+        if (cnt <= 8) sub_node_seg<8>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw);
+        else if (cnt <= 16) sub_node_seg<16>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw);
+        else sub_node_seg<32>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw);
+        if (bg2 == -12345.0 && bf2 == 7 && nc2 == 3) atomicOr(&c.counters[kOpenOvf], bb2);
+      }
+#endif
       if (cnt <= 8) sub_node_seg<8>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw);
       else if (cnt <= 16) sub_node_seg<16>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw);
       else sub_node_seg<32>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw);
@@ -1615,6 +1688,11 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
       double g, mid;
       int bb;
       bool nc;
+#ifdef DML_X2_SUB
+      sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_yq, g, bb, nc, tcw,
+                    MonoQ{mono_of<FC>(c, s, f), e.lo, e.hi}, mid);
+      if (g == -12345.0 && bb == 7) atomicOr(&c.counters[kOpenOvf], (int)nc);
+#endif
       sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_yq, g, bb, nc, tcw,
                     MonoQ{mono_of<FC>(c, s, f), e.lo, e.hi}, mid);
       if (nc) {
