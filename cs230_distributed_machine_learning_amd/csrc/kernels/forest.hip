@@ -1205,10 +1205,66 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   if (tid == RT)
     stage_child(c, s, on.tree, base + 1, on.start + nl, cnt - nl, on.depth + 1, child_key(on.key, 1),
                 2 * (stage_base + (int64_t)blockIdx.x) + 1, rvs);
-  // ---- stable partition: RPT ballot rounds per chunk, one block-level offset exchange
+  // ---- stable partition
 #ifdef DML_X2_PART   // sensitivity build: the (idempotent) partition pass runs twice
   for (int rep_ = 0; rep_ < 2; ++rep_) {
 #endif
+  if (NT > 64 && !reg_rows && (size_t)((cnt + 63) / 64) * 12 <= (size_t)KG * span * sizeof(CT)) {
+    // block tier, streamed node: two passes and two barriers for the whole node (not two per
+    // chunk).  Pass 1 ranks every row (split bin from the histogram pass's scratch, else
+    // gathered) into one ballot word per 64-row group in LDS (the histograms are dead);
+    // one block scan gives every group's left offset; pass 2 re-reads the row ids
+    // (coalesced) and writes each row at its stable rank.
+    uint64_t* lflag = (uint64_t*)hist;                        // [ngrp] left flags
+    int* loff = (int*)(lflag + ((cnt + 63) / 64));            // [ngrp] exclusive left offsets
+    const int ngrp = (cnt + 63) / 64;
+    const int bjs = __builtin_amdgcn_readfirstlane((sc->best_pos < sc->scr_n) ? sc->best_pos : -1);
+    const int fsplit = __builtin_amdgcn_readfirstlane(feat), bsplit = __builtin_amdgcn_readfirstlane(bin);
+    constexpr int U = 4;   // positions per thread per round, all loads issued before the ballots
+    for (int p0 = 0; p0 < cnt; p0 += U * NT) {
+      uint32_t bv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int p = min(p0 + u * NT + tid, cnt - 1);
+        if (bjs >= 0) {
+          bv[u] = c.bscr[(on.start + p) * 16 + bjs];
+        } else {
+          const uint32_t r = rows[p];
+          bv[u] = c.Xb[(int64_t)(r & c.rmask) * c.ld + fsplit];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int p = p0 + u * NT + tid;
+        const uint64_t m = __ballot(p < cnt && (int)bv[u] <= bsplit);
+        if (lane == 0 && p - lane < cnt) lflag[(p - lane) >> 6] = m;
+      }
+    }
+    __syncthreads();
+    // exclusive prefix of the groups' left counts (<= 512 groups: two per thread)
+    {
+      const int g0 = 2 * tid, g1 = 2 * tid + 1;
+      const int c0 = g0 < ngrp ? __popcll(lflag[g0]) : 0, c1 = g1 < ngrp ? __popcll(lflag[g1]) : 0;
+      const int incl = wave::incl_scan<int>(c0 + c1);
+      if (lane == 63) sc->wcnt[wid] = incl;
+      __syncthreads();
+      int wbase = 0;
+      for (int w = 0; w < wid; ++w) wbase += sc->wcnt[w];
+      const int ex = wbase + incl - (c0 + c1);
+      if (g0 < ngrp) loff[g0] = ex;
+      if (g1 < ngrp) loff[g1] = ex + c0;
+    }
+    __syncthreads();
+    for (int p = tid; p < cnt; p += NT) {
+      const uint32_t r = rows[p];
+      const int q = p >> 6;
+      const uint64_t m = lflag[q];
+      const int lft = __popcll(m & ((1ull << (p & 63)) - 1ull));
+      const bool left = (m >> (p & 63)) & 1ull;
+      const int l0 = loff[q];
+      c.rows_next[on.start + (left ? l0 + lft : nl + (q * 64 - l0) + ((p & 63) - lft))] = r;
+    }
+  } else {
   uint32_t* out = c.rows_next + on.start;
   int baseL = 0, baseR = 0;
   // streaming (large-node) partition: the split-feature bins of the next chunk and the row
@@ -1289,6 +1345,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     baseL += totL; baseR += totR;
     if (!reg_rows && RPT == 1) { rrow[0] = nrow; rbin[0] = nbin; nrow = frow; }
   }
+  }   // streamed block-tier / register-rows partition
 #ifdef DML_X2_PART
   }
 #endif
@@ -1802,12 +1859,15 @@ __device__ __forceinline__ uint32_t large_bin(const Ctx& c, uint32_t wd, int f) 
   return c.XbT ? (uint32_t)c.XbT[(int64_t)f * c.n + row] : (uint32_t)c.Xb[(int64_t)row * c.ld + f];
 }
 
-template <int MODE>
+template <int MODE, bool PK>
 __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
   using CT = typename HT<MODE>::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int slot = DML_LSLOT;
   const LState& st = c.lstate[slot];
+  // node state read once (the loop's bscr stores could alias it: a reference would reload it)
+  const int st_pos = __builtin_amdgcn_readfirstlane(st.pos);
+  const int64_t st_start = st.on.start;
   if (st.done) return;
   const int r0 = DML_LCHUNK * c.chunk;
   if (r0 >= st.on.count) return;
@@ -1825,40 +1885,70 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
   const float* ty = tree_y(c, s);
   constexpr int KGL = 16;
   if (g <= KGL) {
-    // 2-deep software pipeline (see k_nodes): next row's bins/payload and the row id two
-    // steps ahead are in flight while this row's histogram atomics run
+    // ping-pong software pipeline with compile-time-counted unconditional gathers (the block
+    // tier's loop in k_nodes): the row id two steps ahead and the next step's bins are in
+    // flight while this step's histogram atomics run, with no vmcnt(0) drain between steps
     constexpr uint32_t INV = 0xFFFFFFFFu;
-    int fj[KGL];
-#pragma unroll
-    for (int j = 0; j < KGL; ++j) fj[j] = j < g ? (int)feats[j] : 0;
-    auto row_at = [&](int r) -> uint32_t { return r < r1 ? rows[r] : INV; };
-    const int t0 = r0 + (int)threadIdx.x;
-    uint32_t ra = row_at(t0), rbn = row_at(t0 + 256);
     using PL = typename PLT<MODE>::T;
-    PL pa = ra != INV ? word_payload<MODE>(c, s, ty, ra) : PL{};
-    uint32_t ba[KGL];
+    const int t0 = r0 + (int)threadIdx.x;
+    auto run = [&](auto Gc) {
+      constexpr int G = decltype(Gc)::value;
+      // feature offsets: feature-major copy (stride n) when present, else the row line
+      const bool fm = c.XbT != nullptr;
+      int64_t fo[G];
 #pragma unroll
-    for (int j = 0; j < KGL; ++j) ba[j] = (j < g && ra != INV) ? large_bin(c, ra, fj[j]) : 0u;
-    for (int r = t0; r < r1; r += 256) {
-      const PL pb = rbn != INV ? word_payload<MODE>(c, s, ty, rbn) : PL{};
-      uint32_t bb[KGL];
-#pragma unroll
-      for (int j = 0; j < KGL; ++j) bb[j] = (j < g && rbn != INV) ? large_bin(c, rbn, fj[j]) : 0u;
-      const uint32_t rc2 = row_at(r + 512);
-      if (ra != INV && st.pos == 0) {   // round 0: bins of visiting positions 0..15 (Ctx::bscr)
-        uint4 v;
-        v.x = ba[0] | ba[1] << 8 | ba[2] << 16 | ba[3] << 24;
-        v.y = ba[4] | ba[5] << 8 | ba[6] << 16 | ba[7] << 24;
-        v.z = ba[8] | ba[9] << 8 | ba[10] << 16 | ba[11] << 24;
-        v.w = ba[12] | ba[13] << 8 | ba[14] << 16 | ba[15] << 24;
-        *(uint4*)(c.bscr + (st.on.start + r) * 16) = v;
+      for (int j = 0; j < G; ++j) {
+        const int64_t f = __builtin_amdgcn_readfirstlane((int)feats[j < g ? j : 0]);
+        fo[j] = fm ? f * c.n : f;
       }
+      const uint8_t* tab = fm ? c.XbT : c.Xb;
+      const int64_t rstride = fm ? 1 : c.ld;
+      auto row_at = [&](int r) -> uint32_t {
+        const uint32_t v = rows[min(r, r1 - 1)];
+        return r < r1 ? v : INV;
+      };
+      auto gather = [&](uint32_t wd, uint32_t* b) {
+        const uint8_t* xr = tab + (int64_t)(wd != INV ? (wd & c.rmask) : 0u) * rstride;
 #pragma unroll
-      for (int j = 0; j < KGL; ++j)
-        if (j < g) hist_add<MODE>(hist + j * span, c, (int)ba[j], pa);
-      ra = rbn; rbn = rc2; pa = pb;
+        for (int j = 0; j < G; ++j) b[j] = (uint32_t)xr[fo[j]];
+      };
+      auto consume = [&](int r, bool valid, const uint32_t* b, const PL& pl) {
+        if (!valid) return;
+        if (st_pos == 0) {   // round 0: bins of visiting positions 0..15 (Ctx::bscr)
+          uint32_t w4[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-      for (int j = 0; j < KGL; ++j) ba[j] = bb[j];
+          for (int j = 0; j < G && j < 16; ++j) w4[j >> 2] |= (j < g ? b[j] & 0xFFu : 0u) << (8 * (j & 3));
+          *(uint4*)(c.bscr + (st_start + r) * 16) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+          if (j < g) hist_add<MODE>(hist + j * span, c, (int)b[j], pl);
+      };
+      uint32_t rA = row_at(t0), rB = row_at(t0 + 256);
+      uint32_t bA[G], bB[G];
+      gather(rA, bA);
+      bool vA = rA != INV, vB = false;
+      PL pA = vA ? word_payload<MODE, PK>(c, s, ty, rA) : PL{}, pB{};
+      for (int r = t0; r < r1; r += 512) {
+        rA = row_at(r + 512);
+        gather(rB, bB);
+        vB = rB != INV;
+        pB = vB ? word_payload<MODE, PK>(c, s, ty, rB) : PL{};
+        consume(r, vA, bA, pA);
+        rB = row_at(r + 768);
+        gather(rA, bA);
+        vA = rA != INV;
+        pA = vA ? word_payload<MODE, PK>(c, s, ty, rA) : PL{};
+        consume(r + 256, vB, bB, pB);
+      }
+    };
+    switch (g) {
+#define DML_G_CASE(N) case N: run(std::integral_constant<int, N>{}); break;
+      DML_G_CASE(1) DML_G_CASE(2) DML_G_CASE(3) DML_G_CASE(4) DML_G_CASE(5) DML_G_CASE(6) DML_G_CASE(7)
+      DML_G_CASE(8) DML_G_CASE(9) DML_G_CASE(10) DML_G_CASE(11) DML_G_CASE(12) DML_G_CASE(13) DML_G_CASE(14)
+      DML_G_CASE(15)
+#undef DML_G_CASE
+      default: run(std::integral_constant<int, KGL>{}); break;
     }
   } else {
     for (int r = r0 + threadIdx.x; r < r1; r += 256) {
@@ -2525,7 +2615,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       HIP_OK(hipFuncSetAttribute((const void*)k_nodes<64, MODE, FCX>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_nodes<DML_BLOCK_NT, MODE, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_nodes<DML_BLOCK_NT, MODE, FCX>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_hist_large<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_hist_large<MODE, false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_hist_large<MODE, true>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_split_large<GM>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       attr_set[MODE] = need;
     }
@@ -2574,7 +2665,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
         HIP_OK(hipMemsetAsync(c.ghist, 0, (size_t)nL * a->kg_large * ghist_feat_bytes(MODE, CH), st));
         HIP_OK(hipMemsetAsync(c.counters + kNeedMore, 0, 4, st));
         const dim3 gh = DML_LARGE_NODE_FAST ? dim3((unsigned)nL, nchunks) : dim3(nchunks, (unsigned)nL);
-        k_hist_large<MODE><<<gh, 256, lds_hl, st>>>(c);
+        if (c.packed) k_hist_large<MODE, true><<<gh, 256, lds_hl, st>>>(c);
+        else k_hist_large<MODE, false><<<gh, 256, lds_hl, st>>>(c);
         k_split_large<GM><<<nL, 256, lds_sl, st>>>(c, cur);
         HIP_OK(hipMemcpyAsync(h + 32, c.counters + kNeedMore, 4, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
