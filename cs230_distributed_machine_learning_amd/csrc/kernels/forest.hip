@@ -127,6 +127,11 @@ struct ForestArgs {
   int64_t nbound;        // double [pool_cap][2] node bounds (lo, hi) when mono != 0
   int64_t fast_crit;     // 1 + the single criterion of a build with no class weights, monotonic
                          // constraints or min_weight_fraction_leaf (node kernels specialised on it); 0 = generic
+  // early predict: a host PredictArgs for the build's fits (0 = none) and a host int32[n_fits]
+  // of the level after which fit f's trees are complete (its max_depth - 1); the builder
+  // launches fit f's predict right after that level on its own stream, overlapping the
+  // deeper fits' remaining levels, and marks the entry -2
+  int64_t early_pred, fit_done_level, n_fits;
 };
 
 constexpr int kTiers = 4;  // 0 subtree, 1 wave, 2 block, 3 large
@@ -2480,6 +2485,19 @@ static SideStreams* side_streams() {
   return &ss;
 }
 
+static hipEvent_t pred_event() {
+  static hipEvent_t e = nullptr;
+  if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+  return e;
+}
+
+// stream of the early per-fit predicts (forest.hip build_impl)
+static hipStream_t pred_stream() {
+  static hipStream_t s = nullptr;
+  if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+  return s;
+}
+
 static int32_t* pinned_counters() {
   static int32_t* p = nullptr;
   if (!p) {
@@ -2514,6 +2532,9 @@ __global__ void k_test_wave_prims(const uint32_t* in, uint32_t* out) {
   o[9 * 64 + lane] = (uint32_t)wave::shift_down1<int>((int)v, lane, -1);
   o[10 * 64 + lane] = (uint32_t)wave::min_u64(((uint64_t)v << 32) | (uint32_t)lane, lane);
 }
+
+struct PredictArgs;
+extern "C" int dml_forest_predict_fit(const PredictArgs* a, int32_t f, hipStream_t st);
 
 extern "C" {
 
@@ -2686,6 +2707,21 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       k_compact<<<(unsigned)((nst + 1023) / 1024), 256, 0, st>>>(c, 1 - cur, nst);
     }
     HIP_OK(hipGetLastError());
+    if (a->early_pred && a->fit_done_level) {   // fits complete after this level: predict them now
+      int32_t* done = (int32_t*)a->fit_done_level;
+      hipStream_t ps = pred_stream();
+      bool any = false;
+      for (int64_t f = 0; f < a->n_fits && ps; ++f) {
+        if (done[f] != levels - 1) continue;
+        if (!any) {
+          HIP_OK(hipEventRecord(pred_event(), st));
+          HIP_OK(hipStreamWaitEvent(ps, pred_event(), 0));
+          any = true;
+        }
+        if (dml_forest_predict_fit((const PredictArgs*)a->early_pred, (int32_t)f, ps) != 0) return 11;
+        done[f] = -2;
+      }
+    }
     uint32_t* t = c.rows_cur; c.rows_cur = c.rows_next; c.rows_next = t;
     cur = 1 - cur;
   }
@@ -2696,6 +2732,10 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     const int64_t P = std::min<int64_t>(h[kPool], a->pool_cap);
     k_mono_clip<<<(unsigned)((P + 255) / 256), 256, 0, st>>>(c, P);
     HIP_OK(hipGetLastError());
+  }
+  if (a->early_pred && pred_stream()) {   // later work on st sees the early predicts' outputs
+    HIP_OK(hipEventRecord(pred_event(), pred_stream()));
+    HIP_OK(hipStreamWaitEvent(st, pred_event(), 0));
   }
   a->levels_out = levels;
   a->large_rounds_out = large_rounds;

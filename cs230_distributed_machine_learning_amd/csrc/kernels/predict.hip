@@ -27,6 +27,7 @@ struct PredictArgs {
   int64_t F, max_rows;
   int64_t d;          // features (bins per row actually read)
   int64_t lds_pitch;  // set by dml_forest_predict: LDS row stride, 0 = no staging
+  int64_t fit_row_off_host;   // optional host copy of fit_row_off (per-fit grid sizes)
 };
 
 // leaf of U consecutive trees [t0, t0 + u_n) for one row, walked in lock-step: the U
@@ -371,6 +372,20 @@ int dml_forest_predict(PredictArgs* a, hipStream_t st) {
   if (u == 16) return launch_predict<16>(a, st);
   if (u == 4) return launch_predict<4>(a, st);
   return launch_predict<8>(a, st);
+}
+
+// predict fit f alone (its trees and held-out rows; outputs stay at their absolute rows) --
+// the forest builder calls this for a fit whose trees are complete while deeper fits of the
+// same build are still growing (forest.hip early predict)
+int dml_forest_predict_fit(const PredictArgs* a, int32_t f, hipStream_t st) {
+  if (f < 0 || f >= a->F) return 2;
+  const int64_t* roff = (const int64_t*)a->fit_row_off_host;
+  PredictArgs b = *a;
+  b.fit_tree_off = a->fit_tree_off + 4 * (int64_t)f;   // int32[F+1] device array, advanced to fit f
+  b.fit_row_off = a->fit_row_off + 8 * (int64_t)f;     // int64[F+1]
+  b.F = 1;
+  b.max_rows = roff ? roff[f + 1] - roff[f] : a->max_rows;
+  return dml_forest_predict(&b, st);
 }
 
 int dml_scores(ScoreArgs* a, hipStream_t st) {

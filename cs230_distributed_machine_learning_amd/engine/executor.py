@@ -28,6 +28,7 @@ import torch
 
 from ..models.base import FitOutput, FitTask, ParamError, family_of, is_classifier
 from ..search import scoring as scoring_mod
+from ..utils import trace
 from ..search.cv import make_split_roles
 
 
@@ -98,7 +99,8 @@ def _scores_for(data, task: FitTask, out: FitOutput, scorer: str):
 
 def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[CandidateResult]:
     """Run every split of the given candidates; returns one result per candidate."""
-    names = prepare_splits(data, spec)
+    with trace.range("run_prepare"):
+        names = prepare_splits(data, spec)
     clf = is_classifier(spec.model_type)
     fam = family_of(spec.model_type)
     self_scored = spec.model_type in getattr(fam, "self_scored", ())
@@ -117,7 +119,8 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
     sharded = getattr(data, "is_row_shard", False)
     if sharded and not getattr(fam, "data_parallel", False):
         raise ValueError(f"{spec.model_type} has no row-sharded (data-parallel) fit; run it task-parallel")
-    tasks, errors = build_tasks(data, spec, candidate_ids)
+    with trace.range("run_tasks"):
+        tasks, errors = build_tasks(data, spec, candidate_ids)
     if scoring_mod.needs_proba(scorer):   # families that only predict labels by default add probabilities
         for t in tasks:
             t.need_proba = True
@@ -133,7 +136,9 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
     outputs: Dict[int, FitOutput] = {}
     if tasks:
         try:
-            for o in fam.run(data, tasks, keep_models=keep):
+            with trace.range("run_family"):
+                fam_out = fam.run(data, tasks, keep_models=keep)
+            for o in fam_out:
                 outputs[o.task_id] = o
             if sharded:   # rank-local held-out predictions -> the global prediction vectors
                 data.gather_outputs(tasks, outputs)
@@ -174,7 +179,8 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
                     break
                 cv_scores.append(float(spec.error_score) if spec.error_score is not None else float("nan"))
                 continue
-            cv_scores.append(_scores_for(data, t, o, scorer))
+            with trace.range("run_scores"):
+                cv_scores.append(_scores_for(data, t, o, scorer))
             for w in o.info.get("warnings", []):
                 if w not in warnings:
                     warnings.append(w)

@@ -274,7 +274,8 @@ class ForestFamily(Family):
                 ymin = float(data.all_reduce(torch.tensor([ymin], dtype=torch.float64, device=data.device), "min")[0])
             if ymin < 0:   # sklearn raises the same
                 raise ParamError("Some value(s) of y are negative which is not allowed for Poisson regression.")
-        Xb = data.binned()
+        with trace.range("forest_plan"):
+            Xb = data.binned()
         sharded = getattr(data, "is_row_shard", False)
         if sharded:
             for t in tasks:   # the row-sharded builder sums histograms; medians need every row
@@ -288,7 +289,8 @@ class ForestFamily(Family):
         # absolute_error trees grow on the host builder (forest_cpu.cpp): batch them apart
         tasks_in = tasks
         tasks = sorted(tasks, key=_host_only)
-        budget = self._budget(data)
+        with trace.range("forest_budget"):
+            budget = self._budget(data)
         if sharded:   # every rank must form the SAME batches: the smallest budget of the group
             budget = float(data.all_reduce(torch.tensor([budget], dtype=torch.float64, device=data.device), "min")[0])
         # row shard: trees per level-synchronous build -- the (tree, row) pair arrays take
@@ -407,6 +409,29 @@ class ForestFamily(Family):
             i += n
         return tab
 
+    def _early_predict(self, data, Xb, batch: List[FitTask], is_reg: bool, mono):
+        """(make, done) for build_gpu's early predict, or None: fit f of depth-limited trees
+        is complete after builder level max_depth - 1."""
+        if os.environ.get("DML_EARLY_PREDICT", "1") == "0" or not _early_ok(data, batch, is_reg, mono):
+            return None
+        done = np.array([t.params["max_depth"] - 1 if t.params["max_depth"] < forest_ops.INT32_MAX else 1 << 30
+                         for t in batch], dtype=np.int32)
+        if not np.any(done < (1 << 30)):
+            return None
+        toff = np.zeros(len(batch) + 1, dtype=np.int64)
+        np.cumsum([t.params["n_estimators"] for t in batch], out=toff[1:])
+        rows = [data.test_rows[t.split] for t in batch]
+        roff = np.zeros(len(batch) + 1, dtype=np.int64)
+        np.cumsum([int(r.numel()) for r in rows], out=roff[1:])
+        rows_cat = torch.cat(rows) if rows else torch.empty(0, dtype=torch.int32, device=data.device)
+        want_proba = (not is_reg) and any(t.need_proba for t in batch)
+        C = data.n_classes
+        VC = 3 if is_reg else C
+        def make(nodes, vals):
+            return forest_ops.GpuPredict(nodes, vals, VC, is_reg, C, Xb, toff, roff, rows_cat, want_proba)
+
+        return make, done
+
     def _run_batch(self, data, Xb, batch: List[FitTask], is_reg: bool, keep_models: bool,
                    tree_chunk: int | None = None) -> List[FitOutput]:
         specs = self._specs(batch)
@@ -431,10 +456,11 @@ class ForestFamily(Family):
                 fb.vals = torch.from_numpy(fb.vals).to(data.device)
         elif data.is_gpu:
             # monotonic_cst grows on the HIP builder too (per-node bounds in every tier)
+            mono = _mono_table(batch, Xb.shape[1], is_reg)
+            early = self._early_predict(data, Xb, batch, is_reg, mono)
             fb = forest_ops.build_gpu(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
                                       data.n_classes, is_reg, self.tiers, reuse_pool=True,
-                                      XbT=data.binned_feature_major(), cw=cw,
-                                      mono=_mono_table(batch, Xb.shape[1], is_reg))
+                                      XbT=data.binned_feature_major(), cw=cw, mono=mono, early_predict=early)
         else:
             fb = forest_ops.build_cpu(Xb.numpy(), data.y_enc, None if not is_reg else data.y_reg.numpy(),
                                       data.roles_np(), specs, data.n_classes, is_reg, cw=cw,
@@ -464,7 +490,14 @@ class ForestFamily(Family):
             np.cumsum([int(r.numel()) for r in rows], out=roff[1:])
             want_proba = (not is_reg) and any(t.need_proba for t in batch)
             proba = None
-            if data.is_gpu:
+            gp = getattr(fb, "predict", None)
+            if gp is not None:
+                # the builder already predicted the fits whose trees were complete before the
+                # last level (ForestArgs.early_pred); the deeper ones are predicted here
+                done = fb.early_done
+                gp.run([f for f in range(len(batch)) if done[f] != -2])
+                pred = gp.result()
+            elif data.is_gpu:
                 rows_cat = torch.cat(rows) if rows else torch.empty(0, dtype=torch.int32, device=data.device)
                 pred = forest_ops.predict(fb, Xb, toff, roff, rows_cat, want_proba=want_proba)
             else:
@@ -490,6 +523,18 @@ class ForestFamily(Family):
             return outs
         finally:   # the node pool is an arena slot: free it for the next batch
             forest_ops.release_pool(fb)
+
+
+def _early_ok(data, batch: List[FitTask], is_reg: bool, mono) -> bool:
+    """A batch whose fits can be predicted by the builder as soon as their trees are
+    complete: nothing rewrites the trees after growth (no max_leaf_nodes / ccp pruning, no
+    monotonic clip, no midpoint refinement of exactly-binned features)."""
+    if mono is not None or any(t.params.get("max_leaf_nodes") or t.params.get("ccp_alpha", 0.0) > 0 for t in batch):
+        return False
+    if getattr(data, "_refine_needed", None) is None:
+        _vals, exact = data.bin_values()
+        data._refine_needed = bool(exact.any())
+    return not data._refine_needed
 
 
 def _host_only(t: FitTask) -> bool:

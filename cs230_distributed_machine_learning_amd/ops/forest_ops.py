@@ -241,11 +241,16 @@ def reg_exponents_of(max_abs_y: float, n: int) -> tuple[int, int]:
 def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,
               specs: np.ndarray, n_classes: int, is_reg: bool, tiers: ForestTiers | None = None,
               ystride: int = 0, reuse_pool: bool = False, XbT: Optional[torch.Tensor] = None,
-              cw: Optional[np.ndarray] = None, mono: Optional[np.ndarray] = None) -> ForestBuild:
+              cw: Optional[np.ndarray] = None, mono: Optional[np.ndarray] = None,
+              early_predict=None) -> ForestBuild:
     """``ystride > 0``: ``yreg`` is a [targets, ystride] matrix and tree t regresses on
     row ``specs[t]['target']`` (gradient boosting's per-fit pseudo-residuals).
     ``reuse_pool``: the node arrays live in the device arena and are valid until the
-    next ``reuse_pool`` build on this device (the caller must be done with them)."""
+    next ``reuse_pool`` build on this device (the caller must be done with them).
+    ``early_predict``: (make(nodes, vals) -> GpuPredict, done int32[F]) -- fit f is predicted
+    by the builder right after level done[f] (its trees are complete by then), overlapping the
+    deeper fits; entries it launched come back as -2 (``ForestBuild.predict`` holds the
+    GpuPredict; the caller predicts the other fits)."""
     lib = native.hip_lib()
     dev = Xb.device
     T = len(specs)
@@ -347,6 +352,14 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
                 nbound[:, 1] = math.inf
                 a.nbound = native.ptr(nbound)
             a.status_out = 0
+            gp = None
+            if early_predict is not None:   # (re)armed per attempt: a pool retry regrows from scratch
+                make, done = early_predict
+                if _attempt == 0:
+                    done0 = done.copy()
+                done[:] = done0
+                gp = make(nodes, vals)
+                a.early_pred, a.fit_done_level, a.n_fits = ctypes.addressof(gp.args), done.ctypes.data, len(done)
             with trace.range("forest_build"):   # host-side launch sequence of every tier
                 rc = lib.dml_forest_build(ctypes.byref(a), stream)
             if rc:
@@ -374,6 +387,9 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
              "rows_total": int(a.rows_total), "build_s": time.perf_counter() - t0, "pool_retries": retries,
              "tier_nodes": [int(a.tier0_nodes), int(a.tier1_nodes), int(a.tier2_nodes), int(a.tier3_nodes)]}
     fb = ForestBuild(nodes[:P], vals[:P], T, VC, is_reg, n_classes, stats)
+    if early_predict is not None:
+        fb.predict = gp
+        fb.early_done = early_predict[1]
     if slot is not None:
         fb.arena_dev = dev   # release_pool(fb) hands the arena slot back
         fb.arena_slot = slot
@@ -564,31 +580,62 @@ def apply(fb: ForestBuild, Xb, t0: int = 0, T: Optional[int] = None):
     return leaf
 
 
+class GpuPredict:
+    """A GPU predict of F fits set up before (or after) their build: device offset arrays,
+    output buffers and the ``PredictArgs`` block.  ``run(fits)`` predicts a subset of the
+    fits (one launch each); the forest builder takes ``args`` and predicts a fit itself as
+    soon as its trees are complete (ForestArgs.early_pred)."""
+
+    def __init__(self, nodes, vals, VC: int, is_reg: bool, n_classes: int, Xb, fit_tree_off, fit_row_off, rows,
+                 want_proba: bool = False):
+        dev = Xb.device
+        F = len(fit_tree_off) - 1
+        total = int(fit_row_off[-1])
+        C = n_classes
+        self.dev, self.F = dev, F
+        self.toff = torch.from_numpy(np.asarray(fit_tree_off, dtype=np.int32)).to(dev)
+        self.roff_host = np.ascontiguousarray(fit_row_off, dtype=np.int64)
+        self.roff = torch.from_numpy(self.roff_host).to(dev)
+        self.rows = rows if isinstance(rows, torch.Tensor) else torch.from_numpy(np.asarray(rows, np.int32)).to(dev)
+        self.out = torch.empty(total, dtype=torch.float32 if is_reg else torch.int32, device=dev)
+        self.proba = torch.empty((total, C), dtype=torch.float32, device=dev) if (want_proba and not is_reg) else None
+        p = native.PredictArgs()
+        p.Xb, p.ld = native.ptr(Xb), Xb.stride(0)
+        p.nodes, p.node_val, p.VC, p.is_reg, p.n_classes = native.ptr(nodes), native.ptr(vals), VC, int(is_reg), C
+        p.fit_tree_off, p.fit_row_off, p.rows = native.ptr(self.toff), native.ptr(self.roff), native.ptr(self.rows)
+        p.out_pred, p.out_proba = native.ptr(self.out), native.ptr(self.proba)
+        p.F = F
+        p.d = int(Xb.shape[1])
+        p.max_rows = int(np.max(np.diff(self.roff_host))) if F else 0
+        p.fit_row_off_host = self.roff_host.ctypes.data
+        self.args = p
+
+    def run(self, fits=None) -> None:
+        lib = native.hip_lib()
+        st = native.stream_handle(self.dev)
+        with trace.range("forest_predict"):
+            if fits is None:
+                rc = lib.dml_forest_predict(ctypes.byref(self.args), st)
+            else:
+                rc = 0
+                for f in fits:
+                    rc = rc or lib.dml_forest_predict_fit(ctypes.byref(self.args), int(f), st)
+        if rc:
+            raise RuntimeError(f"dml_forest_predict failed ({rc})")
+
+    def result(self):
+        return (self.out, self.proba) if self.proba is not None else self.out
+
+
 def predict(fb: ForestBuild, Xb, fit_tree_off: np.ndarray, fit_row_off: np.ndarray, rows, want_proba: bool = False):
     """Predict rows for F fits; trees of fit f are [fit_tree_off[f], fit_tree_off[f+1])."""
     F = len(fit_tree_off) - 1
     total = int(fit_row_off[-1])
     C = fb.n_classes
     if fb.on_gpu:
-        dev = Xb.device
-        lib = native.hip_lib()
-        toff = torch.from_numpy(np.asarray(fit_tree_off, dtype=np.int32)).to(dev)
-        roff = torch.from_numpy(np.asarray(fit_row_off, dtype=np.int64)).to(dev)
-        rows_t = rows if isinstance(rows, torch.Tensor) else torch.from_numpy(np.asarray(rows, np.int32)).to(dev)
-        out = torch.empty(total, dtype=torch.float32 if fb.is_reg else torch.int32, device=dev)
-        proba = torch.empty((total, C), dtype=torch.float32, device=dev) if (want_proba and not fb.is_reg) else None
-        p = native.PredictArgs()
-        p.Xb, p.ld = native.ptr(Xb), Xb.stride(0)
-        p.nodes, p.node_val, p.VC, p.is_reg, p.n_classes = native.ptr(fb.nodes), native.ptr(fb.vals), fb.VC, int(fb.is_reg), C
-        p.fit_tree_off, p.fit_row_off, p.rows = native.ptr(toff), native.ptr(roff), native.ptr(rows_t)
-        p.out_pred, p.out_proba = native.ptr(out), native.ptr(proba)
-        p.F = F
-        p.d = int(Xb.shape[1])
-        p.max_rows = int(np.max(np.diff(fit_row_off))) if F else 0
-        with trace.range("forest_predict"):
-            rc = lib.dml_forest_predict(ctypes.byref(p), native.stream_handle(dev))
-        if rc:
-            raise RuntimeError(f"dml_forest_predict failed ({rc})")
+        gp = GpuPredict(fb.nodes, fb.vals, fb.VC, fb.is_reg, C, Xb, fit_tree_off, fit_row_off, rows, want_proba)
+        gp.run()
+        out, proba = gp.out, gp.proba
         return (out, proba) if want_proba else out
     lib = native.cpu_lib()
     Xb = np.ascontiguousarray(Xb)

@@ -73,13 +73,14 @@ ForestArgs = _i64_struct(
         "ystride", "XbT", "cw",
         "yq_e1", "yq_e2",
         "mono", "nbound", "fast_crit",
+        "early_pred", "fit_done_level", "n_fits",
     ],
 )
 
 PredictArgs = _i64_struct(
     "PredictArgs",
     ["Xb", "ld", "nodes", "node_val", "VC", "is_reg", "n_classes", "fit_tree_off", "fit_row_off", "rows",
-     "out_pred", "out_proba", "F", "max_rows", "d", "lds_pitch"],
+     "out_pred", "out_proba", "F", "max_rows", "d", "lds_pitch", "fit_row_off_host"],
 )
 
 ScoreArgs = _i64_struct("ScoreArgs", ["rows", "fit_row_off", "pred", "ycls", "yreg", "is_reg", "out", "F"])
@@ -171,6 +172,8 @@ def hip_lib() -> ctypes.CDLL:
             lib.dml_forest_build.argtypes = [ctypes.POINTER(ForestArgs), c_vp]
             lib.dml_forest_predict.restype = c_i32
             lib.dml_forest_predict.argtypes = [ctypes.POINTER(PredictArgs), c_vp]
+            lib.dml_forest_predict_fit.restype = c_i32
+            lib.dml_forest_predict_fit.argtypes = [ctypes.POINTER(PredictArgs), c_i32, c_vp]
             lib.dml_scores.restype = c_i32
             lib.dml_scores.argtypes = [ctypes.POINTER(ScoreArgs), c_vp]
             lib.dml_bin.restype = c_i32
