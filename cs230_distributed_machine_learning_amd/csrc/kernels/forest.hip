@@ -52,6 +52,9 @@
 #ifndef DML_KGMAX_WAVE
 #define DML_KGMAX_WAVE 4
 #endif
+#ifndef DML_ROW_WINDOWS
+#define DML_ROW_WINDOWS 1      // block tier: whole-row dwordx4 loads for the first feature group (d <= 112)
+#endif
 #ifndef DML_GINI_PF
 #define DML_GINI_PF 1          // binary Gini: fp32 pre-filter of candidate bins (eval_feature)
 #endif
@@ -1044,6 +1047,82 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
           consume(base + NT, vB, bB, pB);         // chunk k+1
         }
       };
+      // d <= 112 on 16-B aligned rows, first group of >= 8 features: the whole row line comes
+      // in as 7 dwordx4 loads (7 cache-line lookups per row instead of g >= 8 byte gathers --
+      // the gathers are lookup-bound, one line per CU clock) and each feature's byte is
+      // picked out of the 28 loaded dwords by a uniform register index
+      auto runw = [&](auto Gc) {
+        constexpr int G = decltype(Gc)::value;
+        typedef uint32_t v32u __attribute__((ext_vector_type(32)));
+        int fdw[G], fsh[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          const int f = __builtin_amdgcn_readfirstlane((int)feats[j < g ? j : 0]);
+          fdw[j] = f >> 2;
+          fsh[j] = (f & 3) * 8;
+        }
+        auto row_at = [&](int r) -> uint32_t {
+          const uint32_t v = rows[min(r, cnt - 1)];
+          return r < cnt ? v : INV;
+        };
+        auto load_win = [&](uint32_t r, v32u& w) {
+          const uint4* xr = (const uint4*)(c.Xb + (int64_t)(r != INV ? (r & c.rmask) : 0u) * c.ld);
+#pragma unroll
+          for (int k = 0; k < 7; ++k) {
+            const uint4 q = xr[k];
+            w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w;
+          }
+        };
+        auto extract = [&](const v32u& w, uint32_t* b) {
+#pragma unroll
+          for (int j = 0; j < G; ++j) b[j] = (w[fdw[j]] >> fsh[j]) & 0xFFu;
+        };
+        auto consume = [&](int base, bool valid, const uint32_t* b, const PL& pl) {
+          if (NT == 256 && pos == 0 && valid) {
+            uint32_t w4[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < G && j < 16; ++j) w4[j >> 2] |= (j < g ? b[j] : 0u) << (8 * (j & 3));
+            *(uint4*)(c.bscr + (on.start + base + tid) * 16) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+          }
+          if (valid) {
+#pragma unroll
+            for (int j = 0; j < G; ++j)
+              if (j < g) hist_add<MODE>(hist + j * span, c, (int)b[j], pl);
+          }
+        };
+        v32u win;
+        uint32_t bA[G], bB[G];
+        uint32_t rA = row_at(tid), rB = row_at(NT + tid);
+        load_win(rA, win);
+        extract(win, bA);
+        bool vA = rA != INV, vB = false;
+        PL pA = vA ? word_payload<MODE, PK>(c, s, ty, rA) : PL{}, pB{};
+        for (int base = 0; base < cnt; base += 2 * NT) {
+          load_win(rB, win);                      // chunk k+1's row lines
+          rA = row_at(base + 2 * NT + tid);       // chunk k+2's row id
+          consume(base, vA, bA, pA);              // chunk k
+          extract(win, bB);
+          vB = rB != INV;
+          pB = vB ? word_payload<MODE, PK>(c, s, ty, rB) : PL{};
+          load_win(rA, win);                      // chunk k+2's row lines
+          rB = row_at(base + 3 * NT + tid);       // chunk k+3's row id
+          consume(base + NT, vB, bB, pB);         // chunk k+1
+          extract(win, bA);
+          vA = rA != INV;
+          pA = vA ? word_payload<MODE, PK>(c, s, ty, rA) : PL{};
+        }
+      };
+      if (DML_ROW_WINDOWS && NT == 256 && pos == 0 && g >= 8 && d <= 112 && (c.ld & 15) == 0 && c.ld >= 112 &&
+          (((uintptr_t)c.Xb) & 15) == 0) {
+        switch (g) {
+          case 8: runw(std::integral_constant<int, (8 < KGMAX ? 8 : KGMAX)>{}); break;
+          case 9: runw(std::integral_constant<int, (9 < KGMAX ? 9 : KGMAX)>{}); break;
+          case 10: runw(std::integral_constant<int, (10 < KGMAX ? 10 : KGMAX)>{}); break;
+          case 11: runw(std::integral_constant<int, (11 < KGMAX ? 11 : KGMAX)>{}); break;
+          case 12: runw(std::integral_constant<int, (12 < KGMAX ? 12 : KGMAX)>{}); break;
+          default: runw(std::integral_constant<int, KGMAX>{}); break;
+        }
+      } else
       // one instantiation per group size: an extra load per row is an extra cache-line lookup,
       // and the gathers are lookup-bound (one line per CU clock)
       switch (g) {

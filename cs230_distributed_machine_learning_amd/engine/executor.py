@@ -64,6 +64,9 @@ class CandidateResult:
 
 
 def prepare_splits(data, spec: JobSpec) -> List[str]:
+    key = spec.split_key()
+    if key is not None and getattr(data, "_split_key", None) == key and getattr(data, "split_names", None):
+        return list(data.split_names)   # the resident split roles are this job's (every slice re-asks)
     roles, names = make_split_roles(data.y_host, spec.cv if spec.cv else 0, is_classifier(spec.model_type),
                                     holdout=spec.holdout, test_size=spec.test_size,
                                     random_state=spec.random_state)
