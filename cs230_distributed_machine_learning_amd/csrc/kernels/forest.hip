@@ -55,6 +55,9 @@
 #ifndef DML_ROW_WINDOWS
 #define DML_ROW_WINDOWS 1      // block tier: whole-row dwordx4 loads for the first feature group (d <= 112)
 #endif
+#ifndef DML_WAVE_WIN_ROWS
+#define DML_WAVE_WIN_ROWS 4    // wave tier: rows whose line windows are in flight together (1, 2 or 4; 0 = byte gathers)
+#endif
 #ifndef DML_GINI_PF
 #define DML_GINI_PF 1          // binary Gini: fp32 pre-filter of candidate bins (eval_feature)
 #endif
@@ -941,6 +944,41 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   if constexpr (KPRE > 0) {
     if (reg_rows) {
       npre = min(KPRE, min(k + slack, d));
+      if (DML_ROW_WINDOWS && DML_WAVE_WIN_ROWS > 0 && npre >= 8 && d <= 112 && (c.ld & 15) == 0 && c.ld >= 112 &&
+          (((uintptr_t)c.Xb) & 15) == 0) {
+        // whole row lines (7 dwordx4 loads = 7 cache-line lookups per row instead of npre byte
+        // gathers), DML_WAVE_WIN_ROWS rows' lines in flight at a time, each prefetched
+        // position's byte picked out by a uniform register index
+        typedef uint32_t v32u __attribute__((ext_vector_type(32)));
+        int fdw[KPRE], fsh[KPRE];
+#pragma unroll
+        for (int q = 0; q < KPRE; ++q) {
+          const int f = __builtin_amdgcn_readfirstlane(q < npre ? feature_at(fp, q, d) : 0);
+          fdw[q] = f >> 2;
+          fsh[q] = (f & 3) * 8;
+          pre[q] = 0u;
+        }
+        constexpr int WR = DML_WAVE_WIN_ROWS > 0 ? DML_WAVE_WIN_ROWS : 1;
+#pragma unroll
+        for (int u0 = 0; u0 < RPT; u0 += WR) {
+          v32u w[WR];
+#pragma unroll
+          for (int uu = 0; uu < WR; ++uu) {
+            const uint32_t r = rrow[u0 + uu];
+            const uint4* xr = (const uint4*)(c.Xb + (int64_t)(r != 0xFFFFFFFFu ? (r & c.rmask) : 0u) * c.ld);
+#pragma unroll
+            for (int k7 = 0; k7 < 7; ++k7) {
+              const uint4 qv = xr[k7];
+              w[uu][4 * k7] = qv.x; w[uu][4 * k7 + 1] = qv.y; w[uu][4 * k7 + 2] = qv.z; w[uu][4 * k7 + 3] = qv.w;
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < KPRE; ++q)
+            if (q < npre)
+#pragma unroll
+              for (int uu = 0; uu < WR; ++uu) pre[q] |= ((w[uu][fdw[q]] >> fsh[q]) & 0xFFu) << (8 * (u0 + uu));
+        }
+      } else {
       uint32_t raw[KPRE][RPT];
       // row lines of the lane's rows (an absent row reads row 0: every load is unconditional)
       const uint8_t* xr[RPT];
@@ -963,6 +1001,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
 #pragma unroll
         for (int u = 0; u < RPT; ++u) v |= raw[q][u] << (8 * u);
         pre[q] = v;
+      }
       }
     }
   }
