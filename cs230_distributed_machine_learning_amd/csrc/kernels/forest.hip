@@ -1847,7 +1847,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
       const int src = jx < cnt ? cidx[jx] : 0;
       const int cls_j = __shfl(my_cls, src);
       const uint32_t w_j = (uint32_t)__shfl((int)(uint32_t)my_w, src);
-#ifdef DML_X2_SUB   // sensitivity build: every segmented evaluation twice (the first into copies)
+#if defined(DML_X2_SUB) && DML_X2_SUB != 2   // sensitivity build: every segmented evaluation twice (the first into copies)
       {
         int nc2 = nonconst, bf2 = best_f, bb2 = best_b;
         double bg2 = best_g;
@@ -1868,7 +1868,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
       double g, mid;
       int bb;
       bool nc;
-#ifdef DML_X2_SUB
+#if defined(DML_X2_SUB) && DML_X2_SUB != 1   // sensitivity: every one-feature evaluation twice
       sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_yq, g, bb, nc, tcw,
                     MonoQ{mono_of<FC>(c, s, f), e.lo, e.hi}, mid);
       if (g == -12345.0 && bb == 7) atomicOr(&c.counters[kOpenOvf], (int)nc);
