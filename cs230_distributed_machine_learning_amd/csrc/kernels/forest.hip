@@ -790,6 +790,11 @@ __host__ __device__ inline FusedLayout fused_layout(int KG, int span, int elem, 
 // parent's channel sums and the tree weight are prefetched at kernel start, so the
 // decision makes no dependent global round trips.
 __device__ __forceinline__ bool accept_split_v(const Ctx& c, const NodeSpec& s, const double* pv, double Wt, const double* best_left) {
+  // classification with min_impurity_decrease <= 0: the test cannot reject. The impurity
+  // decrease of a Gini / entropy split is >= 0 (concave impurities) and every term of the
+  // computed value is <= log2(64) in magnitude, so its rounding error is ~1e-14, far inside
+  // kEps: the host builder, which evaluates the test, accepts every such split too
+  if (!c.is_reg && s.min_impurity_decrease <= 0.0f) return true;
   double impN, impL, impR, wN, wL, wR;
   if (c.is_reg) {
     wN = pv[0]; wL = best_left[0]; wR = pv[0] - best_left[0];
@@ -807,6 +812,12 @@ __device__ __forceinline__ bool accept_split_v(const Ctx& c, const NodeSpec& s, 
   return !(imp + kEps < (double)s.min_impurity_decrease);
 }
 
+// "impurity > kEps" of a child's value vector; a Gini-specialised binary build decides it on
+// the integer class weights (pure <=> a class is absent: a mixed node of total weight W < 2e7
+// has Gini >= 2 (W - 1) / W^2 > kEps, and a pure one computes exactly 0)
+template <int FC>
+__device__ __forceinline__ bool impure_v(const Ctx& c, const NodeSpec& s, const double* v);
+
 __device__ __forceinline__ double impurity_of_vals(const Ctx& c, const double* v, int crit) {
   if (c.is_reg) return mse_impurity(v[0], v[1], v[2]);
   ClsAcc a;
@@ -815,12 +826,20 @@ __device__ __forceinline__ double impurity_of_vals(const Ctx& c, const double* v
   return cls_impurity(a, crit);
 }
 
+template <int FC>
+__device__ __forceinline__ bool impure_v(const Ctx& c, const NodeSpec& s, const double* v) {
+  if constexpr (FC == kGini)
+    if (c.C == 2) return v[0] > 0.0 && v[1] > 0.0;
+  return impurity_of_vals(c, v, s.criterion) > kEps;
+}
+
 // a wave/block-tier child into its staging slot (k_compact enqueues it): tier -1 = leaf
+template <int FC>
 __device__ __forceinline__ void stage_child(const Ctx& c, const NodeSpec& s, int tree, int node, int64_t start, int count, int depth,
                             uint64_t key, int64_t slot, const double* vals) {
   int tier = -1;
   if (!leaf_by_counts(s, count, depth) && !leaf_by_weight(s, vals_weight(vals, c.C, c.is_reg)) &&
-      impurity_of_vals(c, vals, s.criterion) > kEps)
+      impure_v<FC>(c, s, vals))
     tier = count <= c.sub_max ? 0 : (count <= c.wave_max ? 1 : (count <= c.block_max ? 2 : 3));
   OpenNode on;
   on.tree = tree; on.node = node; on.start = start; on.count = count; on.depth = depth;
@@ -1323,10 +1342,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
   const int feat = sc->best_feat, bin = sc->best_bin, nl = sc->nl;
   constexpr int RT = NT > 64 ? 64 : 1;   // the right child is enqueued by another wave / lane
   if (tid == 0)
-    stage_child(c, s, on.tree, base, on.start, nl, on.depth + 1, child_key(on.key, 0),
+    stage_child<FC>(c, s, on.tree, base, on.start, nl, on.depth + 1, child_key(on.key, 0),
                 2 * (stage_base + (int64_t)blockIdx.x), best_left);
   if (tid == RT)
-    stage_child(c, s, on.tree, base + 1, on.start + nl, cnt - nl, on.depth + 1, child_key(on.key, 1),
+    stage_child<FC>(c, s, on.tree, base + 1, on.start + nl, cnt - nl, on.depth + 1, child_key(on.key, 1),
                 2 * (stage_base + (int64_t)blockIdx.x) + 1, rvs);
   // ---- stable partition
 #ifdef DML_X2_PART   // sensitivity build: the (idempotent) partition pass runs twice
@@ -1655,9 +1674,22 @@ __device__ __forceinline__ void sub_node_seg(const Ctx& c, const NodeSpec& s, co
   // after the sort every lane holds its sorted row's payload, no shuffles (rows of equal
   // keys are interchangeable: the sums at the end of a bin run are the same)
   const uint32_t pay = ((uint32_t)cls_j << 4) | (w_j & 15u);
+  // the first 64 visiting positions, one per lane, computed once for the node; a pass reads
+  // its S positions' features by readlane (the cycle-walking permutation costs ~40 VALU)
+  const int fo = feature_at(fp, min(lane, d - 1), d);
   for (int pos = 0; nonconst < s.max_features && pos < d; pos += S) {
     const bool has_f = pos + seg < d;
-    const int f = has_f ? feature_at(fp, pos + seg, d) : 0;
+    int f = 0;
+    if (pos + S <= 64) {
+#pragma unroll
+      for (int q = 0; q < S; ++q) {
+        const int fq = __builtin_amdgcn_readlane(fo, pos + q);
+        if (seg == q) f = fq;
+      }
+      if (!has_f) f = 0;
+    } else {
+      f = has_f ? feature_at(fp, pos + seg, d) : 0;
+    }
     const int my_bin = (valid_row && has_f) ? (int)xc[src * dp + f] : 0;
     const uint32_t key = valid_row ? ((uint32_t)my_bin << 10) | pay : 0xFFFFFFFFu;
     const uint32_t sk = bitonic_seg<WD>(key, j, lane);
@@ -1886,6 +1918,17 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     const uint64_t lm = __ballot(in && mybin <= best_b) & e.mask;
     const uint64_t rm = e.mask & ~lm;
     // left child statistics (class weights / regression sums) by wave reductions
+    if (!REG && c.C == 2) {   // binary: one packed integer sum (a <= 64-row node weighs < 2^16)
+      const bool inl = (lm >> lane) & 1ull;
+      const uint32_t w = (uint32_t)my_w;
+      const uint32_t x = wave::sum<uint32_t>(inl ? (w | (my_cls == 1 ? w << 16 : 0u)) : 0u, lane);
+      const uint32_t l1 = x >> 16, l0 = (x & 0xFFFFu) - l1;
+      if (lane == 0) {
+        const double v0 = (double)l0 * cwk(tcw, 0), v1 = (double)l1 * cwk(tcw, 1);
+        left_ch[0] = v0; right_ch[0] = pv[0] - v0;
+        left_ch[1] = v1; right_ch[1] = pv[1] - v1;
+      }
+    } else
     for (int k = 0; k < VC; ++k) {
       double v;
       const bool inl = (lm >> lane) & 1ull;
@@ -1926,9 +1969,9 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     if (lane == 0) {
       const int dep = e.depth + 1;
       const bool push_r = !leaf_by_counts(s, nr, dep) && !leaf_by_weight(s, vals_weight(right_ch, c.C, c.is_reg)) &&
-                          impurity_of_vals(c, right_ch, s.criterion) > kEps;
+                          impure_v<FC>(c, s, right_ch);
       const bool push_l = !leaf_by_counts(s, nl, dep) && !leaf_by_weight(s, vals_weight(left_ch, c.C, c.is_reg)) &&
-                          impurity_of_vals(c, left_ch, s.criterion) > kEps;
+                          impure_v<FC>(c, s, left_ch);
       const int mbest = mono_of<FC>(c, s, best_f);
       if (push_r) {
         SubEntry r; r.mask = rm; r.key = child_key(e.key, 1); r.node = base + 1; r.depth = dep;
