@@ -27,7 +27,9 @@ class DeviceData:
     previous chunk; only the uint8 bins stay in HBM (4x smaller: a 400 GB float32 table
     trains as 100 GB of bins).  The quantile edges come from the same 200k-row sample the
     resident path draws (ops/binning.py), so the bins -- and every tree -- are identical.
-    Only tree families run on such a table (``Family.binned_ok``)."""
+    Tree families run on the bins (``Family.binned_ok``); LinearRegression and PCA
+    (``Family.streams_rows``) stream the host rows again in chunks (``stream_rows``)
+    for their moments and test predictions; other families refuse such a table."""
 
     def __init__(self, X, y, classification: bool, device: torch.device | str = "cpu",
                  classes: Optional[np.ndarray] = None, name: str = "", binned_only: bool = False,
@@ -37,10 +39,13 @@ class DeviceData:
         self.binned_only = bool(binned_only)
         self._Xb = None
         self._edges = None
+        self._X_host = None
+        self._chunk_rows = int(chunk_rows)
         if self.binned_only:
             self.X = None
             Xh = X.cpu().numpy() if isinstance(X, torch.Tensor) else X
             self.n, self.d = Xh.shape
+            self._X_host = Xh   # host (or memmap) rows: families with ``streams_rows`` read them in chunks
         elif isinstance(X, torch.Tensor):
             self.X = X.to(self.device, dtype=torch.float32).contiguous()
             self.n, self.d = self.X.shape
@@ -90,6 +95,24 @@ class DeviceData:
     @property
     def is_gpu(self) -> bool:
         return self.device.type == "cuda"
+
+    # ---- out-of-core float32 rows (binned-only tables) ---------------------------------
+    def can_stream_rows(self) -> bool:
+        return self.X is None and self._X_host is not None
+
+    def stream_rows(self, chunk_rows: Optional[int] = None):
+        """Yield (r0, r1, X[r0:r1] as float32 on the device) over a binned-only table's host
+        rows: the float32 table never becomes resident, one chunk (and one pinned staging
+        buffer) at a time.  The resident path keeps using ``self.X``."""
+        if not self.can_stream_rows():
+            raise ValueError("no host rows to stream (the table is resident or was received as bins)")
+        Xh = self._X_host
+        chunk = max(1, min(int(chunk_rows or self._chunk_rows), self.n))
+        pin = torch.empty((chunk, self.d), dtype=torch.float32, pin_memory=self.is_gpu)
+        for r0 in range(0, self.n, chunk):
+            r1 = min(self.n, r0 + chunk)
+            np.copyto(pin[:r1 - r0].numpy(), Xh[r0:r1], casting="same_kind")
+            yield r0, r1, pin[:r1 - r0].to(self.device, non_blocking=False)
 
     # ---- binned copy (trees) -------------------------------------------------------
     def _stream_bin(self, Xh, chunk_rows: int) -> None:

@@ -116,7 +116,8 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
         scorer = scoring_mod.validate_scoring(spec.scoring, clf)
     if not clf and not self_scored and not getattr(data, "y_is_numeric", True):
         raise ValueError(f"{spec.model_type} needs a numeric target column; this target is categorical")
-    if getattr(data, "binned_only", False) and not getattr(fam, "binned_ok", False):
+    streamable = getattr(fam, "streams_rows", False) and getattr(data, "can_stream_rows", lambda: False)()
+    if getattr(data, "binned_only", False) and not getattr(fam, "binned_ok", False) and not streamable:
         raise ValueError(f"{spec.model_type} needs the float32 rows; this table is resident only in binned form "
                          f"(too large for HBM) -- tree models only")
     sharded = getattr(data, "is_row_shard", False)

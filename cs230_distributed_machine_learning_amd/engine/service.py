@@ -361,7 +361,9 @@ class DeviceCache:
 
     def _binned_only(self, ctl: Controller, plan: Dict[str, Any], X) -> bool:
         """Tree jobs on a table too large for HBM as float32 keep only its bins resident."""
-        if not str(self.device).startswith("cuda") or not getattr(family_of(plan["model_type"]), "binned_ok", False):
+        fam = family_of(plan["model_type"])
+        if not str(self.device).startswith("cuda") or not (getattr(fam, "binned_ok", False)
+                                                           or getattr(fam, "streams_rows", False)):
             return False
         import torch
 

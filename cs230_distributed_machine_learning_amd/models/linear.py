@@ -752,10 +752,59 @@ HOST_LBFGS_MAX_WORK = 200_000   # n_train * (d+1) * (K-1): below this a fit runs
 _LIN_DEFAULTS = {"fit_intercept": True, "copy_X": True, "n_jobs": None, "positive": False}
 
 
+def _stream_chunk(data) -> int:
+    # float64 working copies of a chunk stay <= ~512 MB whatever d is
+    return max(1024, min(data._chunk_rows, (1 << 29) // (8 * (data.d + 2))))
+
+
+def streamed_split_moments(data, splits: List[int]) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``LinearRegressionFamily.split_moments`` for a table whose float32 rows are not
+    resident (DeviceData binned-only): one pass over the host rows in chunks, every split's
+    train-row moments of z = [x - c, 1, y - c_y] accumulated in float64 on the device.  The
+    shift c is the first chunk's column mean (moments about any shift are exact sums; a shift
+    near the mean keeps the centring well conditioned)."""
+    from ..search.cv import ROLE_TRAIN
+
+    d = data.d
+    dev = data.device
+    y = data.y_reg.double()
+    S = len(splits)
+    M = torch.zeros((S, d + 2, d + 2), dtype=torch.float64, device=dev)
+    shift = None
+    roles = data.roles[torch.tensor(splits, dtype=torch.long, device=dev)]
+    for r0, r1, Xc in data.stream_rows(_stream_chunk(data)):
+        Xc = Xc.double()
+        yc = y[r0:r1]
+        if shift is None:
+            shift = torch.cat([Xc.mean(0), yc.mean().view(1)])
+        Z = torch.cat([Xc - shift[:d], torch.ones((r1 - r0, 1), dtype=torch.float64, device=dev),
+                       (yc - shift[d]).view(-1, 1)], 1)
+        for i in range(S):
+            Zs = Z[roles[i, r0:r1] == ROLE_TRAIN]
+            M[i] += Zs.t() @ Zs
+    if shift is None:
+        shift = torch.zeros(d + 1, dtype=torch.float64, device=dev)
+    return M, shift
+
+
+def streamed_test_rows(data, split: int, fn):
+    """fn(X test rows of the chunk as float64) for every chunk of a binned-only table, the
+    results concatenated in test-row order (``data.test_rows[split]`` is ascending)."""
+    from ..search.cv import ROLE_TEST
+
+    parts = []
+    for r0, r1, Xc in data.stream_rows(_stream_chunk(data)):
+        m = data.roles[split, r0:r1] == ROLE_TEST
+        if bool(m.any()):
+            parts.append(fn(Xc[m].double()))
+    return torch.cat(parts) if parts else None
+
+
 class LinearRegressionFamily(Family):
     model_types = ("LinearRegression",)
     classifiers = ()
     data_parallel = True   # normal-equation moments all-reduced under a RowShard
+    streams_rows = True    # binned-only tables: moments and predictions over streamed host rows
 
     def resolve(self, model_type, params, n_train, n_features, n_classes):
         p = dict(_LIN_DEFAULTS)
@@ -770,7 +819,11 @@ class LinearRegressionFamily(Family):
         t0 = time.perf_counter()
         X, y = data.X, data.y_reg
         cache: Dict[tuple, tuple] = {}
-        if (data.is_gpu and not getattr(data, "is_row_shard", False)
+        streamed = X is None and getattr(data, "can_stream_rows", lambda: False)()
+        if streamed:
+            splits = sorted({t.split for t in tasks})
+            cache = self._solve_from_moments(data, tasks, streamed_split_moments(data, splits))
+        elif (data.is_gpu and not getattr(data, "is_row_shard", False)
                 and os.environ.get("DML_LINREG_KERNEL", "1") != "0"):
             cache = self._solve_from_moments(data, tasks)
         outs = []
@@ -794,8 +847,13 @@ class LinearRegressionFamily(Family):
                     b0 = ym - xm @ w
                     cache[key] = (w, b0)
             w, b0 = cache[key]
-            te = data.test_rows[t.split].long()
-            pred = (X[te].double() @ w + b0).float()
+            if streamed:
+                pred = streamed_test_rows(data, t.split, lambda Xt, w=w, b0=b0: (Xt @ w + b0).float())
+                if pred is None:
+                    pred = torch.zeros(0, dtype=torch.float32, device=data.device)
+            else:
+                te = data.test_rows[t.split].long()
+                pred = (X[te].double() @ w + b0).float()
             o = FitOutput(task_id=t.task_id, pred=pred, info={"warnings": t.params.get("warnings", [])})
             if keep_models:
                 o.model = {"kind": "linear_regression", "coef": w.cpu().numpy(), "intercept": float(b0),
@@ -835,11 +893,12 @@ class LinearRegressionFamily(Family):
         M = torch.triu(out) + torch.triu(out, 1).transpose(1, 2)   # the kernel fills ti <= tj tiles
         return M[:, :d + 2, :d + 2], shift
 
-    def _solve_from_moments(self, data, tasks) -> Dict[tuple, tuple]:
-        """(split, fit_intercept) -> (w, b0) for every task, from the fused moments."""
+    def _solve_from_moments(self, data, tasks, moments=None) -> Dict[tuple, tuple]:
+        """(split, fit_intercept) -> (w, b0) for every task, from the fused moments
+        (``moments``: precomputed (M, shift), e.g. streamed from host rows)."""
         d = data.d
         splits = sorted({t.split for t in tasks})
-        M, shift = self.split_moments(data, splits)
+        M, shift = moments if moments is not None else self.split_moments(data, splits)
         cx, cy = shift[:d], shift[d]
         out: Dict[tuple, tuple] = {}
         for i, sp in enumerate(splits):

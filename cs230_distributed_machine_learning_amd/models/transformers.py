@@ -82,6 +82,7 @@ class PCAFamily(Family):
     self_scored = ("PCA",)
     data_parallel = True   # row-sharded: [count, sum x, X^T X] and the test log-likelihood sums all-reduced
     dp_when_few = False
+    streams_rows = True    # binned-only tables: covariance and test projections over streamed host rows
 
     def resolve(self, model_type, params, n_train, n_features, n_classes) -> Dict[str, Any]:
         p = dict(_PCA_DEFAULTS)
@@ -110,12 +111,16 @@ class PCAFamily(Family):
         eig: Dict[int, Any] = {}
         outs = []
         fused = {}
-        if data.is_gpu and not getattr(data, "is_row_shard", False) and os.environ.get("DML_LINREG_KERNEL", "1") != "0":
-            # every split's covariance from one pass over X (the LinearRegression moments kernel)
-            from .linear import LinearRegressionFamily
+        streamed = X is None and getattr(data, "can_stream_rows", lambda: False)()
+        if streamed or (data.is_gpu and not getattr(data, "is_row_shard", False)
+                        and os.environ.get("DML_LINREG_KERNEL", "1") != "0"):
+            # every split's covariance from one pass over X (the LinearRegression moments kernel,
+            # or the streamed moments of a table whose float32 rows are not resident)
+            from .linear import LinearRegressionFamily, streamed_split_moments
 
             splits = sorted({t.split for t in tasks})
-            M, shift = LinearRegressionFamily.split_moments(data, splits)
+            M, shift = (streamed_split_moments(data, splits) if streamed
+                        else LinearRegressionFamily.split_moments(data, splits))
             for i, sp in enumerate(splits):
                 cnt, Sx, XX = M[i][d, d], M[i][:d, d], M[i][:d, :d]
                 dm = Sx / cnt.clamp_min(1)
@@ -142,8 +147,15 @@ class PCAFamily(Family):
                     cov = Xc.t() @ Xc / max(1, n - 1)
                 lam, V = torch.linalg.eigh(cov)                       # ascending
                 lam, V = lam.flip(0).clamp_min(0), V.flip(1)
-                te = data.test_rows[t.split].long()
-                Z = (X[te].double() - mean) @ V                        # test rows in the eigenbasis
+                if streamed:
+                    from .linear import streamed_test_rows
+
+                    Z = streamed_test_rows(data, t.split, lambda Xt, mean=mean, V=V: (Xt - mean) @ V)
+                    if Z is None:
+                        Z = torch.zeros((0, d), dtype=torch.float64, device=data.device)
+                else:
+                    te = data.test_rows[t.split].long()
+                    Z = (X[te].double() - mean) @ V                    # test rows in the eigenbasis
                 eig[t.split] = (mean, lam, V, Z, n)
             mean, lam, V, Z, n = eig[t.split]
             ev = lam.cpu().numpy()[: min(n, d)]

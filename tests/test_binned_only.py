@@ -41,6 +41,16 @@ def _check(dev, n, d, chunk, tmp_path):
         assert _scores(res_dd, model, grid) == _scores(bin_dd, model, grid)
     with pytest.raises(ValueError, match="binned form"):
         run_candidates(bin_dd, JobSpec("LogisticRegression", [{"C": 1.0}], cv=3), [0])
+    # LinearRegression / PCA re-stream the host rows for their moments and test rows
+    rng = np.random.RandomState(1)
+    yr = X @ rng.randn(d).astype(np.float32) + 3.0 + 0.1 * rng.randn(n).astype(np.float32)
+    res_r = DeviceData(X, yr, False, dev)
+    bin_r = DeviceData(Xmm, yr, False, dev, binned_only=True, chunk_rows=chunk)
+    assert bin_r.X is None and bin_r.can_stream_rows()
+    for model, grid in (("LinearRegression", {"fit_intercept": [True, False]}),
+                        ("PCA", {"n_components": [2, 5]})):
+        a, b = _scores(res_r, model, grid), _scores(bin_r, model, grid)
+        np.testing.assert_allclose(np.asarray(b), np.asarray(a), rtol=1e-6, atol=1e-6)
 
 
 def test_binned_only_cpu_matches_resident(tmp_path):
