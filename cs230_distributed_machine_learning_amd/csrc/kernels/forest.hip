@@ -61,6 +61,9 @@
 #ifndef DML_GINI_PF
 #define DML_GINI_PF 1          // binary Gini: fp32 pre-filter of candidate bins (eval_feature)
 #endif
+#ifndef DML_EVAL_PAIRS
+#define DML_EVAL_PAIRS 0       // k_nodes: binary-Gini features evaluated two at a time (1 both tiers, 2 wave, 3 block; slower)
+#endif
 #ifndef DML_WAVE_PREFETCH
 #define DML_WAVE_PREFETCH 12   // wave tier: visiting positions whose bins are gathered up front
 #endif
@@ -434,6 +437,129 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
                                  double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after,
                                  const double* cw, MonoQ mq, double* out_mid);
 
+// binary Gini with class weights in [2^-20, 2^20] and no monotonic constraint: the fp32
+// pre-filter path of eval_feature below
+__device__ __forceinline__ bool gini_pf_ok(const NodeSpec& s, double cw0, double cw1) {
+  return DML_GINI_PF && s.criterion == kGini && cw0 >= 0x1p-20 && cw0 <= 0x1p20 && cw1 >= 0x1p-20 && cw1 <= 0x1p20;
+}
+
+// Binary Gini, fp32 pre-filter + fp64 re-scoring (see eval_feature), for NF features at
+// once: feature f's histogram is h + f * FS * span and its outputs sit FS apart.  The NF
+// scans and reductions are independent chains that the scheduler interleaves -- one wave
+// evaluates a wave-tier node's features, so this chain is that tier's critical path.
+// A candidate whose own bin is empty is skipped: its cumulative channels equal the previous
+// bin's, which wins the tie (lowest bin), so the split chosen is unchanged; what is left is
+// usually one contender per lane, re-scored in one pass.
+template <int NF, int FS>
+__device__ DML_EVAL_ATTR void eval_gini_pf(unsigned long long* h, int span, const NodeSpec& s, int lane,
+                                           double* out_gain, int* out_bin, int* out_nc, double* out_left, int CH,
+                                           bool zero_after, double cw0, double cw1) {
+  uint64_t v[NF][4];
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[f][i] = h[f * FS * span + 4 * lane + i];
+  if (zero_after) {
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h[f * FS * span + 4 * lane + i] = 0ull;
+  }
+  uint32_t nz[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    nz[f] = (v[f][0] != 0ull ? 1u : 0u) | (v[f][1] != 0ull ? 2u : 0u) | (v[f][2] != 0ull ? 4u : 0u) |
+            (v[f][3] != 0ull ? 8u : 0u);
+    v[f][1] += v[f][0]; v[f][2] += v[f][1]; v[f][3] += v[f][2];
+  }
+  uint64_t t[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) t[f] = wave::incl_scan_u64(v[f][3]);
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const uint64_t ex = wave::excl_from_incl<uint64_t>(t[f]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[f][i] += ex;
+  }
+  const uint32_t mslu = (uint32_t)s.min_samples_leaf;
+  const float cw0f = (float)cw0, cw1f = (float)cw1;
+  const bool mwl = s.min_weight_leaf > 0.0;
+  uint32_t tr[NF], t0i[NF], t1i[NF];
+  float q[NF][4], qm[NF];
+  bool nc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const uint64_t tv = wave::bcast<uint64_t>(t[f], 63);
+    tr[f] = (uint32_t)(tv >> 42); t0i[f] = (uint32_t)(tv & kPackMask21); t1i[f] = (uint32_t)((tv >> 21) & kPackMask21);
+    const double t0 = (double)t0i[f] * cw0, t1 = (double)t1i[f] * cw1;
+    qm[f] = -INFINITY;
+    nc[f] = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t cv = v[f][i];
+      const uint32_t rl = (uint32_t)(cv >> 42), rr = tr[f] - rl;
+      const uint32_t l0i = (uint32_t)(cv & kPackMask21), l1i = (uint32_t)((cv >> 21) & kPackMask21);
+      nc[f] |= (rl > 0u && rr > 0u);
+      bool ok = ((nz[f] >> i) & 1u) && (lane * 4 + i) != 255 && rl >= mslu && rr >= mslu;
+      if (mwl) {
+        const double l0 = (double)l0i * cw0, l1 = (double)l1i * cw1;
+        ok = ok && !side_too_light(s, l0 + l1, (t0 - l0) + (t1 - l1));
+      }
+      const float a0 = (float)l0i * cw0f, a1 = (float)l1i * cw1f;
+      const float r0 = (float)(t0i[f] - l0i) * cw0f, r1 = (float)(t1i[f] - l1i) * cw1f;
+      const float wl = a0 + a1, wr = r0 + r1;
+      const float num = (a0 * a0 + a1 * a1) * wr + (r0 * r0 + r1 * r1) * wl;
+      q[f][i] = ok ? num * __builtin_amdgcn_rcpf(wl * wr) : -INFINITY;
+      qm[f] = fmaxf(qm[f], q[f][i]);
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < NF; ++f) qm[f] = wave::max_f32(qm[f], lane);
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const float thr = qm[f] - qm[f] * 0x1p-14f;
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m |= (q[f][i] >= thr && q[f][i] != -INFINITY) ? (1u << i) : 0u;
+    const double t0 = (double)t0i[f] * cw0, t1 = (double)t1i[f] * cw1;
+    double best = -INFINITY;
+    int bb = -1;
+    while (__ballot(m != 0u) != 0ull) {
+      if (m != 0u) {
+        const int i = __builtin_ctz(m);
+        m &= m - 1u;
+        const uint64_t cv = i == 0 ? v[f][0] : i == 1 ? v[f][1] : i == 2 ? v[f][2] : v[f][3];
+        const double l0 = (double)(cv & kPackMask21) * cw0, l1 = (double)((cv >> 21) & kPackMask21) * cw1;
+        ClsAcc L, R;
+        L.init(kGini); R.init(kGini);
+        L.add(l0); L.add(l1);
+        R.add(t0 - l0); R.add(t1 - l1);
+        const double g = cls_proxy(L, R, kGini);
+        if (g > best) { best = g; bb = lane * 4 + i; }
+      }
+    }
+    const uint64_t cm = __ballot(bb >= 0);
+    if (__popcll(cm) == 1) {
+      const int src = (int)__builtin_ctzll(cm);
+      best = wave::bcast<double>(best, src);
+      bb = wave::bcast<int>(bb, src);
+    } else {
+      wave::argmax(best, bb, lane);
+    }
+    const bool any_nc = __ballot(nc[f]) != 0ull;
+    const int src = bb >= 0 ? (bb >> 2) : 0, sel = bb >= 0 ? (bb & 3) : 0;
+    const uint64_t mine = sel == 0 ? v[f][0] : sel == 1 ? v[f][1] : sel == 2 ? v[f][2] : v[f][3];
+    const uint64_t cv = wave::bcast<uint64_t>(mine, src);
+    if (lane == 0) {
+      double* ol = out_left + f * FS * CH;
+      ol[0] = bb >= 0 ? (double)(cv & kPackMask21) * cw0 : 0.0;
+      ol[1] = bb >= 0 ? (double)((cv >> 21) & kPackMask21) * cw1 : 0.0;
+      ol[2] = bb >= 0 ? (double)(cv >> 42) : 0.0;
+      out_gain[f * FS] = best; out_bin[f * FS] = bb; out_nc[f * FS] = any_nc ? 1 : 0;
+    }
+  }
+}
+
 // ONE wave evaluates one feature's histogram.  Binary (MODE 1) and regression (MODE 2)
 // histograms are read ONCE into registers (4 bins per lane), scanned with DPP, scored and
 // arg-maxed without writing the scan back to LDS; the histogram is cleared by the same
@@ -447,6 +573,13 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
     eval_feature_lds<MODE>(h, C, CH, s, lane, out_gain, out_bin, out_nc, out_left, zero_after, cw, mq, out_mid);
   } else {
     using CT = typename HT<MODE>::T;
+    if constexpr (MODE == 1) {
+      if (mq.m == 0 && gini_pf_ok(s, cwk(cw, 0), cwk(cw, 1))) {
+        eval_gini_pf<1, 1>(h, 256, s, lane, out_gain, out_bin, out_nc, out_left, CH, zero_after, cwk(cw, 0), cwk(cw, 1));
+        if (out_mid && lane == 0) *out_mid = 0.0;
+        return;
+      }
+    }
     constexpr int NP = MODE == 1 ? 1 : 3;      // planes: packed u64 | (w | rows << 32, w yq, w y2q) integers
     CT v[NP][4];
 #pragma unroll
@@ -1251,7 +1384,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
     }
     __syncthreads();
     PH(2)
-    for (int j = wid; j < g; j += NW) {
+    int j0 = wid;
+#if !defined(DML_X2_EVAL) && DML_EVAL_PAIRS
+    if constexpr (MODE == 1 && (DML_EVAL_PAIRS == 1 || (DML_EVAL_PAIRS == 2) == (NT == 64))) {
+      // features j and j + NW evaluated together (two interleaved chains)
+      const double* cw = tree_cw<FC>(c, on.tree);
+      if (gini_pf_ok(s, cwk(cw, 0), cwk(cw, 1)))
+        for (; j0 + NW < g; j0 += 2 * NW) {
+          if (mono_of<FC>(c, s, feats[j0]) != 0 || mono_of<FC>(c, s, feats[j0 + NW]) != 0) break;
+          eval_gini_pf<2, NW>(hist + j0 * span, span, s, lane, rg + j0, rb + j0, rn + j0, rleft + j0 * c.CH, c.CH, true,
+                              cwk(cw, 0), cwk(cw, 1));
+          if (lane == 0) { rmid[j0] = 0.0; rmid[j0 + NW] = 0.0; }
+        }
+    }
+#endif
+    for (int j = j0; j < g; j += NW) {
 #ifdef DML_X2_EVAL   // sensitivity build: every feature evaluated twice (the first keeps the histogram)
       eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, false,
                          tree_cw<FC>(c, on.tree), &c.rq, MonoQ{mono_of<FC>(c, s, feats[j]), sc->lo, sc->hi}, rmid + j);
@@ -1351,7 +1498,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
 #ifdef DML_X2_PART   // sensitivity build: the (idempotent) partition pass runs twice
   for (int rep_ = 0; rep_ < 2; ++rep_) {
 #endif
-  if (NT > 64 && !reg_rows && (size_t)((cnt + 63) / 64) * 12 <= (size_t)KG * span * sizeof(CT)) {
+  if (NT > 64 && !reg_rows && cnt <= 128 * NT && (size_t)((cnt + 63) / 64) * 12 <= (size_t)KG * span * sizeof(CT)) {
     // block tier, streamed node: two passes and two barriers for the whole node (not two per
     // chunk).  Pass 1 ranks every row (split bin from the histogram pass's scratch, else
     // gathered) into one ballot word per 64-row group in LDS (the histograms are dead);
@@ -1383,7 +1530,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WP
       }
     }
     __syncthreads();
-    // exclusive prefix of the groups' left counts (<= 512 groups: two per thread)
+    // exclusive prefix of the groups' left counts (<= 2 NT groups: two per thread)
     {
       const int g0 = 2 * tid, g1 = 2 * tid + 1;
       const int c0 = g0 < ngrp ? __popcll(lflag[g0]) : 0, c1 = g1 < ngrp ? __popcll(lflag[g1]) : 0;

@@ -113,6 +113,25 @@ def test_gpu_trees_match_cpu(n, d, C, kw, tiers, words, monkeypatch):
     assert np.allclose(sg, sc)
 
 
+def test_gpu_big_block_tier_matches_cpu():
+    """block_max above 32768: block-tier nodes with more than 2 x 256 row groups take the
+    streaming partition (the two-pass one ranks at most 2 groups per thread)."""
+    n, d, C = 150_000, 12, 2
+    X, y = _data(n, d, C)
+    dev = torch.device("cuda:0")
+    edges = binning.quantile_edges(torch.from_numpy(X))
+    Xb_cpu = binning.bin_matrix(torch.from_numpy(X), edges).numpy()
+    Xb = torch.from_numpy(Xb_cpu).to(dev)
+    roles, _ = make_split_roles(y, 3, True, holdout=False)
+    specs = _specs(3, 2, d, max_depth=6)
+    ycls = y.astype(np.int32)
+    g = forest_ops.build_gpu(Xb, torch.from_numpy(ycls).to(dev), None, torch.from_numpy(roles).to(dev), specs, C, False,
+                             forest_ops.ForestTiers(block_max=1 << 17))
+    assert g.stats["tier_nodes"][2] > 0 and g.stats["tier_nodes"][3] == 0
+    c = forest_ops.build_cpu(Xb_cpu, ycls, None, roles, specs, C, False)
+    assert _canon(g.nodes.cpu().numpy(), g.vals.cpu().numpy(), len(specs)) == _canon(c.nodes, c.vals, len(specs))
+
+
 @pytest.mark.parametrize("tiers", range(len(TIERS)))
 @pytest.mark.parametrize("n,d,C", [(4000, 12, 2), (30000, 16, 3)])
 def test_gpu_class_weighted_trees_match_cpu(n, d, C, tiers):
