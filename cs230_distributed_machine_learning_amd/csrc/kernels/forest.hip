@@ -49,6 +49,15 @@
 #else
 #define DML_EVAL_ATTR
 #endif
+#ifndef DML_NODES_WPE_REG
+#define DML_NODES_WPE_REG 2   // regression node kernels: 3 histogram planes + payloads fit 256 VGPRs, no spills
+#endif
+#ifndef DML_NODES_WPE_MC
+#define DML_NODES_WPE_MC 2    // multiclass: C+1 histogram planes; 2 waves per SIMD without spills beats 4 with
+#endif
+#ifndef DML_SUB_SEG_REG
+#define DML_SUB_SEG_REG 1     // regression subtrees: segmented evaluation of nodes <= 32 rows
+#endif
 #ifndef DML_KGMAX_WAVE
 #define DML_KGMAX_WAVE 4
 #endif
@@ -1018,7 +1027,7 @@ __device__ __forceinline__ void hist_add(typename HT<MODE>::T* hj, const Ctx& c,
 }
 
 template <int NT, int MODE, int FC>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DML_NODES_WPE, 8))) void k_nodes(Ctx c, int tier, int set_cur,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? DML_NODES_WPE_REG : (MODE == 0 ? DML_NODES_WPE_MC : DML_NODES_WPE), 8))) void k_nodes(Ctx c, int tier, int set_cur,
                                                                                                    int pair_base, int stage_base) {
   using CT = typename HT<MODE>::T;
   constexpr bool PK = FC >= 0;   // specialised builds have packed row words
@@ -1809,10 +1818,14 @@ __device__ __forceinline__ void argmax_seg(double& g, int& idx, int lane) {
 // row j: `src`); updates the running (nonconst, best) in visiting order exactly like the
 // per-feature loop.  xc: LDS row-bin cache (stride dp); cls_j / w_j: class and weight of
 // compact row j (valid in every segment's lane j).
-template <int WD>
+// Regression (REG): the key carries (bin, compact row j, w); the row's fixed-point target
+// comes from segment lane j by one 64-bit shuffle, and the two integer channels (w, w yq)
+// are scanned per segment -- the same integer prefix sums, hence the same doubles, as
+// sub_eval's one-feature path and the host builder.
+template <int WD, bool REG = false>
 __device__ __forceinline__ void sub_node_seg(const Ctx& c, const NodeSpec& s, const FeatPerm& fp, int cnt, int lane, int src,
                              int cls_j, uint32_t w_j, const uint8_t* xc, int dp, int& nonconst, double& best_g,
-                             int& best_f, int& best_b, const double* cw) {
+                             int& best_f, int& best_b, const double* cw, int64_t yq_j = 0) {
   constexpr int S = 64 / WD;
   const int d = c.d;
   const int seg = lane / WD, j = lane & (WD - 1);
@@ -1820,7 +1833,7 @@ __device__ __forceinline__ void sub_node_seg(const Ctx& c, const NodeSpec& s, co
   // the row's class and weight ride in the low bits of its sort key (bin << 10 | cls << 4 | w):
   // after the sort every lane holds its sorted row's payload, no shuffles (rows of equal
   // keys are interchangeable: the sums at the end of a bin run are the same)
-  const uint32_t pay = ((uint32_t)cls_j << 4) | (w_j & 15u);
+  const uint32_t pay = REG ? (((uint32_t)j << 4) | (w_j & 15u)) : (((uint32_t)cls_j << 4) | (w_j & 15u));
   // the first 64 visiting positions, one per lane, computed once for the node; a pass reads
   // its S positions' features by readlane (the cycle-walking permutation costs ~40 VALU)
   const int fo = feature_at(fp, min(lane, d - 1), d);
@@ -1847,6 +1860,23 @@ __device__ __forceinline__ void sub_node_seg(const Ctx& c, const NodeSpec& s, co
     const bool cand = valid_row && j < cnt - 1 && b != bnext && j + 1 >= s.min_samples_leaf &&
                       cnt - j - 1 >= s.min_samples_leaf;
     const bool ncl = valid_row && j < cnt - 1 && b != bnext;
+    double g = -INFINITY;
+    if constexpr (REG) {
+      const int srcl = seg * WD + (int)((sk >> 4) & 31u);
+      const uint64_t yq = wave::bcast_lane<uint64_t>((uint64_t)yq_j, srcl);
+      const uint64_t wv = valid_row ? (uint64_t)w : 0ull, wy = valid_row ? (uint64_t)((int64_t)w * (int64_t)yq) : 0ull;
+      uint64_t p0 = wave::incl_scan_u64(wv), p1 = wave::incl_scan_u64(wy);
+      uint64_t b0 = 0, b1 = 0, t0 = 0, t1 = 0;
+#pragma unroll
+      for (int q = 0; q < S; ++q) {
+        const uint64_t bq0 = q ? wave::bcast<uint64_t>(p0, q * WD - 1) : 0ull, bq1 = q ? wave::bcast<uint64_t>(p1, q * WD - 1) : 0ull;
+        const uint64_t eq0 = wave::bcast<uint64_t>(p0, q * WD + cnt - 1), eq1 = wave::bcast<uint64_t>(p1, q * WD + cnt - 1);
+        if (seg == q) { b0 = bq0; b1 = bq1; t0 = eq0 - bq0; t1 = eq1 - bq1; }
+      }
+      p0 -= b0; p1 -= b1;
+      const double l0 = (double)p0, tt0 = (double)t0, l1 = reg_s1(p1, c.rq), tt1 = reg_s1(t1, c.rq);
+      if (cand && !side_too_light(s, l0, tt0 - l0)) g = reg_proxy(s.criterion, l0, l1, tt0 - l0, tt1 - l1);
+    } else {
     ClsAcc L, R;
     L.init(s.criterion); R.init(s.criterion);
     // segment-relative inclusive prefix: subtract the inclusive total of the preceding segments
@@ -1881,8 +1911,9 @@ __device__ __forceinline__ void sub_node_seg(const Ctx& c, const NodeSpec& s, co
         R.add(tw - lw);
       }
     }
-    const bool ok = cand && !side_too_light(s, L.w, R.w);
-    double g = ok ? cls_proxy(L, R, s.criterion) : -INFINITY;
+    if (cand && !side_too_light(s, L.w, R.w)) g = cls_proxy(L, R, s.criterion);
+    }
+    const bool ok = g != -INFINITY;
     int bl = ok ? j : 64;
     argmax_seg<WD>(g, bl, lane);
     const int bsel = __shfl(b, seg * WD + (bl & (WD - 1)));
@@ -2017,28 +2048,29 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     int nonconst = 0, best_f = -1, best_b = -1;
     double best_g = -INFINITY, best_mid = 0.0;
     const FeatPerm fp = feat_perm(e.key, d);
-    if (!REG && cache && cnt <= 32 && (FC >= 0 || !c.mono)) {
+    if (cache && cnt <= 32 && (FC >= 0 || !c.mono) && DML_SUB_SEG_REG + !REG > 0) {
       // compact the node's rows: compact row j <- lane of the j-th set bit of the mask
       const bool in = (e.mask >> lane) & 1ull;
       if (in) cidx[lane_prefix(e.mask)] = lane;
       wave_lds_sync();
       const int jx = cnt <= 8 ? (lane & 7) : (cnt <= 16 ? (lane & 15) : (lane & 31));
       const int src = jx < cnt ? cidx[jx] : 0;
-      const int cls_j = __shfl(my_cls, src);
+      const int cls_j = REG ? 0 : __shfl(my_cls, src);
       const uint32_t w_j = (uint32_t)__shfl((int)(uint32_t)my_w, src);
+      const int64_t yq_j = REG ? (int64_t)wave::bcast_lane<uint64_t>((uint64_t)my_yq, src) : 0;
 #if defined(DML_X2_SUB) && DML_X2_SUB != 2   // sensitivity build: every segmented evaluation twice (the first into copies)
       {
         int nc2 = nonconst, bf2 = best_f, bb2 = best_b;
         double bg2 = best_g;
-        if (cnt <= 8) sub_node_seg<8>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw);
-        else if (cnt <= 16) sub_node_seg<16>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw);
-        else sub_node_seg<32>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw);
+        if (cnt <= 8) sub_node_seg<8, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw, yq_j);
+        else if (cnt <= 16) sub_node_seg<16, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw, yq_j);
+        else sub_node_seg<32, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw, yq_j);
         if (bg2 == -12345.0 && bf2 == 7 && nc2 == 3) atomicOr(&c.counters[kOpenOvf], bb2);
       }
 #endif
-      if (cnt <= 8) sub_node_seg<8>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw);
-      else if (cnt <= 16) sub_node_seg<16>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw);
-      else sub_node_seg<32>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw);
+      if (cnt <= 8) sub_node_seg<8, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw, yq_j);
+      else if (cnt <= 16) sub_node_seg<16, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw, yq_j);
+      else sub_node_seg<32, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw, yq_j);
       wave_lds_sync();   // cidx is rewritten by the next node
     } else
     for (int pos = 0; nonconst < s.max_features && pos < d; ++pos) {

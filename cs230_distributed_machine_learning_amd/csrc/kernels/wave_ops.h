@@ -79,6 +79,18 @@ __device__ __forceinline__ T bcast(T v, int src_lane) {
   }
 }
 
+// value of a per-lane source lane (ds_bpermute), 32/64-bit payloads
+template <typename T>
+__device__ __forceinline__ T bcast_lane(T v, int src_lane) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, (uint32_t)__shfl((int)__builtin_bit_cast(uint32_t, v), src_lane));
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)u, src_lane), hi = (uint32_t)__shfl((int)(uint32_t)(u >> 32), src_lane);
+    return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+  }
+}
+
 // lane i <- lane i+1 (lane 63 gets `fill`)
 template <typename T>
 __device__ __forceinline__ T shift_down1(T v, int lane, T fill) {
