@@ -384,9 +384,10 @@ class DeviceCache:
         base = (ds.path, os.path.getmtime(ds.path) if ds.path else 0, tuple(ds.feature_names), ds.target_name, clf)
         # a resident float32 entry serves every job on this table (a tree job reads its bins
         # too), so the free-HBM test below never caches the same table twice; a bins-only
-        # entry serves the tree jobs it was made for
+        # entry serves the tree jobs it was made for, and the families that stream its host rows
         full = base + (False,)
-        tree_ok = getattr(family_of(plan["model_type"]), "binned_ok", False)
+        fam = family_of(plan["model_type"])
+        tree_ok = getattr(fam, "binned_ok", False) or getattr(fam, "streams_rows", False)
         for key in ((full, base + (True,)) if tree_ok else (full,)):
             if key in self._items:
                 self._order.remove(key)
