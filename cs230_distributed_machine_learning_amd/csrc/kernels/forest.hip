@@ -39,7 +39,7 @@
 #define DML_BLOCK_NT 256     // threads per block-tier node
 #endif
 #ifndef DML_NODES_WPE
-#define DML_NODES_WPE 4
+#define DML_NODES_WPE 3        // block tier (binary): 3 waves per SIMD, fewer spills -- 1.3 % faster than 4
 #endif
 // eval_feature is called with an LDS histogram (fused node kernels) and a global one
 // (large tier): inlined, each call site keeps its address space (ds_read / global_load);
@@ -50,7 +50,7 @@
 #define DML_EVAL_ATTR
 #endif
 #ifndef DML_NODES_WPE_WAVE
-#define DML_NODES_WPE_WAVE DML_NODES_WPE
+#define DML_NODES_WPE_WAVE 4   // wave tier (binary): 2 / 3 / 5 / 6 measured slower (ROUND3.md)
 #endif
 #ifndef DML_NODES_WPE_REG
 #define DML_NODES_WPE_REG 2   // regression node kernels: 3 histogram planes + payloads fit 256 VGPRs, no spills
