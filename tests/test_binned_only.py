@@ -106,3 +106,16 @@ def test_broadcast_binned_two_ranks_gloo():
         assert np.array_equal(Xb, ref.binned().numpy()) and np.array_equal(E, ref.edges.numpy())
         assert list(y20) == list(y[:20])
     assert out[0][3] == out[1][3]
+
+
+def test_stream_rows_covers_every_row_once():
+    X, y = _table(1000, 5)
+    dd = DeviceData(X, y, True, "cpu", binned_only=True, chunk_rows=300)
+    got = [(r0, r1, xc.numpy()) for r0, r1, xc in dd.stream_rows()]
+    assert [(a, b) for a, b, _ in got] == [(0, 300), (300, 600), (600, 900), (900, 1000)]
+    assert np.array_equal(np.concatenate([x for _, _, x in got]), X)
+    assert [(a, b) for a, b, _ in dd.stream_rows(5000)] == [(0, 1000)]
+    res = DeviceData(X, y, True, "cpu")
+    assert not res.can_stream_rows()
+    with pytest.raises(ValueError):
+        next(res.stream_rows())
