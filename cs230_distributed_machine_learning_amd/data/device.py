@@ -108,7 +108,12 @@ class DeviceData:
             raise ValueError("no host rows to stream (the table is resident or was received as bins)")
         Xh = self._X_host
         chunk = max(1, min(int(chunk_rows or self._chunk_rows), self.n))
-        pin = torch.empty((chunk, self.d), dtype=torch.float32, pin_memory=self.is_gpu)
+        if not self.is_gpu:   # a fresh host array per chunk (the consumer may keep it)
+            for r0 in range(0, self.n, chunk):
+                r1 = min(self.n, r0 + chunk)
+                yield r0, r1, torch.from_numpy(np.array(Xh[r0:r1], dtype=np.float32))
+            return
+        pin = torch.empty((chunk, self.d), dtype=torch.float32, pin_memory=True)
         for r0 in range(0, self.n, chunk):
             r1 = min(self.n, r0 + chunk)
             np.copyto(pin[:r1 - r0].numpy(), Xh[r0:r1], casting="same_kind")
