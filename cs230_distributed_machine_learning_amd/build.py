@@ -32,13 +32,6 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build the HIP kernels)")
 
 
-def _stale(target: str, sources: list[str]) -> bool:
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(s) > t for s in sources)
-
-
 def _src_hash(sources: list[str], flags: list[str]) -> str:
     import hashlib
 
@@ -60,6 +53,11 @@ def _stale_by_hash(target: str, sources: list[str], flags: list[str]) -> bool:
         return f.read().strip() != _src_hash(sources, flags)
 
 
+def _stamp(target: str, sources: list[str], flags: list[str]) -> None:
+    with open(target + ".srchash", "w") as f:
+        f.write(_src_hash(sources, flags))
+
+
 def _run(cmd: list[str]) -> None:
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
@@ -71,38 +69,48 @@ def build_hip(force: bool = False, out: str = HIP_LIB, extra_flags: tuple = ()) 
     """``out`` / ``extra_flags``: A/B variants of the kernel library (e.g. ``-DDML_PHASE_PROF``
     into ``lib/libdml_hip_phase.so``, loaded through ``DML_HIP_LIB``)."""
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
-    deps = srcs + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
     os.makedirs(LIB, exist_ok=True)
-    if out != HIP_LIB:
-        force = True
-    if force or _stale(HIP_LIB, deps):
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result",
+             "-I", os.path.join(CSRC, "kernels"), *extra_flags]
+    # staleness by CONTENT (sources + headers + flags), never by mtime: the .so files are
+    # git-ignored but travel with the tree to the GPU box, where every file has a fresh
+    # mtime -- an mtime test there could keep a library that does not match the sources
+    if force or _stale_by_hash(out, srcs + hdrs, flags):
         # one hipcc per translation unit, in parallel (forest.hip alone is most of the
-        # build), then one link
+        # build), then one link; a unit whose own content hash is unchanged keeps its object
         from concurrent.futures import ThreadPoolExecutor
 
         objdir = os.path.join(LIB, "obj", os.path.basename(out)[:-3])
         os.makedirs(objdir, exist_ok=True)
-        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result",
-                 "-I", os.path.join(CSRC, "kernels"), *extra_flags]
         objs = [os.path.join(objdir, os.path.basename(s)[:-4] + ".o") for s in srcs]
+
+        def compile_one(so):
+            src, obj = so
+            if force or _stale_by_hash(obj, [src] + hdrs, flags):
+                _run([_hipcc(), *flags, "-c", src, "-o", obj])
+                _stamp(obj, [src] + hdrs, flags)
+
         with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-            list(ex.map(lambda so: _run([_hipcc(), *flags, "-c", so[0], "-o", so[1]]), zip(srcs, objs)))
+            list(ex.map(compile_one, zip(srcs, objs)))
         tmp = out + ".tmp"
         _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", *objs, "-o", tmp])
         os.replace(tmp, out)
+        _stamp(out, srcs + hdrs, flags)
     return out
 
 
 def build_cpu(force: bool = False) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
-    deps = srcs + glob.glob(os.path.join(CSRC, "runtime", "*.h")) + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
+    deps = srcs + sorted(glob.glob(os.path.join(CSRC, "runtime", "*.h")) + glob.glob(os.path.join(CSRC, "kernels", "*.h")))
     os.makedirs(LIB, exist_ok=True)
-    if force or _stale(CPU_LIB, deps):
-        cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
+    cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
+    flags = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-ffp-contract=off"]
+    if force or _stale_by_hash(CPU_LIB, deps, flags):
         tmp = CPU_LIB + ".tmp"
-        _run([cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-ffp-contract=off",
-              "-I", os.path.join(CSRC, "kernels"), *srcs, "-o", tmp])
+        _run([*flags, "-I", os.path.join(CSRC, "kernels"), *srcs, "-o", tmp])
         os.replace(tmp, CPU_LIB)
+        _stamp(CPU_LIB, deps, flags)
     return CPU_LIB
 
 
@@ -123,8 +131,7 @@ def build_sanitized(force: bool = False) -> str:
         tmp = SAN_EXE + ".tmp"
         _run([*flags, "-I", os.path.join(CSRC, "kernels"), *srcs, "-o", tmp])
         os.replace(tmp, SAN_EXE)
-        with open(SAN_EXE + ".srchash", "w") as f:
-            f.write(_src_hash(deps, flags))
+        _stamp(SAN_EXE, deps, flags)
     return SAN_EXE
 
 

@@ -2987,6 +2987,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   }
   const unsigned nchunks = (unsigned)((a->max_active + a->chunk - 1) / a->chunk);
   int cur = 0, levels = 0, large_rounds = 0;
+  int64_t peak_open = 0;   // most open nodes of any level so far (early-predict tail rule)
   for (int i = 0; i < 4; ++i) a->tier_nodes_out[i] = 0;
   while (true) {
     HIP_OK(hipMemcpyAsync(h, c.counters, kNumCounters * 4, hipMemcpyDeviceToHost, st));
@@ -2995,10 +2996,22 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     const int ns = h[cur * kTiers + 0], nw = h[cur * kTiers + 1], nb = h[cur * kTiers + 2], nL = h[cur * kTiers + 3];
     if (ns + nw + nb + nL == 0) break;
     if (++levels > 1 << 20) return 8;
+    const int64_t open_now = (int64_t)ns + nw + nb + nL;
+    peak_open = std::max(peak_open, open_now);
     HIP_OK(hipMemsetAsync(c.counters + (1 - cur) * kTiers, 0, kTiers * 4, st));
     // reserve the child pairs of every wave/block-tier node of this level up front
     const int64_t pair_w = h[kPool], pair_b = pair_w + 2LL * nw, pool_next = pair_b + 2LL * nb;
-    if (pool_next > a->pool_cap) { a->status_out = 1; return 0; }
+    if (pool_next > a->pool_cap) {
+      // pool overflow: the caller regrows with a bigger pool -- first make the stream wait for
+      // any early predict still reading this pool / writing its outputs (their buffers are
+      // freed and re-carved by the retry)
+      if (a->early_pred && pred_stream()) {
+        HIP_OK(hipEventRecord(pred_event(), pred_stream()));
+        HIP_OK(hipStreamWaitEvent(st, pred_event(), 0));
+      }
+      a->status_out = 1;
+      return 0;
+    }
     if (nw + nb) {
       *h_pool = (int32_t)pool_next;
       HIP_OK(hipMemcpyAsync(c.counters + kPool, h_pool, 4, hipMemcpyHostToDevice, st));
@@ -3050,7 +3063,11 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       k_compact<<<(unsigned)((nst + 1023) / 1024), 256, 0, st>>>(c, 1 - cur, nst);
     }
     HIP_OK(hipGetLastError());
-    if (a->early_pred && a->fit_done_level) {   // fits complete after this level: predict them now
+    // fits complete after this level: predict them now -- unless the build is in its tail (few
+    // open nodes left): the predicts then have little tree work to hide behind and, sharing a
+    // hardware queue with a tier stream, hold up the remaining levels; such fits stay marked
+    // and are predicted after the build, all in one launch (ops/forest_ops.py GpuPredict.run)
+    if (a->early_pred && a->fit_done_level && open_now * 16 >= peak_open) {
       int32_t* done = (int32_t*)a->fit_done_level;
       hipStream_t ps = pred_stream();
       bool any = false;

@@ -28,6 +28,7 @@ struct PredictArgs {
   int64_t d;          // features (bins per row actually read)
   int64_t lds_pitch;  // set by dml_forest_predict: LDS row stride, 0 = no staging
   int64_t fit_row_off_host;   // optional host copy of fit_row_off (per-fit grid sizes)
+  int64_t fit_skip;           // optional int32[F] device mask: fits already predicted (early) are skipped
 };
 
 // leaf of U consecutive trees [t0, t0 + u_n) for one row, walked in lock-step: the U
@@ -82,6 +83,7 @@ template <int MAXC, int kPredU>
 __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
   const int f = blockIdx.y;
+  if (a.fit_skip && (GPTR(const int32_t, a.fit_skip))[f]) return;
   const int32_t* toff = GPTR(const int32_t, a.fit_tree_off);
   const int64_t* roff = GPTR(const int64_t, a.fit_row_off);
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -142,6 +144,7 @@ template <int kPredU>
 __global__ __launch_bounds__(256) void k_predict_reg(PredictArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
   const int f = blockIdx.y;
+  if (a.fit_skip && (GPTR(const int32_t, a.fit_skip))[f]) return;
   const int32_t* toff = GPTR(const int32_t, a.fit_tree_off);
   const int64_t* roff = GPTR(const int64_t, a.fit_row_off);
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -384,6 +387,7 @@ int dml_forest_predict_fit(const PredictArgs* a, int32_t f, hipStream_t st) {
   b.fit_tree_off = a->fit_tree_off + 4 * (int64_t)f;   // int32[F+1] device array, advanced to fit f
   b.fit_row_off = a->fit_row_off + 8 * (int64_t)f;     // int64[F+1]
   b.F = 1;
+  b.fit_skip = 0;
   b.max_rows = roff ? roff[f + 1] - roff[f] : a->max_rows;
   return dml_forest_predict(&b, st);
 }

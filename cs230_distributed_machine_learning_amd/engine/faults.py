@@ -16,6 +16,10 @@ reported once and the job hangs below 100 % (D5, master/task_handler.py:91).  He
   after claiming its (k+1)-th slice, i.e. with claimed-but-unpublished work — what a
   crashed GPU process looks like to the controller, which must detect the silence and
   re-queue the slice to the survivors.
+* ``DML_STOP_RANK_IN="<rank>:<collective>"`` (``load`` / ``scores``) makes that rank SIGSTOP
+  itself on entering the named side-group collective: a HUNG peer (its sockets stay open,
+  unlike a dead one), which the survivors' collective timeouts must turn into a fallback;
+  ``DML_FAIL_RANK_IN`` (same form) makes it raise there instead.
 """
 from __future__ import annotations
 
@@ -76,6 +80,32 @@ def reset() -> None:
 def maybe_inject(seed: int, slice_key: str, attempt: int) -> None:
     if plan().should_fail(seed, slice_key, attempt):
         raise InjectedFault(f"injected fault (slice {slice_key}, attempt {attempt})")
+
+
+def _rank_spec(var: str, rank: int, what: str) -> bool:
+    spec = os.environ.get(var, "")
+    if not spec:
+        return False
+    r, _, w = spec.partition(":")
+    return int(r) == rank and w == what
+
+
+def maybe_stop_in_collective(rank: int, what: str) -> None:
+    """Fault injection on entering a side-group collective (``load`` / ``scores``):
+    ``DML_STOP_RANK_IN`` hangs the rank (SIGSTOP), ``DML_FAIL_RANK_IN`` makes it raise before
+    the collective (an OOM while its peers are already inside), ``DML_COLL_DELAY_S`` delays
+    every rank (a long broadcast)."""
+    delay = float(os.environ.get("DML_COLL_DELAY_S", "0") or 0.0)
+    if delay > 0:
+        import time
+
+        time.sleep(delay)
+    if _rank_spec("DML_FAIL_RANK_IN", rank, what):
+        raise InjectedFault(f"injected {what} collective failure on rank {rank}")
+    if _rank_spec("DML_STOP_RANK_IN", rank, what):
+        import signal
+
+        os.kill(os.getpid(), signal.SIGSTOP)
 
 
 def maybe_kill(rank: int, slices_done: int) -> None:

@@ -611,15 +611,26 @@ class GpuPredict:
         self.args = p
 
     def run(self, fits=None) -> None:
+        """Predict ``fits`` (None: all) in ONE launch (grid.y = fit; fits outside the list
+        exit at once through the skip mask) -- the deep fits left after the build's early
+        predicts run concurrently instead of one launch after another."""
         lib = native.hip_lib()
         st = native.stream_handle(self.dev)
         with trace.range("forest_predict"):
-            if fits is None:
+            if fits is not None and len(fits) == 0:
+                return
+            if fits is None or len(fits) == self.F:
+                self.args.fit_skip = 0
                 rc = lib.dml_forest_predict(ctypes.byref(self.args), st)
+            elif len(fits) == 1:
+                rc = lib.dml_forest_predict_fit(ctypes.byref(self.args), int(fits[0]), st)
             else:
-                rc = 0
-                for f in fits:
-                    rc = rc or lib.dml_forest_predict_fit(ctypes.byref(self.args), int(f), st)
+                skip = np.ones(self.F, dtype=np.int32)
+                skip[np.asarray(list(fits), dtype=np.int64)] = 0
+                self._skip = torch.from_numpy(skip).to(self.dev, non_blocking=False)
+                self.args.fit_skip = native.ptr(self._skip)
+                rc = lib.dml_forest_predict(ctypes.byref(self.args), st)
+                self.args.fit_skip = 0
         if rc:
             raise RuntimeError(f"dml_forest_predict failed ({rc})")
 

@@ -69,12 +69,18 @@ def init(backend: Optional[str] = None, timeout_s: float = 1800.0, want_gpu: Opt
         os.environ.setdefault("MASTER_PORT", "29561")
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(world))
-        # RCCL watchdog: a collective that outlives the timeout (a peer rank
-        # died mid-job) is caught by the watchdog, which aborts the communicator and ends
-        # THIS process (mode 1, TearDown) instead of leaving it hung forever; the runner
-        # avoids collectives once a peer is known dead (parallel/runner.py), so this only
-        # fires for a death in the middle of a collective epoch
-        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        # RCCL failure handling: a collective that outlives its timeout (a peer
+        # rank died or hung mid-collective) must not take the service down with it.  Mode 2
+        # (CleanUpOnly) makes the watchdog abort the communicator WITHOUT tearing the process
+        # down, and blocking wait makes the timed-out collective raise in the thread that
+        # issued it -- the runner's collective thread / data-parallel epoch then reports the
+        # error and the dispatcher marks the group broken (parallel/runner.py).  Mode 1
+        # (TearDown) would end every survivor, rank 0 (controller + gateway + store) included.
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
+        os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
+        # the monitor thread std::abort()s a process whose watchdog looks stuck (an abort that
+        # itself blocks): that is a teardown too
+        os.environ.setdefault("TORCH_NCCL_ENABLE_MONITORING", "0")
         timeout_s = float(os.environ.get("DML_COLLECTIVE_TIMEOUT_S", timeout_s))
         kw = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
@@ -100,8 +106,18 @@ def side_group():
     if not info().is_dist:
         return None
     if _SIDE is None:
-        _SIDE = dist.new_group(ranks=list(range(info().world)), backend=info().backend)
+        # a SHORT timeout: a side collective stuck on a dead or hung peer raises here after
+        # side_timeout_s() instead of the default group's long one, and the runner falls back
+        # to host staging / store copies (parallel/runner.py _break_group)
+        _SIDE = dist.new_group(ranks=list(range(info().world)), backend=info().backend,
+                               timeout=datetime.timedelta(seconds=side_timeout_s()))
     return _SIDE
+
+
+def side_timeout_s() -> float:
+    """Per-collective timeout of the side communicator (``DML_SIDE_TIMEOUT_S``, default 120 s:
+    a 40 GB table broadcast over xGMI takes well under that)."""
+    return float(os.environ.get("DML_SIDE_TIMEOUT_S", "120"))
 
 
 def barrier(group=None) -> None:

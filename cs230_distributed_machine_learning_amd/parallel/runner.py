@@ -144,6 +144,16 @@ class LockedStore:
 SCORE_HEAD = 4   # score row: [ok, mean_cv_score, std_cv_score, n_cv, cv_0 .. cv_{n_cv-1}]
 
 
+def score_width(plan: Dict[str, Any]) -> int:
+    """Columns of a job's score rows: the head plus one per CV fold (``cv`` is the user's
+    integer, reference aws-prod/master/task_handler.py:183,203 -- never truncated)."""
+    try:
+        cv = int(plan.get("cv", 5))
+    except (TypeError, ValueError):
+        cv = 5
+    return SCORE_HEAD + max(1, cv)
+
+
 def score_row(ok: bool, result: Dict[str, Any], width: int) -> np.ndarray:
     """A candidate's numeric result as one float64 row (NaN padded) for the scores epoch."""
     row = np.full(width, np.nan, dtype=np.float64)
@@ -237,7 +247,7 @@ class WorkerCore:
         # job's all-gather; rank 0's merged [candidates, width + 1] table per job after it
         self.score_rows: Dict[int, Dict[int, np.ndarray]] = {}
         self.gathered: Dict[int, Any] = {}
-        self.score_width = 64
+        self.intervals: List[tuple] = []      # (kind, wall start, wall end) of collective work
         self.cache_lock = threading.RLock()   # the worker and the collective thread share the cache
         # the side communicator (collective with every rank: built here, by every in-group rank)
         self.side = dist.side_group() if (in_group and self.inf.is_dist) else None
@@ -343,6 +353,8 @@ class WorkerCore:
         """A task of the collective thread (side group, own stream): a dataset broadcast or
         a job's scores all-gather.  Every in-group rank runs the tasks in the same order."""
         t0 = time.perf_counter()
+        tw0 = time.time()
+        faults.maybe_stop_in_collective(self.wid, a["kind"])   # fault injection (tests)
         ctx = torch.cuda.stream(stream) if stream is not None else _null_ctx()
         with ctx:
             if a["kind"] == "load":
@@ -356,7 +368,15 @@ class WorkerCore:
             if stream is not None:
                 stream.synchronize()   # the table is complete before any slice may use it
         out["wall"] = time.perf_counter() - t0
+        self.note_interval("side:" + a["kind"], tw0)
         return out
+
+    def note_interval(self, kind: str, t0: float) -> None:
+        """Wall-clock span of a collective task on this rank (tests check that side-group
+        tasks and data-parallel epochs never overlap)."""
+        self.intervals.append((kind, t0, time.time()))
+        if len(self.intervals) > 4096:
+            del self.intervals[:2048]
 
     def _scores(self, a, group=None) -> Dict[str, Any]:
         """Scores epoch of one job (every rank of the group): each rank contributes the score
@@ -397,8 +417,9 @@ class WorkerCore:
         self.slices_done += 1
         if self.in_group:   # kept for the job's scores epoch (parallel/runner.py header)
             rows = self.score_rows.setdefault(a["seq"], {})
+            width = score_width(msg["plan"])
             for r in results:
-                rows[r.candidate] = score_row(r.ok, r.result or {}, self.score_width)
+                rows[r.candidate] = score_row(r.ok, r.result or {}, width)
         return {"results": _enc_results(results, metrics), "wall": wall, "load_s": load_s,
                 "cache": self.cache_keys()}
 
@@ -406,11 +427,18 @@ class WorkerCore:
         """Data-parallel job on the whole process group: every rank runs every slice in
         order on its row shard (the fits' reductions are collectives), then all ranks
         refit the winner together; rank 0 decides the winner and keeps the model."""
-        from .data_parallel import RowShard, scatter_table
-
         seq = a["seq"]
         msg = self.job_msg(seq)
         plan = msg["plan"]
+        tw0 = time.time()
+        try:
+            return self._dp_run(seq, msg, plan, ctl)
+        finally:
+            self.note_interval("dp", tw0)
+
+    def _dp_run(self, seq, msg, plan, ctl) -> Dict[str, Any]:
+        from .data_parallel import RowShard, scatter_table
+
         X = y = None
         if self.inf.rank == 0:
             ds = ctl.registry.load(msg["dataset_id"], plan["feature_columns"], plan["target_column"])
@@ -677,6 +705,13 @@ class DistributedRunner(Runner):
         self.coll_seq = 0
         self.coll_pending: Dict[int, Dict[str, Any]] = {}
         self._coll_seen = 0
+        # side-group tasks held back while a collective epoch (default group) is queued or
+        # running: the two communicators never have operations in flight at the same time, so
+        # no rank can issue them in a different order than another (RCCL deadlock)
+        self.coll_deferred: List[tuple] = []
+        # a side collective failed or overran its deadline: no more collectives of any kind
+        # (datasets host-staged, scores from the store copies, data-parallel jobs task-parallel)
+        self.group_broken = False
         self._waiting = False                              # the dispatcher is blocked on a wake key
         self._next_liveness = self._next_membership = 0.0
         self._waiter = LockedStore(self.st._s, waiter=_private_client()) if isinstance(self.st, LockedStore) else None
@@ -796,7 +831,7 @@ class DistributedRunner(Runner):
             js.queue.extend(range(len(slices)))
             # datasets travel by collective broadcast while the whole group is alive and
             # nobody joined from outside it; otherwise host-staged
-            js.transport = "rccl" if (dist.info().is_dist and not self.dead) else "staged"
+            js.transport = "rccl" if (dist.info().is_dist and not self.dead and not self.group_broken) else "staged"
             if js.transport == "staged" or self._joiners_alive():
                 self._stage(js)
             self._publish_msg(js)
@@ -834,7 +869,7 @@ class DistributedRunner(Runner):
     def _data_parallel(self, plan, n_todo: int, n_rows: int, n_feat: int) -> bool:
         """Row-sharded data parallelism needs every rank of the group: never once one died."""
         par = plan.get("parallelism", "auto")
-        if par == "task" or not dist.info().is_dist or self.dead or \
+        if par == "task" or not dist.info().is_dist or self.dead or self.group_broken or \
                 not getattr(family_of(plan["model_type"]), "data_parallel", False):
             return False
         if par == "data":
@@ -877,11 +912,13 @@ class DistributedRunner(Runner):
         # a collective epoch owns the process group until every rank has answered
         if self.epoch is not None:
             return
+        if not self.epoch_queue and self.coll_deferred:
+            self._flush_coll()
         if self.epoch_queue:
             ep = self.epoch_queue[0]
             js = ep["job"]
             group = [w for w in self.workers.values() if w.in_group]
-            if self.dead or any(not w.alive for w in group):
+            if self.dead or self.group_broken or any(not w.alive for w in group):
                 # the group is broken: a data-parallel job runs task-parallel instead
                 self.epoch_queue.pop(0)
                 if ep["kind"] == "dp":
@@ -893,7 +930,9 @@ class DistributedRunner(Runner):
                     js.scores_pending = False
                     self._complete(js)
                 return
-            if all(w.busy is None for w in group):
+            # the epoch's collectives (default group) start only once no side-group task is in
+            # flight; new side tasks are deferred meanwhile (_post_coll)
+            if all(w.busy is None for w in group) and not self.coll_pending:
                 if self._drain_since is not None:
                     self.stats["max_drain_wait_s"] = max(self.stats["max_drain_wait_s"],
                                                          time.time() - self._drain_since)
@@ -902,7 +941,7 @@ class DistributedRunner(Runner):
                 self.epoch = {"kind": ep["kind"], "job": js, "waiting": {w.wid for w in group}}
                 payload = {"kind": ep["kind"], "seq": js.seq}
                 if ep["kind"] == "scores":
-                    payload.update(n=len(js.job.subtasks), width=self.core.score_width)
+                    payload.update(n=len(js.job.subtasks), width=score_width(js.plan))
                 for w in group:
                     self._assign(w, payload)
                 return
@@ -963,11 +1002,57 @@ class DistributedRunner(Runner):
         self._post_coll({"kind": "load", "seq": js.seq}, js, dkey=key)
 
     def _post_coll(self, task: Dict[str, Any], js: _JobState, dkey: str = "") -> None:
+        if self.group_broken:
+            self._coll_fallback(task["kind"], js)
+            return
+        if self.epoch is not None or self.epoch_queue:
+            if not any(t[0]["kind"] == task["kind"] and t[1] is js for t in self.coll_deferred):
+                self.coll_deferred.append((task, js, dkey))
+            return
         i = self.coll_seq
         self.coll_seq += 1
         self.st.set(f"coll/{i}", json.dumps(task))
         self.coll_pending[i] = {"kind": task["kind"], "job": js, "dkey": dkey, "t0": time.time(),
                                 "waiting": {w.wid for w in self.workers.values() if w.in_group and w.alive}}
+
+    def _flush_coll(self) -> None:
+        """Post the side-group tasks deferred while a collective epoch held the group."""
+        todo, self.coll_deferred = self.coll_deferred, []
+        for task, js, dkey in todo:
+            if not js.finished:
+                self._post_coll(task, js, dkey)
+
+    def _coll_fallback(self, kind: str, js: _JobState) -> None:
+        """A side-group task that can no longer run: a load becomes host staging, a scores
+        gather leaves the per-slice store copies standing."""
+        if kind == "load":
+            if js.transport == "rccl":
+                js.transport = "staged"
+            self._stage(js)
+        elif kind == "scores" and js.scores_pending:
+            js.scores_pending = False
+            js.scores_via = "store-fallback"
+            self._complete(js)
+
+    def _break_group(self, why: str) -> None:
+        """The side communicator failed (a collective raised or overran its deadline: a rank
+        is dead, hung, or out of memory): no rank issues another collective.  Every pending
+        and deferred side task falls back, every job that counted on RCCL is host-staged.
+        Safe to call more than once."""
+        first = not self.group_broken
+        self.group_broken = True
+        if first:
+            log.error("process group broken (%s): host staging and store copies from now on", why)
+        pending = [(t["kind"], t["job"]) for t in self.coll_pending.values()]
+        pending += [(task["kind"], js) for task, js, _ in self.coll_deferred]
+        self.coll_pending.clear()
+        self.coll_deferred = []
+        for kind, js in pending:
+            self._coll_fallback(kind, js)
+        for js in self.jobs:
+            if not js.finished and js.transport == "rccl":
+                js.transport = "staged"
+                self._stage(js)
 
     def _poll_coll(self) -> bool:
         """Answers of the collective threads (``colldone/<worker>/<task>``)."""
@@ -991,6 +1076,11 @@ class DistributedRunner(Runner):
 
     def _on_coll(self, t: Dict[str, Any], wid: int, out: Dict[str, Any]) -> None:
         js, w = t["job"], self.workers.get(wid)
+        if "error" in out:
+            # the failing rank's collective thread has stopped and its peers are (or will be)
+            # stuck in this collective until the side timeout: the group is broken for good
+            self._break_group(f"{t['kind']} collective failed on worker {wid}: {out['error']}")
+            return
         if t["kind"] == "load":
             if w is not None and "cache" in out:
                 w.loaded = set(out["cache"])
@@ -1154,7 +1244,8 @@ class DistributedRunner(Runner):
     def _collective_scores(self, js: _JobState) -> bool:
         """The job's scores can travel by collective: the whole launch group is alive and
         every slice ran inside it."""
-        return (js.transport == "rccl" and dist.info().is_dist and not self.dead and js.scores_via == "store"
+        return (js.transport == "rccl" and dist.info().is_dist and not self.dead and not self.group_broken
+                and js.scores_via == "store"
                 and all(w.alive for w in self.workers.values() if w.in_group))
 
     def _merge_scores(self, js: _JobState) -> None:
@@ -1194,7 +1285,7 @@ class DistributedRunner(Runner):
             if not js.scores_pending:
                 js.scores_pending = True
                 self._post_coll({"kind": "scores", "seq": js.seq, "n": len(js.job.subtasks),
-                                 "width": self.core.score_width}, js)
+                                 "width": score_width(js.plan)}, js)
             return
         best = pick_refit(self.ctl, js.job, js.plan, js.done[js.held])
         if best is None:
@@ -1236,6 +1327,8 @@ class DistributedRunner(Runner):
         self.epoch["waiting"].discard(w.wid)
         if not self.epoch["waiting"]:
             self.epoch = None
+            if not self.epoch_queue and self.coll_deferred:
+                self._flush_coll()
 
     def _job(self, seq) -> Optional[_JobState]:
         if seq is None:
@@ -1309,6 +1402,12 @@ class DistributedRunner(Runner):
             else:
                 self.ctl.scheduler.heartbeat(self.worker_ids.get(w.wid, ""))
         self.ctl.scheduler.heartbeat(self.worker_ids.get(0, ""))
+        # a side task no rank answered within its deadline (its peers' blocking waits time out
+        # after side_timeout_s; a collective thread that died silently never answers)
+        limit = dist.side_timeout_s() + float(os.environ.get("DML_COLL_GRACE_S", "30"))
+        late = [i for i, t in self.coll_pending.items() if now - t["t0"] > limit]
+        if late:
+            self._break_group(f"side collective task(s) {late} unanswered after {limit:.0f}s")
 
     def _declare_dead(self, w: _Worker, a: Optional[Dict[str, Any]]) -> None:
         w.alive = False
@@ -1327,17 +1426,6 @@ class DistributedRunner(Runner):
             self._epoch_answer(w)
         if w.in_group:
             # pending side-group collectives can no longer complete: loads fall back to
-            # host staging (below), score gathers to the per-slice store copies
-            for i, t in list(self.coll_pending.items()):
-                self.coll_pending.pop(i, None)
-                js = t["job"]
-                if t["kind"] == "scores" and js.scores_pending:
-                    js.scores_pending = False
-                    js.scores_via = "store-fallback"
-                    self._complete(js)
-        # the group is broken for good: pending collectives become host-staged / task-parallel
-        if w.in_group:
-            for js in self.jobs:
-                if not js.finished and js.transport == "rccl":
-                    js.transport = "staged"
-                    self._stage(js)
+            # host staging, score gathers to the per-slice store copies; the group is broken
+            # for good (pending collectives become host-staged / task-parallel)
+            self._break_group(f"worker {w.wid} died")

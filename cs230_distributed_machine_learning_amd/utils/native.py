@@ -80,7 +80,7 @@ ForestArgs = _i64_struct(
 PredictArgs = _i64_struct(
     "PredictArgs",
     ["Xb", "ld", "nodes", "node_val", "VC", "is_reg", "n_classes", "fit_tree_off", "fit_row_off", "rows",
-     "out_pred", "out_proba", "F", "max_rows", "d", "lds_pitch", "fit_row_off_host"],
+     "out_pred", "out_proba", "F", "max_rows", "d", "lds_pitch", "fit_row_off_host", "fit_skip"],
 )
 
 ScoreArgs = _i64_struct("ScoreArgs", ["rows", "fit_row_off", "pred", "ycls", "yreg", "is_reg", "out", "F"])
@@ -103,9 +103,7 @@ def cpu_lib() -> ctypes.CDLL:
     global _cpu
     with _lock:
         if _cpu is None:
-            path = _build.CPU_LIB
-            if not os.path.exists(path) or _build._stale(path, _cpu_sources()):
-                _build.build_cpu()
+            path = _build.build_cpu()   # rebuilds only when the sources' content changed
             lib = _load(path)
             lib.dml_cpu_sizeof_treespec.restype = c_i32
             if lib.dml_cpu_sizeof_treespec() != TREESPEC_DTYPE.itemsize:
@@ -134,12 +132,6 @@ def cpu_lib() -> ctypes.CDLL:
             lib.dml_cpu_dp_step.argtypes = [c_vp, c_i32]
             _cpu = lib
         return _cpu
-
-
-def _cpu_sources():
-    import glob
-
-    return glob.glob(os.path.join(_build.CSRC, "runtime", "*.cpp")) + glob.glob(os.path.join(_build.CSRC, "kernels", "*.h"))
 
 
 def hip_lib() -> ctypes.CDLL:

@@ -162,3 +162,146 @@ def test_worker_joins_running_service_and_leaves():
     workers = {m["worker_id"] for m in metrics}
     assert f"rank{wid}" in workers, workers        # the joiner really ran slices
     assert left["left"] is True
+
+
+# ---- RCCL failure safety and collective ordering (run here on gloo) ---------------
+def _serve_rc(rank, world, port, root, outq, drive_fn, env):
+    """_serve, but rank 0 reports its own exit status through the queue."""
+    _serve(rank, world, port, root, outq, drive_fn, env)
+
+
+def _launch_faulty(world, drive_fn, env, timeout=240):
+    """Like _launch, for runs where a rank hangs (SIGSTOP): the caller gets rank 0's result
+    and exit code; every other process is killed afterwards."""
+    root = tempfile.mkdtemp()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_serve, args=(r, world, port, root, q, drive_fn, env)) for r in range(world)]
+    for p in procs:
+        p.start()
+    t0 = time.time()
+    try:
+        out = q.get(timeout=timeout)
+        procs[0].join(timeout=60)
+        rc0, wall = procs[0].exitcode, time.time() - t0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+    assert out[0] == "ok", out[1]
+    return out[1], rc0, wall
+
+
+def _drive_two_jobs(ctl, runner):
+    sid = ctl.create_session()[1]["session_id"]
+    ctl.download_data(sid, {"dataset_url": "classification?n=3000&d=8&seed=11", "dataset_name": "t",
+                            "dataset_type": "synthetic"})
+    grid = {"min_samples_leaf": [1, 2, 4, 8]}
+    t0 = time.time()
+    st, a = ctl.train(sid, _grid_job("job-1", "t", "RandomForestClassifier", grid, base={"n_estimators": 8}))
+    assert st in (200, 202), a
+    ctl.table.wait_finished(a["job_id"], timeout=180)
+    t1 = time.time() - t0
+    s1 = ctl.check_status(sid, a["job_id"])[1]
+    st, b = ctl.train(sid, _grid_job("job-2", "t", "RandomForestClassifier", {"max_depth": [2, 4]},
+                                     base={"n_estimators": 8}))
+    ctl.table.wait_finished(b["job_id"], timeout=180)
+    s2 = ctl.check_status(sid, b["job_id"])[1]
+    vias = [r.get("scores_via") for r in s1["job_result"]["results"]]
+    return {"s1": s1, "s2": s2, "t1": t1, "broken": runner.group_broken, "vias": vias,
+            "dead": sorted(runner.dead), "pending": len(runner.coll_pending)}
+
+
+def test_hung_rank_in_scores_gather_rank0_survives():
+    """A rank hangs (SIGSTOP, sockets stay open) inside a job's scores all-gather: rank 0's
+    side collective times out (DML_SIDE_TIMEOUT_S) and RAISES instead of tearing the process
+    down; the dispatcher marks the group broken, the job completes from the store copies, the
+    next job runs host-staged, and rank 0 exits 0."""
+    env = {"DML_STOP_RANK_IN": "2:scores", "DML_SIDE_TIMEOUT_S": "6", "DML_DEAD_AFTER_S": "600"}
+    r, rc0, wall = _launch_faulty(3, _drive_two_jobs, env)
+    assert r["s1"]["job_status"] == "completed" and len(r["s1"]["job_result"]["results"]) == 4
+    assert r["s2"]["job_status"] == "completed" and len(r["s2"]["job_result"]["results"]) == 2
+    assert r["broken"] and r["dead"] == [] and r["pending"] == 0, r   # hung, not declared dead
+    assert all(v in (None, "store-fallback") for v in r["vias"]), r["vias"]
+    assert r["t1"] < 6 + 30 + 60, r["t1"]     # within the side timeout (+ deadline grace + fit time)
+    assert rc0 == 0, rc0
+
+
+def test_failed_collective_breaks_group_next_job_completes():
+    """One rank's collective task raises before the gather (an OOM while its peers are already
+    inside): the group is marked broken at once, pending scores fall back to the store copies,
+    and the next job still completes (host-staged)."""
+    env = {"DML_FAIL_RANK_IN": "1:scores", "DML_SIDE_TIMEOUT_S": "6"}
+    r, rc0, _ = _launch_faulty(3, _drive_two_jobs, env)
+    assert r["s1"]["job_status"] == "completed" and r["s2"]["job_status"] == "completed"
+    assert r["broken"] and r["pending"] == 0, r
+    assert rc0 == 0, rc0
+
+
+def _drive_dp_during_broadcast(ctl, runner):
+    sid = ctl.create_session()[1]["session_id"]
+    ctl.download_data(sid, {"dataset_url": "classification?n=4000&d=8&seed=12", "dataset_name": "a",
+                            "dataset_type": "synthetic"})
+    ctl.download_data(sid, {"dataset_url": "classification?n=4000&d=8&seed=13", "dataset_name": "b",
+                            "dataset_type": "synthetic"})
+    # job A needs a broadcast of table "a" (slow: DML_COLL_DELAY_S); the data-parallel job B is
+    # submitted while it is in flight
+    st, a = ctl.train(sid, _grid_job("job-a", "a", "RandomForestClassifier", {"max_depth": [2, 3]},
+                                     base={"n_estimators": 4}))
+    t0 = time.time()
+    while not runner.coll_pending and time.time() - t0 < 30:
+        time.sleep(0.02)
+    in_flight = bool(runner.coll_pending)
+    body = _grid_job("job-b", "b", "LogisticRegression", {"C": [0.5, 1.0]})
+    body["train_params"]["parallelism"] = "data"
+    st, b = ctl.train(sid, body)
+    assert st in (200, 202), b
+    ctl.table.wait_finished(a["job_id"], timeout=180)
+    ctl.table.wait_finished(b["job_id"], timeout=180)
+    return {"in_flight": in_flight, "a": ctl.check_status(sid, a["job_id"])[1]["job_status"],
+            "b": ctl.check_status(sid, b["job_id"])[1]["job_status"], "iv": list(runner.core.intervals)}
+
+
+def test_dp_epoch_never_overlaps_side_collectives():
+    """A data-parallel job (default-group collectives, worker thread) submitted while a
+    side-group broadcast is in flight starts only after it, and no side task is posted while
+    the epoch holds the group: on every rank the two communicators never have operations in
+    flight together (RCCL may deadlock on unordered use of two communicators)."""
+    r = _launch(2, _drive_dp_during_broadcast, env={"DML_COLL_DELAY_S": "1.5"})
+    assert r["in_flight"] and r["a"] == "completed" and r["b"] == "completed", r
+    iv = r["iv"]
+    dp = [(s, e) for k, s, e in iv if k == "dp"]
+    side = [(s, e) for k, s, e in iv if k.startswith("side:")]
+    assert dp and side, iv
+    for s0, e0 in dp:
+        for s1, e1 in side:
+            assert e1 <= s0 or e0 <= s1, (iv,)
+
+
+def test_score_rows_carry_every_fold():
+    """cv > 60 folds: the scores epoch's rows are sized from the job's cv, so J5 keeps every
+    fold score (a fixed 64-column row cut them to 60)."""
+    from cs230_distributed_machine_learning_amd.parallel.runner import SCORE_HEAD, score_row, score_width
+
+    w = score_width({"cv": 80})
+    assert w == SCORE_HEAD + 80
+    row = score_row(True, {"cv_scores": [i / 100 for i in range(80)], "mean_cv_score": 0.4,
+                           "std_cv_score": 0.1}, w)
+    assert int(row[3]) == 80 and row[SCORE_HEAD + 79] == 0.79
+
+
+def _drive_cv80(ctl, runner):
+    sid = ctl.create_session()[1]["session_id"]
+    ctl.download_data(sid, {"dataset_url": "classification?n=800&d=5&seed=14", "dataset_name": "s",
+                            "dataset_type": "synthetic"})
+    st, a = ctl.train(sid, _grid_job("job-cv", "s", "LogisticRegression", {"C": [0.5, 2.0]}, cv=80))
+    ctl.table.wait_finished(a["job_id"], timeout=180)
+    s = ctl.check_status(sid, a["job_id"])[1]
+    return [(len(r["cv_scores"]), r.get("scores_via")) for r in s["job_result"]["results"]]
+
+
+def test_cv80_job_through_scores_epoch():
+    out = _launch(2, _drive_cv80)
+    assert out == [(80, "gloo"), (80, "gloo")], out
