@@ -95,15 +95,19 @@
 
 // optional per-phase cycle accounting of the fused node kernel (-DDML_PHASE_PROF builds only)
 #ifdef DML_PHASE_PROF
-__device__ unsigned long long g_phase[3][8];
+// [0] wave tier, [1] block tier, [2] subtree tier phases (slot 7: nodes), [3] rows per tier +
+// subtree internal-node counts by evaluation path
+__device__ unsigned long long g_phase[4][8];
 #define PH_BEGIN uint64_t _pt = clock64(); uint64_t _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define PH(i) if (threadIdx.x == 0) { const uint64_t _n = clock64(); _acc[i] += _n - _pt; _pt = _n; }
 #define PH_END(t) if (threadIdx.x == 0) { _acc[7] = 1; for (int _i = 0; _i < 8; ++_i) atomicAdd(&g_phase[t][_i], _acc[_i]); \
-                                            atomicAdd(&g_phase[2][t], (unsigned long long)on.count); }
+                                            atomicAdd(&g_phase[3][t], (unsigned long long)on.count); }
+#define PH_CNT(i, v) if (threadIdx.x == 0) atomicAdd(&g_phase[3][i], (unsigned long long)(v));
 #else
 #define PH_BEGIN
 #define PH(i)
 #define PH_END(t)
+#define PH_CNT(i, v)
 #endif
 
 namespace dml {
@@ -1958,6 +1962,7 @@ __device__ __forceinline__ void sub_node_seg(const Ctx& c, const NodeSpec& s, co
 template <bool REG, int FC>
 __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  PH_BEGIN
   const OpenNode on = c.open[set_cur][0][blockIdx.x];
   const NodeSpec s = spec_of<FC>(c, on.tree);
   const int lane = threadIdx.x;
@@ -2043,6 +2048,7 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   int used = 0;
   wave_lds_sync();
   int sp = 1;
+  PH(0)
   while (sp > 0) {
     --sp;
     const SubEntry e = stack[sp];
@@ -2075,6 +2081,9 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
       else if (cnt <= 16) sub_node_seg<16, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw, yq_j);
       else sub_node_seg<32, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw, yq_j);
       wave_lds_sync();   // cidx is rewritten by the next node
+      PH(1)
+      PH_CNT(4, 1)
+      PH_CNT(5, cnt)
     } else
     for (int pos = 0; nonconst < s.max_features && pos < d; ++pos) {
       const int f = feature_at(fp, pos, d);
@@ -2093,6 +2102,11 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
         ++nonconst;
         if (bb >= 0 && g > best_g) { best_g = g; best_f = f; best_b = bb; best_mid = mid; }
       }
+    }
+    if (!(cache && cnt <= 32 && (FC >= 0 || !c.mono) && DML_SUB_SEG_REG + !REG > 0)) {
+      PH(2)
+      PH_CNT(6, 1)
+      PH_CNT(7, cnt)
     }
     if (best_f < 0) continue;
     const int mybin = cache ? xc[lane * dp + best_f] : (lane < cnt0 ? xg[best_f] : 0);
@@ -2170,11 +2184,14 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
     }
     sp = wave::bcast<int>(sp, 0);
     wave_lds_sync();
+    PH(3)
   }
   // reserved-but-unused node pairs become well-formed (unreferenced) leaves, so any
   // pass over the whole pool sees valid records
   const NodeRec leaf{-1, -1};
   for (int i = 2 * used + lane; i < 2 * max_splits; i += 64) c.nodes[pool_base + i] = leaf;
+  PH(4)
+  PH_END(2)
 }
 
 // ------------------------------------------------------------------------------------
@@ -2883,8 +2900,8 @@ extern "C" {
 
 int dml_forest_phase_stats(unsigned long long* out) {
 #ifdef DML_PHASE_PROF
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 24) != hipSuccess) return 1;
-  unsigned long long z[24] = {0};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 32) != hipSuccess) return 1;
+  unsigned long long z[32] = {0};
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) != hipSuccess) return 1;
   return 0;
 #else

@@ -278,14 +278,13 @@ class ForestFamily(Family):
             Xb = data.binned()
         sharded = getattr(data, "is_row_shard", False)
         if sharded:
-            for t in tasks:   # the row-sharded builder sums histograms; medians need every row
-                if t.params.get("criterion") == forest_ops.MAE:
-                    t.params["criterion"] = forest_ops.MSE
-                    t.params.setdefault("warnings", []).append(
-                        "criterion='absolute_error' under a row shard: grown with squared_error")
-                if t.params.get("monotonic_cst") is not None:
-                    t.params["monotonic_cst"] = None
-                    t.params.setdefault("warnings", []).append("monotonic_cst under a row shard: ignored")
+            # the row-sharded builder sums histograms (medians need every row) and keeps no node
+            # bounds: the cluster runner sends such jobs task-parallel (parallel/runner.py
+            # needs_whole_rows); never grow a different estimator than the one requested
+            for t in tasks:
+                if t.params.get("criterion") == forest_ops.MAE or t.params.get("monotonic_cst") is not None:
+                    raise ParamError("criterion='absolute_error' and monotonic_cst need every row on one rank: "
+                                     "run this job with parallelism='task'")
         # absolute_error trees grow on the host builder (forest_cpu.cpp): batch them apart
         tasks_in = tasks
         tasks = sorted(tasks, key=_host_only)

@@ -606,6 +606,16 @@ def worker_loop(core: WorkerCore, ctl: Optional[Controller] = None, heartbeat: b
             hb.stop()
 
 
+def needs_whole_rows(model_type: str, params: Dict[str, Any]) -> bool:
+    """A candidate the row-sharded builders cannot fit exactly: absolute_error trees need
+    per-node weighted medians over every row, and monotonic_cst's node bounds are not part of
+    the row-sharded forest builder -- such a job runs task-parallel (never a silently
+    different estimator; reference aws-prod/worker/worker.py:45,452 forwards params verbatim)."""
+    if not (model_type.startswith("RandomForest") or model_type.startswith("GradientBoosting")):
+        return False
+    return params.get("criterion") == "absolute_error" or params.get("monotonic_cst") is not None
+
+
 def _binned_only_table(ctl: Controller, plan: Dict[str, Any], X, device) -> bool:
     """Same rule as the local device cache (engine/service.py DeviceCache._binned_only)."""
     if getattr(device, "type", str(device)) != "cuda" or not getattr(family_of(plan["model_type"]), "binned_ok", False):
@@ -815,6 +825,12 @@ class DistributedRunner(Runner):
             if not todo:
                 return
             data_par = self._data_parallel(plan, len(todo), n_rows, n_feat)
+            if data_par:
+                whole = [i for i in todo if needs_whole_rows(plan["model_type"], job.subtasks[i].spec["parameters"])]
+                if whole:   # never a silently different model: such a job runs task-parallel
+                    log.warning("job %s: %d candidate(s) need every row on one rank (absolute_error / "
+                                "monotonic_cst): task-parallel instead of row-sharded", job.job_id, len(whole))
+                    data_par = False
             slices = plan_slices(ctl, plan, todo, int(n_rows * 0.8), n_feat, 2,
                                  min_slices=1 if data_par else min(len(todo), 2 * self._n_alive()))
             costs = candidate_costs(plan, int(n_rows * 0.8), n_feat, 2)

@@ -14,6 +14,7 @@ import socket
 import tempfile
 import time
 
+import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
@@ -305,3 +306,44 @@ def _drive_cv80(ctl, runner):
 def test_cv80_job_through_scores_epoch():
     out = _launch(2, _drive_cv80)
     assert out == [(80, "gloo"), (80, "gloo")], out
+
+
+def _mae_mono_job(parallelism):
+    body = _grid_job("job-mae", "r", "RandomForestRegressor",
+                     {"criterion": ["absolute_error", "squared_error"], "max_depth": [3]},
+                     base={"n_estimators": 4, "random_state": 0, "monotonic_cst": [1, 0, 0, 0, 0, -1]})
+    body["train_params"]["parallelism"] = parallelism
+    return body
+
+
+def _drive_mae_dp(ctl, runner):
+    sid = ctl.create_session()[1]["session_id"]
+    ctl.download_data(sid, {"dataset_url": "regression?n=1500&d=6&seed=21", "dataset_name": "r",
+                            "dataset_type": "synthetic"})
+    st, a = ctl.train(sid, _mae_mono_job("data"))
+    assert st in (200, 202), a
+    ctl.table.wait_finished(a["job_id"], timeout=180)
+    s = ctl.check_status(sid, a["job_id"])[1]
+    return {r["parameters"]["criterion"]: r["cv_scores"] for r in s["job_result"]["results"]}
+
+
+def test_row_shard_request_keeps_absolute_error_and_monotonic_cst():
+    """parallelism='data' on a job whose candidates need every row on one rank (absolute_error
+    medians, monotonic_cst node bounds): the cluster runs it task-parallel and returns the
+    local runner's CV scores -- never a silently different estimator."""
+    dist_scores = _launch(3, _drive_mae_dp)
+    root = tempfile.mkdtemp()
+    ctl = Controller(Config.from_env(data_root=root, device="cpu", chunk_target_s=0.0))
+    try:
+        sid = ctl.create_session()[1]["session_id"]
+        ctl.download_data(sid, {"dataset_url": "regression?n=1500&d=6&seed=21", "dataset_name": "r",
+                                "dataset_type": "synthetic"})
+        st, a = ctl.train(sid, _mae_mono_job("task"))
+        ctl.table.wait_finished(a["job_id"], timeout=180)
+        s = ctl.check_status(sid, a["job_id"])[1]
+        local = {r["parameters"]["criterion"]: r["cv_scores"] for r in s["job_result"]["results"]}
+    finally:
+        ctl.shutdown()
+    assert set(dist_scores) == {"absolute_error", "squared_error"}
+    for k in local:
+        assert np.allclose(dist_scores[k], local[k], rtol=0, atol=1e-12), (k, dist_scores[k], local[k])
