@@ -103,11 +103,15 @@ __device__ unsigned long long g_phase[4][8];
 #define PH_END(t) if (threadIdx.x == 0) { _acc[7] = 1; for (int _i = 0; _i < 8; ++_i) atomicAdd(&g_phase[t][_i], _acc[_i]); \
                                             atomicAdd(&g_phase[3][t], (unsigned long long)on.count); }
 #define PH_CNT(i, v) if (threadIdx.x == 0) atomicAdd(&g_phase[3][i], (unsigned long long)(v));
+#define PH_ARGS_DECL , uint64_t& _pt, uint64_t* _acc
+#define PH_ARGS_PASS , _pt, _acc
 #else
 #define PH_BEGIN
 #define PH(i)
 #define PH_END(t)
 #define PH_CNT(i, v)
+#define PH_ARGS_DECL
+#define PH_ARGS_PASS
 #endif
 
 namespace dml {
@@ -157,6 +161,10 @@ struct ForestArgs {
   // launches fit f's predict right after that level on its own stream, overlapping the
   // deeper fits' remaining levels, and marks the entry -2
   int64_t early_pred, fit_done_level, n_fits;
+  // > 0 (binary classification, no monotonic constraints, row cache on): tier 1 holds the
+  // nodes of sub_max < count <= bigsub_max (= wave_max, <= 256) and k_bigsub grows each
+  // one's whole subtree on chip
+  int64_t bigsub_max;
 };
 
 constexpr int kTiers = 4;  // 0 subtree, 1 wave, 2 block, 3 large
@@ -206,6 +214,7 @@ struct Ctx {
   int64_t large_cap;
   int32_t wave_max, block_max, chunk, kg_wave, kg_block, kg_large, slack_wave;
   int32_t sub_max, sub_cache_d;
+  int32_t bigsub_max;    // > 0: tier 1 (sub_max < count <= bigsub_max) is grown by k_bigsub
   int64_t ystride;
   // row words: rows_cur/rows_next hold row | bootstrap weight << rbits | class << (rbits + 4)
   // when `packed` (the weight and label travel with the row through every partition, so
@@ -1959,6 +1968,159 @@ __device__ __forceinline__ void sub_node_seg(const Ctx& c, const NodeSpec& s, co
   }
 }
 
+// Grows the whole subtree under one node of <= 64 rows with ONE wave (k_subtree; k_bigsub
+// for its small nodes): stack[0] / sstats[0..VC) hold the node on entry.  Lane `lane` holds
+// one row of the node: its class / weight / fixed-point target in registers and its bins
+// at xc[my_lr * dp] (IDENT: my_lr == lane).  alloc() (lane 0) hands out the next reserved
+// child pair, or -1.
+template <bool REG, int FC, bool IDENT, class Alloc>
+__device__ __forceinline__ void subtree_dfs(const Ctx& c, const NodeSpec& s, int lane, int my_lr, int my_cls, float my_w,
+                                            int64_t my_yq, int64_t my_y2q, const uint8_t* xc, int dp, bool cache,
+                                            const uint8_t* xg, int cnt0, SubEntry* stack, double* sstats,
+                                            double* left_ch, double* right_ch, int32_t* cidx, double Wt,
+                                            const double* tcw, Alloc alloc PH_ARGS_DECL) {
+  const int d = c.d;
+  const int VC = c.VC;
+  int sp = 1;
+  while (sp > 0) {
+    --sp;
+    const SubEntry e = stack[sp];
+    const double* pv = sstats + sp * VC;
+    const int cnt = __popcll(e.mask);
+    int nonconst = 0, best_f = -1, best_b = -1;
+    double best_g = -INFINITY, best_mid = 0.0;
+    const FeatPerm fp = feat_perm(e.key, d);
+    if (cache && cnt <= 32 && (FC >= 0 || !c.mono) && DML_SUB_SEG_REG + !REG > 0) {
+      // compact the node's rows: compact row j <- lane of the j-th set bit of the mask
+      const bool in = (e.mask >> lane) & 1ull;
+      if (in) cidx[lane_prefix(e.mask)] = lane;
+      wave_lds_sync();
+      const int jx = cnt <= 8 ? (lane & 7) : (cnt <= 16 ? (lane & 15) : (lane & 31));
+      const int src0 = jx < cnt ? cidx[jx] : 0;
+      const int src = IDENT ? src0 : __shfl(my_lr, src0);   // the source lane's cached row
+      const int cls_j = REG ? 0 : __shfl(my_cls, src0);
+      const uint32_t w_j = (uint32_t)__shfl((int)(uint32_t)my_w, src0);
+      const int64_t yq_j = REG ? (int64_t)wave::bcast_lane<uint64_t>((uint64_t)my_yq, src0) : 0;
+#if defined(DML_X2_SUB) && DML_X2_SUB != 2   // sensitivity build: every segmented evaluation twice (the first into copies)
+      {
+        int nc2 = nonconst, bf2 = best_f, bb2 = best_b;
+        double bg2 = best_g;
+        if (cnt <= 8) sub_node_seg<8, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw, yq_j);
+        else if (cnt <= 16) sub_node_seg<16, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw, yq_j);
+        else sub_node_seg<32, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw, yq_j);
+        if (bg2 == -12345.0 && bf2 == 7 && nc2 == 3) atomicOr(&c.counters[kOpenOvf], bb2);
+      }
+#endif
+      if (cnt <= 8) sub_node_seg<8, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw, yq_j);
+      else if (cnt <= 16) sub_node_seg<16, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw, yq_j);
+      else sub_node_seg<32, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw, yq_j);
+      wave_lds_sync();   // cidx is rewritten by the next node
+      PH(1)
+      PH_CNT(4, 1)
+      PH_CNT(5, cnt)
+    } else
+    for (int pos = 0; nonconst < s.max_features && pos < d; ++pos) {
+      const int f = feature_at(fp, pos, d);
+      const int my_bin = cache ? xc[my_lr * dp + f] : (lane < cnt0 ? xg[f] : 0);
+      double g, mid;
+      int bb;
+      bool nc;
+#if defined(DML_X2_SUB) && DML_X2_SUB != 1   // sensitivity: every one-feature evaluation twice
+      sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_yq, g, bb, nc, tcw,
+                    MonoQ{mono_of<FC>(c, s, f), e.lo, e.hi}, mid);
+      if (g == -12345.0 && bb == 7) atomicOr(&c.counters[kOpenOvf], (int)nc);
+#endif
+      sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_yq, g, bb, nc, tcw,
+                    MonoQ{mono_of<FC>(c, s, f), e.lo, e.hi}, mid);
+      if (nc) {
+        ++nonconst;
+        if (bb >= 0 && g > best_g) { best_g = g; best_f = f; best_b = bb; best_mid = mid; }
+      }
+    }
+    if (!(cache && cnt <= 32 && (FC >= 0 || !c.mono) && DML_SUB_SEG_REG + !REG > 0)) {
+      PH(2)
+      PH_CNT(6, 1)
+      PH_CNT(7, cnt)
+    }
+    if (best_f < 0) continue;
+    const int mybin = cache ? xc[my_lr * dp + best_f] : (lane < cnt0 ? xg[best_f] : 0);
+    const bool in = (e.mask >> lane) & 1ull;
+    const uint64_t lm = __ballot(in && mybin <= best_b) & e.mask;
+    const uint64_t rm = e.mask & ~lm;
+    // left child statistics (class weights / regression sums) by wave reductions
+    if (!REG && c.C == 2) {   // binary: one packed integer sum (a <= 64-row node weighs < 2^16)
+      const bool inl = (lm >> lane) & 1ull;
+      const uint32_t w = (uint32_t)my_w;
+      const uint32_t x = wave::sum<uint32_t>(inl ? (w | (my_cls == 1 ? w << 16 : 0u)) : 0u, lane);
+      const uint32_t l1 = x >> 16, l0 = (x & 0xFFFFu) - l1;
+      if (lane == 0) {
+        const double v0 = (double)l0 * cwk(tcw, 0), v1 = (double)l1 * cwk(tcw, 1);
+        left_ch[0] = v0; right_ch[0] = pv[0] - v0;
+        left_ch[1] = v1; right_ch[1] = pv[1] - v1;
+      }
+    } else
+    for (int k = 0; k < VC; ++k) {
+      double v;
+      const bool inl = (lm >> lane) & 1ull;
+      if constexpr (REG) {   // integer sums (exact in any order), then the double channels
+        const int64_t wi = (int64_t)my_w;
+        uint64_t q = !inl ? 0ull : (uint64_t)(k == 0 ? wi : (k == 1 ? wi * my_yq : wi * my_y2q));
+        q = wave::sum<uint64_t>(q, lane);
+        v = k == 0 ? (double)q : (k == 1 ? reg_s1(q, c.rq) : reg_s2(q, c.rq));
+      } else {
+        v = (inl && my_cls == k) ? (double)my_w : 0.0;
+        v = wave::sum<double>(v, lane);     // integer-valued: exact in any order
+        v *= cwk(tcw, k);
+      }
+      if (lane == 0) { left_ch[k] = v; right_ch[k] = pv[k] - v; }
+    }
+    wave_lds_sync();
+    int base = -1;
+    if (lane == 0 && accept_split_v(c, s, pv, Wt, left_ch)) base = alloc();
+    if (lane == 0 && base >= 0) {
+      NodeRec leaf; leaf.split = -1; leaf.left = -1;
+      c.nodes[base] = leaf;
+      c.nodes[base + 1] = leaf;
+      double* lv = c.node_val + (int64_t)base * VC;
+      for (int q = 0; q < VC; ++q) {
+        lv[q] = left_ch[q];
+        lv[VC + q] = right_ch[q];
+      }
+      NodeRec rec; rec.split = pack_split(best_f, best_b); rec.left = base;
+      c.nodes[e.node] = rec;
+      mono_children<FC>(c, e.node, base, mono_of<FC>(c, s, best_f), best_mid);
+    }
+    base = wave::bcast<int>(base, 0);
+    if (base < 0) continue;
+    const int nl = __popcll(lm), nr = cnt - nl;
+    // push right then left (left subtree first); leaf-by-count/purity children are not pushed.
+    // The popped entry's slot `sp` is reused: compute both children's sums before writing.
+    if (lane == 0) {
+      const int dep = e.depth + 1;
+      const bool push_r = !leaf_by_counts(s, nr, dep) && !leaf_by_weight(s, vals_weight(right_ch, c.C, c.is_reg)) &&
+                          impure_v<FC>(c, s, right_ch);
+      const bool push_l = !leaf_by_counts(s, nl, dep) && !leaf_by_weight(s, vals_weight(left_ch, c.C, c.is_reg)) &&
+                          impure_v<FC>(c, s, left_ch);
+      const int mbest = mono_of<FC>(c, s, best_f);
+      if (push_r) {
+        SubEntry r; r.mask = rm; r.key = child_key(e.key, 1); r.node = base + 1; r.depth = dep;
+        mono_child_bounds(mbest, e.lo, e.hi, best_mid, 1, r.lo, r.hi);
+        for (int q = 0; q < VC; ++q) sstats[sp * VC + q] = right_ch[q];
+        stack[sp++] = r;
+      }
+      if (push_l) {
+        SubEntry l; l.mask = lm; l.key = child_key(e.key, 0); l.node = base; l.depth = dep;
+        mono_child_bounds(mbest, e.lo, e.hi, best_mid, 0, l.lo, l.hi);
+        for (int q = 0; q < VC; ++q) sstats[sp * VC + q] = left_ch[q];
+        stack[sp++] = l;
+      }
+    }
+    sp = wave::bcast<int>(sp, 0);
+    wave_lds_sync();
+    PH(3)
+  }
+}
+
 template <bool REG, int FC>
 __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2045,153 +2207,383 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   const double* tcw = REG ? nullptr : tree_cw<FC>(c, on.tree);
   pool_base = wave::bcast<int>(pool_base, 0);
   if (pool_base < 0) return;
-  int used = 0;
+  int used = 0;   // child pairs handed out (lane 0's copy counts)
   wave_lds_sync();
-  int sp = 1;
   PH(0)
-  while (sp > 0) {
-    --sp;
-    const SubEntry e = stack[sp];
-    const double* pv = sstats + sp * VC;
-    const int cnt = __popcll(e.mask);
-    int nonconst = 0, best_f = -1, best_b = -1;
-    double best_g = -INFINITY, best_mid = 0.0;
-    const FeatPerm fp = feat_perm(e.key, d);
-    if (cache && cnt <= 32 && (FC >= 0 || !c.mono) && DML_SUB_SEG_REG + !REG > 0) {
-      // compact the node's rows: compact row j <- lane of the j-th set bit of the mask
-      const bool in = (e.mask >> lane) & 1ull;
-      if (in) cidx[lane_prefix(e.mask)] = lane;
-      wave_lds_sync();
-      const int jx = cnt <= 8 ? (lane & 7) : (cnt <= 16 ? (lane & 15) : (lane & 31));
-      const int src = jx < cnt ? cidx[jx] : 0;
-      const int cls_j = REG ? 0 : __shfl(my_cls, src);
-      const uint32_t w_j = (uint32_t)__shfl((int)(uint32_t)my_w, src);
-      const int64_t yq_j = REG ? (int64_t)wave::bcast_lane<uint64_t>((uint64_t)my_yq, src) : 0;
-#if defined(DML_X2_SUB) && DML_X2_SUB != 2   // sensitivity build: every segmented evaluation twice (the first into copies)
-      {
-        int nc2 = nonconst, bf2 = best_f, bb2 = best_b;
-        double bg2 = best_g;
-        if (cnt <= 8) sub_node_seg<8, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw, yq_j);
-        else if (cnt <= 16) sub_node_seg<16, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw, yq_j);
-        else sub_node_seg<32, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nc2, bg2, bf2, bb2, tcw, yq_j);
-        if (bg2 == -12345.0 && bf2 == 7 && nc2 == 3) atomicOr(&c.counters[kOpenOvf], bb2);
-      }
-#endif
-      if (cnt <= 8) sub_node_seg<8, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw, yq_j);
-      else if (cnt <= 16) sub_node_seg<16, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw, yq_j);
-      else sub_node_seg<32, REG>(c, s, fp, cnt, lane, src, cls_j, w_j, xc, dp, nonconst, best_g, best_f, best_b, tcw, yq_j);
-      wave_lds_sync();   // cidx is rewritten by the next node
-      PH(1)
-      PH_CNT(4, 1)
-      PH_CNT(5, cnt)
-    } else
-    for (int pos = 0; nonconst < s.max_features && pos < d; ++pos) {
-      const int f = feature_at(fp, pos, d);
-      const int my_bin = cache ? xc[lane * dp + f] : (lane < cnt0 ? xg[f] : 0);
-      double g, mid;
-      int bb;
-      bool nc;
-#if defined(DML_X2_SUB) && DML_X2_SUB != 1   // sensitivity: every one-feature evaluation twice
-      sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_yq, g, bb, nc, tcw,
-                    MonoQ{mono_of<FC>(c, s, f), e.lo, e.hi}, mid);
-      if (g == -12345.0 && bb == 7) atomicOr(&c.counters[kOpenOvf], (int)nc);
-#endif
-      sub_eval<REG>(c, s, e.mask, cnt, lane, my_bin, my_cls, my_w, my_yq, g, bb, nc, tcw,
-                    MonoQ{mono_of<FC>(c, s, f), e.lo, e.hi}, mid);
-      if (nc) {
-        ++nonconst;
-        if (bb >= 0 && g > best_g) { best_g = g; best_f = f; best_b = bb; best_mid = mid; }
-      }
-    }
-    if (!(cache && cnt <= 32 && (FC >= 0 || !c.mono) && DML_SUB_SEG_REG + !REG > 0)) {
-      PH(2)
-      PH_CNT(6, 1)
-      PH_CNT(7, cnt)
-    }
-    if (best_f < 0) continue;
-    const int mybin = cache ? xc[lane * dp + best_f] : (lane < cnt0 ? xg[best_f] : 0);
-    const bool in = (e.mask >> lane) & 1ull;
-    const uint64_t lm = __ballot(in && mybin <= best_b) & e.mask;
-    const uint64_t rm = e.mask & ~lm;
-    // left child statistics (class weights / regression sums) by wave reductions
-    if (!REG && c.C == 2) {   // binary: one packed integer sum (a <= 64-row node weighs < 2^16)
-      const bool inl = (lm >> lane) & 1ull;
-      const uint32_t w = (uint32_t)my_w;
-      const uint32_t x = wave::sum<uint32_t>(inl ? (w | (my_cls == 1 ? w << 16 : 0u)) : 0u, lane);
-      const uint32_t l1 = x >> 16, l0 = (x & 0xFFFFu) - l1;
-      if (lane == 0) {
-        const double v0 = (double)l0 * cwk(tcw, 0), v1 = (double)l1 * cwk(tcw, 1);
-        left_ch[0] = v0; right_ch[0] = pv[0] - v0;
-        left_ch[1] = v1; right_ch[1] = pv[1] - v1;
-      }
-    } else
-    for (int k = 0; k < VC; ++k) {
-      double v;
-      const bool inl = (lm >> lane) & 1ull;
-      if constexpr (REG) {   // integer sums (exact in any order), then the double channels
-        const int64_t wi = (int64_t)my_w;
-        uint64_t q = !inl ? 0ull : (uint64_t)(k == 0 ? wi : (k == 1 ? wi * my_yq : wi * my_y2q));
-        q = wave::sum<uint64_t>(q, lane);
-        v = k == 0 ? (double)q : (k == 1 ? reg_s1(q, c.rq) : reg_s2(q, c.rq));
-      } else {
-        v = (inl && my_cls == k) ? (double)my_w : 0.0;
-        v = wave::sum<double>(v, lane);     // integer-valued: exact in any order
-        v *= cwk(tcw, k);
-      }
-      if (lane == 0) { left_ch[k] = v; right_ch[k] = pv[k] - v; }
-    }
-    wave_lds_sync();
-    int base = -1;
-    if (lane == 0 && accept_split_v(c, s, pv, Wt, left_ch) && used < max_splits) {
-      base = pool_base + 2 * used;
-      NodeRec leaf; leaf.split = -1; leaf.left = -1;
-      c.nodes[base] = leaf;
-      c.nodes[base + 1] = leaf;
-      double* lv = c.node_val + (int64_t)base * VC;
-      for (int q = 0; q < VC; ++q) {
-        lv[q] = left_ch[q];
-        lv[VC + q] = right_ch[q];
-      }
-      NodeRec rec; rec.split = pack_split(best_f, best_b); rec.left = base;
-      c.nodes[e.node] = rec;
-      mono_children<FC>(c, e.node, base, mono_of<FC>(c, s, best_f), best_mid);
-    }
-    base = wave::bcast<int>(base, 0);
-    if (base < 0) continue;
-    ++used;
-    const int nl = __popcll(lm), nr = cnt - nl;
-    // push right then left (left subtree first); leaf-by-count/purity children are not pushed.
-    // The popped entry's slot `sp` is reused: compute both children's sums before writing.
-    if (lane == 0) {
-      const int dep = e.depth + 1;
-      const bool push_r = !leaf_by_counts(s, nr, dep) && !leaf_by_weight(s, vals_weight(right_ch, c.C, c.is_reg)) &&
-                          impure_v<FC>(c, s, right_ch);
-      const bool push_l = !leaf_by_counts(s, nl, dep) && !leaf_by_weight(s, vals_weight(left_ch, c.C, c.is_reg)) &&
-                          impure_v<FC>(c, s, left_ch);
-      const int mbest = mono_of<FC>(c, s, best_f);
-      if (push_r) {
-        SubEntry r; r.mask = rm; r.key = child_key(e.key, 1); r.node = base + 1; r.depth = dep;
-        mono_child_bounds(mbest, e.lo, e.hi, best_mid, 1, r.lo, r.hi);
-        for (int q = 0; q < VC; ++q) sstats[sp * VC + q] = right_ch[q];
-        stack[sp++] = r;
-      }
-      if (push_l) {
-        SubEntry l; l.mask = lm; l.key = child_key(e.key, 0); l.node = base; l.depth = dep;
-        mono_child_bounds(mbest, e.lo, e.hi, best_mid, 0, l.lo, l.hi);
-        for (int q = 0; q < VC; ++q) sstats[sp * VC + q] = left_ch[q];
-        stack[sp++] = l;
-      }
-    }
-    sp = wave::bcast<int>(sp, 0);
-    wave_lds_sync();
-    PH(3)
-  }
+  subtree_dfs<REG, FC, true>(c, s, lane, lane, my_cls, my_w, my_yq, my_y2q, xc, dp, cache, xg, cnt0, stack, sstats,
+                             left_ch, right_ch, cidx, Wt, tcw,
+                             [&]() { return used < max_splits ? pool_base + 2 * used++ : -1; } PH_ARGS_PASS);
+  used = wave::bcast<int>(used, 0);
   // reserved-but-unused node pairs become well-formed (unreferenced) leaves, so any
   // pass over the whole pool sees valid records
   const NodeRec leaf{-1, -1};
   for (int i = 2 * used + lane; i < 2 * max_splits; i += 64) c.nodes[pool_base + i] = leaf;
   PH(4)
   PH_END(2)
+}
+
+// ------------------------------------------------------------------------------------
+// big-subtree tier (binary classification): ONE 256-thread workgroup grows the WHOLE
+// subtree under a node of <= bigsub_max (<= 256) rows
+// ------------------------------------------------------------------------------------
+// The node's rows are read from HBM / the Infinity Cache ONCE: their row words, then each
+// row's bin line into an LDS row cache.  (The wave tier gathers every row's line again at
+// each of the two or three levels above the subtree tier, and each of those nodes is a
+// chain of dependent global round trips -- open node, row words, row lines -- issued while
+// the level's block tier keeps the memory system saturated: the phase profile puts 41 % of
+// a wave-tier node's cycles and 41 % of a subtree root's in those loads.)  Below the root
+// every node lives on chip: a node is a range [start, start + cnt) of the workgroup's local
+// row permutation `lp`, and the four waves are independent workers taking nodes from a
+// locked LDS stack:
+//   * cnt > 64:  the wave builds LDS histograms of DML_BIG_KG features at a time from the
+//                cached bins (4 rows per lane), evaluates them with eval_feature -- the wave
+//                and block tiers' routine: same candidates, same fp64 scores -- selects in
+//                visiting order exactly as k_nodes does, partitions its range stably and
+//                pushes the children;
+//   * cnt <= 64: the wave grows the node's whole subtree with subtree_dfs (k_subtree's
+//                sort-based / segmented evaluation), lanes mapped to the range's rows.
+// Child pairs come from the subtree's reserved pool range (k_compact, or one pool atomic).
+#ifndef DML_BIG_KG
+#define DML_BIG_KG 2   // features per histogram group of a big node (2 KB of LDS each)
+#endif
+#ifndef DML_BIG_STACK
+#define DML_BIG_STACK 128   // live entries: disjoint nodes of >= 2 rows of <= 256
+#endif
+
+struct BigEntry {
+  uint64_t key;
+  int32_t node, depth;
+  int32_t start, cnt;
+  double v0, v1;   // class-weight sums of the node (binary)
+};
+
+struct BigShared {
+  int32_t lock, top, pending, used, pool_base, max_splits, overflow, pad;
+};
+
+// per-wave scratch: a big node's histograms + evaluation slots, or a small node's DFS state
+struct BigWave {
+  size_t hist, rg, rb, rn, rleft, cur, dfs_stack, dfs_stats, dfs_lr, dfs_cidx, total;
+};
+
+__host__ __device__ inline BigWave big_wave_layout() {
+  BigWave L;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off = (off + bytes + 15) / 16 * 16; return o; };
+  // big-node view
+  L.hist = take((size_t)DML_BIG_KG * 256 * 8);
+  L.rg = take((size_t)DML_BIG_KG * 8);
+  L.rb = take((size_t)DML_BIG_KG * 4);
+  L.rn = take((size_t)DML_BIG_KG * 4);
+  L.rleft = take((size_t)DML_BIG_KG * 3 * 8);
+  L.cur = take(sizeof(BigEntry));
+  const size_t big_end = off;
+  // small-node (DFS) view, aliased onto the same bytes
+  off = 0;
+  L.dfs_stack = take(64 * sizeof(SubEntry));
+  L.dfs_stats = take(64 * 2 * 8);
+  L.dfs_lr = take(2 * 2 * 8);            // left_ch, right_ch
+  L.dfs_cidx = take(64 * 4);
+  L.total = off > big_end ? off : big_end;
+  return L;
+}
+
+struct BigLayout {
+  size_t sh, stk, rcls, rw, lp, tmp, waves, xc, total;
+};
+
+__host__ __device__ inline BigLayout big_layout(int rmax, int dp) {
+  BigLayout L;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off = (off + bytes + 15) / 16 * 16; return o; };
+  L.sh = take(sizeof(BigShared));
+  L.stk = take((size_t)DML_BIG_STACK * sizeof(BigEntry));
+  L.rcls = take(256);
+  L.rw = take(256);
+  L.lp = take(256);
+  L.tmp = take(256);
+  L.waves = take(4 * big_wave_layout().total);
+  L.xc = take((size_t)rmax * dp);
+  L.total = off;
+  return L;
+}
+
+__device__ __forceinline__ void big_lock(BigShared* sh) {
+  while (atomicCAS(&sh->lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void big_unlock(BigShared* sh) {
+  __threadfence_block();
+  atomicExch(&sh->lock, 0);
+}
+
+template <int FC>
+__global__ __launch_bounds__(256) void k_bigsub(Ctx c, int set_cur) {
+  constexpr bool PK = FC >= 0;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const OpenNode on = c.open[set_cur][1][blockIdx.x];
+  const NodeSpec s = spec_of<FC>(c, on.tree);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int d = c.d, dp = c.sub_cache_d;
+  const BigLayout L = big_layout(c.bigsub_max, dp);
+  const BigWave W = big_wave_layout();
+  BigShared* sh = (BigShared*)(smem + L.sh);
+  BigEntry* stk = (BigEntry*)(smem + L.stk);
+  uint8_t* rcls = smem + L.rcls;
+  uint8_t* rw = smem + L.rw;
+  uint8_t* lp = smem + L.lp;
+  uint8_t* tmp = smem + L.tmp;
+  uint8_t* xc = smem + L.xc;
+  unsigned char* wv = smem + L.waves + (size_t)wid * W.total;
+  const int cnt0 = on.count;
+  // ---- the node's rows, once: row word (weight, class) and the row's bin line
+  if (tid < cnt0) {
+    const uint32_t wd = c.rows_cur[on.start + tid];
+    const uint32_t row = word_row(c, wd);
+    rw[tid] = (uint8_t)word_weight<PK>(c, s, wd);
+    rcls[tid] = (uint8_t)word_cls<PK>(c, wd);
+    lp[tid] = (uint8_t)tid;
+    const uint8_t* xg = c.Xb + (int64_t)row * c.ld;
+    uint32_t* dst = (uint32_t*)(xc + tid * dp);
+    const int nw = dp >> 2;
+    if ((c.ld & 15) == 0 && c.ld >= ((d + 15) & ~15)) {
+      const uint4* src = (const uint4*)xg;
+      const int nseg = (d + 15) >> 4;
+      for (int q0 = 0; q0 < nseg; q0 += 8) {   // 8 loads in flight before the first store
+        uint4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = q0 + i < nseg ? src[q0 + i] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int w0 = 4 * (q0 + i);
+          if (w0 + 0 < nw) dst[w0 + 0] = v[i].x;
+          if (w0 + 1 < nw) dst[w0 + 1] = v[i].y;
+          if (w0 + 2 < nw) dst[w0 + 2] = v[i].z;
+          if (w0 + 3 < nw) dst[w0 + 3] = v[i].w;
+        }
+      }
+    } else {
+      for (int j = 0; j < d; ++j) xc[tid * dp + j] = xg[j];
+    }
+  }
+  if (tid == 0) {
+    // every pair the subtree can need, reserved at once (k_compact for staged nodes)
+    int pool_base = on.pool_base;
+    const int max_splits = subtree_max_splits(s, cnt0, on.depth);
+    const int want = 2 * max_splits;
+    if (pool_base == -1) {
+      pool_base = want > 0 ? atomicAdd(&c.counters[kPool], want) : 0;
+      if (want > 0 && (int64_t)pool_base + want > c.pool_cap) {
+        atomicOr(&c.counters[kOverflow], 1);
+        pool_base = -1;
+      }
+    } else if (pool_base < 0) {
+      pool_base = -1;   // k_compact flagged the overflow
+    }
+    sh->lock = 0; sh->used = 0; sh->pool_base = pool_base; sh->max_splits = max_splits; sh->overflow = 0;
+    BigEntry e;
+    e.key = on.key; e.node = on.node; e.depth = on.depth; e.start = 0; e.cnt = cnt0;
+    e.v0 = c.node_val[(int64_t)on.node * 2]; e.v1 = c.node_val[(int64_t)on.node * 2 + 1];
+    stk[0] = e;
+    sh->top = 1;
+    sh->pending = 1;
+  }
+  __syncthreads();
+  const int pool_base = sh->pool_base, max_splits = sh->max_splits;
+  if (pool_base < 0) return;
+  const double Wt = c.tree_W[on.tree];
+  const double* tcw = tree_cw<FC>(c, on.tree);
+  auto alloc = [&]() -> int {   // lane 0: next reserved child pair
+    const int u = atomicAdd(&sh->used, 1);
+    return u < max_splits ? pool_base + 2 * u : -1;
+  };
+  BigEntry* cur = (BigEntry*)(wv + W.cur);
+  const int k = s.max_features;
+  // ---- worker loop: take a node, grow it (big) or its whole subtree (small), push children
+  for (int spins = 0;;) {
+    int got = 0;
+    if (lane == 0) {
+      big_lock(sh);
+      if (sh->top > 0) {
+        *cur = stk[--sh->top];
+        got = 1;
+      }
+      big_unlock(sh);
+    }
+    got = __builtin_amdgcn_readfirstlane(got);
+    if (!got) {
+      const int pend = __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(&sh->pending, 0) : 0);
+      if (pend == 0) break;
+      if (++spins > (1 << 24)) {   // never expected: bounded so a bug cannot hang the GPU
+        if (lane == 0) atomicOr(&c.counters[kOverflow], 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    wave_lds_sync();
+    const BigEntry e = *cur;
+    const int cnt = e.cnt, start = e.start;
+    if (cnt <= 64) {
+      // ---- small node: the whole subtree below it, one wave (k_subtree's DFS)
+      SubEntry* dstack = (SubEntry*)(wv + W.dfs_stack);
+      double* dstats = (double*)(wv + W.dfs_stats);
+      double* left_ch = (double*)(wv + W.dfs_lr);
+      double* right_ch = left_ch + 2;
+      int32_t* cidx = (int32_t*)(wv + W.dfs_cidx);
+      const int my_lr = lane < cnt ? (int)lp[start + lane] : 0;
+      const int my_cls = lane < cnt ? (int)rcls[my_lr] : 0;
+      const float my_w = lane < cnt ? (float)rw[my_lr] : 0.f;
+      wave_lds_sync();   // `cur` aliases the DFS stack
+      if (lane == 0) {
+        SubEntry r;
+        r.mask = cnt >= 64 ? ~0ull : ((1ull << cnt) - 1ull);
+        r.key = e.key; r.node = e.node; r.depth = e.depth; r.lo = -INFINITY; r.hi = INFINITY;
+        dstack[0] = r;
+        dstats[0] = e.v0; dstats[1] = e.v1;
+      }
+      wave_lds_sync();
+#ifdef DML_PHASE_PROF
+      uint64_t _pt = clock64(); uint64_t _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+      subtree_dfs<false, FC, false>(c, s, lane, my_lr, my_cls, my_w, 0, 0, xc, dp, true, nullptr, cnt, dstack, dstats,
+                                    left_ch, right_ch, cidx, Wt, tcw, alloc PH_ARGS_PASS);
+      if (lane == 0) atomicAdd(&sh->pending, -1);
+      continue;
+    }
+    // ---- big node (65..256 rows): histograms from the cached bins, 4 rows per lane
+    unsigned long long* hist = (unsigned long long*)(wv + W.hist);
+    double* rg = (double*)(wv + W.rg);
+    int* rb = (int*)(wv + W.rb);
+    int* rn = (int*)(wv + W.rn);
+    double* rleft = (double*)(wv + W.rleft);
+    int lr[4];
+    uint64_t pl[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = lane + 64 * u;
+      lr[u] = p < cnt ? (int)lp[start + p] : -1;
+      pl[u] = lr[u] >= 0 ? pack_bin((int)rcls[lr[u]], (uint32_t)rw[lr[u]]) : 0ull;
+    }
+    for (int i = lane; i < DML_BIG_KG * 256; i += 64) hist[i] = 0ull;
+    wave_lds_sync();
+    const FeatPerm fp = feat_perm(e.key, d);
+    int pos = 0, nonconst = 0, best_feat = -1, best_bin = -1;
+    double best_gain = -INFINITY, bl0 = 0.0, bl1 = 0.0;
+    while (nonconst < k && pos < d) {
+      const int g = min(DML_BIG_KG, min(k - nonconst, d - pos));
+      int fj[DML_BIG_KG];
+#pragma unroll
+      for (int j = 0; j < DML_BIG_KG; ++j) fj[j] = __builtin_amdgcn_readfirstlane(j < g ? feature_at(fp, pos + j, d) : 0);
+#pragma unroll
+      for (int j = 0; j < DML_BIG_KG; ++j) {
+        if (j >= g) continue;
+        uint32_t b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[u] = lr[u] >= 0 ? (uint32_t)xc[lr[u] * dp + fj[j]] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (lr[u] >= 0) atomicAdd(&hist[j * 256 + b[u]], (unsigned long long)pl[u]);
+      }
+      wave_lds_sync();
+      for (int j = 0; j < g; ++j)
+        eval_feature<1>(hist + j * 256, 2, 3, s, lane, rg + j, rb + j, rn + j, rleft + j * 3, true, tcw, nullptr,
+                        MonoQ{0, 0.0, 0.0}, nullptr);
+      wave_lds_sync();
+      // select in visiting order (k_nodes' wave-parallel form of select_group)
+      const bool isnc = lane < g && rn[lane] != 0;
+      const uint64_t m = __ballot(isnc);
+      const bool considered = isnc && nonconst + lane_prefix(m) + 1 <= k;
+      const bool has = considered && rb[lane] >= 0;
+      double gj = has ? rg[lane] : -INFINITY;
+      int jj = has ? lane : 64;
+      wave::argmax(gj, jj, lane);
+      if (jj < 64 && gj > best_gain) {
+        best_gain = gj;
+        best_feat = fj[0];
+#pragma unroll
+        for (int j = 1; j < DML_BIG_KG; ++j) if (jj == j) best_feat = fj[j];
+        best_bin = rb[jj];
+        bl0 = rleft[jj * 3]; bl1 = rleft[jj * 3 + 1];
+      }
+      nonconst = min(nonconst + __popcll(m), k);
+      pos += g;
+    }
+    // ---- decision (lane 0) on the node's sums; child pair from the reserved range
+    int base = -1;
+    const double best_left[3] = {bl0, bl1, 0.0};
+    const double pv[2] = {e.v0, e.v1};
+    if (lane == 0 && best_feat >= 0 && accept_split_v(c, s, pv, Wt, best_left)) base = alloc();
+    if (lane == 0 && base >= 0) {
+      NodeRec leaf; leaf.split = -1; leaf.left = -1;
+      c.nodes[base] = leaf;
+      c.nodes[base + 1] = leaf;
+      double* lv = c.node_val + (int64_t)base * 2;
+      lv[0] = bl0; lv[1] = bl1; lv[2] = e.v0 - bl0; lv[3] = e.v1 - bl1;
+      NodeRec rec; rec.split = pack_split(best_feat, best_bin); rec.left = base;
+      c.nodes[e.node] = rec;
+    }
+    base = __builtin_amdgcn_readfirstlane(base);
+    int npush = 0;
+    if (base >= 0) {
+      // ---- stable partition of the node's range (left rows keep their order, then right)
+      uint64_t ml[4], mr[4];
+      int nlw = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool left = lr[u] >= 0 && (int)xc[lr[u] * dp + best_feat] <= best_bin;
+        ml[u] = __ballot(left);
+        mr[u] = __ballot(lr[u] >= 0 && !left);
+        nlw += __popcll(ml[u]);
+      }
+      int offL = 0, offR = nlw;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (lr[u] >= 0) {
+          const bool left = (ml[u] >> lane) & 1ull;
+          tmp[start + (left ? offL + lane_prefix(ml[u]) : offR + lane_prefix(mr[u]))] = (uint8_t)lr[u];
+        }
+        offL += __popcll(ml[u]);
+        offR += __popcll(mr[u]);
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (lr[u] >= 0) lp[start + lane + 64 * u] = tmp[start + lane + 64 * u];
+      wave_lds_sync();
+      if (lane == 0) {
+        const double rv0 = e.v0 - bl0, rv1 = e.v1 - bl1;
+        BigEntry ch[2];
+        ch[0].key = child_key(e.key, 0); ch[0].node = base; ch[0].depth = e.depth + 1;
+        ch[0].start = start; ch[0].cnt = nlw; ch[0].v0 = bl0; ch[0].v1 = bl1;
+        ch[1].key = child_key(e.key, 1); ch[1].node = base + 1; ch[1].depth = e.depth + 1;
+        ch[1].start = start + nlw; ch[1].cnt = cnt - nlw; ch[1].v0 = rv0; ch[1].v1 = rv1;
+        bool push[2];
+        for (int side = 0; side < 2; ++side) {
+          const double vals[2] = {ch[side].v0, ch[side].v1};
+          push[side] = !leaf_by_counts(s, ch[side].cnt, ch[side].depth) && !leaf_by_weight(s, vals[0] + vals[1]) &&
+                       impure_v<FC>(c, s, vals);
+        }
+        npush = (int)push[0] + (int)push[1];
+        if (npush) {
+          big_lock(sh);
+          // right first: the left child is taken next (depth-first, like the other tiers)
+          for (int side = 1; side >= 0; --side) {
+            if (!push[side]) continue;
+            if (sh->top < DML_BIG_STACK) stk[sh->top++] = ch[side];
+            else { sh->overflow = 1; atomicOr(&c.counters[kOverflow], 1); --npush; }
+          }
+          atomicAdd(&sh->pending, npush);
+          big_unlock(sh);
+        }
+      }
+    }
+    if (lane == 0) atomicAdd(&sh->pending, -1);
+  }
+  __syncthreads();
+  // reserved-but-unused node pairs become well-formed (unreferenced) leaves
+  const int used = min(sh->used, max_splits);
+  const NodeRec leaf{-1, -1};
+  for (int i = 2 * used + tid; i < 2 * max_splits; i += 256) c.nodes[pool_base + i] = leaf;
 }
 
 // ------------------------------------------------------------------------------------
@@ -2610,7 +3002,7 @@ __global__ __launch_bounds__(256) void k_compact(Ctx c, int set, int64_t n) {
     const int t = e[u].tier;
     if (t < 0) continue;
     ++cnt[t];
-    if (t == 0) {
+    if (t == 0 || (t == 1 && c.bigsub_max > 0)) {   // whole-subtree tiers: every pair reserved here
       want[u] = 2 * subtree_max_splits(c.specs[e[u].tree], e[u].count, e[u].depth);
       cnt[kTiers] += want[u];
     }
@@ -2644,7 +3036,7 @@ __global__ __launch_bounds__(256) void k_compact(Ctx c, int set, int64_t n) {
 #pragma unroll
     for (int q = 0; q < kTiers; ++q)
       if (q == t) idx = off[q]++;
-    if (t == 0) {
+    if (t == 0 || (t == 1 && c.bigsub_max > 0)) {
       const int pb = off[kTiers];
       off[kTiers] += want[u];
       if (want[u] > 0 && (int64_t)pb + want[u] > c.pool_cap) {
@@ -2801,6 +3193,7 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.slack_wave = (int)a->slack_wave;
   c.sub_max = (int)a->sub_max;
   c.sub_cache_d = (int)a->sub_cache_d;
+  c.bigsub_max = 0;   // set by build_impl for the builds it applies to
   {
     int cbits = 0;
     if (!c.is_reg)
@@ -2956,6 +3349,12 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   if ((size_t)a->workspace_bytes < (size_t)dml_forest_workspace_bytes(a)) return 2;
   Ctx c = make_ctx(a, L);
   const bool fast = a->fast_crit == FCX + 1 && c.packed;   // PK kernels assume packed row words
+  // big-subtree tier (binary): the caller sized tier 1 for it (wave_max <= bigsub_max <= 256)
+  const bool big = MODE == 1 && a->bigsub_max > 0;
+  if (big && (a->bigsub_max > 256 || a->wave_max > a->bigsub_max || a->sub_cache_d <= 0 || a->mono || a->n_classes != 2))
+    return 12;
+  if (big) c.bigsub_max = (int)a->bigsub_max;
+  const size_t lds_big = big ? big_layout((int)a->bigsub_max, (int)a->sub_cache_d).total + 16 : 0;
   uint32_t* rows_a = (uint32_t*)(((unsigned char*)a->workspace) + L.total);
   c.rows_cur = rows_a;
   int32_t* h = pinned_counters();
@@ -2984,10 +3383,10 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   const size_t lds_sl = (size_t)a->kg_large * ghist_feat_bytes(MODE, CH) + a->kg_large * 16 + 16 +
                         (size_t)a->kg_large * CH * 8 + (size_t)a->kg_large * 8 + 64;
   const size_t lds_max = 160 * 1024;
-  if (lds_w > lds_max || lds_b > lds_max || lds_sl > lds_max || lds_s > lds_max) return 7;
+  if (lds_w > lds_max || lds_b > lds_max || lds_sl > lds_max || lds_s > lds_max || lds_big > lds_max) return 7;
   if (a->sub_max > 64) return 9;
   {
-    const int need = (int)std::max(std::max(lds_s, lds_w), std::max(lds_b, lds_sl));
+    const int need = (int)std::max(std::max(std::max(lds_s, lds_w), std::max(lds_b, lds_sl)), lds_big);
     static int attr_set[3] = {0, 0, 0};
     if (need > 64 * 1024 && need > attr_set[MODE]) {
       HIP_OK(hipFuncSetAttribute((const void*)k_subtree<REG, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
@@ -2999,6 +3398,10 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       HIP_OK(hipFuncSetAttribute((const void*)k_hist_large<MODE, false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_hist_large<MODE, true>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_split_large<GM>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      if constexpr (MODE == 1) {
+        HIP_OK(hipFuncSetAttribute((const void*)k_bigsub<FCX>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+        HIP_OK(hipFuncSetAttribute((const void*)k_bigsub<-1>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      }
       attr_set[MODE] = need;
     }
   }
@@ -3016,8 +3419,9 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     const int64_t open_now = (int64_t)ns + nw + nb + nL;
     peak_open = std::max(peak_open, open_now);
     HIP_OK(hipMemsetAsync(c.counters + (1 - cur) * kTiers, 0, kTiers * 4, st));
-    // reserve the child pairs of every wave/block-tier node of this level up front
-    const int64_t pair_w = h[kPool], pair_b = pair_w + 2LL * nw, pool_next = pair_b + 2LL * nb;
+    // reserve the child pairs of every wave/block-tier node of this level up front (a
+    // big-subtree node's pairs were reserved with its subtree's: k_compact / k_bigsub)
+    const int64_t pair_w = h[kPool], pair_b = pair_w + (big ? 0 : 2LL * nw), pool_next = pair_b + 2LL * nb;
     if (pool_next > a->pool_cap) {
       // pool overflow: the caller regrows with a bigger pool -- first make the stream wait for
       // any early predict still reading this pool / writing its outputs (their buffers are
@@ -3029,7 +3433,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       a->status_out = 1;
       return 0;
     }
-    if (nw + nb) {
+    if ((big ? 0 : nw) + nb) {
       *h_pool = (int32_t)pool_next;
       HIP_OK(hipMemcpyAsync(c.counters + kPool, h_pool, 4, hipMemcpyHostToDevice, st));
     }
@@ -3043,14 +3447,30 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       for (int i = 0; i < 3; ++i) HIP_OK(hipStreamWaitEvent(ss->s[i], ss->fork, 0));
       s0 = ss->s[0]; s1 = ss->s[1]; s2 = ss->s[2];
     }
+    // block-tier children stage after the wave tier's (none under the big-subtree tier)
+    const int stage_b = big ? 0 : nw;
     if (fast) {
       if (ns) k_subtree<REG, FCX><<<ns, 64, lds_s, s0>>>(c, cur);
-      if (nw) k_nodes<64, MODE, FCX><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w, 0);
-      if (nb) k_nodes<DML_BLOCK_NT, MODE, FCX><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, nw);
+      if (nw) {
+        if constexpr (MODE == 1) {
+          if (big) k_bigsub<FCX><<<nw, 256, lds_big, s1>>>(c, cur);
+          else k_nodes<64, MODE, FCX><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w, 0);
+        } else {
+          k_nodes<64, MODE, FCX><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w, 0);
+        }
+      }
+      if (nb) k_nodes<DML_BLOCK_NT, MODE, FCX><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
     } else {
       if (ns) k_subtree<REG, -1><<<ns, 64, lds_s, s0>>>(c, cur);
-      if (nw) k_nodes<64, MODE, -1><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w, 0);
-      if (nb) k_nodes<DML_BLOCK_NT, MODE, -1><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, nw);
+      if (nw) {
+        if constexpr (MODE == 1) {
+          if (big) k_bigsub<-1><<<nw, 256, lds_big, s1>>>(c, cur);
+          else k_nodes<64, MODE, -1><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w, 0);
+        } else {
+          k_nodes<64, MODE, -1><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w, 0);
+        }
+      }
+      if (nb) k_nodes<DML_BLOCK_NT, MODE, -1><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
     }
     if (nL) {
       k_large_prep<<<nL, 64, 0, st>>>(c, cur, nL);
@@ -3075,8 +3495,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
         HIP_OK(hipStreamWaitEvent(st, ss->join[i], 0));
       }
     }
-    if (nw + nb) {   // the staged children of the wave/block tiers -> next level's open lists
-      const int64_t nst = 2LL * (nw + nb);
+    if ((big ? 0 : nw) + nb) {   // the staged children of the wave/block tiers -> next level's open lists
+      const int64_t nst = 2LL * ((big ? 0 : nw) + nb);
       k_compact<<<(unsigned)((nst + 1023) / 1024), 256, 0, st>>>(c, 1 - cur, nst);
     }
     HIP_OK(hipGetLastError());

@@ -43,6 +43,12 @@ class ForestTiers:
     kg_block: int = 16
     kg_large: int = 16
     slack_wave: int = 0
+    # binary classification, > 0: nodes of sub_max < count <= bigsub_max grow their WHOLE
+    # subtree in one 4-wave workgroup from an LDS row cache (forest.hip k_bigsub) and tier 1
+    # is capped at it.  Off by default: 1.605 vs 1.050 s on the sweep build (the 25.6 KB row
+    # cache allows 3 workgroups per CU, each mostly one busy wave; nodes of 257..512 rows move
+    # to the block tier) -- profiles/r4_bigsub.md
+    bigsub_max: int = 0
 
     def fitted(self, n_channels: int) -> "ForestTiers":
         """Clamp feature-group sizes to the LDS budget for this channel count."""
@@ -200,7 +206,16 @@ def workspace_bytes(rows_total: int, T: int, d: int, n_classes: int, is_reg: boo
     a.rows_total = int(rows_total)
     a.wave_max, a.block_max, a.chunk = t.wave_max, t.block_max, t.chunk
     a.kg_wave, a.kg_block, a.kg_large, a.slack_wave, a.sub_max = t.kg_wave, t.kg_block, t.kg_large, t.slack_wave, t.sub_max
+    if _bigsub_on(t, is_reg, n_classes, d, None):   # the smaller tier 1 has more block-tier nodes
+        a.wave_max = min(t.wave_max, t.bigsub_max)
     return int(native.hip_lib().dml_forest_workspace_bytes(ctypes.byref(a)))
+
+
+def _bigsub_on(t: "ForestTiers", is_reg: bool, n_classes: int, d: int, mono) -> bool:
+    """The big-subtree tier applies: binary classification, no monotonic constraints, the
+    subtree row cache on (forest.hip k_bigsub; DML_BIGSUB=0 turns it off)."""
+    return (t.bigsub_max > t.sub_max and not is_reg and n_classes == 2 and mono is None
+            and d <= t.sub_cache_max_d and os.environ.get("DML_BIGSUB", "1") != "0")
 
 
 def pool_bytes(pool_cap: int, VC: int) -> int:
@@ -308,6 +323,10 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     a.kg_wave, a.kg_block, a.kg_large, a.slack_wave = tiers.kg_wave, tiers.kg_block, tiers.kg_large, tiers.slack_wave
     a.sub_max = tiers.sub_max
     a.sub_cache_d = _sub_cache_stride(d) if d <= tiers.sub_cache_max_d else 0
+    big = _bigsub_on(tiers, is_reg, n_classes, d, mono_dev) and a.sub_cache_d > 0
+    a.bigsub_max = min(tiers.bigsub_max, 256) if big else 0
+    if big:
+        a.wave_max = min(tiers.wave_max, a.bigsub_max)
     tree_W = torch.empty(T, dtype=torch.float64, device=dev)
     a.tree_W = native.ptr(tree_W)
     ws_bytes = lib.dml_forest_workspace_bytes(ctypes.byref(a))

@@ -59,6 +59,9 @@ TIERS = [
     dict(sub_max=64, wave_max=256, block_max=2048, chunk=1024),
     dict(sub_max=32, wave_max=200, block_max=1024, chunk=512),
     dict(sub_max=0, wave_max=64, block_max=4096, chunk=2048),
+    # the big-subtree tier (k_bigsub, binary builds; off by default)
+    dict(sub_max=64, wave_max=256, block_max=2048, chunk=1024, bigsub_max=256),
+    dict(sub_max=32, wave_max=200, block_max=1024, chunk=512, bigsub_max=200),
 ]
 
 
