@@ -165,6 +165,10 @@ struct ForestArgs {
   // nodes of sub_max < count <= bigsub_max (= wave_max, <= 256) and k_bigsub grows each
   // one's whole subtree on chip
   int64_t bigsub_max;
+  // 1: every tree evaluates every feature (max_features == d: boosting, max_features=None)
+  // -- the large tier then needs exactly ceil(d / kg_large) feature rounds per level, launched
+  // without reading the "need more" flag back after each round
+  int64_t all_features;
 };
 
 constexpr int kTiers = 4;  // 0 subtree, 1 wave, 2 block, 3 large
@@ -3474,7 +3478,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     }
     if (nL) {
       k_large_prep<<<nL, 64, 0, st>>>(c, cur, nL);
-      while (true) {
+      const int fixed_rounds = a->all_features ? (int)((a->d + a->kg_large - 1) / a->kg_large) : 0;
+      for (int round = 0;; ++round) {
         ++large_rounds;
         HIP_OK(hipMemsetAsync(c.ghist, 0, (size_t)nL * a->kg_large * ghist_feat_bytes(MODE, CH), st));
         HIP_OK(hipMemsetAsync(c.counters + kNeedMore, 0, 4, st));
@@ -3482,6 +3487,10 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
         if (c.packed) k_hist_large<MODE, true><<<gh, 256, lds_hl, st>>>(c);
         else k_hist_large<MODE, false><<<gh, 256, lds_hl, st>>>(c);
         k_split_large<GM><<<nL, 256, lds_sl, st>>>(c, cur);
+        if (fixed_rounds) {   // every node visits every feature: the round count is known
+          if (round + 1 >= fixed_rounds) break;
+          continue;
+        }
         HIP_OK(hipMemcpyAsync(h + 32, c.counters + kNeedMore, 4, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
         if (!h[32]) break;

@@ -1,0 +1,252 @@
+// gbrt.hip — gradient-boosting stage kernels for CDNA4 (gfx950).
+//
+// The reference fits GradientBoosting{Classifier,Regressor} through sklearn
+// (aws-prod/worker/worker.py:41,48 whitelist; sklearn ensemble/_gb.py `_fit_stage`: negative
+// gradient, K regression trees, `_update_terminal_regions` line search, raw-score update).
+// models/boosting.py grows stage s of EVERY fit of a batch with one call of the batched tree
+// builder (forest.hip, regression mode); these kernels are the rest of the stage, fused:
+//
+//   k_gb_leafsums  every (tree, in-bag row): walk the stage tree, accumulate the Newton
+//                  numerator / denominator of the row's leaf in LDS (per workgroup), flush
+//                  with one atomic per touched leaf -- replaces apply + boolean masking +
+//                  index_add over fits x rows (the float64 atomics of a depth-3 stage queue on
+//                  a handful of addresses, profiles/r3_gbrt_config6.md)
+//   k_gb_values    one thread per (tree, leaf slot): squared error -> the leaf's node mean
+//                  (the builder's exact integer sums), log-loss / exponential -> one Newton step
+//   k_gb_update    every (tree, row), train and held-out: raw[fit, k] += lr * value(leaf)
+//   k_gb_grad      every (fit, row): the next stage's negative gradient from raw (binomial /
+//                  multinomial / exponential / squared error), float64 for the line search and
+//                  float32 for the tree builder's target matrix
+//
+// A leaf is addressed by its PATH SLOT: 1 at the root, 2 s + (went right) per level, so a
+// tree of depth <= D has slots in [1, 2^(D+1)) and per-tree leaf arrays need no node index.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include "forest_common.h"
+
+namespace dml {
+
+enum GbLoss : int32_t { kGbSq = 0, kGbAbs = 1, kGbHuber = 2, kGbQuant = 3, kGbLog = 4, kGbExp = 5 };
+
+struct GbStageArgs {
+  int64_t Xb, ld, n;          // uint8 bins [n][ld]
+  int64_t nodes, node_val;    // the stage's trees in pool layout (tree j's root = node j), node_val VC = 3
+  int64_t J, K, S;            // trees of the stage, classes per fit (1: binary / regression), slots per tree
+  int64_t tree_raw;           // int32 [J]: row of `raw` tree j updates (fit * K + class)
+  int64_t tree_loss;          // int32 [J] (GbLoss)
+  int64_t tree_lr;            // double [J]
+  int64_t inbag;              // uint8 [J][n]
+  int64_t grad;               // double [J][n]: the stage's negative gradient (tree j's target)
+  int64_t ycls;               // int32 [n] class ids (classification)
+  int64_t slot_sum;           // double [J][S][2]: (numerator, denominator), zeroed by the caller
+  int64_t slot_node;          // int32 [J][S]: leaf node of each slot
+  int64_t slot_val;           // double [J][S]
+  int64_t raw;                // double [F * K][n]
+};
+
+struct GbGradArgs {
+  int64_t n, K, A;            // rows, classes per fit, active fits
+  int64_t fit_raw;            // int32 [A]: first raw row of active fit a (fit * K)
+  int64_t fit_loss;           // int32 [A]
+  int64_t raw;                // double [F * K][n]
+  int64_t ycls;               // int32 [n]
+  int64_t yreg;               // double [n]
+  int64_t grad;               // double [A * K][n] out
+  int64_t tgt;                // float [A * K][n] out
+};
+
+#define GB_PTR(T, v) ((T*)(uintptr_t)(v))
+
+// leaf slot (and leaf node) of one row in tree j
+__device__ __forceinline__ int gb_slot(const NodeRec* __restrict__ nodes, const uint8_t* __restrict__ xr, int j,
+                                       int& leaf) {
+  int node = j, slot = 1;
+  NodeRec r = nodes[node];
+  for (int steps = 0; r.split >= 0 && steps < 64; ++steps) {
+    const int go = xr[r.split >> 8] > (r.split & 255) ? 1 : 0;
+    node = r.left + go;
+    slot = 2 * slot + go;
+    r = nodes[node];
+  }
+  leaf = node;
+  return slot;
+}
+
+template <int S>
+__global__ __launch_bounds__(256) void k_gb_leafsums(GbStageArgs a) {
+  __shared__ double num[S], den[S];
+  __shared__ int nd[S];
+  const int j = blockIdx.y;
+  for (int i = threadIdx.x; i < S; i += 256) { num[i] = 0.0; den[i] = 0.0; nd[i] = -1; }
+  __syncthreads();
+  const int64_t n = a.n;
+  const uint8_t* X = GB_PTR(const uint8_t, a.Xb);
+  const NodeRec* nodes = GB_PTR(const NodeRec, a.nodes);
+  const uint8_t* inb = GB_PTR(const uint8_t, a.inbag) + (int64_t)j * n;
+  const double* g = GB_PTR(const double, a.grad) + (int64_t)j * n;
+  const int32_t* ycls = GB_PTR(const int32_t, a.ycls);
+  const int loss = GB_PTR(const int32_t, a.tree_loss)[j];
+  const int K = (int)a.K;
+  const int cls = GB_PTR(const int32_t, a.tree_raw)[j] % K;
+  const bool newton = loss == kGbLog || loss == kGbExp;
+  const int64_t r0 = (int64_t)blockIdx.x * 1024;
+  for (int u = 0; u < 4; ++u) {
+    const int64_t r = r0 + u * 256 + threadIdx.x;
+    if (r >= n || !inb[r]) continue;
+    int leaf;
+    const int slot = gb_slot(nodes, X + r * a.ld, j, leaf);
+    nd[slot] = leaf;   // every row of the leaf writes the same node
+    if (!newton) continue;
+    const double gv = g[r];
+    double h;
+    if (K > 1) {   // multinomial: p_k = y_k - g, hessian p (1 - p)
+      const double p = (ycls[r] == cls ? 1.0 : 0.0) - gv;
+      h = p * (1.0 - p);
+    } else {
+      const double yb = (double)ycls[r];
+      if (loss == kGbExp) {
+        h = yb > 0.5 ? gv : -gv;
+      } else {
+        const double p = yb - gv;
+        h = p * (1.0 - p);
+      }
+    }
+    atomicAdd(&num[slot], gv);
+    atomicAdd(&den[slot], h);
+  }
+  __syncthreads();
+  double* ss = GB_PTR(double, a.slot_sum) + (int64_t)j * S * 2;
+  int32_t* sn = GB_PTR(int32_t, a.slot_node) + (int64_t)j * S;
+  for (int i = threadIdx.x; i < S; i += 256) {
+    if (nd[i] < 0) continue;
+    sn[i] = nd[i];
+    if (newton) {
+      atomicAdd(&ss[2 * i], num[i]);
+      atomicAdd(&ss[2 * i + 1], den[i]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gb_values(GbStageArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t S = a.S;
+  if (i >= a.J * S) return;
+  const int j = (int)(i / S);
+  const int32_t node = GB_PTR(const int32_t, a.slot_node)[i];
+  double v = 0.0;
+  if (node >= 0) {
+    const int loss = GB_PTR(const int32_t, a.tree_loss)[j];
+    if (loss == kGbLog || loss == kGbExp) {
+      const double* ss = GB_PTR(const double, a.slot_sum) + 2 * i;
+      double num = ss[0];
+      const double den = ss[1];
+      if (a.K > 1) num = num * (double)(a.K - 1) / (double)a.K;
+      v = fabs(den) < 1e-150 ? (num == 0.0 ? 0.0 : copysign(1e150, num)) : num / den;
+    } else {   // squared error: the node mean of the builder's exact sums
+      const double* nv = GB_PTR(const double, a.node_val) + (int64_t)node * 3;
+      v = nv[0] > 0.0 ? nv[1] / fmax(nv[0], 1e-300) : 0.0;
+    }
+  }
+  GB_PTR(double, a.slot_val)[i] = v;
+}
+
+template <int S>
+__global__ __launch_bounds__(256) void k_gb_update(GbStageArgs a) {
+  __shared__ double val[S];
+  const int j = blockIdx.y;
+  for (int i = threadIdx.x; i < S; i += 256) val[i] = GB_PTR(const double, a.slot_val)[(int64_t)j * S + i];
+  __syncthreads();
+  const int64_t n = a.n;
+  const uint8_t* X = GB_PTR(const uint8_t, a.Xb);
+  const NodeRec* nodes = GB_PTR(const NodeRec, a.nodes);
+  double* raw = GB_PTR(double, a.raw) + (int64_t)GB_PTR(const int32_t, a.tree_raw)[j] * n;
+  const double lr = GB_PTR(const double, a.tree_lr)[j];
+  const int64_t r0 = (int64_t)blockIdx.x * 1024;
+  for (int u = 0; u < 4; ++u) {
+    const int64_t r = r0 + u * 256 + threadIdx.x;
+    if (r >= n) continue;
+    int leaf;
+    const int slot = gb_slot(nodes, X + r * a.ld, j, leaf);
+    raw[r] += val[slot] * lr;
+  }
+}
+
+__device__ __forceinline__ double gb_sigmoid(double x) { return 1.0 / (1.0 + exp(-x)); }
+
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_gb_grad(GbGradArgs a) {
+  const int fa = blockIdx.y;
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t n = a.n;
+  if (r >= n) return;
+  const int K = (int)a.K;
+  const int loss = GB_PTR(const int32_t, a.fit_loss)[fa];
+  const double* raw = GB_PTR(const double, a.raw) + (int64_t)GB_PTR(const int32_t, a.fit_raw)[fa] * n;
+  double* g = GB_PTR(double, a.grad) + (int64_t)fa * K * n;
+  float* t = GB_PTR(float, a.tgt) + (int64_t)fa * K * n;
+  if (loss == kGbLog && K > 1) {   // softmax over the fit's K raw rows (max-shifted, like torch)
+    double z[KMAX];
+    double mx = -INFINITY;
+    for (int k = 0; k < K && k < KMAX; ++k) { z[k] = raw[(int64_t)k * n + r]; mx = fmax(mx, z[k]); }
+    double s = 0.0;
+    for (int k = 0; k < K && k < KMAX; ++k) { z[k] = exp(z[k] - mx); s += z[k]; }
+    const int y = GB_PTR(const int32_t, a.ycls)[r];
+    for (int k = 0; k < K && k < KMAX; ++k) {
+      const double v = (y == k ? 1.0 : 0.0) - z[k] / s;
+      g[(int64_t)k * n + r] = v;
+      t[(int64_t)k * n + r] = (float)v;
+    }
+    return;
+  }
+  const double x = raw[r];
+  double v;
+  if (loss == kGbLog) {
+    v = (double)GB_PTR(const int32_t, a.ycls)[r] - gb_sigmoid(x);
+  } else if (loss == kGbExp) {
+    const double yb = (double)GB_PTR(const int32_t, a.ycls)[r];
+    v = yb * exp(-x) - (1.0 - yb) * exp(x);
+  } else {   // squared error
+    v = GB_PTR(const double, a.yreg)[r] - x;
+  }
+  g[r] = v;
+  t[r] = (float)v;
+}
+
+}  // namespace dml
+
+using namespace dml;
+
+extern "C" {
+
+int dml_gb_sizeof_stage_args() { return (int)sizeof(GbStageArgs); }
+int dml_gb_sizeof_grad_args() { return (int)sizeof(GbGradArgs); }
+
+// leaf sums + leaf values + raw update of one stage (slot_sum / slot_node zeroed / -1 by the caller)
+int dml_gb_stage(GbStageArgs* a, hipStream_t st) {
+  if (a->J <= 0 || a->n <= 0) return 0;
+  const dim3 grid((unsigned)((a->n + 1023) / 1024), (unsigned)a->J);
+  switch (a->S) {
+#define GB_CASE(SV)                                                                   \
+    case SV:                                                                          \
+      k_gb_leafsums<SV><<<grid, 256, 0, st>>>(*a);                                    \
+      k_gb_values<<<(unsigned)((a->J * SV + 255) / 256), 256, 0, st>>>(*a);           \
+      k_gb_update<SV><<<grid, 256, 0, st>>>(*a);                                      \
+      break;
+    GB_CASE(4) GB_CASE(8) GB_CASE(16) GB_CASE(32) GB_CASE(64) GB_CASE(128) GB_CASE(256) GB_CASE(512)
+#undef GB_CASE
+    default: return 2;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+int dml_gb_grad(GbGradArgs* a, hipStream_t st) {
+  if (a->A <= 0 || a->n <= 0) return 0;
+  if (a->K > 64) return 2;
+  const dim3 grid((unsigned)((a->n + 255) / 256), (unsigned)a->A);
+  if (a->K <= 8) k_gb_grad<8><<<grid, 256, 0, st>>>(*a);
+  else k_gb_grad<64><<<grid, 256, 0, st>>>(*a);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+}  // extern "C"

@@ -27,7 +27,9 @@ and is reported in the subtask's warnings.
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
 import time
 from typing import Any, Dict, List
 
@@ -297,6 +299,22 @@ class GradientBoostingFamily(Family):
         gens = [torch.Generator(device="cpu").manual_seed(int(s) & 0x7FFFFFFF) for s in seeds]
         kept: List[List[Any]] = [[] for _ in range(F)]
         train_idx = [torch.nonzero(train[f]).squeeze(1) for f in range(F)]
+        # fused HIP stage (csrc/kernels/gbrt.hip): gradient, leaf line search and raw update as
+        # three kernels per stage instead of torch glue (losses with sums-only line searches)
+        fused = (gpu and not sharded and os.environ.get("DML_GB_FUSED", "1") != "0"
+                 and all(t.params["loss"] in (LOSS_SQ, LOSS_LOG, LOSS_EXP) for t in batch)
+                 and max(t.params["max_depth"] for t in batch) <= 8
+                 and getattr(native.hip_lib(), "dml_gb_stage", None) is not None)
+        if fused:
+            lib = native.hip_lib()
+            stream = native.stream_handle(dev)
+            S = max(4, 2 ** (max(t.params["max_depth"] for t in batch) + 1))   # leaf path slots per tree
+            G64 = torch.empty((F * K, n), dtype=torch.float64, device=dev)
+            T32 = torch.empty((F * K, n), dtype=torch.float32, device=dev)
+            ycls32 = data.y_cls.to(torch.int32).contiguous() if clf else torch.zeros(1, dtype=torch.int32, device=dev)
+            yreg64 = torch.zeros(1, dtype=torch.float64, device=dev) if clf else yreg.contiguous()
+            loss_all = np.array([t.params["loss"] for t in batch], dtype=np.int32)   # LOSS_* == gbrt.hip GbLoss
+            lr_all = np.array([t.params["learning_rate"] for t in batch], dtype=np.float64)
         if sharded:   # the global training rows (ascending), for subsample draws equal on every rank
             cnts = [data.all_gather_equal(torch.tensor([int(ti.numel())], device=dev)).cpu().numpy() for ti in train_idx]
             gtrain = [data._gather_rows(ti + data.r0, c) for ti, c in zip(train_idx, cnts)]
@@ -306,14 +324,25 @@ class GradientBoostingFamily(Family):
                 break
             A = len(act)
             act_t = torch.tensor(act, device=dev)
-            R = raw[act_t]                                                 # [A, K, n]
             loss = [batch[f].params["loss"] for f in act]
-            # --- negative gradient (pseudo-residuals) ------------------------------------
-            G = torch.empty_like(R)
             hub_delta: Dict[int, float] = {}
-            for a, f in enumerate(act):
-                G[a], hub_delta[f] = self._neg_grad(batch[f].params, R[a], Y if clf else None,
-                                                    ybin if clf else None, None if clf else yreg, K, train[f])
+            if fused:   # --- negative gradient of every active fit: one kernel -------------------
+                act_np = np.asarray(act, dtype=np.int32)
+                fit_raw = torch.from_numpy(act_np * K).to(dev)
+                fit_loss = torch.from_numpy(loss_all[act_np]).to(dev)
+                ga = native.GbGradArgs(n=n, K=K, A=A, fit_raw=native.ptr(fit_raw), fit_loss=native.ptr(fit_loss),
+                                       raw=native.ptr(raw), ycls=native.ptr(ycls32), yreg=native.ptr(yreg64),
+                                       grad=native.ptr(G64), tgt=native.ptr(T32))
+                rc = lib.dml_gb_grad(ctypes.byref(ga), stream)
+                if rc:
+                    raise RuntimeError(f"dml_gb_grad failed ({rc})")
+            else:
+                R = raw[act_t]                                             # [A, K, n]
+                # --- negative gradient (pseudo-residuals) --------------------------------
+                G = torch.empty_like(R)
+                for a, f in enumerate(act):
+                    G[a], hub_delta[f] = self._neg_grad(batch[f].params, R[a], Y if clf else None,
+                                                        ybin if clf else None, None if clf else yreg, K, train[f])
             # --- in-bag rows: the split's train rows, or a per-stage subsample of them ---
             inbag = train[act_t]
             sub_rows = []
@@ -334,24 +363,8 @@ class GradientBoostingFamily(Family):
             # one role row per tree (roles = in-bag mask of its fit)
             J = A * K
             roles_t = inbag.repeat_interleave(K, dim=0).to(torch.uint8).contiguous()   # [J, n]
-            tgt = G.reshape(J, n).float().contiguous()
-            specs = forest_ops.make_specs(J)
-            for a, f in enumerate(act):
-                rp = batch[f].params
-                for k in range(K):
-                    j = a * K + k
-                    specs[j]["seed"] = native_seed(seeds[f], stage * K + k)
-                    specs[j]["split"] = j
-                    specs[j]["fit"] = j
-                    specs[j]["target"] = j
-                    specs[j]["max_depth"] = rp["max_depth"]
-                    specs[j]["min_samples_split"] = rp["min_samples_split"]
-                    specs[j]["min_samples_leaf"] = rp["min_samples_leaf"]
-                    specs[j]["max_features"] = rp["max_features"]
-                    specs[j]["bootstrap"] = 0
-                    specs[j]["criterion"] = rp.get("criterion", forest_ops.MSE)
-                    specs[j]["min_impurity_decrease"] = rp["min_impurity_decrease"]
-                    specs[j]["min_weight_frac"] = rp.get("min_weight_fraction_leaf", 0.0)
+            tgt = T32[:J] if fused else G.reshape(J, n).float().contiguous()
+            specs = _stage_specs(batch, act, K, seeds, stage)
             limit = np.repeat([batch[f].params.get("max_leaf_nodes", 0) for f in act], K)
             ccp = np.repeat([batch[f].params.get("ccp_alpha", 0.0) for f in act], K)
             if sharded:   # level-synchronous trees over the row shards (ops/forest_dp.py)
@@ -379,7 +392,7 @@ class GradientBoostingFamily(Family):
                 if ccp.any():     # minimal cost-complexity pruning of each stage tree (variance impurity)
                     forest_ops.prune_ccp(fb, specs, ccp)
                 _refine(data, fb, Xb, specs, roles_t)
-                leaf = forest_ops.apply(fb, Xb).long()                     # [J, n]
+                leaf = None if fused else forest_ops.apply(fb, Xb).long()  # [J, n] (the fused stage walks itself)
                 vals = fb.vals
             else:
                 fb = forest_ops.build_cpu(Xb_host, None, tgt.numpy(), roles_t.numpy(), specs, 1, True, ystride=n)
@@ -391,73 +404,35 @@ class GradientBoostingFamily(Family):
                 leaf = torch.from_numpy(forest_ops.apply(fb, Xb_host)).long()
                 vals = torch.from_numpy(fb.vals)
             P = vals.shape[0]
-            # --- leaf values (line search) -----------------------------------------------
-            value = vals[:, 1] / vals[:, 0].clamp_min(1e-300)             # squared error: node mean
-            value = torch.where(vals[:, 0] > 0, value, torch.zeros_like(value))
-            m = roles_t.bool()
-            lf = leaf[m]
-            needs = {l for l in loss if l != LOSS_SQ}
-            if needs:
-                value = value.clone()
-                tree_of = torch.arange(J, device=dev).view(J, 1).expand(J, n)[m]
-                fit_of_tree = torch.tensor([act[j // K] for j in range(J)], device=dev)
-                loss_of_tree = torch.tensor([loss[j // K] for j in range(J)], device=dev)
-                g = G.reshape(J, n)[m]
-                node_loss = torch.full((P,), -1, dtype=torch.long, device=dev)
-                node_loss.scatter_(0, lf, loss_of_tree[tree_of])
-                if LOSS_LOG in needs or LOSS_EXP in needs:
-                    num = leaf_sum(lf, g, P)
-                    if K > 1:
-                        yk = Y[torch.arange(J, device=dev) % K].reshape(J, n)[m]
-                        prob = yk - g
-                        hess = prob * (1 - prob)
-                        num = num * (K - 1) / K
-                    else:
-                        yb = ybin.view(1, n).expand(J, n)[m]
-                        prob = yb - g
-                        hess_log = prob * (1 - prob)
-                        hess_exp = torch.where(yb > 0.5, g, -g)
-                        is_exp = loss_of_tree[tree_of] == LOSS_EXP
-                        hess = torch.where(is_exp, hess_exp, hess_log)
-                    den = leaf_sum(lf, hess, P)
-                    if sharded:   # leaf sums over every rank's rows
-                        num, den = data.all_reduce(num), data.all_reduce(den)
-                    newton = torch.where(den.abs() < 1e-150, torch.where(num == 0, 0.0, torch.sign(num) * 1e150),
-                                         num / torch.where(den.abs() < 1e-150, torch.ones_like(den), den))
-                    sel = (node_loss == LOSS_LOG) | (node_loss == LOSS_EXP)
-                    value = torch.where(sel, newton, value)
-                if needs & {LOSS_ABS, LOSS_HUBER, LOSS_QUANT}:
-                    resid = (yreg.view(1, n) - R.reshape(J, n))[m]        # y - raw (K == 1 for regression)
-                    for lk in needs & {LOSS_ABS, LOSS_HUBER, LOSS_QUANT}:
-                        sel_rows = loss_of_tree[tree_of] == lk
-                        if lk == LOSS_QUANT:
-                            # per-tree alpha: group trees by alpha
-                            for alpha in sorted({batch[act[j // K]].params["alpha"] for j in range(J)
-                                                 if loss[j // K] == lk}):
-                                trees = torch.tensor([j for j in range(J) if loss[j // K] == lk and
-                                                      batch[act[j // K]].params["alpha"] == alpha], device=dev)
-                                rs = sel_rows & torch.isin(tree_of, trees)
-                                pv = _segment_percentile(lf[rs], resid[rs], P, alpha)
-                                value = torch.where(~torch.isnan(pv), pv, value)
-                            continue
-                        med = _segment_percentile(lf[sel_rows], resid[sel_rows], P, 0.5)
-                        if lk == LOSS_ABS:
-                            value = torch.where(~torch.isnan(med), med, value)
-                        else:
-                            delta = torch.zeros(J, dtype=torch.float64, device=dev)
-                            for j in range(J):
-                                if loss[j // K] == LOSS_HUBER:
-                                    delta[j] = hub_delta[act[j // K]]
-                            diff = resid[sel_rows] - med[lf[sel_rows]]
-                            dl = delta[tree_of[sel_rows]]
-                            term = torch.sign(diff) * torch.minimum(dl, diff.abs())
-                            s_ = leaf_sum(lf[sel_rows], term, P)
-                            c_ = torch.bincount(lf[sel_rows], minlength=P).to(torch.float64)
-                            hub = med + s_ / c_.clamp_min(1)
-                            value = torch.where(~torch.isnan(med), hub, value)
-            # --- raw-score update of every row (train and held-out) ------------------------
-            upd = value[leaf].view(A, K, n) * lr[act_t].view(A, 1, 1)
-            raw[act_t] += upd
+            if fused:   # --- leaf line search + raw update of every row: three kernels ------------
+                j_fit = np.repeat(np.asarray(act, dtype=np.int32), K)
+                tree_raw = torch.from_numpy(j_fit * K + np.tile(np.arange(K, dtype=np.int32), A)).to(dev)
+                tree_loss = torch.from_numpy(loss_all[j_fit]).to(dev)
+                tree_lr = torch.from_numpy(lr_all[j_fit]).to(dev)
+                slot_sum = torch.zeros((J, S, 2), dtype=torch.float64, device=dev)
+                slot_node = torch.full((J, S), -1, dtype=torch.int32, device=dev)
+                slot_val = torch.empty((J, S), dtype=torch.float64, device=dev)
+                sa = native.GbStageArgs(Xb=native.ptr(Xb), ld=Xb.stride(0), n=n, nodes=native.ptr(fb.nodes),
+                                        node_val=native.ptr(vals), J=J, K=K, S=S, tree_raw=native.ptr(tree_raw),
+                                        tree_loss=native.ptr(tree_loss), tree_lr=native.ptr(tree_lr),
+                                        inbag=native.ptr(roles_t), grad=native.ptr(G64), ycls=native.ptr(ycls32),
+                                        slot_sum=native.ptr(slot_sum), slot_node=native.ptr(slot_node),
+                                        slot_val=native.ptr(slot_val), raw=native.ptr(raw))
+                rc = lib.dml_gb_stage(ctypes.byref(sa), stream)
+                if rc:
+                    raise RuntimeError(f"dml_gb_stage failed ({rc})")
+                if keep_models:   # node-indexed leaf values for the kept trees
+                    value = torch.zeros(P, dtype=torch.float64, device=dev)
+                    ok = slot_node >= 0
+                    value[slot_node[ok].long()] = slot_val[ok]
+            else:
+                value = self._line_search(batch, act, loss, vals, leaf_of=lambda: leaf, roles_t=roles_t, G=G, R=R,
+                                          Y=Y if clf else None, ybin=ybin if clf else None,
+                                          yreg=None if clf else yreg, K=K, J=J, n=n, P=P, hub_delta=hub_delta,
+                                          sharded=sharded, data=data)
+                # --- raw-score update of every row (train and held-out) --------------------
+                upd = value[leaf].view(A, K, n) * lr[act_t].view(A, 1, 1)
+                raw[act_t] += upd
             for a, f in enumerate(act):
                 if f in val_rows:
                     vl = self._val_loss(batch[f].params, raw[f][:, val_rows[f]], val_rows[f], data, K, hub_delta.get(f))
@@ -476,7 +451,84 @@ class GradientBoostingFamily(Family):
                     kept[f].append([_extract_tree(nodes_np, vals_np * lr_f, a * K + k) for k in range(K)])
         if gpu:
             torch.cuda.synchronize(dev)
-        dt = time.perf_counter() - t0
+        return self._outputs(batch, raw, init, kept, data, K, clf, keep_models, time.perf_counter() - t0)
+
+    @staticmethod
+    def _line_search(batch, act, loss, vals, leaf_of, roles_t, G, R, Y, ybin, yreg, K, J, n, P, hub_delta, sharded,
+                     data):
+        """Leaf values of one stage (torch path): node means for squared error, one Newton
+        step for log-loss / exponential, (weighted) percentiles for absolute / huber / quantile."""
+        dev = vals.device
+        leaf = leaf_of()
+        # --- leaf values (line search) -----------------------------------------------
+        value = vals[:, 1] / vals[:, 0].clamp_min(1e-300)             # squared error: node mean
+        value = torch.where(vals[:, 0] > 0, value, torch.zeros_like(value))
+        m = roles_t.bool()
+        lf = leaf[m]
+        needs = {l for l in loss if l != LOSS_SQ}
+        if needs:
+            value = value.clone()
+            tree_of = torch.arange(J, device=dev).view(J, 1).expand(J, n)[m]
+            fit_of_tree = torch.tensor([act[j // K] for j in range(J)], device=dev)
+            loss_of_tree = torch.tensor([loss[j // K] for j in range(J)], device=dev)
+            g = G.reshape(J, n)[m]
+            node_loss = torch.full((P,), -1, dtype=torch.long, device=dev)
+            node_loss.scatter_(0, lf, loss_of_tree[tree_of])
+            if LOSS_LOG in needs or LOSS_EXP in needs:
+                num = leaf_sum(lf, g, P)
+                if K > 1:
+                    yk = Y[torch.arange(J, device=dev) % K].reshape(J, n)[m]
+                    prob = yk - g
+                    hess = prob * (1 - prob)
+                    num = num * (K - 1) / K
+                else:
+                    yb = ybin.view(1, n).expand(J, n)[m]
+                    prob = yb - g
+                    hess_log = prob * (1 - prob)
+                    hess_exp = torch.where(yb > 0.5, g, -g)
+                    is_exp = loss_of_tree[tree_of] == LOSS_EXP
+                    hess = torch.where(is_exp, hess_exp, hess_log)
+                den = leaf_sum(lf, hess, P)
+                if sharded:   # leaf sums over every rank's rows
+                    num, den = data.all_reduce(num), data.all_reduce(den)
+                newton = torch.where(den.abs() < 1e-150, torch.where(num == 0, 0.0, torch.sign(num) * 1e150),
+                                     num / torch.where(den.abs() < 1e-150, torch.ones_like(den), den))
+                sel = (node_loss == LOSS_LOG) | (node_loss == LOSS_EXP)
+                value = torch.where(sel, newton, value)
+            if needs & {LOSS_ABS, LOSS_HUBER, LOSS_QUANT}:
+                resid = (yreg.view(1, n) - R.reshape(J, n))[m]        # y - raw (K == 1 for regression)
+                for lk in needs & {LOSS_ABS, LOSS_HUBER, LOSS_QUANT}:
+                    sel_rows = loss_of_tree[tree_of] == lk
+                    if lk == LOSS_QUANT:
+                        # per-tree alpha: group trees by alpha
+                        for alpha in sorted({batch[act[j // K]].params["alpha"] for j in range(J)
+                                             if loss[j // K] == lk}):
+                            trees = torch.tensor([j for j in range(J) if loss[j // K] == lk and
+                                                  batch[act[j // K]].params["alpha"] == alpha], device=dev)
+                            rs = sel_rows & torch.isin(tree_of, trees)
+                            pv = _segment_percentile(lf[rs], resid[rs], P, alpha)
+                            value = torch.where(~torch.isnan(pv), pv, value)
+                        continue
+                    med = _segment_percentile(lf[sel_rows], resid[sel_rows], P, 0.5)
+                    if lk == LOSS_ABS:
+                        value = torch.where(~torch.isnan(med), med, value)
+                    else:
+                        delta = torch.zeros(J, dtype=torch.float64, device=dev)
+                        for j in range(J):
+                            if loss[j // K] == LOSS_HUBER:
+                                delta[j] = hub_delta[act[j // K]]
+                        diff = resid[sel_rows] - med[lf[sel_rows]]
+                        dl = delta[tree_of[sel_rows]]
+                        term = torch.sign(diff) * torch.minimum(dl, diff.abs())
+                        s_ = leaf_sum(lf[sel_rows], term, P)
+                        c_ = torch.bincount(lf[sel_rows], minlength=P).to(torch.float64)
+                        hub = med + s_ / c_.clamp_min(1)
+                        value = torch.where(~torch.isnan(med), hub, value)
+        return value
+
+    @staticmethod
+    def _outputs(batch, raw, init, kept, data, K, clf, keep_models, dt) -> List[FitOutput]:
+        F = len(batch)
         outs = []
         for f, t in enumerate(batch):
             rows = data.test_rows[t.split].long()
@@ -547,6 +599,32 @@ class GradientBoostingFamily(Family):
         # huber: delta = alpha-percentile of |y - raw| over the fit's training rows (set_huber_delta)
         delta = float(_percentile_icdf(diff[train_row].abs(), rp["alpha"]))
         return torch.where(diff.abs() <= delta, diff, delta * torch.sign(diff)).view(1, -1), delta
+
+
+def _stage_specs(batch, act: List[int], K: int, seeds: List[int], stage: int) -> np.ndarray:
+    """TreeSpecs of one stage: tree j = a * K + k grows fit act[a]'s class-k tree on target
+    row j with in-bag role row j (built column-wise, not field by field per tree)."""
+    A = len(act)
+    J = A * K
+    specs = forest_ops.make_specs(J)
+    if J == 0:
+        return specs
+    rps = [batch[f].params for f in act]
+    rep = lambda vals, dt: np.repeat(np.asarray(vals, dtype=dt), K)
+    specs["seed"] = [native_seed(seeds[f], stage * K + k) for f in act for k in range(K)]
+    j = np.arange(J, dtype=np.int32)
+    specs["split"] = j
+    specs["fit"] = j
+    specs["target"] = j
+    specs["max_depth"] = rep([rp["max_depth"] for rp in rps], np.int64)
+    specs["min_samples_split"] = rep([rp["min_samples_split"] for rp in rps], np.int64)
+    specs["min_samples_leaf"] = rep([rp["min_samples_leaf"] for rp in rps], np.int64)
+    specs["max_features"] = rep([rp["max_features"] for rp in rps], np.int64)
+    specs["bootstrap"] = 0
+    specs["criterion"] = rep([rp.get("criterion", forest_ops.MSE) for rp in rps], np.int64)
+    specs["min_impurity_decrease"] = rep([rp["min_impurity_decrease"] for rp in rps], np.float64)
+    specs["min_weight_frac"] = rep([rp.get("min_weight_fraction_leaf", 0.0) for rp in rps], np.float64)
+    return specs
 
 
 def _extract_tree(nodes: np.ndarray, values: np.ndarray, root: int):

@@ -307,6 +307,9 @@ class LogisticFamily(Family):
     classifiers = ("LogisticRegression",)
     history = 10
     data_parallel = True   # loss + gradient all-reduced per objective evaluation under a RowShard
+    # binned-only tables (float32 rows too large for HBM): every objective evaluation is one
+    # pass over the host rows in chunks, all candidates x folds of the batch per chunk
+    streams_rows = True
 
     def resolve(self, model_type, params, n_train, n_features, n_classes):
         p = dict(_LR_DEFAULTS)
@@ -370,6 +373,8 @@ class LogisticFamily(Family):
     # --------------------------------------------------------------------------------
     def _objective(self, data, b: _Batch, W: torch.Tensor):
         d = data.d
+        if getattr(b, "streamed", False):
+            return self._objective_streamed(data, b, W)
         if b.mf is not None:   # matrix cores: fused forward + split-K gradient (lr_mfma.hip)
             loss, G = b.mf.objective(data, b, W)
             loss, G = _dp_sum(data, loss), _dp_sum(data, G)
@@ -401,6 +406,43 @@ class LogisticFamily(Family):
         G += reg
         f = loss + 0.5 * b.segsum((W * reg).sum(0)).double()
         return f, G
+
+    @staticmethod
+    def _link_grad(data, b: _Batch, Z: torch.Tensor, y: torch.Tensor, roles: torch.Tensor):
+        """(R, loss[F]) of logits Z over the rows of y / roles (the fused kernel on the GPU)."""
+        if not data.is_gpu:
+            return link_grad_torch(Z, y, roles, b.col0_l, b.K_l, b.kind_l, b.split_l, b.scale.tolist(), b.cw)
+        n = Z.shape[0]
+        R = torch.empty_like(Z)
+        loss = torch.empty(b.F, dtype=torch.float64, device=Z.device)
+        rc = native.hip_lib().dml_lr_link_grad(
+            native.ptr(Z), n, b.M, native.ptr(y), native.ptr(roles), native.ptr(b.col0), native.ptr(b.K),
+            native.ptr(b.kind), native.ptr(b.split), native.ptr(b.scale), b.F, native.ptr(b.cw),
+            int(b.cw.shape[1]) if b.cw is not None else 0, native.ptr(R), native.ptr(loss),
+            native.stream_handle(data.device))
+        if rc:
+            raise RuntimeError("dml_lr_link_grad failed")
+        return R, loss
+
+    def _objective_streamed(self, data, b: _Batch, W: torch.Tensor):
+        """The objective over a binned-only table: the host rows stream through in chunks
+        (DeviceData.stream_rows), each chunk's logits, link gradient and X^T R accumulate
+        into one loss / gradient -- one pass over the table per evaluation, every fit of the
+        batch at once (the same link kernel as the resident path, chunk by chunk)."""
+        d = data.d
+        loss = torch.zeros(b.F, dtype=torch.float64, device=data.device)
+        G = torch.zeros_like(W)
+        bias = W[d] * b.icpt_col
+        for r0, r1, Xc in data.stream_rows(_lr_stream_chunk(data, b.M)):
+            Zc = torch.addmm(bias, Xc, W[:d])
+            Rc, lc = self._link_grad(data, b, Zc, data.y_cls[r0:r1].contiguous(), data.roles[:, r0:r1].contiguous())
+            loss += lc
+            G[:d] += Xc.t() @ Rc
+            G[d] += Rc.sum(0) * b.icpt_col
+        reg = W * b.lam_col
+        reg[d] = reg[d] * b.pen_icpt_col
+        G += reg
+        return loss + 0.5 * b.segsum((W * reg).sum(0)).double(), G
 
     def _solve(self, data, b: _Batch):
         """Batched L-BFGS that stays on the device; columns with an L1 term use OWL-QN
@@ -560,7 +602,11 @@ class LogisticFamily(Family):
         # tiny lbfgs problems (iris-sized): a device launch per objective evaluation is pure
         # latency, so they run on the host with scipy's L-BFGS-B on sklearn's exact float64
         # objective -> same iterates as sklearn even where max_iter stops before convergence
+        streamed = data.X is None and getattr(data, "can_stream_rows", lambda: False)()
+        if data.X is None and not streamed:
+            raise ParamError("LogisticRegression needs the float32 rows (this table arrived as bins only)")
         small = [t for t in tasks if t.params["solver"] == "lbfgs" and not getattr(data, "is_row_shard", False) and
+                 not streamed and
                  data.train_counts[t.split] * (data.d + 1) * max(1, data.n_classes - 1) <= HOST_LBFGS_MAX_WORK]
         if small:
             done = {o.task_id: o for o in self._run_host_lbfgs(data, small, keep_models)}
@@ -571,10 +617,12 @@ class LogisticFamily(Family):
         # memory-budgeted batches of whole fits: Z and R are [n, columns] and the L-BFGS
         # history holds 2 x history [d+1, columns] matrices
         width = 1 if data.n_classes == 2 else data.n_classes
-        use_mf = mfma_enabled(data)
+        use_mf = mfma_enabled(data) and not streamed
         if use_mf:   # resident bf16 operands first, so the budget below sees them
             ops = mfma_operands(data)
             per_col = 4.0 * (ops.npad + (data.d + 1) * (2 * self.history + 10) + 32 * ops.Dp)
+        elif streamed:   # chunk-sized logits / link gradients only
+            per_col = 4.0 * (3 * min(data.n, data._chunk_rows) + (data.d + 1) * (2 * self.history + 6))
         else:
             per_col = 4.0 * (3 * data.n + (data.d + 1) * (2 * self.history + 6))
         budget = 0.45 * torch.cuda.mem_get_info(data.device)[0] if data.is_gpu else 8e9
@@ -586,6 +634,7 @@ class LogisticFamily(Family):
             return outs
         t0 = time.perf_counter()
         b = _Batch(data, tasks)
+        b.streamed = streamed
         if use_mf:
             b.mf = MfmaPlan(data, b)
         W, iters, n_evals = self._solve(data, b)
@@ -638,6 +687,25 @@ class LogisticFamily(Family):
         for f in range(b.F):
             by_split.setdefault(b.split_l[f], []).append(f)
         out: List[torch.Tensor] = [None] * b.F
+        if getattr(b, "streamed", False):   # one pass over the host rows for every split
+            from ..search.cv import ROLE_TEST
+
+            cols_of = {s: torch.cat([torch.arange(b.col0_l[f], b.col0_l[f] + b.K_l[f]) for f in fits]).to(W.device)
+                       for s, fits in by_split.items()}
+            parts: Dict[int, List[torch.Tensor]] = {s: [] for s in by_split}
+            for r0, r1, Xc in data.stream_rows(_lr_stream_chunk(data, b.M)):
+                for s_, cols in cols_of.items():
+                    m = data.roles[s_, r0:r1] == ROLE_TEST
+                    if bool(m.any()):
+                        parts[s_].append(torch.addmm(bias[cols], Xc[m], W[:d, cols]))
+            for s_, fits in by_split.items():
+                Z = torch.cat(parts[s_]) if parts[s_] else torch.empty((0, len(cols_of[s_])), dtype=W.dtype,
+                                                                       device=W.device)
+                o = 0
+                for f in fits:
+                    out[f] = Z[:, o:o + b.K_l[f]]
+                    o += b.K_l[f]
+            return out
         for s, fits in by_split.items():
             te = data.test_rows[s].long()
             cols = torch.cat([torch.arange(b.col0_l[f], b.col0_l[f] + b.K_l[f]) for f in fits]).to(W.device)
@@ -755,6 +823,12 @@ _LIN_DEFAULTS = {"fit_intercept": True, "copy_X": True, "n_jobs": None, "positiv
 def _stream_chunk(data) -> int:
     # float64 working copies of a chunk stay <= ~512 MB whatever d is
     return max(1024, min(data._chunk_rows, (1 << 29) // (8 * (data.d + 2))))
+
+
+def _lr_stream_chunk(data, M: int) -> int:
+    """Rows per streamed chunk of the logistic objective: the chunk's logits and link
+    gradient ([rows, M] float32 each) stay <= ~256 MB."""
+    return max(1024, min(data._chunk_rows, (1 << 26) // max(1, data.d + 2 * M)))
 
 
 def streamed_split_moments(data, splits: List[int]) -> Tuple[torch.Tensor, torch.Tensor]:

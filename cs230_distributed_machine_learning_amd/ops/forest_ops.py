@@ -323,6 +323,7 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     a.kg_wave, a.kg_block, a.kg_large, a.slack_wave = tiers.kg_wave, tiers.kg_block, tiers.kg_large, tiers.slack_wave
     a.sub_max = tiers.sub_max
     a.sub_cache_d = _sub_cache_stride(d) if d <= tiers.sub_cache_max_d else 0
+    a.all_features = int(T > 0 and bool(np.all(specs["max_features"] >= d)))
     big = _bigsub_on(tiers, is_reg, n_classes, d, mono_dev) and a.sub_cache_d > 0
     a.bigsub_max = min(tiers.bigsub_max, 256) if big else 0
     if big:

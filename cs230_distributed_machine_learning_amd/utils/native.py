@@ -74,7 +74,7 @@ ForestArgs = _i64_struct(
         "yq_e1", "yq_e2",
         "mono", "nbound", "fast_crit",
         "early_pred", "fit_done_level", "n_fits",
-        "bigsub_max",
+        "bigsub_max", "all_features",
     ],
 )
 
@@ -92,6 +92,13 @@ LrFwdArgs = _i64_struct(
     ["xh", "xl", "xrows", "wh", "wl", "n", "Kp", "row_tiles", "col_tiles", "row_groups", "bias", "col_fit",
      "fit_col0", "fit_k", "fit_kind", "fit_split", "scale", "cw", "cwC", "y", "roles", "rh", "rl", "kr", "loss"],
 )
+# csrc/kernels/gbrt.hip argument blocks (fused gradient-boosting stage kernels)
+GbStageArgs = _i64_struct(
+    "GbStageArgs",
+    ["Xb", "ld", "n", "nodes", "node_val", "J", "K", "S", "tree_raw", "tree_loss", "tree_lr", "inbag", "grad",
+     "ycls", "slot_sum", "slot_node", "slot_val", "raw"],
+)
+GbGradArgs = _i64_struct("GbGradArgs", ["n", "K", "A", "fit_raw", "fit_loss", "raw", "ycls", "yreg", "grad", "tgt"])
 LrGradArgs = _i64_struct("LrGradArgs", ["rh", "rl", "unused", "xth", "xtl", "m_tiles", "n_tiles", "Kp", "S", "Kc", "out"])
 
 
@@ -206,12 +213,20 @@ def _register_optional(lib) -> None:
         "dml_dp_sizeof_args": (c_i32, []),
         "dml_dp_sizeof_slot": (c_i32, []),
         "dml_dp_step": (c_i32, [c_vp, c_i32, c_vp]),
+        "dml_gb_sizeof_stage_args": (c_i32, []),
+        "dml_gb_sizeof_grad_args": (c_i32, []),
+        "dml_gb_stage": (c_i32, [ctypes.POINTER(GbStageArgs), c_vp]),
+        "dml_gb_grad": (c_i32, [ctypes.POINTER(GbGradArgs), c_vp]),
     }
     for name, (res, args) in table.items():
         fn = getattr(lib, name, None)
         if fn is not None:
             fn.restype = res
             fn.argtypes = args
+    if getattr(lib, "dml_gb_sizeof_stage_args", None) is not None:
+        if (lib.dml_gb_sizeof_stage_args() != ctypes.sizeof(GbStageArgs)
+                or lib.dml_gb_sizeof_grad_args() != ctypes.sizeof(GbGradArgs)):
+            raise RuntimeError("GBRT stage argument layout mismatch between HIP library and Python")
     if getattr(lib, "dml_lr_sizeof_fwd_args", None) is not None:
         if (lib.dml_lr_sizeof_fwd_args() != ctypes.sizeof(LrFwdArgs)
                 or lib.dml_lr_sizeof_grad_args() != ctypes.sizeof(LrGradArgs)):

@@ -3,6 +3,8 @@
 DeviceData(binned_only=True) streams the host rows (numpy / np.memmap) in chunks through
 pinned buffers and keeps only the uint8 bins on the device; the edges come from the same
 row sample the resident path uses, so bins, trees and CV scores are identical."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -40,7 +42,21 @@ def _check(dev, n, d, chunk, tmp_path):
                         ("GradientBoostingClassifier", {"n_estimators": [5], "max_depth": [2]})):
         assert _scores(res_dd, model, grid) == _scores(bin_dd, model, grid)
     with pytest.raises(ValueError, match="binned form"):
-        run_candidates(bin_dd, JobSpec("LogisticRegression", [{"C": 1.0}], cv=3), [0])
+        run_candidates(bin_dd, JobSpec("KNeighborsClassifier", [{"n_neighbors": 3}], cv=3), [0])
+    # LogisticRegression streams the host rows once per objective evaluation (every candidate
+    # x fold of the batch per chunk); the resident comparison runs the same fp32 objective
+    lr_grid = {"C": [0.05, 1.0], "solver": ["lbfgs"], "max_iter": [200]}
+    old = os.environ.get("DML_LR_MFMA")
+    os.environ["DML_LR_MFMA"] = "0"
+    try:
+        a = _scores(res_dd, "LogisticRegression", lr_grid)
+    finally:
+        if old is None:
+            os.environ.pop("DML_LR_MFMA")
+        else:
+            os.environ["DML_LR_MFMA"] = old
+    np.testing.assert_allclose(np.asarray(_scores(bin_dd, "LogisticRegression", lr_grid)), np.asarray(a),
+                               rtol=0, atol=1e-6)
     # LinearRegression / PCA re-stream the host rows for their moments and test rows
     rng = np.random.RandomState(1)
     yr = X @ rng.randn(d).astype(np.float32) + 3.0 + 0.1 * rng.randn(n).astype(np.float32)
