@@ -169,10 +169,13 @@ struct ForestArgs {
   // -- the large tier then needs exactly ceil(d / kg_large) feature rounds per level, launched
   // without reading the "need more" flag back after each round
   int64_t all_features;
+  int64_t sub_small;   // 0 < sub_small < sub_max (<= 32): subtree roots of <= sub_small rows -> tier 4
 };
 
-constexpr int kTiers = 4;  // 0 subtree, 1 wave, 2 block, 3 large
-enum CounterSlot { kCntSets = 0 /*8*/, kPool = 8, kOverflow = 9, kNeedMore = 10, kOpenOvf = 11, kNumCounters = 16 };
+// 0 subtree, 1 wave, 2 block, 3 large, 4 small subtree (<= sub_small rows: the subtree kernel
+// with an LDS row cache of half the size, so twice as many of them fit a CU)
+constexpr int kTiers = 5;
+enum CounterSlot { kCntSets = 0 /*10*/, kPool = 10, kOverflow = 11, kNeedMore = 12, kOpenOvf = 13, kNumCounters = 16 };
 
 struct LState {
   OpenNode on;
@@ -219,6 +222,7 @@ struct Ctx {
   int32_t wave_max, block_max, chunk, kg_wave, kg_block, kg_large, slack_wave;
   int32_t sub_max, sub_cache_d;
   int32_t bigsub_max;    // > 0: tier 1 (sub_max < count <= bigsub_max) is grown by k_bigsub
+  int32_t sub_small;     // 0 < sub_small < sub_max: subtree roots of <= sub_small rows go to tier 4
   int64_t ystride;
   // row words: rows_cur/rows_next hold row | bootstrap weight << rbits | class << (rbits + 4)
   // when `packed` (the weight and label travel with the row through every partition, so
@@ -346,6 +350,12 @@ __device__ double node_weight(const Ctx& c, int node) {
   return w;
 }
 
+// the tier a node of `count` rows is grown by
+__device__ __forceinline__ int tier_of(const Ctx& c, int count) {
+  if (count <= c.sub_max) return count <= c.sub_small ? 4 : 0;
+  return count <= c.wave_max ? 1 : (count <= c.block_max ? 2 : 3);
+}
+
 // decide whether a freshly created node is worth visiting; enqueue it into `set`
 __device__ void enqueue_or_leaf(const Ctx& c, int tree, int node, int64_t start, int count, int depth,
                                 uint64_t key, int set) {
@@ -353,7 +363,7 @@ __device__ void enqueue_or_leaf(const Ctx& c, int tree, int node, int64_t start,
   if (leaf_by_counts(s, count, depth)) return;
   if (leaf_by_weight(s, node_weight(c, node))) return;
   if (node_impurity(c, node, s.criterion) <= kEps) return;
-  const int tier = count <= c.sub_max ? 0 : (count <= c.wave_max ? 1 : (count <= c.block_max ? 2 : 3));
+  const int tier = tier_of(c, count);
   const int idx = atomicAdd(&c.counters[set * kTiers + tier], 1);
   if (idx >= c.open_cap[tier]) {
     atomicOr(&c.counters[kOpenOvf], 1);
@@ -1002,7 +1012,7 @@ __device__ __forceinline__ void stage_child(const Ctx& c, const NodeSpec& s, int
   int tier = -1;
   if (!leaf_by_counts(s, count, depth) && !leaf_by_weight(s, vals_weight(vals, c.C, c.is_reg)) &&
       impure_v<FC>(c, s, vals))
-    tier = count <= c.sub_max ? 0 : (count <= c.wave_max ? 1 : (count <= c.block_max ? 2 : 3));
+    tier = tier_of(c, count);
   OpenNode on;
   on.tree = tree; on.node = node; on.start = start; on.count = count; on.depth = depth;
   on.key = key; on.pool_base = -1; on.tier = tier;
@@ -2125,11 +2135,13 @@ __device__ __forceinline__ void subtree_dfs(const Ctx& c, const NodeSpec& s, int
   }
 }
 
-template <bool REG, int FC>
-__global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
+// SR: rows the LDS layout holds (64; 32 for the small-subtree tier 4, whose roots have
+// <= sub_small <= 32 rows -- the DFS stack never holds more entries than the root has rows)
+template <bool REG, int FC, int SR = 64>
+__global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur, int tier) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   PH_BEGIN
-  const OpenNode on = c.open[set_cur][0][blockIdx.x];
+  const OpenNode on = c.open[set_cur][tier][blockIdx.x];
   const NodeSpec s = spec_of<FC>(c, on.tree);
   const int lane = threadIdx.x;
   const int d = c.d;
@@ -2139,11 +2151,11 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur) {
   // LDS: DFS stack, per-entry channel sums (no global re-reads of node stats), left
   // child sums, row-bin cache
   SubEntry* stack = (SubEntry*)smem;
-  double* sstats = (double*)(stack + 64);            // [64][VC]
-  double* left_ch = sstats + 64 * VC;                // [VC]
+  double* sstats = (double*)(stack + SR);            // [SR][VC]
+  double* left_ch = sstats + SR * VC;                // [VC]
   double* right_ch = left_ch + VC;                   // [VC] (+ pad)
   uint8_t* xc = (uint8_t*)(left_ch + ((2 * VC + 1) & ~1));
-  int32_t* cidx = (int32_t*)(xc + ((64 * c.sub_cache_d + 15) & ~15));   // [64] compaction map
+  int32_t* cidx = (int32_t*)(xc + ((SR * c.sub_cache_d + 15) & ~15));   // [64] compaction map
   const int cnt0 = on.count;
   const uint32_t* rows = c.rows_cur + on.start;
   uint32_t row = 0;
@@ -2997,7 +3009,9 @@ __global__ __launch_bounds__(256) void k_compact(Ctx c, int set, int64_t n) {
   const int64_t i0 = (int64_t)blockIdx.x * 1024 + tid * 4;
   OpenNode e[4];
   int want[4];
-  int cnt[NQ] = {0, 0, 0, 0, 0};
+  int cnt[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) cnt[q] = 0;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     want[u] = 0;
@@ -3006,7 +3020,7 @@ __global__ __launch_bounds__(256) void k_compact(Ctx c, int set, int64_t n) {
     const int t = e[u].tier;
     if (t < 0) continue;
     ++cnt[t];
-    if (t == 0 || (t == 1 && c.bigsub_max > 0)) {   // whole-subtree tiers: every pair reserved here
+    if (t == 0 || t == 4 || (t == 1 && c.bigsub_max > 0)) {   // whole-subtree tiers: every pair reserved here
       want[u] = 2 * subtree_max_splits(c.specs[e[u].tree], e[u].count, e[u].depth);
       cnt[kTiers] += want[u];
     }
@@ -3040,7 +3054,7 @@ __global__ __launch_bounds__(256) void k_compact(Ctx c, int set, int64_t n) {
 #pragma unroll
     for (int q = 0; q < kTiers; ++q)
       if (q == t) idx = off[q]++;
-    if (t == 0 || (t == 1 && c.bigsub_max > 0)) {
+    if (t == 0 || t == 4 || (t == 1 && c.bigsub_max > 0)) {
       const int pb = off[kTiers];
       off[kTiers] += want[u];
       if (want[u] > 0 && (int64_t)pb + want[u] > c.pool_cap) {
@@ -3122,6 +3136,7 @@ static Layout plan(const ForestArgs* a) {
   L.open_cap[2] = R / (a->wave_max + 1) + T + 16;
   L.open_cap[3] = R / (a->block_max + 1) + T + 16;
   L.open_cap[0] = 2 * (L.open_cap[1] + L.open_cap[2] + L.open_cap[3]) + T + 16;
+  L.open_cap[4] = L.open_cap[0];
   L.large_cap = L.open_cap[3];
   L.stage_cap = 2 * (L.open_cap[1] + L.open_cap[2]);
   (void)C;
@@ -3151,10 +3166,10 @@ static size_t fused_lds(const ForestArgs* a, int KG) {
   return fused_layout(KG, span, (int)mode_elem(mode), CH).total + 16;
 }
 
-static size_t sub_lds(const ForestArgs* a) {
+static size_t sub_lds(const ForestArgs* a, int SR = 64) {
   const int VC = a->is_reg ? 3 : (int)a->n_classes;
-  size_t b = 64 * sizeof(SubEntry) + (size_t)64 * VC * 8 + ((2 * VC + 1) & ~1) * 8;
-  b += (size_t)((64 * a->sub_cache_d + 15) & ~15) + 64 * 4 + 16;   // row-bin cache + compaction map
+  size_t b = SR * sizeof(SubEntry) + (size_t)SR * VC * 8 + ((2 * VC + 1) & ~1) * 8;
+  b += (size_t)((SR * a->sub_cache_d + 15) & ~15) + 64 * 4 + 16;   // row-bin cache + compaction map
   return b;
 }
 
@@ -3198,6 +3213,7 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.sub_max = (int)a->sub_max;
   c.sub_cache_d = (int)a->sub_cache_d;
   c.bigsub_max = 0;   // set by build_impl for the builds it applies to
+  c.sub_small = (a->sub_small > 0 && a->sub_small < a->sub_max && a->sub_small <= 32) ? (int)a->sub_small : 0;
   {
     int cbits = 0;
     if (!c.is_reg)
@@ -3379,6 +3395,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   HIP_OK(hipGetLastError());
 
   const size_t lds_s = sub_lds(a);
+  const size_t lds_s32 = sub_lds(a, 32);
   const size_t lds_w = fused_lds(a, (int)a->kg_wave);
   int32_t* h_pool = h + 48;   // pinned slot for the per-level pool reservation (H2D)
   const size_t lds_b = fused_lds(a, (int)a->kg_block);
@@ -3418,9 +3435,10 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     HIP_OK(hipStreamSynchronize(st));
     if (h[kOpenOvf]) { a->status_out = 4; break; }
     const int ns = h[cur * kTiers + 0], nw = h[cur * kTiers + 1], nb = h[cur * kTiers + 2], nL = h[cur * kTiers + 3];
-    if (ns + nw + nb + nL == 0) break;
+    const int ns4 = h[cur * kTiers + 4];
+    if (ns + ns4 + nw + nb + nL == 0) break;
     if (++levels > 1 << 20) return 8;
-    const int64_t open_now = (int64_t)ns + nw + nb + nL;
+    const int64_t open_now = (int64_t)ns + ns4 + nw + nb + nL;
     peak_open = std::max(peak_open, open_now);
     HIP_OK(hipMemsetAsync(c.counters + (1 - cur) * kTiers, 0, kTiers * 4, st));
     // reserve the child pairs of every wave/block-tier node of this level up front (a
@@ -3441,10 +3459,10 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       *h_pool = (int32_t)pool_next;
       HIP_OK(hipMemcpyAsync(c.counters + kPool, h_pool, 4, hipMemcpyHostToDevice, st));
     }
-    a->tier_nodes_out[0] += ns; a->tier_nodes_out[1] += nw; a->tier_nodes_out[2] += nb; a->tier_nodes_out[3] += nL;
+    a->tier_nodes_out[0] += ns + ns4; a->tier_nodes_out[1] += nw; a->tier_nodes_out[2] += nb; a->tier_nodes_out[3] += nL;
     SideStreams* ss = side_streams();
     static const bool serial_tiers = getenv("DML_SERIAL_TIERS") != nullptr;   // profiling: tiers one after another
-    const bool fork = !serial_tiers && ss != nullptr && ((ns > 0) + (nw > 0) + (nb > 0) + (nL > 0)) > 1;
+    const bool fork = !serial_tiers && ss != nullptr && ((ns + ns4 > 0) + (nw > 0) + (nb > 0) + (nL > 0)) > 1;
     hipStream_t s0 = st, s1 = st, s2 = st;
     if (fork) {
       HIP_OK(hipEventRecord(ss->fork, st));
@@ -3454,7 +3472,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     // block-tier children stage after the wave tier's (none under the big-subtree tier)
     const int stage_b = big ? 0 : nw;
     if (fast) {
-      if (ns) k_subtree<REG, FCX><<<ns, 64, lds_s, s0>>>(c, cur);
+      if (ns4) k_subtree<REG, FCX, 32><<<ns4, 64, lds_s32, s0>>>(c, cur, 4);
+      if (ns) k_subtree<REG, FCX><<<ns, 64, lds_s, s0>>>(c, cur, 0);
       if (nw) {
         if constexpr (MODE == 1) {
           if (big) k_bigsub<FCX><<<nw, 256, lds_big, s1>>>(c, cur);
@@ -3465,7 +3484,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       }
       if (nb) k_nodes<DML_BLOCK_NT, MODE, FCX><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
     } else {
-      if (ns) k_subtree<REG, -1><<<ns, 64, lds_s, s0>>>(c, cur);
+      if (ns4) k_subtree<REG, -1, 32><<<ns4, 64, lds_s32, s0>>>(c, cur, 4);
+      if (ns) k_subtree<REG, -1><<<ns, 64, lds_s, s0>>>(c, cur, 0);
       if (nw) {
         if constexpr (MODE == 1) {
           if (big) k_bigsub<-1><<<nw, 256, lds_big, s1>>>(c, cur);

@@ -35,6 +35,7 @@ class ForestTiers:
     """Node-size tiers of the HIP builder (see forest.hip header)."""
 
     sub_max: int = 64          # <= 64 rows: one wave finishes the whole subtree (k_subtree)
+    sub_small: int = 32        # subtree roots of <= 32 rows: tier 4, half-size LDS row cache (2x per CU)
     sub_cache_max_d: int = 256  # cache the subtree's bin rows in LDS when d <= this
     wave_max: int = 512         # sweeps: profiles/r1_forest_ab_experiments.md, r2_tier_sweep.txt
     block_max: int = 32768      # r2 kernels (XbT large tier): 32768 beats 131072 by 4 %
@@ -54,6 +55,10 @@ class ForestTiers:
         """Clamp feature-group sizes to the LDS budget for this channel count."""
         per_feat = n_channels * 256 * 4
         t = ForestTiers(**self.__dict__)
+        for k in t.__dict__:   # experiments: DML_TIER_<FIELD>=<int> overrides a field
+            env = os.environ.get("DML_TIER_" + k.upper())
+            if env:
+                setattr(t, k, int(env))
         t.kg_wave = max(1, min(self.kg_wave, (24 * 1024) // per_feat, 4))     # k_nodes<64>: KGMAX 4
         t.kg_block = max(1, min(self.kg_block, (96 * 1024) // per_feat, 16))  # k_nodes<256>: KGMAX 16
         t.kg_large = max(1, min(self.kg_large, (96 * 1024) // per_feat, 64))
@@ -206,6 +211,7 @@ def workspace_bytes(rows_total: int, T: int, d: int, n_classes: int, is_reg: boo
     a.rows_total = int(rows_total)
     a.wave_max, a.block_max, a.chunk = t.wave_max, t.block_max, t.chunk
     a.kg_wave, a.kg_block, a.kg_large, a.slack_wave, a.sub_max = t.kg_wave, t.kg_block, t.kg_large, t.slack_wave, t.sub_max
+    a.sub_small = t.sub_small
     if _bigsub_on(t, is_reg, n_classes, d, None):   # the smaller tier 1 has more block-tier nodes
         a.wave_max = min(t.wave_max, t.bigsub_max)
     return int(native.hip_lib().dml_forest_workspace_bytes(ctypes.byref(a)))
@@ -303,6 +309,12 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     # one criterion, no class weights / monotonic constraints / min_weight_fraction_leaf: the
     # HIP node kernels specialised on that criterion run (forest.hip spec_of / specialise)
     crits = np.unique(specs["criterion"]) if T else np.zeros(0)
+    if (T and set(crits.tolist()) <= {MSE, FRIEDMAN} and FRIEDMAN in crits
+            and not np.any(specs["min_impurity_decrease"] > 0)):
+        # friedman_mse ranks splits exactly like squared_error (forest_common.h); only the
+        # min_impurity_decrease test differs, and with none set the squared-error kernels grow
+        # the same trees (gradient boosting's default criterion)
+        crits = np.array([MSE])
     a.fast_crit = (int(crits[0]) + 1 if len(crits) == 1 and cw_dev is None and mono_dev is None
                    and not np.any(specs["min_weight_frac"] > 0) else 0)
     a.active_count = native.ptr(active)
@@ -322,6 +334,7 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     a.wave_max, a.block_max, a.chunk = tiers.wave_max, tiers.block_max, tiers.chunk
     a.kg_wave, a.kg_block, a.kg_large, a.slack_wave = tiers.kg_wave, tiers.kg_block, tiers.kg_large, tiers.slack_wave
     a.sub_max = tiers.sub_max
+    a.sub_small = tiers.sub_small
     a.sub_cache_d = _sub_cache_stride(d) if d <= tiers.sub_cache_max_d else 0
     a.all_features = int(T > 0 and bool(np.all(specs["max_features"] >= d)))
     big = _bigsub_on(tiers, is_reg, n_classes, d, mono_dev) and a.sub_cache_d > 0

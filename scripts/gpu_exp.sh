@@ -60,7 +60,7 @@ case "$kind" in
   scaling) timeout -k 10 600 python -u scripts/scaling_sim.py --world 2,4,8 --steps 2 > gpurun_out/exp_scaling.log 2>&1 && cat gpurun_out/exp_scaling.log ;;
   gbrt)    timeout -k 10 600 python -u scripts/bench_configs.py --configs 6 > gpurun_out/exp_gbrt.log 2>&1 && tail -1 gpurun_out/exp_gbrt.log | cut -c1-300 && \
            timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/exp_gbrt_prof -o run -- python3 scripts/bench_configs.py --configs 6 > gpurun_out/exp_gbrt_prof.log 2>&1 && \
-           python scripts/timeline.py gpurun_out/exp_gbrt_prof > gpurun_out/exp_gbrt_busy.txt && rm -f gpurun_out/exp_gbrt_prof/*kernel_trace.csv && head -3 gpurun_out/exp_gbrt_busy.txt ;;
+           python scripts/timeline.py gpurun_out/exp_gbrt_prof k_count_active > gpurun_out/exp_gbrt_busy.txt && rm -f gpurun_out/exp_gbrt_prof/*kernel_trace.csv && head -3 gpurun_out/exp_gbrt_busy.txt ;;
   cluster) timeout -k 10 300 $PYT tests/test_rccl_gpu.py > gpurun_out/exp_rccl_test.log 2>&1 && tail -1 gpurun_out/exp_rccl_test.log && \
            DML_FORCE_PG=1 MASTER_PORT=29602 timeout -k 10 600 python -u scripts/bench_configs.py --configs 5 > gpurun_out/exp_cfg5_dist.log 2>&1 && tail -1 gpurun_out/exp_cfg5_dist.log | cut -c1-300 && \
            DML_FORCE_PG=1 MASTER_PORT=29601 timeout -k 10 900 python -u bench.py --e2e > gpurun_out/exp_e2e_dist.log 2>&1 && tail -1 gpurun_out/exp_e2e_dist.log | cut -c1-300 ;;

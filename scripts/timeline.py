@@ -7,9 +7,12 @@ for f in glob.glob(f"{sys.argv[1]}/**/*kernel_trace.csv", recursive=True):
 iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
 if not iv:
     sys.exit("no kernel trace")
-t_start = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0   # skip the first fraction (warmup)
+arg = sys.argv[2] if len(sys.argv) > 2 else "0"
 span0, span1 = iv[0][0], max(e for _, e, _ in iv)
-cut = span0 + (span1 - span0) * t_start
+try:   # skip the first fraction of the span (warmup) ...
+    cut = span0 + (span1 - span0) * float(arg)
+except ValueError:   # ... or start at the first kernel whose name contains the argument
+    cut = min(s for s, _, n in iv if arg in n)
 iv = [x for x in iv if x[0] >= cut]
 busy, cs, ce = 0, None, None
 for s, e, _ in iv:
