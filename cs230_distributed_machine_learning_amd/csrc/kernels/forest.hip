@@ -362,7 +362,8 @@ __device__ void enqueue_or_leaf(const Ctx& c, int tree, int node, int64_t start,
   const NodeSpec s = spec_of<-1>(c, tree);
   if (leaf_by_counts(s, count, depth)) return;
   if (leaf_by_weight(s, node_weight(c, node))) return;
-  if (node_impurity(c, node, s.criterion) <= kEps) return;
+  if (c.is_reg ? reg_pure(c.node_val + (int64_t)node * c.VC, c.rq) : node_impurity(c, node, s.criterion) <= kEps)
+    return;
   const int tier = tier_of(c, count);
   const int idx = atomicAdd(&c.counters[set * kTiers + tier], 1);
   if (idx >= c.open_cap[tier]) {
@@ -1002,6 +1003,7 @@ template <int FC>
 __device__ __forceinline__ bool impure_v(const Ctx& c, const NodeSpec& s, const double* v) {
   if constexpr (FC == kGini)
     if (c.C == 2) return v[0] > 0.0 && v[1] > 0.0;
+  if (c.is_reg) return !reg_pure(v, c.rq);
   return impurity_of_vals(c, v, s.criterion) > kEps;
 }
 

@@ -237,7 +237,7 @@ DML_HD double cls_proxy(const ClsAcc& l, const ClsAcc& r, int crit) {
 // Regression histograms (both builders, every tier) accumulate per bin, in 64-bit INTEGER
 // arithmetic: sum w and the row count packed as (w | rows << 32), sum w*yq and sum w*y2q,
 // with yq = rint(y 2^e1), y2q = rint(y^2 2^e2).  e1 / e2 are chosen per build (host side,
-// `reg_exponents`) so that no sum over a tree's rows can exceed 2^62 in magnitude.
+// `reg_exponents_counts`) so that no sum over a tree's rows can exceed 2^62 in magnitude.
 // Integer sums are exact in ANY order: GPU atomics no longer make a regression tree
 // depend on arrival order, and the C++ builder, doing the same integer sums, grows the
 // identical tree (sklearn accumulates these sums in float64; the fixed-point grid is
@@ -256,16 +256,31 @@ DML_HD RegScale reg_scale(int e1, int e2) {
   return q;
 }
 
-// exponents of a build: every |sum| <= 15 n max|y| 2^e1 < 2^61 (bootstrap weights <= 15),
-// likewise y^2 for e2 (ops/forest_ops.py `reg_exponents` mirrors this rule exactly)
-DML_HD void reg_exponents(double max_abs_y, int64_t n, int& e1, int& e2) {
+// exponents of a build from the per-target histogram of the targets' frexp exponents
+// (cnt[t][k + kExpOff] rows with |y| in [2^(k-1), 2^k), bucket 0 the zeros):
+// B1 = max_t sum_k c 2^k >= sum|y|, B2 likewise with 4^k >= sum y^2, summed sequentially
+// in bucket order (every term exact); e1 = 61 - exponent(15 B1) so any bootstrap-weighted
+// (w <= 15) sum over a tree's rows stays below 2^61, e2 the same from B2.  The y^2 grid
+// follows the target's total energy, not n max|y|^2 (a node of small targets beside one
+// outlier keeps its variance).  ops/forest_ops.py `reg_exponents_of_counts` is this rule.
+constexpr int kExpOff = 160, kExpBins = 320;
+
+inline void reg_exponents_counts(const int64_t* cnt, int64_t targets, int& e1, int& e2) {
+  double b1 = 0.0, b2 = 0.0;
+  for (int64_t t = 0; t < targets; ++t) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int j = 1; j < kExpBins; ++j) {
+      const double c = (double)cnt[t * kExpBins + j];
+      s1 += c * ldexp(1.0, j - kExpOff);
+      s2 += c * ldexp(1.0, 2 * (j - kExpOff));
+    }
+    b1 = s1 > b1 ? s1 : b1;
+    b2 = s2 > b2 ? s2 : b2;
+  }
+  int k;
   e1 = 0; e2 = 0;
-  if (!(max_abs_y > 0.0) || n <= 0) return;
-  int kw, k;
-  frexp(15.0 * (double)n, &kw);   // 15 n < 2^kw
-  frexp(max_abs_y, &k);           // max|y| < 2^k
-  e1 = 61 - kw - k;
-  e2 = 61 - kw - 2 * k;
+  if (b1 > 0.0) { frexp(15.0 * b1, &k); e1 = 61 - k; }
+  if (b2 > 0.0) { frexp(15.0 * b2, &k); e2 = 61 - k; }
   e1 = e1 < -1000 ? -1000 : (e1 > 1000 ? 1000 : e1);
   e2 = e2 < -1000 ? -1000 : (e2 > 1000 ? 1000 : e2);
 }
@@ -324,6 +339,20 @@ DML_HD double improvement(double W_tree, double W_node, double imp_node, double 
 }
 
 constexpr double kEps = 1e-7;  // sklearn EPSILON for purity / min_impurity_decrease tests
+
+// regression purity.  sklearn stops at impurity <= DBL_EPSILON on float64 sums; ours is
+// formed from the fixed-point sums, whose rounding bounds the impurity a constant target
+// can compute: |S2/W err| <= 2^-e2 / 2, |mean err| <= 2^-e1 / 2, so |imp err| <= 2^-e2 / 2 +
+// |mean| 2^-e1 + 2^-2e1 / 4, plus a few ulps of S2/W.  A node is pure below that bound:
+// nodes of tiny but real variance (small targets, late boosting residuals) keep splitting
+// as in sklearn, where the old absolute 1e-7 made them leaves.
+constexpr double kDblEps = 2.220446049250313e-16;
+DML_HD bool reg_pure(const double* v, const RegScale& q) {
+  if (!(v[0] > 0.0)) return true;
+  const double m = v[1] / v[0];
+  const double tol = 0.5 * q.i2 + fabs(m) * q.i1 + q.i1 * q.i1 + 8.0 * kDblEps * fabs(v[2] / v[0]);
+  return mse_impurity(v[0], v[1], v[2]) <= (tol > kDblEps ? tol : kDblEps);
+}
 
 // the improvement the min_impurity_decrease test reads: sklearn's impurity_improvement(),
 // or for friedman_mse FriedmanMSE.impurity_improvement = (w_r s_l - w_l s_r)^2 /

@@ -105,9 +105,10 @@ DML_HD double dp_impurity(const double* v, int C, int is_reg, int crit) {
 }
 
 // the builders' "grow this node?" rule (forest_cpu.cpp visit())
-DML_HD bool dp_visit(const TreeSpec& t, double count, int depth, const double* v, int C, int is_reg) {
+DML_HD bool dp_visit(const TreeSpec& t, double count, int depth, const double* v, int C, int is_reg,
+                     const RegScale& q) {
   return !(leaf_by_counts(t, (int)count, depth) || leaf_by_weight(t, vals_weight(v, C, is_reg)) ||
-           dp_impurity(v, C, is_reg, t.criterion) <= kEps);
+           (is_reg ? reg_pure(v, q) : dp_impurity(v, C, is_reg, t.criterion) <= kEps));
 }
 
 // Root of tree ``t`` from its all-reduced statistics: class weights (balanced_subsample
@@ -150,7 +151,7 @@ DML_HD int dp_root_one(const DpArgs& a, int t, DpSlot* slot) {
   slot->best_feat = slot->best_bin = -1;
   slot->done = slot->split = 0;
   slot->child = -1;
-  return (count > 0.0 && dp_visit(s, count, 0, v, C, (int)a.is_reg)) ? 1 : 0;
+  return (count > 0.0 && dp_visit(s, count, 0, v, C, (int)a.is_reg, reg_scale((int)a.yq_e1, (int)a.yq_e2))) ? 1 : 0;
 }
 
 // class weight vector of a tree (null = all ones)
@@ -319,7 +320,8 @@ DML_HDM void dp_children_one(const DpArgs& a, int i) {
     c.done = c.split = 0;
     c.child = -1;
     nx[side] = c;
-    op[side] = dp_visit(s, c.count, c.depth, side == 0 ? lv : rv, C, (int)a.is_reg) ? 1 : 0;
+    op[side] = dp_visit(s, c.count, c.depth, side == 0 ? lv : rv, C, (int)a.is_reg,
+                          reg_scale((int)a.yq_e1, (int)a.yq_e2)) ? 1 : 0;
   }
 }
 

@@ -161,7 +161,8 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
   std::vector<double> nlo(1, -INFINITY), nhi(1, INFINITY);   // (helpers: forest_common.h)
   auto node_imp = [&](int node, const double* v) { return mae ? nabs[node] / v[0] : impurity_of(v); };
   auto visit = [&](int count, int depth, const double* v, double imp) {
-    return !(leaf_by_counts(s, count, depth) || leaf_by_weight(s, vals_weight(v, D.C, D.is_reg)) || imp <= kEps);
+    const bool pure = (D.is_reg && !mae) ? reg_pure(v, D.rq) : imp <= kEps;
+    return !(leaf_by_counts(s, count, depth) || leaf_by_weight(s, vals_weight(v, D.C, D.is_reg)) || pure);
   };
 
   std::vector<Job> stack;
@@ -421,21 +422,26 @@ void* dml_cpu_forest_build(const uint8_t* Xb, int64_t ld, int64_t n, int64_t d, 
                            const TreeSpec* specs, int64_t T, int64_t ystride, const double* cw) {
   int e1 = 0, e2 = 0;
   if (is_reg) {   // exponents from the data (entry point of the host self-test)
-    double m = 0.0;
     int64_t targets = 1;
     if (ystride > 0)
       for (int64_t t = 0; t < T; ++t) targets = std::max<int64_t>(targets, (int64_t)specs[t].target + 1);
-    const int64_t len = ystride > 0 ? (targets - 1) * ystride + n : n;
-    for (int64_t i = 0; i < len; ++i) m = std::max(m, fabs((double)yreg[i]));
-    reg_exponents(m, n, e1, e2);
+    std::vector<int64_t> cnt((size_t)targets * kExpBins, 0);
+    for (int64_t t = 0; t < targets; ++t)
+      for (int64_t i = 0; i < n; ++i) {
+        const float y = yreg[(ystride > 0 ? t * ystride : 0) + i];
+        int k = 0;
+        if (y != 0.0f) frexp((double)y, &k);
+        cnt[(size_t)t * kExpBins + (y != 0.0f ? k + kExpOff : 0)]++;
+      }
+    reg_exponents_counts(cnt.data(), targets, e1, e2);
   }
   return dml_cpu_forest_build_mono(Xb, ld, n, d, ycls, yreg, n_classes, is_reg, roles, specs, T, ystride, cw,
                                    nullptr, e1, e2);
 }
 
-void dml_reg_exponents(double max_abs_y, int64_t n, int32_t* out) {
+void dml_reg_exponents(const int64_t* cnt, int64_t targets, int32_t* out) {
   int e1, e2;
-  reg_exponents(max_abs_y, n, e1, e2);
+  reg_exponents_counts(cnt, targets, e1, e2);
   out[0] = e1; out[1] = e2;
 }
 

@@ -38,7 +38,7 @@ import numpy as np
 import torch
 
 from ..utils import native, trace
-from .forest_ops import reg_exponents_of, ForestBuild
+from .forest_ops import reg_exponent_counts, reg_exponents_of_counts, _n_targets, ForestBuild
 
 SLOT_BYTES = 64
 # int32 column of each DpSlot field (forest_dp.h): key 0-1, best_gain 2-3, count 4-5
@@ -126,12 +126,12 @@ def _build_chunk(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[
     stats = {"levels": 0, "rounds": 0, "allreduce_bytes": 0, "hist_s": 0.0, "reduce_s": 0.0}
 
     if is_reg:
-        # the fixed-point exponents of the ONE-GPU build of the whole table: max|y| and
-        # the row count over every rank (forest_common.h reg_exponents)
-        mt = torch.tensor([float(yreg.abs().max()) if yreg.numel() else 0.0, float(n)], dtype=torch.float64,
-                          device=dev)
-        m_all, n_all = reduce(mt[:1].clone(), "max"), reduce(mt[1:].clone(), "sum")
-        a.yq_e1, a.yq_e2 = reg_exponents_of(float(m_all[0]), int(n_all[0]))
+        # the fixed-point exponents of the ONE-GPU build of the whole table: the targets'
+        # exponent histograms summed over every rank (exact counts, forest_common.h
+        # reg_exponents_counts)
+        targets = _n_targets(specs, ystride)
+        cnt = reg_exponent_counts(yreg, n, ystride, targets).to(torch.float64)
+        a.yq_e1, a.yq_e2 = reg_exponents_of_counts(reduce(cnt.reshape(-1).clone(), "sum").round().to(torch.int64))
     # ---- roots: local bootstrap statistics, summed over the ranks ----------------------
     wts = torch.empty((T, n), dtype=torch.uint8, device=dev)
     a.wts = _p(wts)

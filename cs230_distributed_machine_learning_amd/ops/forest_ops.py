@@ -233,30 +233,72 @@ def _carve(buf: torch.Tensor, off: int, shape, dtype) -> torch.Tensor:
     return buf[off:off + n].view(dtype).view(*shape)
 
 
-def reg_exponents(yreg, n: int) -> tuple[int, int]:
-    """Fixed-point exponents (e1, e2) of a regression build: forest_common.h
-    ``reg_exponents`` on max|y| over the whole target array, so the HIP and the C++
-    builders quantise identically (checked against the C rule in the tests)."""
+EXP_OFF, EXP_BINS = 160, 320   # bucket k + EXP_OFF of a target's frexp exponent k (|y| < 2^k)
+
+
+def reg_exponent_counts(yreg, n: int, ystride: int = 0, targets: int = 1):
+    """Per-target histogram of the frexp exponents of the nonzero targets: int64
+    [targets, EXP_BINS] (a torch tensor on ``yreg``'s device, or numpy).  Counts are exact
+    and order-free, so every builder -- and every rank of a row-sharded build, after a sum
+    all-reduce -- derives the same exponents from them (``reg_exponents_of_counts``).
+    ``ystride > 0``: target t is ``yreg[t * ystride : t * ystride + n]``."""
+    targets = max(1, int(targets)) if ystride > 0 else 1
+    if torch.is_tensor(yreg):
+        y = yreg.reshape(-1)
+        rows = y[: (targets - 1) * ystride + n].as_strided((targets, n), (ystride, 1)) if ystride > 0 else y[:n][None]
+        if not bool(torch.isfinite(rows).all()):
+            raise ValueError("regression target contains NaN or infinity")
+        k = torch.frexp(rows.float())[1].to(torch.int64) + EXP_OFF
+        k = torch.where(rows != 0, k, torch.zeros_like(k))          # bucket 0: zeros (never a float32 exponent)
+        k += torch.arange(targets, device=k.device, dtype=torch.int64)[:, None] * EXP_BINS
+        cnt = torch.zeros(targets * EXP_BINS, dtype=torch.int64, device=k.device)
+        cnt.scatter_add_(0, k.reshape(-1), torch.ones_like(k).reshape(-1))
+        return cnt.view(targets, EXP_BINS)
+    y = np.asarray(yreg, dtype=np.float32).reshape(-1)
+    rows = (np.lib.stride_tricks.as_strided(y, (targets, n), (ystride * 4, 4)) if ystride > 0 else y[None, :n])
+    if not np.isfinite(rows).all():
+        raise ValueError("regression target contains NaN or infinity")
+    k = np.frexp(rows)[1].astype(np.int64) + EXP_OFF
+    k[rows == 0] = 0
+    cnt = np.zeros((targets, EXP_BINS), dtype=np.int64)
+    for t in range(targets):
+        cnt[t] = np.bincount(k[t], minlength=EXP_BINS)
+    return cnt
+
+
+def reg_exponents_of_counts(cnt) -> tuple[int, int]:
+    """The fixed-point rule (forest_common.h ``reg_exponents_counts`` is the same loop):
+    B1 = max over targets of sum_k c_k 2^k >= sum |y|, B2 likewise with 4^k >= sum y^2;
+    e1 = 61 - ceil-exponent(15 B1), e2 from 15 B2 -- so any bootstrap-weighted (w <= 15)
+    sum over a tree's rows stays below 2^61 in magnitude.  The y^2 grid is therefore set
+    by the target's total energy, not by n max|y|^2: a node of small targets next to a few
+    huge ones keeps its variance (review finding: one outlier used to zero every small
+    node's y^2 and turn it into a pure leaf).  Exact counts summed in fixed k order: the
+    HIP, the C++ and the row-sharded builders agree bit for bit."""
+    c = np.asarray(cnt.cpu() if torch.is_tensor(cnt) else cnt, dtype=np.int64).reshape(-1, EXP_BINS)
+    k = np.arange(EXP_BINS, dtype=np.float64) - EXP_OFF
+    c = c.astype(np.float64)
+    c[:, 0] = 0.0                                   # bucket 0 holds the zeros
+    # cumsum is a strictly sequential float64 sum in bucket order (the C loop's order);
+    # every term c_k 2^k is exact
+    b1 = float(np.cumsum(c * np.ldexp(1.0, k.astype(np.int64)), axis=1)[:, -1].max())
+    b2 = float(np.cumsum(c * np.ldexp(1.0, 2 * k.astype(np.int64)), axis=1)[:, -1].max())
+    clamp = lambda e: max(-1000, min(1000, e))
+    e1 = clamp(61 - math.frexp(15.0 * b1)[1]) if b1 > 0 else 0
+    e2 = clamp(61 - math.frexp(15.0 * b2)[1]) if b2 > 0 else 0
+    return e1, e2
+
+
+def reg_exponents(yreg, n: int, ystride: int = 0, targets: int = 1) -> tuple[int, int]:
+    """Fixed-point exponents (e1, e2) of a regression build (``reg_exponents_of_counts``
+    of the targets' exponent histogram)."""
     if yreg is None or n <= 0:
         return 0, 0
-    if torch.is_tensor(yreg):
-        m = float(yreg.abs().max()) if yreg.numel() else 0.0
-    else:
-        a = np.asarray(yreg, dtype=np.float32)
-        m = float(np.abs(a).max()) if a.size else 0.0
-    return reg_exponents_of(m, n)
+    return reg_exponents_of_counts(reg_exponent_counts(yreg, n, ystride, targets))
 
 
-def reg_exponents_of(max_abs_y: float, n: int) -> tuple[int, int]:
-    """The exponent rule itself (forest_common.h ``reg_exponents``): every integer sum
-    over a tree's rows stays below 2^61 in magnitude (weights <= 15, n rows)."""
-    if not math.isfinite(max_abs_y):
-        raise ValueError("regression target contains NaN or infinity")
-    if max_abs_y <= 0.0 or n <= 0:
-        return 0, 0
-    kw, k = math.frexp(15.0 * n)[1], math.frexp(max_abs_y)[1]
-    clamp = lambda e: max(-1000, min(1000, e))
-    return clamp(61 - kw - k), clamp(61 - kw - 2 * k)
+def _n_targets(specs: np.ndarray, ystride: int) -> int:
+    return int(specs["target"].max()) + 1 if ystride > 0 and len(specs) else 1
 
 
 def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,
@@ -287,7 +329,7 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     a.ycls = native.ptr(ycls) if ycls is not None else 0
     a.yreg = native.ptr(yreg) if yreg is not None else 0
     a.n_classes, a.is_reg = (n_classes if not is_reg else 1), int(is_reg)
-    a.yq_e1, a.yq_e2 = reg_exponents(yreg, n) if is_reg else (0, 0)
+    a.yq_e1, a.yq_e2 = reg_exponents(yreg, n, ystride, _n_targets(specs, ystride)) if is_reg else (0, 0)
     a.roles, a.n_splits = native.ptr(roles), roles.shape[0]
     a.specs, a.T = native.ptr(specs_dev), T
     a.ystride = int(ystride)
@@ -455,7 +497,7 @@ def build_cpu(Xb: np.ndarray, ycls: Optional[np.ndarray], yreg: Optional[np.ndar
     t0 = time.perf_counter()
     cw = None if (cw is None or is_reg) else np.ascontiguousarray(cw, dtype=np.float64).reshape(T, n_classes)
     mono = None if mono is None else np.ascontiguousarray(mono, dtype=np.int8)
-    e1, e2 = reg_exponents(yreg, n) if is_reg else (0, 0)
+    e1, e2 = reg_exponents(yreg, n, ystride, _n_targets(specs, ystride)) if is_reg else (0, 0)
     h = lib.dml_cpu_forest_build_mono(native.ptr(Xb), d, n, d, native.ptr(ycls), native.ptr(yreg),
                                       (1 if is_reg else n_classes), int(is_reg), native.ptr(roles), native.ptr(specs),
                                       T, int(ystride), native.ptr(cw), native.ptr(mono), e1, e2)

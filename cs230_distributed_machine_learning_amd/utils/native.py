@@ -122,7 +122,7 @@ def cpu_lib() -> ctypes.CDLL:
             lib.dml_cpu_forest_build_mono.restype = c_vp
             lib.dml_cpu_forest_build_mono.argtypes = [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
                                                       c_i64, c_i64, c_vp, c_vp, c_i64, c_i64]
-            lib.dml_reg_exponents.argtypes = [ctypes.c_double, c_i64, c_vp]
+            lib.dml_reg_exponents.argtypes = [c_vp, c_i64, c_vp]
             lib.dml_cpu_forest_apply.argtypes = [c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp]
             lib.dml_cpu_forest_refine.argtypes = [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp]
             lib.dml_cpu_forest_prune.argtypes = [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp]
