@@ -864,14 +864,31 @@ def streamed_split_moments(data, splits: List[int]) -> Tuple[torch.Tensor, torch
 def streamed_test_rows(data, split: int, fn):
     """fn(X test rows of the chunk as float64) for every chunk of a binned-only table, the
     results concatenated in test-row order (``data.test_rows[split]`` is ascending)."""
+    return streamed_test_many(data, [(split, fn)])[0]
+
+
+def streamed_test_many(data, jobs):
+    """``streamed_test_rows`` for many (split, fn) jobs in ONE pass over the host rows (a
+    grid's tasks share the pass instead of re-streaming the table once per task)."""
     from ..search.cv import ROLE_TEST
 
-    parts = []
+    parts = [[] for _ in jobs]
+    splits = sorted({sp for sp, _ in jobs})
     for r0, r1, Xc in data.stream_rows(_stream_chunk(data)):
-        m = data.roles[split, r0:r1] == ROLE_TEST
-        if bool(m.any()):
-            parts.append(fn(Xc[m].double()))
-    return torch.cat(parts) if parts else None
+        Xd = None
+        masks = {}
+        for sp in splits:
+            m = data.roles[sp, r0:r1] == ROLE_TEST
+            if bool(m.any()):
+                masks[sp] = m
+        if not masks:
+            continue
+        Xd = Xc.double()
+        rows = {sp: Xd[m] for sp, m in masks.items()}
+        for i, (sp, fn) in enumerate(jobs):
+            if sp in rows:
+                parts[i].append(fn(rows[sp]))
+    return [torch.cat(p) if p else None for p in parts]
 
 
 class LinearRegressionFamily(Family):
@@ -901,7 +918,15 @@ class LinearRegressionFamily(Family):
                 and os.environ.get("DML_LINREG_KERNEL", "1") != "0"):
             cache = self._solve_from_moments(data, tasks)
         outs = []
-        for t in tasks:
+        preds: Dict[int, torch.Tensor] = {}
+        if streamed:   # every task's test predictions from one more pass over the host rows
+            keys = [(t.split, t.params["fit_intercept"], bool(t.params.get("positive", False))) for t in tasks]
+            uniq = sorted(set(keys), key=keys.index)
+            res = streamed_test_many(data, [(k[0], lambda Xt, w=cache[k][0], b0=cache[k][1]: (Xt @ w + b0).float())
+                                            for k in uniq])
+            byk = dict(zip(uniq, res))
+            preds = {i: byk[k] for i, k in enumerate(keys)}
+        for ti, t in enumerate(tasks):
             pos = bool(t.params.get("positive", False))
             key = (t.split, t.params["fit_intercept"], pos)
             if key not in cache:
@@ -922,7 +947,7 @@ class LinearRegressionFamily(Family):
                     cache[key] = (w, b0)
             w, b0 = cache[key]
             if streamed:
-                pred = streamed_test_rows(data, t.split, lambda Xt, w=w, b0=b0: (Xt @ w + b0).float())
+                pred = preds[ti]
                 if pred is None:
                     pred = torch.zeros(0, dtype=torch.float32, device=data.device)
             else:

@@ -126,6 +126,23 @@ class PCAFamily(Family):
                 dm = Sx / cnt.clamp_min(1)
                 fused[sp] = (shift[:d] + dm, (XX - cnt * torch.outer(dm, dm)) / max(1.0, float(cnt) - 1), int(cnt))
         sharded = getattr(data, "is_row_shard", False)
+        if streamed:
+            # every split's eigenbasis first, then all test projections in ONE pass over the rows
+            from .linear import streamed_test_many
+
+            basis = {}
+            for sp in sorted({t.split for t in tasks}):
+                mean, cov, n = fused[sp]
+                lam, V = torch.linalg.eigh(cov)
+                basis[sp] = (mean, lam.flip(0).clamp_min(0), V.flip(1), n)
+            sps = list(basis)
+            Zs = streamed_test_many(data, [(sp, lambda Xt, mean=basis[sp][0], V=basis[sp][2]: (Xt - mean) @ V)
+                                           for sp in sps])
+            for sp, Z in zip(sps, Zs):
+                mean, lam, V, n = basis[sp]
+                if Z is None:
+                    Z = torch.zeros((0, d), dtype=torch.float64, device=data.device)
+                eig[sp] = (mean, lam, V, Z, n)
         for t in tasks:
             if t.split not in eig:
                 if t.split in fused:
