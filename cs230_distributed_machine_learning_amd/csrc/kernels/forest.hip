@@ -185,6 +185,10 @@ struct LState {
   int32_t best_pos; // visiting position of the best split's feature
   int32_t scr_n;    // positions [0, scr_n) have their bins in Ctx::bscr (round 0, <= 16 features)
   double best_mid;  // monotonic_cst: middle value of the best split
+  // whole-histogram levels (Ctx::full_cur): features [0, scr_id) -- by feature id -- have their
+  // bins in bscr; derive: the histogram is parent - sibling (no row pass), par / sib the
+  // parent's large slot one level up and the sibling's slot at this level
+  int32_t scr_id, derive, par, sib;
 };
 
 struct Ctx {
@@ -218,6 +222,18 @@ struct Ctx {
   double* lbest_left;    // [cap_large][CH]
   void* ghist;           // [cap_large][kg_large][CH][256] (u32 or f32)
   int32_t* lcursor;      // [cap_large][2]
+  // whole-histogram large levels (every tree evaluates every feature and the level's
+  // histograms fit the budget): each large node's histogram over ALL d features,
+  // [slot][d][global planes][256], is kept for the next level, where the larger of two
+  // large-tier siblings takes parent - smaller sibling instead of a pass over its rows.
+  // gf_cur / gf_prev: this level's and the previous level's buffers; pinfo_cur[slot] =
+  // {parent slot, sibling slot, derive?} as written by the previous level's k_split_large,
+  // pinfo_next the same for the next level
+  void* gf_cur;
+  const void* gf_prev;
+  const int4* pinfo_cur;
+  int4* pinfo_next;
+  int32_t full_cur, full_prev;
   int64_t large_cap;
   int32_t wave_max, block_max, chunk, kg_wave, kg_block, kg_large, slack_wave;
   int32_t sub_max, sub_cache_d;
@@ -357,23 +373,25 @@ __device__ __forceinline__ int tier_of(const Ctx& c, int count) {
 }
 
 // decide whether a freshly created node is worth visiting; enqueue it into `set`
-__device__ void enqueue_or_leaf(const Ctx& c, int tree, int node, int64_t start, int count, int depth,
-                                uint64_t key, int set) {
+// (returns the node's index in the next level's large-tier list, else -1)
+__device__ int enqueue_or_leaf(const Ctx& c, int tree, int node, int64_t start, int count, int depth,
+                               uint64_t key, int set) {
   const NodeSpec s = spec_of<-1>(c, tree);
-  if (leaf_by_counts(s, count, depth)) return;
-  if (leaf_by_weight(s, node_weight(c, node))) return;
+  if (leaf_by_counts(s, count, depth)) return -1;
+  if (leaf_by_weight(s, node_weight(c, node))) return -1;
   if (c.is_reg ? reg_pure(c.node_val + (int64_t)node * c.VC, c.rq) : node_impurity(c, node, s.criterion) <= kEps)
-    return;
+    return -1;
   const int tier = tier_of(c, count);
   const int idx = atomicAdd(&c.counters[set * kTiers + tier], 1);
   if (idx >= c.open_cap[tier]) {
     atomicOr(&c.counters[kOpenOvf], 1);
-    return;
+    return -1;
   }
   OpenNode on;
   on.tree = tree; on.node = node; on.start = start; on.count = count; on.depth = depth;
   on.key = key; on.pool_base = -1; on.tier = tier;
   c.open[set][tier][idx] = on;
+  return tier == 3 ? idx : -1;
 }
 
 // node pairs a subtree-tier node reserves: a subtree over cnt0 rows has at most
@@ -2624,6 +2642,18 @@ __global__ __launch_bounds__(64) void k_large_prep(Ctx c, int set_cur, int nL) {
   st.best_mid = 0.0;
   st.best_pos = 1 << 30;
   st.scr_n = st.g <= 16 ? st.g : 0;
+  st.scr_id = 0; st.derive = 0; st.par = -1; st.sib = -1;
+  if (c.full_cur) {
+    // whole-histogram level: round r's row pass covers features [r kg, (r + 1) kg) by id, so
+    // bscr holds features [0, g0) (not visiting positions); a larger sibling is derived
+    st.scr_n = 0;
+    const int g0 = min(c.kg_large, c.d);
+    if (c.full_prev) {
+      const int4 pi = c.pinfo_cur[slot];
+      if (pi.x >= 0) { st.par = pi.x; st.sib = pi.y; st.derive = pi.z; }
+    }
+    st.scr_id = (!st.derive && g0 <= 16) ? g0 : 0;
+  }
   c.lstate[slot] = st;
   c.lcursor[2 * slot] = 0;
   c.lcursor[2 * slot + 1] = 0;
@@ -2634,26 +2664,29 @@ __device__ __forceinline__ uint32_t large_bin(const Ctx& c, uint32_t wd, int f) 
   return c.XbT ? (uint32_t)c.XbT[(int64_t)f * c.n + row] : (uint32_t)c.Xb[(int64_t)row * c.ld + f];
 }
 
+// fround >= 0 (whole-histogram level): the round's features are [fround kg, ...) by id and
+// the histogram goes to the node's whole-feature buffer (Ctx::gf_cur); derived nodes skip
 template <int MODE, bool PK>
-__global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
+__global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
   using CT = typename HT<MODE>::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int slot = DML_LSLOT;
   const LState& st = c.lstate[slot];
   // node state read once (the loop's bscr stores could alias it: a reference would reload it)
-  const int st_pos = __builtin_amdgcn_readfirstlane(st.pos);
+  const int st_pos = fround >= 0 ? fround : __builtin_amdgcn_readfirstlane(st.pos);
   const int64_t st_start = st.on.start;
-  if (st.done) return;
+  if (st.done || (fround >= 0 && st.derive)) return;
   const int r0 = DML_LCHUNK * c.chunk;
   if (r0 >= st.on.count) return;
   const int r1 = min(r0 + c.chunk, st.on.count);
   const NodeSpec s = spec_of<-1>(c, st.on.tree);
-  const int g = st.g;
+  const int f0 = fround >= 0 ? fround * c.kg_large : 0;
+  const int g = fround >= 0 ? min(c.kg_large, c.d - f0) : st.g;
   const int span = hist_planes(MODE, c.CH) * 256;
   __shared__ int16_t feats[64];
   CT* hist = (CT*)smem;
   const int16_t* perm = c.lperm + (int64_t)slot * c.d + st.pos;
-  for (int j = threadIdx.x; j < g; j += 256) feats[j] = perm[j];
+  for (int j = threadIdx.x; j < g; j += 256) feats[j] = fround >= 0 ? (int16_t)(f0 + j) : perm[j];
   for (int i = threadIdx.x; i < g * span; i += 256) hist[i] = (CT)0;
   __syncthreads();
   const uint32_t* rows = c.rows_cur + st.on.start;
@@ -2735,8 +2768,11 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
   // flush into the node's global histogram: unpacked planes [CH][256] (u32) for
   // classification, the three integer planes (u64) for regression
   const int gspan = hist_planes(MODE == 1 ? 0 : MODE, c.CH) * 256;
+  // per-round buffer, or the node's whole-feature buffer at the round's first feature
+  const int64_t goff = fround >= 0 ? ((int64_t)slot * c.d + f0) * gspan : (int64_t)slot * c.kg_large * gspan;
+  void* gbase = fround >= 0 ? c.gf_cur : c.ghist;
   if constexpr (MODE == 1) {
-    uint32_t* gh = (uint32_t*)c.ghist + (int64_t)slot * c.kg_large * gspan;
+    uint32_t* gh = (uint32_t*)gbase + goff;
     for (int i = threadIdx.x; i < g * 256; i += 256) {
       const unsigned long long v = hist[i];
       if (!v) continue;
@@ -2748,12 +2784,29 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c) {
       atomicAdd(&gj[512 + b], (uint32_t)(v >> 42));
     }
   } else {
-    CT* gh = (CT*)c.ghist + (int64_t)slot * c.kg_large * gspan;
+    CT* gh = (CT*)gbase + goff;
     for (int i = threadIdx.x; i < g * span; i += 256) {
       const CT v = hist[i];
       if (v != (CT)0) atomicAdd(&gh[i], v);
     }
   }
+}
+
+// whole-histogram level: a derived node's histogram over all d features = its parent's
+// (previous level) - its sibling's (this level's row pass), in exact integer arithmetic
+// (u32 class / row counts, two's-complement u64 regression sums); MODE = global layout
+template <int MODE>
+__global__ __launch_bounds__(256) void k_hist_derive(Ctx c) {
+  using CT = typename HT<MODE>::T;
+  const int slot = blockIdx.x;
+  const LState& st = c.lstate[slot];
+  if (!st.derive) return;
+  const int64_t per = (int64_t)c.d * hist_planes(MODE, c.CH) * 256;
+  CT* dst = (CT*)c.gf_cur + (int64_t)slot * per;
+  const CT* par = (const CT*)c.gf_prev + (int64_t)st.par * per;
+  const CT* sib = (const CT*)c.gf_cur + (int64_t)st.sib * per;
+  for (int64_t i = (int64_t)blockIdx.y * 1024 + threadIdx.x; i < per && i < (int64_t)(blockIdx.y + 1) * 1024; i += 256)
+    dst[i] = par[i] - sib[i];
 }
 
 // evaluates the node's global histogram; MODE here is the GLOBAL layout (0 or 2)
@@ -2774,9 +2827,17 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   double* rleft = (double*)(rn + c.kg_large + (c.kg_large & 1));
   double* rmid = rleft + (int64_t)c.kg_large * c.CH;   // monotonic_cst middle values
   __shared__ int need_more;
-  const CT* gh = (const CT*)c.ghist + (int64_t)slot * c.kg_large * span;
-  for (int i = tid; i < g * span; i += 256) hist[i] = gh[i];
   const int16_t* feats = c.lperm + (int64_t)slot * c.d + st.pos;
+  if (c.full_cur) {   // whole-feature buffer: the group's features by id
+    const CT* gf = (const CT*)c.gf_cur + (int64_t)slot * c.d * span;
+    for (int i = tid; i < g * span; i += 256) {
+      const int j = i / span;
+      hist[i] = gf[(int64_t)feats[j] * span + (i - j * span)];
+    }
+  } else {
+    const CT* gh = (const CT*)c.ghist + (int64_t)slot * c.kg_large * span;
+    for (int i = tid; i < g * span; i += 256) hist[i] = gh[i];
+  }
   const double nlo = c.nbound ? c.nbound[2 * (int64_t)st.on.node] : -INFINITY;
   const double nhi = c.nbound ? c.nbound[2 * (int64_t)st.on.node + 1] : INFINITY;
   __syncthreads();
@@ -2820,9 +2881,17 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   st.split = 1;
   st.nl = (int)best_left[c.CH - 1];
   const int set_next = 1 - set_cur;
-  enqueue_or_leaf(c, st.on.tree, base, st.on.start, st.nl, st.on.depth + 1, child_key(st.on.key, 0), set_next);
-  enqueue_or_leaf(c, st.on.tree, base + 1, st.on.start + st.nl, st.on.count - st.nl, st.on.depth + 1,
-                  child_key(st.on.key, 1), set_next);
+  const int il = enqueue_or_leaf(c, st.on.tree, base, st.on.start, st.nl, st.on.depth + 1, child_key(st.on.key, 0),
+                                 set_next);
+  const int ir = enqueue_or_leaf(c, st.on.tree, base + 1, st.on.start + st.nl, st.on.count - st.nl, st.on.depth + 1,
+                                 child_key(st.on.key, 1), set_next);
+  if (c.full_cur && il >= 0 && ir >= 0) {
+    // both children are large: the next level passes over the smaller one's rows and
+    // derives the larger (ties: the right child is derived)
+    const int dl = st.nl > st.on.count - st.nl ? 1 : 0;
+    c.pinfo_next[il] = make_int4(slot, ir, dl, 0);
+    c.pinfo_next[ir] = make_int4(slot, il, 1 - dl, 0);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
@@ -2847,7 +2916,8 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
   auto row_at = [&](int r) -> uint32_t { return r < r1 ? rows[r] : INV; };
   // split bin at row position p: from the histogram pass's scratch if the final round's
   // group produced the best split (st.best_j >= 0), else gathered from the table
-  const int bj = st.best_pos < st.scr_n ? st.best_pos : -1;
+  const int bj = st.scr_id > 0 ? (st.best_feat < st.scr_id ? st.best_feat : -1)
+                               : (st.best_pos < st.scr_n ? st.best_pos : -1);
   auto bin_of = [&](int p, uint32_t row) -> int {
     if (row == INV) return 0;
     if (bj >= 0) return (int)c.bscr[(st.on.start + p) * 16 + bj];
@@ -3281,6 +3351,30 @@ static int32_t* pinned_counters() {
   return p;
 }
 
+// whole-histogram large levels: two per-parity node-histogram buffers and two pinfo
+// tables per device, grown on demand (outside the Python-sized workspace: their size
+// follows the level's large-node count, known only at run time)
+struct FullBufs {
+  void* gf[2] = {nullptr, nullptr};
+  size_t gf_bytes[2] = {0, 0};
+  int4* pinfo = nullptr;   // [2][pi_cap]
+  int64_t pi_cap = 0;
+};
+static FullBufs* full_bufs() {
+  static FullBufs b[16];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  return &b[dev];
+}
+static bool ensure_bytes(void*& p, size_t& have, size_t need) {
+  if (have >= need) return true;
+  if (p) { (void)hipFree(p); p = nullptr; have = 0; }
+  const size_t want = need + need / 4;
+  if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return false; }
+  have = want;
+  return true;
+}
+
 }  // namespace dml
 
 using namespace dml;
@@ -3430,6 +3524,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   }
   const unsigned nchunks = (unsigned)((a->max_active + a->chunk - 1) / a->chunk);
   int cur = 0, levels = 0, large_rounds = 0;
+  int fpar = 0;             // whole-histogram buffer parity of this level
+  bool prev_full = false;   // the previous level kept its large nodes' whole histograms
   int64_t peak_open = 0;   // most open nodes of any level so far (early-predict tail rule)
   for (int i = 0; i < 4; ++i) a->tier_nodes_out[i] = 0;
   while (true) {
@@ -3498,7 +3594,48 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       }
       if (nb) k_nodes<DML_BLOCK_NT, MODE, -1><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
     }
-    if (nL) {
+    // whole-histogram level: every tree evaluates every feature and the level's node
+    // histograms over all d features fit the budget -> keep them, and derive the larger of
+    // two large siblings at the next level from its parent's (DML_LARGE_SUB=0: off)
+    const size_t full_node_b = (size_t)a->d * ghist_feat_bytes(MODE, CH);
+    const bool sub_on = !getenv("DML_LARGE_SUB") || atoi(getenv("DML_LARGE_SUB")) != 0;
+    const double sub_gb = getenv("DML_LARGE_SUB_GB") ? atof(getenv("DML_LARGE_SUB_GB")) : 4.0;
+    bool full = sub_on && nL > 0 && a->all_features && (double)nL * full_node_b <= sub_gb * 1e9;
+    FullBufs* fb = full ? full_bufs() : nullptr;
+    if (full && (!fb || !ensure_bytes(fb->gf[fpar], fb->gf_bytes[fpar], (size_t)nL * full_node_b))) full = false;
+    if (full && fb->pi_cap < c.large_cap) {
+      void* pp = fb->pinfo;
+      size_t have = (size_t)fb->pi_cap * 2 * sizeof(int4);
+      if (!ensure_bytes(pp, have, (size_t)c.large_cap * 2 * sizeof(int4))) { fb->pinfo = nullptr; fb->pi_cap = 0; full = false; }
+      else { fb->pinfo = (int4*)pp; fb->pi_cap = (int64_t)(have / (2 * sizeof(int4))); prev_full = false; }
+    }
+    c.full_cur = full ? 1 : 0;
+    c.full_prev = (full && prev_full) ? 1 : 0;
+    if (full) {
+      c.gf_cur = fb->gf[fpar];
+      c.gf_prev = fb->gf[1 - fpar];
+      c.pinfo_cur = fb->pinfo + (int64_t)fpar * fb->pi_cap;
+      c.pinfo_next = fb->pinfo + (int64_t)(1 - fpar) * fb->pi_cap;
+    }
+    if (nL && full) {
+      k_large_prep<<<nL, 64, 0, st>>>(c, cur, nL);
+      const int rounds = (int)((a->d + a->kg_large - 1) / a->kg_large);
+      HIP_OK(hipMemsetAsync(c.gf_cur, 0, (size_t)nL * full_node_b, st));
+      HIP_OK(hipMemsetAsync(c.pinfo_next, 0xFF, (size_t)std::min<int64_t>(2LL * nL, fb->pi_cap) * sizeof(int4), st));
+      const dim3 gh = DML_LARGE_NODE_FAST ? dim3((unsigned)nL, nchunks) : dim3(nchunks, (unsigned)nL);
+      for (int round = 0; round < rounds; ++round) {
+        ++large_rounds;
+        if (c.packed) k_hist_large<MODE, true><<<gh, 256, lds_hl, st>>>(c, round);
+        else k_hist_large<MODE, false><<<gh, 256, lds_hl, st>>>(c, round);
+      }
+      if (c.full_prev) {
+        const int64_t per = (int64_t)a->d * hist_planes(GM, CH) * 256;
+        k_hist_derive<GM><<<dim3((unsigned)nL, (unsigned)((per + 1023) / 1024)), 256, 0, st>>>(c);
+      }
+      for (int round = 0; round < rounds; ++round) k_split_large<GM><<<nL, 256, lds_sl, st>>>(c, cur);
+      const dim3 gp = DML_LARGE_NODE_FAST ? dim3((unsigned)nL, nchunks) : dim3(nchunks, (unsigned)nL);
+      k_partition_large<<<gp, 256, (size_t)((a->chunk + 255) / 256) * 4 * 8, st>>>(c);
+    } else if (nL) {
       k_large_prep<<<nL, 64, 0, st>>>(c, cur, nL);
       const int fixed_rounds = a->all_features ? (int)((a->d + a->kg_large - 1) / a->kg_large) : 0;
       for (int round = 0;; ++round) {
@@ -3506,8 +3643,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
         HIP_OK(hipMemsetAsync(c.ghist, 0, (size_t)nL * a->kg_large * ghist_feat_bytes(MODE, CH), st));
         HIP_OK(hipMemsetAsync(c.counters + kNeedMore, 0, 4, st));
         const dim3 gh = DML_LARGE_NODE_FAST ? dim3((unsigned)nL, nchunks) : dim3(nchunks, (unsigned)nL);
-        if (c.packed) k_hist_large<MODE, true><<<gh, 256, lds_hl, st>>>(c);
-        else k_hist_large<MODE, false><<<gh, 256, lds_hl, st>>>(c);
+        if (c.packed) k_hist_large<MODE, true><<<gh, 256, lds_hl, st>>>(c, -1);
+        else k_hist_large<MODE, false><<<gh, 256, lds_hl, st>>>(c, -1);
         k_split_large<GM><<<nL, 256, lds_sl, st>>>(c, cur);
         if (fixed_rounds) {   // every node visits every feature: the round count is known
           if (round + 1 >= fixed_rounds) break;
@@ -3552,6 +3689,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     }
     uint32_t* t = c.rows_cur; c.rows_cur = c.rows_next; c.rows_next = t;
     cur = 1 - cur;
+    prev_full = full;
+    fpar = 1 - fpar;
   }
   HIP_OK(hipMemcpyAsync(h, c.counters, kNumCounters * 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));

@@ -213,11 +213,51 @@ __global__ __launch_bounds__(256) void k_gb_grad(GbGradArgs a) {
   t[r] = (float)v;
 }
 
+// exponent histogram of regression targets (ops/forest_ops.py reg_exponent_counts; the
+// fixed-point rule forest_common.h reg_exponents_counts): out[t][k + 160] counts target t's
+// nonzero values with frexp exponent k, out[t][0] its zeros, bad[0] the non-finite values.
+// One LDS histogram per workgroup, flushed with one global atomic per nonzero bin.
+constexpr int kExpOffK = 160, kExpBinsK = 320;
+__global__ __launch_bounds__(256) void k_exp_hist(const float* __restrict__ y, int64_t n, int64_t ystride,
+                                                  unsigned long long* out, unsigned long long* bad) {
+  __shared__ unsigned int h[kExpBinsK];
+  __shared__ unsigned int nb;
+  for (int i = threadIdx.x; i < kExpBinsK; i += 256) h[i] = 0u;
+  if (threadIdx.x == 0) nb = 0u;
+  __syncthreads();
+  const int t = blockIdx.y;
+  const float* yt = y + (int64_t)t * ystride;
+  const int64_t i0 = (int64_t)blockIdx.x * 4096;
+  const int64_t i1 = i0 + 4096 < n ? i0 + 4096 : n;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
+    const float v = yt[i];
+    if (!isfinite(v)) { atomicAdd(&nb, 1u); continue; }
+    int k = 0;
+    if (v != 0.0f) frexpf(v, &k);
+    atomicAdd(&h[v != 0.0f ? k + kExpOffK : 0], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kExpBinsK; i += 256)
+    if (h[i]) atomicAdd(&out[(int64_t)t * kExpBinsK + i], (unsigned long long)h[i]);
+  if (threadIdx.x == 0 && nb) atomicAdd(bad, (unsigned long long)nb);
+}
+
 }  // namespace dml
 
 using namespace dml;
 
 extern "C" {
+
+// targets x [n] float32 rows at stride ystride (ystride = n for one target); out int64
+// [targets][320] and bad int64 [1], zeroed by the caller
+int dml_exp_hist(const float* y, int64_t n, int64_t ystride, int64_t targets, int64_t* out, int64_t* bad,
+                 hipStream_t st) {
+  if (n <= 0 || targets <= 0) return 0;
+  if (targets > 65535) return 2;
+  k_exp_hist<<<dim3((unsigned)((n + 4095) / 4096), (unsigned)targets), 256, 0, st>>>(
+      y, n, ystride, (unsigned long long*)out, (unsigned long long*)bad);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
 
 int dml_gb_sizeof_stage_args() { return (int)sizeof(GbStageArgs); }
 int dml_gb_sizeof_grad_args() { return (int)sizeof(GbGradArgs); }

@@ -243,6 +243,18 @@ def reg_exponent_counts(yreg, n: int, ystride: int = 0, targets: int = 1):
     all-reduce -- derives the same exponents from them (``reg_exponents_of_counts``).
     ``ystride > 0``: target t is ``yreg[t * ystride : t * ystride + n]``."""
     targets = max(1, int(targets)) if ystride > 0 else 1
+    if torch.is_tensor(yreg) and yreg.is_cuda and yreg.dtype == torch.float32 and yreg.is_contiguous():
+        # one LDS-histogram kernel (gbrt.hip k_exp_hist): boosting recounts every stage's targets
+        lib = native.hip_lib()
+        cnt = torch.zeros((targets, EXP_BINS), dtype=torch.int64, device=yreg.device)
+        bad = torch.zeros(1, dtype=torch.int64, device=yreg.device)
+        rc = lib.dml_exp_hist(native.ptr(yreg), n, ystride if ystride > 0 else n, targets, native.ptr(cnt),
+                              native.ptr(bad), native.stream_handle(yreg.device))
+        if rc != 0:
+            raise RuntimeError(f"dml_exp_hist failed ({rc})")
+        if int(bad.item()):
+            raise ValueError("regression target contains NaN or infinity")
+        return cnt
     if torch.is_tensor(yreg):
         y = yreg.reshape(-1)
         rows = y[: (targets - 1) * ystride + n].as_strided((targets, n), (ystride, 1)) if ystride > 0 else y[:n][None]

@@ -217,6 +217,7 @@ def _register_optional(lib) -> None:
         "dml_gb_sizeof_grad_args": (c_i32, []),
         "dml_gb_stage": (c_i32, [ctypes.POINTER(GbStageArgs), c_vp]),
         "dml_gb_grad": (c_i32, [ctypes.POINTER(GbGradArgs), c_vp]),
+        "dml_exp_hist": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     }
     for name, (res, args) in table.items():
         fn = getattr(lib, name, None)

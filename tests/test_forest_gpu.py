@@ -416,3 +416,37 @@ def test_gpu_monotonic_cst_family_matches_host_path():
     for g, c in zip(gpu, cpu):
         assert g.ok and c.ok
         assert np.allclose(g.result["cv_scores"], c.result["cv_scores"], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("is_reg", [False, True])
+def test_gpu_whole_histogram_levels_match_cpu(is_reg, monkeypatch):
+    """max_features == d (boosting, max_features=None): large-tier levels keep every node's
+    histogram over all features and derive the larger of two large siblings as parent -
+    smaller sibling (k_hist_derive).  Trees equal the C++ builder's and the row-pass build's
+    (DML_LARGE_SUB=0), node for node."""
+    from sklearn.datasets import make_regression
+
+    n, d = 40000, 12
+    if is_reg:
+        X, y = make_regression(n_samples=n, n_features=d, noise=5.0, random_state=2)
+        X, y = X.astype(np.float32), (y * 3 + 50).astype(np.float32)
+    else:
+        X, y = _data(n, d, 3, seed=5)
+    dev = torch.device("cuda:0")
+    Xb = binning.bin_matrix(torch.from_numpy(X).to(dev), binning.quantile_edges(torch.from_numpy(X).to(dev)))
+    roles, _ = make_split_roles(y, 3, not is_reg, holdout=False)
+    specs = _specs(3, 4, d, k=d, criterion=2 if is_reg else 0, max_depth=9)
+    T = len(specs)
+    tiers = forest_ops.ForestTiers(sub_max=64, wave_max=256, block_max=1024, chunk=1024)
+    yt = torch.from_numpy(y).to(dev)
+    args = (None, yt, torch.from_numpy(roles).to(dev), specs, 1, True) if is_reg else \
+        (yt.to(torch.int32), None, torch.from_numpy(roles).to(dev), specs, 3, False)
+    g = forest_ops.build_gpu(Xb, *args, tiers)
+    assert g.stats["tier_nodes"][3] > 3 * T   # large-tier levels below the roots
+    monkeypatch.setenv("DML_LARGE_SUB", "0")
+    g0 = forest_ops.build_gpu(Xb, *args, tiers)
+    c = forest_ops.build_cpu(Xb.cpu().numpy(), None if is_reg else y.astype(np.int32), y if is_reg else None, roles,
+                             specs, 1 if is_reg else 3, is_reg)
+    gc = _canon(g.nodes.cpu().numpy(), g.vals.cpu().numpy(), T)
+    assert gc == _canon(c.nodes, c.vals, T)
+    assert gc == _canon(g0.nodes.cpu().numpy(), g0.vals.cpu().numpy(), T)

@@ -90,3 +90,20 @@ def test_heavy_tailed_target_tree_matches_sklearn_host():
 @pytest.mark.gpu
 def test_heavy_tailed_target_tree_matches_sklearn_gpu():
     _leaves_match_sklearn("cuda")
+
+
+@pytest.mark.gpu
+def test_exponent_histogram_kernel_matches_numpy():
+    """gbrt.hip k_exp_hist (boosting recounts every stage's targets on the device) against the
+    numpy histogram, multi-target with a row stride, zeros and a wide dynamic range."""
+    rng = np.random.default_rng(4)
+    for T, n, stride in ((1, 100_003, 100_003), (5, 70_000, 70_016)):
+        Y = (rng.standard_t(1.3, size=(T, stride)) * 10.0 ** rng.uniform(-20, 20, size=(T, 1))).astype(np.float32)
+        Y[rng.random(Y.shape) < 0.1] = 0.0
+        want = reg_exponent_counts(Y, n, stride if T > 1 else 0, T)
+        got = reg_exponent_counts(torch.from_numpy(Y).to("cuda").reshape(-1)[: (T - 1) * stride + n] if T > 1
+                                  else torch.from_numpy(Y[0, :n]).to("cuda"), n, stride if T > 1 else 0, T)
+        assert np.array_equal(got.cpu().numpy(), want)
+    bad = torch.tensor([1.0, float("nan"), 2.0], device="cuda")
+    with pytest.raises(ValueError):
+        reg_exponent_counts(bad, 3)
