@@ -234,6 +234,7 @@ struct Ctx {
   const int4* pinfo_cur;
   int4* pinfo_next;
   int32_t full_cur, full_prev;
+  unsigned long long* lyy;   // [cap_large] regression: sum w y2q of the best split's left rows
   int64_t large_cap;
   int32_t wave_max, block_max, chunk, kg_wave, kg_block, kg_large, slack_wave;
   int32_t sub_max, sub_cache_d;
@@ -440,6 +441,11 @@ template <> struct HT<2> { using T = unsigned long long; };
 // planes of one feature's histogram: MODE 1 one packed plane, MODE 2 three integer planes
 // (w | rows << 32, sum w yq, sum w y2q), MODE 0 the CH class/row planes
 __host__ __device__ __forceinline__ int hist_planes(int MODE, int CH) { return MODE == 1 ? 1 : (MODE == 2 ? 3 : CH); }
+// the large tier's regression histograms drop the y^2 plane: a split's choice needs only
+// (w | rows, w yq); the children's sum w y2q comes from the partition pass, which sees
+// every row once (k_partition_large / k_large_finish) -- one u64 LDS atomic fewer per
+// (row, feature) in the kernel that dominates boosting builds
+__host__ __device__ __forceinline__ int large_planes(int MODE, int CH) { return MODE == 2 ? 2 : hist_planes(MODE, CH); }
 
 // histogram payload of one row: MODE 0 cls | w << 32, MODE 1 packed u64, MODE 2 the
 // row's three integer regression terms
@@ -622,7 +628,8 @@ __device__ DML_EVAL_ATTR void eval_gini_pf(unsigned long long* h, int span, cons
 // histograms are read ONCE into registers (4 bins per lane), scanned with DPP, scored and
 // arg-maxed without writing the scan back to LDS; the histogram is cleared by the same
 // lanes right after the read.  Multiclass (MODE 0) keeps the LDS path (C+1 planes).
-template <int MODE>
+// RP: regression planes present (3, or 2 without the y^2 plane: out_left[2] is then 0)
+template <int MODE, int RP = 3>
 __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int CH, const NodeSpec& s, int lane,
                              double* out_gain, int* out_bin, int* out_nc, double* out_left, bool zero_after,
                              const double* cw = nullptr, const RegScale* rq = nullptr, MonoQ mq = MonoQ{0, 0.0, 0.0},
@@ -638,7 +645,7 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
         return;
       }
     }
-    constexpr int NP = MODE == 1 ? 1 : 3;      // planes: packed u64 | (w | rows << 32, w yq, w y2q) integers
+    constexpr int NP = MODE == 1 ? 1 : RP;     // planes: packed u64 | (w | rows << 32, w yq[, w y2q]) integers
     CT v[NP][4];
 #pragma unroll
     for (int q = 0; q < NP; ++q)
@@ -786,20 +793,20 @@ __device__ DML_EVAL_ATTR void eval_feature(typename HT<MODE>::T* h, int C, int C
         out_left[2] = bb >= 0 ? (double)(cv >> 42) : 0.0;
       }
     } else {
-      uint64_t mine[3];
+      uint64_t mine[NP];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
+      for (int q = 0; q < NP; ++q) {
         mine[q] = v[q][0];
 #pragma unroll
         for (int i = 1; i < 4; ++i) if (sel == i) mine[q] = v[q][i];
       }
-      uint64_t cq[3];
+      uint64_t cq[3] = {0ull, 0ull, 0ull};
 #pragma unroll
-      for (int q = 0; q < 3; ++q) cq[q] = wave::bcast<uint64_t>(mine[q], src);
+      for (int q = 0; q < NP; ++q) cq[q] = wave::bcast<uint64_t>(mine[q], src);
       if (lane == 0) {   // channels {w, w y, w y^2, rows}
         out_left[0] = bb >= 0 ? reg_w(cq[0]) : 0.0;
         out_left[1] = bb >= 0 ? reg_s1(cq[1], *rq) : 0.0;
-        out_left[2] = bb >= 0 ? reg_s2(cq[2], *rq) : 0.0;
+        out_left[2] = (bb >= 0 && NP == 3) ? reg_s2(cq[2], *rq) : 0.0;
         out_left[3] = bb >= 0 ? reg_rows(cq[0]) : 0.0;
       }
     }
@@ -871,7 +878,7 @@ __device__ DML_EVAL_ATTR void eval_feature_lds(typename HT<MODE>::T* h, int C, i
   }
 }
 
-template <int MODE>
+template <int MODE, int RP = 3>
 __device__ __forceinline__ void hist_add_row(typename HT<MODE>::T* hist, const Ctx& c, const float* ty,
                                              const int16_t* feats, int g, uint32_t row, uint32_t w, int span) {
   const uint8_t* xr = c.Xb + (int64_t)row * c.ld;
@@ -893,7 +900,7 @@ __device__ __forceinline__ void hist_add_row(typename HT<MODE>::T* hist, const C
       unsigned long long* hj = hist + j * span;
       atomicAdd(&hj[b], p.wr);
       atomicAdd(&hj[256 + b], p.wy);
-      atomicAdd(&hj[512 + b], p.wyy);
+      if (RP == 3) atomicAdd(&hj[512 + b], p.wyy);
     }
   }
 }
@@ -1057,7 +1064,7 @@ __device__ __forceinline__ typename PLT<MODE>::T word_payload(const Ctx& c, cons
   else return reg_payload(c, w, ty[wd & c.rmask]);
 }
 
-template <int MODE>
+template <int MODE, int RP = 3>
 __device__ __forceinline__ void hist_add(typename HT<MODE>::T* hj, const Ctx& c, int b, const typename PLT<MODE>::T& pl) {
 #ifdef DML_X2_ATOMIC   // sensitivity build: every histogram atomic issued twice (the second adds 0)
   if constexpr (MODE == 1) atomicAdd(&hj[b], (unsigned long long)(pl * (uint64_t)((uint32_t)c.n >> 31)));
@@ -1065,7 +1072,7 @@ __device__ __forceinline__ void hist_add(typename HT<MODE>::T* hj, const Ctx& c,
   if constexpr (MODE == 2) {
     atomicAdd(&hj[b], pl.wr);
     atomicAdd(&hj[256 + b], pl.wy);
-    atomicAdd(&hj[512 + b], pl.wyy);
+    if (RP == 3) atomicAdd(&hj[512 + b], pl.wyy);
     return;
   }
   if constexpr (MODE == 0) {
@@ -2643,6 +2650,7 @@ __global__ __launch_bounds__(64) void k_large_prep(Ctx c, int set_cur, int nL) {
   st.best_pos = 1 << 30;
   st.scr_n = st.g <= 16 ? st.g : 0;
   st.scr_id = 0; st.derive = 0; st.par = -1; st.sib = -1;
+  c.lyy[slot] = 0ull;
   if (c.full_cur) {
     // whole-histogram level: round r's row pass covers features [r kg, (r + 1) kg) by id, so
     // bscr holds features [0, g0) (not visiting positions); a larger sibling is derived
@@ -2682,7 +2690,8 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
   const NodeSpec s = spec_of<-1>(c, st.on.tree);
   const int f0 = fround >= 0 ? fround * c.kg_large : 0;
   const int g = fround >= 0 ? min(c.kg_large, c.d - f0) : st.g;
-  const int span = hist_planes(MODE, c.CH) * 256;
+  constexpr int RPL = MODE == 2 ? 2 : 3;
+  const int span = large_planes(MODE, c.CH) * 256;
   __shared__ int16_t feats[64];
   CT* hist = (CT*)smem;
   const int16_t* perm = c.lperm + (int64_t)slot * c.d + st.pos;
@@ -2730,7 +2739,7 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
         }
 #pragma unroll
         for (int j = 0; j < G; ++j)
-          if (j < g) hist_add<MODE>(hist + j * span, c, (int)b[j], pl);
+          if (j < g) hist_add<MODE, RPL>(hist + j * span, c, (int)b[j], pl);
       };
       uint32_t rA = row_at(t0), rB = row_at(t0 + 256);
       uint32_t bA[G], bB[G];
@@ -2761,13 +2770,13 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
   } else {
     for (int r = r0 + threadIdx.x; r < r1; r += 256) {
       const uint32_t row = rows[r];
-      hist_add_row<MODE>(hist, c, ty, feats, g, word_row(c, row), word_weight(c, s, row), span);
+      hist_add_row<MODE, RPL>(hist, c, ty, feats, g, word_row(c, row), word_weight(c, s, row), span);
     }
   }
   __syncthreads();
   // flush into the node's global histogram: unpacked planes [CH][256] (u32) for
   // classification, the three integer planes (u64) for regression
-  const int gspan = hist_planes(MODE == 1 ? 0 : MODE, c.CH) * 256;
+  const int gspan = large_planes(MODE == 1 ? 0 : MODE, c.CH) * 256;
   // per-round buffer, or the node's whole-feature buffer at the round's first feature
   const int64_t goff = fround >= 0 ? ((int64_t)slot * c.d + f0) * gspan : (int64_t)slot * c.kg_large * gspan;
   void* gbase = fround >= 0 ? c.gf_cur : c.ghist;
@@ -2801,13 +2810,15 @@ __global__ __launch_bounds__(256) void k_hist_derive(Ctx c) {
   const int slot = blockIdx.x;
   const LState& st = c.lstate[slot];
   if (!st.derive) return;
-  const int64_t per = (int64_t)c.d * hist_planes(MODE, c.CH) * 256;
+  const int64_t per = (int64_t)c.d * large_planes(MODE, c.CH) * 256;
   CT* dst = (CT*)c.gf_cur + (int64_t)slot * per;
   const CT* par = (const CT*)c.gf_prev + (int64_t)st.par * per;
   const CT* sib = (const CT*)c.gf_cur + (int64_t)st.sib * per;
   for (int64_t i = (int64_t)blockIdx.y * 1024 + threadIdx.x; i < per && i < (int64_t)(blockIdx.y + 1) * 1024; i += 256)
     dst[i] = par[i] - sib[i];
 }
+
+__device__ void large_commit(const Ctx& c, const NodeSpec& s, LState& st, int slot, const double* best_left, int set_cur);
 
 // evaluates the node's global histogram; MODE here is the GLOBAL layout (0 or 2)
 template <int MODE>
@@ -2818,7 +2829,7 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   LState& st = c.lstate[slot];
   if (st.done) return;
   const NodeSpec s = spec_of<-1>(c, st.on.tree);
-  const int g = st.g, span = hist_planes(MODE, c.CH) * 256;
+  const int g = st.g, span = large_planes(MODE, c.CH) * 256;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   CT* hist = (CT*)smem;
   double* rg = (double*)(smem + (size_t)c.kg_large * span * sizeof(CT));
@@ -2842,8 +2853,8 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   const double nhi = c.nbound ? c.nbound[2 * (int64_t)st.on.node + 1] : INFINITY;
   __syncthreads();
   for (int j = wid; j < g; j += 4)
-    eval_feature<MODE>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, false,
-                       tree_cw(c, st.on.tree), &c.rq, MonoQ{mono_of(c, s, feats[j]), nlo, nhi}, rmid + j);
+    eval_feature<MODE, 2>(hist + j * span, c.C, c.CH, s, lane, rg + j, rb + j, rn + j, rleft + j * c.CH, false,
+                          tree_cw(c, st.on.tree), &c.rq, MonoQ{mono_of(c, s, feats[j]), nlo, nhi}, rmid + j);
   __syncthreads();
   double* best_left = c.lbest_left + (int64_t)slot * c.CH;
   if (tid == 0) {
@@ -2873,10 +2884,22 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   }
   if (tid != 0) return;
   st.done = 1;
+  if (c.is_reg) {
+    // regression: the best candidate is partitioned first; k_large_finish adds the left
+    // rows' sum w y2q (from the partition pass) and then accepts / creates / enqueues
+    if (st.best_feat >= 0) { st.split = 2; st.nl = (int)best_left[c.CH - 1]; }
+    return;
+  }
+  large_commit(c, s, st, slot, best_left, set_cur);
+}
+
+// accept the node's best split, create and enqueue its children (+ the next level's
+// sibling table on whole-histogram levels); st.split = 1 when it splits, else 0
+__device__ void large_commit(const Ctx& c, const NodeSpec& s, LState& st, int slot, const double* best_left, int set_cur) {
   int base = -1;
   if (st.best_feat >= 0 && accept_split(c, s, st.on.node, st.on.tree, best_left))
     base = make_children(c, st.on.node, st.best_feat, st.best_bin, best_left);
-  if (base < 0) return;
+  if (base < 0) { st.split = 0; return; }
   mono_children(c, st.on.node, base, mono_of(c, s, st.best_feat), st.best_mid);
   st.split = 1;
   st.nl = (int)best_left[c.CH - 1];
@@ -2950,6 +2973,10 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
   }
   __syncthreads();
   int baseL = tbase[0], baseR = tbase[1];
+  // regression: sum w y2q of the left rows (k_large_finish completes the left child's sums)
+  const NodeSpec s = spec_of<-1>(c, st.on.tree);
+  const float* ty = c.is_reg ? tree_y(c, s) : nullptr;
+  unsigned long long lyy = 0ull;
   for (int t0 = r0; t0 < r1; t0 += 256) {
     const int r = t0 + tid;
     const bool valid = r < r1;
@@ -2970,11 +2997,37 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
     }
     (void)vm;
     if (valid) {
-      if ((ml >> lane) & 1ull) out[baseL + offL + lane_prefix(ml)] = row;
-      else out[nl + baseR + offR + lane_prefix(mr)] = row;
+      if ((ml >> lane) & 1ull) {
+        out[baseL + offL + lane_prefix(ml)] = row;
+        if (ty) {
+          int64_t yq, y2q;
+          reg_quantize(ty[word_row(c, row)], c.rq, yq, y2q);
+          lyy += (unsigned long long)((int64_t)word_weight(c, s, row) * y2q);
+        }
+      } else {
+        out[nl + baseR + offR + lane_prefix(mr)] = row;
+      }
     }
     baseL += totL; baseR += totR;
   }
+  if (ty) {   // exact integer sum: any order
+    lyy = (unsigned long long)wave::sum<uint64_t>((uint64_t)lyy, lane);
+    if (lane == 0 && lyy) atomicAdd(&c.lyy[slot], lyy);
+  }
+}
+
+// regression large nodes after the partition: the left child's sum w y2q completes the
+// best split's statistics, then the split is accepted or the node stays a leaf (its
+// partitioned range is then unused)
+__global__ __launch_bounds__(64) void k_large_finish(Ctx c, int set_cur) {
+  const int slot = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  LState& st = c.lstate[slot];
+  if (st.split != 2) return;
+  const NodeSpec s = spec_of<-1>(c, st.on.tree);
+  double* best_left = c.lbest_left + (int64_t)slot * c.CH;
+  best_left[2] = reg_s2(c.lyy[slot], c.rq);
+  large_commit(c, s, st, slot, best_left, set_cur);
 }
 
 // ------------------------------------------------------------------------------------
@@ -3184,7 +3237,7 @@ __global__ void k_roots(Ctx c) {
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct Layout {
-  size_t rows_b, open[2][kTiers], stage, counters, cursors, lstate, lperm, lbest, ghist, lcursor, bscr, rsum, total;
+  size_t rows_b, open[2][kTiers], stage, counters, cursors, lstate, lperm, lbest, ghist, lcursor, lyy, bscr, rsum, total;
   int64_t stage_cap;
   int64_t open_cap[kTiers], large_cap;
 };
@@ -3195,7 +3248,8 @@ static size_t mode_elem(int mode) { return mode == 0 ? 4 : 8; }
 
 // bytes of one feature's large-tier GLOBAL histogram: u32 [CH][256] (classification,
 // binary unpacked), u64 [3][256] (regression integer planes)
-static size_t ghist_feat_bytes(int mode, int CH) { return mode == 2 ? (size_t)3 * 256 * 8 : (size_t)CH * 256 * 4; }
+// bytes per feature of a large-tier global histogram (large_planes: no y^2 plane)
+static size_t ghist_feat_bytes(int mode, int CH) { return mode == 2 ? (size_t)2 * 256 * 8 : (size_t)CH * 256 * 4; }
 
 static Layout plan(const ForestArgs* a) {
   Layout L{};
@@ -3225,6 +3279,7 @@ static Layout plan(const ForestArgs* a) {
   L.lbest = take((size_t)L.large_cap * CH * 8);
   L.ghist = take((size_t)L.large_cap * a->kg_large * ghist_feat_bytes(build_mode(a), (int)CH));
   L.lcursor = take((size_t)L.large_cap * 8);
+  L.lyy = take((size_t)L.large_cap * 8);
   L.bscr = take((size_t)R * 16);
   L.rsum = take((size_t)T * 3 * 8);
   L.total = off;
@@ -3271,6 +3326,7 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.lbest_left = (double*)(ws + L.lbest);
   c.ghist = (void*)(ws + L.ghist);
   c.lcursor = (int32_t*)(ws + L.lcursor);
+  c.lyy = (unsigned long long*)(ws + L.lyy);
   c.bscr = ws + L.bscr;
   c.rsum = (unsigned long long*)(ws + L.rsum);
   c.mono = (const int8_t*)a->mono;
@@ -3496,14 +3552,21 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   int32_t* h_pool = h + 48;   // pinned slot for the per-level pool reservation (H2D)
   const size_t lds_b = fused_lds(a, (int)a->kg_block);
   const int CH = c.CH;
-  const size_t lds_hl = (size_t)a->kg_large * hist_planes(MODE, CH) * 256 * mode_elem(MODE);
+  // regression: k_hist_large runs ONE workgroup per CU (its dynamic LDS is padded past half
+  // the CU's 160 KB): GBRT config 6 3.40 -> 3.04 s against two per CU with the 64-KB
+  // two-plane histograms; classification is unaffected by the padding (23.15 vs 22.80
+  // CV-fits/s, so it keeps its natural size).  DML_LARGE_LDS_MIN overrides the floor.
+  const size_t lds_hl_floor = getenv("DML_LARGE_LDS_MIN") ? (size_t)atol(getenv("DML_LARGE_LDS_MIN"))
+                                                          : (MODE == 2 ? (size_t)96 * 1024 : 0);
+  const size_t lds_hl = std::max<size_t>((size_t)a->kg_large * large_planes(MODE, CH) * 256 * mode_elem(MODE),
+                                         std::min<size_t>(lds_hl_floor, 150 * 1024));
   const size_t lds_sl = (size_t)a->kg_large * ghist_feat_bytes(MODE, CH) + a->kg_large * 16 + 16 +
                         (size_t)a->kg_large * CH * 8 + (size_t)a->kg_large * 8 + 64;
   const size_t lds_max = 160 * 1024;
   if (lds_w > lds_max || lds_b > lds_max || lds_sl > lds_max || lds_s > lds_max || lds_big > lds_max) return 7;
   if (a->sub_max > 64) return 9;
   {
-    const int need = (int)std::max(std::max(std::max(lds_s, lds_w), std::max(lds_b, lds_sl)), lds_big);
+    const int need = (int)std::max(std::max(std::max(lds_s, lds_w), std::max(lds_b, lds_sl)), std::max(lds_big, lds_hl));
     static int attr_set[3] = {0, 0, 0};
     if (need > 64 * 1024 && need > attr_set[MODE]) {
       HIP_OK(hipFuncSetAttribute((const void*)k_subtree<REG, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
@@ -3629,12 +3692,13 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
         else k_hist_large<MODE, false><<<gh, 256, lds_hl, st>>>(c, round);
       }
       if (c.full_prev) {
-        const int64_t per = (int64_t)a->d * hist_planes(GM, CH) * 256;
+        const int64_t per = (int64_t)a->d * large_planes(GM, CH) * 256;
         k_hist_derive<GM><<<dim3((unsigned)nL, (unsigned)((per + 1023) / 1024)), 256, 0, st>>>(c);
       }
       for (int round = 0; round < rounds; ++round) k_split_large<GM><<<nL, 256, lds_sl, st>>>(c, cur);
       const dim3 gp = DML_LARGE_NODE_FAST ? dim3((unsigned)nL, nchunks) : dim3(nchunks, (unsigned)nL);
       k_partition_large<<<gp, 256, (size_t)((a->chunk + 255) / 256) * 4 * 8, st>>>(c);
+      if (reg) k_large_finish<<<nL, 64, 0, st>>>(c, cur);
     } else if (nL) {
       k_large_prep<<<nL, 64, 0, st>>>(c, cur, nL);
       const int fixed_rounds = a->all_features ? (int)((a->d + a->kg_large - 1) / a->kg_large) : 0;
@@ -3656,6 +3720,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       }
       const dim3 gp = DML_LARGE_NODE_FAST ? dim3((unsigned)nL, nchunks) : dim3(nchunks, (unsigned)nL);
       k_partition_large<<<gp, 256, (size_t)((a->chunk + 255) / 256) * 4 * 8, st>>>(c);
+      if (reg) k_large_finish<<<nL, 64, 0, st>>>(c, cur);
     }
     if (fork) {
       for (int i = 0; i < 3; ++i) {
