@@ -192,7 +192,7 @@ def vote(dist: torch.Tensor, nb_y: torch.Tensor, k: int, weights: str, n_classes
     return ((w * yv).sum(1) / w.sum(1)).float(), None
 
 
-def _merge_topk(d_parts: torch.Tensor, i_parts: torch.Tensor, y_parts: torch.Tensor, K: int):
+def _merge_topk(d_parts: torch.Tensor, i_parts: torch.Tensor, y_parts: torch.Tensor, K: int, with_ids: bool = False):
     """[W, q, K] per-rank candidates -> the global top-K per query in (distance, row id)
     order: the order a one-process stable sort over ascending row ids gives."""
     W, q, k = d_parts.shape
@@ -202,6 +202,8 @@ def _merge_topk(d_parts: torch.Tensor, i_parts: torch.Tensor, y_parts: torch.Ten
     _, o1 = torch.sort(i, dim=1, stable=True)                  # ascending row id ...
     d, i, y = d.gather(1, o1), i.gather(1, o1), y.gather(1, o1)
     _, o2 = torch.sort(d, dim=1, stable=True)                  # ... then distance (stable)
+    if with_ids:
+        return d.gather(1, o2)[:, :K], i.gather(1, o2)[:, :K], y.gather(1, o2)[:, :K]
     return d.gather(1, o2)[:, :K], y.gather(1, o2)[:, :K]
 
 
@@ -273,11 +275,96 @@ def knn_search_sharded(data, splits: List[int], K: int, metric: int, p: float, y
     return out
 
 
+class _ChunkTable:
+    """One streamed chunk of training candidates [r0, r1) followed by a block of query rows,
+    as a table for ``knn_search_hip`` (the role rows of the chunk's rows; queries role 0)."""
+
+    def __init__(self, data, r0: int, Xc: torch.Tensor, Q: torch.Tensor, qpos: Dict[int, Tuple[int, int]]):
+        self.device, self.d = data.device, data.d
+        nc = int(Xc.shape[0])
+        self.X = torch.cat([Xc, Q]).contiguous()
+        self.n = int(self.X.shape[0])
+        self.roles = torch.zeros((data.roles.shape[0], self.n), dtype=torch.uint8, device=self.device)
+        self.roles[:, :nc] = data.roles[:, r0:r0 + nc]
+        self.test_rows = {s: torch.arange(nc + a, nc + b, dtype=torch.int32, device=self.device)
+                          for s, (a, b) in qpos.items()}
+
+    def feature_major(self) -> torch.Tensor:
+        if getattr(self, "_XT", None) is None:
+            self._XT = self.X.t().contiguous()
+        return self._XT
+
+
+def knn_search_streamed(data, splits: List[int], K: int, metric: int, p: float, y: torch.Tensor):
+    """Binned-only tables (float32 rows too large for HBM, DeviceData.stream_rows): the
+    queries -- every split's held-out rows -- are taken in blocks that fit a device budget
+    (``DML_KNN_QBLOCK_GB``, default 8); per block the host rows stream past once in chunks,
+    each chunk's training rows are searched exactly (HIP kernels as for a resident table, or
+    torch) and merged into the running top-K in (distance, row id) order -- the order of the
+    one-pass search, so the neighbours equal the resident path's."""
+    Xh = data._X_host
+    dev = data.device
+    budget = float(os.environ.get("DML_KNN_QBLOCK_GB", "8")) * 1e9
+    per_block = max(1, int(budget // max(1, 4 * data.d)))
+    big = torch.finfo(torch.float32).max
+    # (split, [a, b)) slices of each split's ascending test rows, grouped into query blocks
+    work, cur, used = [], [], 0
+    for s in splits:
+        rows = data.test_rows[s].long()
+        for a in range(0, rows.numel(), per_block):
+            b = min(rows.numel(), a + per_block)
+            if used + (b - a) > per_block and cur:
+                work.append(cur)
+                cur, used = [], 0
+            cur.append((s, a, b))
+            used += b - a
+    if cur:
+        work.append(cur)
+    res = {s: ([], []) for s in splits}
+    for block in work:
+        qidx = torch.cat([data.test_rows[s].long()[a:b] for s, a, b in block])
+        Q = torch.from_numpy(np.array(Xh[qidx.cpu().numpy()], dtype=np.float32)).to(dev)
+        qpos, off = {}, 0
+        for s, a, b in block:
+            qpos[s] = (off, off + (b - a))
+            off += b - a
+        m = off
+        dd = torch.full((m, K), big, dtype=torch.float32, device=dev)
+        ii = torch.full((m, K), 2 ** 62, dtype=torch.long, device=dev)
+        yy = torch.zeros((m, K), dtype=y.dtype, device=dev)
+        for r0, r1, Xc in data.stream_rows():
+            tab = _ChunkTable(data, r0, Xc, Q, qpos)
+            enough = all(int((tab.roles[s, :r1 - r0] == 1).sum()) >= K for s in qpos)
+            if data.is_gpu and K <= KERNEL_KMAX and metric != M_COS and enough:
+                got = knn_search_hip(tab, sorted(qpos), K, metric, p)
+                cd = torch.cat([got[s][0].float() for s, _, _ in block])
+                ci = torch.cat([got[s][1] for s, _, _ in block]) + r0
+            else:
+                cd = torch.full((m, K), big, dtype=torch.float32, device=dev)
+                ci = torch.full((m, K), 2 ** 62, dtype=torch.long, device=dev)
+                for s, (a, b) in qpos.items():
+                    tr = torch.nonzero(tab.roles[s, :r1 - r0] == 1).flatten()
+                    if tr.numel() == 0:
+                        continue
+                    acc, idx = knn_search_torch(tab.X, tab.test_rows[s], tr, K, metric, p)
+                    k = acc.shape[1]
+                    cd[a:b, :k] = acc.float()
+                    ci[a:b, :k] = idx + r0
+            cy = y[ci.clamp_max(data.n - 1)]
+            dd, ii, yy = _merge_topk(torch.stack([dd, cd]), torch.stack([ii, ci]), torch.stack([yy, cy]), K,
+                                     with_ids=True)
+        for s, (a, b) in qpos.items():
+            res[s][0].append(dd[a:b])
+            res[s][1].append(yy[a:b])
+    return {s: (torch.cat(res[s][0]), torch.cat(res[s][1])) for s in splits}
+
+
 class KNeighborsFamily(Family):
     model_types = ("KNeighborsClassifier", "KNeighborsRegressor")
     classifiers = ("KNeighborsClassifier",)
     data_parallel = True   # row-sharded search: per-rank top-K + exact merge (knn_search_sharded)
     dp_when_few = False    # a replicated table is always faster when it fits
+    streams_rows = True    # binned-only tables: exact search over streamed host chunks
 
     def resolve(self, model_type, params, n_train, n_features, n_classes):
         p = dict(_DEFAULTS)
@@ -325,6 +412,8 @@ class KNeighborsFamily(Family):
             kmax = max(t.params["n_neighbors"] for t in ok)
             if getattr(data, "is_row_shard", False):
                 nb = knn_search_sharded(data, splits, kmax, metric, p, y)
+            elif data.X is None and getattr(data, "can_stream_rows", lambda: False)():
+                nb = knn_search_streamed(data, splits, kmax, metric, p, y)
             elif data.is_gpu and kmax <= KERNEL_KMAX and metric != M_COS:
                 nb = {s: (a, y[i]) for s, (a, i) in knn_search_hip(data, splits, kmax, metric, p).items()}
             else:
@@ -337,7 +426,11 @@ class KNeighborsFamily(Family):
                 o = FitOutput(task_id=t.task_id, pred=pred, proba=proba, info={"warnings": t.params["warnings"]})
                 if keep_models:
                     tr = data.train_rows[t.split].long()
-                    Xtr, ytr = data.X[tr], y[tr]
+                    if data.X is None:   # binned-only: the artefact's training rows from the host table
+                        Xtr = torch.from_numpy(np.array(data._X_host[tr.cpu().numpy()], dtype=np.float32))
+                    else:
+                        Xtr = data.X[tr]
+                    ytr = y[tr]
                     if getattr(data, "is_row_shard", False):   # the fitted model holds every rank's rows
                         cnt = data.all_gather_equal(torch.tensor([tr.numel()], device=data.device)).cpu().numpy()
                         Xtr, ytr = data._gather_rows(Xtr, cnt), data._gather_rows(ytr, cnt)

@@ -42,7 +42,18 @@ def _check(dev, n, d, chunk, tmp_path):
                         ("GradientBoostingClassifier", {"n_estimators": [5], "max_depth": [2]})):
         assert _scores(res_dd, model, grid) == _scores(bin_dd, model, grid)
     with pytest.raises(ValueError, match="binned form"):
-        run_candidates(bin_dd, JobSpec("KNeighborsClassifier", [{"n_neighbors": 3}], cv=3), [0])
+        run_candidates(bin_dd, JobSpec("SVC", [{"C": 1.0}], cv=3), [0])
+    # KNN: query blocks of held-out rows against streamed candidate chunks, exact merge
+    knn_grid = {"n_neighbors": [1, 5, 12], "weights": ["uniform", "distance"], "p": [1, 2]}
+    old_q = os.environ.get("DML_KNN_QBLOCK_GB")
+    os.environ["DML_KNN_QBLOCK_GB"] = str(700 * d * 4 / 1e9)     # several query blocks
+    try:
+        assert _scores(res_dd, "KNeighborsClassifier", knn_grid) == _scores(bin_dd, "KNeighborsClassifier", knn_grid)
+    finally:
+        if old_q is None:
+            os.environ.pop("DML_KNN_QBLOCK_GB")
+        else:
+            os.environ["DML_KNN_QBLOCK_GB"] = old_q
     # LogisticRegression streams the host rows once per objective evaluation (every candidate
     # x fold of the batch per chunk); the resident comparison runs the same fp32 objective
     lr_grid = {"C": [0.05, 1.0], "solver": ["lbfgs"], "max_iter": [200]}
