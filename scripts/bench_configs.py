@@ -116,6 +116,18 @@ def _config5_data(root):
 
 
 def _config5_drive(ctl, runner_name):
+    # untimed warm-up job: the dataset's first load (parse, placement; on the cluster runner
+    # also the side communicator's first collective) is a once-per-service cost, reported
+    # separately as load_s, so both runners are timed on the same steady-state queue
+    t_w = time.time()
+    sid0 = ctl.create_session()[1]["session_id"]
+    st, _ = ctl.train(sid0, {"job_id": "warm", "dataset_id": "mixed", "train_params": {"target_column": "label"},
+                             "model_details": {"model_type": "RandomForestClassifier", "search_type": "GridSearchCV",
+                                               "hyperparameters": {"base_estimator_params": {}, "cv_params": {"cv": 2},
+                                                                   "search_params": {"param_grid": {"n_estimators": [2]}}}}})
+    assert st == 200
+    ctl.table.wait_finished("warm", timeout=3600)
+    load_s = time.time() - t_w
     jobs = []
     t0 = time.time()
     for s in range(4):
@@ -143,7 +155,8 @@ def _config5_drive(ctl, runner_name):
         assert st["job_status"] == "completed", st
         fits += st["total_subtasks"] * 6
         workers |= {m.get("worker_id") for m in ctl.metrics(sid, jid)[1]}
-    _emit(5, fits, time.time() - t0, jobs=len(jobs), sessions=4, runner=runner_name, workers=sorted(workers))
+    _emit(5, fits, time.time() - t0, jobs=len(jobs), sessions=4, runner=runner_name, workers=sorted(workers),
+          load_s=round(load_s, 3))
 
 
 def config5(dev):
