@@ -40,6 +40,11 @@ class ForestTiers:
     wave_max: int = 512         # sweeps: profiles/r1_forest_ab_experiments.md, r2_tier_sweep.txt
     block_max: int = 32768      # r2 kernels (XbT large tier): 32768 beats 131072 by 4 %
     chunk: int = 16384
+    # builds whose trees all evaluate every feature (boosting, max_features=None) whose
+    # whole-feature large-tier histograms fit DML_LARGE_SUB_GB: nodes above this many rows take
+    # the large tier, where the larger of two siblings is derived from the parent's histogram
+    # (GBRT config 6: 6.38 -> 7.32 CV-fits/s at 2048, 7.17 at 8192, 7.27 at 1024)
+    block_max_all: int = 2048
     kg_wave: int = 4
     kg_block: int = 16
     kg_large: int = 16
@@ -391,6 +396,12 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     a.sub_small = tiers.sub_small
     a.sub_cache_d = _sub_cache_stride(d) if d <= tiers.sub_cache_max_d else 0
     a.all_features = int(T > 0 and bool(np.all(specs["max_features"] >= d)))
+    if a.all_features and 0 < tiers.block_max_all < a.block_max:
+        depth = int(min(30, specs["max_depth"].max()))
+        per_level = T * min(a.max_active // tiers.block_max_all + 1, 1 << depth)
+        node_b = d * 256 * (2 * 8 if is_reg else (n_classes + 1) * 4)   # forest.hip ghist_feat_bytes
+        if per_level * node_b <= float(os.environ.get("DML_LARGE_SUB_GB", "4")) * 1e9:
+            a.block_max = tiers.block_max_all
     big = _bigsub_on(tiers, is_reg, n_classes, d, mono_dev) and a.sub_cache_d > 0
     a.bigsub_max = min(tiers.bigsub_max, 256) if big else 0
     if big:
