@@ -301,6 +301,30 @@ DML_HD void reg_quantize(float y, const RegScale& q, int64_t& yq, int64_t& y2q) 
   y2q = reg_round((yd * yd) * q.s2);
 }
 
+// ---- absolute_error (MAE) in fixed point ----------------------------------------------
+// sum w |yq - med| of a set with total weight W and sum w yq S, from the median's prefix
+// (wle / sle: weight and sum w yq of the ranks up to and including the median, in y order):
+// med (2 wle - W) + (S - 2 sle), in modular unsigned arithmetic -- exact whenever the result
+// fits (it is < 1.5 * 2^62: W |med| <= 2 sum w |yq| < 2^62 under reg_exponents_counts)
+DML_HD int64_t mae_absdev(int64_t W, int64_t S, int64_t medq, int64_t wle, int64_t sle) {
+  const uint64_t a = (uint64_t)medq * (uint64_t)(2 * wle - W);
+  const uint64_t b = (uint64_t)S - 2ull * (uint64_t)sle;
+  return (int64_t)(a + b);
+}
+
+// node value of an MAE node, {W, W med, ab + W med^2}: v1 / v0 is the median predict reads
+// (sklearn's WeightedMedianCalculator: the mean of the two middle values when the prefix
+// weight lands exactly on W / 2) and mse_impurity(v) the MAE impurity; ab is the exact abs
+// deviation (c / cs: the prefix up to and including the lower median, medq its target).
+// Both builders call this with the same integers, so their node values are identical.
+DML_HD double mae_node_value(int64_t W, int64_t S, int64_t c, int64_t cs, int64_t medq, double ylo, double yhi,
+                             bool tie, const RegScale& q, double* v) {
+  const double med = tie ? (ylo + yhi) / 2.0 : ylo;
+  const double ab = (double)mae_absdev(W, S, medq, c, cs) * q.i1;
+  v[0] = (double)W; v[1] = (double)W * med; v[2] = ab + (double)W * med * med;
+  return ab;
+}
+
 constexpr uint64_t kRegLo32 = 0xFFFFFFFFull;
 // the double channels of integer sums (w | rows << 32, sum w yq, sum w y2q)
 DML_HD double reg_w(uint64_t wr) { return (double)(wr & kRegLo32); }

@@ -44,34 +44,35 @@ struct Data {
 
 struct Job { int node, start, count, depth; uint64_t key; double lo, hi; };
 
-// Fenwick tree over the y-ranks of one node's rows: weights and weighted targets
+// Fenwick tree over the y-ranks of one node's rows: integer weights and weighted
+// fixed-point targets (w yq, forest_common.h reg_quantize), so the abs deviations -- and the
+// MAE split choice -- are exact integers, the same on the HIP builder (forest_mae.hip)
 struct Fenwick {
   int m = 0;
-  std::vector<double> w, s;
-  void reset(int m_) { m = m_; w.assign(m + 1, 0.0); s.assign(m + 1, 0.0); }
-  void fill(const double* ws, const double* ys) {   // every rank present: linear build
-    for (int i = 1; i <= m; ++i) { w[i] = ws[i - 1]; s[i] = ws[i - 1] * ys[i - 1]; }
+  std::vector<int64_t> w, s;
+  void reset(int m_) { m = m_; w.assign(m + 1, 0); s.assign(m + 1, 0); }
+  void fill(const int64_t* ws, const int64_t* yq) {   // every rank present: linear build
+    for (int i = 1; i <= m; ++i) { w[i] = ws[i - 1]; s[i] = ws[i - 1] * yq[i - 1]; }
     for (int i = 1; i <= m; ++i) {
       const int j = i + (i & -i);
       if (j <= m) { w[j] += w[i]; s[j] += s[i]; }
     }
   }
-  void add(int r, double dw, double ds) {
+  void add(int r, int64_t dw, int64_t ds) {
     for (int i = r + 1; i <= m; i += i & -i) { w[i] += dw; s[i] += ds; }
   }
-  // sum w |y - median| of the set (total weight W, weighted sum S): the deviation is the
+  // sum w |yq - median| of the set (total weight W, weighted sum S): the deviation is the
   // same for every median of the set, so take the lowest rank whose prefix reaches W/2
-  double absdev(double W, double S, const double* ys) const {
+  int64_t absdev(int64_t W, int64_t S, const int64_t* yq) const {
     int pos = 0, step = 1;
     while (step * 2 <= m) step *= 2;
-    double cw = 0.0, cs = 0.0;
+    int64_t cw = 0;
     for (; step; step >>= 1)
-      if (pos + step <= m && cw + w[pos + step] < W * 0.5) { pos += step; cw += w[pos]; cs += s[pos]; }
-    const double med = ys[pos];   // rank pos (0-based) is the first with prefix >= W/2
-    double wle = 0.0, sle = 0.0;
-    for (int i = pos + 1; i > 0; i -= i & -i) { wle += w[i]; sle += s[i]; }
-    return med * wle - sle + (S - sle) - med * (W - wle);
+      if (pos + step <= m && 2 * (cw + w[pos + step]) < W) { pos += step; cw += w[pos]; }
+    return mae_absdev(W, S, yq[pos], prefix_w(pos), prefix_s(pos));
   }
+  int64_t prefix_w(int pos) const { int64_t r = 0; for (int i = pos + 1; i > 0; i -= i & -i) r += w[i]; return r; }
+  int64_t prefix_s(int pos) const { int64_t r = 0; for (int i = pos + 1; i > 0; i -= i & -i) r += s[i]; return r; }
 };
 
 static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& out) {
@@ -108,27 +109,28 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
   const bool mae = D.is_reg && s.criterion == kMAE;
   std::vector<double> nabs;
   std::vector<uint32_t> ord;
-  std::vector<double> ys, ws;
+  std::vector<double> ys;
+  std::vector<int64_t> ws, yqs;
   std::vector<int32_t> rank_of(mae ? D.n : 0);
   Fenwick fl, fr;
   auto sort_rows = [&](int start, int count) {   // node rows by (y, row id)
     ord.assign(rows.begin() + start, rows.begin() + start + count);
     std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return Y[a] < Y[b] || (Y[a] == Y[b] && a < b); });
-    ys.resize(count); ws.resize(count);
-    for (int k = 0; k < count; ++k) { ys[k] = (double)Y[ord[k]]; ws[k] = (double)wrow[ord[k]]; rank_of[ord[k]] = k; }
+    ys.resize(count); ws.resize(count); yqs.resize(count);
+    for (int k = 0; k < count; ++k) {
+      ys[k] = (double)Y[ord[k]]; ws[k] = (int64_t)wrow[ord[k]]; yqs[k] = YQ[ord[k]]; rank_of[ord[k]] = k;
+    }
   };
   auto mae_node = [&](int start, int count, double* v) {   // sklearn WeightedMedianCalculator
     sort_rows(start, count);
-    double W = 0.0;
-    for (int k = 0; k < count; ++k) W += ws[k];
-    double c = 0.0;
+    int64_t W = 0, S = 0;
+    for (int k = 0; k < count; ++k) { W += ws[k]; S += ws[k] * yqs[k]; }
+    int64_t c = 0, cs = 0;
     int k = 0;
-    while (k < count && c < W * 0.5) c += ws[k++];
-    const double med = (c == W * 0.5 && k < count) ? (ys[k - 1] + ys[k]) / 2.0 : ys[k > 0 ? k - 1 : 0];
-    double ab = 0.0;
-    for (int i = 0; i < count; ++i) ab += ws[i] * fabs(ys[i] - med);
-    v[0] = W; v[1] = W * med; v[2] = ab + W * med * med;
-    return ab;
+    while (k < count && 2 * c < W) { c += ws[k]; cs += ws[k] * yqs[k]; ++k; }
+    const int km = k > 0 ? k - 1 : 0;
+    return mae_node_value(W, S, c, cs, yqs[km], ys[km], (2 * c == W && k < count) ? ys[k] : ys[km],
+                          2 * c == W && k < count, D.rq, v);
   };
   if (mae && !rows.empty()) nabs.push_back(mae_node(0, (int)rows.size(), root.data()));
   // class weights multiply the (integer) class sums: root statistics here, every
@@ -181,11 +183,11 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
     const uint32_t* nr = rows.data() + jb.start;
     double mae_l = 0.0, mae_r = 0.0;   // abs sums of the best split's sides
     double best_mid = 0.0;             // mean of the best split's two side values
-    double Wn = 0.0, Sn = 0.0;
+    int64_t Wn = 0, Sn = 0;
     int bcnt[256];
     if (mae) {
       sort_rows(jb.start, jb.count);
-      for (int k = 0; k < jb.count; ++k) { Wn += ws[k]; Sn += ws[k] * ys[k]; }
+      for (int k = 0; k < jb.count; ++k) { Wn += ws[k]; Sn += ws[k] * yqs[k]; }
     }
     while (nonconst < s.max_features && pos < D.d) {
       const int f = feature_at(fp, pos, D.d);
@@ -203,14 +205,14 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
         std::vector<uint32_t> byb(jb.count);
         { std::vector<int> cur(boff.begin(), boff.end() - 1);
           for (int i = 0; i < jb.count; ++i) byb[cur[D.Xb[(int64_t)nr[i] * D.ld + f]]++] = nr[i]; }
-        fl.reset(jb.count); fr.reset(jb.count); fr.fill(ws.data(), ys.data());
-        double Wl = 0.0, Sl = 0.0;
+        fl.reset(jb.count); fr.reset(jb.count); fr.fill(ws.data(), yqs.data());
+        int64_t Wl = 0, Sl = 0;
         int nl = 0;
         for (int b = 0; b < 255; ++b) {
           if (!bcnt[b]) continue;
           for (int i = boff[b]; i < boff[b + 1]; ++i) {
             const int k = rank_of[byb[i]];
-            const double w = ws[k], wy = w * ys[k];
+            const int64_t w = ws[k], wy = w * yqs[k];
             fl.add(k, w, wy); fr.add(k, -w, -wy);
             Wl += w; Sl += wy;
           }
@@ -219,12 +221,13 @@ static void build_tree(const Data& D, const TreeSpec& s_in, int64_t t, CpuTree& 
           if (nrr == 0) break;
           nc = true;
           if (nl < s.min_samples_leaf || nrr < s.min_samples_leaf) continue;
-          if (side_too_light(s, Wl, Wn - Wl)) continue;
-          const double al = fl.absdev(Wl, Sl, ys.data()), ar = fr.absdev(Wn - Wl, Sn - Sl, ys.data());
-          const double g = -(al + ar);
+          if (side_too_light(s, (double)Wl, (double)(Wn - Wl))) continue;
+          const int64_t al = fl.absdev(Wl, Sl, yqs.data()), ar = fr.absdev(Wn - Wl, Sn - Sl, yqs.data());
+          // the gain -(al + ar) as a double of the exact integer sum (the HIP builder's value)
+          const double g = -((double)al + (double)ar);
           if (g > g_best) {
             g_best = g; b_best = b;
-            if (g > best_gain) { mae_l = al; mae_r = ar; best_left[0] = Wl; }
+            if (g > best_gain) { mae_l = (double)al * D.rq.i1; mae_r = (double)ar * D.rq.i1; best_left[0] = (double)Wl; }
           }
         }
         if (nc) {

@@ -8,7 +8,7 @@ of whole fits, then every fit's held-out rows are predicted in one launch.
 
 Supported: n_estimators, criterion (gini/entropy/log_loss; squared_error; friedman_mse, whose splits are
 squared_error's; poisson -- sklearn's proxy sum_l log(mean_l) + sum_r log(mean_r);
-absolute_error: exact, on the host builder), max_depth,
+absolute_error: exact weighted medians, on its own GPU builder), max_depth,
 min_samples_split, min_samples_leaf (int or fraction), max_features (sqrt/log2/None/
 int/float), bootstrap, max_samples, min_impurity_decrease, max_leaf_nodes (sklearn's
 best-first tree: the grown tree is cut to its best-first top, ops/forest_ops.py
@@ -21,7 +21,9 @@ ccp_alpha > 0 prunes every grown tree to its minimal cost-complexity subtree
 (bootstrap counts x class weights, as sklearn's sample weights) inside the builders;
 monotonic_cst (regression and binary classification, sklearn's bounds and clipping) grows
 on the HIP builder in every tier (per-node bounds, identical to the host builder's trees);
-criterion="absolute_error" grows on the C++ host builder.
+criterion="absolute_error" grows on the GPU MAE builder (csrc/kernels/forest_mae.hip; rows kept
+in target order, exact fixed-point abs deviations) -- node for node the C++ host builder's trees,
+which grow it on CPU data.
 """
 from __future__ import annotations
 
@@ -285,7 +287,7 @@ class ForestFamily(Family):
                 if t.params.get("criterion") == forest_ops.MAE or t.params.get("monotonic_cst") is not None:
                     raise ParamError("criterion='absolute_error' and monotonic_cst need every row on one rank: "
                                      "run this job with parallelism='task'")
-        # absolute_error trees grow on the host builder (forest_cpu.cpp): batch them apart
+        # absolute_error trees grow on their own builder (forest_mae.hip / forest_cpu.cpp): batch them apart
         tasks_in = tasks
         tasks = sorted(tasks, key=_host_only)
         with trace.range("forest_budget"):
@@ -443,9 +445,13 @@ class ForestFamily(Family):
             fb = forest_dp.build_dp(Xb, data.y_cls, None if not is_reg else data.y_reg, data.roles, specs,
                                     data.n_classes, is_reg, data.r0, reduce=data.all_reduce, cw=cw, comm=data,
                                     tree_chunk=tree_chunk)
+        elif _host_only(batch[0]) and data.is_gpu and os.environ.get("DML_MAE_GPU", "1") != "0":
+            # absolute_error on the GPU: the MAE builder (forest_mae.hip), node for node the
+            # host builder's trees (rows in target order, exact fixed-point abs deviations)
+            fb = forest_ops.build_gpu_mae(Xb, data.y_reg, data.roles, specs)
         elif _host_only(batch[0]):
-            # exact absolute_error (per-node weighted medians) grows on the host builder;
-            # the pruning / refine / predict steps below run where the data lives
+            # exact absolute_error (per-node weighted medians) on the host builder (CPU data,
+            # or DML_MAE_GPU=0); the pruning / refine / predict steps below run where the data lives
             mono = _mono_table(batch, Xb.shape[1], is_reg)
             ycls = None if is_reg else np.asarray(data.y_enc, dtype=np.int32)
             fb = forest_ops.build_cpu(Xb.cpu().numpy(), ycls, None if not is_reg else data.y_reg.cpu().numpy(),

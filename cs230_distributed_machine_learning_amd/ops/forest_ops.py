@@ -26,7 +26,7 @@ import torch
 from ..utils import native
 from ..utils import trace
 
-GINI, ENTROPY, MSE, POISSON, MAE, FRIEDMAN = 0, 1, 2, 3, 4, 5   # MAE: host builder only (build_cpu)
+GINI, ENTROPY, MSE, POISSON, MAE, FRIEDMAN = 0, 1, 2, 3, 4, 5   # MAE: build_cpu / build_gpu_mae
 INT32_MAX = 2**31 - 1
 
 
@@ -316,6 +316,58 @@ def reg_exponents(yreg, n: int, ystride: int = 0, targets: int = 1) -> tuple[int
 
 def _n_targets(specs: np.ndarray, ystride: int) -> int:
     return int(specs["target"].max()) + 1 if ystride > 0 and len(specs) else 1
+
+
+def build_gpu_mae(Xb: torch.Tensor, yreg: torch.Tensor, roles: torch.Tensor, specs: np.ndarray) -> ForestBuild:
+    """criterion="absolute_error" regression trees on the GPU (csrc/kernels/forest_mae.hip):
+    rows kept in (y, row id) order, exact fixed-point abs deviations -- the host builder's
+    trees node for node.  ``yreg`` float32 [n] on the device."""
+    lib = native.hip_lib()
+    dev = Xb.device
+    n, d = Xb.shape
+    T = len(specs)
+    y = yreg.float().contiguous()
+    specs_dev = torch.from_numpy(specs.view(np.uint8).copy()).to(dev)
+    e1, e2 = reg_exponents(y, n)
+    perm = torch.sort(y, stable=True).indices.to(torch.int32).contiguous()   # (y, row id) order
+    counts = torch.zeros(T, dtype=torch.int32, device=dev)
+    a = native.MaeArgs()
+    a.Xb, a.ld, a.n, a.d = native.ptr(Xb), Xb.stride(0), n, d
+    a.yreg, a.roles, a.specs, a.T, a.perm = native.ptr(y), native.ptr(roles), native.ptr(specs_dev), T, native.ptr(perm)
+    a.yq_e1, a.yq_e2, a.counts = e1, e2, native.ptr(counts)
+    stream = native.stream_handle(dev)
+    t0 = time.perf_counter()
+    with trace.range("forest_count"):
+        if lib.dml_mae_count(ctypes.byref(a), stream):
+            raise RuntimeError(f"dml_mae_count failed: {native.hip_error(lib)}")
+        cnt = counts.cpu().numpy().astype(np.int64)
+    row_off = np.zeros(T + 1, dtype=np.int64)
+    np.cumsum(cnt, out=row_off[1:])
+    row_off_dev = torch.from_numpy(row_off).to(dev)
+    pool_cap = _pool_bound(cnt, specs) + T
+    rows_a = torch.empty(max(1, int(row_off[-1])), dtype=torch.int32, device=dev)
+    rows_b = torch.empty_like(rows_a)
+    nodes = torch.empty((pool_cap, 2), dtype=torch.int32, device=dev)
+    vals = torch.empty((pool_cap, 3), dtype=torch.float64, device=dev)
+    nabs = torch.empty(pool_cap, dtype=torch.float64, device=dev)
+    osz = int(lib.dml_mae_sizeof_open())
+    open_a = torch.empty(pool_cap * osz, dtype=torch.uint8, device=dev)
+    open_b = torch.empty_like(open_a)
+    counters = torch.zeros(8, dtype=torch.int32, device=dev)
+    tree_W = torch.empty(T, dtype=torch.float64, device=dev)
+    a.row_off, a.rows_a, a.rows_b = native.ptr(row_off_dev), native.ptr(rows_a), native.ptr(rows_b)
+    a.nodes, a.vals, a.nabs, a.pool_cap = native.ptr(nodes), native.ptr(vals), native.ptr(nabs), pool_cap
+    a.open_a, a.open_b, a.open_cap = native.ptr(open_a), native.ptr(open_b), pool_cap
+    a.counters, a.tree_W = native.ptr(counters), native.ptr(tree_W)
+    with trace.range("forest_build"):
+        if lib.dml_mae_build(ctypes.byref(a), stream):
+            raise RuntimeError(f"dml_mae_build failed: {native.hip_error(lib)}")
+    if a.status_out:
+        raise RuntimeError(f"dml_mae_build status {a.status_out} (1: node pool overflow)")
+    P = int(a.n_nodes_out)
+    return ForestBuild(nodes[:P], vals[:P], T, 3, True, 1,
+                       stats={"levels": int(a.levels_out), "nodes": P, "build_s": time.perf_counter() - t0,
+                              "builder": "gpu-mae"})
 
 
 def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[torch.Tensor], roles: torch.Tensor,

@@ -99,6 +99,13 @@ GbStageArgs = _i64_struct(
      "ycls", "slot_sum", "slot_node", "slot_val", "raw"],
 )
 GbGradArgs = _i64_struct("GbGradArgs", ["n", "K", "A", "fit_raw", "fit_loss", "raw", "ycls", "yreg", "grad", "tgt"])
+# csrc/kernels/forest_mae.hip (criterion="absolute_error" builder)
+MaeArgs = _i64_struct(
+    "MaeArgs",
+    ["Xb", "ld", "n", "d", "yreg", "roles", "specs", "T", "perm", "yq_e1", "yq_e2", "counts", "row_off", "rows_a",
+     "rows_b", "nodes", "vals", "nabs", "pool_cap", "open_a", "open_b", "open_cap", "counters", "tree_W",
+     "n_nodes_out", "levels_out", "status_out"],
+)
 LrGradArgs = _i64_struct("LrGradArgs", ["rh", "rl", "unused", "xth", "xtl", "m_tiles", "n_tiles", "Kp", "S", "Kc", "out"])
 
 
@@ -218,6 +225,10 @@ def _register_optional(lib) -> None:
         "dml_gb_stage": (c_i32, [ctypes.POINTER(GbStageArgs), c_vp]),
         "dml_gb_grad": (c_i32, [ctypes.POINTER(GbGradArgs), c_vp]),
         "dml_exp_hist": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
+        "dml_mae_sizeof_args": (c_i32, []),
+        "dml_mae_sizeof_open": (c_i32, []),
+        "dml_mae_count": (c_i32, [ctypes.POINTER(MaeArgs), c_vp]),
+        "dml_mae_build": (c_i32, [ctypes.POINTER(MaeArgs), c_vp]),
     }
     for name, (res, args) in table.items():
         fn = getattr(lib, name, None)
@@ -228,6 +239,8 @@ def _register_optional(lib) -> None:
         if (lib.dml_gb_sizeof_stage_args() != ctypes.sizeof(GbStageArgs)
                 or lib.dml_gb_sizeof_grad_args() != ctypes.sizeof(GbGradArgs)):
             raise RuntimeError("GBRT stage argument layout mismatch between HIP library and Python")
+    if getattr(lib, "dml_mae_sizeof_args", None) is not None and lib.dml_mae_sizeof_args() != ctypes.sizeof(MaeArgs):
+        raise RuntimeError("MAE builder argument layout mismatch between HIP library and Python")
     if getattr(lib, "dml_lr_sizeof_fwd_args", None) is not None:
         if (lib.dml_lr_sizeof_fwd_args() != ctypes.sizeof(LrFwdArgs)
                 or lib.dml_lr_sizeof_grad_args() != ctypes.sizeof(LrGradArgs)):

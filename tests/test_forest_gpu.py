@@ -335,10 +335,10 @@ def test_gpu_predict_proba_matches_cpu():
 
 @pytest.mark.gpu
 def test_gpu_absolute_error_family_matches_host_path():
-    """criterion='absolute_error' on device-resident data: the host builder grows the
-    trees (per-node medians), then pruning, refine and the HIP predict + scoring run on
-    the GPU -- the same CV scores as the all-host path, and a mixed MAE / squared_error
-    grid keeps each candidate's own criterion."""
+    """criterion='absolute_error' on device-resident data: the GPU MAE builder grows the
+    trees (forest_mae.hip), then pruning, refine and the HIP predict + scoring run on the
+    GPU -- the same CV scores as the all-host path, and a mixed MAE / squared_error grid
+    keeps each candidate's own criterion."""
     from cs230_distributed_machine_learning_amd.data.device import DeviceData
     from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
 
@@ -352,7 +352,7 @@ def test_gpu_absolute_error_family_matches_host_path():
     cpu = run_candidates(DeviceData(X, y, False, "cpu"), spec, range(len(cands)))
     for i, (g, c) in enumerate(zip(gpu, cpu)):
         assert g.ok and c.ok
-        # absolute_error: the same host-built trees, predicted by the HIP kernel; the
+        # absolute_error: trees equal to the host builder's, predicted by the HIP kernel; the
         # squared_error candidates come from the GPU builder, whose float histogram sums
         # make trees close to, not equal to, the host's (test_gpu_regression_close_to_cpu)
         tol = 1e-6 if cands[i]["criterion"] == "absolute_error" else 2e-2
@@ -450,3 +450,61 @@ def test_gpu_whole_histogram_levels_match_cpu(is_reg, monkeypatch):
     gc = _canon(g.nodes.cpu().numpy(), g.vals.cpu().numpy(), T)
     assert gc == _canon(c.nodes, c.vals, T)
     assert gc == _canon(g0.nodes.cpu().numpy(), g0.vals.cpu().numpy(), T)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(),                                               # bootstrap, full depth
+    dict(msl=3, max_depth=7),
+    dict(k=3, mid=0.02),                                  # feature sampling, min_impurity_decrease
+    dict(bootstrap=0, mwf=0.01, mss=6),
+])
+def test_gpu_absolute_error_trees_match_cpu(kw):
+    """criterion="absolute_error" on the GPU MAE builder (forest_mae.hip): rows in target
+    order, exact fixed-point abs deviations -- the host builder's trees node for node
+    (splits, medians, abs deviations in the node values)."""
+    rng = np.random.RandomState(7)
+    n, d = 6000, 6
+    X = rng.randint(0, 20, size=(n, d)).astype(np.float32)
+    X[:, 3] = rng.randn(n)                                 # one continuous column
+    y = (X[:, 0] - 0.7 * X[:, 1] + 3 * rng.standard_t(2, n)).astype(np.float32)
+    y[rng.rand(n) < 0.1] = 0.0                             # repeated targets: median ties
+    dev = torch.device("cuda:0")
+    Xb = binning.bin_matrix(torch.from_numpy(X).to(dev), binning.quantile_edges(torch.from_numpy(X).to(dev)))
+    roles, _ = make_split_roles(y, 3, False, holdout=False)
+    specs = _specs(3, 3, d, criterion=forest_ops.MAE, **{k: v for k, v in kw.items() if k != "k"},
+                   k=kw.get("k", d))
+    T = len(specs)
+    g = forest_ops.build_gpu_mae(Xb, torch.from_numpy(y).to(dev), torch.from_numpy(roles).to(dev), specs)
+    c = forest_ops.build_cpu(Xb.cpu().numpy(), None, y, roles, specs, 1, True)
+    gc = _canon(g.nodes.cpu().numpy(), g.vals.cpu().numpy(), T)
+    cc = _canon(c.nodes, c.vals, T)
+    assert sum(map(len, gc)) == sum(map(len, cc)) > 10 * T
+    assert gc == cc
+
+
+@pytest.mark.parametrize("extra,seeds", [({}, (1, 3, 6)), ({"max_depth": 4}, (1, 2)),
+                                         ({"max_leaf_nodes": 12}, (1, 2)), ({"ccp_alpha": 0.05}, (1, 2))])
+def test_gpu_absolute_error_matches_sklearn(extra, seeds):
+    """The GPU-grown absolute_error trees against sklearn's (exactly binned columns), the
+    same check (and seeds: full-depth trees on other seeds hit equal-gain ties between
+    features) tests/test_models_cpu.py makes for the host builder."""
+    from sklearn.ensemble import RandomForestRegressor
+
+    from cs230_distributed_machine_learning_amd.data.device import DeviceData
+    from cs230_distributed_machine_learning_amd.engine.service import refit_model
+
+    rng = np.random.default_rng(3)
+    X = rng.integers(0, 8, size=(400, 4)).astype(np.float32)
+    y = np.round((1.5 * X[:, 0] - X[:, 1] + rng.standard_t(2, 400)) * 8) / 8
+    for seed in seeds:
+        params = {"n_estimators": 1, "bootstrap": False, "max_features": None, "criterion": "absolute_error",
+                  "min_samples_leaf": 3, "random_state": seed, **extra}
+        m = refit_model({"model_type": "RandomForestRegressor", "scoring": None}, params,
+                        DeviceData(X, y, False, "cuda:0"))
+        sk = RandomForestRegressor(**params).fit(X, y).estimators_[0].tree_
+        nodes, vals = np.asarray(m["nodes"]), np.asarray(m["vals"])
+        leaves = nodes[:, 0] < 0
+        ours = np.sort(vals[leaves, 1] / vals[leaves, 0])
+        ref = np.sort(sk.value[sk.children_left == -1][:, 0, 0])
+        assert len(ours) == len(ref)
+        np.testing.assert_allclose(ours, ref, rtol=1e-9)
