@@ -94,8 +94,14 @@ def maybe_stop_in_collective(rank: int, what: str) -> None:
     """Fault injection on entering a side-group collective (``load`` / ``scores``):
     ``DML_STOP_RANK_IN`` hangs the rank (SIGSTOP), ``DML_FAIL_RANK_IN`` makes it raise before
     the collective (an OOM while its peers are already inside), ``DML_COLL_DELAY_S`` delays
-    every rank (a long broadcast)."""
+    every rank (a long broadcast), ``DML_DELAY_RANK_IN`` one rank (a slow peer)."""
     delay = float(os.environ.get("DML_COLL_DELAY_S", "0") or 0.0)
+    # DML_DELAY_RANK_IN="rank:kind:seconds": ONE slow (not hung) rank entering that collective
+    slow = os.environ.get("DML_DELAY_RANK_IN", "")
+    if slow:
+        r, k, sec = slow.split(":")
+        if int(r) == rank and k in (what, "*"):
+            delay += float(sec)
     if delay > 0:
         import time
 

@@ -40,10 +40,26 @@ def _job(dataset, target, model, grid, cv=3, base=None):
 
 
 DATASETS = [("iris", "species"), ("wine", "target"), ("breast_cancer", "target")]
+# the heavy rehearsal's extra table: a 4.8 MB float32 broadcast to every rank, slices of seconds
+HEAVY = ("synth", "target", "classification?n=62500&d=20&informative=8&noise=1.0&seed=4&gen=blocks")
 
 
-def _jobs():
-    """(session, dataset, body) of the rehearsal: 2 sessions x 3 datasets, mixed families."""
+def _datasets(heavy: bool):
+    return DATASETS + ([HEAVY[:2]] if heavy else [])
+
+
+def _register(ctl, sid, heavy: bool):
+    for name, _t in DATASETS:
+        st, _ = ctl.download_data(sid, {"dataset_url": name, "dataset_name": name, "dataset_type": "sklearn"})
+        assert st == 200, name
+    if heavy:
+        st, _ = ctl.download_data(sid, {"dataset_url": HEAVY[2], "dataset_name": HEAVY[0], "dataset_type": "synthetic"})
+        assert st == 200, HEAVY
+
+
+def _jobs(heavy: bool = False):
+    """(session, dataset, body) of the rehearsal: 2 sessions x 3 datasets, mixed families
+    (+ the heavy table's RandomForest and LogisticRegression searches)."""
     rf = {"max_depth": [2, 4, None], "min_samples_leaf": [1, 3]}
     lr = {"C": [0.1, 1.0, 10.0], "solver": ["lbfgs", "liblinear"]}
     gb = {"n_estimators": [10, 20], "max_depth": [2, 3]}
@@ -54,14 +70,21 @@ def _jobs():
                                  ("LogisticRegression", lr, {"max_iter": 300}),
                                  ("GradientBoostingClassifier", gb, {"random_state": 5})][(s + d) % 3]
             out.append((s, name, _job(name, tgt, model, grid, base=base)))
+    if heavy:
+        out.append((0, HEAVY[0], _job(HEAVY[0], HEAVY[1], "RandomForestClassifier",
+                                      {"max_depth": [8, None], "min_samples_leaf": [1, 4]},
+                                      base={"n_estimators": 16, "random_state": 1})))
+        out.append((1, HEAVY[0], _job(HEAVY[0], HEAVY[1], "LogisticRegression", {"C": [0.1, 1.0]},
+                                      base={"max_iter": 200})))
     return out
 
 
-def _rank_main(rank, world, port, root, kill, outq):
+def _rank_main(rank, world, port, root, kill, outq, heavy=False, env_extra=None):
     env = dict(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                LOCAL_RANK=str(rank), OMP_NUM_THREADS="1", DML_DEAD_AFTER_S="3")
     if kill is not None:
         env["DML_KILL_RANK_AFTER"] = f"{kill}:1"     # rank `kill` dies holding its 2nd slice
+    env.update(env_extra or {})
     os.environ.update(env)
     import threading
 
@@ -83,14 +106,11 @@ def _rank_main(rank, world, port, root, kill, outq):
     def drive():
         try:
             sids = [ctl.create_session()[1]["session_id"] for _ in range(2)]
-            for name, _t in DATASETS:
-                st, _ = ctl.download_data(sids[0], {"dataset_url": name, "dataset_name": name,
-                                                    "dataset_type": "sklearn"})
-                assert st == 200, name
+            _register(ctl, sids[0], heavy)
             t0 = time.time()
             ops0 = runner.store_ops()
             acks = []
-            for s, name, body in _jobs():   # every job submitted at once: concurrent searches
+            for s, name, body in _jobs(heavy):   # every job submitted at once: concurrent searches
                 st, ack = ctl.train(sids[s], body)
                 assert st in (200, 202), ack
                 acks.append((s, name, body["model_details"]["model_type"], ack["job_id"]))
@@ -131,17 +151,16 @@ def _rank_main(rank, world, port, root, kill, outq):
     os._exit(0)       # a peer may be dead: skip the collective teardown
 
 
-def local_scores(body_jobs=None) -> list:
+def local_scores(body_jobs=None, heavy: bool = False) -> list:
     """The same jobs through the one-process LocalRunner (per-candidate CV scores)."""
     from cs230_distributed_machine_learning_amd.config import Config
     from cs230_distributed_machine_learning_amd.engine.service import Controller
 
     ctl = Controller(Config(data_root=tempfile.mkdtemp(prefix="dml_local_"), device="cpu", chunk_target_s=0.0))
     sid = ctl.create_session()[1]["session_id"]
-    for name, _t in DATASETS:
-        ctl.download_data(sid, {"dataset_url": name, "dataset_name": name, "dataset_type": "sklearn"})
+    _register(ctl, sid, heavy)
     out = []
-    for s, name, body in (body_jobs or _jobs()):
+    for s, name, body in (body_jobs or _jobs(heavy)):
         st, ack = ctl.train(sid, body)
         ctl.table.wait_finished(ack["job_id"], timeout=600)
         res = (ctl.check_status(sid, ack["job_id"])[1].get("job_result") or {}).get("results") or []
@@ -150,14 +169,15 @@ def local_scores(body_jobs=None) -> list:
     return out
 
 
-def run(world: int = 8, kill=None, timeout_s: float = 900.0) -> dict:
+def run(world: int = 8, kill=None, timeout_s: float = 900.0, heavy: bool = False, env_extra=None) -> dict:
     import torch.multiprocessing as mp
 
     root = tempfile.mkdtemp(prefix="dml_rehearsal_")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, root, kill, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, root, kill, q, heavy, env_extra))
+             for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -180,8 +200,9 @@ if __name__ == "__main__":
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--kill", type=int, default=None)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--heavy", action="store_true", help="add the 62.5k x 20 table's RF / LR searches")
     args = ap.parse_args()
-    r = run(args.world, args.kill)
+    r = run(args.world, args.kill, heavy=args.heavy)
     line = json.dumps(r)
     print(line)
     if args.json:

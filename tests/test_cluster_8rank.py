@@ -42,3 +42,19 @@ def test_eight_ranks_with_a_killed_rank():
     r = cr.run(world=8, kill=5, timeout_s=600)
     _check(r, [5])
     assert r["exitcodes"][5] == 17   # died by the injected crash, holding a slice
+
+
+def test_eight_ranks_heavy_table_with_a_slow_rank_in_the_scores_gather():
+    """Round-3 verdict: the rehearsal also needs slices of seconds, a multi-MB broadcast and
+    a slow (not dead) rank inside a scores gather.  A 62.5k x 20 table joins the three small
+    ones (RandomForest slices of seconds on one CPU each); rank 3 enters every scores
+    gather 4 s late (DML_DELAY_RANK_IN, below the side group's timeout): every job still
+    completes with its scores from the collective, equal to the one-process runner's."""
+    import cluster_rehearsal as cr
+
+    r = cr.run(world=8, kill=None, timeout_s=900, heavy=True,
+               env_extra={"DML_DELAY_RANK_IN": "3:scores:4", "DML_SIDE_TIMEOUT_S": "60"})
+    _check(r, [])
+    assert all(j["scores_via"] == ["gloo"] for j in r["jobs"]), [j["scores_via"] for j in r["jobs"]]
+    norm = lambda v: json.loads(json.dumps(v))
+    assert norm([j["scores"] for j in r["jobs"]]) == norm(cr.local_scores(heavy=True))
