@@ -3431,9 +3431,30 @@ static bool ensure_bytes(void*& p, size_t& have, size_t need) {
   return true;
 }
 
+// free the current device's whole-histogram buffers (ops/forest_ops.py _Arena.clear: another
+// family needs the HBM); the next whole-histogram level allocates them again
+static int release_full_bufs() {
+  FullBufs* b = full_bufs();
+  if (!b) return 0;
+  if (b->gf[0] || b->gf[1] || b->pinfo) {
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
+    for (int i = 0; i < 2; ++i) {
+      if (b->gf[i]) (void)hipFree(b->gf[i]);
+      b->gf[i] = nullptr;
+      b->gf_bytes[i] = 0;
+    }
+    if (b->pinfo) (void)hipFree(b->pinfo);
+    b->pinfo = nullptr;
+    b->pi_cap = 0;
+  }
+  return 0;
+}
+
 }  // namespace dml
 
 using namespace dml;
+
+extern "C" int dml_forest_release_scratch() { return release_full_bufs(); }
 
 // kernel-level test hooks (tests/test_forest_gpu.py): wave primitives vs ds_bpermute
 // out layout per block of 64: [sorted | scan | xor1 | xor2 | xor4 | xor8 | xor16 | xor32 |

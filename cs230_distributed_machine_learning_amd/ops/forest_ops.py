@@ -195,6 +195,9 @@ class _Arena:
                 del self.bufs[k]
         if drop:
             torch.cuda.empty_cache()
+        # the builder's own whole-histogram buffers (forest.hip FullBufs, outside this arena)
+        with torch.cuda.device(dev):
+            native.hip_lib().dml_forest_release_scratch()
 
     def held_bytes(self, dev: torch.device) -> int:
         idx = dev.index if dev.index is not None else torch.cuda.current_device()

@@ -225,6 +225,7 @@ def _register_optional(lib) -> None:
         "dml_gb_stage": (c_i32, [ctypes.POINTER(GbStageArgs), c_vp]),
         "dml_gb_grad": (c_i32, [ctypes.POINTER(GbGradArgs), c_vp]),
         "dml_exp_hist": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
+        "dml_forest_release_scratch": (c_i32, []),
         "dml_mae_sizeof_args": (c_i32, []),
         "dml_mae_sizeof_open": (c_i32, []),
         "dml_mae_count": (c_i32, [ctypes.POINTER(MaeArgs), c_vp]),
