@@ -49,6 +49,9 @@
 #else
 #define DML_EVAL_ATTR
 #endif
+#ifndef DML_PART_U2
+#define DML_PART_U2 4          // block-tier partition pass 2: row positions per thread per round
+#endif
 #ifndef DML_NODES_WPE_WAVE
 #define DML_NODES_WPE_WAVE 4   // wave tier (binary): 2 / 3 / 5 / 6 measured slower (ROUND3.md)
 #endif
@@ -1610,14 +1613,25 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
       if (g1 < ngrp) loff[g1] = ex + c0;
     }
     __syncthreads();
-    for (int p = tid; p < cnt; p += NT) {
-      const uint32_t r = rows[p];
-      const int q = p >> 6;
-      const uint64_t m = lflag[q];
-      const int lft = __popcll(m & ((1ull << (p & 63)) - 1ull));
-      const bool left = (m >> (p & 63)) & 1ull;
-      const int l0 = loff[q];
-      c.rows_next[on.start + (left ? l0 + lft : nl + (q * 64 - l0) + ((p & 63) - lft))] = r;
+    // pass 2, U2 positions per thread per round: the row-id loads of a round are issued
+    // (unconditionally, clamped) before its stores, so consecutive rounds do not each wait a
+    // full memory round trip behind the previous round's store
+    constexpr int U2 = DML_PART_U2;
+    for (int p0 = tid; p0 < cnt; p0 += U2 * NT) {
+      uint32_t rr[U2];
+#pragma unroll
+      for (int u = 0; u < U2; ++u) rr[u] = rows[min(p0 + u * NT, cnt - 1)];
+#pragma unroll
+      for (int u = 0; u < U2; ++u) {
+        const int p = p0 + u * NT;
+        if (p >= cnt) break;
+        const int q = p >> 6;
+        const uint64_t m = lflag[q];
+        const int lft = __popcll(m & ((1ull << (p & 63)) - 1ull));
+        const bool left = (m >> (p & 63)) & 1ull;
+        const int l0 = loff[q];
+        c.rows_next[on.start + (left ? l0 + lft : nl + (q * 64 - l0) + ((p & 63) - lft))] = rr[u];
+      }
     }
   } else {
   uint32_t* out = c.rows_next + on.start;
@@ -2977,10 +2991,21 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
   const NodeSpec s = spec_of<-1>(c, st.on.tree);
   const float* ty = c.is_reg ? tree_y(c, s) : nullptr;
   unsigned long long lyy = 0ull;
+  // row ids of DML_PART_U2 256-row steps are loaded (clamped, unconditionally) before the
+  // steps' stores: consecutive steps do not each wait a memory round trip
+  constexpr int U2 = DML_PART_U2;
+  uint32_t rq[U2];
   for (int t0 = r0; t0 < r1; t0 += 256) {
     const int r = t0 + tid;
     const bool valid = r < r1;
-    const uint32_t row = valid ? rows[r] : 0u;
+    const int uq = ((t0 - r0) >> 8) % U2;
+    if (uq == 0) {
+#pragma unroll
+      for (int u = 0; u < U2; ++u) rq[u] = rows[min(r + 256 * u, r1 - 1)];
+    }
+    uint32_t row = rq[0];
+#pragma unroll
+    for (int u = 1; u < U2; ++u) if (uq == u) row = rq[u];
     const int wi = (t0 - r0) / 64;
     const uint64_t ml = lflag[wi + wid];
     const uint64_t vm = valid ? ~0ull : 0ull;
