@@ -175,6 +175,7 @@ int main() {
   forest_case(false, kGini);
   forest_case(false, kEntropy);
   forest_case(true, kMSE);
+  forest_case(true, kMAE);   // integer Fenwick sweep + exact abs deviations (forest_common.h mae_absdev)
   sched_case();
   if (g_fail) {
     std::fprintf(stderr, "%d checks failed\n", g_fail);
