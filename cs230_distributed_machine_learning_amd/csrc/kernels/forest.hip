@@ -3116,6 +3116,11 @@ __global__ __launch_bounds__(256) void k_fill_active(Ctx c) {
   __syncthreads();
   int p = base_s + wcnt[8 + wid] + incl - mine;
   uint32_t* out = c.rows_cur + c.row_off[t];
+  // root sums: per-thread integer partials, one wave reduction, ONE LDS atomic per wave and
+  // channel (a per-row atomic on the same 2-3 addresses serialises every lane of the wave)
+  constexpr int kCW = 8;
+  uint32_t cw8[kCW] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  uint64_t rs0 = 0ull, rs1 = 0ull, rs2 = 0ull;
   for (int i = 0; i < 4; ++i) {
     if (!act[i]) continue;
     const uint32_t r = (uint32_t)(r0 + tid * 4 + i);
@@ -3127,11 +3132,30 @@ __global__ __launch_bounds__(256) void k_fill_active(Ctx c) {
     out[p++] = wd;
     if constexpr (REG) {
       const RegPL q = reg_payload(c, wts[i], tree_y(c, s)[r]);
-      atomicAdd(&racc[0], (unsigned long long)wts[i]);
-      atomicAdd(&racc[1], q.wy);
-      atomicAdd(&racc[2], q.wyy);
+      rs0 += (uint64_t)wts[i]; rs1 += (uint64_t)q.wy; rs2 += (uint64_t)q.wyy;
     } else {
-      atomicAdd(&acc[c.ycls[r]], (double)wts[i]);
+      const int y = c.ycls[r];
+      if (c.C <= kCW) {
+#pragma unroll
+        for (int k = 0; k < kCW; ++k) cw8[k] += (k == y) ? wts[i] : 0u;
+      } else {
+        atomicAdd(&acc[y], (double)wts[i]);
+      }
+    }
+  }
+  if constexpr (REG) {
+    rs0 = wave::sum<uint64_t>(rs0, lane); rs1 = wave::sum<uint64_t>(rs1, lane); rs2 = wave::sum<uint64_t>(rs2, lane);
+    if (lane == 0) {
+      if (rs0) atomicAdd(&racc[0], (unsigned long long)rs0);
+      if (rs1) atomicAdd(&racc[1], (unsigned long long)rs1);
+      if (rs2) atomicAdd(&racc[2], (unsigned long long)rs2);
+    }
+  } else if (c.C <= kCW) {
+#pragma unroll
+    for (int k = 0; k < kCW; ++k) {
+      if (k >= c.C) break;
+      const uint32_t v = wave::sum<uint32_t>(cw8[k], lane);   // integer class weights: exact
+      if (lane == 0 && v) atomicAdd(&acc[k], (double)v);
     }
   }
   __syncthreads();
