@@ -358,6 +358,16 @@ def build_gpu_mae(Xb: torch.Tensor, yreg: torch.Tensor, roles: torch.Tensor, spe
     open_b = torch.empty_like(open_a)
     counters = torch.zeros(8, dtype=torch.int32, device=dev)
     tree_W = torch.empty(T, dtype=torch.float64, device=dev)
+    # nodes of >= big_rows rows evaluate their first P visiting positions on one workgroup
+    # each (a level holds at most rows / big_rows + T of them)
+    big_rows = max(256, int(os.environ.get("DML_MAE_BIG_ROWS", "8192")))
+    P = int(min(d, int(specs["max_features"].max()) + 2)) if T else 1
+    big_cap = int(row_off[-1]) // big_rows + T + 1
+    big_a = torch.empty(big_cap * osz, dtype=torch.uint8, device=dev)
+    big_b = torch.empty_like(big_a)
+    res = torch.empty(big_cap * P * int(lib.dml_mae_sizeof_res()), dtype=torch.uint8, device=dev)
+    a.big_a, a.big_b, a.big_cap = native.ptr(big_a), native.ptr(big_b), big_cap
+    a.res, a.P, a.big_rows = native.ptr(res), P, big_rows
     a.row_off, a.rows_a, a.rows_b = native.ptr(row_off_dev), native.ptr(rows_a), native.ptr(rows_b)
     a.nodes, a.vals, a.nabs, a.pool_cap = native.ptr(nodes), native.ptr(vals), native.ptr(nabs), pool_cap
     a.open_a, a.open_b, a.open_cap = native.ptr(open_a), native.ptr(open_b), pool_cap

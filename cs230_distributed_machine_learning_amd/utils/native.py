@@ -104,7 +104,7 @@ MaeArgs = _i64_struct(
     "MaeArgs",
     ["Xb", "ld", "n", "d", "yreg", "roles", "specs", "T", "perm", "yq_e1", "yq_e2", "counts", "row_off", "rows_a",
      "rows_b", "nodes", "vals", "nabs", "pool_cap", "open_a", "open_b", "open_cap", "counters", "tree_W",
-     "n_nodes_out", "levels_out", "status_out"],
+     "n_nodes_out", "levels_out", "status_out", "big_a", "big_b", "big_cap", "res", "P", "big_rows"],
 )
 LrGradArgs = _i64_struct("LrGradArgs", ["rh", "rl", "unused", "xth", "xtl", "m_tiles", "n_tiles", "Kp", "S", "Kc", "out"])
 
@@ -228,6 +228,7 @@ def _register_optional(lib) -> None:
         "dml_forest_release_scratch": (c_i32, []),
         "dml_mae_sizeof_args": (c_i32, []),
         "dml_mae_sizeof_open": (c_i32, []),
+        "dml_mae_sizeof_res": (c_i32, []),
         "dml_mae_count": (c_i32, [ctypes.POINTER(MaeArgs), c_vp]),
         "dml_mae_build": (c_i32, [ctypes.POINTER(MaeArgs), c_vp]),
     }

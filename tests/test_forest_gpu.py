@@ -458,10 +458,14 @@ def test_gpu_whole_histogram_levels_match_cpu(is_reg, monkeypatch):
     dict(k=3, mid=0.02),                                  # feature sampling, min_impurity_decrease
     dict(bootstrap=0, mwf=0.01, mss=6),
 ])
-def test_gpu_absolute_error_trees_match_cpu(kw):
+@pytest.mark.parametrize("big_rows", [None, "256"])
+def test_gpu_absolute_error_trees_match_cpu(kw, big_rows, monkeypatch):
     """criterion="absolute_error" on the GPU MAE builder (forest_mae.hip): rows in target
     order, exact fixed-point abs deviations -- the host builder's trees node for node
-    (splits, medians, abs deviations in the node values)."""
+    (splits, medians, abs deviations in the node values).  big_rows=256: nodes of >= 256
+    rows take the feature-parallel path (k_mae_eval + k_mae_decide)."""
+    if big_rows:
+        monkeypatch.setenv("DML_MAE_BIG_ROWS", big_rows)
     rng = np.random.RandomState(7)
     n, d = 6000, 6
     X = rng.randint(0, 20, size=(n, d)).astype(np.float32)
