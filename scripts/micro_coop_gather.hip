@@ -13,7 +13,8 @@
 //
 // Each row visit adds G = 10 bins into a per-workgroup LDS histogram (G x 256 u32), as the
 // block tier does.  Table: N rows x 112 B, random row ids.
-//   hipcc --offload-arch=gfx950 -O3 -o /tmp/mcg scripts/micro_coop_gather.hip && /tmp/mcg
+//   hipcc --offload-arch=gfx950 -O3 -o scripts/micro_coop_gather.bin scripts/micro_coop_gather.hip
+//   (run the binary on the GPU box: ./scripts/micro_coop_gather.bin [rows] [visits] [row pitch])
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
