@@ -237,6 +237,14 @@ struct Ctx {
   const int4* pinfo_cur;
   int4* pinfo_next;
   int32_t full_cur, full_prev;
+  // whole-histogram levels: every (large node, visiting position)'s split candidate, from
+  // k_split_full (one wave per feature, all features of all nodes in one launch), selected in
+  // visiting order by k_split_full_select: [slot][d] (+ [CH] for the left sums)
+  double* fr_g;
+  double* fr_mid;
+  double* fr_left;
+  int32_t* fr_b;
+  int32_t* fr_n;
   unsigned long long* lyy;   // [cap_large] regression: sum w y2q of the best split's left rows
   int64_t large_cap;
   int32_t wave_max, block_max, chunk, kg_wave, kg_block, kg_large, slack_wave;
@@ -1067,6 +1075,40 @@ __device__ __forceinline__ typename PLT<MODE>::T word_payload(const Ctx& c, cons
   else return reg_payload(c, w, ty[wd & c.rmask]);
 }
 
+// Pipelined payloads, in two halves.  payload_fetch issues the row's payload LOAD (regression:
+// its target) unconditionally -- an absent row (0xFFFFFFFF) reads row 0 -- right after the step's
+// bin gathers; payload_finish turns it into the payload when the step is consumed.  The old
+// single-step `valid ? word_payload(...) : PL{}` put that load under an exec mask and used its
+// value at once: the compiler then waited with vmcnt(0), i.e. for the NEXT step's bin gathers
+// too, which drained the software pipeline every half-iteration (k_hist_large<2> ISA: one
+// vmcnt(0) per step; 75 % of its wave cycles waiting, profiles/r4_gbrt_hist_large_pmc.txt).
+// Classification payloads live in the packed row word (no load); the unpacked fallback keeps
+// word_payload's own loads.
+struct PRaw {
+  uint32_t wd;
+  float y;
+};
+
+template <int MODE, bool PK = false>
+__device__ __forceinline__ PRaw payload_fetch(const Ctx& c, const float* ty, uint32_t wd) {
+  PRaw r;
+  r.wd = wd;
+  r.y = 0.0f;
+  if constexpr (MODE == 2) r.y = ty[(wd != 0xFFFFFFFFu ? wd : 0u) & c.rmask];
+  return r;
+}
+
+template <int MODE, bool PK = false>
+__device__ __forceinline__ typename PLT<MODE>::T payload_finish(const Ctx& c, const NodeSpec& s, const float* ty,
+                                                                const PRaw& r) {
+  if constexpr (MODE == 2) {
+    const uint32_t w = (PK || c.packed) ? (r.wd >> c.rbits) & 15u : boot_weight(s, r.wd);
+    return reg_payload(c, w, r.y);
+  } else {
+    return word_payload<MODE, PK>(c, s, ty, r.wd);
+  }
+}
+
 template <int MODE, int RP = 3>
 __device__ __forceinline__ void hist_add(typename HT<MODE>::T* hj, const Ctx& c, int b, const typename PLT<MODE>::T& pl) {
 #ifdef DML_X2_ATOMIC   // sensitivity build: every histogram atomic issued twice (the second adds 0)
@@ -1139,21 +1181,31 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
   uint32_t rrow[RPT], rbin[RPT];
   using PL = typename PLT<MODE>::T;
   PL rpl[RPT];
+  PRaw rpr[RPT];
+  // row ids, then the payload loads (payload_fetch: unconditional, so they stay counted in
+  // flight while the bin gathers issue), then the payloads once the gathers are out
   auto load_rows = [&](int base) {
 #pragma unroll
     for (int u = 0; u < RPT; ++u) {
       const int r = base + tid + NT * u;
       rrow[u] = r < cnt ? rows[r] : 0xFFFFFFFFu;
     }
+  };
+  auto fetch_rows = [&]() {
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) rpr[u] = payload_fetch<MODE, PK>(c, ty, rrow[u]);
+  };
+  auto finish_rows = [&]() {
 #pragma unroll
     for (int u = 0; u < RPT; ++u)
-      rpl[u] = rrow[u] != 0xFFFFFFFFu ? word_payload<MODE, PK>(c, s, ty, rrow[u]) : PL{};
+      rpl[u] = rrow[u] != 0xFFFFFFFFu ? payload_finish<MODE, PK>(c, s, ty, rpr[u]) : PL{};
   };
   if (reg_rows) load_rows(0);
 #pragma unroll
   for (int u = 0; u < RPT; ++u) rbin[u] = 0;
   __syncthreads();
   PH(0)
+  if (reg_rows) fetch_rows();
   const int k = s.max_features;
   uint32_t pk[KGMAX];   // register rows: the group's bins packed 4 x u8 per feature (live across eval)
   // wave tier, register rows: the bins of the first KPRE visiting positions are gathered
@@ -1226,6 +1278,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
       }
     }
   }
+  if (reg_rows) finish_rows();
   while (true) {
     // wave-uniform loop state in SGPRs: the per-group bounds (g) are then scalar branches, not
     // exec masks (a masked load merges into a phi whose copies force vmcnt(0) waits)
@@ -1276,7 +1329,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
           for (int j = 0; j < G; ++j) b[j] |= (uint32_t)xr[fj[j] + ((uint32_t)c.n >> 31)];
 #endif
         };
-        auto consume = [&](int base, bool valid, const uint32_t* b, const PL& pl) {
+        auto consume = [&](int base, bool valid, const uint32_t* b, const PRaw& pr) {
           if (NT == 256 && pos == 0 && valid) {
             uint32_t w4[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -1284,6 +1337,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
             *(uint4*)(c.bscr + (on.start + base + tid) * 16) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
           }
           if (valid) {
+            const PL pl = payload_finish<MODE, PK>(c, s, ty, pr);
 #pragma unroll
             for (int j = 0; j < G; ++j)
               if (j < g) hist_add<MODE>(hist + j * span, c, (int)b[j], pl);
@@ -1292,18 +1346,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
         uint32_t rA = row_at(tid), rB = row_at(NT + tid);
         uint32_t bA[G], bB[G];
         gather(rA, bA);
+        PRaw pA = payload_fetch<MODE, PK>(c, ty, rA), pB;
         bool vA = rA != INV, vB = false;
-        PL pA = vA ? word_payload<MODE, PK>(c, s, ty, rA) : PL{}, pB{};
         for (int base = 0; base < cnt; base += 2 * NT) {
           rA = row_at(base + 2 * NT + tid);       // chunk k+2's row id
           gather(rB, bB);                         // chunk k+1's bins
+          pB = payload_fetch<MODE, PK>(c, ty, rB);
           vB = rB != INV;
-          pB = vB ? word_payload<MODE, PK>(c, s, ty, rB) : PL{};
           consume(base, vA, bA, pA);              // chunk k
           rB = row_at(base + 3 * NT + tid);       // chunk k+3's row id
           gather(rA, bA);                         // chunk k+2's bins
+          pA = payload_fetch<MODE, PK>(c, ty, rA);
           vA = rA != INV;
-          pA = vA ? word_payload<MODE, PK>(c, s, ty, rA) : PL{};
           consume(base + NT, vB, bB, pB);         // chunk k+1
         }
       };
@@ -1337,7 +1391,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
 #pragma unroll
           for (int j = 0; j < G; ++j) b[j] = (w[fdw[j]] >> fsh[j]) & 0xFFu;
         };
-        auto consume = [&](int base, bool valid, const uint32_t* b, const PL& pl) {
+        auto consume = [&](int base, bool valid, const uint32_t* b, const PRaw& pr) {
           if (NT == 256 && pos == 0 && valid) {
             uint32_t w4[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -1345,6 +1399,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
             *(uint4*)(c.bscr + (on.start + base + tid) * 16) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
           }
           if (valid) {
+            const PL pl = payload_finish<MODE, PK>(c, s, ty, pr);
 #pragma unroll
             for (int j = 0; j < G; ++j)
               if (j < g) hist_add<MODE>(hist + j * span, c, (int)b[j], pl);
@@ -1354,22 +1409,22 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
         uint32_t bA[G], bB[G];
         uint32_t rA = row_at(tid), rB = row_at(NT + tid);
         load_win(rA, win);
+        PRaw pA = payload_fetch<MODE, PK>(c, ty, rA), pB;
         extract(win, bA);
         bool vA = rA != INV, vB = false;
-        PL pA = vA ? word_payload<MODE, PK>(c, s, ty, rA) : PL{}, pB{};
         for (int base = 0; base < cnt; base += 2 * NT) {
           load_win(rB, win);                      // chunk k+1's row lines
+          pB = payload_fetch<MODE, PK>(c, ty, rB);
           rA = row_at(base + 2 * NT + tid);       // chunk k+2's row id
           consume(base, vA, bA, pA);              // chunk k
           extract(win, bB);
           vB = rB != INV;
-          pB = vB ? word_payload<MODE, PK>(c, s, ty, rB) : PL{};
           load_win(rA, win);                      // chunk k+2's row lines
+          pA = payload_fetch<MODE, PK>(c, ty, rA);
           rB = row_at(base + 3 * NT + tid);       // chunk k+3's row id
           consume(base + NT, vB, bB, pB);         // chunk k+1
           extract(win, bA);
           vA = rA != INV;
-          pA = vA ? word_payload<MODE, PK>(c, s, ty, rA) : PL{};
         }
       };
       if (DML_ROW_WINDOWS && NT == 256 && pos == 0 && g >= 8 && d <= 112 && (c.ld & 15) == 0 && c.ld >= 112 &&
@@ -1395,7 +1450,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
       }
     } else
     for (int base = 0; base < cnt; base += NT * RPT) {
-      if (!reg_rows) load_rows(base);
+      if (!reg_rows) { load_rows(base); fetch_rows(); }
       // all g x RPT bin loads are issued before the first histogram atomic
       uint32_t bins[KGMAX][RPT];
 #pragma unroll
@@ -1407,6 +1462,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
             bins[j][u] = rrow[u] != 0xFFFFFFFFu ? (uint32_t)c.Xb[(int64_t)(rrow[u] & c.rmask) * c.ld + f] : 0u;
         }
       }
+      if (!reg_rows) finish_rows();
 #pragma unroll
       for (int j = 0; j < KGMAX; ++j) {
         if (j < g) {
@@ -2656,7 +2712,8 @@ __global__ __launch_bounds__(64) void k_large_prep(Ctx c, int set_cur, int nL) {
   int16_t* feats = c.lperm + (int64_t)slot * c.d;
   st.g = min(c.kg_large, min(s.max_features, c.d));
   const FeatPerm fp = feat_perm(st.on.key, c.d);
-  for (int j = lane; j < st.g; j += 64) feats[j] = (int16_t)feature_at(fp, j, c.d);
+  const int nperm = c.full_cur ? c.d : st.g;   // whole-histogram level: the whole visiting order
+  for (int j = lane; j < nperm; j += 64) feats[j] = (int16_t)feature_at(fp, j, c.d);
   if (lane != 0) return;
   st.pos = 0; st.nonconst = 0; st.done = 0; st.best_feat = -1; st.best_bin = -1; st.split = 0; st.nl = 0;
   st.best_gain = -INFINITY;
@@ -2743,7 +2800,7 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
 #pragma unroll
         for (int j = 0; j < G; ++j) b[j] = (uint32_t)xr[fo[j]];
       };
-      auto consume = [&](int r, bool valid, const uint32_t* b, const PL& pl) {
+      auto consume = [&](int r, bool valid, const uint32_t* b, const PRaw& pr) {
         if (!valid) return;
         if (st_pos == 0) {   // round 0: bins of visiting positions 0..15 (Ctx::bscr)
           uint32_t w4[4] = {0u, 0u, 0u, 0u};
@@ -2751,6 +2808,7 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
           for (int j = 0; j < G && j < 16; ++j) w4[j >> 2] |= (j < g ? b[j] & 0xFFu : 0u) << (8 * (j & 3));
           *(uint4*)(c.bscr + (st_start + r) * 16) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
         }
+        const PL pl = payload_finish<MODE, PK>(c, s, ty, pr);
 #pragma unroll
         for (int j = 0; j < G; ++j)
           if (j < g) hist_add<MODE, RPL>(hist + j * span, c, (int)b[j], pl);
@@ -2758,18 +2816,18 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
       uint32_t rA = row_at(t0), rB = row_at(t0 + 256);
       uint32_t bA[G], bB[G];
       gather(rA, bA);
+      PRaw pA = payload_fetch<MODE, PK>(c, ty, rA), pB;
       bool vA = rA != INV, vB = false;
-      PL pA = vA ? word_payload<MODE, PK>(c, s, ty, rA) : PL{}, pB{};
       for (int r = t0; r < r1; r += 512) {
         rA = row_at(r + 512);
         gather(rB, bB);
+        pB = payload_fetch<MODE, PK>(c, ty, rB);
         vB = rB != INV;
-        pB = vB ? word_payload<MODE, PK>(c, s, ty, rB) : PL{};
         consume(r, vA, bA, pA);
         rB = row_at(r + 768);
         gather(rA, bA);
+        pA = payload_fetch<MODE, PK>(c, ty, rA);
         vA = rA != INV;
-        pA = vA ? word_payload<MODE, PK>(c, s, ty, rA) : PL{};
         consume(r + 256, vB, bB, pB);
       }
     };
@@ -2907,6 +2965,66 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   large_commit(c, s, st, slot, best_left, set_cur);
 }
 
+// whole-histogram level, all split candidates at once: workgroup (slot, q) evaluates visiting
+// positions 4q .. 4q+3 of large node `slot`, one wave each, from the node's whole-feature
+// histogram (Ctx::gf_cur).  Replaces ceil(d / kg_large) dependent k_split_large launches of nL
+// workgroups each (20 workgroups on a 256-CU chip for a boosting stage of 20 trees).  The
+// regression layout is evaluated straight from global memory (eval_feature reads 4 bins per
+// lane); the class-plane layout is staged in LDS (eval_feature_lds scans in place).
+template <int GM>
+__global__ __launch_bounds__(256) void k_split_full(Ctx c) {
+  using CT = typename HT<GM>::T;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int slot = blockIdx.x;
+  const LState& st = c.lstate[slot];
+  if (st.done) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int p = blockIdx.y * 4 + wid;
+  const bool active = p < c.d;
+  const NodeSpec s = spec_of<-1>(c, st.on.tree);
+  const int span = large_planes(GM, c.CH) * 256;
+  const int f = active ? (int)c.lperm[(int64_t)slot * c.d + p] : 0;
+  CT* h = (CT*)c.gf_cur + ((int64_t)slot * c.d + f) * span;
+  if constexpr (GM == 0) {
+    CT* lh = (CT*)smem + (int64_t)wid * span;
+    for (int i = lane; i < span && active; i += 64) lh[i] = h[i];
+    h = lh;
+    __syncthreads();
+  }
+  if (!active) return;
+  const double nlo = c.nbound ? c.nbound[2 * (int64_t)st.on.node] : -INFINITY;
+  const double nhi = c.nbound ? c.nbound[2 * (int64_t)st.on.node + 1] : INFINITY;
+  const int64_t o = (int64_t)slot * c.d + p;
+  eval_feature<GM, 2>(h, c.C, c.CH, s, lane, c.fr_g + o, c.fr_b + o, c.fr_n + o, c.fr_left + o * c.CH, false,
+                      tree_cw(c, st.on.tree), &c.rq, MonoQ{mono_of(c, s, f), nlo, nhi}, c.fr_mid + o);
+}
+
+// the node's best candidate in visiting order (select_group over all d positions: the same
+// order, ties and non-constant count as the per-group rounds), then the k_split_large tail
+template <int GM>
+__global__ __launch_bounds__(64) void k_split_full_select(Ctx c, int set_cur) {
+  const int slot = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  LState& st = c.lstate[slot];
+  if (st.done) return;
+  const NodeSpec s = spec_of<-1>(c, st.on.tree);
+  const int64_t o = (int64_t)slot * c.d;
+  double* best_left = c.lbest_left + (int64_t)slot * c.CH;
+  int nc = st.nonconst, bf = st.best_feat, bbin = st.best_bin, uj;
+  double bg = st.best_gain;
+  select_group(c, s, c.lperm + o, c.d, c.fr_g + o, c.fr_b + o, c.fr_n + o, c.fr_left + o * c.CH, best_left, nc, bg,
+               bf, bbin, uj);
+  st.nonconst = nc; st.best_gain = bg; st.best_feat = bf; st.best_bin = bbin;
+  if (uj >= 0) { st.best_pos = uj; st.best_mid = c.fr_mid[o + uj]; }
+  st.pos = c.d;
+  st.done = 1;
+  if (c.is_reg) {   // as k_split_large: partition first, k_large_finish accepts
+    if (st.best_feat >= 0) { st.split = 2; st.nl = (int)best_left[c.CH - 1]; }
+    return;
+  }
+  large_commit(c, s, st, slot, best_left, set_cur);
+}
+
 // accept the node's best split, create and enqueue its children (+ the next level's
 // sibling table on whole-histogram levels); st.split = 1 when it splits, else 0
 __device__ void large_commit(const Ctx& c, const NodeSpec& s, LState& st, int slot, const double* best_left, int set_cur) {
@@ -2960,20 +3078,39 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
     if (bj >= 0) return (int)c.bscr[(st.on.start + p) * 16 + bj];
     return (int)c.Xb[(int64_t)(row & c.rmask) * c.ld + feat];
   };
+  // regression: sum w y2q of the left rows (k_large_finish completes the left child's sums),
+  // accumulated in pass 1 from targets fetched one step ahead with the split bins -- fetched
+  // unconditionally (an absent row reads row 0): a target load under the left-row mask, used
+  // at once, would wait for every older load (vmcnt(0)), i.e. for the prefetched steps too
+  const NodeSpec s = spec_of<-1>(c, st.on.tree);
+  const float* ty = c.is_reg ? tree_y(c, s) : nullptr;
+  auto y_of = [&](uint32_t row) -> float { return ty ? ty[(row != INV ? row : 0u) & c.rmask] : 0.0f; };
+  unsigned long long lyy = 0ull;
   int myL = 0;
   {
     uint32_t ra = row_at(r0 + tid);
     int ba = bin_of(r0 + tid, ra);
+    float ya = y_of(ra);
     uint32_t rbn = row_at(r0 + tid + 256);
     for (int t0 = r0; t0 < r1; t0 += 256) {
       const int bb = bin_of(t0 + 256 + tid, rbn);
+      const float yb = y_of(rbn);
       const uint32_t rc2 = row_at(t0 + 512 + tid);
       const bool left = ra != INV && ba <= bin;
       const uint64_t ml = __ballot(left);
       if (lane == 0) lflag[(t0 - r0) / 64 + wid] = ml;
       myL += left ? 1 : 0;
-      ra = rbn; ba = bb; rbn = rc2;
+      if (ty && left) {
+        int64_t yq, y2q;
+        reg_quantize(ya, c.rq, yq, y2q);
+        lyy += (unsigned long long)((int64_t)word_weight(c, s, ra) * y2q);
+      }
+      ra = rbn; ba = bb; ya = yb; rbn = rc2;
     }
+  }
+  if (ty) {   // exact integer sum: any order
+    lyy = (unsigned long long)wave::sum<uint64_t>((uint64_t)lyy, lane);
+    if (lane == 0 && lyy) atomicAdd(&c.lyy[slot], lyy);
   }
   // block totals -> one atomic pair for the whole chunk
   for (int m = 32; m >= 1; m >>= 1) myL += __shfl_xor(myL, m);
@@ -2987,10 +3124,6 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
   }
   __syncthreads();
   int baseL = tbase[0], baseR = tbase[1];
-  // regression: sum w y2q of the left rows (k_large_finish completes the left child's sums)
-  const NodeSpec s = spec_of<-1>(c, st.on.tree);
-  const float* ty = c.is_reg ? tree_y(c, s) : nullptr;
-  unsigned long long lyy = 0ull;
   // row ids of DML_PART_U2 256-row steps are loaded (clamped, unconditionally) before the
   // steps' stores: consecutive steps do not each wait a memory round trip
   constexpr int U2 = DML_PART_U2;
@@ -3022,22 +3155,10 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
     }
     (void)vm;
     if (valid) {
-      if ((ml >> lane) & 1ull) {
-        out[baseL + offL + lane_prefix(ml)] = row;
-        if (ty) {
-          int64_t yq, y2q;
-          reg_quantize(ty[word_row(c, row)], c.rq, yq, y2q);
-          lyy += (unsigned long long)((int64_t)word_weight(c, s, row) * y2q);
-        }
-      } else {
-        out[nl + baseR + offR + lane_prefix(mr)] = row;
-      }
+      if ((ml >> lane) & 1ull) out[baseL + offL + lane_prefix(ml)] = row;
+      else out[nl + baseR + offR + lane_prefix(mr)] = row;
     }
     baseL += totL; baseR += totR;
-  }
-  if (ty) {   // exact integer sum: any order
-    lyy = (unsigned long long)wave::sum<uint64_t>((uint64_t)lyy, lane);
-    if (lane == 0 && lyy) atomicAdd(&c.lyy[slot], lyy);
   }
 }
 
@@ -3464,6 +3585,8 @@ struct FullBufs {
   size_t gf_bytes[2] = {0, 0};
   int4* pinfo = nullptr;   // [2][pi_cap]
   int64_t pi_cap = 0;
+  void* fr = nullptr;      // k_split_full's per-(node, position) candidates
+  size_t fr_bytes = 0;
 };
 static FullBufs* full_bufs() {
   static FullBufs b[16];
@@ -3485,7 +3608,7 @@ static bool ensure_bytes(void*& p, size_t& have, size_t need) {
 static int release_full_bufs() {
   FullBufs* b = full_bufs();
   if (!b) return 0;
-  if (b->gf[0] || b->gf[1] || b->pinfo) {
+  if (b->gf[0] || b->gf[1] || b->pinfo || b->fr) {
     if (hipDeviceSynchronize() != hipSuccess) return 1;
     for (int i = 0; i < 2; ++i) {
       if (b->gf[i]) (void)hipFree(b->gf[i]);
@@ -3495,6 +3618,9 @@ static int release_full_bufs() {
     if (b->pinfo) (void)hipFree(b->pinfo);
     b->pinfo = nullptr;
     b->pi_cap = 0;
+    if (b->fr) (void)hipFree(b->fr);
+    b->fr = nullptr;
+    b->fr_bytes = 0;
   }
   return 0;
 }
@@ -3742,9 +3868,18 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       if (!ensure_bytes(pp, have, (size_t)c.large_cap * 2 * sizeof(int4))) { fb->pinfo = nullptr; fb->pi_cap = 0; full = false; }
       else { fb->pinfo = (int4*)pp; fb->pi_cap = (int64_t)(have / (2 * sizeof(int4))); prev_full = false; }
     }
+    // k_split_full's candidate arrays: [nL][d] gain, mid, [CH] left sums (double), bin, nc (int)
+    const size_t fr_per = (size_t)a->d * (16 + 8 * (size_t)CH + 8);
+    if (full && !ensure_bytes(fb->fr, fb->fr_bytes, (size_t)nL * fr_per + 64)) full = false;
     c.full_cur = full ? 1 : 0;
     c.full_prev = (full && prev_full) ? 1 : 0;
     if (full) {
+      const size_t nd = (size_t)nL * a->d;
+      c.fr_g = (double*)fb->fr;
+      c.fr_mid = c.fr_g + nd;
+      c.fr_left = c.fr_mid + nd;
+      c.fr_b = (int32_t*)(c.fr_left + nd * CH);
+      c.fr_n = c.fr_b + nd;
       c.gf_cur = fb->gf[fpar];
       c.gf_prev = fb->gf[1 - fpar];
       c.pinfo_cur = fb->pinfo + (int64_t)fpar * fb->pi_cap;
@@ -3765,7 +3900,15 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
         const int64_t per = (int64_t)a->d * large_planes(GM, CH) * 256;
         k_hist_derive<GM><<<dim3((unsigned)nL, (unsigned)((per + 1023) / 1024)), 256, 0, st>>>(c);
       }
-      for (int round = 0; round < rounds; ++round) k_split_large<GM><<<nL, 256, lds_sl, st>>>(c, cur);
+      // every candidate in one launch (class planes staged in LDS: 4 features' worth, within
+      // the default 64 KB; more classes than that keep the per-group rounds)
+      const size_t lds_sf = GM == 0 ? (size_t)4 * ghist_feat_bytes(0, CH) : 0;
+      if (lds_sf <= 64 * 1024) {
+        k_split_full<GM><<<dim3((unsigned)nL, (unsigned)((a->d + 3) / 4)), 256, lds_sf, st>>>(c);
+        k_split_full_select<GM><<<nL, 64, 0, st>>>(c, cur);
+      } else {
+        for (int round = 0; round < rounds; ++round) k_split_large<GM><<<nL, 256, lds_sl, st>>>(c, cur);
+      }
       const dim3 gp = DML_LARGE_NODE_FAST ? dim3((unsigned)nL, nchunks) : dim3(nchunks, (unsigned)nL);
       k_partition_large<<<gp, 256, (size_t)((a->chunk + 255) / 256) * 4 * 8, st>>>(c);
       if (reg) k_large_finish<<<nL, 64, 0, st>>>(c, cur);

@@ -43,6 +43,7 @@ struct GbStageArgs {
   int64_t slot_node;          // int32 [J][S]: leaf node of each slot
   int64_t slot_val;           // double [J][S]
   int64_t raw;                // double [F * K][n]
+  int64_t XbT;                // optional feature-major bins uint8 [d][n] (0: walk the row-major Xb)
 };
 
 struct GbGradArgs {
@@ -58,31 +59,60 @@ struct GbGradArgs {
 
 #define GB_PTR(T, v) ((T*)(uintptr_t)(v))
 
-// leaf slot (and leaf node) of one row in tree j
-__device__ __forceinline__ int gb_slot(const NodeRec* __restrict__ nodes, const uint8_t* __restrict__ xr, int j,
-                                       int& leaf) {
-  int node = j, slot = 1;
-  NodeRec r = nodes[node];
-  for (int steps = 0; r.split >= 0 && steps < 64; ++steps) {
-    const int go = xr[r.split >> 8] > (r.split & 255) ? 1 : 0;
-    node = r.left + go;
-    slot = 2 * slot + go;
-    r = nodes[node];
+// Tree j as a path-slot table in LDS: tsplit[slot] = the split of the node at that slot (-1:
+// leaf or unreachable), tnode[slot] = its node index.  Thread t resolves slot t by walking its
+// path bits from the root once per workgroup; the rows then walk the table (one LDS read and
+// one bin load per level) instead of chasing node records through global memory.
+template <int S>
+__device__ __forceinline__ void gb_load_tree(const NodeRec* __restrict__ nodes, int j, int32_t* tsplit,
+                                             int32_t* tnode) {
+  for (int t = threadIdx.x; t < S; t += 256) {
+    int node = -1, split = -1;
+    if (t >= 1) {
+      const int depth = 31 - __clz(t);
+      node = j;
+      for (int l = depth - 1; l >= 0 && node >= 0; --l) {
+        const NodeRec r = nodes[node];
+        node = r.split >= 0 ? r.left + ((t >> l) & 1) : -1;
+      }
+      if (node >= 0) split = nodes[node].split;
+    }
+    tsplit[t] = split;
+    tnode[t] = node;
   }
-  leaf = node;
-  return slot;
+}
+
+// leaf slot of row r: feature-major bins (XbT, stride n) when given -- the rows of a workgroup
+// are consecutive, so lanes at the same node read consecutive bytes of one feature -- else the
+// row's line of the row-major table.  A tree of depth D stays below slot 2^(D+1) <= S.
+template <int S>
+__device__ __forceinline__ int gb_walk(const int32_t* tsplit, const uint8_t* __restrict__ X, int64_t ld,
+                                       const uint8_t* __restrict__ XT, int64_t n, int64_t r) {
+  int slot = 1;
+  int sp = tsplit[1];
+  while (sp >= 0) {
+    const int f = sp >> 8;
+    const int b = XT ? (int)XT[(int64_t)f * n + r] : (int)X[r * ld + f];
+    slot = 2 * slot + (b > (sp & 255) ? 1 : 0);
+    if (slot >= S) break;   // malformed tree guard (cannot happen for depth < log2 S)
+    sp = tsplit[slot];
+  }
+  return slot < S ? slot : 1;
 }
 
 template <int S>
 __global__ __launch_bounds__(256) void k_gb_leafsums(GbStageArgs a) {
   __shared__ double num[S], den[S];
-  __shared__ int nd[S];
+  __shared__ int32_t tsplit[S], tnode[S];
+  __shared__ int hit[S];
   const int j = blockIdx.y;
-  for (int i = threadIdx.x; i < S; i += 256) { num[i] = 0.0; den[i] = 0.0; nd[i] = -1; }
+  const NodeRec* nodes = GB_PTR(const NodeRec, a.nodes);
+  gb_load_tree<S>(nodes, j, tsplit, tnode);
+  for (int i = threadIdx.x; i < S; i += 256) { num[i] = 0.0; den[i] = 0.0; hit[i] = 0; }
   __syncthreads();
   const int64_t n = a.n;
   const uint8_t* X = GB_PTR(const uint8_t, a.Xb);
-  const NodeRec* nodes = GB_PTR(const NodeRec, a.nodes);
+  const uint8_t* XT = GB_PTR(const uint8_t, a.XbT);
   const uint8_t* inb = GB_PTR(const uint8_t, a.inbag) + (int64_t)j * n;
   const double* g = GB_PTR(const double, a.grad) + (int64_t)j * n;
   const int32_t* ycls = GB_PTR(const int32_t, a.ycls);
@@ -94,9 +124,8 @@ __global__ __launch_bounds__(256) void k_gb_leafsums(GbStageArgs a) {
   for (int u = 0; u < 4; ++u) {
     const int64_t r = r0 + u * 256 + threadIdx.x;
     if (r >= n || !inb[r]) continue;
-    int leaf;
-    const int slot = gb_slot(nodes, X + r * a.ld, j, leaf);
-    nd[slot] = leaf;   // every row of the leaf writes the same node
+    const int slot = gb_walk<S>(tsplit, X, a.ld, XT, n, r);
+    hit[slot] = 1;   // every row of the leaf writes the same flag
     if (!newton) continue;
     const double gv = g[r];
     double h;
@@ -119,8 +148,8 @@ __global__ __launch_bounds__(256) void k_gb_leafsums(GbStageArgs a) {
   double* ss = GB_PTR(double, a.slot_sum) + (int64_t)j * S * 2;
   int32_t* sn = GB_PTR(int32_t, a.slot_node) + (int64_t)j * S;
   for (int i = threadIdx.x; i < S; i += 256) {
-    if (nd[i] < 0) continue;
-    sn[i] = nd[i];
+    if (!hit[i]) continue;
+    sn[i] = tnode[i];
     if (newton) {
       atomicAdd(&ss[2 * i], num[i]);
       atomicAdd(&ss[2 * i + 1], den[i]);
@@ -154,21 +183,21 @@ __global__ __launch_bounds__(256) void k_gb_values(GbStageArgs a) {
 template <int S>
 __global__ __launch_bounds__(256) void k_gb_update(GbStageArgs a) {
   __shared__ double val[S];
+  __shared__ int32_t tsplit[S], tnode[S];
   const int j = blockIdx.y;
+  gb_load_tree<S>(GB_PTR(const NodeRec, a.nodes), j, tsplit, tnode);
   for (int i = threadIdx.x; i < S; i += 256) val[i] = GB_PTR(const double, a.slot_val)[(int64_t)j * S + i];
   __syncthreads();
   const int64_t n = a.n;
   const uint8_t* X = GB_PTR(const uint8_t, a.Xb);
-  const NodeRec* nodes = GB_PTR(const NodeRec, a.nodes);
+  const uint8_t* XT = GB_PTR(const uint8_t, a.XbT);
   double* raw = GB_PTR(double, a.raw) + (int64_t)GB_PTR(const int32_t, a.tree_raw)[j] * n;
   const double lr = GB_PTR(const double, a.tree_lr)[j];
   const int64_t r0 = (int64_t)blockIdx.x * 1024;
   for (int u = 0; u < 4; ++u) {
     const int64_t r = r0 + u * 256 + threadIdx.x;
     if (r >= n) continue;
-    int leaf;
-    const int slot = gb_slot(nodes, X + r * a.ld, j, leaf);
-    raw[r] += val[slot] * lr;
+    raw[r] += val[gb_walk<S>(tsplit, X, a.ld, XT, n, r)] * lr;
   }
 }
 

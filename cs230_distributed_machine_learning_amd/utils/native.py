@@ -96,7 +96,7 @@ LrFwdArgs = _i64_struct(
 GbStageArgs = _i64_struct(
     "GbStageArgs",
     ["Xb", "ld", "n", "nodes", "node_val", "J", "K", "S", "tree_raw", "tree_loss", "tree_lr", "inbag", "grad",
-     "ycls", "slot_sum", "slot_node", "slot_val", "raw"],
+     "ycls", "slot_sum", "slot_node", "slot_val", "raw", "XbT"],
 )
 GbGradArgs = _i64_struct("GbGradArgs", ["n", "K", "A", "fit_raw", "fit_loss", "raw", "ycls", "yreg", "grad", "tgt"])
 # csrc/kernels/forest_mae.hip (criterion="absolute_error" builder)
