@@ -1109,6 +1109,15 @@ __device__ __forceinline__ typename PLT<MODE>::T payload_finish(const Ctx& c, co
   }
 }
 
+// large-tier regression, unit row weights: u32 row count in the slice's first KB + the w yq plane
+template <int MODE>
+__device__ __forceinline__ void hist_add_unit(typename HT<MODE>::T* hj, int b, const typename PLT<MODE>::T& pl) {
+  if constexpr (MODE == 2) {
+    atomicAdd((uint32_t*)hj + b, 1u);
+    atomicAdd(&hj[256 + b], pl.wy);
+  }
+}
+
 template <int MODE, int RP = 3>
 __device__ __forceinline__ void hist_add(typename HT<MODE>::T* hj, const Ctx& c, int b, const typename PLT<MODE>::T& pl) {
 #ifdef DML_X2_ATOMIC   // sensitivity build: every histogram atomic issued twice (the second adds 0)
@@ -2772,6 +2781,10 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
   const uint32_t* rows = c.rows_cur + st.on.start;
   const float* ty = tree_y(c, s);
   constexpr int KGL = 16;
+  // regression tree without bootstrap: every active row weighs 1, so the (w | rows << 32)
+  // plane is a row count -- kept as u32 LDS counters (ds_add_u32: half the bytes and bank
+  // pairs of the u64 add) in the first KB of each feature's 4-KB slice, widened at the flush
+  const bool uw = MODE == 2 && s.bootstrap == 0 && g <= KGL;
   if (g <= KGL) {
     // ping-pong software pipeline with compile-time-counted unconditional gathers (the block
     // tier's loop in k_nodes): the row id two steps ahead and the next step's bins are in
@@ -2779,8 +2792,9 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
     constexpr uint32_t INV = 0xFFFFFFFFu;
     using PL = typename PLT<MODE>::T;
     const int t0 = r0 + (int)threadIdx.x;
-    auto run = [&](auto Gc) {
+    auto run = [&](auto Gc, auto UWc) {
       constexpr int G = decltype(Gc)::value;
+      constexpr bool UW = decltype(UWc)::value;
       // feature offsets: feature-major copy (stride n) when present, else the row line
       const bool fm = c.XbT != nullptr;
       int64_t fo[G];
@@ -2809,9 +2823,15 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
           *(uint4*)(c.bscr + (st_start + r) * 16) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
         }
         const PL pl = payload_finish<MODE, PK>(c, s, ty, pr);
+        if constexpr (MODE == 2 && UW) {
 #pragma unroll
-        for (int j = 0; j < G; ++j)
-          if (j < g) hist_add<MODE, RPL>(hist + j * span, c, (int)b[j], pl);
+          for (int j = 0; j < G; ++j)
+            if (j < g) hist_add_unit<MODE>(hist + j * span, (int)b[j], pl);
+        } else {
+#pragma unroll
+          for (int j = 0; j < G; ++j)
+            if (j < g) hist_add<MODE, RPL>(hist + j * span, c, (int)b[j], pl);
+        }
       };
       uint32_t rA = row_at(t0), rB = row_at(t0 + 256);
       uint32_t bA[G], bB[G];
@@ -2831,13 +2851,21 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
         consume(r + 256, vB, bB, pB);
       }
     };
-    switch (g) {
-#define DML_G_CASE(N) case N: run(std::integral_constant<int, N>{}); break;
-      DML_G_CASE(1) DML_G_CASE(2) DML_G_CASE(3) DML_G_CASE(4) DML_G_CASE(5) DML_G_CASE(6) DML_G_CASE(7)
-      DML_G_CASE(8) DML_G_CASE(9) DML_G_CASE(10) DML_G_CASE(11) DML_G_CASE(12) DML_G_CASE(13) DML_G_CASE(14)
-      DML_G_CASE(15)
+    auto rung = [&](auto UWc) {
+      switch (g) {
+#define DML_G_CASE(N) case N: run(std::integral_constant<int, N>{}, UWc); break;
+        DML_G_CASE(1) DML_G_CASE(2) DML_G_CASE(3) DML_G_CASE(4) DML_G_CASE(5) DML_G_CASE(6) DML_G_CASE(7)
+        DML_G_CASE(8) DML_G_CASE(9) DML_G_CASE(10) DML_G_CASE(11) DML_G_CASE(12) DML_G_CASE(13) DML_G_CASE(14)
+        DML_G_CASE(15)
 #undef DML_G_CASE
-      default: run(std::integral_constant<int, KGL>{}); break;
+        default: run(std::integral_constant<int, KGL>{}, UWc); break;
+      }
+    };
+    if constexpr (MODE == 2) {
+      if (uw) rung(std::true_type{});
+      else rung(std::false_type{});
+    } else {
+      rung(std::false_type{});
     }
   } else {
     for (int r = r0 + threadIdx.x; r < r1; r += 256) {
@@ -2867,7 +2895,12 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
   } else {
     CT* gh = (CT*)gbase + goff;
     for (int i = threadIdx.x; i < g * span; i += 256) {
-      const CT v = hist[i];
+      CT v = hist[i];
+      if (MODE == 2 && uw && (i % span) < 256) {   // u32 row counts -> (w | rows << 32), w = rows
+        const int j = i / span, b = i % span;
+        const unsigned long long n1 = ((const uint32_t*)(hist + j * span))[b];
+        v = (CT)(n1 | (n1 << 32));
+      }
       if (v != (CT)0) atomicAdd(&gh[i], v);
     }
   }
@@ -2999,23 +3032,43 @@ __global__ __launch_bounds__(256) void k_split_full(Ctx c) {
                       tree_cw(c, st.on.tree), &c.rq, MonoQ{mono_of(c, s, f), nlo, nhi}, c.fr_mid + o);
 }
 
-// the node's best candidate in visiting order (select_group over all d positions: the same
-// order, ties and non-constant count as the per-group rounds), then the k_split_large tail
+// the node's best candidate in visiting order, 64 positions per step (k_nodes' wave-parallel
+// form of select_group: the same order, ties and non-constant count as the per-group rounds),
+// then the k_split_large tail
 template <int GM>
 __global__ __launch_bounds__(64) void k_split_full_select(Ctx c, int set_cur) {
   const int slot = blockIdx.x;
-  if (threadIdx.x != 0) return;
+  const int lane = threadIdx.x;
   LState& st = c.lstate[slot];
   if (st.done) return;
   const NodeSpec s = spec_of<-1>(c, st.on.tree);
+  const int k = s.max_features;
   const int64_t o = (int64_t)slot * c.d;
   double* best_left = c.lbest_left + (int64_t)slot * c.CH;
-  int nc = st.nonconst, bf = st.best_feat, bbin = st.best_bin, uj;
-  double bg = st.best_gain;
-  select_group(c, s, c.lperm + o, c.d, c.fr_g + o, c.fr_b + o, c.fr_n + o, c.fr_left + o * c.CH, best_left, nc, bg,
-               bf, bbin, uj);
-  st.nonconst = nc; st.best_gain = bg; st.best_feat = bf; st.best_bin = bbin;
-  if (uj >= 0) { st.best_pos = uj; st.best_mid = c.fr_mid[o + uj]; }
+  int nonconst = st.nonconst, best_pos = -1;
+  double best_gain = st.best_gain;
+  for (int q0 = 0; q0 < c.d && nonconst < k; q0 += 64) {
+    const int p = q0 + lane;
+    const bool isnc = p < c.d && c.fr_n[o + p] != 0;
+    const uint64_t m = __ballot(isnc);
+    const bool considered = isnc && nonconst + lane_prefix(m) + 1 <= k;
+    const bool has = considered && c.fr_b[o + p] >= 0;
+    double gj = has ? c.fr_g[o + p] : -INFINITY;
+    int jj = has ? p : (1 << 30);
+    wave::argmax(gj, jj, lane);
+    if (jj < (1 << 30) && gj > best_gain) { best_gain = gj; best_pos = jj; }
+    nonconst = min(nonconst + __popcll(m), k);
+  }
+  if (best_pos >= 0 && lane < c.CH) best_left[lane] = c.fr_left[(o + best_pos) * c.CH + lane];
+  if (lane != 0) return;
+  st.nonconst = nonconst;
+  if (best_pos >= 0) {
+    st.best_gain = best_gain;
+    st.best_feat = c.lperm[o + best_pos];
+    st.best_bin = c.fr_b[o + best_pos];
+    st.best_pos = best_pos;
+    st.best_mid = c.fr_mid[o + best_pos];
+  }
   st.pos = c.d;
   st.done = 1;
   if (c.is_reg) {   // as k_split_large: partition first, k_large_finish accepts
@@ -3070,12 +3123,16 @@ __global__ __launch_bounds__(256) void k_partition_large(Ctx c) {
   constexpr uint32_t INV = 0xFFFFFFFFu;
   auto row_at = [&](int r) -> uint32_t { return r < r1 ? rows[r] : INV; };
   // split bin at row position p: from the histogram pass's scratch if the final round's
-  // group produced the best split (st.best_j >= 0), else gathered from the table
+  // group produced the best split (st.best_j >= 0), else gathered from the table -- its
+  // feature-major copy when present (a node's rows are sorted: lanes read neighbouring bytes
+  // of one feature line instead of one row line each)
   const int bj = st.scr_id > 0 ? (st.best_feat < st.scr_id ? st.best_feat : -1)
                                : (st.best_pos < st.scr_n ? st.best_pos : -1);
+  const uint8_t* xfeat = c.XbT ? c.XbT + (int64_t)feat * c.n : nullptr;
   auto bin_of = [&](int p, uint32_t row) -> int {
     if (row == INV) return 0;
     if (bj >= 0) return (int)c.bscr[(st.on.start + p) * 16 + bj];
+    if (xfeat) return (int)xfeat[row & c.rmask];
     return (int)c.Xb[(int64_t)(row & c.rmask) * c.ld + feat];
   };
   // regression: sum w y2q of the left rows (k_large_finish completes the left child's sums),
@@ -3748,12 +3805,12 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   int32_t* h_pool = h + 48;   // pinned slot for the per-level pool reservation (H2D)
   const size_t lds_b = fused_lds(a, (int)a->kg_block);
   const int CH = c.CH;
-  // regression: k_hist_large runs ONE workgroup per CU (its dynamic LDS is padded past half
-  // the CU's 160 KB): GBRT config 6 3.40 -> 3.04 s against two per CU with the 64-KB
-  // two-plane histograms; classification is unaffected by the padding (23.15 vs 22.80
-  // CV-fits/s, so it keeps its natural size).  DML_LARGE_LDS_MIN overrides the floor.
-  const size_t lds_hl_floor = getenv("DML_LARGE_LDS_MIN") ? (size_t)atol(getenv("DML_LARGE_LDS_MIN"))
-                                                          : (MODE == 2 ? (size_t)96 * 1024 : 0);
+  // k_hist_large's dynamic LDS, optionally padded (DML_LARGE_LDS_MIN bytes) to cap its
+  // workgroups per CU.  No padding: once the regression payload loads stopped draining the
+  // gather pipeline (payload_fetch), two and more workgroups per CU beat one (GBRT config 6
+  // 13.7 -> 14.9 CV-fits/s at 8192-row chunks; the 96-KB floor used before was measured on
+  // the draining loop).
+  const size_t lds_hl_floor = getenv("DML_LARGE_LDS_MIN") ? (size_t)atol(getenv("DML_LARGE_LDS_MIN")) : 0;
   const size_t lds_hl = std::max<size_t>((size_t)a->kg_large * large_planes(MODE, CH) * 256 * mode_elem(MODE),
                                          std::min<size_t>(lds_hl_floor, 150 * 1024));
   const size_t lds_sl = (size_t)a->kg_large * ghist_feat_bytes(MODE, CH) + a->kg_large * 16 + 16 +

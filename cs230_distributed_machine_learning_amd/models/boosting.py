@@ -318,18 +318,32 @@ class GradientBoostingFamily(Family):
         if sharded:   # the global training rows (ascending), for subsample draws equal on every rank
             cnts = [data.all_gather_equal(torch.tensor([int(ti.numel())], device=dev)).cpu().numpy() for ti in train_idx]
             gtrain = [data._gather_rows(ti + data.r0, c) for ti, c in zip(train_idx, cnts)]
+        # per-active-set device constants, made once: a pageable host->device copy per stage
+        # waits for the stream, i.e. for the previous stage's kernels, before the next stage's
+        # launches are even issued (the active set only changes when a fit stops)
+        consts: Dict[tuple, Dict[str, Any]] = {}
         for stage in range(max(n_est)):
             act = [f for f in range(F) if stage < n_est[f]]
             if not act:
                 break
             A = len(act)
-            act_t = torch.tensor(act, device=dev)
+            cst = consts.get(tuple(act))
+            if cst is None:
+                consts.clear()
+                cst = consts[tuple(act)] = {"act_t": torch.tensor(act, device=dev)}
+                if fused:
+                    act_np = np.asarray(act, dtype=np.int32)
+                    j_fit = np.repeat(act_np, K)
+                    cst["fit_raw"] = torch.from_numpy(act_np * K).to(dev)
+                    cst["fit_loss"] = torch.from_numpy(loss_all[act_np]).to(dev)
+                    cst["tree_raw"] = torch.from_numpy(j_fit * K + np.tile(np.arange(K, dtype=np.int32), A)).to(dev)
+                    cst["tree_loss"] = torch.from_numpy(loss_all[j_fit]).to(dev)
+                    cst["tree_lr"] = torch.from_numpy(lr_all[j_fit]).to(dev)
+            act_t = cst["act_t"]
             loss = [batch[f].params["loss"] for f in act]
             hub_delta: Dict[int, float] = {}
             if fused:   # --- negative gradient of every active fit: one kernel -------------------
-                act_np = np.asarray(act, dtype=np.int32)
-                fit_raw = torch.from_numpy(act_np * K).to(dev)
-                fit_loss = torch.from_numpy(loss_all[act_np]).to(dev)
+                fit_raw, fit_loss = cst["fit_raw"], cst["fit_loss"]
                 ga = native.GbGradArgs(n=n, K=K, A=A, fit_raw=native.ptr(fit_raw), fit_loss=native.ptr(fit_loss),
                                        raw=native.ptr(raw), ycls=native.ptr(ycls32), yreg=native.ptr(yreg64),
                                        grad=native.ptr(G64), tgt=native.ptr(T32))
@@ -360,9 +374,14 @@ class GradientBoostingFamily(Family):
                     row[sel] = True
                     inbag[a] = row
                     sub_rows.append(a)
-            # one role row per tree (roles = in-bag mask of its fit)
+            # one role row per tree (roles = in-bag mask of its fit); fixed while the active set
+            # is, unless a fit subsamples
             J = A * K
-            roles_t = inbag.repeat_interleave(K, dim=0).to(torch.uint8).contiguous()   # [J, n]
+            roles_t = cst.get("roles_t") if not sub_rows else None
+            if roles_t is None:
+                roles_t = inbag.repeat_interleave(K, dim=0).to(torch.uint8).contiguous()   # [J, n]
+                if not sub_rows:
+                    cst["roles_t"] = roles_t
             tgt = T32[:J] if fused else G.reshape(J, n).float().contiguous()
             specs = _stage_specs(batch, act, K, seeds, stage)
             limit = np.repeat([batch[f].params.get("max_leaf_nodes", 0) for f in act], K)
@@ -408,10 +427,7 @@ class GradientBoostingFamily(Family):
                 vals = torch.from_numpy(fb.vals)
             P = vals.shape[0]
             if fused:   # --- leaf line search + raw update of every row: three kernels ------------
-                j_fit = np.repeat(np.asarray(act, dtype=np.int32), K)
-                tree_raw = torch.from_numpy(j_fit * K + np.tile(np.arange(K, dtype=np.int32), A)).to(dev)
-                tree_loss = torch.from_numpy(loss_all[j_fit]).to(dev)
-                tree_lr = torch.from_numpy(lr_all[j_fit]).to(dev)
+                tree_raw, tree_loss, tree_lr = cst["tree_raw"], cst["tree_loss"], cst["tree_lr"]
                 slot_sum = torch.zeros((J, S, 2), dtype=torch.float64, device=dev)
                 slot_node = torch.full((J, S), -1, dtype=torch.int32, device=dev)
                 slot_val = torch.empty((J, S), dtype=torch.float64, device=dev)

@@ -562,7 +562,11 @@ def _mono_table(batch, d: int, is_reg: bool):
 def _refine(data, fb, Xb, specs, roles) -> None:
     """sklearn midpoint thresholds where the binning is exact (no-op on quantile-binned data)."""
     vals, exact = data.bin_values()
-    if not bool(exact.any()):
+    # cached per dataset: a device-side any() per call is a host/GPU sync (boosting calls
+    # this once per stage)
+    if getattr(data, "_refine_needed", None) is None:
+        data._refine_needed = bool(exact.any())
+    if not data._refine_needed:
         return
     if data.is_gpu:
         forest_ops.refine_thresholds(fb, Xb, specs, roles, vals, exact)

@@ -48,6 +48,12 @@ class ForestTiers:
     kg_wave: int = 4
     kg_block: int = 16
     kg_large: int = 16
+    # regression builds (boosting stages): smaller large-tier row chunks and feature rounds,
+    # i.e. more, smaller workgroups in flight (several per CU) -- config 6 repeated sweep:
+    # 13.7 (16384-row chunks) -> 14.9 (8192) -> 15.4 CV-fits/s (4096);
+    # profiles/r4_gbrt_cfg6_chunk_sweep.txt
+    chunk_reg: int = 4096
+    kg_large_reg: int = 16
     slack_wave: int = 0
     # binary classification, > 0: nodes of sub_max < count <= bigsub_max grow their WHOLE
     # subtree in one 4-wave workgroup from an LDS row cache (forest.hip k_bigsub) and tier 1
@@ -64,9 +70,10 @@ class ForestTiers:
             env = os.environ.get("DML_TIER_" + k.upper())
             if env:
                 setattr(t, k, int(env))
-        t.kg_wave = max(1, min(self.kg_wave, (24 * 1024) // per_feat, 4))     # k_nodes<64>: KGMAX 4
-        t.kg_block = max(1, min(self.kg_block, (96 * 1024) // per_feat, 16))  # k_nodes<256>: KGMAX 16
-        t.kg_large = max(1, min(self.kg_large, (96 * 1024) // per_feat, 64))
+        t.kg_wave = max(1, min(t.kg_wave, (24 * 1024) // per_feat, 4))     # k_nodes<64>: KGMAX 4
+        t.kg_block = max(1, min(t.kg_block, (96 * 1024) // per_feat, 16))  # k_nodes<256>: KGMAX 16
+        t.kg_large = max(1, min(t.kg_large, (96 * 1024) // per_feat, 64))
+        t.kg_large_reg = max(1, min(t.kg_large_reg, (96 * 1024) // per_feat, 64))
         return t
 
 
@@ -244,12 +251,25 @@ def _carve(buf: torch.Tensor, off: int, shape, dtype) -> torch.Tensor:
 EXP_OFF, EXP_BINS = 160, 320   # bucket k + EXP_OFF of a target's frexp exponent k (|y| < 2^k)
 
 
-def reg_exponent_counts(yreg, n: int, ystride: int = 0, targets: int = 1):
+def _h2d(arr: np.ndarray, dev) -> torch.Tensor:
+    """Host array -> device without a host/GPU rendezvous: staged through pinned memory and
+    copied on the stream (a pageable copy blocks the host until the stream has drained, so the
+    GPU sits idle while the host prepares the next launches).  The caching host allocator keeps
+    the pinned staging buffer alive until the copy has run."""
+    t = torch.from_numpy(np.ascontiguousarray(arr))
+    if dev.type != "cuda":
+        return t.to(dev)
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
+def reg_exponent_counts(yreg, n: int, ystride: int = 0, targets: int = 1, defer: bool = False):
     """Per-target histogram of the frexp exponents of the nonzero targets: int64
     [targets, EXP_BINS] (a torch tensor on ``yreg``'s device, or numpy).  Counts are exact
     and order-free, so every builder -- and every rank of a row-sharded build, after a sum
     all-reduce -- derives the same exponents from them (``reg_exponents_of_counts``).
-    ``ystride > 0``: target t is ``yreg[t * ystride : t * ystride + n]``."""
+    ``ystride > 0``: target t is ``yreg[t * ystride : t * ystride + n]``.
+    ``defer`` (device path): return a callable that checks and returns the counts, so the
+    caller can read them back with its own next host/GPU sync."""
     targets = max(1, int(targets)) if ystride > 0 else 1
     if torch.is_tensor(yreg) and yreg.is_cuda and yreg.dtype == torch.float32 and yreg.is_contiguous():
         # one LDS-histogram kernel (gbrt.hip k_exp_hist): boosting recounts every stage's targets
@@ -260,9 +280,13 @@ def reg_exponent_counts(yreg, n: int, ystride: int = 0, targets: int = 1):
                               native.ptr(bad), native.stream_handle(yreg.device))
         if rc != 0:
             raise RuntimeError(f"dml_exp_hist failed ({rc})")
-        if int(bad.item()):
-            raise ValueError("regression target contains NaN or infinity")
-        return cnt
+
+        def resolve():
+            if int(bad.item()):
+                raise ValueError("regression target contains NaN or infinity")
+            return cnt
+
+        return resolve if defer else resolve()
     if torch.is_tensor(yreg):
         y = yreg.reshape(-1)
         rows = y[: (targets - 1) * ystride + n].as_strided((targets, n), (ystride, 1)) if ystride > 0 else y[:n][None]
@@ -404,14 +428,18 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     VC = 3 if is_reg else n_classes
     tiers = (tiers or ForestTiers()).fitted(CH)
     stream = native.stream_handle(dev)
-    specs_dev = torch.from_numpy(specs.view(np.uint8).copy()).to(dev)
+    specs_dev = _h2d(specs.view(np.uint8), dev)
     active = torch.zeros(T, dtype=torch.int32, device=dev)
     a = native.ForestArgs()
     a.Xb, a.ld, a.n, a.d = native.ptr(Xb), Xb.stride(0), n, d
     a.ycls = native.ptr(ycls) if ycls is not None else 0
     a.yreg = native.ptr(yreg) if yreg is not None else 0
     a.n_classes, a.is_reg = (n_classes if not is_reg else 1), int(is_reg)
-    a.yq_e1, a.yq_e2 = reg_exponents(yreg, n, ystride, _n_targets(specs, ystride)) if is_reg else (0, 0)
+    # the targets' exponent histogram is launched here and read back together with the
+    # active-row counts below (one host/GPU sync for both)
+    exp_cnt = (reg_exponent_counts(yreg, n, ystride, _n_targets(specs, ystride), defer=True)
+               if is_reg and yreg is not None and n > 0 else None)
+    a.yq_e1, a.yq_e2 = 0, 0
     a.roles, a.n_splits = native.ptr(roles), roles.shape[0]
     a.specs, a.T = native.ptr(specs_dev), T
     a.ystride = int(ystride)
@@ -421,13 +449,13 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     # class-weight table [T, C] float64 (rows of cw_mode 2 trees are filled by the kernel)
     cw_dev = None
     if cw is not None and not is_reg:
-        cw_dev = torch.from_numpy(np.ascontiguousarray(cw, dtype=np.float64).reshape(T, n_classes)).to(dev)
+        cw_dev = _h2d(np.ascontiguousarray(cw, dtype=np.float64).reshape(T, n_classes), dev)
     a.cw = native.ptr(cw_dev) if cw_dev is not None else 0
     # monotonic_cst: int8 [fits][d] rows indexed by the specs' "fit" (classifier rows
     # constrain the class-0 fraction, i.e. arrive negated) + per-node bounds
     mono_dev = None
     if mono is not None and np.any(mono):
-        mono_dev = torch.from_numpy(np.ascontiguousarray(mono, dtype=np.int8)).to(dev)
+        mono_dev = _h2d(np.ascontiguousarray(mono, dtype=np.int8), dev)
     a.mono = native.ptr(mono_dev) if mono_dev is not None else 0
     a.nbound = 0
     # one criterion, no class weights / monotonic constraints / min_weight_fraction_leaf: the
@@ -448,15 +476,19 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
         if rc:
             raise RuntimeError(f"dml_forest_count failed ({rc}): {native.hip_error(lib)}")
         counts = active.cpu().numpy().astype(np.int64)
+    if exp_cnt is not None:
+        cnt = exp_cnt() if callable(exp_cnt) else exp_cnt
+        a.yq_e1, a.yq_e2 = reg_exponents_of_counts(cnt)
     row_off = np.zeros(T + 1, dtype=np.int64)
     np.cumsum(counts, out=row_off[1:])
-    row_off_dev = torch.from_numpy(row_off).to(dev)
+    row_off_dev = _h2d(row_off, dev)
     a.row_off = native.ptr(row_off_dev)
     a.rows_total = int(row_off[-1])
     a.max_active = int(counts.max()) if T else 0
     pool_cap = _pool_bound(counts, specs) + T
-    a.wave_max, a.block_max, a.chunk = tiers.wave_max, tiers.block_max, tiers.chunk
-    a.kg_wave, a.kg_block, a.kg_large, a.slack_wave = tiers.kg_wave, tiers.kg_block, tiers.kg_large, tiers.slack_wave
+    a.wave_max, a.block_max, a.chunk = tiers.wave_max, tiers.block_max, (tiers.chunk_reg if is_reg else tiers.chunk)
+    a.kg_wave, a.kg_block, a.slack_wave = tiers.kg_wave, tiers.kg_block, tiers.slack_wave
+    a.kg_large = tiers.kg_large_reg if is_reg else tiers.kg_large
     a.sub_max = tiers.sub_max
     a.sub_small = tiers.sub_small
     a.sub_cache_d = _sub_cache_stride(d) if d <= tiers.sub_cache_max_d else 0
