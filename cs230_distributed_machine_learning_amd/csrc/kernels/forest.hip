@@ -237,6 +237,7 @@ struct Ctx {
   const int4* pinfo_cur;
   int4* pinfo_next;
   int32_t full_cur, full_prev;
+  int64_t pi_cap;        // entries of each pinfo table
   // whole-histogram levels: every (large node, visiting position)'s split candidate, from
   // k_split_full (one wave per feature, all features of all nodes in one launch), selected in
   // visiting order by k_split_full_select: [slot][d] (+ [CH] for the left sums)
@@ -2732,6 +2733,10 @@ __global__ __launch_bounds__(64) void k_large_prep(Ctx c, int set_cur, int nL) {
   st.scr_id = 0; st.derive = 0; st.par = -1; st.sib = -1;
   c.lyy[slot] = 0ull;
   if (c.full_cur) {
+    // the next level's sibling table: its large nodes (<= 2 per node here) start as "no parent"
+    const int4 none = make_int4(-1, -1, -1, -1);
+    if (2 * slot < c.pi_cap) c.pinfo_next[2 * slot] = none;
+    if (2 * slot + 1 < c.pi_cap) c.pinfo_next[2 * slot + 1] = none;
     // whole-histogram level: round r's row pass covers features [r kg, (r + 1) kg) by id, so
     // bscr holds features [0, g0) (not visiting positions); a larger sibling is derived
     st.scr_n = 0;
@@ -3347,6 +3352,16 @@ __global__ __launch_bounds__(256) void k_fill_active(Ctx c) {
 
 __global__ void k_init_counters(Ctx c) { c.counters[kPool] = c.T; }
 
+// per-level setup in one launch: zero the next level's open-list counters (set `set`) and,
+// pool >= 0, publish the level's node-pair reservation -- replaces a memset and a host->device
+// copy, i.e. two of the commands the host issues one by one while the GPU waits right after
+// the level's count read-back
+__global__ void k_level_setup(Ctx c, int set, int pool) {
+  const int i = threadIdx.x;
+  if (i < kTiers) c.counters[set * kTiers + i] = 0;
+  if (i == kTiers && pool >= 0) c.counters[kPool] = pool;
+}
+
 // Buckets one level's staged wave/block-tier children into the next level's open lists.
 // 1024 staging slots per workgroup; each tier's positions come from wave scans and ONE atomic
 // per tier per workgroup, and the subtree tier's node pairs (subtree_max_splits) are reserved
@@ -3802,7 +3817,6 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   const size_t lds_s = sub_lds(a);
   const size_t lds_s32 = sub_lds(a, 32);
   const size_t lds_w = fused_lds(a, (int)a->kg_wave);
-  int32_t* h_pool = h + 48;   // pinned slot for the per-level pool reservation (H2D)
   const size_t lds_b = fused_lds(a, (int)a->kg_block);
   const int CH = c.CH;
   // k_hist_large's dynamic LDS, optionally padded (DML_LARGE_LDS_MIN bytes) to cap its
@@ -3854,7 +3868,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     if (++levels > 1 << 20) return 8;
     const int64_t open_now = (int64_t)ns + ns4 + nw + nb + nL;
     peak_open = std::max(peak_open, open_now);
-    HIP_OK(hipMemsetAsync(c.counters + (1 - cur) * kTiers, 0, kTiers * 4, st));
+    int level_pool = -1;   // k_level_setup below
     // reserve the child pairs of every wave/block-tier node of this level up front (a
     // big-subtree node's pairs were reserved with its subtree's: k_compact / k_bigsub)
     const int64_t pair_w = h[kPool], pair_b = pair_w + (big ? 0 : 2LL * nw), pool_next = pair_b + 2LL * nb;
@@ -3869,10 +3883,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       a->status_out = 1;
       return 0;
     }
-    if ((big ? 0 : nw) + nb) {
-      *h_pool = (int32_t)pool_next;
-      HIP_OK(hipMemcpyAsync(c.counters + kPool, h_pool, 4, hipMemcpyHostToDevice, st));
-    }
+    if ((big ? 0 : nw) + nb) level_pool = (int)pool_next;
+    k_level_setup<<<1, 64, 0, st>>>(c, 1 - cur, level_pool);
     a->tier_nodes_out[0] += ns + ns4; a->tier_nodes_out[1] += nw; a->tier_nodes_out[2] += nb; a->tier_nodes_out[3] += nL;
     SideStreams* ss = side_streams();
     static const bool serial_tiers = getenv("DML_SERIAL_TIERS") != nullptr;   // profiling: tiers one after another
@@ -3941,12 +3953,12 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       c.gf_prev = fb->gf[1 - fpar];
       c.pinfo_cur = fb->pinfo + (int64_t)fpar * fb->pi_cap;
       c.pinfo_next = fb->pinfo + (int64_t)(1 - fpar) * fb->pi_cap;
+      c.pi_cap = fb->pi_cap;
     }
     if (nL && full) {
       k_large_prep<<<nL, 64, 0, st>>>(c, cur, nL);
       const int rounds = (int)((a->d + a->kg_large - 1) / a->kg_large);
       HIP_OK(hipMemsetAsync(c.gf_cur, 0, (size_t)nL * full_node_b, st));
-      HIP_OK(hipMemsetAsync(c.pinfo_next, 0xFF, (size_t)std::min<int64_t>(2LL * nL, fb->pi_cap) * sizeof(int4), st));
       const dim3 gh = DML_LARGE_NODE_FAST ? dim3((unsigned)nL, nchunks) : dim3(nchunks, (unsigned)nL);
       for (int round = 0; round < rounds; ++round) {
         ++large_rounds;

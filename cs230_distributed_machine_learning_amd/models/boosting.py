@@ -408,7 +408,10 @@ class GradientBoostingFamily(Family):
                 # feature-major bins: the large tier's gathers of a dense sorted row set coalesce
                 # (64 rows of one feature in 1-2 cache lines instead of 64 row lines)
                 xbt = data.binned_feature_major() if hasattr(data, "binned_feature_major") else None
-                fb = forest_ops.build_gpu(Xb, None, tgt, roles_t, specs, 1, True, self.tiers, ystride=n, XbT=xbt)
+                # per-tree active-row counts: fixed while the roles are (no subsample draw)
+                ccache = cst.setdefault("count_cache", {}) if not sub_rows else None
+                fb = forest_ops.build_gpu(Xb, None, tgt, roles_t, specs, 1, True, self.tiers, ystride=n, XbT=xbt,
+                                          count_cache=ccache)
                 if limit.any():   # sklearn's best-first tree (friedman_mse and squared_error rank splits alike)
                     forest_ops.prune_max_leaves(fb, specs, limit)
                 if ccp.any():     # minimal cost-complexity pruning of each stage tree (variance impurity)

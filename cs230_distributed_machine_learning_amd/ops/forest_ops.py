@@ -411,7 +411,7 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
               specs: np.ndarray, n_classes: int, is_reg: bool, tiers: ForestTiers | None = None,
               ystride: int = 0, reuse_pool: bool = False, XbT: Optional[torch.Tensor] = None,
               cw: Optional[np.ndarray] = None, mono: Optional[np.ndarray] = None,
-              early_predict=None) -> ForestBuild:
+              early_predict=None, count_cache: Optional[dict] = None) -> ForestBuild:
     """``ystride > 0``: ``yreg`` is a [targets, ystride] matrix and tree t regresses on
     row ``specs[t]['target']`` (gradient boosting's per-fit pseudo-residuals).
     ``reuse_pool``: the node arrays live in the device arena and are valid until the
@@ -419,7 +419,10 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     ``early_predict``: (make(nodes, vals) -> GpuPredict, done int32[F]) -- fit f is predicted
     by the builder right after level done[f] (its trees are complete by then), overlapping the
     deeper fits; entries it launched come back as -2 (``ForestBuild.predict`` holds the
-    GpuPredict; the caller predicts the other fits)."""
+    GpuPredict; the caller predicts the other fits).
+    ``count_cache``: a dict kept by the caller for as long as ``roles`` and the specs' split /
+    bootstrap fields stay the same (boosting stages of one active set): the per-tree active-row
+    counts are computed once into it and reused (no count kernel, no read-back)."""
     lib = native.hip_lib()
     dev = Xb.device
     T = len(specs)
@@ -429,7 +432,8 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     tiers = (tiers or ForestTiers()).fitted(CH)
     stream = native.stream_handle(dev)
     specs_dev = _h2d(specs.view(np.uint8), dev)
-    active = torch.zeros(T, dtype=torch.int32, device=dev)
+    cached = count_cache is not None and "active" in count_cache
+    active = count_cache["active"] if cached else torch.zeros(T, dtype=torch.int32, device=dev)
     a = native.ForestArgs()
     a.Xb, a.ld, a.n, a.d = native.ptr(Xb), Xb.stride(0), n, d
     a.ycls = native.ptr(ycls) if ycls is not None else 0
@@ -472,16 +476,22 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     a.active_count = native.ptr(active)
     t0 = time.perf_counter()
     with trace.range("forest_count"):
-        rc = lib.dml_forest_count(ctypes.byref(a), stream)
-        if rc:
-            raise RuntimeError(f"dml_forest_count failed ({rc}): {native.hip_error(lib)}")
-        counts = active.cpu().numpy().astype(np.int64)
+        if cached:
+            counts, row_off, row_off_dev = count_cache["counts"], count_cache["row_off"], count_cache["row_off_dev"]
+        else:
+            rc = lib.dml_forest_count(ctypes.byref(a), stream)
+            if rc:
+                raise RuntimeError(f"dml_forest_count failed ({rc}): {native.hip_error(lib)}")
+            counts = active.cpu().numpy().astype(np.int64)
     if exp_cnt is not None:
         cnt = exp_cnt() if callable(exp_cnt) else exp_cnt
         a.yq_e1, a.yq_e2 = reg_exponents_of_counts(cnt)
-    row_off = np.zeros(T + 1, dtype=np.int64)
-    np.cumsum(counts, out=row_off[1:])
-    row_off_dev = _h2d(row_off, dev)
+    if not cached:
+        row_off = np.zeros(T + 1, dtype=np.int64)
+        np.cumsum(counts, out=row_off[1:])
+        row_off_dev = _h2d(row_off, dev)
+        if count_cache is not None:
+            count_cache.update(active=active, counts=counts, row_off=row_off, row_off_dev=row_off_dev)
     a.row_off = native.ptr(row_off_dev)
     a.rows_total = int(row_off[-1])
     a.max_active = int(counts.max()) if T else 0
