@@ -2899,12 +2899,20 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
     }
   } else {
     CT* gh = (CT*)gbase + goff;
+    // whole-feature buffers of unit-weight trees keep the count plane as u32 row counts too
+    // (gcnt: half the flush atomics' bytes for that plane; see whole_counts_u32)
+    const bool gcnt = MODE == 2 && fround >= 0 && s.bootstrap == 0;
     for (int i = threadIdx.x; i < g * span; i += 256) {
       CT v = hist[i];
-      if (MODE == 2 && uw && (i % span) < 256) {   // u32 row counts -> (w | rows << 32), w = rows
-        const int j = i / span, b = i % span;
-        const unsigned long long n1 = ((const uint32_t*)(hist + j * span))[b];
-        v = (CT)(n1 | (n1 << 32));
+      const int j = i / span, b = i - j * span;
+      if (MODE == 2 && b < 256 && (uw || gcnt)) {
+        // row count of bin b: the u32 LDS counters, or rows << 32 of the (w | rows << 32) plane
+        const uint32_t n1 = uw ? ((const uint32_t*)(hist + j * span))[b] : (uint32_t)((uint64_t)v >> 32);
+        if (gcnt) {
+          if (n1) atomicAdd((uint32_t*)(gh + j * span) + b, n1);
+          continue;
+        }
+        v = (CT)((unsigned long long)n1 | ((unsigned long long)n1 << 32));   // w = rows
       }
       if (v != (CT)0) atomicAdd(&gh[i], v);
     }
@@ -2930,6 +2938,18 @@ __global__ __launch_bounds__(256) void k_hist_derive(Ctx c) {
 
 __device__ void large_commit(const Ctx& c, const NodeSpec& s, LState& st, int slot, const double* best_left, int set_cur);
 
+// whole-feature regression histogram of a unit-weight tree: bins 0..255 of the count plane are
+// u32 row counts (k_hist_large's gcnt flush) in the plane's first KB; element i of the usual
+// (w | rows << 32, w yq) layout.  Derivation (parent - sibling, as u64 words) stays exact on the
+// packed counts: every parent bin count >= the sibling's, so no borrow crosses a u32 boundary.
+__device__ __forceinline__ unsigned long long whole_counts_u32(const unsigned long long* h, int i) {
+  if (i < 256) {
+    const unsigned long long n1 = ((const uint32_t*)h)[i];
+    return n1 | (n1 << 32);
+  }
+  return h[i];
+}
+
 // evaluates the node's global histogram; MODE here is the GLOBAL layout (0 or 2)
 template <int MODE>
 __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
@@ -2951,9 +2971,12 @@ __global__ __launch_bounds__(256) void k_split_large(Ctx c, int set_cur) {
   const int16_t* feats = c.lperm + (int64_t)slot * c.d + st.pos;
   if (c.full_cur) {   // whole-feature buffer: the group's features by id
     const CT* gf = (const CT*)c.gf_cur + (int64_t)slot * c.d * span;
+    const bool gcnt = MODE == 2 && s.bootstrap == 0;
     for (int i = tid; i < g * span; i += 256) {
       const int j = i / span;
-      hist[i] = gf[(int64_t)feats[j] * span + (i - j * span)];
+      const CT* hf = gf + (int64_t)feats[j] * span;
+      if constexpr (MODE == 2) hist[i] = gcnt ? (CT)whole_counts_u32(hf, i - j * span) : hf[i - j * span];
+      else hist[i] = hf[i - j * span];
     }
   } else {
     const CT* gh = (const CT*)c.ghist + (int64_t)slot * c.kg_large * span;
@@ -3028,6 +3051,13 @@ __global__ __launch_bounds__(256) void k_split_full(Ctx c) {
     for (int i = lane; i < span && active; i += 64) lh[i] = h[i];
     h = lh;
     __syncthreads();
+  } else {
+    if (s.bootstrap == 0) {   // u32 count plane (whole_counts_u32) -> the evaluator's layout, in LDS
+      CT* lh = (CT*)smem + (int64_t)wid * span;
+      for (int i = lane; i < span && active; i += 64) lh[i] = (CT)whole_counts_u32(h, i);
+      h = lh;
+      __syncthreads();
+    }
   }
   if (!active) return;
   const double nlo = c.nbound ? c.nbound[2 * (int64_t)st.on.node] : -INFINITY;
@@ -3971,7 +4001,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       }
       // every candidate in one launch (class planes staged in LDS: 4 features' worth, within
       // the default 64 KB; more classes than that keep the per-group rounds)
-      const size_t lds_sf = GM == 0 ? (size_t)4 * ghist_feat_bytes(0, CH) : 0;
+      const size_t lds_sf = (size_t)4 * ghist_feat_bytes(GM, CH);
       if (lds_sf <= 64 * 1024) {
         k_split_full<GM><<<dim3((unsigned)nL, (unsigned)((a->d + 3) / 4)), 256, lds_sf, st>>>(c);
         k_split_full_select<GM><<<nL, 64, 0, st>>>(c, cur);

@@ -418,8 +418,8 @@ def test_gpu_monotonic_cst_family_matches_host_path():
         assert np.allclose(g.result["cv_scores"], c.result["cv_scores"], rtol=0, atol=1e-12)
 
 
-@pytest.mark.parametrize("is_reg", [False, True])
-def test_gpu_whole_histogram_levels_match_cpu(is_reg, monkeypatch):
+@pytest.mark.parametrize("is_reg,boot", [(False, 1), (True, 1), (True, 0)])
+def test_gpu_whole_histogram_levels_match_cpu(is_reg, boot, monkeypatch):
     """max_features == d (boosting, max_features=None): large-tier levels keep every node's
     histogram over all features and derive the larger of two large siblings as parent -
     smaller sibling (k_hist_derive).  Trees equal the C++ builder's and the row-pass build's
@@ -435,9 +435,11 @@ def test_gpu_whole_histogram_levels_match_cpu(is_reg, monkeypatch):
     dev = torch.device("cuda:0")
     Xb = binning.bin_matrix(torch.from_numpy(X).to(dev), binning.quantile_edges(torch.from_numpy(X).to(dev)))
     roles, _ = make_split_roles(y, 3, not is_reg, holdout=False)
-    specs = _specs(3, 4, d, k=d, criterion=2 if is_reg else 0, max_depth=9)
+    # boot 0: unit row weights -- the regression large tier keeps u32 row counts in LDS and in
+    # the whole-feature buffers (k_hist_large gcnt, whole_counts_u32)
+    specs = _specs(3, 4, d, k=d, criterion=2 if is_reg else 0, max_depth=9, bootstrap=boot)
     T = len(specs)
-    tiers = forest_ops.ForestTiers(sub_max=64, wave_max=256, block_max=1024, chunk=1024)
+    tiers = forest_ops.ForestTiers(sub_max=64, wave_max=256, block_max=1024, chunk=1024, chunk_reg=1024)
     yt = torch.from_numpy(y).to(dev)
     args = (None, yt, torch.from_numpy(roles).to(dev), specs, 1, True) if is_reg else \
         (yt.to(torch.int32), None, torch.from_numpy(roles).to(dev), specs, 3, False)
