@@ -32,14 +32,63 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build the HIP kernels)")
 
 
+def _portable_flag(f: str) -> str:
+    """A flag as it enters the content hash: paths relative to the package, a compiler by
+    basename -- a tree moved to another path (the GPU box's scratch copy) hashes the same."""
+    if os.path.isabs(f):
+        return os.path.relpath(f, CSRC) if f.startswith(CSRC) else os.path.basename(f)
+    return f
+
+
+_VERSIONS: dict = {}
+
+
+def _compiler_version(exe: str) -> str:
+    if exe not in _VERSIONS:
+        try:
+            out = subprocess.run([exe, "--version"], capture_output=True, text=True, timeout=60).stdout
+            _VERSIONS[exe] = out.splitlines()[0] if out else ""
+        except Exception:
+            _VERSIONS[exe] = ""
+    return _VERSIONS[exe]
+
+
 def _src_hash(sources: list[str], flags: list[str]) -> str:
     import hashlib
 
-    h = hashlib.sha256(" ".join(flags).encode())
-    for s in sorted(sources):
+    h = hashlib.sha256(" ".join(_portable_flag(f) for f in flags).encode())
+    for f in flags[:1]:   # the compiler (first flag for the C++ builds) by version, not by path
+        if os.path.isabs(f) and os.path.exists(f):
+            h.update(_compiler_version(f).encode())
+    for s in sorted(sources, key=lambda p: os.path.relpath(p, CSRC)):
         with open(s, "rb") as f:
-            h.update(s.encode() + b"\0" + f.read())
+            h.update(os.path.relpath(s, CSRC).encode() + b"\0" + f.read())
     return h.hexdigest()
+
+
+class _BuildLock:
+    """An exclusive fcntl lock on ``lib/.build.lock``: ranks that start together (torchrun)
+    check staleness, build and stamp one at a time -- the first builds, the rest find the
+    stamp current and load the finished library."""
+
+    def __enter__(self):
+        import fcntl
+
+        os.makedirs(LIB, exist_ok=True)
+        self.f = open(os.path.join(LIB, ".build.lock"), "w")
+        fcntl.flock(self.f, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *a):
+        import fcntl
+
+        fcntl.flock(self.f, fcntl.LOCK_UN)
+        self.f.close()
+        return False
+
+
+def _tmp(out: str) -> str:
+    return f"{out}.{os.getpid()}.tmp"
 
 
 def _stale_by_hash(target: str, sources: list[str], flags: list[str]) -> bool:
@@ -76,28 +125,33 @@ def build_hip(force: bool = False, out: str = HIP_LIB, extra_flags: tuple = ()) 
     # staleness by CONTENT (sources + headers + flags), never by mtime: the .so files are
     # git-ignored but travel with the tree to the GPU box, where every file has a fresh
     # mtime -- an mtime test there could keep a library that does not match the sources
-    if force or _stale_by_hash(out, srcs + hdrs, flags):
-        # one hipcc per translation unit, in parallel (forest.hip alone is most of the
-        # build), then one link; a unit whose own content hash is unchanged keeps its object
-        from concurrent.futures import ThreadPoolExecutor
-
-        objdir = os.path.join(LIB, "obj", os.path.basename(out)[:-3])
-        os.makedirs(objdir, exist_ok=True)
-        objs = [os.path.join(objdir, os.path.basename(s)[:-4] + ".o") for s in srcs]
-
-        def compile_one(so):
-            src, obj = so
-            if force or _stale_by_hash(obj, [src] + hdrs, flags):
-                _run([_hipcc(), *flags, "-c", src, "-o", obj])
-                _stamp(obj, [src] + hdrs, flags)
-
-        with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-            list(ex.map(compile_one, zip(srcs, objs)))
-        tmp = out + ".tmp"
-        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", *objs, "-o", tmp])
-        os.replace(tmp, out)
-        _stamp(out, srcs + hdrs, flags)
+    with _BuildLock():
+        if force or _stale_by_hash(out, srcs + hdrs, flags):
+            _build_hip_locked(out, srcs, hdrs, flags, force)
     return out
+
+
+def _build_hip_locked(out, srcs, hdrs, flags, force) -> None:
+    # one hipcc per translation unit, in parallel (forest.hip alone is most of the
+    # build), then one link; a unit whose own content hash is unchanged keeps its object
+    from concurrent.futures import ThreadPoolExecutor
+
+    objdir = os.path.join(LIB, "obj", os.path.basename(out)[:-3])
+    os.makedirs(objdir, exist_ok=True)
+    objs = [os.path.join(objdir, os.path.basename(s)[:-4] + ".o") for s in srcs]
+
+    def compile_one(so):
+        src, obj = so
+        if force or _stale_by_hash(obj, [src] + hdrs, flags):
+            _run([_hipcc(), *flags, "-c", src, "-o", obj])
+            _stamp(obj, [src] + hdrs, flags)
+
+    with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        list(ex.map(compile_one, zip(srcs, objs)))
+    tmp = _tmp(out)
+    _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", *objs, "-o", tmp])
+    os.replace(tmp, out)
+    _stamp(out, srcs + hdrs, flags)
 
 
 def build_cpu(force: bool = False) -> str:
@@ -106,11 +160,12 @@ def build_cpu(force: bool = False) -> str:
     os.makedirs(LIB, exist_ok=True)
     cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
     flags = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-ffp-contract=off"]
-    if force or _stale_by_hash(CPU_LIB, deps, flags):
-        tmp = CPU_LIB + ".tmp"
-        _run([*flags, "-I", os.path.join(CSRC, "kernels"), *srcs, "-o", tmp])
-        os.replace(tmp, CPU_LIB)
-        _stamp(CPU_LIB, deps, flags)
+    with _BuildLock():
+        if force or _stale_by_hash(CPU_LIB, deps, flags):
+            tmp = _tmp(CPU_LIB)
+            _run([*flags, "-I", os.path.join(CSRC, "kernels"), *srcs, "-o", tmp])
+            os.replace(tmp, CPU_LIB)
+            _stamp(CPU_LIB, deps, flags)
     return CPU_LIB
 
 
@@ -127,11 +182,12 @@ def build_sanitized(force: bool = False) -> str:
     cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
     flags = [cxx, "-O1", "-g", "-std=c++17", "-fopenmp", "-ffp-contract=off", "-fsanitize=address,undefined",
              "-fno-sanitize-recover=all", "-fno-omit-frame-pointer"]
-    if force or _stale_by_hash(SAN_EXE, deps, flags):
-        tmp = SAN_EXE + ".tmp"
-        _run([*flags, "-I", os.path.join(CSRC, "kernels"), *srcs, "-o", tmp])
-        os.replace(tmp, SAN_EXE)
-        _stamp(SAN_EXE, deps, flags)
+    with _BuildLock():
+        if force or _stale_by_hash(SAN_EXE, deps, flags):
+            tmp = _tmp(SAN_EXE)
+            _run([*flags, "-I", os.path.join(CSRC, "kernels"), *srcs, "-o", tmp])
+            os.replace(tmp, SAN_EXE)
+            _stamp(SAN_EXE, deps, flags)
     return SAN_EXE
 
 

@@ -278,8 +278,26 @@ class MLTaskManager:
             if bar is not None:
                 bar.close()
 
-    def download_best_model(self, job_id=None, model_path=None, model_id=None, dest: Optional[str] = None):
-        """Fetch the stored best model (``.npz`` artefact); returns the local path."""
+    @staticmethod
+    def load_model(path: str):
+        """A downloaded ``.npz`` artefact as an estimator-like object with ``predict``,
+        ``predict_proba`` / ``decision_function`` (classifiers), ``score`` and ``transform``
+        (PCA) -- the usable model the reference hands over as a pickle
+        (DistributedLibrary/src/distributed_ml/core.py:201-206); loading executes nothing."""
+        from ..engine.model_store import load_predictor
+
+        return load_predictor(path)
+
+    def download_best_model(self, job_id=None, model_path=None, model_id=None, dest: Optional[str] = None,
+                            load: bool = False):
+        """Fetch the stored best model (``.npz`` artefact); returns the local path, or with
+        ``load=True`` the loaded estimator (:meth:`load_model`)."""
+        out = self._download_model(job_id, model_path, model_id, dest)
+        if load and isinstance(out, str):
+            return self.load_model(out)
+        return out
+
+    def _download_model(self, job_id=None, model_path=None, model_id=None, dest: Optional[str] = None):
         job_id = job_id or self.job_id
         body = {"model_path": model_path, "model_id": model_id}
         if self._local is not None:

@@ -301,7 +301,7 @@ class GradientBoostingFamily(Family):
         train_idx = [torch.nonzero(train[f]).squeeze(1) for f in range(F)]
         # fused HIP stage (csrc/kernels/gbrt.hip): gradient, leaf line search and raw update as
         # three kernels per stage instead of torch glue (losses with sums-only line searches)
-        fused = (gpu and not sharded and os.environ.get("DML_GB_FUSED", "1") != "0"
+        fused = (gpu and not sharded and os.environ.get("DML_GB_FUSED", "1") != "0" and K <= 64
                  and all(t.params["loss"] in (LOSS_SQ, LOSS_LOG, LOSS_EXP) for t in batch)
                  and max(t.params["max_depth"] for t in batch) <= 8
                  and getattr(native.hip_lib(), "dml_gb_stage", None) is not None)

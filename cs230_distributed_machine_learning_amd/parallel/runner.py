@@ -312,7 +312,14 @@ class WorkerCore:
             binned = ctl is not None and _binned_only_table(ctl, plan, X, self.device)
             self.store_raw().set(mode_key, "binned" if binned else "full")
         else:
-            self.store_raw().wait([mode_key])
+            # on the side group, bounded like the side collectives themselves: a rank 0 that
+            # fails before publishing the mode must not hold this thread past the side deadline
+            if group is not None:
+                import datetime
+
+                self.store_raw().wait([mode_key], datetime.timedelta(seconds=dist.side_timeout_s()))
+            else:
+                self.store_raw().wait([mode_key])
             binned = self.store_raw().get(mode_key).decode() == "binned"
         if binned:   # tree job on a table too large for HBM as float32: bins only
             dd = pdata.broadcast_binned(X, y, clf, self.device, name=msg["dataset_id"], group=group, tag=tag)
@@ -610,8 +617,13 @@ def needs_whole_rows(model_type: str, params: Dict[str, Any]) -> bool:
     """A candidate the row-sharded builders cannot fit exactly: absolute_error trees need
     per-node weighted medians over every row, and monotonic_cst's node bounds are not part of
     the row-sharded forest builder -- such a job runs task-parallel (never a silently
-    different estimator; reference aws-prod/worker/worker.py:45,452 forwards params verbatim)."""
-    if not (model_type.startswith("RandomForest") or model_type.startswith("GradientBoosting")):
+    different estimator; reference aws-prod/worker/worker.py:45,452 forwards params verbatim).
+    GradientBoosting: leaf percentiles (absolute_error / huber / quantile losses) and the
+    early-stopping validation split are not sums over row shards (models/boosting.py _boost)."""
+    if model_type.startswith("GradientBoosting"):
+        return (params.get("loss") in ("absolute_error", "lad", "huber", "quantile")
+                or bool(params.get("n_iter_no_change")) or params.get("monotonic_cst") is not None)
+    if not model_type.startswith("RandomForest"):
         return False
     return params.get("criterion") == "absolute_error" or params.get("monotonic_cst") is not None
 
@@ -1061,6 +1073,16 @@ class DistributedRunner(Runner):
             log.error("process group broken (%s): host staging and store copies from now on", why)
         pending = [(t["kind"], t["job"]) for t in self.coll_pending.values()]
         pending += [(task["kind"], js) for task, js, _ in self.coll_deferred]
+        # the abandoned tasks' store keys: a posted task becomes a stop (a collective thread
+        # that has not reached it yet exits instead of entering a collective on the broken
+        # group) and answers already written are dropped (a later one is never read)
+        for i, t in self.coll_pending.items():
+            try:
+                self.st.set(f"coll/{i}", json.dumps({"kind": "stop"}))
+                for wid in t.get("waiting", ()):
+                    self.st.delete_key(f"colldone/{wid}/{i}")
+            except Exception:  # pragma: no cover - store gone with the service
+                pass
         self.coll_pending.clear()
         self.coll_deferred = []
         for kind, js in pending:

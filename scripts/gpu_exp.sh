@@ -66,5 +66,11 @@ case "$kind" in
            DML_FORCE_PG=1 MASTER_PORT=29601 timeout -k 10 900 python -u bench.py --e2e > gpurun_out/exp_e2e_dist.log 2>&1 && tail -1 gpurun_out/exp_e2e_dist.log | cut -c1-300 ;;
   rccljob) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/exp_rccljob -o run -- python3 -m pytest -x -q tests/test_rccl_gpu.py > gpurun_out/exp_rccljob.log 2>&1 && \
            rm -f gpurun_out/exp_rccljob/*kernel_trace.csv && grep -i -c "nccl\|rccl" gpurun_out/exp_rccljob/run_kernel_stats.csv ;;
+  lrprof)  args=${*:-10000000 1000 2560}
+           timeout -k 10 300 python -u scripts/lr_kernel_bench.py $args > gpurun_out/exp_lrk.log 2>&1 && tail -1 gpurun_out/exp_lrk.log && \
+           timeout -s KILL 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lr_kt -o p -- python3 scripts/lr_kernel_bench.py $args > gpurun_out/lr_kt.log 2>&1 && echo KT_OK && \
+           timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/lr_a -o p -- python3 scripts/lr_kernel_bench.py $args > gpurun_out/lr_a.log 2>&1 && echo PA_OK && \
+           timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE TCC_HIT_sum GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/lr_b -o p -- python3 scripts/lr_kernel_bench.py $args > gpurun_out/lr_b.log 2>&1 && echo PB_OK && \
+           timeout -k 10 400 python -u bench.py --config lr --steps 2 --warmup 1 > gpurun_out/exp_lrbench.log 2>&1 && tail -1 gpurun_out/exp_lrbench.log | cut -c1-1500 ;;
   *) echo "unknown kind $kind"; exit 2 ;;
 esac
