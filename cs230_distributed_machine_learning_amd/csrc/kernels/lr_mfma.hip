@@ -64,6 +64,7 @@ struct FwdArgs {
   int64_t y, roles;              // int32 [n], uint8 [S x n]
   int64_t rh, rl, kr;            // R^T hi/lo, K-tiled over col_tiles*BN rows, kr (= xrows) deep
   int64_t loss;                  // double [F] (accumulated; caller zeroes)
+  int64_t lpart;                 // v3: double [row_tiles x col_tiles*BN] per-item column loss partials
 };
 
 struct GradArgs {
@@ -192,6 +193,12 @@ __device__ __forceinline__ void gemm_tile(const Operands& op, int64_t row0, int6
   for (int64_t k = kb; k < ke; k += BK) {
     if (k + BK < ke) glds_stage(op, row0, col0, k + BK, smem + (cur ^ 1) * STAGE, tid);
     mma_stage(smem + cur * STAGE, acc, wm, wn, lane);
+#ifndef LRM_NO_SCHED_FENCE
+    // keep every MFMA of the step ahead of the barrier: the scheduler otherwise hoists the
+    // barrier (and its vmcnt(0) drain of the next stage's LDS-DMA) to just after the last
+    // fragment read, leaving only half the step's MFMAs to cover the DMA latency
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     __syncthreads();   // drains this wave's LDS-DMA (vmcnt(0)) and publishes the stage
     cur ^= 1;
   }
@@ -439,6 +446,264 @@ __global__ __launch_bounds__(256) void k_split_hilo(const float* __restrict__ sr
   }
 }
 
+
+// ---- v3: 256 x 128 output tiles, 8 waves, 3-stage LDS-DMA ring, one workgroup per CU ----------
+// The 2-stage kernels above leave a stage's DMA latency covered by ONE step of MFMAs (and two
+// workgroups per CU at 64 KB of staging each); the forward's W^T operand (all fits' columns,
+// 10 MB at 2560 fits) does not stay in an XCD's 4 MB L2, so its misses outlast that cover.  Here
+// a stage is loaded TWO steps ahead (3 buffers x 48 KB), the barrier waits with a counted
+// vmcnt (the newest stage stays in flight across it), and a 256-row tile halves the forward's
+// W^T traffic per row.  The forward walks a static round-robin of (row tile, column tile) items
+// per XCD (row tiles rt % 8 == XCD, so a row tile's 20-odd column items share that XCD's L2);
+// each item writes its per-column loss partials to lpart (summed over row tiles by the host).
+namespace v3 {
+constexpr int WMW = 4, WNW = 2;
+constexpr int TM = 64 * WMW, TN = 64 * WNW;             // 256 x 128
+constexpr int NT = 64 * WMW * WNW;                      // 512 threads
+constexpr int NST = 3;
+constexpr int APART = TM * BK, BPART = TN * BK;         // bf16 elements of one part of one stage
+constexpr int STG = 2 * APART + 2 * BPART;
+constexpr int STG_BYTES = NST * STG * 2;                // 144 KB
+constexpr int A_INSTR = APART * 2 / 1024;               // 1-KiB wave-instructions per A part
+constexpr int B_INSTR = BPART * 2 / 1024;
+constexpr int STAGE_INSTR = 2 * A_INSTR + 2 * B_INSTR;
+constexpr int PER_WAVE = STAGE_INSTR / (NT / 64);       // LDS-DMA instructions per wave per stage
+static_assert(STAGE_INSTR % (NT / 64) == 0, "stage must split evenly over the waves");
+static_assert(TM * TN * 4 + 4 * TN * 8 + TM * 4 <= STG_BYTES, "epilogue scratch must fit the staging LDS");
+}  // namespace v3
+
+// counted wait for this wave's LDS-DMA + its LDS reads, then the workgroup barrier.  Inline asm
+// (not __syncthreads, whose fence drains vmcnt(0)): the newest stage stays in flight.
+template <int N>
+__device__ __forceinline__ void v3_wait_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void v3_glds_piece(const uint16_t* src, uint16_t* dst, int slot0, int lane) {
+  const int p = slot0 + lane, row = p >> 2;
+  const int srci = row * 4 + swz(row, p & 3);   // swizzle on the source side (swz is an involution)
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(uintptr_t)(src + srci * 8),
+                                   (__attribute__((address_space(3))) void*)(dst + slot0 * 8), 16, 0, 0);
+}
+
+// one stage = 48 one-KiB pieces; wave w fetches pieces 2w, 2w+1 of A hi and of A lo and piece w
+// of B hi and of B lo (6 per wave, parts fixed at compile time, w wave-uniform)
+__device__ __forceinline__ void v3_glds_stage(const Operands& op, int64_t row0, int64_t col0, int64_t k0,
+                                              uint16_t* st, int w, int lane) {
+  using namespace v3;
+  static_assert(A_INSTR == 2 * (NT / 64) && B_INSTR == NT / 64, "piece split assumes 8 waves, 256 x 128");
+  const int64_t ab = ((k0 >> 5) * op.arows + row0) * BK, bb = ((k0 >> 5) * op.brows + col0) * BK;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    v3_glds_piece(op.ah + ab, st, (2 * w + h) * 64, lane);
+    v3_glds_piece(op.al + ab, st + APART, (2 * w + h) * 64, lane);
+  }
+  v3_glds_piece(op.bh + bb, st + 2 * APART, w * 64, lane);
+  v3_glds_piece(op.bl + bb, st + 2 * APART + BPART, w * 64, lane);
+}
+
+__device__ __forceinline__ void v3_mma(const uint16_t* st, f32x4 (&acc)[4][4], int wm, int wn, int lane) {
+  using namespace v3;
+  const int r = lane & 15, g = lane >> 4;
+  bf16x8 ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int arow = wm * 64 + i * 16 + r;
+    const int brow = wn * 64 + i * 16 + r;
+    ah[i] = frag(st, arow, g);
+    al[i] = frag(st + APART, arow, g);
+    bh[i] = frag(st + 2 * APART, brow, g);
+    bl[i] = frag(st + 2 * APART + BPART, brow, g);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+    }
+}
+
+// C[row0:+256, col0:+128] over k in [kb, ke) (bf16x3); every wave owns a 64 x 64 quadrant.
+// Ends with a barrier after every DMA has landed (the staging LDS is free afterwards).
+__device__ __forceinline__ void v3_gemm(const Operands& op, int64_t row0, int64_t col0, int64_t kb, int64_t ke,
+                                        uint16_t* smem, f32x4 (&acc)[4][4], int tid) {
+  using namespace v3;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t nk = (ke - kb) / BK;
+  if (nk <= 0) return;
+  const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), wm = w >> 1, wn = w & 1;
+  v3_glds_stage(op, row0, col0, kb, smem, w, lane);
+  if (nk > 1) v3_glds_stage(op, row0, col0, kb + BK, smem + STG, w, lane);
+  int cur = 0;   // buffer of step t (t % 3)
+  for (int64_t t = 0; t < nk; ++t) {
+    // stage t landed (stage t+1 may stay in flight); every wave is done with step t-1's buffer
+    if (t + 1 < nk) v3_wait_barrier<PER_WAVE>();
+    else v3_wait_barrier<0>();
+    const int nxt = cur == 0 ? 2 : cur - 1;   // (t + 2) % 3 == (t - 1) % 3
+    if (t + 2 < nk) v3_glds_stage(op, row0, col0, kb + (t + 2) * BK, smem + nxt * STG, w, lane);
+    v3_mma(smem + cur * STG, acc, wm, wn, lane);
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+  v3_wait_barrier<0>();
+}
+
+__global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
+  using namespace v3;
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[STG_BYTES];
+  uint16_t* smem = reinterpret_cast<uint16_t*>(smem_raw);
+  float* zs = reinterpret_cast<float*>(smem_raw);                              // Z tile, after the GEMM
+  double* lq = reinterpret_cast<double*>(smem_raw + TM * TN * 4);              // [4][TN] row-quarter partials
+  int32_t* ys = reinterpret_cast<int32_t*>(smem_raw + TM * TN * 4 + 4 * TN * 8);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  const int64_t b = blockIdx.x, xcd = b & 7, slot = b >> 3, slots = gridDim.x >> 3;
+  const int64_t rt_here = a.row_tiles > xcd ? (a.row_tiles - xcd + 7) / 8 : 0;
+  const int64_t items = rt_here * a.col_tiles;
+  const auto col_fit = GPTR(const int32_t, a.col_fit);
+  const auto bias = GPTR(const float, a.bias);
+  const auto y = GPTR(const int32_t, a.y);
+  const auto roles = GPTR(const uint8_t, a.roles);
+  const auto lpart = GPTR(double, a.lpart);
+  const Operands op{reinterpret_cast<const uint16_t*>(a.xh), reinterpret_cast<const uint16_t*>(a.xl), a.xrows,
+                    reinterpret_cast<const uint16_t*>(a.wh), reinterpret_cast<const uint16_t*>(a.wl),
+                    a.col_tiles * TN};
+  const int64_t Mp = a.col_tiles * TN;
+  const int c = tid & (TN - 1), rq = tid >> 7;   // epilogue: column c of the tile, 64-row quarter rq
+  for (int64_t it = slot; it < items; it += slots) {
+    const int64_t rt = xcd + 8 * (it / a.col_tiles), ct = it % a.col_tiles;
+    const int64_t row0 = rt * TM, col0 = ct * TN;
+    f32x4 acc[4][4];
+    v3_gemm(op, row0, col0, 0, a.Kp, smem, acc, tid);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wn * 64 + j * 16 + (lane & 15);
+        const float bv = bias[col0 + col];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = wm * 64 + i * 16 + (lane >> 4) * 4 + e;
+          zs[zidx(row, col)] = acc[i][j][e] + bv;
+        }
+      }
+    if (tid < TM) ys[tid] = row0 + tid < a.n ? y[row0 + tid] : 0;
+    __syncthreads();
+    // the lead column of a fit owns the fit's k columns for its 64 rows
+    const int f = col_fit[col0 + c];
+    const bool lead = f >= 0 && reinterpret_cast<const int32_t*>(a.fit_col0)[f] == col0 + c;
+    double lossq = 0.0;
+    if (lead) {
+      const int k = reinterpret_cast<const int32_t*>(a.fit_k)[f];
+      const int kind = reinterpret_cast<const int32_t*>(a.fit_kind)[f];
+      const int64_t role_off = (int64_t)reinterpret_cast<const int32_t*>(a.fit_split)[f] * a.n;
+      const float s0 = reinterpret_cast<const float*>(a.scale)[f];
+      const float* cwf = a.cw ? GPTR(const float, a.cw) + (int64_t)f * a.cwC : nullptr;
+      const auto RH = GPTR(uint16_t, a.rh) + (col0 + c) * BK;
+      const auto RL = GPTR(uint16_t, a.rl) + (col0 + c) * BK;
+      float lsum = 0.f;
+      for (int rr = 0; rr < 64; rr += 8) {
+        const int lr0 = rq * 64 + rr;
+        const int64_t g0 = row0 + lr0;
+        float sc[8];
+        int yv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int64_t g = g0 + e;
+          yv[e] = ys[lr0 + e];
+          const bool tr = g < a.n && roles[role_off + g] == 1;
+          sc[e] = tr ? (cwf ? s0 * cwf[yv[e]] : s0) : 0.f;
+        }
+        if (kind == 1) {
+          float lse[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float m = zs[zidx(lr0 + e, c)];
+            for (int jj = 1; jj < k; ++jj) m = fmaxf(m, zs[zidx(lr0 + e, c + jj)]);
+            float se = 0.f;
+            for (int jj = 0; jj < k; ++jj) se += __expf(zs[zidx(lr0 + e, c + jj)] - m);
+            lse[e] = m + __logf(se);
+            lsum += sc[e] * (lse[e] - zs[zidx(lr0 + e, c + yv[e])]);
+          }
+          for (int jj = 0; jj < k; ++jj) {
+            float r[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              r[e] = (__expf(zs[zidx(lr0 + e, c + jj)] - lse[e]) - (yv[e] == jj ? 1.f : 0.f)) * sc[e];
+            u32x4 hv, lv;
+            split8(r, hv, lv);
+            const int64_t off = ((g0 >> 5) * Mp + jj) * BK + (g0 & (BK - 1));
+            *(gvec_w)(RH + off) = hv;
+            *(gvec_w)(RL + off) = lv;
+          }
+        } else {
+          for (int jj = 0; jj < k; ++jj) {
+            float r[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float z = zs[zidx(lr0 + e, c + jj)];
+              const bool pos = kind == 0 ? yv[e] == 1 : yv[e] == jj;
+              const float ex = __expf(-fabsf(z));
+              const float inv = __builtin_amdgcn_rcpf(1.f + ex);
+              const float p = z >= 0.f ? inv : ex * inv;
+              const float t = pos ? -z : z;
+              lsum += sc[e] * (fmaxf(t, 0.f) + __logf(1.f + ex));
+              r[e] = (p - (pos ? 1.f : 0.f)) * sc[e];
+            }
+            u32x4 hv, lv;
+            split8(r, hv, lv);
+            const int64_t off = ((g0 >> 5) * Mp + jj) * BK + (g0 & (BK - 1));
+            *(gvec_w)(RH + off) = hv;
+            *(gvec_w)(RL + off) = lv;
+          }
+        }
+      }
+      lossq = (double)lsum;
+    }
+    lq[rq * TN + c] = lossq;
+    __syncthreads();
+    if (rq == 0) lpart[rt * Mp + col0 + c] = lq[c] + lq[TN + c] + lq[2 * TN + c] + lq[3 * TN + c];
+    __syncthreads();   // Z tile / labels / partials read before the next item's staging writes
+  }
+}
+
+__global__ __launch_bounds__(v3::NT, 1) void k_lr_grad3(GradArgs a) {
+  using namespace v3;
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[STG_BYTES];
+  uint16_t* smem = reinterpret_cast<uint16_t*>(smem_raw);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  const int64_t b = blockIdx.x, xcd = b & 7, local = b >> 3;
+  const int64_t tiles = a.m_tiles * a.n_tiles;
+  const int64_t tile = local % tiles;
+  const int64_t s = (local / tiles) * 8 + xcd;
+  if (s >= a.S) return;   // workgroup-uniform, before any barrier
+  const int64_t mt = tile / a.n_tiles, nt = tile % a.n_tiles;
+  const int64_t kb = s * a.Kc;
+  const int64_t ke = kb + a.Kc < a.Kp ? kb + a.Kc : a.Kp;
+  const Operands op{reinterpret_cast<const uint16_t*>(a.rh), reinterpret_cast<const uint16_t*>(a.rl),
+                    a.m_tiles * TM, reinterpret_cast<const uint16_t*>(a.xth), reinterpret_cast<const uint16_t*>(a.xtl),
+                    a.n_tiles * TN};
+  f32x4 acc[4][4];
+  v3_gemm(op, mt * TM, nt * TN, kb, ke, smem, acc, tid);
+  const int64_t ldo = a.n_tiles * TN;
+  const auto out = GPTR(float, a.out) + s * (a.m_tiles * TM) * ldo;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t col = nt * TN + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t row = mt * TM + wm * 64 + i * 16 + (lane >> 4) * 4 + e;
+        out[row * ldo + col] = acc[i][j][e];
+      }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -470,6 +735,27 @@ int dml_split_hilo(const float* src, int64_t rows, int64_t cols, int64_t ld, uin
   dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((cols + 63) / 64));
   if (grid.y > 65535) return 2;
   k_split_hilo<<<grid, 256, 0, st>>>(src, rows, cols, ld, hi, lo, drows, transpose);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// v3 (256 x 128 tiles, 3-stage ring): the row tile of X (forward) / of R^T (gradient)
+int dml_lr_v3_row_tile() { return v3::TM; }
+
+int dml_lr_mfma_fwd3(const FwdArgs* a, hipStream_t st) {
+  if (a->row_tiles <= 0 || a->col_tiles <= 0) return 0;
+  if (a->Kp % BK || a->row_groups % 8 || a->row_groups <= 0 || !a->lpart) return 2;
+  if (a->xrows != a->row_tiles * v3::TM || a->kr != a->xrows) return 2;
+  if (a->row_groups > 0x7fffffff) return 2;
+  k_lr_fwd3<<<(unsigned)a->row_groups, v3::NT, 0, st>>>(*a);   // row_groups = workgroups (persistent)
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+int dml_lr_mfma_grad3(const GradArgs* a, hipStream_t st) {
+  if (a->m_tiles <= 0 || a->n_tiles <= 0) return 0;
+  if (a->Kp % BK || a->Kc % BK || a->S % 8 || a->S <= 0 || a->S * a->Kc < a->Kp) return 2;
+  const int64_t blocks = a->m_tiles * a->n_tiles * a->S;
+  if (blocks > 0x7fffffff) return 2;
+  k_lr_grad3<<<(unsigned)blocks, v3::NT, 0, st>>>(*a);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

@@ -16,8 +16,9 @@ reported once and the job hangs below 100 % (D5, master/task_handler.py:91).  He
   after claiming its (k+1)-th slice, i.e. with claimed-but-unpublished work — what a
   crashed GPU process looks like to the controller, which must detect the silence and
   re-queue the slice to the survivors.
-* ``DML_STOP_RANK_IN="<rank>:<collective>"`` (``load`` / ``scores``) makes that rank SIGSTOP
-  itself on entering the named side-group collective: a HUNG peer (its sockets stay open,
+* ``DML_STOP_RANK_IN="<rank>:<collective>"`` (``load`` / ``scores`` side-group tasks, ``dp``
+  a data-parallel epoch, right after its table scatter) makes that rank SIGSTOP
+  itself on entering the named collective: a HUNG peer (its sockets stay open,
   unlike a dead one), which the survivors' collective timeouts must turn into a fallback;
   ``DML_FAIL_RANK_IN`` (same form) makes it raise there instead.
 """
@@ -132,6 +133,8 @@ def run_with_retries(fn, seed: int, slice_key: str, retries: Optional[int] = Non
             maybe_inject(seed, slice_key, attempt)
             return fn(), attempt + 1, None
         except (RuntimeError, OSError, MemoryError) as e:  # OOM / injected / transient: retry the batch
+            if getattr(e, "abort_epoch", False):   # a row-sharded collective failed: never retried here
+                raise
             if reraise is not None and reraise(e):
                 raise
             last = e

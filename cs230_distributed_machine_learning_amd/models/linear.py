@@ -101,7 +101,16 @@ def class_weight_vector(data, split: int, cw):
     return w
 
 
-_TILE = 128   # output tile of csrc/kernels/lr_mfma.hip (dml_lr_mfma_tile)
+_TILE = 128   # output tile of csrc/kernels/lr_mfma.hip (dml_lr_mfma_tile): a fit's columns never straddle one
+_ROW_TILE = 256   # v3 kernels' row tile (dml_lr_v3_row_tile): X rows and R^T rows (= padded columns)
+
+
+def lr_v3(lib, M: int) -> bool:
+    """The 3-stage 256 x 128 MFMA kernels (k_lr_fwd3 / k_lr_grad3, one workgroup per CU) for
+    batches of more than 256 columns; smaller batches keep the 128 x 128 two-workgroup kernels
+    (a 256-row gradient tile would be mostly padding).  DML_LR_V3=0 forces the older kernels."""
+    return (M > 256 and os.environ.get("DML_LR_V3", "1") != "0"
+            and getattr(lib, "dml_lr_mfma_fwd3", None) is not None)
 
 
 def _dp_sum(data, t: torch.Tensor) -> torch.Tensor:
@@ -131,7 +140,7 @@ class MfmaOperands:
     def __init__(self, data):
         lib = native.hip_lib()
         n, d, dev = data.n, data.d, data.device
-        self.npad = _roundup(n, _TILE)
+        self.npad = _roundup(n, _ROW_TILE)
         self.Kp = _roundup(d, 32)
         self.Dp = _roundup(d + 1, _TILE)
         bf = torch.bfloat16
@@ -175,7 +184,10 @@ class MfmaPlan:
                 m = _roundup(m, _TILE)
             pcol0.append(m)
             m += k
-        self.Mp = _roundup(max(m, 1), _TILE)
+        self.v3 = lr_v3(lib, m)
+        if self.v3 and lib.dml_lr_v3_row_tile() != _ROW_TILE:
+            raise RuntimeError("lr_mfma v3 row tile mismatch")
+        self.Mp = _roundup(max(m, 1), _ROW_TILE if self.v3 else _TILE)
         col_tiles = self.Mp // _TILE
         self.colmap = torch.tensor([c0 + j for c0, k in zip(pcol0, b.K_l) for j in range(k)], dtype=torch.long,
                                    device=dev)
@@ -190,14 +202,25 @@ class MfmaPlan:
         self.rh = torch.zeros((ops.npad // 32, self.Mp, 32), dtype=bf, device=dev)   # pad columns stay 0
         self.rl = torch.zeros_like(self.rh)
         self.loss = torch.zeros(b.F, dtype=torch.float64, device=dev)
-        # forward: persistent, at most the resident workgroups (2 per CU), row groups % 8 == 0
-        row_tiles = ops.npad // _TILE
-        resident = 2 * torch.cuda.get_device_properties(dev).multi_processor_count
-        rg = max(8, (resident // col_tiles) // 8 * 8)
-        rg = min(rg, _roundup(row_tiles, 8))
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        self.lpart = None
+        if self.v3:
+            # forward: one persistent workgroup per CU (8 per XCD walk their XCD's row tiles);
+            # gradient: 256-row R^T tiles x 128-row X^T tiles x K slices
+            row_tiles = ops.npad // _ROW_TILE
+            rg = max(8, cus // 8 * 8)
+            self.lpart = torch.empty((row_tiles, self.Mp), dtype=torch.float64, device=dev)
+            m_tiles, resident = self.Mp // _ROW_TILE, cus
+        else:
+            # forward: persistent, at most the resident workgroups (2 per CU), row groups % 8 == 0
+            row_tiles = ops.npad // _TILE
+            resident = 2 * cus
+            rg = max(8, (resident // col_tiles) // 8 * 8)
+            rg = min(rg, _roundup(row_tiles, 8))
+            m_tiles = col_tiles
         # gradient: output tiles x K slices >= ~4 waves of workgroups; slices % 8 == 0
         n_tiles = ops.Dp // _TILE
-        tiles = col_tiles * n_tiles
+        tiles = m_tiles * n_tiles
         S = _roundup(-(-4 * resident // tiles), 8)
         Kc = _roundup(-(-ops.npad // S), 32)
         S = _roundup(-(-ops.npad // Kc), 8)
@@ -208,9 +231,10 @@ class MfmaPlan:
             row_tiles=row_tiles, col_tiles=col_tiles, row_groups=rg, bias=p(self.bias), col_fit=p(self.col_fit),
             fit_col0=p(self.fit_col0), fit_k=p(b.K), fit_kind=p(b.kind), fit_split=p(b.split), scale=p(b.scale),
             cw=p(b.cw), cwC=int(b.cw.shape[1]) if b.cw is not None else 0, y=p(data.y_cls), roles=p(data.roles),
-            rh=p(self.rh), rl=p(self.rl), kr=ops.npad, loss=p(self.loss))
+            rh=p(self.rh), rl=p(self.rl), kr=ops.npad, loss=p(self.loss), lpart=p(self.lpart))
+        self.fit_col0_l = self.fit_col0.long()
         self.grad = native.LrGradArgs(
-            rh=p(self.rh), rl=p(self.rl), unused=0, xth=p(ops.xth), xtl=p(ops.xtl), m_tiles=col_tiles,
+            rh=p(self.rh), rl=p(self.rl), unused=0, xth=p(ops.xth), xtl=p(ops.xtl), m_tiles=m_tiles,
             n_tiles=n_tiles, Kp=ops.npad, S=S, Kc=Kc, out=p(self.slabs))
 
     def objective(self, data, b: "_Batch", W: torch.Tensor):
@@ -227,11 +251,18 @@ class MfmaPlan:
         self.loss.zero_()
         lib = native.hip_lib()
         st = native.stream_handle(data.device)
-        rc = lib.dml_lr_mfma_fwd(ctypes.byref(self.fwd), st)
-        if rc == 0:
-            rc = lib.dml_lr_mfma_grad(ctypes.byref(self.grad), st)
+        if self.v3:
+            rc = lib.dml_lr_mfma_fwd3(ctypes.byref(self.fwd), st)
+            if rc == 0:
+                rc = lib.dml_lr_mfma_grad3(ctypes.byref(self.grad), st)
+        else:
+            rc = lib.dml_lr_mfma_fwd(ctypes.byref(self.fwd), st)
+            if rc == 0:
+                rc = lib.dml_lr_mfma_grad(ctypes.byref(self.grad), st)
         if rc:
             raise RuntimeError(f"lr_mfma launch failed ({rc})")
+        if self.v3:   # every (row tile, column) partial written once: fixed-order sum over row tiles
+            self.loss.copy_(self.lpart.sum(0)[self.fit_col0_l])
         GT = self.slabs.sum(0)
         G = torch.empty_like(W)
         G[:d] = GT[self.colmap, :d].t()

@@ -48,15 +48,34 @@ def shard_bounds(n: int, world: int, rank: int):
     return r0, r0 + base + (1 if rank < rem else 0)
 
 
-def scatter_table(X: Optional[np.ndarray], y: Optional[np.ndarray], device: torch.device):
+def _guarded(fn):
+    """Run a collective of a row-sharded epoch; any failure (timeout on a dead or hung peer,
+    communicator abort) becomes ``dist.CollectiveError``, which aborts the epoch."""
+    try:
+        return fn()
+    except dist.CollectiveError:
+        raise
+    except Exception as e:
+        raise dist.CollectiveError(f"row-shard collective failed: {type(e).__name__}: {e}") from e
+
+
+def scatter_table(X: Optional[np.ndarray], y: Optional[np.ndarray], device: torch.device, group=None):
     """Rank 0 passes host arrays; every rank returns (X_shard_dev, y_global_host, r0).
 
     X moves by chunked point-to-point sends from rank 0 (each rank receives only its
     rows; rank 0 holds its own block plus one chunk); y (n values) is broadcast to
-    every rank."""
+    every rank.  ``group``: the data-parallel communicator (dist.dp_group; its ranks are
+    the global ranks)."""
     inf = dist.info()
     if not inf.is_dist:
         return torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).to(device), np.asarray(y), 0
+    return _guarded(lambda: _scatter(X, y, device, group))
+
+
+def _scatter(X, y, device, group):
+    import datetime
+
+    inf = dist.info()
     st = dist.store()
     key = "dataset/dp_meta"
     if inf.rank == 0:
@@ -70,7 +89,7 @@ def scatter_table(X: Optional[np.ndarray], y: Optional[np.ndarray], device: torc
             y_num = y.astype(np.float64)
         st.set(key, json.dumps(meta))
     else:
-        st.wait([key])
+        st.wait([key], datetime.timedelta(seconds=dist.dp_timeout_s() if group is not None else 1800.0))
         meta = json.loads(st.get(key))
     n, d, world = meta["n"], meta["d"], inf.world
     r0, r1 = shard_bounds(n, world, inf.rank)
@@ -87,14 +106,14 @@ def scatter_table(X: Optional[np.ndarray], y: Optional[np.ndarray], device: torc
             a, b = shard_bounds(n, world, k)
             for c0 in range(a, b, ch):
                 c1 = min(b, c0 + ch)
-                torch.distributed.send(Xt[c0:c1].to(device), dst=k)
+                torch.distributed.send(Xt[c0:c1].to(device), dst=k, group=group)
     else:
         for c0 in range(r0, r1, ch):
             c1 = min(r1, c0 + ch)
-            torch.distributed.recv(recv[c0 - r0:c1 - r0], src=0)
+            torch.distributed.recv(recv[c0 - r0:c1 - r0], src=0, group=group)
     yd = torch.from_numpy(y_num).to(device) if inf.rank == 0 else torch.empty((n,), dtype=torch.float64, device=device)
-    dist.broadcast(yd, 0)
-    dist.barrier()
+    dist.broadcast(yd, 0, group=group)
+    dist.barrier(group=group)
     if inf.rank == 0:
         st.delete_key(key)
         return recv, y, r0
@@ -135,7 +154,7 @@ class RowShard(DeviceData):
         if dist.info().is_dist:
             ro = {"sum": torch.distributed.ReduceOp.SUM, "min": torch.distributed.ReduceOp.MIN,
                   "max": torch.distributed.ReduceOp.MAX}[op]
-            torch.distributed.all_reduce(t, op=ro, group=self.group)
+            _guarded(lambda: torch.distributed.all_reduce(t, op=ro, group=self.group))
         return t
 
     # reduce-scatter / all-gather over equal row blocks (row-sharded forests: each rank
@@ -156,9 +175,9 @@ class RowShard(DeviceData):
         q = t.shape[0] // w
         if dist.info().backend == "nccl":
             out = torch.empty((q,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-            torch.distributed.reduce_scatter_tensor(out, t.contiguous(), group=self.group)
+            _guarded(lambda: torch.distributed.reduce_scatter_tensor(out, t.contiguous(), group=self.group))
             return out
-        torch.distributed.all_reduce(t, group=self.group)    # gloo: no reduce-scatter
+        _guarded(lambda: torch.distributed.all_reduce(t, group=self.group))    # gloo: no reduce-scatter
         return t[self.rank * q:(self.rank + 1) * q]
 
     def all_gather_equal(self, t: torch.Tensor) -> torch.Tensor:
@@ -169,10 +188,10 @@ class RowShard(DeviceData):
         t = t.contiguous()
         if dist.info().backend == "nccl":
             out = torch.empty((w * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-            torch.distributed.all_gather_into_tensor(out, t, group=self.group)
+            _guarded(lambda: torch.distributed.all_gather_into_tensor(out, t, group=self.group))
             return out
         parts = [torch.empty_like(t) for _ in range(w)]
-        torch.distributed.all_gather(parts, t, group=self.group)
+        _guarded(lambda: torch.distributed.all_gather(parts, t, group=self.group))
         return torch.cat(parts)
 
     def _world_bounds(self):
@@ -229,7 +248,7 @@ class RowShard(DeviceData):
         pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         pad[:t.shape[0]] = t
         parts = [torch.empty_like(pad) for _ in counts]
-        torch.distributed.all_gather(parts, pad, group=self.group)
+        _guarded(lambda: torch.distributed.all_gather(parts, pad, group=self.group))
         return torch.cat([p[:int(c)] for p, c in zip(parts, counts)])
 
     # ---- splits -----------------------------------------------------------------------

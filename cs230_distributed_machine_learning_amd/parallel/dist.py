@@ -114,6 +114,39 @@ def side_group():
     return _SIDE
 
 
+_DP = None
+
+
+class CollectiveError(RuntimeError):
+    """A collective of a row-sharded (data-parallel) epoch failed or timed out: a peer died,
+    hung, or ran out of memory.  The epoch's communicator is unusable from here on, so the
+    error aborts the whole epoch (never a per-batch retry, never "failed candidates") and the
+    dispatcher re-runs the job task-parallel on the survivors (parallel/runner.py)."""
+
+    abort_epoch = True
+
+
+def dp_group():
+    """The communicator of data-parallel epochs (created collectively at WorkerCore setup,
+    after ``side_group``): its own SHORT per-collective timeout, so a rank that dies or hangs
+    mid-epoch costs the survivors ``dp_timeout_s()`` -- not the default group's 30 minutes --
+    before their collective raises.  None when not distributed."""
+    global _DP
+    if not info().is_dist:
+        return None
+    if _DP is None:
+        _DP = dist.new_group(ranks=list(range(info().world)), backend=info().backend,
+                             timeout=datetime.timedelta(seconds=dp_timeout_s()))
+    return _DP
+
+
+def dp_timeout_s() -> float:
+    """Per-collective timeout of the data-parallel communicator (``DML_DP_TIMEOUT_S``,
+    default 300 s: covers rank 0 parsing a large table while its peers wait in the scatter;
+    every later collective of an epoch is a sub-second all-reduce between equal shards)."""
+    return float(os.environ.get("DML_DP_TIMEOUT_S", "300"))
+
+
 def side_timeout_s() -> float:
     """Per-collective timeout of the side communicator (``DML_SIDE_TIMEOUT_S``, default 120 s:
     a 40 GB table broadcast over xGMI takes well under that)."""
@@ -210,8 +243,9 @@ def service_client(timeout_s: float = 300.0):
 
 
 def destroy() -> None:
-    global _INFO, _SIDE
+    global _INFO, _SIDE, _DP
     _SIDE = None
+    _DP = None
     if dist.is_initialized():
         dist.destroy_process_group()
     _INFO = None

@@ -251,6 +251,9 @@ class WorkerCore:
         self.cache_lock = threading.RLock()   # the worker and the collective thread share the cache
         # the side communicator (collective with every rank: built here, by every in-group rank)
         self.side = dist.side_group() if (in_group and self.inf.is_dist) else None
+        # the data-parallel communicator (short timeout; created collectively right after the
+        # side group, in the same order on every in-group rank)
+        self.dp = dist.dp_group() if (in_group and self.inf.is_dist) else None
 
     # ---- job messages and datasets ------------------------------------------------------
     def job_msg(self, seq: int) -> Dict[str, Any]:
@@ -450,8 +453,10 @@ class WorkerCore:
         if self.inf.rank == 0:
             ds = ctl.registry.load(msg["dataset_id"], plan["feature_columns"], plan["target_column"])
             X, y = ds.X, ds.y
-        Xs, y_glob, r0 = scatter_table(X, y, self.device)
-        dd = RowShard(Xs, y_glob, r0, is_classifier(plan["model_type"]), self.device, name=msg["dataset_id"])
+        Xs, y_glob, r0 = scatter_table(X, y, self.device, group=self.dp)
+        dd = RowShard(Xs, y_glob, r0, is_classifier(plan["model_type"]), self.device, name=msg["dataset_id"],
+                      group=self.dp)
+        faults.maybe_stop_in_collective(self.wid, "dp")   # fault injection: a rank hangs mid-epoch
         out: List[Dict[str, Any]] = []
         results_all = []
         for ids in msg["slices"]:
@@ -464,7 +469,11 @@ class WorkerCore:
             job = ctl.table.get(msg["session_id"], msg["job_id"])
             best = pick_refit(ctl, job, plan, results_all)
             self.store.set(f"job/{seq}/refit", str(best if best is not None else -1))
-        self.store.wait([f"job/{seq}/refit"])
+        else:
+            try:
+                self.store.wait([f"job/{seq}/refit"], timeout=dist.dp_timeout_s())
+            except TimeoutError as e:   # rank 0 left the epoch (its collective failed first)
+                raise dist.CollectiveError(f"no refit decision from rank 0 within {dist.dp_timeout_s():.0f}s") from e
         best_i = int(self.store.get(f"job/{seq}/refit"))
         model_path = None
         if best_i >= 0:
@@ -804,7 +813,7 @@ class DistributedRunner(Runner):
                     self._liveness()
                 self._dispatch()
                 active = any(not js.finished for js in self.jobs) or any(
-                    w.busy is not None for w in self.workers.values() if w.alive)
+                    w.busy is not None and not w.busy.get("abandoned") for w in self.workers.values() if w.alive)
                 if stopping and not active:
                     break
                 if not active and not busy:
@@ -1205,6 +1214,9 @@ class DistributedRunner(Runner):
             self._epoch_answer(w)
             return
         if kind == "dp":
+            if w.wid == 0 and js is not None and "error" in out:
+                self._dp_failed(js, out["error"])
+                return
             self._epoch_answer(w)
             if w.wid == 0 and js is not None:
                 self._finish_dp(js, out)
@@ -1340,10 +1352,44 @@ class DistributedRunner(Runner):
         js.finished = True
         self._cleanup_job(js)
 
+    def _dp_failed(self, js: _JobState, err: str) -> None:
+        """A data-parallel epoch failed (a collective timed out on a dead or hung member, or
+        raised): the reference re-places a lost worker's tasks and keeps serving
+        (aws-prod/scheduler/scheduler_service.py:205-247).  Here the epoch is abandoned at
+        once -- ranks still inside it answer when their own collective times out; a hung one
+        never does and simply gets no more work -- the group is broken for good (no rank
+        issues another collective), and the job is re-cut and re-run TASK-parallel on the
+        survivors from the host-staged table.  Nothing of the failed epoch was published."""
+        log.error("data-parallel epoch of job %s failed (%s): re-running it task-parallel on the survivors",
+                  js.job.job_id, err)
+        if self.epoch is not None:
+            for wid in self.epoch["waiting"]:
+                ww = self.workers.get(wid)
+                if ww is not None and ww.busy is not None:
+                    ww.busy["abandoned"] = True   # its late answer frees it; a hung rank stays parked
+            self.epoch = None
+        self._break_group(f"data-parallel epoch failed: {err}")
+        ids = [c for sl in js.slices for c in sl]
+        js.slices = plan_slices(self.ctl, js.plan, ids, js.n_train, js.n_feat, 2,
+                                min_slices=min(len(ids), 2 * max(1, self._n_alive())))
+        js.est = [self.ctl.scheduler.estimate(js.plan["model_type"], sum(js.cand_costs[c] for c in sl))
+                  for sl in js.slices]
+        js.queue = collections.deque(range(len(js.slices)))
+        js.inflight.clear()
+        js.done.clear()
+        js.metrics.clear()
+        js.retired.clear()
+        js.rechunked = True
+        js.mode = "task"
+        js.transport = "staged"
+        js.msg["slices"] = js.slices
+        js.staged_ready = False
+        self._stage(js)
+        self.stats["dp_requeued"] = self.stats.get("dp_requeued", 0) + 1
+
     def _finish_dp(self, js: _JobState, out: Dict[str, Any]) -> None:
-        if "error" in out:
-            self._fail_job(js.job, RuntimeError(out["error"]))
-            js.finished = True
+        if "error" in out:   # (rank 0's error answers go through _dp_failed)
+            self._dp_failed(js, out["error"])
             return
         slices = out.get("dp_slices", [])
         best_i, path = out.get("refit", -1), out.get("model_path")

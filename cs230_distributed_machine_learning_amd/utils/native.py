@@ -90,7 +90,8 @@ ScoreArgs = _i64_struct("ScoreArgs", ["rows", "fit_row_off", "pred", "ycls", "yr
 LrFwdArgs = _i64_struct(
     "LrFwdArgs",
     ["xh", "xl", "xrows", "wh", "wl", "n", "Kp", "row_tiles", "col_tiles", "row_groups", "bias", "col_fit",
-     "fit_col0", "fit_k", "fit_kind", "fit_split", "scale", "cw", "cwC", "y", "roles", "rh", "rl", "kr", "loss"],
+     "fit_col0", "fit_k", "fit_kind", "fit_split", "scale", "cw", "cwC", "y", "roles", "rh", "rl", "kr", "loss",
+     "lpart"],
 )
 # csrc/kernels/gbrt.hip argument blocks (fused gradient-boosting stage kernels)
 GbStageArgs = _i64_struct(
@@ -214,6 +215,9 @@ def _register_optional(lib) -> None:
         "dml_lr_mfma_tile": (c_i32, []),
         "dml_lr_mfma_fwd": (c_i32, [ctypes.POINTER(LrFwdArgs), c_vp]),
         "dml_lr_mfma_grad": (c_i32, [ctypes.POINTER(LrGradArgs), c_vp]),
+        "dml_lr_v3_row_tile": (c_i32, []),
+        "dml_lr_mfma_fwd3": (c_i32, [ctypes.POINTER(LrFwdArgs), c_vp]),
+        "dml_lr_mfma_grad3": (c_i32, [ctypes.POINTER(LrGradArgs), c_vp]),
         "dml_split_hilo": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp]),
         "dml_lr_sizeof_fwd_args": (c_i32, []),
         "dml_lr_sizeof_grad_args": (c_i32, []),

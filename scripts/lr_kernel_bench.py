@@ -26,9 +26,12 @@ b.mf = linear.MfmaPlan(dd, b)
 b.mf.objective(dd, b, W)
 lib = native.hip_lib()
 st = native.stream_handle(dev)
-out = {"lib": os.path.basename(os.environ.get("DML_HIP_LIB", "default"))}
-for name, fn, args in (("fwd", lib.dml_lr_mfma_fwd, b.mf.fwd), ("grad", lib.dml_lr_mfma_grad, b.mf.grad)):
-    fn(ctypes.byref(args), st)
+out = {"lib": os.path.basename(os.environ.get("DML_HIP_LIB", "default")), "v3": bool(b.mf.v3), "Mp": b.mf.Mp}
+fwd_fn = lib.dml_lr_mfma_fwd3 if b.mf.v3 else lib.dml_lr_mfma_fwd
+grad_fn = lib.dml_lr_mfma_grad3 if b.mf.v3 else lib.dml_lr_mfma_grad
+for name, fn, args in (("fwd", fwd_fn, b.mf.fwd), ("grad", grad_fn, b.mf.grad)):
+    rc = fn(ctypes.byref(args), st)
+    assert rc == 0, (name, rc)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()

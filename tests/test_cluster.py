@@ -347,3 +347,65 @@ def test_row_shard_request_keeps_absolute_error_and_monotonic_cst():
     assert set(dist_scores) == {"absolute_error", "squared_error"}
     for k in local:
         assert np.allclose(dist_scores[k], local[k], rtol=0, atol=1e-12), (k, dist_scores[k], local[k])
+
+
+# ---- a rank dies or hangs inside a row-sharded (data-parallel) epoch -------------------------
+def _dp_lr_job(parallelism):
+    body = _grid_job("job-dp", "dpt", "LogisticRegression", {"C": [0.1, 1.0, 10.0]})
+    body["train_params"]["parallelism"] = parallelism
+    return body
+
+
+def _drive_dp_hang(ctl, runner):
+    sid = ctl.create_session()[1]["session_id"]
+    ctl.download_data(sid, {"dataset_url": "classification?n=3000&d=8&seed=31", "dataset_name": "dpt",
+                            "dataset_type": "synthetic"})
+    t0 = time.time()
+    st, a = ctl.train(sid, _dp_lr_job("data"))
+    assert st in (200, 202), a
+    ctl.table.wait_finished(a["job_id"], timeout=200)
+    t1 = time.time() - t0
+    s = ctl.check_status(sid, a["job_id"])[1]
+    # the service keeps serving: a second job on the same table completes too
+    st, b = ctl.train(sid, _grid_job("job-next", "dpt", "LogisticRegression", {"C": [2.0]}))
+    ctl.table.wait_finished(b["job_id"], timeout=120)
+    s2 = ctl.check_status(sid, b["job_id"])[1]
+    return {"status": s["job_status"], "t1": t1, "requeued": runner.stats.get("dp_requeued", 0),
+            "broken": runner.group_broken, "next": s2["job_status"],
+            "scores": {r["parameters"]["C"]: r["cv_scores"] for r in s["job_result"]["results"]}}
+
+
+def _local_dp_lr_scores():
+    root = tempfile.mkdtemp()
+    ctl = Controller(Config.from_env(data_root=root, device="cpu", chunk_target_s=0.0))
+    try:
+        sid = ctl.create_session()[1]["session_id"]
+        ctl.download_data(sid, {"dataset_url": "classification?n=3000&d=8&seed=31", "dataset_name": "dpt",
+                                "dataset_type": "synthetic"})
+        st, a = ctl.train(sid, _dp_lr_job("task"))
+        ctl.table.wait_finished(a["job_id"], timeout=180)
+        s = ctl.check_status(sid, a["job_id"])[1]
+        return {r["parameters"]["C"]: r["cv_scores"] for r in s["job_result"]["results"]}
+    finally:
+        ctl.shutdown()
+
+
+@pytest.mark.parametrize("fault", ["stop", "fail"])
+def test_rank_lost_inside_data_parallel_epoch_job_reruns_task_parallel(fault):
+    """A rank hangs (SIGSTOP) or raises inside a row-sharded LogisticRegression epoch: the
+    survivors' data-parallel collectives time out after DML_DP_TIMEOUT_S (their own
+    communicator, not the default group's 30 min), rank 0 abandons the epoch, breaks the group
+    and re-runs the job TASK-parallel on the survivors (reference re-places a dead worker's
+    tasks, aws-prod/scheduler/scheduler_service.py:205-247).  The job completes with the local
+    runner's CV scores, the next job completes, and rank 0 exits 0."""
+    var = "DML_STOP_RANK_IN" if fault == "stop" else "DML_FAIL_RANK_IN"
+    env = {var: "2:dp", "DML_DP_TIMEOUT_S": "8", "DML_SIDE_TIMEOUT_S": "8", "DML_DEAD_AFTER_S": "600"}
+    r, rc0, wall = _launch_faulty(3, _drive_dp_hang, env)
+    assert r["status"] == "completed" and r["next"] == "completed", r
+    assert r["requeued"] == 1 and r["broken"], r
+    assert r["t1"] < 8 + 60, r["t1"]          # the epoch timeout plus re-run time, not 30 minutes
+    local = _local_dp_lr_scores()
+    assert set(r["scores"]) == set(local)
+    for k in local:
+        assert np.allclose(r["scores"][k], local[k], rtol=0, atol=1e-12), (k, r["scores"][k], local[k])
+    assert rc0 == 0, rc0

@@ -144,9 +144,11 @@ def _lr_batch(dd, specs):
     return fam, linear._Batch(dd, tasks)
 
 
-@pytest.mark.parametrize("C_cls,n,d", [(2, 3001, 70), (3, 2500, 45), (4, 700, 300)])
-def test_lr_mfma_objective_matches_fp32(C_cls, n, d):
-    """Matrix-core (bf16x3) objective vs the fp32 GEMM + link-kernel path: loss and gradient."""
+@pytest.mark.parametrize("C_cls,n,d,fits", [(2, 3001, 70, 40), (3, 2500, 45, 40), (4, 700, 300, 40),
+                                            (2, 5003, 130, 300), (3, 2100, 64, 130)])
+def test_lr_mfma_objective_matches_fp32(C_cls, n, d, fits):
+    """Matrix-core (bf16x3) objective vs the fp32 GEMM + link-kernel path: loss and gradient.
+    Batches of more than 256 columns run the 3-stage 256 x 128 kernels (k_lr_fwd3 / k_lr_grad3)."""
     from cs230_distributed_machine_learning_amd.models import linear
 
     rng = np.random.RandomState(C_cls * 7 + d)
@@ -155,7 +157,7 @@ def test_lr_mfma_objective_matches_fp32(C_cls, n, d):
     dd = _dd(X, y, True, "cuda:0")
     S = len(dd.split_names)
     specs = []
-    for i in range(40):   # softmax / OvR (liblinear) / class-weighted, assorted splits and C
+    for i in range(fits):   # softmax / OvR (liblinear) / class-weighted, assorted splits and C
         p = {"C": float(10.0 ** rng.uniform(-2, 2)), "solver": ["lbfgs", "liblinear"][i % 2]}
         if i % 5 == 0:
             p["class_weight"] = "balanced"
@@ -164,6 +166,7 @@ def test_lr_mfma_objective_matches_fp32(C_cls, n, d):
     W = torch.randn((d + 1, b.M), device="cuda:0") * 0.05
     f0, G0 = fam._objective(dd, b, W)
     b.mf = linear.MfmaPlan(dd, b)
+    assert b.mf.v3 == (b.M > 256)
     f1, G1 = fam._objective(dd, b, W)
     torch.cuda.synchronize()
     torch.testing.assert_close(f1, f0, rtol=2e-5, atol=1e-6)
