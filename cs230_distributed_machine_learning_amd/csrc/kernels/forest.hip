@@ -55,6 +55,9 @@
 #ifndef DML_NODES_WPE_WAVE
 #define DML_NODES_WPE_WAVE 4   // wave tier (binary): 2 / 3 / 5 / 6 measured slower (ROUND3.md)
 #endif
+#ifndef DML_NODES_WPE_WAVE_MAX
+#define DML_NODES_WPE_WAVE_MAX 8   // wave tier (binary) occupancy cap: 8 -> 64 VGPRs (spills), lower -> more VGPRs
+#endif
 #ifndef DML_NODES_WPE_REG
 #define DML_NODES_WPE_REG 2   // regression node kernels: 3 histogram planes + payloads fit 256 VGPRs, no spills
 #endif
@@ -1139,7 +1142,7 @@ __device__ __forceinline__ void hist_add(typename HT<MODE>::T* hj, const Ctx& c,
 }
 
 template <int NT, int MODE, int FC>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? DML_NODES_WPE_REG : (MODE == 0 ? DML_NODES_WPE_MC : (NT == 64 ? DML_NODES_WPE_WAVE : DML_NODES_WPE)), 8))) void k_nodes(Ctx c, int tier, int set_cur,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? DML_NODES_WPE_REG : (MODE == 0 ? DML_NODES_WPE_MC : (NT == 64 ? DML_NODES_WPE_WAVE : DML_NODES_WPE)), (MODE == 1 && NT == 64) ? DML_NODES_WPE_WAVE_MAX : 8))) void k_nodes(Ctx c, int tier, int set_cur,
                                                                                                    int pair_base, int stage_base) {
   using CT = typename HT<MODE>::T;
   constexpr bool PK = FC >= 0;   // specialised builds have packed row words

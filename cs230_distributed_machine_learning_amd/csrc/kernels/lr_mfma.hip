@@ -39,6 +39,7 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 #ifndef LRM_PASSES
 #define LRM_PASSES 3   // A/B instrumentation: 1 = hi*hi only, 0 = no MFMA (never in production)
@@ -65,6 +66,10 @@ struct FwdArgs {
   int64_t rh, rl, kr;            // R^T hi/lo, K-tiled over col_tiles*BN rows, kr (= xrows) deep
   int64_t loss;                  // double [F] (accumulated; caller zeroes)
   int64_t lpart;                 // v3: double [row_tiles x col_tiles*BN] per-item column loss partials
+  int64_t col_info;              // v3: int32 [Mp] kind << 28 | split << 16 | positive class (-1: padding)
+  int64_t col_scale;             // v3: float [Mp] the column's fit's loss scale
+  int64_t n_splits;              // v3: role rows of `roles`
+  int64_t softmax_any;           // v3: 1 if any fit is multinomial (Z tile through LDS)
 };
 
 struct GradArgs {
@@ -193,10 +198,10 @@ __device__ __forceinline__ void gemm_tile(const Operands& op, int64_t row0, int6
   for (int64_t k = kb; k < ke; k += BK) {
     if (k + BK < ke) glds_stage(op, row0, col0, k + BK, smem + (cur ^ 1) * STAGE, tid);
     mma_stage(smem + cur * STAGE, acc, wm, wn, lane);
-#ifndef LRM_NO_SCHED_FENCE
-    // keep every MFMA of the step ahead of the barrier: the scheduler otherwise hoists the
-    // barrier (and its vmcnt(0) drain of the next stage's LDS-DMA) to just after the last
-    // fragment read, leaving only half the step's MFMAs to cover the DMA latency
+#ifdef LRM_SCHED_FENCE
+    // A/B only: every MFMA of the step ahead of the barrier (the scheduler otherwise hoists the
+    // barrier to just after the last fragment read) -- measured slower: fwd 228 -> 245 ms,
+    // grad 135 -> 188 ms at 10M x 1000 x 2560 (profiles/r5_lr_ab.txt)
     __builtin_amdgcn_sched_barrier(0);
 #endif
     __syncthreads();   // drains this wave's LDS-DMA (vmcnt(0)) and publishes the stage
@@ -553,13 +558,19 @@ __device__ __forceinline__ void v3_gemm(const Operands& op, int64_t row0, int64_
   v3_wait_barrier<0>();
 }
 
+constexpr int V3_ROLE_ROWS = 8;   // role rows staged per item in LDS (cv <= 7 + holdout; more: read from HBM)
+
 __global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
   using namespace v3;
-  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[STG_BYTES];
+  // staging ring + (past it) the item's labels and role rows: loaded at the item's start (in
+  // flight under its GEMM), stored once the GEMM has drained.  ONE LDS object: with separate
+  // __shared__ arrays the compiler's wait pass makes every fragment read wait vmcnt(0)
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[STG_BYTES + TM * 4 + V3_ROLE_ROWS * TM];
+  int32_t* eps_y = reinterpret_cast<int32_t*>(smem_raw + STG_BYTES);
+  uint8_t* eps_r = smem_raw + STG_BYTES + TM * 4;
   uint16_t* smem = reinterpret_cast<uint16_t*>(smem_raw);
-  float* zs = reinterpret_cast<float*>(smem_raw);                              // Z tile, after the GEMM
-  double* lq = reinterpret_cast<double*>(smem_raw + TM * TN * 4);              // [4][TN] row-quarter partials
-  int32_t* ys = reinterpret_cast<int32_t*>(smem_raw + TM * TN * 4 + 4 * TN * 8);
+  float* zs = reinterpret_cast<float*>(smem_raw);                              // Z tile (softmax batches)
+  double* lq = reinterpret_cast<double*>(smem_raw + TM * TN * 4);              // [4][TN] partials
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
   const int64_t b = blockIdx.x, xcd = b & 7, slot = b >> 3, slots = gridDim.x >> 3;
   const int64_t rt_here = a.row_tiles > xcd ? (a.row_tiles - xcd + 7) / 8 : 0;
@@ -569,104 +580,203 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
   const auto y = GPTR(const int32_t, a.y);
   const auto roles = GPTR(const uint8_t, a.roles);
   const auto lpart = GPTR(double, a.lpart);
+  const auto cinfo_g = GPTR(const int32_t, a.col_info);
+  const auto cscale_g = GPTR(const float, a.col_scale);
+  const auto cwt = a.cw ? GPTR(const float, a.cw) : nullptr;
   const Operands op{reinterpret_cast<const uint16_t*>(a.xh), reinterpret_cast<const uint16_t*>(a.xl), a.xrows,
                     reinterpret_cast<const uint16_t*>(a.wh), reinterpret_cast<const uint16_t*>(a.wl),
                     a.col_tiles * TN};
   const int64_t Mp = a.col_tiles * TN;
-  const int c = tid & (TN - 1), rq = tid >> 7;   // epilogue: column c of the tile, 64-row quarter rq
+  const bool softmax = a.softmax_any != 0;
+  const int S = (int)a.n_splits;
+  const bool stage_roles = S <= V3_ROLE_ROWS;
+  const int nchunk = stage_roles ? S * (TM / 4) : 0;   // 4-row role chunks of the item (<= NT)
+  static_assert(V3_ROLE_ROWS * (TM / 4) <= NT, "one role chunk per thread");
   for (int64_t it = slot; it < items; it += slots) {
     const int64_t rt = xcd + 8 * (it / a.col_tiles), ct = it % a.col_tiles;
     const int64_t row0 = rt * TM, col0 = ct * TN;
+    // ---- item prologue: epilogue operands in flight under the GEMM.  Every load is
+    // unconditional (clamped address, value selected after the GEMM): a load under a branch
+    // merges into a phi whose copy waits vmcnt(0) -- i.e. would drain the GEMM's DMA ring
+    const int ty = tid & (TM - 1);
+    const int32_t ypre = y[min(row0 + ty, (int64_t)a.n - 1)];
+    uint32_t rpre = 0;
+    {
+      const int chk = tid < nchunk ? tid : 0, sp = chk / (TM / 4), r4 = (chk % (TM / 4)) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        rpre |= (uint32_t)roles[(int64_t)sp * a.n + min(row0 + r4 + e, (int64_t)a.n - 1)] << (8 * e);
+    }
+    int32_t cinfo[4], cfit[4];
+    float cscale[4], cbias[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t gc = col0 + wn * 64 + j * 16 + (lane & 15);
+      cinfo[j] = cinfo_g[gc];
+      cscale[j] = cscale_g[gc];
+      cbias[j] = bias[gc];
+      cfit[j] = col_fit[gc];
+    }
     f32x4 acc[4][4];
     v3_gemm(op, row0, col0, 0, a.Kp, smem, acc, tid);
+    if (tid < TM) eps_y[tid] = row0 + tid < a.n ? ypre : 0;
+    if (tid < nchunk) {   // rows past n read as role 0 (held out)
+      const int r4 = (tid % (TM / 4)) * 4;
+      uint32_t v = rpre;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int e = 0; e < 4; ++e)
+        if (row0 + r4 + e >= a.n) v &= ~(0xFFu << (8 * e));
+      *reinterpret_cast<uint32_t*>(eps_r + tid * 4) = v;
+    }
+    __syncthreads();
+    auto role_at = [&](int sp, int lrow) -> int {
+      if (stage_roles) return eps_r[sp * TM + lrow];
+      const int64_t g = row0 + lrow;
+      return g < a.n ? (int)roles[(int64_t)sp * a.n + g] : 0;
+    };
+    if (!softmax) {
+      // ---- register epilogue: every column is an independent sigmoid (binary / OvR)
+      float lsum[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int col = wn * 64 + j * 16 + (lane & 15);
-        const float bv = bias[col0 + col];
+        const int ci = cinfo[j];
+        if (ci < 0) continue;                                 // padding column: R stays 0
+        const int kind = ci >> 28, sp = (ci >> 16) & 0xFFF, tgt = ci & 0xFFFF;
+        const int64_t gc = col0 + wn * 64 + j * 16 + (lane & 15);
+        const auto RH = GPTR(uint16_t, a.rh) + gc * BK;
+        const auto RL = GPTR(uint16_t, a.rl) + gc * BK;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = wm * 64 + i * 16 + (lane >> 4) * 4 + e;
-          zs[zidx(row, col)] = acc[i][j][e] + bv;
+        for (int i = 0; i < 4; ++i) {
+          const int lr0 = wm * 64 + i * 16 + (lane >> 4) * 4;
+          float r[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int lrow = lr0 + e;
+            const int yv = eps_y[lrow];
+            const bool tr = row0 + lrow < a.n && role_at(sp, lrow) == 1;
+            const float sc = tr ? (cwt ? cscale[j] * cwt[(int64_t)cfit[j] * a.cwC + yv] : cscale[j]) : 0.f;
+            const float z = acc[i][j][e] + cbias[j];
+            const bool pos = kind == 0 ? yv == 1 : yv == tgt;
+            const float ex = __expf(-fabsf(z));                    // one exp, one log, one rcp
+            const float inv = __builtin_amdgcn_rcpf(1.f + ex);
+            const float p = z >= 0.f ? inv : ex * inv;
+            const float t = pos ? -z : z;
+            lsum[j] += sc * (fmaxf(t, 0.f) + __logf(1.f + ex));
+            r[e] = (p - (pos ? 1.f : 0.f)) * sc;
+          }
+          u32x2 hv, lv;
+          {
+            const __bf16 h0 = (__bf16)r[0], h1 = (__bf16)r[1], h2 = (__bf16)r[2], h3 = (__bf16)r[3];
+            const __bf16 l0 = (__bf16)(r[0] - (float)h0), l1 = (__bf16)(r[1] - (float)h1);
+            const __bf16 l2 = (__bf16)(r[2] - (float)h2), l3 = (__bf16)(r[3] - (float)h3);
+            hv.x = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+            hv.y = (uint32_t)__builtin_bit_cast(uint16_t, h2) | ((uint32_t)__builtin_bit_cast(uint16_t, h3) << 16);
+            lv.x = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+            lv.y = (uint32_t)__builtin_bit_cast(uint16_t, l2) | ((uint32_t)__builtin_bit_cast(uint16_t, l3) << 16);
+          }
+          const int64_t g0 = row0 + lr0;   // 4 consecutive rows inside one 32-row K block
+          const int64_t off = (g0 >> 5) * Mp * BK + (g0 & (BK - 1));
+          *(__attribute__((address_space(1))) u32x2*)(RH + off) = hv;
+          *(__attribute__((address_space(1))) u32x2*)(RL + off) = lv;
         }
       }
-    if (tid < TM) ys[tid] = row0 + tid < a.n ? y[row0 + tid] : 0;
-    __syncthreads();
-    // the lead column of a fit owns the fit's k columns for its 64 rows
-    const int f = col_fit[col0 + c];
-    const bool lead = f >= 0 && reinterpret_cast<const int32_t*>(a.fit_col0)[f] == col0 + c;
-    double lossq = 0.0;
-    if (lead) {
-      const int k = reinterpret_cast<const int32_t*>(a.fit_k)[f];
-      const int kind = reinterpret_cast<const int32_t*>(a.fit_kind)[f];
-      const int64_t role_off = (int64_t)reinterpret_cast<const int32_t*>(a.fit_split)[f] * a.n;
-      const float s0 = reinterpret_cast<const float*>(a.scale)[f];
-      const float* cwf = a.cw ? GPTR(const float, a.cw) + (int64_t)f * a.cwC : nullptr;
-      const auto RH = GPTR(uint16_t, a.rh) + (col0 + c) * BK;
-      const auto RL = GPTR(uint16_t, a.rl) + (col0 + c) * BK;
-      float lsum = 0.f;
-      for (int rr = 0; rr < 64; rr += 8) {
-        const int lr0 = rq * 64 + rr;
-        const int64_t g0 = row0 + lr0;
-        float sc[8];
-        int yv[8];
+      // column sums: the 4 lanes of a column (lane >> 4), then the 4 row-waves (wm) in LDS
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int64_t g = g0 + e;
-          yv[e] = ys[lr0 + e];
-          const bool tr = g < a.n && roles[role_off + g] == 1;
-          sc[e] = tr ? (cwf ? s0 * cwf[yv[e]] : s0) : 0.f;
+      for (int j = 0; j < 4; ++j) {
+        double v = (double)lsum[j];
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        if (lane < 16) lq[wm * TN + wn * 64 + j * 16 + lane] = v;
+      }
+    } else {
+      // ---- multinomial batches: Z tile through LDS, the lead column of a fit owns its k columns
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = wn * 64 + j * 16 + (lane & 15);
+          const float bv = bias[col0 + col];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = wm * 64 + i * 16 + (lane >> 4) * 4 + e;
+            zs[zidx(row, col)] = acc[i][j][e] + bv;
+          }
         }
-        if (kind == 1) {
-          float lse[8];
+      __syncthreads();
+      const int c = tid & (TN - 1), rq = tid >> 7;
+      const int f = col_fit[col0 + c];
+      const bool lead = f >= 0 && reinterpret_cast<const int32_t*>(a.fit_col0)[f] == col0 + c;
+      double lossq = 0.0;
+      if (lead) {
+        const int k = reinterpret_cast<const int32_t*>(a.fit_k)[f];
+        const int kind = reinterpret_cast<const int32_t*>(a.fit_kind)[f];
+        const int sp = reinterpret_cast<const int32_t*>(a.fit_split)[f];
+        const float s0 = reinterpret_cast<const float*>(a.scale)[f];
+        const float* cwf = a.cw ? GPTR(const float, a.cw) + (int64_t)f * a.cwC : nullptr;
+        const auto RH = GPTR(uint16_t, a.rh) + (col0 + c) * BK;
+        const auto RL = GPTR(uint16_t, a.rl) + (col0 + c) * BK;
+        float lsumq = 0.f;
+        for (int rr = 0; rr < 64; rr += 8) {
+          const int lr0 = rq * 64 + rr;
+          const int64_t g0 = row0 + lr0;
+          float sc[8];
+          int yv[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            float m = zs[zidx(lr0 + e, c)];
-            for (int jj = 1; jj < k; ++jj) m = fmaxf(m, zs[zidx(lr0 + e, c + jj)]);
-            float se = 0.f;
-            for (int jj = 0; jj < k; ++jj) se += __expf(zs[zidx(lr0 + e, c + jj)] - m);
-            lse[e] = m + __logf(se);
-            lsum += sc[e] * (lse[e] - zs[zidx(lr0 + e, c + yv[e])]);
+            yv[e] = eps_y[lr0 + e];
+            const bool tr = g0 + e < a.n && role_at(sp, lr0 + e) == 1;
+            sc[e] = tr ? (cwf ? s0 * cwf[yv[e]] : s0) : 0.f;
           }
-          for (int jj = 0; jj < k; ++jj) {
-            float r[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              r[e] = (__expf(zs[zidx(lr0 + e, c + jj)] - lse[e]) - (yv[e] == jj ? 1.f : 0.f)) * sc[e];
-            u32x4 hv, lv;
-            split8(r, hv, lv);
-            const int64_t off = ((g0 >> 5) * Mp + jj) * BK + (g0 & (BK - 1));
-            *(gvec_w)(RH + off) = hv;
-            *(gvec_w)(RL + off) = lv;
-          }
-        } else {
-          for (int jj = 0; jj < k; ++jj) {
-            float r[8];
+          if (kind == 1) {
+            float lse[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const float z = zs[zidx(lr0 + e, c + jj)];
-              const bool pos = kind == 0 ? yv[e] == 1 : yv[e] == jj;
-              const float ex = __expf(-fabsf(z));
-              const float inv = __builtin_amdgcn_rcpf(1.f + ex);
-              const float p = z >= 0.f ? inv : ex * inv;
-              const float t = pos ? -z : z;
-              lsum += sc[e] * (fmaxf(t, 0.f) + __logf(1.f + ex));
-              r[e] = (p - (pos ? 1.f : 0.f)) * sc[e];
+              float m = zs[zidx(lr0 + e, c)];
+              for (int jj = 1; jj < k; ++jj) m = fmaxf(m, zs[zidx(lr0 + e, c + jj)]);
+              float se = 0.f;
+              for (int jj = 0; jj < k; ++jj) se += __expf(zs[zidx(lr0 + e, c + jj)] - m);
+              lse[e] = m + __logf(se);
+              lsumq += sc[e] * (lse[e] - zs[zidx(lr0 + e, c + yv[e])]);
             }
-            u32x4 hv, lv;
-            split8(r, hv, lv);
-            const int64_t off = ((g0 >> 5) * Mp + jj) * BK + (g0 & (BK - 1));
-            *(gvec_w)(RH + off) = hv;
-            *(gvec_w)(RL + off) = lv;
+            for (int jj = 0; jj < k; ++jj) {
+              float r[8];
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                r[e] = (__expf(zs[zidx(lr0 + e, c + jj)] - lse[e]) - (yv[e] == jj ? 1.f : 0.f)) * sc[e];
+              u32x4 hv, lv;
+              split8(r, hv, lv);
+              const int64_t off = ((g0 >> 5) * Mp + jj) * BK + (g0 & (BK - 1));
+              *(gvec_w)(RH + off) = hv;
+              *(gvec_w)(RL + off) = lv;
+            }
+          } else {
+            for (int jj = 0; jj < k; ++jj) {
+              float r[8];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const float z = zs[zidx(lr0 + e, c + jj)];
+                const bool pos = kind == 0 ? yv[e] == 1 : yv[e] == jj;
+                const float ex = __expf(-fabsf(z));
+                const float inv = __builtin_amdgcn_rcpf(1.f + ex);
+                const float p = z >= 0.f ? inv : ex * inv;
+                const float t = pos ? -z : z;
+                lsumq += sc[e] * (fmaxf(t, 0.f) + __logf(1.f + ex));
+                r[e] = (p - (pos ? 1.f : 0.f)) * sc[e];
+              }
+              u32x4 hv, lv;
+              split8(r, hv, lv);
+              const int64_t off = ((g0 >> 5) * Mp + jj) * BK + (g0 & (BK - 1));
+              *(gvec_w)(RH + off) = hv;
+              *(gvec_w)(RL + off) = lv;
+            }
           }
         }
+        lossq = (double)lsumq;
       }
-      lossq = (double)lsum;
+      lq[rq * TN + c] = lossq;
     }
-    lq[rq * TN + c] = lossq;
     __syncthreads();
-    if (rq == 0) lpart[rt * Mp + col0 + c] = lq[c] + lq[TN + c] + lq[2 * TN + c] + lq[3 * TN + c];
+    if (tid < TN) lpart[rt * Mp + col0 + tid] = lq[tid] + lq[TN + tid] + lq[2 * TN + tid] + lq[3 * TN + tid];
     __syncthreads();   // Z tile / labels / partials read before the next item's staging writes
   }
 }
@@ -743,7 +853,8 @@ int dml_lr_v3_row_tile() { return v3::TM; }
 
 int dml_lr_mfma_fwd3(const FwdArgs* a, hipStream_t st) {
   if (a->row_tiles <= 0 || a->col_tiles <= 0) return 0;
-  if (a->Kp % BK || a->row_groups % 8 || a->row_groups <= 0 || !a->lpart) return 2;
+  if (a->Kp % BK || a->row_groups % 8 || a->row_groups <= 0 || !a->lpart || a->n_splits <= 0) return 2;
+  if (!a->col_info || !a->col_scale) return 2;
   if (a->xrows != a->row_tiles * v3::TM || a->kr != a->xrows) return 2;
   if (a->row_groups > 0x7fffffff) return 2;
   k_lr_fwd3<<<(unsigned)a->row_groups, v3::NT, 0, st>>>(*a);   // row_groups = workgroups (persistent)

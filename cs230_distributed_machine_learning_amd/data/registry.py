@@ -58,6 +58,7 @@ class DatasetRegistry:
         os.makedirs(self.datasets_dir, exist_ok=True)
         os.makedirs(self.configs_dir, exist_ok=True)
         self._cache: Dict[tuple, TabularDataset] = {}
+        self._meta_cache: Dict[tuple, Dict[str, Any]] = {}
         self._lock = threading.Lock()
 
     # ---- paths -----------------------------------------------------------------------
@@ -173,10 +174,19 @@ class DatasetRegistry:
         return ds
 
     def metadata(self, name: str) -> Dict[str, Any]:
+        """{n_rows, n_cols, size_mb}, cached per (file, mtime): the cluster dispatcher asks at
+        every job admission, and counting a large CSV's rows would stall it for seconds."""
         path = self.find_file(name)
         if path is None:
             return {}
-        return file_metadata(path)
+        key = ("__meta__", path, os.path.getmtime(path))
+        with self._lock:
+            hit = self._meta_cache.get(key)
+        if hit is None:
+            hit = file_metadata(path)
+            with self._lock:
+                self._meta_cache[key] = hit
+        return dict(hit)
 
 
 def file_metadata(path: str) -> Dict[str, Any]:

@@ -203,8 +203,23 @@ class MfmaPlan:
         self.rl = torch.zeros_like(self.rh)
         self.loss = torch.zeros(b.F, dtype=torch.float64, device=dev)
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        self.lpart = None
+        self.lpart = self.col_info = self.col_scale = None
+        self.softmax_any = any(kd == KIND_SOFTMAX for kd in b.kind_l)
         if self.v3:
+            # per padded column: kind << 28 | split << 16 | positive class (OvR column j: class j),
+            # -1 on padding; and the fit's loss scale (k_lr_fwd3's register epilogue)
+            info = np.full(self.Mp, -1, dtype=np.int64)
+            cscale = np.zeros(self.Mp, dtype=np.float32)
+            sc_host = b.scale.cpu().numpy()
+            for f, (c0, k, kd, sp) in enumerate(zip(pcol0, b.K_l, b.kind_l, b.split_l)):
+                if sp >= 4096:
+                    raise RuntimeError("lr_mfma v3: split index out of range")
+                for j in range(k):
+                    info[c0 + j] = (kd << 28) | (sp << 16) | (j if kd == KIND_OVR else 1)
+                    cscale[c0 + j] = sc_host[f]
+            self.col_info = torch.from_numpy(info.astype(np.int32)).to(dev)
+            self.col_scale = torch.from_numpy(cscale).to(dev)
+            self.k_uniform = len(set(b.K_l)) == 1
             # forward: one persistent workgroup per CU (8 per XCD walk their XCD's row tiles);
             # gradient: 256-row R^T tiles x 128-row X^T tiles x K slices
             row_tiles = ops.npad // _ROW_TILE
@@ -231,7 +246,9 @@ class MfmaPlan:
             row_tiles=row_tiles, col_tiles=col_tiles, row_groups=rg, bias=p(self.bias), col_fit=p(self.col_fit),
             fit_col0=p(self.fit_col0), fit_k=p(b.K), fit_kind=p(b.kind), fit_split=p(b.split), scale=p(b.scale),
             cw=p(b.cw), cwC=int(b.cw.shape[1]) if b.cw is not None else 0, y=p(data.y_cls), roles=p(data.roles),
-            rh=p(self.rh), rl=p(self.rl), kr=ops.npad, loss=p(self.loss), lpart=p(self.lpart))
+            rh=p(self.rh), rl=p(self.rl), kr=ops.npad, loss=p(self.loss), lpart=p(self.lpart),
+            col_info=p(self.col_info), col_scale=p(self.col_scale), n_splits=int(data.roles.shape[0]),
+            softmax_any=int(self.softmax_any))
         self.fit_col0_l = self.fit_col0.long()
         self.grad = native.LrGradArgs(
             rh=p(self.rh), rl=p(self.rl), unused=0, xth=p(ops.xth), xtl=p(ops.xtl), m_tiles=m_tiles,
@@ -261,8 +278,14 @@ class MfmaPlan:
                 rc = lib.dml_lr_mfma_grad(ctypes.byref(self.grad), st)
         if rc:
             raise RuntimeError(f"lr_mfma launch failed ({rc})")
-        if self.v3:   # every (row tile, column) partial written once: fixed-order sum over row tiles
-            self.loss.copy_(self.lpart.sum(0)[self.fit_col0_l])
+        if self.v3:
+            # every (row tile, column) partial is written once; fixed-order sums over row tiles,
+            # then over each fit's columns (OvR: k sigmoid columns; binary / softmax: one)
+            colsum = self.lpart.sum(0)[self.colmap]
+            if self.k_uniform:
+                self.loss.copy_(colsum.view(b.F, -1).sum(1))
+            else:
+                self.loss.copy_(torch.zeros_like(self.loss).index_add_(0, b.col_fit, colsum))
         GT = self.slabs.sum(0)
         G = torch.empty_like(W)
         G[:d] = GT[self.colmap, :d].t()

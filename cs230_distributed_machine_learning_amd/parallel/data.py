@@ -160,8 +160,16 @@ def share_bins(dd, group=None) -> None:
 # not in the process group at all).  Rank 0 parses the table once and writes it to a
 # host file (tmpfs by default); every rank memory-maps it and copies it to its own GPU over
 # its own PCIe link -- no rank waits for another.
-def stage_host(X: np.ndarray, y: np.ndarray, path: str) -> str:
+def _y_path(path: str) -> str:
+    return path + ".y.npz"
+
+
+def stage_host(X: np.ndarray, y: np.ndarray, path: str, threads: int = 8) -> str:
+    """Write the table for host-staged / sharded loads: X as a raw ``.npy`` (memory-mappable:
+    a rank reads only the rows it copies) filled by ``threads`` parallel row-chunk copies
+    (numpy releases the GIL for them), y + label metadata in a small sidecar."""
     import os
+    from concurrent.futures import ThreadPoolExecutor
 
     y = np.asarray(y)
     meta = {"n": int(X.shape[0]), "d": int(X.shape[1])}
@@ -172,20 +180,81 @@ def stage_host(X: np.ndarray, y: np.ndarray, path: str) -> str:
     else:
         meta["y"] = str(y.dtype)
         y_arr = y
-    tmp = path + ".tmp.npz"
-    np.savez(tmp, X=np.ascontiguousarray(X, dtype=np.float32), y=y_arr, meta=np.array(json.dumps(meta)))
+    tmp = path + ".tmp.npy"
+    mm = np.lib.format.open_memmap(tmp, mode="w+", dtype=np.float32, shape=tuple(X.shape))
+    n = X.shape[0]
+    step = max(1, -(-n // max(1, threads * 4)))
+
+    def copy(r0):
+        mm[r0:r0 + step] = X[r0:r0 + step]
+
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as ex:
+        list(ex.map(copy, range(0, n, step)))
+    mm.flush()
+    del mm
+    ytmp = _y_path(path) + ".tmp.npz"
+    np.savez(ytmp, y=y_arr, meta=np.array(json.dumps(meta)))
+    os.replace(ytmp, _y_path(path))   # the sidecar first: a reader that sees X sees its labels
     os.replace(tmp, path)
     return path
 
 
-def load_staged(path: str, device: torch.device):
-    """(X on ``device``, y host array) from a file written by ``stage_host``."""
-    with np.load(path, allow_pickle=False) as z:
+def _staged_labels(path: str):
+    with np.load(_y_path(path), allow_pickle=False) as z:
         meta = json.loads(str(z["meta"]))
-        X = torch.from_numpy(np.ascontiguousarray(z["X"])).to(device)
         y = z["y"]
     if meta["y"] == "codes":
         y = np.asarray(meta["classes"], dtype=object)[y.astype(np.int64)]
     else:
         y = y.astype(np.dtype(meta["y"]))
-    return X, y
+    return meta, y
+
+
+def _mapped_rows(Xm, device) -> torch.Tensor:
+    """Rows of a read-only memory map on ``device``: a device copy straight from the mapped
+    pages, or (CPU) a private writable copy -- never a tensor aliasing the read-only map."""
+    import warnings
+
+    dev = torch.device(device)
+    if dev.type == "cpu":
+        return torch.from_numpy(np.array(Xm, dtype=np.float32))
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", UserWarning)   # read-only source of a copy: nothing writes it
+        return torch.from_numpy(np.asarray(Xm)).to(dev)
+
+
+def load_staged(path: str, device: torch.device):
+    """(X on ``device``, y host array) from a file written by ``stage_host``."""
+    _, y = _staged_labels(path)
+    return _mapped_rows(np.load(path, mmap_mode="r", allow_pickle=False), device), y
+
+
+def sharded_load(path: str, device: torch.device, group=None):
+    """Every rank of the group assembles the staged table: each copies ONLY its 1/N row block
+    from the memory-mapped host file to its own GPU (N PCIe links in parallel instead of rank
+    0's one), then one ``all_gather_into_tensor`` over xGMI (gloo: all_gather) completes the
+    table on every rank.  Returns (X on ``device``, y host array, H2D seconds of
+    this rank's block)."""
+    import time
+
+    inf = dist.info()
+    meta, y = _staged_labels(path)
+    n, d = meta["n"], meta["d"]
+    Xm = np.load(path, mmap_mode="r", allow_pickle=False)
+    if not inf.is_dist or inf.world == 1:
+        t0 = time.perf_counter()
+        X = _mapped_rows(Xm, device)
+        return X, y, time.perf_counter() - t0
+    W = inf.world
+    q = -(-n // W)                                   # equal blocks (the last one padded)
+    r0, r1 = min(n, inf.rank * q), min(n, (inf.rank + 1) * q)
+    shard = torch.zeros((q, d), dtype=torch.float32, device=device)
+    t0 = time.perf_counter()
+    if r1 > r0:
+        shard[:r1 - r0].copy_(_mapped_rows(Xm[r0:r1], device))
+    if shard.is_cuda:
+        torch.cuda.synchronize(device)
+    h2d = time.perf_counter() - t0
+    full = dist.all_gather_rows(shard, group=group)   # [W * q, d] in rank order
+    dist.barrier(group=group)
+    return full[:n], y, h2d

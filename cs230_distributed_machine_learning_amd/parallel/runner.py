@@ -251,6 +251,8 @@ class WorkerCore:
         self.cache_lock = threading.RLock()   # the worker and the collective thread share the cache
         # the side communicator (collective with every rank: built here, by every in-group rank)
         self.side = dist.side_group() if (in_group and self.inf.is_dist) else None
+        self.stage_dir: Optional[str] = None    # rank 0: the dispatcher's host staging directory
+        self.load_h2d_s: List[float] = []       # this rank's H2D seconds per collective load
         # the data-parallel communicator (short timeout; created collectively right after the
         # side group, in the same order on every in-group rank)
         self.dp = dist.dp_group() if (in_group and self.inf.is_dist) else None
@@ -313,7 +315,15 @@ class WorkerCore:
             ds = ctl.registry.load(msg["dataset_id"], plan["feature_columns"], plan["target_column"])
             X, y = ds.X, ds.y
             binned = ctl is not None and _binned_only_table(ctl, plan, X, self.device)
-            self.store_raw().set(mode_key, "binned" if binned else "full")
+            mode = "binned" if binned else "full"
+            if not binned and self.inf.world > 1 and self.stage_dir and X.nbytes >= shard_load_min_bytes():
+                # large table: staged once on the host, every rank copies its own 1/N row block
+                # over its own PCIe link, one all-gather over xGMI completes it (sharded_load)
+                path = staged_path(self.stage_dir, msg["dataset_key"])
+                if not os.path.exists(path):
+                    pdata.stage_host(X, y, path)
+                mode = "sharded:" + path
+            self.store_raw().set(mode_key, mode)
         else:
             # on the side group, bounded like the side collectives themselves: a rank 0 that
             # fails before publishing the mode must not hold this thread past the side deadline
@@ -323,8 +333,15 @@ class WorkerCore:
                 self.store_raw().wait([mode_key], datetime.timedelta(seconds=dist.side_timeout_s()))
             else:
                 self.store_raw().wait([mode_key])
-            binned = self.store_raw().get(mode_key).decode() == "binned"
-        if binned:   # tree job on a table too large for HBM as float32: bins only
+            mode = self.store_raw().get(mode_key).decode()
+            binned = mode == "binned"
+        if mode.startswith("sharded:"):
+            Xd, y_host, h2d = pdata.sharded_load(mode[len("sharded:"):], self.device, group=group)
+            self.load_h2d_s.append(h2d)
+            dd = DeviceData(Xd, y_host, clf, self.device, name=msg["dataset_id"])
+            if _needs_bins(plan):
+                pdata.share_bins(dd, group=group)
+        elif binned:   # tree job on a table too large for HBM as float32: bins only
             dd = pdata.broadcast_binned(X, y, clf, self.device, name=msg["dataset_id"], group=group, tag=tag)
         else:
             Xd, y_host = pdata.broadcast_table(X, y, self.device, group=group, tag=tag)
@@ -622,6 +639,17 @@ def worker_loop(core: WorkerCore, ctl: Optional[Controller] = None, heartbeat: b
             hb.stop()
 
 
+def staged_path(stage_dir: str, dataset_key: str) -> str:
+    """Host staging file of a dataset (parallel/data.py stage_host: raw .npy + label sidecar)."""
+    return os.path.join(stage_dir, f"{zlib.crc32(dataset_key.encode()) & 0xFFFFFFFF:08x}.npy")
+
+
+def shard_load_min_bytes() -> int:
+    """Tables of at least this many float32 bytes (``DML_SHARD_LOAD_MIN_MB``, default 1024) load
+    sharded: rank 0 stages them once, each rank copies 1/N of the rows, one all-gather."""
+    return int(float(os.environ.get("DML_SHARD_LOAD_MIN_MB", "1024")) * (1 << 20))
+
+
 def needs_whole_rows(model_type: str, params: Dict[str, Any]) -> bool:
     """A candidate the row-sharded builders cannot fit exactly: absolute_error trees need
     per-node weighted medians over every row, and monotonic_cst's node bounds are not part of
@@ -753,6 +781,7 @@ class DistributedRunner(Runner):
         self._stage_dir = os.environ.get("DML_STAGE_DIR") or (
             tempfile.mkdtemp(prefix="dml_stage_", dir="/dev/shm") if os.path.isdir("/dev/shm") else tempfile.mkdtemp())
         self._t0 = time.time()
+        core.stage_dir = self._stage_dir   # rank 0's collective loads stage large tables here
 
     def bind(self, controller: Controller) -> None:
         super().bind(controller)
@@ -789,6 +818,13 @@ class DistributedRunner(Runner):
 
     # ---- main loop ---------------------------------------------------------------------
     def serve_forever(self, idle_poll_s: float = 0.05) -> None:
+        # rank 0's process runs the dispatcher, the gateway, its own worker and the collective
+        # thread: a 1 ms GIL switch interval (default 5 ms) bounds how long a worker thread's
+        # Python stretch can hold an answer's dispatch back (config-5 rehearsal, 8 ranks:
+        # profiles/r5_config5_8rank_gloo_dispatch.jsonl)
+        import sys
+
+        sys.setswitchinterval(float(os.environ.get("DML_GIL_SWITCH_S", "0.001")))
         w0 = threading.Thread(target=worker_loop, args=(self.core, self.ctl, False), daemon=True,
                               name="dml-rank0-worker")
         w0.start()
@@ -889,8 +925,7 @@ class DistributedRunner(Runner):
         if js.staged_ready:
             return
         ds = self.ctl.registry.load(js.job.dataset_id, js.plan["feature_columns"], js.plan["target_column"])
-        name = f"{zlib.crc32(js.msg['dataset_key'].encode()) & 0xFFFFFFFF:08x}.npz"
-        path = os.path.join(self._stage_dir, name)
+        path = staged_path(self._stage_dir, js.msg["dataset_key"])
         if not os.path.exists(path):
             pdata.stage_host(ds.X, ds.y, path)
         js.msg["staged"] = path
@@ -1193,6 +1228,12 @@ class DistributedRunner(Runner):
             got = True
             self.stats["answers"] += 1
             self._t_answer[w.wid] = float(out.get("t_post", time.time()))
+            # control-plane lag: a worker's answer posted -> consumed by the dispatcher (the
+            # dispatch latency above also counts time the worker waited for queued work)
+            lag = self.stats.setdefault("answer_lag_s", [])
+            lag.append(max(0.0, time.time() - self._t_answer[w.wid]))
+            if len(lag) > 100000:
+                del lag[:50000]
             if "fatal" in out:
                 log.error("worker %d reported a device fault (%s): re-queueing its work", w.wid, out["fatal"])
                 self._declare_dead(w, a)

@@ -91,7 +91,7 @@ LrFwdArgs = _i64_struct(
     "LrFwdArgs",
     ["xh", "xl", "xrows", "wh", "wl", "n", "Kp", "row_tiles", "col_tiles", "row_groups", "bias", "col_fit",
      "fit_col0", "fit_k", "fit_kind", "fit_split", "scale", "cw", "cwC", "y", "roles", "rh", "rl", "kr", "loss",
-     "lpart"],
+     "lpart", "col_info", "col_scale", "n_splits", "softmax_any"],
 )
 # csrc/kernels/gbrt.hip argument blocks (fused gradient-boosting stage kernels)
 GbStageArgs = _i64_struct(

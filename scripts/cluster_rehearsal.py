@@ -79,7 +79,50 @@ def _jobs(heavy: bool = False):
     return out
 
 
-def _rank_main(rank, world, port, root, kill, outq, heavy=False, env_extra=None):
+# BASELINE config 5's queue shape (scripts/bench_configs.py config5: 4 sessions x (RF grid of 4
+# candidates + LR RandomizedSearchCV of 16) at cv=5, submitted together) on a CPU-sized table
+C5_TABLE = ("mixed", "target", "classification?n=20000&d=20&informative=5&noise=1.0&seed=0")
+
+
+def _config5_jobs():
+    out = []
+    for s in range(4):
+        out.append((s, C5_TABLE[0], {"dataset_id": C5_TABLE[0], "train_params": {"target_column": "target"},
+                                     "model_details": {"model_type": "RandomForestClassifier",
+                                                       "search_type": "GridSearchCV", "hyperparameters": {
+                                                           "base_estimator_params": {}, "cv_params": {"cv": 5},
+                                                           "search_params": {"param_grid": {
+                                                               "n_estimators": [10, 20], "max_depth": [6, None]}}}}}))
+        out.append((s, C5_TABLE[0], {"dataset_id": C5_TABLE[0], "train_params": {"target_column": "target"},
+                                     "model_details": {"model_type": "LogisticRegression",
+                                                       "search_type": "RandomizedSearchCV", "hyperparameters": {
+                                                           "base_estimator_params": {}, "cv_params": {"cv": 5},
+                                                           "search_params": {"param_distributions": {
+                                                               "C": {"dist": "loguniform", "a": 1e-3, "b": 1e2}},
+                                                               "n_iter": 16, "random_state": s}}}}))
+    return out
+
+
+def _poll_gateway(port, targets, stop, lat):
+    """Poll GET /check_status of the running jobs through the HTTP gateway (what a client's
+    progress bar does) until ``stop``; record each request's latency."""
+    import requests
+
+    sess = requests.Session()
+    i = 0
+    while not stop.is_set() and targets:
+        sid, jid = targets[i % len(targets)]
+        i += 1
+        t0 = time.perf_counter()
+        try:
+            sess.get(f"http://127.0.0.1:{port}/check_status/{sid}/{jid}", timeout=30)
+            lat.append(time.perf_counter() - t0)
+        except Exception:
+            pass
+        time.sleep(0.005)
+
+
+def _rank_main(rank, world, port, root, kill, outq, heavy=False, env_extra=None, queue="mixed"):
     env = dict(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                LOCAL_RANK=str(rank), OMP_NUM_THREADS="1", DML_DEAD_AFTER_S="3")
     if kill is not None:
@@ -103,17 +146,40 @@ def _rank_main(rank, world, port, root, kill, outq, heavy=False, env_extra=None)
     runner = DistributedRunner(core)
     ctl = Controller(cfg, runner=runner)
 
+    gw_lat: list = []
+    gw_targets: list = []
+    gw_stop = threading.Event()
+
     def drive():
         try:
-            sids = [ctl.create_session()[1]["session_id"] for _ in range(2)]
-            _register(ctl, sids[0], heavy)
+            if queue == "config5":
+                sids = [ctl.create_session()[1]["session_id"] for _ in range(4)]
+                st, _ = ctl.download_data(sids[0], {"dataset_url": C5_TABLE[2], "dataset_name": C5_TABLE[0],
+                                                    "dataset_type": "synthetic"})
+                assert st == 200
+                jobs_in = _config5_jobs()
+                from cs230_distributed_machine_learning_amd.gateway.app import serve
+
+                gw_port = _free_port()
+                serve(ctl, port=gw_port, block=False)
+                time.sleep(1.0)
+            else:
+                sids = [ctl.create_session()[1]["session_id"] for _ in range(2)]
+                _register(ctl, sids[0], heavy)
+                jobs_in = _jobs(heavy)
             t0 = time.time()
             ops0 = runner.store_ops()
             acks = []
-            for s, name, body in _jobs(heavy):   # every job submitted at once: concurrent searches
+            for s, name, body in jobs_in:   # every job submitted at once: concurrent searches
                 st, ack = ctl.train(sids[s], body)
                 assert st in (200, 202), ack
                 acks.append((s, name, body["model_details"]["model_type"], ack["job_id"]))
+            poller = None
+            if queue == "config5":
+                gw_targets.extend((sids[s], jid) for s, _n, _m, jid in acks)
+                poller = threading.Thread(target=_poll_gateway, args=(gw_port, gw_targets, gw_stop, gw_lat),
+                                          daemon=True)
+                poller.start()
             jobs = []
             for s, name, model, jid in acks:
                 ctl.table.wait_finished(jid, timeout=600)
@@ -126,8 +192,15 @@ def _rank_main(rank, world, port, root, kill, outq, heavy=False, env_extra=None)
                              "scores": sorted((json.dumps(r.get("parameters"), sort_keys=True), r.get("cv_scores"))
                                               for r in res)})
             wall = time.time() - t0
+            gw_stop.set()
+            if poller is not None:
+                poller.join(timeout=10)
             lat = sorted(runner.stats["dispatch_latency_s"])
             pct = lambda q: round(lat[min(len(lat) - 1, int(q * len(lat)))] * 1e3, 2) if lat else None
+            al = sorted(runner.stats.get("answer_lag_s", []))
+            apct = lambda q: round(al[min(len(al) - 1, int(q * len(al)))] * 1e3, 2) if al else None
+            gl = sorted(gw_lat)
+            gpct = lambda q: round(gl[min(len(gl) - 1, int(q * len(gl)))] * 1e3, 2) if gl else None
             ops = runner.store_ops() - ops0
             outq.put(("ok", {"world": world, "killed": kill, "dead": sorted(runner.dead), "wall_s": round(wall, 2),
                              "jobs": jobs, "dispatcher_loops": runner.stats["loops"],
@@ -135,7 +208,12 @@ def _rank_main(rank, world, port, root, kill, outq, heavy=False, env_extra=None)
                              "max_drain_wait_s": round(runner.stats["max_drain_wait_s"], 3),
                              "rank0_store_ops_per_s": round(ops / max(wall, 1e-9), 1),
                              "dispatch_latency_ms": {"p50": pct(0.5), "p90": pct(0.9), "p99": pct(0.99),
-                                                     "max": pct(1.0), "n": len(lat)}}))
+                                                     "max": pct(1.0), "n": len(lat)},
+                             "answer_lag_ms": {"p50": apct(0.5), "p90": apct(0.9), "p99": apct(0.99),
+                                               "max": apct(1.0), "n": len(al)},
+                             "queue": queue,
+                             "gateway_check_status_ms": {"p50": gpct(0.5), "p90": gpct(0.9), "p99": gpct(0.99),
+                                                         "max": gpct(1.0), "n": len(gl)} if gl else None}))
         except Exception:  # pragma: no cover
             import traceback
 
@@ -169,14 +247,15 @@ def local_scores(body_jobs=None, heavy: bool = False) -> list:
     return out
 
 
-def run(world: int = 8, kill=None, timeout_s: float = 900.0, heavy: bool = False, env_extra=None) -> dict:
+def run(world: int = 8, kill=None, timeout_s: float = 900.0, heavy: bool = False, env_extra=None,
+        queue: str = "mixed") -> dict:
     import torch.multiprocessing as mp
 
     root = tempfile.mkdtemp(prefix="dml_rehearsal_")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, root, kill, q, heavy, env_extra))
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, root, kill, q, heavy, env_extra, queue))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -201,8 +280,10 @@ if __name__ == "__main__":
     ap.add_argument("--kill", type=int, default=None)
     ap.add_argument("--json", default=None)
     ap.add_argument("--heavy", action="store_true", help="add the 62.5k x 20 table's RF / LR searches")
+    ap.add_argument("--queue", choices=("mixed", "config5"), default="mixed",
+                    help="config5: BASELINE config 5's queue shape, /check_status polled through the gateway")
     args = ap.parse_args()
-    r = run(args.world, args.kill, heavy=args.heavy)
+    r = run(args.world, args.kill, heavy=args.heavy, queue=args.queue)
     line = json.dumps(r)
     print(line)
     if args.json:
