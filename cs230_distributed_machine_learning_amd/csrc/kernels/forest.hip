@@ -39,7 +39,11 @@
 #define DML_BLOCK_NT 256     // threads per block-tier node
 #endif
 #ifndef DML_NODES_WPE
-#define DML_NODES_WPE 3        // block tier (binary): 3 waves per SIMD, fewer spills -- 1.3 % faster than 4
+// block tier (binary): 4 waves per SIMD = 4 workgroups per CU.  With the register-rows paths
+// compiled out (DML_BLOCK_STREAM_ONLY) and the window loop's bins packed 4 per register the
+// kernel fits 127 VGPRs without spills (it needed 168 at 3 waves before): sweep build
+// 1.029 -> 1.008 s (profiles/r5_block_occupancy.txt)
+#define DML_NODES_WPE 4
 #endif
 // eval_feature is called with an LDS histogram (fused node kernels) and a global one
 // (large tier): inlined, each call site keeps its address space (ds_read / global_load);
@@ -57,6 +61,12 @@
 #endif
 #ifndef DML_NODES_WPE_WAVE_MAX
 #define DML_NODES_WPE_WAVE_MAX 8   // wave tier (binary) occupancy cap: 8 -> 64 VGPRs (spills), lower -> more VGPRs
+#endif
+#ifndef DML_KGMAX_BLOCK
+#define DML_KGMAX_BLOCK 16     // block tier: largest feature group with register-resident bins
+#endif
+#ifndef DML_BLOCK_STREAM_ONLY
+#define DML_BLOCK_STREAM_ONLY 1   // block-tier nodes (> wave_max >= 256 rows) always stream their rows
 #endif
 #ifndef DML_NODES_WPE_REG
 #define DML_NODES_WPE_REG 2   // regression node kernels: 3 histogram planes + payloads fit 256 VGPRs, no spills
@@ -1150,7 +1160,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
   constexpr int RPT = NT == 64 ? 4 : DML_RPT_BLOCK;   // rows per thread in registers (<= 4: packed u8 x 4)
   static_assert(RPT >= 1 && RPT <= 4, "RPT");
   static_assert(2 * RPT * (NT / 64) <= 32, "Scratch::wcnt too small for this NT x RPT");
-  constexpr int KGMAX = NT == 64 ? DML_KGMAX_WAVE : 16;   // feature-group bound (register-resident bins)
+  constexpr int KGMAX = NT == 64 ? DML_KGMAX_WAVE : DML_KGMAX_BLOCK;   // feature-group bound (register-resident bins)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   PH_BEGIN
   const OpenNode on = c.open[set_cur][tier][blockIdx.x];
@@ -1190,7 +1200,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
   const int cnt = on.count;
   // rows (+ bootstrap weight + label payload) of a <= NT*RPT-row node stay in registers
   // for every feature group and the partition; larger nodes stream in NT*RPT chunks.
-  const bool reg_rows = cnt <= NT * RPT;
+  // (block tier, DML_BLOCK_STREAM_ONLY: nodes there have > wave_max >= NT rows, so the
+  // register-rows paths are compiled out of it -- their registers no longer bound its occupancy)
+  const bool reg_rows = (NT > 64 && DML_BLOCK_STREAM_ONLY) ? false : cnt <= NT * RPT;
   uint32_t rrow[RPT], rbin[RPT];
   using PL = typename PLT<MODE>::T;
   PL rpl[RPT];
@@ -1400,26 +1412,30 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
             w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w;
           }
         };
+        // the group's bins stay packed 4 x u8 per register between extract and consume (the
+        // layout of the row's bscr slot): 2 x ceil(G/4) registers for the two chunks in flight
+        // instead of 2 x G -- the block tier's occupancy is bounded by this loop's registers
+        constexpr int NPK = (G + 3) / 4;
         auto extract = [&](const v32u& w, uint32_t* b) {
 #pragma unroll
-          for (int j = 0; j < G; ++j) b[j] = (w[fdw[j]] >> fsh[j]) & 0xFFu;
+          for (int q = 0; q < NPK; ++q) b[q] = 0u;
+#pragma unroll
+          for (int j = 0; j < G; ++j) b[j >> 2] |= (j < g ? (w[fdw[j]] >> fsh[j]) & 0xFFu : 0u) << (8 * (j & 3));
         };
         auto consume = [&](int base, bool valid, const uint32_t* b, const PRaw& pr) {
-          if (NT == 256 && pos == 0 && valid) {
-            uint32_t w4[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-            for (int j = 0; j < G && j < 16; ++j) w4[j >> 2] |= (j < g ? b[j] : 0u) << (8 * (j & 3));
-            *(uint4*)(c.bscr + (on.start + base + tid) * 16) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-          }
+          if (NT == 256 && pos == 0 && valid)
+            *(uint4*)(c.bscr + (on.start + base + tid) * 16) =
+                make_uint4(b[0], NPK > 1 ? b[NPK > 1 ? 1 : 0] : 0u, NPK > 2 ? b[NPK > 2 ? 2 : 0] : 0u,
+                           NPK > 3 ? b[NPK > 3 ? 3 : 0] : 0u);
           if (valid) {
             const PL pl = payload_finish<MODE, PK>(c, s, ty, pr);
 #pragma unroll
             for (int j = 0; j < G; ++j)
-              if (j < g) hist_add<MODE>(hist + j * span, c, (int)b[j], pl);
+              if (j < g) hist_add<MODE>(hist + j * span, c, (int)((b[j >> 2] >> (8 * (j & 3))) & 0xFFu), pl);
           }
         };
         v32u win;
-        uint32_t bA[G], bB[G];
+        uint32_t bA[NPK], bB[NPK];
         uint32_t rA = row_at(tid), rB = row_at(NT + tid);
         load_win(rA, win);
         PRaw pA = payload_fetch<MODE, PK>(c, ty, rA), pB;
@@ -3850,7 +3866,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   const size_t lds_s = sub_lds(a);
   const size_t lds_s32 = sub_lds(a, 32);
   const size_t lds_w = fused_lds(a, (int)a->kg_wave);
-  const size_t lds_b = fused_lds(a, (int)a->kg_block);
+  const size_t lds_b = fused_lds(a, (int)std::min<int64_t>(a->kg_block, DML_KGMAX_BLOCK));   // the kernel's KG
   const int CH = c.CH;
   // k_hist_large's dynamic LDS, optionally padded (DML_LARGE_LDS_MIN bytes) to cap its
   // workgroups per CU.  No padding: once the regression payload loads stopped draining the

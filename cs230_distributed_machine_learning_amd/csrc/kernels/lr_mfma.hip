@@ -70,6 +70,7 @@ struct FwdArgs {
   int64_t col_scale;             // v3: float [Mp] the column's fit's loss scale
   int64_t n_splits;              // v3: role rows of `roles`
   int64_t softmax_any;           // v3: 1 if any fit is multinomial (Z tile through LDS)
+  int64_t row_base;              // v3 row chunks: first (256-row) tile of the chunk; R^T rows are local
 };
 
 struct GradArgs {
@@ -78,6 +79,8 @@ struct GradArgs {
   int64_t m_tiles, n_tiles, Kp;  // Kp = rows of the dataset, padded
   int64_t S, Kc;                 // K slices (multiple of 8) and slice length (multiple of BK)
   int64_t out;                   // float [S x m_tiles*BM x n_tiles*BN] partial G^T slabs
+  int64_t bk_off;                // v3 row chunks: the chunk's first data row (B = X^T's k offset)
+  int64_t slab0;                 // v3 row chunks: first output slab of this chunk
 };
 
 struct Operands {
@@ -87,6 +90,7 @@ struct Operands {
   const uint16_t* bh;
   const uint16_t* bl;
   int64_t brows;
+  int64_t bk_off;  // B's k index = A's + bk_off (v3 gradient over a row chunk; multiple of 32)
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (((row >> 2) & 1) << 1); }
@@ -498,7 +502,7 @@ __device__ __forceinline__ void v3_glds_stage(const Operands& op, int64_t row0, 
                                               uint16_t* st, int w, int lane) {
   using namespace v3;
   static_assert(A_INSTR == 2 * (NT / 64) && B_INSTR == NT / 64, "piece split assumes 8 waves, 256 x 128");
-  const int64_t ab = ((k0 >> 5) * op.arows + row0) * BK, bb = ((k0 >> 5) * op.brows + col0) * BK;
+  const int64_t ab = ((k0 >> 5) * op.arows + row0) * BK, bb = (((k0 + op.bk_off) >> 5) * op.brows + col0) * BK;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     v3_glds_piece(op.ah + ab, st, (2 * w + h) * 64, lane);
@@ -573,8 +577,11 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
   double* lq = reinterpret_cast<double*>(smem_raw + TM * TN * 4);              // [4][TN] partials
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
   const int64_t b = blockIdx.x, xcd = b & 7, slot = b >> 3, slots = gridDim.x >> 3;
+  // row tiles of this launch: [row_base, row_base + row_tiles) of X; R^T (and its K-tiled
+  // layout) covers only the launch's rows (local row index = global - row_base * TM)
   const int64_t rt_here = a.row_tiles > xcd ? (a.row_tiles - xcd + 7) / 8 : 0;
   const int64_t items = rt_here * a.col_tiles;
+  const int64_t rbase = a.row_base * TM;
   const auto col_fit = GPTR(const int32_t, a.col_fit);
   const auto bias = GPTR(const float, a.bias);
   const auto y = GPTR(const int32_t, a.y);
@@ -593,7 +600,8 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
   const int nchunk = stage_roles ? S * (TM / 4) : 0;   // 4-row role chunks of the item (<= NT)
   static_assert(V3_ROLE_ROWS * (TM / 4) <= NT, "one role chunk per thread");
   for (int64_t it = slot; it < items; it += slots) {
-    const int64_t rt = xcd + 8 * (it / a.col_tiles), ct = it % a.col_tiles;
+    const int64_t rtl = xcd + 8 * (it / a.col_tiles), ct = it % a.col_tiles;
+    const int64_t rt = a.row_base + rtl;               // global row tile
     const int64_t row0 = rt * TM, col0 = ct * TN;
     // ---- item prologue: epilogue operands in flight under the GEMM.  Every load is
     // unconditional (clamped address, value selected after the GEMM): a load under a branch
@@ -674,7 +682,7 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
             lv.x = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
             lv.y = (uint32_t)__builtin_bit_cast(uint16_t, l2) | ((uint32_t)__builtin_bit_cast(uint16_t, l3) << 16);
           }
-          const int64_t g0 = row0 + lr0;   // 4 consecutive rows inside one 32-row K block
+          const int64_t g0 = row0 - rbase + lr0;   // local row; 4 consecutive rows inside one 32-row K block
           const int64_t off = (g0 >> 5) * Mp * BK + (g0 & (BK - 1));
           *(__attribute__((address_space(1))) u32x2*)(RH + off) = hv;
           *(__attribute__((address_space(1))) u32x2*)(RL + off) = lv;
@@ -718,13 +726,13 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
         float lsumq = 0.f;
         for (int rr = 0; rr < 64; rr += 8) {
           const int lr0 = rq * 64 + rr;
-          const int64_t g0 = row0 + lr0;
+          const int64_t g0 = row0 - rbase + lr0;   // local row of the R^T chunk
           float sc[8];
           int yv[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             yv[e] = eps_y[lr0 + e];
-            const bool tr = g0 + e < a.n && role_at(sp, lr0 + e) == 1;
+            const bool tr = row0 + lr0 + e < a.n && role_at(sp, lr0 + e) == 1;
             sc[e] = tr ? (cwf ? s0 * cwf[yv[e]] : s0) : 0.f;
           }
           if (kind == 1) {
@@ -796,11 +804,11 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_grad3(GradArgs a) {
   const int64_t ke = kb + a.Kc < a.Kp ? kb + a.Kc : a.Kp;
   const Operands op{reinterpret_cast<const uint16_t*>(a.rh), reinterpret_cast<const uint16_t*>(a.rl),
                     a.m_tiles * TM, reinterpret_cast<const uint16_t*>(a.xth), reinterpret_cast<const uint16_t*>(a.xtl),
-                    a.n_tiles * TN};
+                    a.n_tiles * TN, a.bk_off};
   f32x4 acc[4][4];
   v3_gemm(op, mt * TM, nt * TN, kb, ke, smem, acc, tid);
   const int64_t ldo = a.n_tiles * TN;
-  const auto out = GPTR(float, a.out) + s * (a.m_tiles * TM) * ldo;
+  const auto out = GPTR(float, a.out) + (a.slab0 + s) * (a.m_tiles * TM) * ldo;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -855,7 +863,7 @@ int dml_lr_mfma_fwd3(const FwdArgs* a, hipStream_t st) {
   if (a->row_tiles <= 0 || a->col_tiles <= 0) return 0;
   if (a->Kp % BK || a->row_groups % 8 || a->row_groups <= 0 || !a->lpart || a->n_splits <= 0) return 2;
   if (!a->col_info || !a->col_scale) return 2;
-  if (a->xrows != a->row_tiles * v3::TM || a->kr != a->xrows) return 2;
+  if (a->row_base < 0 || (a->row_base + a->row_tiles) * v3::TM > a->xrows || a->kr != a->row_tiles * v3::TM) return 2;
   if (a->row_groups > 0x7fffffff) return 2;
   k_lr_fwd3<<<(unsigned)a->row_groups, v3::NT, 0, st>>>(*a);   // row_groups = workgroups (persistent)
   return hipGetLastError() == hipSuccess ? 0 : 1;
@@ -864,6 +872,7 @@ int dml_lr_mfma_fwd3(const FwdArgs* a, hipStream_t st) {
 int dml_lr_mfma_grad3(const GradArgs* a, hipStream_t st) {
   if (a->m_tiles <= 0 || a->n_tiles <= 0) return 0;
   if (a->Kp % BK || a->Kc % BK || a->S % 8 || a->S <= 0 || a->S * a->Kc < a->Kp) return 2;
+  if (a->bk_off % BK || a->bk_off < 0 || a->slab0 < 0) return 2;
   const int64_t blocks = a->m_tiles * a->n_tiles * a->S;
   if (blocks > 0x7fffffff) return 2;
   k_lr_grad3<<<(unsigned)blocks, v3::NT, 0, st>>>(*a);

@@ -93,7 +93,36 @@ def build_tasks(data, spec: JobSpec, candidate_ids: Sequence[int]):
     return tasks, errors
 
 
-def _scores_for(data, task: FitTask, out: FitOutput, scorer: str):
+def _batched_scores(data, tasks, outputs: Dict[int, FitOutput], scorer: str) -> Dict[int, float]:
+    """Accuracy of every device fit in a few launches and ONE device->host read: fits are
+    grouped by split (same held-out rows), their predictions stacked and scored together --
+    instead of one reduction and one host sync per fit (a 2,560-fit LogisticRegression batch
+    spent 0.27 s per search in per-fit syncs).  Exact: a mean of 0/1 counts is the same
+    double whatever the reduction order (so only accuracy is batched here)."""
+    if scorer != "accuracy" or not getattr(data, "is_gpu", False):
+        return {}
+    by_split: Dict[int, List[FitTask]] = {}
+    for t in tasks:
+        o = outputs.get(t.task_id)
+        if o is None or o.error or not isinstance(o.pred, torch.Tensor) or not o.pred.is_cuda:
+            continue
+        by_split.setdefault(t.split, []).append(t)
+    ids, vals = [], []
+    for sp, ts in by_split.items():
+        y = data.test_targets(sp)
+        if y.numel() == 0 or any(outputs[t.task_id].pred.numel() != y.numel() for t in ts):
+            continue
+        P = torch.stack([outputs[t.task_id].pred.reshape(-1) for t in ts])
+        vals.append((P.long() == y.long().view(1, -1)).double().mean(1))
+        ids.extend(t.task_id for t in ts)
+    if not vals:
+        return {}
+    return dict(zip(ids, torch.cat(vals).cpu().tolist()))
+
+
+def _scores_for(data, task: FitTask, out: FitOutput, scorer: str, pre: Optional[Dict[int, float]] = None):
+    if pre is not None and task.task_id in pre:
+        return pre[task.task_id]
     if scorer == "score":
         return float(out.info["score"])
     y = data.test_targets(task.split)
@@ -161,6 +190,8 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
         by_cand.setdefault(t.candidate, []).append(t)
     cv_idx = [i for i, n in enumerate(names) if n.startswith("cv")]
     hold_idx = names.index("holdout") if "holdout" in names else None
+    with trace.range("run_scores"):
+        pre = _batched_scores(data, [t for t in tasks if t.split in cv_idx], outputs, scorer)
     results: List[CandidateResult] = []
     for c in candidate_ids:
         if c in errors and c not in by_cand:
@@ -184,7 +215,7 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
                 cv_scores.append(float(spec.error_score) if spec.error_score is not None else float("nan"))
                 continue
             with trace.range("run_scores"):
-                cv_scores.append(_scores_for(data, t, o, scorer))
+                cv_scores.append(_scores_for(data, t, o, scorer, pre))
             for w in o.info.get("warnings", []):
                 if w not in warnings:
                     warnings.append(w)

@@ -31,7 +31,7 @@ from typing import Any, Dict, List, Tuple
 import numpy as np
 import torch
 
-from ..utils import native
+from ..utils import native, trace
 from .base import Family, FitOutput, FitTask, ParamError, as_bool, as_float, as_int, register, seed_of
 
 KIND_BINARY, KIND_SOFTMAX, KIND_OVR = 0, 1, 2
@@ -199,12 +199,12 @@ class MfmaPlan:
         self.wh = torch.zeros((ops.Kp // 32, self.Mp, 32), dtype=bf, device=dev)  # K-tiled copies
         self.wl = torch.zeros_like(self.wh)
         self.bias = torch.zeros(self.Mp, dtype=torch.float32, device=dev)
-        self.rh = torch.zeros((ops.npad // 32, self.Mp, 32), dtype=bf, device=dev)   # pad columns stay 0
-        self.rl = torch.zeros_like(self.rh)
         self.loss = torch.zeros(b.F, dtype=torch.float64, device=dev)
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         self.lpart = self.col_info = self.col_scale = None
         self.softmax_any = any(kd == KIND_SOFTMAX for kd in b.kind_l)
+        n_tiles = ops.Dp // _TILE
+        p = native.ptr
         if self.v3:
             # per padded column: kind << 28 | split << 16 | positive class (OvR column j: class j),
             # -1 on padding; and the fit's loss scale (k_lr_fwd3's register epilogue)
@@ -220,39 +220,64 @@ class MfmaPlan:
             self.col_info = torch.from_numpy(info.astype(np.int32)).to(dev)
             self.col_scale = torch.from_numpy(cscale).to(dev)
             self.k_uniform = len(set(b.K_l)) == 1
-            # forward: one persistent workgroup per CU (8 per XCD walk their XCD's row tiles);
-            # gradient: 256-row R^T tiles x 128-row X^T tiles x K slices
-            row_tiles = ops.npad // _ROW_TILE
-            rg = max(8, cus // 8 * 8)
-            self.lpart = torch.empty((row_tiles, self.Mp), dtype=torch.float64, device=dev)
-            m_tiles, resident = self.Mp // _ROW_TILE, cus
+            # ROW CHUNKS: the residual R^T exists for one chunk of rows at a time (forward of the
+            # chunk, then the chunk's split-K gradient into its own slabs), so a batch's memory is
+            # R^T of one chunk (<= DML_LR_RT_GB, default 16 GB) instead of 4 bytes per (row, column)
+            # of the whole table -- every fit of a config-4 search fits ONE batch
+            rt_budget = float(os.environ.get("DML_LR_RT_GB", "16")) * 2 ** 30
+            chunk = max(_ROW_TILE, int(rt_budget // (4 * self.Mp)) // _ROW_TILE * _ROW_TILE)
+            chunk = min(chunk, ops.npad)
+            self.n_chunks = -(-ops.npad // chunk)
+            self.rh = torch.zeros((chunk // 32, self.Mp, 32), dtype=bf, device=dev)   # pad columns stay 0
+            self.rl = torch.zeros_like(self.rh)
+            self.lpart = torch.empty((ops.npad // _ROW_TILE, self.Mp), dtype=torch.float64, device=dev)
+            m_tiles = self.Mp // _ROW_TILE
+            tiles = m_tiles * n_tiles
+            S = _roundup(-(-4 * cus // tiles), 8)              # >= ~4 waves of workgroups per chunk
+            Kc = _roundup(-(-chunk // S), 32)
+            S = _roundup(-(-chunk // Kc), 8)
+            self.slabs = torch.empty((self.n_chunks * S, self.Mp, ops.Dp), dtype=torch.float32, device=dev)
+            rg = max(8, cus // 8 * 8)   # forward: one persistent workgroup per CU
+            self.fwd_l, self.grad_l = [], []
+            for ci in range(self.n_chunks):
+                r0 = ci * chunk
+                rows_c = min(chunk, ops.npad - r0)
+                self.fwd_l.append(native.LrFwdArgs(
+                    xh=p(ops.xh), xl=p(ops.xl), xrows=ops.npad, wh=p(self.wh), wl=p(self.wl), n=data.n, Kp=ops.Kp,
+                    row_tiles=rows_c // _ROW_TILE, col_tiles=col_tiles, row_groups=rg, bias=p(self.bias),
+                    col_fit=p(self.col_fit), fit_col0=p(self.fit_col0), fit_k=p(b.K), fit_kind=p(b.kind),
+                    fit_split=p(b.split), scale=p(b.scale), cw=p(b.cw),
+                    cwC=int(b.cw.shape[1]) if b.cw is not None else 0, y=p(data.y_cls), roles=p(data.roles),
+                    rh=p(self.rh), rl=p(self.rl), kr=rows_c, loss=p(self.loss), lpart=p(self.lpart),
+                    col_info=p(self.col_info), col_scale=p(self.col_scale), n_splits=int(data.roles.shape[0]),
+                    softmax_any=int(self.softmax_any), row_base=r0 // _ROW_TILE))
+                self.grad_l.append(native.LrGradArgs(
+                    rh=p(self.rh), rl=p(self.rl), unused=0, xth=p(ops.xth), xtl=p(ops.xtl), m_tiles=m_tiles,
+                    n_tiles=n_tiles, Kp=rows_c, S=S, Kc=Kc, out=p(self.slabs), bk_off=r0, slab0=ci * S))
         else:
+            self.rh = torch.zeros((ops.npad // 32, self.Mp, 32), dtype=bf, device=dev)   # pad columns stay 0
+            self.rl = torch.zeros_like(self.rh)
             # forward: persistent, at most the resident workgroups (2 per CU), row groups % 8 == 0
             row_tiles = ops.npad // _TILE
             resident = 2 * cus
             rg = max(8, (resident // col_tiles) // 8 * 8)
             rg = min(rg, _roundup(row_tiles, 8))
-            m_tiles = col_tiles
-        # gradient: output tiles x K slices >= ~4 waves of workgroups; slices % 8 == 0
-        n_tiles = ops.Dp // _TILE
-        tiles = m_tiles * n_tiles
-        S = _roundup(-(-4 * resident // tiles), 8)
-        Kc = _roundup(-(-ops.npad // S), 32)
-        S = _roundup(-(-ops.npad // Kc), 8)
-        self.slabs = torch.empty((S, self.Mp, ops.Dp), dtype=torch.float32, device=dev)
-        p = native.ptr
-        self.fwd = native.LrFwdArgs(
-            xh=p(ops.xh), xl=p(ops.xl), xrows=ops.npad, wh=p(self.wh), wl=p(self.wl), n=data.n, Kp=ops.Kp,
-            row_tiles=row_tiles, col_tiles=col_tiles, row_groups=rg, bias=p(self.bias), col_fit=p(self.col_fit),
-            fit_col0=p(self.fit_col0), fit_k=p(b.K), fit_kind=p(b.kind), fit_split=p(b.split), scale=p(b.scale),
-            cw=p(b.cw), cwC=int(b.cw.shape[1]) if b.cw is not None else 0, y=p(data.y_cls), roles=p(data.roles),
-            rh=p(self.rh), rl=p(self.rl), kr=ops.npad, loss=p(self.loss), lpart=p(self.lpart),
-            col_info=p(self.col_info), col_scale=p(self.col_scale), n_splits=int(data.roles.shape[0]),
-            softmax_any=int(self.softmax_any))
+            # gradient: output tiles x K slices >= ~4 waves of workgroups; slices % 8 == 0
+            tiles = col_tiles * n_tiles
+            S = _roundup(-(-4 * resident // tiles), 8)
+            Kc = _roundup(-(-ops.npad // S), 32)
+            S = _roundup(-(-ops.npad // Kc), 8)
+            self.slabs = torch.empty((S, self.Mp, ops.Dp), dtype=torch.float32, device=dev)
+            self.fwd = native.LrFwdArgs(
+                xh=p(ops.xh), xl=p(ops.xl), xrows=ops.npad, wh=p(self.wh), wl=p(self.wl), n=data.n, Kp=ops.Kp,
+                row_tiles=row_tiles, col_tiles=col_tiles, row_groups=rg, bias=p(self.bias), col_fit=p(self.col_fit),
+                fit_col0=p(self.fit_col0), fit_k=p(b.K), fit_kind=p(b.kind), fit_split=p(b.split), scale=p(b.scale),
+                cw=p(b.cw), cwC=int(b.cw.shape[1]) if b.cw is not None else 0, y=p(data.y_cls), roles=p(data.roles),
+                rh=p(self.rh), rl=p(self.rl), kr=ops.npad, loss=p(self.loss))
+            self.grad = native.LrGradArgs(
+                rh=p(self.rh), rl=p(self.rl), unused=0, xth=p(ops.xth), xtl=p(ops.xtl), m_tiles=col_tiles,
+                n_tiles=n_tiles, Kp=ops.npad, S=S, Kc=Kc, out=p(self.slabs))
         self.fit_col0_l = self.fit_col0.long()
-        self.grad = native.LrGradArgs(
-            rh=p(self.rh), rl=p(self.rl), unused=0, xth=p(ops.xth), xtl=p(ops.xtl), m_tiles=m_tiles,
-            n_tiles=n_tiles, Kp=ops.npad, S=S, Kc=Kc, out=p(self.slabs))
 
     def objective(self, data, b: "_Batch", W: torch.Tensor):
         """(loss [F] float64, data gradient [d+1, M]) of the unregularised objective."""
@@ -268,10 +293,14 @@ class MfmaPlan:
         self.loss.zero_()
         lib = native.hip_lib()
         st = native.stream_handle(data.device)
-        if self.v3:
-            rc = lib.dml_lr_mfma_fwd3(ctypes.byref(self.fwd), st)
-            if rc == 0:
-                rc = lib.dml_lr_mfma_grad3(ctypes.byref(self.grad), st)
+        if self.v3:   # row chunks in order on one stream: chunk c+1's forward reuses R^T after c's gradient
+            rc = 0
+            for fa, ga in zip(self.fwd_l, self.grad_l):
+                rc = lib.dml_lr_mfma_fwd3(ctypes.byref(fa), st)
+                if rc == 0:
+                    rc = lib.dml_lr_mfma_grad3(ctypes.byref(ga), st)
+                if rc:
+                    break
         else:
             rc = lib.dml_lr_mfma_fwd(ctypes.byref(self.fwd), st)
             if rc == 0:
@@ -674,7 +703,11 @@ class LogisticFamily(Family):
         use_mf = mfma_enabled(data) and not streamed
         if use_mf:   # resident bf16 operands first, so the budget below sees them
             ops = mfma_operands(data)
-            per_col = 4.0 * (ops.npad + (data.d + 1) * (2 * self.history + 10) + 32 * ops.Dp)
+            if lr_v3(native.hip_lib(), len(tasks) * width):
+                # row-chunked objective: R^T of one chunk (DML_LR_RT_GB) is a fixed cost, not per column
+                per_col = 4.0 * ((data.d + 1) * (2 * self.history + 10) + 128 * ops.Dp)
+            else:
+                per_col = 4.0 * (ops.npad + (data.d + 1) * (2 * self.history + 10) + 32 * ops.Dp)
         elif streamed:   # chunk-sized logits / link gradients only
             per_col = 4.0 * (3 * min(data.n, data._chunk_rows) + (data.d + 1) * (2 * self.history + 6))
         else:
@@ -687,14 +720,17 @@ class LogisticFamily(Family):
                 outs.extend(self.run(data, tasks[i:i + cap], keep_models))
             return outs
         t0 = time.perf_counter()
-        b = _Batch(data, tasks)
-        b.streamed = streamed
-        if use_mf:
-            b.mf = MfmaPlan(data, b)
-        W, iters, n_evals = self._solve(data, b)
+        with trace.range("lr_plan"):
+            b = _Batch(data, tasks)
+            b.streamed = streamed
+            if use_mf:
+                b.mf = MfmaPlan(data, b)
+        with trace.range("lr_solve"):
+            W, iters, n_evals = self._solve(data, b)
         b.mf = None   # release R^T / slabs before the prediction GEMMs
         d = data.d
-        Zte = self._test_logits(data, b, W)
+        with trace.range("lr_test_logits"):
+            Zte = self._test_logits(data, b, W)
         iters_h = iters.cpu().tolist()
         self.last_solve_stats["iterations_max"] = max(iters_h, default=0)
         outs = []

@@ -27,16 +27,22 @@ b.mf.objective(dd, b, W)
 lib = native.hip_lib()
 st = native.stream_handle(dev)
 out = {"lib": os.path.basename(os.environ.get("DML_HIP_LIB", "default")), "v3": bool(b.mf.v3), "Mp": b.mf.Mp}
-fwd_fn = lib.dml_lr_mfma_fwd3 if b.mf.v3 else lib.dml_lr_mfma_fwd
-grad_fn = lib.dml_lr_mfma_grad3 if b.mf.v3 else lib.dml_lr_mfma_grad
-for name, fn, args in (("fwd", fwd_fn, b.mf.fwd), ("grad", grad_fn, b.mf.grad)):
-    rc = fn(ctypes.byref(args), st)
-    assert rc == 0, (name, rc)
+if b.mf.v3:   # row chunks: (forward, gradient) launches per chunk
+    calls = {"fwd": [(lib.dml_lr_mfma_fwd3, a) for a in b.mf.fwd_l],
+             "grad": [(lib.dml_lr_mfma_grad3, a) for a in b.mf.grad_l]}
+    out["chunks"] = b.mf.n_chunks
+else:
+    calls = {"fwd": [(lib.dml_lr_mfma_fwd, b.mf.fwd)], "grad": [(lib.dml_lr_mfma_grad, b.mf.grad)]}
+for name, lst in calls.items():
+    for fn, args in lst:
+        rc = fn(ctypes.byref(args), st)
+        assert rc == 0, (name, rc)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(5):
-        fn(ctypes.byref(args), st)
+        for fn, args in lst:
+            fn(ctypes.byref(args), st)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 5

@@ -144,11 +144,16 @@ def _lr_batch(dd, specs):
     return fam, linear._Batch(dd, tasks)
 
 
-@pytest.mark.parametrize("C_cls,n,d,fits", [(2, 3001, 70, 40), (3, 2500, 45, 40), (4, 700, 300, 40),
-                                            (2, 5003, 130, 300), (3, 2100, 64, 130)])
-def test_lr_mfma_objective_matches_fp32(C_cls, n, d, fits):
+@pytest.mark.parametrize("C_cls,n,d,fits,rt_gb", [(2, 3001, 70, 40, None), (3, 2500, 45, 40, None),
+                                                  (4, 700, 300, 40, None), (2, 5003, 130, 300, None),
+                                                  (3, 2100, 64, 130, None), (2, 5003, 130, 300, "0.004"),
+                                                  (3, 2100, 64, 130, "0.002")])
+def test_lr_mfma_objective_matches_fp32(C_cls, n, d, fits, rt_gb, monkeypatch):
     """Matrix-core (bf16x3) objective vs the fp32 GEMM + link-kernel path: loss and gradient.
-    Batches of more than 256 columns run the 3-stage 256 x 128 kernels (k_lr_fwd3 / k_lr_grad3)."""
+    Batches of more than 256 columns run the 3-stage 256 x 128 kernels (k_lr_fwd3 / k_lr_grad3);
+    ``rt_gb`` caps the residual buffer so the objective runs over several row chunks."""
+    if rt_gb is not None:
+        monkeypatch.setenv("DML_LR_RT_GB", rt_gb)
     from cs230_distributed_machine_learning_amd.models import linear
 
     rng = np.random.RandomState(C_cls * 7 + d)
@@ -167,6 +172,8 @@ def test_lr_mfma_objective_matches_fp32(C_cls, n, d, fits):
     f0, G0 = fam._objective(dd, b, W)
     b.mf = linear.MfmaPlan(dd, b)
     assert b.mf.v3 == (b.M > 256)
+    if rt_gb is not None:
+        assert b.mf.n_chunks > 1
     f1, G1 = fam._objective(dd, b, W)
     torch.cuda.synchronize()
     torch.testing.assert_close(f1, f0, rtol=2e-5, atol=1e-6)
