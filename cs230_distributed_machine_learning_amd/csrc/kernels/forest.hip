@@ -56,6 +56,9 @@
 #ifndef DML_PART_U2
 #define DML_PART_U2 4          // block-tier partition pass 2: row positions per thread per round
 #endif
+#ifndef DML_PART_KEEP
+#define DML_PART_KEEP 2        // block-tier partition: rounds whose row ids pass 1 keeps in registers (0/1/2: 1.018/1.014/1.009 s sweep build, r5 e6)
+#endif
 #ifndef DML_NODES_WPE_WAVE
 #define DML_NODES_WPE_WAVE 4   // wave tier (binary): 2 / 3 / 5 / 6 measured slower (ROUND3.md)
 #endif
@@ -1664,17 +1667,30 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
     const int bjs = __builtin_amdgcn_readfirstlane((sc->best_pos < sc->scr_n) ? sc->best_pos : -1);
     const int fsplit = __builtin_amdgcn_readfirstlane(feat), bsplit = __builtin_amdgcn_readfirstlane(bin);
     constexpr int U = 4;   // positions per thread per round, all loads issued before the ballots
-    for (int p0 = 0; p0 < cnt; p0 += U * NT) {
+    // the row ids of the first KR rounds are loaded WITH the split bins and kept in registers
+    // for pass 2 (which then issues no loads for them): one memory round trip less per round
+    // for nodes of <= KR * U * NT rows (most block-tier nodes)
+    constexpr int KR = DML_PART_KEEP;
+    static_assert(DML_PART_U2 == U, "pass 2 walks the positions of pass 1");
+    uint32_t rk[KR > 0 ? KR : 1][U];
+#pragma unroll
+    for (int q = 0; q < (KR > 0 ? KR : 1); ++q)
+#pragma unroll
+      for (int u = 0; u < U; ++u) rk[q][u] = 0u;
+    for (int p0 = 0, q = 0; p0 < cnt; p0 += U * NT, ++q) {
       uint32_t bv[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int p = min(p0 + u * NT + tid, cnt - 1);
+        const uint32_t r = (KR > 0 || bjs < 0) ? rows[p] : 0u;
         if (bjs >= 0) {
           bv[u] = c.bscr[(on.start + p) * 16 + bjs];
         } else {
-          const uint32_t r = rows[p];
           bv[u] = c.Xb[(int64_t)(r & c.rmask) * c.ld + fsplit];
         }
+#pragma unroll
+        for (int qq = 0; qq < KR; ++qq)
+          if (qq == q) rk[qq][u] = r;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1702,10 +1718,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
     // (unconditionally, clamped) before its stores, so consecutive rounds do not each wait a
     // full memory round trip behind the previous round's store
     constexpr int U2 = DML_PART_U2;
-    for (int p0 = tid; p0 < cnt; p0 += U2 * NT) {
+    for (int p0 = tid, q = 0; p0 < cnt; p0 += U2 * NT, ++q) {
       uint32_t rr[U2];
+      if (q < KR) {   // kept from pass 1 (uniform branch: q is the round index)
 #pragma unroll
-      for (int u = 0; u < U2; ++u) rr[u] = rows[min(p0 + u * NT, cnt - 1)];
+        for (int qq = 0; qq < KR; ++qq)
+          if (qq == q)
+#pragma unroll
+            for (int u = 0; u < U2; ++u) rr[u] = rk[qq][u];
+      } else {
+#pragma unroll
+        for (int u = 0; u < U2; ++u) rr[u] = rows[min(p0 + u * NT, cnt - 1)];
+      }
 #pragma unroll
       for (int u = 0; u < U2; ++u) {
         const int p = p0 + u * NT;

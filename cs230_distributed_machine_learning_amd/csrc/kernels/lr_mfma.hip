@@ -645,6 +645,10 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
     if (!softmax) {
       // ---- register epilogue: every column is an independent sigmoid (binary / OvR)
       float lsum[4] = {0.f, 0.f, 0.f, 0.f};
+      // the lane's 4 x 4 rows: labels as one 16-B LDS read per row quad (not one per element)
+      int4 yq[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) yq[i] = *reinterpret_cast<const int4*>(eps_y + wm * 64 + i * 16 + (lane >> 4) * 4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int ci = cinfo[j];
@@ -656,12 +660,15 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int lr0 = wm * 64 + i * 16 + (lane >> 4) * 4;
+          // the quad's 4 role bytes in one 4-B LDS read (staged rows; else per element)
+          const uint32_t rq4 = stage_roles ? *reinterpret_cast<const uint32_t*>(eps_r + sp * TM + lr0) : 0u;
           float r[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int lrow = lr0 + e;
-            const int yv = eps_y[lrow];
-            const bool tr = row0 + lrow < a.n && role_at(sp, lrow) == 1;
+            const int yv = e == 0 ? yq[i].x : e == 1 ? yq[i].y : e == 2 ? yq[i].z : yq[i].w;
+            const int rl = stage_roles ? (int)((rq4 >> (8 * e)) & 0xFFu) : role_at(sp, lrow);
+            const bool tr = row0 + lrow < a.n && rl == 1;
             const float sc = tr ? (cwt ? cscale[j] * cwt[(int64_t)cfit[j] * a.cwC + yv] : cscale[j]) : 0.f;
             const float z = acc[i][j][e] + cbias[j];
             const bool pos = kind == 0 ? yv == 1 : yv == tgt;
