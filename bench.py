@@ -340,6 +340,7 @@ def run_lr(args) -> int:
         from cs230_distributed_machine_learning_amd.utils import trace
 
         print("phases:", json.dumps(trace.summary()), file=sys.stderr, flush=True)
+        print("solve:", json.dumps(stats), file=sys.stderr, flush=True)
         line = {
             "metric": "CV-fits/sec (whole node), RandomizedSearchCV LogisticRegression n_iter=512 cv=5 on 10M×1000",
             "value": round(value, 4), "unit": "CV-fits/s", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,

@@ -71,6 +71,10 @@ struct FwdArgs {
   int64_t n_splits;              // v3: role rows of `roles`
   int64_t softmax_any;           // v3: 1 if any fit is multinomial (Z tile through LDS)
   int64_t row_base;              // v3 row chunks: first (256-row) tile of the chunk; R^T rows are local
+  int64_t live;                  // v3 (nullable): int32 [1 + col_tiles] = n_live, then the column tiles
+                                 // holding a still-active fit (the others are skipped: their R^T and
+                                 // loss partials keep stale values the solver never reads)
+  int64_t w_zero;                // v3: 1 if every weight is 0 (logits = bias; the GEMM is skipped)
 };
 
 struct GradArgs {
@@ -81,6 +85,7 @@ struct GradArgs {
   int64_t out;                   // float [S x m_tiles*BM x n_tiles*BN] partial G^T slabs
   int64_t bk_off;                // v3 row chunks: the chunk's first data row (B = X^T's k offset)
   int64_t slab0;                 // v3 row chunks: first output slab of this chunk
+  int64_t mlive;                 // v3 (nullable): int32 per m tile, 0 = no active fit (workgroups exit)
 };
 
 struct Operands {
@@ -580,7 +585,9 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
   // row tiles of this launch: [row_base, row_base + row_tiles) of X; R^T (and its K-tiled
   // layout) covers only the launch's rows (local row index = global - row_base * TM)
   const int64_t rt_here = a.row_tiles > xcd ? (a.row_tiles - xcd + 7) / 8 : 0;
-  const int64_t items = rt_here * a.col_tiles;
+  const auto live = a.live ? GPTR(const int32_t, a.live) : nullptr;
+  const int64_t n_ct = live ? __builtin_amdgcn_readfirstlane(live[0]) : a.col_tiles;   // live column tiles
+  const int64_t items = rt_here * n_ct;
   const int64_t rbase = a.row_base * TM;
   const auto col_fit = GPTR(const int32_t, a.col_fit);
   const auto bias = GPTR(const float, a.bias);
@@ -597,10 +604,12 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
   const bool softmax = a.softmax_any != 0;
   const int S = (int)a.n_splits;
   const bool stage_roles = S <= V3_ROLE_ROWS;
+  const bool w_zero = a.w_zero != 0;
   const int nchunk = stage_roles ? S * (TM / 4) : 0;   // 4-row role chunks of the item (<= NT)
   static_assert(V3_ROLE_ROWS * (TM / 4) <= NT, "one role chunk per thread");
   for (int64_t it = slot; it < items; it += slots) {
-    const int64_t rtl = xcd + 8 * (it / a.col_tiles), ct = it % a.col_tiles;
+    const int64_t rtl = xcd + 8 * (it / n_ct);
+    const int64_t ct = live ? __builtin_amdgcn_readfirstlane(live[1 + it % n_ct]) : it % n_ct;
     const int64_t rt = a.row_base + rtl;               // global row tile
     const int64_t row0 = rt * TM, col0 = ct * TN;
     // ---- item prologue: epilogue operands in flight under the GEMM.  Every load is
@@ -626,7 +635,14 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
       cfit[j] = col_fit[gc];
     }
     f32x4 acc[4][4];
-    v3_gemm(op, row0, col0, 0, a.Kp, smem, acc, tid);
+    if (w_zero) {   // W = 0 (the solver's first evaluation): Z = bias, no GEMM
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
+      v3_gemm(op, row0, col0, 0, a.Kp, smem, acc, tid);
+    }
     if (tid < TM) eps_y[tid] = row0 + tid < a.n ? ypre : 0;
     if (tid < nchunk) {   // rows past n read as role 0 (held out)
       const int r4 = (tid % (TM / 4)) * 4;
@@ -807,6 +823,7 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_grad3(GradArgs a) {
   const int64_t s = (local / tiles) * 8 + xcd;
   if (s >= a.S) return;   // workgroup-uniform, before any barrier
   const int64_t mt = tile / a.n_tiles, nt = tile % a.n_tiles;
+  if (a.mlive && GPTR(const int32_t, a.mlive)[mt] == 0) return;   // every fit of the m tile has stopped
   const int64_t kb = s * a.Kc;
   const int64_t ke = kb + a.Kc < a.Kp ? kb + a.Kc : a.Kp;
   const Operands op{reinterpret_cast<const uint16_t*>(a.rh), reinterpret_cast<const uint16_t*>(a.rl),

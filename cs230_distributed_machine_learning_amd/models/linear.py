@@ -26,7 +26,7 @@ import ctypes
 import math
 import os
 import time
-from typing import Any, Dict, List, Tuple
+from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -177,12 +177,18 @@ class MfmaPlan:
             raise RuntimeError("lr_mfma tile mismatch")
         self.ops = ops = mfma_operands(data)
         dev = data.device
-        # padded column layout: no fit's column group straddles a 128-column tile
-        pcol0, m = [], 0
-        for k in b.K_l:
+        # padded column layout: no fit's column group straddles a 128-column tile.  Fits are
+        # laid out by (objective, C): fits that stop at similar iterations share column tiles,
+        # so the tiles of stopped fits empty out and the kernels skip them (``live`` below)
+        def _order_key(f):
+            rp = b.tasks[f].params
+            return (bool(rp.get("penalize_intercept")), float("inf") if rp.get("C") is None else float(rp["C"]))
+        pcol0, m = [0] * len(b.K_l), 0
+        for f in sorted(range(len(b.K_l)), key=_order_key):
+            k = b.K_l[f]
             if (m % _TILE) + k > _TILE:
                 m = _roundup(m, _TILE)
-            pcol0.append(m)
+            pcol0[f] = m
             m += k
         self.v3 = lr_v3(lib, m)
         if self.v3 and lib.dml_lr_v3_row_tile() != _ROW_TILE:
@@ -233,6 +239,12 @@ class MfmaPlan:
             self.lpart = torch.empty((ops.npad // _ROW_TILE, self.Mp), dtype=torch.float64, device=dev)
             m_tiles = self.Mp // _ROW_TILE
             tiles = m_tiles * n_tiles
+            # column tiles still holding an active fit: [n_live, tile ids...] (forward) and one
+            # flag per 256-column gradient tile; set on the device each evaluation (no host sync)
+            self.live = torch.cat([torch.tensor([col_tiles], dtype=torch.int32),
+                                   torch.arange(col_tiles, dtype=torch.int32)]).to(dev)
+            self.mlive = torch.ones(m_tiles, dtype=torch.int32, device=dev)
+            self.skip_done = os.environ.get("DML_LR_SKIP_DONE", "1") != "0"
             S = _roundup(-(-4 * cus // tiles), 8)              # >= ~4 waves of workgroups per chunk
             Kc = _roundup(-(-chunk // S), 32)
             S = _roundup(-(-chunk // Kc), 8)
@@ -250,10 +262,11 @@ class MfmaPlan:
                     cwC=int(b.cw.shape[1]) if b.cw is not None else 0, y=p(data.y_cls), roles=p(data.roles),
                     rh=p(self.rh), rl=p(self.rl), kr=rows_c, loss=p(self.loss), lpart=p(self.lpart),
                     col_info=p(self.col_info), col_scale=p(self.col_scale), n_splits=int(data.roles.shape[0]),
-                    softmax_any=int(self.softmax_any), row_base=r0 // _ROW_TILE))
+                    softmax_any=int(self.softmax_any), row_base=r0 // _ROW_TILE, live=p(self.live)))
                 self.grad_l.append(native.LrGradArgs(
                     rh=p(self.rh), rl=p(self.rl), unused=0, xth=p(ops.xth), xtl=p(ops.xtl), m_tiles=m_tiles,
-                    n_tiles=n_tiles, Kp=rows_c, S=S, Kc=Kc, out=p(self.slabs), bk_off=r0, slab0=ci * S))
+                    n_tiles=n_tiles, Kp=rows_c, S=S, Kc=Kc, out=p(self.slabs), bk_off=r0, slab0=ci * S,
+                    mlive=p(self.mlive)))
         else:
             self.rh = torch.zeros((ops.npad // 32, self.Mp, 32), dtype=bf, device=dev)   # pad columns stay 0
             self.rl = torch.zeros_like(self.rh)
@@ -279,9 +292,34 @@ class MfmaPlan:
                 n_tiles=n_tiles, Kp=ops.npad, S=S, Kc=Kc, out=p(self.slabs))
         self.fit_col0_l = self.fit_col0.long()
 
-    def objective(self, data, b: "_Batch", W: torch.Tensor):
-        """(loss [F] float64, data gradient [d+1, M]) of the unregularised objective."""
+    def set_active(self, b: "_Batch", active: Optional[torch.Tensor]):
+        """Mark the column tiles whose fits have all stopped (v3 kernels skip them; the
+        solver only reads the loss / gradient of active fits)."""
+        if not self.v3:
+            return
+        col_tiles = self.Mp // _TILE
+        if active is None or not self.skip_done:
+            self.live[0] = col_tiles
+            self.live[1:] = torch.arange(col_tiles, dtype=torch.int32, device=self.live.device)
+            self.mlive.fill_(1)
+            return
+        colact = torch.zeros(self.Mp, dtype=torch.bool, device=active.device)
+        colact[self.colmap] = active[b.col_fit]
+        tl = colact.view(col_tiles, _TILE).any(1)
+        self.live[0] = tl.sum().to(torch.int32)
+        self.live[1:] = torch.argsort((~tl).to(torch.int32), stable=True).to(torch.int32)   # live tiles first
+        self.mlive.copy_(tl.view(-1, _ROW_TILE // _TILE).any(1).to(torch.int32))
+
+    def objective(self, data, b: "_Batch", W: torch.Tensor, active: Optional[torch.Tensor] = None,
+                  w_zero: bool = False):
+        """(loss [F] float64, data gradient [d+1, M]) of the unregularised objective; with
+        ``active``, entries of stopped fits may be stale.  ``w_zero``: the caller knows W == 0
+        (the solver's start), so the forward GEMM is skipped (exactly: its result is 0)."""
         d = data.d
+        self.set_active(b, active)
+        if self.v3:
+            for fa in self.fwd_l:
+                fa.w_zero = int(w_zero)
         Wt = W[:d].t()
         hi = Wt.to(torch.bfloat16)
         self.w_lin[0, self.colmap, :d] = hi
@@ -454,12 +492,13 @@ class LogisticFamily(Family):
         return max(1, rp["max_iter"]) * n_train * (n_features + 1) * max(1, n_classes - 1) * 4e-12 + 1e-3
 
     # --------------------------------------------------------------------------------
-    def _objective(self, data, b: _Batch, W: torch.Tensor):
+    def _objective(self, data, b: _Batch, W: torch.Tensor, active: Optional[torch.Tensor] = None,
+                   w_zero: bool = False):
         d = data.d
         if getattr(b, "streamed", False):
             return self._objective_streamed(data, b, W)
         if b.mf is not None:   # matrix cores: fused forward + split-K gradient (lr_mfma.hip)
-            loss, G = b.mf.objective(data, b, W)
+            loss, G = b.mf.objective(data, b, W, active, w_zero)
             loss, G = _dp_sum(data, loss), _dp_sum(data, G)
             reg = W * b.lam_col
             reg[d] = reg[d] * b.pen_icpt_col
@@ -544,7 +583,7 @@ class LogisticFamily(Family):
         H, Fn = self.history, b.F
         col = b.col_fit
         W = torch.zeros((d + 1, b.M), dtype=torch.float32, device=dev)
-        f, G = self._objective(data, b, W)
+        f, G = self._objective(data, b, W, w_zero=True)
         l1 = None
         if b.has_l1:
             l1 = b.l1_col.view(1, -1).repeat(d + 1, 1)
@@ -628,8 +667,10 @@ class LogisticFamily(Family):
         else:
             running = False
         max_steps = max_it * 31
+        act_hist = []   # active fits per step (device scalars, read once at the end)
         while running and steps < max_steps:
-            ft, Gt = self._objective(data, b, Wt)
+            act_hist.append(active.sum())
+            ft, Gt = self._objective(data, b, Wt, active)
             Ft = total(ft, Wt)
             n_evals += 1
             steps += 1
@@ -674,7 +715,8 @@ class LogisticFamily(Family):
             if steps % sync_every == 0:
                 host_syncs += 1
                 running = bool(active.any())
-        self.last_solve_stats = {"host_syncs": host_syncs, "steps": steps, "sync_every": sync_every}
+        self.last_solve_stats = {"host_syncs": host_syncs, "steps": steps, "sync_every": sync_every,
+                                 "active_per_step": torch.stack(act_hist).tolist() if act_hist else []}
         return W, iters, n_evals
 
     def run(self, data, tasks: List[FitTask], keep_models: bool = False) -> List[FitOutput]:
@@ -733,6 +775,9 @@ class LogisticFamily(Family):
             Zte = self._test_logits(data, b, W)
         iters_h = iters.cpu().tolist()
         self.last_solve_stats["iterations_max"] = max(iters_h, default=0)
+        self.last_solve_stats["iterations_hist"] = {int(k): int(v) for k, v in
+                                                    zip(*np.unique(np.asarray(iters_h, dtype=np.int64), return_counts=True))}
+        self.last_solve_stats["evals"] = int(n_evals)
         outs = []
         # binary fits: every fit of a split predicted by ONE threshold over the split's logit
         # block (not a handful of launches per fit -- 2,560 fits spent ~0.3 s in them);

@@ -91,7 +91,7 @@ LrFwdArgs = _i64_struct(
     "LrFwdArgs",
     ["xh", "xl", "xrows", "wh", "wl", "n", "Kp", "row_tiles", "col_tiles", "row_groups", "bias", "col_fit",
      "fit_col0", "fit_k", "fit_kind", "fit_split", "scale", "cw", "cwC", "y", "roles", "rh", "rl", "kr", "loss",
-     "lpart", "col_info", "col_scale", "n_splits", "softmax_any", "row_base"],
+     "lpart", "col_info", "col_scale", "n_splits", "softmax_any", "row_base", "live", "w_zero"],
 )
 # csrc/kernels/gbrt.hip argument blocks (fused gradient-boosting stage kernels)
 GbStageArgs = _i64_struct(
@@ -108,7 +108,7 @@ MaeArgs = _i64_struct(
      "n_nodes_out", "levels_out", "status_out", "big_a", "big_b", "big_cap", "res", "P", "big_rows"],
 )
 LrGradArgs = _i64_struct("LrGradArgs", ["rh", "rl", "unused", "xth", "xtl", "m_tiles", "n_tiles", "Kp", "S", "Kc", "out",
-                                        "bk_off", "slab0"])
+                                        "bk_off", "slab0", "mlive"])
 
 
 def _load(path: str) -> ctypes.CDLL:

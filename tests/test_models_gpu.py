@@ -181,6 +181,45 @@ def test_lr_mfma_objective_matches_fp32(C_cls, n, d, fits, rt_gb, monkeypatch):
     assert float(((G1 - G0).abs() / scale).max()) < 2e-4
 
 
+@pytest.mark.parametrize("rt_gb", [None, "0.004"])
+def test_lr_mfma_skips_tiles_of_stopped_fits(rt_gb, monkeypatch):
+    """With an ``active`` mask the v3 kernels skip column tiles whose fits all stopped; the
+    loss and gradient of every active fit are bit-identical to the full evaluation."""
+    if rt_gb is not None:
+        monkeypatch.setenv("DML_LR_RT_GB", rt_gb)
+    from cs230_distributed_machine_learning_amd.models import linear
+
+    rng = np.random.RandomState(11)
+    n, d = 5003, 130
+    X = (rng.randn(n, d) * rng.uniform(0.1, 3.0, d)).astype(np.float32)
+    y = rng.randint(0, 2, n)
+    dd = _dd(X, y, True, "cuda:0")
+    S = len(dd.split_names)
+    Cs = 10.0 ** rng.uniform(-2, 2, 300)
+    specs = [({"C": float(c), "solver": ["lbfgs", "liblinear"][i % 2]}, i % S) for i, c in enumerate(Cs)]
+    fam, b = _lr_batch(dd, specs)
+    b.mf = linear.MfmaPlan(dd, b)
+    assert b.mf.v3
+    W = torch.randn((d + 1, b.M), device="cuda:0") * 0.05
+    f_all, G_all = fam._objective(dd, b, W)
+    # stopped: every liblinear fit and the lbfgs fits of small C -> whole column tiles go idle
+    act = torch.tensor([(i % 2 == 0) and c > 1.0 for i, c in enumerate(Cs)], device="cuda:0")
+    f_act, G_act = fam._objective(dd, b, W, act)
+    torch.cuda.synchronize()
+    col_tiles = b.mf.Mp // linear._TILE
+    assert 0 < int(b.mf.live[0]) < col_tiles
+    assert torch.equal(f_act[act], f_all[act])
+    cols = act[b.col_fit]
+    assert torch.equal(G_act[:, cols], G_all[:, cols])
+    f_again, G_again = fam._objective(dd, b, W)          # no mask: every tile again
+    assert torch.equal(f_again, f_all) and torch.equal(G_again, G_all)
+    # the solver's first evaluation (W = 0) skips the forward GEMM: same result
+    W0 = torch.zeros_like(W)
+    f0, G0 = fam._objective(dd, b, W0)
+    f0z, G0z = fam._objective(dd, b, W0, w_zero=True)
+    assert torch.equal(f0z, f0) and torch.equal(G0z, G0)
+
+
 def test_lr_mfma_fits_match_fp32_path(monkeypatch):
     """Whole batched L-BFGS solves on the matrix cores reach the fp32 path's CV scores."""
     rng = np.random.RandomState(5)
@@ -195,6 +234,23 @@ def test_lr_mfma_fits_match_fp32_path(monkeypatch):
         assert all(r.ok for r in res), [r.error for r in res]
         out[flag] = np.array([r.result["mean_cv_score"] for r in res])
     np.testing.assert_allclose(out["1"], out["0"], atol=1e-3)
+
+
+def test_lr_solve_skipping_stopped_fits_is_exact(monkeypatch):
+    """A v3 batch (> 256 columns) solved with and without skipping stopped fits' tiles:
+    identical fits (the skip only drops work whose results the solver never reads)."""
+    rng = np.random.RandomState(8)
+    X = rng.randn(20000, 40).astype(np.float32)
+    y = (X @ rng.randn(40) + 2 * rng.randn(20000) > 0).astype(int)
+    grid = [{"C": float(c), "solver": s} for c in 10.0 ** np.linspace(-3, 2, 30) for s in ("lbfgs", "liblinear")]
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("DML_LR_SKIP_DONE", flag)
+        dd = DeviceData(X, y, True, "cuda:0")
+        res = run_candidates(dd, JobSpec("LogisticRegression", grid, cv=5), range(len(grid)))
+        assert all(r.ok for r in res), [r.error for r in res]
+        out[flag] = np.array([r.result["mean_cv_score"] for r in res])
+    np.testing.assert_array_equal(out["1"], out["0"])
 
 
 def test_lr_gpu_grid_matches_cpu():
