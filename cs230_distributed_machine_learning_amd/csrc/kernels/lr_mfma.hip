@@ -44,6 +44,9 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #ifndef LRM_PASSES
 #define LRM_PASSES 3   // A/B instrumentation: 1 = hi*hi only, 0 = no MFMA (never in production)
 #endif
+#ifndef LRM_EPI_PROBE
+#define LRM_EPI_PROBE 0   // A/B instrumentation: 1 = fwd3 epilogue without the link math (never in production)
+#endif
 
 constexpr int BM = 128, BN = 128, BK = 32;
 constexpr int THREADS = 256;
@@ -688,12 +691,17 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
             const float sc = tr ? (cwt ? cscale[j] * cwt[(int64_t)cfit[j] * a.cwC + yv] : cscale[j]) : 0.f;
             const float z = acc[i][j][e] + cbias[j];
             const bool pos = kind == 0 ? yv == 1 : yv == tgt;
+#if LRM_EPI_PROBE   // timing probe only (wrong results): the link math replaced by one multiply
+            lsum[j] += sc * z;
+            r[e] = (z - (pos ? 1.f : 0.f)) * sc;
+#else
             const float ex = __expf(-fabsf(z));                    // one exp, one log, one rcp
             const float inv = __builtin_amdgcn_rcpf(1.f + ex);
             const float p = z >= 0.f ? inv : ex * inv;
             const float t = pos ? -z : z;
             lsum[j] += sc * (fmaxf(t, 0.f) + __logf(1.f + ex));
             r[e] = (p - (pos ? 1.f : 0.f)) * sc;
+#endif
           }
           u32x2 hv, lv;
           {

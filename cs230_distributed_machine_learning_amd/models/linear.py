@@ -291,6 +291,7 @@ class MfmaPlan:
                 rh=p(self.rh), rl=p(self.rl), unused=0, xth=p(ops.xth), xtl=p(ops.xtl), m_tiles=col_tiles,
                 n_tiles=n_tiles, Kp=ops.npad, S=S, Kc=Kc, out=p(self.slabs))
         self.fit_col0_l = self.fit_col0.long()
+        self.zero_groups = _zero_groups(data, b)   # the solver's W = 0 start (LogisticFamily._objective_at_zero)
 
     def set_active(self, b: "_Batch", active: Optional[torch.Tensor]):
         """Mark the column tiles whose fits have all stopped (v3 kernels skip them; the
@@ -360,6 +361,32 @@ class MfmaPlan:
         return self.loss.clone(), G
 
 
+def _zero_groups(data, b: "_Batch"):
+    """At W = 0 every logit is 0, so fits with the same (split, link, classes, loss scale,
+    class weights) have IDENTICAL residual columns.  Returns (sub-batch of one representative
+    per group, source column of every batch column, representative of every fit), or None
+    when there are too few duplicates to pay (or no resident fp32 rows).  Host-side keys
+    only; built with the plan, so the solve itself stays free of host syncs."""
+    if os.environ.get("DML_LR_ZERO_DEDUP", "1") == "0" or getattr(b, "streamed", False) or \
+            getattr(data, "X", None) is None:
+        return None
+    groups: Dict[tuple, int] = {}
+    rep = []
+    for f in range(b.F):
+        key = (b.split_l[f], b.kind_l[f], b.K_l[f], b.scale_l[f], repr(b.tasks[f].params.get("class_weight")))
+        rep.append(groups.setdefault(key, len(groups)))
+    if len(groups) * 4 > b.F:
+        return None
+    reps = [0] * len(groups)
+    for f in reversed(range(b.F)):
+        reps[rep[f]] = f
+    sub = _Batch(data, [b.tasks[f] for f in reps])
+    dev = data.device
+    src = torch.tensor([sub.col0_l[rep[f]] + j for f in range(b.F) for j in range(b.K_l[f])],
+                       dtype=torch.long, device=dev)
+    return sub, src, torch.tensor(rep, dtype=torch.long, device=dev)
+
+
 class _Batch:
     """Column layout of a batch of logistic fits."""
 
@@ -399,6 +426,7 @@ class _Batch:
         i32 = lambda v: torch.tensor(v, dtype=torch.int32, device=dev)
         self.col0_l, self.K_l, self.kind_l, self.split_l = col0, K, kind, split
         self.col0, self.K, self.kind, self.split = i32(col0), i32(K), i32(kind), i32(split)
+        self.scale_l = scale
         self.scale = torch.tensor(scale, dtype=torch.float32, device=dev)
         self.col_fit = torch.repeat_interleave(torch.arange(self.F, device=dev), torch.tensor(K, device=dev))
         lam_t = torch.tensor(lam, dtype=torch.float32, device=dev)
@@ -566,6 +594,24 @@ class LogisticFamily(Family):
         G += reg
         return loss + 0.5 * b.segsum((W * reg).sum(0)).double(), G
 
+    def _objective_at_zero(self, data, b: _Batch):
+        """The objective at the solver's start W = 0 from one representative fit per residual
+        group (``_zero_groups``; a config-4 search has 5 groups for 2,560 fits): one fp32 GEMM
+        of X^T against a handful of columns, the group's loss / gradient columns copied to its
+        fits.  None when grouping does not pay."""
+        zg = b.mf.zero_groups if b.mf is not None else _zero_groups(data, b)
+        if zg is None:
+            return None
+        sub, src, rep_t = zg
+        d, dev = data.d, data.device
+        Z = torch.zeros((data.X.shape[0], sub.M), dtype=torch.float32, device=dev)
+        R, loss_s = self._link_grad(data, sub, Z, data.y_cls, data.roles)
+        GTs = data.X.t() @ R
+        G = torch.empty((d + 1, b.M), dtype=torch.float32, device=dev)
+        G[:d] = GTs[:, src]
+        G[d] = R.sum(0)[src] * b.icpt_col
+        return _dp_sum(data, loss_s[rep_t]), _dp_sum(data, G)      # the penalty is 0 at W = 0
+
     def _solve(self, data, b: _Batch):
         """Batched L-BFGS that stays on the device; columns with an L1 term use OWL-QN
         (Andrew & Gao 2007): pseudo-gradient, orthant-constrained direction and line
@@ -583,7 +629,8 @@ class LogisticFamily(Family):
         H, Fn = self.history, b.F
         col = b.col_fit
         W = torch.zeros((d + 1, b.M), dtype=torch.float32, device=dev)
-        f, G = self._objective(data, b, W, w_zero=True)
+        start = self._objective_at_zero(data, b) if b.mf is not None else None
+        f, G = start if start is not None else self._objective(data, b, W, w_zero=True)
         l1 = None
         if b.has_l1:
             l1 = b.l1_col.view(1, -1).repeat(d + 1, 1)
@@ -715,7 +762,7 @@ class LogisticFamily(Family):
             if steps % sync_every == 0:
                 host_syncs += 1
                 running = bool(active.any())
-        self.last_solve_stats = {"host_syncs": host_syncs, "steps": steps, "sync_every": sync_every,
+        self.last_solve_stats = {"host_syncs": host_syncs + bool(act_hist), "steps": steps, "sync_every": sync_every,
                                  "active_per_step": torch.stack(act_hist).tolist() if act_hist else []}
         return W, iters, n_evals
 

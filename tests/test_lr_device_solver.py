@@ -90,3 +90,29 @@ def test_device_lbfgs_sync_count_hook_gpu():
     assert it >= 10
     assert syncs <= it, (syncs, it, fam.last_solve_stats)     # every synchronising call, counted by torch
     assert syncs <= fam.last_solve_stats["host_syncs"] + 1
+
+
+@pytest.mark.parametrize("n_classes", [2, 3])
+def test_objective_at_zero_shares_group_residuals(n_classes):
+    """At W = 0 every logit is 0, so fits of one (split, link, scale, class weights) group
+    share their residual columns: the grouped start equals the full objective."""
+    X, y = make_classification(600, 12, n_informative=6, n_classes=n_classes, random_state=4)
+    dd = DeviceData(X.astype(np.float32), y, True, "cpu")
+    roles, names = make_split_roles(y, 5, True, holdout=False)
+    dd.set_splits(roles, names)
+    fam = linear.LogisticFamily()
+    grid = [{"C": c, "solver": s} for c in (0.01, 0.1, 0.3, 1.0, 3.0, 10.0) for s in ("lbfgs", "liblinear")]
+    grid += [{"C": 1.0, "class_weight": "balanced"}, {"C": 2.0, "fit_intercept": False}]
+    tasks = []
+    for i, p in enumerate(grid):
+        for sp in range(len(names)):
+            rp = fam.resolve("LogisticRegression", p, dd.n, dd.d, dd.n_classes)
+            tasks.append(FitTask(task_id=len(tasks), candidate=i, split=sp, model_type="LogisticRegression", params=rp))
+    b = linear._Batch(dd, tasks)
+    W = torch.zeros((dd.d + 1, b.M))
+    f_ref, G_ref = fam._objective(dd, b, W)
+    start = fam._objective_at_zero(dd, b)
+    assert start is not None
+    f0, G0 = start
+    torch.testing.assert_close(f0, f_ref, rtol=1e-6, atol=1e-9)
+    torch.testing.assert_close(G0, G_ref, rtol=1e-5, atol=1e-7)

@@ -218,6 +218,10 @@ def test_lr_mfma_skips_tiles_of_stopped_fits(rt_gb, monkeypatch):
     f0, G0 = fam._objective(dd, b, W0)
     f0z, G0z = fam._objective(dd, b, W0, w_zero=True)
     assert torch.equal(f0z, f0) and torch.equal(G0z, G0)
+    # ... and the grouped fp32 start the solver actually uses agrees with it
+    fg, Gg = fam._objective_at_zero(dd, b)
+    torch.testing.assert_close(fg, f0, rtol=2e-5, atol=1e-6)
+    assert float(((Gg - G0).abs() / G0.abs().amax(0, keepdim=True).clamp_min(1e-6)).max()) < 2e-4
 
 
 def test_lr_mfma_fits_match_fp32_path(monkeypatch):
