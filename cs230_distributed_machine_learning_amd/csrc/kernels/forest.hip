@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 #include "forest_common.h"
 #include "wave_ops.h"
 
@@ -3691,8 +3692,14 @@ static SideStreams* side_streams() {
   static SideStreams ss;
   if (!ss.ok) {
     bool good = hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) == hipSuccess;
+    // DML_TIER_PRIO: stream priorities of the (subtree, wave, block) tier streams as 3 digits,
+    // 0 = normal, 1 = high (e.g. "001": the block tier -- the level's critical path -- first)
+    const char* pr = getenv("DML_TIER_PRIO");
+    int lo_pr = 0, hi_pr = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo_pr, &hi_pr) != hipSuccess) lo_pr = hi_pr = 0;
     for (int i = 0; i < 3 && good; ++i) {
-      good = hipStreamCreateWithFlags(&ss.s[i], hipStreamNonBlocking) == hipSuccess &&
+      const bool high = pr && (int)strlen(pr) > i && pr[i] == '1';
+      good = hipStreamCreateWithPriority(&ss.s[i], hipStreamNonBlocking, high ? hi_pr : lo_pr) == hipSuccess &&
              hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming) == hipSuccess;
     }
     ss.ok = good;
@@ -3970,6 +3977,13 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     }
     // block-tier children stage after the wave tier's (none under the big-subtree tier)
     const int stage_b = big ? 0 : nw;
+    // DML_BLOCK_FIRST: launch the block tier before the subtree / wave tiers
+    static const bool block_first = getenv("DML_BLOCK_FIRST") && atoi(getenv("DML_BLOCK_FIRST")) != 0;
+    if (block_first && nb) {
+      if (fast) k_nodes<DML_BLOCK_NT, MODE, FCX><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
+      else k_nodes<DML_BLOCK_NT, MODE, -1><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
+    }
+    const int nb_late = block_first ? 0 : nb;
     if (fast) {
       if (ns4) k_subtree<REG, FCX, 32><<<ns4, 64, lds_s32, s0>>>(c, cur, 4);
       if (ns) k_subtree<REG, FCX><<<ns, 64, lds_s, s0>>>(c, cur, 0);
@@ -3981,7 +3995,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
           k_nodes<64, MODE, FCX><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w, 0);
         }
       }
-      if (nb) k_nodes<DML_BLOCK_NT, MODE, FCX><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
+      if (nb_late) k_nodes<DML_BLOCK_NT, MODE, FCX><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
     } else {
       if (ns4) k_subtree<REG, -1, 32><<<ns4, 64, lds_s32, s0>>>(c, cur, 4);
       if (ns) k_subtree<REG, -1><<<ns, 64, lds_s, s0>>>(c, cur, 0);
@@ -3993,7 +4007,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
           k_nodes<64, MODE, -1><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w, 0);
         }
       }
-      if (nb) k_nodes<DML_BLOCK_NT, MODE, -1><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
+      if (nb_late) k_nodes<DML_BLOCK_NT, MODE, -1><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
     }
     // whole-histogram level: every tree evaluates every feature and the level's node
     // histograms over all d features fit the budget -> keep them, and derive the larger of
