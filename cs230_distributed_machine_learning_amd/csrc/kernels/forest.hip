@@ -3680,6 +3680,14 @@ static hipError_t g_last_err = hipSuccess;
     }                                                   \
   } while (0)
 
+// build LANES: independent builds driven concurrently from different host threads, each on
+// its own stream (boosting runs its fits in two lanes so one lane's kernels fill the GPU while
+// the other's host thread waits on a level read-back).  Every host-side resource of a build --
+// side streams, pinned read-back words, whole-histogram buffers, early-predict stream -- is
+// per (lane, device); a thread selects its lane with dml_forest_set_lane (default 0).
+constexpr int kLanes = 4;
+static thread_local int t_lane = 0;
+
 // side streams so the four node tiers of a level overlap (their tails otherwise
 // serialise: a level's few large nodes leave most CUs idle while small nodes wait)
 struct SideStreams {
@@ -3689,7 +3697,8 @@ struct SideStreams {
 };
 
 static SideStreams* side_streams() {
-  static SideStreams ss;
+  static SideStreams lanes[kLanes];
+  SideStreams& ss = lanes[t_lane];
   if (!ss.ok) {
     bool good = hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) == hipSuccess;
     // DML_TIER_PRIO: stream priorities of the (subtree, wave, block) tier streams as 3 digits,
@@ -3709,20 +3718,23 @@ static SideStreams* side_streams() {
 }
 
 static hipEvent_t pred_event() {
-  static hipEvent_t e = nullptr;
+  static hipEvent_t ev[kLanes] = {};
+  hipEvent_t& e = ev[t_lane];
   if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
   return e;
 }
 
 // stream of the early per-fit predicts (forest.hip build_impl)
 static hipStream_t pred_stream() {
-  static hipStream_t s = nullptr;
+  static hipStream_t st[kLanes] = {};
+  hipStream_t& s = st[t_lane];
   if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
   return s;
 }
 
 static int32_t* pinned_counters() {
-  static int32_t* p = nullptr;
+  static int32_t* pl[kLanes] = {};
+  int32_t*& p = pl[t_lane];
   if (!p) {
     if (hipHostMalloc((void**)&p, 64 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess) p = nullptr;
   }
@@ -3740,11 +3752,11 @@ struct FullBufs {
   void* fr = nullptr;      // k_split_full's per-(node, position) candidates
   size_t fr_bytes = 0;
 };
-static FullBufs* full_bufs() {
-  static FullBufs b[16];
+static FullBufs g_full_bufs[kLanes][16];
+static FullBufs* full_bufs(int lane = -1) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
-  return &b[dev];
+  return &g_full_bufs[lane < 0 ? t_lane : lane][dev];
 }
 static bool ensure_bytes(void*& p, size_t& have, size_t need) {
   if (have >= need) return true;
@@ -3758,7 +3770,8 @@ static bool ensure_bytes(void*& p, size_t& have, size_t need) {
 // free the current device's whole-histogram buffers (ops/forest_ops.py _Arena.clear: another
 // family needs the HBM); the next whole-histogram level allocates them again
 static int release_full_bufs() {
-  FullBufs* b = full_bufs();
+  for (int lane = 0; lane < kLanes; ++lane) {
+  FullBufs* b = full_bufs(lane);
   if (!b) return 0;
   if (b->gf[0] || b->gf[1] || b->pinfo || b->fr) {
     if (hipDeviceSynchronize() != hipSuccess) return 1;
@@ -3774,6 +3787,7 @@ static int release_full_bufs() {
     b->fr = nullptr;
     b->fr_bytes = 0;
   }
+  }
   return 0;
 }
 
@@ -3782,6 +3796,12 @@ static int release_full_bufs() {
 using namespace dml;
 
 extern "C" int dml_forest_release_scratch() { return release_full_bufs(); }
+// the calling host thread's build lane (0 .. kLanes-1); returns the lane count
+extern "C" int dml_forest_set_lane(int lane) {
+  if (lane < 0 || lane >= kLanes) return -1;
+  t_lane = lane;
+  return kLanes;
+}
 
 // kernel-level test hooks (tests/test_forest_gpu.py): wave primitives vs ds_bpermute
 // out layout per block of 64: [sorted | scan | xor1 | xor2 | xor4 | xor8 | xor16 | xor32 |

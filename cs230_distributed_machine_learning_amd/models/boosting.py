@@ -30,6 +30,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import threading
 import time
 from typing import Any, Dict, List
 
@@ -197,7 +198,67 @@ class GradientBoostingFamily(Family):
         cap = max(1, int(budget // max(1.0, per_fit)))
         outs: List[FitOutput] = []
         for i in range(0, len(tasks), cap):
-            outs.extend(self._boost(data, tasks[i:i + cap], K, keep_models))
+            outs.extend(self._boost_lanes(data, tasks[i:i + cap], K, keep_models))
+        return outs
+
+    def _boost_lanes(self, data, batch: List[FitTask], K: int, keep_models: bool) -> List[FitOutput]:
+        """A device batch split over build LANES (DML_GB_LANES, default 2): each lane boosts its
+        share of the fits from its own host thread on its own stream.  A stage is a chain of
+        short launches with a host read-back per tree level; with one lane the GPU idles during
+        every read-back, with two the other lane's kernels run meanwhile.  Fits are independent,
+        so the results are those of one lane (same kernels, same order inside each fit)."""
+        lanes = max(1, min(4, int(os.environ.get("DML_GB_LANES", "2"))))
+        if (not data.is_gpu or getattr(data, "is_row_shard", False) or lanes < 2 or len(batch) < 2
+                or getattr(native.hip_lib(), "dml_forest_set_lane", None) is None):
+            return self._boost(data, batch, K, keep_models)
+        lanes = min(lanes, len(batch))
+        # longest-processing-time split of the fits (stage count x depth x trees per stage)
+        w = [t.params["n_estimators"] * max(1, min(t.params["max_depth"], 12)) for t in batch]
+        groups: List[List[int]] = [[] for _ in range(lanes)]
+        load = [0] * lanes
+        for i in sorted(range(len(batch)), key=lambda i: -w[i]):
+            g = load.index(min(load))
+            groups[g].append(i)
+            load[g] += w[i]
+        groups = [sorted(g) for g in groups if g]
+        # lazily built per-dataset state, made once here (not raced by the lanes)
+        data.binned()
+        if hasattr(data, "binned_feature_major"):
+            data.binned_feature_major()
+        data.bin_values()
+        dev = data.device
+        main = torch.cuda.current_stream(dev)
+        streams = [torch.cuda.Stream(dev) for _ in groups]
+        results: List[Any] = [None] * len(groups)
+        errors: List[Any] = [None] * len(groups)
+
+        def work(li: int) -> None:
+            try:
+                forest_ops.set_build_lane(li)
+                streams[li].wait_stream(main)
+                with torch.cuda.device(dev), torch.cuda.stream(streams[li]):
+                    results[li] = self._boost(data, [batch[i] for i in groups[li]], K, keep_models)
+            except BaseException as e:   # re-raised on the caller's thread
+                errors[li] = e
+            finally:
+                forest_ops.set_build_lane(0)
+
+        threads = [threading.Thread(target=work, args=(li,), name=f"gb-lane{li}", daemon=True)
+                   for li in range(1, len(groups))]
+        for th in threads:
+            th.start()
+        work(0)
+        for th in threads:
+            th.join()
+        for st in streams:
+            main.wait_stream(st)
+        for e in errors:
+            if e is not None:
+                raise e
+        outs: List[Any] = [None] * len(batch)
+        for g, res in zip(groups, results):
+            for i, o in zip(g, res):
+                outs[i] = o
         return outs
 
     # ------------------------------------------------------------------------------------

@@ -714,9 +714,12 @@ class LogisticFamily(Family):
         else:
             running = False
         max_steps = max_it * 31
-        act_hist = []   # active fits per step (device scalars, read once at the end)
+        # DML_LR_TRACE_ACTIVE=1: active fits per step (device scalars, read once at the end --
+        # one extra host sync, so diagnostics only)
+        act_hist = [] if os.environ.get("DML_LR_TRACE_ACTIVE") == "1" else None
         while running and steps < max_steps:
-            act_hist.append(active.sum())
+            if act_hist is not None:
+                act_hist.append(active.sum())
             ft, Gt = self._objective(data, b, Wt, active)
             Ft = total(ft, Wt)
             n_evals += 1
@@ -762,8 +765,9 @@ class LogisticFamily(Family):
             if steps % sync_every == 0:
                 host_syncs += 1
                 running = bool(active.any())
-        self.last_solve_stats = {"host_syncs": host_syncs + bool(act_hist), "steps": steps, "sync_every": sync_every,
-                                 "active_per_step": torch.stack(act_hist).tolist() if act_hist else []}
+        self.last_solve_stats = {"host_syncs": host_syncs + bool(act_hist), "steps": steps, "sync_every": sync_every}
+        if act_hist:
+            self.last_solve_stats["active_per_step"] = torch.stack(act_hist).tolist()
         return W, iters, n_evals
 
     def run(self, data, tasks: List[FitTask], keep_models: bool = False) -> List[FitOutput]:

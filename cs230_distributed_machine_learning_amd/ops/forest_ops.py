@@ -251,6 +251,22 @@ def _carve(buf: torch.Tensor, off: int, shape, dtype) -> torch.Tensor:
 EXP_OFF, EXP_BINS = 160, 320   # bucket k + EXP_OFF of a target's frexp exponent k (|y| < 2^k)
 
 
+_LANE = threading.local()
+
+
+def set_build_lane(lane: int) -> None:
+    """Select the calling thread's build lane (forest.hip ``dml_forest_set_lane``): concurrent
+    builds from different host threads need different lanes -- each lane has its own side
+    streams, read-back words, whole-histogram buffers and workspace arena slot."""
+    if native.hip_lib().dml_forest_set_lane(int(lane)) < 0:
+        raise ValueError(f"build lane {lane} out of range")
+    _LANE.v = int(lane)
+
+
+def build_lane() -> int:
+    return getattr(_LANE, "v", 0)
+
+
 def _h2d(arr: np.ndarray, dev) -> torch.Tensor:
     """Host array -> device without a host/GPU rendezvous: staged through pinned memory and
     copied on the stream (a pageable copy blocks the host until the stream has drained, so the
@@ -523,9 +539,10 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     # Otherwise (boosting keeps its trees): arena workspace + freshly allocated pool.
     slot = None
     ws_buf = None
+    ws_slot = "ws" if build_lane() == 0 else f"ws{build_lane()}"   # one workspace per lane
     if not reuse_pool:
         with trace.range("forest_alloc"):
-            ws_buf = ARENA.take(dev, "ws", ws_bytes)
+            ws_buf = ARENA.take(dev, ws_slot, ws_bytes)
             workspace = ws_buf[:ws_bytes] if ws_buf is not None else torch.empty(ws_bytes, dtype=torch.uint8,
                                                                                   device=dev)
     retries = 0
@@ -585,7 +602,7 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     finally:
         # stream order keeps the next build's kernels behind this build's on the same stream
         if ws_buf is not None:
-            ARENA.give(dev, "ws")
+            ARENA.give(dev, ws_slot)
     P = int(a.n_nodes_out)
     del workspace
     stats = {"levels": int(a.levels_out), "large_rounds": int(a.large_rounds_out), "nodes": P,

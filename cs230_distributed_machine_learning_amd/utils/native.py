@@ -206,6 +206,7 @@ def _register_optional(lib) -> None:
         "dml_forest_apply": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp]),
         "dml_forest_prune": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp]),
         "dml_svm_sizeof_prob": (c_i32, []),
+        "dml_forest_set_lane": (c_i32, [c_i32]),
         "dml_forest_refine": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
                                       c_vp]),
         "dml_svm_smo_split": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

@@ -98,6 +98,42 @@ def test_gbrt_gpu_close_to_cpu(model, clf, loss):
         np.testing.assert_allclose(out["cuda:0"], out["cpu"], atol=5e-3)
 
 
+@pytest.mark.parametrize("model,n_classes,loss", [("GradientBoostingClassifier", 3, "log_loss"),
+                                                  ("GradientBoostingClassifier", 2, "exponential"),
+                                                  ("GradientBoostingClassifier", 2, "log_loss"),
+                                                  ("GradientBoostingRegressor", 0, "squared_error")])
+def test_gbrt_fused_stage_matches_torch_stage(model, n_classes, loss, monkeypatch, tmp_path):
+    """The fused HIP stage (gbrt.hip: gradient, leaf line search, raw update) against the
+    torch stage on the same device: same CV scores, and -- with the models kept (the refit
+    path) -- the same predictions from the stored artefacts."""
+    from cs230_distributed_machine_learning_amd.engine.model_store import load_predictor, save_model
+
+    rng = np.random.RandomState(3)
+    X = np.round(rng.randn(3000, 6), 1).astype(np.float32)
+    if n_classes:
+        y = np.digitize(X[:, 0] + 0.5 * X[:, 1] * X[:, 2], [-0.5, 0.5][: n_classes - 1]).astype(int)
+    else:
+        y = (2 * X[:, 0] + X[:, 1] * X[:, 2] + 0.1 * rng.randn(3000)).astype(np.float32)
+    grid = list(ParameterGrid({"n_estimators": [8, 20], "max_depth": [2, 4], "loss": [loss],
+                               "learning_rate": [0.3]}))
+    out, preds = {}, {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DML_GB_FUSED", flag)
+        dd = _dd(X, y, bool(n_classes), "cuda:0", cv=3)
+        spec = JobSpec(model, grid, cv=3, holdout=True, test_size=0.2, random_state=0, keep_models="all")
+        res = run_candidates(dd, spec, range(len(grid)))
+        assert all(r.ok for r in res), [r.error for r in res]
+        out[flag] = np.array([r.result["mean_cv_score"] for r in res])
+        preds[flag] = [load_predictor(save_model(r.model, str(tmp_path / f"m{flag}_{i}.npz"))).predict(X[:500])
+                       for i, r in enumerate(res)]
+    np.testing.assert_allclose(out["1"], out["0"], rtol=0, atol=1e-9 if loss == "squared_error" else 2e-3)
+    for a, b in zip(preds["1"], preds["0"]):
+        if n_classes:
+            assert np.mean(a == b) >= 0.995
+        else:
+            np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6)
+
+
 def test_lr_link_grad_kernel_matches_torch():
     from cs230_distributed_machine_learning_amd.models import linear
     from cs230_distributed_machine_learning_amd.utils import native
