@@ -190,6 +190,11 @@ struct ForestArgs {
   // without reading the "need more" flag back after each round
   int64_t all_features;
   int64_t sub_small;   // 0 < sub_small < sub_max (<= 32): subtree roots of <= sub_small rows -> tier 4
+  // boosting (regression, unit weights, whole-histogram roots): uint32 [T][d][256] row counts
+  // of every tree's ROOT histogram.  The root's rows are the fit's training rows at every stage
+  // of an active set, so its count planes never change: root_counts_valid = 0 -> this build's
+  // root level stores them, 1 -> the root level skips its count atomics and copies them in
+  int64_t root_counts, root_counts_valid;
 };
 
 // 0 subtree, 1 wave, 2 block, 3 large, 4 small subtree (<= sub_small rows: the subtree kernel
@@ -254,6 +259,8 @@ struct Ctx {
   const int4* pinfo_cur;
   int4* pinfo_next;
   int32_t full_cur, full_prev;
+  int32_t root_cnt_skip;       // root level of a build with cached root counts: no count atomics
+  uint32_t* root_counts;       // ForestArgs::root_counts (null: none)
   int64_t pi_cap;        // entries of each pinfo table
   // whole-histogram levels: every (large node, visiting position)'s split candidate, from
   // k_split_full (one wave per feature, all features of all nodes in one launch), selected in
@@ -1134,6 +1141,12 @@ __device__ __forceinline__ void hist_add_unit(typename HT<MODE>::T* hj, int b, c
     atomicAdd((uint32_t*)hj + b, 1u);
     atomicAdd(&hj[256 + b], pl.wy);
   }
+}
+
+// the same with the count plane supplied elsewhere (boosting roots: ForestArgs::root_counts)
+template <int MODE>
+__device__ __forceinline__ void hist_add_wy(typename HT<MODE>::T* hj, int b, const typename PLT<MODE>::T& pl) {
+  if constexpr (MODE == 2) atomicAdd(&hj[256 + b], pl.wy);
 }
 
 template <int MODE, int RP = 3>
@@ -2834,6 +2847,9 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
   // plane is a row count -- kept as u32 LDS counters (ds_add_u32: half the bytes and bank
   // pairs of the u64 add) in the first KB of each feature's 4-KB slice, widened at the flush
   const bool uw = MODE == 2 && s.bootstrap == 0 && g <= KGL;
+  // cached root counts (boosting): the count plane is copied in by k_root_counts, so only the
+  // w yq plane is accumulated (one LDS atomic per (row, feature) instead of two)
+  const bool skipc = uw && fround >= 0 && c.root_cnt_skip != 0;
   if (g <= KGL) {
     // ping-pong software pipeline with compile-time-counted unconditional gathers (the block
     // tier's loop in k_nodes): the row id two steps ahead and the next step's bins are in
@@ -2873,9 +2889,15 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
         }
         const PL pl = payload_finish<MODE, PK>(c, s, ty, pr);
         if constexpr (MODE == 2 && UW) {
+          if (skipc) {   // wave-uniform: the count plane comes from the root-count cache
 #pragma unroll
-          for (int j = 0; j < G; ++j)
-            if (j < g) hist_add_unit<MODE>(hist + j * span, (int)b[j], pl);
+            for (int j = 0; j < G; ++j)
+              if (j < g) hist_add_wy<MODE>(hist + j * span, (int)b[j], pl);
+          } else {
+#pragma unroll
+            for (int j = 0; j < G; ++j)
+              if (j < g) hist_add_unit<MODE>(hist + j * span, (int)b[j], pl);
+          }
         } else {
 #pragma unroll
           for (int j = 0; j < G; ++j)
@@ -2949,6 +2971,7 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
     for (int i = threadIdx.x; i < g * span; i += 256) {
       CT v = hist[i];
       const int j = i / span, b = i - j * span;
+      if (MODE == 2 && b < 256 && skipc) continue;   // count plane: copied from the root-count cache
       if (MODE == 2 && b < 256 && (uw || gcnt)) {
         // row count of bin b: the u32 LDS counters, or rows << 32 of the (w | rows << 32) plane
         const uint32_t n1 = uw ? ((const uint32_t*)(hist + j * span))[b] : (uint32_t)((uint64_t)v >> 32);
@@ -2961,6 +2984,20 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
       if (v != (CT)0) atomicAdd(&gh[i], v);
     }
   }
+}
+
+// boosting roots: the u32 count planes of the root histograms (gf_cur, gcnt layout: the first KB
+// of each feature's count plane) <-> the per-tree cache ForestArgs::root_counts.  save = 1 stores
+// a build's root counts, save = 0 copies them into a build that skipped its count atomics.
+__global__ __launch_bounds__(256) void k_root_counts(Ctx c, int save) {
+  const int slot = blockIdx.x, f = blockIdx.y;
+  const int64_t gspan = (int64_t)large_planes(2, c.CH) * 256;
+  const int tree = c.lstate[slot].on.tree;
+  uint32_t* g = (uint32_t*)((unsigned long long*)c.gf_cur + ((int64_t)slot * c.d + f) * gspan);
+  uint32_t* r = c.root_counts + ((int64_t)tree * c.d + f) * 256;
+  const int b = threadIdx.x;
+  if (save) r[b] = g[b];
+  else g[b] = r[b];
 }
 
 // whole-histogram level: a derived node's histogram over all d features = its parent's
@@ -4062,16 +4099,27 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       c.pinfo_next = fb->pinfo + (int64_t)(1 - fpar) * fb->pi_cap;
       c.pi_cap = fb->pi_cap;
     }
+    // boosting root level with a root-count cache (roots only: every open node is a large root)
+    const bool root_cache = MODE == 2 && full && levels == 1 && a->root_counts && nL == (int)a->T &&
+                            ns + ns4 + nw + nb == 0;
+    c.root_counts = root_cache ? (uint32_t*)a->root_counts : nullptr;
+    c.root_cnt_skip = root_cache && a->root_counts_valid ? 1 : 0;
     if (nL && full) {
       k_large_prep<<<nL, 64, 0, st>>>(c, cur, nL);
       const int rounds = (int)((a->d + a->kg_large - 1) / a->kg_large);
       HIP_OK(hipMemsetAsync(c.gf_cur, 0, (size_t)nL * full_node_b, st));
+      if (c.root_cnt_skip) k_root_counts<<<dim3((unsigned)nL, (unsigned)a->d), 256, 0, st>>>(c, 0);
       const dim3 gh = DML_LARGE_NODE_FAST ? dim3((unsigned)nL, nchunks) : dim3(nchunks, (unsigned)nL);
       for (int round = 0; round < rounds; ++round) {
         ++large_rounds;
         if (c.packed) k_hist_large<MODE, true><<<gh, 256, lds_hl, st>>>(c, round);
         else k_hist_large<MODE, false><<<gh, 256, lds_hl, st>>>(c, round);
       }
+      if (root_cache && !c.root_cnt_skip) {
+        k_root_counts<<<dim3((unsigned)nL, (unsigned)a->d), 256, 0, st>>>(c, 1);
+        a->root_counts_valid = 1;   // in/out: the cache now holds this active set's root counts
+      }
+      c.root_cnt_skip = 0;
       if (c.full_prev) {
         const int64_t per = (int64_t)a->d * large_planes(GM, CH) * 256;
         k_hist_derive<GM><<<dim3((unsigned)nL, (unsigned)((per + 1023) / 1024)), 256, 0, st>>>(c);

@@ -471,8 +471,11 @@ class GradientBoostingFamily(Family):
                 xbt = data.binned_feature_major() if hasattr(data, "binned_feature_major") else None
                 # per-tree active-row counts: fixed while the roles are (no subsample draw)
                 ccache = cst.setdefault("count_cache", {}) if not sub_rows else None
+                # the roots' row-count histograms are fixed while the roles are (DML_GB_ROOT_CACHE=0: off)
+                rcache = (cst.setdefault("root_counts", {})
+                          if not sub_rows and os.environ.get("DML_GB_ROOT_CACHE", "1") != "0" else None)
                 fb = forest_ops.build_gpu(Xb, None, tgt, roles_t, specs, 1, True, self.tiers, ystride=n, XbT=xbt,
-                                          count_cache=ccache)
+                                          count_cache=ccache, root_counts=rcache)
                 if limit.any():   # sklearn's best-first tree (friedman_mse and squared_error rank splits alike)
                     forest_ops.prune_max_leaves(fb, specs, limit)
                 if ccp.any():     # minimal cost-complexity pruning of each stage tree (variance impurity)

@@ -427,7 +427,8 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
               specs: np.ndarray, n_classes: int, is_reg: bool, tiers: ForestTiers | None = None,
               ystride: int = 0, reuse_pool: bool = False, XbT: Optional[torch.Tensor] = None,
               cw: Optional[np.ndarray] = None, mono: Optional[np.ndarray] = None,
-              early_predict=None, count_cache: Optional[dict] = None) -> ForestBuild:
+              early_predict=None, count_cache: Optional[dict] = None,
+              root_counts: Optional[dict] = None) -> ForestBuild:
     """``ystride > 0``: ``yreg`` is a [targets, ystride] matrix and tree t regresses on
     row ``specs[t]['target']`` (gradient boosting's per-fit pseudo-residuals).
     ``reuse_pool``: the node arrays live in the device arena and are valid until the
@@ -438,7 +439,10 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     GpuPredict; the caller predicts the other fits).
     ``count_cache``: a dict kept by the caller for as long as ``roles`` and the specs' split /
     bootstrap fields stay the same (boosting stages of one active set): the per-tree active-row
-    counts are computed once into it and reused (no count kernel, no read-back)."""
+    counts are computed once into it and reused (no count kernel, no read-back).
+    ``root_counts`` (boosting, same lifetime as ``count_cache``): a dict holding a uint32
+    [T, d, 256] device cache of the trees' root-histogram row counts; the first build fills it
+    (``valid`` becomes 1), later builds skip the root level's count atomics and copy them in."""
     lib = native.hip_lib()
     dev = Xb.device
     T = len(specs)
@@ -490,6 +494,12 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     a.fast_crit = (int(crits[0]) + 1 if len(crits) == 1 and cw_dev is None and mono_dev is None
                    and not np.any(specs["min_weight_frac"] > 0) else 0)
     a.active_count = native.ptr(active)
+    if root_counts is not None and is_reg and T:
+        buf = root_counts.get("buf")
+        if buf is None or buf.numel() != T * d * 256:
+            buf = root_counts["buf"] = torch.empty(T * d * 256, dtype=torch.int32, device=dev)
+            root_counts["valid"] = 0
+        a.root_counts, a.root_counts_valid = native.ptr(buf), int(root_counts.get("valid", 0))
     t0 = time.perf_counter()
     with trace.range("forest_count"):
         if cached:
@@ -603,6 +613,8 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
         # stream order keeps the next build's kernels behind this build's on the same stream
         if ws_buf is not None:
             ARENA.give(dev, ws_slot)
+    if root_counts is not None and a.root_counts:
+        root_counts["valid"] = int(a.root_counts_valid)
     P = int(a.n_nodes_out)
     del workspace
     stats = {"levels": int(a.levels_out), "large_rounds": int(a.large_rounds_out), "nodes": P,

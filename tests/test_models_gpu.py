@@ -134,6 +134,26 @@ def test_gbrt_fused_stage_matches_torch_stage(model, n_classes, loss, monkeypatc
             np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("model,clf", [("GradientBoostingRegressor", False), ("GradientBoostingClassifier", True)])
+def test_gbrt_root_count_cache_is_exact(model, clf, monkeypatch):
+    """Boosting builds reuse the roots' row-count histograms across stages (they only depend on
+    the training rows): the ensembles are identical with and without the cache, one lane or two."""
+    rng = np.random.RandomState(4)
+    X = rng.randn(200_000, 20).astype(np.float32)      # large-tier roots (> block_max rows)
+    y = (X[:, 0] + X[:, 1] * X[:, 2] > 0).astype(int) if clf else (X[:, 0] + 0.3 * X[:, 3] ** 2).astype(np.float32)
+    grid = list(ParameterGrid({"n_estimators": [6, 12], "max_depth": [3]}))
+    out = {}
+    for cache, lanes in (("0", "1"), ("1", "1"), ("1", "2")):
+        monkeypatch.setenv("DML_GB_ROOT_CACHE", cache)
+        monkeypatch.setenv("DML_GB_LANES", lanes)
+        dd = _dd(X, y, clf, "cuda:0", cv=3)
+        res = run_candidates(dd, JobSpec(model, grid, cv=3), range(len(grid)))
+        assert all(r.ok for r in res), [r.error for r in res]
+        out[cache + lanes] = np.array([r.result["mean_cv_score"] for r in res])
+    np.testing.assert_array_equal(out["11"], out["01"])
+    np.testing.assert_array_equal(out["12"], out["01"])
+
+
 def test_lr_link_grad_kernel_matches_torch():
     from cs230_distributed_machine_learning_amd.models import linear
     from cs230_distributed_machine_learning_amd.utils import native
