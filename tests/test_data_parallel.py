@@ -243,3 +243,18 @@ def test_row_sharded_lr_on_gpu_matches_single_process():
                    KNN_GRID[:2], cv=3)
     for (cv_s, hold), (cv_r, hold_r) in zip(o0[3], ref_knn):
         assert np.allclose(cv_s, cv_r, atol=1e-3), (cv_s, cv_r)
+
+
+def test_needs_whole_rows_routes_gbrt_losses_task_parallel():
+    """GradientBoosting candidates the row-sharded booster rejects (leaf percentiles, the
+    early-stopping validation split, monotonic bounds) are routed task-parallel by the cluster."""
+    from cs230_distributed_machine_learning_amd.parallel.runner import needs_whole_rows
+
+    for loss in ("absolute_error", "huber", "quantile"):
+        assert needs_whole_rows("GradientBoostingRegressor", {"loss": loss})
+    assert needs_whole_rows("GradientBoostingClassifier", {"n_iter_no_change": 5})
+    assert needs_whole_rows("GradientBoostingRegressor", {"monotonic_cst": [1, 0]})
+    assert not needs_whole_rows("GradientBoostingRegressor", {"loss": "squared_error"})
+    assert not needs_whole_rows("GradientBoostingClassifier", {"loss": "log_loss", "n_iter_no_change": None})
+    assert needs_whole_rows("RandomForestRegressor", {"criterion": "absolute_error"})
+    assert not needs_whole_rows("LogisticRegression", {"C": 1.0})
