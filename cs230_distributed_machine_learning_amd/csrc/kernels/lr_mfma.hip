@@ -44,6 +44,9 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #ifndef LRM_PASSES
 #define LRM_PASSES 3   // A/B instrumentation: 1 = hi*hi only, 0 = no MFMA (never in production)
 #endif
+#ifndef LRM_DMA_HALF
+#define LRM_DMA_HALF 0   // A/B instrumentation: 1 = half of the k-steps stage operands (never in production)
+#endif
 #ifndef LRM_EPI_PROBE
 #define LRM_EPI_PROBE 0   // A/B instrumentation: 1 = fwd3 epilogue without the link math (never in production)
 #endif
@@ -569,7 +572,11 @@ __device__ __forceinline__ void v3_gemm(const Operands& op, int64_t row0, int64_
     if (t + 1 < nk) v3_wait_barrier<PER_WAVE>();
     else v3_wait_barrier<0>();
     const int nxt = cur == 0 ? 2 : cur - 1;   // (t + 2) % 3 == (t - 1) % 3
+#if LRM_DMA_HALF   // timing probe only (wrong results): the ring is refilled every other k-step
+    if (t + 2 < nk && (t & 1) == 0) v3_glds_stage(op, row0, col0, kb + (t + 2) * BK, smem + nxt * STG, w, lane);
+#else
     if (t + 2 < nk) v3_glds_stage(op, row0, col0, kb + (t + 2) * BK, smem + nxt * STG, w, lane);
+#endif
     v3_mma(smem + cur * STG, acc, wm, wn, lane);
     cur = cur == 2 ? 0 : cur + 1;
   }
