@@ -18,6 +18,12 @@
 //                  multinomial / exponential / squared error), float64 for the line search and
 //                  float32 for the tree builder's target matrix
 //
+//   k_sel_*        percentile losses (absolute_error / huber / quantile): sklearn's inverted-CDF
+//                  percentile of every (tree, leaf)'s residuals -- and huber's delta, the alpha
+//                  percentile of every fit's |residual| over its training rows -- by an exact
+//                  8-pass radix select on order-preserving 64-bit keys of the float64 values
+//                  (one histogram pass + one pick pass per byte), no sort
+//
 // A leaf is addressed by its PATH SLOT: 1 at the root, 2 s + (went right) per level, so a
 // tree of depth <= D has slots in [1, 2^(D+1)) and per-tree leaf arrays need no node index.
 #include <hip/hip_runtime.h>
@@ -44,6 +50,14 @@ struct GbStageArgs {
   int64_t slot_val;           // double [J][S]
   int64_t raw;                // double [F * K][n]
   int64_t XbT;                // optional feature-major bins uint8 [d][n] (0: walk the row-major Xb)
+  // percentile losses (pct_any = 1 when some tree's loss is absolute_error / huber / quantile)
+  int64_t pct_any;
+  int64_t yreg;               // double [n]
+  int64_t slot_of;            // uint16 [J][n] scratch: the in-bag row's leaf slot (0xFFFF: not in-bag)
+  int64_t sel_hist;           // uint32 [J * S][256] scratch, zeroed by the caller
+  int64_t sel_state;          // uint64 [J * S][4] scratch (prefix, mask, rank, count)
+  int64_t tree_q;             // double [J]: the leaf percentile (0.5; quantile: alpha)
+  int64_t tree_delta;         // double [J]: huber delta of the tree's fit at this stage
 };
 
 struct GbGradArgs {
@@ -55,6 +69,11 @@ struct GbGradArgs {
   int64_t yreg;               // double [n]
   int64_t grad;               // double [A * K][n] out
   int64_t tgt;                // float [A * K][n] out
+  int64_t fit_alpha;          // double [A]: quantile / huber alpha (percentile losses)
+  int64_t fit_delta;          // double [A]: huber delta, written by dml_gb_huber_delta
+  int64_t fit_train;          // uint8 [A][n]: the fit's training rows (huber delta)
+  int64_t sel_hist;           // uint32 [A][256] scratch (huber delta select), zeroed by the caller
+  int64_t sel_state;          // uint64 [A][4] scratch
 };
 
 #define GB_PTR(T, v) ((T*)(uintptr_t)(v))
@@ -123,9 +142,14 @@ __global__ __launch_bounds__(256) void k_gb_leafsums(GbStageArgs a) {
   const int64_t r0 = (int64_t)blockIdx.x * 1024;
   for (int u = 0; u < 4; ++u) {
     const int64_t r = r0 + u * 256 + threadIdx.x;
-    if (r >= n || !inb[r]) continue;
+    if (r >= n) continue;
+    if (!inb[r]) {   // (subsampled stages change the in-bag set: every row's entry is rewritten)
+      if (a.pct_any) GB_PTR(uint16_t, a.slot_of)[(int64_t)j * n + r] = (uint16_t)0xFFFF;
+      continue;
+    }
     const int slot = gb_walk<S>(tsplit, X, a.ld, XT, n, r);
     hit[slot] = 1;   // every row of the leaf writes the same flag
+    if (a.pct_any) GB_PTR(uint16_t, a.slot_of)[(int64_t)j * n + r] = (uint16_t)slot;
     if (!newton) continue;
     const double gv = g[r];
     double h;
@@ -157,6 +181,180 @@ __global__ __launch_bounds__(256) void k_gb_leafsums(GbStageArgs a) {
   }
 }
 
+// ---- exact radix select ------------------------------------------------------------
+constexpr int kSelRows = 8192;   // rows per workgroup of a byte pass (amortises the LDS counters)
+// order-preserving 64-bit key of a double (negative values reversed), and back
+__device__ __forceinline__ unsigned long long gb_double_key(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double gb_key_to_double(unsigned long long k) {
+  return __longlong_as_double((k >> 63) ? (long long)(k & 0x7FFFFFFFFFFFFFFFull) : (long long)~k);
+}
+
+// one byte pass: every segment member whose key matches the segment's prefix (the bytes fixed
+// so far) counts its next byte.  MODE 0: segments (tree j, leaf slot), key = y - raw of tree j's
+// in-bag rows of a percentile loss; MODE 1: segments = active fits, key = |y - raw| over the
+// fit's training rows (huber delta).  Per-workgroup LDS counters when a grid row's segments fit
+// (S <= 64 slots x 256), flushed with one global atomic per nonzero counter.
+template <int MODE, int SEGS>
+__device__ __forceinline__ void gb_sel_pass(int64_t n, int row_seg, int nseg_row, const double* __restrict__ yreg,
+                                            const double* __restrict__ raw, const uint8_t* __restrict__ member,
+                                            const uint16_t* __restrict__ slot_of, int loss_ok,
+                                            const unsigned long long* __restrict__ state, unsigned int* __restrict__ hist,
+                                            int shift) {
+  __shared__ unsigned int lh[SEGS > 0 ? SEGS * 256 : 1];
+  if (SEGS > 0) {
+    for (int i = threadIdx.x; i < SEGS * 256; i += 256) lh[i] = 0u;
+    __syncthreads();
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * kSelRows;
+  if (loss_ok) {
+    for (int u = 0; u < kSelRows / 256; ++u) {
+      const int64_t r = r0 + u * 256 + threadIdx.x;
+      if (r >= n) break;
+      int local;
+      double v;
+      if (MODE == 0) {
+        const int sl = slot_of[r];
+        if (sl == 0xFFFF) continue;
+        local = sl;
+        v = yreg[r] - raw[r];
+      } else {
+        if (!member[r]) continue;
+        local = 0;
+        v = fabs(yreg[r] - raw[r]);
+      }
+      const int seg = row_seg + local;
+      const unsigned long long key = gb_double_key(v);
+      const unsigned long long* stt = state + 4 * (int64_t)seg;
+      if ((key & stt[1]) != stt[0]) continue;
+      const int byte = (int)((key >> shift) & 255ull);
+      if (SEGS > 0) atomicAdd(&lh[local * 256 + byte], 1u);
+      else atomicAdd(&hist[(int64_t)seg * 256 + byte], 1u);
+    }
+  }
+  if (SEGS > 0) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < nseg_row * 256 && i < SEGS * 256; i += 256)
+      if (lh[i]) atomicAdd(&hist[(int64_t)row_seg * 256 + i], lh[i]);
+  }
+}
+
+template <int SEGS>
+__global__ __launch_bounds__(256) void k_sel_leaf(GbStageArgs a, int shift) {
+  const int j = blockIdx.y;
+  const int loss = GB_PTR(const int32_t, a.tree_loss)[j];
+  const int ok = loss == kGbAbs || loss == kGbQuant || loss == kGbHuber;
+  const int64_t n = a.n;
+  gb_sel_pass<0, SEGS>(n, j * (int)a.S, (int)a.S, GB_PTR(const double, a.yreg),
+                       GB_PTR(const double, a.raw) + (int64_t)GB_PTR(const int32_t, a.tree_raw)[j] * n, nullptr,
+                       GB_PTR(const uint16_t, a.slot_of) + (int64_t)j * n, ok,
+                       GB_PTR(const unsigned long long, a.sel_state), GB_PTR(unsigned int, a.sel_hist), shift);
+}
+
+__global__ __launch_bounds__(256) void k_sel_fit(GbGradArgs a, int shift) {
+  const int fa = blockIdx.y;
+  const int ok = GB_PTR(const int32_t, a.fit_loss)[fa] == kGbHuber;
+  const int64_t n = a.n;
+  gb_sel_pass<1, 1>(n, fa, 1, GB_PTR(const double, a.yreg),
+                    GB_PTR(const double, a.raw) + (int64_t)GB_PTR(const int32_t, a.fit_raw)[fa] * n,
+                    GB_PTR(const uint8_t, a.fit_train) + (int64_t)fa * n, nullptr, ok,
+                    GB_PTR(const unsigned long long, a.sel_state), GB_PTR(unsigned int, a.sel_hist), shift);
+}
+
+// one wave per segment: the byte holding the target rank (pass 0 also fixes the rank from the
+// segment's member count and its percentile q: inverted CDF, k = ceil(q m) - 1, the torch path's
+// _segment_percentile); the counters are cleared for the next pass.  state: prefix, mask, rank, m
+__global__ __launch_bounds__(64) void k_sel_pick(unsigned long long* state, unsigned int* hist, const double* q,
+                                                 int64_t nseg, int64_t q_div, int shift) {
+  const int64_t i = blockIdx.x;
+  const int lane = threadIdx.x;
+  unsigned long long* st = state + 4 * i;
+  unsigned int* h = hist + i * 256;
+  const uint4 c4 = *(const uint4*)(h + 4 * lane);   // bins 4 lane .. 4 lane + 3
+  *(uint4*)(h + 4 * lane) = make_uint4(0u, 0u, 0u, 0u);
+  const unsigned long long mine = (unsigned long long)c4.x + c4.y + c4.z + c4.w;
+  unsigned long long incl = mine;   // inclusive prefix over lanes
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  const unsigned long long total = __shfl(incl, 63);
+  unsigned long long k;
+  if (shift == 56) {   // pass 0: every member counted once
+    long long kk = 0;
+    if (total > 0) {
+      kk = (long long)ceil(q[i / q_div] * (double)total - 1e-12) - 1;
+      kk = kk < 0 ? 0 : (kk > (long long)total - 1 ? (long long)total - 1 : kk);
+    }
+    k = (unsigned long long)kk;
+    if (lane == 0) st[3] = total;
+  } else {
+    k = st[2];
+  }
+  if (total == 0) {   // empty segment (or no member left): nothing to fix
+    if (lane == 0) st[2] = k;
+    return;
+  }
+  const unsigned long long excl = incl - mine;
+  const unsigned long long hit = __ballot(k >= excl && k < incl);
+  const int src = hit ? __ffsll((long long)hit) - 1 : 63;
+  if (lane == src) {
+    unsigned long long cum = excl;
+    int b = 0;
+    const unsigned int cs[4] = {c4.x, c4.y, c4.z, c4.w};
+    for (; b < 3; ++b) {
+      if (k < cum + cs[b]) break;
+      cum += cs[b];
+    }
+    st[0] |= (unsigned long long)(4 * lane + b) << shift;
+    st[1] |= 255ull << shift;
+    st[2] = k - cum;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_sel_init(unsigned long long* state, int64_t nseg) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nseg) return;
+  state[4 * i] = 0ull; state[4 * i + 1] = 0ull; state[4 * i + 2] = 0ull; state[4 * i + 3] = 0ull;
+}
+
+// huber leaf line search: sum over the leaf's in-bag rows of sign(d) min(delta, |d|), d = resid -
+// median, and the member count, into slot_sum (then k_gb_values: median + sum / count)
+template <int S>
+__global__ __launch_bounds__(256) void k_gb_huber_terms(GbStageArgs a) {
+  __shared__ double sm[S], cn[S];
+  const int j = blockIdx.y;
+  if (GB_PTR(const int32_t, a.tree_loss)[j] != kGbHuber) return;   // workgroup-uniform
+  for (int i = threadIdx.x; i < S; i += 256) { sm[i] = 0.0; cn[i] = 0.0; }
+  __syncthreads();
+  const int64_t n = a.n;
+  const uint16_t* so = GB_PTR(const uint16_t, a.slot_of) + (int64_t)j * n;
+  const double* raw = GB_PTR(const double, a.raw) + (int64_t)GB_PTR(const int32_t, a.tree_raw)[j] * n;
+  const double* y = GB_PTR(const double, a.yreg);
+  const unsigned long long* st = GB_PTR(const unsigned long long, a.sel_state) + (int64_t)j * S * 4;
+  const double delta = GB_PTR(const double, a.tree_delta)[j];
+  const int64_t r0 = (int64_t)blockIdx.x * 1024;
+  for (int u = 0; u < 4; ++u) {
+    const int64_t r = r0 + u * 256 + threadIdx.x;
+    if (r >= n) break;
+    const int sl = so[r];
+    if (sl == 0xFFFF) continue;
+    const double d = (y[r] - raw[r]) - gb_key_to_double(st[4 * sl]);
+    const double t = d > 0.0 ? fmin(delta, d) : (d < 0.0 ? -fmin(delta, -d) : 0.0);
+    atomicAdd(&sm[sl], t);
+    atomicAdd(&cn[sl], 1.0);
+  }
+  __syncthreads();
+  double* ss = GB_PTR(double, a.slot_sum) + (int64_t)j * S * 2;
+  for (int i = threadIdx.x; i < S; i += 256)
+    if (cn[i] > 0.0) {
+      atomicAdd(&ss[2 * i], sm[i]);
+      atomicAdd(&ss[2 * i + 1], cn[i]);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_gb_values(GbStageArgs a) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t S = a.S;
@@ -166,7 +364,14 @@ __global__ __launch_bounds__(256) void k_gb_values(GbStageArgs a) {
   double v = 0.0;
   if (node >= 0) {
     const int loss = GB_PTR(const int32_t, a.tree_loss)[j];
-    if (loss == kGbLog || loss == kGbExp) {
+    if (loss == kGbAbs || loss == kGbQuant || loss == kGbHuber) {
+      const double med = gb_key_to_double(GB_PTR(const unsigned long long, a.sel_state)[4 * i]);
+      v = med;
+      if (loss == kGbHuber) {   // med + mean of the clipped deviations (k_gb_huber_terms)
+        const double* ss = GB_PTR(const double, a.slot_sum) + 2 * i;
+        v = med + ss[0] / fmax(ss[1], 1.0);
+      }
+    } else if (loss == kGbLog || loss == kGbExp) {
       const double* ss = GB_PTR(const double, a.slot_sum) + 2 * i;
       double num = ss[0];
       const double den = ss[1];
@@ -203,6 +408,13 @@ __global__ __launch_bounds__(256) void k_gb_update(GbStageArgs a) {
 
 __device__ __forceinline__ double gb_sigmoid(double x) { return 1.0 / (1.0 + exp(-x)); }
 
+__global__ __launch_bounds__(256) void k_sel_delta(GbGradArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.A) return;
+  const unsigned long long* st = GB_PTR(const unsigned long long, a.sel_state) + 4 * i;
+  GB_PTR(double, a.fit_delta)[i] = st[3] ? gb_key_to_double(st[0]) : 0.0;
+}
+
 template <int KMAX>
 __global__ __launch_bounds__(256) void k_gb_grad(GbGradArgs a) {
   const int fa = blockIdx.y;
@@ -235,8 +447,19 @@ __global__ __launch_bounds__(256) void k_gb_grad(GbGradArgs a) {
   } else if (loss == kGbExp) {
     const double yb = (double)GB_PTR(const int32_t, a.ycls)[r];
     v = yb * exp(-x) - (1.0 - yb) * exp(x);
-  } else {   // squared error
-    v = GB_PTR(const double, a.yreg)[r] - x;
+  } else {   // squared error and the percentile losses, from the residual
+    const double diff = GB_PTR(const double, a.yreg)[r] - x;
+    if (loss == kGbAbs) {
+      v = diff > 0.0 ? 1.0 : (diff < 0.0 ? -1.0 : 0.0);
+    } else if (loss == kGbQuant) {
+      const double al = GB_PTR(const double, a.fit_alpha)[fa];
+      v = diff >= 0.0 ? al : al - 1.0;
+    } else if (loss == kGbHuber) {
+      const double dl = GB_PTR(const double, a.fit_delta)[fa];
+      v = fabs(diff) <= dl ? diff : (diff > 0.0 ? dl : (diff < 0.0 ? -dl : 0.0));
+    } else {
+      v = diff;
+    }
   }
   g[r] = v;
   t[r] = (float)v;
@@ -271,6 +494,22 @@ __global__ __launch_bounds__(256) void k_exp_hist(const float* __restrict__ y, i
   if (threadIdx.x == 0 && nb) atomicAdd(bad, (unsigned long long)nb);
 }
 
+// the 8 byte passes of the (tree, leaf) percentile select (state zeroed, hist zero on entry)
+template <int SV>
+int leaf_select(GbStageArgs* a, dim3 grid, hipStream_t st) {
+  if (!a->slot_of || !a->sel_hist || !a->sel_state || !a->tree_q || !a->yreg) return 2;
+  const int64_t nseg = a->J * SV;
+  k_sel_init<<<(unsigned)((nseg + 255) / 256), 256, 0, st>>>((unsigned long long*)a->sel_state, nseg);
+  const dim3 gsel((unsigned)((a->n + kSelRows - 1) / kSelRows), grid.y);
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    if (SV <= 64) k_sel_leaf<(SV <= 64 ? SV : 1)><<<gsel, 256, 0, st>>>(*a, shift);
+    else k_sel_leaf<0><<<gsel, 256, 0, st>>>(*a, shift);
+    k_sel_pick<<<(unsigned)nseg, 64, 0, st>>>((unsigned long long*)a->sel_state, (unsigned int*)a->sel_hist,
+                                             (const double*)a->tree_q, nseg, SV, shift);
+  }
+  return 0;
+}
+
 }  // namespace dml
 
 using namespace dml;
@@ -299,6 +538,10 @@ int dml_gb_stage(GbStageArgs* a, hipStream_t st) {
 #define GB_CASE(SV)                                                                   \
     case SV:                                                                          \
       k_gb_leafsums<SV><<<grid, 256, 0, st>>>(*a);                                    \
+      if (a->pct_any) {                                                               \
+        if (leaf_select<SV>(a, grid, st)) return 2;                                   \
+        k_gb_huber_terms<SV><<<grid, 256, 0, st>>>(*a);                               \
+      }                                                                               \
       k_gb_values<<<(unsigned)((a->J * SV + 255) / 256), 256, 0, st>>>(*a);           \
       k_gb_update<SV><<<grid, 256, 0, st>>>(*a);                                      \
       break;
@@ -306,6 +549,22 @@ int dml_gb_stage(GbStageArgs* a, hipStream_t st) {
 #undef GB_CASE
     default: return 2;
   }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// huber delta of every active fit: the alpha percentile (inverted CDF) of |y - raw| over the
+// fit's training rows, into fit_delta (fits of other losses are skipped)
+int dml_gb_huber_delta(GbGradArgs* a, hipStream_t st) {
+  if (a->A <= 0 || a->n <= 0) return 0;
+  if (!a->fit_train || !a->sel_hist || !a->sel_state || !a->fit_alpha || !a->fit_delta || !a->yreg) return 2;
+  const dim3 grid((unsigned)((a->n + kSelRows - 1) / kSelRows), (unsigned)a->A);
+  k_sel_init<<<(unsigned)((a->A + 255) / 256), 256, 0, st>>>((unsigned long long*)a->sel_state, a->A);
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    k_sel_fit<<<grid, 256, 0, st>>>(*a, shift);
+    k_sel_pick<<<(unsigned)a->A, 64, 0, st>>>((unsigned long long*)a->sel_state, (unsigned int*)a->sel_hist,
+                                             (const double*)a->fit_alpha, a->A, 1, shift);
+  }
+  k_sel_delta<<<(unsigned)((a->A + 255) / 256), 256, 0, st>>>(*a);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

@@ -362,8 +362,14 @@ class GradientBoostingFamily(Family):
         train_idx = [torch.nonzero(train[f]).squeeze(1) for f in range(F)]
         # fused HIP stage (csrc/kernels/gbrt.hip): gradient, leaf line search and raw update as
         # three kernels per stage instead of torch glue (losses with sums-only line searches)
+        # percentile losses (absolute_error / huber / quantile) run fused too: leaf percentiles and
+        # huber's delta by the exact radix select of gbrt.hip (early stopping keeps the torch path:
+        # its validation loss needs huber's delta on the host every stage)
+        pct = (LOSS_ABS, LOSS_HUBER, LOSS_QUANT)
         fused = (gpu and not sharded and os.environ.get("DML_GB_FUSED", "1") != "0" and K <= 64
-                 and all(t.params["loss"] in (LOSS_SQ, LOSS_LOG, LOSS_EXP) for t in batch)
+                 and all(t.params["loss"] in (LOSS_SQ, LOSS_LOG, LOSS_EXP) or
+                         (t.params["loss"] in pct and not clf and not t.params.get("n_iter_no_change"))
+                         for t in batch)
                  and max(t.params["max_depth"] for t in batch) <= 8
                  and getattr(native.hip_lib(), "dml_gb_stage", None) is not None)
         if fused:
@@ -376,6 +382,13 @@ class GradientBoostingFamily(Family):
             yreg64 = torch.zeros(1, dtype=torch.float64, device=dev) if clf else yreg.contiguous()
             loss_all = np.array([t.params["loss"] for t in batch], dtype=np.int32)   # LOSS_* == gbrt.hip GbLoss
             lr_all = np.array([t.params["learning_rate"] for t in batch], dtype=np.float64)
+            pct_any = bool(np.isin(loss_all, pct).any())
+            alpha_all = np.array([float(t.params.get("alpha", 0.9)) for t in batch], dtype=np.float64)
+            if pct_any:   # select scratch: leaf slot per (tree, row), byte counters (kept zero), states
+                slot_of = torch.empty((F * K, n), dtype=torch.int16, device=dev)
+                sel_hist = torch.zeros(max(F * K * S, F) * 256, dtype=torch.int32, device=dev)
+                sel_state = torch.empty(max(F * K * S, F) * 4, dtype=torch.int64, device=dev)
+                fit_delta = torch.zeros(F, dtype=torch.float64, device=dev)
         if sharded:   # the global training rows (ascending), for subsample draws equal on every rank
             cnts = [data.all_gather_equal(torch.tensor([int(ti.numel())], device=dev)).cpu().numpy() for ti in train_idx]
             gtrain = [data._gather_rows(ti + data.r0, c) for ti, c in zip(train_idx, cnts)]
@@ -400,6 +413,11 @@ class GradientBoostingFamily(Family):
                     cst["tree_raw"] = torch.from_numpy(j_fit * K + np.tile(np.arange(K, dtype=np.int32), A)).to(dev)
                     cst["tree_loss"] = torch.from_numpy(loss_all[j_fit]).to(dev)
                     cst["tree_lr"] = torch.from_numpy(lr_all[j_fit]).to(dev)
+                    if pct_any:
+                        cst["fit_alpha"] = torch.from_numpy(alpha_all[act_np]).to(dev)
+                        cst["tree_q"] = torch.from_numpy(np.where(loss_all[j_fit] == LOSS_QUANT, alpha_all[j_fit],
+                                                                  0.5)).to(dev)
+                        cst["fit_train"] = train[torch.from_numpy(act_np).to(dev).long()].to(torch.uint8).contiguous()
             act_t = cst["act_t"]
             loss = [batch[f].params["loss"] for f in act]
             hub_delta: Dict[int, float] = {}
@@ -408,6 +426,14 @@ class GradientBoostingFamily(Family):
                 ga = native.GbGradArgs(n=n, K=K, A=A, fit_raw=native.ptr(fit_raw), fit_loss=native.ptr(fit_loss),
                                        raw=native.ptr(raw), ycls=native.ptr(ycls32), yreg=native.ptr(yreg64),
                                        grad=native.ptr(G64), tgt=native.ptr(T32))
+                if pct_any:
+                    ga.fit_alpha, ga.fit_delta = native.ptr(cst["fit_alpha"]), native.ptr(fit_delta)
+                    ga.fit_train, ga.sel_hist, ga.sel_state = (native.ptr(cst["fit_train"]), native.ptr(sel_hist),
+                                                               native.ptr(sel_state))
+                    if LOSS_HUBER in loss_all[act]:   # delta = alpha percentile of |y - raw| over training rows
+                        rc = lib.dml_gb_huber_delta(ctypes.byref(ga), stream)
+                        if rc:
+                            raise RuntimeError(f"dml_gb_huber_delta failed ({rc})")
                 rc = lib.dml_gb_grad(ctypes.byref(ga), stream)
                 if rc:
                     raise RuntimeError(f"dml_gb_grad failed ({rc})")
@@ -505,6 +531,10 @@ class GradientBoostingFamily(Family):
                                         slot_sum=native.ptr(slot_sum), slot_node=native.ptr(slot_node),
                                         slot_val=native.ptr(slot_val), raw=native.ptr(raw),
                                         XbT=native.ptr(xbt) if xbt is not None else 0)
+                if pct_any:
+                    sa.pct_any, sa.yreg, sa.slot_of = 1, native.ptr(yreg64), native.ptr(slot_of)
+                    sa.sel_hist, sa.sel_state = native.ptr(sel_hist), native.ptr(sel_state)
+                    sa.tree_q, sa.tree_delta = native.ptr(cst["tree_q"]), native.ptr(fit_delta)
                 rc = lib.dml_gb_stage(ctypes.byref(sa), stream)
                 if rc:
                     raise RuntimeError(f"dml_gb_stage failed ({rc})")

@@ -201,15 +201,26 @@ def config5(dev):
     ctl.shutdown()
 
 
-def config6(dev):
+def config6(dev, loss=None):
+    """Config 6: GradientBoostingClassifier GridSearchCV (4 points x cv5) on 1M x 100; with
+    ``loss`` (e.g. huber): the same grid as a GradientBoostingRegressor of that loss on a
+    continuous target of the same table (the percentile-loss stage kernels)."""
+    from cs230_distributed_machine_learning_amd.data.device import DeviceData
     from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
     from cs230_distributed_machine_learning_amd.search.grid import expand_candidates
     from cs230_distributed_machine_learning_amd.utils import trace
 
     dd = _synthetic(1_000_000, 100, dev)
     grid = {"n_estimators": [100, 200], "max_depth": [3, 5]}
+    model = "GradientBoostingClassifier"
+    if loss:
+        g = torch.Generator(device=dev).manual_seed(5)
+        yr = dd.X[:, :10].sum(1) + 0.5 * torch.randn(dd.n, device=dev, generator=g)
+        dd = DeviceData(dd.X, yr.float(), classification=False, device=dev, name="synthetic-reg-1Mx100")
+        grid["loss"] = [loss]
+        model = "GradientBoostingRegressor"
     cands = expand_candidates("GridSearchCV", {"param_grid": grid})
-    spec = JobSpec("GradientBoostingClassifier", cands, cv=5, holdout=False, keep_models="none")
+    spec = JobSpec(model, cands, cv=5, holdout=False, keep_models="none")
     dd.binned()
     torch.cuda.synchronize(dev) if dev.type == "cuda" else None
     trace.summary(reset=True)
@@ -227,6 +238,7 @@ def main():
     ap.add_argument("--configs", default="1,2,4,5")
     ap.add_argument("--lr-rows", type=int, default=2_000_000)
     ap.add_argument("--gpus", type=int, default=1, help="config 5 on N ranks (relaunches under torchrun)")
+    ap.add_argument("--gb-loss", default=None, help="config 6 as a GradientBoostingRegressor of this loss")
     args = ap.parse_args()
     if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         import subprocess
@@ -246,7 +258,7 @@ def main():
     if 5 in want:
         config5(dev)
     if 6 in want:
-        config6(dev)
+        config6(dev, args.gb_loss)
 
 
 if __name__ == "__main__":

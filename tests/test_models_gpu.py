@@ -98,14 +98,21 @@ def test_gbrt_gpu_close_to_cpu(model, clf, loss):
         np.testing.assert_allclose(out["cuda:0"], out["cpu"], atol=5e-3)
 
 
-@pytest.mark.parametrize("model,n_classes,loss", [("GradientBoostingClassifier", 3, "log_loss"),
-                                                  ("GradientBoostingClassifier", 2, "exponential"),
-                                                  ("GradientBoostingClassifier", 2, "log_loss"),
-                                                  ("GradientBoostingRegressor", 0, "squared_error")])
-def test_gbrt_fused_stage_matches_torch_stage(model, n_classes, loss, monkeypatch, tmp_path):
-    """The fused HIP stage (gbrt.hip: gradient, leaf line search, raw update) against the
-    torch stage on the same device: same CV scores, and -- with the models kept (the refit
-    path) -- the same predictions from the stored artefacts."""
+@pytest.mark.parametrize("model,n_classes,loss,extra", [
+    ("GradientBoostingClassifier", 3, "log_loss", {}),
+    ("GradientBoostingClassifier", 2, "exponential", {}),
+    ("GradientBoostingClassifier", 2, "log_loss", {}),
+    ("GradientBoostingRegressor", 0, "squared_error", {}),
+    ("GradientBoostingRegressor", 0, "absolute_error", {}),
+    ("GradientBoostingRegressor", 0, "huber", {"alpha": [0.8]}),
+    ("GradientBoostingRegressor", 0, "quantile", {"alpha": [0.3]}),
+    ("GradientBoostingRegressor", 0, "absolute_error", {"subsample": [0.6]}),
+    ("GradientBoostingRegressor", 0, "huber", {"subsample": [0.7]})])
+def test_gbrt_fused_stage_matches_torch_stage(model, n_classes, loss, extra, monkeypatch, tmp_path):
+    """The fused HIP stage (gbrt.hip: gradient, leaf line search -- Newton steps, or the exact
+    radix-select leaf percentiles and huber delta -- raw update) against the torch stage on the
+    same device: same CV scores, and -- with the models kept (the refit path) -- the same
+    predictions from the stored artefacts."""
     from cs230_distributed_machine_learning_amd.engine.model_store import load_predictor, save_model
 
     rng = np.random.RandomState(3)
@@ -115,7 +122,7 @@ def test_gbrt_fused_stage_matches_torch_stage(model, n_classes, loss, monkeypatc
     else:
         y = (2 * X[:, 0] + X[:, 1] * X[:, 2] + 0.1 * rng.randn(3000)).astype(np.float32)
     grid = list(ParameterGrid({"n_estimators": [8, 20], "max_depth": [2, 4], "loss": [loss],
-                               "learning_rate": [0.3]}))
+                               "learning_rate": [0.3], **extra}))
     out, preds = {}, {}
     for flag in ("1", "0"):
         monkeypatch.setenv("DML_GB_FUSED", flag)
@@ -126,7 +133,8 @@ def test_gbrt_fused_stage_matches_torch_stage(model, n_classes, loss, monkeypatc
         out[flag] = np.array([r.result["mean_cv_score"] for r in res])
         preds[flag] = [load_predictor(save_model(r.model, str(tmp_path / f"m{flag}_{i}.npz"))).predict(X[:500])
                        for i, r in enumerate(res)]
-    np.testing.assert_allclose(out["1"], out["0"], rtol=0, atol=1e-9 if loss == "squared_error" else 2e-3)
+    exact = loss in ("squared_error", "absolute_error", "quantile", "huber")
+    np.testing.assert_allclose(out["1"], out["0"], rtol=0, atol=1e-9 if exact else 2e-3)
     for a, b in zip(preds["1"], preds["0"]):
         if n_classes:
             assert np.mean(a == b) >= 0.995
