@@ -119,6 +119,19 @@ class DeviceData:
             np.copyto(pin[:r1 - r0].numpy(), Xh[r0:r1], casting="same_kind")
             yield r0, r1, pin[:r1 - r0].to(self.device, non_blocking=False)
 
+    def host_view(self) -> "DeviceData":
+        """A CPU DeviceData over a binned-only table's host rows (same target, classes and
+        name): the host solvers of families without a streamed or binned fit (SVC/SVR) train
+        on it.  Made once per table; the caller sets its splits (executor.prepare_splits)."""
+        if not self.can_stream_rows():
+            raise ValueError("no host rows (the table is resident or was received as bins)")
+        hv = getattr(self, "_host_view", None)
+        if hv is None:
+            hv = DeviceData(np.asarray(self._X_host, dtype=np.float32), self.y_host, self.classification, "cpu",
+                            classes=self.classes, name=f"{self.name}@host")
+            self._host_view = hv
+        return hv
+
     # ---- binned copy (trees) -------------------------------------------------------
     def _stream_bin(self, Xh, chunk_rows: int) -> None:
         from ..ops import binning

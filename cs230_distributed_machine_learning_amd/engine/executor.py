@@ -147,8 +147,15 @@ def run_candidates(data, spec: JobSpec, candidate_ids: Sequence[int]) -> List[Ca
         raise ValueError(f"{spec.model_type} needs a numeric target column; this target is categorical")
     streamable = getattr(fam, "streams_rows", False) and getattr(data, "can_stream_rows", lambda: False)()
     if getattr(data, "binned_only", False) and not getattr(fam, "binned_ok", False) and not streamable:
-        raise ValueError(f"{spec.model_type} needs the float32 rows; this table is resident only in binned form "
-                         f"(too large for HBM) -- tree models only")
+        if getattr(fam, "host_ok", False) and getattr(data, "can_stream_rows", lambda: False)():
+            # a family with a host solver (SVC/SVR) fits on the host rows of the table, which the
+            # reference also requires to fit in RAM; same splits, same scorer, CPU predictions
+            data = data.host_view()
+            with trace.range("run_prepare"):
+                names = prepare_splits(data, spec)
+        else:
+            raise ValueError(f"{spec.model_type} needs the float32 rows; this table is resident only in binned "
+                             f"form (too large for HBM) -- tree models only")
     sharded = getattr(data, "is_row_shard", False)
     if sharded and not getattr(fam, "data_parallel", False):
         raise ValueError(f"{spec.model_type} has no row-sharded (data-parallel) fit; run it task-parallel")

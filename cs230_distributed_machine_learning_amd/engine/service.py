@@ -363,7 +363,8 @@ class DeviceCache:
         """Tree jobs on a table too large for HBM as float32 keep only its bins resident."""
         fam = family_of(plan["model_type"])
         if not str(self.device).startswith("cuda") or not (getattr(fam, "binned_ok", False)
-                                                           or getattr(fam, "streams_rows", False)):
+                                                           or getattr(fam, "streams_rows", False)
+                                                           or getattr(fam, "host_ok", False)):
             return False
         import torch
 
@@ -387,7 +388,8 @@ class DeviceCache:
         # entry serves the tree jobs it was made for, and the families that stream its host rows
         full = base + (False,)
         fam = family_of(plan["model_type"])
-        tree_ok = getattr(fam, "binned_ok", False) or getattr(fam, "streams_rows", False)
+        tree_ok = (getattr(fam, "binned_ok", False) or getattr(fam, "streams_rows", False)
+                   or getattr(fam, "host_ok", False))
         for key in ((full, base + (True,)) if tree_ok else (full,)):
             if key in self._items:
                 self._order.remove(key)

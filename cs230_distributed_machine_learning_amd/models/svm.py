@@ -72,6 +72,10 @@ def _ovr_argmax(dec, ti, pairs, m, C, dev) -> torch.Tensor:
 
 class SVMFamily(Family):
     model_types = (_SVC, _SVR)
+    # binned-only tables (float32 rows too large for HBM): the fits run on the host rows with
+    # the host SMO -- the reference trains SVC/SVR on any table that fits in RAM
+    # (aws-prod/worker/worker.py:40,47,406-425); engine/executor.py run_candidates
+    host_ok = True
     classifiers = (_SVC,)
 
     def resolve(self, model_type, params, n_train, n_features, n_classes) -> Dict[str, Any]:

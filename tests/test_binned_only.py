@@ -41,8 +41,6 @@ def _check(dev, n, d, chunk, tmp_path):
     for model, grid in (("RandomForestClassifier", {"n_estimators": [8], "max_depth": [4, None]}),
                         ("GradientBoostingClassifier", {"n_estimators": [5], "max_depth": [2]})):
         assert _scores(res_dd, model, grid) == _scores(bin_dd, model, grid)
-    with pytest.raises(ValueError, match="binned form"):
-        run_candidates(bin_dd, JobSpec("SVC", [{"C": 1.0}], cv=3), [0])
     # KNN: query blocks of held-out rows against streamed candidate chunks, exact merge
     knn_grid = {"n_neighbors": [1, 5, 12], "weights": ["uniform", "distance"], "p": [1, 2]}
     old_q = os.environ.get("DML_KNN_QBLOCK_GB")
@@ -78,6 +76,26 @@ def _check(dev, n, d, chunk, tmp_path):
                         ("PCA", {"n_components": [2, 5]})):
         a, b = _scores(res_r, model, grid), _scores(bin_r, model, grid)
         np.testing.assert_allclose(np.asarray(b), np.asarray(a), rtol=1e-6, atol=1e-6)
+
+
+def test_binned_only_svm_trains_on_host_rows(tmp_path):
+    """SVC / SVR on a binned-only table: the host SMO on the table's host rows (the reference
+    trains them on any table that fits in RAM), the same CV scores as a resident CPU table."""
+    X, y = _table(1200, 6, seed=3)
+    mm = np.lib.format.open_memmap(str(tmp_path / "X.npy"), mode="w+", dtype=np.float32, shape=X.shape)
+    mm[:] = X
+    mm.flush()
+    Xmm = np.load(str(tmp_path / "X.npy"), mmap_mode="r")
+    yr = (X[:, 0] * 2 + X[:, 1]).astype(np.float32)
+    for clf, model, yy in ((True, "SVC", y), (False, "SVR", yr)):
+        res = DeviceData(X, yy, clf, "cpu")
+        binned = DeviceData(Xmm, yy, clf, "cpu", binned_only=True, chunk_rows=500)
+        grid = {"C": [0.5, 2.0]}
+        assert _scores(binned, model, grid) == _scores(res, model, grid)
+    with pytest.raises(ValueError, match="binned form"):   # no host rows (bins received from a peer)
+        nohost = DeviceData(Xmm, y, True, "cpu", binned_only=True)
+        nohost._X_host = None
+        run_candidates(nohost, JobSpec("SVC", [{"C": 1.0}], cv=3), [0])
 
 
 def test_binned_only_cpu_matches_resident(tmp_path):
