@@ -57,6 +57,9 @@
 #ifndef DML_PART_U2
 #define DML_PART_U2 4          // block-tier partition pass 2: row positions per thread per round
 #endif
+#ifndef DML_KGL_LARGE
+#define DML_KGL_LARGE 16       // k_hist_large: widest feature group of the pipelined (and unit-weight) loop
+#endif
 #ifndef DML_PART_KEEP
 #define DML_PART_KEEP 2        // block-tier partition: rounds whose row ids pass 1 keeps in registers (0/1/2: 1.018/1.014/1.009 s sweep build, r5 e6)
 #endif
@@ -2842,14 +2845,14 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
   __syncthreads();
   const uint32_t* rows = c.rows_cur + st.on.start;
   const float* ty = tree_y(c, s);
-  constexpr int KGL = 16;
+  constexpr int KGL = DML_KGL_LARGE;
   // regression tree without bootstrap: every active row weighs 1, so the (w | rows << 32)
   // plane is a row count -- kept as u32 LDS counters (ds_add_u32: half the bytes and bank
   // pairs of the u64 add) in the first KB of each feature's 4-KB slice, widened at the flush
   const bool uw = MODE == 2 && s.bootstrap == 0 && g <= KGL;
   // cached root counts (boosting): the count plane is copied in by k_root_counts, so only the
   // w yq plane is accumulated (one LDS atomic per (row, feature) instead of two)
-  const bool skipc = uw && fround >= 0 && c.root_cnt_skip != 0;
+  const bool skipc = MODE == 2 && s.bootstrap == 0 && fround >= 0 && c.root_cnt_skip != 0;
   if (g <= KGL) {
     // ping-pong software pipeline with compile-time-counted unconditional gathers (the block
     // tier's loop in k_nodes): the row id two steps ahead and the next step's bins are in
@@ -2937,6 +2940,31 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
       else rung(std::false_type{});
     } else {
       rung(std::false_type{});
+    }
+  } else if constexpr (MODE == 2) {
+    // wide groups (g > KGL, e.g. boosting's whole-feature rounds of 24): per row, the bins of 8
+    // features at a time from the row's line, all 8 loads issued before their atomics (the
+    // visiting list is padded to a multiple of 8 with its first feature, so the loads are
+    // unconditional; the atomics stop at g); the count plane is skipped when cached
+    for (int j = g + threadIdx.x; j < ((g + 7) & ~7) && j < 64; j += 256) feats[j] = feats[0];
+    __syncthreads();
+    for (int r = r0 + threadIdx.x; r < r1; r += 256) {
+      const uint32_t wd = rows[r];
+      const uint32_t row = word_row(c, wd);
+      const RegPL p = reg_payload(c, word_weight(c, s, wd), ty[row]);
+      const uint8_t* xr = c.Xb + (int64_t)row * c.ld;
+      for (int j0 = 0; j0 < g; j0 += 8) {
+        uint32_t bb[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) bb[u] = xr[feats[j0 + u]];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (j0 + u >= g) break;
+          CT* hj = hist + (j0 + u) * span;
+          if (!skipc) atomicAdd(&hj[bb[u]], p.wr);
+          atomicAdd(&hj[256 + bb[u]], p.wy);
+        }
+      }
     }
   } else {
     for (int r = r0 + threadIdx.x; r < r1; r += 256) {

@@ -142,10 +142,13 @@ def test_gbrt_fused_stage_matches_torch_stage(model, n_classes, loss, extra, mon
             np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("kg", [None, "24"])
 @pytest.mark.parametrize("model,clf", [("GradientBoostingRegressor", False), ("GradientBoostingClassifier", True)])
-def test_gbrt_root_count_cache_is_exact(model, clf, monkeypatch):
+def test_gbrt_root_count_cache_is_exact(model, clf, kg, monkeypatch):
     """Boosting builds reuse the roots' row-count histograms across stages (they only depend on
     the training rows): the ensembles are identical with and without the cache, one lane or two."""
+    if kg is not None:   # feature groups wider than the pipelined loop's 16: the generic row loop
+        monkeypatch.setenv("DML_TIER_KG_LARGE_REG", kg)
     rng = np.random.RandomState(4)
     X = rng.randn(200_000, 20).astype(np.float32)      # large-tier roots (> block_max rows)
     y = (X[:, 0] + X[:, 1] * X[:, 2] > 0).astype(int) if clf else (X[:, 0] + 0.3 * X[:, 3] ** 2).astype(np.float32)
