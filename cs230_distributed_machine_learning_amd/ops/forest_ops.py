@@ -38,7 +38,8 @@ class ForestTiers:
     sub_small: int = 32        # subtree roots of <= 32 rows: tier 4, half-size LDS row cache (2x per CU)
     sub_cache_max_d: int = 256  # cache the subtree's bin rows in LDS when d <= this
     wave_max: int = 512         # sweeps: profiles/r1_forest_ab_experiments.md, r2_tier_sweep.txt
-    block_max: int = 32768      # r2 kernels (XbT large tier): 32768 beats 131072 by 4 %
+    block_max: int = 65536      # r5 (block tier at 4 WGs/CU): 65536 vs 32768 -1.7 % sweep build, bench +2.6 %
+                                # (profiles/r5_block_max_sweep.txt; r2 kernels: 32768 beat 131072 by 4 %)
     chunk: int = 16384
     # builds whose trees all evaluate every feature (boosting, max_features=None) whose
     # whole-feature large-tier histograms fit DML_LARGE_SUB_GB: nodes above this many rows take
