@@ -26,6 +26,7 @@
 //
 // A leaf is addressed by its PATH SLOT: 1 at the root, 2 s + (went right) per level, so a
 // tree of depth <= D has slots in [1, 2^(D+1)) and per-tree leaf arrays need no node index.
+// Depths up to 10 (S = 2048: 56 KB of leaf-sum LDS per workgroup, uint16 slot ids).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
@@ -58,6 +59,11 @@ struct GbStageArgs {
   int64_t sel_state;          // uint64 [J * S][4] scratch (prefix, mask, rank, count)
   int64_t tree_q;             // double [J]: the leaf percentile (0.5; quantile: alpha)
   int64_t tree_delta;         // double [J]: huber delta of the tree's fit at this stage
+  // 0: the whole stage in one call.  Row-sharded stages run it in phases with all-reduces
+  // between them (models/boosting.py): 1 = leaf sums (every leaf slot of the tree table gets its
+  // node, rows or not: a rank may hold none of a leaf's in-bag rows), 2 = leaf values + raw
+  // update, 3 = huber leaf terms (after the select of dml_gb_sel_step)
+  int64_t phase;
 };
 
 struct GbGradArgs {
@@ -172,7 +178,7 @@ __global__ __launch_bounds__(256) void k_gb_leafsums(GbStageArgs a) {
   double* ss = GB_PTR(double, a.slot_sum) + (int64_t)j * S * 2;
   int32_t* sn = GB_PTR(int32_t, a.slot_node) + (int64_t)j * S;
   for (int i = threadIdx.x; i < S; i += 256) {
-    if (!hit[i]) continue;
+    if (!hit[i] && !(a.phase != 0 && tsplit[i] < 0 && tnode[i] >= 0)) continue;
     sn[i] = tnode[i];
     if (newton) {
       atomicAdd(&ss[2 * i], num[i]);
@@ -533,6 +539,7 @@ int dml_gb_sizeof_grad_args() { return (int)sizeof(GbGradArgs); }
 // leaf sums + leaf values + raw update of one stage (slot_sum / slot_node zeroed / -1 by the caller)
 int dml_gb_stage(GbStageArgs* a, hipStream_t st) {
   if (a->J <= 0 || a->n <= 0) return 0;
+  if (a->phase != 0) return 2;
   const dim3 grid((unsigned)((a->n + 1023) / 1024), (unsigned)a->J);
   switch (a->S) {
 #define GB_CASE(SV)                                                                   \
@@ -545,9 +552,68 @@ int dml_gb_stage(GbStageArgs* a, hipStream_t st) {
       k_gb_values<<<(unsigned)((a->J * SV + 255) / 256), 256, 0, st>>>(*a);           \
       k_gb_update<SV><<<grid, 256, 0, st>>>(*a);                                      \
       break;
-    GB_CASE(4) GB_CASE(8) GB_CASE(16) GB_CASE(32) GB_CASE(64) GB_CASE(128) GB_CASE(256) GB_CASE(512)
+    GB_CASE(4) GB_CASE(8) GB_CASE(16) GB_CASE(32) GB_CASE(64) GB_CASE(128) GB_CASE(256) GB_CASE(512) GB_CASE(1024)
+    GB_CASE(2048)
 #undef GB_CASE
     default: return 2;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// one phase of a row-sharded stage (GbStageArgs::phase 1..3; the caller all-reduces between)
+int dml_gb_stage_phase(GbStageArgs* a, hipStream_t st) {
+  if (a->J <= 0 || a->n <= 0) return 0;
+  if (a->phase < 1 || a->phase > 3) return 2;
+  const dim3 grid((unsigned)((a->n + 1023) / 1024), (unsigned)a->J);
+  switch (a->S) {
+#define GB_CASE(SV)                                                                   \
+    case SV:                                                                          \
+      if (a->phase == 1) k_gb_leafsums<SV><<<grid, 256, 0, st>>>(*a);                 \
+      if (a->phase == 3) k_gb_huber_terms<SV><<<grid, 256, 0, st>>>(*a);              \
+      if (a->phase == 2) {                                                            \
+        k_gb_values<<<(unsigned)((a->J * SV + 255) / 256), 256, 0, st>>>(*a);         \
+        k_gb_update<SV><<<grid, 256, 0, st>>>(*a);                                    \
+      }                                                                               \
+      break;
+    GB_CASE(4) GB_CASE(8) GB_CASE(16) GB_CASE(32) GB_CASE(64) GB_CASE(128) GB_CASE(256) GB_CASE(512) GB_CASE(1024)
+    GB_CASE(2048)
+#undef GB_CASE
+    default: return 2;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// one step of the (tree, leaf) percentile select of a row-sharded stage: which = 0 clears the
+// states, 1 counts this rank's byte `shift` into sel_hist (the caller then all-reduces it),
+// 2 picks the byte from the summed counts (and clears them)
+int dml_gb_sel_step(GbStageArgs* a, int which, int shift, hipStream_t st) {
+  if (a->J <= 0) return 0;
+  if (!a->slot_of || !a->sel_hist || !a->sel_state || !a->tree_q || !a->yreg) return 2;
+  if (shift < 0 || shift > 56 || (shift & 7)) return 2;
+  const int64_t nseg = a->J * a->S;
+  if (which == 0) {
+    k_sel_init<<<(unsigned)((nseg + 255) / 256), 256, 0, st>>>((unsigned long long*)a->sel_state, nseg);
+  } else if (which == 1) {
+    if (a->n > 0) {
+      const dim3 gsel((unsigned)((a->n + kSelRows - 1) / kSelRows), (unsigned)a->J);
+      if (a->S <= 64) {
+        switch (a->S) {
+          case 4: k_sel_leaf<4><<<gsel, 256, 0, st>>>(*a, shift); break;
+          case 8: k_sel_leaf<8><<<gsel, 256, 0, st>>>(*a, shift); break;
+          case 16: k_sel_leaf<16><<<gsel, 256, 0, st>>>(*a, shift); break;
+          case 32: k_sel_leaf<32><<<gsel, 256, 0, st>>>(*a, shift); break;
+          case 64: k_sel_leaf<64><<<gsel, 256, 0, st>>>(*a, shift); break;
+          default: return 2;
+        }
+      } else {
+        k_sel_leaf<0><<<gsel, 256, 0, st>>>(*a, shift);
+      }
+    }
+  } else if (which == 2) {
+    k_sel_pick<<<(unsigned)nseg, 64, 0, st>>>((unsigned long long*)a->sel_state, (unsigned int*)a->sel_hist,
+                                             (const double*)a->tree_q, nseg, a->S, shift);
+  } else {
+    return 2;
   }
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
@@ -565,6 +631,28 @@ int dml_gb_huber_delta(GbGradArgs* a, hipStream_t st) {
                                              (const double*)a->fit_alpha, a->A, 1, shift);
   }
   k_sel_delta<<<(unsigned)((a->A + 255) / 256), 256, 0, st>>>(*a);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// one step of the huber-delta select of a row-sharded stage (which: 0 init, 1 count this rank's
+// rows, 2 pick from the all-reduced counts, 3 write fit_delta)
+int dml_gb_fit_sel_step(GbGradArgs* a, int which, int shift, hipStream_t st) {
+  if (a->A <= 0) return 0;
+  if (!a->fit_train || !a->sel_hist || !a->sel_state || !a->fit_alpha || !a->fit_delta || !a->yreg) return 2;
+  if (shift < 0 || shift > 56 || (shift & 7)) return 2;
+  if (which == 0) {
+    k_sel_init<<<(unsigned)((a->A + 255) / 256), 256, 0, st>>>((unsigned long long*)a->sel_state, a->A);
+  } else if (which == 1) {
+    if (a->n > 0)
+      k_sel_fit<<<dim3((unsigned)((a->n + kSelRows - 1) / kSelRows), (unsigned)a->A), 256, 0, st>>>(*a, shift);
+  } else if (which == 2) {
+    k_sel_pick<<<(unsigned)a->A, 64, 0, st>>>((unsigned long long*)a->sel_state, (unsigned int*)a->sel_hist,
+                                             (const double*)a->fit_alpha, a->A, 1, shift);
+  } else if (which == 3) {
+    k_sel_delta<<<(unsigned)((a->A + 255) / 256), 256, 0, st>>>(*a);
+  } else {
+    return 2;
+  }
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

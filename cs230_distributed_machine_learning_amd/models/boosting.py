@@ -32,7 +32,7 @@ import math
 import os
 import threading
 import time
-from typing import Any, Dict, List
+from typing import Any, Dict, List, Optional
 
 import numpy as np
 import torch
@@ -81,6 +81,55 @@ def _max_features(v, d):
 
 
 # ---- percentiles (numpy 'linear' for the initial estimate, sklearn inverted-CDF in leaves) ----
+def sharded_pct_ok() -> bool:
+    """The row-sharded fused stage (phased gbrt.hip entry points) is in the loaded library."""
+    try:
+        lib = native.hip_lib()
+    except Exception:
+        return False
+    return all(getattr(lib, f, None) is not None for f in ("dml_gb_stage_phase", "dml_gb_sel_step",
+                                                           "dml_gb_fit_sel_step"))
+
+
+def _radix_select(step, args, stream, data, hist: torch.Tensor, finish: int = -1) -> None:
+    """The exact 8-pass radix select of gbrt.hip over every rank's rows: each pass counts this
+    rank's keys' next byte, the counters are summed over the ranks, and every rank picks the
+    same byte from the sums (so all ranks hold the same percentile)."""
+    def call(which, shift):
+        rc = step(ctypes.byref(args), which, shift, stream)
+        if rc:
+            raise RuntimeError(f"gbrt select step {which} failed ({rc})")
+
+    call(0, 56)
+    for shift in range(56, -1, -8):
+        call(1, shift)
+        data.all_reduce(hist)
+        call(2, shift)
+    if finish >= 0:
+        call(finish, 0)
+
+
+def _sharded_stage(lib, sa, stream, data, slot_sum: torch.Tensor, sel_hist: Optional[torch.Tensor], newton: bool,
+                   huber: bool) -> None:
+    """Leaf line search + raw update of a row-sharded stage: the fused kernels in phases, with
+    the per-leaf Newton / huber sums and the percentile select's byte counts all-reduced."""
+    def phase(p):
+        sa.phase = p
+        rc = lib.dml_gb_stage_phase(ctypes.byref(sa), stream)
+        if rc:
+            raise RuntimeError(f"dml_gb_stage_phase({p}) failed ({rc})")
+
+    phase(1)                                         # leaf slots, local Newton sums
+    if sel_hist is not None:                         # leaf percentiles over every rank's rows
+        _radix_select(lib.dml_gb_sel_step, sa, stream, data, sel_hist)
+        if huber:
+            phase(3)                                 # local clipped-deviation sums
+    if newton or huber:
+        data.all_reduce(slot_sum)
+    phase(2)                                         # leaf values + raw update of the local rows
+    sa.phase = 0
+
+
 def _percentile_linear(v: torch.Tensor, q: float) -> torch.Tensor:
     s, _ = torch.sort(v)
     m = s.numel()
@@ -282,6 +331,10 @@ class GradientBoostingFamily(Family):
                     out[:] = lp - lp.mean()
                 return out
             y = data.y_reg[train].double()
+            if loss in (LOSS_ABS, LOSS_HUBER, LOSS_QUANT):   # percentile of the global training targets
+                cnt = data.all_gather_equal(torch.tensor([int(y.numel())], device=y.device)).cpu().numpy()
+                out[0] = _percentile_linear(data._gather_rows(y, cnt), 0.5 if loss != LOSS_QUANT else rp["alpha"])
+                return out
             acc = data.all_reduce(torch.stack([y.sum(), torch.tensor(float(y.numel()), dtype=torch.float64,
                                                                      device=y.device)]))
             out[0] = acc[0] / acc[1].clamp_min(1)
@@ -319,11 +372,14 @@ class GradientBoostingFamily(Family):
         clf = data.classification
         sharded = getattr(data, "is_row_shard", False)
         if sharded:
-            bad = [t for t in batch if t.params["loss"] in (LOSS_ABS, LOSS_HUBER, LOSS_QUANT) or
-                   t.params.get("n_iter_no_change")]
-            if bad:   # leaf percentiles / the held-out split are not sums over ranks
+            # the held-out early-stopping split is not a sum over ranks; leaf percentiles are,
+            # as byte histograms of the fused stage's radix select (GPU only)
+            bad = [t for t in batch if t.params.get("n_iter_no_change") or
+                   (t.params["loss"] in (LOSS_ABS, LOSS_HUBER, LOSS_QUANT) and not (gpu and sharded_pct_ok()))]
+            if bad:
                 raise ParamError("row-sharded GradientBoosting supports squared_error, log_loss and exponential "
-                                 "losses without n_iter_no_change; run this job task-parallel")
+                                 "losses (and, on GPU, absolute_error / huber / quantile) without "
+                                 "n_iter_no_change; run this job task-parallel")
         # early stopping (n_iter_no_change): sklearn holds out validation_fraction of the
         # fit's training rows (train_test_split, stratified for classifiers, seeded by
         # random_state) and stops when the validation loss has not improved by tol over
@@ -366,12 +422,18 @@ class GradientBoostingFamily(Family):
         # huber's delta by the exact radix select of gbrt.hip (early stopping keeps the torch path:
         # its validation loss needs huber's delta on the host every stage)
         pct = (LOSS_ABS, LOSS_HUBER, LOSS_QUANT)
-        fused = (gpu and not sharded and os.environ.get("DML_GB_FUSED", "1") != "0" and K <= 64
+        # row-sharded stages run the same kernels in phases, with the leaf sums and the select
+        # counters all-reduced between them (_sharded_stage)
+        fused = (gpu and os.environ.get("DML_GB_FUSED", "1") != "0" and K <= 64
                  and all(t.params["loss"] in (LOSS_SQ, LOSS_LOG, LOSS_EXP) or
                          (t.params["loss"] in pct and not clf and not t.params.get("n_iter_no_change"))
                          for t in batch)
-                 and max(t.params["max_depth"] for t in batch) <= 8
-                 and getattr(native.hip_lib(), "dml_gb_stage", None) is not None)
+                 and max(t.params["max_depth"] for t in batch) <= 10   # gbrt.hip: S <= 2048 path slots
+                 and getattr(native.hip_lib(), "dml_gb_stage", None) is not None
+                 and (not sharded or sharded_pct_ok()))
+        if sharded and not fused and any(t.params["loss"] in pct for t in batch):
+            raise ParamError("row-sharded GradientBoosting with absolute_error / huber / quantile losses needs "
+                             "the fused GPU stage (max_depth <= 10); run this job task-parallel")
         if fused:
             lib = native.hip_lib()
             stream = native.stream_handle(dev)
@@ -431,9 +493,12 @@ class GradientBoostingFamily(Family):
                     ga.fit_train, ga.sel_hist, ga.sel_state = (native.ptr(cst["fit_train"]), native.ptr(sel_hist),
                                                                native.ptr(sel_state))
                     if LOSS_HUBER in loss_all[act]:   # delta = alpha percentile of |y - raw| over training rows
-                        rc = lib.dml_gb_huber_delta(ctypes.byref(ga), stream)
-                        if rc:
-                            raise RuntimeError(f"dml_gb_huber_delta failed ({rc})")
+                        if sharded:   # byte counts summed over the ranks' rows between passes
+                            _radix_select(lib.dml_gb_fit_sel_step, ga, stream, data, sel_hist[:A * 256], 3)
+                        else:
+                            rc = lib.dml_gb_huber_delta(ctypes.byref(ga), stream)
+                            if rc:
+                                raise RuntimeError(f"dml_gb_huber_delta failed ({rc})")
                 rc = lib.dml_gb_grad(ctypes.byref(ga), stream)
                 if rc:
                     raise RuntimeError(f"dml_gb_grad failed ({rc})")
@@ -489,7 +554,12 @@ class GradientBoostingFamily(Family):
                     nodes_t = fb.nodes if gpu else torch.from_numpy(fb.nodes)
                     fbt = forest_ops.ForestBuild(nodes_t, fb.vals, fb.n_trees, fb.VC, True, 1)
                     forest_dp.refine_dp(fbt, Xb, roles_t, specs, data.r0, bv, ex, reduce=data.all_reduce)
-                leaf = forest_ops.apply(fb, Xb).long() if gpu else torch.from_numpy(forest_ops.apply(fb, Xb_host)).long()
+                xbt = None
+                if fused:   # the fused stage walks the trees itself
+                    leaf = None
+                else:
+                    leaf = (forest_ops.apply(fb, Xb).long() if gpu
+                            else torch.from_numpy(forest_ops.apply(fb, Xb_host)).long())
                 vals = fb.vals if gpu else torch.from_numpy(fb.vals)
             elif gpu:
                 # feature-major bins: the large tier's gathers of a dense sorted row set coalesce
@@ -535,9 +605,14 @@ class GradientBoostingFamily(Family):
                     sa.pct_any, sa.yreg, sa.slot_of = 1, native.ptr(yreg64), native.ptr(slot_of)
                     sa.sel_hist, sa.sel_state = native.ptr(sel_hist), native.ptr(sel_state)
                     sa.tree_q, sa.tree_delta = native.ptr(cst["tree_q"]), native.ptr(fit_delta)
-                rc = lib.dml_gb_stage(ctypes.byref(sa), stream)
-                if rc:
-                    raise RuntimeError(f"dml_gb_stage failed ({rc})")
+                if sharded:
+                    _sharded_stage(lib, sa, stream, data, slot_sum, sel_hist[:J * S * 256] if pct_any else None,
+                                   newton=bool(np.isin(loss_all[act], (LOSS_LOG, LOSS_EXP)).any()),
+                                   huber=LOSS_HUBER in loss_all[act])
+                else:
+                    rc = lib.dml_gb_stage(ctypes.byref(sa), stream)
+                    if rc:
+                        raise RuntimeError(f"dml_gb_stage failed ({rc})")
                 if keep_models:   # node-indexed leaf values for the kept trees
                     value = torch.zeros(P, dtype=torch.float64, device=dev)
                     ok = slot_node >= 0

@@ -650,19 +650,30 @@ def shard_load_min_bytes() -> int:
     return int(float(os.environ.get("DML_SHARD_LOAD_MIN_MB", "1024")) * (1 << 20))
 
 
-def needs_whole_rows(model_type: str, params: Dict[str, Any]) -> bool:
+def needs_whole_rows(model_type: str, params: Dict[str, Any], gpu: bool = False) -> bool:
     """A candidate the row-sharded builders cannot fit exactly: absolute_error trees need
     per-node weighted medians over every row, and monotonic_cst's node bounds are not part of
     the row-sharded forest builder -- such a job runs task-parallel (never a silently
     different estimator; reference aws-prod/worker/worker.py:45,452 forwards params verbatim).
-    GradientBoosting: leaf percentiles (absolute_error / huber / quantile losses) and the
-    early-stopping validation split are not sums over row shards (models/boosting.py _boost)."""
+    GradientBoosting: the early-stopping validation split is not a sum over row shards; leaf
+    percentiles (absolute_error / huber / quantile losses) are only on GPU workers (``gpu``),
+    where the fused stage's radix select all-reduces its byte counts (models/boosting.py
+    _sharded_stage) for trees of depth <= 10."""
     if model_type.startswith("GradientBoosting"):
-        return (params.get("loss") in ("absolute_error", "lad", "huber", "quantile")
+        pct = params.get("loss") in ("absolute_error", "lad", "huber", "quantile")
+        md = params.get("max_depth", 3)
+        pct_ok = gpu and md is not None and int(md) <= 10
+        return ((pct and not pct_ok)
                 or bool(params.get("n_iter_no_change")) or params.get("monotonic_cst") is not None)
     if not model_type.startswith("RandomForest"):
         return False
     return params.get("criterion") == "absolute_error" or params.get("monotonic_cst") is not None
+
+
+def _sharded_pct_ok() -> bool:
+    from ..models.boosting import sharded_pct_ok
+
+    return sharded_pct_ok()
 
 
 def _binned_only_table(ctl: Controller, plan: Dict[str, Any], X, device) -> bool:
@@ -883,7 +894,9 @@ class DistributedRunner(Runner):
                 return
             data_par = self._data_parallel(plan, len(todo), n_rows, n_feat)
             if data_par:
-                whole = [i for i in todo if needs_whole_rows(plan["model_type"], job.subtasks[i].spec["parameters"])]
+                gpu = getattr(self.core.device, "type", "") == "cuda" and _sharded_pct_ok()
+                whole = [i for i in todo if needs_whole_rows(plan["model_type"], job.subtasks[i].spec["parameters"],
+                                                             gpu=gpu)]
                 if whole:   # never a silently different model: such a job runs task-parallel
                     log.warning("job %s: %d candidate(s) need every row on one rank (absolute_error / "
                                 "monotonic_cst): task-parallel instead of row-sharded", job.job_id, len(whole))

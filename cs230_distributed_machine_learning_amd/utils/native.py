@@ -98,7 +98,7 @@ GbStageArgs = _i64_struct(
     "GbStageArgs",
     ["Xb", "ld", "n", "nodes", "node_val", "J", "K", "S", "tree_raw", "tree_loss", "tree_lr", "inbag", "grad",
      "ycls", "slot_sum", "slot_node", "slot_val", "raw", "XbT", "pct_any", "yreg", "slot_of", "sel_hist", "sel_state",
-     "tree_q", "tree_delta"],
+     "tree_q", "tree_delta", "phase"],
 )
 GbGradArgs = _i64_struct("GbGradArgs", ["n", "K", "A", "fit_raw", "fit_loss", "raw", "ycls", "yreg", "grad", "tgt",
                                         "fit_alpha", "fit_delta", "fit_train", "sel_hist", "sel_state"])
@@ -233,6 +233,9 @@ def _register_optional(lib) -> None:
         "dml_gb_stage": (c_i32, [ctypes.POINTER(GbStageArgs), c_vp]),
         "dml_gb_grad": (c_i32, [ctypes.POINTER(GbGradArgs), c_vp]),
         "dml_gb_huber_delta": (c_i32, [ctypes.POINTER(GbGradArgs), c_vp]),
+        "dml_gb_stage_phase": (c_i32, [ctypes.POINTER(GbStageArgs), c_vp]),
+        "dml_gb_sel_step": (c_i32, [ctypes.POINTER(GbStageArgs), c_i32, c_i32, c_vp]),
+        "dml_gb_fit_sel_step": (c_i32, [ctypes.POINTER(GbGradArgs), c_i32, c_i32, c_vp]),
         "dml_exp_hist": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
         "dml_forest_release_scratch": (c_i32, []),
         "dml_mae_sizeof_args": (c_i32, []),

@@ -195,7 +195,22 @@ def _gpu_rank(rank, world, port, outq):
         sh = RowShard(X[a:b], y_cls, a, True, inf.device)
         lr = _run(sh, X, y_cls, "LogisticRegression", GPU_GRID)
         knn = _run(sh, X, y_cls, "KNeighborsClassifier", KNN_GRID[:2], cv=3)
-        outq.put(("ok", rank, lr, knn))
+        # row-sharded boosting on the fused stage (phased gbrt.hip kernels + all-reduces)
+        lib = native.hip_lib()
+        phase_fn, calls = lib.dml_gb_stage_phase, []
+
+        def counted(*a):
+            calls.append(1)
+            return phase_fn(*a)
+
+        lib.dml_gb_stage_phase = counted
+        Xg, yg_cls, yg_reg = _table(n=12000, d=10, seed=2)
+        a, b = shard_bounds(len(Xg), world, rank)
+        gbc = _run(RowShard(Xg[a:b], yg_cls, a, True, inf.device), Xg, yg_cls, "GradientBoostingClassifier",
+                   GB_GPU_GRID, cv=3)
+        gbr = _run(RowShard(Xg[a:b], yg_reg, a, False, inf.device), Xg, yg_reg, "GradientBoostingRegressor",
+                   GBR_GPU_GRID, cv=3)
+        outq.put(("ok", rank, lr, knn, gbc, gbr, len(calls)))
         dist.destroy()
     except Exception:  # pragma: no cover
         import traceback
@@ -203,6 +218,12 @@ def _gpu_rank(rank, world, port, outq):
         outq.put(("err", rank, traceback.format_exc()))
 
 
+GB_GPU_GRID = [{"n_estimators": 10, "max_depth": 3, "learning_rate": 0.3, "random_state": 1},
+               {"n_estimators": 6, "max_depth": 4, "subsample": 0.7, "random_state": 2}]
+GBR_GPU_GRID = [{"n_estimators": 8, "max_depth": 3, "learning_rate": 0.3, "loss": loss, "random_state": 1}
+                for loss in ("squared_error", "absolute_error", "huber", "quantile")] + \
+               [{"n_estimators": 5, "max_depth": 9, "loss": "huber", "alpha": 0.7, "subsample": 0.8,
+                 "random_state": 4}]
 GPU_GRID = [{"C": c, "solver": "lbfgs", "max_iter": 60} for c in (0.01, 1.0)] + \
            [{"C": 0.3, "solver": "liblinear", "class_weight": "balanced", "max_iter": 60}]
 
@@ -243,6 +264,18 @@ def test_row_sharded_lr_on_gpu_matches_single_process():
                    KNN_GRID[:2], cv=3)
     for (cv_s, hold), (cv_r, hold_r) in zip(o0[3], ref_knn):
         assert np.allclose(cv_s, cv_r, atol=1e-3), (cv_s, cv_r)
+    # row-sharded boosting: the fused stage ran on every rank; same scores on both ranks and
+    # (regression trees from fp32 histograms summed over ranks: near-tie splits may differ)
+    # close to the one-GPU fits
+    assert o0[6] > 0 and o1[6] == o0[6]
+    assert o0[4] == o1[4] and o0[5] == o1[5]
+    Xg, yg_cls, yg_reg = _table(n=12000, d=10, seed=2)
+    ref_gbc = _run(DeviceData(Xg, yg_cls, True, torch.device("cuda:0")), Xg, yg_cls, "GradientBoostingClassifier",
+                   GB_GPU_GRID, cv=3)
+    ref_gbr = _run(DeviceData(Xg, yg_reg, False, torch.device("cuda:0")), Xg, yg_reg, "GradientBoostingRegressor",
+                   GBR_GPU_GRID, cv=3)
+    for (cv_s, hold), (cv_r, hold_r) in zip(o0[4] + o0[5], ref_gbc + ref_gbr):
+        assert np.allclose(cv_s, cv_r, atol=0.02) and abs(hold - hold_r) <= 0.02, (cv_s, cv_r)
 
 
 def test_needs_whole_rows_routes_gbrt_losses_task_parallel():
@@ -255,6 +288,10 @@ def test_needs_whole_rows_routes_gbrt_losses_task_parallel():
     assert needs_whole_rows("GradientBoostingClassifier", {"n_iter_no_change": 5})
     assert needs_whole_rows("GradientBoostingRegressor", {"monotonic_cst": [1, 0]})
     assert not needs_whole_rows("GradientBoostingRegressor", {"loss": "squared_error"})
+    # GPU workers: the fused stage's select all-reduces its byte counts (depth <= 10)
+    assert not needs_whole_rows("GradientBoostingRegressor", {"loss": "huber", "max_depth": 5}, gpu=True)
+    assert needs_whole_rows("GradientBoostingRegressor", {"loss": "quantile", "max_depth": 12}, gpu=True)
+    assert needs_whole_rows("GradientBoostingRegressor", {"loss": "huber", "n_iter_no_change": 3}, gpu=True)
     assert not needs_whole_rows("GradientBoostingClassifier", {"loss": "log_loss", "n_iter_no_change": None})
     assert needs_whole_rows("RandomForestRegressor", {"criterion": "absolute_error"})
     assert not needs_whole_rows("LogisticRegression", {"C": 1.0})

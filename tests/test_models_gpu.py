@@ -107,7 +107,11 @@ def test_gbrt_gpu_close_to_cpu(model, clf, loss):
     ("GradientBoostingRegressor", 0, "huber", {"alpha": [0.8]}),
     ("GradientBoostingRegressor", 0, "quantile", {"alpha": [0.3]}),
     ("GradientBoostingRegressor", 0, "absolute_error", {"subsample": [0.6]}),
-    ("GradientBoostingRegressor", 0, "huber", {"subsample": [0.7]})])
+    ("GradientBoostingRegressor", 0, "huber", {"subsample": [0.7]}),
+    # deep trees: 1024 / 2048 path slots per tree
+    ("GradientBoostingRegressor", 0, "squared_error", {"max_depth": [7, 10]}),
+    ("GradientBoostingRegressor", 0, "quantile", {"max_depth": [9], "alpha": [0.4]}),
+    ("GradientBoostingClassifier", 3, "log_loss", {"max_depth": [10]})])
 def test_gbrt_fused_stage_matches_torch_stage(model, n_classes, loss, extra, monkeypatch, tmp_path):
     """The fused HIP stage (gbrt.hip: gradient, leaf line search -- Newton steps, or the exact
     radix-select leaf percentiles and huber delta -- raw update) against the torch stage on the
@@ -124,12 +128,24 @@ def test_gbrt_fused_stage_matches_torch_stage(model, n_classes, loss, extra, mon
     grid = list(ParameterGrid({"n_estimators": [8, 20], "max_depth": [2, 4], "loss": [loss],
                                "learning_rate": [0.3], **extra}))
     out, preds = {}, {}
+    from cs230_distributed_machine_learning_amd.utils import native
+
+    lib = native.hip_lib()
+    stage_fn, calls = lib.dml_gb_stage, []
+
+    def counted(*args):
+        calls.append(1)
+        return stage_fn(*args)
+
+    monkeypatch.setattr(lib, "dml_gb_stage", counted, raising=False)
     for flag in ("1", "0"):
         monkeypatch.setenv("DML_GB_FUSED", flag)
+        n0 = len(calls)
         dd = _dd(X, y, bool(n_classes), "cuda:0", cv=3)
         spec = JobSpec(model, grid, cv=3, holdout=True, test_size=0.2, random_state=0, keep_models="all")
         res = run_candidates(dd, spec, range(len(grid)))
         assert all(r.ok for r in res), [r.error for r in res]
+        assert (len(calls) > n0) == (flag == "1")   # the fused stage ran exactly when enabled
         out[flag] = np.array([r.result["mean_cv_score"] for r in res])
         preds[flag] = [load_predictor(save_model(r.model, str(tmp_path / f"m{flag}_{i}.npz"))).predict(X[:500])
                        for i, r in enumerate(res)]
