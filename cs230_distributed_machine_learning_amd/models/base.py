@@ -145,6 +145,43 @@ def as_float(v, name, lo=None, hi=None, allow_none=False):
     return v
 
 
+def prefix_groups(tasks: Sequence[FitTask], ok=None):
+    """Exact sharing of ensemble prefixes inside one batch of fits.
+
+    Fits that differ only in ``n_estimators``, on the same split, with an explicit
+    ``random_state``, grow the SAME first trees / stages: tree j's seed depends only on the
+    random state and j (forest.py ``native_seed``; boosting draws its subsamples and feature
+    orders from the same seeded generators stage by stage), exactly as sklearn's estimators
+    with a fixed random_state do.  Only the longest fit of such a group (the leader) is
+    grown; every shorter one (a follower) is scored from the leader's first n_estimators
+    trees / stages -- the same model, bit for bit, as growing it alone.  ``ok(task)`` excludes
+    fits whose later stages change earlier results (early stopping).  DML_PREFIX_SHARE=0
+    turns the sharing off.  Returns (leaders in input order, {leader task_id: followers}).
+    The reference grows every candidate separately (aws-prod/worker/worker.py:315-341)."""
+    import os
+
+    if os.environ.get("DML_PREFIX_SHARE", "1") == "0":
+        return list(tasks), {}
+    groups: Dict[Any, List[FitTask]] = {}
+    for t in tasks:
+        p = t.params
+        if p.get("seed") is None or "n_estimators" not in p or (ok is not None and not ok(t)):
+            key: Any = ("solo", t.task_id)
+        else:
+            key = (t.split, t.model_type, t.need_proba,
+                   repr(sorted((k, repr(v)) for k, v in p.items() if k not in ("n_estimators", "warnings"))))
+        groups.setdefault(key, []).append(t)
+    leaders, follow = [], {}
+    for g in groups.values():
+        g = sorted(g, key=lambda t: t.params["n_estimators"] if "n_estimators" in t.params else 0)
+        leaders.append(g[-1])
+        if len(g) > 1:
+            follow[g[-1].task_id] = g[:-1]
+    order = {t.task_id: i for i, t in enumerate(tasks)}
+    leaders.sort(key=lambda t: order[t.task_id])
+    return leaders, follow
+
+
 def seed_of(random_state) -> Optional[int]:
     """random_state on the wire: int, None, or a str(RandomState) -> None."""
     if random_state is None:

@@ -40,7 +40,8 @@ import torch
 from ..ops import forest_ops
 from ..search import cv as cv_mod
 from ..utils import native
-from .base import Family, FitOutput, FitTask, ParamError, as_bool, as_float, as_int, register, seed_of
+from .base import (Family, FitOutput, FitTask, ParamError, as_bool, as_float, as_int, prefix_groups, register,
+                   seed_of)
 from .forest import _count_param, _refine, native_seed
 
 _CLS = "GradientBoostingClassifier"
@@ -245,12 +246,17 @@ class GradientBoostingFamily(Family):
         if getattr(data, "is_row_shard", False):   # every rank must cut the same batches
             budget = float(data.all_reduce(torch.tensor([budget], dtype=torch.float64, device=data.device), "min")[0])
         cap = max(1, int(budget // max(1.0, per_fit)))
-        outs: List[FitOutput] = []
-        for i in range(0, len(tasks), cap):
-            outs.extend(self._boost_lanes(data, tasks[i:i + cap], K, keep_models))
-        return outs
+        # fits differing only in n_estimators (explicit random_state, no early stopping): the
+        # longest one is boosted, the shorter ones are its stage prefixes (models/base.py)
+        leaders, follow = prefix_groups(tasks, ok=lambda t: not t.params.get("n_iter_no_change"))
+        outs: Dict[int, FitOutput] = {}
+        for i in range(0, len(leaders), cap):
+            for o in self._boost_lanes(data, leaders[i:i + cap], K, keep_models, follow):
+                outs[o.task_id] = o
+        return [outs[t.task_id] for t in tasks]
 
-    def _boost_lanes(self, data, batch: List[FitTask], K: int, keep_models: bool) -> List[FitOutput]:
+    def _boost_lanes(self, data, batch: List[FitTask], K: int, keep_models: bool,
+                     follow: Optional[Dict[int, List[FitTask]]] = None) -> List[FitOutput]:
         """A device batch split over build LANES (DML_GB_LANES, default 2): each lane boosts its
         share of the fits from its own host thread on its own stream.  A stage is a chain of
         short launches with a host read-back per tree level; with one lane the GPU idles during
@@ -259,7 +265,7 @@ class GradientBoostingFamily(Family):
         lanes = max(1, min(4, int(os.environ.get("DML_GB_LANES", "2"))))
         if (not data.is_gpu or getattr(data, "is_row_shard", False) or lanes < 2 or len(batch) < 2
                 or getattr(native.hip_lib(), "dml_forest_set_lane", None) is None):
-            return self._boost(data, batch, K, keep_models)
+            return self._boost(data, batch, K, keep_models, follow)
         lanes = min(lanes, len(batch))
         # longest-processing-time split of the fits (stage count x depth x trees per stage)
         w = [t.params["n_estimators"] * max(1, min(t.params["max_depth"], 12)) for t in batch]
@@ -286,7 +292,7 @@ class GradientBoostingFamily(Family):
                 forest_ops.set_build_lane(li)
                 streams[li].wait_stream(main)
                 with torch.cuda.device(dev), torch.cuda.stream(streams[li]):
-                    results[li] = self._boost(data, [batch[i] for i in groups[li]], K, keep_models)
+                    results[li] = self._boost(data, [batch[i] for i in groups[li]], K, keep_models, follow)
             except BaseException as e:   # re-raised on the caller's thread
                 errors[li] = e
             finally:
@@ -304,11 +310,7 @@ class GradientBoostingFamily(Family):
         for e in errors:
             if e is not None:
                 raise e
-        outs: List[Any] = [None] * len(batch)
-        for g, res in zip(groups, results):
-            for i, o in zip(g, res):
-                outs[i] = o
-        return outs
+        return [o for res in results for o in res]   # leaders and their prefix fits (run orders them)
 
     # ------------------------------------------------------------------------------------
     def _init_raw(self, data, t: FitTask, train: torch.Tensor, K: int) -> torch.Tensor:
@@ -361,8 +363,17 @@ class GradientBoostingFamily(Family):
             out[0] = _percentile_linear(y, rp["alpha"])
         return out
 
-    def _boost(self, data, batch: List[FitTask], K: int, keep_models: bool) -> List[FitOutput]:
+    def _boost(self, data, batch: List[FitTask], K: int, keep_models: bool,
+               follow: Optional[Dict[int, List[FitTask]]] = None) -> List[FitOutput]:
         t0 = time.perf_counter()
+        # prefix fits (prefix_groups): raw scores of leader f after its first m stages
+        follow = follow or {}
+        checkpoints: Dict[int, Dict[int, List[FitTask]]] = {}
+        for f, t in enumerate(batch):
+            for fo in follow.get(t.task_id, []):
+                checkpoints.setdefault(f, {}).setdefault(fo.params["n_estimators"], []).append(fo)
+        keep_fit = [t.keep or any(fo.keep for fo in follow.get(t.task_id, [])) for t in batch]
+        snaps: List[Any] = []
         dev, n, gpu = data.device, data.n, data.is_gpu
         F = len(batch)
         Xb = data.binned()
@@ -637,13 +648,23 @@ class GradientBoostingFamily(Family):
                 vals_np = value.cpu().numpy()
                 nodes_np = fb.nodes.cpu().numpy() if isinstance(fb.nodes, torch.Tensor) else fb.nodes
                 for a, f in enumerate(act):
-                    if not batch[f].keep:
+                    if not keep_fit[f]:
                         continue
                     lr_f = float(lr[f])
                     kept[f].append([_extract_tree(nodes_np, vals_np * lr_f, a * K + k) for k in range(K)])
+            for f in act:   # prefix fits that end at this stage
+                for fo in checkpoints.get(f, {}).get(stage + 1, []):
+                    snaps.append((fo, f, raw[f].clone()))
         if gpu:
             torch.cuda.synchronize(dev)
-        return self._outputs(batch, raw, init, kept, data, K, clf, keep_models, time.perf_counter() - t0)
+        dt = time.perf_counter() - t0
+        outs = self._outputs(batch, raw, init, kept, data, K, clf, keep_models, dt)
+        if snaps:
+            outs += self._outputs([s[0] for s in snaps], torch.stack([s[2] for s in snaps]),
+                                  torch.stack([init[s[1]] for s in snaps]),
+                                  [kept[s[1]][:s[0].params["n_estimators"]] for s in snaps], data, K, clf,
+                                  keep_models, dt)
+        return outs
 
     @staticmethod
     def _line_search(batch, act, loss, vals, leaf_of, roles_t, G, R, Y, ybin, yreg, K, J, n, P, hub_delta, sharded,

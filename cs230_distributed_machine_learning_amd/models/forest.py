@@ -30,14 +30,15 @@ from __future__ import annotations
 import math
 import os
 import time
-from typing import Any, Dict, List
+from typing import Any, Dict, List, Optional
 
 import numpy as np
 import torch
 
 from ..ops import forest_ops
 from ..utils import native, trace
-from .base import Family, FitOutput, FitTask, ParamError, as_bool, as_float, as_int, register, seed_of
+from .base import (Family, FitOutput, FitTask, ParamError, as_bool, as_float, as_int, prefix_groups, register,
+                   seed_of)
 
 _CLS = "RandomForestClassifier"
 _REG = "RandomForestRegressor"
@@ -289,6 +290,11 @@ class ForestFamily(Family):
                                      "run this job with parallelism='task'")
         # absolute_error trees grow on their own builder (forest_mae.hip / forest_cpu.cpp): batch them apart
         tasks_in = tasks
+        # fits differing only in n_estimators with an explicit random_state grow the same first
+        # trees: only the largest is grown, the others predict from its first trees (base.py)
+        follow: Dict[int, List[FitTask]] = {}
+        if not sharded:
+            tasks, follow = prefix_groups(tasks)
         tasks = sorted(tasks, key=_host_only)
         with trace.range("forest_budget"):
             budget = self._budget(data)
@@ -340,7 +346,7 @@ class ForestFamily(Family):
                   f"{[len(b) for b in batches]}", file=sys.stderr, flush=True)
         for batch in batches:
             with trace.range("forest_batch"):
-                out_b = self._run_batch(data, Xb, batch, is_reg, keep_models, tree_chunk)
+                out_b = self._run_batch(data, Xb, batch, is_reg, keep_models, tree_chunk, follow)
             for o in out_b:
                 outs[o.task_id] = o
         return [outs[t.task_id] for t in tasks_in]
@@ -434,7 +440,8 @@ class ForestFamily(Family):
         return make, done
 
     def _run_batch(self, data, Xb, batch: List[FitTask], is_reg: bool, keep_models: bool,
-                   tree_chunk: int | None = None) -> List[FitOutput]:
+                   tree_chunk: int | None = None, follow: Optional[Dict[int, List[FitTask]]] = None
+                   ) -> List[FitOutput]:
         specs = self._specs(batch)
         cw = self.class_weight_table(data, batch, specs)
         t0 = time.perf_counter()
@@ -525,6 +532,23 @@ class ForestFamily(Family):
                 if keep_models and t.keep:
                     o.model = extract_forest(fb, int(toff[f]), int(toff[f + 1]), data, t)
                 outs.append(o)
+                for fo in (follow or {}).get(t.task_id, []):   # prefix fits: leader f's first m trees
+                    m = int(fo.params["n_estimators"])
+                    toff_f = np.array([toff[f], toff[f] + m], dtype=np.int64)
+                    roff_f = np.array([0, int(rows[f].numel())], dtype=np.int64)
+                    if data.is_gpu:
+                        pf = forest_ops.predict(fb, Xb, toff_f, roff_f, rows[f], want_proba=want_proba)
+                    else:
+                        pf = forest_ops.predict(fb, Xb.numpy(), toff_f, roff_f, rows[f].numpy(), want_proba=want_proba)
+                        pf = ((torch.from_numpy(pf[0]), torch.from_numpy(pf[1])) if want_proba
+                              else torch.from_numpy(pf))
+                    pf, prf = pf if want_proba else (pf, None)
+                    of = FitOutput(task_id=fo.task_id, pred=pf, proba=prf, fit_seconds=dt * m / total_trees,
+                                   info={"warnings": fo.params.get("warnings", []), "batch_stats": dict(fb.stats),
+                                         "prefix_of": t.task_id})
+                    if keep_models and fo.keep:
+                        of.model = extract_forest(fb, int(toff[f]), int(toff[f]) + m, data, fo)
+                    outs.append(of)
             return outs
         finally:   # the node pool is an arena slot: free it for the next batch
             forest_ops.release_pool(fb)

@@ -64,12 +64,14 @@ def _synthetic(rows, d, dev, seed=0):
     return DeviceData(X, y, classification=True, device=dev, name=f"synthetic-{rows}x{d}")
 
 
-def config2(dev):
+def config2(dev, random_state=None):
     from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
     from cs230_distributed_machine_learning_amd.search.grid import expand_candidates
 
     dd = _synthetic(1_000_000, 100, dev)
     grid = {"n_estimators": [50, 100, 150, 200], "max_depth": [10, 20, 30, None], "min_samples_leaf": [1, 2, 4, 8]}
+    if random_state is not None:   # fixed seeds: exact n_estimators prefix sharing (models/base.py)
+        grid["random_state"] = [random_state]
     cands = expand_candidates("GridSearchCV", {"param_grid": grid})
     spec = JobSpec("RandomForestClassifier", cands, cv=5, holdout=False, keep_models="none")
     dd.binned()
@@ -81,7 +83,8 @@ def config2(dev):
         assert all(r.ok for r in res)
         done += 5 * len(res)
     torch.cuda.synchronize(dev) if dev.type == "cuda" else None
-    _emit(2, done, time.time() - t0, grid_points=len(cands))
+    _emit(2, done, time.time() - t0, grid_points=len(cands), random_state=random_state,
+          prefix_share=os.environ.get("DML_PREFIX_SHARE", "1") != "0")
 
 
 def config4(dev, rows):
@@ -201,7 +204,7 @@ def config5(dev):
     ctl.shutdown()
 
 
-def config6(dev, loss=None):
+def config6(dev, loss=None, depths=None, estimators=None, random_state=None):
     """Config 6: GradientBoostingClassifier GridSearchCV (4 points x cv5) on 1M x 100; with
     ``loss`` (e.g. huber): the same grid as a GradientBoostingRegressor of that loss on a
     continuous target of the same table (the percentile-loss stage kernels)."""
@@ -211,7 +214,9 @@ def config6(dev, loss=None):
     from cs230_distributed_machine_learning_amd.utils import trace
 
     dd = _synthetic(1_000_000, 100, dev)
-    grid = {"n_estimators": [100, 200], "max_depth": [3, 5]}
+    grid = {"n_estimators": estimators or [100, 200], "max_depth": depths or [3, 5]}
+    if random_state is not None:
+        grid["random_state"] = [random_state]
     model = "GradientBoostingClassifier"
     if loss:
         g = torch.Generator(device=dev).manual_seed(5)
@@ -230,7 +235,8 @@ def config6(dev, loss=None):
     dt = time.time() - t0
     assert all(r.ok for r in res), [r.error for r in res if not r.ok]
     _emit(6, 5 * len(res), dt, grid_points=len(cands), stages_total=5 * sum(int(c["n_estimators"]) for c in cands),
-          best_mean_cv=round(max(r.result["mean_cv_score"] for r in res), 4), phases=trace.summary())
+          best_mean_cv=round(max(r.result["mean_cv_score"] for r in res), 4), random_state=random_state,
+          prefix_share=os.environ.get("DML_PREFIX_SHARE", "1") != "0", phases=trace.summary())
 
 
 def main():
@@ -239,6 +245,10 @@ def main():
     ap.add_argument("--lr-rows", type=int, default=2_000_000)
     ap.add_argument("--gpus", type=int, default=1, help="config 5 on N ranks (relaunches under torchrun)")
     ap.add_argument("--gb-loss", default=None, help="config 6 as a GradientBoostingRegressor of this loss")
+    ap.add_argument("--gb-depths", default=None, help="config 6 variant: comma-separated max_depth values")
+    ap.add_argument("--gb-estimators", default=None, help="config 6 variant: comma-separated n_estimators values")
+    ap.add_argument("--random-state", type=int, default=None,
+                    help="configs 2 / 6: a fixed random_state in the grid (exact n_estimators prefix sharing)")
     args = ap.parse_args()
     if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         import subprocess
@@ -252,13 +262,14 @@ def main():
     if 1 in want:
         config1()
     if 2 in want:
-        config2(dev)
+        config2(dev, args.random_state)
     if 4 in want:
         config4(dev, args.lr_rows)
     if 5 in want:
         config5(dev)
     if 6 in want:
-        config6(dev, args.gb_loss)
+        ints = lambda v: [int(x) for x in v.split(",")] if v else None
+        config6(dev, args.gb_loss, ints(args.gb_depths), ints(args.gb_estimators), args.random_state)
 
 
 if __name__ == "__main__":
