@@ -96,6 +96,9 @@ def job_plan(request: Dict[str, Any]) -> Dict[str, Any]:
         "holdout": bool(tp.get("holdout", True)),
         "feature_columns": tp.get("feature_columns"), "target_column": tp.get("target_column"),
         "parallelism": par,
+        # the estimator's fixed parameters (J2 merges them into every candidate): the slice
+        # planner reads random_state from them (prefix_units)
+        "base_params": dict(hp.get("base_estimator_params") or {}) if search_type else dict(hp),
     }
 
 
@@ -565,16 +568,41 @@ def presize_for_job(plan: Dict[str, Any], params: List[Dict[str, Any]], dd, slic
         traceback.print_exc()
 
 
+def prefix_units(plan: Dict[str, Any], todo: List[int]) -> List[List[int]]:
+    """Candidates that one device batch can grow as ONE ensemble (models/base.py
+    ``prefix_groups``: forests / boosting differing only in n_estimators, with a fixed
+    random_state, no early stopping) form one scheduling unit, so a slice never splits a group
+    and its cost is the longest member's; every other candidate is a unit of its own."""
+    import os
+
+    mt = plan["model_type"]
+    if not (mt.startswith("RandomForest") or mt.startswith("GradientBoosting")) or \
+            os.environ.get("DML_PREFIX_SHARE", "1") == "0":
+        return [[i] for i in todo]
+    units: Dict[Any, List[int]] = {}
+    for i in todo:
+        c = {**(plan.get("base_params") or {}), **plan["candidates"][i]}
+        if c.get("random_state") in (None, "None") or c.get("n_iter_no_change") not in (None, "None"):
+            key: Any = ("solo", i)
+        else:
+            key = repr(sorted((k, repr(v)) for k, v in c.items() if k != "n_estimators"))
+        units.setdefault(key, []).append(i)
+    return list(units.values())
+
+
 def plan_slices(ctl: Controller, plan: Dict[str, Any], todo: List[int], n_train: int, d: int, n_classes: int,
                 min_slices: int = 1) -> List[List[int]]:
-    """LPT order (most expensive first) cut into ~chunk_target_s slices."""
+    """LPT order (most expensive first) cut into ~chunk_target_s slices, over scheduling units
+    (``prefix_units``: a prefix-sharing group is priced at its longest member)."""
     costs = candidate_costs(plan, n_train, d, n_classes)
-    order = sorted(todo, key=lambda i: -costs[i])
-    est = [ctl.scheduler.estimate(plan["model_type"], costs[i]) for i in order]
+    units = prefix_units(plan, todo)
+    ucost = [max(costs[i] for i in u) for u in units]
+    order = sorted(range(len(units)), key=lambda k: -ucost[k])
+    est = [ctl.scheduler.estimate(plan["model_type"], ucost[k]) for k in order]
     chunk_ids = chunk_units(est, ctl.config.chunk_target_s, min_slices)
     slices: Dict[int, List[int]] = {}
-    for i, c in zip(order, chunk_ids):
-        slices.setdefault(int(c), []).append(i)
+    for k, c in zip(order, chunk_ids):
+        slices.setdefault(int(c), []).extend(units[k])
     return [slices[k] for k in sorted(slices)]
 
 

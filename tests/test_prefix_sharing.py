@@ -108,3 +108,28 @@ def test_prefix_groups_need_a_fixed_random_state():
     finally:
         del os.environ["DML_PREFIX_SHARE"]
     assert base.prefix_groups is prefix_groups
+
+
+def test_slice_planner_keeps_prefix_groups_together():
+    """The runner's slices (engine/service.py plan_slices) never split a prefix group, and a
+    group is priced at its longest member (the work one device batch actually does)."""
+    from types import SimpleNamespace
+
+    from cs230_distributed_machine_learning_amd.engine.service import plan_slices, prefix_units
+    from cs230_distributed_machine_learning_amd.search.grid import expand_candidates
+
+    cands = expand_candidates("GridSearchCV", {"param_grid": {"n_estimators": [50, 100, 150, 200],
+                                                              "max_depth": [4, 8, 12], "min_samples_leaf": [1, 5]}})
+    plan = {"model_type": "RandomForestClassifier", "candidates": cands, "cv": 5, "holdout": False,
+            "base_params": {"random_state": 3}}
+    units = prefix_units(plan, list(range(len(cands))))
+    assert len(units) == 6 and all(len(u) == 4 for u in units)
+    assert all(len({repr({k: v for k, v in cands[i].items() if k != "n_estimators"}) for i in u}) == 1 for u in units)
+    ctl = SimpleNamespace(scheduler=SimpleNamespace(estimate=lambda mt, c: c), config=SimpleNamespace(chunk_target_s=1e-9))
+    slices = plan_slices(ctl, plan, list(range(len(cands))), 10000, 10, 2, min_slices=6)
+    assert sorted(map(sorted, slices)) == sorted(map(sorted, units))
+    # no fixed random_state (or another family): every candidate is its own unit
+    plan["base_params"] = {}
+    assert len(prefix_units(plan, list(range(len(cands))))) == len(cands)
+    assert len(prefix_units(dict(plan, model_type="LogisticRegression", base_params={"random_state": 1}),
+                            [0, 1, 2])) == 3
