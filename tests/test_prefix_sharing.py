@@ -30,7 +30,9 @@ def _fit_all(model, clf, grid, monkeypatch, tmp_path, share, dev="cpu"):
     monkeypatch.setenv("DML_PREFIX_SHARE", "1" if share else "0")
     X, y = _table(clf)
     dd = DeviceData(X, y, clf, dev)
-    spec = JobSpec(model, grid, cv=3, holdout=True, test_size=0.2, random_state=0, keep_models="all")
+    # classifiers scored on probabilities: the prefix fits' predict_proba path too
+    spec = JobSpec(model, grid, cv=3, holdout=True, test_size=0.2, random_state=0, keep_models="all",
+                   scoring="neg_log_loss" if clf else None)
     res = run_candidates(dd, spec, range(len(grid)))
     assert all(r.ok for r in res), [r.error for r in res if not r.ok]
     scores = [r.result["cv_scores"] for r in res]
