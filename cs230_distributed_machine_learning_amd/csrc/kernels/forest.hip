@@ -198,6 +198,10 @@ struct ForestArgs {
   // of an active set, so its count planes never change: root_counts_valid = 0 -> this build's
   // root level stores them, 1 -> the root level skips its count atomics and copies them in
   int64_t root_counts, root_counts_valid;
+  // regression build whose every tree has unit row weights (no bootstrap: boosting): the large
+  // tier's LDS histograms drop the unused half of the count plane (3 KB instead of 4 KB per
+  // feature: 16 features in 48 KB, three workgroups per CU instead of two)
+  int64_t large_unit;
 };
 
 // 0 subtree, 1 wave, 2 block, 3 large, 4 small subtree (<= sub_small rows: the subtree kernel
@@ -263,6 +267,7 @@ struct Ctx {
   int4* pinfo_next;
   int32_t full_cur, full_prev;
   int32_t root_cnt_skip;       // root level of a build with cached root counts: no count atomics
+  int32_t large_compact;       // ForestArgs::large_unit (and kg_large <= DML_KGL_LARGE): 3-KB LDS slices
   uint32_t* root_counts;       // ForestArgs::root_counts (null: none)
   int64_t pi_cap;        // entries of each pinfo table
   // whole-histogram levels: every (large node, visiting position)'s split candidate, from
@@ -1138,18 +1143,21 @@ __device__ __forceinline__ typename PLT<MODE>::T payload_finish(const Ctx& c, co
 }
 
 // large-tier regression, unit row weights: u32 row count in the slice's first KB + the w yq plane
+// (wo: the w yq plane's offset in the slice -- 256, or 128 in the compact 3-KB slices)
 template <int MODE>
-__device__ __forceinline__ void hist_add_unit(typename HT<MODE>::T* hj, int b, const typename PLT<MODE>::T& pl) {
+__device__ __forceinline__ void hist_add_unit(typename HT<MODE>::T* hj, int b, const typename PLT<MODE>::T& pl,
+                                              int wo) {
   if constexpr (MODE == 2) {
     atomicAdd((uint32_t*)hj + b, 1u);
-    atomicAdd(&hj[256 + b], pl.wy);
+    atomicAdd(&hj[wo + b], pl.wy);
   }
 }
 
 // the same with the count plane supplied elsewhere (boosting roots: ForestArgs::root_counts)
 template <int MODE>
-__device__ __forceinline__ void hist_add_wy(typename HT<MODE>::T* hj, int b, const typename PLT<MODE>::T& pl) {
-  if constexpr (MODE == 2) atomicAdd(&hj[256 + b], pl.wy);
+__device__ __forceinline__ void hist_add_wy(typename HT<MODE>::T* hj, int b, const typename PLT<MODE>::T& pl,
+                                            int wo) {
+  if constexpr (MODE == 2) atomicAdd(&hj[wo + b], pl.wy);
 }
 
 template <int MODE, int RP = 3>
@@ -2837,11 +2845,15 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
   const int g = fround >= 0 ? min(c.kg_large, c.d - f0) : st.g;
   constexpr int RPL = MODE == 2 ? 2 : 3;
   const int span = large_planes(MODE, c.CH) * 256;
+  // compact slices (unit-weight regression builds, host-checked): u32 counts in 128 words, then
+  // the w yq plane -- LDS stride ls = 384 words per feature instead of span = 512
+  const bool compact = MODE == 2 && c.large_compact != 0;
+  const int ls = compact ? 384 : span, wo = compact ? 128 : 256;
   __shared__ int16_t feats[64];
   CT* hist = (CT*)smem;
   const int16_t* perm = c.lperm + (int64_t)slot * c.d + st.pos;
   for (int j = threadIdx.x; j < g; j += 256) feats[j] = fround >= 0 ? (int16_t)(f0 + j) : perm[j];
-  for (int i = threadIdx.x; i < g * span; i += 256) hist[i] = (CT)0;
+  for (int i = threadIdx.x; i < g * ls; i += 256) hist[i] = (CT)0;
   __syncthreads();
   const uint32_t* rows = c.rows_cur + st.on.start;
   const float* ty = tree_y(c, s);
@@ -2895,11 +2907,11 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
           if (skipc) {   // wave-uniform: the count plane comes from the root-count cache
 #pragma unroll
             for (int j = 0; j < G; ++j)
-              if (j < g) hist_add_wy<MODE>(hist + j * span, (int)b[j], pl);
+              if (j < g) hist_add_wy<MODE>(hist + j * ls, (int)b[j], pl, wo);
           } else {
 #pragma unroll
             for (int j = 0; j < G; ++j)
-              if (j < g) hist_add_unit<MODE>(hist + j * span, (int)b[j], pl);
+              if (j < g) hist_add_unit<MODE>(hist + j * ls, (int)b[j], pl, wo);
           }
         } else {
 #pragma unroll
@@ -2997,12 +3009,13 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
     // (gcnt: half the flush atomics' bytes for that plane; see whole_counts_u32)
     const bool gcnt = MODE == 2 && fround >= 0 && s.bootstrap == 0;
     for (int i = threadIdx.x; i < g * span; i += 256) {
-      CT v = hist[i];
       const int j = i / span, b = i - j * span;
       if (MODE == 2 && b < 256 && skipc) continue;   // count plane: copied from the root-count cache
+      // LDS word of global element (j, b): the same index, or (compact) the w yq plane at wo
+      CT v = (MODE == 2 && b >= 256) ? hist[j * ls + wo + (b - 256)] : (compact ? (CT)0 : hist[i]);
       if (MODE == 2 && b < 256 && (uw || gcnt)) {
         // row count of bin b: the u32 LDS counters, or rows << 32 of the (w | rows << 32) plane
-        const uint32_t n1 = uw ? ((const uint32_t*)(hist + j * span))[b] : (uint32_t)((uint64_t)v >> 32);
+        const uint32_t n1 = uw ? ((const uint32_t*)(hist + j * ls))[b] : (uint32_t)((uint64_t)v >> 32);
         if (gcnt) {
           if (n1) atomicAdd((uint32_t*)(gh + j * span) + b, n1);
           continue;
@@ -3718,6 +3731,7 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.large_cap = L.large_cap;
   c.wave_max = (int)a->wave_max; c.block_max = (int)a->block_max; c.chunk = (int)a->chunk;
   c.kg_wave = (int)a->kg_wave; c.kg_block = (int)a->kg_block; c.kg_large = (int)a->kg_large;
+  c.large_compact = (c.is_reg && a->large_unit && a->kg_large <= DML_KGL_LARGE && !getenv("DML_LARGE_NO_COMPACT")) ? 1 : 0;
   c.slack_wave = (int)a->slack_wave;
   c.sub_max = (int)a->sub_max;
   c.sub_cache_d = (int)a->sub_cache_d;
@@ -3990,7 +4004,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   // 13.7 -> 14.9 CV-fits/s at 8192-row chunks; the 96-KB floor used before was measured on
   // the draining loop).
   const size_t lds_hl_floor = getenv("DML_LARGE_LDS_MIN") ? (size_t)atol(getenv("DML_LARGE_LDS_MIN")) : 0;
-  const size_t lds_hl = std::max<size_t>((size_t)a->kg_large * large_planes(MODE, CH) * 256 * mode_elem(MODE),
+  const size_t lds_hl = std::max<size_t>((size_t)a->kg_large * (c.large_compact ? 384 : large_planes(MODE, CH) * 256) *
+                                             mode_elem(MODE),
                                          std::min<size_t>(lds_hl_floor, 150 * 1024));
   const size_t lds_sl = (size_t)a->kg_large * ghist_feat_bytes(MODE, CH) + a->kg_large * 16 + 16 +
                         (size_t)a->kg_large * CH * 8 + (size_t)a->kg_large * 8 + 64;

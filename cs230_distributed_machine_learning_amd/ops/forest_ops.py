@@ -495,6 +495,8 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     a.fast_crit = (int(crits[0]) + 1 if len(crits) == 1 and cw_dev is None and mono_dev is None
                    and not np.any(specs["min_weight_frac"] > 0) else 0)
     a.active_count = native.ptr(active)
+    # every tree unit-weight (no bootstrap, e.g. boosting stages): compact large-tier LDS slices
+    a.large_unit = int(bool(is_reg and T and np.all(specs["bootstrap"] == 0)))
     if root_counts is not None and is_reg and T:
         buf = root_counts.get("buf")
         if buf is None or buf.numel() != T * d * 256:

@@ -74,7 +74,7 @@ ForestArgs = _i64_struct(
         "yq_e1", "yq_e2",
         "mono", "nbound", "fast_crit",
         "early_pred", "fit_done_level", "n_fits",
-        "bigsub_max", "all_features", "sub_small", "root_counts", "root_counts_valid",
+        "bigsub_max", "all_features", "sub_small", "root_counts", "root_counts_valid", "large_unit",
     ],
 )
 
