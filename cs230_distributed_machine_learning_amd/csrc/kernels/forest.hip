@@ -268,6 +268,7 @@ struct Ctx {
   int32_t full_cur, full_prev;
   int32_t root_cnt_skip;       // root level of a build with cached root counts: no count atomics
   int32_t large_compact;       // ForestArgs::large_unit (and kg_large <= DML_KGL_LARGE): 3-KB LDS slices
+  int32_t fm_div;              // k_hist_large: feature-major gathers only for nodes >= n / fm_div rows (0: all)
   uint32_t* root_counts;       // ForestArgs::root_counts (null: none)
   int64_t pi_cap;        // entries of each pinfo table
   // whole-histogram levels: every (large node, visiting position)'s split candidate, from
@@ -2876,7 +2877,9 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
       constexpr int G = decltype(Gc)::value;
       constexpr bool UW = decltype(UWc)::value;
       // feature offsets: feature-major copy (stride n) when present, else the row line
-      const bool fm = c.XbT != nullptr;
+      // (DML_LARGE_FM_DIV = k > 0: nodes holding under 1/k of the table's rows read the row-major
+      // lines instead -- one line per row for every feature of the round)
+      const bool fm = c.XbT != nullptr && (c.fm_div == 0 || (int64_t)st.on.count * c.fm_div >= (int64_t)c.n);
       int64_t fo[G];
 #pragma unroll
       for (int j = 0; j < G; ++j) {
@@ -3731,6 +3734,7 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.large_cap = L.large_cap;
   c.wave_max = (int)a->wave_max; c.block_max = (int)a->block_max; c.chunk = (int)a->chunk;
   c.kg_wave = (int)a->kg_wave; c.kg_block = (int)a->kg_block; c.kg_large = (int)a->kg_large;
+  c.fm_div = getenv("DML_LARGE_FM_DIV") ? atoi(getenv("DML_LARGE_FM_DIV")) : 0;
   c.large_compact = (c.is_reg && a->large_unit && a->kg_large <= DML_KGL_LARGE && !getenv("DML_LARGE_NO_COMPACT")) ? 1 : 0;
   c.slack_wave = (int)a->slack_wave;
   c.sub_max = (int)a->sub_max;

@@ -1,0 +1,186 @@
+// Boosting root-histogram microbenchmark: LDS atomics per (row, feature, tree) vs a bin-sorted
+// row order per feature.
+//
+// Question: a boosting stage's root histograms (every tree's whole training set, every feature)
+// are the largest level of each tree.  The builder adds one fixed-point w yq per (row, feature,
+// tree) with an LDS atomic (k_hist_large).  The bins never change across stages, so each
+// feature's rows can be sorted by bin ONCE: a root histogram is then a segmented sum of the
+// trees' targets gathered in that order -- register accumulation, an LDS atomic only where the
+// bin changes, all T trees of a stage per gathered row (T floats in one contiguous record).
+//
+//   A  atomics : grid (row chunk, tree, feature group); bins from the feature-major copy
+//                (coalesced), target per (row, tree), one u64 LDS atomic per (row, feature)
+//   B  sorted  : grid (position chunk, feature); per position: its row id and bin (streamed),
+//                the row's T targets (one 16-B-aligned record, gathered), T int64 register sums
+//
+// Both produce the same exact int64 histograms [T][d][256] (checked).  Synthetic: n rows, d
+// features with uniform bins, T trees whose training rows are 80 % of the rows.
+//   hipcc --offload-arch=gfx950 -O3 -o scripts/micro_root_hist.bin scripts/micro_root_hist.hip
+//   ./scripts/micro_root_hist.bin [n=1000000] [d=100] [T=20]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+constexpr int TMAX = 20;      // trees per stage (register sums in B)
+constexpr int KG = 15;        // features per workgroup in A (the production width for d = 100)
+constexpr int CHUNK_A = 4096; // rows per workgroup in A (the production regression chunk)
+constexpr int PER = 64;       // consecutive sorted positions per thread in B
+constexpr int UNR = 4;        // positions gathered ahead in B
+
+__device__ __forceinline__ long long quant(float y, double s) { return __double2ll_rn((double)y * s); }
+
+// A: LDS atomics, targets [T][n] (0 outside the tree's training rows)
+__global__ __launch_bounds__(256) void k_atomic(const uint8_t* __restrict__ XT, const float* __restrict__ y, int n,
+                                                int d, double s, unsigned long long* out) {
+  __shared__ unsigned long long h[KG * 256];
+  const int t = blockIdx.y, f0 = blockIdx.z * KG;
+  const int g = min(KG, d - f0);
+  for (int i = threadIdx.x; i < KG * 256; i += 256) h[i] = 0ull;
+  __syncthreads();
+  const int r0 = blockIdx.x * CHUNK_A, r1 = min(r0 + CHUNK_A, n);
+  const float* yt = y + (int64_t)t * n;
+  for (int r = r0 + threadIdx.x; r < r1; r += 256) {
+    const float v = yt[r];
+    if (v == 0.0f) continue;   // out of the tree's training rows
+    const long long q = quant(v, s);
+    uint32_t b[KG];
+#pragma unroll
+    for (int j = 0; j < KG; ++j) b[j] = j < g ? XT[(int64_t)(f0 + j) * n + r] : 0u;
+#pragma unroll
+    for (int j = 0; j < KG; ++j)
+      if (j < g) atomicAdd(&h[j * 256 + b[j]], (unsigned long long)q);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < g * 256; i += 256)
+    if (h[i]) atomicAdd(&out[((int64_t)t * d + f0 + i / 256) * 256 + (i & 255)], h[i]);
+}
+
+// B: bin-sorted positions; ytr [n][T] (one record per row), perm / sbin [d][n]
+template <int T>
+__global__ __launch_bounds__(256) void k_sorted(const uint32_t* __restrict__ perm, const uint8_t* __restrict__ sbin,
+                                                const float* __restrict__ ytr, int n, int d, double s,
+                                                unsigned long long* out) {
+  __shared__ unsigned long long h[256 * T];
+  for (int i = threadIdx.x; i < 256 * T; i += 256) h[i] = 0ull;
+  __syncthreads();
+  const int f = blockIdx.y;
+  const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * PER;
+  const uint32_t* pf = perm + (int64_t)f * n;
+  const uint8_t* bf = sbin + (int64_t)f * n;
+  long long acc[T];
+#pragma unroll
+  for (int k = 0; k < T; ++k) acc[k] = 0;
+  int cur = p0 < n ? bf[p0] : 0;
+  for (int64_t p = p0; p < p0 + PER && p < n; p += UNR) {
+    float4 rec[UNR][T / 4];
+    int bins[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t q = min<int64_t>(p + u, n - 1);
+      const uint32_t row = pf[q];
+      bins[u] = (p + u < n && p + u < p0 + PER) ? (int)bf[q] : -1;
+      const float4* src = (const float4*)(ytr + (int64_t)row * T);
+#pragma unroll
+      for (int k = 0; k < T / 4; ++k) rec[u][k] = src[k];
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (bins[u] < 0) break;
+      if (bins[u] != cur) {
+#pragma unroll
+        for (int k = 0; k < T; ++k)
+          if (acc[k]) { atomicAdd(&h[cur * T + k], (unsigned long long)acc[k]); acc[k] = 0; }
+        cur = bins[u];
+      }
+      const float* v = (const float*)rec[u];
+#pragma unroll
+      for (int k = 0; k < T; ++k) acc[k] += quant(v[k], s);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < T; ++k)
+    if (acc[k]) atomicAdd(&h[cur * T + k], (unsigned long long)acc[k]);
+  __syncthreads();
+  for (int i = threadIdx.x; i < 256 * T; i += 256)
+    if (h[i]) atomicAdd(&out[((int64_t)(i % T) * d + f) * 256 + i / T], h[i]);
+}
+
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 1000000;
+  const int d = argc > 2 ? atoi(argv[2]) : 100;
+  const int T = TMAX;
+  const double s = 1099511627776.0;   // 2^40 grid
+  std::vector<uint8_t> XT((size_t)d * n);
+  std::vector<float> y((size_t)T * n), ytr((size_t)n * T);
+  uint64_t st = 88172645463325252ull;
+  auto rnd = [&]() { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st; };
+  for (auto& b : XT) b = (uint8_t)(rnd() & 255);
+  for (int t = 0; t < T; ++t)
+    for (int r = 0; r < n; ++r) {
+      const bool inb = (rnd() % 5) != 0;
+      const float v = inb ? (float)((int64_t)(rnd() % 2000001) - 1000000) * 1e-6f + 1e-7f : 0.0f;
+      y[(size_t)t * n + r] = v;
+      ytr[(size_t)r * T + t] = v;
+    }
+  // per feature: rows in bin order (counting sort), and the sorted bins
+  std::vector<uint32_t> perm((size_t)d * n);
+  std::vector<uint8_t> sbin((size_t)d * n);
+  for (int f = 0; f < d; ++f) {
+    int cnt[257] = {0};
+    for (int r = 0; r < n; ++r) ++cnt[XT[(size_t)f * n + r] + 1];
+    for (int b = 0; b < 256; ++b) cnt[b + 1] += cnt[b];
+    for (int r = 0; r < n; ++r) {
+      const int b = XT[(size_t)f * n + r];
+      const int pos = cnt[b]++;
+      perm[(size_t)f * n + pos] = (uint32_t)r;
+      sbin[(size_t)f * n + pos] = (uint8_t)b;
+    }
+  }
+  uint8_t *dXT, *dsb;
+  float *dy, *dytr;
+  uint32_t* dperm;
+  unsigned long long *oA, *oB;
+  const size_t hbytes = (size_t)T * d * 256 * 8;
+  CK(hipMalloc(&dXT, XT.size())); CK(hipMalloc(&dsb, sbin.size()));
+  CK(hipMalloc(&dy, y.size() * 4)); CK(hipMalloc(&dytr, ytr.size() * 4));
+  CK(hipMalloc(&dperm, perm.size() * 4));
+  CK(hipMalloc(&oA, hbytes)); CK(hipMalloc(&oB, hbytes));
+  CK(hipMemcpy(dXT, XT.data(), XT.size(), hipMemcpyHostToDevice));
+  CK(hipMemcpy(dsb, sbin.data(), sbin.size(), hipMemcpyHostToDevice));
+  CK(hipMemcpy(dy, y.data(), y.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dytr, ytr.data(), ytr.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dperm, perm.data(), perm.size() * 4, hipMemcpyHostToDevice));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  const dim3 gA((n + CHUNK_A - 1) / CHUNK_A, T, (d + KG - 1) / KG);
+  const dim3 gB((unsigned)((n + 256 * PER - 1) / (256 * PER)), d);
+  float best[2] = {1e30f, 1e30f};
+  for (int it = 0; it < 6; ++it) {
+    for (int k = 0; k < 2; ++k) {
+      unsigned long long* o = k ? oB : oA;
+      CK(hipMemset(o, 0, hbytes));
+      CK(hipEventRecord(e0));
+      if (k == 0) k_atomic<<<gA, 256>>>(dXT, dy, n, d, s, oA);
+      else k_sorted<TMAX><<<gB, 256>>>(dperm, dsb, dytr, n, d, s, oB);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      if (it > 0) best[k] = std::min(best[k], ms);
+    }
+  }
+  std::vector<unsigned long long> hA(hbytes / 8), hB(hbytes / 8);
+  CK(hipMemcpy(hA.data(), oA, hbytes, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(hB.data(), oB, hbytes, hipMemcpyDeviceToHost));
+  size_t bad = 0;
+  for (size_t i = 0; i < hA.size(); ++i) bad += hA[i] != hB[i];
+  printf("{\"n\": %d, \"d\": %d, \"trees\": %d, \"atomic_ms\": %.3f, \"sorted_ms\": %.3f, \"speedup\": %.2f, "
+         "\"mismatches\": %zu}\n", n, d, T, best[0], best[1], best[0] / best[1], bad);
+  return bad ? 1 : 0;
+}
