@@ -430,14 +430,14 @@ class GradientBoostingFamily(Family):
         # fused HIP stage (csrc/kernels/gbrt.hip): gradient, leaf line search and raw update as
         # three kernels per stage instead of torch glue (losses with sums-only line searches)
         # percentile losses (absolute_error / huber / quantile) run fused too: leaf percentiles and
-        # huber's delta by the exact radix select of gbrt.hip (early stopping keeps the torch path:
-        # its validation loss needs huber's delta on the host every stage)
+        # huber's delta by the exact radix select of gbrt.hip (early stopping reads the stage's
+        # delta from the device for huber's validation loss)
         pct = (LOSS_ABS, LOSS_HUBER, LOSS_QUANT)
         # row-sharded stages run the same kernels in phases, with the leaf sums and the select
         # counters all-reduced between them (_sharded_stage)
         fused = (gpu and os.environ.get("DML_GB_FUSED", "1") != "0" and K <= 64
                  and all(t.params["loss"] in (LOSS_SQ, LOSS_LOG, LOSS_EXP) or
-                         (t.params["loss"] in pct and not clf and not t.params.get("n_iter_no_change"))
+                         (t.params["loss"] in pct and not clf)
                          for t in batch)
                  and max(t.params["max_depth"] for t in batch) <= 10   # gbrt.hip: S <= 2048 path slots
                  and getattr(native.hip_lib(), "dml_gb_stage", None) is not None
@@ -510,6 +510,9 @@ class GradientBoostingFamily(Family):
                             rc = lib.dml_gb_huber_delta(ctypes.byref(ga), stream)
                             if rc:
                                 raise RuntimeError(f"dml_gb_huber_delta failed ({rc})")
+                        for a, f in enumerate(act):   # early stopping: the stage's delta (read lazily)
+                            if f in val_rows and loss_all[f] == LOSS_HUBER:
+                                hub_delta[f] = fit_delta[a].clone()
                 rc = lib.dml_gb_grad(ctypes.byref(ga), stream)
                 if rc:
                     raise RuntimeError(f"dml_gb_grad failed ({rc})")

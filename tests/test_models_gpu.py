@@ -111,7 +111,10 @@ def test_gbrt_gpu_close_to_cpu(model, clf, loss):
     # deep trees: 1024 / 2048 path slots per tree
     ("GradientBoostingRegressor", 0, "squared_error", {"max_depth": [7, 10]}),
     ("GradientBoostingRegressor", 0, "quantile", {"max_depth": [9], "alpha": [0.4]}),
-    ("GradientBoostingClassifier", 3, "log_loss", {"max_depth": [10]})])
+    ("GradientBoostingClassifier", 3, "log_loss", {"max_depth": [10]}),
+    # early stopping on the percentile losses (huber's validation loss at the device delta)
+    ("GradientBoostingRegressor", 0, "huber", {"n_iter_no_change": [2], "validation_fraction": [0.2]}),
+    ("GradientBoostingRegressor", 0, "quantile", {"n_iter_no_change": [3], "alpha": [0.6]})])
 def test_gbrt_fused_stage_matches_torch_stage(model, n_classes, loss, extra, monkeypatch, tmp_path):
     """The fused HIP stage (gbrt.hip: gradient, leaf line search -- Newton steps, or the exact
     radix-select leaf percentiles and huber delta -- raw update) against the torch stage on the
