@@ -202,6 +202,10 @@ struct ForestArgs {
   // tier's LDS histograms drop the unused half of the count plane (3 KB instead of 4 KB per
   // feature: 16 features in 48 KB, three workgroups per CU instead of two)
   int64_t large_unit;
+  // unit-weight regression build whose fixed-point targets satisfy |yq| < 2^39 (ops/forest_ops.py
+  // checks it from the exponent histogram) with <= 4095-row large-tier chunks: the large tier's
+  // row count and w yq share ONE u64 LDS atomic, (1 << 52) + yq + 2^39 per row (kPack*)
+  int64_t large_pack;
 };
 
 // 0 subtree, 1 wave, 2 block, 3 large, 4 small subtree (<= sub_small rows: the subtree kernel
@@ -269,6 +273,7 @@ struct Ctx {
   int32_t root_cnt_skip;       // root level of a build with cached root counts: no count atomics
   int32_t large_compact;       // ForestArgs::large_unit (and kg_large <= DML_KGL_LARGE): 3-KB LDS slices
   int32_t fm_div;              // k_hist_large: feature-major gathers only for nodes >= n / fm_div rows (0: all)
+  int32_t large_pack;          // ForestArgs::large_pack (with large_compact): packed count | w yq words
   uint32_t* root_counts;       // ForestArgs::root_counts (null: none)
   int64_t pi_cap;        // entries of each pinfo table
   // whole-histogram levels: every (large node, visiting position)'s split candidate, from
@@ -1152,6 +1157,22 @@ __device__ __forceinline__ void hist_add_unit(typename HT<MODE>::T* hj, int b, c
     atomicAdd((uint32_t*)hj + b, 1u);
     atomicAdd(&hj[wo + b], pl.wy);
   }
+}
+
+// packed LDS words of a large_pack build: one u64 atomic per (row, feature) carries the row
+// count (bits 52..63, <= 4095 rows per workgroup) and the biased w yq (yq + 2^39 > 0, so the
+// 52-bit field never borrows from the count; its sum over <= 4095 rows stays below 2^52)
+constexpr int kPackShift = 52;
+constexpr unsigned long long kPackBias = 1ull << 39;
+template <int MODE>
+__device__ __forceinline__ void hist_add_packed(typename HT<MODE>::T* hj, int b, const typename PLT<MODE>::T& pl,
+                                                int wo) {
+  if constexpr (MODE == 2) atomicAdd(&hj[wo + b], (1ull << kPackShift) + ((unsigned long long)pl.wy + kPackBias));
+}
+// a packed word -> (row count, w yq) in the two's-complement u64 of the regression planes
+__device__ __forceinline__ uint32_t pack_count(unsigned long long v) { return (uint32_t)(v >> kPackShift); }
+__device__ __forceinline__ unsigned long long pack_wy(unsigned long long v) {
+  return (v & ((1ull << kPackShift) - 1)) - ((v >> kPackShift) << 39);
 }
 
 // the same with the count plane supplied elsewhere (boosting roots: ForestArgs::root_counts)
@@ -2849,7 +2870,9 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
   // compact slices (unit-weight regression builds, host-checked): u32 counts in 128 words, then
   // the w yq plane -- LDS stride ls = 384 words per feature instead of span = 512
   const bool compact = MODE == 2 && c.large_compact != 0;
-  const int ls = compact ? 384 : span, wo = compact ? 128 : 256;
+  // packed builds: one u64 word per bin (count | w yq), 2 KB per feature
+  const bool packed = compact && c.large_pack != 0;
+  const int ls = packed ? 256 : (compact ? 384 : span), wo = packed ? 0 : (compact ? 128 : 256);
   __shared__ int16_t feats[64];
   CT* hist = (CT*)smem;
   const int16_t* perm = c.lperm + (int64_t)slot * c.d + st.pos;
@@ -2911,6 +2934,10 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
 #pragma unroll
             for (int j = 0; j < G; ++j)
               if (j < g) hist_add_wy<MODE>(hist + j * ls, (int)b[j], pl, wo);
+          } else if (packed) {   // wave-uniform: count and w yq in one atomic
+#pragma unroll
+            for (int j = 0; j < G; ++j)
+              if (j < g) hist_add_packed<MODE>(hist + j * ls, (int)b[j], pl, wo);
           } else {
 #pragma unroll
             for (int j = 0; j < G; ++j)
@@ -3014,11 +3041,15 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
     for (int i = threadIdx.x; i < g * span; i += 256) {
       const int j = i / span, b = i - j * span;
       if (MODE == 2 && b < 256 && skipc) continue;   // count plane: copied from the root-count cache
-      // LDS word of global element (j, b): the same index, or (compact) the w yq plane at wo
+      // LDS word of global element (j, b): the same index, or (compact) the w yq plane at wo;
+      // packed words (not at a cached root) hold both the count and the biased w yq
+      const bool pk = packed && !skipc;
       CT v = (MODE == 2 && b >= 256) ? hist[j * ls + wo + (b - 256)] : (compact ? (CT)0 : hist[i]);
+      if (MODE == 2 && b >= 256 && pk) v = (CT)pack_wy((unsigned long long)v);
       if (MODE == 2 && b < 256 && (uw || gcnt)) {
         // row count of bin b: the u32 LDS counters, or rows << 32 of the (w | rows << 32) plane
-        const uint32_t n1 = uw ? ((const uint32_t*)(hist + j * ls))[b] : (uint32_t)((uint64_t)v >> 32);
+        const uint32_t n1 = pk ? pack_count((unsigned long long)hist[j * ls + wo + b])
+                               : (uw ? ((const uint32_t*)(hist + j * ls))[b] : (uint32_t)((uint64_t)v >> 32));
         if (gcnt) {
           if (n1) atomicAdd((uint32_t*)(gh + j * span) + b, n1);
           continue;
@@ -3736,6 +3767,7 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.kg_wave = (int)a->kg_wave; c.kg_block = (int)a->kg_block; c.kg_large = (int)a->kg_large;
   c.fm_div = getenv("DML_LARGE_FM_DIV") ? atoi(getenv("DML_LARGE_FM_DIV")) : 0;
   c.large_compact = (c.is_reg && a->large_unit && a->kg_large <= DML_KGL_LARGE && !getenv("DML_LARGE_NO_COMPACT")) ? 1 : 0;
+  c.large_pack = (c.large_compact && a->large_pack && a->chunk <= 4095 && !getenv("DML_LARGE_NO_PACK")) ? 1 : 0;
   c.slack_wave = (int)a->slack_wave;
   c.sub_max = (int)a->sub_max;
   c.sub_cache_d = (int)a->sub_cache_d;
@@ -4008,7 +4040,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
   // 13.7 -> 14.9 CV-fits/s at 8192-row chunks; the 96-KB floor used before was measured on
   // the draining loop).
   const size_t lds_hl_floor = getenv("DML_LARGE_LDS_MIN") ? (size_t)atol(getenv("DML_LARGE_LDS_MIN")) : 0;
-  const size_t lds_hl = std::max<size_t>((size_t)a->kg_large * (c.large_compact ? 384 : large_planes(MODE, CH) * 256) *
+  const size_t lds_hl = std::max<size_t>((size_t)a->kg_large *
+                                             (c.large_pack ? 256 : (c.large_compact ? 384 : large_planes(MODE, CH) * 256)) *
                                              mode_elem(MODE),
                                          std::min<size_t>(lds_hl_floor, 150 * 1024));
   const size_t lds_sl = (size_t)a->kg_large * ghist_feat_bytes(MODE, CH) + a->kg_large * 16 + 16 +

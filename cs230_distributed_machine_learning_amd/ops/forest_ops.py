@@ -327,6 +327,13 @@ def reg_exponent_counts(yreg, n: int, ystride: int = 0, targets: int = 1, defer:
     return cnt
 
 
+def _max_exponent(cnt):
+    """k such that every target of the exponent histogram has |y| < 2^k (None: all zero)."""
+    c = np.asarray(cnt.cpu() if torch.is_tensor(cnt) else cnt, dtype=np.int64).reshape(-1, EXP_BINS)
+    nz = np.nonzero(c[:, 1:].any(axis=0))[0]
+    return int(nz[-1] + 1 - EXP_OFF) if len(nz) else None
+
+
 def reg_exponents_of_counts(cnt) -> tuple[int, int]:
     """The fixed-point rule (forest_common.h ``reg_exponents_counts`` is the same loop):
     B1 = max over targets of sum_k c_k 2^k >= sum |y|, B2 likewise with 4^k >= sum y^2;
@@ -512,9 +519,11 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
             if rc:
                 raise RuntimeError(f"dml_forest_count failed ({rc}): {native.hip_error(lib)}")
             counts = active.cpu().numpy().astype(np.int64)
+    kmax = None   # |y| < 2^kmax for every target of the build (exponent histogram)
     if exp_cnt is not None:
         cnt = exp_cnt() if callable(exp_cnt) else exp_cnt
         a.yq_e1, a.yq_e2 = reg_exponents_of_counts(cnt)
+        kmax = _max_exponent(cnt)
     if not cached:
         row_off = np.zeros(T + 1, dtype=np.int64)
         np.cumsum(counts, out=row_off[1:])
@@ -528,6 +537,15 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     a.wave_max, a.block_max, a.chunk = tiers.wave_max, tiers.block_max, (tiers.chunk_reg if is_reg else tiers.chunk)
     a.kg_wave, a.kg_block, a.slack_wave = tiers.kg_wave, tiers.kg_block, tiers.slack_wave
     a.kg_large = tiers.kg_large_reg if is_reg else tiers.kg_large
+    # unit-weight regression build whose fixed-point targets stay below 2^39 in magnitude:
+    # the large tier packs each row's count and w yq into ONE u64 LDS atomic (forest.hip
+    # kPackShift; <= 4095 rows per workgroup) -- the count atomic was ~3/4 of the histogram
+    # time below the boosting root (profiles/r5_gbrt_root_hist_micro.txt)
+    a.large_pack = 0
+    if (is_reg and a.large_unit and kmax is not None and kmax + int(a.yq_e1) <= 38
+            and os.environ.get("DML_LARGE_NO_PACK", "0") == "0"):
+        a.large_pack = 1
+        a.chunk = min(int(a.chunk), 3840)
     if is_reg and d > 0:
         # whole-feature regression rounds of equal width (100 features: 7 rounds of 15 / 10,
         # not 6 of 16 and one of 4) -- GBRT config 6 16.7 -> 17.1 CV-fits/s,

@@ -75,6 +75,7 @@ ForestArgs = _i64_struct(
         "mono", "nbound", "fast_crit",
         "early_pred", "fit_done_level", "n_fits",
         "bigsub_max", "all_features", "sub_small", "root_counts", "root_counts_valid", "large_unit",
+        "large_pack",
     ],
 )
 
