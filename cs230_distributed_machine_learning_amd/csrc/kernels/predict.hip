@@ -29,6 +29,8 @@ struct PredictArgs {
   int64_t lds_pitch;  // set by dml_forest_predict: LDS row stride, 0 = no staging
   int64_t fit_row_off_host;   // optional host copy of fit_row_off (per-fit grid sizes)
   int64_t fit_skip;           // optional int32[F] device mask: fits already predicted (early) are skipped
+  int64_t fit_depth_cap;      // optional int32[F]: fit f reads its trees only down to this depth (<= 0: all);
+                              // prefix fits of a deeper grown forest (models/base.py prefix_groups)
 };
 
 // leaf of U consecutive trees [t0, t0 + u_n) for one row, walked in lock-step: the U
@@ -36,14 +38,14 @@ struct PredictArgs {
 // instead of one (tree traversal is latency-bound)
 template <int kPredU>
 __device__ __forceinline__ void leaves_u(const NodeRec* __restrict__ nodes, const uint8_t* __restrict__ xr, int t0,
-                                         int u_n, int (&leaf)[kPredU]) {
+                                         int u_n, int (&leaf)[kPredU], int cap) {
   NodeRec nr[kPredU];
 #pragma unroll
   for (int u = 0; u < kPredU; ++u) {
     leaf[u] = t0 + u;
     nr[u] = u < u_n ? nodes[leaf[u]] : NodeRec{-1, -1};
   }
-  for (int steps = 0; steps < 1 << 20; ++steps) {
+  for (int steps = 0; steps < cap; ++steps) {   // step s: every unfinished tree at depth s
     bool any = false;
 #pragma unroll
     for (int u = 0; u < kPredU; ++u) any |= nr[u].split >= 0;
@@ -56,6 +58,12 @@ __device__ __forceinline__ void leaves_u(const NodeRec* __restrict__ nodes, cons
       }
     }
   }
+}
+
+// depth cap of fit f (1 << 20: none)
+__device__ __forceinline__ int depth_cap(const PredictArgs& a, int f) {
+  const int c = a.fit_depth_cap ? (GPTR(const int32_t, a.fit_depth_cap))[f] : 0;
+  return c > 0 ? c : 1 << 20;
 }
 
 // The block's 256 rows are staged in LDS once (dword stride odd -> a wave whose lanes
@@ -98,6 +106,7 @@ __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
     xr = GPTR(const uint8_t, a.Xb) + (int64_t)(GPTR(const int32_t, a.rows))[r0 + i] * a.ld;
   }
   const int C = (int)a.n_classes;
+  const int cap = depth_cap(a, f);
   const NodeRec* nodes = GPTR(const NodeRec, a.nodes);
   const double* val = GPTR(const double, a.node_val);
   float p[MAXC];
@@ -107,7 +116,7 @@ __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
   for (int t = toff[f]; t < tend; t += kPredU) {
     int leaf[kPredU];
     const int u_n = min(kPredU, tend - t);
-    leaves_u<kPredU>(nodes, xr, t, u_n, leaf);
+    leaves_u<kPredU>(nodes, xr, t, u_n, leaf, cap);
     // accumulate in tree order (bit-identical to the host predictor)
 #pragma unroll
     for (int u = 0; u < kPredU; ++u) {
@@ -160,13 +169,14 @@ __global__ __launch_bounds__(256) void k_predict_reg(PredictArgs a) {
   }
   const NodeRec* nodes = GPTR(const NodeRec, a.nodes);
   const double* val = GPTR(const double, a.node_val);
+  const int cap = depth_cap(a, f);
   double acc = 0.0;
   int nt = 0;
   const int tend = toff[f + 1];
   for (int t = toff[f]; t < tend; t += kPredU) {
     int leaf[kPredU];
     const int u_n = min(kPredU, tend - t);
-    leaves_u<kPredU>(nodes, xr, t, u_n, leaf);
+    leaves_u<kPredU>(nodes, xr, t, u_n, leaf, cap);
 #pragma unroll
     for (int u = 0; u < kPredU; ++u) {
       if (u >= u_n) break;
@@ -388,6 +398,7 @@ int dml_forest_predict_fit(const PredictArgs* a, int32_t f, hipStream_t st) {
   b.fit_row_off = a->fit_row_off + 8 * (int64_t)f;     // int64[F+1]
   b.F = 1;
   b.fit_skip = 0;
+  if (a->fit_depth_cap) b.fit_depth_cap = a->fit_depth_cap + 4 * (int64_t)f;
   b.max_rows = roff ? roff[f + 1] - roff[f] : a->max_rows;
   return dml_forest_predict(&b, st);
 }

@@ -585,7 +585,13 @@ def prefix_units(plan: Dict[str, Any], todo: List[int]) -> List[List[int]]:
         if c.get("random_state") in (None, "None") or c.get("n_iter_no_change") not in (None, "None"):
             key: Any = ("solo", i)
         else:
-            key = repr(sorted((k, repr(v)) for k, v in c.items() if k != "n_estimators"))
+            # forests also nest max_depth (prefix_groups depth=True) unless pruning / monotonic
+            # clipping rewrites the grown trees
+            drop = {"n_estimators"}
+            if mt.startswith("RandomForest") and not c.get("max_leaf_nodes") and not c.get("ccp_alpha") and \
+                    c.get("monotonic_cst") is None:
+                drop.add("max_depth")
+            key = repr(sorted((k, repr(v)) for k, v in c.items() if k not in drop))
         units.setdefault(key, []).append(i)
     return list(units.values())
 

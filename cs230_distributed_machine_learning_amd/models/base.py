@@ -145,7 +145,7 @@ def as_float(v, name, lo=None, hi=None, allow_none=False):
     return v
 
 
-def prefix_groups(tasks: Sequence[FitTask], ok=None):
+def prefix_groups(tasks: Sequence[FitTask], ok=None, depth: bool = False):
     """Exact sharing of ensemble prefixes inside one batch of fits.
 
     Fits that differ only in ``n_estimators``, on the same split, with an explicit
@@ -154,29 +154,64 @@ def prefix_groups(tasks: Sequence[FitTask], ok=None):
     orders from the same seeded generators stage by stage), exactly as sklearn's estimators
     with a fixed random_state do.  Only the longest fit of such a group (the leader) is
     grown; every shorter one (a follower) is scored from the leader's first n_estimators
-    trees / stages -- the same model, bit for bit, as growing it alone.  ``ok(task)`` excludes
-    fits whose later stages change earlier results (early stopping).  DML_PREFIX_SHARE=0
-    turns the sharing off.  Returns (leaders in input order, {leader task_id: followers}).
-    The reference grows every candidate separately (aws-prod/worker/worker.py:315-341)."""
+    trees / stages -- the same model, bit for bit, as growing it alone.  ``depth=True``
+    (forests on the GPU predictor) also nests ``max_depth``: a tree grown to depth D holds the
+    tree grown to d < D as its top d levels (same node-keyed feature orders, same splits; a
+    node at depth d is that tree's leaf, with its stored class sums), so one leader with the
+    most trees AND the deepest trees serves every (n_estimators, max_depth) of its group --
+    unless pruning (max_leaf_nodes, ccp_alpha) or monotonic clipping rewrite the grown trees.
+    ``ok(task)`` excludes fits whose later stages change earlier results (early stopping).
+    DML_PREFIX_SHARE=0 turns the sharing off.  Returns (leaders in input order,
+    {leader task_id: followers}).  The reference grows every candidate separately
+    (aws-prod/worker/worker.py:315-341)."""
     import os
 
     if os.environ.get("DML_PREFIX_SHARE", "1") == "0":
         return list(tasks), {}
+
+    def nested_depth(t: FitTask) -> bool:
+        p = t.params
+        return (depth and "max_depth" in p and not p.get("max_leaf_nodes") and not p.get("ccp_alpha", 0.0)
+                and p.get("monotonic_cst") is None)
+
+    def key_of(t: FitTask, drop) -> Any:
+        return (t.split, t.model_type, t.need_proba,
+                repr(sorted((k, repr(v)) for k, v in t.params.items() if k not in drop)))
+
     groups: Dict[Any, List[FitTask]] = {}
     for t in tasks:
         p = t.params
         if p.get("seed") is None or "n_estimators" not in p or (ok is not None and not ok(t)):
             key: Any = ("solo", t.task_id)
+        elif nested_depth(t):
+            key = ("depth",) + key_of(t, ("n_estimators", "max_depth", "warnings"))
         else:
-            key = (t.split, t.model_type, t.need_proba,
-                   repr(sorted((k, repr(v)) for k, v in p.items() if k not in ("n_estimators", "warnings"))))
+            key = key_of(t, ("n_estimators", "warnings"))
         groups.setdefault(key, []).append(t)
     leaders, follow = [], {}
-    for g in groups.values():
-        g = sorted(g, key=lambda t: t.params["n_estimators"] if "n_estimators" in t.params else 0)
-        leaders.append(g[-1])
-        if len(g) > 1:
-            follow[g[-1].task_id] = g[:-1]
+
+    def emit(g: List[FitTask], lead: FitTask) -> None:
+        leaders.append(lead)
+        rest = [t for t in g if t is not lead]
+        if rest:
+            follow[lead.task_id] = rest
+
+    for key, g in groups.items():
+        n_of = lambda t: t.params.get("n_estimators", 0)
+        if key[0] == "depth":
+            nmax = max(n_of(t) for t in g)
+            dmax = max(t.params["max_depth"] for t in g)
+            lead = next((t for t in g if n_of(t) == nmax and t.params["max_depth"] == dmax), None)
+            if lead is not None:
+                emit(g, lead)
+                continue
+            subs: Dict[Any, List[FitTask]] = {}   # no dominating fit: share n_estimators only
+            for t in g:
+                subs.setdefault(t.params["max_depth"], []).append(t)
+            for sg in subs.values():
+                emit(sg, max(sg, key=n_of))
+            continue
+        emit(g, max(g, key=n_of))
     order = {t.task_id: i for i, t in enumerate(tasks)}
     leaders.sort(key=lambda t: order[t.task_id])
     return leaders, follow

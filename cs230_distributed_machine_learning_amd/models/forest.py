@@ -293,8 +293,8 @@ class ForestFamily(Family):
         # fits differing only in n_estimators with an explicit random_state grow the same first
         # trees: only the largest is grown, the others predict from its first trees (base.py)
         follow: Dict[int, List[FitTask]] = {}
-        if not sharded:
-            tasks, follow = prefix_groups(tasks)
+        if not sharded:   # on the GPU predictor also max_depth prefixes (depth-capped predicts)
+            tasks, follow = prefix_groups(tasks, depth=data.is_gpu)
         tasks = sorted(tasks, key=_host_only)
         with trace.range("forest_budget"):
             budget = self._budget(data)
@@ -534,10 +534,13 @@ class ForestFamily(Family):
                 outs.append(o)
                 for fo in (follow or {}).get(t.task_id, []):   # prefix fits: leader f's first m trees
                     m = int(fo.params["n_estimators"])
+                    # ... read down to the follower's max_depth when it is shallower (0: whole trees)
+                    cap = int(fo.params["max_depth"]) if fo.params["max_depth"] < t.params["max_depth"] else 0
                     toff_f = np.array([toff[f], toff[f] + m], dtype=np.int64)
                     roff_f = np.array([0, int(rows[f].numel())], dtype=np.int64)
                     if data.is_gpu:
-                        pf = forest_ops.predict(fb, Xb, toff_f, roff_f, rows[f], want_proba=want_proba)
+                        pf = forest_ops.predict(fb, Xb, toff_f, roff_f, rows[f], want_proba=want_proba,
+                                                depth_cap=np.array([cap], dtype=np.int32) if cap else None)
                     else:
                         pf = forest_ops.predict(fb, Xb.numpy(), toff_f, roff_f, rows[f].numpy(), want_proba=want_proba)
                         pf = ((torch.from_numpy(pf[0]), torch.from_numpy(pf[1])) if want_proba
@@ -547,7 +550,7 @@ class ForestFamily(Family):
                                    info={"warnings": fo.params.get("warnings", []), "batch_stats": dict(fb.stats),
                                          "prefix_of": t.task_id})
                     if keep_models and fo.keep:
-                        of.model = extract_forest(fb, int(toff[f]), int(toff[f]) + m, data, fo)
+                        of.model = extract_forest(fb, int(toff[f]), int(toff[f]) + m, data, fo, depth_cap=cap)
                     outs.append(of)
             return outs
         finally:   # the node pool is an arena slot: free it for the next batch
@@ -605,7 +608,7 @@ def native_seed(base: int, tree: int) -> int:
     return x
 
 
-def extract_forest(fb, t0: int, t1: int, data, task: FitTask) -> Dict[str, Any]:
+def extract_forest(fb, t0: int, t1: int, data, task: FitTask, depth_cap: int = 0) -> Dict[str, Any]:
     """Renumber trees [t0, t1) of a batch pool into a standalone forest in pool layout.
 
     Layout matches the kernels' contract: tree j's root is node j, every other node
@@ -613,28 +616,34 @@ def extract_forest(fb, t0: int, t1: int, data, task: FitTask) -> Dict[str, Any]:
     HIP/C++ predictors (``roots`` is kept for readability).  The renumbering is
     breadth-first and vectorised level by level on the pool's own device (a full-depth
     forest on 1M rows has ~10^8 nodes: a per-node host loop would take minutes), and only
-    the extracted nodes leave the device.
+    the extracted nodes leave the device.  ``depth_cap`` > 0 keeps the top depth_cap levels
+    (nodes at that depth become leaves with their stored sums: a max_depth prefix fit).
     """
     nodes = fb.nodes if isinstance(fb.nodes, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(fb.nodes))
     vals = fb.vals if isinstance(fb.vals, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(fb.vals))
     dev = nodes.device
     T = t1 - t0
-    order, lefts = [], []
+    order, lefts, splits = [], [], []
     fo = torch.arange(t0, t1, dtype=torch.int64, device=dev)
     nxt = T
+    level = 0
     while fo.numel():
         rec = nodes[fo]
         internal = rec[:, 0] >= 0
+        if depth_cap > 0 and level >= depth_cap:
+            internal = torch.zeros_like(internal)
         k = int(internal.sum())
         left_new = torch.full((fo.numel(),), -1, dtype=torch.int32, device=dev)
         left_new[internal] = (nxt + 2 * torch.arange(k, device=dev)).to(torch.int32)
         order.append(fo)
         lefts.append(left_new)
+        splits.append(torch.where(internal, rec[:, 0], torch.full_like(rec[:, 0], -1)))
+        level += 1
         l_old = rec[internal, 1].to(torch.int64)
         fo = torch.stack([l_old, l_old + 1], 1).reshape(-1)   # children pairs stay adjacent
         nxt += 2 * k
     old = torch.cat(order)
-    nn = torch.stack([nodes[old, 0], torch.cat(lefts)], 1).cpu().numpy().astype(np.int32)
+    nn = torch.stack([torch.cat(splits), torch.cat(lefts)], 1).cpu().numpy().astype(np.int32)
     vv = vals[old].cpu().numpy().astype(np.float64)
     return {
         "kind": "forest",

@@ -847,7 +847,7 @@ class GpuPredict:
     soon as its trees are complete (ForestArgs.early_pred)."""
 
     def __init__(self, nodes, vals, VC: int, is_reg: bool, n_classes: int, Xb, fit_tree_off, fit_row_off, rows,
-                 want_proba: bool = False):
+                 want_proba: bool = False, depth_cap=None):
         dev = Xb.device
         F = len(fit_tree_off) - 1
         total = int(fit_row_off[-1])
@@ -868,6 +868,9 @@ class GpuPredict:
         p.d = int(Xb.shape[1])
         p.max_rows = int(np.max(np.diff(self.roff_host))) if F else 0
         p.fit_row_off_host = self.roff_host.ctypes.data
+        if depth_cap is not None:   # int32 [F]: fit f walks its trees down to this depth (<= 0: all)
+            self._cap = torch.from_numpy(np.ascontiguousarray(depth_cap, dtype=np.int32)).to(dev)
+            p.fit_depth_cap = native.ptr(self._cap)
         self.args = p
 
     def run(self, fits=None) -> None:
@@ -898,16 +901,21 @@ class GpuPredict:
         return (self.out, self.proba) if self.proba is not None else self.out
 
 
-def predict(fb: ForestBuild, Xb, fit_tree_off: np.ndarray, fit_row_off: np.ndarray, rows, want_proba: bool = False):
-    """Predict rows for F fits; trees of fit f are [fit_tree_off[f], fit_tree_off[f+1])."""
+def predict(fb: ForestBuild, Xb, fit_tree_off: np.ndarray, fit_row_off: np.ndarray, rows, want_proba: bool = False,
+            depth_cap=None):
+    """Predict rows for F fits; trees of fit f are [fit_tree_off[f], fit_tree_off[f+1]) (GPU:
+    read down to depth_cap[f] when given -- a max_depth prefix of deeper grown trees)."""
     F = len(fit_tree_off) - 1
     total = int(fit_row_off[-1])
     C = fb.n_classes
     if fb.on_gpu:
-        gp = GpuPredict(fb.nodes, fb.vals, fb.VC, fb.is_reg, C, Xb, fit_tree_off, fit_row_off, rows, want_proba)
+        gp = GpuPredict(fb.nodes, fb.vals, fb.VC, fb.is_reg, C, Xb, fit_tree_off, fit_row_off, rows, want_proba,
+                        depth_cap=depth_cap)
         gp.run()
         out, proba = gp.out, gp.proba
         return (out, proba) if want_proba else out
+    if depth_cap is not None and np.any(np.asarray(depth_cap) > 0):
+        raise ValueError("depth-capped predict runs on the GPU predictor only")
     lib = native.cpu_lib()
     Xb = np.ascontiguousarray(Xb)
     rows_np = np.ascontiguousarray(rows, dtype=np.int32)

@@ -64,7 +64,7 @@ def _synthetic(rows, d, dev, seed=0):
     return DeviceData(X, y, classification=True, device=dev, name=f"synthetic-{rows}x{d}")
 
 
-def config2(dev, random_state=None):
+def config2(dev, random_state=None, whole=False):
     from cs230_distributed_machine_learning_amd.engine.executor import JobSpec, run_candidates
     from cs230_distributed_machine_learning_amd.search.grid import expand_candidates
 
@@ -78,12 +78,13 @@ def config2(dev, random_state=None):
     torch.cuda.synchronize(dev) if dev.type == "cuda" else None
     t0 = time.time()
     done = 0
-    for i in range(0, len(cands), 4):   # 4 candidates (20 fits) per device batch
-        res = run_candidates(dd, spec, list(range(i, min(i + 4, len(cands)))))
+    step = len(cands) if whole else 4   # 4 candidates (20 fits) per device batch, or the whole grid
+    for i in range(0, len(cands), step):
+        res = run_candidates(dd, spec, list(range(i, min(i + step, len(cands)))))
         assert all(r.ok for r in res)
         done += 5 * len(res)
     torch.cuda.synchronize(dev) if dev.type == "cuda" else None
-    _emit(2, done, time.time() - t0, grid_points=len(cands), random_state=random_state,
+    _emit(2, done, time.time() - t0, grid_points=len(cands), random_state=random_state, whole_grid_call=whole,
           prefix_share=os.environ.get("DML_PREFIX_SHARE", "1") != "0")
 
 
@@ -247,6 +248,7 @@ def main():
     ap.add_argument("--gb-loss", default=None, help="config 6 as a GradientBoostingRegressor of this loss")
     ap.add_argument("--gb-depths", default=None, help="config 6 variant: comma-separated max_depth values")
     ap.add_argument("--gb-estimators", default=None, help="config 6 variant: comma-separated n_estimators values")
+    ap.add_argument("--whole", action="store_true", help="config 2: the whole grid in one run_candidates call")
     ap.add_argument("--random-state", type=int, default=None,
                     help="configs 2 / 6: a fixed random_state in the grid (exact n_estimators prefix sharing)")
     args = ap.parse_args()
@@ -262,7 +264,7 @@ def main():
     if 1 in want:
         config1()
     if 2 in want:
-        config2(dev, args.random_state)
+        config2(dev, args.random_state, args.whole)
     if 4 in want:
         config4(dev, args.lr_rows)
     if 5 in want:

@@ -48,6 +48,10 @@ def _fit_all(model, clf, grid, monkeypatch, tmp_path, share, dev="cpu"):
                                           "subsample": [0.8]}),
     ("GradientBoostingRegressor", False, {"n_estimators": [3, 7, 10], "loss": ["squared_error", "huber"],
                                           "random_state": [0]}),
+    # forests on the GPU also nest max_depth: one leader (most and deepest trees) per split
+    ("RandomForestClassifier", True, {"n_estimators": [3, 6], "max_depth": [2, 4, None], "min_samples_split": [2, 9],
+                                      "random_state": [5]}),
+    ("RandomForestRegressor", False, {"n_estimators": [2, 5], "max_depth": [3, None], "random_state": [2]}),
 ])
 @pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
 def test_prefix_sharing_is_exact(model, clf, grid, dev, monkeypatch, tmp_path):
@@ -70,8 +74,10 @@ def test_prefix_sharing_is_exact(model, clf, grid, dev, monkeypatch, tmp_path):
     grown.update(forest=0, gbrt=0)
     s_off, p_off = _fit_all(model, clf, grid, monkeypatch, tmp_path, False, dev)
     n_off = sum(grown.values())
-    # fewer fits grown: one per (fold, n_estimators-free parameter set)
-    groups = len(grid) // len({c["n_estimators"] for c in grid})
+    # fewer fits grown: one per (fold, n_estimators-free parameter set) -- on the GPU forests also
+    # share max_depth, one per (fold, parameter set free of n_estimators and max_depth)
+    nest = {"n_estimators"} | ({"max_depth"} if dev != "cpu" and model.startswith("RandomForest") else set())
+    groups = len({repr(sorted((k, v) for k, v in c.items() if k not in nest)) for c in grid})
     assert n_off == 4 * len(grid) and n_on == 4 * groups, (n_on, n_off)
     if model.startswith("RandomForest"):
         assert s_on == s_off
@@ -125,13 +131,18 @@ def test_slice_planner_keeps_prefix_groups_together():
     plan = {"model_type": "RandomForestClassifier", "candidates": cands, "cv": 5, "holdout": False,
             "base_params": {"random_state": 3}}
     units = prefix_units(plan, list(range(len(cands))))
-    assert len(units) == 6 and all(len(u) == 4 for u in units)
-    assert all(len({repr({k: v for k, v in cands[i].items() if k != "n_estimators"}) for i in u}) == 1 for u in units)
+    # forests nest n_estimators AND max_depth: one unit per min_samples_leaf
+    assert len(units) == 2 and all(len(u) == 12 for u in units)
+    nest = ("n_estimators", "max_depth")
+    assert all(len({repr({k: v for k, v in cands[i].items() if k not in nest}) for i in u}) == 1 for u in units)
     ctl = SimpleNamespace(scheduler=SimpleNamespace(estimate=lambda mt, c: c), config=SimpleNamespace(chunk_target_s=1e-9))
-    slices = plan_slices(ctl, plan, list(range(len(cands))), 10000, 10, 2, min_slices=6)
+    slices = plan_slices(ctl, plan, list(range(len(cands))), 10000, 10, 2, min_slices=2)
     assert sorted(map(sorted, slices)) == sorted(map(sorted, units))
     # no fixed random_state (or another family): every candidate is its own unit
     plan["base_params"] = {}
     assert len(prefix_units(plan, list(range(len(cands))))) == len(cands)
     assert len(prefix_units(dict(plan, model_type="LogisticRegression", base_params={"random_state": 1}),
                             [0, 1, 2])) == 3
+    # boosting nests n_estimators only
+    gb = dict(plan, model_type="GradientBoostingClassifier", base_params={"random_state": 1})
+    assert len(prefix_units(gb, list(range(len(cands))))) == 6
