@@ -3873,21 +3873,12 @@ static FullBufs* full_bufs(int lane = -1) {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
   return &g_full_bufs[lane < 0 ? t_lane : lane][dev];
 }
-// grows geometrically (2x, >= 32 MB): every regrowth is a hipFree -- a device-wide sync that
-// idled both boosting lanes for ~3 ms, 25 times per config-6 run at the old 1.25x steps
-// (profiles/r5_final_gbrt_cfg6_gaps.txt); a failed 2x request falls back to the exact size
 static bool ensure_bytes(void*& p, size_t& have, size_t need) {
   if (have >= need) return true;
   if (p) { (void)hipFree(p); p = nullptr; have = 0; }
-#ifdef DML_GROW_125   // A/B build: the old 1.25x steps
   const size_t want = need + need / 4;
-#else
-  const size_t want = std::max<size_t>(2 * need, (size_t)32 << 20);
-#endif
-  if (hipMalloc(&p, want) == hipSuccess) { have = want; return true; }
-  (void)hipGetLastError();
-  if (hipMalloc(&p, need) != hipSuccess) { p = nullptr; (void)hipGetLastError(); return false; }
-  have = need;
+  if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return false; }
+  have = want;
   return true;
 }
 

@@ -462,6 +462,11 @@ class GradientBoostingFamily(Family):
                 sel_hist = torch.zeros(max(F * K * S, F) * 256, dtype=torch.int32, device=dev)
                 sel_state = torch.empty(max(F * K * S, F) * 4, dtype=torch.int64, device=dev)
                 fit_delta = torch.zeros(F, dtype=torch.float64, device=dev)
+            # per-stage leaf tables, allocated once at the batch's size and sliced per stage (a fresh
+            # allocation per active-set size cost ~1 ms of allocator time before the stage kernels)
+            slot_sum_all = torch.empty((F * K, S, 2), dtype=torch.float64, device=dev)
+            slot_node_all = torch.empty((F * K, S), dtype=torch.int32, device=dev)
+            slot_val_all = torch.empty((F * K, S), dtype=torch.float64, device=dev)
         if sharded:   # the global training rows (ascending), for subsample draws equal on every rank
             cnts = [data.all_gather_equal(torch.tensor([int(ti.numel())], device=dev)).cpu().numpy() for ti in train_idx]
             gtrain = [data._gather_rows(ti + data.r0, c) for ti, c in zip(train_idx, cnts)]
@@ -605,9 +610,7 @@ class GradientBoostingFamily(Family):
             P = vals.shape[0]
             if fused:   # --- leaf line search + raw update of every row: three kernels ------------
                 tree_raw, tree_loss, tree_lr = cst["tree_raw"], cst["tree_loss"], cst["tree_lr"]
-                slot_sum = torch.zeros((J, S, 2), dtype=torch.float64, device=dev)
-                slot_node = torch.full((J, S), -1, dtype=torch.int32, device=dev)
-                slot_val = torch.empty((J, S), dtype=torch.float64, device=dev)
+                slot_sum, slot_node, slot_val = slot_sum_all[:J].zero_(), slot_node_all[:J].fill_(-1), slot_val_all[:J]
                 sa = native.GbStageArgs(Xb=native.ptr(Xb), ld=Xb.stride(0), n=n, nodes=native.ptr(fb.nodes),
                                         node_val=native.ptr(vals), J=J, K=K, S=S, tree_raw=native.ptr(tree_raw),
                                         tree_loss=native.ptr(tree_loss), tree_lr=native.ptr(tree_lr),
