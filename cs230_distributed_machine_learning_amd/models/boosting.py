@@ -82,6 +82,9 @@ def _max_features(v, d):
 
 
 # ---- percentiles (numpy 'linear' for the initial estimate, sklearn inverted-CDF in leaves) ----
+_LANE_STREAMS: Dict[Any, List[Any]] = {}   # device -> the boosting lanes' streams (made once)
+
+
 def sharded_pct_ok() -> bool:
     """The row-sharded fused stage (phased gbrt.hip entry points) is in the loaded library."""
     try:
@@ -257,12 +260,12 @@ class GradientBoostingFamily(Family):
 
     def _boost_lanes(self, data, batch: List[FitTask], K: int, keep_models: bool,
                      follow: Optional[Dict[int, List[FitTask]]] = None) -> List[FitOutput]:
-        """A device batch split over build LANES (DML_GB_LANES, default 2): each lane boosts its
+        """A device batch split over build LANES (DML_GB_LANES, default 3): each lane boosts its
         share of the fits from its own host thread on its own stream.  A stage is a chain of
         short launches with a host read-back per tree level; with one lane the GPU idles during
         every read-back, with two the other lane's kernels run meanwhile.  Fits are independent,
         so the results are those of one lane (same kernels, same order inside each fit)."""
-        lanes = max(1, min(4, int(os.environ.get("DML_GB_LANES", "2"))))
+        lanes = max(1, min(4, int(os.environ.get("DML_GB_LANES", "3"))))
         if (not data.is_gpu or getattr(data, "is_row_shard", False) or lanes < 2 or len(batch) < 2
                 or getattr(native.hip_lib(), "dml_forest_set_lane", None) is None):
             return self._boost(data, batch, K, keep_models, follow)
@@ -283,7 +286,15 @@ class GradientBoostingFamily(Family):
         data.bin_values()
         dev = data.device
         main = torch.cuda.current_stream(dev)
-        streams = [torch.cuda.Stream(dev) for _ in groups]
+        # the lanes' streams are made once per device and reused by every later batch: streams
+        # drawn fresh from torch's pool land on other hardware queues each time, and a job whose two
+        # lane streams shared a queue with each other (or with the builder's side streams) ran ~40 %
+        # slower (the second of back-to-back config-6 jobs: 1.53 vs 1.08 s,
+        # profiles/r5_gbrt_cfg6_back_to_back.txt)
+        pool = _LANE_STREAMS.setdefault(dev, [])
+        while len(pool) < len(groups):
+            pool.append(torch.cuda.Stream(dev))
+        streams = pool[:len(groups)]
         results: List[Any] = [None] * len(groups)
         errors: List[Any] = [None] * len(groups)
 

@@ -228,7 +228,17 @@ def config6(dev, loss=None, depths=None, estimators=None, random_state=None):
     cands = expand_candidates("GridSearchCV", {"param_grid": grid})
     spec = JobSpec(model, cands, cv=5, holdout=False, keep_models="none")
     dd.binned()
+    if os.environ.get("DML_C6_WARMUP", "1") != "0":
+        # untimed warmup fit (as bench.py's warmup steps): first kernel launches load their code
+        # objects, the device arenas and caching allocator reach their sizes
+        warm = [dict(c, n_estimators=3) for c in cands if c["n_estimators"] == min(x["n_estimators"] for x in cands)]
+        run_candidates(dd, JobSpec(model, warm, cv=5, holdout=False, keep_models="none"), list(range(len(warm))))
     torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    for rep in range(int(os.environ.get("DML_C6_REPEAT", "1")) - 1):   # study: back-to-back jobs
+        t0 = time.time()
+        run_candidates(dd, spec, list(range(len(cands))))
+        torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+        print(f"repeat {rep}: {time.time() - t0:.3f} s", file=sys.stderr, flush=True)
     trace.summary(reset=True)
     t0 = time.time()
     res = run_candidates(dd, spec, list(range(len(cands))))
