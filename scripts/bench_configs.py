@@ -7,7 +7,12 @@
   4  RandomizedSearchCV LogisticRegression n_iter=512 cv=5 on --lr-rows x 1000 dense
   5  mixed queue: concurrent RF + LR jobs from several sessions through the controller
   6  GradientBoostingClassifier GridSearchCV n_estimators {100, 200} x max_depth {3, 5},
-     cv=5, 1M x 100 synthetic, 1 GPU (every fit of the grid boosted in one stage loop)
+     cv=5, 1M x 100 synthetic, 1 GPU (every fit of the grid boosted in one stage loop), timed
+     after an untimed warmup fit (DML_C6_WARMUP=0: the cold first job); --gb-loss / --gb-depths /
+     --gb-estimators / --random-state give its variants
+
+  configs 2 and 6 take --random-state N (a fixed random_state in the grid: exact n_estimators /
+  max_depth prefix sharing, models/base.py prefix_groups); config 2 --whole runs its grid as one call
 
     python scripts/bench_configs.py --configs 1,2,4,5 [--lr-rows 10000000]
 
