@@ -15,10 +15,18 @@ Differences, by design:
 * D27/D28 — worker ids are never reused, and an unknown heartbeat answers 404 so the
   worker re-registers.
 Placement is the native LPT core in csrc/runtime/sched.cpp.
+
+The learned state (per-algorithm calibration, its decayed sums and each device's speed
+factor) is persisted as JSON next to the job journal after every update and reloaded at
+start, as the reference persists and reloads its runtime predictor
+(aws-prod/scheduler/scheduler_service.py:44-46,82): a restarted service slices its first
+search with the warm calibration instead of 1.0 s per cost unit.
 """
 from __future__ import annotations
 
 import ctypes
+import json
+import os
 import threading
 import time
 from dataclasses import asdict, dataclass, field
@@ -59,7 +67,8 @@ class Unit:
 
 
 class Scheduler:
-    def __init__(self, dead_after_s: float = 10.0, algo_weight: Optional[Dict[str, float]] = None, ema: float = 0.3):
+    def __init__(self, dead_after_s: float = 10.0, algo_weight: Optional[Dict[str, float]] = None, ema: float = 0.3,
+                 state_path: Optional[str] = None):
         self._lock = threading.RLock()
         self.workers: Dict[str, WorkerState] = {}
         self._next_id = 1
@@ -70,13 +79,57 @@ class Scheduler:
         self.ema = ema
         self.assigned: Dict[str, Tuple[str, Unit, float]] = {}   # unit_id -> (worker, unit, reserved seconds)
         self.held: List[Unit] = []
+        self.device_speed: Dict[str, float] = {}   # "host/device" -> speed factor (survives re-registration)
+        self.state_path = state_path
+        if state_path:
+            self._load_state()
+
+    # ---- persisted calibration -------------------------------------------------------------
+    @staticmethod
+    def _dev_key(w: WorkerState) -> str:
+        return f"{w.host}/{w.device}"
+
+    def state(self) -> Dict:
+        with self._lock:
+            for w in self.workers.values():
+                self.device_speed[self._dev_key(w)] = w.speed_factor
+            return {"version": 1, "calib": dict(self.calib),
+                    "calib_sums": {a: list(v) for a, v in self._calib_sums.items()},
+                    "device_speed": dict(self.device_speed)}
+
+    def _load_state(self) -> None:
+        try:
+            with open(self.state_path, "r", encoding="utf-8") as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            return
+        if not isinstance(d, dict) or d.get("version") != 1:
+            return
+        try:
+            self.calib = {str(a): float(v) for a, v in d.get("calib", {}).items() if float(v) > 0}
+            self._calib_sums = {str(a): (float(v[0]), float(v[1])) for a, v in d.get("calib_sums", {}).items()}
+            self.device_speed = {str(k): max(0.05, float(v)) for k, v in d.get("device_speed", {}).items()}
+        except (TypeError, ValueError, IndexError):
+            self.calib, self._calib_sums, self.device_speed = {}, {}, {}
+
+    def save_state(self) -> None:
+        if not self.state_path:
+            return
+        st = self.state()
+        os.makedirs(os.path.dirname(os.path.abspath(self.state_path)), exist_ok=True)
+        tmp = f"{self.state_path}.{os.getpid()}.{threading.get_ident()}.tmp"
+        with open(tmp, "w", encoding="utf-8") as f:
+            json.dump(st, f)
+        os.replace(tmp, self.state_path)
 
     # ---- membership ----------------------------------------------------------------------
     def register(self, host: str = "local", mem_capacity_mb: int = 0, device: str = "cpu") -> str:
         with self._lock:
             wid = str(self._next_id)
             self._next_id += 1
-            self.workers[wid] = WorkerState(worker_id=wid, host=host, device=device, mem_capacity_mb=int(mem_capacity_mb))
+            w = WorkerState(worker_id=wid, host=host, device=device, mem_capacity_mb=int(mem_capacity_mb))
+            w.speed_factor = self.device_speed.get(self._dev_key(w), 1.0)
+            self.workers[wid] = w
             return wid
 
     def heartbeat(self, worker_id: str) -> bool:
@@ -144,7 +197,13 @@ class Scheduler:
                     pred = self.estimate(unit.algo, unit.cost)
                     ratio = pred / seconds if seconds > 0 else 1.0
                     w.speed_factor = max(0.05, (1 - self.ema) * w.speed_factor + self.ema * ratio * w.speed_factor)
+                    self.device_speed[self._dev_key(w)] = w.speed_factor
             self.complete(unit.unit_id)
+            if self.state_path and unit.cost > 0 and seconds > 0:
+                try:
+                    self.save_state()
+                except OSError:
+                    pass
 
     # ---- placement ---------------------------------------------------------------------------
     def place(self, units: Sequence[Unit]) -> Dict[str, List[Unit]]:

@@ -102,13 +102,21 @@ def job_plan(request: Dict[str, Any]) -> Dict[str, Any]:
     }
 
 
+def scheduler_state_path(config: Config) -> Optional[str]:
+    """Where the scheduler's learned calibration lives: next to the job journal."""
+    if not config.journal:
+        return None
+    return os.path.join(os.path.dirname(os.path.abspath(config.journal)), "scheduler_state.json")
+
+
 class Controller:
     def __init__(self, config: Optional[Config] = None, runner: Optional["Runner"] = None):
         self.config = config or Config.from_env()
         self.registry = DatasetRegistry(self.config.data_root)
         self.models = ModelStore(self.config.models_dir)
         self.table = JobTable(self.config.journal)
-        self.scheduler = Scheduler(self.config.dead_after_s, self.config.algo_weight)
+        self.scheduler = Scheduler(self.config.dead_after_s, self.config.algo_weight,
+                                   state_path=scheduler_state_path(self.config))
         self.runner = runner or LocalRunner(self)
         if runner is not None:
             runner.bind(self)
