@@ -20,7 +20,9 @@ reported once and the job hangs below 100 % (D5, master/task_handler.py:91).  He
   a data-parallel epoch, right after its table scatter) makes that rank SIGSTOP
   itself on entering the named collective: a HUNG peer (its sockets stay open,
   unlike a dead one), which the survivors' collective timeouts must turn into a fallback;
-  ``DML_FAIL_RANK_IN`` (same form) makes it raise there instead.
+  ``DML_FAIL_RANK_IN`` (same form) makes it raise there instead;
+  ``DML_OOM_RANK_IN`` (same form, ``load``) makes it run out of memory allocating the
+  load's receive buffers (every rank then gives that load up together).
 """
 from __future__ import annotations
 
@@ -32,6 +34,10 @@ from typing import Optional, Tuple
 
 class InjectedFault(RuntimeError):
     pass
+
+
+class InjectedOOM(RuntimeError):
+    """Stands in for ``torch.cuda.OutOfMemoryError`` on a CPU box (fault injection)."""
 
 
 @dataclass(frozen=True)
@@ -113,6 +119,22 @@ def maybe_stop_in_collective(rank: int, what: str) -> None:
         import signal
 
         os.kill(os.getpid(), signal.SIGSTOP)
+
+
+def maybe_oom_in_collective(rank: int, what: str) -> None:
+    """``DML_OOM_RANK_IN="<rank>:<collective>"``: that rank runs out of memory allocating its
+    receive buffers for the named side-group task (``load``)."""
+    if _rank_spec("DML_OOM_RANK_IN", rank, what):
+        raise InjectedOOM(f"injected out-of-memory allocating the {what} buffers on rank {rank}")
+
+
+def maybe_delay_staging() -> None:
+    """``DML_STAGE_DELAY_S``: every host staging takes that much longer (a large table)."""
+    d = float(os.environ.get("DML_STAGE_DELAY_S", "0") or 0.0)
+    if d > 0:
+        import time
+
+        time.sleep(d)
 
 
 def maybe_kill(rank: int, slices_done: int) -> None:

@@ -138,8 +138,12 @@ class Controller:
             "models": supported_models()}
 
     def health(self) -> Resp:
-        return 200, {"status": "healthy", "timestamp": time.time(), **self.table.summary(),
-                     "workers": len(self.scheduler.alive_workers())}
+        body = {"status": "healthy", "timestamp": time.time(), **self.table.summary(),
+                "workers": len(self.scheduler.alive_workers())}
+        info = getattr(self.runner, "cluster_info", None)
+        if info is not None:   # the collective plane (generation, members, per-job transport)
+            body["cluster"] = info()
+        return 200, body
 
     def create_session(self) -> Resp:
         return 201, {"message": "Session created", "session_id": self.table.create_session()}

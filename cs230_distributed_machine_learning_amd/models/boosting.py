@@ -270,6 +270,16 @@ class GradientBoostingFamily(Family):
                 or getattr(native.hip_lib(), "dml_forest_set_lane", None) is None):
             return self._boost(data, batch, K, keep_models, follow)
         lanes = min(lanes, len(batch))
+        # each lane holds its own workspace arena slot and whole-histogram buffers for its share
+        # of the batch (the batch cap in ``run`` prices one build): drop lanes until the batch
+        # state plus every lane's workspace fits the free HBM
+        per_fit = K * data.n * (8 + 4 + 4 + 1) * 1.5
+        free = torch.cuda.mem_get_info(data.device)[0]
+        lane_ws = lambda L: 2.0 * per_fit * (-(-len(batch) // L)) + (256 << 20)   # noqa: E731
+        while lanes > 1 and len(batch) * per_fit + lanes * lane_ws(lanes) > 0.9 * free:
+            lanes -= 1
+        if lanes < 2:
+            return self._boost(data, batch, K, keep_models, follow)
         # longest-processing-time split of the fits (stage count x depth x trees per stage)
         w = [t.params["n_estimators"] * max(1, min(t.params["max_depth"], 12)) for t in batch]
         groups: List[List[int]] = [[] for _ in range(lanes)]

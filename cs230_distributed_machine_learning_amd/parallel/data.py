@@ -15,11 +15,14 @@ ranks grow identical trees for identical seeds.
 from __future__ import annotations
 
 import json
-from typing import Optional
+import os
+import threading
+from typing import Callable, Dict, Optional, Set, Tuple
 
 import numpy as np
 import torch
 
+from ..engine import faults
 from . import dist
 
 
@@ -48,8 +51,26 @@ def broadcast_table(X: Optional[np.ndarray], y: Optional[np.ndarray], device: to
     else:
         st.wait([key])
         meta = json.loads(st.get(key))
-        yd = torch.empty((meta["n"],), dtype=torch.float64, device=device)
-    Xd = torch.empty((meta["n"], meta["d"]), dtype=torch.float32, device=device)
+        yd = None
+    # every rank allocates its receive buffers, then all vote: a rank out of memory makes
+    # EVERY rank give the load up before the broadcast (CollectiveAborted), instead of
+    # leaving its peers inside a collective it never joins
+    Xd, err = None, None
+    try:
+        faults.maybe_oom_in_collective(inf.rank, "load")
+        if yd is None:
+            yd = torch.empty((meta["n"],), dtype=torch.float64, device=device)
+        Xd = torch.empty((meta["n"], meta["d"]), dtype=torch.float32, device=device)
+    except torch.cuda.OutOfMemoryError as e:
+        err = e
+    except faults.InjectedOOM as e:
+        err = e
+    if not dist.vote_all_ok(err is None, group=group):
+        Xd = yd = None
+        if inf.rank == 0:
+            st.delete_key(key)
+        raise dist.CollectiveAborted(f"table load given up on every rank: a rank could not allocate "
+                                     f"its {meta['n']}x{meta['d']} buffer" + (f" ({err})" if err else ""))
     _pipelined_broadcast(X if inf.rank == 0 else None, Xd, group=group)
     dist.broadcast(yd, 0, group=group)
     dist.barrier(group=group)
@@ -164,11 +185,50 @@ def _y_path(path: str) -> str:
     return path + ".y.npz"
 
 
+_STAGE_LOCK = threading.Lock()
+_STAGE_PATH_LOCKS: Dict[str, threading.Lock] = {}
+_STAGE_PINNED: Set[str] = set()
+
+
+def _path_lock(path: str) -> threading.Lock:
+    with _STAGE_LOCK:
+        return _STAGE_PATH_LOCKS.setdefault(path, threading.Lock())
+
+
+def ensure_staged(load: Callable[[], Tuple[np.ndarray, np.ndarray]], path: str, pin: bool = False) -> str:
+    """Stage the table at ``path`` exactly once per process, whichever thread asks first
+    (rank 0's staging thread for host-staged jobs, its collective thread for sharded loads):
+    a per-path lock makes a second caller wait for the first one's file instead of
+    truncating it under a reader.  ``load()`` is called only when the file is missing.
+    ``pin``: a host-staged job reads the file; ``release_staged`` keeps pinned files."""
+    with _path_lock(path):
+        if pin:
+            _STAGE_PINNED.add(path)
+        if not os.path.exists(path):
+            X, y = load()
+            stage_host(X, y, path)
+    return path
+
+
+def release_staged(path: str) -> bool:
+    """Delete a staged table no host-staged job reads (a sharded load's transient copy in
+    ``/dev/shm`` is host RAM on top of the registry's parsed copy)."""
+    with _path_lock(path):
+        if path in _STAGE_PINNED:
+            return False
+        for p in (path, _y_path(path)):
+            try:
+                os.remove(p)
+            except OSError:
+                pass
+        return True
+
+
 def stage_host(X: np.ndarray, y: np.ndarray, path: str, threads: int = 8) -> str:
     """Write the table for host-staged / sharded loads: X as a raw ``.npy`` (memory-mappable:
     a rank reads only the rows it copies) filled by ``threads`` parallel row-chunk copies
-    (numpy releases the GIL for them), y + label metadata in a small sidecar."""
-    import os
+    (numpy releases the GIL for them), y + label metadata in a small sidecar.  Temporary
+    names are unique per process and thread, and the final names appear by atomic rename."""
     from concurrent.futures import ThreadPoolExecutor
 
     y = np.asarray(y)
@@ -180,7 +240,8 @@ def stage_host(X: np.ndarray, y: np.ndarray, path: str, threads: int = 8) -> str
     else:
         meta["y"] = str(y.dtype)
         y_arr = y
-    tmp = path + ".tmp.npy"
+    uniq = f"{os.getpid()}.{threading.get_ident()}"
+    tmp = f"{path}.{uniq}.tmp.npy"
     mm = np.lib.format.open_memmap(tmp, mode="w+", dtype=np.float32, shape=tuple(X.shape))
     n = X.shape[0]
     step = max(1, -(-n // max(1, threads * 4)))
@@ -192,7 +253,7 @@ def stage_host(X: np.ndarray, y: np.ndarray, path: str, threads: int = 8) -> str
         list(ex.map(copy, range(0, n, step)))
     mm.flush()
     del mm
-    ytmp = _y_path(path) + ".tmp.npz"
+    ytmp = f"{_y_path(path)}.{uniq}.tmp.npz"
     np.savez(ytmp, y=y_arr, meta=np.array(json.dumps(meta)))
     os.replace(ytmp, _y_path(path))   # the sidecar first: a reader that sees X sees its labels
     os.replace(tmp, path)
@@ -248,13 +309,23 @@ def sharded_load(path: str, device: torch.device, group=None):
     W = inf.world
     q = -(-n // W)                                   # equal blocks (the last one padded)
     r0, r1 = min(n, inf.rank * q), min(n, (inf.rank + 1) * q)
-    shard = torch.zeros((q, d), dtype=torch.float32, device=device)
+    shard = full = None
+    try:   # both buffers first, then a vote: an OOM on one rank aborts the load on every rank
+        faults.maybe_oom_in_collective(inf.rank, "load")
+        shard = torch.zeros((q, d), dtype=torch.float32, device=device)
+        full = torch.empty((W * q, d), dtype=torch.float32, device=device)
+        ok = True
+    except (torch.cuda.OutOfMemoryError, faults.InjectedOOM):
+        ok = False
+    if not dist.vote_all_ok(ok, group=group):
+        shard = full = None
+        raise dist.CollectiveAborted(f"sharded load given up on every rank: a rank could not allocate {n}x{d}")
     t0 = time.perf_counter()
     if r1 > r0:
         shard[:r1 - r0].copy_(_mapped_rows(Xm[r0:r1], device))
     if shard.is_cuda:
         torch.cuda.synchronize(device)
     h2d = time.perf_counter() - t0
-    full = dist.all_gather_rows(shard, group=group)   # [W * q, d] in rank order
+    full = dist.all_gather_rows(shard, group=group, out=full)   # [W * q, d] in rank order
     dist.barrier(group=group)
     return full[:n], y, h2d

@@ -38,6 +38,22 @@ class DistInfo:
 
 
 _INFO: Optional[DistInfo] = None
+_GEN = 0   # communicator generation of the current default group (0 = the launch group)
+
+
+def _failure_env() -> None:
+    """RCCL failure handling: a collective that outlives its timeout (a peer
+    rank died or hung mid-collective) must not take the service down with it.  Mode 2
+    (CleanUpOnly) makes the watchdog abort the communicator WITHOUT tearing the process
+    down, and blocking wait makes the timed-out collective raise in the thread that issued
+    it -- the runner's collective thread / data-parallel epoch then reports the error and
+    the dispatcher re-forms the group (parallel/runner.py).  Mode 1 (TearDown) would end
+    every survivor, rank 0 (controller + gateway + store) included.  The monitor thread
+    std::abort()s a process whose watchdog looks stuck (an abort that itself blocks): that
+    is a teardown too."""
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
+    os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
+    os.environ.setdefault("TORCH_NCCL_ENABLE_MONITORING", "0")
 
 
 def init(backend: Optional[str] = None, timeout_s: float = 1800.0, want_gpu: Optional[bool] = None) -> DistInfo:
@@ -69,18 +85,7 @@ def init(backend: Optional[str] = None, timeout_s: float = 1800.0, want_gpu: Opt
         os.environ.setdefault("MASTER_PORT", "29561")
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(world))
-        # RCCL failure handling: a collective that outlives its timeout (a peer
-        # rank died or hung mid-collective) must not take the service down with it.  Mode 2
-        # (CleanUpOnly) makes the watchdog abort the communicator WITHOUT tearing the process
-        # down, and blocking wait makes the timed-out collective raise in the thread that
-        # issued it -- the runner's collective thread / data-parallel epoch then reports the
-        # error and the dispatcher marks the group broken (parallel/runner.py).  Mode 1
-        # (TearDown) would end every survivor, rank 0 (controller + gateway + store) included.
-        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
-        os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
-        # the monitor thread std::abort()s a process whose watchdog looks stuck (an abort that
-        # itself blocks): that is a teardown too
-        os.environ.setdefault("TORCH_NCCL_ENABLE_MONITORING", "0")
+        _failure_env()
         timeout_s = float(os.environ.get("DML_COLLECTIVE_TIMEOUT_S", timeout_s))
         kw = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
@@ -92,6 +97,95 @@ def init(backend: Optional[str] = None, timeout_s: float = 1800.0, want_gpu: Opt
 
 def info() -> DistInfo:
     return _INFO or DistInfo()
+
+
+def generation() -> int:
+    return _GEN
+
+
+def regroup_timeout_s() -> float:
+    """How long a communicator re-formation waits for every member (``DML_REGROUP_TIMEOUT_S``,
+    default 60 s); also the per-collective timeout of the re-formed default group's setup."""
+    return float(os.environ.get("DML_REGROUP_TIMEOUT_S", "60"))
+
+
+class RegroupError(RuntimeError):
+    """A communicator generation could not be formed (a member never arrived or failed)."""
+
+
+def regroup(base_store, gen: int, rank: int, world: int, backend: str, device: torch.device,
+            local_rank: int = 0, timeout_s: Optional[float] = None) -> DistInfo:
+    """Leave the current process group (if any) and join communicator generation ``gen``:
+    ``world`` members, this process at ``rank``, rendezvous under the store prefix
+    ``gen<g>/`` of the service's control-plane store ``base_store`` -- the same TCPStore the
+    launch group used, so survivors, respawned ranks and processes that joined later
+    (which never had a process group) meet on equal terms.  The side and data-parallel
+    communicators are rebuilt on the new group.  Every member calls this with the same
+    ``gen``/``world``/``backend``; a member that is missing after ``timeout_s`` makes every
+    other member raise ``RegroupError`` before any communicator is built (a presence
+    rendezvous on the store precedes the process-group constructor, which would otherwise
+    block for its full timeout).  On failure this process is left with NO process group."""
+    global _INFO, _SIDE, _DP, _GEN
+    from torch.distributed import PrefixStore
+
+    timeout_s = regroup_timeout_s() if timeout_s is None else float(timeout_s)
+    _SIDE = None
+    _DP = None
+    if dist.is_initialized():
+        try:
+            dist.destroy_process_group()
+        except Exception:   # a communicator already aborted by its watchdog
+            pass
+    _INFO = DistInfo(rank, world, local_rank, device, "none")
+    st = PrefixStore(f"gen{gen}", base_store)
+    st.set(f"here/{rank}", "1")
+    try:
+        st.wait([f"here/{r}" for r in range(world)], datetime.timedelta(seconds=timeout_s))
+    except Exception as e:
+        raise RegroupError(f"generation {gen}: not every member arrived within {timeout_s:.0f}s") from e
+    _failure_env()
+    coll_timeout = float(os.environ.get("DML_COLLECTIVE_TIMEOUT_S", "1800"))
+    kw = dict(backend=backend, store=PrefixStore("pg", st), rank=rank, world_size=world,
+              timeout=datetime.timedelta(seconds=coll_timeout))
+    if backend == "nccl":
+        kw["device_id"] = device
+    try:
+        dist.init_process_group(**kw)
+    except Exception as e:
+        raise RegroupError(f"generation {gen}: process group init failed: {e}") from e
+    _INFO = DistInfo(rank, world, local_rank, device, backend)
+    _GEN = gen
+    try:
+        side_group()
+        dp_group()
+    except Exception as e:
+        _SIDE = _DP = None
+        try:
+            dist.destroy_process_group()
+        except Exception:
+            pass
+        _INFO = DistInfo(rank, world, local_rank, device, "none")
+        raise RegroupError(f"generation {gen}: side / data-parallel communicators failed: {e}") from e
+    # every member is through: the presence keys can go (rank 0 only, after a barrier)
+    barrier()
+    if rank == 0:
+        for r in range(world):
+            st.delete_key(f"here/{r}")
+    return _INFO
+
+
+def leave_group() -> None:
+    """Drop this process's communicators (a member that failed a re-formation, or that left
+    the group): ``info().is_dist`` is False until the next ``regroup``."""
+    global _INFO, _SIDE, _DP
+    _SIDE = _DP = None
+    if dist.is_initialized():
+        try:
+            dist.destroy_process_group()
+        except Exception:
+            pass
+    if _INFO is not None:
+        _INFO = DistInfo(_INFO.rank, _INFO.world, _INFO.local_rank, _INFO.device, "none")
 
 
 _SIDE = None
@@ -115,6 +209,26 @@ def side_group():
 
 
 _DP = None
+
+
+class CollectiveAborted(RuntimeError):
+    """Every rank of a side-group task gave it up TOGETHER before any large collective was
+    entered (a rank could not allocate its buffers -- OOM -- or rank 0 could not prepare the
+    table): the communicator is intact, only this task falls back (host staging)."""
+
+    consistent = True
+
+
+def vote_all_ok(ok: bool, group=None) -> bool:
+    """True when every rank of ``group`` passed ``ok`` (one tiny MIN all-reduce).  Used before
+    a large collective so a rank that cannot take part (OOM on its receive buffer) makes
+    every rank skip the collective, instead of leaving its peers stuck inside it."""
+    if not info().is_dist:
+        return ok
+    dev = info().device if info().backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
 
 
 class CollectiveError(RuntimeError):
@@ -167,13 +281,15 @@ def broadcast(t: torch.Tensor, src: int = 0, group=None) -> torch.Tensor:
     return t
 
 
-def all_gather_rows(shard: torch.Tensor, group=None) -> torch.Tensor:
-    """Concatenate equal-size row shards of every rank (rank order) on every rank."""
+def all_gather_rows(shard: torch.Tensor, group=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Concatenate equal-size row shards of every rank (rank order) on every rank (into
+    ``out`` when given: a caller that pre-allocates can vote on the allocation first)."""
     inf = info()
     if not inf.is_dist:
         return shard
     shard = shard.contiguous()
-    out = torch.empty((shard.shape[0] * inf.world, *shard.shape[1:]), dtype=shard.dtype, device=shard.device)
+    if out is None:
+        out = torch.empty((shard.shape[0] * inf.world, *shard.shape[1:]), dtype=shard.dtype, device=shard.device)
     if inf.backend == "nccl":
         dist.all_gather_into_tensor(out, shard, group=group)
     else:
@@ -243,9 +359,10 @@ def service_client(timeout_s: float = 300.0):
 
 
 def destroy() -> None:
-    global _INFO, _SIDE, _DP
+    global _INFO, _SIDE, _DP, _GEN
     _SIDE = None
     _DP = None
+    _GEN = 0
     if dist.is_initialized():
         dist.destroy_process_group()
     _INFO = None

@@ -50,6 +50,7 @@ from __future__ import annotations
 import collections
 import json
 import os
+import queue
 import tempfile
 import threading
 import time
@@ -256,6 +257,51 @@ class WorkerCore:
         # the data-parallel communicator (short timeout; created collectively right after the
         # side group, in the same order on every in-group rank)
         self.dp = dist.dp_group() if (in_group and self.inf.is_dist) else None
+        self._coll_thread: Optional[threading.Thread] = None
+        self.gen = 0                            # communicator generation this rank belongs to
+
+    # ---- communicator generations -------------------------------------------------------
+    def start_collective_thread(self, ctl: Optional[Controller], start: int = 0) -> None:
+        if self.side is None:
+            return
+        t = threading.Thread(target=collective_loop, args=(self, ctl, start), daemon=True,
+                             name=f"dml-coll-{self.wid}-g{self.gen}")
+        self._coll_thread = t
+        t.start()
+
+    def regroup(self, a: Dict[str, Any], ctl: Optional[Controller]) -> Dict[str, Any]:
+        """Join communicator generation ``a['gen']`` (dispatcher's regroup epoch): stop this
+        rank's collective thread (the dispatcher posted a stop at the end of the task
+        stream), leave the old process group, rendezvous with the other members on the
+        control-plane store and build the new default / side / data-parallel communicators
+        (parallel/dist.py regroup), then restart the collective thread at ``coll_base``.
+        Survivors, respawned ranks and processes that joined later all become members."""
+        t0 = time.perf_counter()
+        old = self._coll_thread
+        if old is not None and old.is_alive():
+            old.join(timeout=dist.side_timeout_s() + 30.0)
+            if old.is_alive():
+                raise dist.RegroupError("the collective thread is still inside an old-generation collective")
+        self._coll_thread = None
+        members = [int(m) for m in a["members"]]
+        rank = members.index(self.wid)
+        dev = self.device
+        local = dev.index if (dev.type == "cuda" and dev.index is not None) else 0
+        self.side = self.dp = None
+        self.in_group = False
+        try:
+            dist.regroup(self.store._s, int(a["gen"]), rank, len(members), a["backend"], dev, local_rank=local)
+        except Exception:
+            dist.leave_group()
+            self.inf = dist.info()
+            raise
+        self.inf = dist.info()
+        self.gen = int(a["gen"])
+        self.in_group = True
+        self.side = dist.side_group()
+        self.dp = dist.dp_group()
+        self.start_collective_thread(ctl, int(a["coll_base"]))
+        return {"gen": self.gen, "rank": rank, "world": len(members), "wall": time.perf_counter() - t0}
 
     # ---- job messages and datasets ------------------------------------------------------
     def job_msg(self, seq: int) -> Dict[str, Any]:
@@ -312,28 +358,31 @@ class WorkerCore:
         X = y = None
         mode_key = "dataset/mode" + tag
         if self.inf.rank == 0:
-            ds = ctl.registry.load(msg["dataset_id"], plan["feature_columns"], plan["target_column"])
-            X, y = ds.X, ds.y
-            binned = ctl is not None and _binned_only_table(ctl, plan, X, self.device)
-            mode = "binned" if binned else "full"
-            if not binned and self.inf.world > 1 and self.stage_dir and X.nbytes >= shard_load_min_bytes():
-                # large table: staged once on the host, every rank copies its own 1/N row block
-                # over its own PCIe link, one all-gather over xGMI completes it (sharded_load)
-                path = staged_path(self.stage_dir, msg["dataset_key"])
-                if not os.path.exists(path):
-                    pdata.stage_host(X, y, path)
-                mode = "sharded:" + path
+            try:
+                ds = ctl.registry.load(msg["dataset_id"], plan["feature_columns"], plan["target_column"])
+                X, y = ds.X, ds.y
+                binned = ctl is not None and _binned_only_table(ctl, plan, X, self.device)
+                mode = "binned" if binned else "full"
+                if not binned and self.inf.world > 1 and self.stage_dir and X.nbytes >= shard_load_min_bytes():
+                    # large table: staged once on the host, every rank copies its own 1/N row
+                    # block over its own PCIe link, one all-gather over xGMI completes it
+                    path = pdata.ensure_staged(lambda: (X, y), staged_path(self.stage_dir, msg["dataset_key"]))
+                    mode = "sharded:" + path
+            except Exception as e:   # every rank gives the load up together: no collective entered
+                self.store_raw().set(mode_key, f"error:{type(e).__name__}: {e}")
+                raise dist.CollectiveAborted(f"rank 0 could not prepare {msg['dataset_id']!r}: {e}") from e
             self.store_raw().set(mode_key, mode)
         else:
-            # on the side group, bounded like the side collectives themselves: a rank 0 that
-            # fails before publishing the mode must not hold this thread past the side deadline
-            if group is not None:
-                import datetime
+            # rank 0 parses (and, for a large table, host-stages) before it publishes the mode:
+            # that is not a collective, so it is bounded by the load-preparation deadline, not
+            # by the side timeout (a 1 GB+ CSV parse can outlast the latter); a rank 0 that
+            # fails publishes an error mode instead
+            import datetime
 
-                self.store_raw().wait([mode_key], datetime.timedelta(seconds=dist.side_timeout_s()))
-            else:
-                self.store_raw().wait([mode_key])
+            self.store_raw().wait([mode_key], datetime.timedelta(seconds=load_prep_timeout_s()))
             mode = self.store_raw().get(mode_key).decode()
+            if mode.startswith("error:"):
+                raise dist.CollectiveAborted(f"rank 0 could not prepare {msg['dataset_id']!r}: {mode[6:]}")
             binned = mode == "binned"
         if mode.startswith("sharded:"):
             Xd, y_host, h2d = pdata.sharded_load(mode[len("sharded:"):], self.device, group=group)
@@ -351,6 +400,8 @@ class WorkerCore:
         dist.barrier(group=group)
         if self.inf.rank == 0:
             self.store_raw().delete_key(mode_key)
+            if mode.startswith("sharded:"):   # the transient host copy, unless a staged job reads it
+                pdata.release_staged(mode[len("sharded:"):])
         self._keep(msg["dataset_key"], dd)
         return dd
 
@@ -372,6 +423,8 @@ class WorkerCore:
             return self._dp(a, ctl)
         if kind == "refit":
             return self._refit(a, ctl)
+        if kind == "regroup":
+            return self.regroup(a, ctl)
         if kind == "scores":
             return self._scores(a)
         raise ValueError(f"unknown assignment kind {kind!r}")
@@ -540,17 +593,20 @@ class _null_ctx:
         return False
 
 
-def collective_loop(core: WorkerCore, ctl: Optional[Controller] = None) -> None:
+def collective_loop(core: WorkerCore, ctl: Optional[Controller] = None, start: int = 0) -> None:
     """An in-group rank's collective thread: runs the dispatcher's collective tasks
-    (``coll/<i>``: dataset broadcasts, job score gathers) in order on the side group and
-    its own stream while the worker thread keeps running slices.  A failed collective
-    means the group is broken: the thread reports it and stops."""
+    (``coll/<i>``, from ``start``: dataset broadcasts, job score gathers) in order on the
+    side group and its own stream while the worker thread keeps running slices.  A task
+    every rank gave up together (``CollectiveAborted``: an OOM vote, a table rank 0 could
+    not prepare) is answered and the thread goes on; any other failure means the
+    communicator is unusable: the thread reports it and stops (the dispatcher re-forms the
+    group, ``WorkerCore.regroup``)."""
     st = LockedStore(core.store._s, waiter=_private_client())
     stream = None
     if core.device.type == "cuda":
         torch.cuda.set_device(core.device)
         stream = torch.cuda.Stream(core.device)
-    i = 0
+    i = start
     while True:
         key = f"coll/{i}"
         try:
@@ -569,6 +625,9 @@ def collective_loop(core: WorkerCore, ctl: Optional[Controller] = None) -> None:
         failed = False
         try:
             out = core.collective(a, ctl, stream)
+        except dist.CollectiveAborted as e:
+            log.warning("worker %d: side task %d given up on every rank: %s", core.wid, i, e)
+            out = {"error": f"{type(e).__name__}: {e}", "aborted": True}
         except Exception as e:
             traceback.print_exc()
             out, failed = {"error": f"{type(e).__name__}: {e}"}, True
@@ -602,8 +661,7 @@ def worker_loop(core: WorkerCore, ctl: Optional[Controller] = None, heartbeat: b
     exits non-zero; the dispatcher re-queues its slice to the survivors."""
     st, wid = core.store, core.wid
     hb = _Heartbeat(st, wid) if heartbeat else None
-    if core.side is not None:   # this rank's collective thread (side group)
-        threading.Thread(target=collective_loop, args=(core, ctl), daemon=True, name=f"dml-coll-{wid}").start()
+    core.start_collective_thread(ctl)   # this rank's collective thread (side group), when in a group
     k = 0
     try:
         while True:
@@ -644,6 +702,12 @@ def staged_path(stage_dir: str, dataset_key: str) -> str:
     return os.path.join(stage_dir, f"{zlib.crc32(dataset_key.encode()) & 0xFFFFFFFF:08x}.npy")
 
 
+def load_prep_timeout_s() -> float:
+    """How long peers wait for rank 0 to parse / stage a table before a collective load
+    (``DML_LOAD_PREP_TIMEOUT_S``, default 1800 s)."""
+    return float(os.environ.get("DML_LOAD_PREP_TIMEOUT_S", "1800"))
+
+
 def shard_load_min_bytes() -> int:
     """Tables of at least this many float32 bytes (``DML_SHARD_LOAD_MIN_MB``, default 1024) load
     sharded: rank 0 stages them once, each rank copies 1/N of the rows, one all-gather."""
@@ -662,7 +726,10 @@ def needs_whole_rows(model_type: str, params: Dict[str, Any], gpu: bool = False)
     if model_type.startswith("GradientBoosting"):
         pct = params.get("loss") in ("absolute_error", "lad", "huber", "quantile")
         md = params.get("max_depth", 3)
-        pct_ok = gpu and md is not None and int(md) <= 10
+        try:
+            pct_ok = gpu and md is not None and int(md) <= 10
+        except (TypeError, ValueError):   # a malformed depth fails that candidate in its own fit
+            pct_ok = False
         return ((pct and not pct_ok)
                 or bool(params.get("n_iter_no_change")) or params.get("monotonic_cst") is not None)
     if not model_type.startswith("RandomForest"):
@@ -746,6 +813,7 @@ class _Worker:
     loaded: Set[str] = field(default_factory=set)
     alive: bool = True
     joined_at: float = 0.0
+    joined: bool = False                    # came in through join_cluster (not a launch rank)
 
 
 class DistributedRunner(Runner):
@@ -793,6 +861,32 @@ class DistributedRunner(Runner):
             tempfile.mkdtemp(prefix="dml_stage_", dir="/dev/shm") if os.path.isdir("/dev/shm") else tempfile.mkdtemp())
         self._t0 = time.time()
         core.stage_dir = self._stage_dir   # rank 0's collective loads stage large tables here
+        # communicator generations: after a rank death, a broken side collective or a new
+        # member, rank 0 re-forms the process group over every live worker (regroup epoch)
+        self.distributed = inf.is_dist
+        self._backend = inf.backend
+        self.gen = 0
+        self._gen_next = 1
+        self.regroup_enabled = os.environ.get("DML_REGROUP", "1") != "0"
+        self.regroup_failures = 0
+        self._regroup_after = 0.0
+        self._regroup_drain_since: Optional[float] = None
+        self._suspect: Set[int] = set()                    # never answered a regroup
+        self._hb_age: Dict[int, float] = {}                # seconds since each worker's last heartbeat
+        self.stats.update(regroups=0, regroup_failures=0, generation=0, stage_log=[])
+        self.job_log: "collections.OrderedDict[str, Dict[str, Any]]" = collections.OrderedDict()
+        # admission and host staging run OFF the dispatch thread (a 40 GB table's parse and
+        # host write would stall every other job's dispatch): admission on one worker thread
+        # (jobs keep their order), staging on two (a small table is not queued behind a
+        # large one); results come back through queues the dispatcher drains
+        from concurrent.futures import ThreadPoolExecutor
+
+        self._admit_pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dml-admit")
+        self._stage_pool = ThreadPoolExecutor(max_workers=2, thread_name_prefix="dml-stage")
+        self._admitted: "queue.Queue" = queue.Queue()
+        self._staged_q: "queue.Queue" = queue.Queue()
+        self._staging: Set[int] = set()
+        self._admitting = 0
 
     def bind(self, controller: Controller) -> None:
         super().bind(controller)
@@ -849,7 +943,9 @@ class DistributedRunner(Runner):
                 for job in new:
                     self._admit(job)
                 self.stats["loops"] += 1
-                busy = self._poll_results()
+                busy = self._poll_admitted()
+                busy = self._poll_staged() or busy
+                busy = self._poll_results() or busy
                 busy = self._poll_coll() or busy
                 now = time.time()
                 if now >= self._next_membership:
@@ -859,7 +955,7 @@ class DistributedRunner(Runner):
                     self._next_liveness = now + 0.5
                     self._liveness()
                 self._dispatch()
-                active = any(not js.finished for js in self.jobs) or any(
+                active = any(not js.finished for js in self.jobs) or self._admitting > 0 or any(
                     w.busy is not None and not w.busy.get("abandoned") for w in self.workers.values() if w.alive)
                 if stopping and not active:
                     break
@@ -879,14 +975,47 @@ class DistributedRunner(Runner):
                 if w.alive:
                     self._assign(w, {"kind": "stop"})
             w0.join(timeout=30)
+            self._admit_pool.shutdown(wait=False)
+            self._stage_pool.shutdown(wait=True)
             self._cleanup_stage()
 
     # ---- admission -----------------------------------------------------------------------
     def _admit(self, job: Job) -> None:
-        ctl = self.ctl
+        """Hand the job to the admission thread: the request is parsed and the table's
+        metadata read (a first look at a large CSV counts its rows) there, not here."""
+        self._admitting += 1
+        self.stats.setdefault("submit_t", {})[job.job_id] = time.time()
+        self._admit_pool.submit(self._prepare, job)
+
+    def _prepare(self, job: Job) -> None:
+        """(admission thread) everything about a job that does not touch dispatcher state."""
         try:
             plan = job_plan(job.request)
-            meta = ctl.registry.metadata(job.dataset_id)
+            meta = self.ctl.registry.metadata(job.dataset_id)
+            key = dataset_key(self.ctl.registry, job.dataset_id, plan)
+            self._admitted.put((job, (plan, meta, key), None))
+        except Exception as e:
+            self._admitted.put((job, None, e))
+        self._poke()
+
+    def _poll_admitted(self) -> bool:
+        got = False
+        while True:
+            try:
+                job, prep, err = self._admitted.get_nowait()
+            except queue.Empty:
+                return got
+            got = True
+            self._admitting -= 1
+            if err is not None:
+                traceback.print_exception(type(err), err, err.__traceback__)
+                self._fail_job(job, err)
+                continue
+            self._admit_prepared(job, *prep)
+
+    def _admit_prepared(self, job: Job, plan: Dict[str, Any], meta: Dict[str, Any], key: str) -> None:
+        ctl = self.ctl
+        try:
             n_rows = int(meta.get("n_rows", 1000))
             n_feat = max(1, int(meta.get("n_cols", 2)) - 1)
             todo = [sub.index for sub in job.subtasks if sub.status not in ("completed", "failed")]
@@ -908,7 +1037,7 @@ class DistributedRunner(Runner):
             seq = self.seq
             self.seq += 1
             msg = {"job_id": job.job_id, "session_id": job.session_id, "dataset_id": job.dataset_id,
-                   "dataset_key": dataset_key(ctl.registry, job.dataset_id, plan), "plan": plan,
+                   "dataset_key": key, "plan": plan,
                    "slices": slices, "params": [sub.spec["parameters"] for sub in job.subtasks],
                    "subtask_ids": [sub.subtask_id for sub in job.subtasks], "seed": job_seed(job.job_id),
                    "keep_models": ctl.config.keep_models, "models_root": ctl.models.root}
@@ -917,7 +1046,8 @@ class DistributedRunner(Runner):
             js.queue.extend(range(len(slices)))
             # datasets travel by collective broadcast while the whole group is alive and
             # nobody joined from outside it; otherwise host-staged
-            js.transport = "rccl" if (dist.info().is_dist and not self.dead and not self.group_broken) else "staged"
+            # (DML_TRANSPORT=staged: always host-staged, e.g. a host whose xGMI is shared)
+            js.transport = "rccl" if (self._group_ok() and os.environ.get("DML_TRANSPORT") != "staged") else "staged"
             if js.transport == "staged" or self._joiners_alive():
                 self._stage(js)
             self._publish_msg(js)
@@ -927,6 +1057,7 @@ class DistributedRunner(Runner):
             self.session_used.setdefault(job.session_id, 0.0)
             if js.mode == "data":
                 self.epoch_queue.append({"kind": "dp", "job": js})
+            self._log_job(js)
         except Exception as e:
             traceback.print_exc()
             self._fail_job(job, e)
@@ -935,15 +1066,76 @@ class DistributedRunner(Runner):
         self.st.set(f"job/{js.seq}", json.dumps(json_safe(js.msg)))
 
     def _stage(self, js: _JobState) -> None:
-        if js.staged_ready:
+        """Ask the staging thread for the job's host-staged table (non-blocking): its slices
+        are handed out once ``_poll_staged`` sees the file (``staged_ready``)."""
+        if js.staged_ready or js.seq in self._staging:
             return
-        ds = self.ctl.registry.load(js.job.dataset_id, js.plan["feature_columns"], js.plan["target_column"])
+        self._staging.add(js.seq)
         path = staged_path(self._stage_dir, js.msg["dataset_key"])
-        if not os.path.exists(path):
-            pdata.stage_host(ds.X, ds.y, path)
-        js.msg["staged"] = path
-        js.staged_ready = True
-        self._publish_msg(js)
+        reg, ds_id, fc, tc = self.ctl.registry, js.job.dataset_id, js.plan["feature_columns"], js.plan["target_column"]
+
+        def load():
+            ds = reg.load(ds_id, fc, tc)
+            return ds.X, ds.y
+
+        def work():
+            t0 = time.time()
+            try:
+                faults.maybe_delay_staging()
+                pdata.ensure_staged(load, path, pin=True)
+                self._staged_q.put((js, path, None))
+            except Exception as e:
+                self._staged_q.put((js, path, e))
+            nbytes = os.path.getsize(path) if os.path.exists(path) else 0
+            self.stats["stage_log"].append((js.job.job_id, t0, time.time(), nbytes))
+            self._poke()
+
+        self._stage_pool.submit(work)
+
+    def _poll_staged(self) -> bool:
+        got = False
+        while True:
+            try:
+                js, path, err = self._staged_q.get_nowait()
+            except queue.Empty:
+                return got
+            got = True
+            self._staging.discard(js.seq)
+            if js.finished:
+                continue
+            if err is not None:
+                log.error("host staging of %s failed: %s", js.job.dataset_id, err)
+                self._fail_job(js.job, err)
+                js.finished = True
+                self._cleanup_job(js)
+                continue
+            js.msg["staged"] = path
+            js.staged_ready = True
+            self._publish_msg(js)
+            ent = self.job_log.get(js.job.job_id)
+            if ent is not None:
+                ent["staged_t"] = time.time()
+
+    def _group_ok(self) -> bool:
+        """Collectives may be issued: a process group exists and nothing broke it since the
+        current generation formed."""
+        return self.distributed and dist.info().is_dist and not self.dead and not self.group_broken
+
+    def _log_job(self, js: _JobState) -> None:
+        """Per-job transport / mode / generation (cluster_info; bounded)."""
+        ent = self.job_log.setdefault(js.job.job_id, {"admitted_t": time.time()})
+        ent.update(transport=js.transport, mode=js.mode, generation=self.gen, scores_via=js.scores_via)
+        while len(self.job_log) > 256:
+            self.job_log.popitem(last=False)
+
+    def cluster_info(self) -> Dict[str, Any]:
+        """The collective plane's state (/health): generation, members, regroup counters and
+        the last jobs' transport."""
+        return {"generation": self.gen, "world": self.world, "group_ok": self._group_ok(),
+                "members": sorted(w.wid for w in self.workers.values() if w.alive and w.in_group),
+                "workers": sorted(w.wid for w in self.workers.values() if w.alive),
+                "regroups": self.stats["regroups"], "regroup_failures": self.stats["regroup_failures"],
+                "jobs": dict(self.job_log)}
 
     def _cleanup_stage(self) -> None:
         import shutil
@@ -954,7 +1146,7 @@ class DistributedRunner(Runner):
     def _data_parallel(self, plan, n_todo: int, n_rows: int, n_feat: int) -> bool:
         """Row-sharded data parallelism needs every rank of the group: never once one died."""
         par = plan.get("parallelism", "auto")
-        if par == "task" or not dist.info().is_dist or self.dead or self.group_broken or \
+        if par == "task" or not self._group_ok() or \
                 not getattr(family_of(plan["model_type"]), "data_parallel", False):
             return False
         if par == "data":
@@ -997,14 +1189,17 @@ class DistributedRunner(Runner):
         # a collective epoch owns the process group until every rank has answered
         if self.epoch is not None:
             return
+        if self._regroup_due() and self._regroup_step():
+            return   # re-forming the group (draining its members first)
         if not self.epoch_queue and self.coll_deferred:
             self._flush_coll()
         if self.epoch_queue:
             ep = self.epoch_queue[0]
             js = ep["job"]
             group = [w for w in self.workers.values() if w.in_group]
-            if self.dead or self.group_broken or any(not w.alive for w in group):
-                # the group is broken: a data-parallel job runs task-parallel instead
+            if not self._group_ok() or any(not w.alive for w in group):
+                # the group is broken (and will not be re-formed): a data-parallel job runs
+                # task-parallel instead
                 self.epoch_queue.pop(0)
                 if ep["kind"] == "dp":
                     js.mode = "task"
@@ -1041,6 +1236,9 @@ class DistributedRunner(Runner):
                 if key not in w0.loaded and js.transport == "rccl":
                     self._request_load(js)
                     return
+                if key not in w0.loaded and js.transport != "rccl" and not js.staged_ready:
+                    self._stage(js)
+                    continue
                 self._assign(w0, {"kind": "refit", "seq": js.seq, "candidate": js.refit_candidate})
                 js.refit_pending = False
                 js.refit_inflight = True
@@ -1057,6 +1255,9 @@ class DistributedRunner(Runner):
             est = js.est[i]
             self.session_used[js.job.session_id] = self.session_used.get(js.job.session_id, 0.0) + est
             self._assign(w, {"kind": "slice", "seq": js.seq, "slice": i, "ids": js.slices[i]}, est)
+            ent = self.job_log.get(js.job.job_id)
+            if ent is not None and "first_slice_t" not in ent:
+                ent["first_slice_t"] = time.time()
 
     def _next_slice(self, w: _Worker):
         """Fair share: the next slice comes from the job of the least-served session (ties:
@@ -1070,8 +1271,9 @@ class DistributedRunner(Runner):
                 if js.transport == "rccl" and w.in_group:
                     self._request_load(js)
                     continue
-                if not js.staged_ready:
+                if not js.staged_ready:   # the staging thread publishes it; other jobs meanwhile
                     self._stage(js)
+                    continue
             cands.append(js)
         if not cands:
             return None, None
@@ -1126,8 +1328,9 @@ class DistributedRunner(Runner):
         Safe to call more than once."""
         first = not self.group_broken
         self.group_broken = True
+        self._membership_changed()
         if first:
-            log.error("process group broken (%s): host staging and store copies from now on", why)
+            log.error("process group broken (%s): host staging and store copies until it is re-formed", why)
         pending = [(t["kind"], t["job"]) for t in self.coll_pending.values()]
         pending += [(task["kind"], js) for task, js, _ in self.coll_deferred]
         # the abandoned tasks' store keys: a posted task becomes a stop (a collective thread
@@ -1171,9 +1374,24 @@ class DistributedRunner(Runner):
 
     def _on_coll(self, t: Dict[str, Any], wid: int, out: Dict[str, Any]) -> None:
         js, w = t["job"], self.workers.get(wid)
+        if "error" in out and out.get("aborted"):
+            # every rank gave this task up together before the collective (OOM vote, table
+            # preparation failed): the communicator is intact; this job's table is
+            # host-staged instead and the worker that could not take it re-plans its slices
+            # on its own (host copy, bounded retries)
+            if t["kind"] == "load" and js.transport == "rccl":
+                log.warning("collective load of %s given up on every rank (%s): host-staging this job only",
+                            js.job.dataset_id, out["error"])
+                js.transport = "staged"
+                self._stage(js)
+                self._log_job(js)
+            elif t["kind"] == "scores" and wid == 0:
+                self._coll_fallback("scores", js)
+            return
         if "error" in out:
             # the failing rank's collective thread has stopped and its peers are (or will be)
-            # stuck in this collective until the side timeout: the group is broken for good
+            # stuck in this collective until the side timeout: the group is broken until the
+            # dispatcher re-forms it (_regroup_step)
             self._break_group(f"{t['kind']} collective failed on worker {wid}: {out['error']}")
             return
         if t["kind"] == "load":
@@ -1256,6 +1474,16 @@ class DistributedRunner(Runner):
 
     def _on_result(self, w: _Worker, a: Dict[str, Any], out: Dict[str, Any]) -> None:
         kind = a["kind"]
+        if kind == "regroup":
+            self._suspect.discard(w.wid)
+            ep = self.epoch
+            if ep is not None and ep["kind"] == "regroup" and ep["gen"] == a["gen"]:
+                if "error" in out:
+                    ep["failed"][w.wid] = out["error"]
+                else:
+                    ep["ok"].add(w.wid)
+                self._epoch_answer(w)
+            return
         js = self._job(a.get("seq"))
         if kind == "load":
             if "cache" in out:
@@ -1348,7 +1576,7 @@ class DistributedRunner(Runner):
     def _collective_scores(self, js: _JobState) -> bool:
         """The job's scores can travel by collective: the whole launch group is alive and
         every slice ran inside it."""
-        return (js.transport == "rccl" and dist.info().is_dist and not self.dead and not self.group_broken
+        return (js.transport == "rccl" and self._group_ok()
                 and js.scores_via == "store"
                 and all(w.alive for w in self.workers.values() if w.in_group))
 
@@ -1437,8 +1665,9 @@ class DistributedRunner(Runner):
         js.mode = "task"
         js.transport = "staged"
         js.msg["slices"] = js.slices
-        js.staged_ready = False
+        self._publish_msg(js)
         self._stage(js)
+        self._log_job(js)
         self.stats["dp_requeued"] = self.stats.get("dp_requeued", 0) + 1
 
     def _finish_dp(self, js: _JobState, out: Dict[str, Any]) -> None:
@@ -1464,7 +1693,9 @@ class DistributedRunner(Runner):
             return
         self.epoch["waiting"].discard(w.wid)
         if not self.epoch["waiting"]:
-            self.epoch = None
+            ep, self.epoch = self.epoch, None
+            if ep["kind"] == "regroup":
+                self._finish_regroup(ep)
             if not self.epoch_queue and self.coll_deferred:
                 self._flush_coll()
 
@@ -1477,6 +1708,8 @@ class DistributedRunner(Runner):
         return None
 
     def _cleanup_job(self, js: _JobState) -> None:
+        if js.job.job_id in self.job_log:
+            self.job_log[js.job.job_id]["scores_via"] = js.scores_via
         self.st.delete_key(f"job/{js.seq}")
         self.st.delete_key(f"job/{js.seq}/refit")
         self.jobs = [j for j in self.jobs if not j.finished]
@@ -1494,12 +1727,13 @@ class DistributedRunner(Runner):
                 return
             info = json.loads(self.st.get(key))
             wid = int(info["wid"])
-            self.workers[wid] = _Worker(wid, False, joined_at=time.time())
+            self.workers[wid] = _Worker(wid, False, joined_at=time.time(), joined=True)
             self.worker_ids[wid] = self.ctl.scheduler.register(f"rank{wid}", int(info.get("mem_mb", 0)),
                                                                info.get("device", "cpu"))
             log.info("worker %d joined (%s)", wid, info.get("device"))
             self._joined += 1
-            for js in self.jobs:   # joiners read host-staged datasets
+            self._membership_changed()   # the next generation takes the joiner in
+            for js in self.jobs:   # until then it reads host-staged datasets
                 if not js.finished and not js.staged_ready:
                     self._stage(js)
 
@@ -1517,10 +1751,13 @@ class DistributedRunner(Runner):
     def remove_worker(self, wid: int) -> bool:
         """Graceful leave (/unsubscribe): finish the current assignment, get no more."""
         w = self.workers.get(wid)
-        if w is None or not w.alive or w.in_group:
+        if w is None or not w.alive or not w.joined:
             return False
         self._assign(w, {"kind": "stop"})
         w.alive = False
+        if w.in_group:   # it was a member of the current generation: re-form without it
+            w.in_group = False
+            self._break_group(f"worker {wid} left")
         return True
 
     def _liveness(self) -> None:
@@ -1534,6 +1771,7 @@ class DistributedRunner(Runner):
                 hb = now
             if hb is None:   # never beat: silent since we first looked
                 hb = self._hb_missing_since.setdefault(w.wid, now)
+            self._hb_age[w.wid] = now - hb
             if now - hb > self.ctl.config.dead_after_s:
                 log.warning("worker %d missed heartbeats for %.1fs: declared dead", w.wid, now - hb)
                 self._declare_dead(w, w.busy)
@@ -1546,10 +1784,25 @@ class DistributedRunner(Runner):
         late = [i for i, t in self.coll_pending.items() if now - t["t0"] > limit]
         if late:
             self._break_group(f"side collective task(s) {late} unanswered after {limit:.0f}s")
+        ep = self.epoch
+        if ep is not None and ep["kind"] == "regroup" and \
+                now - ep["t0"] > dist.regroup_timeout_s() + float(os.environ.get("DML_COLL_GRACE_S", "30")):
+            for wid in list(ep["waiting"]):   # never answered: hung; excluded from the next try
+                ww = self.workers.get(wid)
+                if ww is not None and ww.busy is not None:
+                    ww.busy["abandoned"] = True
+                ep["failed"][wid] = "no answer"
+                self._suspect.add(wid)
+            ep["waiting"].clear()
+            self.epoch = None
+            self._finish_regroup(ep)
 
     def _declare_dead(self, w: _Worker, a: Optional[Dict[str, Any]]) -> None:
         w.alive = False
         w.busy = None
+        self._membership_changed()
+        if self.epoch is not None and self.epoch["kind"] == "regroup" and w.wid in self.epoch["waiting"]:
+            self.epoch["failed"][w.wid] = "died"
         if w.in_group:
             self.dead.add(w.wid)
         self.ctl.scheduler.unsubscribe(self.worker_ids.get(w.wid, ""))
@@ -1567,3 +1820,84 @@ class DistributedRunner(Runner):
             # host staging, score gathers to the per-slice store copies; the group is broken
             # for good (pending collectives become host-staged / task-parallel)
             self._break_group(f"worker {w.wid} died")
+
+    # ---- communicator generations ------------------------------------------------------------
+    def _membership_changed(self) -> None:
+        """A member died, left, joined or broke a collective: re-form the group soon (a short
+        delay batches a death with the respawn that follows it)."""
+        self._regroup_after = max(self._regroup_after, time.time() + float(os.environ.get("DML_REGROUP_DELAY_S", "1")))
+
+    def _regroup_due(self) -> bool:
+        if not (self.distributed and self.regroup_enabled):
+            return False
+        if self.regroup_failures >= int(os.environ.get("DML_REGROUP_MAX_FAILURES", "5")):
+            return False
+        if time.time() < self._regroup_after:
+            return False
+        return self.group_broken or bool(self.dead) or any(
+            not w.in_group for w in self.workers.values() if w.alive and w.wid not in self._suspect)
+
+    def _regroup_step(self) -> bool:
+        """Start a regroup epoch once the future members are idle: every live worker (rank 0
+        first, then by worker id) except one parked on an abandoned assignment (hung) or
+        that never answered the last regroup.  Returns True while the dispatcher must hold
+        new work back (draining the members) or the epoch is running."""
+        now = time.time()
+        members = [w for w in sorted(self.workers.values(), key=lambda w: w.wid)
+                   if w.alive and w.wid not in self._suspect and not (w.busy is not None and w.busy.get("abandoned"))]
+        if not members or members[0].wid != 0:
+            return False
+        if any(self._hb_age.get(w.wid, 0.0) > 3 * HB_PERIOD_S for w in members):
+            return False   # a member went quiet (dying?): keep dispatching until liveness decides
+        busy = [w for w in members if w.busy is not None]
+        if busy or self.coll_pending or self.coll_deferred:
+            if self._regroup_drain_since is None:
+                self._regroup_drain_since = now
+            if now - self._regroup_drain_since < float(os.environ.get("DML_REGROUP_DRAIN_S", "120")):
+                return True   # no new slices until the members are idle
+            members = [w for w in members if w.busy is None]   # long slices: form without them
+            if self.coll_pending or not members or members[0].wid != 0:
+                return True
+        self._regroup_drain_since = None
+        gen = self._gen_next
+        self._gen_next += 1
+        # every old-generation collective thread ends at a stop appended to the task stream
+        try:
+            self.st.set(f"coll/{self.coll_seq}", json.dumps({"kind": "stop"}))
+        except Exception:  # pragma: no cover - store gone with the service
+            return False
+        self.coll_seq += 1
+        wids = [w.wid for w in members]
+        payload = {"kind": "regroup", "gen": gen, "members": wids, "backend": self._backend,
+                   "coll_base": self.coll_seq}
+        self.epoch = {"kind": "regroup", "gen": gen, "members": wids, "waiting": set(wids), "ok": set(),
+                      "failed": {}, "t0": now}
+        log.info("re-forming the process group: generation %d over workers %s", gen, wids)
+        for w in members:
+            self._assign(w, payload)
+        return True
+
+    def _finish_regroup(self, ep: Dict[str, Any]) -> None:
+        members = set(ep["members"])
+        if not ep["failed"] and ep["ok"] == members:
+            self.gen = ep["gen"]
+            for w in self.workers.values():
+                w.in_group = w.alive and w.wid in members
+            self.dead = set()
+            self.group_broken = False
+            self.world = len(members)
+            self.regroup_failures = 0
+            self.stats["regroups"] += 1
+            self.stats["generation"] = self.gen
+            log.info("process group re-formed: generation %d, %d members %s (%.2fs)", self.gen, len(members),
+                     sorted(members), time.time() - ep["t0"])
+            return
+        self.regroup_failures += 1
+        self.stats["regroup_failures"] += 1
+        self.group_broken = True
+        for w in self.workers.values():
+            if w.wid in members:
+                w.in_group = False   # no member is sure to hold a usable communicator
+        backoff = min(60.0, float(os.environ.get("DML_REGROUP_BACKOFF_S", "2")) * 2 ** (self.regroup_failures - 1))
+        self._regroup_after = time.time() + backoff
+        log.error("re-forming generation %d failed (%s); retry in %.0fs", ep["gen"], ep["failed"], backoff)

@@ -7,10 +7,15 @@ runs in one process with the local runner.  Replaces the reference's docker-comp
 topology of master + scheduler + 4 workers + Kafka + Redis (aws-prod/docker-compose.yml).
 
 The parent process (which never touches a GPU) starts the ranks as its own children
-and supervises them: a worker rank that dies is reported and NOT restarted -- the
-dispatcher on rank 0 re-queues its work to the survivors -- and rank 0 (the service)
-keeps running; only rank 0 exiting ends the service.  (torchrun's elastic agent would
-instead tear the whole group down, controller included, when any worker exits.)
+and supervises them: when a worker rank dies, the dispatcher on rank 0 re-queues its work
+to the survivors and re-forms the process group without it, and the supervisor starts a
+FRESH child on the same GPU that joins the running service (``--join``; never an exec of
+the dead process), with bounded restarts per GPU (``--respawn``, default 3) and a
+back-off; rank 0 then takes the replacement into the next communicator generation, so
+the GPU gets the same service as every other (reference: a restarted worker re-registers
+and is served like any other, aws-prod/worker/worker.py:90-112 -> scheduler.py:105-117).
+Only rank 0 exiting ends the service.  (torchrun's elastic agent would instead tear the
+whole group down, controller included, when any worker exits.)
 
 Extra capacity can join a running service at any time (elastic membership, reference
 aws-prod/scheduler/scheduler.py:105-117):
@@ -43,7 +48,10 @@ def _supervise(args, argv) -> int:
                 p.terminate()
 
     signal.signal(signal.SIGTERM, stop)
-    reported = set()
+    slot = {r: procs[r] for r in range(1, args.gpus)}   # GPU r -> its current worker process
+    restarts = {r: 0 for r in slot}
+    due = {}                                             # GPU r -> time its replacement starts
+    dev_kind = "cpu" if (getattr(args, "device", None) == "cpu") else "cuda"
     try:
         while True:
             rc0 = procs[0].poll()
@@ -56,12 +64,35 @@ def _supervise(args, argv) -> int:
                     except subprocess.TimeoutExpired:
                         p.kill()
                 return rc0
-            for r, p in enumerate(procs[1:], start=1):
-                rc = p.poll()
-                if rc is not None and r not in reported:
-                    reported.add(r)
-                    print(f"[serve] rank {r} exited with code {rc}; rank 0 re-queues its work to the survivors",
+            now = time.time()
+            for r, p in list(slot.items()):
+                if p is None or p.poll() is None:
+                    continue
+                rc = p.returncode
+                slot[r] = None
+                if rc == 0:              # a graceful leave (/unsubscribe): not restarted
+                    print(f"[serve] worker on GPU {r} left", file=sys.stderr, flush=True)
+                    continue
+                if restarts[r] >= args.respawn:
+                    print(f"[serve] worker on GPU {r} exited with code {rc}; restart budget spent, GPU left idle",
                           file=sys.stderr, flush=True)
+                    continue
+                restarts[r] += 1
+                due[r] = now + min(30.0, args.respawn_backoff * 2 ** (restarts[r] - 1))
+                print(f"[serve] worker on GPU {r} exited with code {rc}; rank 0 re-queues its work, a replacement "
+                      f"joins in {due[r] - now:.1f}s (restart {restarts[r]}/{args.respawn})", file=sys.stderr,
+                      flush=True)
+            for r, t in list(due.items()):
+                if now < t:
+                    continue
+                del due[r]
+                env = dict(env0, WORLD_SIZE="1", RANK="0", LOCAL_RANK=str(r))
+                dev = "cpu" if dev_kind == "cpu" else f"cuda:{r}"
+                cmd = [sys.executable, "-m", "cs230_distributed_machine_learning_amd.serve",
+                       "--join", f"127.0.0.1:{args.master_port}", "--device", dev]
+                p = subprocess.Popen(cmd, env=env)
+                procs.append(p)
+                slot[r] = p
             time.sleep(0.5)
     except KeyboardInterrupt:
         stop()
@@ -74,6 +105,10 @@ def main(argv=None) -> int:
     ap.add_argument("--master-port", type=int, default=29541)
     ap.add_argument("--join", default=None, metavar="HOST:PORT",
                     help="join a running service (its --master-port) as an extra worker")
+    ap.add_argument("--respawn", type=int, default=3,
+                    help="restarts per GPU of a worker rank that died (a fresh process that joins)")
+    ap.add_argument("--respawn-backoff", type=float, default=1.0,
+                    help="seconds before the first restart of a GPU's worker (doubles per restart)")
     from .config import Config
 
     Config.add_cli(ap)
@@ -124,8 +159,8 @@ def main(argv=None) -> int:
             runner.serve_forever()
         except KeyboardInterrupt:
             runner.shutdown()
-        if runner.dead:
-            os._exit(0)   # a peer is gone: the process-group teardown would wait for it
+        if runner.dead or runner.group_broken or runner.gen > 0:
+            os._exit(0)   # a peer is gone or the group was re-formed: a teardown could wait for it
     else:
         worker_loop(core)
     dist.destroy()

@@ -140,7 +140,7 @@ def _drive_join(ctl, runner):
     ctl.download_data(sid, {"dataset_url": "classification?n=6000&d=10&seed=5", "dataset_name": "mid",
                             "dataset_type": "synthetic"})
     t0 = time.time()
-    while not any(not w.in_group and w.alive for w in runner.workers.values()):
+    while not any(w.joined and w.alive for w in runner.workers.values()):
         if time.time() - t0 > 60:
             raise RuntimeError("joiner never arrived")
         time.sleep(0.1)
@@ -149,7 +149,7 @@ def _drive_join(ctl, runner):
     ctl.table.wait_finished(a["job_id"], timeout=240)
     status = ctl.check_status(sid, a["job_id"])[1]
     metrics = ctl.metrics(sid, a["job_id"])[1]
-    joined = [w for w in runner.workers.values() if not w.in_group]
+    joined = [w for w in runner.workers.values() if w.joined]
     sched_id = runner.worker_ids[joined[0].wid]
     sub = ctl.subscribe({"host": "newbox", "device": "cpu"})[1]   # the REST answer points at the store
     assert sub["status"] == "join" and sub["join"]["port"] > 0 and "--join" in sub["command"], sub
@@ -220,7 +220,7 @@ def test_hung_rank_in_scores_gather_rank0_survives():
     side collective times out (DML_SIDE_TIMEOUT_S) and RAISES instead of tearing the process
     down; the dispatcher marks the group broken, the job completes from the store copies, the
     next job runs host-staged, and rank 0 exits 0."""
-    env = {"DML_STOP_RANK_IN": "2:scores", "DML_SIDE_TIMEOUT_S": "6", "DML_DEAD_AFTER_S": "600"}
+    env = {"DML_STOP_RANK_IN": "2:scores", "DML_SIDE_TIMEOUT_S": "6", "DML_DEAD_AFTER_S": "600", "DML_REGROUP": "0"}
     r, rc0, wall = _launch_faulty(3, _drive_two_jobs, env)
     assert r["s1"]["job_status"] == "completed" and len(r["s1"]["job_result"]["results"]) == 4
     assert r["s2"]["job_status"] == "completed" and len(r["s2"]["job_result"]["results"]) == 2
@@ -234,7 +234,7 @@ def test_failed_collective_breaks_group_next_job_completes():
     """One rank's collective task raises before the gather (an OOM while its peers are already
     inside): the group is marked broken at once, pending scores fall back to the store copies,
     and the next job still completes (host-staged)."""
-    env = {"DML_FAIL_RANK_IN": "1:scores", "DML_SIDE_TIMEOUT_S": "6"}
+    env = {"DML_FAIL_RANK_IN": "1:scores", "DML_SIDE_TIMEOUT_S": "6", "DML_REGROUP": "0"}
     r, rc0, _ = _launch_faulty(3, _drive_two_jobs, env)
     assert r["s1"]["job_status"] == "completed" and r["s2"]["job_status"] == "completed"
     assert r["broken"] and r["pending"] == 0, r
@@ -399,7 +399,8 @@ def test_rank_lost_inside_data_parallel_epoch_job_reruns_task_parallel(fault):
     tasks, aws-prod/scheduler/scheduler_service.py:205-247).  The job completes with the local
     runner's CV scores, the next job completes, and rank 0 exits 0."""
     var = "DML_STOP_RANK_IN" if fault == "stop" else "DML_FAIL_RANK_IN"
-    env = {var: "2:dp", "DML_DP_TIMEOUT_S": "8", "DML_SIDE_TIMEOUT_S": "8", "DML_DEAD_AFTER_S": "600"}
+    env = {var: "2:dp", "DML_DP_TIMEOUT_S": "8", "DML_SIDE_TIMEOUT_S": "8", "DML_DEAD_AFTER_S": "600",
+           "DML_REGROUP": "0"}
     r, rc0, wall = _launch_faulty(3, _drive_dp_hang, env)
     assert r["status"] == "completed" and r["next"] == "completed", r
     assert r["requeued"] == 1 and r["broken"], r

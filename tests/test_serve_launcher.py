@@ -73,7 +73,7 @@ def test_worker_rank_death_under_real_launcher(tmp_path):
         st = _wait_done(c, sid, jid, 200)
         assert st["job_status"] == "completed" and len(st["job_result"]["results"]) == 12, st
         text = (tmp_path / "serve.log").read_text()
-        assert "rank 1 exited" in text, text[-3000:]          # the worker really died ...
+        assert "worker on GPU 1 exited" in text, text[-3000:]   # the worker really died ...
         assert proc.poll() is None                            # ... and the service did not
         # a new dataset after the death: served by the survivor
         r = c.post(f"/download_data/{sid}", json={"dataset_url": "classification?n=3000&d=8&seed=2",
