@@ -81,6 +81,14 @@ struct FwdArgs {
                                  // holding a still-active fit (the others are skipped: their R^T and
                                  // loss partials keep stale values the solver never reads)
   int64_t w_zero;                // v3: 1 if every weight is 0 (logits = bias; the GEMM is skipped)
+  // v3 fold-grouped rows (nullable): the operand rows are permuted so that each split's rows
+  // without a training role form whole row tiles; an item whose column tile belongs to ONE
+  // split (ct_split[ct] >= 0) and whose row tile holds no training row of it
+  // (rt_skip[split * rt_stride + rt] != 0) skips its GEMM: its logits only ever meet a zero
+  // loss scale, so the epilogue writes exact zeros to R^T and the loss partials
+  int64_t ct_split;              // int32 [col_tiles]: the split of every fit column of the tile, -1 mixed
+  int64_t rt_skip;               // uint8 [n_splits x rt_stride]
+  int64_t rt_stride;             // row tiles of the whole operand (xrows / 256)
 };
 
 struct GradArgs {
@@ -92,6 +100,8 @@ struct GradArgs {
   int64_t bk_off;                // v3 row chunks: the chunk's first data row (B = X^T's k offset)
   int64_t slab0;                 // v3 row chunks: first output slab of this chunk
   int64_t mlive;                 // v3 (nullable): int32 per m tile, 0 = no active fit (workgroups exit)
+  int64_t kskip;                 // v3 (nullable): int32 [m_tiles x S]: the slice holds no training row of
+                                 // the m tile's split (fold-grouped rows): the slab is written as zeros
 };
 
 struct Operands {
@@ -444,13 +454,14 @@ __global__ __launch_bounds__(THREADS, 2) void k_lr_grad(GradArgs a) {
 // blockIdx.x walks 64-row tiles (rows can be ~10M), blockIdx.y 64-column tiles.
 __global__ __launch_bounds__(256) void k_split_hilo(const float* __restrict__ src, int64_t rows, int64_t cols,
                                                      int64_t ld, uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
-                                                     int64_t drows, int transpose) {
+                                                     int64_t drows, int transpose, const int64_t* __restrict__ perm) {
   __shared__ float tile[64][65];
   const int64_t r0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int i = ty; i < 64; i += 4) {
     const int64_t r = r0 + i, c = c0 + tx;
-    tile[i][tx] = (r < rows && c < cols) ? src[r * ld + c] : 0.f;
+    // operand row r holds source row perm[r] (fold-grouped rows; identity without perm)
+    tile[i][tx] = (r < rows && c < cols) ? src[(perm ? perm[r] : r) * ld + c] : 0.f;
   }
   __syncthreads();
   for (int i = ty; i < 64; i += 4) {
@@ -628,6 +639,12 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
     const int64_t ct = live ? __builtin_amdgcn_readfirstlane(live[1 + it % n_ct]) : it % n_ct;
     const int64_t rt = a.row_base + rtl;               // global row tile
     const int64_t row0 = rt * TM, col0 = ct * TN;
+    // fold-grouped rows: no training row of this column tile's split in the row tile
+    bool skip_gemm = false;
+    if (a.ct_split) {
+      const int cs = __builtin_amdgcn_readfirstlane(GPTR(const int32_t, a.ct_split)[ct]);
+      if (cs >= 0) skip_gemm = GPTR(const uint8_t, a.rt_skip)[(int64_t)cs * a.rt_stride + rt] != 0;
+    }
     // ---- item prologue: epilogue operands in flight under the GEMM.  Every load is
     // unconditional (clamped address, value selected after the GEMM): a load under a branch
     // merges into a phi whose copy waits vmcnt(0) -- i.e. would drain the GEMM's DMA ring
@@ -651,7 +668,7 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_fwd3(FwdArgs a) {
       cfit[j] = col_fit[gc];
     }
     f32x4 acc[4][4];
-    if (w_zero) {   // W = 0 (the solver's first evaluation): Z = bias, no GEMM
+    if (w_zero || skip_gemm) {   // W = 0 (the solver's first evaluation): Z = bias, no GEMM; or no training row
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -847,6 +864,14 @@ __global__ __launch_bounds__(v3::NT, 1) void k_lr_grad3(GradArgs a) {
   if (a.mlive && GPTR(const int32_t, a.mlive)[mt] == 0) return;   // every fit of the m tile has stopped
   const int64_t kb = s * a.Kc;
   const int64_t ke = kb + a.Kc < a.Kp ? kb + a.Kc : a.Kp;
+  if (a.kskip && GPTR(const int32_t, a.kskip)[mt * a.S + s] != 0) {
+    // fold-grouped rows: the slice holds no training row of the m tile's split (R^T is 0 there)
+    const int64_t ldo = a.n_tiles * TN;
+    const auto out = GPTR(float, a.out) + (a.slab0 + s) * (a.m_tiles * TM) * ldo;
+    const int64_t col = nt * TN + (tid & (TN - 1));
+    for (int64_t row = mt * TM + (tid >> 7); row < (mt + 1) * TM; row += NT / TN) out[row * ldo + col] = 0.f;
+    return;
+  }
   const Operands op{reinterpret_cast<const uint16_t*>(a.rh), reinterpret_cast<const uint16_t*>(a.rl),
                     a.m_tiles * TM, reinterpret_cast<const uint16_t*>(a.xth), reinterpret_cast<const uint16_t*>(a.xtl),
                     a.n_tiles * TN, a.bk_off};
@@ -893,11 +918,11 @@ int dml_lr_mfma_grad(const GradArgs* a, hipStream_t st) {
 }
 
 int dml_split_hilo(const float* src, int64_t rows, int64_t cols, int64_t ld, uint16_t* hi, uint16_t* lo,
-                   int64_t drows, int32_t transpose, hipStream_t st) {
+                   int64_t drows, int32_t transpose, const int64_t* perm, hipStream_t st) {
   if (rows <= 0 || cols <= 0) return 0;
   dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((cols + 63) / 64));
   if (grid.y > 65535) return 2;
-  k_split_hilo<<<grid, 256, 0, st>>>(src, rows, cols, ld, hi, lo, drows, transpose);
+  k_split_hilo<<<grid, 256, 0, st>>>(src, rows, cols, ld, hi, lo, drows, transpose, perm);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -909,6 +934,7 @@ int dml_lr_mfma_fwd3(const FwdArgs* a, hipStream_t st) {
   if (a->Kp % BK || a->row_groups % 8 || a->row_groups <= 0 || !a->lpart || a->n_splits <= 0) return 2;
   if (!a->col_info || !a->col_scale) return 2;
   if (a->row_base < 0 || (a->row_base + a->row_tiles) * v3::TM > a->xrows || a->kr != a->row_tiles * v3::TM) return 2;
+  if (a->ct_split && (!a->rt_skip || a->rt_stride * v3::TM != a->xrows)) return 2;
   if (a->row_groups > 0x7fffffff) return 2;
   k_lr_fwd3<<<(unsigned)a->row_groups, v3::NT, 0, st>>>(*a);   // row_groups = workgroups (persistent)
   return hipGetLastError() == hipSuccess ? 0 : 1;

@@ -130,12 +130,31 @@ def mfma_enabled(data) -> bool:
     return data.is_gpu and os.environ.get("DML_LR_MFMA", "1") != "0"
 
 
+def fold_grouped_perm(roles: torch.Tensor) -> torch.Tensor:
+    """Row order that groups rows with the same role in every split: a stable sort by the
+    role tuple (split 0 most significant).  For k-fold CV every fold's rows become ONE
+    contiguous block, so each split's non-training rows fill whole 256-row tiles that its
+    fits' objective can skip (they only ever meet a zero loss scale)."""
+    S = roles.shape[0]
+    key = torch.zeros(roles.shape[1], dtype=torch.int64, device=roles.device)
+    for s in range(S):
+        key = key * 3 + roles[s].to(torch.int64)
+    return torch.argsort(key, stable=True)
+
+
 class MfmaOperands:
     """bf16 hi/lo operand copies of one dataset for the MFMA objective, built once and kept
     resident next to the fp32 X (8 more bytes per element; 10M x 1000 -> 82 GB of the
     288 GB HBM): ``X`` (forward A operand, K = features padded to 32) and ``X^T`` with a row
     of ones appended (gradient B operand, K = rows; the ones row yields the intercept
-    gradient), both in the kernel's K-tiled layout ``[K/32, rows, 32]``."""
+    gradient), both in the kernel's K-tiled layout ``[K/32, rows, 32]``.
+
+    Fold-grouped rows (``DML_LR_FOLD_ROWS``, default on): the operand rows are permuted by
+    ``fold_grouped_perm`` of the dataset's split roles, with labels and roles permuted
+    alike (``y``, ``roles``).  The objective is a sum over rows, so the order changes no
+    term; but each split's rows without a training role now fill whole row tiles, and the
+    v3 kernels skip those tiles for that split's fits (``rt_skip``): 5-fold CV spends no
+    matrix-core work on the 20 % of rows each fit holds out."""
 
     def __init__(self, data):
         lib = native.hip_lib()
@@ -149,17 +168,45 @@ class MfmaOperands:
         self.xth = torch.zeros((self.npad // 32, self.Dp, 32), dtype=bf, device=dev)
         self.xtl = torch.zeros_like(self.xth)
         st = native.stream_handle(dev)
+        roles = getattr(data, "roles", None)
+        self.roles_key = roles.clone() if roles is not None else None   # the split roles this layout is for
+        perm = None
+        if (roles is not None and roles.shape[0] >= 2 and os.environ.get("DML_LR_FOLD_ROWS", "1") != "0"
+                and getattr(data, "y_cls", None) is not None):
+            perm = fold_grouped_perm(roles)
+        self.perm = perm
         for hi, lo, drows, tr in ((self.xh, self.xl, self.npad, 0), (self.xth, self.xtl, self.Dp, 1)):
-            rc = lib.dml_split_hilo(native.ptr(data.X), n, d, d, native.ptr(hi), native.ptr(lo), drows, tr, st)
+            rc = lib.dml_split_hilo(native.ptr(data.X), n, d, d, native.ptr(hi), native.ptr(lo), drows, tr,
+                                    native.ptr(perm) if perm is not None else None, st)
             if rc:
                 raise RuntimeError(f"dml_split_hilo failed ({rc})")
         ones = torch.zeros(self.npad, dtype=bf, device=dev)
         ones[:n] = 1.0
         self.xth[:, d, :] = ones.view(-1, 32)
+        # labels / roles in operand row order, and each split's row tiles without a training row
+        self.y = data.y_cls[perm].contiguous() if perm is not None else data.y_cls
+        self.roles = roles[:, perm].contiguous() if perm is not None else roles
+        self.rt_skip = None
+        self.blk32_train = None
+        if perm is not None:
+            S = roles.shape[0]
+            tr = torch.zeros((S, self.npad), dtype=torch.bool, device=dev)
+            tr[:, :n] = self.roles == 1
+            self.rt_skip = (~tr.view(S, self.npad // _ROW_TILE, _ROW_TILE).any(2)).to(torch.uint8).contiguous()
+            # per 32-row block (the K granularity of the gradient's slices), host side
+            self.blk32_train = tr.view(S, self.npad // 32, 32).any(2).cpu().numpy()
+
+    def matches(self, data) -> bool:
+        roles = getattr(data, "roles", None)
+        if self.roles_key is None or roles is None:
+            return self.roles_key is None and roles is None
+        return self.roles_key.shape == roles.shape and bool(torch.equal(self.roles_key, roles))
 
 
 def mfma_operands(data) -> MfmaOperands:
     ops = getattr(data, "_lr_mfma_ops", None)
+    if ops is not None and not ops.matches(data):   # other split roles: another row grouping
+        data._lr_mfma_ops = ops = None
     if ops is None:
         ops = MfmaOperands(data)
         data._lr_mfma_ops = ops
@@ -183,14 +230,30 @@ class MfmaPlan:
         def _order_key(f):
             rp = b.tasks[f].params
             return (bool(rp.get("penalize_intercept")), float("inf") if rp.get("C") is None else float(rp["C"]))
-        pcol0, m = [0] * len(b.K_l), 0
-        for f in sorted(range(len(b.K_l)), key=_order_key):
-            k = b.K_l[f]
-            if (m % _TILE) + k > _TILE:
-                m = _roundup(m, _TILE)
-            pcol0[f] = m
-            m += k
+
+        def layout(by_split: bool):
+            # by_split: fits of one split are contiguous and a split starts a 256-column m tile
+            # (fold-grouped rows: a tile of one split can skip that split's held-out row tiles)
+            pc, m_, prev = [0] * len(b.K_l), 0, None
+            key = (lambda f: (b.split_l[f],) + _order_key(f)) if by_split else _order_key
+            for f in sorted(range(len(b.K_l)), key=key):
+                k = b.K_l[f]
+                if by_split and prev is not None and b.split_l[f] != prev:
+                    m_ = _roundup(m_, _ROW_TILE)
+                prev = b.split_l[f]
+                if (m_ % _TILE) + k > _TILE:
+                    m_ = _roundup(m_, _TILE)
+                pc[f] = m_
+                m_ += k
+            return pc, m_
+
+        pcol0, m = layout(False)
         self.v3 = lr_v3(lib, m)
+        self.by_split = False
+        if self.v3 and ops.rt_skip is not None and len(set(b.split_l)) > 1:
+            pg, mg = layout(True)
+            if _roundup(mg, _ROW_TILE) <= 1.1 * _roundup(m, _ROW_TILE):   # padding costs < 10 %
+                pcol0, m, self.by_split = pg, mg, True
         if self.v3 and lib.dml_lr_v3_row_tile() != _ROW_TILE:
             raise RuntimeError("lr_mfma v3 row tile mismatch")
         self.Mp = _roundup(max(m, 1), _ROW_TILE if self.v3 else _TILE)
@@ -248,6 +311,35 @@ class MfmaPlan:
             S = _roundup(-(-4 * cus // tiles), 8)              # >= ~4 waves of workgroups per chunk
             Kc = _roundup(-(-chunk // S), 32)
             S = _roundup(-(-chunk // Kc), 8)
+            # fold-grouped rows: the split of every column tile / m tile (-1 mixed or none), and
+            # per row chunk the gradient slices without a training row of the m tile's split
+            self.ct_split = self.kskip_l = None
+            if self.by_split:
+                cts = np.full(col_tiles, -2, dtype=np.int64)   # -2: no fit column
+                for f, (c0, k) in enumerate(zip(pcol0, b.K_l)):
+                    for ct in {c0 // _TILE, (c0 + k - 1) // _TILE}:
+                        cts[ct] = b.split_l[f] if cts[ct] in (-2, b.split_l[f]) else -1
+                mts = np.full(m_tiles, -1, dtype=np.int64)
+                for mt in range(m_tiles):
+                    vals = {int(v) for v in cts[2 * mt:2 * mt + 2] if v != -2}
+                    mts[mt] = vals.pop() if len(vals) == 1 else -1
+                self.ct_split = torch.from_numpy(np.where(cts == -2, -1, cts).astype(np.int32)).to(dev)
+                csum = np.concatenate([np.zeros((ops.blk32_train.shape[0], 1), dtype=np.int64),
+                                       np.cumsum(ops.blk32_train, axis=1)], axis=1)   # [splits, blocks + 1]
+                self.kskip_l = []
+                for ci in range(self.n_chunks):
+                    r0 = ci * chunk
+                    rows_c = min(chunk, ops.npad - r0)
+                    ks = np.zeros((m_tiles, S), dtype=np.int32)
+                    for mt in range(m_tiles):
+                        sp = int(mts[mt])
+                        if sp < 0:
+                            continue
+                        for k in range(S):
+                            a0, a1 = r0 + k * Kc, r0 + min((k + 1) * Kc, rows_c)
+                            if a1 > a0 and csum[sp, a1 // 32] - csum[sp, a0 // 32] == 0:
+                                ks[mt, k] = 1
+                    self.kskip_l.append(torch.from_numpy(ks).to(dev))
             self.slabs = torch.empty((self.n_chunks * S, self.Mp, ops.Dp), dtype=torch.float32, device=dev)
             rg = max(8, cus // 8 * 8)   # forward: one persistent workgroup per CU
             self.fwd_l, self.grad_l = [], []
@@ -259,14 +351,16 @@ class MfmaPlan:
                     row_tiles=rows_c // _ROW_TILE, col_tiles=col_tiles, row_groups=rg, bias=p(self.bias),
                     col_fit=p(self.col_fit), fit_col0=p(self.fit_col0), fit_k=p(b.K), fit_kind=p(b.kind),
                     fit_split=p(b.split), scale=p(b.scale), cw=p(b.cw),
-                    cwC=int(b.cw.shape[1]) if b.cw is not None else 0, y=p(data.y_cls), roles=p(data.roles),
+                    cwC=int(b.cw.shape[1]) if b.cw is not None else 0, y=p(ops.y), roles=p(ops.roles),
                     rh=p(self.rh), rl=p(self.rl), kr=rows_c, loss=p(self.loss), lpart=p(self.lpart),
                     col_info=p(self.col_info), col_scale=p(self.col_scale), n_splits=int(data.roles.shape[0]),
-                    softmax_any=int(self.softmax_any), row_base=r0 // _ROW_TILE, live=p(self.live)))
+                    softmax_any=int(self.softmax_any), row_base=r0 // _ROW_TILE, live=p(self.live),
+                    ct_split=p(self.ct_split), rt_skip=p(ops.rt_skip) if self.by_split else 0,
+                    rt_stride=ops.npad // _ROW_TILE))
                 self.grad_l.append(native.LrGradArgs(
                     rh=p(self.rh), rl=p(self.rl), unused=0, xth=p(ops.xth), xtl=p(ops.xtl), m_tiles=m_tiles,
                     n_tiles=n_tiles, Kp=rows_c, S=S, Kc=Kc, out=p(self.slabs), bk_off=r0, slab0=ci * S,
-                    mlive=p(self.mlive)))
+                    mlive=p(self.mlive), kskip=p(self.kskip_l[ci]) if self.kskip_l else 0))
         else:
             self.rh = torch.zeros((ops.npad // 32, self.Mp, 32), dtype=bf, device=dev)   # pad columns stay 0
             self.rl = torch.zeros_like(self.rh)
@@ -285,7 +379,7 @@ class MfmaPlan:
                 xh=p(ops.xh), xl=p(ops.xl), xrows=ops.npad, wh=p(self.wh), wl=p(self.wl), n=data.n, Kp=ops.Kp,
                 row_tiles=row_tiles, col_tiles=col_tiles, row_groups=rg, bias=p(self.bias), col_fit=p(self.col_fit),
                 fit_col0=p(self.fit_col0), fit_k=p(b.K), fit_kind=p(b.kind), fit_split=p(b.split), scale=p(b.scale),
-                cw=p(b.cw), cwC=int(b.cw.shape[1]) if b.cw is not None else 0, y=p(data.y_cls), roles=p(data.roles),
+                cw=p(b.cw), cwC=int(b.cw.shape[1]) if b.cw is not None else 0, y=p(ops.y), roles=p(ops.roles),
                 rh=p(self.rh), rl=p(self.rl), kr=ops.npad, loss=p(self.loss))
             self.grad = native.LrGradArgs(
                 rh=p(self.rh), rl=p(self.rl), unused=0, xth=p(ops.xth), xtl=p(ops.xtl), m_tiles=col_tiles,

@@ -92,7 +92,8 @@ LrFwdArgs = _i64_struct(
     "LrFwdArgs",
     ["xh", "xl", "xrows", "wh", "wl", "n", "Kp", "row_tiles", "col_tiles", "row_groups", "bias", "col_fit",
      "fit_col0", "fit_k", "fit_kind", "fit_split", "scale", "cw", "cwC", "y", "roles", "rh", "rl", "kr", "loss",
-     "lpart", "col_info", "col_scale", "n_splits", "softmax_any", "row_base", "live", "w_zero"],
+     "lpart", "col_info", "col_scale", "n_splits", "softmax_any", "row_base", "live", "w_zero", "ct_split", "rt_skip",
+     "rt_stride"],
 )
 # csrc/kernels/gbrt.hip argument blocks (fused gradient-boosting stage kernels)
 GbStageArgs = _i64_struct(
@@ -111,7 +112,7 @@ MaeArgs = _i64_struct(
      "n_nodes_out", "levels_out", "status_out", "big_a", "big_b", "big_cap", "res", "P", "big_rows"],
 )
 LrGradArgs = _i64_struct("LrGradArgs", ["rh", "rl", "unused", "xth", "xtl", "m_tiles", "n_tiles", "Kp", "S", "Kc", "out",
-                                        "bk_off", "slab0", "mlive"])
+                                        "bk_off", "slab0", "mlive", "kskip"])
 
 
 def _load(path: str) -> ctypes.CDLL:
@@ -223,7 +224,7 @@ def _register_optional(lib) -> None:
         "dml_lr_v3_row_tile": (c_i32, []),
         "dml_lr_mfma_fwd3": (c_i32, [ctypes.POINTER(LrFwdArgs), c_vp]),
         "dml_lr_mfma_grad3": (c_i32, [ctypes.POINTER(LrGradArgs), c_vp]),
-        "dml_split_hilo": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp]),
+        "dml_split_hilo": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
         "dml_lr_sizeof_fwd_args": (c_i32, []),
         "dml_lr_sizeof_grad_args": (c_i32, []),
         "dml_dp_sizeof_args": (c_i32, []),
