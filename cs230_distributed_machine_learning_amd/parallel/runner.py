@@ -1247,6 +1247,10 @@ class DistributedRunner(Runner):
                 continue
             js, i = self._next_slice(w)
             if js is None:
+                # nothing this worker can run yet: the dispatch-latency clock (answer -> next
+                # slice) restarts, so idle time without runnable work is not counted as latency
+                if w.wid in self._t_answer:
+                    self._t_answer[w.wid] = time.time()
                 if self.epoch_queue:
                     return
                 continue
