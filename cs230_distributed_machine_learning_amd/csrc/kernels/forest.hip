@@ -2392,6 +2392,18 @@ __global__ __launch_bounds__(64) void k_subtree(Ctx c, int set_cur, int tier) {
       for (int j = 0; j < d; ++j) xc[lane * dp + j] = xg[j];
     }
   }
+#ifdef DML_X2_SUBSETUP   // sensitivity build: the setup's dependent chain (row word -> row line) twice
+  if (cache && lane < cnt0 && (c.ld & 15) == 0) {
+    const uint32_t msk = (uint32_t)c.n >> 31;   // 0 at run time, unknown to the compiler
+    const uint32_t wd2 = rows[lane + (int)((xc[lane * dp] & 1u) * msk)];
+    const uint4* src2 = (const uint4*)(c.Xb + (int64_t)word_row(c, wd2) * c.ld);
+    uint32_t* dst = (uint32_t*)(xc + lane * dp);
+    for (int q = 0; q < ((d + 15) >> 4); ++q) {
+      const uint4 v = src2[q];
+      dst[0] |= (v.x | v.y | v.z | v.w) & msk;
+    }
+  }
+#endif
   // a subtree over cnt0 rows has at most cnt0 - 1 splits: all its node pairs are reserved at
   // once -- by k_compact for staged nodes (on.pool_base), else with ONE pool atomic here
   // (unused pairs stay unreferenced)
