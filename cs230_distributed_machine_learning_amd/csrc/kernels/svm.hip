@@ -293,10 +293,16 @@ __global__ __launch_bounds__(NT) void k_smo(const float* __restrict__ X, int64_t
 // Co-residency: a record spin needs all B workgroups of its problem running; the host
 // keeps the grid within the occupancy bound (checked in dml_svm_smo_split) and every spin
 // gives up after kSpinLimit polls (status 3: the host reports an error, no hang).
-constexpr int kRecW = 10;                 // 64-bit words per record
-constexpr int kMaxB = 24;                 // workgroups per problem (B * kRecW <= NT readers)
+constexpr int kRecW = 12;                 // 64-bit words per record
+constexpr int kMaxB = 21;                 // workgroups per problem (B * kRecW <= NT: records read in one round;
+                                          // 39 measured slower, 12.5 vs 11.4 s: longer exchanges)
 constexpr int kMaxSlots = 1 << 16;        // cache slots per problem
 constexpr uint64_t kSpinLimit = 1ull << 22;  // ~5 s of polling: a stuck peer ends the launch, not the GPU
+constexpr int kTagN = 4096;               // LDS row -> slot tags in front of the cache map (power of two)
+// kSweepU: variables per thread per sweep step.  The wide variant (8: a slice of <= 2048
+// rows is ONE step, one memory round trip per sweep) holds more registers (one wave per
+// SIMD), so the host uses it only when few problems remain (the long tail of a search:
+// the last large-C problems); 4 keeps two waves per SIMD for the crowded early launches.
 
 __device__ __forceinline__ void rec_put(uint64_t* w, uint32_t tag, uint32_t payload) {
   __hip_atomic_store(w, ((uint64_t)tag << 32) | payload, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -312,6 +318,35 @@ struct SplitCtx {
   int64_t r0, r1;
 };
 
+// a working-set candidate with the values its exchange record carries (G, alpha, C, y, QD,
+// K(i, t)): the lane that found it already holds them, so the record needs no global load
+// after the block reduction
+struct CandP {
+  double v;
+  int idx;
+  double g, a, c;
+  float y, q, k;
+};
+
+template <bool MAX>
+__device__ CandP block_reduce_p(CandP c, CandP* red) {
+  for (int m = 32; m >= 1; m >>= 1) {
+    CandP o;
+    o.v = __shfl_xor(c.v, m); o.idx = __shfl_xor(c.idx, m);
+    o.g = __shfl_xor(c.g, m); o.a = __shfl_xor(c.a, m); o.c = __shfl_xor(c.c, m);
+    o.y = __shfl_xor(c.y, m); o.q = __shfl_xor(c.q, m); o.k = __shfl_xor(c.k, m);
+    if (better<MAX>(o.v, o.idx, c.v, c.idx)) c = o;
+  }
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[wid] = c;
+  __syncthreads();
+  CandP r = red[0];
+  for (int w = 1; w < NT / 64; ++w)
+    if (better<MAX>(red[w].v, red[w].idx, r.v, r.idx)) r = red[w];
+  __syncthreads();
+  return r;
+}
+
 // publish this workgroup's record (payload words v[0..n)) and gather all B records of the
 // exchange into pay[B][kRecW]; returns false if a spin gave up
 __device__ bool exchange(uint64_t* rec, const SplitCtx& sc, uint32_t seq, const uint32_t* v, int n,
@@ -319,8 +354,9 @@ __device__ bool exchange(uint64_t* rec, const SplitCtx& sc, uint32_t seq, const 
   uint64_t* mine = rec + ((int64_t)(seq & 1) * sc.B + sc.w) * kRecW;
   if (threadIdx.x < n) rec_put(mine + threadIdx.x, seq, v[threadIdx.x]);
   const int total = sc.B * kRecW;
-  if (threadIdx.x < total && (threadIdx.x % kRecW) < n) {
-    const uint64_t* src = rec + (int64_t)(seq & 1) * sc.B * kRecW + threadIdx.x;
+  for (int q = threadIdx.x; q < total; q += NT) {
+    if ((q % kRecW) >= n) continue;
+    const uint64_t* src = rec + (int64_t)(seq & 1) * sc.B * kRecW + q;
     uint64_t x;
     uint64_t spins = 0;
     while (true) {
@@ -329,7 +365,7 @@ __device__ bool exchange(uint64_t* rec, const SplitCtx& sc, uint32_t seq, const 
       if (++spins > kSpinLimit) { *abort_flag = 1; break; }
       __builtin_amdgcn_s_sleep(1);
     }
-    pay[threadIdx.x] = (uint32_t)x;
+    pay[q] = (uint32_t)x;
   }
   __syncthreads();
   return *abort_flag == 0;
@@ -369,19 +405,34 @@ __device__ void column_slice(const SvmProb& p, const float* __restrict__ X, int6
     int64_t rr[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) rr[k] = min(rb + k * NT, r1 - 1);   // clamped: the tail recomputes a valid row
-#pragma unroll 4
-    for (int64_t f = 0; f < d; ++f) {
-      const float a = lds ? xs[f] : base[f * nr + src];
-      const float* xf = base + f * nr;
-      if (kernel == KRBF) {
+    // features in blocks of kColF: the block's 4 x kColF loads are all issued before its
+    // first FMA (a cache miss is a memory round trip per BLOCK of features, not per 4);
+    // the FMA order per row is unchanged (f ascending), so every entry is the same float
+    constexpr int kColF = 16;
+    for (int64_t f0 = 0; f0 < d; f0 += kColF) {
+      float xv[kColF][4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float t = a - xf[rr[k]];
-          acc[k] = __builtin_fmaf(t, t, acc[k]);
+      for (int q = 0; q < kColF; ++q) {
+        const int64_t f = min(f0 + q, d - 1);
+        const float* xf = base + f * nr;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xv[q][k] = xf[rr[k]];
+      }
+#pragma unroll
+      for (int q = 0; q < kColF; ++q) {
+        if (f0 + q >= d) break;
+        const int64_t f = f0 + q;
+        const float a = lds ? xs[f] : base[f * nr + src];
+        if (kernel == KRBF) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float t = a - xv[q][k];
+            acc[k] = __builtin_fmaf(t, t, acc[k]);
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc[k] = __builtin_fmaf(a, xv[q][k], acc[k]);
         }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) acc[k] = __builtin_fmaf(a, xf[rr[k]], acc[k]);
       }
     }
 #pragma unroll
@@ -400,14 +451,28 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   return x;
 }
 
+// The workgroup's replica of the map is fronted by an LDS tag array (kTagN direct-mapped
+// row -> slot entries, kept exact: set on every lookup, cleared when a slot's old row is
+// evicted), so a hit on a recently used row costs one LDS read instead of a global round
+// trip and two barriers (SMO revisits a small working set: ~90 % of the lookups hit).
 __device__ float* cache_column(const SvmProb& p, const float* X, int64_t d, float* kc, int32_t* slot_of,
                                int32_t* row_of, uint32_t* stamp, uint32_t tick, int64_t row, const SplitCtx& sc,
-                               float* xs, int* s_slot, int* s_red) {
-  if (threadIdx.x == 0) *s_slot = slot_of[row];
-  __syncthreads();
-  int slot = *s_slot;
+                               float* xs, int* s_slot, int* s_red, int32_t* tag_row, int32_t* tag_slot,
+                               int* s_miss) {
+  const int h = (int)(row & (kTagN - 1));
+  if (tag_row[h] == (int32_t)row) {   // uniform: every thread reads the same LDS word
+    const int slot = tag_slot[h];
+    if (threadIdx.x == 0) stamp[slot] = tick;
+    return kc + p.coff + (int64_t)slot * p.nrows;
+  }
+  int slot = __builtin_amdgcn_readfirstlane(slot_of[row]);   // the same word in every lane
   const bool hit = slot >= 0;
-  if (!hit) {
+  __syncthreads();   // every thread has read the tag before thread 0 rewrites it
+  if (hit) {
+    if (threadIdx.x == 0) { tag_row[h] = (int32_t)row; tag_slot[h] = slot; stamp[slot] = tick; }
+    return kc + p.coff + (int64_t)slot * p.nrows;
+  }
+  {
     const uint32_t cand = sc.S <= NT ? (uint32_t)threadIdx.x : mix32(tick * 2654435761U + threadIdx.x) % (uint32_t)sc.S;
     uint64_t best = cand < (uint32_t)sc.S ? (((uint64_t)stamp[cand] << 32) | cand) : ~0ull;
     for (int m = 32; m >= 1; m >>= 1) {
@@ -424,21 +489,28 @@ __device__ float* cache_column(const SvmProb& p, const float* X, int64_t d, floa
       }
       const int v = (int)(uint32_t)bb;
       const int old = row_of[v];
-      if (old >= 0) slot_of[old] = -1;
+      if (old >= 0) {
+        slot_of[old] = -1;
+        if (tag_row[old & (kTagN - 1)] == old) tag_row[old & (kTagN - 1)] = -1;
+      }
       slot_of[row] = v;
       row_of[v] = (int32_t)row;
+      tag_row[h] = (int32_t)row;
+      tag_slot[h] = v;
       *s_slot = v;
+      ++*s_miss;   // (profiling)
     }
     __syncthreads();
     slot = *s_slot;
   }
   if (threadIdx.x == 0) stamp[slot] = tick;
   float* col = kc + p.coff + (int64_t)slot * p.nrows;
-  if (!hit) column_slice(p, X, d, row, xs, col, sc.r0, sc.r1);
+  column_slice(p, X, d, row, xs, col, sc.r0, sc.r1);
   __syncthreads();
   return col;
 }
 
+template <int kSweepU>
 __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, int64_t d, const SvmProb* probs,
                                                   int B, int S, const float* __restrict__ yv,
                                                   const double* __restrict__ Cv, const float* __restrict__ qd,
@@ -455,12 +527,16 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
   const SvmProb p = probs[pid];
   if (p.status != 0) return;
   __shared__ float xs[kMaxLdsD];
-  __shared__ Cand red[NT / 64];
+  __shared__ CandP red[NT / 64];
   __shared__ double redd[NT / 64];
   __shared__ uint32_t pay[kMaxB * kRecW];
   __shared__ int s_slot, s_abort;
   __shared__ uint32_t vals[kRecW];
   __shared__ int s_red[2 * (NT / 64)];
+  __shared__ int32_t tag_row[kTagN], tag_slot[kTagN];
+  __shared__ int s_miss;
+  for (int q = threadIdx.x; q < kTagN; q += NT) tag_row[q] = -1;
+  if (threadIdx.x == 0) s_miss = 0;
   SplitCtx sc;
   sc.B = B;
   sc.w = blockIdx.x - pid * B;
@@ -488,67 +564,76 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
   uint32_t seq = 0;
   const int64_t stop_at = min(p.max_iter, it + chunk);
   auto local_i = [&]() {
-    Cand ci{-kInf, -1};
+    CandP ci{-kInf, -1, 0.0, 0.0, 0.0, 0.f, 0.f, 0.f};
     for (int sgi = 0; sgi < nseg; ++sgi)
       for (int64_t t = sc.r0 + sgi * nr + threadIdx.x; t < sc.r1 + sgi * nr; t += NT) {
-        const double yt = y[t];
-        const bool up = yt > 0 ? !is_upper(a[t], C[t]) : !is_lower(a[t]);
+        const double yt = y[t], at = a[t], Ct = C[t], gt = g[t];
+        const bool up = yt > 0 ? !is_upper(at, Ct) : !is_lower(at);
         if (up) {
-          const double v = -yt * g[t];
-          if (better<true>(v, (int)t, ci.v, ci.idx)) { ci.v = v; ci.idx = (int)t; }
+          const double v = -yt * gt;
+          if (better<true>(v, (int)t, ci.v, ci.idx))
+            ci = CandP{v, (int)t, gt, at, Ct, (float)yt, QD[rowof(t)], 0.f};
         }
       }
     return ci;
   };
-  Cand ci = local_i();
+  CandP ci = local_i();
   while (true) {
     if (it >= stop_at) { status = it >= p.max_iter ? 2 : 0; break; }
     // ---- exchange 1: i = argmax over I_up of -y G (with G_i, alpha_i) ----
-    const Cand bi_l = block_reduce<true>(ci, red);
+    const CandP bi_l = block_reduce_p<true>(ci, red);
     if (threadIdx.x == 0) {
+      // the candidate's own per-variable values travel with it (G, alpha, y, QD, C: no
+      // dependent loads, here or by the other workgroups once the winner is known)
       const int t = bi_l.idx;
       vals[0] = lo32(bi_l.v); vals[1] = hi32(bi_l.v); vals[2] = (uint32_t)t;
-      const double gi = t >= 0 ? g[t] : 0.0, ai = t >= 0 ? a[t] : 0.0;
-      vals[3] = lo32(gi); vals[4] = hi32(gi); vals[5] = lo32(ai); vals[6] = hi32(ai);
+      vals[3] = lo32(bi_l.g); vals[4] = hi32(bi_l.g); vals[5] = lo32(bi_l.a); vals[6] = hi32(bi_l.a);
+      vals[7] = __float_as_uint(bi_l.y); vals[8] = __float_as_uint(bi_l.q);
+      vals[9] = lo32(bi_l.c); vals[10] = hi32(bi_l.c);
     }
     __syncthreads();
     SVM_PH(0)
-    if (!exchange(rec, sc, ++seq, vals, 7, pay, &s_abort)) { status = 3; break; }
+    if (!exchange(rec, sc, ++seq, vals, 11, pay, &s_abort)) { status = 3; break; }
     SVM_PH(1)
-    double Gmax = -kInf, gi = 0.0, ai_old = 0.0;
+    double Gmax = -kInf, gi = 0.0, ai_old = 0.0, Ci = 0.0;
+    float yi_f = 0.f, QDi_f = 0.f;
     int i = -1;
     for (int q = 0; q < B; ++q) {
       const uint32_t* r = pay + q * kRecW;
       const int idx = (int)r[2];
       const double v = mkd(r[0], r[1]);
-      if (better<true>(v, idx, Gmax, i)) { Gmax = v; i = idx; gi = mkd(r[3], r[4]); ai_old = mkd(r[5], r[6]); }
+      if (better<true>(v, idx, Gmax, i)) {
+        Gmax = v; i = idx; gi = mkd(r[3], r[4]); ai_old = mkd(r[5], r[6]);
+        yi_f = __uint_as_float(r[7]); QDi_f = __uint_as_float(r[8]); Ci = mkd(r[9], r[10]);
+      }
     }
     __syncthreads();
     if (i < 0) { status = 1; break; }
-    const double yi = y[i];
+    const double yi = yi_f;
     const int64_t ri = rowof(i);
     const uint32_t tick = (uint32_t)(2 * (it + 1));
-    if (do_prof && threadIdx.x == 0 && slot_of[ri] < 0) ph[7] += 1;
-    const float* Ki = cache_column(p, X, d, kc, slot_of, row_of, stamp, tick, ri, sc, xs, &s_slot, s_red);
+    const float* Ki = cache_column(p, X, d, kc, slot_of, row_of, stamp, tick, ri, sc, xs, &s_slot, s_red, tag_row,
+                                   tag_slot, &s_miss);
     SVM_PH(2)
     // ---- local j candidates (second-order gain) + max over I_low of y G ----
     // 4 variables per thread per step, every load issued before any use (latency-bound
     // sweep); selection ties break by index, so the visiting order does not matter
-    Cand cj{kInf, -1};
+    CandP cj{kInf, -1, 0.0, 0.0, 0.0, 0.f, 0.f, 0.f};
     double gmax2 = -kInf;
-    const double QDi = QD[ri];
+    const double QDi = QDi_f;
     for (int sgi = 0; sgi < nseg; ++sgi) {
       const int64_t lo = sc.r0 + sgi * nr, hi = sc.r1 + sgi * nr;
-      for (int64_t tb = lo + threadIdx.x; tb < hi; tb += 4 * NT) {
-        double yk[4], ak[4], Ck[4], gk[4], kk[4], qk[4];
+      for (int64_t tb = lo + threadIdx.x; tb < hi; tb += kSweepU * NT) {
+        float yk[kSweepU], kk[kSweepU], qk[kSweepU];
+        double ak[kSweepU], Ck[kSweepU], gk[kSweepU];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kSweepU; ++k) {
           const int64_t t = min(tb + k * NT, hi - 1);
           const int64_t rt = rowof(t);
-          yk[k] = y[t]; ak[k] = a[t]; Ck[k] = C[t]; gk[k] = g[t]; kk[k] = (double)Ki[rt]; qk[k] = QD[rt];
+          yk[k] = y[t]; ak[k] = a[t]; Ck[k] = C[t]; gk[k] = g[t]; kk[k] = Ki[rt]; qk[k] = QD[rt];
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kSweepU; ++k) {
           const int64_t t = tb + k * NT;
           if (t >= hi) break;
           const double yt = yk[k];
@@ -557,9 +642,10 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
               const double gd = Gmax + gk[k];
               gmax2 = fmax(gmax2, gk[k]);
               if (gd > 0) {
-                double qc = QDi + qk[k] - 2.0 * yi * (yi * yt * kk[k]);
+                double qc = QDi + (double)qk[k] - 2.0 * yi * (yi * yt * (double)kk[k]);
                 const double od = qc > 0 ? -(gd * gd) / qc : -(gd * gd) / kTau;
-                if (better<false>(od, (int)t, cj.v, cj.idx)) { cj.v = od; cj.idx = (int)t; }
+                if (better<false>(od, (int)t, cj.v, cj.idx))
+                  cj = CandP{od, (int)t, gk[k], ak[k], Ck[k], yk[k], qk[k], kk[k]};
               }
             }
           } else {
@@ -567,49 +653,57 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
               const double gd = Gmax - gk[k];
               gmax2 = fmax(gmax2, -gk[k]);
               if (gd > 0) {
-                double qc = QDi + qk[k] + 2.0 * yi * (yi * yt * kk[k]);
+                double qc = QDi + (double)qk[k] + 2.0 * yi * (yi * yt * (double)kk[k]);
                 const double od = qc > 0 ? -(gd * gd) / qc : -(gd * gd) / kTau;
-                if (better<false>(od, (int)t, cj.v, cj.idx)) { cj.v = od; cj.idx = (int)t; }
+                if (better<false>(od, (int)t, cj.v, cj.idx))
+                  cj = CandP{od, (int)t, gk[k], ak[k], Ck[k], yk[k], qk[k], kk[k]};
               }
             }
           }
         }
       }
     }
-    const Cand bj_l = block_reduce<false>(cj, red);
+    const CandP bj_l = block_reduce_p<false>(cj, red);
     const double gm2_l = block_max(gmax2, redd);
     if (threadIdx.x == 0) {
+      // K(i, j) of the slice's j comes from the slice of column i it just filled: the entry
+      // kernel_pair would recompute with the same arithmetic (every workgroup takes it from
+      // the winning record, no workgroup recomputes it)
       const int t = bj_l.idx;
       vals[0] = lo32(bj_l.v); vals[1] = hi32(bj_l.v); vals[2] = (uint32_t)t;
-      const double gj = t >= 0 ? g[t] : 0.0, aj = t >= 0 ? a[t] : 0.0;
-      vals[3] = lo32(gj); vals[4] = hi32(gj); vals[5] = lo32(aj); vals[6] = hi32(aj);
-      vals[7] = lo32(gm2_l); vals[8] = hi32(gm2_l);
+      vals[3] = lo32(bj_l.g); vals[4] = hi32(bj_l.g); vals[5] = lo32(bj_l.a); vals[6] = hi32(bj_l.a);
+      vals[7] = lo32(gm2_l); vals[8] = hi32(gm2_l); vals[9] = __float_as_uint(bj_l.k);
+      vals[10] = __float_as_uint(bj_l.y); vals[11] = __float_as_uint(bj_l.q);
     }
     __syncthreads();
     SVM_PH(3)
     // ---- exchange 2 ----
-    if (!exchange(rec, sc, ++seq, vals, 9, pay, &s_abort)) { status = 3; break; }
+    if (!exchange(rec, sc, ++seq, vals, 12, pay, &s_abort)) { status = 3; break; }
     SVM_PH(4)
     double bjv = kInf, gj = 0.0, aj_old = 0.0, Gmax2 = -kInf;
+    float kij = 0.f, yj_f = 0.f, QDj_f = 0.f;
     int j = -1;
     for (int q = 0; q < B; ++q) {
       const uint32_t* r = pay + q * kRecW;
       const int idx = (int)r[2];
       const double v = mkd(r[0], r[1]);
-      if (better<false>(v, idx, bjv, j)) { bjv = v; j = idx; gj = mkd(r[3], r[4]); aj_old = mkd(r[5], r[6]); }
+      if (better<false>(v, idx, bjv, j)) {
+        bjv = v; j = idx; gj = mkd(r[3], r[4]); aj_old = mkd(r[5], r[6]); kij = __uint_as_float(r[9]);
+        yj_f = __uint_as_float(r[10]); QDj_f = __uint_as_float(r[11]);
+      }
       Gmax2 = fmax(Gmax2, mkd(r[7], r[8]));
     }
     __syncthreads();
     if (Gmax + Gmax2 < p.eps || j < 0) { status = 1; break; }
-    const double yj = y[j];
+    const double Cj = C[j];   // issued before the cache lookup, used by the update
+    const double yj = yj_f;
     const int64_t rj = rowof(j);
-    if (do_prof && threadIdx.x == 0 && slot_of[rj] < 0) ph[7] += 1;
-    const float* Kj = cache_column(p, X, d, kc, slot_of, row_of, stamp, tick + 1, rj, sc, xs, &s_slot, s_red);
+    const float* Kj = cache_column(p, X, d, kc, slot_of, row_of, stamp, tick + 1, rj, sc, xs, &s_slot, s_red, tag_row,
+                                   tag_slot, &s_miss);
     SVM_PH(5)
     // ---- two-variable update: every workgroup computes the same values ----
-    const double Ci = C[i], Cj = C[j];
-    const double Qij = yi * yj * (double)kernel_pair(p, X, d, ri, rj);
-    const double QDj = QD[rj];
+    const double Qij = yi * yj * (double)kij;
+    const double QDj = QDj_f;
     double ai = ai_old, aj = aj_old;
     if (yi != yj) {
       double qc = QDi + QDj + 2.0 * Qij;
@@ -640,28 +734,29 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
     }
     __syncthreads();
     // gradient update of this slice fused with its next i candidates (4 per thread per step)
-    ci = Cand{-kInf, -1};
+    ci = CandP{-kInf, -1, 0.0, 0.0, 0.0, 0.f, 0.f, 0.f};
     for (int sgi = 0; sgi < nseg; ++sgi) {
       const int64_t lo = sc.r0 + sgi * nr, hi = sc.r1 + sgi * nr;
-      for (int64_t tb = lo + threadIdx.x; tb < hi; tb += 4 * NT) {
-        double yk[4], ak[4], Ck[4], gk[4], kik[4], kjk[4];
+      for (int64_t tb = lo + threadIdx.x; tb < hi; tb += kSweepU * NT) {
+        float yk[kSweepU], kik[kSweepU], kjk[kSweepU], qk[kSweepU];
+        double ak[kSweepU], Ck[kSweepU], gk[kSweepU];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kSweepU; ++k) {
           const int64_t t = min(tb + k * NT, hi - 1);
           const int64_t rt = rowof(t);
-          yk[k] = y[t]; ak[k] = a[t]; Ck[k] = C[t]; gk[k] = g[t]; kik[k] = (double)Ki[rt]; kjk[k] = (double)Kj[rt];
+          yk[k] = y[t]; ak[k] = a[t]; Ck[k] = C[t]; gk[k] = g[t]; kik[k] = Ki[rt]; kjk[k] = Kj[rt]; qk[k] = QD[rt];
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kSweepU; ++k) {
           const int64_t t = tb + k * NT;
           if (t >= hi) break;
           const double yt = yk[k];
-          const double gt = gk[k] + yt * (yi * kik[k] * dai + yj * kjk[k] * daj);
+          const double gt = gk[k] + yt * (yi * (double)kik[k] * dai + yj * (double)kjk[k] * daj);
           g[t] = gt;
           const bool up = yt > 0 ? !is_upper(ak[k], Ck[k]) : !is_lower(ak[k]);
           if (up) {
             const double v = -yt * gt;
-            if (better<true>(v, (int)t, ci.v, ci.idx)) { ci.v = v; ci.idx = (int)t; }
+            if (better<true>(v, (int)t, ci.v, ci.idx)) ci = CandP{v, (int)t, gt, ak[k], Ck[k], yk[k], qk[k], 0.f};
           }
         }
       }
@@ -671,8 +766,10 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
     SVM_PH(6)
   }
 #undef SVM_PH
-  if (do_prof && threadIdx.x == 0)
+  if (do_prof && threadIdx.x == 0) {
+    ph[7] = s_miss;
     for (int k = 0; k < 8; ++k) prof[k] += ph[k];
+  }
   if (threadIdx.x == 0 && sc.w == 0) {
     out_state[2 * pid] = it;
     out_state[2 * pid + 1] = status;
@@ -695,34 +792,44 @@ int dml_svm_smo(const float* X, int64_t d, void* probs, int64_t nprob, const flo
 
 // Split solver: probs (device, read-only) x B workgroups each; S cache slots per problem
 // (2 <= S <= 1024); kc: cache columns (coff per problem); meta: per-problem per-workgroup
-// maps (moff; slot_of = -1, row_of = -1, stamp = 0 initially); recs: nprob * 2 * B * 10
+// maps (moff; slot_of = -1, row_of = -1, stamp = 0 initially); recs: nprob * 2 * B * kRecW
 // zeroed words; out_state: [nprob][2] (iterations, status) written by workgroup 0.
+// wide: the 8-variables-per-step sweep variant (see kSweepU above)
 int dml_svm_smo_split(const float* X, int64_t d, const void* probs, int64_t nprob, int32_t B, int32_t S,
                       const float* y, const double* C, const float* qd, double* alpha, double* G, float* kc,
                       int32_t* meta, uint64_t* recs, int64_t* out_state, int64_t chunk, int64_t* prof,
-                      hipStream_t st) {
+                      int32_t wide, hipStream_t st) {
   if (nprob <= 0) return 0;
   if (B < 1 || B > kMaxB || S < 2 || S > kMaxSlots) return 2;
   if (B > 1) {   // every workgroup of the grid must be resident at once (record spins)
     int per_cu = 0, dev = 0;
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 3;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_smo_split, NT, 0) != hipSuccess) return 3;
+    const hipError_t oe = wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_smo_split<8>, NT, 0)
+                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_smo_split<4>, NT, 0);
+    if (oe != hipSuccess) return 3;
     if ((int64_t)nprob * B > (int64_t)per_cu * prop.multiProcessorCount / 2) return 4;
   }
-  k_smo_split<<<(unsigned)(nprob * B), NT, 0, st>>>(X, d, (const SvmProb*)probs, B, S, y, C, qd, alpha, G, kc, meta,
-                                                     recs, out_state, chunk, prof);
+  if (wide)
+    k_smo_split<8><<<(unsigned)(nprob * B), NT, 0, st>>>(X, d, (const SvmProb*)probs, B, S, y, C, qd, alpha, G, kc,
+                                                          meta, recs, out_state, chunk, prof);
+  else
+    k_smo_split<4><<<(unsigned)(nprob * B), NT, 0, st>>>(X, d, (const SvmProb*)probs, B, S, y, C, qd, alpha, G, kc,
+                                                          meta, recs, out_state, chunk, prof);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
-int dml_svm_split_limits(int32_t* max_b, int32_t* max_slots) {
+// workgroups the host may launch at once (narrow variant; *wide_resident: the wide one's)
+int dml_svm_split_limits(int32_t* max_b, int32_t* max_slots, int32_t* wide_resident) {
   *max_b = kMaxB;
   *max_slots = kMaxSlots;
-  int per_cu = 0, dev = 0;
+  int per_cu = 0, per_cu_w = 0, dev = 0;
   hipDeviceProp_t prop;
   if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_smo_split, NT, 0) != hipSuccess) return -1;
-  return per_cu * prop.multiProcessorCount / 2;   // workgroups the host may launch at once
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_smo_split<4>, NT, 0) != hipSuccess) return -1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_w, k_smo_split<8>, NT, 0) != hipSuccess) return -1;
+  if (wide_resident) *wide_resident = per_cu_w * prop.multiProcessorCount / 2;
+  return per_cu * prop.multiProcessorCount / 2;
 }
 
 }  // extern "C"

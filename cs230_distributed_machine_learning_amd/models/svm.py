@@ -48,7 +48,7 @@ PROB_DTYPE = np.dtype([("xoff", "<i8"), ("roff", "<i8"), ("nrows", "<i8"), ("L",
 CHUNK_ITERS = 20000
 SPLIT_CHUNK_ITERS = 50000
 CACHE_FRACTION = 0.25        # of free HBM for the kernel-column caches (libsvm cache_size analogue) ...
-CACHE_MAX_GB = 24.0          # ... and at most this much (DML_SVM_CACHE_GB)
+CACHE_MAX_GB = 48.0          # ... and at most this much (DML_SVM_CACHE_GB; 288 GB of HBM per MI355X)
 MIN_ROWS_PER_WG = 1024       # split a problem over workgroups only down to this slice size
 
 
@@ -285,8 +285,9 @@ class SVMFamily(Family):
         cannot run here (the caller uses the one-workgroup kernel)."""
         dev = data.device
         nprob = len(P)
-        max_b, max_slots = ctypes.c_int32(0), ctypes.c_int32(0)
-        resident = int(lib.dml_svm_split_limits(ctypes.byref(max_b), ctypes.byref(max_slots)))
+        max_b, max_slots, wide_res = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int32(0)
+        resident = int(lib.dml_svm_split_limits(ctypes.byref(max_b), ctypes.byref(max_slots), ctypes.byref(wide_res)))
+        wide_ok = os.environ.get("DML_SVM_WIDE", "1") != "0"
         nr = P["nrows"].astype(np.int64)
         if resident <= 0 or nprob == 0:
             return False
@@ -309,7 +310,7 @@ class SVMFamily(Family):
         meta = torch.from_numpy(meta_np).to(dev)
         kc = torch.empty(int((nr * S).sum()), dtype=torch.float32, device=dev)
         prof = torch.zeros(8, dtype=torch.int64, device=dev) if os.environ.get("DML_SVM_PROFILE") else None
-        launches, B_prev, B_hist = 0, 0, []
+        launches, B_prev, B_hist, wide_n = 0, 0, [], 0
         while True:
             run = np.nonzero(P["status"] == 0)[0]
             if run.size == 0:
@@ -326,17 +327,22 @@ class SVMFamily(Family):
                     view[1:B] = view[0]
             Pr = np.ascontiguousarray(P[run])
             Pd = torch.from_numpy(Pr.view(np.uint8).copy()).to(dev)
-            recs = torch.zeros(run.size * 2 * B * 10, dtype=torch.int64, device=dev)
+            recs = torch.zeros(run.size * 2 * B * 12, dtype=torch.int64, device=dev)   # svm.hip kRecW
             out_state = torch.zeros(2 * run.size, dtype=torch.int64, device=dev)
+            # the wide sweep (8 variables per thread per step: one round trip per sweep for a
+            # slice of <= 2048 rows) once the remaining problems fit its lower occupancy
+            wide = int(wide_ok and (B == 1 or run.size * B <= int(wide_res.value))
+                       and int(nr[run].max()) <= 8 * 256 * B)
             rc = lib.dml_svm_smo_split(native.ptr(Xrs), data.d, native.ptr(Pd), run.size, B, S, native.ptr(y),
                                        native.ptr(C), native.ptr(qd), native.ptr(alpha), native.ptr(G), native.ptr(kc),
                                        native.ptr(meta), native.ptr(recs), native.ptr(out_state), SPLIT_CHUNK_ITERS,
-                                       native.ptr(prof), native.stream_handle(dev))
+                                       native.ptr(prof), wide, native.stream_handle(dev))
             if rc == 4 and launches == 0:
                 return False
             if rc:
                 raise RuntimeError(f"dml_svm_smo_split failed ({rc})")
             launches += 1
+            wide_n += wide
             B_prev = B
             B_hist.append(B)
             st = out_state.view(run.size, 2).cpu().numpy()
@@ -345,6 +351,7 @@ class SVMFamily(Family):
             if (P["status"] == 3).any():
                 raise RuntimeError("SMO workgroups of a problem lost contact (not co-resident?)")
         self.last_solve_stats = {"solver": "split", "problems": nprob, "workgroups_per_problem": max(B_hist),
+                                 "wide_launches": wide_n,
                                  "workgroups_per_launch": B_hist, "cache_slots": S, "launches": launches,
                                  "iterations_max": int(P["iters"].max()), "iterations_sum": int(P["iters"].sum())}
         if prof is not None:   # first running problem, workgroup 0: 100 MHz ticks -> microseconds per phase

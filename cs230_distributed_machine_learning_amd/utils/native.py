@@ -214,8 +214,8 @@ def _register_optional(lib) -> None:
         "dml_forest_refine": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
                                       c_vp]),
         "dml_svm_smo_split": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                      c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
-        "dml_svm_split_limits": (c_i32, [c_vp, c_vp]),
+                                      c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp]),
+        "dml_svm_split_limits": (c_i32, [c_vp, c_vp, c_vp]),
         "dml_svm_smo": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
         "dml_split_moments": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp]),
         "dml_lr_mfma_tile": (c_i32, []),
