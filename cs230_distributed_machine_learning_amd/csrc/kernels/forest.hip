@@ -2908,13 +2908,20 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
     constexpr uint32_t INV = 0xFFFFFFFFu;
     using PL = typename PLT<MODE>::T;
     const int t0 = r0 + (int)threadIdx.x;
-    auto run = [&](auto Gc, auto UWc) {
+    // feature offsets: feature-major copy (stride n) when present, else the row line
+    // (DML_LARGE_FM_DIV = k > 0: nodes holding under 1/k of the table's rows read the row-major
+    // lines instead -- one line per row for every feature of the round)
+    const bool fm = c.XbT != nullptr && (c.fm_div == 0 || (int64_t)st.on.count * c.fm_div >= (int64_t)c.n);
+    // row windows (RW): a whole-histogram round reads features [f0, f0 + g) -- contiguous ids, at
+    // most two aligned 16-B pieces of the row line -- so a sparse node's row-major gather is two
+    // dwordx4 loads of one cache line per row (the bytes picked out by uniform register index)
+    // instead of g byte loads; a feature-major gather of a node holding 1/2^k of the rows pays
+    // ~2^k / 128 line lookups per (row, feature)
+    const bool rwin = !fm && fround >= 0 && (c.ld & 15) == 0 && g <= 16 && c.ld >= 32;
+    auto run = [&](auto Gc, auto UWc, auto RWc) __attribute__((always_inline)) {
       constexpr int G = decltype(Gc)::value;
       constexpr bool UW = decltype(UWc)::value;
-      // feature offsets: feature-major copy (stride n) when present, else the row line
-      // (DML_LARGE_FM_DIV = k > 0: nodes holding under 1/k of the table's rows read the row-major
-      // lines instead -- one line per row for every feature of the round)
-      const bool fm = c.XbT != nullptr && (c.fm_div == 0 || (int64_t)st.on.count * c.fm_div >= (int64_t)c.n);
+      constexpr bool RW = decltype(RWc)::value;
       int64_t fo[G];
 #pragma unroll
       for (int j = 0; j < G; ++j) {
@@ -2927,10 +2934,35 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
         const uint32_t v = rows[min(r, r1 - 1)];
         return r < r1 ? v : INV;
       };
-      auto gather = [&](uint32_t wd, uint32_t* b) {
-        const uint8_t* xr = tab + (int64_t)(wd != INV ? (wd & c.rmask) : 0u) * rstride;
+      // RW: the two 16-B pieces covering the round's bytes, the dword / shift of each feature
+      const int q0 = __builtin_amdgcn_readfirstlane(f0 >> 4);
+      const int q1 = __builtin_amdgcn_readfirstlane(min(q0 + 1, (int)(c.ld >> 4) - 1));
+      int wi[G], wsh[G];
 #pragma unroll
-        for (int j = 0; j < G; ++j) b[j] = (uint32_t)xr[fo[j]];
+      for (int j = 0; j < G; ++j) {
+        const int p = (f0 & 15) + (j < g ? j : 0);
+        wi[j] = __builtin_amdgcn_readfirstlane(p >> 2);
+        wsh[j] = (p & 3) * 8;
+      }
+      auto gather = [&](uint32_t wd, uint32_t* b) {
+#ifdef DML_PROBE_NOGATHER   // timing probe only (wrong histograms): bins from the row id, no table read
+#pragma unroll
+        for (int j = 0; j < G; ++j) b[j] = (wd + 37u * (uint32_t)j) & 0xFFu;
+#else
+        if constexpr (RW) {
+          typedef uint32_t v8u __attribute__((ext_vector_type(8)));
+          const uint4* xr = (const uint4*)(c.Xb + (int64_t)(wd != INV ? (wd & c.rmask) : 0u) * c.ld);
+          const uint4 v0 = xr[q0], v1 = xr[q1];
+          v8u w;
+          w[0] = v0.x; w[1] = v0.y; w[2] = v0.z; w[3] = v0.w; w[4] = v1.x; w[5] = v1.y; w[6] = v1.z; w[7] = v1.w;
+#pragma unroll
+          for (int j = 0; j < G; ++j) b[j] = (w[wi[j]] >> wsh[j]) & 0xFFu;
+        } else {
+          const uint8_t* xr = tab + (int64_t)(wd != INV ? (wd & c.rmask) : 0u) * rstride;
+#pragma unroll
+          for (int j = 0; j < G; ++j) b[j] = (uint32_t)xr[fo[j]];
+        }
+#endif
       };
       auto consume = [&](int r, bool valid, const uint32_t* b, const PRaw& pr) {
         if (!valid) return;
@@ -2979,21 +3011,25 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
         consume(r + 256, vB, bB, pB);
       }
     };
-    auto rung = [&](auto UWc) {
+    auto rung = [&](auto UWc, auto RWc) __attribute__((always_inline)) {
       switch (g) {
-#define DML_G_CASE(N) case N: run(std::integral_constant<int, N>{}, UWc); break;
+#define DML_G_CASE(N) case N: run(std::integral_constant<int, N>{}, UWc, RWc); break;
         DML_G_CASE(1) DML_G_CASE(2) DML_G_CASE(3) DML_G_CASE(4) DML_G_CASE(5) DML_G_CASE(6) DML_G_CASE(7)
         DML_G_CASE(8) DML_G_CASE(9) DML_G_CASE(10) DML_G_CASE(11) DML_G_CASE(12) DML_G_CASE(13) DML_G_CASE(14)
         DML_G_CASE(15)
 #undef DML_G_CASE
-        default: run(std::integral_constant<int, KGL>{}, UWc); break;
+        default: run(std::integral_constant<int, KGL>{}, UWc, RWc); break;
       }
     };
     if constexpr (MODE == 2) {
-      if (uw) rung(std::true_type{});
-      else rung(std::false_type{});
+      // row windows only where boosting runs them (unit-weight whole-feature rounds), ONE
+      // instantiation (G = KGL; features past g are masked): more copies of this loop made the
+      // compiler outline it (a function call per row step)
+      if (uw && rwin) run(std::integral_constant<int, KGL>{}, std::true_type{}, std::true_type{});
+      else if (uw) rung(std::true_type{}, std::false_type{});
+      else rung(std::false_type{}, std::false_type{});
     } else {
-      rung(std::false_type{});
+      rung(std::false_type{}, std::false_type{});
     }
   } else if constexpr (MODE == 2) {
     // wide groups (g > KGL, e.g. boosting's whole-feature rounds of 24): per row, the bins of 8
@@ -3068,7 +3104,11 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
         }
         v = (CT)((unsigned long long)n1 | ((unsigned long long)n1 << 32));   // w = rows
       }
+#ifndef DML_PROBE_NOFLUSH   // timing probe only (wrong histograms): no global flush atomics
       if (v != (CT)0) atomicAdd(&gh[i], v);
+#else
+      if (v == (CT)0x5A5A5A5A5A5Aull) gh[i] = v;   // keeps the LDS reads live
+#endif
     }
   }
 }

@@ -167,7 +167,8 @@ def test_gbrt_root_count_cache_is_exact(model, clf, kg, monkeypatch):
     """Boosting builds reuse the roots' row-count histograms across stages (they only depend on
     the training rows): the ensembles are identical with and without the cache, one lane or two,
     with the large tier's packed count | w yq words, its compact 3-KB LDS slices or the 4-KB ones
-    (DML_LARGE_NO_PACK, DML_LARGE_NO_COMPACT)."""
+    (DML_LARGE_NO_PACK, DML_LARGE_NO_COMPACT), and with row-window gathers for sparse nodes
+    (DML_LARGE_FM_DIV)."""
     if kg is not None:   # feature groups wider than the pipelined loop's 16: the generic row loop
         monkeypatch.setenv("DML_TIER_KG_LARGE_REG", kg)
     rng = np.random.RandomState(4)
@@ -175,9 +176,13 @@ def test_gbrt_root_count_cache_is_exact(model, clf, kg, monkeypatch):
     y = (X[:, 0] + X[:, 1] * X[:, 2] > 0).astype(int) if clf else (X[:, 0] + 0.3 * X[:, 3] ** 2).astype(np.float32)
     grid = list(ParameterGrid({"n_estimators": [6, 12], "max_depth": [3]}))
     out = {}
-    for cache, lanes in (("0", "1"), ("1", "1"), ("1", "2"), ("0", "P"), ("0", "L")):
+    for cache, lanes in (("0", "1"), ("1", "1"), ("1", "2"), ("1", "W"), ("0", "P"), ("0", "L")):
         monkeypatch.setenv("DML_GB_ROOT_CACHE", cache)
-        monkeypatch.setenv("DML_GB_LANES", "1" if lanes in "LP" else lanes)
+        monkeypatch.setenv("DML_GB_LANES", "1" if lanes in "LPW" else lanes)
+        if lanes == "W":   # row windows: nodes under n / 2 rows gather row-major 16-B pieces
+            monkeypatch.setenv("DML_LARGE_FM_DIV", "2")
+        else:
+            monkeypatch.delenv("DML_LARGE_FM_DIV", raising=False)
         if lanes == "P":   # two atomics per (row, feature) instead of the packed count | w yq word
             monkeypatch.setenv("DML_LARGE_NO_PACK", "1")
         if lanes == "L":
@@ -188,6 +193,7 @@ def test_gbrt_root_count_cache_is_exact(model, clf, kg, monkeypatch):
         out[cache + lanes] = np.array([r.result["mean_cv_score"] for r in res])
     np.testing.assert_array_equal(out["11"], out["01"])
     np.testing.assert_array_equal(out["12"], out["01"])
+    np.testing.assert_array_equal(out["1W"], out["01"])
     np.testing.assert_array_equal(out["0L"], out["01"])
     np.testing.assert_array_equal(out["0P"], out["01"])
 
