@@ -272,7 +272,7 @@ struct Ctx {
   int32_t full_cur, full_prev;
   int32_t root_cnt_skip;       // root level of a build with cached root counts: no count atomics
   int32_t large_compact;       // ForestArgs::large_unit (and kg_large <= DML_KGL_LARGE): 3-KB LDS slices
-  int32_t fm_div;              // k_hist_large: feature-major gathers only for nodes >= n / fm_div rows (0: all)
+  int32_t fm_div;              // k_hist_large: row-window gathers for boosting nodes < n / fm_div rows (0: none)
   int32_t large_pack;          // ForestArgs::large_pack (with large_compact): packed count | w yq words
   uint32_t* root_counts;       // ForestArgs::root_counts (null: none)
   int64_t pi_cap;        // entries of each pinfo table
@@ -2908,16 +2908,17 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
     constexpr uint32_t INV = 0xFFFFFFFFu;
     using PL = typename PLT<MODE>::T;
     const int t0 = r0 + (int)threadIdx.x;
-    // feature offsets: feature-major copy (stride n) when present, else the row line
-    // (DML_LARGE_FM_DIV = k > 0: nodes holding under 1/k of the table's rows read the row-major
-    // lines instead -- one line per row for every feature of the round)
-    const bool fm = c.XbT != nullptr && (c.fm_div == 0 || (int64_t)st.on.count * c.fm_div >= (int64_t)c.n);
     // row windows (RW): a whole-histogram round reads features [f0, f0 + g) -- contiguous ids, at
     // most two aligned 16-B pieces of the row line -- so a sparse node's row-major gather is two
     // dwordx4 loads of one cache line per row (the bytes picked out by uniform register index)
-    // instead of g byte loads; a feature-major gather of a node holding 1/2^k of the rows pays
-    // ~2^k / 128 line lookups per (row, feature)
-    const bool rwin = !fm && fround >= 0 && (c.ld & 15) == 0 && g <= 16 && c.ld >= 32;
+    // instead of g byte loads, while a feature-major gather of a node holding 1/2^k of the rows
+    // pays ~2^k / 128 line lookups per (row, feature).  Nodes under n / fm_div rows
+    // (DML_LARGE_FM_DIV, default 8; 0 = never) of unit-weight whole-feature rounds (boosting) use
+    // them: GBRT config 6 18.2 -> 20.4 CV-fits/s (profiles/r6_gbrt_cfg6_row_windows.txt)
+    const bool rwin = MODE == 2 && uw && fround >= 0 && (c.ld & 15) == 0 && g <= 16 && c.ld >= 32 &&
+                      c.fm_div > 0 && (int64_t)st.on.count * c.fm_div < (int64_t)c.n;
+    // feature offsets otherwise: the feature-major copy (stride n) when present, else the row line
+    const bool fm = c.XbT != nullptr && !rwin;
     auto run = [&](auto Gc, auto UWc, auto RWc) __attribute__((always_inline)) {
       constexpr int G = decltype(Gc)::value;
       constexpr bool UW = decltype(UWc)::value;
@@ -3817,7 +3818,7 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.large_cap = L.large_cap;
   c.wave_max = (int)a->wave_max; c.block_max = (int)a->block_max; c.chunk = (int)a->chunk;
   c.kg_wave = (int)a->kg_wave; c.kg_block = (int)a->kg_block; c.kg_large = (int)a->kg_large;
-  c.fm_div = getenv("DML_LARGE_FM_DIV") ? atoi(getenv("DML_LARGE_FM_DIV")) : 0;
+  c.fm_div = getenv("DML_LARGE_FM_DIV") ? atoi(getenv("DML_LARGE_FM_DIV")) : 8;
   c.large_compact = (c.is_reg && a->large_unit && a->kg_large <= DML_KGL_LARGE && !getenv("DML_LARGE_NO_COMPACT")) ? 1 : 0;
   c.large_pack = (c.large_compact && a->large_pack && a->chunk <= 4095 && !getenv("DML_LARGE_NO_PACK")) ? 1 : 0;
   c.slack_wave = (int)a->slack_wave;

@@ -179,10 +179,8 @@ def test_gbrt_root_count_cache_is_exact(model, clf, kg, monkeypatch):
     for cache, lanes in (("0", "1"), ("1", "1"), ("1", "2"), ("1", "W"), ("0", "P"), ("0", "L")):
         monkeypatch.setenv("DML_GB_ROOT_CACHE", cache)
         monkeypatch.setenv("DML_GB_LANES", "1" if lanes in "LPW" else lanes)
-        if lanes == "W":   # row windows: nodes under n / 2 rows gather row-major 16-B pieces
-            monkeypatch.setenv("DML_LARGE_FM_DIV", "2")
-        else:
-            monkeypatch.delenv("DML_LARGE_FM_DIV", raising=False)
+        # row windows for nodes under n / 2 rows ("W"), or feature-major gathers everywhere
+        monkeypatch.setenv("DML_LARGE_FM_DIV", "2" if lanes == "W" else "0")
         if lanes == "P":   # two atomics per (row, feature) instead of the packed count | w yq word
             monkeypatch.setenv("DML_LARGE_NO_PACK", "1")
         if lanes == "L":
