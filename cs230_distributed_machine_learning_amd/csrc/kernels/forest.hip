@@ -60,6 +60,9 @@
 #ifndef DML_KGL_LARGE
 #define DML_KGL_LARGE 16       // k_hist_large: widest feature group of the pipelined (and unit-weight) loop
 #endif
+#ifndef DML_KGW_LARGE
+#define DML_KGW_LARGE 32       // k_hist_large: widest round of a row-window node (two 16-B pieces of the line)
+#endif
 #ifndef DML_PART_KEEP
 #define DML_PART_KEEP 2        // block-tier partition: rounds whose row ids pass 1 keeps in registers (0/1/2: 1.018/1.014/1.009 s sweep build, r5 e6)
 #endif
@@ -273,6 +276,7 @@ struct Ctx {
   int32_t root_cnt_skip;       // root level of a build with cached root counts: no count atomics
   int32_t large_compact;       // ForestArgs::large_unit (and kg_large <= DML_KGL_LARGE): 3-KB LDS slices
   int32_t fm_div;              // k_hist_large: row-window gathers for boosting nodes < n / fm_div rows (0: none)
+  int32_t kg_rw;               // k_hist_large: features per round of a row-window node (multiple of 16; 0: kg_large)
   int32_t large_pack;          // ForestArgs::large_pack (with large_compact): packed count | w yq words
   uint32_t* root_counts;       // ForestArgs::root_counts (null: none)
   int64_t pi_cap;        // entries of each pinfo table
@@ -2875,8 +2879,15 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
   if (r0 >= st.on.count) return;
   const int r1 = min(r0 + c.chunk, st.on.count);
   const NodeSpec s = spec_of<-1>(c, st.on.tree);
-  const int f0 = fround >= 0 ? fround * c.kg_large : 0;
-  const int g = fround >= 0 ? min(c.kg_large, c.d - f0) : st.g;
+  // row-window node: a sparse node (under n / fm_div rows) of a unit-weight whole-feature level
+  // (boosting).  Its rounds are kg_rw features wide when the host set that (fewer rounds: each
+  // round re-reads one cache line per row), kg_large otherwise; a node past its last round exits
+  const bool rw_node = MODE == 2 && fround >= 0 && s.bootstrap == 0 && c.fm_div > 0 && (c.ld & 15) == 0 &&
+                       c.ld >= 32 && (int64_t)st.on.count * c.fm_div < (int64_t)c.n;
+  const int kgr = (rw_node && c.kg_rw > 0) ? c.kg_rw : c.kg_large;
+  const int f0 = fround >= 0 ? fround * kgr : 0;
+  if (fround >= 0 && f0 >= c.d) return;
+  const int g = fround >= 0 ? min(kgr, c.d - f0) : st.g;
   constexpr int RPL = MODE == 2 ? 2 : 3;
   const int span = large_planes(MODE, c.CH) * 256;
   // compact slices (unit-weight regression builds, host-checked): u32 counts in 128 words, then
@@ -2897,11 +2908,12 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
   // regression tree without bootstrap: every active row weighs 1, so the (w | rows << 32)
   // plane is a row count -- kept as u32 LDS counters (ds_add_u32: half the bytes and bank
   // pairs of the u64 add) in the first KB of each feature's 4-KB slice, widened at the flush
-  const bool uw = MODE == 2 && s.bootstrap == 0 && g <= KGL;
+  constexpr int KGW = DML_KGW_LARGE;
+  const bool uw = MODE == 2 && s.bootstrap == 0 && g <= (rw_node ? KGW : KGL);
   // cached root counts (boosting): the count plane is copied in by k_root_counts, so only the
   // w yq plane is accumulated (one LDS atomic per (row, feature) instead of two)
   const bool skipc = MODE == 2 && s.bootstrap == 0 && fround >= 0 && c.root_cnt_skip != 0;
-  if (g <= KGL) {
+  if (g <= KGL || (uw && rw_node)) {
     // ping-pong software pipeline with compile-time-counted unconditional gathers (the block
     // tier's loop in k_nodes): the row id two steps ahead and the next step's bins are in
     // flight while this step's histogram atomics run, with no vmcnt(0) drain between steps
@@ -2913,10 +2925,8 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
     // dwordx4 loads of one cache line per row (the bytes picked out by uniform register index)
     // instead of g byte loads, while a feature-major gather of a node holding 1/2^k of the rows
     // pays ~2^k / 128 line lookups per (row, feature).  Nodes under n / fm_div rows
-    // (DML_LARGE_FM_DIV, default 8; 0 = never) of unit-weight whole-feature rounds (boosting) use
-    // them: GBRT config 6 18.2 -> 20.4 CV-fits/s (profiles/r6_gbrt_cfg6_row_windows.txt)
-    const bool rwin = MODE == 2 && uw && fround >= 0 && (c.ld & 15) == 0 && g <= 16 && c.ld >= 32 &&
-                      c.fm_div > 0 && (int64_t)st.on.count * c.fm_div < (int64_t)c.n;
+    // (DML_LARGE_FM_DIV, opt-in; see the Ctx setup) of unit-weight whole-feature rounds (boosting)
+    const bool rwin = rw_node && uw && (f0 & 15) + g <= 32;
     // feature offsets otherwise: the feature-major copy (stride n) when present, else the row line
     const bool fm = c.XbT != nullptr && !rwin;
     auto run = [&](auto Gc, auto UWc, auto RWc) __attribute__((always_inline)) {
@@ -3026,7 +3036,7 @@ __global__ __launch_bounds__(256) void k_hist_large(Ctx c, int fround) {
       // row windows only where boosting runs them (unit-weight whole-feature rounds), ONE
       // instantiation (G = KGL; features past g are masked): more copies of this loop made the
       // compiler outline it (a function call per row step)
-      if (uw && rwin) run(std::integral_constant<int, KGL>{}, std::true_type{}, std::true_type{});
+      if (uw && rwin) run(std::integral_constant<int, KGW>{}, std::true_type{}, std::true_type{});
       else if (uw) rung(std::true_type{}, std::false_type{});
       else rung(std::false_type{}, std::false_type{});
     } else {
@@ -3818,7 +3828,14 @@ static Ctx make_ctx(const ForestArgs* a, const Layout& L) {
   c.large_cap = L.large_cap;
   c.wave_max = (int)a->wave_max; c.block_max = (int)a->block_max; c.chunk = (int)a->chunk;
   c.kg_wave = (int)a->kg_wave; c.kg_block = (int)a->kg_block; c.kg_large = (int)a->kg_large;
-  c.fm_div = getenv("DML_LARGE_FM_DIV") ? atoi(getenv("DML_LARGE_FM_DIV")) : 8;
+  // row windows: opt-in (DML_LARGE_FM_DIV=8: +12 % on a single config-6 job after the warmup fit,
+  // but back-to-back jobs gain nothing and their histogram kernels run ~25 % longer under three
+  // concurrent lanes -- the sparse levels then touch the row-major table AND the feature-major
+  // copy; profiles/r6_gbrt_cfg6_row_windows.txt)
+  c.fm_div = getenv("DML_LARGE_FM_DIV") ? atoi(getenv("DML_LARGE_FM_DIV")) : 0;
+  // row-window rounds kg_rw features wide (DML_LARGE_KG_RW: a multiple of 16, <= 32; 0 = kg_large)
+  c.kg_rw = getenv("DML_LARGE_KG_RW") ? atoi(getenv("DML_LARGE_KG_RW")) : 0;
+  if (c.kg_rw < 0 || c.kg_rw > DML_KGW_LARGE || (c.kg_rw & 15) != 0 || !c.is_reg || !c.fm_div) c.kg_rw = 0;
   c.large_compact = (c.is_reg && a->large_unit && a->kg_large <= DML_KGL_LARGE && !getenv("DML_LARGE_NO_COMPACT")) ? 1 : 0;
   c.large_pack = (c.large_compact && a->large_pack && a->chunk <= 4095 && !getenv("DML_LARGE_NO_PACK")) ? 1 : 0;
   c.slack_wave = (int)a->slack_wave;
@@ -4097,13 +4114,18 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
                                              (c.large_pack ? 256 : (c.large_compact ? 384 : large_planes(MODE, CH) * 256)) *
                                              mode_elem(MODE),
                                          std::min<size_t>(lds_hl_floor, 150 * 1024));
+  // levels that can hold row-window nodes (below the top two) size the LDS for kg_rw-wide rounds
+  const size_t lds_hl_rw = std::max<size_t>(lds_hl, (size_t)std::max<int>(c.kg_rw, (int)a->kg_large) *
+                                                        (c.large_pack ? 256 : (c.large_compact ? 384 : large_planes(MODE, CH) * 256)) *
+                                                        mode_elem(MODE));
   const size_t lds_sl = (size_t)a->kg_large * ghist_feat_bytes(MODE, CH) + a->kg_large * 16 + 16 +
                         (size_t)a->kg_large * CH * 8 + (size_t)a->kg_large * 8 + 64;
   const size_t lds_max = 160 * 1024;
   if (lds_w > lds_max || lds_b > lds_max || lds_sl > lds_max || lds_s > lds_max || lds_big > lds_max) return 7;
   if (a->sub_max > 64) return 9;
   {
-    const int need = (int)std::max(std::max(std::max(lds_s, lds_w), std::max(lds_b, lds_sl)), std::max(lds_big, lds_hl));
+    const int need = (int)std::max(std::max(std::max(lds_s, lds_w), std::max(lds_b, lds_sl)),
+                                   std::max(lds_big, std::max(lds_hl, lds_hl_rw)));
     static int attr_set[3] = {0, 0, 0};
     if (need > 64 * 1024 && need > attr_set[MODE]) {
       HIP_OK(hipFuncSetAttribute((const void*)k_subtree<REG, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
@@ -4243,10 +4265,15 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       HIP_OK(hipMemsetAsync(c.gf_cur, 0, (size_t)nL * full_node_b, st));
       if (c.root_cnt_skip) k_root_counts<<<dim3((unsigned)nL, (unsigned)a->d), 256, 0, st>>>(c, 0);
       const dim3 gh = DML_LARGE_NODE_FAST ? dim3((unsigned)nL, nchunks) : dim3(nchunks, (unsigned)nL);
+      // below the top two levels a node may be a row-window node with kg_rw-wide rounds: the
+      // rounds' LDS covers kg_rw features (its later rounds exit at once for such nodes)
+      Ctx cr = c;
+      if (levels < 3) cr.kg_rw = 0;
+      const size_t lds_round = cr.kg_rw > 0 ? lds_hl_rw : lds_hl;
       for (int round = 0; round < rounds; ++round) {
         ++large_rounds;
-        if (c.packed) k_hist_large<MODE, true><<<gh, 256, lds_hl, st>>>(c, round);
-        else k_hist_large<MODE, false><<<gh, 256, lds_hl, st>>>(c, round);
+        if (c.packed) k_hist_large<MODE, true><<<gh, 256, lds_round, st>>>(cr, round);
+        else k_hist_large<MODE, false><<<gh, 256, lds_round, st>>>(cr, round);
       }
       if (root_cache && !c.root_cnt_skip) {
         k_root_counts<<<dim3((unsigned)nL, (unsigned)a->d), 256, 0, st>>>(c, 1);

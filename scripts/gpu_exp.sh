@@ -29,7 +29,8 @@
 #                                       envsweep "LIB=cur LIB=cg2" lrk
 #                                     targets: bench (bench.py --steps 10 --warmup 3), c6 (config 6),
 #                                     lrk (lr_kernel_bench 10M x 1000 x 2560), lrbench (bench.py --config lr),
-#                                     tiers (sweep_tiers.py forest build), c6prof (config 6 + top kernels)
+#                                     tiers (sweep_tiers.py forest build), c6prof (config 6 + top kernels),
+#                                     c6rep (config 6, five back-to-back jobs in one process: seconds each)
 #   whole                             kernel trace over the driver's exact bench command -> GPU busy
 #   lrpmc                             the LR objective's PMC passes (MFMA busy, LDS, TCC, TA)
 #   baseline                          round-start numbers: bench kernel stats, LR config 4, GBRT config 6, SVC
@@ -111,6 +112,8 @@ case "$kind" in
                         echo "[$st] $(tail -1 $log | cut -c1-200)" ;;
                tiers)   env "${envs[@]}" timeout -k 10 300 python -u scripts/sweep_tiers.py > $log 2>&1 || exit 1
                         echo "[$st] $(grep build $log | tail -1 | cut -c1-80)" ;;
+               c6rep)   env "${envs[@]}" DML_C6_REPEAT=5 timeout -k 10 400 python -u scripts/bench_configs.py --configs 6 > $log 2>&1 || exit 1
+                        echo "[$st] $(grep -o 'repeat [0-9]: [0-9.]* s' $log | tr '\n' ' ') $(grep -o '"seconds": [0-9.]*' $log)" ;;
                c6prof)  env "${envs[@]}" timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/sweep_prof$i -o run -- python3 scripts/bench_configs.py --configs 6 > $log 2>&1 || exit 1
                         rm -f gpurun_out/sweep_prof$i/*kernel_trace.csv
                         echo "[$st] $(grep -o '"cv_fits_per_s[^,]*' $log)"
