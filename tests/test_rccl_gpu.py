@@ -102,3 +102,65 @@ def test_rccl_world1_collectives_and_cluster_runner(tmp_path, monkeypatch):
         assert all(js.transport == "rccl" for js in runner.jobs) and not runner.dead
     finally:
         dist.destroy()
+
+
+@pytest.mark.gpu
+def test_rccl_group_reforms_after_break(tmp_path, monkeypatch):
+    """A side collective fails on the RCCL group (injected): the group is broken, rank 0
+    re-forms it as communicator generation 1 (destroy + a fresh ``nccl`` init on the same
+    store, parallel/dist.py regroup), and the next jobs travel by RCCL again -- a task-parallel
+    job's scores all-gathered on the new group and a row-sharded job on its data-parallel
+    communicator."""
+    import time
+
+    for k, v in dict(DML_FORCE_PG="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
+                     WORLD_SIZE="1", LOCAL_RANK="0", DML_SIDE_TIMEOUT_S="20", DML_REGROUP_DELAY_S="0.2").items():
+        monkeypatch.setenv(k, v)
+    from cs230_distributed_machine_learning_amd.engine.service import Controller
+    from cs230_distributed_machine_learning_amd.parallel import dist
+    from cs230_distributed_machine_learning_amd.parallel.runner import DistributedRunner, WorkerCore
+
+    dist.destroy()
+    inf = dist.init(want_gpu=True, timeout_s=300)
+    try:
+        core = WorkerCore(inf.device)
+        runner = DistributedRunner(core)
+        ctl = Controller(Config(data_root=str(tmp_path), device="cuda:0", chunk_target_s=0.0), runner=runner)
+        t = threading.Thread(target=runner.serve_forever, daemon=True)
+        t.start()
+
+        def run(name, body):
+            st, ack = ctl.train(sid, dict(body, job_id=name))
+            assert st in (200, 202), ack
+            assert ctl.table.wait_finished(name, timeout=300)
+            return ctl.check_status(sid, name)[1]
+
+        try:
+            sid = ctl.create_session()[1]["session_id"]
+            assert ctl.download_data(sid, {"dataset_url": "iris", "dataset_name": "iris",
+                                           "dataset_type": "sklearn"})[0] == 200
+            monkeypatch.setenv("DML_FAIL_RANK_IN", "0:scores")    # the next scores gather raises
+            broken = run("rf-break", _job("RandomForestClassifier", {"n_estimators": [8], "max_depth": [3, None]}))
+            t0 = time.time()
+            while not runner.group_broken and time.time() - t0 < 60:
+                time.sleep(0.05)
+            monkeypatch.delenv("DML_FAIL_RANK_IN")
+            t0 = time.time()
+            while (runner.group_broken or runner.stats["regroups"] < 1) and time.time() - t0 < 120:
+                time.sleep(0.05)
+            assert runner.stats["regroups"] >= 1 and not runner.group_broken, runner.stats
+            lr = run("lr-gen1", _job("LogisticRegression", {"C": [0.1, 1.0, 10.0]}))
+            dp = run("lr-dp-gen1", _job("LogisticRegression", {"C": [1.0, 10.0]}, par="data"))
+        finally:
+            runner.shutdown()
+            t.join(timeout=120)
+        assert broken["job_status"] == "completed"
+        for st in (lr, dp):
+            assert st["job_status"] == "completed" and st["best_result"]["mean_cv_score"] > 0.85, st
+        log = runner.job_log
+        assert log["lr-gen1"]["transport"] == "rccl" and log["lr-gen1"]["generation"] >= 1, log
+        assert all(r.get("scores_via") == "rccl" for r in lr["job_result"]["results"]), lr["job_result"]["results"]
+        assert log["lr-dp-gen1"]["mode"] == "data" and log["lr-dp-gen1"]["generation"] >= 1, log
+        assert dist.generation() >= 1 and dist.info().backend == "nccl"
+    finally:
+        dist.destroy()
