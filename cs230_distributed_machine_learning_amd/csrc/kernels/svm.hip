@@ -328,22 +328,31 @@ struct CandP {
   float y, q, k;
 };
 
+// the block's best candidate: a wave butterfly over (value, index, source lane) only -- the
+// winning lane then stores its whole record -- and, fused into the same pass (one pair of
+// barriers), the block max of `mx` (the j sweep's max over I_low of y G)
 template <bool MAX>
-__device__ CandP block_reduce_p(CandP c, CandP* red) {
+__device__ CandP block_reduce_p(CandP c, CandP* red, double& mx, double* redd) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  double v = c.v;
+  int idx = c.idx, src = lane;
   for (int m = 32; m >= 1; m >>= 1) {
-    CandP o;
-    o.v = __shfl_xor(c.v, m); o.idx = __shfl_xor(c.idx, m);
-    o.g = __shfl_xor(c.g, m); o.a = __shfl_xor(c.a, m); o.c = __shfl_xor(c.c, m);
-    o.y = __shfl_xor(c.y, m); o.q = __shfl_xor(c.q, m); o.k = __shfl_xor(c.k, m);
-    if (better<MAX>(o.v, o.idx, c.v, c.idx)) c = o;
+    const double ov = __shfl_xor(v, m);
+    const int oi = __shfl_xor(idx, m), os = __shfl_xor(src, m);
+    if (better<MAX>(ov, oi, v, idx)) { v = ov; idx = oi; src = os; }
+    mx = fmax(mx, __shfl_xor(mx, m));
   }
-  const int wid = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) red[wid] = c;
+  if (lane == src) red[wid] = c;        // the wave's winner (src is wave-uniform after the butterfly)
+  if (lane == 0) redd[wid] = mx;
   __syncthreads();
   CandP r = red[0];
-  for (int w = 1; w < NT / 64; ++w)
+  double m2 = redd[0];
+  for (int w = 1; w < NT / 64; ++w) {
     if (better<MAX>(red[w].v, red[w].idx, r.v, r.idx)) r = red[w];
+    m2 = fmax(m2, redd[w]);
+  }
   __syncthreads();
+  mx = m2;
   return r;
 }
 
@@ -369,6 +378,34 @@ __device__ bool exchange(uint64_t* rec, const SplitCtx& sc, uint32_t seq, const 
   }
   __syncthreads();
   return *abort_flag == 0;
+}
+
+// the winning record of an exchange (wave 0: lane q holds record q, a butterfly argmax with
+// the `better` order -- a strict total order on (value, index) pairs, so the same record the
+// sequential scan picks), and for MAX = false the max over all records of the double at
+// words [7, 8] (Gmax2).  Every thread then reads only the winner's words (one LDS broadcast
+// each) instead of scanning all B records itself.
+template <bool MAX>
+__device__ void pick_record(const uint32_t* pay, int B, int* s_win, double* s_g2) {
+  if (threadIdx.x < 64) {
+    const int q = threadIdx.x;
+    const uint32_t* r = pay + q * kRecW;
+    double v = q < B ? mkd(r[0], r[1]) : 0.0;
+    int idx = q < B ? (int)r[2] : -1;
+    int who = q;
+    double g2 = (!MAX && q < B) ? mkd(r[7], r[8]) : -kInf;
+    for (int m = 32; m >= 1; m >>= 1) {
+      const double ov = __shfl_xor(v, m);
+      const int oi = __shfl_xor(idx, m), ow = __shfl_xor(who, m);
+      if (better<MAX>(ov, oi, v, idx)) { v = ov; idx = oi; who = ow; }
+      if (!MAX) g2 = fmax(g2, __shfl_xor(g2, m));
+    }
+    if (q == 0) {
+      *s_win = idx >= 0 ? who : -1;
+      if (!MAX) *s_g2 = g2;
+    }
+  }
+  __syncthreads();
 }
 
 // kernel value of rowset rows (a, b) -- the same arithmetic as kernel_column's entry
@@ -534,7 +571,8 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
   __shared__ uint32_t vals[kRecW];
   __shared__ int s_red[2 * (NT / 64)];
   __shared__ int32_t tag_row[kTagN], tag_slot[kTagN];
-  __shared__ int s_miss;
+  __shared__ int s_miss, s_win;
+  __shared__ double s_g2;
   for (int q = threadIdx.x; q < kTagN; q += NT) tag_row[q] = -1;
   if (threadIdx.x == 0) s_miss = 0;
   SplitCtx sc;
@@ -581,7 +619,8 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
   while (true) {
     if (it >= stop_at) { status = it >= p.max_iter ? 2 : 0; break; }
     // ---- exchange 1: i = argmax over I_up of -y G (with G_i, alpha_i) ----
-    const CandP bi_l = block_reduce_p<true>(ci, red);
+    double unused_mx = -kInf;
+    const CandP bi_l = block_reduce_p<true>(ci, red, unused_mx, redd);
     if (threadIdx.x == 0) {
       // the candidate's own per-variable values travel with it (G, alpha, y, QD, C: no
       // dependent loads, here or by the other workgroups once the winner is known)
@@ -598,14 +637,11 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
     double Gmax = -kInf, gi = 0.0, ai_old = 0.0, Ci = 0.0;
     float yi_f = 0.f, QDi_f = 0.f;
     int i = -1;
-    for (int q = 0; q < B; ++q) {
-      const uint32_t* r = pay + q * kRecW;
-      const int idx = (int)r[2];
-      const double v = mkd(r[0], r[1]);
-      if (better<true>(v, idx, Gmax, i)) {
-        Gmax = v; i = idx; gi = mkd(r[3], r[4]); ai_old = mkd(r[5], r[6]);
-        yi_f = __uint_as_float(r[7]); QDi_f = __uint_as_float(r[8]); Ci = mkd(r[9], r[10]);
-      }
+    pick_record<true>(pay, B, &s_win, &s_g2);
+    if (s_win >= 0) {
+      const uint32_t* r = pay + s_win * kRecW;
+      Gmax = mkd(r[0], r[1]); i = (int)r[2]; gi = mkd(r[3], r[4]); ai_old = mkd(r[5], r[6]);
+      yi_f = __uint_as_float(r[7]); QDi_f = __uint_as_float(r[8]); Ci = mkd(r[9], r[10]);
     }
     __syncthreads();
     if (i < 0) { status = 1; break; }
@@ -663,8 +699,8 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
         }
       }
     }
-    const CandP bj_l = block_reduce_p<false>(cj, red);
-    const double gm2_l = block_max(gmax2, redd);
+    double gm2_l = gmax2;
+    const CandP bj_l = block_reduce_p<false>(cj, red, gm2_l, redd);
     if (threadIdx.x == 0) {
       // K(i, j) of the slice's j comes from the slice of column i it just filled: the entry
       // kernel_pair would recompute with the same arithmetic (every workgroup takes it from
@@ -683,15 +719,12 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
     double bjv = kInf, gj = 0.0, aj_old = 0.0, Gmax2 = -kInf;
     float kij = 0.f, yj_f = 0.f, QDj_f = 0.f;
     int j = -1;
-    for (int q = 0; q < B; ++q) {
-      const uint32_t* r = pay + q * kRecW;
-      const int idx = (int)r[2];
-      const double v = mkd(r[0], r[1]);
-      if (better<false>(v, idx, bjv, j)) {
-        bjv = v; j = idx; gj = mkd(r[3], r[4]); aj_old = mkd(r[5], r[6]); kij = __uint_as_float(r[9]);
-        yj_f = __uint_as_float(r[10]); QDj_f = __uint_as_float(r[11]);
-      }
-      Gmax2 = fmax(Gmax2, mkd(r[7], r[8]));
+    pick_record<false>(pay, B, &s_win, &s_g2);
+    Gmax2 = s_g2;
+    if (s_win >= 0) {
+      const uint32_t* r = pay + s_win * kRecW;
+      bjv = mkd(r[0], r[1]); j = (int)r[2]; gj = mkd(r[3], r[4]); aj_old = mkd(r[5], r[6]);
+      kij = __uint_as_float(r[9]); yj_f = __uint_as_float(r[10]); QDj_f = __uint_as_float(r[11]);
     }
     __syncthreads();
     if (Gmax + Gmax2 < p.eps || j < 0) { status = 1; break; }
