@@ -37,8 +37,15 @@
 #error "DML_RPT_BLOCK must be 1..4"
 #endif
 #ifndef DML_BLOCK_NT
-#define DML_BLOCK_NT 256     // threads per block-tier node
+// threads per block-tier node of a binary-classification build: 2 waves.  With the LDS slab
+// sized to the batch's max_features (10: 22 KB) 7 nodes share a CU instead of 4 at 256
+// threads -- the per-node serial phases (setup, split selection, partition scan) overlap
+// across more nodes (sweep build 0.988 -> 0.974 s, 0.960 s with wave_max 256;
+// profiles/r6_block_nt128_sweep.txt).  Multiclass / regression builds keep 4 waves: their
+// wider histogram planes (up to 96 KB of LDS) allow only 1-2 nodes per CU.
+#define DML_BLOCK_NT 128
 #endif
+template <int MODE> constexpr int block_nt() { return MODE == 1 ? DML_BLOCK_NT : 256; }
 #ifndef DML_NODES_WPE
 // block tier (binary): 4 waves per SIMD = 4 workgroups per CU.  With the register-rows paths
 // compiled out (DML_BLOCK_STREAM_ONLY) and the window loop's bins packed 4 per register the
@@ -1409,7 +1416,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
 #endif
         };
         auto consume = [&](int base, bool valid, const uint32_t* b, const PRaw& pr) {
-          if (NT == 256 && pos == 0 && valid) {
+          if (NT > 64 && pos == 0 && valid) {
             uint32_t w4[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
             for (int j = 0; j < G && j < 16; ++j) w4[j >> 2] |= (j < g ? b[j] & 0xFFu : 0u) << (8 * (j & 3));
@@ -1477,7 +1484,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
           for (int j = 0; j < G; ++j) b[j >> 2] |= (j < g ? (w[fdw[j]] >> fsh[j]) & 0xFFu : 0u) << (8 * (j & 3));
         };
         auto consume = [&](int base, bool valid, const uint32_t* b, const PRaw& pr) {
-          if (NT == 256 && pos == 0 && valid)
+          if (NT > 64 && pos == 0 && valid)
             *(uint4*)(c.bscr + (on.start + base + tid) * 16) =
                 make_uint4(b[0], NPK > 1 ? b[NPK > 1 ? 1 : 0] : 0u, NPK > 2 ? b[NPK > 2 ? 2 : 0] : 0u,
                            NPK > 3 ? b[NPK > 3 ? 3 : 0] : 0u);
@@ -1510,7 +1517,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
           vA = rA != INV;
         }
       };
-      if (DML_ROW_WINDOWS && NT == 256 && pos == 0 && g >= 8 && d <= 112 && (c.ld & 15) == 0 && c.ld >= 112 &&
+      if (DML_ROW_WINDOWS && NT > 64 && pos == 0 && g >= 8 && d <= 112 && (c.ld & 15) == 0 && c.ld >= 112 &&
           (((uintptr_t)c.Xb) & 15) == 0) {
         switch (g) {
           case 8: runw(std::integral_constant<int, (8 < KGMAX ? 8 : KGMAX)>{}); break;
@@ -1555,7 +1562,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
             if (rrow[u] != 0xFFFFFFFFu) hist_add<MODE>(hj, c, (int)bins[j][u], rpl[u]);
         }
       }
-      if (NT == 256 && !reg_rows && pos == 0) {
+      if (NT > 64 && !reg_rows && pos == 0) {
         // streamed block-tier node, RPT rows per thread: the first group's bins (<= 16
         // visiting positions) into each row's scratch slot, as the one-row pipeline does
 #pragma unroll
@@ -1639,7 +1646,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
         sc->best_j = upd ? jj : -1;
         // bscr slots: byte q of a row's 16-B slot = visiting position q (written by the
         // streamed histogram passes: the block tier's first group, the wave tier's groups)
-        if (!reg_rows) sc->scr_n = NT == 256 ? (pos == 0 ? min(g, 16) : sc->scr_n) : min(16, pos + g);
+        if (!reg_rows) sc->scr_n = NT > 64 ? (pos == 0 ? min(g, 16) : sc->scr_n) : min(16, pos + g);
         sc->nonconst = min(nc0 + __popcll(m), k);
         sc->pos = pos + g;
       }
@@ -4132,8 +4139,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
       HIP_OK(hipFuncSetAttribute((const void*)k_subtree<REG, FCX>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_nodes<64, MODE, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_nodes<64, MODE, FCX>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<DML_BLOCK_NT, MODE, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<DML_BLOCK_NT, MODE, FCX>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<block_nt<MODE>(), MODE, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      HIP_OK(hipFuncSetAttribute((const void*)k_nodes<block_nt<MODE>(), MODE, FCX>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_hist_large<MODE, false>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_hist_large<MODE, true>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       HIP_OK(hipFuncSetAttribute((const void*)k_split_large<GM>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
@@ -4192,8 +4199,8 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
     // DML_BLOCK_FIRST: launch the block tier before the subtree / wave tiers
     static const bool block_first = getenv("DML_BLOCK_FIRST") && atoi(getenv("DML_BLOCK_FIRST")) != 0;
     if (block_first && nb) {
-      if (fast) k_nodes<DML_BLOCK_NT, MODE, FCX><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
-      else k_nodes<DML_BLOCK_NT, MODE, -1><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
+      if (fast) k_nodes<block_nt<MODE>(), MODE, FCX><<<nb, block_nt<MODE>(), lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
+      else k_nodes<block_nt<MODE>(), MODE, -1><<<nb, block_nt<MODE>(), lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
     }
     const int nb_late = block_first ? 0 : nb;
     if (fast) {
@@ -4207,7 +4214,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
           k_nodes<64, MODE, FCX><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w, 0);
         }
       }
-      if (nb_late) k_nodes<DML_BLOCK_NT, MODE, FCX><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
+      if (nb_late) k_nodes<block_nt<MODE>(), MODE, FCX><<<nb, block_nt<MODE>(), lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
     } else {
       if (ns4) k_subtree<REG, -1, 32><<<ns4, 64, lds_s32, s0>>>(c, cur, 4);
       if (ns) k_subtree<REG, -1><<<ns, 64, lds_s, s0>>>(c, cur, 0);
@@ -4219,7 +4226,7 @@ static int build_impl(ForestArgs* a, hipStream_t st) {
           k_nodes<64, MODE, -1><<<nw, 64, lds_w, s1>>>(c, 1, cur, (int)pair_w, 0);
         }
       }
-      if (nb_late) k_nodes<DML_BLOCK_NT, MODE, -1><<<nb, DML_BLOCK_NT, lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
+      if (nb_late) k_nodes<block_nt<MODE>(), MODE, -1><<<nb, block_nt<MODE>(), lds_b, s2>>>(c, 2, cur, (int)pair_b, stage_b);
     }
     // whole-histogram level: every tree evaluates every feature and the level's node
     // histograms over all d features fit the budget -> keep them, and derive the larger of

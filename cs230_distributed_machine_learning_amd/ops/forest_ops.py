@@ -38,6 +38,9 @@ class ForestTiers:
     sub_small: int = 32        # subtree roots of <= 32 rows: tier 4, half-size LDS row cache (2x per CU)
     sub_cache_max_d: int = 256  # cache the subtree's bin rows in LDS when d <= this
     wave_max: int = 512         # sweeps: profiles/r1_forest_ab_experiments.md, r2_tier_sweep.txt
+    # binary classification (2-wave block-tier nodes, forest.hip DML_BLOCK_NT): the block tier
+    # takes nodes above 256 rows -- sweep build 0.974 -> 0.960 s (profiles/r6_block_nt128_sweep.txt)
+    wave_max_bin: int = 256
     block_max: int = 65536      # r5 (block tier at 4 WGs/CU): 65536 vs 32768 -1.7 % sweep build, bench +2.6 %
                                 # (profiles/r5_block_max_sweep.txt; r2 kernels: 32768 beat 131072 by 4 %)
     chunk: int = 16384
@@ -71,6 +74,8 @@ class ForestTiers:
             env = os.environ.get("DML_TIER_" + k.upper())
             if env:
                 setattr(t, k, int(env))
+        if n_channels == 3 and not os.environ.get("DML_TIER_WAVE_MAX"):   # binary classification
+            t.wave_max = min(t.wave_max, t.wave_max_bin)
         t.kg_wave = max(1, min(t.kg_wave, (24 * 1024) // per_feat, 4))     # k_nodes<64>: KGMAX 4
         t.kg_block = max(1, min(t.kg_block, (96 * 1024) // per_feat, 16))  # k_nodes<256>: KGMAX 16
         t.kg_large = max(1, min(t.kg_large, (96 * 1024) // per_feat, 64))
@@ -536,6 +541,12 @@ def build_gpu(Xb: torch.Tensor, ycls: Optional[torch.Tensor], yreg: Optional[tor
     pool_cap = _pool_bound(counts, specs) + T
     a.wave_max, a.block_max, a.chunk = tiers.wave_max, tiers.block_max, (tiers.chunk_reg if is_reg else tiers.chunk)
     a.kg_wave, a.kg_block, a.slack_wave = tiers.kg_wave, tiers.kg_block, tiers.slack_wave
+    if T and os.environ.get("DML_TIER_KG_BLOCK") is None:
+        # block tier: feature groups no wider than the batch's largest max_features (a node's
+        # first group is min(kg_block, max_features) features either way, so no tree changes):
+        # the LDS histogram slab shrinks with it (max_features=10: 22 KB instead of 34 KB,
+        # 7 instead of 4 block-tier nodes per CU)
+        a.kg_block = max(1, min(int(a.kg_block), int(min(d, int(specs["max_features"].max())))))
     a.kg_large = tiers.kg_large_reg if is_reg else tiers.kg_large
     # unit-weight regression build whose fixed-point targets stay below 2^39 in magnitude:
     # the large tier packs each row's count and w yq into ONE u64 LDS atomic (forest.hip
