@@ -24,6 +24,6 @@ for i,L in enumerate(lev):
     parts=[]
     for r in L:
         n=r[0].split('(')[0].replace('void ','').replace('dml::','')
-        if any(k in n for k in ('k_nodes','k_subtree','k_bigsub','k_hist_large','k_partition_large','k_predict')):
+        if any(k in n for k in ('k_nodes','k_subtree','k_bigsub','k_hist_large','k_split_large','k_partition_large','k_predict')):
             parts.append(f"{n[:14]}:{(r[2]-r[1])/1e3:.0f}us/{r[3]//max(1,r[4])}")
     print(f"L{i:2d} start {(s-t0)/1e6:7.1f} span {(e-s)/1e3:8.0f}us  "+" ".join(parts))
