@@ -19,6 +19,8 @@
 #include <stdint.h>
 #include <math.h>
 
+#include "wave_ops.h"
+
 namespace {
 
 constexpr int NT = 256;
@@ -76,11 +78,11 @@ __device__ __forceinline__ bool better(double av, int ai, double bv, int bi) {
 
 template <bool MAX>
 __device__ Cand block_reduce(Cand c, Cand* red) {
-  for (int m = 32; m >= 1; m >>= 1) {
-    const double ov = __shfl_xor(c.v, m);
-    const int oi = __shfl_xor(c.idx, m);
-    if (better<MAX>(ov, oi, c.v, c.idx)) { c.v = ov; c.idx = oi; }
-  }
+  const int lane = threadIdx.x & 63;
+#define SVM_BR(M) { const double ov = dml::wave::shfl_xor<M>(c.v, lane); const int oi = dml::wave::shfl_xor<M>(c.idx, lane); \
+                    if (better<MAX>(ov, oi, c.v, c.idx)) { c.v = ov; c.idx = oi; } }
+  SVM_BR(32) SVM_BR(16) SVM_BR(8) SVM_BR(4) SVM_BR(2) SVM_BR(1)
+#undef SVM_BR
   const int wid = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) red[wid] = c;
   __syncthreads();
@@ -92,7 +94,10 @@ __device__ Cand block_reduce(Cand c, Cand* red) {
 }
 
 __device__ double block_max(double v, double* red) {
-  for (int m = 32; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m));
+  const int lane = threadIdx.x & 63;
+  v = fmax(v, dml::wave::shfl_xor<32>(v, lane)); v = fmax(v, dml::wave::shfl_xor<16>(v, lane));
+  v = fmax(v, dml::wave::shfl_xor<8>(v, lane)); v = fmax(v, dml::wave::shfl_xor<4>(v, lane));
+  v = fmax(v, dml::wave::shfl_xor<2>(v, lane)); v = fmax(v, dml::wave::shfl_xor<1>(v, lane));
   const int wid = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) red[wid] = v;
   __syncthreads();
@@ -336,12 +341,13 @@ __device__ CandP block_reduce_p(CandP c, CandP* red, double& mx, double* redd) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   double v = c.v;
   int idx = c.idx, src = lane;
-  for (int m = 32; m >= 1; m >>= 1) {
-    const double ov = __shfl_xor(v, m);
-    const int oi = __shfl_xor(idx, m), os = __shfl_xor(src, m);
-    if (better<MAX>(ov, oi, v, idx)) { v = ov; idx = oi; src = os; }
-    mx = fmax(mx, __shfl_xor(mx, m));
-  }
+  // butterfly steps on DPP / permlane (VALU), not ds_bpermute (an LDS round trip per step)
+#define SVM_BRP(M) { const double ov = dml::wave::shfl_xor<M>(v, lane); \
+                     const int oi = dml::wave::shfl_xor<M>(idx, lane), os = dml::wave::shfl_xor<M>(src, lane); \
+                     if (better<MAX>(ov, oi, v, idx)) { v = ov; idx = oi; src = os; } \
+                     mx = fmax(mx, dml::wave::shfl_xor<M>(mx, lane)); }
+  SVM_BRP(32) SVM_BRP(16) SVM_BRP(8) SVM_BRP(4) SVM_BRP(2) SVM_BRP(1)
+#undef SVM_BRP
   if (lane == src) red[wid] = c;        // the wave's winner (src is wave-uniform after the butterfly)
   if (lane == 0) redd[wid] = mx;
   __syncthreads();
@@ -394,12 +400,12 @@ __device__ void pick_record(const uint32_t* pay, int B, int* s_win, double* s_g2
     int idx = q < B ? (int)r[2] : -1;
     int who = q;
     double g2 = (!MAX && q < B) ? mkd(r[7], r[8]) : -kInf;
-    for (int m = 32; m >= 1; m >>= 1) {
-      const double ov = __shfl_xor(v, m);
-      const int oi = __shfl_xor(idx, m), ow = __shfl_xor(who, m);
-      if (better<MAX>(ov, oi, v, idx)) { v = ov; idx = oi; who = ow; }
-      if (!MAX) g2 = fmax(g2, __shfl_xor(g2, m));
-    }
+#define SVM_PR(M) { const double ov = dml::wave::shfl_xor<M>(v, q); \
+                    const int oi = dml::wave::shfl_xor<M>(idx, q), ow = dml::wave::shfl_xor<M>(who, q); \
+                    if (better<MAX>(ov, oi, v, idx)) { v = ov; idx = oi; who = ow; } \
+                    if (!MAX) g2 = fmax(g2, dml::wave::shfl_xor<M>(g2, q)); }
+    SVM_PR(32) SVM_PR(16) SVM_PR(8) SVM_PR(4) SVM_PR(2) SVM_PR(1)
+#undef SVM_PR
     if (q == 0) {
       *s_win = idx >= 0 ? who : -1;
       if (!MAX) *s_g2 = g2;
@@ -596,6 +602,22 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
   __syncthreads();
   auto rowof = [&](int64_t t) { return (p.svr && t >= nr) ? t - nr : t; };
   const int nseg = p.svr ? 2 : 1;             // this slice's variables: [r0,r1) (+ nr for SVR)
+  // wide variant, one-segment slice of <= kSweepU * NT variables: the slice's y, alpha, C, G and
+  // QD stay in registers for the whole launch (thread tid owns variables r0 + tid + k NT), so
+  // each sweep loads only its kernel-column entries; G / alpha go back to memory at the end
+  constexpr int RU = kSweepU == 8 ? 8 : 1;
+  const bool regst = kSweepU == 8 && nseg == 1 && sc.r1 - sc.r0 <= (int64_t)kSweepU * NT;
+  float rs_y[RU], rs_q[RU], rs_ki[RU];
+  double rs_a[RU], rs_C[RU], rs_g[RU];
+  if constexpr (kSweepU == 8) {
+    if (regst) {
+#pragma unroll
+      for (int k = 0; k < RU; ++k) {
+        const int64_t t = min(sc.r0 + threadIdx.x + k * NT, sc.r1 - 1);
+        rs_y[k] = y[t]; rs_a[k] = a[t]; rs_C[k] = C[t]; rs_g[k] = g[t]; rs_q[k] = QD[t]; rs_ki[k] = 0.f;
+      }
+    }
+  }
 
   int64_t it = p.iters;
   int status = 0;
@@ -603,6 +625,22 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
   const int64_t stop_at = min(p.max_iter, it + chunk);
   auto local_i = [&]() {
     CandP ci{-kInf, -1, 0.0, 0.0, 0.0, 0.f, 0.f, 0.f};
+    if constexpr (kSweepU == 8) {
+      if (regst) {
+#pragma unroll
+        for (int k = 0; k < RU; ++k) {
+          const int64_t t = sc.r0 + threadIdx.x + k * NT;
+          if (t >= sc.r1) break;
+          const bool up = rs_y[k] > 0 ? !is_upper(rs_a[k], rs_C[k]) : !is_lower(rs_a[k]);
+          if (up) {
+            const double v = -(double)rs_y[k] * rs_g[k];
+            if (better<true>(v, (int)t, ci.v, ci.idx))
+              ci = CandP{v, (int)t, rs_g[k], rs_a[k], rs_C[k], rs_y[k], rs_q[k], 0.f};
+          }
+        }
+        return ci;
+      }
+    }
     for (int sgi = 0; sgi < nseg; ++sgi)
       for (int64_t t = sc.r0 + sgi * nr + threadIdx.x; t < sc.r1 + sgi * nr; t += NT) {
         const double yt = y[t], at = a[t], Ct = C[t], gt = g[t];
@@ -657,7 +695,45 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
     CandP cj{kInf, -1, 0.0, 0.0, 0.0, 0.f, 0.f, 0.f};
     double gmax2 = -kInf;
     const double QDi = QDi_f;
-    for (int sgi = 0; sgi < nseg; ++sgi) {
+    // one j candidate: the same selection arithmetic for both state layouts
+    auto j_cand = [&](int64_t t, double yt, double at, double Ct, double gt, float qt, float kt) {
+      if (yt > 0) {
+        if (!is_lower(at)) {
+          const double gd = Gmax + gt;
+          gmax2 = fmax(gmax2, gt);
+          if (gd > 0) {
+            double qc = QDi + (double)qt - 2.0 * yi * (yi * yt * (double)kt);
+            const double od = qc > 0 ? -(gd * gd) / qc : -(gd * gd) / kTau;
+            if (better<false>(od, (int)t, cj.v, cj.idx)) cj = CandP{od, (int)t, gt, at, Ct, (float)yt, qt, kt};
+          }
+        }
+      } else {
+        if (!is_upper(at, Ct)) {
+          const double gd = Gmax - gt;
+          gmax2 = fmax(gmax2, -gt);
+          if (gd > 0) {
+            double qc = QDi + (double)qt + 2.0 * yi * (yi * yt * (double)kt);
+            const double od = qc > 0 ? -(gd * gd) / qc : -(gd * gd) / kTau;
+            if (better<false>(od, (int)t, cj.v, cj.idx)) cj = CandP{od, (int)t, gt, at, Ct, (float)yt, qt, kt};
+          }
+        }
+      }
+    };
+    bool swept = false;
+    if constexpr (kSweepU == 8) {
+      if (regst) {   // registers hold the slice: only column i's entries are loaded
+#pragma unroll
+        for (int k = 0; k < RU; ++k) rs_ki[k] = Ki[min(sc.r0 + threadIdx.x + k * NT, sc.r1 - 1)];
+#pragma unroll
+        for (int k = 0; k < RU; ++k) {
+          const int64_t t = sc.r0 + threadIdx.x + k * NT;
+          if (t >= sc.r1) break;
+          j_cand(t, (double)rs_y[k], rs_a[k], rs_C[k], rs_g[k], rs_q[k], rs_ki[k]);
+        }
+        swept = true;
+      }
+    }
+    for (int sgi = 0; sgi < nseg && !swept; ++sgi) {
       const int64_t lo = sc.r0 + sgi * nr, hi = sc.r1 + sgi * nr;
       for (int64_t tb = lo + threadIdx.x; tb < hi; tb += kSweepU * NT) {
         float yk[kSweepU], kk[kSweepU], qk[kSweepU];
@@ -672,30 +748,7 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
         for (int k = 0; k < kSweepU; ++k) {
           const int64_t t = tb + k * NT;
           if (t >= hi) break;
-          const double yt = yk[k];
-          if (yt > 0) {
-            if (!is_lower(ak[k])) {
-              const double gd = Gmax + gk[k];
-              gmax2 = fmax(gmax2, gk[k]);
-              if (gd > 0) {
-                double qc = QDi + (double)qk[k] - 2.0 * yi * (yi * yt * (double)kk[k]);
-                const double od = qc > 0 ? -(gd * gd) / qc : -(gd * gd) / kTau;
-                if (better<false>(od, (int)t, cj.v, cj.idx))
-                  cj = CandP{od, (int)t, gk[k], ak[k], Ck[k], yk[k], qk[k], kk[k]};
-              }
-            }
-          } else {
-            if (!is_upper(ak[k], Ck[k])) {
-              const double gd = Gmax - gk[k];
-              gmax2 = fmax(gmax2, -gk[k]);
-              if (gd > 0) {
-                double qc = QDi + (double)qk[k] + 2.0 * yi * (yi * yt * (double)kk[k]);
-                const double od = qc > 0 ? -(gd * gd) / qc : -(gd * gd) / kTau;
-                if (better<false>(od, (int)t, cj.v, cj.idx))
-                  cj = CandP{od, (int)t, gk[k], ak[k], Ck[k], yk[k], qk[k], kk[k]};
-              }
-            }
-          }
+          j_cand(t, (double)yk[k], ak[k], Ck[k], gk[k], qk[k], kk[k]);
         }
       }
     }
@@ -768,7 +821,31 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
     __syncthreads();
     // gradient update of this slice fused with its next i candidates (4 per thread per step)
     ci = CandP{-kInf, -1, 0.0, 0.0, 0.0, 0.f, 0.f, 0.f};
-    for (int sgi = 0; sgi < nseg; ++sgi) {
+    bool updated = false;
+    if constexpr (kSweepU == 8) {
+      if (regst) {   // column i's entries are still in registers from the j sweep
+        float kjr[RU];
+#pragma unroll
+        for (int k = 0; k < RU; ++k) kjr[k] = Kj[min(sc.r0 + threadIdx.x + k * NT, sc.r1 - 1)];
+#pragma unroll
+        for (int k = 0; k < RU; ++k) {
+          const int64_t t = sc.r0 + threadIdx.x + k * NT;
+          if (t >= sc.r1) break;
+          if (t == i) rs_a[k] = ai;
+          if (t == j) rs_a[k] = aj;
+          const double yt = rs_y[k];
+          const double gt = rs_g[k] + yt * (yi * (double)rs_ki[k] * dai + yj * (double)kjr[k] * daj);
+          rs_g[k] = gt;
+          const bool up = yt > 0 ? !is_upper(rs_a[k], rs_C[k]) : !is_lower(rs_a[k]);
+          if (up) {
+            const double v = -yt * gt;
+            if (better<true>(v, (int)t, ci.v, ci.idx)) ci = CandP{v, (int)t, gt, rs_a[k], rs_C[k], rs_y[k], rs_q[k], 0.f};
+          }
+        }
+        updated = true;
+      }
+    }
+    for (int sgi = 0; sgi < nseg && !updated; ++sgi) {
       const int64_t lo = sc.r0 + sgi * nr, hi = sc.r1 + sgi * nr;
       for (int64_t tb = lo + threadIdx.x; tb < hi; tb += kSweepU * NT) {
         float yk[kSweepU], kik[kSweepU], kjk[kSweepU], qk[kSweepU];
@@ -799,6 +876,15 @@ __global__ __launch_bounds__(NT) void k_smo_split(const float* __restrict__ X, i
     SVM_PH(6)
   }
 #undef SVM_PH
+  if constexpr (kSweepU == 8) {
+    if (regst) {   // the slice's G and alpha back to memory (the host resumes or finishes from them)
+#pragma unroll
+      for (int k = 0; k < RU; ++k) {
+        const int64_t t = sc.r0 + threadIdx.x + k * NT;
+        if (t < sc.r1) { g[t] = rs_g[k]; a[t] = rs_a[k]; }
+      }
+    }
+  }
   if (do_prof && threadIdx.x == 0) {
     ph[7] = s_miss;
     for (int k = 0; k < 8; ++k) prof[k] += ph[k];

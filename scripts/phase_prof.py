@@ -9,7 +9,7 @@ out = np.zeros(32, dtype=np.uint64)
 lib.dml_forest_phase_stats.argtypes = [ctypes.c_void_p]
 rc = lib.dml_forest_phase_stats(out.ctypes.data)
 names = ["setup", "feat_extract", "hist", "eval", "select", "decision", "partition", "nodes"]
-for t, tn in enumerate(["wave(64)", "block(256)"]):
+for t, tn in enumerate(["wave(64)", "block"]):
     v = out[t * 8:(t + 1) * 8].astype(float)
     n = v[7] or 1
     tot = v[:7].sum()
