@@ -514,3 +514,33 @@ def test_gpu_absolute_error_matches_sklearn(extra, seeds):
         ref = np.sort(sk.value[sk.children_left == -1][:, 0, 0])
         assert len(ours) == len(ref)
         np.testing.assert_allclose(ours, ref, rtol=1e-9)
+
+
+def test_gpu_block_tier_settings_do_not_change_trees(monkeypatch):
+    """Round 6 block-tier settings (2-wave binary nodes, kg_block = the batch's largest
+    max_features, binary wave_max 256) against the round-5 ones (kg_block 16, wave_max 512):
+    the same trees, node for node -- feature groups and tier thresholds never change a tree."""
+    n, d, C = 120_000, 24, 2
+    X, y = _data(n, d, C, seed=3)
+    dev = torch.device("cuda:0")
+    edges = binning.quantile_edges(torch.from_numpy(X))
+    Xb_cpu = binning.bin_matrix(torch.from_numpy(X), edges).numpy()
+    Xb = torch.from_numpy(Xb_cpu).to(dev)
+    roles, _ = make_split_roles(y, 3, True, holdout=False)
+    specs = _specs(3, 4, d, msl=2)
+    specs["max_features"][:4] = 5      # a batch of mixed max_features: kg_block = 9 here
+    specs["max_features"][4:8] = 9
+    ycls = torch.from_numpy(y.astype(np.int32)).to(dev)
+    rl = torch.from_numpy(roles).to(dev)
+    builds = {}
+    for name, env in (("auto", {}), ("r5", {"DML_TIER_KG_BLOCK": "16", "DML_TIER_WAVE_MAX": "512"})):
+        for k in ("DML_TIER_KG_BLOCK", "DML_TIER_WAVE_MAX"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        g = forest_ops.build_gpu(Xb, ycls, None, rl, specs, C, False, forest_ops.ForestTiers())
+        assert g.stats["tier_nodes"][2] > 0   # the block tier ran
+        builds[name] = _canon(g.nodes.cpu().numpy(), g.vals.cpu().numpy(), len(specs))
+    assert builds["auto"] == builds["r5"]
+    c = forest_ops.build_cpu(Xb_cpu, y.astype(np.int32), None, roles, specs, C, False)
+    assert builds["auto"] == _canon(c.nodes, c.vals, len(specs))

@@ -23,3 +23,17 @@ def test_feature_groups_clamped_to_lds_budget(monkeypatch):
 def test_regression_defaults():
     t = ForestTiers().fitted(4)
     assert t.chunk_reg == 4096 and t.chunk == 16384
+
+
+def test_forest_tiers_binary_wave_max(monkeypatch):
+    """Binary classification (3 histogram channels) caps the wave tier at wave_max_bin; other
+    builds keep wave_max; DML_TIER_WAVE_MAX overrides both (ops/forest_ops.py ForestTiers.fitted)."""
+    from cs230_distributed_machine_learning_amd.ops.forest_ops import ForestTiers
+
+    monkeypatch.delenv("DML_TIER_WAVE_MAX", raising=False)
+    t = ForestTiers()
+    assert t.fitted(3).wave_max == t.wave_max_bin == 256
+    assert t.fitted(4).wave_max == t.wave_max == 512      # regression / 3 classes
+    assert t.fitted(6).wave_max == 512
+    monkeypatch.setenv("DML_TIER_WAVE_MAX", "384")
+    assert t.fitted(3).wave_max == 384 and t.fitted(4).wave_max == 384
