@@ -544,3 +544,27 @@ def test_gpu_block_tier_settings_do_not_change_trees(monkeypatch):
     assert builds["auto"] == builds["r5"]
     c = forest_ops.build_cpu(Xb_cpu, y.astype(np.int32), None, roles, specs, C, False)
     assert builds["auto"] == _canon(c.nodes, c.vals, len(specs))
+
+
+@pytest.mark.parametrize("n_fits,msl,depth", [(3, 1, 14), (2, 4, 2**31 - 1)])
+def test_gpu_row_window_path_matches_cpu(n_fits, msl, depth):
+    """d = 100 on 128-byte rows (the engine's padded layout, ops/binning.py row_pitch): the block
+    tier's first feature group and the wave tier's prefetch read whole row lines (dwordx4
+    windows) -- the bench's path, node for node against the C++ builder."""
+    n, d, C = 80_000, 100, 2
+    X, y = _data(n, d, C, seed=11)
+    dev = torch.device("cuda:0")
+    edges = binning.quantile_edges(torch.from_numpy(X))
+    Xb_cpu = binning.bin_matrix(torch.from_numpy(X), edges).numpy()
+    pad = torch.zeros((n, 128), dtype=torch.uint8, device=dev)
+    pad[:, :d] = torch.from_numpy(Xb_cpu).to(dev)
+    Xb = pad[:, :d]
+    assert Xb.stride(0) == 128
+    roles, _ = make_split_roles(y, n_fits, True, holdout=False)
+    specs = _specs(n_fits, 3, d, msl=msl, max_depth=depth)   # max_features sqrt(100) = 10
+    ycls = y.astype(np.int32)
+    g = forest_ops.build_gpu(Xb, torch.from_numpy(ycls).to(dev), None, torch.from_numpy(roles).to(dev), specs, C,
+                             False, forest_ops.ForestTiers())
+    assert g.stats["tier_nodes"][1] > 0 and g.stats["tier_nodes"][2] > 0   # wave and block tiers ran
+    c = forest_ops.build_cpu(Xb_cpu, ycls, None, roles, specs, C, False)
+    assert _canon(g.nodes.cpu().numpy(), g.vals.cpu().numpy(), len(specs)) == _canon(c.nodes, c.vals, len(specs))
