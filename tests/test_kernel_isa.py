@@ -23,6 +23,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 SCRATCH_OK = {
     "k_nodesILi64ELi1E": 72,      # wave tier, binary: row-window prefetch at the 128-VGPR cap
     "k_nodesILi256ELi1E": 12,     # block tier, binary: partition row ids kept from pass 1
+    "k_nodesILi128ELi1E": 12,     # the same kernel at 2 waves per node (binary builds' block tier)
     "k_dp_split_wave": 160,       # row-sharded forest: per-lane candidate arrays
     "k_dp_split": 560,
     "k_gb_gradILi64E": 528,       # multinomial boosting gradient with K > 8 classes
