@@ -48,7 +48,7 @@ def _job(job_id, dataset, model, grid, parallelism=None, base=None, cv=3):
     return body
 
 
-RF_A = ("job-a", "RandomForestClassifier", {"min_samples_leaf": [1, 2, 3, 4, 5, 6, 7, 8]}, {"n_estimators": 6})
+RF_A = ("job-a", "RandomForestClassifier", {"min_samples_leaf": list(range(1, 13))}, {"n_estimators": 6})
 LR_B = ("job-b", "LogisticRegression", {"C": [0.5, 2.0]}, None)
 LR_C = ("job-c", "LogisticRegression", {"C": [0.1, 1.0, 10.0]}, None)
 DATA = {"dataset_url": "classification?n=3000&d=8&seed=41", "dataset_name": "t", "dataset_type": "synthetic"}
@@ -113,7 +113,7 @@ def test_killed_rank_respawns_and_group_reforms(tmp_path):
     job travels by collective (transport "rccl", scores all-gathered on the new group) and a
     forced data-parallel job runs row-sharded on the new group with the local scores."""
     port, mport = _free_port(), _free_port()
-    env = dict(os.environ, DML_KILL_RANK_AFTER="2:1", DML_DEAD_AFTER_S="3", OMP_NUM_THREADS="1",
+    env = dict(os.environ, DML_KILL_RANK_AFTER="2:0", DML_DEAD_AFTER_S="3", OMP_NUM_THREADS="1",
                DML_REGROUP_DELAY_S="0.5", DML_SIDE_TIMEOUT_S="20", DML_DP_TIMEOUT_S="30", PYTHONPATH=ROOT)
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, "-m", "cs230_distributed_machine_learning_amd.serve", "--gpus", "4", "--device", "cpu",
@@ -138,7 +138,7 @@ def test_killed_rank_respawns_and_group_reforms(tmp_path):
         jid, model, grid, base = RF_A
         assert svc.post(f"/train/{sid}", _job(jid, "t", model, grid, base=base)).status_code in (200, 202)
         a = svc.wait_job(sid, jid)
-        assert a["job_status"] == "completed" and len(a["job_result"]["results"]) == 8, a
+        assert a["job_status"] == "completed" and len(a["job_result"]["results"]) == len(RF_A[2]["min_samples_leaf"]), a
         # the replacement joined and the group was re-formed over 4 live workers, one of them
         # the new process (worker ids >= 4096 are joiners)
         cl = svc.wait_cluster(lambda c: c["group_ok"] and len(c["members"]) == 4 and max(c["members"]) >= 4096
