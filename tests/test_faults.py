@@ -118,8 +118,16 @@ def _rank_main(rank, world, port, root, outq):
             try:
                 sid = ctl.create_session()[1]["session_id"]
                 ctl.download_data(sid, {"dataset_url": "iris", "dataset_name": "iris", "dataset_type": "sklearn"})
+                # every rank's worker loop is polling (its heartbeat key exists) before the job
+                # that rank 2 must die in: on a loaded host a late rank 2 could otherwise miss every
+                # slice of it and never reach the injected crash
+                t_hb = time.time()
+                while not all(runner.st.check([f"hb/{r}"]) for r in range(world)) and time.time() - t_hb < 120:
+                    time.sleep(0.05)
                 out = []
-                for jid, grid in (("j-kill", {"C": [0.01, 0.03, 0.1, 0.3, 1.0, 3.0, 10.0, 30.0, 100.0, 300.0, 1000.0, 3000.0]}),
+                # j-kill: enough slices that rank 2 claims one however late it finished loading
+                kill_c = [round(0.01 * 1.25 ** i, 6) for i in range(48)]
+                for jid, grid in (("j-kill", {"C": kill_c}),
                                   ("j-after", {"C": [0.5, 5.0]})):
                     st, ack = ctl.train(sid, _j1(jid, "LogisticRegression", grid))
                     ctl.table.wait_finished(ack["job_id"], timeout=120)
@@ -171,7 +179,7 @@ def test_killed_rank_slices_are_requeued():
     (st1, m1), (st2, m2), (st3, t3) = out[1]
     assert out[2] == [2]                                   # rank 2 was declared dead
     assert procs[2].exitcode == 17                         # ... because it crashed (injected)
-    assert st1["job_status"] == "completed" and len(st1["job_result"]["results"]) == 12
+    assert st1["job_status"] == "completed" and len(st1["job_result"]["results"]) == 48
     assert all("cv_scores" in r for r in st1["job_result"]["results"])
     assert {m["worker_id"] for m in m1} <= {"rank0", "rank1", "rank2"}
     assert st2["job_status"] == "completed" and len(st2["job_result"]["results"]) == 2
