@@ -44,7 +44,7 @@ def _wait_done(c, sid, jid, timeout):
 @pytest.mark.timeout(400)
 def test_worker_rank_death_under_real_launcher(tmp_path):
     port, mport = _free_port(), _free_port()
-    env = dict(os.environ, DML_KILL_RANK_AFTER="1:1", OMP_NUM_THREADS="2", PYTHONUNBUFFERED="1")
+    env = dict(os.environ, DML_KILL_RANK_AFTER="1:0", OMP_NUM_THREADS="2", PYTHONUNBUFFERED="1")
     env.pop("WORLD_SIZE", None)
     env.pop("RANK", None)
     log = open(tmp_path / "serve.log", "w")
@@ -69,9 +69,9 @@ def test_worker_rank_death_under_real_launcher(tmp_path):
                                                   "dataset_type": "sklearn"})
         assert r.status_code == 200, r.text
         jid = c.post(f"/train/{sid}", json=_job("iris", "species", {"max_depth": [2, 3, 4, 5, 6, None],
-                                                                     "min_samples_leaf": [1, 2]})).json()["job_id"]
+                                                                     "min_samples_leaf": [1, 2, 3, 4]})).json()["job_id"]
         st = _wait_done(c, sid, jid, 200)
-        assert st["job_status"] == "completed" and len(st["job_result"]["results"]) == 12, st
+        assert st["job_status"] == "completed" and len(st["job_result"]["results"]) == 24, st
         text = (tmp_path / "serve.log").read_text()
         assert "worker on GPU 1 exited" in text, text[-3000:]   # the worker really died ...
         assert proc.poll() is None                            # ... and the service did not
