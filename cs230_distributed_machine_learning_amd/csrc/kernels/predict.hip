@@ -31,33 +31,106 @@ struct PredictArgs {
   int64_t fit_skip;           // optional int32[F] device mask: fits already predicted (early) are skipped
   int64_t fit_depth_cap;      // optional int32[F]: fit f reads its trees only down to this depth (<= 0: all);
                               // prefix fits of a deeper grown forest (models/base.py prefix_groups)
+  int64_t toptab;             // optional NodeRec[trees][kTopSlots]: every tree's first kTopLv levels in heap
+                              // order (k_top_fill), walked from LDS; 0 = every level from the node pool
+  int64_t max_trees;          // max trees of one fit (k_top_fill grid)
 };
+
+// The first kTopLv levels of a tree are shared by every row that walks it: they are
+// gathered once per predict into a heap-ordered table (slot s: children 2s+1 / 2s+2;
+// a slot under a leaf holds {-1, -1}), and a block copies the table of the U trees it is
+// walking into LDS with one coalesced read.  Those levels then cost LDS reads instead of
+// dependent 8-B gathers through TA / L2 (the walk's first levels are L2 hits, so the
+// saving is address-processing and latency, not HBM bytes).
+#ifndef DML_PRED_TOP_LV
+#define DML_PRED_TOP_LV 7
+#endif
+constexpr int kTopLv = DML_PRED_TOP_LV;
+constexpr int kTopSlots = 1 << kTopLv;   // 2^kTopLv - 1 used + 1 pad
+static_assert(kTopLv >= 1 && kTopSlots <= 256, "ops/forest_ops.py TOP_SLOTS_MAX allocates 256 slots per tree");
 
 // leaf of U consecutive trees [t0, t0 + u_n) for one row, walked in lock-step: the U
 // dependent node-load chains are independent, so U requests are in flight per thread
 // instead of one (tree traversal is latency-bound)
+// top (LDS, [kPredU][kTopSlots]) or nullptr: the group's top-level table (see kTopLv)
 template <int kPredU>
 __device__ __forceinline__ void leaves_u(const NodeRec* __restrict__ nodes, const uint8_t* __restrict__ xr, int t0,
-                                         int u_n, int (&leaf)[kPredU], int cap) {
+                                         int u_n, int (&leaf)[kPredU], int cap, const NodeRec* top) {
   NodeRec nr[kPredU];
+  int sl[kPredU];
 #pragma unroll
   for (int u = 0; u < kPredU; ++u) {
     leaf[u] = t0 + u;
-    nr[u] = u < u_n ? nodes[leaf[u]] : NodeRec{-1, -1};
+    sl[u] = 0;
+    nr[u] = u < u_n ? (top ? top[u * kTopSlots] : nodes[leaf[u]]) : NodeRec{-1, -1};
   }
   for (int steps = 0; steps < cap; ++steps) {   // step s: every unfinished tree at depth s
     bool any = false;
 #pragma unroll
     for (int u = 0; u < kPredU; ++u) any |= nr[u].split >= 0;
     if (!any) break;
+    if (top && steps + 1 < kTopLv) {   // depth steps + 1 is in the LDS table (uniform branch)
 #pragma unroll
-    for (int u = 0; u < kPredU; ++u) {
-      if (nr[u].split >= 0) {
-        leaf[u] = nr[u].left + (xr[nr[u].split >> 8] > (nr[u].split & 255) ? 1 : 0);
-        nr[u] = nodes[leaf[u]];
+      for (int u = 0; u < kPredU; ++u) {
+        if (nr[u].split >= 0) {
+          const int b = xr[nr[u].split >> 8] > (nr[u].split & 255) ? 1 : 0;
+          leaf[u] = nr[u].left + b;
+          sl[u] = 2 * sl[u] + 1 + b;
+          nr[u] = top[u * kTopSlots + sl[u]];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kPredU; ++u) {
+        if (nr[u].split >= 0) {
+          leaf[u] = nr[u].left + (xr[nr[u].split >> 8] > (nr[u].split & 255) ? 1 : 0);
+          nr[u] = nodes[leaf[u]];
+        }
       }
     }
   }
+}
+
+// the top-level table of every tree of the launch's fits: one wave per tree, one level per
+// round (lane i < 2^l fills slot 2^l - 1 + i from its parent's record)
+__global__ __launch_bounds__(256) void k_top_fill(PredictArgs a) {
+  __shared__ NodeRec recs[4][kTopSlots];
+  const int f = blockIdx.y;
+  if (a.fit_skip && (GPTR(const int32_t, a.fit_skip))[f]) return;
+  const int32_t* toff = GPTR(const int32_t, a.fit_tree_off);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int t = toff[f] + (int)blockIdx.x * 4 + w;
+  if (t >= toff[f + 1]) return;   // wave-uniform; the rounds below synchronise within the wave only
+  const NodeRec* nodes = GPTR(const NodeRec, a.nodes);
+  NodeRec* r = recs[w];
+  if (lane == 0) r[0] = nodes[t];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int l = 1; l < kTopLv; ++l) {
+    const int n = 1 << l;
+    for (int i = lane; i < n; i += 64) {
+      const int s = n - 1 + i;
+      const NodeRec pr = r[(s - 1) >> 1];
+      r[s] = pr.split >= 0 ? nodes[pr.left + ((s - 1) & 1)] : NodeRec{-1, -1};
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  NodeRec* out = GPTR(NodeRec, a.toptab) + (int64_t)t * kTopSlots;
+  for (int s = lane; s < kTopSlots; s += 64) out[s] = s < kTopSlots - 1 ? r[s] : NodeRec{-1, -1};
+}
+
+// copy the top tables of trees [t, t + u_n) into LDS (block-wide; every thread of the block calls)
+template <int kPredU>
+__device__ __forceinline__ void load_top(const PredictArgs& a, NodeRec* top, int t, int u_n) {
+  __syncthreads();   // the previous group's walks are done with the table
+  const uint4* src = (const uint4*)(GPTR(const NodeRec, a.toptab) + (int64_t)t * kTopSlots);
+  uint4* dst = (uint4*)top;
+  for (int k = threadIdx.x; k < kPredU * kTopSlots / 2; k += 256)
+    if (k < u_n * (kTopSlots / 2)) dst[k] = src[k];
+  __syncthreads();
 }
 
 // depth cap of fit f (1 << 20: none)
@@ -87,6 +160,9 @@ __device__ __forceinline__ const uint8_t* stage_rows(const PredictArgs& a, uint8
   return xs + threadIdx.x * P;
 }
 
+// byte offset of the top table in the dynamic LDS (after the staged rows, 16-B aligned)
+__device__ __forceinline__ int64_t top_lds_off(const PredictArgs& a) { return (a.lds_pitch * 256 + 15) & ~15; }
+
 template <int MAXC, int kPredU>
 __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
@@ -97,13 +173,17 @@ __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t r0 = roff[f], nr = roff[f + 1] - r0;
   if ((int64_t)blockIdx.x * 256 >= nr) return;
+  // with the top table every thread stays to the end (block-wide table loads); a thread
+  // past the fit's rows walks nothing and writes nothing
+  const bool live = i < nr;
+  NodeRec* top = a.toptab ? (NodeRec*)(xs_lds + top_lds_off(a)) : nullptr;
   const uint8_t* xr;
   if (a.lds_pitch) {
     xr = stage_rows(a, xs_lds, r0, nr);
-    if (i >= nr) return;
+    if (!live && !top) return;
   } else {
-    if (i >= nr) return;
-    xr = GPTR(const uint8_t, a.Xb) + (int64_t)(GPTR(const int32_t, a.rows))[r0 + i] * a.ld;
+    if (!live && !top) return;
+    xr = GPTR(const uint8_t, a.Xb) + (int64_t)(GPTR(const int32_t, a.rows))[r0 + (live ? i : 0)] * a.ld;
   }
   const int C = (int)a.n_classes;
   const int cap = depth_cap(a, f);
@@ -115,8 +195,9 @@ __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
   const int tend = toff[f + 1];
   for (int t = toff[f]; t < tend; t += kPredU) {
     int leaf[kPredU];
-    const int u_n = min(kPredU, tend - t);
-    leaves_u<kPredU>(nodes, xr, t, u_n, leaf, cap);
+    const int u_all = min(kPredU, tend - t), u_n = live ? u_all : 0;
+    if (top) load_top<kPredU>(a, top, t, u_all);
+    leaves_u<kPredU>(nodes, xr, t, u_n, leaf, cap, top);
     // accumulate in tree order (bit-identical to the host predictor)
 #pragma unroll
     for (int u = 0; u < kPredU; ++u) {
@@ -134,6 +215,7 @@ __global__ __launch_bounds__(256) void k_predict_cls(PredictArgs a) {
       }
     }
   }
+  if (!live) return;
   int best = 0;
   float bv = p[0];
 #pragma unroll
@@ -159,13 +241,17 @@ __global__ __launch_bounds__(256) void k_predict_reg(PredictArgs a) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t r0 = roff[f], nr = roff[f + 1] - r0;
   if ((int64_t)blockIdx.x * 256 >= nr) return;
+  // with the top table every thread stays to the end (block-wide table loads); a thread
+  // past the fit's rows walks nothing and writes nothing
+  const bool live = i < nr;
+  NodeRec* top = a.toptab ? (NodeRec*)(xs_lds + top_lds_off(a)) : nullptr;
   const uint8_t* xr;
   if (a.lds_pitch) {
     xr = stage_rows(a, xs_lds, r0, nr);
-    if (i >= nr) return;
+    if (!live && !top) return;
   } else {
-    if (i >= nr) return;
-    xr = GPTR(const uint8_t, a.Xb) + (int64_t)(GPTR(const int32_t, a.rows))[r0 + i] * a.ld;
+    if (!live && !top) return;
+    xr = GPTR(const uint8_t, a.Xb) + (int64_t)(GPTR(const int32_t, a.rows))[r0 + (live ? i : 0)] * a.ld;
   }
   const NodeRec* nodes = GPTR(const NodeRec, a.nodes);
   const double* val = GPTR(const double, a.node_val);
@@ -175,8 +261,9 @@ __global__ __launch_bounds__(256) void k_predict_reg(PredictArgs a) {
   const int tend = toff[f + 1];
   for (int t = toff[f]; t < tend; t += kPredU) {
     int leaf[kPredU];
-    const int u_n = min(kPredU, tend - t);
-    leaves_u<kPredU>(nodes, xr, t, u_n, leaf, cap);
+    const int u_all = min(kPredU, tend - t), u_n = live ? u_all : 0;
+    if (top) load_top<kPredU>(a, top, t, u_all);
+    leaves_u<kPredU>(nodes, xr, t, u_n, leaf, cap, top);
 #pragma unroll
     for (int u = 0; u < kPredU; ++u) {
       if (u >= u_n) break;
@@ -184,6 +271,7 @@ __global__ __launch_bounds__(256) void k_predict_reg(PredictArgs a) {
       if (v[0] > 0.0) { acc += v[1] / v[0]; ++nt; }
     }
   }
+  if (!live) return;
   (GPTR(float, a.out_pred))[r0 + i] = nt ? (float)(acc / nt) : 0.f;
 }
 
@@ -310,7 +398,16 @@ template <int U>
 static int launch_predict(PredictArgs* a, hipStream_t st) {
   dim3 grid((unsigned)((a->max_rows + 255) / 256), (unsigned)a->F);
   a->lds_pitch = predict_pitch(a);
-  const size_t lds = (size_t)a->lds_pitch * 256;
+  size_t lds = (size_t)a->lds_pitch * 256;
+  static const bool top_off = getenv("DML_PRED_NO_TOP") != nullptr;
+  PredictArgs b = *a;   // the launch's copy: the top table only when it fits the LDS
+  const size_t lds_top = ((lds + 15) & ~(size_t)15) + (size_t)U * kTopSlots * sizeof(NodeRec);
+  if (top_off || lds_top > 64 * 1024 || a->max_trees <= 0) b.toptab = 0;
+  if (b.toptab) {
+    k_top_fill<<<dim3((unsigned)((b.max_trees + 3) / 4), (unsigned)b.F), 256, 0, st>>>(b);
+    lds = lds_top;
+  }
+  a = &b;
   if (a->is_reg) {
     k_predict_reg<U><<<grid, 256, lds, st>>>(*a);
   } else {

@@ -245,6 +245,9 @@ def _bigsub_on(t: "ForestTiers", is_reg: bool, n_classes: int, d: int, mono) -> 
             and d <= t.sub_cache_max_d and os.environ.get("DML_BIGSUB", "1") != "0")
 
 
+TOP_SLOTS_MAX = 256   # room per tree for predict.hip's top table (kTopSlots = 1 << kTopLv <= 256)
+
+
 def pool_bytes(pool_cap: int, VC: int) -> int:
     return (pool_cap * 8 + 255) // 256 * 256 + pool_cap * VC * 8
 
@@ -882,6 +885,12 @@ class GpuPredict:
         if depth_cap is not None:   # int32 [F]: fit f walks its trees down to this depth (<= 0: all)
             self._cap = torch.from_numpy(np.ascontiguousarray(depth_cap, dtype=np.int32)).to(dev)
             p.fit_depth_cap = native.ptr(self._cap)
+        toff = np.asarray(fit_tree_off, dtype=np.int64)
+        if F and int(toff[-1]) > 0:
+            # every tree's first levels, heap-ordered (predict.hip k_top_fill), read by the walk
+            # from LDS: up to TOP_SLOTS_MAX NodeRecs (8 B) per tree, indexed by tree id
+            self._top = torch.empty((int(toff.max()) * TOP_SLOTS_MAX, 2), dtype=torch.int32, device=dev)
+            p.toptab, p.max_trees = native.ptr(self._top), int(np.max(np.diff(toff)))
         self.args = p
 
     def run(self, fits=None) -> None:

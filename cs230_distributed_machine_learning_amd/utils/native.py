@@ -82,7 +82,8 @@ ForestArgs = _i64_struct(
 PredictArgs = _i64_struct(
     "PredictArgs",
     ["Xb", "ld", "nodes", "node_val", "VC", "is_reg", "n_classes", "fit_tree_off", "fit_row_off", "rows",
-     "out_pred", "out_proba", "F", "max_rows", "d", "lds_pitch", "fit_row_off_host", "fit_skip", "fit_depth_cap"],
+     "out_pred", "out_proba", "F", "max_rows", "d", "lds_pitch", "fit_row_off_host", "fit_skip", "fit_depth_cap",
+     "toptab", "max_trees"],
 )
 
 ScoreArgs = _i64_struct("ScoreArgs", ["rows", "fit_row_off", "pred", "ycls", "yreg", "is_reg", "out", "F"])
