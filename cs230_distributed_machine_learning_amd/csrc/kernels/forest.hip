@@ -3517,23 +3517,48 @@ __global__ __launch_bounds__(64) void k_large_finish(Ctx c, int set_cur) {
 // ------------------------------------------------------------------------------------
 // tree roots: active-row count, fill, root statistics
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_count_active(Ctx c) {
-  const int t = blockIdx.y;
-  const NodeSpec s = spec_of<-1>(c, t);
-  const uint8_t* role = c.roles + (int64_t)s.split * c.n;
-  int cnt = 0;
+// A block counts 1024 rows for kCntG trees: the row half of the bootstrap hash
+// (hash_u32's inner splitmix64 of the row counter) is the same for every tree, so it is
+// computed once per row and group, and "weight > 0" is one compare against the smallest
+// Poisson threshold instead of the whole inverse-CDF table (exactly boot_weight(...) > 0).
+constexpr int kCntG = 8;
+__global__ __launch_bounds__(256) void k_count_active(Ctx c, int T) {
+  const int t0 = blockIdx.y * kCntG;
   const int r0 = blockIdx.x * 1024;
-  for (int i = 0; i < 4; ++i) {
-    const int r = r0 + i * 256 + threadIdx.x;
-    if (r < c.n && role[r] == 1 && boot_weight(s, (uint32_t)r) > 0) ++cnt;
+  uint64_t inner[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    inner[i] = boot_row_key((uint32_t)(r0 + i * 256 + threadIdx.x));
+  __shared__ int red[kCntG][4];
+  for (int g = 0; g < kCntG; ++g) {
+    const int t = t0 + g;
+    int cnt = 0;
+    if (t < T) {   // block-uniform
+      const NodeSpec s = spec_of<-1>(c, t);
+      const uint8_t* role = c.roles + (int64_t)s.split * c.n;
+      uint32_t tmin = s.pois_cdf[0];
+      for (int j = 1; j < kPoisTable; ++j) tmin = min(tmin, s.pois_cdf[j]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = r0 + i * 256 + threadIdx.x;
+        if (r < c.n && role[r] == 1) {
+          bool on = true;
+          if (s.bootstrap) {
+            const uint32_t u = (uint32_t)(splitmix64(s.seed ^ inner[i]) >> 32);
+            on = s.bootstrap == 2 ? u < s.pois_cdf[0] : u >= tmin;
+          }
+          cnt += on;
+        }
+      }
+    }
+    for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+    if ((threadIdx.x & 63) == 0) red[g][threadIdx.x >> 6] = cnt;
   }
-  __shared__ int red[4];
-  for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const int tot = red[0] + red[1] + red[2] + red[3];
-    if (tot) atomicAdd(&c.active_count[t], tot);
+  if (threadIdx.x < kCntG && t0 + (int)threadIdx.x < T) {
+    const int g = threadIdx.x;
+    const int tot = red[g][0] + red[g][1] + red[g][2] + red[g][3];
+    if (tot) atomicAdd(&c.active_count[t0 + g], tot);
   }
 }
 
@@ -4082,8 +4107,8 @@ int dml_forest_count(ForestArgs* a, hipStream_t st) {
   c.n = (int)a->n; c.roles = (const uint8_t*)a->roles; c.specs = (const TreeSpec*)a->specs;
   c.active_count = (int32_t*)a->active_count;
   HIP_OK(hipMemsetAsync(c.active_count, 0, a->T * 4, st));
-  dim3 grid((unsigned)((a->n + 1023) / 1024), (unsigned)a->T);
-  k_count_active<<<grid, 256, 0, st>>>(c);
+  dim3 grid((unsigned)((a->n + 1023) / 1024), (unsigned)((a->T + kCntG - 1) / kCntG));
+  k_count_active<<<grid, 256, 0, st>>>(c, (int)a->T);
   HIP_OK(hipGetLastError());
   return 0;
 }

@@ -99,6 +99,12 @@ DML_HD uint32_t hash_u32(uint64_t key, uint64_t ctr) {
 
 // bootstrap weight of `row` for the tree (TS: TreeSpec, or any view with its fields --
 // the HIP node kernels pass a register-resident NodeSpec)
+// the row half of boot_weight's hash (hash_u32's inner splitmix64): the same for every
+// tree, so k_count_active computes it once per row for a group of trees
+DML_HD uint64_t boot_row_key(uint32_t row) {
+  return splitmix64(0xB0075ull * 0x100000000ull + row + 0x632BE59BD9B4E019ull);
+}
+
 template <class TS>
 DML_HD uint32_t boot_weight(const TS& t, uint32_t row) {
   if (!t.bootstrap) return 1u;
